@@ -1,0 +1,168 @@
+#!/usr/bin/env python
+"""Headline benchmark: RAFT training throughput (image pairs / s, whole node).
+
+Config (BASELINE.json): RAFT full, FlyingChairs-shape 368x496 synthetic pairs, iters=12, per-GPU
+batch 12, bf16 autocast, random-init weights, full training step (forward + sequence loss +
+backward + RCCL gradient all-reduce + grad-clip + fused AdamW + OneCycle).  Weak scaling: per-GPU
+work is fixed, ``value`` is the aggregate over all ranks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--impl hip|torch] [--alternate_corr]
+
+N>1 is launched by the driver via ``python -m torch.distributed.run --nproc-per-node N ... bench.py
+--gpus N``; this script reads RANK / LOCAL_RANK / WORLD_SIZE from the environment.
+``--impl torch`` runs the stock reference-semantics ops (MIOpen convs, grid_sample CorrBlock,
+unfold upsampling, eager loss): that is the baseline the HIP path is compared with.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = ('training image-pairs/sec (whole node), RAFT FlyingChairs 368x496 iters=12, '
+          'at 1/2/4/8 MI355X')
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=12, help='per-GPU batch')
+    ap.add_argument('--size', type=int, nargs=2, default=[368, 496])
+    ap.add_argument('--iters', type=int, default=12)
+    ap.add_argument('--impl', choices=['hip', 'torch'], default='hip')
+    ap.add_argument('--precision', choices=['bf16', 'fp16', 'fp32'], default='bf16')
+    ap.add_argument('--alternate_corr', action='store_true')
+    ap.add_argument('--channels_last', action='store_true')
+    ap.add_argument('--small', action='store_true')
+    ap.add_argument('--profile', type=str, default=None, help='torch.profiler trace dir')
+    ap.add_argument('--json_out', type=str, default=None)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse(argv)
+    import torch
+    from pytorch_raft_amd.parallel import dist as pdist
+    from pytorch_raft_amd.models.raft import RAFT
+    from pytorch_raft_amd.engine.trainer import TrainState
+    from pytorch_raft_amd.data.synthetic import device_batches
+
+    if int(os.environ.get('WORLD_SIZE', '1')) != a.gpus and a.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # convenience: self-launch when run directly with --gpus N
+        import subprocess
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+               '--nproc-per-node', str(a.gpus), '--master-addr', '127.0.0.1',
+               '--master-port', '29533', os.path.abspath(__file__)] + (argv or sys.argv[1:])
+        sys.exit(subprocess.call(cmd))
+
+    device = pdist.init_distributed()
+    world = pdist.world_size()
+    rank = pdist.rank()
+    torch.manual_seed(1234 + rank)
+    torch.backends.cudnn.benchmark = True
+
+    margs = argparse.Namespace(
+        small=a.small, mixed_precision=a.precision != 'fp32',
+        amp_dtype='float16' if a.precision == 'fp16' else 'bfloat16',
+        alternate_corr=a.alternate_corr, dropout=0.0,
+        corr_impl='torch' if a.impl == 'torch' else 'auto',
+        channels_last=a.channels_last,
+        lr=4e-4, wdecay=1e-4, epsilon=1e-8, num_steps=100000, iters=a.iters, gamma=0.8,
+        clip=1.0, add_noise=False)
+    torch.manual_seed(1234)  # identical init on every rank (also broadcast below)
+    model = RAFT(margs).to(device)
+    if a.channels_last:
+        model = model.to(memory_format=torch.channels_last)
+    model.train()
+    pdist.broadcast_module(model)
+    if a.impl == 'torch':
+        import pytorch_raft_amd.ops.loss as L
+        _orig = L.sequence_loss
+
+        def _torch_loss(*x, **k):
+            k['impl'] = 'torch'
+            return _orig(*x, **k)
+        import pytorch_raft_amd.engine.trainer as T
+        T.sequence_loss = _torch_loss
+    st = TrainState(model, margs, device)
+
+    h, w = a.size
+    batches = device_batches(a.batch, h, w, device, count=2, seed=17 * rank)
+
+    def run(n):
+        for k in range(n):
+            i1, i2, fl, va = batches[k % len(batches)]
+            st.step(i1, i2, fl, va)
+
+    run(a.warmup)
+    if device.type == 'cuda':
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats()
+    pdist.barrier(device)
+    prof = None
+    if a.profile and rank == 0:
+        from torch.profiler import profile, ProfilerActivity
+        prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=False)
+        prof.__enter__()
+    t0 = time.perf_counter()
+    run(a.steps)
+    if device.type == 'cuda':
+        torch.cuda.synchronize()
+    pdist.barrier(device)
+    elapsed = time.perf_counter() - t0
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(a.profile, exist_ok=True)
+        with open(os.path.join(a.profile, 'ops.txt'), 'w') as f:
+            f.write(prof.key_averages().table(sort_by='cuda_time_total', row_limit=60))
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    if pdist.is_dist():
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t.item())
+    peak = torch.cuda.max_memory_allocated(device) / 2 ** 30 if device.type == 'cuda' else 0.0
+    ok = st.check_finite()
+    pairs = a.batch * world * a.steps
+    value = pairs / elapsed
+    res = {
+        'metric': METRIC,
+        'value': round(value, 3),
+        'unit': 'image-pairs/s',
+        'n_gpus': world,
+        'steps': a.steps,
+        'warmup': a.warmup,
+        'ms_per_step': round(1000.0 * elapsed / a.steps, 3),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': a.precision,
+        'data': 'synthetic (random smooth texture pairs, 368x496, generated on device; random-init weights)',
+        'config': {
+            'model': 'RAFT-small' if a.small else 'RAFT (full, 5.26M params)',
+            'global_batch': a.batch * world,
+            'per_gpu_batch': a.batch,
+            'seq_len': None,
+            'image_size': [h, w],
+            'iters': a.iters,
+            'parallelism': 'dp%d' % world,
+            'impl': a.impl,
+            'corr': 'alternate(on-the-fly)' if a.alternate_corr else 'all-pairs',
+        },
+        'peak_hbm_gib_rank0': round(peak, 2),
+        'loss_finite': ok,
+    }
+    if rank == 0:
+        line = json.dumps(res)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, 'w') as f:
+                f.write(line + '\n')
+    pdist.destroy()
+
+
+if __name__ == '__main__':
+    main()

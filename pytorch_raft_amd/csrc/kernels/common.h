@@ -1,0 +1,55 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels of pytorch_raft_amd.
+//
+// Kernels are written for wave64 and compiled only with --offload-arch=gfx950.  They expose plain
+// C++ launch functions (raw pointers + a hipStream_t) declared in launchers.h; the torch-facing
+// validation / dispatch lives in ../bindings.cpp, so these translation units never include torch
+// headers and compile in seconds.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define RAFT_WAVE 64
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float raft_bf16_to_f32(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+// round-to-nearest-even f32 -> bf16 bits (inputs here are finite activations)
+__device__ __forceinline__ uint16_t raft_f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+template <typename T> struct Ld;
+template <> struct Ld<float> {
+  __device__ __forceinline__ static float get(const float* p, int64_t i) { return p[i]; }
+};
+template <> struct Ld<uint16_t> {
+  __device__ __forceinline__ static float get(const uint16_t* p, int64_t i) {
+    return raft_bf16_to_f32(p[i]);
+  }
+};
+
+template <typename T> struct St;
+template <> struct St<float> {
+  __device__ __forceinline__ static void put(float* p, int64_t i, float v) { p[i] = v; }
+};
+template <> struct St<uint16_t> {
+  __device__ __forceinline__ static void put(uint16_t* p, int64_t i, float v) {
+    p[i] = raft_f32_to_bf16(v);
+  }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+static inline unsigned raft_cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }

@@ -1,0 +1,177 @@
+// Fused multi-level (2r+1)^2 bilinear window lookup on the all-pairs pyramid (forward + backward).
+//
+// Replaces, per GRU iteration, the reference's per-level linspace/meshgrid + `F.grid_sample`
+// (align_corners=True, zero padding) + view/cat/permute/contiguous chain (`core/corr.py:29-50`,
+// `core/utils/utils.py:57-71`) -- 4 levels x ~8 ATen ops each -- with one launch.
+//
+// Semantics: a window's taps share one fractional offset, so each thread (one query pixel, one
+// level) walks the (2r+2) x (2r+2) integer neighbourhood row by row, blends horizontally once per
+// row and vertically between consecutive rows.  Output channel = level*(2r+1)^2 + ix*(2r+1) + iy
+// (x-offset-major, `SURVEY.md` §2.7 item 7); taps outside the plane read 0.
+//
+// Backward: every query pixel owns its own correlation plane in every level, so the adjoint is a
+// race-free read-modify-write of that pixel's (2r+2)^2 neighbourhood (no atomics, deterministic)
+// into a pyramid-gradient buffer that persists across all iterations of the step; the reference
+// instead materialises and zero-fills a dense plane-sized gradient per level per iteration.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+struct PyrC {
+  const float* lvl[4];
+  int h[4];
+  int w[4];
+};
+struct PyrG {
+  float* lvl[4];
+  int h[4];
+  int w[4];
+};
+
+__device__ __forceinline__ float clamp_coord(float v) { return fminf(fmaxf(v, -1.0e7f), 1.0e7f); }
+
+template <int R>
+__global__ __launch_bounds__(64) void corr_lookup_fwd_kernel(PyrC pyr, const float* __restrict__ coords,
+                                                            float* __restrict__ out, int B, int H,
+                                                            int W, int levels) {
+  constexpr int D = 2 * R + 1;
+  const int N = H * W;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)B * levels * N) return;
+  const int i = (int)(t % N);
+  const int l = (int)((t / N) % levels);
+  const int b = (int)(t / ((int64_t)N * levels));
+  const int hl = pyr.h[l], wl = pyr.w[l];
+  const float inv = 1.0f / (float)(1 << l);
+  const float cx = clamp_coord(coords[((int64_t)b * 2 + 0) * N + i] * inv);
+  const float cy = clamp_coord(coords[((int64_t)b * 2 + 1) * N + i] * inv);
+  const float fx = floorf(cx), fy = floorf(cy);
+  const float ax = cx - fx, ay = cy - fy;
+  const int xs = (int)fx - R, ys = (int)fy - R;
+  const float* P = pyr.lvl[l] + ((int64_t)b * N + i) * hl * wl;
+  float* O = out + ((int64_t)b * levels * D * D + l * D * D) * N + i;
+
+  float hprev[D], hcur[D];
+#pragma unroll
+  for (int yy = 0; yy <= D; ++yy) {
+    const int gy = ys + yy;
+    const bool rowok = (gy >= 0) && (gy < hl);
+    float v[D + 1];
+#pragma unroll
+    for (int xx = 0; xx <= D; ++xx) {
+      const int gx = xs + xx;
+      v[xx] = (rowok && gx >= 0 && gx < wl) ? P[(int64_t)gy * wl + gx] : 0.f;
+    }
+#pragma unroll
+    for (int ix = 0; ix < D; ++ix) hcur[ix] = (1.f - ax) * v[ix] + ax * v[ix + 1];
+    if (yy > 0) {
+      const int iy = yy - 1;
+#pragma unroll
+      for (int ix = 0; ix < D; ++ix)
+        O[(int64_t)(ix * D + iy) * N] = (1.f - ay) * hprev[ix] + ay * hcur[ix];
+    }
+#pragma unroll
+    for (int ix = 0; ix < D; ++ix) hprev[ix] = hcur[ix];
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(64) void corr_lookup_bwd_kernel(PyrG g, const float* __restrict__ coords,
+                                                            const float* __restrict__ dout, int B,
+                                                            int H, int W, int levels) {
+  constexpr int D = 2 * R + 1;
+  const int N = H * W;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)B * levels * N) return;
+  const int i = (int)(t % N);
+  const int l = (int)((t / N) % levels);
+  const int b = (int)(t / ((int64_t)N * levels));
+  const int hl = g.h[l], wl = g.w[l];
+  const float inv = 1.0f / (float)(1 << l);
+  const float cx = clamp_coord(coords[((int64_t)b * 2 + 0) * N + i] * inv);
+  const float cy = clamp_coord(coords[((int64_t)b * 2 + 1) * N + i] * inv);
+  const float fx = floorf(cx), fy = floorf(cy);
+  const float ax = cx - fx, ay = cy - fy;
+  const int xs = (int)fx - R, ys = (int)fy - R;
+  float* G = g.lvl[l] + ((int64_t)b * N + i) * hl * wl;
+  const float* dO = dout + ((int64_t)b * levels * D * D + l * D * D) * N + i;
+
+  // hs_iy[xx] = (1-ax) d[xx][iy] + ax d[xx-1][iy]  (horizontal adjoint of tap row iy)
+  float hprev[D + 1];
+#pragma unroll
+  for (int xx = 0; xx <= D; ++xx) hprev[xx] = 0.f;
+#pragma unroll
+  for (int yy = 0; yy <= D; ++yy) {
+    float hcur[D + 1];
+    if (yy < D) {
+      float d[D];
+#pragma unroll
+      for (int ix = 0; ix < D; ++ix) d[ix] = dO[(int64_t)(ix * D + yy) * N];
+#pragma unroll
+      for (int xx = 0; xx <= D; ++xx) {
+        float s = 0.f;
+        if (xx < D) s += (1.f - ax) * d[xx];
+        if (xx > 0) s += ax * d[xx - 1];
+        hcur[xx] = s;
+      }
+    } else {
+#pragma unroll
+      for (int xx = 0; xx <= D; ++xx) hcur[xx] = 0.f;
+    }
+    const int gy = ys + yy;
+    if (gy >= 0 && gy < hl) {
+#pragma unroll
+      for (int xx = 0; xx <= D; ++xx) {
+        const int gx = xs + xx;
+        if (gx >= 0 && gx < wl) G[(int64_t)gy * wl + gx] += (1.f - ay) * hcur[xx] + ay * hprev[xx];
+      }
+    }
+#pragma unroll
+    for (int xx = 0; xx <= D; ++xx) hprev[xx] = hcur[xx];
+  }
+}
+
+template <typename P>
+P make_pyr(float* const* lvl, const int* hs, const int* ws, int levels) {
+  P p;
+  for (int l = 0; l < 4; ++l) {
+    p.lvl[l] = l < levels ? lvl[l] : nullptr;
+    p.h[l] = l < levels ? hs[l] : 0;
+    p.w[l] = l < levels ? ws[l] : 0;
+  }
+  return p;
+}
+
+}  // namespace
+
+bool launch_corr_lookup_fwd(const float* const* lvl, const int* hs, const int* ws, int levels,
+                            const float* coords, float* out, int B, int H, int W, int radius,
+                            hipStream_t stream) {
+  PyrC p;
+  for (int l = 0; l < 4; ++l) {
+    p.lvl[l] = l < levels ? lvl[l] : nullptr;
+    p.h[l] = l < levels ? hs[l] : 0;
+    p.w[l] = l < levels ? ws[l] : 0;
+  }
+  const int64_t total = (int64_t)B * levels * H * W;
+  dim3 grid(raft_cdiv(total, 64));
+  switch (radius) {
+    case 3: hipLaunchKernelGGL(corr_lookup_fwd_kernel<3>, grid, dim3(64), 0, stream, p, coords, out, B, H, W, levels); return true;
+    case 4: hipLaunchKernelGGL(corr_lookup_fwd_kernel<4>, grid, dim3(64), 0, stream, p, coords, out, B, H, W, levels); return true;
+    default: return false;
+  }
+}
+
+bool launch_corr_lookup_bwd(float* const* glvl, const int* hs, const int* ws, int levels,
+                            const float* coords, const float* dout, int B, int H, int W, int radius,
+                            hipStream_t stream) {
+  PyrG p = make_pyr<PyrG>(glvl, hs, ws, levels);
+  const int64_t total = (int64_t)B * levels * H * W;
+  dim3 grid(raft_cdiv(total, 64));
+  switch (radius) {
+    case 3: hipLaunchKernelGGL(corr_lookup_bwd_kernel<3>, grid, dim3(64), 0, stream, p, coords, dout, B, H, W, levels); return true;
+    case 4: hipLaunchKernelGGL(corr_lookup_bwd_kernel<4>, grid, dim3(64), 0, stream, p, coords, dout, B, H, W, levels); return true;
+    default: return false;
+  }
+}

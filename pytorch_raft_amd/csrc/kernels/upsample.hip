@@ -1,0 +1,191 @@
+// Convex 8x upsampling of a 1/8-resolution flow field (forward + backward), and upflow8.
+//
+// Reference `RAFT.upsample_flow` (`core/raft.py:72-83`) is view -> softmax over the 9 neighbours ->
+// F.unfold(8*flow, 3x3, pad 1) -> weighted sum -> 6-D permute -> reshape: five ATen kernels and two
+// full-resolution temporaries per call.  Here one kernel reads the 576-channel mask once and writes
+// the full-resolution flow; the backward is one kernel for d(mask) plus a tiny gather for d(flow).
+//
+// Mask channel m = k*64 + a*8 + b  (k = ky*3 + kx neighbour, (a, b) = sub-pixel row/col);
+// output pixel (8y + a, 8x + b); neighbour (ky, kx) of cell (y, x) is (y+ky-1, x+kx-1), zero outside.
+//
+// Work split: a 256-thread workgroup owns 64 consecutive cells of one row (lane = cell, so every mask
+// read is a coalesced 256-B row) and 4 groups of 16 sub-pixels.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+template <typename TM>
+__global__ __launch_bounds__(256) void convex_up_fwd_kernel(const float* __restrict__ flow,
+                                                            const TM* __restrict__ mask,
+                                                            float* __restrict__ out, int H, int W) {
+  const int xi = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int x = blockIdx.x * 64 + xi, y = blockIdx.y, b = blockIdx.z;
+  if (x >= W) return;
+  const int64_t HW = (int64_t)H * W;
+  const float* F = flow + (int64_t)b * 2 * HW;
+  float nf[9][2];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    nf[k][0] = ok ? 8.f * F[(int64_t)yy * W + xx] : 0.f;
+    nf[k][1] = ok ? 8.f * F[HW + (int64_t)yy * W + xx] : 0.f;
+  }
+  const TM* M = mask + (int64_t)b * 576 * HW + (int64_t)y * W + x;
+  float* O = out + (int64_t)b * 2 * 64 * HW;
+  const int W8 = 8 * W;
+  for (int s = g * 16; s < g * 16 + 16; ++s) {
+    float m[9];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      m[k] = Ld<TM>::get(M, (int64_t)(k * 64 + s) * HW);
+      mx = fmaxf(mx, m[k]);
+    }
+    float den = 0.f, o0 = 0.f, o1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const float e = __expf(m[k] - mx);
+      den += e;
+      o0 += e * nf[k][0];
+      o1 += e * nf[k][1];
+    }
+    const float inv = 1.f / den;
+    const int64_t oy = 8 * y + (s >> 3), ox = 8 * x + (s & 7);
+    O[oy * W8 + ox] = o0 * inv;
+    O[64 * HW + oy * W8 + ox] = o1 * inv;
+  }
+}
+
+// d(mask) directly; per-cell neighbour weights Wk[k][c] = sum_s p_k(s) * dout_c(s) go to `wbuf`
+// (B, 18, H, W) and are gathered into d(flow) by convex_up_bwd_flow_kernel.
+template <typename TM>
+__global__ __launch_bounds__(256) void convex_up_bwd_kernel(const float* __restrict__ flow,
+                                                            const TM* __restrict__ mask,
+                                                            const float* __restrict__ dout,
+                                                            TM* __restrict__ dmask,
+                                                            float* __restrict__ wbuf, int H, int W) {
+  __shared__ float red[4][18][64];
+  const int xi = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int x = blockIdx.x * 64 + xi, y = blockIdx.y, b = blockIdx.z;
+  const bool active = x < W;
+  const int64_t HW = (int64_t)H * W;
+  float acc[9][2];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc[k][0] = acc[k][1] = 0.f;
+  if (active) {
+    const float* F = flow + (int64_t)b * 2 * HW;
+    float nf[9][2];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      nf[k][0] = ok ? 8.f * F[(int64_t)yy * W + xx] : 0.f;
+      nf[k][1] = ok ? 8.f * F[HW + (int64_t)yy * W + xx] : 0.f;
+    }
+    const int64_t cell = (int64_t)y * W + x;
+    const TM* M = mask + (int64_t)b * 576 * HW + cell;
+    TM* DM = dmask + (int64_t)b * 576 * HW + cell;
+    const float* DO = dout + (int64_t)b * 2 * 64 * HW;
+    const int W8 = 8 * W;
+    for (int s = g * 16; s < g * 16 + 16; ++s) {
+      float m[9];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        m[k] = Ld<TM>::get(M, (int64_t)(k * 64 + s) * HW);
+        mx = fmaxf(mx, m[k]);
+      }
+      float den = 0.f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        m[k] = __expf(m[k] - mx);
+        den += m[k];
+      }
+      const float inv = 1.f / den;
+      const int64_t oy = 8 * y + (s >> 3), ox = 8 * x + (s & 7);
+      const float d0 = DO[oy * W8 + ox], d1 = DO[64 * HW + oy * W8 + ox];
+      float gk[9], dot = 0.f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        m[k] *= inv;  // p_k
+        gk[k] = d0 * nf[k][0] + d1 * nf[k][1];
+        dot += m[k] * gk[k];
+        acc[k][0] += m[k] * d0;
+        acc[k][1] += m[k] * d1;
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k)
+        St<TM>::put(DM, (int64_t)(k * 64 + s) * HW, m[k] * (gk[k] - dot));
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    red[g][2 * k][xi] = acc[k][0];
+    red[g][2 * k + 1][xi] = acc[k][1];
+  }
+  __syncthreads();
+  // 18 x 64 partial sums reduced over the 4 groups; 256 threads cover 4.5 rounds
+  for (int e = threadIdx.x; e < 18 * 64; e += 256) {
+    const int c = e >> 6, xx = e & 63;
+    const int gx = blockIdx.x * 64 + xx;
+    if (gx < W) {
+      const float v = red[0][c][xx] + red[1][c][xx] + red[2][c][xx] + red[3][c][xx];
+      wbuf[((int64_t)b * 18 + c) * HW + (int64_t)y * W + gx] = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void convex_up_bwd_flow_kernel(const float* __restrict__ wbuf,
+                                                                 float* __restrict__ dflow, int B,
+                                                                 int H, int W) {
+  const int64_t HW = (int64_t)H * W;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)B * HW) return;
+  const int x = (int)(t % W), y = (int)((t / W) % H);
+  const int64_t b = t / HW;
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    // the cell whose neighbour k is (y, x)
+    const int cy = y - (k / 3 - 1), cx = x - (k % 3 - 1);
+    if (cy >= 0 && cy < H && cx >= 0 && cx < W) {
+      const int64_t o = (int64_t)cy * W + cx;
+      s0 += wbuf[(b * 18 + 2 * k) * HW + o];
+      s1 += wbuf[(b * 18 + 2 * k + 1) * HW + o];
+    }
+  }
+  dflow[(b * 2) * HW + (int64_t)y * W + x] = 8.f * s0;
+  dflow[(b * 2 + 1) * HW + (int64_t)y * W + x] = 8.f * s1;
+}
+
+}  // namespace
+
+bool launch_convex_up_fwd(const float* flow, const void* mask, int mask_is_bf16, float* out, int B,
+                          int H, int W, hipStream_t stream) {
+  dim3 grid(raft_cdiv(W, 64), H, B);
+  if (mask_is_bf16)
+    hipLaunchKernelGGL(convex_up_fwd_kernel<uint16_t>, grid, dim3(256), 0, stream, flow,
+                       (const uint16_t*)mask, out, H, W);
+  else
+    hipLaunchKernelGGL(convex_up_fwd_kernel<float>, grid, dim3(256), 0, stream, flow,
+                       (const float*)mask, out, H, W);
+  return true;
+}
+
+bool launch_convex_up_bwd(const float* flow, const void* mask, int mask_is_bf16, const float* dout,
+                          void* dmask, float* wbuf, float* dflow, int B, int H, int W,
+                          hipStream_t stream) {
+  dim3 grid(raft_cdiv(W, 64), H, B);
+  if (mask_is_bf16)
+    hipLaunchKernelGGL(convex_up_bwd_kernel<uint16_t>, grid, dim3(256), 0, stream, flow,
+                       (const uint16_t*)mask, dout, (uint16_t*)dmask, wbuf, H, W);
+  else
+    hipLaunchKernelGGL(convex_up_bwd_kernel<float>, grid, dim3(256), 0, stream, flow,
+                       (const float*)mask, dout, (float*)dmask, wbuf, H, W);
+  const int64_t total = (int64_t)B * H * W;
+  hipLaunchKernelGGL(convex_up_bwd_flow_kernel, dim3(raft_cdiv(total, 256)), dim3(256), 0, stream,
+                     wbuf, dflow, B, H, W);
+  return true;
+}

@@ -1,0 +1,155 @@
+"""Feature / context encoders.
+
+Behavioural parity with the reference encoders (`core/extractor.py:6-267`):
+
+* ``BasicEncoder``  (full model)  conv7x7/s2 3->64, norm, ReLU, 3 stages of two residual blocks
+  (64, 96/s2, 128/s2) and a 1x1 projection (`core/extractor.py:118-192`).
+* ``SmallEncoder``  (small model) same skeleton with bottleneck blocks 32 -> 32 -> 64 -> 96
+  (`core/extractor.py:195-267`).
+* A list/tuple input is run as ONE batched call and split back (`core/extractor.py:171-174,189-190`),
+  which is what lets fnet see both frames in a single set of kernel launches.
+
+State-dict schema is kept identical (`SURVEY.md` §2.5), including the strided residual block that
+registers the same norm module as both ``norm3`` and ``downsample.1`` (`core/extractor.py:26,44-45`).
+
+MI355X notes: the encoders are plain convolutions and stay on PyTorch-ROCm (MIOpen) under bf16
+autocast; ``to_channels_last()`` switches the weights to NHWC so MIOpen picks its NHWC implicit-GEMM
+solvers, which is the layout the rest of the HIP hot path consumes.
+"""
+import torch
+import torch.nn as nn
+
+
+def make_norm(kind, channels, groups=None):
+    """Normalisation factory used by every block (`core/extractor.py:14-36`)."""
+    if kind == 'group':
+        return nn.GroupNorm(num_groups=groups if groups is not None else channels // 8,
+                            num_channels=channels)
+    if kind == 'batch':
+        return nn.BatchNorm2d(channels)
+    if kind == 'instance':
+        return nn.InstanceNorm2d(channels)
+    if kind == 'none':
+        return nn.Sequential()
+    raise ValueError('unknown norm_fn %r' % (kind,))
+
+
+class ResidualBlock(nn.Module):
+    """Two 3x3 convs + identity / strided 1x1 shortcut (`core/extractor.py:6-56`)."""
+
+    def __init__(self, in_planes, planes, norm_fn='group', stride=1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(in_planes, planes, kernel_size=3, padding=1, stride=stride)
+        self.conv2 = nn.Conv2d(planes, planes, kernel_size=3, padding=1)
+        self.relu = nn.ReLU(inplace=True)
+        g = planes // 8
+        self.norm1 = make_norm(norm_fn, planes, g)
+        self.norm2 = make_norm(norm_fn, planes, g)
+        if stride == 1:
+            self.downsample = None
+        else:
+            # the same module object under two names -> both key sets appear in state_dict
+            self.norm3 = make_norm(norm_fn, planes, g)
+            self.downsample = nn.Sequential(
+                nn.Conv2d(in_planes, planes, kernel_size=1, stride=stride), self.norm3)
+
+    def forward(self, x):
+        y = self.relu(self.norm1(self.conv1(x)))
+        y = self.relu(self.norm2(self.conv2(y)))
+        if self.downsample is not None:
+            x = self.downsample(x)
+        return self.relu(x + y)
+
+
+class BottleneckBlock(nn.Module):
+    """1x1 -> 3x3 (strided) -> 1x1 bottleneck (`core/extractor.py:60-116`)."""
+
+    def __init__(self, in_planes, planes, norm_fn='group', stride=1):
+        super().__init__()
+        mid = planes // 4
+        self.conv1 = nn.Conv2d(in_planes, mid, kernel_size=1, padding=0)
+        self.conv2 = nn.Conv2d(mid, mid, kernel_size=3, padding=1, stride=stride)
+        self.conv3 = nn.Conv2d(mid, planes, kernel_size=1, padding=0)
+        self.relu = nn.ReLU(inplace=True)
+        g = planes // 8
+        self.norm1 = make_norm(norm_fn, mid, g)
+        self.norm2 = make_norm(norm_fn, mid, g)
+        self.norm3 = make_norm(norm_fn, planes, g)
+        if stride == 1:
+            self.downsample = None
+        else:
+            self.norm4 = make_norm(norm_fn, planes, g)
+            self.downsample = nn.Sequential(
+                nn.Conv2d(in_planes, planes, kernel_size=1, stride=stride), self.norm4)
+
+    def forward(self, x):
+        y = self.relu(self.norm1(self.conv1(x)))
+        y = self.relu(self.norm2(self.conv2(y)))
+        y = self.relu(self.norm3(self.conv3(y)))
+        if self.downsample is not None:
+            x = self.downsample(x)
+        return self.relu(x + y)
+
+
+class _Encoder(nn.Module):
+    """Shared skeleton of both encoders: stem, three 2-block stages, 1x1 head."""
+
+    block = None
+    widths = ()
+
+    def __init__(self, output_dim=128, norm_fn='batch', dropout=0.0):
+        super().__init__()
+        self.norm_fn = norm_fn
+        stem = self.widths[0]
+        self.norm1 = make_norm(norm_fn, stem, 8)
+        self.conv1 = nn.Conv2d(3, stem, kernel_size=7, stride=2, padding=3)
+        self.relu1 = nn.ReLU(inplace=True)
+
+        self.in_planes = stem
+        self.layer1 = self._make_layer(self.widths[1], stride=1)
+        self.layer2 = self._make_layer(self.widths[2], stride=2)
+        self.layer3 = self._make_layer(self.widths[3], stride=2)
+        self.conv2 = nn.Conv2d(self.widths[3], output_dim, kernel_size=1)
+        self.dropout = nn.Dropout2d(p=dropout) if dropout > 0 else None
+        self._init_weights()
+
+    def _init_weights(self):
+        # kaiming(fan_out) convs, unit/zero affine norms (`core/extractor.py:150-157`)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode='fan_out', nonlinearity='relu')
+            elif isinstance(m, (nn.BatchNorm2d, nn.InstanceNorm2d, nn.GroupNorm)):
+                if m.weight is not None:
+                    nn.init.constant_(m.weight, 1)
+                if m.bias is not None:
+                    nn.init.constant_(m.bias, 0)
+
+    def _make_layer(self, dim, stride=1):
+        first = self.block(self.in_planes, dim, self.norm_fn, stride=stride)
+        second = self.block(dim, dim, self.norm_fn, stride=1)
+        self.in_planes = dim
+        return nn.Sequential(first, second)
+
+    def forward(self, x):
+        batched = isinstance(x, (list, tuple))
+        if batched:
+            n = x[0].shape[0]
+            x = torch.cat(x, dim=0)
+        x = self.relu1(self.norm1(self.conv1(x)))
+        x = self.layer3(self.layer2(self.layer1(x)))
+        x = self.conv2(x)
+        if self.training and self.dropout is not None:
+            x = self.dropout(x)
+        if batched:
+            x = torch.split(x, [n, n], dim=0)
+        return x
+
+
+class BasicEncoder(_Encoder):
+    block = ResidualBlock
+    widths = (64, 64, 96, 128)
+
+
+class SmallEncoder(_Encoder):
+    block = BottleneckBlock
+    widths = (32, 32, 64, 96)

@@ -1,0 +1,142 @@
+"""RAFT (Recurrent All-Pairs Field Transforms) -- the one model family of the reference.
+
+API and numerics contract follow `core/raft.py:24-144` (`SURVEY.md` §2.7):
+
+* ``RAFT(args)`` reads ``args.small`` / ``args.mixed_precision`` (+ optional ``dropout``,
+  ``alternate_corr``) and WRITES ``args.corr_levels`` / ``args.corr_radius`` (preserved quirk).
+* ``forward(image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False)`` takes float
+  0..255 (B,3,H,W) images and returns the list of ``iters`` full-resolution flows, or
+  ``(flow_low, flow_up)`` in test mode.
+
+MI355X-specific extensions (all optional ``args`` attributes, defaults chosen for gfx950):
+
+* ``corr_impl``   'auto' (HIP kernels on GPU, torch on CPU) | 'hip' | 'torch'
+* ``amp_dtype``   autocast dtype for ``mixed_precision`` -- 'bfloat16' (default; MI355X MFMA native)
+                  or 'float16' (reference behaviour on CUDA)
+* ``channels_last`` run the encoders in NHWC (MIOpen's NHWC implicit-GEMM solvers)
+
+In test mode the convex upsampling runs only after the last iteration (the reference computes and
+discards it every iteration, `core/raft.py:133-142`); outputs are identical.
+"""
+import torch
+import torch.nn as nn
+
+from .update import BasicUpdateBlock, SmallUpdateBlock
+from .extractor import BasicEncoder, SmallEncoder
+from .corr import CorrBlock, AlternateCorrBlock
+from ..utils.utils import coords_grid, upflow8
+from ..ops.upsample import convex_upsample
+
+
+def _get(args, name, default):
+    return getattr(args, name, default)
+
+
+class RAFT(nn.Module):
+    def __init__(self, args):
+        super().__init__()
+        self.args = args
+        if args.small:
+            self.hidden_dim = hdim = 96
+            self.context_dim = cdim = 64
+            args.corr_levels = 4
+            args.corr_radius = 3
+        else:
+            self.hidden_dim = hdim = 128
+            self.context_dim = cdim = 128
+            args.corr_levels = 4
+            args.corr_radius = 4
+        if not hasattr(self.args, 'dropout'):
+            self.args.dropout = 0
+        if not hasattr(self.args, 'alternate_corr'):
+            self.args.alternate_corr = False
+
+        if args.small:
+            self.fnet = SmallEncoder(output_dim=128, norm_fn='instance', dropout=args.dropout)
+            self.cnet = SmallEncoder(output_dim=hdim + cdim, norm_fn='none', dropout=args.dropout)
+            self.update_block = SmallUpdateBlock(self.args, hidden_dim=hdim)
+        else:
+            self.fnet = BasicEncoder(output_dim=256, norm_fn='instance', dropout=args.dropout)
+            self.cnet = BasicEncoder(output_dim=hdim + cdim, norm_fn='batch', dropout=args.dropout)
+            self.update_block = BasicUpdateBlock(self.args, hidden_dim=hdim)
+
+    # ------------------------------------------------------------------ configuration helpers
+    @property
+    def corr_impl(self):
+        return _get(self.args, 'corr_impl', 'auto')
+
+    @property
+    def amp_dtype(self):
+        name = _get(self.args, 'amp_dtype', 'bfloat16')
+        return {'bfloat16': torch.bfloat16, 'bf16': torch.bfloat16,
+                'float16': torch.float16, 'fp16': torch.float16}[name]
+
+    def _autocast(self, device):
+        enabled = bool(self.args.mixed_precision) and device.type == 'cuda'
+        return torch.autocast(device_type=device.type, dtype=self.amp_dtype, enabled=enabled)
+
+    def freeze_bn(self):
+        for m in self.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.eval()
+
+    def initialize_flow(self, img):
+        """flow = coords1 - coords0 on the 1/8 grid."""
+        n, _, h, w = img.shape
+        coords0 = coords_grid(n, h // 8, w // 8, device=img.device)
+        coords1 = coords_grid(n, h // 8, w // 8, device=img.device)
+        return coords0, coords1
+
+    def upsample_flow(self, flow, mask):
+        """[H/8, W/8, 2] -> [H, W, 2] convex combination (HIP kernel on GPU)."""
+        impl = 'torch' if self.corr_impl == 'torch' else 'auto'
+        return convex_upsample(flow, mask, impl=impl)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False):
+        image1 = (2 * (image1 / 255.0) - 1.0).contiguous()
+        image2 = (2 * (image2 / 255.0) - 1.0).contiguous()
+        hdim, cdim = self.hidden_dim, self.context_dim
+        dev = image1.device
+        cl = bool(_get(self.args, 'channels_last', False))
+        if cl:
+            image1 = image1.contiguous(memory_format=torch.channels_last)
+            image2 = image2.contiguous(memory_format=torch.channels_last)
+
+        with self._autocast(dev):
+            fmap1, fmap2 = self.fnet([image1, image2])
+        fmap1 = fmap1.float().contiguous()
+        fmap2 = fmap2.float().contiguous()
+        block = AlternateCorrBlock if self.args.alternate_corr else CorrBlock
+        corr_fn = block(fmap1, fmap2, radius=self.args.corr_radius, impl=self.corr_impl)
+
+        with self._autocast(dev):
+            cnet = self.cnet(image1)
+            net, inp = torch.split(cnet, [hdim, cdim], dim=1)
+            net = torch.tanh(net)
+            inp = torch.relu(inp)
+
+        coords0, coords1 = self.initialize_flow(image1)
+        if flow_init is not None:
+            coords1 = coords1 + flow_init
+
+        flow_predictions = []
+        flow_up = None
+        for itr in range(iters):
+            coords1 = coords1.detach()
+            corr = corr_fn(coords1)
+            flow = coords1 - coords0
+            with self._autocast(dev):
+                net, up_mask, delta_flow = self.update_block(net, inp, corr, flow)
+            coords1 = coords1 + delta_flow
+            if test_mode and itr < iters - 1:
+                continue
+            if up_mask is None:
+                flow_up = upflow8(coords1 - coords0)
+            else:
+                flow_up = self.upsample_flow(coords1 - coords0, up_mask)
+            flow_predictions.append(flow_up)
+
+        if test_mode:
+            return coords1 - coords0, flow_up
+        return flow_predictions

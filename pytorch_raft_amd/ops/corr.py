@@ -1,0 +1,156 @@
+"""Autograd wrappers around the HIP correlation kernels.
+
+Design (MI355X-first, see `SURVEY.md` §7.4 item 3):
+
+* ``AllPairsVolume`` builds the 4-level all-pairs pyramid with ONE fused MFMA kernel
+  (csrc/kernels/corr_allpairs.hip) instead of bmm + 3 avg_pool2d (`core/corr.py:19-27,52-60`).
+* The pyramid is produced by an autograd node that outputs a 0-d *token*; every per-iteration
+  lookup consumes that token.  Lookup backward accumulates straight into ONE pyramid-gradient buffer
+  owned by the volume (race-free RMW, csrc/kernels/corr_lookup.hip) and returns an empty token grad.
+  Autograd runs the build node's backward only after all lookups' backward, at which point a single
+  pass folds the pyramid gradient (avg-pool adjoint, 1/sqrt(C)) and two GEMMs produce d(fmap1),
+  d(fmap2).  The reference instead allocates + zero-fills a dense plane-sized gradient per level per
+  iteration inside grid_sample backward and lets autograd add them up.
+* ``OnTheFlyVolume`` is the differentiable counterpart of the reference's forward-only
+  ``alt_cuda_corr`` (csrc/kernels/corr_onthefly.hip) with the same token scheme for d(fmap2 levels).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+
+def available(required=False):
+    return _ext.gpu_path_enabled(required=required)
+
+
+class _State:
+    """Mutable holder shared between the build node and its lookups."""
+
+    def __init__(self):
+        self.grad = None
+        self.grad_f1 = None
+
+
+class _AllPairsBuild(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fmap1, fmap2, levels, state):
+        ops = _ext.ops()
+        pyr = ops.corr_build(fmap1, fmap2, levels)
+        state.pyramid = pyr
+        ctx.state = state
+        ctx.save_for_backward(fmap1, fmap2)
+        token = fmap1.new_zeros(())
+        return token
+
+    @staticmethod
+    def backward(ctx, _dtoken):
+        st = ctx.state
+        fmap1, fmap2 = ctx.saved_tensors
+        if st.grad is None:
+            return None, None, None, None
+        b, c, h, w = fmap1.shape
+        dcorr = _ext.ops().corr_pyr_grad_reduce(st.grad, 1.0 / math.sqrt(c))  # (B, N, N)
+        st.grad = None
+        st.pyramid = None
+        f1 = fmap1.view(b, c, h * w)
+        f2 = fmap2.view(b, c, h * w)
+        # dF1 = F2 dC^T, dF2 = F1 dC  (library GEMMs: plain fp32 bmm)
+        g1 = torch.bmm(f2, dcorr.transpose(1, 2)).view(b, c, h, w)
+        g2 = torch.bmm(f1, dcorr).view(b, c, h, w)
+        return g1, g2, None, None
+
+
+class _AllPairsLookup(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, token, coords, radius, state):
+        out = _ext.ops().corr_lookup_fwd(state.pyramid, coords, radius)
+        ctx.state = state
+        ctx.radius = radius
+        ctx.save_for_backward(coords)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        st = ctx.state
+        (coords,) = ctx.saved_tensors
+        if st.grad is None:
+            st.grad = [torch.zeros_like(p) for p in st.pyramid]
+        _ext.ops().corr_lookup_bwd_(st.grad, coords, dout.contiguous().float(), ctx.radius)
+        return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None
+
+
+class AllPairsVolume:
+    def __init__(self, fmap1, fmap2, num_levels=4):
+        self.state = _State()
+        self.levels = num_levels
+        self.token = _AllPairsBuild.apply(fmap1.contiguous(), fmap2.contiguous(), num_levels,
+                                          self.state)
+
+    @property
+    def pyramid(self):
+        return self.state.pyramid
+
+    def lookup(self, coords, radius):
+        return _AllPairsLookup.apply(self.token, coords.contiguous().float(), radius, self.state)
+
+
+def _pool_nhwc(x):
+    # avg-pool 2x2 (floor) on an NHWC tensor via the NCHW view, returned NHWC-contiguous
+    return F.avg_pool2d(x.permute(0, 3, 1, 2), 2, stride=2).permute(0, 2, 3, 1).contiguous()
+
+
+class _OTFBuild(torch.autograd.Function):
+    """fmap1 (B,C,H,W), pyramid of fmap2 (list) -> token; keeps NHWC copies in ``state``."""
+
+    @staticmethod
+    def forward(ctx, fmap1, *args):
+        state = args[-1]
+        f2_levels = args[:-1]
+        state.f1 = fmap1.permute(0, 2, 3, 1).contiguous()
+        state.f2 = [f.permute(0, 2, 3, 1).contiguous() for f in f2_levels]
+        ctx.state = state
+        ctx.nlev = len(f2_levels)
+        return fmap1.new_zeros(())
+
+    @staticmethod
+    def backward(ctx, _dtoken):
+        st = ctx.state
+        if st.grad is None:
+            return (None,) * (ctx.nlev + 2)
+        g1 = st.grad_f1.permute(0, 3, 1, 2)
+        g2 = [g.permute(0, 3, 1, 2) for g in st.grad]
+        st.grad = st.grad_f1 = None
+        return (g1, *g2, None)
+
+
+class _OTFLookup(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, token, coords, radius, state):
+        out = _ext.ops().corr_otf_fwd(state.f1, state.f2, coords, radius)  # (B,H,W,L*D*D)
+        ctx.state = state
+        ctx.radius = radius
+        ctx.save_for_backward(coords)
+        return out.permute(0, 3, 1, 2)  # NCHW-shaped, channels_last strides
+
+    @staticmethod
+    def backward(ctx, dout):
+        st = ctx.state
+        (coords,) = ctx.saved_tensors
+        if st.grad is None:
+            st.grad = [torch.zeros_like(f) for f in st.f2]
+            st.grad_f1 = torch.zeros_like(st.f1)
+        d = dout.float().permute(0, 2, 3, 1).contiguous()
+        _ext.ops().corr_otf_bwd_(st.f1, st.f2, coords, d, st.grad_f1, st.grad, ctx.radius)
+        return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None
+
+
+class OnTheFlyVolume:
+    def __init__(self, fmap1, fmap2_pyramid):
+        self.state = _State()
+        self.token = _OTFBuild.apply(fmap1.contiguous(), *fmap2_pyramid, self.state)
+
+    def lookup(self, coords, radius):
+        return _OTFLookup.apply(self.token, coords.contiguous().float(), radius, self.state)

@@ -1,0 +1,42 @@
+"""Convex 8x flow upsampling (reference `core/raft.py:72-83`) -- HIP kernel + pure-torch oracle."""
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+
+def torch_convex_upsample(flow, mask):
+    """Reference-semantics implementation (also the CPU path)."""
+    n, _, h, w = flow.shape
+    m = mask.view(n, 1, 9, 8, 8, h, w)
+    m = torch.softmax(m, dim=2)
+    up = F.unfold(8 * flow, [3, 3], padding=1).view(n, 2, 9, 1, 1, h, w)
+    up = torch.sum(m * up, dim=2)
+    up = up.permute(0, 1, 4, 2, 5, 3)
+    return up.reshape(n, 2, 8 * h, 8 * w)
+
+
+class _ConvexUpsample(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flow, mask):
+        flow = flow.contiguous().float()
+        mask = mask.contiguous()
+        if mask.dtype not in (torch.float32, torch.bfloat16):
+            mask = mask.float()
+        ctx.save_for_backward(flow, mask)
+        ctx.mask_dtype = mask.dtype
+        return _ext.ops().convex_up_fwd(flow, mask)
+
+    @staticmethod
+    def backward(ctx, dout):
+        flow, mask = ctx.saved_tensors
+        dflow, dmask = _ext.ops().convex_up_bwd(flow, mask, dout.contiguous().float())
+        return dflow, dmask
+
+
+def convex_upsample(flow, mask, impl='auto'):
+    if impl != 'torch' and flow.is_cuda and _ext.gpu_path_enabled(required=(impl == 'hip')):
+        out_dtype = torch.promote_types(flow.dtype, mask.dtype)
+        out = _ConvexUpsample.apply(flow, mask)
+        return out if out_dtype == torch.float32 else out.to(out_dtype)
+    return torch_convex_upsample(flow, mask)

@@ -1,0 +1,147 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (GPU only)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_raft_amd.models.corr import (torch_corr_pyramid, torch_corr_lookup,
+                                          torch_onthefly_corr, CorrBlock, AlternateCorrBlock)
+from pytorch_raft_amd.ops.upsample import torch_convex_upsample, convex_upsample
+from pytorch_raft_amd.ops.loss import torch_sequence_loss, sequence_loss
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _coords(b, h, w, spread=6.0, seed=0):
+    g = torch.Generator(device='cpu').manual_seed(seed)
+    ys, xs = torch.meshgrid(torch.arange(h).float(), torch.arange(w).float(), indexing='ij')
+    base = torch.stack([xs, ys])[None].repeat(b, 1, 1, 1)
+    c = base + spread * torch.randn(b, 2, h, w, generator=g)
+    # a few far out-of-range coordinates exercise the zero padding
+    c[:, :, 0, 0] = -50.0
+    c[:, :, -1, -1] = 500.0
+    return c.to(DEV)
+
+
+@pytest.mark.parametrize('shape', [(2, 256, 16, 20), (1, 256, 46, 62), (2, 128, 13, 19)])
+def test_corr_build_matches_torch(ext_ops, shape):
+    b, c, h, w = shape
+    f1 = torch.randn(shape, device=DEV)
+    f2 = torch.randn(shape, device=DEV)
+    levels = 4 if min(h, w) >= 16 else 3
+    got = ext_ops.corr_build(f1, f2, levels)
+    ref = torch_corr_pyramid(f1, f2, levels)
+    for g, r in zip(got, ref):
+        r = r.view(b, h * w, *r.shape[-2:])
+        assert g.shape == r.shape
+        torch.testing.assert_close(g, r, atol=2e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize('radius,c', [(4, 256), (3, 128)])
+@pytest.mark.parametrize('hw', [(16, 20), (13, 19)])
+def test_lookup_fwd_bwd_matches_grid_sample(ext_ops, radius, c, hw):
+    h, w = hw
+    b = 2
+    f1 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    f2 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    coords = _coords(b, h, w)
+    levels = 3 if min(h, w) < 16 else 4
+
+    # torch oracle through grid_sample autograd
+    pyr = torch_corr_pyramid(f1, f2, levels)
+    ref = torch_corr_lookup(pyr, coords, radius)
+    gout = torch.randn_like(ref)
+    (ref * gout).sum().backward()
+    g1_ref, g2_ref = f1.grad.clone(), f2.grad.clone()
+    f1.grad = f2.grad = None
+
+    blk = CorrBlock(f1, f2, num_levels=levels, radius=radius, impl='hip')
+    assert blk.hip
+    out = blk(coords)
+    torch.testing.assert_close(out, ref, atol=2e-4, rtol=1e-4)
+    # two lookups share the volume -> gradients accumulate in the persistent buffer
+    out2 = blk(coords + 0.37)
+    ref2 = torch_corr_lookup(pyr, coords + 0.37, radius)
+    torch.testing.assert_close(out2, ref2, atol=2e-4, rtol=1e-4)
+    (out * gout).sum().backward()
+    torch.testing.assert_close(f1.grad, g1_ref, atol=2e-3, rtol=1e-3)
+    torch.testing.assert_close(f2.grad, g2_ref, atol=2e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize('radius,c', [(4, 256), (3, 128)])
+def test_onthefly_matches_allpairs(ext_ops, radius, c):
+    b, h, w = 2, 16, 24
+    f1 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    f2 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    coords = _coords(b, h, w, seed=3)
+    pyr = torch_corr_pyramid(f1, f2, 4)
+    ref = torch_corr_lookup(pyr, coords, radius)
+    gout = torch.randn_like(ref)
+    (ref * gout).sum().backward()
+    g1_ref, g2_ref = f1.grad.clone(), f2.grad.clone()
+    f1.grad = f2.grad = None
+
+    blk = AlternateCorrBlock(f1, f2, num_levels=4, radius=radius, impl='hip')
+    assert blk.hip
+    out = blk(coords)
+    torch.testing.assert_close(out, ref, atol=2e-4, rtol=1e-4)
+    (out * gout).sum().backward()
+    torch.testing.assert_close(f1.grad, g1_ref, atol=2e-3, rtol=1e-3)
+    torch.testing.assert_close(f2.grad, g2_ref, atol=2e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize('mask_dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('hw', [(8, 9), (46, 62), (5, 70)])
+def test_convex_upsample_fwd_bwd(ext_ops, mask_dtype, hw):
+    h, w = hw
+    b = 2
+    flow = torch.randn(b, 2, h, w, device=DEV, requires_grad=True)
+    mask = (3 * torch.randn(b, 576, h, w, device=DEV)).to(mask_dtype).requires_grad_(True)
+    ref = torch_convex_upsample(flow, mask.float())
+    g = torch.randn_like(ref)
+    (ref * g).sum().backward()
+    gf_ref, gm_ref = flow.grad.clone(), mask.grad.clone().float()
+    flow.grad = mask.grad = None
+    out = convex_upsample(flow, mask, impl='hip')
+    torch.testing.assert_close(out.float(), ref, atol=1e-4, rtol=1e-4)
+    (out.float() * g).sum().backward()
+    torch.testing.assert_close(flow.grad, gf_ref, atol=1e-3, rtol=1e-4)
+    tol = 1e-4 if mask_dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(mask.grad.float(), gm_ref, atol=tol, rtol=tol)
+
+
+def test_sequence_loss_fwd_bwd(ext_ops):
+    b, h, w, n = 2, 40, 56, 5
+    gt = 30 * torch.randn(b, 2, h, w, device=DEV)
+    gt[0, :, :4] = 500.0  # beyond MAX_FLOW -> masked
+    valid = (torch.rand(b, h, w, device=DEV) > 0.2).float()
+    preds = [(gt + torch.randn_like(gt) * (i + 1)).requires_grad_(True) for i in range(n)]
+    lr, mr = torch_sequence_loss(preds, gt, valid, 0.8)
+    lr.backward()
+    gref = [p.grad.clone() for p in preds]
+    for p in preds:
+        p.grad = None
+    lh, mh = sequence_loss(preds, gt, valid, 0.8, impl='hip')
+    torch.testing.assert_close(lh, lr, atol=1e-5, rtol=1e-5)
+    for k in ('epe', '1px', '3px', '5px'):
+        torch.testing.assert_close(mh[k], mr[k], atol=1e-5, rtol=1e-5)
+    lh.backward()
+    for p, g in zip(preds, gref):
+        torch.testing.assert_close(p.grad, g, atol=1e-9, rtol=1e-5)
+
+
+def test_lookup_deterministic(ext_ops):
+    b, c, h, w = 2, 256, 16, 16
+    f1 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    f2 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    coords = _coords(b, h, w)
+    grads = []
+    for _ in range(2):
+        blk = CorrBlock(f1, f2, radius=4, impl='hip')
+        out = blk(coords)
+        out.square().sum().backward()
+        grads.append((f1.grad.clone(), f2.grad.clone()))
+        f1.grad = f2.grad = None
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
