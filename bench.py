@@ -41,7 +41,23 @@ def parse(argv=None):
     ap.add_argument('--small', action='store_true')
     ap.add_argument('--profile', type=str, default=None, help='torch.profiler trace dir')
     ap.add_argument('--json_out', type=str, default=None)
+    ap.add_argument('--roctx_region', action='store_true',
+                    help='bracket the timed steps with roctxProfilerResume/Pause '
+                         '(use with rocprofv3 --selected-regions)')
     return ap.parse_args(argv)
+
+
+def _roctx():
+    import ctypes
+    for name in ('librocprofiler-sdk-roctx.so.1', '/opt/rocm/lib/librocprofiler-sdk-roctx.so'):
+        try:
+            lib = ctypes.CDLL(name)
+            lib.roctxProfilerResume.argtypes = [ctypes.c_uint64]
+            lib.roctxProfilerPause.argtypes = [ctypes.c_uint64]
+            return lib
+        except OSError:
+            continue
+    return None
 
 
 def main(argv=None):
@@ -109,12 +125,17 @@ def main(argv=None):
         from torch.profiler import profile, ProfilerActivity
         prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=False)
         prof.__enter__()
+    roctx = _roctx() if a.roctx_region else None
+    if roctx is not None:
+        roctx.roctxProfilerResume(0)
     t0 = time.perf_counter()
     run(a.steps)
     if device.type == 'cuda':
         torch.cuda.synchronize()
     pdist.barrier(device)
     elapsed = time.perf_counter() - t0
+    if roctx is not None:
+        roctx.roctxProfilerPause(0)
     if prof is not None:
         prof.__exit__(None, None, None)
         os.makedirs(a.profile, exist_ok=True)

@@ -1,0 +1,7 @@
+"""Make the repo root importable so the flat `core/` compat modules can re-export the package."""
+import os
+import sys
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _ROOT not in sys.path:
+    sys.path.insert(0, _ROOT)

@@ -289,6 +289,40 @@ std::vector<Tensor> seq_loss_bwd(const std::vector<Tensor>& preds, const Tensor&
   return grads;
 }
 
+// ------------------------------------------------------------------ warping sampler
+void check_warp(const Tensor& img, const Tensor& flow) {
+  check_cuda_f32(img, "image");
+  check_cuda_f32(flow, "flow");
+  TORCH_CHECK(img.dim() == 4 && flow.dim() == 4 && flow.size(1) == 2 && img.size(0) == flow.size(0) &&
+                  img.size(2) == flow.size(2) && img.size(3) == flow.size(3),
+              "image (B,C,H,W) and flow (B,2,H,W) must match");
+}
+
+Tensor warp_fwd(const Tensor& img, const Tensor& flow, double sx, double bx, double sy, double by) {
+  check_warp(img, flow);
+  c10::DeviceGuard g(img.device());
+  Tensor out = at::empty_like(img);
+  launch_warp_fwd(img.data_ptr<float>(), flow.data_ptr<float>(), out.data_ptr<float>(),
+                  (int)img.size(0), (int)img.size(1), (int)img.size(2), (int)img.size(3), (float)sx,
+                  (float)bx, (float)sy, (float)by, cur_stream());
+  return out;
+}
+
+std::vector<Tensor> warp_bwd(const Tensor& img, const Tensor& flow, const Tensor& dout, double sx,
+                             double bx, double sy, double by) {
+  check_warp(img, flow);
+  check_cuda_f32(dout, "grad_out");
+  TORCH_CHECK(dout.sizes() == img.sizes(), "grad_out shape mismatch");
+  c10::DeviceGuard g(img.device());
+  Tensor dimg = at::zeros_like(img);
+  Tensor dflow = at::empty_like(flow);
+  launch_warp_bwd(img.data_ptr<float>(), flow.data_ptr<float>(), dout.data_ptr<float>(),
+                  dimg.data_ptr<float>(), dflow.data_ptr<float>(), (int)img.size(0),
+                  (int)img.size(1), (int)img.size(2), (int)img.size(3), (float)sx, (float)bx,
+                  (float)sy, (float)by, cur_stream());
+  return {dimg, dflow};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(raft_amd, m) {
@@ -302,6 +336,8 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout) -> Tensor[]");
   m.def("seq_loss_fwd(Tensor[] preds, Tensor gt, Tensor valid, float gamma, float max_flow) -> Tensor");
   m.def("seq_loss_bwd(Tensor[] preds, Tensor gt, Tensor valid, Tensor dloss, float gamma, float max_flow) -> Tensor[]");
+  m.def("warp_fwd(Tensor img, Tensor flow, float sx, float bx, float sy, float by) -> Tensor");
+  m.def("warp_bwd(Tensor img, Tensor flow, Tensor dout, float sx, float bx, float sy, float by) -> Tensor[]");
 }
 
 TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
@@ -315,4 +351,6 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("convex_up_bwd", &convex_up_bwd);
   m.impl("seq_loss_fwd", &seq_loss_fwd);
   m.impl("seq_loss_bwd", &seq_loss_bwd);
+  m.impl("warp_fwd", &warp_fwd);
+  m.impl("warp_bwd", &warp_bwd);
 }

@@ -50,3 +50,10 @@ void launch_seq_loss_fwd(const PredPtrs& preds, int n, const float* gt, const fl
 void launch_seq_loss_bwd(const PredPtrs& preds, const PredPtrsMut& grads, int n, const float* gt,
                          const float* valid, const float* dloss, float gamma, float max_flow, int B,
                          int64_t HW, hipStream_t stream);
+
+// ---- flow warping sampler (sampler.hip)
+void launch_warp_fwd(const float* img, const float* flow, float* out, int B, int C, int H, int W,
+                     float sx, float bx, float sy, float by, hipStream_t stream);
+void launch_warp_bwd(const float* img, const float* flow, const float* dout, float* dimg,
+                     float* dflow, int B, int C, int H, int W, float sx, float bx, float sy,
+                     float by, hipStream_t stream);

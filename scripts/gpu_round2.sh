@@ -1,0 +1,9 @@
+#!/bin/bash
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 --channels_last > gpurun_out/bench_hip_cl.log 2>&1
+rc=$?; tail -1 gpurun_out/bench_hip_cl.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+bash scripts/gpu_profile.sh hip && bash scripts/gpu_profile.sh hipcl --channels_last
