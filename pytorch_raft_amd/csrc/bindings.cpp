@@ -323,6 +323,89 @@ std::vector<Tensor> warp_bwd(const Tensor& img, const Tensor& flow, const Tensor
   return {dimg, dflow};
 }
 
+// ------------------------------------------------------------------ implicit-GEMM convolution
+// All activations are NHWC bf16 tensors of shape (B, H, W, C_buffer); a "segment" is a channel
+// slice [off, off + cnt) of such a buffer.  Geometry is validated here so the kernel's pointer
+// arithmetic can never leave an allocation.
+void check_nhwc(const Tensor& t, int64_t B, int64_t H, int64_t W, const char* name, at::ScalarType st) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), name, " must be a contiguous GPU tensor");
+  TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
+  TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(1) == H && t.size(2) == W, name,
+              " must be (B,H,W,C) matching the conv geometry");
+}
+
+void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_off,
+               const std::vector<int64_t>& in_cnt, const Tensor& wpk,
+               const c10::optional<Tensor>& bias, int64_t kh, int64_t kw, int64_t ph, int64_t pw,
+               int64_t cout, int64_t cin_small, int64_t epi, int64_t bn, double scale,
+               int64_t split, const std::vector<Tensor>& outs, const std::vector<int64_t>& out_off,
+               const std::vector<Tensor>& aux, const std::vector<int64_t>& aux_off) {
+  TORCH_CHECK(!ins.empty() && ins.size() <= 3, "1..3 input segments");
+  TORCH_CHECK(in_off.size() == ins.size() && in_cnt.size() == ins.size(), "segment spec mismatch");
+  TORCH_CHECK(bn == 128 || bn == 64 || bn == 32, "bn must be 128/64/32");
+  const int64_t B = ins[0].size(0), H = ins[0].size(1), W = ins[0].size(2);
+  c10::DeviceGuard g(ins[0].device());
+  ConvFwdArgs a{};
+  a.nseg = (int)ins.size();
+  int64_t cin_pad = 0;
+  for (size_t s = 0; s < ins.size(); ++s) {
+    check_nhwc(ins[s], B, H, W, "conv input", at::kBFloat16);
+    TORCH_CHECK(in_off[s] >= 0 && in_off[s] + in_cnt[s] <= ins[s].size(3), "segment out of range");
+    TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
+    if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 32 == 0, "segment channels must be a multiple of 32");
+    a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
+    a.seg[s].stride = (int)ins[s].size(3);
+    a.seg[s].cnt = (int)in_cnt[s];
+    cin_pad += in_cnt[s];
+  }
+  a.cin_pad = (int)cin_pad;
+  a.cin_small = (int)cin_small;
+  if (cin_small) TORCH_CHECK(ins.size() == 1 && cin_small <= in_cnt[0], "small-Cin path takes one segment");
+  a.B = (int)B; a.H = (int)H; a.W = (int)W;
+  a.KH = (int)kh; a.KW = (int)kw; a.PH = (int)ph; a.PW = (int)pw;
+  TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == at::kBFloat16 && wpk.dim() == 2,
+              "packed weight must be a contiguous bf16 (Npad, Kpad) tensor");
+  const int64_t kneed = cin_small ? ((kh * kw * cin_small + 31) / 32) * 32 : kh * kw * cin_pad;
+  TORCH_CHECK(wpk.size(1) == kneed, "packed weight K mismatch: ", wpk.size(1), " vs ", kneed);
+  TORCH_CHECK(wpk.size(0) >= ((cout + bn - 1) / bn) * bn, "packed weight has too few rows");
+  a.wpk = reinterpret_cast<const uint16_t*>(wpk.data_ptr<at::BFloat16>());
+  a.kpad = (int)wpk.size(1);
+  if (bias.has_value() && bias->defined()) {
+    check_cuda_f32(*bias, "bias");
+    TORCH_CHECK(bias->numel() >= cout, "bias too short");
+    a.bias = bias->data_ptr<float>();
+  }
+  a.cout = (int)cout;
+  a.scale = (float)scale;
+  a.split = (int)split;
+  const bool f32out = (epi == EPI_F32 || epi == EPI_ACC_F32);
+  const int64_t need_out = (epi == EPI_GRU_ZR) ? 3 : (epi == EPI_GRU_Q ? 2 : 1);
+  TORCH_CHECK((int64_t)outs.size() == need_out && out_off.size() == outs.size(), "wrong output count");
+  const int64_t out_ch[3] = {epi == EPI_GRU_ZR ? split : cout, epi == EPI_GRU_ZR ? cout - split : cout,
+                             cout - split};
+  void** optr[3] = {&a.out0, &a.out1, &a.out2};
+  int* ostr[3] = {&a.out0_stride, &a.out1_stride, &a.out2_stride};
+  for (size_t o = 0; o < outs.size(); ++o) {
+    check_nhwc(outs[o], B, H, W, "conv output", f32out ? at::kFloat : at::kBFloat16);
+    TORCH_CHECK(out_off[o] >= 0 && out_off[o] + out_ch[o] <= outs[o].size(3), "output slice out of range");
+    *optr[o] = f32out ? (void*)(outs[o].data_ptr<float>() + out_off[o])
+                      : (void*)(reinterpret_cast<uint16_t*>(outs[o].data_ptr<at::BFloat16>()) + out_off[o]);
+    *ostr[o] = (int)outs[o].size(3);
+  }
+  const int64_t need_aux = (epi == EPI_GRU_ZR) ? 1 : (epi == EPI_GRU_Q ? 2 : 0);
+  TORCH_CHECK((int64_t)aux.size() == need_aux && aux_off.size() == aux.size(), "wrong aux count");
+  const uint16_t** aptr[2] = {&a.aux0, &a.aux1};
+  int* astr[2] = {&a.aux0_stride, &a.aux1_stride};
+  for (size_t o = 0; o < aux.size(); ++o) {
+    check_nhwc(aux[o], B, H, W, "conv aux", at::kBFloat16);
+    const int64_t ch = (epi == EPI_GRU_ZR) ? cout - split : cout;
+    TORCH_CHECK(aux_off[o] >= 0 && aux_off[o] + ch <= aux[o].size(3), "aux slice out of range");
+    *aptr[o] = reinterpret_cast<const uint16_t*>(aux[o].data_ptr<at::BFloat16>()) + aux_off[o];
+    *astr[o] = (int)aux[o].size(3);
+  }
+  TORCH_CHECK(launch_conv_fwd(a, (int)epi, (int)bn, cin_small != 0, cur_stream()), "bad epilogue");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(raft_amd, m) {
@@ -338,6 +421,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("seq_loss_bwd(Tensor[] preds, Tensor gt, Tensor valid, Tensor dloss, float gamma, float max_flow) -> Tensor[]");
   m.def("warp_fwd(Tensor img, Tensor flow, float sx, float bx, float sy, float by) -> Tensor");
   m.def("warp_bwd(Tensor img, Tensor flow, Tensor dout, float sx, float bx, float sy, float by) -> Tensor[]");
+  m.def("conv_fwd_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, Tensor? bias, int kh, int kw, int ph, int pw, int cout, int cin_small, int epi, int bn, float scale, int split, Tensor(a!)[] outs, int[] out_off, Tensor[] aux, int[] aux_off) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
@@ -353,4 +437,5 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("seq_loss_bwd", &seq_loss_bwd);
   m.impl("warp_fwd", &warp_fwd);
   m.impl("warp_bwd", &warp_bwd);
+  m.impl("conv_fwd_", &conv_fwd_);
 }

@@ -57,3 +57,45 @@ void launch_warp_fwd(const float* img, const float* flow, float* out, int B, int
 void launch_warp_bwd(const float* img, const float* flow, const float* dout, float* dimg,
                      float* dflow, int B, int C, int H, int W, float sx, float bx, float sy,
                      float by, hipStream_t stream);
+
+// ---- implicit-GEMM convolution (conv_igemm.hip / conv_wgrad.hip)
+enum ConvEpilogue {
+  EPI_BF16 = 0,       // out0 bf16 = (acc + bias) * scale
+  EPI_RELU_BF16 = 1,  // out0 bf16 = relu(acc + bias)
+  EPI_F32 = 2,        // out0 f32 = (acc + bias) * scale
+  EPI_ACC_F32 = 3,    // out0 f32 += (acc + bias) * scale
+  EPI_GRU_ZR = 4,     // n < split: out0 = sigmoid (z); else out1 = sigmoid * aux0 (r*h), out2 = r
+  EPI_GRU_Q = 5,      // q = tanh; out0 = aux0 + aux1 * (q - aux0) (h'), out1 = q
+};
+
+struct Seg {
+  const uint16_t* ptr;  // bf16 NHWC base, already offset to the segment's first channel
+  int stride;           // elements between consecutive pixels
+  int cnt;              // channels (multiple of 32 unless SMALLC)
+};
+
+struct ConvFwdArgs {
+  Seg seg[3];
+  int nseg;
+  int cin_pad;    // sum of segment channel counts (multiple of 32)
+  int cin_small;  // SMALLC: true input channels (K = KH*KW*cin_small densely packed)
+  int B, H, W, KH, KW, PH, PW;
+  const uint16_t* wpk;  // packed weights [Npad][kpad] bf16
+  int kpad;
+  const float* bias;    // may be null
+  int cout;
+  void* out0;
+  int out0_stride;
+  void* out1;
+  int out1_stride;
+  void* out2;
+  int out2_stride;
+  const uint16_t* aux0;
+  int aux0_stride;
+  const uint16_t* aux1;
+  int aux1_stride;
+  float scale;
+  int split;
+};
+
+bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStream_t stream);

@@ -1,0 +1,88 @@
+"""NHWC bf16 implicit-GEMM convolution on MFMA (csrc/kernels/conv_igemm.hip, conv_wgrad.hip).
+
+Activation convention: a *buffer* is a contiguous (B, H, W, C) bf16 tensor; a *segment* is a channel
+slice ``(buffer, offset, count)``.  A conv reads the virtual concatenation of up to three segments
+(torch.cat never materialises) and writes its result into a channel slice of an output buffer.
+
+Weights stay in the nn.Conv2d modules (checkpoint layout untouched) and are re-packed once per
+optimizer step (``pack_weight``) to the kernel layout [Npad][KH*KW][CinPad] bf16, where each input
+segment's real channels are placed at its padded offset (e.g. the 324 correlation channels live in
+a 352-channel buffer whose tail is zero).
+"""
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+EPI_BF16, EPI_RELU_BF16, EPI_F32, EPI_ACC_F32, EPI_GRU_ZR, EPI_GRU_Q = range(6)
+
+
+def round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+def pick_bn(cout):
+    if cout <= 32:
+        return 32
+    if cout % 128 == 0 or cout == 126:
+        return 128
+    return 64
+
+
+def pack_weight(w, seg_real, seg_pad, npad_mult=128):
+    """(Cout, Cin, KH, KW) -> (Npad, KH*KW*sum(seg_pad)) bf16.
+
+    ``seg_real[i]`` input channels of the module map to a ``seg_pad[i]``-wide slot in the packed K.
+    """
+    cout, cin, kh, kw = w.shape
+    assert sum(seg_real) == cin, (seg_real, cin)
+    parts = []
+    off = 0
+    for r, p in zip(seg_real, seg_pad):
+        part = w[:, off:off + r]
+        if p > r:
+            part = F.pad(part, (0, 0, 0, 0, 0, p - r))
+        parts.append(part)
+        off += r
+    wp = torch.cat(parts, dim=1)                      # (Cout, CinPad, KH, KW)
+    wp = wp.permute(0, 2, 3, 1).reshape(cout, -1)     # (Cout, KH*KW*CinPad), k = tap*CinPad + c
+    npad = round_up(cout, npad_mult)
+    if npad > cout:
+        wp = F.pad(wp, (0, 0, 0, npad - cout))
+    return wp.to(torch.bfloat16).contiguous()
+
+
+def pack_weight_small(w, npad_mult=128):
+    """Dense-K packing for tiny Cin: k = tap*Cin + c, padded to a multiple of 32."""
+    cout, cin, kh, kw = w.shape
+    wp = w.permute(0, 2, 3, 1).reshape(cout, kh * kw * cin)
+    kp = round_up(kh * kw * cin, 32)
+    wp = F.pad(wp, (0, kp - kh * kw * cin, 0, round_up(cout, npad_mult) - cout))
+    return wp.to(torch.bfloat16).contiguous()
+
+
+def pack_weight_dgrad(w, out_real, out_pad, npad_mult=128):
+    """Weights of the adjoint conv: W'[ci][tap'][co] = W[co][ci][flip(tap')]; the adjoint's input
+    segments are the forward output channels (real ``out_real`` in ``out_pad`` slots)."""
+    wt = w.flip(2, 3).transpose(0, 1).contiguous()   # (Cin, Cout, KH, KW)
+    return pack_weight(wt, out_real, out_pad, npad_mult)
+
+
+def conv_fwd(segs, wpk, bias, ksize, pad, cout, epi, outs, out_offs, aux=(), aux_offs=(),
+             scale=1.0, split=0, cin_small=0, bn=None):
+    """Launch the implicit-GEMM conv.  ``segs`` = [(buffer, offset, count)], ``outs`` buffers."""
+    ops = _ext.ops()
+    ins = [s[0] for s in segs]
+    ops.conv_fwd_(ins, [int(s[1]) for s in segs], [int(s[2]) for s in segs], wpk, bias,
+                  int(ksize[0]), int(ksize[1]), int(pad[0]), int(pad[1]), int(cout), int(cin_small),
+                  int(epi), int(bn or pick_bn(cout)), float(scale), int(split), list(outs),
+                  [int(o) for o in out_offs], list(aux), [int(o) for o in aux_offs])
+
+
+def nhwc(x, dtype=torch.bfloat16):
+    """NCHW tensor -> contiguous (B, H, W, C) buffer."""
+    return x.permute(0, 2, 3, 1).to(dtype).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2)

@@ -1,0 +1,127 @@
+"""Implicit-GEMM MFMA conv kernel vs a plain PyTorch fp32 conv of the same bf16 operands."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_raft_amd.ops import conv as C
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _ref(x_nchw, w, b, pad):
+    # fp32 reference on the bf16-rounded operands
+    return F.conv2d(x_nchw.to(torch.bfloat16).float(), w.to(torch.bfloat16).float(), b, padding=pad)
+
+
+@pytest.mark.parametrize('cin,cout,k,epi', [
+    (256, 192, (3, 3), C.EPI_RELU_BF16),
+    (384, 256, (1, 5), C.EPI_BF16),
+    (384, 128, (5, 1), C.EPI_F32),
+    (128, 576, (1, 1), C.EPI_F32),
+    (256, 2, (3, 3), C.EPI_F32),
+    (128, 126, (3, 3), C.EPI_RELU_BF16),
+])
+def test_conv_fwd_single_segment(ext_ops, cin, cout, k, epi):
+    torch.manual_seed(0)
+    B, H, W = 2, 13, 21
+    x = torch.randn(B, cin, H, W, device=DEV)
+    w = torch.randn(cout, cin, *k, device=DEV) / (cin * k[0] * k[1]) ** 0.5
+    b = torch.randn(cout, device=DEV)
+    pad = (k[0] // 2, k[1] // 2)
+    ref = _ref(x, w, b, pad)
+    if epi == C.EPI_RELU_BF16:
+        ref = ref.relu()
+    xb = C.nhwc(x)
+    wpk = C.pack_weight(w, [cin], [cin])
+    f32 = epi in (C.EPI_F32, C.EPI_ACC_F32)
+    out = torch.zeros(B, H, W, cout + 6, device=DEV, dtype=torch.float32 if f32 else torch.bfloat16)
+    C.conv_fwd([(xb, 0, cin)], wpk, b, k, pad, cout, epi, [out], [3])
+    got = C.nchw(out[..., 3:3 + cout]).float()
+    tol = 2e-2 if not f32 else 2e-3
+    torch.testing.assert_close(got, ref, atol=tol * max(1.0, ref.abs().max().item()), rtol=tol)
+    assert torch.all(out[..., :3] == 0) and torch.all(out[..., 3 + cout:] == 0)
+
+
+def test_conv_fwd_multi_segment_padded(ext_ops):
+    torch.manual_seed(1)
+    B, H, W = 2, 9, 17
+    # 324 real channels in a 352-wide buffer + a 64-channel second segment at an offset
+    x1 = torch.randn(B, 324, H, W, device=DEV)
+    x2 = torch.randn(B, 64, H, W, device=DEV)
+    w = torch.randn(96, 388, 3, 3, device=DEV) / 60
+    b = torch.randn(96, device=DEV)
+    ref = _ref(torch.cat([x1, x2], 1), w, b, (1, 1))
+    buf1 = torch.zeros(B, H, W, 352, device=DEV, dtype=torch.bfloat16)
+    buf1[..., :324] = C.nhwc(x1)
+    buf2 = torch.zeros(B, H, W, 128, device=DEV, dtype=torch.bfloat16)
+    buf2[..., 32:96] = C.nhwc(x2)
+    wpk = C.pack_weight(w, [324, 64], [352, 64])
+    out = torch.empty(B, H, W, 96, device=DEV)
+    C.conv_fwd([(buf1, 0, 352), (buf2, 32, 64)], wpk, b, (3, 3), (1, 1), 96, C.EPI_F32, [out], [0])
+    torch.testing.assert_close(C.nchw(out), ref, atol=2e-3, rtol=2e-3)
+
+
+def test_conv_fwd_small_cin(ext_ops):
+    torch.manual_seed(2)
+    B, H, W = 3, 11, 15
+    x = torch.randn(B, 2, H, W, device=DEV) * 4
+    w = torch.randn(128, 2, 7, 7, device=DEV) / 10
+    b = torch.randn(128, device=DEV)
+    ref = _ref(x, w, b, (3, 3)).relu()
+    buf = torch.zeros(B, H, W, 8, device=DEV, dtype=torch.bfloat16)
+    buf[..., :2] = C.nhwc(x)
+    wpk = C.pack_weight_small(w)
+    out = torch.empty(B, H, W, 128, device=DEV, dtype=torch.bfloat16)
+    C.conv_fwd([(buf, 0, 8)], wpk, b, (7, 7), (3, 3), 128, C.EPI_RELU_BF16, [out], [0], cin_small=2)
+    torch.testing.assert_close(C.nchw(out).float(), ref, atol=3e-2, rtol=2e-2)
+
+
+def test_conv_gru_epilogues(ext_ops):
+    torch.manual_seed(3)
+    B, H, W, hd = 2, 10, 14, 128
+    h = torch.randn(B, hd, H, W, device=DEV).tanh()
+    x = torch.randn(B, 256, H, W, device=DEV)
+    wzr = torch.randn(2 * hd, hd + 256, 1, 5, device=DEV) / 40
+    bzr = torch.randn(2 * hd, device=DEV) * 0.1
+    wq = torch.randn(hd, hd + 256, 1, 5, device=DEV) / 40
+    bq = torch.randn(hd, device=DEV) * 0.1
+    hb, xb = C.nhwc(h), C.nhwc(x)
+    hr, xr = hb.float().permute(0, 3, 1, 2), xb.float().permute(0, 3, 1, 2)
+    zr = torch.sigmoid(_ref(torch.cat([hr, xr], 1), wzr, bzr, (0, 2)))
+    z, r = zr[:, :hd], zr[:, hd:]
+    z_b, r_b = z.to(torch.bfloat16).float(), r.to(torch.bfloat16).float()
+    rh = (r_b * hr).to(torch.bfloat16).float()
+    q = torch.tanh(_ref(torch.cat([rh, xr], 1), wq, bq, (0, 2)))
+    hn = hr + z_b * (q - hr)
+
+    zbuf = torch.empty(B, H, W, hd, device=DEV, dtype=torch.bfloat16)
+    rhbuf = torch.empty_like(zbuf)
+    rbuf = torch.empty_like(zbuf)
+    C.conv_fwd([(hb, 0, hd), (xb, 0, 256)], C.pack_weight(wzr, [hd, 256], [hd, 256]), bzr, (1, 5),
+               (0, 2), 2 * hd, C.EPI_GRU_ZR, [zbuf, rhbuf, rbuf], [0, 0, 0], aux=[hb], aux_offs=[0],
+               split=hd)
+    torch.testing.assert_close(C.nchw(zbuf).float(), z, atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(C.nchw(rbuf).float(), r, atol=1e-2, rtol=1e-2)
+    hnew = torch.empty_like(zbuf)
+    qbuf = torch.empty_like(zbuf)
+    C.conv_fwd([(rhbuf, 0, hd), (xb, 0, 256)], C.pack_weight(wq, [hd, 256], [hd, 256]), bq, (1, 5),
+               (0, 2), hd, C.EPI_GRU_Q, [hnew, qbuf], [0, 0], aux=[hb, zbuf], aux_offs=[0, 0])
+    torch.testing.assert_close(C.nchw(qbuf).float(), q, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(C.nchw(hnew).float(), hn, atol=3e-2, rtol=3e-2)
+
+
+def test_conv_dgrad_via_flipped_weights(ext_ops):
+    torch.manual_seed(4)
+    B, H, W = 2, 12, 16
+    for cin, cout, k in [(256, 192, (3, 3)), (384, 128, (1, 5)), (384, 256, (5, 1))]:
+        pad = (k[0] // 2, k[1] // 2)
+        x = torch.randn(B, cin, H, W, device=DEV, requires_grad=True)
+        w = (torch.randn(cout, cin, *k, device=DEV) / 30).to(torch.bfloat16).float()
+        g = torch.randn(B, cout, H, W, device=DEV).to(torch.bfloat16).float()
+        F.conv2d(x, w, None, padding=pad).backward(g)
+        gb = C.nhwc(g)
+        dx = torch.zeros(B, H, W, cin, device=DEV)
+        C.conv_fwd([(gb, 0, cout)], C.pack_weight_dgrad(w, [cout], [cout]), None, k, pad, cin,
+                   C.EPI_ACC_F32, [dx], [0])
+        torch.testing.assert_close(C.nchw(dx), x.grad, atol=5e-3, rtol=5e-3)
