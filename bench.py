@@ -39,6 +39,8 @@ def parse(argv=None):
     ap.add_argument('--alternate_corr', action='store_true')
     ap.add_argument('--channels_last', action='store_true')
     ap.add_argument('--small', action='store_true')
+    ap.add_argument('--no_hipgraph', action='store_true',
+                    help='eager step (default on GPU: forward+backward and update captured as hipGraphs)')
     ap.add_argument('--profile', type=str, default=None, help='torch.profiler trace dir')
     ap.add_argument('--json_out', type=str, default=None)
     ap.add_argument('--roctx_region', action='store_true',
@@ -105,17 +107,29 @@ def main(argv=None):
             return _orig(*x, **k)
         import pytorch_raft_amd.engine.trainer as T
         T.sequence_loss = _torch_loss
-    st = TrainState(model, margs, device)
+    use_graph = (device.type == 'cuda' and not a.no_hipgraph and a.impl == 'hip'
+                 and a.precision != 'fp16')
+    st = TrainState(model, margs, device, graph_ready=use_graph)
 
     h, w = a.size
     batches = device_batches(a.batch, h, w, device, count=2, seed=17 * rank)
 
+    if use_graph:
+        from pytorch_raft_amd.engine.trainer import GraphedTrainStep
+        # capture runs a.warmup real (eager) training steps first, then records the graphs
+        stepper = GraphedTrainStep(st, batches[0], warmup=max(1, a.warmup))
+    else:
+        stepper = st
+
     def run(n):
         for k in range(n):
             i1, i2, fl, va = batches[k % len(batches)]
-            st.step(i1, i2, fl, va)
+            stepper.step(i1, i2, fl, va)
 
-    run(a.warmup)
+    if use_graph:
+        run(1)  # first replay
+    else:
+        run(a.warmup)
     if device.type == 'cuda':
         torch.cuda.synchronize()
         torch.cuda.reset_peak_memory_stats()
@@ -172,6 +186,7 @@ def main(argv=None):
             'parallelism': 'dp%d' % world,
             'impl': a.impl,
             'corr': 'alternate(on-the-fly)' if a.alternate_corr else 'all-pairs',
+            'hipgraph': use_graph,
         },
         'peak_hbm_gib_rank0': round(peak, 2),
         'loss_finite': ok,

@@ -406,6 +406,50 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   TORCH_CHECK(launch_conv_fwd(a, (int)epi, (int)bn, cin_small != 0, cur_stream()), "bad epilogue");
 }
 
+// dw (cout, kpad) fp32 += sum_p g[p][:cout] (x) im2col(ins)[p][:]; db (cout) fp32 += colsum(g)
+void conv_wgrad_(const Tensor& g, int64_t g_off, const std::vector<Tensor>& ins,
+                 const std::vector<int64_t>& in_off, const std::vector<int64_t>& in_cnt,
+                 int64_t kh, int64_t kw, int64_t ph, int64_t pw, int64_t cout, int64_t cin_small,
+                 const Tensor& dw, const c10::optional<Tensor>& db, int64_t pix_per_split) {
+  TORCH_CHECK(!ins.empty() && ins.size() <= 3, "1..3 input segments");
+  const int64_t B = g.size(0), H = g.size(1), W = g.size(2);
+  check_nhwc(g, B, H, W, "grad", at::kBFloat16);
+  TORCH_CHECK(g_off >= 0 && g_off + cout <= g.size(3), "grad slice out of range");
+  c10::DeviceGuard gd(g.device());
+  ConvWgradArgs a{};
+  a.g = reinterpret_cast<const uint16_t*>(g.data_ptr<at::BFloat16>()) + g_off;
+  a.g_stride = (int)g.size(3);
+  a.nseg = (int)ins.size();
+  int64_t cin_pad = 0;
+  for (size_t s = 0; s < ins.size(); ++s) {
+    check_nhwc(ins[s], B, H, W, "wgrad input", at::kBFloat16);
+    TORCH_CHECK(in_off[s] >= 0 && in_off[s] + in_cnt[s] <= ins[s].size(3), "segment out of range");
+    TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
+    if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 8 == 0, "segment channels must be a multiple of 8");
+    a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
+    a.seg[s].stride = (int)ins[s].size(3);
+    a.seg[s].cnt = (int)in_cnt[s];
+    cin_pad += in_cnt[s];
+  }
+  a.cin_pad = (int)cin_pad;
+  a.cin_small = (int)cin_small;
+  a.B = (int)B; a.H = (int)H; a.W = (int)W;
+  a.KH = (int)kh; a.KW = (int)kw; a.PH = (int)ph; a.PW = (int)pw;
+  a.cout = (int)cout;
+  check_cuda_f32(dw, "grad_weight");
+  const int64_t kpad = cin_small ? ((kh * kw * cin_small + 31) / 32) * 32 : kh * kw * cin_pad;
+  TORCH_CHECK(dw.dim() == 2 && dw.size(0) == cout && dw.size(1) == kpad, "grad_weight must be (cout, kpad)");
+  a.dw = dw.data_ptr<float>();
+  a.kpad = (int)kpad;
+  a.pix_per_split = (int)std::max<int64_t>(32, pix_per_split);
+  launch_conv_wgrad(a, cout > 64 ? 128 : 64, cin_small != 0, cur_stream());
+  if (db.has_value() && db->defined()) {
+    check_cuda_f32(*db, "grad_bias");
+    TORCH_CHECK(db->numel() == cout, "grad_bias size");
+    launch_col_sum(a.g, a.g_stride, (int)cout, (int)(B * H * W), db->data_ptr<float>(), cur_stream());
+  }
+}
+
 }  // namespace
 
 TORCH_LIBRARY(raft_amd, m) {
@@ -422,6 +466,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("warp_fwd(Tensor img, Tensor flow, float sx, float bx, float sy, float by) -> Tensor");
   m.def("warp_bwd(Tensor img, Tensor flow, Tensor dout, float sx, float bx, float sy, float by) -> Tensor[]");
   m.def("conv_fwd_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, Tensor? bias, int kh, int kw, int ph, int pw, int cout, int cin_small, int epi, int bn, float scale, int split, Tensor(a!)[] outs, int[] out_off, Tensor[] aux, int[] aux_off) -> ()");
+  m.def("conv_wgrad_(Tensor g, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, int cin_small, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
@@ -438,4 +483,5 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("warp_fwd", &warp_fwd);
   m.impl("warp_bwd", &warp_bwd);
   m.impl("conv_fwd_", &conv_fwd_);
+  m.impl("conv_wgrad_", &conv_wgrad_);
 }

@@ -99,3 +99,20 @@ struct ConvFwdArgs {
 };
 
 bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStream_t stream);
+
+struct ConvWgradArgs {
+  const uint16_t* g;  // dL/d(pre-activation), NHWC bf16, offset to channel 0
+  int g_stride;
+  Seg seg[3];
+  int nseg;
+  int cin_pad;
+  int cin_small;
+  int B, H, W, KH, KW, PH, PW;
+  int cout;
+  float* dw;  // [cout][kpad] fp32, accumulated
+  int kpad;
+  int pix_per_split;
+};
+
+bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, hipStream_t stream);
+void launch_col_sum(const uint16_t* g, int stride, int cout, int P, float* db, hipStream_t stream);

@@ -12,11 +12,13 @@ def count_parameters(model):
     return sum(p.numel() for p in model.parameters() if p.requires_grad)
 
 
-def fetch_optimizer(args, model, fused=None):
+def fetch_optimizer(args, model, fused=None, capturable=False):
     params = [p for p in model.parameters() if p.requires_grad]
     if fused is None:
         fused = bool(params) and params[0].is_cuda
     kw = dict(lr=args.lr, weight_decay=args.wdecay, eps=args.epsilon)
+    if capturable:
+        kw['capturable'] = True
     try:
         optimizer = optim.AdamW(params, fused=fused, **kw)
     except (RuntimeError, TypeError):

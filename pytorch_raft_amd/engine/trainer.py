@@ -5,12 +5,23 @@ Reference hot loop (`train.py:161-181`): zero_grad -> H2D copy -> optional noise
 unscale / clip / step / schedule / scaler update.
 
 Here the step is host-sync free: noise comes from the device RNG, the loss and its metrics are one
-fused HIP reduction kept on the device, gradients are all-reduced over RCCL in buckets overlapped
-with backward (``parallel.dist.GradSync``), clipping uses the foreach global norm and AdamW is the
-fused multi-tensor kernel.  A device-side non-finite flag is accumulated for failure detection and
-checked by the caller at its logging cadence.
+fused HIP reduction kept on the device, clipping uses the foreach global norm and AdamW is the fused
+multi-tensor kernel.  Two execution modes:
+
+* eager (``TrainState.step``): gradients are all-reduced over RCCL in buckets overlapped with
+  backward on a side HIP stream (``parallel.dist.GradSync``);
+* HIP-graph (``GraphedTrainStep``): RAFT issues thousands of small kernels per step (12 GRU
+  iterations forward + backward), so on MI355X the eager step is launch-bound.  The whole
+  forward + loss + backward is captured once into a hipGraph (torch.cuda.CUDAGraph == hipGraph on
+  ROCm) and replayed; gradients land in ONE flat buffer (``p.grad`` are views into it), which is
+  all-reduced with a single RCCL call outside the graph, and the clip + fused-AdamW update is a
+  second graph.  The learning rate lives in a device tensor so the OneCycle schedule keeps working
+  under replay.
+
+A device-side non-finite flag is accumulated for failure detection and checked at logging cadence.
 """
 import torch
+import torch.distributed as dist
 
 from ..ops.loss import sequence_loss
 from ..parallel import dist as pdist
@@ -18,16 +29,16 @@ from .optim import fetch_optimizer, clip_grad_norm_
 
 
 class TrainState:
-    def __init__(self, model, args, device, sync=True):
+    def __init__(self, model, args, device, sync=True, graph_ready=False):
         self.model = model
         self.args = args
         self.device = device
-        self.optimizer, self.scheduler = fetch_optimizer(args, model)
+        self.optimizer, self.scheduler = fetch_optimizer(args, model, capturable=graph_ready)
         amp_fp16 = bool(getattr(args, 'mixed_precision', False)) and \
             getattr(args, 'amp_dtype', 'bfloat16') in ('float16', 'fp16')
         self.scaler = torch.amp.GradScaler('cuda', enabled=amp_fp16 and device.type == 'cuda')
         self.sync = None
-        if sync and pdist.world_size() > 1:
+        if sync and pdist.world_size() > 1 and not graph_ready:
             self.sync = pdist.GradSync(model, bucket_mb=getattr(args, 'bucket_mb', 8.0),
                                        order=pdist.raft_grad_order)
         self.has_buffers = any(True for _ in model.buffers())
@@ -41,27 +52,33 @@ class TrainState:
         image2 = (image2 + stdv * torch.randn_like(image2)).clamp(0.0, 255.0)
         return image1, image2
 
-    def step(self, image1, image2, flow, valid):
+    def forward_backward(self, image1, image2, flow, valid):
         args = self.args
-        model = self.model
-        self.optimizer.zero_grad(set_to_none=True)
         if getattr(args, 'add_noise', False):
             image1, image2 = self.add_noise(image1, image2)
-        if self.has_buffers and pdist.world_size() > 1:
-            pdist.broadcast_buffers(model)  # DataParallel semantics: replica 0's BN stats
-        preds = model(image1, image2, iters=args.iters)
+        preds = self.model(image1, image2, iters=args.iters)
         loss, metrics = sequence_loss(preds, flow, valid, args.gamma)
-        if self.sync is not None:
-            self.sync.prepare()
         self.scaler.scale(loss).backward()
-        if self.sync is not None:
-            self.sync.finish()
+        return loss, metrics
+
+    def apply_update(self, loss):
         self.scaler.unscale_(self.optimizer)
-        clip_grad_norm_(model.parameters(), args.clip)
+        clip_grad_norm_(self.model.parameters(), self.args.clip)
         self.scaler.step(self.optimizer)
-        self.scheduler.step()
         self.scaler.update()
         self.nonfinite += (~torch.isfinite(loss.detach())).float()
+
+    def step(self, image1, image2, flow, valid):
+        self.optimizer.zero_grad(set_to_none=True)
+        if self.has_buffers and pdist.world_size() > 1:
+            pdist.broadcast_buffers(self.model)  # DataParallel semantics: replica 0's BN stats
+        if self.sync is not None:
+            self.sync.prepare()
+        loss, metrics = self.forward_backward(image1, image2, flow, valid)
+        if self.sync is not None:
+            self.sync.finish()
+        self.apply_update(loss)
+        self.scheduler.step()
         self.total_steps += 1
         metrics = dict(metrics)
         metrics['loss'] = loss.detach()
@@ -75,3 +92,91 @@ class TrainState:
             torch.distributed.all_reduce(t)
             bad = float(t.item())
         return bad == 0.0
+
+
+class GraphedTrainStep:
+    """hipGraph-captured training step around a ``TrainState`` built with ``graph_ready=True``."""
+
+    def __init__(self, st, example, warmup=3):
+        assert st.device.type == 'cuda', 'graph capture needs a GPU'
+        assert not st.scaler.is_enabled(), 'use bf16 autocast (no GradScaler) with graph capture'
+        self.st = st
+        self.world = pdist.world_size()
+        model = st.model
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        numel = sum(p.numel() for p in self.params)
+        self.flat = torch.zeros(numel, device=st.device, dtype=torch.float32)
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            p.grad = self.flat[off:off + n].view_as(p)
+            off += n
+        # learning rate as a device tensor (fused AdamW reads it in-graph)
+        self.lr = []
+        for g in st.optimizer.param_groups:
+            t = torch.tensor(float(g['lr']), device=st.device, dtype=torch.float32)
+            g['lr'] = t
+            self.lr.append(t)
+        self.static = [t.clone() for t in example]
+
+        stream = torch.cuda.Stream(device=st.device)
+        stream.wait_stream(torch.cuda.current_stream(st.device))
+        with torch.cuda.stream(stream):
+            for _ in range(warmup):  # MIOpen find / allocator warm-up; these are real steps
+                loss, _ = self._fwd_bwd()
+                self._post()
+                self._update_graphable(loss)
+                self._sched()
+        torch.cuda.current_stream(st.device).wait_stream(stream)
+        torch.cuda.synchronize(st.device)
+
+        self.g_fb = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_fb):
+            self.loss, self.metrics = self._fwd_bwd()
+        self.g_up = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_up, pool=self.g_fb.pool()):
+            self._update_graphable(self.loss)
+        self.warmup_steps = warmup
+
+    def _fwd_bwd(self):
+        self.flat.zero_()
+        return self.st.forward_backward(*self.static)
+
+    def _post(self):
+        if self.world > 1:
+            dist.all_reduce(self.flat)
+            self.flat.div_(self.world)
+
+    def _update_graphable(self, loss):
+        st = self.st
+        clip_grad_norm_(self.params, st.args.clip)
+        st.optimizer.step()
+        st.nonfinite += (~torch.isfinite(loss.detach())).float()
+
+    def _sched(self):
+        st = self.st
+        st.scheduler.step()
+        for g, t in zip(st.optimizer.param_groups, self.lr):
+            v = g['lr']
+            if not torch.is_tensor(v):
+                t.fill_(float(v))
+                g['lr'] = t
+
+    def step(self, image1, image2, flow, valid):
+        st = self.st
+        for s, x in zip(self.static, (image1, image2, flow, valid)):
+            if s.data_ptr() != x.data_ptr():
+                s.copy_(x, non_blocking=True)
+        if st.has_buffers and self.world > 1:
+            pdist.broadcast_buffers(st.model)
+        self.g_fb.replay()
+        self._post()
+        self.g_up.replay()
+        self._sched()
+        st.total_steps += 1
+        metrics = dict(self.metrics)
+        metrics['loss'] = self.loss.detach()
+        return self.loss, metrics
+
+    def check_finite(self):
+        return self.st.check_finite()

@@ -86,3 +86,39 @@ def nhwc(x, dtype=torch.bfloat16):
 
 def nchw(x):
     return x.permute(0, 3, 1, 2)
+
+
+def conv_wgrad(g, g_off, segs, ksize, pad, cout, dw, db=None, cin_small=0, pix_per_split=None):
+    """dw (cout, kpad) fp32 += weight gradient in packed-K layout; db (cout) fp32 += bias grad.
+
+    ``g`` is the bf16 NHWC gradient w.r.t. the conv's pre-activation output (channels
+    [g_off, g_off+cout)); ``segs`` the forward input segments.
+    """
+    ops = _ext.ops()
+    if pix_per_split is None:
+        p = g.shape[0] * g.shape[1] * g.shape[2]
+        # enough workgroups to cover 256 CUs a few times over, >= 2 K-steps each
+        tiles = max(1, (cout + 127) // 128) * max(1, (dw.shape[1] + 127) // 128)
+        splits = max(1, min(p // 64, (1024 + tiles - 1) // tiles))
+        pix_per_split = round_up((p + splits - 1) // splits, 32)
+    ops.conv_wgrad_(g, int(g_off), [s[0] for s in segs], [int(s[1]) for s in segs],
+                    [int(s[2]) for s in segs], int(ksize[0]), int(ksize[1]), int(pad[0]),
+                    int(pad[1]), int(cout), int(cin_small), dw, db, int(pix_per_split))
+
+
+def unpack_weight_grad(dw, cout, cin_real_segs, cin_pad_segs, ksize):
+    """(cout, KH*KW*CinPad) packed gradient -> (Cout, Cin, KH, KW) module layout."""
+    kh, kw = ksize
+    cin_pad = sum(cin_pad_segs)
+    g = dw.view(cout, kh, kw, cin_pad).permute(0, 3, 1, 2)
+    parts = []
+    off = 0
+    for r, p in zip(cin_real_segs, cin_pad_segs):
+        parts.append(g[:, off:off + r])
+        off += p
+    return torch.cat(parts, dim=1) if len(parts) > 1 else parts[0].contiguous()
+
+
+def unpack_weight_grad_small(dw, cout, cin, ksize):
+    kh, kw = ksize
+    return dw[:, :kh * kw * cin].reshape(cout, kh, kw, cin).permute(0, 3, 1, 2).contiguous()

@@ -125,3 +125,51 @@ def test_conv_dgrad_via_flipped_weights(ext_ops):
         C.conv_fwd([(gb, 0, cout)], C.pack_weight_dgrad(w, [cout], [cout]), None, k, pad, cin,
                    C.EPI_ACC_F32, [dx], [0])
         torch.testing.assert_close(C.nchw(dx), x.grad, atol=5e-3, rtol=5e-3)
+
+
+@pytest.mark.parametrize('cin,cout,k,segs', [
+    (256, 192, (3, 3), None),
+    (384, 256, (1, 5), (128, 256)),
+    (128, 576, (1, 1), None),
+    (256, 2, (3, 3), None),
+    (96, 126, (3, 3), None),
+])
+def test_conv_wgrad(ext_ops, cin, cout, k, segs):
+    torch.manual_seed(5)
+    B, H, W = 2, 11, 19
+    pad = (k[0] // 2, k[1] // 2)
+    x = torch.randn(B, cin, H, W, device=DEV).to(torch.bfloat16).float()
+    w = torch.randn(cout, cin, *k, device=DEV, requires_grad=True)
+    b = torch.zeros(cout, device=DEV, requires_grad=True)
+    g = torch.randn(B, cout, H, W, device=DEV).to(torch.bfloat16).float()
+    F.conv2d(x, w, b, padding=pad).backward(g)
+    xb = C.nhwc(x)
+    if segs is None:
+        seg_list, real, padc = [(xb, 0, cin)], [cin], [cin]
+    else:
+        seg_list = [(C.nhwc(x[:, :segs[0]]), 0, segs[0]), (C.nhwc(x[:, segs[0]:]), 0, segs[1])]
+        real = padc = list(segs)
+    gb = torch.zeros(B, H, W, C.round_up(cout, 8), device=DEV, dtype=torch.bfloat16)
+    gb[..., :cout] = C.nhwc(g)
+    dw = torch.zeros(cout, k[0] * k[1] * cin, device=DEV)
+    db = torch.zeros(cout, device=DEV)
+    C.conv_wgrad(gb, 0, seg_list, k, pad, cout, dw, db)
+    got = C.unpack_weight_grad(dw, cout, real, padc, k)
+    scale = w.grad.abs().max().item()
+    torch.testing.assert_close(got, w.grad, atol=2e-3 * scale, rtol=1e-3)
+    torch.testing.assert_close(db, b.grad, atol=1e-3 * b.grad.abs().max().item(), rtol=1e-3)
+
+
+def test_conv_wgrad_small_cin(ext_ops):
+    torch.manual_seed(6)
+    B, H, W = 2, 9, 13
+    x = (torch.randn(B, 2, H, W, device=DEV) * 3).to(torch.bfloat16).float()
+    w = torch.randn(128, 2, 7, 7, device=DEV, requires_grad=True)
+    g = torch.randn(B, 128, H, W, device=DEV).to(torch.bfloat16).float()
+    F.conv2d(x, w, None, padding=3).backward(g)
+    buf = torch.zeros(B, H, W, 8, device=DEV, dtype=torch.bfloat16)
+    buf[..., :2] = C.nhwc(x)
+    dw = torch.zeros(128, 128, device=DEV)
+    C.conv_wgrad(C.nhwc(g), 0, [(buf, 0, 8)], (7, 7), (3, 3), 128, dw, None, cin_small=2)
+    got = C.unpack_weight_grad_small(dw, 128, 2, (7, 7))
+    torch.testing.assert_close(got, w.grad, atol=2e-3 * w.grad.abs().max().item(), rtol=1e-3)
