@@ -84,13 +84,39 @@ Tensor corr_lookup_fwd(const std::vector<Tensor>& pyr, const Tensor& coords, int
   TORCH_CHECK(L.h[0] == H && L.w[0] == W, "pyramid level 0 must match coords grid");
   const int64_t D = 2 * radius + 1;
   const int levels = (int)pyr.size();
-  Tensor out = at::empty({B, levels * D * D, H, W}, coords.options());
+  const int64_t N = H * W, Ct = levels * D * D;
+  Tensor out = at::empty({B, Ct, H, W}, coords.options());
   std::vector<const float*> cp(L.ptr.begin(), L.ptr.end());
   TORCH_CHECK(launch_corr_lookup_fwd(cp.data(), L.h.data(), L.w.data(), levels,
-                                     coords.data_ptr<float>(), out.data_ptr<float>(), (int)B,
-                                     (int)H, (int)W, (int)radius, cur_stream()),
+                                     coords.data_ptr<float>(), out.data_ptr<float>(), 0, Ct * N, 1,
+                                     N, (int)B, (int)H, (int)W, (int)radius, cur_stream()),
               "unsupported radius");
   return out;
+}
+
+// writes bf16 taps into channels [0, L*D*D) of an NHWC (B,H,W,Cbuf) buffer (the fused update
+// block's correlation input); the caller owns the zero padding of the remaining channels
+void corr_lookup_nhwc_(const std::vector<Tensor>& pyr, const Tensor& coords, int64_t radius,
+                       const Tensor& out) {
+  check_cuda_f32(coords, "coords");
+  TORCH_CHECK(coords.dim() == 4 && coords.size(1) == 2, "coords must be (B,2,H,W)");
+  TORCH_CHECK(radius == 3 || radius == 4, "radius must be 3 or 4");
+  c10::DeviceGuard g(coords.device());
+  const int64_t B = coords.size(0), H = coords.size(2), W = coords.size(3);
+  Levels L = levels_of(pyr, B * H * W, "pyramid");
+  TORCH_CHECK(L.h[0] == H && L.w[0] == W, "pyramid level 0 must match coords grid");
+  const int64_t D = 2 * radius + 1;
+  const int levels = (int)pyr.size();
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.scalar_type() == at::kBFloat16 &&
+                  out.dim() == 4 && out.size(0) == B && out.size(1) == H && out.size(2) == W &&
+                  out.size(3) >= levels * D * D,
+              "out must be a contiguous bf16 (B,H,W,C>=L*D*D) buffer");
+  const int64_t Cb = out.size(3);
+  std::vector<const float*> cp(L.ptr.begin(), L.ptr.end());
+  TORCH_CHECK(launch_corr_lookup_fwd(cp.data(), L.h.data(), L.w.data(), levels,
+                                     coords.data_ptr<float>(), out.data_ptr(), 1, H * W * Cb, Cb, 1,
+                                     (int)B, (int)H, (int)W, (int)radius, cur_stream()),
+              "unsupported radius");
 }
 
 void corr_lookup_bwd_(const std::vector<Tensor>& gpyr, const Tensor& coords, const Tensor& dout,
@@ -102,11 +128,16 @@ void corr_lookup_bwd_(const std::vector<Tensor>& gpyr, const Tensor& coords, con
   const int64_t B = coords.size(0), H = coords.size(2), W = coords.size(3);
   Levels L = levels_of(gpyr, B * H * W, "grad pyramid");
   const int64_t D = 2 * radius + 1;
-  TORCH_CHECK(dout.dim() == 4 && dout.size(0) == B && dout.size(1) == (int64_t)gpyr.size() * D * D &&
-                  dout.size(2) == H && dout.size(3) == W,
-              "grad_corr shape mismatch");
+  const int64_t Ct = (int64_t)gpyr.size() * D * D, N = H * W;
+  const bool nhwc = dout.dim() == 4 && dout.size(0) == B && dout.size(1) == H && dout.size(2) == W &&
+                    dout.size(3) >= Ct;
+  const bool nchw = dout.dim() == 4 && dout.size(0) == B && dout.size(1) == Ct && dout.size(2) == H &&
+                    dout.size(3) == W;
+  TORCH_CHECK(nchw || nhwc, "grad_corr must be (B,L*D*D,H,W) or (B,H,W,C>=L*D*D)");
+  const int64_t Cb = nhwc && !nchw ? dout.size(3) : Ct;
   TORCH_CHECK(launch_corr_lookup_bwd(L.ptr.data(), L.h.data(), L.w.data(), (int)gpyr.size(),
-                                     coords.data_ptr<float>(), dout.data_ptr<float>(), (int)B,
+                                     coords.data_ptr<float>(), dout.data_ptr<float>(),
+                                     nchw ? Ct * N : N * Cb, nchw ? 1 : Cb, nchw ? N : 1, (int)B,
                                      (int)H, (int)W, (int)radius, cur_stream()),
               "unsupported radius");
 }
@@ -200,29 +231,36 @@ int mask_kind(const Tensor& m) {
   return m.scalar_type() == at::kBFloat16 ? 1 : 0;
 }
 
-Tensor convex_up_fwd(const Tensor& flow, const Tensor& mask) {
-  check_cuda_f32(flow, "flow");
+// mask is (B,576,H,W) contiguous (nhwc=false) or (B,H,W,576) contiguous (nhwc=true)
+void check_mask(const Tensor& mask, int64_t B, int64_t H, int64_t W, bool nhwc) {
   TORCH_CHECK(mask.is_cuda() && mask.is_contiguous(), "mask must be a contiguous GPU tensor");
+  const bool ok = nhwc ? (mask.dim() == 4 && mask.size(0) == B && mask.size(1) == H &&
+                          mask.size(2) == W && mask.size(3) == 576)
+                       : (mask.dim() == 4 && mask.size(0) == B && mask.size(1) == 576 &&
+                          mask.size(2) == H && mask.size(3) == W);
+  TORCH_CHECK(ok, nhwc ? "mask must be (B,H,W,576)" : "mask must be (B,576,H,W)");
+}
+
+Tensor convex_up_fwd(const Tensor& flow, const Tensor& mask, bool nhwc) {
+  check_cuda_f32(flow, "flow");
   TORCH_CHECK(flow.dim() == 4 && flow.size(1) == 2, "flow must be (B,2,H,W)");
   const int64_t B = flow.size(0), H = flow.size(2), W = flow.size(3);
-  TORCH_CHECK(mask.dim() == 4 && mask.size(0) == B && mask.size(1) == 576 && mask.size(2) == H &&
-                  mask.size(3) == W,
-              "mask must be (B,576,H,W)");
+  check_mask(mask, B, H, W, nhwc);
   c10::DeviceGuard g(flow.device());
   Tensor out = at::empty({B, 2, 8 * H, 8 * W}, flow.options());
-  launch_convex_up_fwd(flow.data_ptr<float>(), mask.data_ptr(), mask_kind(mask),
-                       out.data_ptr<float>(), (int)B, (int)H, (int)W, cur_stream());
+  const int64_t HW = H * W;
+  launch_convex_up_fwd(flow.data_ptr<float>(), mask.data_ptr(), mask_kind(mask), 576 * HW,
+                       nhwc ? 1 : HW, nhwc ? 576 : 1, out.data_ptr<float>(), (int)B, (int)H,
+                       (int)W, cur_stream());
   return out;
 }
 
-std::vector<Tensor> convex_up_bwd(const Tensor& flow, const Tensor& mask, const Tensor& dout) {
+std::vector<Tensor> convex_up_bwd(const Tensor& flow, const Tensor& mask, const Tensor& dout,
+                                  bool nhwc) {
   check_cuda_f32(flow, "flow");
   check_cuda_f32(dout, "grad_out");
-  TORCH_CHECK(mask.is_cuda() && mask.is_contiguous(), "mask must be a contiguous GPU tensor");
   const int64_t B = flow.size(0), H = flow.size(2), W = flow.size(3);
-  TORCH_CHECK(mask.dim() == 4 && mask.size(0) == B && mask.size(1) == 576 && mask.size(2) == H &&
-                  mask.size(3) == W,
-              "mask must be (B,576,H,W)");
+  check_mask(mask, B, H, W, nhwc);
   TORCH_CHECK(dout.dim() == 4 && dout.size(0) == B && dout.size(1) == 2 && dout.size(2) == 8 * H &&
                   dout.size(3) == 8 * W,
               "grad_out must be (B,2,8H,8W)");
@@ -230,9 +268,11 @@ std::vector<Tensor> convex_up_bwd(const Tensor& flow, const Tensor& mask, const 
   Tensor dmask = at::empty_like(mask);
   Tensor dflow = at::empty_like(flow);
   Tensor wbuf = at::empty({B, 18, H, W}, flow.options());
-  launch_convex_up_bwd(flow.data_ptr<float>(), mask.data_ptr(), mask_kind(mask),
-                       dout.data_ptr<float>(), dmask.data_ptr(), wbuf.data_ptr<float>(),
-                       dflow.data_ptr<float>(), (int)B, (int)H, (int)W, cur_stream());
+  const int64_t HW = H * W;
+  launch_convex_up_bwd(flow.data_ptr<float>(), mask.data_ptr(), mask_kind(mask), 576 * HW,
+                       nhwc ? 1 : HW, nhwc ? 576 : 1, dout.data_ptr<float>(), dmask.data_ptr(),
+                       wbuf.data_ptr<float>(), dflow.data_ptr<float>(), (int)B, (int)H, (int)W,
+                       cur_stream());
   return {dflow, dmask};
 }
 
@@ -378,9 +418,22 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   a.cout = (int)cout;
   a.scale = (float)scale;
   a.split = (int)split;
-  const bool f32out = (epi == EPI_F32 || epi == EPI_ACC_F32);
+  TORCH_CHECK(epi != EPI_DGRAD, "use conv_dgrad_ for the dgrad epilogue");
+  const bool f32out = (epi == EPI_F32 || epi == EPI_ACC_F32 || epi == EPI_F32_NCHW);
   const int64_t need_out = (epi == EPI_GRU_ZR) ? 3 : (epi == EPI_GRU_Q ? 2 : 1);
   TORCH_CHECK((int64_t)outs.size() == need_out && out_off.size() == outs.size(), "wrong output count");
+  if (epi == EPI_F32_NCHW) {
+    const Tensor& o = outs[0];
+    TORCH_CHECK(o.is_cuda() && o.is_contiguous() && o.scalar_type() == at::kFloat && o.dim() == 4 &&
+                    o.size(0) == B && o.size(1) == cout && o.size(2) == H && o.size(3) == W &&
+                    out_off[0] == 0,
+                "NCHW output must be a contiguous fp32 (B,cout,H,W) tensor");
+    a.out0 = o.data_ptr<float>();
+    a.out0_stride = 0;
+    TORCH_CHECK(aux.empty(), "no aux for the NCHW epilogue");
+    TORCH_CHECK(launch_conv_fwd(a, (int)epi, (int)bn, cin_small != 0, cur_stream()), "bad epilogue");
+    return;
+  }
   const int64_t out_ch[3] = {epi == EPI_GRU_ZR ? split : cout, epi == EPI_GRU_ZR ? cout - split : cout,
                              cout - split};
   void** optr[3] = {&a.out0, &a.out1, &a.out2};
@@ -450,6 +503,147 @@ void conv_wgrad_(const Tensor& g, int64_t g_off, const std::vector<Tensor>& ins,
   }
 }
 
+// Input gradient of a stride-1 "same" conv = the forward kernel on flipped/transposed packed
+// weights; the result's channels are scattered over up to 3 fp32 NHWC slices (store or +=).
+void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_off,
+                 const std::vector<int64_t>& in_cnt, const Tensor& wpk, int64_t kh, int64_t kw,
+                 int64_t ph, int64_t pw, int64_t cin_small, double scale,
+                 const std::vector<Tensor>& outs, const std::vector<int64_t>& out_off,
+                 const std::vector<int64_t>& out_cnt, const std::vector<int64_t>& out_real,
+                 const std::vector<int64_t>& out_acc) {
+  TORCH_CHECK(!ins.empty() && ins.size() <= 3 && !outs.empty() && outs.size() <= 3, "1..3 segments");
+  TORCH_CHECK(in_off.size() == ins.size() && in_cnt.size() == ins.size(), "input spec mismatch");
+  TORCH_CHECK(out_off.size() == outs.size() && out_cnt.size() == outs.size() &&
+                  out_real.size() == outs.size() && out_acc.size() == outs.size(),
+              "output spec mismatch");
+  const int64_t B = ins[0].size(0), H = ins[0].size(1), W = ins[0].size(2);
+  c10::DeviceGuard g(ins[0].device());
+  ConvFwdArgs a{};
+  a.nseg = (int)ins.size();
+  int64_t cin_pad = 0;
+  for (size_t s = 0; s < ins.size(); ++s) {
+    check_nhwc(ins[s], B, H, W, "dgrad input", at::kBFloat16);
+    TORCH_CHECK(in_off[s] >= 0 && in_off[s] + in_cnt[s] <= ins[s].size(3), "segment out of range");
+    TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
+    if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 32 == 0, "segment channels must be a multiple of 32");
+    a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
+    a.seg[s].stride = (int)ins[s].size(3);
+    a.seg[s].cnt = (int)in_cnt[s];
+    cin_pad += in_cnt[s];
+  }
+  a.cin_pad = (int)cin_pad;
+  a.cin_small = (int)cin_small;
+  a.B = (int)B; a.H = (int)H; a.W = (int)W;
+  a.KH = (int)kh; a.KW = (int)kw; a.PH = (int)ph; a.PW = (int)pw;
+  int64_t cout = 0;
+  a.noseg = (int)outs.size();
+  for (size_t o = 0; o < outs.size(); ++o) {
+    check_nhwc(outs[o], B, H, W, "dgrad output", at::kFloat);
+    TORCH_CHECK(out_real[o] <= out_cnt[o] && out_off[o] >= 0 && out_off[o] + out_real[o] <= outs[o].size(3),
+                "dgrad output slice out of range");
+    a.oseg[o].ptr = outs[o].data_ptr<float>() + out_off[o];
+    a.oseg[o].stride = (int)outs[o].size(3);
+    a.oseg[o].cnt = (int)out_cnt[o];
+    a.oseg[o].real = (int)out_real[o];
+    a.oseg[o].acc = (int)out_acc[o];
+    cout += out_cnt[o];
+  }
+  a.cout = (int)cout;
+  const int bn = (cout % 128 == 0) ? 128 : 64;
+  TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == at::kBFloat16 && wpk.dim() == 2,
+              "packed weight must be a contiguous bf16 (Npad, Kpad) tensor");
+  const int64_t kneed = cin_small ? ((kh * kw * cin_small + 31) / 32) * 32 : kh * kw * cin_pad;
+  TORCH_CHECK(wpk.size(1) == kneed, "packed dgrad weight K mismatch: ", wpk.size(1), " vs ", kneed);
+  TORCH_CHECK(wpk.size(0) >= ((cout + bn - 1) / bn) * bn, "packed dgrad weight has too few rows");
+  a.wpk = reinterpret_cast<const uint16_t*>(wpk.data_ptr<at::BFloat16>());
+  a.kpad = (int)wpk.size(1);
+  a.bias = nullptr;
+  a.scale = (float)scale;
+  TORCH_CHECK(launch_conv_fwd(a, EPI_DGRAD, bn, cin_small != 0, cur_stream()), "dgrad launch");
+}
+
+// ------------------------------------------------------------------ update-block elementwise
+const uint16_t* bf16p(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr<at::BFloat16>()); }
+uint16_t* bf16m(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr<at::BFloat16>()); }
+
+void check_pc(const Tensor& t, int64_t P, int64_t C, at::ScalarType st, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == st, name, ": wrong device/dtype/layout");
+  TORCH_CHECK(t.numel() == P * C, name, ": expected ", P, " x ", C, " elements");
+}
+
+// out[:, o_off:o_off+C] (bf16) = g[:, g_off:g_off+C] * scale * [y[:, y_off:] > 0]
+void relu_bwd_(const Tensor& g, int64_t g_off, const c10::optional<Tensor>& y, int64_t y_off,
+               const Tensor& out, int64_t o_off, int64_t C, double scale) {
+  TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.scalar_type() == at::kFloat && g.dim() == 4, "g: fp32 NHWC");
+  const int64_t B = g.size(0), H = g.size(1), W = g.size(2), P = B * H * W;
+  TORCH_CHECK(g_off + C <= g.size(3), "g slice");
+  check_nhwc(out, B, H, W, "relu_bwd out", at::kBFloat16);
+  TORCH_CHECK(o_off + C <= out.size(3), "out slice");
+  const uint16_t* yp = nullptr;
+  int ys = 0;
+  if (y.has_value() && y->defined()) {
+    check_nhwc(*y, B, H, W, "relu_bwd y", at::kBFloat16);
+    TORCH_CHECK(y_off + C <= y->size(3), "y slice");
+    yp = bf16p(*y) + y_off;
+    ys = (int)y->size(3);
+  }
+  c10::DeviceGuard gd(g.device());
+  launch_relu_bwd(g.data_ptr<float>() + g_off, (int)g.size(3), yp, ys, bf16m(out) + o_off,
+                  (int)out.size(3), (int)P, (int)C, (float)scale, cur_stream());
+}
+
+void gru_q_bwd_(const Tensor& dh, const Tensor& z, const Tensor& q, const Tensor& hprev,
+                const Tensor& dpre_q, const Tensor& dz, const Tensor& dhprev) {
+  TORCH_CHECK(dh.dim() == 4, "dh must be (B,H,W,hd)");
+  const int64_t P = dh.size(0) * dh.size(1) * dh.size(2), hd = dh.size(3);
+  check_pc(dh, P, hd, at::kFloat, "dh");
+  check_pc(z, P, hd, at::kBFloat16, "z");
+  check_pc(q, P, hd, at::kBFloat16, "q");
+  check_pc(hprev, P, hd, at::kBFloat16, "hprev");
+  check_pc(dpre_q, P, hd, at::kBFloat16, "dpre_q");
+  check_pc(dz, P, hd, at::kFloat, "dz");
+  check_pc(dhprev, P, hd, at::kFloat, "dhprev");
+  c10::DeviceGuard gd(dh.device());
+  launch_gru_q_bwd(dh.data_ptr<float>(), bf16p(z), bf16p(q), bf16p(hprev), bf16m(dpre_q),
+                   dz.data_ptr<float>(), dhprev.data_ptr<float>(), (int)P, (int)hd, cur_stream());
+}
+
+void gru_zr_bwd_(const Tensor& drh, const Tensor& dz, const Tensor& z, const Tensor& r,
+                 const Tensor& hprev, const Tensor& dpre_zr, const Tensor& dhprev) {
+  TORCH_CHECK(drh.dim() == 4, "drh must be (B,H,W,hd)");
+  const int64_t P = drh.size(0) * drh.size(1) * drh.size(2), hd = drh.size(3);
+  check_pc(drh, P, hd, at::kFloat, "drh");
+  check_pc(dz, P, hd, at::kFloat, "dz");
+  check_pc(z, P, hd, at::kBFloat16, "z");
+  check_pc(r, P, hd, at::kBFloat16, "r");
+  check_pc(hprev, P, hd, at::kBFloat16, "hprev");
+  check_pc(dpre_zr, P, 2 * hd, at::kBFloat16, "dpre_zr");
+  check_pc(dhprev, P, hd, at::kFloat, "dhprev");
+  c10::DeviceGuard gd(drh.device());
+  launch_gru_zr_bwd(drh.data_ptr<float>(), dz.data_ptr<float>(), bf16p(z), bf16p(r), bf16p(hprev),
+                    bf16m(dpre_zr), dhprev.data_ptr<float>(), (int)P, (int)hd, cur_stream());
+}
+
+// flow (B,2,H,W) fp32 -> flowb (B,H,W,8) bf16 [fx, fy, 0...]; optionally slot[..., off:off+2] = flow
+void flow_prep_(const Tensor& flow, const Tensor& flowb, const c10::optional<Tensor>& slot,
+                int64_t slot_off) {
+  check_cuda_f32(flow, "flow");
+  TORCH_CHECK(flow.dim() == 4 && flow.size(1) == 2, "flow must be (B,2,H,W)");
+  const int64_t B = flow.size(0), H = flow.size(2), W = flow.size(3);
+  check_nhwc(flowb, B, H, W, "flowb", at::kBFloat16);
+  TORCH_CHECK(flowb.size(3) == 8, "flowb must have 8 channels");
+  uint16_t* sp = nullptr;
+  int ss = 0;
+  if (slot.has_value() && slot->defined()) {
+    check_nhwc(*slot, B, H, W, "slot", at::kBFloat16);
+    TORCH_CHECK(slot_off + 2 <= slot->size(3), "slot range");
+    sp = bf16m(*slot) + slot_off;
+    ss = (int)slot->size(3);
+  }
+  c10::DeviceGuard gd(flow.device());
+  launch_flow_prep(flow.data_ptr<float>(), bf16m(flowb), sp, ss, (int)B, (int)(H * W), cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(raft_amd, m) {
@@ -459,8 +653,14 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_pyr_grad_reduce(Tensor[] gpyr, float inv_sqrt_c) -> Tensor");
   m.def("corr_otf_fwd(Tensor f1, Tensor[] f2, Tensor coords, int radius) -> Tensor");
   m.def("corr_otf_bwd_(Tensor f1, Tensor[] f2, Tensor coords, Tensor dout, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
-  m.def("convex_up_fwd(Tensor flow, Tensor mask) -> Tensor");
-  m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout) -> Tensor[]");
+  m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");
+  m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout, bool nhwc=False) -> Tensor[]");
+  m.def("corr_lookup_nhwc_(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
+  m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc) -> ()");
+  m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale) -> ()");
+  m.def("gru_q_bwd_(Tensor dh, Tensor z, Tensor q, Tensor hprev, Tensor(a!) dpre_q, Tensor(b!) dz, Tensor(c!) dhprev) -> ()");
+  m.def("gru_zr_bwd_(Tensor drh, Tensor dz, Tensor z, Tensor r, Tensor hprev, Tensor(a!) dpre_zr, Tensor(b!) dhprev) -> ()");
+  m.def("flow_prep_(Tensor flow, Tensor(a!) flowb, Tensor(b!)? slot, int slot_off) -> ()");
   m.def("seq_loss_fwd(Tensor[] preds, Tensor gt, Tensor valid, float gamma, float max_flow) -> Tensor");
   m.def("seq_loss_bwd(Tensor[] preds, Tensor gt, Tensor valid, Tensor dloss, float gamma, float max_flow) -> Tensor[]");
   m.def("warp_fwd(Tensor img, Tensor flow, float sx, float bx, float sy, float by) -> Tensor");
@@ -484,4 +684,10 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("warp_bwd", &warp_bwd);
   m.impl("conv_fwd_", &conv_fwd_);
   m.impl("conv_wgrad_", &conv_wgrad_);
+  m.impl("corr_lookup_nhwc_", &corr_lookup_nhwc_);
+  m.impl("conv_dgrad_", &conv_dgrad_);
+  m.impl("relu_bwd_", &relu_bwd_);
+  m.impl("gru_q_bwd_", &gru_q_bwd_);
+  m.impl("gru_zr_bwd_", &gru_zr_bwd_);
+  m.impl("flow_prep_", &flow_prep_);
 }

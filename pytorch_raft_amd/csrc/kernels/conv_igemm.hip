@@ -222,6 +222,21 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(ConvFwdArgs a) {
             ((uint16_t*)a.out1)[(int64_t)m * a.out1_stride + c] = raft_f32_to_bf16(g * h);  // r*h
             ((uint16_t*)a.out2)[(int64_t)m * a.out2_stride + c] = raft_f32_to_bf16(g);      // r
           }
+        } else if constexpr (EPI == EPI_DGRAD) {
+          // output channel n -> one of up to 3 fp32 gradient buffers (store or accumulate)
+          int s = 0, base = 0;
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            if (s + 1 < a.noseg && n >= base + a.oseg[s].cnt) { base += a.oseg[s].cnt; ++s; }
+          const OSeg o = a.oseg[s];
+          const int c = n - base;
+          if (o.ptr != nullptr && c < o.real) {
+            float* dst = o.ptr + (int64_t)m * o.stride + c;
+            if (o.acc) *dst += v; else *dst = v;
+          }
+        } else if constexpr (EPI == EPI_F32_NCHW) {
+          const int b = m / HW, yx = m - b * HW;
+          ((float*)a.out0)[((int64_t)b * a.cout + n) * HW + yx] = v;
         } else if constexpr (EPI == EPI_GRU_Q) {
           const float q = tanhf_(v);
           const float h = raft_bf16_to_f32(a.aux0[(int64_t)m * a.aux0_stride + n]);
@@ -264,6 +279,8 @@ bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStre
     case EPI_ACC_F32: launch_epi<EPI_ACC_F32>(a, bn, smallc, stream); return true;
     case EPI_GRU_ZR: launch_epi<EPI_GRU_ZR>(a, bn, false, stream); return true;
     case EPI_GRU_Q: launch_epi<EPI_GRU_Q>(a, bn, false, stream); return true;
+    case EPI_DGRAD: launch_epi<EPI_DGRAD>(a, bn, smallc, stream); return true;
+    case EPI_F32_NCHW: launch_epi<EPI_F32_NCHW>(a, bn, smallc, stream); return true;
     default: return false;
   }
 }

@@ -31,10 +31,17 @@ struct PyrG {
 
 __device__ __forceinline__ float clamp_coord(float v) { return fminf(fmaxf(v, -1.0e7f), 1.0e7f); }
 
-template <int R>
+// Output addressing: element (b, pixel i, channel ch) at b*os.b + i*os.p + ch*os.c, so one kernel
+// writes NCHW fp32 (reference layout) or NHWC bf16 straight into the fused update block's input
+// buffer (channel stride 1, zero-padded pixel stride).
+struct OStride {
+  int64_t b, p, c;
+};
+
+template <int R, typename TO>
 __global__ __launch_bounds__(64) void corr_lookup_fwd_kernel(PyrC pyr, const float* __restrict__ coords,
-                                                            float* __restrict__ out, int B, int H,
-                                                            int W, int levels) {
+                                                            TO* __restrict__ out, OStride os, int B,
+                                                            int H, int W, int levels) {
   constexpr int D = 2 * R + 1;
   const int N = H * W;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -50,7 +57,7 @@ __global__ __launch_bounds__(64) void corr_lookup_fwd_kernel(PyrC pyr, const flo
   const float ax = cx - fx, ay = cy - fy;
   const int xs = (int)fx - R, ys = (int)fy - R;
   const float* P = pyr.lvl[l] + ((int64_t)b * N + i) * hl * wl;
-  float* O = out + ((int64_t)b * levels * D * D + l * D * D) * N + i;
+  TO* O = out + b * os.b + i * os.p + (int64_t)l * D * D * os.c;
 
   float hprev[D], hcur[D];
 #pragma unroll
@@ -69,7 +76,7 @@ __global__ __launch_bounds__(64) void corr_lookup_fwd_kernel(PyrC pyr, const flo
       const int iy = yy - 1;
 #pragma unroll
       for (int ix = 0; ix < D; ++ix)
-        O[(int64_t)(ix * D + iy) * N] = (1.f - ay) * hprev[ix] + ay * hcur[ix];
+        St<TO>::put(O, (int64_t)(ix * D + iy) * os.c, (1.f - ay) * hprev[ix] + ay * hcur[ix]);
     }
 #pragma unroll
     for (int ix = 0; ix < D; ++ix) hprev[ix] = hcur[ix];
@@ -78,8 +85,8 @@ __global__ __launch_bounds__(64) void corr_lookup_fwd_kernel(PyrC pyr, const flo
 
 template <int R>
 __global__ __launch_bounds__(64) void corr_lookup_bwd_kernel(PyrG g, const float* __restrict__ coords,
-                                                            const float* __restrict__ dout, int B,
-                                                            int H, int W, int levels) {
+                                                            const float* __restrict__ dout, OStride os,
+                                                            int B, int H, int W, int levels) {
   constexpr int D = 2 * R + 1;
   const int N = H * W;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -95,7 +102,7 @@ __global__ __launch_bounds__(64) void corr_lookup_bwd_kernel(PyrG g, const float
   const float ax = cx - fx, ay = cy - fy;
   const int xs = (int)fx - R, ys = (int)fy - R;
   float* G = g.lvl[l] + ((int64_t)b * N + i) * hl * wl;
-  const float* dO = dout + ((int64_t)b * levels * D * D + l * D * D) * N + i;
+  const float* dO = dout + b * os.b + i * os.p + (int64_t)l * D * D * os.c;
 
   // hs_iy[xx] = (1-ax) d[xx][iy] + ax d[xx-1][iy]  (horizontal adjoint of tap row iy)
   float hprev[D + 1];
@@ -107,7 +114,7 @@ __global__ __launch_bounds__(64) void corr_lookup_bwd_kernel(PyrG g, const float
     if (yy < D) {
       float d[D];
 #pragma unroll
-      for (int ix = 0; ix < D; ++ix) d[ix] = dO[(int64_t)(ix * D + yy) * N];
+      for (int ix = 0; ix < D; ++ix) d[ix] = dO[(int64_t)(ix * D + yy) * os.c];
 #pragma unroll
       for (int xx = 0; xx <= D; ++xx) {
         float s = 0.f;
@@ -145,33 +152,36 @@ P make_pyr(float* const* lvl, const int* hs, const int* ws, int levels) {
 
 }  // namespace
 
+// out layout: element (b, i, ch) at b*bs + i*ps + ch*cs; out_bf16 selects bf16 storage
 bool launch_corr_lookup_fwd(const float* const* lvl, const int* hs, const int* ws, int levels,
-                            const float* coords, float* out, int B, int H, int W, int radius,
-                            hipStream_t stream) {
+                            const float* coords, void* out, int out_bf16, int64_t bs, int64_t ps,
+                            int64_t cs, int B, int H, int W, int radius, hipStream_t stream) {
   PyrC p;
   for (int l = 0; l < 4; ++l) {
     p.lvl[l] = l < levels ? lvl[l] : nullptr;
     p.h[l] = l < levels ? hs[l] : 0;
     p.w[l] = l < levels ? ws[l] : 0;
   }
+  OStride os{bs, ps, cs};
   const int64_t total = (int64_t)B * levels * H * W;
   dim3 grid(raft_cdiv(total, 64));
-  switch (radius) {
-    case 3: hipLaunchKernelGGL(corr_lookup_fwd_kernel<3>, grid, dim3(64), 0, stream, p, coords, out, B, H, W, levels); return true;
-    case 4: hipLaunchKernelGGL(corr_lookup_fwd_kernel<4>, grid, dim3(64), 0, stream, p, coords, out, B, H, W, levels); return true;
-    default: return false;
-  }
+#define LK(R, T) hipLaunchKernelGGL((corr_lookup_fwd_kernel<R, T>), grid, dim3(64), 0, stream, p, coords, (T*)out, os, B, H, W, levels)
+  if (radius == 3) { if (out_bf16) LK(3, uint16_t); else LK(3, float); return true; }
+  if (radius == 4) { if (out_bf16) LK(4, uint16_t); else LK(4, float); return true; }
+#undef LK
+  return false;
 }
 
 bool launch_corr_lookup_bwd(float* const* glvl, const int* hs, const int* ws, int levels,
-                            const float* coords, const float* dout, int B, int H, int W, int radius,
-                            hipStream_t stream) {
+                            const float* coords, const float* dout, int64_t bs, int64_t ps,
+                            int64_t cs, int B, int H, int W, int radius, hipStream_t stream) {
   PyrG p = make_pyr<PyrG>(glvl, hs, ws, levels);
+  OStride os{bs, ps, cs};
   const int64_t total = (int64_t)B * levels * H * W;
   dim3 grid(raft_cdiv(total, 64));
   switch (radius) {
-    case 3: hipLaunchKernelGGL(corr_lookup_bwd_kernel<3>, grid, dim3(64), 0, stream, p, coords, dout, B, H, W, levels); return true;
-    case 4: hipLaunchKernelGGL(corr_lookup_bwd_kernel<4>, grid, dim3(64), 0, stream, p, coords, dout, B, H, W, levels); return true;
+    case 3: hipLaunchKernelGGL(corr_lookup_bwd_kernel<3>, grid, dim3(64), 0, stream, p, coords, dout, os, B, H, W, levels); return true;
+    case 4: hipLaunchKernelGGL(corr_lookup_bwd_kernel<4>, grid, dim3(64), 0, stream, p, coords, dout, os, B, H, W, levels); return true;
     default: return false;
   }
 }

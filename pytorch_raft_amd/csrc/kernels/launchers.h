@@ -20,11 +20,11 @@ void launch_corr_pyr_grad_reduce(float* const* glvl, const int* hs, const int* w
 
 // ---- window lookup (corr_lookup.hip); return false for an unsupported radius
 bool launch_corr_lookup_fwd(const float* const* lvl, const int* hs, const int* ws, int levels,
-                            const float* coords, float* out, int B, int H, int W, int radius,
-                            hipStream_t stream);
+                            const float* coords, void* out, int out_bf16, int64_t bs, int64_t ps,
+                            int64_t cs, int B, int H, int W, int radius, hipStream_t stream);
 bool launch_corr_lookup_bwd(float* const* glvl, const int* hs, const int* ws, int levels,
-                            const float* coords, const float* dout, int B, int H, int W, int radius,
-                            hipStream_t stream);
+                            const float* coords, const float* dout, int64_t bs, int64_t ps,
+                            int64_t cs, int B, int H, int W, int radius, hipStream_t stream);
 
 // ---- on-the-fly correlation (corr_onthefly.hip)
 bool launch_corr_otf_fwd(const float* f1, const float* const* f2lvl, const int* hs, const int* ws,
@@ -36,11 +36,13 @@ bool launch_corr_otf_bwd(const float* f1, const float* const* f2lvl, const int* 
                          hipStream_t stream);
 
 // ---- convex upsample (upsample.hip)
-bool launch_convex_up_fwd(const float* flow, const void* mask, int mask_is_bf16, float* out, int B,
-                          int H, int W, hipStream_t stream);
-bool launch_convex_up_bwd(const float* flow, const void* mask, int mask_is_bf16, const float* dout,
-                          void* dmask, float* wbuf, float* dflow, int B, int H, int W,
+// mask element (b, ch, y, x) at b*mbs + ch*mcs + (y*W+x)*mps  (NCHW: mcs=HW, mps=1; NHWC: mcs=1, mps=576)
+bool launch_convex_up_fwd(const float* flow, const void* mask, int mask_is_bf16, int64_t mbs,
+                          int64_t mcs, int64_t mps, float* out, int B, int H, int W,
                           hipStream_t stream);
+bool launch_convex_up_bwd(const float* flow, const void* mask, int mask_is_bf16, int64_t mbs,
+                          int64_t mcs, int64_t mps, const float* dout, void* dmask, float* wbuf,
+                          float* dflow, int B, int H, int W, hipStream_t stream);
 
 // ---- sequence loss (loss.hip)
 int seq_loss_partial_count();
@@ -66,12 +68,22 @@ enum ConvEpilogue {
   EPI_ACC_F32 = 3,    // out0 f32 += (acc + bias) * scale
   EPI_GRU_ZR = 4,     // n < split: out0 = sigmoid (z); else out1 = sigmoid * aux0 (r*h), out2 = r
   EPI_GRU_Q = 5,      // q = tanh; out0 = aux0 + aux1 * (q - aux0) (h'), out1 = q
+  EPI_DGRAD = 6,      // output channels split over oseg[] fp32 buffers (store or accumulate)
+  EPI_F32_NCHW = 7,   // out0 f32 NCHW (B, cout, H, W)
 };
 
 struct Seg {
   const uint16_t* ptr;  // bf16 NHWC base, already offset to the segment's first channel
   int stride;           // elements between consecutive pixels
   int cnt;              // channels (multiple of 32 unless SMALLC)
+};
+
+struct OSeg {
+  float* ptr;  // fp32 NHWC base offset to the segment's first channel (null: discard)
+  int stride;
+  int cnt;     // channel slots of this segment in the conv's output
+  int real;    // channels actually written (< cnt for zero-padded slots)
+  int acc;     // 1: +=, 0: =
 };
 
 struct ConvFwdArgs {
@@ -96,6 +108,8 @@ struct ConvFwdArgs {
   int aux1_stride;
   float scale;
   int split;
+  OSeg oseg[3];
+  int noseg;
 };
 
 bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStream_t stream);
@@ -116,3 +130,14 @@ struct ConvWgradArgs {
 
 bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, hipStream_t stream);
 void launch_col_sum(const uint16_t* g, int stride, int cout, int P, float* db, hipStream_t stream);
+
+// ---- fused update-block elementwise kernels (update_ew.hip)
+void launch_relu_bwd(const float* g, int gs, const uint16_t* y, int ys, uint16_t* out, int os, int P,
+                     int C, float scale, hipStream_t stream);
+void launch_gru_q_bwd(const float* dh, const uint16_t* z, const uint16_t* q, const uint16_t* hprev,
+                      uint16_t* dpre_q, float* dz, float* dhprev, int P, int hd, hipStream_t stream);
+void launch_gru_zr_bwd(const float* drh, const float* dz, const uint16_t* z, const uint16_t* r,
+                       const uint16_t* hprev, uint16_t* dpre_zr, float* dhprev, int P, int hd,
+                       hipStream_t stream);
+void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int slot_stride, int B,
+                      int HW, hipStream_t stream);

@@ -1,0 +1,119 @@
+// Fused elementwise kernels of the HIP update block (forward prep + backward gate algebra).
+//
+// The reference's SepConvGRU half-step (`core/update.py:45-58`) is, per half-step, cat -> conv ->
+// sigmoid, cat -> conv -> sigmoid, mul, cat -> conv -> tanh, 1-z, mul, mul, add; autograd then runs
+// the adjoint of each of those as separate kernels.  The forward gates are fused into the conv
+// epilogues (conv_igemm.hip); these kernels are the backward gate algebra, each ONE pass over
+// (pixels x 128) that turns the incoming fp32 gradient into the bf16 pre-activation gradients the
+// dgrad / wgrad MFMA kernels consume:
+//
+//   gru_q_bwd   h' = h + z (q - h):  dq = dh' z ; d(pre_q) = dq (1 - q^2) ; dz = dh' (q - h) ;
+//               dh = dh' (1 - z)
+//   gru_zr_bwd  rh = r h:  dr = d(rh) h ; dh += d(rh) r ;
+//               d(pre_z) = dz z (1 - z) ; d(pre_r) = dr r (1 - r)
+//   relu_bwd    d(pre) = g * [y > 0] (optionally scaled), fp32 -> bf16, strided channel slices
+//   flow_prep   (B,2,H,W) fp32 flow -> bf16 NHWC for the 7x7 flow conv + the GRU input slot
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__ g, int gs,
+                                                       const uint16_t* __restrict__ y, int ys,
+                                                       uint16_t* __restrict__ out, int os, int P,
+                                                       int C, float scale) {
+  const int64_t total = (int64_t)P * C;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = t / C;
+    const int c = (int)(t - p * C);
+    float v = g[p * gs + c] * scale;
+    if (y != nullptr && !(raft_bf16_to_f32(y[p * ys + c]) > 0.f)) v = 0.f;
+    out[p * os + c] = raft_f32_to_bf16(v);
+  }
+}
+
+// hd = hidden width (128 / 96).  dpre_q (bf16, stride dq_s), dz (f32 P x hd), dh_prev (f32 P x hd)
+__global__ __launch_bounds__(256) void gru_q_bwd_kernel(const float* __restrict__ dh, const uint16_t* __restrict__ z,
+                                                        const uint16_t* __restrict__ q, const uint16_t* __restrict__ hprev,
+                                                        uint16_t* __restrict__ dpre_q, float* __restrict__ dz,
+                                                        float* __restrict__ dhprev, int P, int hd) {
+  const int64_t total = (int64_t)P * hd;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const float g = dh[t];
+    const float zz = raft_bf16_to_f32(z[t]);
+    const float qq = raft_bf16_to_f32(q[t]);
+    const float hh = raft_bf16_to_f32(hprev[t]);
+    dpre_q[t] = raft_f32_to_bf16(g * zz * (1.f - qq * qq));
+    dz[t] = g * (qq - hh);
+    dhprev[t] = g * (1.f - zz);
+  }
+}
+
+// dpre_zr (bf16 P x 2hd: [z | r]), dhprev += drh * r
+__global__ __launch_bounds__(256) void gru_zr_bwd_kernel(const float* __restrict__ drh, const float* __restrict__ dz,
+                                                         const uint16_t* __restrict__ z, const uint16_t* __restrict__ r,
+                                                         const uint16_t* __restrict__ hprev, uint16_t* __restrict__ dpre_zr,
+                                                         float* __restrict__ dhprev, int P, int hd) {
+  const int64_t total = (int64_t)P * hd;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = t / hd;
+    const int c = (int)(t - p * hd);
+    const float zz = raft_bf16_to_f32(z[t]);
+    const float rr = raft_bf16_to_f32(r[t]);
+    const float hh = raft_bf16_to_f32(hprev[t]);
+    const float g = drh[t];
+    dpre_zr[p * 2 * hd + c] = raft_f32_to_bf16(dz[t] * zz * (1.f - zz));
+    dpre_zr[p * 2 * hd + hd + c] = raft_f32_to_bf16(g * hh * rr * (1.f - rr));
+    dhprev[t] += g * rr;
+  }
+}
+
+__global__ __launch_bounds__(256) void flow_prep_kernel(const float* __restrict__ flow, uint16_t* __restrict__ flowb,
+                                                        uint16_t* __restrict__ slot, int slot_stride, int B, int HW) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)B * HW) return;
+  const int64_t b = t / HW, yx = t - b * HW;
+  const uint16_t fx = raft_f32_to_bf16(flow[(b * 2) * HW + yx]);
+  const uint16_t fy = raft_f32_to_bf16(flow[(b * 2 + 1) * HW + yx]);
+  uint4 v = make_uint4(fx | ((uint32_t)fy << 16), 0, 0, 0);
+  *reinterpret_cast<uint4*>(flowb + t * 8) = v;
+  if (slot != nullptr) {
+    slot[t * slot_stride] = fx;
+    slot[t * slot_stride + 1] = fy;
+  }
+}
+
+inline unsigned ew_blocks(int64_t total) {
+  return (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 16);
+}
+
+}  // namespace
+
+void launch_relu_bwd(const float* g, int gs, const uint16_t* y, int ys, uint16_t* out, int os, int P,
+                     int C, float scale, hipStream_t stream) {
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(ew_blocks((int64_t)P * C)), dim3(256), 0, stream, g, gs, y,
+                     ys, out, os, P, C, scale);
+}
+
+void launch_gru_q_bwd(const float* dh, const uint16_t* z, const uint16_t* q, const uint16_t* hprev,
+                      uint16_t* dpre_q, float* dz, float* dhprev, int P, int hd, hipStream_t stream) {
+  hipLaunchKernelGGL(gru_q_bwd_kernel, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream, dh, z, q,
+                     hprev, dpre_q, dz, dhprev, P, hd);
+}
+
+void launch_gru_zr_bwd(const float* drh, const float* dz, const uint16_t* z, const uint16_t* r,
+                       const uint16_t* hprev, uint16_t* dpre_zr, float* dhprev, int P, int hd,
+                       hipStream_t stream) {
+  hipLaunchKernelGGL(gru_zr_bwd_kernel, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream, drh, dz,
+                     z, r, hprev, dpre_zr, dhprev, P, hd);
+}
+
+void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int slot_stride, int B,
+                      int HW, hipStream_t stream) {
+  const int64_t total = (int64_t)B * HW;
+  hipLaunchKernelGGL(flow_prep_kernel, dim3(raft_cdiv(total, 256)), dim3(256), 0, stream, flow, flowb,
+                     slot, slot_stride, B, HW);
+}

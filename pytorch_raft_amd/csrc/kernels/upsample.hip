@@ -17,7 +17,8 @@ namespace {
 
 template <typename TM>
 __global__ __launch_bounds__(256) void convex_up_fwd_kernel(const float* __restrict__ flow,
-                                                            const TM* __restrict__ mask,
+                                                            const TM* __restrict__ mask, int64_t mbs,
+                                                            int64_t mcs, int64_t mps,
                                                             float* __restrict__ out, int H, int W) {
   const int xi = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int x = blockIdx.x * 64 + xi, y = blockIdx.y, b = blockIdx.z;
@@ -32,7 +33,7 @@ __global__ __launch_bounds__(256) void convex_up_fwd_kernel(const float* __restr
     nf[k][0] = ok ? 8.f * F[(int64_t)yy * W + xx] : 0.f;
     nf[k][1] = ok ? 8.f * F[HW + (int64_t)yy * W + xx] : 0.f;
   }
-  const TM* M = mask + (int64_t)b * 576 * HW + (int64_t)y * W + x;
+  const TM* M = mask + (int64_t)b * mbs + ((int64_t)y * W + x) * mps;
   float* O = out + (int64_t)b * 2 * 64 * HW;
   const int W8 = 8 * W;
   for (int s = g * 16; s < g * 16 + 16; ++s) {
@@ -40,7 +41,7 @@ __global__ __launch_bounds__(256) void convex_up_fwd_kernel(const float* __restr
     float mx = -INFINITY;
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
-      m[k] = Ld<TM>::get(M, (int64_t)(k * 64 + s) * HW);
+      m[k] = Ld<TM>::get(M, (int64_t)(k * 64 + s) * mcs);
       mx = fmaxf(mx, m[k]);
     }
     float den = 0.f, o0 = 0.f, o1 = 0.f;
@@ -63,6 +64,7 @@ __global__ __launch_bounds__(256) void convex_up_fwd_kernel(const float* __restr
 template <typename TM>
 __global__ __launch_bounds__(256) void convex_up_bwd_kernel(const float* __restrict__ flow,
                                                             const TM* __restrict__ mask,
+                                                            int64_t mbs, int64_t mcs, int64_t mps,
                                                             const float* __restrict__ dout,
                                                             TM* __restrict__ dmask,
                                                             float* __restrict__ wbuf, int H, int W) {
@@ -85,8 +87,8 @@ __global__ __launch_bounds__(256) void convex_up_bwd_kernel(const float* __restr
       nf[k][1] = ok ? 8.f * F[HW + (int64_t)yy * W + xx] : 0.f;
     }
     const int64_t cell = (int64_t)y * W + x;
-    const TM* M = mask + (int64_t)b * 576 * HW + cell;
-    TM* DM = dmask + (int64_t)b * 576 * HW + cell;
+    const TM* M = mask + (int64_t)b * mbs + cell * mps;
+    TM* DM = dmask + (int64_t)b * mbs + cell * mps;
     const float* DO = dout + (int64_t)b * 2 * 64 * HW;
     const int W8 = 8 * W;
     for (int s = g * 16; s < g * 16 + 16; ++s) {
@@ -94,7 +96,7 @@ __global__ __launch_bounds__(256) void convex_up_bwd_kernel(const float* __restr
       float mx = -INFINITY;
 #pragma unroll
       for (int k = 0; k < 9; ++k) {
-        m[k] = Ld<TM>::get(M, (int64_t)(k * 64 + s) * HW);
+        m[k] = Ld<TM>::get(M, (int64_t)(k * 64 + s) * mcs);
         mx = fmaxf(mx, m[k]);
       }
       float den = 0.f;
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(256) void convex_up_bwd_kernel(const float* __restr
       }
 #pragma unroll
       for (int k = 0; k < 9; ++k)
-        St<TM>::put(DM, (int64_t)(k * 64 + s) * HW, m[k] * (gk[k] - dot));
+        St<TM>::put(DM, (int64_t)(k * 64 + s) * mcs, m[k] * (gk[k] - dot));
     }
   }
 #pragma unroll
@@ -162,28 +164,29 @@ __global__ __launch_bounds__(256) void convex_up_bwd_flow_kernel(const float* __
 
 }  // namespace
 
-bool launch_convex_up_fwd(const float* flow, const void* mask, int mask_is_bf16, float* out, int B,
-                          int H, int W, hipStream_t stream) {
-  dim3 grid(raft_cdiv(W, 64), H, B);
-  if (mask_is_bf16)
-    hipLaunchKernelGGL(convex_up_fwd_kernel<uint16_t>, grid, dim3(256), 0, stream, flow,
-                       (const uint16_t*)mask, out, H, W);
-  else
-    hipLaunchKernelGGL(convex_up_fwd_kernel<float>, grid, dim3(256), 0, stream, flow,
-                       (const float*)mask, out, H, W);
-  return true;
-}
-
-bool launch_convex_up_bwd(const float* flow, const void* mask, int mask_is_bf16, const float* dout,
-                          void* dmask, float* wbuf, float* dflow, int B, int H, int W,
+bool launch_convex_up_fwd(const float* flow, const void* mask, int mask_is_bf16, int64_t mbs,
+                          int64_t mcs, int64_t mps, float* out, int B, int H, int W,
                           hipStream_t stream) {
   dim3 grid(raft_cdiv(W, 64), H, B);
   if (mask_is_bf16)
+    hipLaunchKernelGGL(convex_up_fwd_kernel<uint16_t>, grid, dim3(256), 0, stream, flow,
+                       (const uint16_t*)mask, mbs, mcs, mps, out, H, W);
+  else
+    hipLaunchKernelGGL(convex_up_fwd_kernel<float>, grid, dim3(256), 0, stream, flow,
+                       (const float*)mask, mbs, mcs, mps, out, H, W);
+  return true;
+}
+
+bool launch_convex_up_bwd(const float* flow, const void* mask, int mask_is_bf16, int64_t mbs,
+                          int64_t mcs, int64_t mps, const float* dout, void* dmask, float* wbuf,
+                          float* dflow, int B, int H, int W, hipStream_t stream) {
+  dim3 grid(raft_cdiv(W, 64), H, B);
+  if (mask_is_bf16)
     hipLaunchKernelGGL(convex_up_bwd_kernel<uint16_t>, grid, dim3(256), 0, stream, flow,
-                       (const uint16_t*)mask, dout, (uint16_t*)dmask, wbuf, H, W);
+                       (const uint16_t*)mask, mbs, mcs, mps, dout, (uint16_t*)dmask, wbuf, H, W);
   else
     hipLaunchKernelGGL(convex_up_bwd_kernel<float>, grid, dim3(256), 0, stream, flow,
-                       (const float*)mask, dout, (float*)dmask, wbuf, H, W);
+                       (const float*)mask, mbs, mcs, mps, dout, (float*)dmask, wbuf, H, W);
   const int64_t total = (int64_t)B * H * W;
   hipLaunchKernelGGL(convex_up_bwd_flow_kernel, dim3(raft_cdiv(total, 256)), dim3(256), 0, stream,
                      wbuf, dflow, B, H, W);

@@ -131,9 +131,22 @@ class CorrBlock:
             return self.volume.lookup(coords, self.radius)
         return torch_corr_lookup(self.corr_pyramid, coords, self.radius)
 
+    def lookup_nhwc(self, coords, cbuf):
+        """bf16 (B,H,W,cbuf) zero-padded taps for the fused HIP update block."""
+        if self.hip:
+            return self.volume.lookup_nhwc(coords, self.radius, cbuf)
+        return _to_nhwc_padded(self(coords), cbuf)
+
     @staticmethod
     def corr(fmap1, fmap2):
         return torch_corr_volume(fmap1, fmap2)
+
+
+def _to_nhwc_padded(corr, cbuf):
+    x = corr.permute(0, 2, 3, 1).to(torch.bfloat16)
+    if cbuf > x.shape[-1]:
+        x = F.pad(x, (0, cbuf - x.shape[-1]))
+    return x.contiguous()
 
 
 class AlternateCorrBlock:
@@ -156,3 +169,6 @@ class AlternateCorrBlock:
         if self.hip:
             return self.volume.lookup(coords, self.radius)
         return torch_onthefly_corr(self.pyramid2, self.fmap1, coords, self.radius)
+
+    def lookup_nhwc(self, coords, cbuf):
+        return _to_nhwc_padded(self(coords), cbuf)

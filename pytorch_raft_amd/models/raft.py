@@ -120,6 +120,9 @@ class RAFT(nn.Module):
         if flow_init is not None:
             coords1 = coords1 + flow_init
 
+        if self._use_fused_update(image1):
+            return self._iterate_fused(net, inp, corr_fn, coords0, coords1, iters, test_mode)
+
         flow_predictions = []
         flow_up = None
         for itr in range(iters):
@@ -137,6 +140,40 @@ class RAFT(nn.Module):
                 flow_up = self.upsample_flow(coords1 - coords0, up_mask)
             flow_predictions.append(flow_up)
 
+        if test_mode:
+            return coords1 - coords0, flow_up
+        return flow_predictions
+
+    # ------------------------------------------------------------------ fused HIP update path
+    def _use_fused_update(self, img):
+        """Fused MFMA update block: GPU, full model, bf16 mixed precision (its compute dtype)."""
+        impl = _get(self.args, 'update_impl', 'auto')
+        if impl == 'torch' or self.corr_impl == 'torch' or self.args.small or not img.is_cuda:
+            return False
+        if not (self.args.mixed_precision and self.amp_dtype == torch.bfloat16):
+            if impl == 'hip':
+                raise ValueError("update_impl='hip' needs mixed_precision with amp_dtype='bfloat16'")
+            return False
+        from ..ops import update_hip
+        return update_hip.available(required=(impl == 'hip'))
+
+    def _iterate_fused(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
+        from ..ops.update_hip import HipUpdateBlock
+        hub = HipUpdateBlock(self.update_block)
+        h = net.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+        x = inp.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+        flow_predictions = []
+        flow_up = None
+        for itr in range(iters):
+            coords1 = coords1.detach()
+            corr = corr_fn.lookup_nhwc(coords1, 352)
+            flow = coords1 - coords0
+            h, delta_flow, up_mask = hub(h, x, corr, flow)
+            coords1 = coords1 + delta_flow
+            if test_mode and itr < iters - 1:
+                continue
+            flow_up = convex_upsample(coords1 - coords0, up_mask, nhwc=True)
+            flow_predictions.append(flow_up)
         if test_mode:
             return coords1 - coords0, flow_up
         return flow_predictions

@@ -82,6 +82,30 @@ class _AllPairsLookup(torch.autograd.Function):
         return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None
 
 
+class _AllPairsLookupNHWC(torch.autograd.Function):
+    """Lookup writing bf16 taps into a zero-padded NHWC (B,H,W,cbuf) buffer: the direct input of
+    the fused update block's first 1x1 conv (no NCHW->NHWC transpose, no fp32->bf16 cast kernel)."""
+
+    @staticmethod
+    def forward(ctx, token, coords, radius, state, cbuf):
+        b, _, h, w = coords.shape
+        out = torch.zeros(b, h, w, cbuf, device=coords.device, dtype=torch.bfloat16)
+        _ext.ops().corr_lookup_nhwc_(state.pyramid, coords, radius, out)
+        ctx.state = state
+        ctx.radius = radius
+        ctx.save_for_backward(coords)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        st = ctx.state
+        (coords,) = ctx.saved_tensors
+        if st.grad is None:
+            st.grad = [torch.zeros_like(p) for p in st.pyramid]
+        _ext.ops().corr_lookup_bwd_(st.grad, coords, dout.float().contiguous(), ctx.radius)
+        return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None, None
+
+
 class AllPairsVolume:
     def __init__(self, fmap1, fmap2, num_levels=4):
         self.state = _State()
@@ -95,6 +119,10 @@ class AllPairsVolume:
 
     def lookup(self, coords, radius):
         return _AllPairsLookup.apply(self.token, coords.contiguous().float(), radius, self.state)
+
+    def lookup_nhwc(self, coords, radius, cbuf):
+        return _AllPairsLookupNHWC.apply(self.token, coords.contiguous().float(), radius, self.state,
+                                         cbuf)
 
 
 def _pool_nhwc(x):

@@ -1,0 +1,346 @@
+"""Fused HIP update block for RAFT (full model): motion encoder + SepConvGRU + flow/mask heads.
+
+Reference: `core/update.py:79-136` (BasicMotionEncoder, SepConvGRU, FlowHead, mask head) executed
+once per GRU iteration under autocast.  Eager PyTorch runs ~110 ATen ops per iteration forward and
+~280 forward+backward (cat, cast, conv, bias-grad reductions, sigmoid/tanh/mul/add and their
+adjoints); on MI355X the step is dominated by per-kernel overhead rather than FLOPs.
+
+This module runs one iteration as ONE autograd node built from the hand-written gfx950 kernels:
+
+forward (12 MFMA implicit-GEMM convs + 1 prep kernel, NHWC bf16, fp32 accumulation)::
+
+    corr(352, from the lookup kernel) -c1(1x1,relu)-> c1(256) -c2(3x3,relu)-> cf[0:192]
+    flow -prep-> flowb(8) -f1(7x7,relu, dense-K small-Cin path)-> f1(128) -f2(3x3,relu)-> cf[192:256]
+    cf -conv(3x3,relu)-> mf[0:126] ; mf[126:128] = flow
+    [h | inp | mf] -zr1(1x5, sigmoid epilogue)-> z1, r1, r1*h
+    [r1*h | inp | mf] -q1(1x5, tanh + GRU-update epilogue)-> h1, q1         (same for 5x1 -> h2)
+    h2 -head(3x3, relu; flow_head.conv1 | mask.0 fused N=512)-> fm(512)
+    fm[0:256] -f2(3x3)-> delta (fp32, NCHW)     fm[256:512] -mask.2(1x1, x0.25)-> mask (NHWC bf16)
+
+backward: bf16 pre-activation gradients from fused elementwise kernels (relu / GRU gate algebra),
+dgrad = the same conv kernel on flipped/transposed weights writing fp32 gradients into channel
+slices (virtual concat outputs, store or accumulate), wgrad = the split-K MFMA kernel with
+transposing LDS reads accumulating into per-step fp32 packed weight-gradient buffers.
+
+Weights are packed once per forward pass by ``_UpdateWeights`` whose backward (run by autograd
+after every iteration's backward) unpacks the accumulated packed gradients into the nn.Conv2d
+``.grad`` tensors -- the checkpoint layout is unchanged.
+"""
+import torch
+
+from . import _ext
+from . import conv as C
+
+HD = 128  # hidden / context width of the full model
+
+
+class _LayerSpec:
+    """Geometry of one conv of the fused block."""
+
+    def __init__(self, name, cout, ksize, in_real, in_pad, small=False, relu=False, scale=1.0):
+        self.name = name
+        self.cout = cout
+        self.k = ksize
+        self.pad = (ksize[0] // 2, ksize[1] // 2)
+        self.in_real = in_real
+        self.in_pad = in_pad
+        self.small = small
+        self.relu = relu
+        self.scale = scale
+
+
+SPECS = [
+    _LayerSpec('c1', 256, (1, 1), [324], [352]),
+    _LayerSpec('c2', 192, (3, 3), [256], [256]),
+    _LayerSpec('f1', 128, (7, 7), [2], [8], small=True),
+    _LayerSpec('f2', 64, (3, 3), [128], [128]),
+    _LayerSpec('conv', 126, (3, 3), [256], [256]),
+    _LayerSpec('zr1', 256, (1, 5), [128, 128, 128], [128, 128, 128]),
+    _LayerSpec('q1', 128, (1, 5), [128, 128, 128], [128, 128, 128]),
+    _LayerSpec('zr2', 256, (5, 1), [128, 128, 128], [128, 128, 128]),
+    _LayerSpec('q2', 128, (5, 1), [128, 128, 128], [128, 128, 128]),
+    _LayerSpec('head', 512, (3, 3), [128], [128]),
+    _LayerSpec('fh2', 2, (3, 3), [256], [256]),
+    _LayerSpec('m2', 576, (1, 1), [256], [256], scale=0.25),
+]
+SPEC = {s.name: s for s in SPECS}
+
+
+def module_params(ub):
+    """(weight, bias) tensors of each fused layer, in SPECS order, from a BasicUpdateBlock."""
+    e, g, fh, mk = ub.encoder, ub.gru, ub.flow_head, ub.mask
+    return {
+        'c1': [(e.convc1.weight, e.convc1.bias)],
+        'c2': [(e.convc2.weight, e.convc2.bias)],
+        'f1': [(e.convf1.weight, e.convf1.bias)],
+        'f2': [(e.convf2.weight, e.convf2.bias)],
+        'conv': [(e.conv.weight, e.conv.bias)],
+        'zr1': [(g.convz1.weight, g.convz1.bias), (g.convr1.weight, g.convr1.bias)],
+        'q1': [(g.convq1.weight, g.convq1.bias)],
+        'zr2': [(g.convz2.weight, g.convz2.bias), (g.convr2.weight, g.convr2.bias)],
+        'q2': [(g.convq2.weight, g.convq2.bias)],
+        'head': [(fh.conv1.weight, fh.conv1.bias), (mk[0].weight, mk[0].bias)],
+        'fh2': [(fh.conv2.weight, fh.conv2.bias)],
+        'm2': [(mk[2].weight, mk[2].bias)],
+    }
+
+
+def flat_params(ub):
+    mp = module_params(ub)
+    out = []
+    for s in SPECS:
+        for w, b in mp[s.name]:
+            out += [w, b]
+    return out
+
+
+class _Packed:
+    """Per-step packed weights (bf16) + packed fp32 gradient accumulators."""
+
+    def __init__(self, params_by_layer, device, need_grad):
+        self.w = {}
+        self.wd = {}
+        self.b = {}
+        self.kpad = {}
+        self.dw = {}
+        self.db = {}
+        with torch.no_grad():
+            for s in SPECS:
+                ws = [w for w, _ in params_by_layer[s.name]]
+                bs = [b for _, b in params_by_layer[s.name]]
+                w = ws[0] if len(ws) == 1 else torch.cat(ws, 0)
+                b = bs[0] if len(bs) == 1 else torch.cat(bs, 0)
+                w = w.float()
+                if s.small:
+                    self.w[s.name] = C.pack_weight_small(w)
+                else:
+                    self.w[s.name] = C.pack_weight(w, s.in_real, s.in_pad)
+                self.kpad[s.name] = self.w[s.name].shape[1]
+                self.b[s.name] = b.float().contiguous()
+                if need_grad and s.name != 'f1':
+                    # adjoint conv: inputs = this layer's output channels, outputs = its inputs
+                    if s.name == 'fh2':
+                        wt = w.flip(2, 3).transpose(0, 1).contiguous()  # (256, 2, 3, 3)
+                        self.wd[s.name] = C.pack_weight_small(wt)
+                    else:
+                        cout_pad = C.round_up(s.cout, 32)
+                        wt = w
+                        if cout_pad > s.cout:
+                            wt = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 0, 0, cout_pad - s.cout))
+                        wt = wt.flip(2, 3).transpose(0, 1).contiguous()  # (Cin, CoutPad, kh, kw)
+                        if sum(s.in_pad) > sum(s.in_real):
+                            # padded input slots become zero output rows of the adjoint
+                            parts, off = [], 0
+                            for r, p in zip(s.in_real, s.in_pad):
+                                part = wt[off:off + r]
+                                if p > r:
+                                    part = torch.nn.functional.pad(part, (0, 0, 0, 0, 0, 0, 0, p - r))
+                                parts.append(part)
+                                off += r
+                            wt = torch.cat(parts, 0)
+                        self.wd[s.name] = C.pack_weight(wt, [cout_pad], [cout_pad])
+                if need_grad:
+                    self.dw[s.name] = torch.zeros(s.cout, self.kpad[s.name], device=device)
+                    self.db[s.name] = torch.zeros(s.cout, device=device)
+
+
+class _State:
+    def __init__(self):
+        self.packed = None
+
+
+class _UpdateWeights(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, state, *params):
+        ub = state.ub
+        by_layer = module_params(ub)
+        state.packed = _Packed(by_layer, params[0].device, need_grad=state.need_grad)
+        ctx.state = state
+        ctx.n = len(params)
+        return params[0].new_zeros(())
+
+    @staticmethod
+    def backward(ctx, _tok):
+        pk = ctx.state.packed
+        grads = []
+        for s in SPECS:
+            dw, db = pk.dw[s.name], pk.db[s.name]
+            if s.scale != 1.0:
+                dw = dw * s.scale
+                db = db * s.scale
+            if s.small:
+                wg = C.unpack_weight_grad_small(dw, s.cout, s.in_real[0], s.k)
+            else:
+                wg = C.unpack_weight_grad(dw, s.cout, s.in_real, s.in_pad, s.k)
+            n_parts = 2 if s.name in ('zr1', 'zr2', 'head') else 1
+            if n_parts == 1:
+                grads += [wg, db]
+            else:
+                h = s.cout // 2
+                grads += [wg[:h], db[:h], wg[h:], db[h:]]
+        ctx.state.packed = None
+        return (None, *grads)
+
+
+def _bf16(shape, dev):
+    return torch.empty(*shape, device=dev, dtype=torch.bfloat16)
+
+
+def _f32(shape, dev, zero=False):
+    return (torch.zeros if zero else torch.empty)(*shape, device=dev, dtype=torch.float32)
+
+
+class _UpdateIter(torch.autograd.Function):
+    """One GRU iteration.  Inputs: token, h (B,H,W,128) bf16, inp (B,H,W,128) bf16,
+    corr (B,H,W,352) bf16, flow (B,2,H,W) fp32.  Outputs: h', delta (B,2,H,W) fp32,
+    mask (B,H,W,576) bf16 (already x0.25)."""
+
+    @staticmethod
+    def forward(ctx, token, h, inp, corr, flow, state):
+        pk = state.packed
+        B, H, W, _ = h.shape
+        dev = h.device
+        sh = (B, H, W)
+        flowb = torch.zeros(*sh, 8, device=dev, dtype=torch.bfloat16)
+        mf = _bf16(sh + (128,), dev)
+        ops = _ext.ops()
+        ops.flow_prep_(flow, flowb, mf, 126)
+        c1 = _bf16(sh + (256,), dev)
+        cf = _bf16(sh + (256,), dev)
+        f1 = _bf16(sh + (128,), dev)
+
+        def conv(name, segs, epi, outs, offs, aux=(), aux_offs=(), split=0):
+            s = SPEC[name]
+            C.conv_fwd(segs, pk.w[name], pk.b[name], s.k, s.pad, s.cout, epi, outs, offs, aux,
+                       aux_offs, scale=s.scale, split=split, cin_small=2 if s.small else 0)
+
+        conv('c1', [(corr, 0, 352)], C.EPI_RELU_BF16, [c1], [0])
+        conv('c2', [(c1, 0, 256)], C.EPI_RELU_BF16, [cf], [0])
+        conv('f1', [(flowb, 0, 8)], C.EPI_RELU_BF16, [f1], [0])
+        conv('f2', [(f1, 0, 128)], C.EPI_RELU_BF16, [cf], [192])
+        conv('conv', [(cf, 0, 256)], C.EPI_RELU_BF16, [mf], [0])
+        gates = {}
+        hin = h
+        for tag in ('1', '2'):
+            z, rh, r = _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev)
+            conv('zr' + tag, [(hin, 0, HD), (inp, 0, HD), (mf, 0, 128)], C.EPI_GRU_ZR, [z, rh, r],
+                 [0, 0, 0], aux=[hin], aux_offs=[0], split=HD)
+            hn, q = _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev)
+            conv('q' + tag, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)], C.EPI_GRU_Q, [hn, q], [0, 0],
+                 aux=[hin, z], aux_offs=[0, 0])
+            gates[tag] = (hin, z, rh, r, q)
+            hin = hn
+        h2 = hin
+        fm = _bf16(sh + (512,), dev)
+        conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0])
+        delta = torch.empty(B, 2, H, W, device=dev, dtype=torch.float32)
+        conv('fh2', [(fm, 0, 256)], C.EPI_F32_NCHW, [delta], [0])
+        mask = _bf16(sh + (576,), dev)
+        conv('m2', [(fm, 256, 256)], C.EPI_BF16, [mask], [0])
+
+        ctx.state = state
+        g1, g2 = gates['1'], gates['2']
+        ctx.save_for_backward(corr, flowb, c1, cf, f1, mf, inp, *g1, *g2, h2, fm)
+        return h2, delta, mask
+
+    @staticmethod
+    def backward(ctx, gh, gdelta, gmask):
+        pk = ctx.state.packed
+        (corr, flowb, c1, cf, f1, mf, inp, h0, z1, rh1, r1, q1, h1, z2, rh2, r2, q2, h2, fm) = \
+            ctx.saved_tensors
+        B, H, W, _ = h2.shape
+        P = B * H * W
+        dev = h2.device
+        sh = (B, H, W)
+        ops = _ext.ops()
+
+        def wgrad(name, g, g_off, segs):
+            s = SPEC[name]
+            C.conv_wgrad(g, g_off, segs, s.k, s.pad, s.cout, pk.dw[name], pk.db[name],
+                         cin_small=2 if s.small else 0)
+
+        def dgrad(name, gsegs, outs, small=False, scale=1.0):
+            """outs: list of (buffer fp32, offset, slot_cnt, real, acc)."""
+            s = SPEC[name]
+            ops.conv_dgrad_([g[0] for g in gsegs], [g[1] for g in gsegs], [g[2] for g in gsegs],
+                            pk.wd[name], s.k[0], s.k[1], s.pad[0], s.pad[1], 2 if small else 0,
+                            float(scale), [o[0] for o in outs], [o[1] for o in outs],
+                            [o[2] for o in outs], [o[3] for o in outs], [o[4] for o in outs])
+
+        # ---- mask head (mask = 0.25 * conv(fm[256:]))
+        gmask = gmask.contiguous()
+        if gmask.dtype != torch.bfloat16:
+            gmask = gmask.to(torch.bfloat16)
+        dfm = _f32(sh + (512,), dev)
+        wgrad('m2', gmask, 0, [(fm, 256, 256)])
+        dgrad('m2', [(gmask, 0, 576)], [(dfm, 256, 256, 256, 0)], scale=0.25)
+        # ---- flow head conv2 -> delta
+        gd = torch.zeros(*sh, 8, device=dev, dtype=torch.bfloat16)
+        ops.flow_prep_(gdelta.contiguous().float(), gd, None, 0)
+        wgrad('fh2', gd, 0, [(fm, 0, 256)])
+        dgrad('fh2', [(gd, 0, 8)], [(dfm, 0, 256, 256, 0)], small=True)
+        # ---- head (relu)
+        dpre_head = _bf16(sh + (512,), dev)
+        ops.relu_bwd_(dfm, 0, fm, 0, dpre_head, 0, 512, 1.0)
+        wgrad('head', dpre_head, 0, [(h2, 0, HD)])
+        dh = gh.float().contiguous() if gh is not None else _f32(sh + (HD,), dev, zero=True)
+        dgrad('head', [(dpre_head, 0, 512)], [(dh, 0, HD, HD, 1)])
+
+        dinp = _f32(sh + (HD,), dev, zero=True)
+        dmf = _f32(sh + (128,), dev, zero=True)
+        for tag, (hin, z, rh, r, q) in (('2', (h1, z2, rh2, r2, q2)), ('1', (h0, z1, rh1, r1, q1))):
+            dpre_q = _bf16(sh + (HD,), dev)
+            dz = _f32(sh + (HD,), dev)
+            dhp = _f32(sh + (HD,), dev)
+            ops.gru_q_bwd_(dh, z, q, hin, dpre_q, dz, dhp)
+            wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)])
+            drh = _f32(sh + (HD,), dev)
+            dgrad('q' + tag, [(dpre_q, 0, HD)],
+                  [(drh, 0, HD, HD, 0), (dinp, 0, HD, HD, 1), (dmf, 0, 128, 128, 1)])
+            dpre_zr = _bf16(sh + (2 * HD,), dev)
+            ops.gru_zr_bwd_(drh, dz, z, r, hin, dpre_zr, dhp)
+            wgrad('zr' + tag, dpre_zr, 0, [(hin, 0, HD), (inp, 0, HD), (mf, 0, 128)])
+            dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)],
+                  [(dhp, 0, HD, HD, 1), (dinp, 0, HD, HD, 1), (dmf, 0, 128, 128, 1)])
+            dh = dhp
+        # ---- motion encoder
+        dpre_conv = _bf16(sh + (128,), dev)
+        ops.relu_bwd_(dmf, 0, mf, 0, dpre_conv, 0, 128, 1.0)
+        wgrad('conv', dpre_conv, 0, [(cf, 0, 256)])
+        dcf = _f32(sh + (256,), dev)
+        dgrad('conv', [(dpre_conv, 0, 128)], [(dcf, 0, 256, 256, 0)])
+        dpre_cf = _bf16(sh + (256,), dev)
+        ops.relu_bwd_(dcf, 0, cf, 0, dpre_cf, 0, 256, 1.0)
+        wgrad('c2', dpre_cf, 0, [(c1, 0, 256)])
+        wgrad('f2', dpre_cf, 192, [(f1, 0, 128)])
+        dc1 = _f32(sh + (256,), dev)
+        dgrad('c2', [(dpre_cf, 0, 192)], [(dc1, 0, 256, 256, 0)])
+        df1 = _f32(sh + (128,), dev)
+        dgrad('f2', [(dpre_cf, 192, 64)], [(df1, 0, 128, 128, 0)])
+        dpre_f1 = _bf16(sh + (128,), dev)
+        ops.relu_bwd_(df1, 0, f1, 0, dpre_f1, 0, 128, 1.0)
+        wgrad('f1', dpre_f1, 0, [(flowb, 0, 8)])
+        dpre_c1 = _bf16(sh + (256,), dev)
+        ops.relu_bwd_(dc1, 0, c1, 0, dpre_c1, 0, 256, 1.0)
+        wgrad('c1', dpre_c1, 0, [(corr, 0, 352)])
+        dcorr = _f32(sh + (352,), dev)
+        dgrad('c1', [(dpre_c1, 0, 256)], [(dcorr, 0, 352, 324, 0)])  # slots 324.. unused
+        return (torch.zeros((), device=dev), dh, dinp, dcorr, None, None)
+
+
+class HipUpdateBlock:
+    """Drives the fused iterations for one forward pass of a BasicUpdateBlock."""
+
+    def __init__(self, update_block):
+        self.state = _State()
+        self.state.ub = update_block
+        params = flat_params(update_block)
+        self.state.need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        self.token = _UpdateWeights.apply(self.state, *params)
+
+    def __call__(self, h, inp, corr, flow):
+        return _UpdateIter.apply(self.token, h, inp, corr, flow, self.state)
+
+
+def available(required=False):
+    return _ext.gpu_path_enabled(required=required)

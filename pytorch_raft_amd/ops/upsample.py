@@ -18,25 +18,28 @@ def torch_convex_upsample(flow, mask):
 
 class _ConvexUpsample(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, flow, mask):
+    def forward(ctx, flow, mask, nhwc):
         flow = flow.contiguous().float()
         mask = mask.contiguous()
         if mask.dtype not in (torch.float32, torch.bfloat16):
             mask = mask.float()
         ctx.save_for_backward(flow, mask)
-        ctx.mask_dtype = mask.dtype
-        return _ext.ops().convex_up_fwd(flow, mask)
+        ctx.nhwc = nhwc
+        return _ext.ops().convex_up_fwd(flow, mask, nhwc)
 
     @staticmethod
     def backward(ctx, dout):
         flow, mask = ctx.saved_tensors
-        dflow, dmask = _ext.ops().convex_up_bwd(flow, mask, dout.contiguous().float())
-        return dflow, dmask
+        dflow, dmask = _ext.ops().convex_up_bwd(flow, mask, dout.contiguous().float(), ctx.nhwc)
+        return dflow, dmask, None
 
 
-def convex_upsample(flow, mask, impl='auto'):
+def convex_upsample(flow, mask, impl='auto', nhwc=False):
+    """``mask`` is (B,576,H,W), or (B,H,W,576) with ``nhwc=True`` (the fused update block's layout)."""
     if impl != 'torch' and flow.is_cuda and _ext.gpu_path_enabled(required=(impl == 'hip')):
         out_dtype = torch.promote_types(flow.dtype, mask.dtype)
-        out = _ConvexUpsample.apply(flow, mask)
+        out = _ConvexUpsample.apply(flow, mask, nhwc)
         return out if out_dtype == torch.float32 else out.to(out_dtype)
+    if nhwc:
+        mask = mask.permute(0, 3, 1, 2)
     return torch_convex_upsample(flow, mask)
