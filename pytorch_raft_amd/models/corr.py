@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from ..utils.utils import bilinear_sampler
 from ..ops import corr as corr_ops
+from ..ops import _ext
 
 
 def _window_delta(r, device, dtype=torch.float32):
@@ -108,7 +109,7 @@ def torch_onthefly_corr(fmap_pyramid2, fmap1, coords, radius):
 def _use_hip(t, impl):
     if impl == 'torch':
         return False
-    if not t.is_cuda:
+    if not _ext.device_ok(t):
         return False
     return corr_ops.available(required=(impl == 'hip'))
 

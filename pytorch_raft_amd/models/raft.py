@@ -26,6 +26,7 @@ from .extractor import BasicEncoder, SmallEncoder
 from .corr import CorrBlock, AlternateCorrBlock
 from ..utils.utils import coords_grid, upflow8
 from ..ops.upsample import convex_upsample
+from ..ops import _ext
 
 
 def _get(args, name, default):
@@ -148,7 +149,7 @@ class RAFT(nn.Module):
     def _use_fused_update(self, img):
         """Fused MFMA update block: GPU, full model, bf16 mixed precision (its compute dtype)."""
         impl = _get(self.args, 'update_impl', 'auto')
-        if impl == 'torch' or self.corr_impl == 'torch' or self.args.small or not img.is_cuda:
+        if impl == 'torch' or self.corr_impl == 'torch' or self.args.small or not _ext.device_ok(img):
             return False
         if not (self.args.mixed_precision and self.amp_dtype == torch.bfloat16):
             if impl == 'hip':

@@ -62,6 +62,8 @@ def gpu_path_enabled(required=False):
     ``required`` forces an error when the extension is missing.  Without it a missing extension on
     a GPU machine still raises unless RAFT_AMD_ALLOW_FALLBACK=1.
     """
+    if _DRY['on']:
+        return True
     if _try_load():
         return True
     if required or not fallback_allowed():
@@ -71,4 +73,76 @@ def gpu_path_enabled(required=False):
 
 
 def ops():
+    if _DRY['on']:
+        return _DRY['ops']
     return require()
+
+
+def device_ok(t):
+    """True if ``t`` should take the HIP path (a GPU tensor, or any tensor during a dry run)."""
+    return bool(t.is_cuda) or _DRY['on']
+
+
+# ---------------------------------------------------------------------------------------------
+# Dry run: execute the full HIP-path orchestration on CPU with every native op replaced by a
+# schema-checking stub (arguments are validated against the registered TORCH_LIBRARY schema; ops
+# that return tensors return zeros of the right shape).  Used by the CPU test-suite to catch
+# Python-side bugs of GPU-only code paths without a GPU.
+_DRY = {'on': False, 'ops': None}
+
+
+class _DryOps:
+    def __init__(self, returns):
+        torch.ops.load_library(LIB_PATH)
+        self._returns = returns
+        self.calls = []
+
+    def __getattr__(self, name):
+        op = getattr(torch.ops.raft_amd, name)
+        schema = op.default._schema
+
+        def call(*args):
+            params = list(schema.arguments)
+            required = [p for p in params if not p.has_default_value()]
+            if not (len(required) <= len(args) <= len(params)):
+                raise TypeError('%s: %d args for schema %s' % (name, len(args), schema))
+            for p, v in zip(params, args):
+                t = str(p.type)
+                ok = True
+                if t == 'Tensor':
+                    ok = isinstance(v, torch.Tensor)
+                elif t == 'Optional[Tensor]' or t == 'Tensor?':
+                    ok = v is None or isinstance(v, torch.Tensor)
+                elif t in ('List[Tensor]', 'Tensor[]'):
+                    ok = isinstance(v, (list, tuple)) and all(isinstance(x, torch.Tensor) for x in v)
+                elif t == 'int':
+                    ok = isinstance(v, int) and not isinstance(v, bool)
+                elif t == 'float':
+                    ok = isinstance(v, (int, float)) and not isinstance(v, bool)
+                elif t in ('List[int]', 'int[]'):
+                    ok = isinstance(v, (list, tuple)) and all(isinstance(x, int) for x in v)
+                elif t == 'bool':
+                    ok = isinstance(v, bool)
+                if not ok:
+                    raise TypeError('%s: argument %s expects %s, got %r' % (name, p.name, t, type(v)))
+            self.calls.append(name)
+            fn = self._returns.get(name)
+            return fn(*args) if fn is not None else None
+        return call
+
+
+class dry_run:
+    """Context manager enabling the dry run (see above)."""
+
+    def __init__(self, returns):
+        self.returns = returns
+
+    def __enter__(self):
+        _DRY['ops'] = _DryOps(self.returns)
+        _DRY['on'] = True
+        return _DRY['ops']
+
+    def __exit__(self, *a):
+        _DRY['on'] = False
+        _DRY['ops'] = None
+        return False

@@ -14,7 +14,8 @@ import torch.nn.functional as F
 
 from . import _ext
 
-EPI_BF16, EPI_RELU_BF16, EPI_F32, EPI_ACC_F32, EPI_GRU_ZR, EPI_GRU_Q = range(6)
+(EPI_BF16, EPI_RELU_BF16, EPI_F32, EPI_ACC_F32, EPI_GRU_ZR, EPI_GRU_Q, EPI_DGRAD,
+ EPI_F32_NCHW) = range(8)
 
 
 def round_up(x, m):

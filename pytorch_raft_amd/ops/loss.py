@@ -50,7 +50,7 @@ class _SeqLoss(torch.autograd.Function):
 
 
 def sequence_loss(flow_preds, flow_gt, valid, gamma=0.8, max_flow=MAX_FLOW, impl='auto'):
-    use_hip = (impl != 'torch' and flow_gt.is_cuda and len(flow_preds) <= 32
+    use_hip = (impl != 'torch' and _ext.device_ok(flow_gt) and len(flow_preds) <= 32
                and _ext.gpu_path_enabled(required=(impl == 'hip')))
     if not use_hip:
         return torch_sequence_loss(flow_preds, flow_gt, valid, gamma, max_flow)

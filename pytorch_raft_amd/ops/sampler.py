@@ -50,7 +50,7 @@ class _Warp(torch.autograd.Function):
 
 
 def warp_image(x, flo, convention='reference', impl='auto'):
-    if impl != 'torch' and x.is_cuda and _ext.gpu_path_enabled(required=(impl == 'hip')):
+    if impl != 'torch' and _ext.device_ok(x) and _ext.gpu_path_enabled(required=(impl == 'hip')):
         h, w = x.shape[-2:]
         p = _affine(convention, h, w)
         return _Warp.apply(x.float().contiguous(), flo.float().contiguous(), *p)

@@ -36,7 +36,7 @@ class _ConvexUpsample(torch.autograd.Function):
 
 def convex_upsample(flow, mask, impl='auto', nhwc=False):
     """``mask`` is (B,576,H,W), or (B,H,W,576) with ``nhwc=True`` (the fused update block's layout)."""
-    if impl != 'torch' and flow.is_cuda and _ext.gpu_path_enabled(required=(impl == 'hip')):
+    if impl != 'torch' and _ext.device_ok(flow) and _ext.gpu_path_enabled(required=(impl == 'hip')):
         out_dtype = torch.promote_types(flow.dtype, mask.dtype)
         out = _ConvexUpsample.apply(flow, mask, nhwc)
         return out if out_dtype == torch.float32 else out.to(out_dtype)
