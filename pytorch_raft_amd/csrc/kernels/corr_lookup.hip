@@ -42,13 +42,18 @@ template <int R, typename TO>
 __global__ __launch_bounds__(64) void corr_lookup_fwd_kernel(PyrC pyr, const float* __restrict__ coords,
                                                             TO* __restrict__ out, OStride os, int B,
                                                             int H, int W, int levels) {
+  // one thread per (batch, level, tap row iy, query pixel): 9x the parallelism of a
+  // thread-per-pixel walk, so the scattered window reads are latency-hidden
   constexpr int D = 2 * R + 1;
   const int N = H * W;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)B * levels * N) return;
+  if (t >= (int64_t)B * levels * D * N) return;
   const int i = (int)(t % N);
-  const int l = (int)((t / N) % levels);
-  const int b = (int)(t / ((int64_t)N * levels));
+  int64_t rest = t / N;
+  const int iy = (int)(rest % D);
+  rest /= D;
+  const int l = (int)(rest % levels);
+  const int b = (int)(rest / levels);
   const int hl = pyr.h[l], wl = pyr.w[l];
   const float inv = 1.0f / (float)(1 << l);
   const float cx = clamp_coord(coords[((int64_t)b * 2 + 0) * N + i] * inv);
@@ -59,10 +64,10 @@ __global__ __launch_bounds__(64) void corr_lookup_fwd_kernel(PyrC pyr, const flo
   const float* P = pyr.lvl[l] + ((int64_t)b * N + i) * hl * wl;
   TO* O = out + b * os.b + i * os.p + (int64_t)l * D * D * os.c;
 
-  float hprev[D], hcur[D];
+  float hr[2][D];
 #pragma unroll
-  for (int yy = 0; yy <= D; ++yy) {
-    const int gy = ys + yy;
+  for (int k = 0; k < 2; ++k) {
+    const int gy = ys + iy + k;
     const bool rowok = (gy >= 0) && (gy < hl);
     float v[D + 1];
 #pragma unroll
@@ -71,29 +76,30 @@ __global__ __launch_bounds__(64) void corr_lookup_fwd_kernel(PyrC pyr, const flo
       v[xx] = (rowok && gx >= 0 && gx < wl) ? P[(int64_t)gy * wl + gx] : 0.f;
     }
 #pragma unroll
-    for (int ix = 0; ix < D; ++ix) hcur[ix] = (1.f - ax) * v[ix] + ax * v[ix + 1];
-    if (yy > 0) {
-      const int iy = yy - 1;
-#pragma unroll
-      for (int ix = 0; ix < D; ++ix)
-        St<TO>::put(O, (int64_t)(ix * D + iy) * os.c, (1.f - ay) * hprev[ix] + ay * hcur[ix]);
-    }
-#pragma unroll
-    for (int ix = 0; ix < D; ++ix) hprev[ix] = hcur[ix];
+    for (int ix = 0; ix < D; ++ix) hr[k][ix] = (1.f - ax) * v[ix] + ax * v[ix + 1];
   }
+#pragma unroll
+  for (int ix = 0; ix < D; ++ix)
+    St<TO>::put(O, (int64_t)(ix * D + iy) * os.c, (1.f - ay) * hr[0][ix] + ay * hr[1][ix]);
 }
 
 template <int R>
 __global__ __launch_bounds__(64) void corr_lookup_bwd_kernel(PyrG g, const float* __restrict__ coords,
                                                             const float* __restrict__ dout, OStride os,
                                                             int B, int H, int W, int levels) {
+  // one thread per (batch, level, integer window row yy, query pixel); each thread owns one row
+  // of the pixel's private plane, so the read-modify-writes never race
   constexpr int D = 2 * R + 1;
+  constexpr int E = D + 1;
   const int N = H * W;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)B * levels * N) return;
+  if (t >= (int64_t)B * levels * E * N) return;
   const int i = (int)(t % N);
-  const int l = (int)((t / N) % levels);
-  const int b = (int)(t / ((int64_t)N * levels));
+  int64_t rest = t / N;
+  const int yy = (int)(rest % E);
+  rest /= E;
+  const int l = (int)(rest % levels);
+  const int b = (int)(rest / levels);
   const int hl = g.h[l], wl = g.w[l];
   const float inv = 1.0f / (float)(1 << l);
   const float cx = clamp_coord(coords[((int64_t)b * 2 + 0) * N + i] * inv);
@@ -101,41 +107,36 @@ __global__ __launch_bounds__(64) void corr_lookup_bwd_kernel(PyrG g, const float
   const float fx = floorf(cx), fy = floorf(cy);
   const float ax = cx - fx, ay = cy - fy;
   const int xs = (int)fx - R, ys = (int)fy - R;
-  float* G = g.lvl[l] + ((int64_t)b * N + i) * hl * wl;
+  const int gy = ys + yy;
+  if (gy < 0 || gy >= hl) return;
+  float* G = g.lvl[l] + ((int64_t)b * N + i) * hl * wl + (int64_t)gy * wl;
   const float* dO = dout + b * os.b + i * os.p + (int64_t)l * D * D * os.c;
 
-  // hs_iy[xx] = (1-ax) d[xx][iy] + ax d[xx-1][iy]  (horizontal adjoint of tap row iy)
-  float hprev[D + 1];
+  // row yy collects tap row yy (weight 1-ay) and tap row yy-1 (weight ay); horizontally the
+  // adjoint of x-interpolation: hs[xx] = (1-ax) d[xx] + ax d[xx-1]
+  float acc[E];
 #pragma unroll
-  for (int xx = 0; xx <= D; ++xx) hprev[xx] = 0.f;
+  for (int xx = 0; xx < E; ++xx) acc[xx] = 0.f;
 #pragma unroll
-  for (int yy = 0; yy <= D; ++yy) {
-    float hcur[D + 1];
-    if (yy < D) {
-      float d[D];
+  for (int k = 0; k < 2; ++k) {
+    const int iy = yy - k;
+    if (iy < 0 || iy >= D) continue;
+    const float wy = k == 0 ? (1.f - ay) : ay;
+    float d[D];
 #pragma unroll
-      for (int ix = 0; ix < D; ++ix) d[ix] = dO[(int64_t)(ix * D + yy) * os.c];
+    for (int ix = 0; ix < D; ++ix) d[ix] = dO[(int64_t)(ix * D + iy) * os.c];
 #pragma unroll
-      for (int xx = 0; xx <= D; ++xx) {
-        float s = 0.f;
-        if (xx < D) s += (1.f - ax) * d[xx];
-        if (xx > 0) s += ax * d[xx - 1];
-        hcur[xx] = s;
-      }
-    } else {
-#pragma unroll
-      for (int xx = 0; xx <= D; ++xx) hcur[xx] = 0.f;
+    for (int xx = 0; xx < E; ++xx) {
+      float s = 0.f;
+      if (xx < D) s += (1.f - ax) * d[xx];
+      if (xx > 0) s += ax * d[xx - 1];
+      acc[xx] += wy * s;
     }
-    const int gy = ys + yy;
-    if (gy >= 0 && gy < hl) {
+  }
 #pragma unroll
-      for (int xx = 0; xx <= D; ++xx) {
-        const int gx = xs + xx;
-        if (gx >= 0 && gx < wl) G[(int64_t)gy * wl + gx] += (1.f - ay) * hcur[xx] + ay * hprev[xx];
-      }
-    }
-#pragma unroll
-    for (int xx = 0; xx <= D; ++xx) hprev[xx] = hcur[xx];
+  for (int xx = 0; xx < E; ++xx) {
+    const int gx = xs + xx;
+    if (gx >= 0 && gx < wl) G[gx] += acc[xx];
   }
 }
 
@@ -163,7 +164,7 @@ bool launch_corr_lookup_fwd(const float* const* lvl, const int* hs, const int* w
     p.w[l] = l < levels ? ws[l] : 0;
   }
   OStride os{bs, ps, cs};
-  const int64_t total = (int64_t)B * levels * H * W;
+  const int64_t total = (int64_t)B * levels * (2 * radius + 1) * H * W;
   dim3 grid(raft_cdiv(total, 64));
 #define LK(R, T) hipLaunchKernelGGL((corr_lookup_fwd_kernel<R, T>), grid, dim3(64), 0, stream, p, coords, (T*)out, os, B, H, W, levels)
   if (radius == 3) { if (out_bf16) LK(3, uint16_t); else LK(3, float); return true; }
@@ -177,7 +178,7 @@ bool launch_corr_lookup_bwd(float* const* glvl, const int* hs, const int* ws, in
                             int64_t cs, int B, int H, int W, int radius, hipStream_t stream) {
   PyrG p = make_pyr<PyrG>(glvl, hs, ws, levels);
   OStride os{bs, ps, cs};
-  const int64_t total = (int64_t)B * levels * H * W;
+  const int64_t total = (int64_t)B * levels * (2 * radius + 2) * H * W;
   dim3 grid(raft_cdiv(total, 64));
   switch (radius) {
     case 3: hipLaunchKernelGGL(corr_lookup_bwd_kernel<3>, grid, dim3(64), 0, stream, p, coords, dout, os, B, H, W, levels); return true;
