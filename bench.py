@@ -123,10 +123,14 @@ def main(argv=None):
     else:
         stepper = st
 
+    host_issue = []
+
     def run(n):
         for k in range(n):
             i1, i2, fl, va = batches[k % len(batches)]
+            t_issue = time.perf_counter()
             stepper.step(i1, i2, fl, va)
+            host_issue.append(time.perf_counter() - t_issue)
 
     if use_graph:
         run(1)  # first replay
@@ -192,6 +196,8 @@ def main(argv=None):
         },
         'peak_hbm_gib_rank0': round(peak, 2),
         'loss_finite': ok,
+        # host time to issue one step (asynchronous launches); ~= ms_per_step means host-bound
+        'host_issue_ms': round(1000.0 * sum(host_issue[-a.steps:]) / max(1, a.steps), 3),
     }
     if rank == 0:
         line = json.dumps(res)

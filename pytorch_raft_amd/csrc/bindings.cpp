@@ -112,11 +112,65 @@ void corr_lookup_nhwc_(const std::vector<Tensor>& pyr, const Tensor& coords, int
                   out.size(3) >= levels * D * D,
               "out must be a contiguous bf16 (B,H,W,C>=L*D*D) buffer");
   const int64_t Cb = out.size(3);
+  TORCH_CHECK(Cb % 8 == 0, "out channels must be a multiple of 8");
   std::vector<const float*> cp(L.ptr.begin(), L.ptr.end());
-  TORCH_CHECK(launch_corr_lookup_fwd(cp.data(), L.h.data(), L.w.data(), levels,
-                                     coords.data_ptr<float>(), out.data_ptr(), 1, H * W * Cb, Cb, 1,
-                                     (int)B, (int)H, (int)W, (int)radius, cur_stream()),
+  // LDS-tiled kernel writes whole pixel rows including the zero padding
+  TORCH_CHECK(launch_corr_lookup_tile(cp.data(), L.h.data(), L.w.data(), levels,
+                                      coords.data_ptr<float>(),
+                                      reinterpret_cast<uint16_t*>(out.data_ptr<at::BFloat16>()),
+                                      (int)Cb, (int)B, (int)H, (int)W, (int)radius, cur_stream()),
               "unsupported radius");
+}
+
+// per-iteration compact window gradient: (B, N, L, 2r+2, 2r+2) fp32 from a bf16 NHWC tap gradient
+Tensor corr_window_grad(const Tensor& coords, const Tensor& dout, int64_t levels, int64_t radius) {
+  check_cuda_f32(coords, "coords");
+  TORCH_CHECK(coords.dim() == 4 && coords.size(1) == 2, "coords must be (B,2,H,W)");
+  TORCH_CHECK(radius == 3 || radius == 4, "radius must be 3 or 4");
+  TORCH_CHECK(levels >= 1 && levels <= 4, "levels must be 1..4");
+  const int64_t B = coords.size(0), H = coords.size(2), W = coords.size(3);
+  const int64_t D = 2 * radius + 1, E = D + 1;
+  TORCH_CHECK(dout.is_cuda() && dout.is_contiguous() && dout.scalar_type() == at::kBFloat16 &&
+                  dout.dim() == 4 && dout.size(0) == B && dout.size(1) == H && dout.size(2) == W &&
+                  dout.size(3) % 8 == 0 && dout.size(3) >= (levels * D * D + 7) / 8 * 8,
+              "grad must be a contiguous bf16 (B,H,W,Cbuf) tensor");
+  c10::DeviceGuard g(coords.device());
+  Tensor wg = at::empty({B, H * W, levels, E, E}, coords.options());
+  TORCH_CHECK(launch_corr_window_grad(coords.data_ptr<float>(),
+                                      reinterpret_cast<const uint16_t*>(dout.data_ptr<at::BFloat16>()),
+                                      (int)dout.size(3), wg.data_ptr<float>(), (int)B, (int)H, (int)W,
+                                      (int)levels, (int)radius, cur_stream()),
+              "unsupported radius");
+  return wg;
+}
+
+// sum of all iterations' window gradients -> dcorr (B, N, N) = level-0 gradient * 1/sqrt(C)
+Tensor corr_window_reduce(const std::vector<Tensor>& coords, const std::vector<Tensor>& wgs,
+                          int64_t H, int64_t W, int64_t levels, int64_t radius, double inv_sqrt_c) {
+  TORCH_CHECK(!coords.empty() && coords.size() == wgs.size() && coords.size() <= RAFT_MAX_WIN,
+              "1..", RAFT_MAX_WIN, " iterations");
+  const int64_t B = coords[0].size(0), N = H * W;
+  const int64_t E = 2 * radius + 2;
+  WinList wl{};
+  for (size_t k = 0; k < coords.size(); ++k) {
+    check_cuda_f32(coords[k], "coords");
+    check_cuda_f32(wgs[k], "window grad");
+    TORCH_CHECK(coords[k].dim() == 4 && coords[k].size(0) == B && coords[k].size(1) == 2 &&
+                    coords[k].size(2) == H && coords[k].size(3) == W,
+                "coords shape");
+    TORCH_CHECK(wgs[k].numel() == B * N * levels * E * E, "window grad shape");
+    wl.coords[k] = coords[k].data_ptr<float>();
+    wl.wg[k] = wgs[k].data_ptr<float>();
+  }
+  wl.n = (int)coords.size();
+  const int lds = corr_window_reduce_lds_bytes((int)H, (int)W, (int)levels);
+  TORCH_CHECK(lds <= 64 * 1024, "feature map too large for the LDS plane reduction");
+  c10::DeviceGuard g(coords[0].device());
+  Tensor out = at::empty({B, N, N}, coords[0].options());
+  TORCH_CHECK(launch_corr_window_reduce(wl, (int)levels, (int)B, (int)H, (int)W, (int)radius,
+                                        (float)inv_sqrt_c, out.data_ptr<float>(), cur_stream()),
+              "unsupported radius");
+  return out;
 }
 
 void corr_lookup_bwd_(const std::vector<Tensor>& gpyr, const Tensor& coords, const Tensor& dout,
@@ -249,6 +303,12 @@ Tensor convex_up_fwd(const Tensor& flow, const Tensor& mask, bool nhwc) {
   c10::DeviceGuard g(flow.device());
   Tensor out = at::empty({B, 2, 8 * H, 8 * W}, flow.options());
   const int64_t HW = H * W;
+  if (nhwc && mask_kind(mask) == 1) {
+    launch_convex_up_nhwc_fwd(flow.data_ptr<float>(),
+                              reinterpret_cast<const uint16_t*>(mask.data_ptr<at::BFloat16>()),
+                              out.data_ptr<float>(), (int)B, (int)H, (int)W, cur_stream());
+    return out;
+  }
   launch_convex_up_fwd(flow.data_ptr<float>(), mask.data_ptr(), mask_kind(mask), 576 * HW,
                        nhwc ? 1 : HW, nhwc ? 576 : 1, out.data_ptr<float>(), (int)B, (int)H,
                        (int)W, cur_stream());
@@ -269,6 +329,15 @@ std::vector<Tensor> convex_up_bwd(const Tensor& flow, const Tensor& mask, const 
   Tensor dflow = at::empty_like(flow);
   Tensor wbuf = at::empty({B, 18, H, W}, flow.options());
   const int64_t HW = H * W;
+  if (nhwc && mask_kind(mask) == 1) {
+    launch_convex_up_nhwc_bwd(flow.data_ptr<float>(),
+                              reinterpret_cast<const uint16_t*>(mask.data_ptr<at::BFloat16>()),
+                              dout.data_ptr<float>(),
+                              reinterpret_cast<uint16_t*>(dmask.data_ptr<at::BFloat16>()),
+                              wbuf.data_ptr<float>(), dflow.data_ptr<float>(), (int)B, (int)H,
+                              (int)W, cur_stream());
+    return {dflow, dmask};
+  }
   launch_convex_up_bwd(flow.data_ptr<float>(), mask.data_ptr(), mask_kind(mask), 576 * HW,
                        nhwc ? 1 : HW, nhwc ? 576 : 1, dout.data_ptr<float>(), dmask.data_ptr(),
                        wbuf.data_ptr<float>(), dflow.data_ptr<float>(), (int)B, (int)H, (int)W,
@@ -656,6 +725,8 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");
   m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout, bool nhwc=False) -> Tensor[]");
   m.def("corr_lookup_nhwc_(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
+  m.def("corr_window_grad(Tensor coords, Tensor dout, int levels, int radius) -> Tensor");
+  m.def("corr_window_reduce(Tensor[] coords, Tensor[] wgs, int H, int W, int levels, int radius, float inv_sqrt_c) -> Tensor");
   m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc) -> ()");
   m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale) -> ()");
   m.def("gru_q_bwd_(Tensor dh, Tensor z, Tensor q, Tensor hprev, Tensor(a!) dpre_q, Tensor(b!) dz, Tensor(c!) dhprev) -> ()");
@@ -685,6 +756,8 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("conv_fwd_", &conv_fwd_);
   m.impl("conv_wgrad_", &conv_wgrad_);
   m.impl("corr_lookup_nhwc_", &corr_lookup_nhwc_);
+  m.impl("corr_window_grad", &corr_window_grad);
+  m.impl("corr_window_reduce", &corr_window_reduce);
   m.impl("conv_dgrad_", &conv_dgrad_);
   m.impl("relu_bwd_", &relu_bwd_);
   m.impl("gru_q_bwd_", &gru_q_bwd_);

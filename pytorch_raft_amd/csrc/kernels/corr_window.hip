@@ -1,0 +1,249 @@
+// NHWC correlation lookup for the fused update block + window-compact backward.
+//
+// Forward (corr_lookup_tile_kernel): a workgroup owns 64 consecutive query pixels; 256 threads
+// compute the (levels x (2r+1)) tap rows of all 64 pixels into an LDS tile, then the tile is
+// written out as whole 704-B pixel rows of the bf16 (B,H,W,Cbuf) buffer the first 1x1 conv reads,
+// zero padding included (no separate memset, no scattered 2-byte stores).
+//
+// Backward, two phases instead of a dense read-modify-write of the whole pyramid gradient:
+//  1. per iteration (corr_window_grad_kernel): the adjoint of one pixel's bilinear window is a
+//     (2r+2)^2 integer-position patch per level; it is written COMPACTLY, [b][i][level][row][col]
+//     fp32 -- fully coalesced, ~55 MB per iteration at chairs/B=12 instead of RMW traffic spread
+//     over a 500 MB buffer.
+//  2. once per step (corr_window_reduce_kernel): a workgroup per query pixel accumulates every
+//     iteration's patches into per-level planes held in LDS (iterations in a fixed order ->
+//     deterministic), applies the avg-pool adjoint (level l cell -> its 2^l x 2^l level-0 block,
+//     weight 4^-l) and 1/sqrt(C), and streams the level-0 gradient row of dcorr (B, N, N) out once.
+//     That matrix feeds the two backward GEMMs (dF1 = F2 dC^T, dF2 = F1 dC).
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+struct PyrC4 {
+  const float* lvl[4];
+  int h[4];
+  int w[4];
+};
+
+__device__ __forceinline__ float clampc(float v) { return fminf(fmaxf(v, -1.0e7f), 1.0e7f); }
+
+constexpr int TP = 64;  // pixels per workgroup
+
+template <int R>
+__global__ __launch_bounds__(256) void corr_lookup_tile_kernel(PyrC4 pyr, const float* __restrict__ coords,
+                                                               uint16_t* __restrict__ out, int cbuf,
+                                                               int B, int H, int W, int levels) {
+  constexpr int D = 2 * R + 1;
+  constexpr int ROW = (4 * D * D + 7) / 8 * 8;  // bf16 per LDS pixel row (16-B multiple)
+  __shared__ __attribute__((aligned(16))) uint16_t tile[TP * ROW];
+  const int N = H * W;
+  const int tiles = (N + TP - 1) / TP;
+  const int b = blockIdx.x / tiles;
+  const int i0 = (blockIdx.x % tiles) * TP;
+  const int items = TP * levels * D;
+  for (int it = threadIdx.x; it < items; it += 256) {
+    const int px = it % TP;
+    const int rest = it / TP;
+    const int iy = rest % D, l = rest / D;
+    const int i = i0 + px;
+    if (i >= N) continue;
+    const int hl = pyr.h[l], wl = pyr.w[l];
+    const float inv = 1.0f / (float)(1 << l);
+    const float cx = clampc(coords[((int64_t)b * 2) * N + i] * inv);
+    const float cy = clampc(coords[((int64_t)b * 2 + 1) * N + i] * inv);
+    const float fx = floorf(cx), fy = floorf(cy);
+    const float ax = cx - fx, ay = cy - fy;
+    const int xs = (int)fx - R, ys = (int)fy - R;
+    const float* P = pyr.lvl[l] + ((int64_t)b * N + i) * hl * wl;
+    float hr[2][D];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int gy = ys + iy + k;
+      const bool rowok = gy >= 0 && gy < hl;
+      float v[D + 1];
+#pragma unroll
+      for (int xx = 0; xx <= D; ++xx) {
+        const int gx = xs + xx;
+        v[xx] = (rowok && gx >= 0 && gx < wl) ? P[(int64_t)gy * wl + gx] : 0.f;
+      }
+#pragma unroll
+      for (int ix = 0; ix < D; ++ix) hr[k][ix] = (1.f - ax) * v[ix] + ax * v[ix + 1];
+    }
+    uint16_t* T = tile + px * ROW + l * D * D;
+#pragma unroll
+    for (int ix = 0; ix < D; ++ix)
+      T[ix * D + iy] = raft_f32_to_bf16((1.f - ay) * hr[0][ix] + ay * hr[1][ix]);
+  }
+  __syncthreads();
+  const int ctot = levels * D * D;
+  const int chunks = cbuf / 8;
+  for (int e = threadIdx.x; e < TP * chunks; e += 256) {
+    const int px = e / chunks, ch = e % chunks;
+    const int i = i0 + px;
+    if (i >= N) continue;
+    uint16_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = ch * 8 + q;
+      v[q] = c < ctot ? tile[px * ROW + c] : (uint16_t)0;
+    }
+    *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i) * cbuf + ch * 8) =
+        make_uint4(v[0] | ((uint32_t)v[1] << 16), v[2] | ((uint32_t)v[3] << 16),
+                   v[4] | ((uint32_t)v[5] << 16), v[6] | ((uint32_t)v[7] << 16));
+  }
+}
+
+// dout: (B,H,W,cbuf) bf16 (channels [0, L*D*D) used); wg: (B, N, L, E, E) fp32
+template <int R>
+__global__ __launch_bounds__(256) void corr_window_grad_kernel(const float* __restrict__ coords,
+                                                               const uint16_t* __restrict__ dout,
+                                                               int cbuf, float* __restrict__ wg,
+                                                               int B, int H, int W, int levels) {
+  constexpr int D = 2 * R + 1, E = D + 1;
+  constexpr int ROW = (4 * D * D + 7) / 8 * 8;
+  __shared__ __attribute__((aligned(16))) uint16_t tile[TP * ROW];
+  const int N = H * W;
+  const int tiles = (N + TP - 1) / TP;
+  const int b = blockIdx.x / tiles;
+  const int i0 = (blockIdx.x % tiles) * TP;
+  const int ctot = levels * D * D;
+  // stage the 64 pixels' incoming tap gradients (coalesced rows)
+  const int chunks = (ctot + 7) / 8;
+  for (int e = threadIdx.x; e < TP * chunks; e += 256) {
+    const int px = e / chunks, ch = e % chunks;
+    const int i = i0 + px;
+    if (i >= N) continue;
+    const uint4 v = *reinterpret_cast<const uint4*>(dout + ((int64_t)b * N + i) * cbuf + ch * 8);
+    *reinterpret_cast<uint4*>(tile + px * ROW + ch * 8) = v;
+  }
+  __syncthreads();
+  const int items = TP * levels * E;
+  for (int it = threadIdx.x; it < items; it += 256) {
+    const int yy = it % E;
+    const int rest = it / E;
+    const int l = rest % levels, px = rest / levels;
+    const int i = i0 + px;
+    if (i >= N) continue;
+    const float inv = 1.0f / (float)(1 << l);
+    const float cx = clampc(coords[((int64_t)b * 2) * N + i] * inv);
+    const float cy = clampc(coords[((int64_t)b * 2 + 1) * N + i] * inv);
+    const float ax = cx - floorf(cx), ay = cy - floorf(cy);
+    const uint16_t* T = tile + px * ROW + l * D * D;
+    float acc[E];
+#pragma unroll
+    for (int xx = 0; xx < E; ++xx) acc[xx] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int iy = yy - k;
+      if (iy < 0 || iy >= D) continue;
+      const float wy = k == 0 ? (1.f - ay) : ay;
+      float d[D];
+#pragma unroll
+      for (int ix = 0; ix < D; ++ix) d[ix] = raft_bf16_to_f32(T[ix * D + iy]);
+#pragma unroll
+      for (int xx = 0; xx < E; ++xx) {
+        float s = 0.f;
+        if (xx < D) s += (1.f - ax) * d[xx];
+        if (xx > 0) s += ax * d[xx - 1];
+        acc[xx] += wy * s;
+      }
+    }
+    float* dst = wg + ((((int64_t)b * N + i) * levels + l) * E + yy) * E;
+#pragma unroll
+    for (int xx = 0; xx < E; ++xx) dst[xx] = acc[xx];
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void corr_window_reduce_kernel(WinList wl_, int levels, int B, int H,
+                                                                 int W, float inv_sqrt_c,
+                                                                 float* __restrict__ out) {
+  constexpr int D = 2 * R + 1, E = D + 1;
+  extern __shared__ float planes[];
+  const int N = H * W;
+  const int b = blockIdx.x / N, i = blockIdx.x % N;
+  int hs[4], ws[4], off[4];
+  int tot = 0;
+  {
+    int h = H, w = W;
+    for (int l = 0; l < 4; ++l) {
+      hs[l] = h; ws[l] = w; off[l] = tot;
+      if (l < levels) tot += h * w;
+      h >>= 1; w >>= 1;
+    }
+  }
+  for (int e = threadIdx.x; e < tot; e += 256) planes[e] = 0.f;
+  __syncthreads();
+  for (int k = 0; k < wl_.n; ++k) {
+    const float* C = wl_.coords[k];
+    const float* G = wl_.wg[k] + ((int64_t)b * N + i) * levels * E * E;
+    const float x = C[((int64_t)b * 2) * N + i], y = C[((int64_t)b * 2 + 1) * N + i];
+    for (int e = threadIdx.x; e < levels * E * E; e += 256) {
+      const int l = e / (E * E), yy = (e / E) % E, xx = e % E;
+      const float inv = 1.0f / (float)(1 << l);
+      const int xs = (int)floorf(clampc(x * inv)) - R, ys = (int)floorf(clampc(y * inv)) - R;
+      const int gy = ys + yy, gx = xs + xx;
+      if (gy >= 0 && gy < hs[l] && gx >= 0 && gx < ws[l])
+        planes[off[l] + gy * ws[l] + gx] += G[e];
+    }
+    __syncthreads();
+  }
+  float* O = out + ((int64_t)b * N + i) * N;
+  for (int e = threadIdx.x; e < N; e += 256) {
+    const int y = e / W, x = e % W;
+    float v = planes[e];
+    float s = 0.25f;
+    for (int l = 1; l < levels; ++l) {
+      const int yl = y >> l, xl = x >> l;
+      if (yl < hs[l] && xl < ws[l]) v += s * planes[off[l] + yl * ws[l] + xl];
+      s *= 0.25f;
+    }
+    O[e] = v * inv_sqrt_c;
+  }
+}
+
+}  // namespace
+
+bool launch_corr_lookup_tile(const float* const* lvl, const int* hs, const int* ws, int levels,
+                             const float* coords, uint16_t* out, int cbuf, int B, int H, int W,
+                             int radius, hipStream_t stream) {
+  PyrC4 p;
+  for (int l = 0; l < 4; ++l) {
+    p.lvl[l] = l < levels ? lvl[l] : nullptr;
+    p.h[l] = l < levels ? hs[l] : 0;
+    p.w[l] = l < levels ? ws[l] : 0;
+  }
+  const int N = H * W;
+  dim3 grid((unsigned)(B * ((N + TP - 1) / TP)));
+  if (radius == 4) hipLaunchKernelGGL(corr_lookup_tile_kernel<4>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+  else if (radius == 3) hipLaunchKernelGGL(corr_lookup_tile_kernel<3>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+  else return false;
+  return true;
+}
+
+bool launch_corr_window_grad(const float* coords, const uint16_t* dout, int cbuf, float* wg, int B,
+                             int H, int W, int levels, int radius, hipStream_t stream) {
+  const int N = H * W;
+  dim3 grid((unsigned)(B * ((N + TP - 1) / TP)));
+  if (radius == 4) hipLaunchKernelGGL(corr_window_grad_kernel<4>, grid, dim3(256), 0, stream, coords, dout, cbuf, wg, B, H, W, levels);
+  else if (radius == 3) hipLaunchKernelGGL(corr_window_grad_kernel<3>, grid, dim3(256), 0, stream, coords, dout, cbuf, wg, B, H, W, levels);
+  else return false;
+  return true;
+}
+
+int corr_window_reduce_lds_bytes(int H, int W, int levels) {
+  int tot = 0, h = H, w = W;
+  for (int l = 0; l < levels; ++l) { tot += h * w; h >>= 1; w >>= 1; }
+  return tot * 4;
+}
+
+bool launch_corr_window_reduce(const WinList& wl, int levels, int B, int H, int W, int radius,
+                               float inv_sqrt_c, float* out, hipStream_t stream) {
+  const int lds = corr_window_reduce_lds_bytes(H, W, levels);
+  dim3 grid((unsigned)(B * H * W));
+  if (radius == 4) hipLaunchKernelGGL(corr_window_reduce_kernel<4>, grid, dim3(256), lds, stream, wl, levels, B, H, W, inv_sqrt_c, out);
+  else if (radius == 3) hipLaunchKernelGGL(corr_window_reduce_kernel<3>, grid, dim3(256), lds, stream, wl, levels, B, H, W, inv_sqrt_c, out);
+  else return false;
+  return true;
+}

@@ -141,3 +141,26 @@ void launch_gru_zr_bwd(const float* drh, const float* dz, const uint16_t* z, con
                        hipStream_t stream);
 void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int slot_stride, int B,
                       int HW, hipStream_t stream);
+
+// ---- NHWC lookup tile + window-compact backward (corr_window.hip)
+#define RAFT_MAX_WIN 32
+struct WinList {
+  const float* coords[RAFT_MAX_WIN];  // (B,2,H,W) per iteration
+  const float* wg[RAFT_MAX_WIN];      // (B,N,L,E,E) per iteration
+  int n;
+};
+bool launch_corr_lookup_tile(const float* const* lvl, const int* hs, const int* ws, int levels,
+                             const float* coords, uint16_t* out, int cbuf, int B, int H, int W,
+                             int radius, hipStream_t stream);
+bool launch_corr_window_grad(const float* coords, const uint16_t* dout, int cbuf, float* wg, int B,
+                             int H, int W, int levels, int radius, hipStream_t stream);
+int corr_window_reduce_lds_bytes(int H, int W, int levels);
+bool launch_corr_window_reduce(const WinList& wl, int levels, int B, int H, int W, int radius,
+                               float inv_sqrt_c, float* out, hipStream_t stream);
+
+// ---- NHWC convex upsample (upsample.hip)
+bool launch_convex_up_nhwc_fwd(const float* flow, const uint16_t* mask, float* out, int B, int H,
+                               int W, hipStream_t stream);
+bool launch_convex_up_nhwc_bwd(const float* flow, const uint16_t* mask, const float* dout,
+                               uint16_t* dmask, float* wbuf, float* dflow, int B, int H, int W,
+                               hipStream_t stream);

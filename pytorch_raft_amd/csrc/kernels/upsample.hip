@@ -162,7 +162,128 @@ __global__ __launch_bounds__(256) void convex_up_bwd_flow_kernel(const float* __
   dflow[(b * 2 + 1) * HW + (int64_t)y * W + x] = 8.f * s1;
 }
 
+// ---- NHWC bf16 mask (B,H,W,576) as written by the fused update block: one wave per cell,
+// lane = sub-pixel s, so the 9 mask reads per lane are 9 coalesced 128-B rows.
+__device__ __forceinline__ void cell_flows(const float* F, int64_t HW, int y, int x, int H, int W,
+                                           float (&nf)[9][2]) {
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const int yy = y + k / 3 - 1, xx = x + k % 3 - 1;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    nf[k][0] = ok ? 8.f * F[(int64_t)yy * W + xx] : 0.f;
+    nf[k][1] = ok ? 8.f * F[HW + (int64_t)yy * W + xx] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void convex_up_nhwc_fwd_kernel(const float* __restrict__ flow,
+                                                                 const uint16_t* __restrict__ mask,
+                                                                 float* __restrict__ out, int B,
+                                                                 int H, int W) {
+  const int s = threadIdx.x & 63;
+  const int64_t cell = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t HW = (int64_t)H * W;
+  if (cell >= (int64_t)B * HW) return;
+  const int64_t b = cell / HW;
+  const int yx = (int)(cell - b * HW), y = yx / W, x = yx % W;
+  float nf[9][2];
+  cell_flows(flow + b * 2 * HW, HW, y, x, H, W, nf);
+  const uint16_t* M = mask + cell * 576;
+  float m[9], mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    m[k] = raft_bf16_to_f32(M[k * 64 + s]);
+    mx = fmaxf(mx, m[k]);
+  }
+  float den = 0.f, o0 = 0.f, o1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const float e = __expf(m[k] - mx);
+    den += e;
+    o0 += e * nf[k][0];
+    o1 += e * nf[k][1];
+  }
+  const float inv = 1.f / den;
+  const int64_t W8 = 8 * (int64_t)W;
+  const int64_t o = (int64_t)(8 * y + (s >> 3)) * W8 + 8 * x + (s & 7);
+  float* O = out + b * 2 * 64 * HW;
+  O[o] = o0 * inv;
+  O[64 * HW + o] = o1 * inv;
+}
+
+__global__ __launch_bounds__(256) void convex_up_nhwc_bwd_kernel(const float* __restrict__ flow,
+                                                                 const uint16_t* __restrict__ mask,
+                                                                 const float* __restrict__ dout,
+                                                                 uint16_t* __restrict__ dmask,
+                                                                 float* __restrict__ wbuf, int B,
+                                                                 int H, int W) {
+  const int s = threadIdx.x & 63;
+  const int64_t cell = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t HW = (int64_t)H * W;
+  if (cell >= (int64_t)B * HW) return;  // whole wave exits together (cell is wave-uniform)
+  const int64_t b = cell / HW;
+  const int yx = (int)(cell - b * HW), y = yx / W, x = yx % W;
+  float nf[9][2];
+  cell_flows(flow + b * 2 * HW, HW, y, x, H, W, nf);
+  const uint16_t* M = mask + cell * 576;
+  float p[9], mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    p[k] = raft_bf16_to_f32(M[k * 64 + s]);
+    mx = fmaxf(mx, p[k]);
+  }
+  float den = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    p[k] = __expf(p[k] - mx);
+    den += p[k];
+  }
+  const float inv = 1.f / den;
+  const int64_t W8 = 8 * (int64_t)W;
+  const int64_t o = (int64_t)(8 * y + (s >> 3)) * W8 + 8 * x + (s & 7);
+  const float* DO = dout + b * 2 * 64 * HW;
+  const float d0 = DO[o], d1 = DO[64 * HW + o];
+  float g[9], dot = 0.f;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    p[k] *= inv;
+    g[k] = d0 * nf[k][0] + d1 * nf[k][1];
+    dot += p[k] * g[k];
+  }
+  uint16_t* DM = dmask + cell * 576;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) DM[k * 64 + s] = raft_f32_to_bf16(p[k] * (g[k] - dot));
+  // neighbour weights W[k][c] = sum_s p_k d_c, reduced across the wave
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const float w0 = wave_sum(p[k] * d0);
+    const float w1 = wave_sum(p[k] * d1);
+    if (s == 0) {
+      wbuf[(b * 18 + 2 * k) * HW + yx] = w0;
+      wbuf[(b * 18 + 2 * k + 1) * HW + yx] = w1;
+    }
+  }
+}
+
 }  // namespace
+
+bool launch_convex_up_nhwc_fwd(const float* flow, const uint16_t* mask, float* out, int B, int H,
+                               int W, hipStream_t stream) {
+  const int64_t cells = (int64_t)B * H * W;
+  hipLaunchKernelGGL(convex_up_nhwc_fwd_kernel, dim3(raft_cdiv(cells, 4)), dim3(256), 0, stream,
+                     flow, mask, out, B, H, W);
+  return true;
+}
+
+bool launch_convex_up_nhwc_bwd(const float* flow, const uint16_t* mask, const float* dout,
+                               uint16_t* dmask, float* wbuf, float* dflow, int B, int H, int W,
+                               hipStream_t stream) {
+  const int64_t cells = (int64_t)B * H * W;
+  hipLaunchKernelGGL(convex_up_nhwc_bwd_kernel, dim3(raft_cdiv(cells, 4)), dim3(256), 0, stream,
+                     flow, mask, dout, dmask, wbuf, B, H, W);
+  hipLaunchKernelGGL(convex_up_bwd_flow_kernel, dim3(raft_cdiv(cells, 256)), dim3(256), 0, stream,
+                     wbuf, dflow, B, H, W);
+  return true;
+}
 
 bool launch_convex_up_fwd(const float* flow, const void* mask, int mask_is_bf16, int64_t mbs,
                           int64_t mcs, int64_t mps, float* out, int B, int H, int W,

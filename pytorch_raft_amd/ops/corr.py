@@ -32,6 +32,8 @@ class _State:
     def __init__(self):
         self.grad = None
         self.grad_f1 = None
+        self.windows = []
+        self.radius = None
 
 
 class _AllPairsBuild(torch.autograd.Function):
@@ -49,11 +51,18 @@ class _AllPairsBuild(torch.autograd.Function):
     def backward(ctx, _dtoken):
         st = ctx.state
         fmap1, fmap2 = ctx.saved_tensors
-        if st.grad is None:
+        if st.grad is None and not st.windows:
             return None, None, None, None
         b, c, h, w = fmap1.shape
-        dcorr = _ext.ops().corr_pyr_grad_reduce(st.grad, 1.0 / math.sqrt(c))  # (B, N, N)
+        dcorr = None
+        if st.grad is not None:
+            dcorr = _ext.ops().corr_pyr_grad_reduce(st.grad, 1.0 / math.sqrt(c))  # (B, N, N)
+        if st.windows:
+            dw = _ext.ops().corr_window_reduce([x[0] for x in st.windows], [x[1] for x in st.windows],
+                                               h, w, len(st.pyramid), st.radius, 1.0 / math.sqrt(c))
+            dcorr = dw if dcorr is None else dcorr + dw
         st.grad = None
+        st.windows = []
         st.pyramid = None
         f1 = fmap1.view(b, c, h * w)
         f2 = fmap2.view(b, c, h * w)
@@ -100,10 +109,27 @@ class _AllPairsLookupNHWC(torch.autograd.Function):
     def backward(ctx, dout):
         st = ctx.state
         (coords,) = ctx.saved_tensors
-        if st.grad is None:
-            st.grad = [torch.zeros_like(p) for p in st.pyramid]
-        _ext.ops().corr_lookup_bwd_(st.grad, coords, dout.float().contiguous(), ctx.radius)
+        b, _, h, w = coords.shape
+        levels = len(st.pyramid)
+        if _window_reduce_fits(h, w, levels) and len(st.windows) < 32:
+            # compact per-iteration window gradient; folded into dcorr once per step
+            wg = _ext.ops().corr_window_grad(coords, dout.to(torch.bfloat16).contiguous(), levels,
+                                             ctx.radius)
+            st.windows.append((coords, wg))
+            st.radius = ctx.radius
+        else:
+            if st.grad is None:
+                st.grad = [torch.zeros_like(p) for p in st.pyramid]
+            _ext.ops().corr_lookup_bwd_(st.grad, coords, dout.float().contiguous(), ctx.radius)
         return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None, None
+
+
+def _window_reduce_fits(h, w, levels):
+    tot, hh, ww = 0, h, w
+    for _ in range(levels):
+        tot += hh * ww
+        hh, ww = hh // 2, ww // 2
+    return tot * 4 <= 64 * 1024
 
 
 class AllPairsVolume:

@@ -50,7 +50,15 @@ def _returns():
         b, h, w, c = f1.shape
         return torch.zeros(b, h, w, len(f2) * (2 * r + 1) ** 2)
 
+    def win_grad(coords, dout, levels, r):
+        b, _, h, w = coords.shape
+        return torch.zeros(b, h * w, levels, 2 * r + 2, 2 * r + 2)
+
+    def win_reduce(coords, wgs, h, w, levels, r, s):
+        return torch.zeros(coords[0].shape[0], h * w, h * w)
+
     return {'corr_build': corr_build, 'corr_lookup_fwd': lookup, 'corr_pyr_grad_reduce': reduce,
+            'corr_window_grad': win_grad, 'corr_window_reduce': win_reduce,
             'convex_up_fwd': cup_fwd, 'convex_up_bwd': cup_bwd, 'seq_loss_fwd': loss_fwd,
             'seq_loss_bwd': loss_bwd, 'corr_otf_fwd': otf}
 
@@ -73,7 +81,7 @@ def test_dry_run_fused_training_step(alternate):
     assert {'conv_fwd_', 'conv_dgrad_', 'conv_wgrad_', 'gru_q_bwd_', 'gru_zr_bwd_', 'relu_bwd_',
             'flow_prep_', 'convex_up_fwd', 'convex_up_bwd', 'seq_loss_fwd'} <= names, names
     if not alternate:
-        assert {'corr_build', 'corr_lookup_nhwc_', 'corr_lookup_bwd_', 'corr_pyr_grad_reduce'} <= names
+        assert {'corr_build', 'corr_lookup_nhwc_', 'corr_window_grad', 'corr_window_reduce'} <= names
     # every update-block parameter received a gradient through the fused backward
     for n, p in m.named_parameters():
         if n.startswith('update_block'):

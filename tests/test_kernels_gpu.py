@@ -145,3 +145,55 @@ def test_lookup_deterministic(ext_ops):
         grads.append((f1.grad.clone(), f2.grad.clone()))
         f1.grad = f2.grad = None
     assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+
+
+@pytest.mark.parametrize('hw', [(16, 20), (13, 19), (46, 62)])
+def test_lookup_nhwc_window_backward(ext_ops, hw):
+    """bf16 NHWC lookup (fused update-block input) + compact window backward vs grid_sample."""
+    h, w = hw
+    b, c, radius = 2, 256, 4
+    f1 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    f2 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    levels = 3 if min(h, w) < 16 else 4
+    coords = [_coords(b, h, w, seed=s) for s in range(3)]
+    pyr = torch_corr_pyramid(f1, f2, levels)
+    gouts = [torch.randn(b, h, w, 352, device=DEV).to(torch.bfloat16) for _ in coords]
+    loss = 0
+    for co, go in zip(coords, gouts):
+        ref = torch_corr_lookup(pyr, co, radius)  # (b, L*81, h, w)
+        loss = loss + (ref.permute(0, 2, 3, 1) * go[..., :ref.shape[1]].float()).sum()
+    loss.backward()
+    g1_ref, g2_ref = f1.grad.clone(), f2.grad.clone()
+    f1.grad = f2.grad = None
+
+    blk = CorrBlock(f1, f2, num_levels=levels, radius=radius, impl='hip')
+    loss = 0
+    for co, go in zip(coords, gouts):
+        out = blk.lookup_nhwc(co, 352)
+        assert out.shape == (b, h, w, 352) and out.dtype == torch.bfloat16
+        nc = levels * 81
+        ref = torch_corr_lookup(pyr, co, radius).permute(0, 2, 3, 1)
+        torch.testing.assert_close(out[..., :nc].float(), ref.detach(), atol=3e-2, rtol=1e-2)
+        assert torch.all(out[..., nc:] == 0)
+        loss = loss + (out.float() * go.float()).sum()
+    loss.backward()
+    torch.testing.assert_close(f1.grad, g1_ref, atol=3e-3, rtol=3e-3)
+    torch.testing.assert_close(f2.grad, g2_ref, atol=3e-3, rtol=3e-3)
+
+
+@pytest.mark.parametrize('hw', [(8, 9), (46, 62)])
+def test_convex_upsample_nhwc(ext_ops, hw):
+    h, w = hw
+    b = 2
+    flow = torch.randn(b, 2, h, w, device=DEV, requires_grad=True)
+    mask = (3 * torch.randn(b, h, w, 576, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    ref = torch_convex_upsample(flow, mask.float().permute(0, 3, 1, 2))
+    g = torch.randn_like(ref)
+    (ref * g).sum().backward()
+    gf_ref, gm_ref = flow.grad.clone(), mask.grad.clone().float()
+    flow.grad = mask.grad = None
+    out = convex_upsample(flow, mask, impl='hip', nhwc=True)
+    torch.testing.assert_close(out.float(), ref, atol=1e-4, rtol=1e-4)
+    (out.float() * g).sum().backward()
+    torch.testing.assert_close(flow.grad, gf_ref, atol=1e-3, rtol=1e-4)
+    torch.testing.assert_close(mask.grad.float(), gm_ref, atol=2e-2, rtol=2e-2)
