@@ -211,70 +211,109 @@ Tensor corr_pyr_grad_reduce(const std::vector<Tensor>& gpyr, double inv_sqrt_c) 
 }
 
 // ------------------------------------------------------------------ on-the-fly correlation
-struct NhwcLevels {
-  std::vector<const float*> cptr;
-  std::vector<float*> ptr;
+struct Bf16Levels {
+  std::vector<const uint16_t*> ptr;
   std::vector<int> h, w;
 };
 
-NhwcLevels nhwc_levels(const std::vector<Tensor>& lv, int64_t B, int64_t C, const char* name) {
-  TORCH_CHECK(!lv.empty() && lv.size() <= 4, name, ": 1..4 levels required");
-  NhwcLevels L;
+void check_cuda_bf16(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16, got ", t.scalar_type());
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+// fmap2 pyramid (NHWC bf16): level l is (B, floor(h/2^l), floor(w/2^l), C)
+Bf16Levels otf_levels(const std::vector<Tensor>& lv, int64_t B, int64_t C, int64_t H, int64_t W) {
+  TORCH_CHECK(!lv.empty() && lv.size() <= 4, "fmap2 pyramid: 1..4 levels required");
+  Bf16Levels L;
+  int64_t h = H, w = W;
   for (const auto& t : lv) {
-    check_cuda_f32(t, name);
-    TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(3) == C, name, " must be (B,h,w,C)");
-    L.cptr.push_back(t.data_ptr<float>());
-    L.ptr.push_back(t.data_ptr<float>());
-    L.h.push_back((int)t.size(1));
-    L.w.push_back((int)t.size(2));
+    check_cuda_bf16(t, "fmap2 level");
+    TORCH_CHECK(t.dim() == 4 && t.size(0) == B && t.size(1) == h && t.size(2) == w &&
+                    t.size(3) == C,
+                "fmap2 level must be (B, h/2^l, w/2^l, C) NHWC");
+    TORCH_CHECK(h >= 1 && w >= 1, "feature map too small for the pyramid");
+    L.ptr.push_back(reinterpret_cast<const uint16_t*>(t.data_ptr()));
+    L.h.push_back((int)h);
+    L.w.push_back((int)w);
+    h /= 2;
+    w /= 2;
   }
   return L;
 }
 
-Tensor corr_otf_fwd(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor& coords,
-                    int64_t radius) {
-  check_cuda_f32(f1, "fmap1");
+void otf_common_checks(const Tensor& f1, const Tensor& coords, int64_t radius) {
+  check_cuda_bf16(f1, "fmap1");
   check_cuda_f32(coords, "coords");
-  TORCH_CHECK(f1.dim() == 4, "fmap1 must be (B,H,W,C)");
-  const int64_t B = f1.size(0), H = f1.size(1), W = f1.size(2), C = f1.size(3);
-  TORCH_CHECK(coords.dim() == 4 && coords.size(0) == B && coords.size(1) == 2 &&
-                  coords.size(2) == H && coords.size(3) == W,
+  TORCH_CHECK(f1.dim() == 4, "fmap1 must be (B,H,W,C) NHWC");
+  TORCH_CHECK(f1.size(3) == 128 || f1.size(3) == 256, "on-the-fly corr supports C = 128/256");
+  TORCH_CHECK(radius == 3 || radius == 4, "radius must be 3 or 4");
+  TORCH_CHECK(coords.dim() == 4 && coords.size(0) == f1.size(0) && coords.size(1) == 2 &&
+                  coords.size(2) == f1.size(1) && coords.size(3) == f1.size(2),
               "coords must be (B,2,H,W)");
+}
+
+// out (B,H,W,S) fp32 or bf16, S >= L*(2r+1)^2; channels past L*(2r+1)^2 are zero-filled
+// lo = [] (bf16 operands) or [f1_lo, f2_lo levels...] (split-bf16, fp32-accurate)
+void corr_otf_fwd_(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor& coords,
+                   int64_t radius, const Tensor& out, const std::vector<Tensor>& lo) {
+  otf_common_checks(f1, coords, radius);
+  const int64_t B = f1.size(0), H = f1.size(1), W = f1.size(2), C = f1.size(3);
   c10::DeviceGuard g(f1.device());
-  NhwcLevels L = nhwc_levels(f2, B, C, "fmap2 pyramid");
-  TORCH_CHECK(L.h[0] == H && L.w[0] == W, "fmap2 level 0 must match fmap1");
+  Bf16Levels L = otf_levels(f2, B, C, H, W);
+  const uint16_t* f1lo = nullptr;
+  Bf16Levels LL;
+  if (!lo.empty()) {
+    TORCH_CHECK(lo.size() == f2.size() + 1, "lo must be [f1_lo, f2_lo levels...]");
+    check_cuda_bf16(lo[0], "fmap1 lo");
+    TORCH_CHECK(lo[0].sizes() == f1.sizes(), "fmap1 lo shape mismatch");
+    f1lo = reinterpret_cast<const uint16_t*>(lo[0].data_ptr());
+    LL = otf_levels(std::vector<Tensor>(lo.begin() + 1, lo.end()), B, C, H, W);
+  }
   const int64_t D = 2 * radius + 1;
-  Tensor out = at::empty({B, H, W, (int64_t)f2.size() * D * D}, f1.options());
-  TORCH_CHECK(launch_corr_otf_fwd(f1.data_ptr<float>(), L.cptr.data(), L.h.data(), L.w.data(),
-                                  (int)f2.size(), coords.data_ptr<float>(), out.data_ptr<float>(),
-                                  (int)B, (int)C, (int)H, (int)W, (int)radius, cur_stream()),
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.dim() == 4 && out.size(0) == B &&
+                  out.size(1) == H && out.size(2) == W && out.size(3) >= (int64_t)f2.size() * D * D,
+              "out must be contiguous (B,H,W,S) with S >= levels*(2r+1)^2");
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16,
+              "out must be float32 or bfloat16");
+  TORCH_CHECK(launch_corr_otf_fwd(reinterpret_cast<const uint16_t*>(f1.data_ptr()), L.ptr.data(),
+                                  f1lo, f1lo ? LL.ptr.data() : nullptr, L.h.data(), L.w.data(),
+                                  (int)f2.size(),
+                                  coords.data_ptr<float>(), out.data_ptr(),
+                                  out.scalar_type() == at::kBFloat16, (int)out.size(3), (int)B,
+                                  (int)C, (int)H, (int)W, (int)radius, cur_stream()),
               "on-the-fly corr supports radius 3/4 with C = 128/256");
-  return out;
 }
 
 void corr_otf_bwd_(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor& coords,
                    const Tensor& dout, const Tensor& df1, const std::vector<Tensor>& df2,
                    int64_t radius) {
-  check_cuda_f32(f1, "fmap1");
-  check_cuda_f32(coords, "coords");
-  check_cuda_f32(dout, "grad_corr");
-  check_cuda_f32(df1, "grad_fmap1");
+  otf_common_checks(f1, coords, radius);
   const int64_t B = f1.size(0), H = f1.size(1), W = f1.size(2), C = f1.size(3);
-  TORCH_CHECK(df1.sizes() == f1.sizes(), "grad_fmap1 shape mismatch");
+  check_cuda_f32(df1, "grad_fmap1");
+  TORCH_CHECK(df1.sizes() == f1.sizes(), "grad_fmap1 must be (B,H,W,C)");
   const int64_t D = 2 * radius + 1;
-  TORCH_CHECK(dout.dim() == 4 && dout.size(0) == B && dout.size(1) == H && dout.size(2) == W &&
-                  dout.size(3) == (int64_t)f2.size() * D * D,
-              "grad_corr must be (B,H,W,L*D*D) contiguous");
+  TORCH_CHECK(dout.is_cuda() && dout.is_contiguous() && dout.dim() == 4 && dout.size(0) == B &&
+                  dout.size(1) == H && dout.size(2) == W &&
+                  dout.size(3) >= (int64_t)f2.size() * D * D,
+              "grad_corr must be contiguous (B,H,W,S) with S >= levels*(2r+1)^2");
+  TORCH_CHECK(dout.scalar_type() == at::kFloat || dout.scalar_type() == at::kBFloat16,
+              "grad_corr must be float32 or bfloat16");
   TORCH_CHECK(f2.size() == df2.size(), "level count mismatch");
   c10::DeviceGuard g(f1.device());
-  NhwcLevels L = nhwc_levels(f2, B, C, "fmap2 pyramid");
-  NhwcLevels G = nhwc_levels(df2, B, C, "grad fmap2 pyramid");
-  for (size_t l = 0; l < f2.size(); ++l)
-    TORCH_CHECK(L.h[l] == G.h[l] && L.w[l] == G.w[l], "grad pyramid shape mismatch");
-  TORCH_CHECK(launch_corr_otf_bwd(f1.data_ptr<float>(), L.cptr.data(), L.h.data(), L.w.data(),
-                                  (int)f2.size(), coords.data_ptr<float>(), dout.data_ptr<float>(),
-                                  df1.data_ptr<float>(), G.ptr.data(), (int)B, (int)C, (int)H,
-                                  (int)W, (int)radius, cur_stream()),
+  Bf16Levels L = otf_levels(f2, B, C, H, W);
+  std::vector<float*> gp;
+  for (size_t l = 0; l < df2.size(); ++l) {
+    check_cuda_f32(df2[l], "grad fmap2 level");
+    TORCH_CHECK(df2[l].sizes() == f2[l].sizes(), "grad fmap2 level shape mismatch");
+    gp.push_back(df2[l].data_ptr<float>());
+  }
+  TORCH_CHECK(launch_corr_otf_bwd(reinterpret_cast<const uint16_t*>(f1.data_ptr()), L.ptr.data(),
+                                  L.h.data(), L.w.data(), (int)f2.size(),
+                                  coords.data_ptr<float>(), dout.data_ptr(),
+                                  dout.scalar_type() == at::kBFloat16, (int)dout.size(3),
+                                  df1.data_ptr<float>(), gp.data(), (int)B, (int)C, (int)H, (int)W,
+                                  (int)radius, cur_stream()),
               "on-the-fly corr supports radius 3/4 with C = 128/256");
 }
 
@@ -720,7 +759,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_lookup_fwd(Tensor[] pyr, Tensor coords, int radius) -> Tensor");
   m.def("corr_lookup_bwd_(Tensor(a!)[] gpyr, Tensor coords, Tensor dout, int radius) -> ()");
   m.def("corr_pyr_grad_reduce(Tensor[] gpyr, float inv_sqrt_c) -> Tensor");
-  m.def("corr_otf_fwd(Tensor f1, Tensor[] f2, Tensor coords, int radius) -> Tensor");
+  m.def("corr_otf_fwd_(Tensor f1, Tensor[] f2, Tensor coords, int radius, Tensor(a!) out, Tensor[] lo) -> ()");
   m.def("corr_otf_bwd_(Tensor f1, Tensor[] f2, Tensor coords, Tensor dout, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");
   m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout, bool nhwc=False) -> Tensor[]");
@@ -745,7 +784,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("corr_lookup_fwd", &corr_lookup_fwd);
   m.impl("corr_lookup_bwd_", &corr_lookup_bwd_);
   m.impl("corr_pyr_grad_reduce", &corr_pyr_grad_reduce);
-  m.impl("corr_otf_fwd", &corr_otf_fwd);
+  m.impl("corr_otf_fwd_", &corr_otf_fwd_);
   m.impl("corr_otf_bwd_", &corr_otf_bwd_);
   m.impl("convex_up_fwd", &convex_up_fwd);
   m.impl("convex_up_bwd", &convex_up_bwd);

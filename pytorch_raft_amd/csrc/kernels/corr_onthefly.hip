@@ -1,201 +1,444 @@
-// On-the-fly ("alternate") correlation lookup, forward + backward, O(HW * r^2) memory.
+// On-the-fly ("alternate") correlation lookup on MFMA, forward + backward, O(HW * r^2) memory.
 //
 // Capability parity with `alt_cuda_corr` (`alt_cuda_corr/correlation_kernel.cu:18-119` forward,
-// `:122-256` backward) and `AlternateCorrBlock` (`core/corr.py:63-91`), re-designed for wave64:
+// `:122-256` backward) and `AlternateCorrBlock` (`core/corr.py:63-91`), re-designed for CDNA4:
 //
-// * one wave per query pixel; its fmap1 row (C channels) lives in registers, C/64 channels per lane,
-//   so every fmap2 row read is one coalesced 512 B / 1 KiB wave access (the reference stages
-//   32-channel slices through LDS from a 32-thread block, i.e. half a wave on CDNA);
-// * the (2r+2)^2 integer-position dot products are finished with a 64-way reduce-scatter across the
-//   lanes (63 shuffles per 64 positions instead of 6 per position), after which lane p owns
-//   position p and the (2r+1)^2 bilinear taps are blended from LDS;
-// * output is written channels-last (B, H, W, L*(2r+1)^2) so each pixel's taps are contiguous; the
-//   Python side returns it as an NCHW-shaped channels_last tensor;
-// * explicit bounds on every coordinate (the reference backward reads coords out of range when
-//   H % 4 or W % 8 != 0) and no reliance on lock-step execution for LDS hand-offs;
-// * the backward is wired into autograd (the reference's is unreachable): d(fmap1) per wave in
-//   registers, d(fmap2 level) via float atomics into a buffer that persists across iterations.
+// * A workgroup owns an 8x8 tile of query pixels (64 = two 32-row MFMA blocks).  Per pyramid level
+//   it takes the bounding box of the tile's (2r+2)^2 integer windows, clipped to the map (flow is
+//   locally smooth, so at chairs this is ~18x18 positions at level 0 and shrinks with the level),
+//   and computes the dense tile GEMM S = F1_tile (64 x C) * F2_box^T (C x U) with
+//   v_mfma_f32_32x32x16_bf16 (fp32 accumulation).  fmap2 rows are streamed through LDS in chunks
+//   of 64 positions (register prefetch of the next chunk overlaps the MFMAs); the fmap1 fragments
+//   stay in registers for all levels.  Each accumulator element is dropped into the owning pixel's
+//   private (2r+2)^2 window in LDS, from which the (2r+1)^2 bilinear taps are blended.  The
+//   reference does the same dots one 32-channel slice at a time on scalar FMAs.
+// * Backward per level: the bilinear adjoint gives each pixel's window gradient dW (LDS); per chunk
+//   dS (64 px x 64 pos, bf16) is scattered from dW, then two MFMA GEMMs run with transposed LDS
+//   fragments (ds_read_b64_tr_b16):  dF1_tile += dS * F2_chunk (kept in registers across chunks and
+//   levels, one plain store per tile) and dF2_chunk = dS^T * F1_tile (fp32 atomics, 128-B
+//   segments, into a per-level gradient buffer that persists across GRU iterations).
+// * Pixels whose window misses the map entirely do not widen the box; every coordinate is clamped
+//   and bounds-checked (the reference backward reads coords out of range when H % 4 or W % 8 != 0,
+//   and relies on 32-thread lock-step for its LDS hand-offs).
+// * Output is written channels-last (B, H, W, S) at channel l*(2r+1)^2 + tap, x-offset-major tap
+//   order (`core/corr.py:37-43`); the channels [L*(2r+1)^2, S) are zero-filled so the bf16 variant
+//   feeds the fused update block's first 1x1 conv directly.
 #include "common.h"
 #include "launchers.h"
 
 namespace {
 
-struct F2Lvls {
-  const float* lvl[4];
-  int h[4];
-  int w[4];
-};
-struct G2Lvls {
-  float* lvl[4];
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4_t;
+
+constexpr int TPX = 8;     // query tile width
+constexpr int TP = 64;     // query pixels per tile (8 x 8)
+constexpr int NCH = 64;    // fmap2 positions per LDS chunk
+constexpr int NT = 256;
+
+struct OtfLvls {
+  const uint16_t* f2[4];
+  float* g2[4];
   int h[4];
   int w[4];
 };
 
-__device__ __forceinline__ float clampc(float v) { return fminf(fmaxf(v, -1.0e7f), 1.0e7f); }
+__device__ __forceinline__ float clampc(float v) { return fminf(fmaxf(v, -1.0e6f), 1.0e6f); }
 
-// v[0..63] per lane -> lane L returns sum over lanes of v[L]
-__device__ __forceinline__ float reduce_scatter64(float (&v)[64], int lane) {
+__device__ __forceinline__ int wave_min_i(int v) {
 #pragma unroll
-  for (int s = 32; s >= 1; s >>= 1) {
-    const bool up = (lane & s) != 0;
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
-    for (int j = 0; j < s; ++j) {
-      const float send = up ? v[j] : v[j + s];
-      const float keep = up ? v[j + s] : v[j];
-      v[j] = keep + __shfl_xor(send, s, 64);
-    }
-  }
-  return v[0];
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
 }
 
-template <int R, int CPL>
-__global__ __launch_bounds__(256) void corr_otf_fwd_kernel(const float* __restrict__ f1, F2Lvls f2,
-                                                           const float* __restrict__ coords,
-                                                           float* __restrict__ out, int B, int H,
-                                                           int W, int levels, float inv_sqrt_c) {
-  constexpr int D = 2 * R + 1;
-  constexpr int E = D + 1;       // integer positions per axis
-  constexpr int NP = E * E;      // <= 100
-  constexpr int NB = (NP + 63) / 64;
-  constexpr int C = CPL * 64;
-  __shared__ float dots[4][NB * 64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int N = H * W;
-  const int64_t pix = (int64_t)blockIdx.x * 4 + wv;
-  const bool active = pix < (int64_t)B * N;
-  const int b = active ? (int)(pix / N) : 0;
-  const int i = active ? (int)(pix % N) : 0;
+struct Geo {
+  int x0[TP], y0[TP];
+  float ax[TP], ay[TP];
+  int box[4];  // bx0, by0, bw, bh
+};
 
-  float a[CPL];
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) a[c] = active ? f1[((int64_t)b * N + i) * C + lane * CPL + c] : 0.f;
-  const float x = active ? coords[((int64_t)b * 2) * N + i] : 0.f;
-  const float y = active ? coords[((int64_t)b * 2 + 1) * N + i] : 0.f;
-  const int ctot = levels * D * D;
-  float* O = out + pix * ctot;
+// wave 0, lane = tile pixel: window origin / fractions at level l and the tile's clipped box
+template <int R>
+__device__ __forceinline__ void tile_geometry(Geo& g, int lane, bool act, float x, float y, int l,
+                                              int hl, int wl) {
+  constexpr int E = 2 * R + 2;
+  const float inv = 1.f / (float)(1 << l);
+  const float cx = clampc(x * inv), cy = clampc(y * inv);
+  const float fx = floorf(cx), fy = floorf(cy);
+  const int x0 = (int)fx - R, y0 = (int)fy - R;
+  const bool hit = act && x0 <= wl - 1 && x0 + E - 1 >= 0 && y0 <= hl - 1 && y0 + E - 1 >= 0;
+  g.x0[lane] = act ? x0 : -(1 << 28);
+  g.y0[lane] = act ? y0 : -(1 << 28);
+  g.ax[lane] = cx - fx;
+  g.ay[lane] = cy - fy;
+  const int mnx = wave_min_i(hit ? x0 : 0x7fffffff);
+  const int mxx = wave_max_i(hit ? x0 + E - 1 : -0x7fffffff);
+  const int mny = wave_min_i(hit ? y0 : 0x7fffffff);
+  const int mxy = wave_max_i(hit ? y0 + E - 1 : -0x7fffffff);
+  if (lane == 0) {
+    const int bx0 = max(mnx, 0), bx1 = min(mxx, wl - 1);
+    const int by0 = max(mny, 0), by1 = min(mxy, hl - 1);
+    const bool ok = bx1 >= bx0 && by1 >= by0;
+    g.box[0] = bx0;
+    g.box[1] = by0;
+    g.box[2] = ok ? bx1 - bx0 + 1 : 0;
+    g.box[3] = ok ? by1 - by0 + 1 : 0;
+  }
+}
 
-  for (int l = 0; l < levels; ++l) {
-    const float inv = 1.f / (float)(1 << l);
-    const float cx = clampc(x * inv), cy = clampc(y * inv);
-    const float fx = floorf(cx), fy = floorf(cy);
-    const float ax = cx - fx, ay = cy - fy;
-    const int xs = (int)fx - R, ys = (int)fy - R;
-    const int hl = f2.h[l], wl = f2.w[l];
-    const float* F2 = f2.lvl[l] + (int64_t)b * hl * wl * C;
+__device__ __forceinline__ bf16x8_t ld_frag(const uint16_t* p) {
+  return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(p));
+}
+__device__ __forceinline__ bf16x8_t zero_frag() {
+  return __builtin_bit_cast(bf16x8_t, make_uint4(0, 0, 0, 0));
+}
+// 8-deep K fragment of a [k][col] LDS matrix (row stride S elements) for columns base..base+31
+__device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* X, int S, int kbase, int base,
+                                            int lane) {
+  const int gi = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  const int col = base + (gi & 1) * 16 + 4 * pp;
+  const int row = kbase + (gi >> 1) * 8 + q;
+  bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(X + row * S + col));
+  bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(X + (row + 4) * S + col));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// chunk of NCH fmap2 positions of the box -> registers (zero rows past U)
+template <int C>
+struct ChunkLoader {
+  static constexpr int LPR = C / 8;             // 16-B units per position row
+  static constexpr int PER = NCH * LPR / NT;    // units per thread
+  uint4 r[PER];
+  __device__ __forceinline__ void load(const uint16_t* F2, int wl, int bx0, int by0, int bw, int U,
+                                       int c, int tid) {
 #pragma unroll
-    for (int pb = 0; pb < NB; ++pb) {
-      float v[64];
-#pragma unroll
-      for (int j = 0; j < 64; ++j) {
-        const int p = pb * 64 + j;
-        const int px = xs + p % E, py = ys + p / E;
-        float s = 0.f;
-        if (p < NP && px >= 0 && px < wl && py >= 0 && py < hl) {
-          const float* row = F2 + ((int64_t)py * wl + px) * C + lane * CPL;
-#pragma unroll
-          for (int c = 0; c < CPL; ++c) s += a[c] * row[c];
-        }
-        v[j] = s;
+    for (int j = 0; j < PER; ++j) {
+      const int e = tid + j * NT;
+      const int n = e / LPR, q = e % LPR;
+      const int pos = c * NCH + n;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (pos < U) {
+        const int iy = by0 + pos / bw, ix = bx0 + pos % bw;
+        v = *reinterpret_cast<const uint4*>(F2 + ((int64_t)iy * wl + ix) * C + q * 8);
       }
-      dots[wv][pb * 64 + lane] = reduce_scatter64(v, lane);
+      r[j] = v;
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* Bs, int RS, int tid) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int e = tid + j * NT;
+      const int n = e / LPR, q = e % LPR;
+      *reinterpret_cast<uint4*>(Bs + n * RS + q * 8) = r[j];
+    }
+  }
+};
+
+// SPLIT: fp32-accurate mode, operands carried as bf16 hi + lo parts (x ~= hi + lo) and
+// S = hi*hi + hi*lo + lo*hi on three MFMAs (~2^-16 relative error instead of bf16's 2^-9).
+template <int R, int C, typename TO, bool SPLIT>
+__global__ __launch_bounds__(NT, SPLIT ? 1 : 2) void corr_otf_fwd_kernel(
+    const uint16_t* __restrict__ f1, const uint16_t* __restrict__ f1lo, OtfLvls lv, OtfLvls lo,
+    const float* __restrict__ coords, TO* __restrict__ out, int ostride, int B, int H, int W, int levels, int tiles_x, int tiles_y,
+    float isc) {
+  constexpr int D = 2 * R + 1, E = D + 1, NP = E * E, DD = D * D;
+  constexpr int KS = C / 16;
+  constexpr int RS = C + 16;  // padded LDS row (bf16)
+  constexpr int NB = SPLIT ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[NB * NCH * RS];
+  __shared__ float win[TP * NP];
+  __shared__ Geo geo;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int mb = wave & 1, nh = wave >> 1;
+  int t = blockIdx.x;
+  const int tx = t % tiles_x;
+  t /= tiles_x;
+  const int ty = t % tiles_y;
+  const int b = t / tiles_y;
+  const int HW = H * W;
+
+  // fmap1 fragments of this wave's 32 pixels, all K, kept for every level
+  bf16x8_t af[KS], afl[SPLIT ? KS : 1];
+  {
+    const int p = mb * 32 + (lane & 31);
+    const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
+    const bool act = py < H && px < W;
+    const int64_t off = ((int64_t)b * HW + (act ? py * W + px : 0)) * C + 8 * (lane >> 5);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) af[s] = act ? ld_frag(f1 + off + 16 * s) : zero_frag();
+    if constexpr (SPLIT) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) afl[s] = act ? ld_frag(f1lo + off + 16 * s) : zero_frag();
+    }
+  }
+  // wave 0 owns the per-pixel coordinates
+  float cxv = 0.f, cyv = 0.f;
+  bool cact = false;
+  if (wave == 0) {
+    const int py = ty * TPX + lane / TPX, px = tx * TPX + lane % TPX;
+    cact = py < H && px < W;
+    if (cact) {
+      cxv = coords[((int64_t)b * 2) * HW + py * W + px];
+      cyv = coords[((int64_t)b * 2 + 1) * HW + py * W + px];
+    }
+  }
+
+  ChunkLoader<C> ld, ldl;
+  for (int l = 0; l < levels; ++l) {
+    const int hl = lv.h[l], wl = lv.w[l];
+    if (wave == 0) tile_geometry<R>(geo, lane, cact, cxv, cyv, l, hl, wl);
+    for (int e = tid; e < TP * NP; e += NT) win[e] = 0.f;
+    __syncthreads();
+    const int bx0 = geo.box[0], by0 = geo.box[1], bw = geo.box[2], bh = geo.box[3];
+    const int U = bw * bh;
+    const int nchunk = (U + NCH - 1) / NCH;
+    const int64_t boff = (int64_t)b * hl * wl * C;
+    const uint16_t* F2 = lv.f2[l] + boff;
+    const uint16_t* F2l = SPLIT ? lo.f2[l] + boff : nullptr;
+    if (nchunk > 0) {
+      ld.load(F2, wl, bx0, by0, bw, U, 0, tid);
+      if constexpr (SPLIT) ldl.load(F2l, wl, bx0, by0, bw, U, 0, tid);
+    }
+    for (int c = 0; c < nchunk; ++c) {
+      ld.store(Bs, RS, tid);
+      if constexpr (SPLIT) ldl.store(Bs + NCH * RS, RS, tid);
+      __syncthreads();
+      if (c + 1 < nchunk) {
+        ld.load(F2, wl, bx0, by0, bw, U, c + 1, tid);
+        if constexpr (SPLIT) ldl.load(F2l, wl, bx0, by0, bw, U, c + 1, tid);
+      }
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const int nb = nh * 32 + (lane & 31);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8_t bf = ld_frag(Bs + nb * RS + 16 * s + 8 * (lane >> 5));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bf, acc, 0, 0, 0);
+        if constexpr (SPLIT) {
+          const bf16x8_t bl = ld_frag(Bs + (NCH + nb) * RS + 16 * s + 8 * (lane >> 5));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bl, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afl[s], bf, acc, 0, 0, 0);
+        }
+      }
+      const int pos = c * NCH + nb;
+      if (pos < U) {
+        const int iy = by0 + pos / bw, ix = bx0 + pos % bw;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int p = mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const int rx = ix - geo.x0[p], ry = iy - geo.y0[p];
+          if ((unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E)
+            win[p * NP + ry * E + rx] = acc[r] * isc;
+        }
+      }
+      __syncthreads();
+    }
+    // bilinear taps from the windows (x-offset-major tap order)
+    for (int e = tid; e < TP * DD; e += NT) {
+      const int p = e / DD, tt = e % DD;
+      const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
+      if (py >= H || px >= W) continue;
+      const int ix = tt / D, iy = tt % D;
+      const float* w0 = &win[p * NP + iy * E + ix];
+      const float ax = geo.ax[p], ay = geo.ay[p];
+      const float v = (1.f - ay) * ((1.f - ax) * w0[0] + ax * w0[1]) +
+                      ay * ((1.f - ax) * w0[E] + ax * w0[E + 1]);
+      St<TO>::put(out, ((int64_t)b * HW + py * W + px) * ostride + l * DD + tt, v);
     }
     __syncthreads();
-    for (int t = lane; t < D * D; t += 64) {
-      const int ix = t / D, iy = t % D;
-      const float* d0 = &dots[wv][iy * E + ix];
-      const float* d1 = d0 + E;
-      const float val = (1.f - ay) * ((1.f - ax) * d0[0] + ax * d0[1]) +
-                        ay * ((1.f - ax) * d1[0] + ax * d1[1]);
-      if (active) O[l * D * D + t] = val * inv_sqrt_c;
+  }
+  const int pad = ostride - levels * DD;
+  if (pad > 0) {
+    for (int e = tid; e < TP * pad; e += NT) {
+      const int p = e / pad, cc = e % pad;
+      const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
+      if (py < H && px < W)
+        St<TO>::put(out, ((int64_t)b * HW + py * W + px) * ostride + levels * DD + cc, 0.f);
     }
-    __syncthreads();
   }
 }
 
-template <int R, int CPL>
-__global__ __launch_bounds__(256) void corr_otf_bwd_kernel(const float* __restrict__ f1, F2Lvls f2,
-                                                           const float* __restrict__ coords,
-                                                           const float* __restrict__ dout,
-                                                           float* __restrict__ df1, G2Lvls df2,
-                                                           int B, int H, int W, int levels,
-                                                           float inv_sqrt_c) {
-  constexpr int D = 2 * R + 1;
-  constexpr int E = D + 1;
-  constexpr int NP = E * E;
-  constexpr int C = CPL * 64;
-  __shared__ float gpos[4][128];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int N = H * W;
-  const int64_t pix = (int64_t)blockIdx.x * 4 + wv;
-  const bool active = pix < (int64_t)B * N;
-  const int b = active ? (int)(pix / N) : 0;
-  const int i = active ? (int)(pix % N) : 0;
+template <int R, int C, typename TD>
+__global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
+    const uint16_t* __restrict__ f1, OtfLvls lv, const float* __restrict__ coords,
+    const TD* __restrict__ dout, int dstride, float* __restrict__ df1, int B, int H, int W,
+    int levels, int tiles_x, int tiles_y, float isc) {
+  constexpr int D = 2 * R + 1, E = D + 1, NP = E * E, DD = D * D;
+  constexpr int RS = C + 16;       // [row][channel] bf16 rows (fmap1 tile, fmap2 chunk)
+  constexpr int SS = NCH + 16;     // dS [pixel][position] bf16 rows
+  constexpr int WC = C / 4;        // channels per wave
+  constexpr int TN = WC / 32;      // 32-column MFMA blocks per wave
+  __shared__ __attribute__((aligned(16))) uint16_t F1s[TP * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[NCH * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t dS[TP * SS];
+  __shared__ float dwin[TP * NP];
+  __shared__ Geo geo;
 
-  float a[CPL], ga[CPL];
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    a[c] = active ? f1[((int64_t)b * N + i) * C + lane * CPL + c] : 0.f;
-    ga[c] = 0.f;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int t = blockIdx.x;
+  const int tx = t % tiles_x;
+  t /= tiles_x;
+  const int ty = t % tiles_y;
+  const int b = t / tiles_y;
+  const int HW = H * W;
+
+  // fmap1 tile -> LDS [pixel][channel]
+  for (int e = tid; e < TP * (C / 8); e += NT) {
+    const int p = e / (C / 8), q = e % (C / 8);
+    const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (py < H && px < W)
+      v = *reinterpret_cast<const uint4*>(f1 + ((int64_t)b * HW + py * W + px) * C + q * 8);
+    *reinterpret_cast<uint4*>(F1s + p * RS + q * 8) = v;
   }
-  const float x = active ? coords[((int64_t)b * 2) * N + i] : 0.f;
-  const float y = active ? coords[((int64_t)b * 2 + 1) * N + i] : 0.f;
-  const int ctot = levels * D * D;
-  const float* dO = dout + pix * ctot;
+  float cxv = 0.f, cyv = 0.f;
+  bool cact = false;
+  if (wave == 0) {
+    const int py = ty * TPX + lane / TPX, px = tx * TPX + lane % TPX;
+    cact = py < H && px < W;
+    if (cact) {
+      cxv = coords[((int64_t)b * 2) * HW + py * W + px];
+      cyv = coords[((int64_t)b * 2 + 1) * HW + py * W + px];
+    }
+  }
 
+  f32x16 g1[2][TN];  // dF1: 64 pixels x this wave's WC channels
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) g1[i][j][r] = 0.f;
+
+  ChunkLoader<C> ld;
   for (int l = 0; l < levels; ++l) {
-    const float inv = 1.f / (float)(1 << l);
-    const float cx = clampc(x * inv), cy = clampc(y * inv);
-    const float fx = floorf(cx), fy = floorf(cy);
-    const float ax = cx - fx, ay = cy - fy;
-    const int xs = (int)fx - R, ys = (int)fy - R;
-    const int hl = f2.h[l], wl = f2.w[l];
-    // adjoint of the bilinear blend: position (px_i, py_i) collects from up to 4 taps
-    for (int p = lane; p < 128; p += 64) {
+    const int hl = lv.h[l], wl = lv.w[l];
+    if (wave == 0) tile_geometry<R>(geo, lane, cact, cxv, cyv, l, hl, wl);
+    __syncthreads();
+    // adjoint of the bilinear blend: window position (qx, qy) collects from up to 4 taps
+    for (int e = tid; e < TP * NP; e += NT) {
+      const int p = e / NP, qq = e % NP;
+      const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
       float g = 0.f;
-      if (p < NP && active) {
-        const int qx = p % E, qy = p / E;
+      if (py < H && px < W) {
+        const int qx = qq % E, qy = qq / E;
+        const float ax = geo.ax[p], ay = geo.ay[p];
+        const TD* dO = dout + ((int64_t)b * HW + py * W + px) * dstride + l * DD;
 #pragma unroll
         for (int dyi = 0; dyi < 2; ++dyi)
 #pragma unroll
           for (int dxi = 0; dxi < 2; ++dxi) {
             const int ix = qx - dxi, iy = qy - dyi;
-            if (ix >= 0 && ix < D && iy >= 0 && iy < D) {
-              const float wx = dxi ? ax : 1.f - ax;
-              const float wy = dyi ? ay : 1.f - ay;
-              g += wx * wy * dO[l * D * D + ix * D + iy];
-            }
+            if (ix >= 0 && ix < D && iy >= 0 && iy < D)
+              g += (dxi ? ax : 1.f - ax) * (dyi ? ay : 1.f - ay) * Ld<TD>::get(dO, ix * D + iy);
           }
       }
-      gpos[wv][p] = g * inv_sqrt_c;
+      dwin[e] = g * isc;
     }
     __syncthreads();
-    const float* F2 = f2.lvl[l] + (int64_t)b * hl * wl * C;
-    float* G2 = df2.lvl[l] + (int64_t)b * hl * wl * C;
-    for (int p = 0; p < NP; ++p) {
-      const float g = gpos[wv][p];
-      const int px = xs + p % E, py = ys + p / E;
-      if (g != 0.f && px >= 0 && px < wl && py >= 0 && py < hl) {
-        const int64_t off = ((int64_t)py * wl + px) * C + lane * CPL;
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-          ga[c] += g * F2[off + c];
-          atomicAdd(&G2[off + c], g * a[c]);
+    const int bx0 = geo.box[0], by0 = geo.box[1], bw = geo.box[2], bh = geo.box[3];
+    const int U = bw * bh;
+    const int nchunk = (U + NCH - 1) / NCH;
+    const uint16_t* F2 = lv.f2[l] + (int64_t)b * hl * wl * C;
+    float* G2 = lv.g2[l] + (int64_t)b * hl * wl * C;
+    if (nchunk > 0) ld.load(F2, wl, bx0, by0, bw, U, 0, tid);
+    for (int c = 0; c < nchunk; ++c) {
+      ld.store(Bs, RS, tid);
+      // dS chunk from the windows
+      for (int e = tid; e < TP * NCH; e += NT) {
+        const int p = e / NCH, n = e % NCH;
+        const int pos = c * NCH + n;
+        float v = 0.f;
+        if (pos < U) {
+          const int iy = by0 + pos / bw, ix = bx0 + pos % bw;
+          const int rx = ix - geo.x0[p], ry = iy - geo.y0[p];
+          if ((unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E)
+            v = dwin[p * NP + ry * E + rx];
         }
+        dS[p * SS + n] = raft_f32_to_bf16(v);
       }
-    }
-    __syncthreads();
-  }
-  if (active) {
+      __syncthreads();
+      if (c + 1 < nchunk) ld.load(F2, wl, bx0, by0, bw, U, c + 1, tid);
+
+      // dF1 (64 px x WC) += dS (64 px x 64 pos) * F2 chunk (64 pos x WC)
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) df1[((int64_t)b * N + i) * C + lane * CPL + c] += ga[c];
+      for (int ks = 0; ks < NCH / 16; ++ks) {
+        bf16x8_t a[2], bb[TN];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          a[i] = ld_frag(dS + (i * 32 + (lane & 31)) * SS + 16 * ks + 8 * (lane >> 5));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bb[j] = tr_frag(Bs, RS, 16 * ks, wave * WC + j * 32, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            g1[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bb[j], g1[i][j], 0, 0, 0);
+      }
+      // dF2 chunk (64 pos x WC) = dS^T (64 pos x 64 px) * F1 tile (64 px x WC)
+      f32x16 g2[2][TN];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) g2[i][j][r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < TP / 16; ++ks) {
+        bf16x8_t a[2], bb[TN];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = tr_frag(dS, SS, 16 * ks, i * 32, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bb[j] = tr_frag(F1s, RS, 16 * ks, wave * WC + j * 32, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            g2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bb[j], g2[i][j], 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int pos = c * NCH + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (pos >= U) continue;
+          const int iy = by0 + pos / bw, ix = bx0 + pos % bw;
+          float* dst = G2 + ((int64_t)iy * wl + ix) * C + wave * WC + (lane & 31);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) atomicAdd(dst + j * 32, g2[i][j][r]);
+        }
+      __syncthreads();
+    }
+    __syncthreads();  // every wave has read this level's box before wave 0 rewrites `geo`
   }
+  // dF1: the tile owns its pixels (launches on one stream are ordered) -> plain read-modify-write
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int p = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
+      if (py >= H || px >= W) continue;
+      float* dst = df1 + ((int64_t)b * HW + py * W + px) * C + wave * WC + (lane & 31);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) dst[j * 32] += g1[i][j][r];
+    }
 }
 
-template <typename P, typename T>
-P make_lvls(T* const* lvl, const int* hs, const int* ws, int levels) {
-  P p;
+OtfLvls make_lvls(const uint16_t* const* f2, float* const* g2, const int* hs, const int* ws,
+                  int levels) {
+  OtfLvls p;
   for (int l = 0; l < 4; ++l) {
-    p.lvl[l] = l < levels ? lvl[l] : nullptr;
+    p.f2[l] = l < levels ? f2[l] : nullptr;
+    p.g2[l] = (g2 && l < levels) ? g2[l] : nullptr;
     p.h[l] = l < levels ? hs[l] : 0;
     p.w[l] = l < levels ? ws[l] : 0;
   }
@@ -204,31 +447,55 @@ P make_lvls(T* const* lvl, const int* hs, const int* ws, int levels) {
 
 }  // namespace
 
-#define OTF_DISPATCH(KERNEL, ...)                                                             \
-  do {                                                                                        \
-    if (radius == 4 && C == 256) { hipLaunchKernelGGL((KERNEL<4, 4>), __VA_ARGS__); return true; } \
-    if (radius == 3 && C == 128) { hipLaunchKernelGGL((KERNEL<3, 2>), __VA_ARGS__); return true; } \
-    if (radius == 4 && C == 128) { hipLaunchKernelGGL((KERNEL<4, 2>), __VA_ARGS__); return true; } \
-    if (radius == 3 && C == 256) { hipLaunchKernelGGL((KERNEL<3, 4>), __VA_ARGS__); return true; } \
-    return false;                                                                             \
+#define OTF_CASES(LAUNCH)                                        \
+  do {                                                           \
+    if (radius == 4 && C == 256) { LAUNCH(4, 256); return true; } \
+    if (radius == 3 && C == 128) { LAUNCH(3, 128); return true; } \
+    if (radius == 4 && C == 128) { LAUNCH(4, 128); return true; } \
+    if (radius == 3 && C == 256) { LAUNCH(3, 256); return true; } \
+    return false;                                                \
   } while (0)
 
-bool launch_corr_otf_fwd(const float* f1, const float* const* f2lvl, const int* hs, const int* ws,
-                         int levels, const float* coords, float* out, int B, int C, int H, int W,
-                         int radius, hipStream_t stream) {
-  F2Lvls p = make_lvls<F2Lvls>(f2lvl, hs, ws, levels);
-  dim3 grid(raft_cdiv((int64_t)B * H * W, 4));
+bool launch_corr_otf_fwd(const uint16_t* f1, const uint16_t* const* f2lvl, const uint16_t* f1lo,
+                         const uint16_t* const* f2lo, const int* hs, const int* ws, int levels,
+                         const float* coords, void* out, int out_bf16, int ostride, int B, int C,
+                         int H, int W, int radius, hipStream_t stream) {
+  const OtfLvls p = make_lvls(f2lvl, nullptr, hs, ws, levels);
+  const OtfLvls q = make_lvls(f2lo ? f2lo : f2lvl, nullptr, hs, ws, levels);
+  const bool split = f1lo != nullptr && f2lo != nullptr;
+  const int tx = (W + TPX - 1) / TPX, ty = (H + TPX - 1) / TPX;
+  const dim3 grid((unsigned)(B * tx * ty));
   const float isc = 1.f / sqrtf((float)C);
-  OTF_DISPATCH(corr_otf_fwd_kernel, grid, dim3(256), 0, stream, f1, p, coords, out, B, H, W, levels, isc);
+#define FWD(RR, CC, TO, SP)                                                                     \
+  hipLaunchKernelGGL((corr_otf_fwd_kernel<RR, CC, TO, SP>), grid, dim3(NT), 0, stream, f1, f1lo, \
+                     p, q, coords, (TO*)out, ostride, B, H, W, levels, tx, ty, isc)
+#define FWD_BF16(RR, CC) FWD(RR, CC, uint16_t, false)
+#define FWD_F32(RR, CC) FWD(RR, CC, float, false)
+#define FWD_BF16_SPLIT(RR, CC) FWD(RR, CC, uint16_t, true)
+#define FWD_F32_SPLIT(RR, CC) FWD(RR, CC, float, true)
+  if (split) {
+    if (out_bf16) OTF_CASES(FWD_BF16_SPLIT);
+    OTF_CASES(FWD_F32_SPLIT);
+  }
+  if (out_bf16) OTF_CASES(FWD_BF16);
+  OTF_CASES(FWD_F32);
+#undef FWD
 }
 
-bool launch_corr_otf_bwd(const float* f1, const float* const* f2lvl, const int* hs, const int* ws,
-                         int levels, const float* coords, const float* dout, float* df1,
-                         float* const* df2lvl, int B, int C, int H, int W, int radius,
-                         hipStream_t stream) {
-  F2Lvls p = make_lvls<F2Lvls>(f2lvl, hs, ws, levels);
-  G2Lvls g = make_lvls<G2Lvls>(df2lvl, hs, ws, levels);
-  dim3 grid(raft_cdiv((int64_t)B * H * W, 4));
+bool launch_corr_otf_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const int* hs,
+                         const int* ws, int levels, const float* coords, const void* dout,
+                         int dout_bf16, int dstride, float* df1, float* const* df2lvl, int B,
+                         int C, int H, int W, int radius, hipStream_t stream) {
+  const OtfLvls p = make_lvls(f2lvl, df2lvl, hs, ws, levels);
+  const int tx = (W + TPX - 1) / TPX, ty = (H + TPX - 1) / TPX;
+  const dim3 grid((unsigned)(B * tx * ty));
   const float isc = 1.f / sqrtf((float)C);
-  OTF_DISPATCH(corr_otf_bwd_kernel, grid, dim3(256), 0, stream, f1, p, coords, dout, df1, g, B, H, W, levels, isc);
+#define BWD(RR, CC, TD)                                                                         \
+  hipLaunchKernelGGL((corr_otf_bwd_kernel<RR, CC, TD>), grid, dim3(NT), 0, stream, f1, p, coords, \
+                     (const TD*)dout, dstride, df1, B, H, W, levels, tx, ty, isc)
+#define BWD_BF16(RR, CC) BWD(RR, CC, uint16_t)
+#define BWD_F32(RR, CC) BWD(RR, CC, float)
+  if (dout_bf16) OTF_CASES(BWD_BF16);
+  OTF_CASES(BWD_F32);
+#undef BWD
 }

@@ -26,14 +26,16 @@ bool launch_corr_lookup_bwd(float* const* glvl, const int* hs, const int* ws, in
                             const float* coords, const float* dout, int64_t bs, int64_t ps,
                             int64_t cs, int B, int H, int W, int radius, hipStream_t stream);
 
-// ---- on-the-fly correlation (corr_onthefly.hip)
-bool launch_corr_otf_fwd(const float* f1, const float* const* f2lvl, const int* hs, const int* ws,
-                         int levels, const float* coords, float* out, int B, int C, int H, int W,
-                         int radius, hipStream_t stream);
-bool launch_corr_otf_bwd(const float* f1, const float* const* f2lvl, const int* hs, const int* ws,
-                         int levels, const float* coords, const float* dout, float* df1,
-                         float* const* df2lvl, int B, int C, int H, int W, int radius,
-                         hipStream_t stream);
+// ---- on-the-fly correlation (corr_onthefly.hip); fmaps are NHWC bf16, out / dout (B,H,W,stride)
+// f1lo / f2lo (nullable): bf16 low parts -> fp32-accurate split-bf16 forward
+bool launch_corr_otf_fwd(const uint16_t* f1, const uint16_t* const* f2lvl, const uint16_t* f1lo,
+                         const uint16_t* const* f2lo, const int* hs, const int* ws, int levels,
+                         const float* coords, void* out, int out_bf16, int ostride, int B, int C,
+                         int H, int W, int radius, hipStream_t stream);
+bool launch_corr_otf_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const int* hs,
+                         const int* ws, int levels, const float* coords, const void* dout,
+                         int dout_bf16, int dstride, float* df1, float* const* df2lvl, int B,
+                         int C, int H, int W, int radius, hipStream_t stream);
 
 // ---- convex upsample (upsample.hip)
 // mask element (b, ch, y, x) at b*mbs + ch*mcs + (y*W+x)*mps  (NCHW: mcs=HW, mps=1; NHWC: mcs=1, mps=576)

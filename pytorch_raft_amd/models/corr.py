@@ -117,7 +117,7 @@ def _use_hip(t, impl):
 class CorrBlock:
     """All-pairs correlation pyramid with a (2r+1)^2 window lookup per level."""
 
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, impl='auto'):
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, impl='auto', precision='fp32'):
         self.num_levels = num_levels
         self.radius = radius
         self.hip = _use_hip(fmap1, impl)
@@ -153,7 +153,7 @@ def _to_nhwc_padded(corr, cbuf):
 class AlternateCorrBlock:
     """On-the-fly correlation: O(HW * r^2) memory instead of O((HW)^2); differentiable."""
 
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, impl='auto'):
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, impl='auto', precision='fp32'):
         self.num_levels = num_levels
         self.radius = radius
         self.hip = _use_hip(fmap1, impl)
@@ -164,7 +164,7 @@ class AlternateCorrBlock:
             pyr.append(F.avg_pool2d(pyr[-1], 2, stride=2))
         self.pyramid2 = pyr
         if self.hip:
-            self.volume = corr_ops.OnTheFlyVolume(self.fmap1, self.pyramid2)
+            self.volume = corr_ops.OnTheFlyVolume(self.fmap1, self.pyramid2, precision)
 
     def __call__(self, coords):
         if self.hip:
@@ -172,4 +172,7 @@ class AlternateCorrBlock:
         return torch_onthefly_corr(self.pyramid2, self.fmap1, coords, self.radius)
 
     def lookup_nhwc(self, coords, cbuf):
+        """bf16 (B,H,W,cbuf) zero-padded taps for the fused HIP update block."""
+        if self.hip:
+            return self.volume.lookup_nhwc(coords, self.radius, cbuf)
         return _to_nhwc_padded(self(coords), cbuf)

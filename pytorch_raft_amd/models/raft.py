@@ -108,8 +108,13 @@ class RAFT(nn.Module):
             fmap1, fmap2 = self.fnet([image1, image2])
         fmap1 = fmap1.float().contiguous()
         fmap2 = fmap2.float().contiguous()
-        block = AlternateCorrBlock if self.args.alternate_corr else CorrBlock
-        corr_fn = block(fmap1, fmap2, radius=self.args.corr_radius, impl=self.corr_impl)
+        if self.args.alternate_corr:
+            # mixed precision: bf16 MFMA operands; fp32 model: split-bf16 (fp32-accurate) forward
+            corr_fn = AlternateCorrBlock(fmap1, fmap2, radius=self.args.corr_radius,
+                                         impl=self.corr_impl,
+                                         precision='bf16' if self.args.mixed_precision else 'fp32')
+        else:
+            corr_fn = CorrBlock(fmap1, fmap2, radius=self.args.corr_radius, impl=self.corr_impl)
 
         with self._autocast(dev):
             cnet = self.cnet(image1)

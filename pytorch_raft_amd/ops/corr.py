@@ -12,7 +12,8 @@ Design (MI355X-first, see `SURVEY.md` §7.4 item 3):
   d(fmap2).  The reference instead allocates + zero-fills a dense plane-sized gradient per level per
   iteration inside grid_sample backward and lets autograd add them up.
 * ``OnTheFlyVolume`` is the differentiable counterpart of the reference's forward-only
-  ``alt_cuda_corr`` (csrc/kernels/corr_onthefly.hip) with the same token scheme for d(fmap2 levels).
+  ``alt_cuda_corr`` (csrc/kernels/corr_onthefly.hip: 8x8 query tiles, MFMA tile-GEMM against the
+  tile's fmap2 bounding box) with the same token scheme for d(fmap1), d(fmap2 levels).
 """
 import math
 
@@ -157,14 +158,22 @@ def _pool_nhwc(x):
 
 
 class _OTFBuild(torch.autograd.Function):
-    """fmap1 (B,C,H,W), pyramid of fmap2 (list) -> token; keeps NHWC copies in ``state``."""
+    """fmap1 (B,C,H,W), pyramid of fmap2 (list) -> token; keeps NHWC bf16 MFMA operands in
+    ``state`` (converted once per step, not per lookup as `core/corr.py:82-83` does)."""
 
     @staticmethod
     def forward(ctx, fmap1, *args):
         state = args[-1]
         f2_levels = args[:-1]
-        state.f1 = fmap1.permute(0, 2, 3, 1).contiguous()
-        state.f2 = [f.permute(0, 2, 3, 1).contiguous() for f in f2_levels]
+        f1 = fmap1.permute(0, 2, 3, 1)
+        f2 = [f.permute(0, 2, 3, 1) for f in f2_levels]
+        state.f1 = f1.to(torch.bfloat16).contiguous()
+        state.f2 = [f.to(torch.bfloat16).contiguous() for f in f2]
+        state.lo = []
+        if state.precision == 'fp32':
+            # x = hi + lo with both parts bf16: the kernel's 3-MFMA split product is fp32-accurate
+            state.lo = [(f1 - state.f1.float()).to(torch.bfloat16).contiguous()]
+            state.lo += [(f - h.float()).to(torch.bfloat16).contiguous() for f, h in zip(f2, state.f2)]
         ctx.state = state
         ctx.nlev = len(f2_levels)
         return fmap1.new_zeros(())
@@ -177,13 +186,26 @@ class _OTFBuild(torch.autograd.Function):
         g1 = st.grad_f1.permute(0, 3, 1, 2)
         g2 = [g.permute(0, 3, 1, 2) for g in st.grad]
         st.grad = st.grad_f1 = None
+        st.f1 = st.f2 = st.lo = None
         return (g1, *g2, None)
+
+
+def _otf_backward(st, coords, dout, radius):
+    if st.grad is None:
+        st.grad = [torch.zeros(f.shape, device=f.device, dtype=torch.float32) for f in st.f2]
+        st.grad_f1 = torch.zeros(st.f1.shape, device=st.f1.device, dtype=torch.float32)
+    if dout.dtype not in (torch.float32, torch.bfloat16):
+        dout = dout.float()
+    _ext.ops().corr_otf_bwd_(st.f1, st.f2, coords, dout.contiguous(), st.grad_f1, st.grad, radius)
 
 
 class _OTFLookup(torch.autograd.Function):
     @staticmethod
     def forward(ctx, token, coords, radius, state):
-        out = _ext.ops().corr_otf_fwd(state.f1, state.f2, coords, radius)  # (B,H,W,L*D*D)
+        b, _, h, w = coords.shape
+        nc = len(state.f2) * (2 * radius + 1) ** 2
+        out = torch.empty(b, h, w, nc, device=coords.device, dtype=torch.float32)
+        _ext.ops().corr_otf_fwd_(state.f1, state.f2, coords, radius, out, state.lo)
         ctx.state = state
         ctx.radius = radius
         ctx.save_for_backward(coords)
@@ -191,20 +213,44 @@ class _OTFLookup(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        st = ctx.state
         (coords,) = ctx.saved_tensors
-        if st.grad is None:
-            st.grad = [torch.zeros_like(f) for f in st.f2]
-            st.grad_f1 = torch.zeros_like(st.f1)
-        d = dout.float().permute(0, 2, 3, 1).contiguous()
-        _ext.ops().corr_otf_bwd_(st.f1, st.f2, coords, d, st.grad_f1, st.grad, ctx.radius)
+        _otf_backward(ctx.state, coords, dout.float().permute(0, 2, 3, 1), ctx.radius)
         return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None
 
 
+class _OTFLookupNHWC(torch.autograd.Function):
+    """bf16 taps straight into the zero-padded (B,H,W,cbuf) input of the fused update block."""
+
+    @staticmethod
+    def forward(ctx, token, coords, radius, state, cbuf):
+        b, _, h, w = coords.shape
+        out = torch.empty(b, h, w, cbuf, device=coords.device, dtype=torch.bfloat16)
+        _ext.ops().corr_otf_fwd_(state.f1, state.f2, coords, radius, out, state.lo)
+        ctx.state = state
+        ctx.radius = radius
+        ctx.save_for_backward(coords)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (coords,) = ctx.saved_tensors
+        _otf_backward(ctx.state, coords, dout, ctx.radius)
+        return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None, None
+
+
 class OnTheFlyVolume:
-    def __init__(self, fmap1, fmap2_pyramid):
+    """precision: 'bf16' (MFMA operands bf16, fp32 accumulation) or 'fp32' (split-bf16 forward,
+    ~2^-16 relative error; the backward always uses bf16 operands with fp32 accumulation)."""
+
+    def __init__(self, fmap1, fmap2_pyramid, precision='fp32'):
+        assert precision in ('bf16', 'fp32'), precision
         self.state = _State()
+        self.state.precision = precision
         self.token = _OTFBuild.apply(fmap1.contiguous(), *fmap2_pyramid, self.state)
 
     def lookup(self, coords, radius):
         return _OTFLookup.apply(self.token, coords.contiguous().float(), radius, self.state)
+
+    def lookup_nhwc(self, coords, radius, cbuf):
+        return _OTFLookupNHWC.apply(self.token, coords.contiguous().float(), radius, self.state,
+                                    cbuf)

@@ -46,10 +46,6 @@ def _returns():
     def loss_bwd(preds, gt, valid, dl, g, m):
         return [torch.zeros_like(p) for p in preds]
 
-    def otf(f1, f2, coords, r):
-        b, h, w, c = f1.shape
-        return torch.zeros(b, h, w, len(f2) * (2 * r + 1) ** 2)
-
     def win_grad(coords, dout, levels, r):
         b, _, h, w = coords.shape
         return torch.zeros(b, h * w, levels, 2 * r + 2, 2 * r + 2)
@@ -60,7 +56,7 @@ def _returns():
     return {'corr_build': corr_build, 'corr_lookup_fwd': lookup, 'corr_pyr_grad_reduce': reduce,
             'corr_window_grad': win_grad, 'corr_window_reduce': win_reduce,
             'convex_up_fwd': cup_fwd, 'convex_up_bwd': cup_bwd, 'seq_loss_fwd': loss_fwd,
-            'seq_loss_bwd': loss_bwd, 'corr_otf_fwd': otf}
+            'seq_loss_bwd': loss_bwd}
 
 
 @pytest.mark.parametrize('alternate', [False, True])
@@ -82,6 +78,8 @@ def test_dry_run_fused_training_step(alternate):
             'flow_prep_', 'convex_up_fwd', 'convex_up_bwd', 'seq_loss_fwd'} <= names, names
     if not alternate:
         assert {'corr_build', 'corr_lookup_nhwc_', 'corr_window_grad', 'corr_window_reduce'} <= names
+    else:
+        assert {'corr_otf_fwd_', 'corr_otf_bwd_'} <= names
     # every update-block parameter received a gradient through the fused backward
     for n, p in m.named_parameters():
         if n.startswith('update_block'):

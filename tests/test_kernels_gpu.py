@@ -70,26 +70,63 @@ def test_lookup_fwd_bwd_matches_grid_sample(ext_ops, radius, c, hw):
     torch.testing.assert_close(f2.grad, g2_ref, atol=2e-3, rtol=1e-3)
 
 
+def _rel(a, b):
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
 @pytest.mark.parametrize('radius,c', [(4, 256), (3, 128)])
-def test_onthefly_matches_allpairs(ext_ops, radius, c):
-    b, h, w = 2, 16, 24
+@pytest.mark.parametrize('hw,spread', [((16, 24), 6.0), ((13, 19), 2.0), ((46, 62), 3.0)])
+def test_onthefly_matches_allpairs(ext_ops, radius, c, hw, spread, precision):
+    """MFMA on-the-fly lookup (split-bf16 or bf16 operands, fp32 accumulation) vs the fp32
+    grid_sample oracle; the backward always runs bf16 operands."""
+    h, w = hw
+    b = 2
     f1 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
     f2 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
-    coords = _coords(b, h, w, seed=3)
-    pyr = torch_corr_pyramid(f1, f2, 4)
-    ref = torch_corr_lookup(pyr, coords, radius)
-    gout = torch.randn_like(ref)
-    (ref * gout).sum().backward()
+    coords = _coords(b, h, w, spread=spread, seed=3)
+    levels = 4 if min(h, w) >= 16 else 3
+    pyr = torch_corr_pyramid(f1, f2, levels)
+    refs = [torch_corr_lookup(pyr, coords, radius), torch_corr_lookup(pyr, coords + 1.3, radius)]
+    gouts = [torch.randn_like(r) for r in refs]
+    sum((r * g).sum() for r, g in zip(refs, gouts)).backward()
     g1_ref, g2_ref = f1.grad.clone(), f2.grad.clone()
     f1.grad = f2.grad = None
 
-    blk = AlternateCorrBlock(f1, f2, num_levels=4, radius=radius, impl='hip')
+    blk = AlternateCorrBlock(f1, f2, num_levels=levels, radius=radius, impl='hip',
+                             precision=precision)
     assert blk.hip
-    out = blk(coords)
-    torch.testing.assert_close(out, ref, atol=2e-4, rtol=1e-4)
-    (out * gout).sum().backward()
-    torch.testing.assert_close(f1.grad, g1_ref, atol=2e-3, rtol=1e-3)
-    torch.testing.assert_close(f2.grad, g2_ref, atol=2e-3, rtol=1e-3)
+    outs = [blk(coords), blk(coords + 1.3)]
+    for o, r in zip(outs, refs):
+        if precision == 'fp32':
+            torch.testing.assert_close(o, r.detach(), atol=1e-3, rtol=1e-3)
+        else:
+            torch.testing.assert_close(o, r.detach(), atol=3e-2, rtol=2e-2)
+            assert _rel(o, r.detach()) < 5e-3
+    sum((o * g).sum() for o, g in zip(outs, gouts)).backward()
+    assert _rel(f1.grad, g1_ref) < 1e-2
+    assert _rel(f2.grad, g2_ref) < 1e-2
+
+
+def test_onthefly_nhwc_bf16(ext_ops):
+    b, c, h, w, radius = 2, 256, 46, 62, 4
+    f1 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    f2 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    coords = _coords(b, h, w, spread=2.0, seed=5)
+    pyr = torch_corr_pyramid(f1, f2, 4)
+    ref = torch_corr_lookup(pyr, coords, radius).permute(0, 2, 3, 1)
+    gout = torch.randn(b, h, w, 352, device=DEV)
+    (ref * gout[..., :324]).sum().backward()
+    g1_ref, g2_ref = f1.grad.clone(), f2.grad.clone()
+    f1.grad = f2.grad = None
+    blk = AlternateCorrBlock(f1, f2, num_levels=4, radius=radius, impl='hip', precision='bf16')
+    out = blk.lookup_nhwc(coords, 352)
+    assert out.shape == (b, h, w, 352) and out.dtype == torch.bfloat16
+    assert torch.all(out[..., 324:] == 0)
+    assert _rel(out[..., :324].float(), ref.detach()) < 8e-3
+    (out.float() * gout).sum().backward()
+    assert _rel(f1.grad, g1_ref) < 1e-2
+    assert _rel(f2.grad, g2_ref) < 1e-2
 
 
 @pytest.mark.parametrize('mask_dtype', [torch.float32, torch.bfloat16])

@@ -70,3 +70,18 @@ def test_native_library_loaded(ext_ops):
     assert _ext.loaded()
     maps = open('/proc/self/maps').read()
     assert os.path.basename(_ext.LIB_PATH) in maps
+
+
+def test_alternate_training_grads_match_allpairs(ext_ops):
+    """On-the-fly (MFMA, bf16 backward operands) vs all-pairs HIP path: same loss gradients."""
+    i1, i2, flow, valid = make_pair_batch(2, 128, 160, device=DEV)
+    from pytorch_raft_amd.ops.loss import sequence_loss
+    grads = {}
+    for alt in (False, True):
+        m = _model('hip', alternate=alt).train()
+        preds = m(i1, i2, iters=3)
+        loss, _ = sequence_loss(preds, flow, valid, 0.8)
+        loss.backward()
+        grads[alt] = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+    rel = (grads[True] - grads[False]).norm() / grads[False].norm()
+    assert rel < 2e-2, rel
