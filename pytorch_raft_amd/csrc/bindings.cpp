@@ -317,6 +317,43 @@ void corr_otf_bwd_(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor
               "on-the-fly corr supports radius 3/4 with C = 128/256");
 }
 
+// every iteration's gradient at once: coords[k] (B,2,H,W), wgs[k] (B,N,L,E,E) from corr_window_grad
+void corr_otf_window_bwd_(const Tensor& f1, const std::vector<Tensor>& f2,
+                          const std::vector<Tensor>& coords, const std::vector<Tensor>& wgs,
+                          const Tensor& df1, const std::vector<Tensor>& df2, int64_t radius) {
+  TORCH_CHECK(!coords.empty() && coords.size() == wgs.size() && coords.size() <= RAFT_MAX_WIN,
+              "1..", RAFT_MAX_WIN, " iterations");
+  otf_common_checks(f1, coords[0], radius);
+  const int64_t B = f1.size(0), H = f1.size(1), W = f1.size(2), C = f1.size(3);
+  const int64_t levels = (int64_t)f2.size(), E = 2 * radius + 2;
+  check_cuda_f32(df1, "grad_fmap1");
+  TORCH_CHECK(df1.sizes() == f1.sizes(), "grad_fmap1 must be (B,H,W,C)");
+  TORCH_CHECK(f2.size() == df2.size(), "level count mismatch");
+  WinList wl{};
+  for (size_t k = 0; k < coords.size(); ++k) {
+    check_cuda_f32(coords[k], "coords");
+    check_cuda_f32(wgs[k], "window grad");
+    TORCH_CHECK(coords[k].sizes() == coords[0].sizes(), "coords shape");
+    TORCH_CHECK(wgs[k].numel() == B * H * W * levels * E * E, "window grad shape");
+    wl.coords[k] = coords[k].data_ptr<float>();
+    wl.wg[k] = wgs[k].data_ptr<float>();
+  }
+  wl.n = (int)coords.size();
+  c10::DeviceGuard g(f1.device());
+  Bf16Levels L = otf_levels(f2, B, C, H, W);
+  std::vector<float*> gp;
+  for (size_t l = 0; l < df2.size(); ++l) {
+    check_cuda_f32(df2[l], "grad fmap2 level");
+    TORCH_CHECK(df2[l].sizes() == f2[l].sizes(), "grad fmap2 level shape mismatch");
+    gp.push_back(df2[l].data_ptr<float>());
+  }
+  TORCH_CHECK(launch_corr_otf_window_bwd(reinterpret_cast<const uint16_t*>(f1.data_ptr()),
+                                         L.ptr.data(), L.h.data(), L.w.data(), (int)levels, wl,
+                                         df1.data_ptr<float>(), gp.data(), (int)B, (int)C, (int)H,
+                                         (int)W, (int)radius, cur_stream()),
+              "on-the-fly corr supports radius 3/4 with C = 128/256");
+}
+
 // ------------------------------------------------------------------ convex upsample
 int mask_kind(const Tensor& m) {
   TORCH_CHECK(m.scalar_type() == at::kFloat || m.scalar_type() == at::kBFloat16,
@@ -761,6 +798,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_pyr_grad_reduce(Tensor[] gpyr, float inv_sqrt_c) -> Tensor");
   m.def("corr_otf_fwd_(Tensor f1, Tensor[] f2, Tensor coords, int radius, Tensor(a!) out, Tensor[] lo) -> ()");
   m.def("corr_otf_bwd_(Tensor f1, Tensor[] f2, Tensor coords, Tensor dout, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
+  m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] wgs, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");
   m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout, bool nhwc=False) -> Tensor[]");
   m.def("corr_lookup_nhwc_(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
@@ -786,6 +824,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("corr_pyr_grad_reduce", &corr_pyr_grad_reduce);
   m.impl("corr_otf_fwd_", &corr_otf_fwd_);
   m.impl("corr_otf_bwd_", &corr_otf_bwd_);
+  m.impl("corr_otf_window_bwd_", &corr_otf_window_bwd_);
   m.impl("convex_up_fwd", &convex_up_fwd);
   m.impl("convex_up_bwd", &convex_up_bwd);
   m.impl("seq_loss_fwd", &seq_loss_fwd);

@@ -266,20 +266,68 @@ __global__ __launch_bounds__(NT, SPLIT ? 1 : 2) void corr_otf_fwd_kernel(
   }
 }
 
-template <int R, int C, typename TD>
+// wave 0, lane = tile pixel: window origins of every iteration in `wl` at level l + the union box
+template <int R>
+__device__ __forceinline__ void tile_geometry_multi(int (*gx)[TP], int (*gy)[TP], int* box,
+                                                    const WinList& wl, int lane, bool act,
+                                                    int64_t cidx, int HW, int l, int hl, int w_l) {
+  constexpr int E = 2 * R + 2;
+  const float inv = 1.f / (float)(1 << l);
+  int mnx = 0x7fffffff, mxx = -0x7fffffff, mny = 0x7fffffff, mxy = -0x7fffffff;
+  for (int it = 0; it < wl.n; ++it) {
+    int x0 = -(1 << 28), y0 = -(1 << 28);
+    if (act) {
+      const float cx = clampc(wl.coords[it][cidx] * inv);
+      const float cy = clampc(wl.coords[it][cidx + HW] * inv);
+      x0 = (int)floorf(cx) - R;
+      y0 = (int)floorf(cy) - R;
+      if (x0 <= w_l - 1 && x0 + E - 1 >= 0 && y0 <= hl - 1 && y0 + E - 1 >= 0) {
+        mnx = min(mnx, x0);
+        mxx = max(mxx, x0 + E - 1);
+        mny = min(mny, y0);
+        mxy = max(mxy, y0 + E - 1);
+      } else {
+        x0 = y0 = -(1 << 28);  // misses the map: contributes nothing
+      }
+    }
+    gx[it][lane] = x0;
+    gy[it][lane] = y0;
+  }
+  mnx = wave_min_i(mnx);
+  mxx = wave_max_i(mxx);
+  mny = wave_min_i(mny);
+  mxy = wave_max_i(mxy);
+  if (lane == 0) {
+    const int bx0 = max(mnx, 0), bx1 = min(mxx, w_l - 1);
+    const int by0 = max(mny, 0), by1 = min(mxy, hl - 1);
+    const bool ok = bx1 >= bx0 && by1 >= by0;
+    box[0] = bx0;
+    box[1] = by0;
+    box[2] = ok ? bx1 - bx0 + 1 : 0;
+    box[3] = ok ? by1 - by0 + 1 : 0;
+  }
+}
+
+// MULTI = false: one lookup's gradient, dout (B,H,W,dstride) -> bilinear adjoint in LDS.
+// MULTI = true : every iteration of the step at once from compact window gradients
+//                wg_it (B,N,L,E,E) (corr_window_grad_kernel), so the fmap2 box GEMMs and the
+//                dF2 atomics run once per step over the union box instead of once per iteration.
+template <int R, int C, typename TD, bool MULTI>
 __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
     const uint16_t* __restrict__ f1, OtfLvls lv, const float* __restrict__ coords,
-    const TD* __restrict__ dout, int dstride, float* __restrict__ df1, int B, int H, int W,
-    int levels, int tiles_x, int tiles_y, float isc) {
+    const TD* __restrict__ dout, int dstride, WinList wl, float* __restrict__ df1, int B, int H,
+    int W, int levels, int tiles_x, int tiles_y, float isc) {
   constexpr int D = 2 * R + 1, E = D + 1, NP = E * E, DD = D * D;
   constexpr int RS = C + 16;       // [row][channel] bf16 rows (fmap1 tile, fmap2 chunk)
   constexpr int SS = NCH + 16;     // dS [pixel][position] bf16 rows
   constexpr int WC = C / 4;        // channels per wave
   constexpr int TN = WC / 32;      // 32-column MFMA blocks per wave
+  constexpr int NIT = MULTI ? RAFT_MAX_WIN : 1;
   __shared__ __attribute__((aligned(16))) uint16_t F1s[TP * RS];
   __shared__ __attribute__((aligned(16))) uint16_t Bs[NCH * RS];
   __shared__ __attribute__((aligned(16))) uint16_t dS[TP * SS];
-  __shared__ float dwin[TP * NP];
+  __shared__ float dwin[MULTI ? 1 : TP * NP];
+  __shared__ int gx[NIT][TP], gy[NIT][TP];
   __shared__ Geo geo;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -301,12 +349,14 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
   }
   float cxv = 0.f, cyv = 0.f;
   bool cact = false;
+  int64_t cidx = 0;
   if (wave == 0) {
     const int py = ty * TPX + lane / TPX, px = tx * TPX + lane % TPX;
     cact = py < H && px < W;
-    if (cact) {
-      cxv = coords[((int64_t)b * 2) * HW + py * W + px];
-      cyv = coords[((int64_t)b * 2 + 1) * HW + py * W + px];
+    cidx = (int64_t)b * 2 * HW + (cact ? py * W + px : 0);
+    if (cact && !MULTI) {
+      cxv = coords[cidx];
+      cyv = coords[cidx + HW];
     }
   }
 
@@ -320,53 +370,74 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
 
   ChunkLoader<C> ld;
   for (int l = 0; l < levels; ++l) {
-    const int hl = lv.h[l], wl = lv.w[l];
-    if (wave == 0) tile_geometry<R>(geo, lane, cact, cxv, cyv, l, hl, wl);
-    __syncthreads();
-    // adjoint of the bilinear blend: window position (qx, qy) collects from up to 4 taps
-    for (int e = tid; e < TP * NP; e += NT) {
-      const int p = e / NP, qq = e % NP;
-      const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
-      float g = 0.f;
-      if (py < H && px < W) {
-        const int qx = qq % E, qy = qq / E;
-        const float ax = geo.ax[p], ay = geo.ay[p];
-        const TD* dO = dout + ((int64_t)b * HW + py * W + px) * dstride + l * DD;
-#pragma unroll
-        for (int dyi = 0; dyi < 2; ++dyi)
-#pragma unroll
-          for (int dxi = 0; dxi < 2; ++dxi) {
-            const int ix = qx - dxi, iy = qy - dyi;
-            if (ix >= 0 && ix < D && iy >= 0 && iy < D)
-              g += (dxi ? ax : 1.f - ax) * (dyi ? ay : 1.f - ay) * Ld<TD>::get(dO, ix * D + iy);
-          }
+    const int hl = lv.h[l], wl_ = lv.w[l];
+    if (wave == 0) {
+      if constexpr (MULTI) {
+        tile_geometry_multi<R>(gx, gy, geo.box, wl, lane, cact, cidx, HW, l, hl, wl_);
+      } else {
+        tile_geometry<R>(geo, lane, cact, cxv, cyv, l, hl, wl_);
+        gx[0][lane] = geo.x0[lane];
+        gy[0][lane] = geo.y0[lane];
       }
-      dwin[e] = g * isc;
     }
     __syncthreads();
+    if constexpr (!MULTI) {
+      // adjoint of the bilinear blend: window position (qx, qy) collects from up to 4 taps
+      for (int e = tid; e < TP * NP; e += NT) {
+        const int p = e / NP, qq = e % NP;
+        const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
+        float g = 0.f;
+        if (py < H && px < W) {
+          const int qx = qq % E, qy = qq / E;
+          const float ax = geo.ax[p], ay = geo.ay[p];
+          const TD* dO = dout + ((int64_t)b * HW + py * W + px) * dstride + l * DD;
+#pragma unroll
+          for (int dyi = 0; dyi < 2; ++dyi)
+#pragma unroll
+            for (int dxi = 0; dxi < 2; ++dxi) {
+              const int ix = qx - dxi, iy = qy - dyi;
+              if (ix >= 0 && ix < D && iy >= 0 && iy < D)
+                g += (dxi ? ax : 1.f - ax) * (dyi ? ay : 1.f - ay) * Ld<TD>::get(dO, ix * D + iy);
+            }
+        }
+        dwin[e] = g * isc;
+      }
+      __syncthreads();
+    }
     const int bx0 = geo.box[0], by0 = geo.box[1], bw = geo.box[2], bh = geo.box[3];
     const int U = bw * bh;
     const int nchunk = (U + NCH - 1) / NCH;
-    const uint16_t* F2 = lv.f2[l] + (int64_t)b * hl * wl * C;
-    float* G2 = lv.g2[l] + (int64_t)b * hl * wl * C;
-    if (nchunk > 0) ld.load(F2, wl, bx0, by0, bw, U, 0, tid);
+    const uint16_t* F2 = lv.f2[l] + (int64_t)b * hl * wl_ * C;
+    float* G2 = lv.g2[l] + (int64_t)b * hl * wl_ * C;
+    if (nchunk > 0) ld.load(F2, wl_, bx0, by0, bw, U, 0, tid);
     for (int c = 0; c < nchunk; ++c) {
       ld.store(Bs, RS, tid);
-      // dS chunk from the windows
+      // dS chunk (64 px x 64 positions)
       for (int e = tid; e < TP * NCH; e += NT) {
         const int p = e / NCH, n = e % NCH;
         const int pos = c * NCH + n;
         float v = 0.f;
         if (pos < U) {
           const int iy = by0 + pos / bw, ix = bx0 + pos % bw;
-          const int rx = ix - geo.x0[p], ry = iy - geo.y0[p];
-          if ((unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E)
-            v = dwin[p * NP + ry * E + rx];
+          if constexpr (MULTI) {
+            const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
+            const int64_t wrow = (((int64_t)b * HW + py * W + px) * levels + l) * NP;
+            for (int it = 0; it < wl.n; ++it) {  // fixed order -> deterministic
+              const int rx = ix - gx[it][p], ry = iy - gy[it][p];
+              if ((unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E)
+                v += wl.wg[it][wrow + ry * E + rx];
+            }
+            v *= isc;
+          } else {
+            const int rx = ix - gx[0][p], ry = iy - gy[0][p];
+            if ((unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E)
+              v = dwin[p * NP + ry * E + rx];
+          }
         }
         dS[p * SS + n] = raft_f32_to_bf16(v);
       }
       __syncthreads();
-      if (c + 1 < nchunk) ld.load(F2, wl, bx0, by0, bw, U, c + 1, tid);
+      if (c + 1 < nchunk) ld.load(F2, wl_, bx0, by0, bw, U, c + 1, tid);
 
       // dF1 (64 px x WC) += dS (64 px x 64 pos) * F2 chunk (64 pos x WC)
 #pragma unroll
@@ -411,13 +482,13 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
           const int pos = c * NCH + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           if (pos >= U) continue;
           const int iy = by0 + pos / bw, ix = bx0 + pos % bw;
-          float* dst = G2 + ((int64_t)iy * wl + ix) * C + wave * WC + (lane & 31);
+          float* dst = G2 + ((int64_t)iy * wl_ + ix) * C + wave * WC + (lane & 31);
 #pragma unroll
           for (int j = 0; j < TN; ++j) atomicAdd(dst + j * 32, g2[i][j][r]);
         }
       __syncthreads();
     }
-    __syncthreads();  // every wave has read this level's box before wave 0 rewrites `geo`
+    __syncthreads();  // every wave has read this level's box before wave 0 rewrites it
   }
   // dF1: the tile owns its pixels (launches on one stream are ordered) -> plain read-modify-write
 #pragma unroll
@@ -490,12 +561,30 @@ bool launch_corr_otf_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
   const int tx = (W + TPX - 1) / TPX, ty = (H + TPX - 1) / TPX;
   const dim3 grid((unsigned)(B * tx * ty));
   const float isc = 1.f / sqrtf((float)C);
-#define BWD(RR, CC, TD)                                                                         \
-  hipLaunchKernelGGL((corr_otf_bwd_kernel<RR, CC, TD>), grid, dim3(NT), 0, stream, f1, p, coords, \
-                     (const TD*)dout, dstride, df1, B, H, W, levels, tx, ty, isc)
+  WinList none;
+  none.n = 0;
+#define BWD(RR, CC, TD)                                                                        \
+  hipLaunchKernelGGL((corr_otf_bwd_kernel<RR, CC, TD, false>), grid, dim3(NT), 0, stream, f1, p, \
+                     coords, (const TD*)dout, dstride, none, df1, B, H, W, levels, tx, ty, isc)
 #define BWD_BF16(RR, CC) BWD(RR, CC, uint16_t)
 #define BWD_F32(RR, CC) BWD(RR, CC, float)
   if (dout_bf16) OTF_CASES(BWD_BF16);
   OTF_CASES(BWD_F32);
 #undef BWD
+}
+
+bool launch_corr_otf_window_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const int* hs,
+                                const int* ws, int levels, const WinList& wl, float* df1,
+                                float* const* df2lvl, int B, int C, int H, int W, int radius,
+                                hipStream_t stream) {
+  if (wl.n < 1 || wl.n > RAFT_MAX_WIN) return false;
+  const OtfLvls p = make_lvls(f2lvl, df2lvl, hs, ws, levels);
+  const int tx = (W + TPX - 1) / TPX, ty = (H + TPX - 1) / TPX;
+  const dim3 grid((unsigned)(B * tx * ty));
+  const float isc = 1.f / sqrtf((float)C);
+#define BWDW(RR, CC)                                                                           \
+  hipLaunchKernelGGL((corr_otf_bwd_kernel<RR, CC, float, true>), grid, dim3(NT), 0, stream, f1, \
+                     p, nullptr, (const float*)nullptr, 0, wl, df1, B, H, W, levels, tx, ty, isc)
+  OTF_CASES(BWDW);
+#undef BWDW
 }

@@ -37,6 +37,13 @@ bool launch_corr_otf_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
                          int dout_bf16, int dstride, float* df1, float* const* df2lvl, int B,
                          int C, int H, int W, int radius, hipStream_t stream);
 
+// all iterations of a step at once from compact window gradients (see corr_window.hip)
+struct WinList;
+bool launch_corr_otf_window_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const int* hs,
+                                const int* ws, int levels, const WinList& wl, float* df1,
+                                float* const* df2lvl, int B, int C, int H, int W, int radius,
+                                hipStream_t stream);
+
 // ---- convex upsample (upsample.hip)
 // mask element (b, ch, y, x) at b*mbs + ch*mcs + (y*W+x)*mps  (NCHW: mcs=HW, mps=1; NHWC: mcs=1, mps=576)
 bool launch_convex_up_fwd(const float* flow, const void* mask, int mask_is_bf16, int64_t mbs,

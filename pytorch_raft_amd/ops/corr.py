@@ -181,6 +181,12 @@ class _OTFBuild(torch.autograd.Function):
     @staticmethod
     def backward(ctx, _dtoken):
         st = ctx.state
+        if st.windows:
+            _otf_alloc_grads(st)
+            _ext.ops().corr_otf_window_bwd_(st.f1, st.f2, [w[0] for w in st.windows],
+                                            [w[1] for w in st.windows], st.grad_f1, st.grad,
+                                            st.radius)
+            st.windows = []
         if st.grad is None:
             return (None,) * (ctx.nlev + 2)
         g1 = st.grad_f1.permute(0, 3, 1, 2)
@@ -190,10 +196,14 @@ class _OTFBuild(torch.autograd.Function):
         return (g1, *g2, None)
 
 
-def _otf_backward(st, coords, dout, radius):
+def _otf_alloc_grads(st):
     if st.grad is None:
         st.grad = [torch.zeros(f.shape, device=f.device, dtype=torch.float32) for f in st.f2]
         st.grad_f1 = torch.zeros(st.f1.shape, device=st.f1.device, dtype=torch.float32)
+
+
+def _otf_backward(st, coords, dout, radius):
+    _otf_alloc_grads(st)
     if dout.dtype not in (torch.float32, torch.bfloat16):
         dout = dout.float()
     _ext.ops().corr_otf_bwd_(st.f1, st.f2, coords, dout.contiguous(), st.grad_f1, st.grad, radius)
@@ -233,8 +243,17 @@ class _OTFLookupNHWC(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        st = ctx.state
         (coords,) = ctx.saved_tensors
-        _otf_backward(ctx.state, coords, dout, ctx.radius)
+        if len(st.windows) < 32 and dout.shape[-1] % 8 == 0:
+            # compact per-iteration window gradient; the MFMA box GEMMs + dF2 atomics then run ONCE
+            # per step over all iterations (build node backward) instead of once per iteration
+            wg = _ext.ops().corr_window_grad(coords, dout.to(torch.bfloat16).contiguous(),
+                                             len(st.f2), ctx.radius)
+            st.windows.append((coords, wg))
+            st.radius = ctx.radius
+        else:
+            _otf_backward(st, coords, dout, ctx.radius)
         return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None, None
 
 
