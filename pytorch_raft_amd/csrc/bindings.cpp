@@ -537,7 +537,7 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
     check_nhwc(ins[s], B, H, W, "conv input", at::kBFloat16);
     TORCH_CHECK(in_off[s] >= 0 && in_off[s] + in_cnt[s] <= ins[s].size(3), "segment out of range");
     TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
-    if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 32 == 0, "segment channels must be a multiple of 32");
+    if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 64 == 0, "segment channels must be a multiple of 64");
     a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
@@ -550,7 +550,7 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   a.KH = (int)kh; a.KW = (int)kw; a.PH = (int)ph; a.PW = (int)pw;
   TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == at::kBFloat16 && wpk.dim() == 2,
               "packed weight must be a contiguous bf16 (Npad, Kpad) tensor");
-  const int64_t kneed = cin_small ? ((kh * kw * cin_small + 31) / 32) * 32 : kh * kw * cin_pad;
+  const int64_t kneed = cin_small ? ((kh * kw * cin_small + 63) / 64) * 64 : kh * kw * cin_pad;
   TORCH_CHECK(wpk.size(1) == kneed, "packed weight K mismatch: ", wpk.size(1), " vs ", kneed);
   TORCH_CHECK(wpk.size(0) >= ((cout + bn - 1) / bn) * bn, "packed weight has too few rows");
   a.wpk = reinterpret_cast<const uint16_t*>(wpk.data_ptr<at::BFloat16>());
@@ -635,17 +635,18 @@ void conv_wgrad_(const Tensor& g, int64_t g_off, const std::vector<Tensor>& ins,
   a.KH = (int)kh; a.KW = (int)kw; a.PH = (int)ph; a.PW = (int)pw;
   a.cout = (int)cout;
   check_cuda_f32(dw, "grad_weight");
-  const int64_t kpad = cin_small ? ((kh * kw * cin_small + 31) / 32) * 32 : kh * kw * cin_pad;
+  const int64_t kpad = cin_small ? ((kh * kw * cin_small + 63) / 64) * 64 : kh * kw * cin_pad;
   TORCH_CHECK(dw.dim() == 2 && dw.size(0) == cout && dw.size(1) == kpad, "grad_weight must be (cout, kpad)");
   a.dw = dw.data_ptr<float>();
   a.kpad = (int)kpad;
-  a.pix_per_split = (int)std::max<int64_t>(32, pix_per_split);
-  launch_conv_wgrad(a, cout > 64 ? 128 : 64, cin_small != 0, cur_stream());
+  a.pix_per_split = (int)std::max<int64_t>(64, (pix_per_split + 63) / 64 * 64);
+  float* dbp = nullptr;
   if (db.has_value() && db->defined()) {
     check_cuda_f32(*db, "grad_bias");
     TORCH_CHECK(db->numel() == cout, "grad_bias size");
-    launch_col_sum(a.g, a.g_stride, (int)cout, (int)(B * H * W), db->data_ptr<float>(), cur_stream());
+    dbp = db->data_ptr<float>();
   }
+  launch_conv_wgrad(a, cout > 64 ? 128 : 64, cin_small != 0, dbp, cur_stream());
 }
 
 // Input gradient of a stride-1 "same" conv = the forward kernel on flipped/transposed packed
@@ -670,7 +671,7 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     check_nhwc(ins[s], B, H, W, "dgrad input", at::kBFloat16);
     TORCH_CHECK(in_off[s] >= 0 && in_off[s] + in_cnt[s] <= ins[s].size(3), "segment out of range");
     TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
-    if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 32 == 0, "segment channels must be a multiple of 32");
+    if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 64 == 0, "segment channels must be a multiple of 64");
     a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
@@ -697,7 +698,7 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   const int bn = (cout % 128 == 0) ? 128 : 64;
   TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == at::kBFloat16 && wpk.dim() == 2,
               "packed weight must be a contiguous bf16 (Npad, Kpad) tensor");
-  const int64_t kneed = cin_small ? ((kh * kw * cin_small + 31) / 32) * 32 : kh * kw * cin_pad;
+  const int64_t kneed = cin_small ? ((kh * kw * cin_small + 63) / 64) * 64 : kh * kw * cin_pad;
   TORCH_CHECK(wpk.size(1) == kneed, "packed dgrad weight K mismatch: ", wpk.size(1), " vs ", kneed);
   TORCH_CHECK(wpk.size(0) >= ((cout + bn - 1) / bn) * bn, "packed dgrad weight has too few rows");
   a.wpk = reinterpret_cast<const uint16_t*>(wpk.data_ptr<at::BFloat16>());

@@ -8,12 +8,12 @@
 //   GEMM view  M = pixels (B*H*W), N = Cout, K = KH*KW*Cin;  A = input patch rows gathered on the
 //              fly from NHWC bf16 activations (no im2col buffer), B = weights pre-packed per step
 //              as [Npad][KH*KW][CinPad] bf16 (k contiguous).
-//   Tiling     workgroup = 4 waves (256 threads), tile BM x BN (128x128 / 128x64 / 128x32),
-//              BK = 32 (one filter tap x 32 channels), v_mfma_f32_32x32x16_bf16 with fp32
-//              accumulators; A/B staged global -> registers -> LDS with a 2-deep LDS ring (the next
-//              K-step's global loads are in flight during the current step's MFMAs); LDS rows are
-//              64 B and XOR-swizzled on the 16-B chunk index so ds_read_b128 fragment reads are
-//              bank-conflict free.
+//   Tiling     workgroup = 4 waves (256 threads), tile BM x BN (128|64 x 128|64, 128x32),
+//              BK = 64 (one filter tap x 64 channels), v_mfma_f32_32x32x16_bf16 with fp32
+//              accumulators; A/B staged global -> registers -> LDS: two register sets keep the
+//              loads of the next TWO K-steps in flight during the current step's MFMAs, two LDS
+//              buffers, one barrier per step; LDS rows are 128 B and XOR-swizzled on the 16-B
+//              chunk index so ds_read_b128 fragment reads are bank-conflict free.
 //   Inputs     "virtual concat": up to 3 NHWC channel segments from different buffers form the
 //              input channels (e.g. [h | x] for the GRU), so no torch.cat copies exist.
 //   Epilogues  fused per element: bias, scale, ReLU, bf16/fp32 store into a channel slice of a
@@ -27,15 +27,17 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cmath>
+
 namespace {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-constexpr int BK = 32;
+constexpr int BK = 64;   // K per pipeline step: one filter tap x 64 channels (128-B LDS rows)
 constexpr int NT = 256;
 
-__device__ __forceinline__ int swz(int row, int chunk) {  // 16-B chunk index within a 64-B row
-  return row * 4 + (chunk ^ ((row >> 2) & 3));
-}
+// 16-B chunk `chunk` (0..7) of LDS row `row` (128 B): XOR swizzle on the row's low 3 bits so the 8
+// lanes of a ds_read_b128 phase (8 consecutive rows, same logical chunk) hit 8 distinct bank groups
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + __expf(-v)); }
 __device__ __forceinline__ float tanhf_(float v) {
@@ -44,14 +46,17 @@ __device__ __forceinline__ float tanhf_(float v) {
   return copysignf(t, v);
 }
 
+// Pipeline (per 64-deep K step, one barrier):  global loads for step t+2 are issued into one of
+// two register sets before the MFMAs of step t (two steps = ~1000+ MFMA cycles of latency cover),
+// the other set (step t+1, loaded one step earlier) is written to the idle LDS buffer after them.
 template <int BM, int BN, int WM, int WN, int EPI, bool SMALLC>
-__global__ __launch_bounds__(NT) void conv_fwd_kernel(ConvFwdArgs a) {
+__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int WAVES_N = BN / WN;
   static_assert((BM / WM) * WAVES_N == 4, "4 waves per workgroup");
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int A_CHUNKS = BM * 4;  // 16-B chunks per A stage
-  constexpr int B_CHUNKS = BN * 4;
-  constexpr int A_PER = (A_CHUNKS + NT - 1) / NT;
+  constexpr int A_CHUNKS = BM * 8;  // 16-B chunks per A stage
+  constexpr int B_CHUNKS = BN * 8;
+  constexpr int A_PER = A_CHUNKS / NT;
   constexpr int B_PER = (B_CHUNKS + NT - 1) / NT;
 
   __shared__ __attribute__((aligned(16))) uint4 As[2][A_CHUNKS];
@@ -63,14 +68,14 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(ConvFwdArgs a) {
   const int P = a.B * HW;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
 
-  // per-thread A rows (fixed over the K loop)
+  // per-thread A rows (fixed over the K loop): chunk e -> row e>>3, 16-B column e&7
   int a_b[A_PER], a_y[A_PER], a_x[A_PER];
   bool a_ok[A_PER];
 #pragma unroll
   for (int j = 0; j < A_PER; ++j) {
     const int e = tid + j * NT;
-    const int m = m0 + (e >> 2);
-    a_ok[j] = (e < A_CHUNKS) && (m < P);
+    const int m = m0 + (e >> 3);
+    a_ok[j] = m < P;
     const int mm = a_ok[j] ? m : 0;
     a_b[j] = mm / HW;
     const int r = mm - a_b[j] * HW;
@@ -81,8 +86,7 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(ConvFwdArgs a) {
   const int nchunk = SMALLC ? 0 : a.cin_pad / BK;
   const int steps = SMALLC ? a.kpad / BK : a.KH * a.KW * nchunk;
 
-  uint4 ra[A_PER], rb[B_PER];
-  auto load = [&](int t) {
+  auto load = [&](int t, uint4 (&ra)[A_PER], uint4 (&rb)[B_PER]) {
     if constexpr (!SMALLC) {
       const int tap = t / nchunk, ch = t - tap * nchunk;
       const int kh = tap / a.KW, kw = tap - kh * a.KW;
@@ -99,7 +103,7 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(ConvFwdArgs a) {
         uint4 v = make_uint4(0, 0, 0, 0);
         if (a_ok[j] && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
           const uint16_t* p = sg.ptr + ((int64_t)(a_b[j] * a.H + yy) * a.W + xx) * sg.stride +
-                              (c0 - sbase) + (e & 3) * 8;
+                              (c0 - sbase) + (e & 7) * 8;
           v = *reinterpret_cast<const uint4*>(p);
         }
         ra[j] = v;
@@ -115,7 +119,7 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(ConvFwdArgs a) {
         uint16_t vals[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          const int k = t * BK + (e & 3) * 8 + q;
+          const int k = t * BK + (e & 7) * 8 + q;
           uint16_t v = 0;
           if (a_ok[j] && k < ktot) {
             const int tap = k / cs, c = k - tap * cs;
@@ -135,22 +139,22 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(ConvFwdArgs a) {
       const int e = tid + j * NT;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (e < B_CHUNKS) {
-        const int n = n0 + (e >> 2);
-        v = *reinterpret_cast<const uint4*>(a.wpk + (int64_t)n * a.kpad + t * BK + (e & 3) * 8);
+        const int n = n0 + (e >> 3);
+        v = *reinterpret_cast<const uint4*>(a.wpk + (int64_t)n * a.kpad + t * BK + (e & 7) * 8);
       }
       rb[j] = v;
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const uint4 (&ra)[A_PER], const uint4 (&rb)[B_PER]) {
 #pragma unroll
     for (int j = 0; j < A_PER; ++j) {
       const int e = tid + j * NT;
-      if (e < A_CHUNKS) As[buf][swz(e >> 2, e & 3)] = ra[j];
+      As[buf][swz(e >> 3, e & 7)] = ra[j];
     }
 #pragma unroll
     for (int j = 0; j < B_PER; ++j) {
       const int e = tid + j * NT;
-      if (e < B_CHUNKS) Bs[buf][swz(e >> 2, e & 3)] = rb[j];
+      if (e < B_CHUNKS) Bs[buf][swz(e >> 3, e & 7)] = rb[j];
     }
   };
 
@@ -162,24 +166,19 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int t = 0; t < steps; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < steps) load(t + 1);
+  auto compute = [&](int buf) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int kk = 0; kk < BK / 16; ++kk) {
       bf16x8_t af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WM + i * 32 + (lane & 31);
-        af[i] = __builtin_bit_cast(bf16x8_t, As[cur][swz(row, s * 2 + (lane >> 5))]);
+        af[i] = __builtin_bit_cast(bf16x8_t, As[buf][swz(row, kk * 2 + (lane >> 5))]);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WN + j * 32 + (lane & 31);
-        bfr[j] = __builtin_bit_cast(bf16x8_t, Bs[cur][swz(row, s * 2 + (lane >> 5))]);
+        bfr[j] = __builtin_bit_cast(bf16x8_t, Bs[buf][swz(row, kk * 2 + (lane >> 5))]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -187,7 +186,24 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(ConvFwdArgs a) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < steps) store(cur ^ 1);
+  };
+
+  uint4 ra0[A_PER], rb0[B_PER], ra1[A_PER], rb1[B_PER];
+  load(0, ra0, rb0);
+  if (steps > 1) load(1, ra1, rb1);
+  store(0, ra0, rb0);
+  __syncthreads();
+  for (int t = 0; t < steps; t += 2) {
+    // even step: LDS[0] = step t, regs1 = step t+1 (in flight), regs0 free
+    if (t + 2 < steps) load(t + 2, ra0, rb0);
+    compute(0);
+    if (t + 1 < steps) store(1, ra1, rb1);
+    __syncthreads();
+    if (t + 1 >= steps) break;
+    // odd step: LDS[1] = step t+1, regs0 = step t+2 (in flight), regs1 free
+    if (t + 3 < steps) load(t + 3, ra1, rb1);
+    compute(1);
+    if (t + 2 < steps) store(0, ra0, rb0);
     __syncthreads();
   }
 
@@ -248,15 +264,40 @@ __global__ __launch_bounds__(NT) void conv_fwd_kernel(ConvFwdArgs a) {
     }
 }
 
+// Tile choice: M = B*H*W is ~34k pixels at chairs (267 x 128 rows), so 128-row tiles leave the
+// 256 CUs with ~1.05 "rounds" of work for N <= 256 -- BM = 64 doubles the tile count and cuts the
+// tail; 128-row tiles keep the better LDS reuse when there are already many tiles.
+int pick_bm(int P, int cout, int bn) {
+  const int nt = (cout + bn - 1) / bn;
+  const int t128 = ((P + 127) / 128) * nt;
+  const int t64 = ((P + 63) / 64) * nt;
+  const double slots128 = 256.0 * 2, slots64 = 256.0 * 3;
+  // rounds x per-tile time (a 64-row tile costs ~0.55 of a 128-row one: lower fragment reuse)
+  const double c128 = std::ceil(t128 / slots128) * 1.0;
+  const double c64 = std::ceil(t64 / slots64) * 0.55;
+  return c64 < c128 ? 64 : 128;
+}
+
 template <int EPI, bool SMALLC>
 void launch_cfg(const ConvFwdArgs& a, int bn, hipStream_t stream) {
   const int P = a.B * a.H * a.W;
+  const int bm = pick_bm(P, a.cout, bn);
   if (bn == 128) {
-    dim3 grid(raft_cdiv(P, 128), raft_cdiv(a.cout, 128));
-    hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 64, 64, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
+    if (bm == 128) {
+      dim3 grid(raft_cdiv(P, 128), raft_cdiv(a.cout, 128));
+      hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 64, 64, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
+    } else {
+      dim3 grid(raft_cdiv(P, 64), raft_cdiv(a.cout, 128));
+      hipLaunchKernelGGL((conv_fwd_kernel<64, 128, 32, 64, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
+    }
   } else if (bn == 64) {
-    dim3 grid(raft_cdiv(P, 128), raft_cdiv(a.cout, 64));
-    hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 64, 32, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
+    if (bm == 128) {
+      dim3 grid(raft_cdiv(P, 128), raft_cdiv(a.cout, 64));
+      hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 64, 32, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
+    } else {
+      dim3 grid(raft_cdiv(P, 64), raft_cdiv(a.cout, 64));
+      hipLaunchKernelGGL((conv_fwd_kernel<64, 64, 32, 32, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
+    }
   } else {
     dim3 grid(raft_cdiv(P, 128), raft_cdiv(a.cout, 32));
     hipLaunchKernelGGL((conv_fwd_kernel<128, 32, 32, 32, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);

@@ -12,7 +12,10 @@
 // workgroups (split-K); each workgroup's 128x128 fp32 partial tile is added with 128-B-segment
 // float atomics (the shape MI355X's memory-side atomic units run at full rate).
 //
-// Bias gradient: a column-sum kernel over G (deterministic two-level reduction).
+// Pipeline: 64 pixels per step, two register sets (loads of the next two steps in flight during
+// the current step's MFMAs), two LDS buffers, one barrier per step.
+// Bias gradient: the column sums of G are accumulated from the LDS tiles by the workgroups of the
+// first K-tile column (no extra pass over G); col_sum_kernel remains for callers without wgrad.
 #include "common.h"
 #include "launchers.h"
 
@@ -22,10 +25,10 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4_t;
 constexpr int NT = 256;
-constexpr int BKP = 32;  // pixels per stage
+constexpr int BKP = 64;  // pixels per pipeline step
 
 template <int BM, int BN, bool SMALLC>
-__global__ __launch_bounds__(NT) void conv_wgrad_kernel(ConvWgradArgs a) {
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(ConvWgradArgs a, float* __restrict__ db) {
   // 4 waves as 2 x 2, each owns (BM/2) x (BN/2)
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
@@ -33,8 +36,11 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int XCH = BKP * BN / 8;
   constexpr int G_PER = (GCH + NT - 1) / NT;
   constexpr int X_PER = (XCH + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) uint16_t Gs[2][BKP * BM];
-  __shared__ __attribute__((aligned(16))) uint16_t Xs[2][BKP * BN];
+  // rows padded by 16 bf16 (32 B): the 4 rows of a ds_read_b64_tr_b16 16-lane group land on
+  // disjoint bank ranges
+  constexpr int GS = BM + 16, XS = BN + 16;
+  __shared__ __attribute__((aligned(16))) uint16_t Gs[2][BKP * GS];
+  __shared__ __attribute__((aligned(16))) uint16_t Xs[2][BKP * XS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -47,8 +53,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(ConvWgradArgs a) {
   const int p_end = min(P, p_begin + a.pix_per_split);
   const int ktot_small = a.KH * a.KW * a.cin_small;
 
-  uint4 rg[G_PER], rx[X_PER];
-  auto load = [&](int pbase) {
+  auto load = [&](int pbase, uint4 (&rg)[G_PER], uint4 (&rx)[X_PER]) {
 #pragma unroll
     for (int j = 0; j < G_PER; ++j) {
       const int e = tid + j * NT;
@@ -116,16 +121,18 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(ConvWgradArgs a) {
       rx[j] = v;
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const uint4 (&rg)[G_PER], const uint4 (&rx)[X_PER]) {
 #pragma unroll
     for (int j = 0; j < G_PER; ++j) {
       const int e = tid + j * NT;
-      if (e < GCH) reinterpret_cast<uint4*>(Gs[buf])[e] = rg[j];
+      const int row = e / (BM / 8), ch = e % (BM / 8);
+      if (e < GCH) *reinterpret_cast<uint4*>(&Gs[buf][row * GS + ch * 8]) = rg[j];
     }
 #pragma unroll
     for (int j = 0; j < X_PER; ++j) {
       const int e = tid + j * NT;
-      if (e < XCH) reinterpret_cast<uint4*>(Xs[buf])[e] = rx[j];
+      const int row = e / (BN / 8), ch = e % (BN / 8);
+      if (e < XCH) *reinterpret_cast<uint4*>(&Xs[buf][row * XS + ch * 8]) = rx[j];
     }
   };
 
@@ -138,15 +145,10 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(ConvWgradArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int gi = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
-  const int steps = (p_end - p_begin + BKP - 1) / BKP;
-  if (steps > 0) {
-    load(p_begin);
-    store(0);
-  }
-  __syncthreads();
-  for (int t = 0; t < steps; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < steps) load(p_begin + (t + 1) * BKP);
+  // bias gradient (column sums of G) rides along in the first K-tile column of workgroups
+  const bool do_bias = db != nullptr && tn == 0;
+  float bsum = 0.f;
+  auto compute = [&](int cur) {
 #pragma unroll
     for (int s = 0; s < BKP / 16; ++s) {
       bf16x8_t af[TM], bfr[TN];
@@ -155,9 +157,9 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(ConvWgradArgs a) {
         const int col = wm * WM + i * 32 + (gi & 1) * 16 + 4 * pp;
         const int row = s * 16 + (gi >> 1) * 8 + q;
         bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lds_bf16x4_t*)(&Gs[cur][row * BM + col]));
+            (lds_bf16x4_t*)(&Gs[cur][row * GS + col]));
         bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lds_bf16x4_t*)(&Gs[cur][(row + 4) * BM + col]));
+            (lds_bf16x4_t*)(&Gs[cur][(row + 4) * GS + col]));
         af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
@@ -165,9 +167,9 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(ConvWgradArgs a) {
         const int col = wn * WN + j * 32 + (gi & 1) * 16 + 4 * pp;
         const int row = s * 16 + (gi >> 1) * 8 + q;
         bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lds_bf16x4_t*)(&Xs[cur][row * BN + col]));
+            (lds_bf16x4_t*)(&Xs[cur][row * XS + col]));
         bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lds_bf16x4_t*)(&Xs[cur][(row + 4) * BN + col]));
+            (lds_bf16x4_t*)(&Xs[cur][(row + 4) * XS + col]));
         bfr[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
@@ -176,10 +178,39 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(ConvWgradArgs a) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (t + 1 < steps) store(cur ^ 1);
+    if (do_bias) {
+      // NT / BM threads per column, each a contiguous run of rows
+      constexpr int TPC = NT / BM, RPT = BKP / TPC;
+      const int c = tid % BM, r0 = (tid / BM) * RPT;
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) bsum += raft_bf16_to_f32(Gs[cur][(r0 + r) * GS + c]);
+    }
+  };
+
+  const int steps = (p_end - p_begin + BKP - 1) / BKP;
+  uint4 rg0[G_PER], rx0[X_PER], rg1[G_PER], rx1[X_PER];
+  if (steps > 0) {
+    load(p_begin, rg0, rx0);
+    if (steps > 1) load(p_begin + BKP, rg1, rx1);
+    store(0, rg0, rx0);
+  }
+  __syncthreads();
+  for (int t = 0; t < steps; t += 2) {
+    if (t + 2 < steps) load(p_begin + (t + 2) * BKP, rg0, rx0);
+    compute(0);
+    if (t + 1 < steps) store(1, rg1, rx1);
+    __syncthreads();
+    if (t + 1 >= steps) break;
+    if (t + 3 < steps) load(p_begin + (t + 3) * BKP, rg1, rx1);
+    compute(1);
+    if (t + 2 < steps) store(0, rg0, rx0);
     __syncthreads();
   }
   if (steps == 0) return;
+  if (do_bias) {
+    const int c = m0 + tid % BM;
+    if (c < a.cout) atomicAdd(db + c, bsum);
+  }
 
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -215,19 +246,20 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const uint16_t* __restrict
 
 }  // namespace
 
-bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, hipStream_t stream) {
+bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, float* db,
+                       hipStream_t stream) {
   const int P = a.B * a.H * a.W;
   const int splits = (P + a.pix_per_split - 1) / a.pix_per_split;
   constexpr int BN = 128;
   const int tiles_n = (a.kpad + BN - 1) / BN;
   if (bm == 128) {
     dim3 grid(raft_cdiv(a.cout, 128) * tiles_n, splits);
-    if (smallc) hipLaunchKernelGGL((conv_wgrad_kernel<128, BN, true>), grid, dim3(NT), 0, stream, a);
-    else hipLaunchKernelGGL((conv_wgrad_kernel<128, BN, false>), grid, dim3(NT), 0, stream, a);
+    if (smallc) hipLaunchKernelGGL((conv_wgrad_kernel<128, BN, true>), grid, dim3(NT), 0, stream, a, db);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<128, BN, false>), grid, dim3(NT), 0, stream, a, db);
   } else {
     dim3 grid(raft_cdiv(a.cout, 64) * tiles_n, splits);
-    if (smallc) hipLaunchKernelGGL((conv_wgrad_kernel<64, BN, true>), grid, dim3(NT), 0, stream, a);
-    else hipLaunchKernelGGL((conv_wgrad_kernel<64, BN, false>), grid, dim3(NT), 0, stream, a);
+    if (smallc) hipLaunchKernelGGL((conv_wgrad_kernel<64, BN, true>), grid, dim3(NT), 0, stream, a, db);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<64, BN, false>), grid, dim3(NT), 0, stream, a, db);
   }
   return true;
 }

@@ -137,7 +137,8 @@ struct ConvWgradArgs {
   int pix_per_split;
 };
 
-bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, hipStream_t stream);
+// db (nullable): fp32 bias gradient += column sums of G (fused)
+bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, float* db, hipStream_t stream);
 void launch_col_sum(const uint16_t* g, int stride, int cout, int P, float* db, hipStream_t stream);
 
 // ---- fused update-block elementwise kernels (update_ew.hip)

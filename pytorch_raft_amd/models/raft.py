@@ -164,7 +164,7 @@ class RAFT(nn.Module):
         return update_hip.available(required=(impl == 'hip'))
 
     def _iterate_fused(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
-        from ..ops.update_hip import HipUpdateBlock
+        from ..ops.update_hip import HipUpdateBlock, CORR_BUF
         hub = HipUpdateBlock(self.update_block)
         h = net.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
         x = inp.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
@@ -172,7 +172,7 @@ class RAFT(nn.Module):
         flow_up = None
         for itr in range(iters):
             coords1 = coords1.detach()
-            corr = corr_fn.lookup_nhwc(coords1, 352)
+            corr = corr_fn.lookup_nhwc(coords1, CORR_BUF)
             flow = coords1 - coords0
             h, delta_flow, up_mask = hub(h, x, corr, flow)
             coords1 = coords1 + delta_flow

@@ -7,7 +7,7 @@ slice ``(buffer, offset, count)``.  A conv reads the virtual concatenation of up
 Weights stay in the nn.Conv2d modules (checkpoint layout untouched) and are re-packed once per
 optimizer step (``pack_weight``) to the kernel layout [Npad][KH*KW][CinPad] bf16, where each input
 segment's real channels are placed at its padded offset (e.g. the 324 correlation channels live in
-a 352-channel buffer whose tail is zero).
+a 384-channel buffer whose tail is zero).  Segment widths are multiples of 64 = the kernel's K step.
 """
 import torch
 import torch.nn.functional as F
@@ -54,10 +54,10 @@ def pack_weight(w, seg_real, seg_pad, npad_mult=128):
 
 
 def pack_weight_small(w, npad_mult=128):
-    """Dense-K packing for tiny Cin: k = tap*Cin + c, padded to a multiple of 32."""
+    """Dense-K packing for tiny Cin: k = tap*Cin + c, padded to a multiple of 64 (one K step)."""
     cout, cin, kh, kw = w.shape
     wp = w.permute(0, 2, 3, 1).reshape(cout, kh * kw * cin)
-    kp = round_up(kh * kw * cin, 32)
+    kp = round_up(kh * kw * cin, 64)
     wp = F.pad(wp, (0, kp - kh * kw * cin, 0, round_up(cout, npad_mult) - cout))
     return wp.to(torch.bfloat16).contiguous()
 
@@ -98,10 +98,11 @@ def conv_wgrad(g, g_off, segs, ksize, pad, cout, dw, db=None, cin_small=0, pix_p
     ops = _ext.ops()
     if pix_per_split is None:
         p = g.shape[0] * g.shape[1] * g.shape[2]
-        # enough workgroups to cover 256 CUs a few times over, >= 2 K-steps each
+        # ~one full round of workgroups (256 CUs x 2 resident): split-K partials are combined
+        # with fp32 atomics, whose count grows with the number of splits
         tiles = max(1, (cout + 127) // 128) * max(1, (dw.shape[1] + 127) // 128)
-        splits = max(1, min(p // 64, (1024 + tiles - 1) // tiles))
-        pix_per_split = round_up((p + splits - 1) // splits, 32)
+        splits = max(1, min(p // 128, (512 + tiles - 1) // tiles))
+        pix_per_split = round_up((p + splits - 1) // splits, 64)
     ops.conv_wgrad_(g, int(g_off), [s[0] for s in segs], [int(s[1]) for s in segs],
                     [int(s[2]) for s in segs], int(ksize[0]), int(ksize[1]), int(pad[0]),
                     int(pad[1]), int(cout), int(cin_small), dw, db, int(pix_per_split))

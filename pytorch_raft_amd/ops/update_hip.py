@@ -9,7 +9,7 @@ This module runs one iteration as ONE autograd node built from the hand-written 
 
 forward (12 MFMA implicit-GEMM convs + 1 prep kernel, NHWC bf16, fp32 accumulation)::
 
-    corr(352, from the lookup kernel) -c1(1x1,relu)-> c1(256) -c2(3x3,relu)-> cf[0:192]
+    corr(384, from the lookup kernel) -c1(1x1,relu)-> c1(256) -c2(3x3,relu)-> cf[0:192]
     flow -prep-> flowb(8) -f1(7x7,relu, dense-K small-Cin path)-> f1(128) -f2(3x3,relu)-> cf[192:256]
     cf -conv(3x3,relu)-> mf[0:126] ; mf[126:128] = flow
     [h | inp | mf] -zr1(1x5, sigmoid epilogue)-> z1, r1, r1*h
@@ -32,6 +32,7 @@ from . import _ext
 from . import conv as C
 
 HD = 128  # hidden / context width of the full model
+CORR_BUF = 384  # lookup taps (4 x 81 = 324) zero-padded to a multiple of the conv K step (64)
 
 
 class _LayerSpec:
@@ -50,7 +51,7 @@ class _LayerSpec:
 
 
 SPECS = [
-    _LayerSpec('c1', 256, (1, 1), [324], [352]),
+    _LayerSpec('c1', 256, (1, 1), [324], [CORR_BUF]),
     _LayerSpec('c2', 192, (3, 3), [256], [256]),
     _LayerSpec('f1', 128, (7, 7), [2], [8], small=True),
     _LayerSpec('f2', 64, (3, 3), [128], [128]),
@@ -192,7 +193,7 @@ def _f32(shape, dev, zero=False):
 
 class _UpdateIter(torch.autograd.Function):
     """One GRU iteration.  Inputs: token, h (B,H,W,128) bf16, inp (B,H,W,128) bf16,
-    corr (B,H,W,352) bf16, flow (B,2,H,W) fp32.  Outputs: h', delta (B,2,H,W) fp32,
+    corr (B,H,W,CORR_BUF) bf16, flow (B,2,H,W) fp32.  Outputs: h', delta (B,2,H,W) fp32,
     mask (B,H,W,576) bf16 (already x0.25)."""
 
     @staticmethod
@@ -214,7 +215,7 @@ class _UpdateIter(torch.autograd.Function):
             C.conv_fwd(segs, pk.w[name], pk.b[name], s.k, s.pad, s.cout, epi, outs, offs, aux,
                        aux_offs, scale=s.scale, split=split, cin_small=2 if s.small else 0)
 
-        conv('c1', [(corr, 0, 352)], C.EPI_RELU_BF16, [c1], [0])
+        conv('c1', [(corr, 0, CORR_BUF)], C.EPI_RELU_BF16, [c1], [0])
         conv('c2', [(c1, 0, 256)], C.EPI_RELU_BF16, [cf], [0])
         conv('f1', [(flowb, 0, 8)], C.EPI_RELU_BF16, [f1], [0])
         conv('f2', [(f1, 0, 128)], C.EPI_RELU_BF16, [cf], [192])
@@ -322,9 +323,9 @@ class _UpdateIter(torch.autograd.Function):
         wgrad('f1', dpre_f1, 0, [(flowb, 0, 8)])
         dpre_c1 = _bf16(sh + (256,), dev)
         ops.relu_bwd_(dc1, 0, c1, 0, dpre_c1, 0, 256, 1.0)
-        wgrad('c1', dpre_c1, 0, [(corr, 0, 352)])
-        dcorr = _f32(sh + (352,), dev)
-        dgrad('c1', [(dpre_c1, 0, 256)], [(dcorr, 0, 352, 324, 0)])  # slots 324.. unused
+        wgrad('c1', dpre_c1, 0, [(corr, 0, CORR_BUF)])
+        dcorr = _f32(sh + (CORR_BUF,), dev)
+        dgrad('c1', [(dpre_c1, 0, 256)], [(dcorr, 0, CORR_BUF, 324, 0)])  # slots 324.. unused
         return (torch.zeros((), device=dev), dh, dinp, dcorr, None, None)
 
 

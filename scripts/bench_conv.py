@@ -13,7 +13,7 @@ import torch.nn.functional as F  # noqa: E402
 from pytorch_raft_amd.ops import conv as C  # noqa: E402
 
 SHAPES = [  # name, cin, cout, k, epi
-    ('convc1 1x1 324->256', 352, 256, (1, 1), C.EPI_RELU_BF16),
+    ('convc1 1x1 324->256', 384, 256, (1, 1), C.EPI_RELU_BF16),
     ('convc2 3x3 256->192', 256, 192, (3, 3), C.EPI_RELU_BF16),
     ('convf2 3x3 128->64', 128, 64, (3, 3), C.EPI_RELU_BF16),
     ('conv   3x3 256->126', 256, 126, (3, 3), C.EPI_RELU_BF16),
@@ -40,8 +40,9 @@ def main():
     B, H, W = 12, 46, 62
     dev = 'cuda'
     torch.backends.cudnn.benchmark = True
-    tot_ours = tot_miopen = 0.0
-    print('%-22s %10s %10s %10s %10s' % ('conv', 'ours_us', 'ours_TF', 'miopen_us', 'miopen_TF'))
+    tot_ours = tot_miopen = tot_wg = 0.0
+    print('%-22s %10s %10s %10s %10s %10s %10s' % ('conv', 'ours_us', 'ours_TF', 'miopen_us',
+                                                   'miopen_TF', 'wgrad_us', 'wgrad_TF'))
     for name, cin, cout, k, epi in SHAPES:
         pad = (k[0] // 2, k[1] // 2)
         x = torch.randn(B, cin, H, W, device=dev, dtype=torch.bfloat16)
@@ -57,11 +58,18 @@ def main():
         wcl = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         bb = b.to(torch.bfloat16)
         t_mi = timeit(lambda: F.conv2d(xcl, wcl, bb, padding=pad))
+        g = torch.randn(B, H, W, C.round_up(cout, 8), device=dev, dtype=torch.bfloat16)
+        dw = torch.zeros(cout, wpk.shape[1], device=dev)
+        db = torch.zeros(cout, device=dev)
+        t_wg = timeit(lambda: C.conv_wgrad(g, 0, [(xb, 0, cin)], k, pad, cout, dw, db))
         tot_ours += t_ours
         tot_miopen += t_mi
-        print('%-22s %10.1f %10.1f %10.1f %10.1f' % (name, t_ours * 1e6, flops / t_ours / 1e12,
-                                                      t_mi * 1e6, flops / t_mi / 1e12))
-    print('total per update-block forward: ours %.3f ms, MIOpen(NHWC) %.3f ms' % (tot_ours * 1e3, tot_miopen * 1e3))
+        tot_wg += t_wg
+        print('%-22s %10.1f %10.1f %10.1f %10.1f %10.1f %10.1f' % (
+            name, t_ours * 1e6, flops / t_ours / 1e12, t_mi * 1e6, flops / t_mi / 1e12,
+            t_wg * 1e6, flops / t_wg / 1e12))
+    print('total per update-block forward: ours %.3f ms, MIOpen(NHWC) %.3f ms; wgrad %.3f ms' % (
+        tot_ours * 1e3, tot_miopen * 1e3, tot_wg * 1e3))
 
 
 if __name__ == '__main__':

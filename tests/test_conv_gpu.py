@@ -46,19 +46,19 @@ def test_conv_fwd_single_segment(ext_ops, cin, cout, k, epi):
 def test_conv_fwd_multi_segment_padded(ext_ops):
     torch.manual_seed(1)
     B, H, W = 2, 9, 17
-    # 324 real channels in a 352-wide buffer + a 64-channel second segment at an offset
+    # 324 real channels in a 384-wide buffer + a 64-channel second segment at an offset
     x1 = torch.randn(B, 324, H, W, device=DEV)
     x2 = torch.randn(B, 64, H, W, device=DEV)
     w = torch.randn(96, 388, 3, 3, device=DEV) / 60
     b = torch.randn(96, device=DEV)
     ref = _ref(torch.cat([x1, x2], 1), w, b, (1, 1))
-    buf1 = torch.zeros(B, H, W, 352, device=DEV, dtype=torch.bfloat16)
+    buf1 = torch.zeros(B, H, W, 384, device=DEV, dtype=torch.bfloat16)
     buf1[..., :324] = C.nhwc(x1)
     buf2 = torch.zeros(B, H, W, 128, device=DEV, dtype=torch.bfloat16)
     buf2[..., 32:96] = C.nhwc(x2)
-    wpk = C.pack_weight(w, [324, 64], [352, 64])
+    wpk = C.pack_weight(w, [324, 64], [384, 64])
     out = torch.empty(B, H, W, 96, device=DEV)
-    C.conv_fwd([(buf1, 0, 352), (buf2, 32, 64)], wpk, b, (3, 3), (1, 1), 96, C.EPI_F32, [out], [0])
+    C.conv_fwd([(buf1, 0, 384), (buf2, 32, 64)], wpk, b, (3, 3), (1, 1), 96, C.EPI_F32, [out], [0])
     torch.testing.assert_close(C.nchw(out), ref, atol=2e-3, rtol=2e-3)
 
 

@@ -120,7 +120,7 @@ def test_onthefly_nhwc_bf16(ext_ops, hw):
     coords = [_coords(b, h, w, spread=2.0 + s, seed=5 + s) for s in range(3)]
     nc = levels * 81
     pyr = torch_corr_pyramid(f1, f2, levels)
-    gouts = [torch.randn(b, h, w, 352, device=DEV) for _ in coords]
+    gouts = [torch.randn(b, h, w, 384, device=DEV) for _ in coords]
     refs = [torch_corr_lookup(pyr, co, radius).permute(0, 2, 3, 1) for co in coords]
     sum((r * g[..., :nc]).sum() for r, g in zip(refs, gouts)).backward()
     g1_ref, g2_ref = f1.grad.clone(), f2.grad.clone()
@@ -129,9 +129,9 @@ def test_onthefly_nhwc_bf16(ext_ops, hw):
         f1.grad = f2.grad = None
         blk = AlternateCorrBlock(f1, f2, num_levels=levels, radius=radius, impl='hip',
                                  precision='bf16')
-        outs = [blk.lookup_nhwc(co, 352) for co in coords]
+        outs = [blk.lookup_nhwc(co, 384) for co in coords]
         for o, r in zip(outs, refs):
-            assert o.shape == (b, h, w, 352) and o.dtype == torch.bfloat16
+            assert o.shape == (b, h, w, 384) and o.dtype == torch.bfloat16
             assert torch.all(o[..., nc:] == 0)
             assert _rel(o[..., :nc].float(), r.detach()) < 8e-3
         sum((o.float() * g).sum() for o, g in zip(outs, gouts)).backward()
@@ -206,7 +206,7 @@ def test_lookup_nhwc_window_backward(ext_ops, hw):
     levels = 3 if min(h, w) < 16 else 4
     coords = [_coords(b, h, w, seed=s) for s in range(3)]
     pyr = torch_corr_pyramid(f1, f2, levels)
-    gouts = [torch.randn(b, h, w, 352, device=DEV).to(torch.bfloat16) for _ in coords]
+    gouts = [torch.randn(b, h, w, 384, device=DEV).to(torch.bfloat16) for _ in coords]
     loss = 0
     for co, go in zip(coords, gouts):
         ref = torch_corr_lookup(pyr, co, radius)  # (b, L*81, h, w)
@@ -218,8 +218,8 @@ def test_lookup_nhwc_window_backward(ext_ops, hw):
     blk = CorrBlock(f1, f2, num_levels=levels, radius=radius, impl='hip')
     loss = 0
     for co, go in zip(coords, gouts):
-        out = blk.lookup_nhwc(co, 352)
-        assert out.shape == (b, h, w, 352) and out.dtype == torch.bfloat16
+        out = blk.lookup_nhwc(co, 384)
+        assert out.shape == (b, h, w, 384) and out.dtype == torch.bfloat16
         nc = levels * 81
         ref = torch_corr_lookup(pyr, co, radius).permute(0, 2, 3, 1)
         torch.testing.assert_close(out[..., :nc].float(), ref.detach(), atol=3e-2, rtol=1e-2)
