@@ -604,6 +604,12 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   TORCH_CHECK(launch_conv_fwd(a, (int)epi, (int)bn, cin_small != 0, cur_stream()), "bad epilogue");
 }
 
+std::vector<int64_t> conv_tune_table() {
+  std::vector<int> buf(12 * 512);
+  const int n = conv_tuned_table(buf.data(), 512);
+  return std::vector<int64_t>(buf.begin(), buf.begin() + 12 * n);
+}
+
 // dw (cout, kpad) fp32 += sum_p g[p][:cout] (x) im2col(ins)[p][:]; db (cout) fp32 += colsum(g)
 void conv_wgrad_(const Tensor& g, int64_t g_off, const std::vector<Tensor>& ins,
                  const std::vector<int64_t>& in_off, const std::vector<int64_t>& in_cnt,
@@ -799,6 +805,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_pyr_grad_reduce(Tensor[] gpyr, float inv_sqrt_c) -> Tensor");
   m.def("corr_otf_fwd_(Tensor f1, Tensor[] f2, Tensor coords, int radius, Tensor(a!) out, Tensor[] lo) -> ()");
   m.def("corr_otf_bwd_(Tensor f1, Tensor[] f2, Tensor coords, Tensor dout, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
+  m.def("conv_tune_table() -> int[]", &conv_tune_table);
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] wgs, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");
   m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout, bool nhwc=False) -> Tensor[]");

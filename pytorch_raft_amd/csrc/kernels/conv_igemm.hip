@@ -28,6 +28,10 @@
 #include "launchers.h"
 
 #include <cmath>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 namespace {
 
@@ -49,11 +53,22 @@ __device__ __forceinline__ float tanhf_(float v) {
 // Pipeline (per 64-deep K step, one barrier):  global loads for step t+2 are issued into one of
 // two register sets before the MFMAs of step t (two steps = ~1000+ MFMA cycles of latency cover),
 // the other set (step t+1, loaded one step earlier) is written to the idle LDS buffer after them.
-template <int BM, int BN, int WM, int WN, int EPI, bool SMALLC>
-__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs a) {
-  constexpr int WAVES_N = BN / WN;
-  static_assert((BM / WM) * WAVES_N == 4, "4 waves per workgroup");
-  constexpr int TM = WM / 32, TN = WN / 32;
+// Wave tile (32*TM) x (32*TN); WVM x (4/WVM) waves -> block tile BM x BN.  Larger wave tiles
+// cut LDS traffic per MFMA ((TM+TN)/(TM*TN) fragment reads per MFMA): at 2x2 the four SIMDs
+// already need the LDS's full 128 B/clk, so the big-M configs (4x2, 5x2) exist for that reason.
+template <int TM, int TN, int WVM>
+struct ConvTile {
+  static constexpr int WVN = 4 / WVM;
+  static constexpr int BM = 32 * TM * WVM, BN = 32 * TN * WVN;
+  static constexpr int LDS = 2 * (BM + BN) * 128;
+  static constexpr int OCC = LDS <= 65536 && TM * TN <= 4 ? 2 : 1;
+};
+
+template <int TM, int TN, int WVM, int EPI, bool SMALLC>
+__global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_kernel(ConvFwdArgs a) {
+  using T = ConvTile<TM, TN, WVM>;
+  constexpr int BM = T::BM, BN = T::BN, WM = 32 * TM, WN = 32 * TN;
+  constexpr int WAVES_N = T::WVN;
   constexpr int A_CHUNKS = BM * 8;  // 16-B chunks per A stage
   constexpr int B_CHUNKS = BN * 8;
   constexpr int A_PER = A_CHUNKS / NT;
@@ -68,19 +83,19 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs a) {
   const int P = a.B * HW;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
 
-  // per-thread A rows (fixed over the K loop): chunk e -> row e>>3, 16-B column e&7
-  int a_b[A_PER], a_y[A_PER], a_x[A_PER];
-  bool a_ok[A_PER];
+  // per-thread A rows (fixed over the K loop): chunk e -> row e>>3, 16-B column e&7;
+  // kept as (image row b*H + y, x) with y = -2^20 marking rows past P
+  int a_by[A_PER], a_x[A_PER];
 #pragma unroll
   for (int j = 0; j < A_PER; ++j) {
     const int e = tid + j * NT;
     const int m = m0 + (e >> 3);
-    a_ok[j] = m < P;
-    const int mm = a_ok[j] ? m : 0;
-    a_b[j] = mm / HW;
-    const int r = mm - a_b[j] * HW;
-    a_y[j] = r / a.W;
-    a_x[j] = r - a_y[j] * a.W;
+    const int mm = m < P ? m : 0;
+    const int b = mm / HW;
+    const int r = mm - b * HW;
+    const int y = r / a.W;
+    a_x[j] = r - y * a.W;
+    a_by[j] = m < P ? b * a.H + y : -(1 << 20);
   }
 
   const int nchunk = SMALLC ? 0 : a.cin_pad / BK;
@@ -99,10 +114,11 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
       for (int j = 0; j < A_PER; ++j) {
         const int e = tid + j * NT;
-        const int yy = a_y[j] + kh - a.PH, xx = a_x[j] + kw - a.PW;
+        const int y = a_by[j] % a.H;  // negative for rows past P
+        const int yy = y + kh - a.PH, xx = a_x[j] + kw - a.PW;
         uint4 v = make_uint4(0, 0, 0, 0);
-        if (a_ok[j] && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
-          const uint16_t* p = sg.ptr + ((int64_t)(a_b[j] * a.H + yy) * a.W + xx) * sg.stride +
+        if (a_by[j] >= 0 && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
+          const uint16_t* p = sg.ptr + ((int64_t)(a_by[j] + kh - a.PH) * a.W + xx) * sg.stride +
                               (c0 - sbase) + (e & 7) * 8;
           v = *reinterpret_cast<const uint4*>(p);
         }
@@ -121,12 +137,12 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs a) {
         for (int q = 0; q < 8; ++q) {
           const int k = t * BK + (e & 7) * 8 + q;
           uint16_t v = 0;
-          if (a_ok[j] && k < ktot) {
+          if (a_by[j] >= 0 && k < ktot) {
             const int tap = k / cs, c = k - tap * cs;
             const int kh = tap / a.KW, kw = tap - kh * a.KW;
-            const int yy = a_y[j] + kh - a.PH, xx = a_x[j] + kw - a.PW;
+            const int yy = a_by[j] % a.H + kh - a.PH, xx = a_x[j] + kw - a.PW;
             if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
-              v = sg.ptr[((int64_t)(a_b[j] * a.H + yy) * a.W + xx) * sg.stride + c];
+              v = sg.ptr[((int64_t)(a_by[j] + kh - a.PH) * a.W + xx) * sg.stride + c];
           }
           vals[q] = v;
         }
@@ -188,23 +204,38 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs a) {
     }
   };
 
-  uint4 ra0[A_PER], rb0[B_PER], ra1[A_PER], rb1[B_PER];
-  load(0, ra0, rb0);
-  if (steps > 1) load(1, ra1, rb1);
-  store(0, ra0, rb0);
-  __syncthreads();
-  for (int t = 0; t < steps; t += 2) {
-    // even step: LDS[0] = step t, regs1 = step t+1 (in flight), regs0 free
-    if (t + 2 < steps) load(t + 2, ra0, rb0);
-    compute(0);
-    if (t + 1 < steps) store(1, ra1, rb1);
+  if constexpr (TM * TN >= 8) {
+    // big wave tiles: one register set (the step's 32+ MFMAs per wave cover one load latency)
+    uint4 ra[A_PER], rb[B_PER];
+    load(0, ra, rb);
+    store(0, ra, rb);
     __syncthreads();
-    if (t + 1 >= steps) break;
-    // odd step: LDS[1] = step t+1, regs0 = step t+2 (in flight), regs1 free
-    if (t + 3 < steps) load(t + 3, ra1, rb1);
-    compute(1);
-    if (t + 2 < steps) store(0, ra0, rb0);
+    for (int t = 0; t < steps; ++t) {
+      const int cur = t & 1;
+      if (t + 1 < steps) load(t + 1, ra, rb);
+      compute(cur);
+      if (t + 1 < steps) store(cur ^ 1, ra, rb);
+      __syncthreads();
+    }
+  } else {
+    uint4 ra0[A_PER], rb0[B_PER], ra1[A_PER], rb1[B_PER];
+    load(0, ra0, rb0);
+    if (steps > 1) load(1, ra1, rb1);
+    store(0, ra0, rb0);
     __syncthreads();
+    for (int t = 0; t < steps; t += 2) {
+      // even step: LDS[0] = step t, regs1 = step t+1 (in flight), regs0 free
+      if (t + 2 < steps) load(t + 2, ra0, rb0);
+      compute(0);
+      if (t + 1 < steps) store(1, ra1, rb1);
+      __syncthreads();
+      if (t + 1 >= steps) break;
+      // odd step: LDS[1] = step t+1, regs0 = step t+2 (in flight), regs1 free
+      if (t + 3 < steps) load(t + 3, ra1, rb1);
+      compute(1);
+      if (t + 2 < steps) store(0, ra0, rb0);
+      __syncthreads();
+    }
   }
 
   // ---------------------------------------------------------------- fused epilogue
@@ -264,64 +295,193 @@ __global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(ConvFwdArgs a) {
     }
 }
 
-// Tile choice: M = B*H*W is ~34k pixels at chairs (267 x 128 rows), so 128-row tiles leave the
-// 256 CUs with ~1.05 "rounds" of work for N <= 256 -- BM = 64 doubles the tile count and cuts the
-// tail; 128-row tiles keep the better LDS reuse when there are already many tiles.
-int pick_bm(int P, int cout, int bn) {
-  const int nt = (cout + bn - 1) / bn;
-  const int t128 = ((P + 127) / 128) * nt;
-  const int t64 = ((P + 63) / 64) * nt;
-  const double slots128 = 256.0 * 2, slots64 = 256.0 * 3;
-  // rounds x per-tile time (a 64-row tile costs ~0.55 of a 128-row one: lower fragment reuse)
-  const double c128 = std::ceil(t128 / slots128) * 1.0;
-  const double c64 = std::ceil(t64 / slots64) * 0.55;
-  return c64 < c128 ? 64 : 128;
+// ------------------------------------------------------------------ tile configurations
+struct CfgDesc {
+  int tm, tn, wvm, bm, bn;
+  bool small_ok;
+};
+// (keep in sync with the dispatch switch below)
+constexpr CfgDesc kCfgs[] = {
+    {2, 2, 2, 128, 128, true},  {1, 2, 2, 64, 128, true},  {2, 1, 2, 128, 64, false},
+    {1, 1, 2, 64, 64, false},   {1, 1, 4, 128, 32, true},  {4, 2, 2, 256, 128, false},
+    {5, 2, 1, 160, 256, false}, {5, 1, 1, 160, 128, false}, {4, 2, 1, 128, 256, false},
+    {3, 2, 1, 96, 256, false},
+};
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+template <int EPI, bool SMALLC, int TM, int TN, int WVM>
+void launch_one(const ConvFwdArgs& a, hipStream_t stream) {
+  using T = ConvTile<TM, TN, WVM>;
+  const int P = a.B * a.H * a.W;
+  dim3 grid(raft_cdiv(P, T::BM), raft_cdiv(a.cout, T::BN));
+  hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WVM, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
 }
 
 template <int EPI, bool SMALLC>
-void launch_cfg(const ConvFwdArgs& a, int bn, hipStream_t stream) {
-  const int P = a.B * a.H * a.W;
-  const int bm = pick_bm(P, a.cout, bn);
-  if (bn == 128) {
-    if (bm == 128) {
-      dim3 grid(raft_cdiv(P, 128), raft_cdiv(a.cout, 128));
-      hipLaunchKernelGGL((conv_fwd_kernel<128, 128, 64, 64, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
-    } else {
-      dim3 grid(raft_cdiv(P, 64), raft_cdiv(a.cout, 128));
-      hipLaunchKernelGGL((conv_fwd_kernel<64, 128, 32, 64, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
-    }
-  } else if (bn == 64) {
-    if (bm == 128) {
-      dim3 grid(raft_cdiv(P, 128), raft_cdiv(a.cout, 64));
-      hipLaunchKernelGGL((conv_fwd_kernel<128, 64, 64, 32, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
-    } else {
-      dim3 grid(raft_cdiv(P, 64), raft_cdiv(a.cout, 64));
-      hipLaunchKernelGGL((conv_fwd_kernel<64, 64, 32, 32, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
+bool launch_cfg_idx(const ConvFwdArgs& a, int idx, hipStream_t stream) {
+  if constexpr (SMALLC) {
+    switch (idx) {
+      case 0: launch_one<EPI, true, 2, 2, 2>(a, stream); return true;
+      case 1: launch_one<EPI, true, 1, 2, 2>(a, stream); return true;
+      case 4: launch_one<EPI, true, 1, 1, 4>(a, stream); return true;
+      default: return false;
     }
   } else {
-    dim3 grid(raft_cdiv(P, 128), raft_cdiv(a.cout, 32));
-    hipLaunchKernelGGL((conv_fwd_kernel<128, 32, 32, 32, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
+    switch (idx) {
+      case 0: launch_one<EPI, false, 2, 2, 2>(a, stream); return true;
+      case 1: launch_one<EPI, false, 1, 2, 2>(a, stream); return true;
+      case 2: launch_one<EPI, false, 2, 1, 2>(a, stream); return true;
+      case 3: launch_one<EPI, false, 1, 1, 2>(a, stream); return true;
+      case 4: launch_one<EPI, false, 1, 1, 4>(a, stream); return true;
+      case 5: launch_one<EPI, false, 4, 2, 2>(a, stream); return true;
+      case 6:  // the GRU epilogues spill at this tile (160 fp32 accumulators + gate math)
+        if constexpr (EPI == EPI_GRU_ZR || EPI == EPI_GRU_Q) return false;
+        else { launch_one<EPI, false, 5, 2, 1>(a, stream); return true; }
+      case 7: launch_one<EPI, false, 5, 1, 1>(a, stream); return true;
+      case 8: launch_one<EPI, false, 4, 2, 1>(a, stream); return true;
+      case 9: launch_one<EPI, false, 3, 2, 1>(a, stream); return true;
+      default: return false;
+    }
   }
 }
 
-template <int EPI>
-void launch_epi(const ConvFwdArgs& a, int bn, bool smallc, hipStream_t stream) {
-  if (smallc) launch_cfg<EPI, true>(a, bn, stream);
-  else launch_cfg<EPI, false>(a, bn, stream);
+bool launch_epi_idx(const ConvFwdArgs& a, int epi, int idx, bool smallc, hipStream_t stream) {
+#define RAFT_EPI_CASE(E) \
+  case E: return smallc ? launch_cfg_idx<E, true>(a, idx, stream) : launch_cfg_idx<E, false>(a, idx, stream);
+  switch (epi) {
+    RAFT_EPI_CASE(EPI_BF16)
+    RAFT_EPI_CASE(EPI_RELU_BF16)
+    RAFT_EPI_CASE(EPI_F32)
+    RAFT_EPI_CASE(EPI_ACC_F32)
+    RAFT_EPI_CASE(EPI_DGRAD)
+    RAFT_EPI_CASE(EPI_F32_NCHW)
+    case EPI_GRU_ZR: return !smallc && launch_cfg_idx<EPI_GRU_ZR, false>(a, idx, stream);
+    case EPI_GRU_Q: return !smallc && launch_cfg_idx<EPI_GRU_Q, false>(a, idx, stream);
+    default: return false;
+  }
+#undef RAFT_EPI_CASE
+}
+
+bool cfg_allowed(int idx, int cout, bool smallc, int epi) {
+  const CfgDesc& c = kCfgs[idx];
+  if (smallc && !c.small_ok) return false;
+  if (idx == 6 && (epi == EPI_GRU_ZR || epi == EPI_GRU_Q)) return false;
+  const int npad = (cout + 31) / 32 * 32;
+  return c.bn <= 2 * npad || c.bn <= 32;  // no config more than half empty in N
+}
+
+// Analytic fallback (stream capture / autotune disabled): rounds of workgroups x tile cost,
+// with the 2x2-wave tiles' LDS-bandwidth penalty.
+int heuristic_cfg(int P, int cout, bool smallc, int epi) {
+  double best = 1e30;
+  int bi = 0;
+  for (int i = 0; i < kNumCfgs; ++i) {
+    if (!cfg_allowed(i, cout, smallc, epi)) continue;
+    const CfgDesc& c = kCfgs[i];
+    const int tiles = raft_cdiv(P, c.bm) * raft_cdiv(cout, c.bn);
+    const int occ = (2 * (c.bm + c.bn) * 128 <= 65536 && c.tm * c.tn <= 4) ? 2 : 1;
+    const double rounds = std::ceil(tiles / (256.0 * occ));
+    const double ratio = double(c.tm + c.tn) / double(c.tm * c.tn);  // LDS KB per MFMA
+    const double eff = std::min(1.0, 0.8 / ratio);
+    const double cost = rounds * c.bm * c.bn / (eff * occ);
+    if (cost < best) { best = cost; bi = i; }
+  }
+  return bi;
+}
+
+struct TuneKey {
+  int P, H, W, KH, KW, cin, cout, small, f32out;
+  bool operator<(const TuneKey& o) const {
+    return std::tie(P, H, W, KH, KW, cin, cout, small, f32out) <
+           std::tie(o.P, o.H, o.W, o.KH, o.KW, o.cin, o.cout, o.small, o.f32out);
+  }
+};
+std::map<TuneKey, int> g_tuned;
+std::mutex g_tune_mu;
+float* g_scratch = nullptr;
+size_t g_scratch_bytes = 0;
+
+// Time every allowed config once on the real operands (output into a private scratch buffer
+// through the fp32 epilogue) and cache the fastest.  Runs only outside stream capture.
+int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
+  const int P = a.B * a.H * a.W;
+  const size_t need = (size_t)P * ((a.cout + 255) / 256 * 256) * sizeof(float);
+  if (need > g_scratch_bytes) {
+    if (g_scratch) (void)hipFree(g_scratch);
+    if (hipMalloc(&g_scratch, need) != hipSuccess) { g_scratch = nullptr; g_scratch_bytes = 0; return -1; }
+    g_scratch_bytes = need;
+  }
+  ConvFwdArgs t = a;
+  t.out0 = g_scratch;
+  t.out0_stride = (a.cout + 255) / 256 * 256;
+  t.noseg = 0;
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  int best = -1;
+  float best_ms = 1e30f;
+  for (int i = 0; i < kNumCfgs; ++i) {
+    if (!cfg_allowed(i, a.cout, smallc, epi)) continue;
+    launch_epi_idx(t, EPI_F32, i, smallc, stream);  // warm (code load, caches)
+    (void)hipEventRecord(e0, stream);
+    for (int r = 0; r < 3; ++r) launch_epi_idx(t, EPI_F32, i, smallc, stream);
+    (void)hipEventRecord(e1, stream);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best_ms) { best_ms = ms; best = i; }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return best;
+}
+
+int choose_cfg(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
+  static const int forced = [] {
+    const char* e = getenv("RAFT_CONV_CFG");
+    return e ? atoi(e) : -1;
+  }();
+  static const bool tune = [] {
+    const char* e = getenv("RAFT_CONV_AUTOTUNE");
+    return !(e && e[0] == '0');
+  }();
+  const int P = a.B * a.H * a.W;
+  if (forced >= 0 && forced < kNumCfgs && cfg_allowed(forced, a.cout, smallc, epi)) return forced;
+  const bool f32out = epi == EPI_F32 || epi == EPI_ACC_F32 || epi == EPI_DGRAD || epi == EPI_F32_NCHW;
+  const int eclass = f32out ? 1 : ((epi == EPI_GRU_ZR || epi == EPI_GRU_Q) ? 2 : 0);
+  const TuneKey key{P, a.H, a.W, a.KH, a.KW, smallc ? a.cin_small : a.cin_pad, a.cout, (int)smallc,
+                    eclass};
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  auto it = g_tuned.find(key);
+  if (it != g_tuned.end()) return it->second;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(stream, &cs);
+  int idx = -1;
+  if (tune && cs == hipStreamCaptureStatusNone) idx = autotune(a, epi, smallc, stream);
+  if (idx < 0) idx = heuristic_cfg(P, a.cout, smallc, epi);
+  if (cs == hipStreamCaptureStatusNone) g_tuned[key] = idx;
+  return idx;
 }
 
 }  // namespace
 
 bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStream_t stream) {
-  switch (epi) {
-    case EPI_BF16: launch_epi<EPI_BF16>(a, bn, smallc, stream); return true;
-    case EPI_RELU_BF16: launch_epi<EPI_RELU_BF16>(a, bn, smallc, stream); return true;
-    case EPI_F32: launch_epi<EPI_F32>(a, bn, smallc, stream); return true;
-    case EPI_ACC_F32: launch_epi<EPI_ACC_F32>(a, bn, smallc, stream); return true;
-    case EPI_GRU_ZR: launch_epi<EPI_GRU_ZR>(a, bn, false, stream); return true;
-    case EPI_GRU_Q: launch_epi<EPI_GRU_Q>(a, bn, false, stream); return true;
-    case EPI_DGRAD: launch_epi<EPI_DGRAD>(a, bn, smallc, stream); return true;
-    case EPI_F32_NCHW: launch_epi<EPI_F32_NCHW>(a, bn, smallc, stream); return true;
-    default: return false;
+  (void)bn;  // tile shape is chosen per geometry (autotuned once, cached)
+  const int idx = choose_cfg(a, epi, smallc, stream);
+  return launch_epi_idx(a, epi, idx, smallc, stream);
+}
+
+int conv_tuned_table(int* out, int max_rows) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  int n = 0;
+  for (const auto& kv : g_tuned) {
+    if (n >= max_rows) break;
+    const TuneKey& k = kv.first;
+    const CfgDesc& c = kCfgs[kv.second];
+    const int row[12] = {k.P, k.H, k.W, k.KH, k.KW, k.cin, k.cout, k.small, k.f32out, kv.second,
+                         c.bm, c.bn};
+    for (int i = 0; i < 12; ++i) out[n * 12 + i] = row[i];
+    ++n;
   }
+  return n;
 }

@@ -121,7 +121,11 @@ struct ConvFwdArgs {
   int noseg;
 };
 
+// tile shape chosen per geometry: autotuned once (outside stream capture) and cached;
+// RAFT_CONV_CFG=<idx> forces a config, RAFT_CONV_AUTOTUNE=0 uses the analytic heuristic
 bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStream_t stream);
+// rows of 12 ints: P H W KH KW cin cout small epi_class cfg BM BN
+int conv_tuned_table(int* out, int max_rows);
 
 struct ConvWgradArgs {
   const uint16_t* g;  // dL/d(pre-activation), NHWC bf16, offset to channel 0

@@ -72,5 +72,15 @@ def main():
         tot_ours * 1e3, tot_miopen * 1e3, tot_wg * 1e3))
 
 
+
+
+def print_tuned():
+    t = torch.ops.raft_amd.conv_tune_table()
+    print('autotuned conv configs: P H W KH KW cin cout small epi_class cfg BM BN')
+    for i in range(0, len(t), 12):
+        print('  ', t[i:i + 12])
+
+
 if __name__ == '__main__':
     main()
+    print_tuned()
