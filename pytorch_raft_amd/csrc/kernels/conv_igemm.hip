@@ -154,10 +154,10 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
     for (int j = 0; j < B_PER; ++j) {
       const int e = tid + j * NT;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (e < B_CHUNKS) {
-        const int n = n0 + (e >> 3);
+      const int n = n0 + (e >> 3);
+      // rows past cout are zero weights; never read them (the packed tensor may end at cout)
+      if (e < B_CHUNKS && n < a.cout)
         v = *reinterpret_cast<const uint4*>(a.wpk + (int64_t)n * a.kpad + t * BK + (e & 7) * 8);
-      }
       rb[j] = v;
     }
   };
