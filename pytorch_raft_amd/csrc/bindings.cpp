@@ -538,6 +538,7 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
     TORCH_CHECK(in_off[s] >= 0 && in_off[s] + in_cnt[s] <= ins[s].size(3), "segment out of range");
     TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
     if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 64 == 0, "segment channels must be a multiple of 64");
+    TORCH_CHECK(ins[s].numel() * 2 < (int64_t(1) << 31), "conv input exceeds the 2 GiB buffer-descriptor range");
     a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
@@ -618,7 +619,10 @@ void conv_wgrad_(const Tensor& g, int64_t g_off, const std::vector<Tensor>& ins,
   TORCH_CHECK(!ins.empty() && ins.size() <= 3, "1..3 input segments");
   const int64_t B = g.size(0), H = g.size(1), W = g.size(2);
   check_nhwc(g, B, H, W, "grad", at::kBFloat16);
-  TORCH_CHECK(g_off >= 0 && g_off + cout <= g.size(3), "grad slice out of range");
+  // the kernel reads G in whole 8-channel chunks: the slice rounded up to 8 must lie in the row
+  TORCH_CHECK(g_off >= 0 && g_off % 8 == 0 && g_off + (cout + 7) / 8 * 8 <= g.size(3),
+              "grad slice out of range (cout rounded up to 8 channels must fit the row)");
+  TORCH_CHECK(g.numel() * 2 < (int64_t(1) << 31), "grad exceeds the 2 GiB buffer-descriptor range");
   c10::DeviceGuard gd(g.device());
   ConvWgradArgs a{};
   a.g = reinterpret_cast<const uint16_t*>(g.data_ptr<at::BFloat16>()) + g_off;
@@ -630,6 +634,8 @@ void conv_wgrad_(const Tensor& g, int64_t g_off, const std::vector<Tensor>& ins,
     TORCH_CHECK(in_off[s] >= 0 && in_off[s] + in_cnt[s] <= ins[s].size(3), "segment out of range");
     TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
     if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 8 == 0, "segment channels must be a multiple of 8");
+    TORCH_CHECK(ins[s].numel() * 2 < (int64_t(1) << 31), "wgrad input exceeds the 2 GiB buffer-descriptor range");
+    TORCH_CHECK(ins[s].numel() * 2 < (int64_t(1) << 31), "conv input exceeds the 2 GiB buffer-descriptor range");
     a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
@@ -678,6 +684,7 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     TORCH_CHECK(in_off[s] >= 0 && in_off[s] + in_cnt[s] <= ins[s].size(3), "segment out of range");
     TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
     if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 64 == 0, "segment channels must be a multiple of 64");
+    TORCH_CHECK(ins[s].numel() * 2 < (int64_t(1) << 31), "conv input exceeds the 2 GiB buffer-descriptor range");
     a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];

@@ -39,9 +39,22 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 constexpr int BK = 64;   // K per pipeline step: one filter tap x 64 channels (128-B LDS rows)
 constexpr int NT = 256;
 
-// 16-B chunk `chunk` (0..7) of LDS row `row` (128 B): XOR swizzle on the row's low 3 bits so the 8
-// lanes of a ds_read_b128 phase (8 consecutive rows, same logical chunk) hit 8 distinct bank groups
-__device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
+// 16-B chunk `chunk` (0..7) of LDS row `row` (128 B).  A 256-B bank row holds two LDS rows; a
+// ds_read_b128 fragment read serves 16 lanes = 16 consecutive rows at one logical chunk per pass, so
+// the XOR key is (row >> 1) & 7: each row-parity class of the 16 rows lands on 8 distinct 16-B
+// slots and the pass is conflict-free (the ds_write_b128 tile stores stay conflict-free too).
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ ((row >> 1) & 7)); }
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t OOB = 0x80000000u;  // voffset past every num_records: the load returns zeros
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 buf_load16(rsrc_t r, uint32_t voff) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+  return __builtin_bit_cast(uint4, v);
+}
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + __expf(-v)); }
 __device__ __forceinline__ float tanhf_(float v) {
@@ -84,22 +97,30 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
 
   // per-thread A rows (fixed over the K loop): chunk e -> row e>>3, 16-B column e&7;
-  // kept as (image row b*H + y, x) with y = -2^20 marking rows past P
-  int a_by[A_PER], a_x[A_PER];
+  // (pixel index, y, x) with y = -2^20 marking rows past P
+  int a_pix[A_PER], a_y[A_PER], a_x[A_PER];
 #pragma unroll
   for (int j = 0; j < A_PER; ++j) {
     const int e = tid + j * NT;
     const int m = m0 + (e >> 3);
     const int mm = m < P ? m : 0;
-    const int b = mm / HW;
-    const int r = mm - b * HW;
-    const int y = r / a.W;
-    a_x[j] = r - y * a.W;
-    a_by[j] = m < P ? b * a.H + y : -(1 << 20);
+    const int r = mm % HW;
+    a_pix[j] = mm;
+    a_y[j] = m < P ? r / a.W : -(1 << 20);
+    a_x[j] = r % a.W;
   }
 
   const int nchunk = SMALLC ? 0 : a.cin_pad / BK;
   const int steps = SMALLC ? a.kpad / BK : a.KH * a.KW * nchunk;
+  // buffer descriptors: out-of-range offsets (padding taps, rows past P, weight rows past cout)
+  // read as zeros with no branch and no register pre-zeroing
+  rsrc_t seg_rs[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int qq = q < a.nseg ? q : 0;
+    seg_rs[q] = make_rsrc(a.seg[qq].ptr, (uint32_t)P * a.seg[qq].stride * 2u);
+  }
+  const rsrc_t w_rs = make_rsrc(a.wpk, (uint32_t)a.cout * a.kpad * 2u);
 
   auto load = [&](int t, uint4 (&ra)[A_PER], uint4 (&rb)[B_PER]) {
     if constexpr (!SMALLC) {
@@ -110,19 +131,18 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
 #pragma unroll
       for (int q = 0; q < 2; ++q)
         if (s + 1 < a.nseg && c0 >= sbase + a.seg[s].cnt) { sbase += a.seg[s].cnt; ++s; }
-      const Seg sg = a.seg[s];
+      const rsrc_t rs = s == 0 ? seg_rs[0] : (s == 1 ? seg_rs[1] : seg_rs[2]);
+      const int stride = a.seg[s].stride;
+      const int dy = kh - a.PH, dx = kw - a.PW;
+      const int dpix = dy * a.W + dx;
+      const int coff = c0 - sbase;
 #pragma unroll
       for (int j = 0; j < A_PER; ++j) {
         const int e = tid + j * NT;
-        const int y = a_by[j] % a.H;  // negative for rows past P
-        const int yy = y + kh - a.PH, xx = a_x[j] + kw - a.PW;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (a_by[j] >= 0 && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
-          const uint16_t* p = sg.ptr + ((int64_t)(a_by[j] + kh - a.PH) * a.W + xx) * sg.stride +
-                              (c0 - sbase) + (e & 7) * 8;
-          v = *reinterpret_cast<const uint4*>(p);
-        }
-        ra[j] = v;
+        const int yy = a_y[j] + dy, xx = a_x[j] + dx;
+        const bool ok = (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+        const uint32_t off = (uint32_t)(((a_pix[j] + dpix) * stride + coff + (e & 7) * 8) * 2);
+        ra[j] = buf_load16(rs, ok ? off : OOB);
       }
     } else {
       // dense K = tap * cs + c ; each thread gathers 8 consecutive k of one row per chunk
@@ -137,12 +157,12 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
         for (int q = 0; q < 8; ++q) {
           const int k = t * BK + (e & 7) * 8 + q;
           uint16_t v = 0;
-          if (a_by[j] >= 0 && k < ktot) {
+          if (a_y[j] >= 0 && k < ktot) {
             const int tap = k / cs, c = k - tap * cs;
             const int kh = tap / a.KW, kw = tap - kh * a.KW;
-            const int yy = a_by[j] % a.H + kh - a.PH, xx = a_x[j] + kw - a.PW;
+            const int yy = a_y[j] + kh - a.PH, xx = a_x[j] + kw - a.PW;
             if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
-              v = sg.ptr[((int64_t)(a_by[j] + kh - a.PH) * a.W + xx) * sg.stride + c];
+              v = sg.ptr[(int64_t)(a_pix[j] + (kh - a.PH) * a.W + (kw - a.PW)) * sg.stride + c];
           }
           vals[q] = v;
         }
@@ -153,12 +173,10 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
 #pragma unroll
     for (int j = 0; j < B_PER; ++j) {
       const int e = tid + j * NT;
-      uint4 v = make_uint4(0, 0, 0, 0);
       const int n = n0 + (e >> 3);
-      // rows past cout are zero weights; never read them (the packed tensor may end at cout)
-      if (e < B_CHUNKS && n < a.cout)
-        v = *reinterpret_cast<const uint4*>(a.wpk + (int64_t)n * a.kpad + t * BK + (e & 7) * 8);
-      rb[j] = v;
+      // rows past cout read as zeros (range-checked descriptor); the packed tensor may end there
+      const uint32_t off = (uint32_t)(((int64_t)n * a.kpad + t * BK + (e & 7) * 8) * 2);
+      rb[j] = buf_load16(w_rs, e < B_CHUNKS ? off : OOB);
     }
   };
   auto store = [&](int buf, const uint4 (&ra)[A_PER], const uint4 (&rb)[B_PER]) {
@@ -207,33 +225,37 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
   if constexpr (TM * TN >= 8) {
     // big wave tiles: one register set (the step's 32+ MFMAs per wave cover one load latency)
     uint4 ra[A_PER], rb[B_PER];
+    const int last = steps - 1;
     load(0, ra, rb);
     store(0, ra, rb);
     __syncthreads();
     for (int t = 0; t < steps; ++t) {
       const int cur = t & 1;
-      if (t + 1 < steps) load(t + 1, ra, rb);
+      load(min(t + 1, last), ra, rb);
       compute(cur);
-      if (t + 1 < steps) store(cur ^ 1, ra, rb);
+      store(cur ^ 1, ra, rb);
       __syncthreads();
     }
   } else {
+    // loads / stores are unconditional (the last steps re-load the final K step): no branch
+    // around a memory op, so hipcc's counted waits keep the newer register set in flight
     uint4 ra0[A_PER], rb0[B_PER], ra1[A_PER], rb1[B_PER];
+    const int last = steps - 1;
     load(0, ra0, rb0);
-    if (steps > 1) load(1, ra1, rb1);
+    load(min(1, last), ra1, rb1);
     store(0, ra0, rb0);
     __syncthreads();
     for (int t = 0; t < steps; t += 2) {
       // even step: LDS[0] = step t, regs1 = step t+1 (in flight), regs0 free
-      if (t + 2 < steps) load(t + 2, ra0, rb0);
+      load(min(t + 2, last), ra0, rb0);
       compute(0);
-      if (t + 1 < steps) store(1, ra1, rb1);
+      store(1, ra1, rb1);
       __syncthreads();
       if (t + 1 >= steps) break;
       // odd step: LDS[1] = step t+1, regs0 = step t+2 (in flight), regs1 free
-      if (t + 3 < steps) load(t + 3, ra1, rb1);
+      load(min(t + 3, last), ra1, rb1);
       compute(1);
-      if (t + 2 < steps) store(0, ra0, rb0);
+      store(0, ra0, rb0);
       __syncthreads();
     }
   }

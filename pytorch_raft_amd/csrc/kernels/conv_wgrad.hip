@@ -52,74 +52,117 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(ConvWgradArgs a, floa
   const int p_begin = blockIdx.y * a.pix_per_split;
   const int p_end = min(P, p_begin + a.pix_per_split);
   const int ktot_small = a.KH * a.KW * a.cin_small;
+  typedef __amdgpu_buffer_rsrc_t rsrc_t;
+  constexpr uint32_t OOB = 0x80000000u;  // past every num_records: the buffer load returns zeros
+  auto mk = [](const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  };
+  auto ld16 = [](rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  };
+  const rsrc_t g_rs = mk(a.g, (uint32_t)P * a.g_stride * 2u);
+  rsrc_t seg_rs[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int qq = q < a.nseg ? q : 0;
+    seg_rs[q] = mk(a.seg[qq].ptr, (uint32_t)P * a.seg[qq].stride * 2u);
+  }
+
+  // G chunks: fixed column n per thread, row (pixel) advances by BKP per step
+  int g_row[G_PER];
+  bool g_ok[G_PER];
+#pragma unroll
+  for (int j = 0; j < G_PER; ++j) {
+    const int e = tid + j * NT;
+    g_row[j] = e / (BM / 8);
+    g_ok[j] = e < GCH && m0 + (e % (BM / 8)) * 8 < a.cout;
+  }
+  // X chunks: the packed-K column (tap, channel, segment) is fixed per thread -> decoded once;
+  // the pixel (p, y, x) of each chunk is advanced incrementally by BKP per step
+  int x_dpix[X_PER], x_dy[X_PER], x_dx[X_PER], x_coff[X_PER], x_seg[X_PER], x_stride[X_PER];
+  int x_p[X_PER], x_y[X_PER], x_x[X_PER];
+  bool x_ok[X_PER];
+#pragma unroll
+  for (int j = 0; j < X_PER; ++j) {
+    const int e = tid + j * NT;
+    const int row = e / (BN / 8), ch = e % (BN / 8);
+    const int kc = k0 + ch * 8;
+    x_ok[j] = e < XCH && kc < a.kpad;
+    int dy = 0, dx = 0, coff = 0, sidx = 0;
+    if (!SMALLC) {
+      const int tap = kc / a.cin_pad, c = kc - tap * a.cin_pad;
+      const int kh = tap / a.KW, kw = tap - kh * a.KW;
+      dy = kh - a.PH;
+      dx = kw - a.PW;
+      int sbase = 0;
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (sidx + 1 < a.nseg && c >= sbase + a.seg[sidx].cnt) { sbase += a.seg[sidx].cnt; ++sidx; }
+      coff = c - sbase;
+    }
+    x_dy[j] = dy;
+    x_dx[j] = dx;
+    x_dpix[j] = dy * a.W + dx;
+    x_coff[j] = coff;
+    x_seg[j] = sidx;
+    x_stride[j] = a.seg[sidx].stride;
+    const int p = p_begin + row;
+    const int pp = p < P ? p : 0;
+    const int r = pp % HW;
+    x_p[j] = p;
+    x_y[j] = r / a.W;
+    x_x[j] = r - (r / a.W) * a.W;
+  }
+  auto advance = [&]() {  // every chunk's pixel += BKP
+#pragma unroll
+    for (int j = 0; j < X_PER; ++j) {
+      x_p[j] += BKP;
+      int xx = x_x[j] + BKP, yy = x_y[j];
+      while (xx >= a.W) { xx -= a.W; yy = (yy + 1 == a.H) ? 0 : yy + 1; }
+      x_x[j] = xx;
+      x_y[j] = yy;
+    }
+  };
 
   auto load = [&](int pbase, uint4 (&rg)[G_PER], uint4 (&rx)[X_PER]) {
 #pragma unroll
     for (int j = 0; j < G_PER; ++j) {
       const int e = tid + j * NT;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (e < GCH) {
-        const int row = e / (BM / 8), ch = e % (BM / 8);
-        const int p = pbase + row, n = m0 + ch * 8;
-        if (p < p_end) {
-          const uint16_t* src = a.g + (int64_t)p * a.g_stride + n;
-          if (n + 8 <= a.cout) {
-            v = *reinterpret_cast<const uint4*>(src);
-          } else if (n < a.cout) {
-            uint16_t t[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) t[q] = (n + q < a.cout) ? src[q] : 0;
-            v = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
-          }
-        }
-      }
-      rg[j] = v;
+      const int p = pbase + g_row[j];
+      const uint32_t off = (uint32_t)(((int64_t)p * a.g_stride + m0 + (e % (BM / 8)) * 8) * 2);
+      rg[j] = ld16(g_rs, (g_ok[j] && p < p_end) ? off : OOB);
     }
 #pragma unroll
     for (int j = 0; j < X_PER; ++j) {
-      const int e = tid + j * NT;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (e < XCH) {
-        const int row = e / (BN / 8), ch = e % (BN / 8);
-        const int p = pbase + row;
-        const int kc = k0 + ch * 8;
-        if (p < p_end && kc < a.kpad) {
-          const int b = p / HW;
-          const int rr = p - b * HW;
-          const int y = rr / a.W, x = rr - (rr / a.W) * a.W;
-          if constexpr (!SMALLC) {
-            const int tap = kc / a.cin_pad, c = kc - tap * a.cin_pad;
+      const int p = x_p[j];
+      if constexpr (!SMALLC) {
+        const int yy = x_y[j] + x_dy[j], xx = x_x[j] + x_dx[j];
+        const bool ok = x_ok[j] && p < p_end && (unsigned)yy < (unsigned)a.H &&
+                        (unsigned)xx < (unsigned)a.W;
+        const uint32_t off = (uint32_t)(((p + x_dpix[j]) * x_stride[j] + x_coff[j]) * 2);
+        const rsrc_t rs = x_seg[j] == 0 ? seg_rs[0] : (x_seg[j] == 1 ? seg_rs[1] : seg_rs[2]);
+        rx[j] = ld16(rs, ok ? off : OOB);
+      } else {
+        const int e = tid + j * NT;
+        const int kc = k0 + (e % (BN / 8)) * 8;
+        uint16_t t[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int k = kc + q;
+          uint16_t val = 0;
+          if (x_ok[j] && p < p_end && k < ktot_small) {
+            const int tap = k / a.cin_small, c = k - tap * a.cin_small;
             const int kh = tap / a.KW, kw = tap - kh * a.KW;
-            const int yy = y + kh - a.PH, xx = x + kw - a.PW;
-            if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W) {
-              int s = 0, sbase = 0;
-#pragma unroll
-              for (int q = 0; q < 2; ++q)
-                if (s + 1 < a.nseg && c >= sbase + a.seg[s].cnt) { sbase += a.seg[s].cnt; ++s; }
-              const Seg sg = a.seg[s];
-              v = *reinterpret_cast<const uint4*>(sg.ptr + ((int64_t)(b * a.H + yy) * a.W + xx) * sg.stride + (c - sbase));
-            }
-          } else {
-            uint16_t t[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const int k = kc + q;
-              uint16_t val = 0;
-              if (k < ktot_small) {
-                const int tap = k / a.cin_small, c = k - tap * a.cin_small;
-                const int kh = tap / a.KW, kw = tap - kh * a.KW;
-                const int yy = y + kh - a.PH, xx = x + kw - a.PW;
-                if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
-                  val = a.seg[0].ptr[((int64_t)(b * a.H + yy) * a.W + xx) * a.seg[0].stride + c];
-              }
-              t[q] = val;
-            }
-            v = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
+            const int yy = x_y[j] + kh - a.PH, xx = x_x[j] + kw - a.PW;
+            if (yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
+              val = a.seg[0].ptr[(int64_t)(p + (kh - a.PH) * a.W + (kw - a.PW)) * a.seg[0].stride + c];
           }
+          t[q] = val;
         }
+        rx[j] = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
       }
-      rx[j] = v;
     }
+    advance();
   };
   auto store = [&](int buf, const uint4 (&rg)[G_PER], const uint4 (&rx)[X_PER]) {
 #pragma unroll
@@ -187,26 +230,26 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(ConvWgradArgs a, floa
     }
   };
 
+  // loads past p_end read zeros (range check), so the pipeline runs unconditionally: no branch
+  // around a memory op, and hipcc keeps the newer register set in flight across each store
   const int steps = (p_end - p_begin + BKP - 1) / BKP;
+  if (steps <= 0) return;
   uint4 rg0[G_PER], rx0[X_PER], rg1[G_PER], rx1[X_PER];
-  if (steps > 0) {
-    load(p_begin, rg0, rx0);
-    if (steps > 1) load(p_begin + BKP, rg1, rx1);
-    store(0, rg0, rx0);
-  }
+  load(p_begin, rg0, rx0);
+  load(p_begin + BKP, rg1, rx1);
+  store(0, rg0, rx0);
   __syncthreads();
   for (int t = 0; t < steps; t += 2) {
-    if (t + 2 < steps) load(p_begin + (t + 2) * BKP, rg0, rx0);
+    load(p_begin + (t + 2) * BKP, rg0, rx0);
     compute(0);
-    if (t + 1 < steps) store(1, rg1, rx1);
+    store(1, rg1, rx1);
     __syncthreads();
     if (t + 1 >= steps) break;
-    if (t + 3 < steps) load(p_begin + (t + 3) * BKP, rg1, rx1);
+    load(p_begin + (t + 3) * BKP, rg1, rx1);
     compute(1);
-    if (t + 2 < steps) store(0, rg0, rx0);
+    store(0, rg0, rx0);
     __syncthreads();
   }
-  if (steps == 0) return;
   if (do_bias) {
     const int c = m0 + tid % BM;
     if (c < a.cout) atomicAdd(db + c, bsum);
