@@ -668,7 +668,9 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
                  int64_t ph, int64_t pw, int64_t cin_small, double scale,
                  const std::vector<Tensor>& outs, const std::vector<int64_t>& out_off,
                  const std::vector<int64_t>& out_cnt, const std::vector<int64_t>& out_real,
-                 const std::vector<int64_t>& out_acc) {
+                 const std::vector<int64_t>& out_acc, const std::vector<Tensor>& relu_y,
+                 const std::vector<int64_t>& relu_off) {
+  TORCH_CHECK(relu_y.size() == relu_off.size(), "relu spec mismatch");
   TORCH_CHECK(!ins.empty() && ins.size() <= 3 && !outs.empty() && outs.size() <= 3, "1..3 segments");
   TORCH_CHECK(in_off.size() == ins.size() && in_cnt.size() == ins.size(), "input spec mismatch");
   TORCH_CHECK(out_off.size() == outs.size() && out_cnt.size() == outs.size() &&
@@ -697,10 +699,27 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   int64_t cout = 0;
   a.noseg = (int)outs.size();
   for (size_t o = 0; o < outs.size(); ++o) {
-    check_nhwc(outs[o], B, H, W, "dgrad output", at::kFloat);
+    const bool relu_mode = outs[o].scalar_type() == at::kBFloat16;
+    check_nhwc(outs[o], B, H, W, "dgrad output", relu_mode ? at::kBFloat16 : at::kFloat);
     TORCH_CHECK(out_real[o] <= out_cnt[o] && out_off[o] >= 0 && out_off[o] + out_real[o] <= outs[o].size(3),
                 "dgrad output slice out of range");
-    a.oseg[o].ptr = outs[o].data_ptr<float>() + out_off[o];
+    if (relu_mode) {
+      // bf16 output = relu-gated gradient; relu_y[o] is the forward relu output of these channels
+      TORCH_CHECK(o < relu_y.size(), "bf16 dgrad output needs its relu output tensor");
+      const Tensor& y = relu_y[o];
+      check_nhwc(y, B, H, W, "relu output", at::kBFloat16);
+      TORCH_CHECK(relu_off[o] >= 0 && relu_off[o] + out_real[o] <= y.size(3), "relu output slice out of range");
+      TORCH_CHECK(!out_acc[o], "the relu-gated bf16 output cannot accumulate");
+      a.oseg[o].ptr = nullptr;
+      a.oseg[o].ob = reinterpret_cast<uint16_t*>(outs[o].data_ptr<at::BFloat16>()) + out_off[o];
+      a.oseg[o].ob_stride = (int)outs[o].size(3);
+      a.oseg[o].ry = reinterpret_cast<const uint16_t*>(y.data_ptr<at::BFloat16>()) + relu_off[o];
+      a.oseg[o].ry_stride = (int)y.size(3);
+    } else {
+      a.oseg[o].ptr = outs[o].data_ptr<float>() + out_off[o];
+      a.oseg[o].ob = nullptr;
+      a.oseg[o].ry = nullptr;
+    }
     a.oseg[o].stride = (int)outs[o].size(3);
     a.oseg[o].cnt = (int)out_cnt[o];
     a.oseg[o].real = (int)out_real[o];
@@ -819,7 +838,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_lookup_nhwc_(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
   m.def("corr_window_grad(Tensor coords, Tensor dout, int levels, int radius) -> Tensor");
   m.def("corr_window_reduce(Tensor[] coords, Tensor[] wgs, int H, int W, int levels, int radius, float inv_sqrt_c) -> Tensor");
-  m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc) -> ()");
+  m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off) -> ()");
   m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale) -> ()");
   m.def("gru_q_bwd_(Tensor dh, Tensor z, Tensor q, Tensor hprev, Tensor(a!) dpre_q, Tensor(b!) dz, Tensor(c!) dhprev) -> ()");
   m.def("gru_zr_bwd_(Tensor drh, Tensor dz, Tensor z, Tensor r, Tensor hprev, Tensor(a!) dpre_zr, Tensor(b!) dhprev) -> ()");

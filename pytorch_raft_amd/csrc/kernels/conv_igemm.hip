@@ -261,6 +261,9 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
   }
 
   // ---------------------------------------------------------------- fused epilogue
+  // Two phases per 32x32 accumulator tile: every load the epilogue needs (aux operands, the old
+  // value of an accumulated output) is issued first, then the stores.  Interleaved load/store
+  // pairs through possibly-aliasing pointers would serialize into one memory round trip each.
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -268,9 +271,61 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
       const int n = n0 + wn * WN + j * 32 + (lane & 31);
       if (n >= a.cout) continue;
       const float bias = a.bias ? a.bias[n] : 0.f;
+      int mrow[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mrow[r] = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      // DGRAD: the column's output segment (fixed per lane for this tile)
+      float* dptr = nullptr;
+      int dstride = 0;
+      bool dacc = false;
+      uint16_t* bptr = nullptr;
+      const uint16_t* yptr = nullptr;
+      int bstride = 0, ystride = 0;
+      if constexpr (EPI == EPI_DGRAD) {
+        int s = 0, base = 0;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          if (s + 1 < a.noseg && n >= base + a.oseg[s].cnt) { base += a.oseg[s].cnt; ++s; }
+        const OSeg o = a.oseg[s];
+        const int c = n - base;
+        if (c < o.real) {
+          if (o.ob != nullptr) {
+            bptr = o.ob + c;
+            bstride = o.ob_stride;
+            yptr = o.ry + c;
+            ystride = o.ry_stride;
+          } else if (o.ptr != nullptr) {
+            dptr = o.ptr + c;
+            dstride = o.stride;
+            dacc = o.acc != 0;
+          }
+        }
+      }
+      float pre0[16], pre1[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int m = mrow[r];
+        const bool ok = m < P;
+        pre0[r] = 0.f;
+        pre1[r] = 0.f;
+        if constexpr (EPI == EPI_ACC_F32) {
+          if (ok) pre0[r] = ((const float*)a.out0)[(int64_t)m * a.out0_stride + n];
+        } else if constexpr (EPI == EPI_DGRAD) {
+          if (ok && dacc) pre0[r] = dptr[(int64_t)m * dstride];
+          if (ok && yptr != nullptr) pre0[r] = raft_bf16_to_f32(yptr[(int64_t)m * ystride]);
+        } else if constexpr (EPI == EPI_GRU_ZR) {
+          if (ok && n >= a.split)
+            pre0[r] = raft_bf16_to_f32(a.aux0[(int64_t)m * a.aux0_stride + (n - a.split)]);
+        } else if constexpr (EPI == EPI_GRU_Q) {
+          if (ok) {
+            pre0[r] = raft_bf16_to_f32(a.aux0[(int64_t)m * a.aux0_stride + n]);
+            pre1[r] = raft_bf16_to_f32(a.aux1[(int64_t)m * a.aux1_stride + n]);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mrow[r];
         if (m >= P) continue;
         const float v = (acc[i][j][r] + bias) * a.scale;
         if constexpr (EPI == EPI_BF16) {
@@ -280,36 +335,26 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
         } else if constexpr (EPI == EPI_F32) {
           ((float*)a.out0)[(int64_t)m * a.out0_stride + n] = v;
         } else if constexpr (EPI == EPI_ACC_F32) {
-          ((float*)a.out0)[(int64_t)m * a.out0_stride + n] += v;
+          ((float*)a.out0)[(int64_t)m * a.out0_stride + n] = pre0[r] + v;
         } else if constexpr (EPI == EPI_GRU_ZR) {
           const float g = sigmoidf_(v);
           if (n < a.split) {
             ((uint16_t*)a.out0)[(int64_t)m * a.out0_stride + n] = raft_f32_to_bf16(g);  // z
           } else {
             const int c = n - a.split;
-            const float h = raft_bf16_to_f32(a.aux0[(int64_t)m * a.aux0_stride + c]);
-            ((uint16_t*)a.out1)[(int64_t)m * a.out1_stride + c] = raft_f32_to_bf16(g * h);  // r*h
-            ((uint16_t*)a.out2)[(int64_t)m * a.out2_stride + c] = raft_f32_to_bf16(g);      // r
+            ((uint16_t*)a.out1)[(int64_t)m * a.out1_stride + c] = raft_f32_to_bf16(g * pre0[r]);  // r*h
+            ((uint16_t*)a.out2)[(int64_t)m * a.out2_stride + c] = raft_f32_to_bf16(g);            // r
           }
         } else if constexpr (EPI == EPI_DGRAD) {
           // output channel n -> one of up to 3 fp32 gradient buffers (store or accumulate)
-          int s = 0, base = 0;
-#pragma unroll
-          for (int q = 0; q < 2; ++q)
-            if (s + 1 < a.noseg && n >= base + a.oseg[s].cnt) { base += a.oseg[s].cnt; ++s; }
-          const OSeg o = a.oseg[s];
-          const int c = n - base;
-          if (o.ptr != nullptr && c < o.real) {
-            float* dst = o.ptr + (int64_t)m * o.stride + c;
-            if (o.acc) *dst += v; else *dst = v;
-          }
+          if (dptr != nullptr) dptr[(int64_t)m * dstride] = dacc ? pre0[r] + v : v;
+          if (bptr != nullptr) bptr[(int64_t)m * bstride] = raft_f32_to_bf16(pre0[r] > 0.f ? v : 0.f);
         } else if constexpr (EPI == EPI_F32_NCHW) {
           const int b = m / HW, yx = m - b * HW;
           ((float*)a.out0)[((int64_t)b * a.cout + n) * HW + yx] = v;
         } else if constexpr (EPI == EPI_GRU_Q) {
           const float q = tanhf_(v);
-          const float h = raft_bf16_to_f32(a.aux0[(int64_t)m * a.aux0_stride + n]);
-          const float z = raft_bf16_to_f32(a.aux1[(int64_t)m * a.aux1_stride + n]);
+          const float h = pre0[r], z = pre1[r];
           ((uint16_t*)a.out0)[(int64_t)m * a.out0_stride + n] = raft_f32_to_bf16(h + z * (q - h));
           ((uint16_t*)a.out1)[(int64_t)m * a.out1_stride + n] = raft_f32_to_bf16(q);
         }

@@ -93,6 +93,12 @@ struct OSeg {
   int cnt;     // channel slots of this segment in the conv's output
   int real;    // channels actually written (< cnt for zero-padded slots)
   int acc;     // 1: +=, 0: =
+  // relu-gated bf16 mode (ob != null): ob = bf16(ry > 0 ? v : 0) -- the gradient w.r.t. the
+  // pre-activation of a ReLU whose output ry is this segment's forward input (fuses relu_bwd)
+  uint16_t* ob;
+  int ob_stride;
+  const uint16_t* ry;
+  int ry_stride;
 };
 
 struct ConvFwdArgs {

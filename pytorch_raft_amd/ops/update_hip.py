@@ -261,28 +261,31 @@ class _UpdateIter(torch.autograd.Function):
                          cin_small=2 if s.small else 0)
 
         def dgrad(name, gsegs, outs, small=False, scale=1.0):
-            """outs: list of (buffer fp32, offset, slot_cnt, real, acc)."""
+            """outs: list of (buffer fp32, offset, slot_cnt, real, acc) or, fusing the backward of a
+            ReLU, (buffer bf16, offset, slot_cnt, real, 0, relu_out, relu_out_offset)."""
             s = SPEC[name]
+            ry = [o[5] if len(o) > 5 else o[0] for o in outs]
+            roff = [int(o[6]) if len(o) > 5 else 0 for o in outs]
             ops.conv_dgrad_([g[0] for g in gsegs], [g[1] for g in gsegs], [g[2] for g in gsegs],
                             pk.wd[name], s.k[0], s.k[1], s.pad[0], s.pad[1], 2 if small else 0,
                             float(scale), [o[0] for o in outs], [o[1] for o in outs],
-                            [o[2] for o in outs], [o[3] for o in outs], [o[4] for o in outs])
+                            [o[2] for o in outs], [o[3] for o in outs], [o[4] for o in outs],
+                            ry, roff)
 
         # ---- mask head (mask = 0.25 * conv(fm[256:]))
         gmask = gmask.contiguous()
         if gmask.dtype != torch.bfloat16:
             gmask = gmask.to(torch.bfloat16)
-        dfm = _f32(sh + (512,), dev)
+        # the head's ReLU backward is fused into both dgrad epilogues (bf16 pre-activation grads)
+        dpre_head = _bf16(sh + (512,), dev)
         wgrad('m2', gmask, 0, [(fm, 256, 256)])
-        dgrad('m2', [(gmask, 0, 576)], [(dfm, 256, 256, 256, 0)], scale=0.25)
+        dgrad('m2', [(gmask, 0, 576)], [(dpre_head, 256, 256, 256, 0, fm, 256)], scale=0.25)
         # ---- flow head conv2 -> delta
         gd = torch.zeros(*sh, 8, device=dev, dtype=torch.bfloat16)
         ops.flow_prep_(gdelta.contiguous().float(), gd, None, 0)
         wgrad('fh2', gd, 0, [(fm, 0, 256)])
-        dgrad('fh2', [(gd, 0, 8)], [(dfm, 0, 256, 256, 0)], small=True)
-        # ---- head (relu)
-        dpre_head = _bf16(sh + (512,), dev)
-        ops.relu_bwd_(dfm, 0, fm, 0, dpre_head, 0, 512, 1.0)
+        dgrad('fh2', [(gd, 0, 8)], [(dpre_head, 0, 256, 256, 0, fm, 0)], small=True)
+        # ---- head
         wgrad('head', dpre_head, 0, [(h2, 0, HD)])
         dh = gh.float().contiguous() if gh is not None else _f32(sh + (HD,), dev, zero=True)
         dgrad('head', [(dpre_head, 0, 512)], [(dh, 0, HD, HD, 1)])
@@ -308,21 +311,15 @@ class _UpdateIter(torch.autograd.Function):
         dpre_conv = _bf16(sh + (128,), dev)
         ops.relu_bwd_(dmf, 0, mf, 0, dpre_conv, 0, 128, 1.0)
         wgrad('conv', dpre_conv, 0, [(cf, 0, 256)])
-        dcf = _f32(sh + (256,), dev)
-        dgrad('conv', [(dpre_conv, 0, 128)], [(dcf, 0, 256, 256, 0)])
         dpre_cf = _bf16(sh + (256,), dev)
-        ops.relu_bwd_(dcf, 0, cf, 0, dpre_cf, 0, 256, 1.0)
+        dgrad('conv', [(dpre_conv, 0, 128)], [(dpre_cf, 0, 256, 256, 0, cf, 0)])
         wgrad('c2', dpre_cf, 0, [(c1, 0, 256)])
         wgrad('f2', dpre_cf, 192, [(f1, 0, 128)])
-        dc1 = _f32(sh + (256,), dev)
-        dgrad('c2', [(dpre_cf, 0, 192)], [(dc1, 0, 256, 256, 0)])
-        df1 = _f32(sh + (128,), dev)
-        dgrad('f2', [(dpre_cf, 192, 64)], [(df1, 0, 128, 128, 0)])
-        dpre_f1 = _bf16(sh + (128,), dev)
-        ops.relu_bwd_(df1, 0, f1, 0, dpre_f1, 0, 128, 1.0)
-        wgrad('f1', dpre_f1, 0, [(flowb, 0, 8)])
         dpre_c1 = _bf16(sh + (256,), dev)
-        ops.relu_bwd_(dc1, 0, c1, 0, dpre_c1, 0, 256, 1.0)
+        dgrad('c2', [(dpre_cf, 0, 192)], [(dpre_c1, 0, 256, 256, 0, c1, 0)])
+        dpre_f1 = _bf16(sh + (128,), dev)
+        dgrad('f2', [(dpre_cf, 192, 64)], [(dpre_f1, 0, 128, 128, 0, f1, 0)])
+        wgrad('f1', dpre_f1, 0, [(flowb, 0, 8)])
         wgrad('c1', dpre_c1, 0, [(corr, 0, CORR_BUF)])
         dcorr = _f32(sh + (CORR_BUF,), dev)
         dgrad('c1', [(dpre_c1, 0, 256)], [(dcorr, 0, CORR_BUF, 324, 0)])  # slots 324.. unused

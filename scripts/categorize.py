@@ -1,0 +1,27 @@
+"""Group a prof_diff.py kernel summary into categories (ms/step)."""
+import re
+import sys
+
+CATS = [('ours conv fwd', r'conv_fwd_kernel<[^>]*, [0-57], (true|false)>'),
+        ('ours dgrad', r'conv_fwd_kernel<[^>]*, 6, '), ('ours wgrad', r'conv_wgrad'),
+        ('miopen conv', r'igemm|grouped_conv|naive_conv|gemm|Conv'), ('transpose', r'transpose'),
+        ('bn/norm', r'batch_norm|BatchNorm|InstanceNorm|instance_norm|welford|Norm'),
+        ('reduce', r'reduce_kernel'),
+        ('elementwise', r'elementwise|vectorized|SubTensor|OpTensor|Cast|copy_kernel|unrolled'),
+        ('corr', r'corr_'), ('upsample', r'convex'), ('update ew', r'relu_bwd|gru_|flow_prep'),
+        ('copy', r'copyBuffer'), ('loss', r'seq_loss'), ('adam', r'adam|Adam|multi_tensor')]
+tot = {}
+for line in open(sys.argv[1]):
+    if not re.match(r'\s*[\d.]+%', line):
+        continue
+    parts = line.split(None, 4)
+    ms, name = float(parts[3]), parts[4]
+    for c, pat in CATS:
+        if re.search(pat, name):
+            tot[c] = tot.get(c, 0) + ms
+            break
+    else:
+        tot['other'] = tot.get('other', 0) + ms
+for c, v in sorted(tot.items(), key=lambda x: -x[1]):
+    print('%-15s %7.2f' % (c, v))
+print('%-15s %7.2f' % ('total(top70)', sum(tot.values())))

@@ -173,3 +173,22 @@ def test_conv_wgrad_small_cin(ext_ops):
     C.conv_wgrad(C.nhwc(g), 0, [(buf, 0, 8)], (7, 7), (3, 3), 128, dw, None, cin_small=2)
     got = C.unpack_weight_grad_small(dw, 128, 2, (7, 7))
     torch.testing.assert_close(got, w.grad, atol=2e-3 * w.grad.abs().max().item(), rtol=1e-3)
+
+
+def test_conv_dgrad_relu_gated_bf16(ext_ops):
+    """conv_dgrad_ with a bf16 output segment: the ReLU backward of the layer below is fused in."""
+    torch.manual_seed(7)
+    B, H, W, cin, cout, k = 2, 12, 16, 256, 192, (3, 3)
+    pad = (1, 1)
+    x = torch.randn(B, cin, H, W, device=DEV, requires_grad=True)
+    w = (torch.randn(cout, cin, *k, device=DEV) / 30).to(torch.bfloat16).float()
+    g = torch.randn(B, cout, H, W, device=DEV).to(torch.bfloat16).float()
+    F.conv2d(x, w, None, padding=pad).backward(g)
+    y = torch.randn(B, H, W, cin + 64, device=DEV).relu().to(torch.bfloat16)  # relu output, offset 32
+    ref = x.grad * (y[..., 32:32 + cin].permute(0, 3, 1, 2).float() > 0)
+    out = torch.full((B, H, W, cin + 16), 7.0, device=DEV, dtype=torch.bfloat16)
+    wd = C.pack_weight_dgrad(w, [cout], [cout])
+    torch.ops.raft_amd.conv_dgrad_([C.nhwc(g)], [0], [cout], wd, 3, 3, 1, 1, 0, 1.0, [out], [8],
+                                   [cin], [cin], [0], [y], [32])
+    torch.testing.assert_close(C.nchw(out[..., 8:8 + cin]).float(), ref, atol=2e-2, rtol=2e-2)
+    assert torch.all(out[..., :8] == 7.0) and torch.all(out[..., 8 + cin:] == 7.0)
