@@ -740,6 +740,123 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   TORCH_CHECK(launch_conv_fwd(a, EPI_DGRAD, bn, cin_small != 0, cur_stream()), "dgrad launch");
 }
 
+// ------------------------------------------------------------------ encoder norm + activation
+// Tensors are NCHW-shaped channels_last bf16 (the memory is NHWC).
+void check_cl_bf16(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4, name,
+              ": must be a 4-D bf16 GPU tensor");
+  TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name, ": must be channels_last");
+  TORCH_CHECK(t.size(1) % 8 == 0 && t.size(1) <= 256, name, ": channels must be a multiple of 8, <= 256");
+}
+const float* opt_f32(const c10::optional<Tensor>& t, int64_t n, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_cuda_f32(*t, name);
+  TORCH_CHECK(t->numel() == n, name, ": size mismatch");
+  return t->data_ptr<float>();
+}
+
+// y = act(norm(x + cbias)) [+ res, relu]; returns (mean, invstd) for the backward
+std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
+                              const c10::optional<Tensor>& gamma, const c10::optional<Tensor>& beta,
+                              const c10::optional<Tensor>& cbias,
+                              const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
+                              double momentum, double eps, const c10::optional<Tensor>& res,
+                              const Tensor& y) {
+  check_cl_bf16(x, "x");
+  check_cl_bf16(y, "y");
+  TORCH_CHECK(y.sizes() == x.sizes(), "y shape");
+  TORCH_CHECK(mode >= 0 && mode <= 3, "mode");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  c10::DeviceGuard g(x.device());
+  const float* gp = opt_f32(gamma, C, "gamma");
+  const float* bp = opt_f32(beta, C, "beta");
+  const float* cb = opt_f32(cbias, C, "conv bias");
+  float* rm = const_cast<float*>(opt_f32(rmean, C, "running_mean"));
+  float* rv = const_cast<float*>(opt_f32(rvar, C, "running_var"));
+  if (mode == 2) TORCH_CHECK(rm && rv, "eval batch norm needs running stats");
+  const uint16_t* rp = nullptr;
+  if (res.has_value() && res->defined()) {
+    check_cl_bf16(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes(), "res shape");
+    rp = reinterpret_cast<const uint16_t*>(res->data_ptr<at::BFloat16>());
+  }
+  const int groups = mode == 0 ? (int)N : 1;
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({groups, C}, fo), invstd = at::empty({groups, C}, fo);
+  Tensor scale = at::empty({N, C}, fo), shift = at::empty({N, C}, fo);
+  const uint16_t* xp = reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>());
+  int ppb = 0, nblk = 0;
+  Tensor part;
+  if (mode <= 1) {
+    nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
+    part = at::empty({groups, nblk, 2, C}, fo);
+    launch_norm_stats(xp, (int)N, (int)HW, (int)C, mode == 0, part.data_ptr<float>(), nblk, ppb,
+                      cur_stream());
+  }
+  launch_norm_finalize(mode <= 1 ? part.data_ptr<float>() : nullptr, xp, (int)N, (int)HW, (int)C,
+                       (int)mode, nblk, gp, bp, cb, rm, rv, (float)momentum, (float)eps,
+                       mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                       shift.data_ptr<float>(), cur_stream());
+  launch_norm_apply(xp, scale.data_ptr<float>(), shift.data_ptr<float>(), (int)N, (int)HW, (int)C,
+                    (int)relu, rp, reinterpret_cast<uint16_t*>(y.data_ptr<at::BFloat16>()), cur_stream());
+  return {mean, invstd};
+}
+
+// dx (bf16) and += parameter grads; y = the forward output when relu (mask), else ignored
+void norm_bwd_(const Tensor& dy, const Tensor& y, const Tensor& x, const Tensor& mean,
+               const Tensor& invstd, int64_t mode, int64_t relu, const c10::optional<Tensor>& gamma,
+               const c10::optional<Tensor>& dgamma, const c10::optional<Tensor>& dbeta,
+               const c10::optional<Tensor>& dcbias, const Tensor& dx) {
+  check_cl_bf16(dy, "dy");
+  check_cl_bf16(y, "y");
+  check_cl_bf16(x, "x");
+  check_cl_bf16(dx, "dx");
+  TORCH_CHECK(dy.sizes() == x.sizes() && y.sizes() == x.sizes() && dx.sizes() == x.sizes(), "shapes");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  const int groups = mode == 0 ? (int)N : 1;
+  check_cuda_f32(mean, "mean");
+  check_cuda_f32(invstd, "invstd");
+  TORCH_CHECK(mean.numel() == groups * C && invstd.numel() == groups * C, "stat shapes");
+  c10::DeviceGuard g(x.device());
+  const float* gp = opt_f32(gamma, C, "gamma");
+  float* dg = const_cast<float*>(opt_f32(dgamma, C, "dgamma"));
+  float* db = const_cast<float*>(opt_f32(dbeta, C, "dbeta"));
+  float* dc = const_cast<float*>(opt_f32(dcbias, C, "dcbias"));
+  int ppb = 0;
+  const int nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor part = at::empty({groups, nblk, 3, C}, fo);
+  Tensor coef = at::empty({groups, C, 3}, fo);
+  launch_norm_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr<at::BFloat16>()),
+                  reinterpret_cast<const uint16_t*>(y.data_ptr<at::BFloat16>()),
+                  reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>()), mean.data_ptr<float>(),
+                  invstd.data_ptr<float>(), (int)N, (int)HW, (int)C, (int)mode, (int)relu, gp,
+                  part.data_ptr<float>(), nblk, ppb, coef.data_ptr<float>(), dg, db, dc,
+                  reinterpret_cast<uint16_t*>(dx.data_ptr<at::BFloat16>()), cur_stream());
+}
+
+void add_relu_(const Tensor& a, const Tensor& b, const Tensor& out) {
+  check_cl_bf16(a, "a");
+  check_cl_bf16(b, "b");
+  check_cl_bf16(out, "out");
+  TORCH_CHECK(a.sizes() == b.sizes() && out.sizes() == a.sizes(), "shapes");
+  c10::DeviceGuard g(a.device());
+  launch_add_relu(reinterpret_cast<const uint16_t*>(a.data_ptr<at::BFloat16>()),
+                  reinterpret_cast<const uint16_t*>(b.data_ptr<at::BFloat16>()),
+                  reinterpret_cast<uint16_t*>(out.data_ptr<at::BFloat16>()), a.numel(), cur_stream());
+}
+
+void relu_mask_(const Tensor& dy, const Tensor& y, const Tensor& g) {
+  check_cl_bf16(dy, "dy");
+  check_cl_bf16(y, "y");
+  check_cl_bf16(g, "g");
+  TORCH_CHECK(dy.sizes() == y.sizes() && g.sizes() == y.sizes(), "shapes");
+  c10::DeviceGuard gd(y.device());
+  launch_relu_mask(reinterpret_cast<const uint16_t*>(dy.data_ptr<at::BFloat16>()),
+                   reinterpret_cast<const uint16_t*>(y.data_ptr<at::BFloat16>()),
+                   reinterpret_cast<uint16_t*>(g.data_ptr<at::BFloat16>()), y.numel(), cur_stream());
+}
+
 // ------------------------------------------------------------------ update-block elementwise
 const uint16_t* bf16p(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr<at::BFloat16>()); }
 uint16_t* bf16m(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr<at::BFloat16>()); }
@@ -832,6 +949,10 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_otf_fwd_(Tensor f1, Tensor[] f2, Tensor coords, int radius, Tensor(a!) out, Tensor[] lo) -> ()");
   m.def("corr_otf_bwd_(Tensor f1, Tensor[] f2, Tensor coords, Tensor dout, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("conv_tune_table() -> int[]", &conv_tune_table);
+  m.def("norm_fwd_(Tensor x, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor? cbias, Tensor(a!)? rmean, Tensor(b!)? rvar, float momentum, float eps, Tensor? res, Tensor(c!) y) -> Tensor[]");
+  m.def("norm_bwd_(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx) -> ()");
+  m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
+  m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] wgs, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");
   m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout, bool nhwc=False) -> Tensor[]");
@@ -859,6 +980,10 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("corr_otf_fwd_", &corr_otf_fwd_);
   m.impl("corr_otf_bwd_", &corr_otf_bwd_);
   m.impl("corr_otf_window_bwd_", &corr_otf_window_bwd_);
+  m.impl("norm_fwd_", &norm_fwd_);
+  m.impl("norm_bwd_", &norm_bwd_);
+  m.impl("add_relu_", &add_relu_);
+  m.impl("relu_mask_", &relu_mask_);
   m.impl("convex_up_fwd", &convex_up_fwd);
   m.impl("convex_up_bwd", &convex_up_bwd);
   m.impl("seq_loss_fwd", &seq_loss_fwd);

@@ -1,0 +1,429 @@
+// Fused NHWC normalisation + activation for the RAFT encoders (fnet: InstanceNorm, cnet: BatchNorm).
+//
+// Reference: `core/extractor.py:6-56,118-192` -- conv -> norm -> ReLU, residual add -> ReLU, run as
+// NCHW PyTorch ops under autocast.  On ROCm that is MIOpen convs bracketed by NCHW<->NHWC transposes,
+// InstanceNorm lowered to batch_norm on a (1, N*C, H, W) view, separate ReLU / add kernels and an
+// ATen reduction per conv for the bias gradient.  Here the encoders run channels-last (MIOpen NHWC
+// convs, no transposes) and every norm is four memory passes of bf16 NHWC data:
+//
+//   stats     per (image, channel) [instance] or per channel [batch] shifted sums  sum(x-K),
+//             sum((x-K)^2) -> per-workgroup partials (deterministic, no atomics)
+//   finalize  partials -> mean / invstd, the affine fold into one scale/shift per (image, channel),
+//             BatchNorm running-stat update; the conv bias is folded here too (it cancels in a
+//             training-mode norm, and shifts the eval-mode one), so the conv runs without bias
+//   apply     y = act(x * scale + shift) [+ residual, ReLU]     (16-B vectors, 8 channels/thread)
+//   backward  partial sums of g, g*xhat, xhat (g = dy masked by the ReLU) -> finalize -> one pass
+//             dx = A*g + B*xhat + C.  The conv-bias gradient falls out of the same sums.
+//
+// Channel counts are multiples of 8 up to 256; a thread owns one 16-B channel group of a pixel.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ void unpack8(uint4 v, float (&f)[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = (uint32_t)raft_f32_to_bf16(f[2 * i]) | ((uint32_t)raft_f32_to_bf16(f[2 * i + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// grid.x = blocks per group-range, grid.y = image (instance) or 1 (batch: range = all images)
+// partial layout [group_img][blk][2][C]
+__global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restrict__ x, int HW,
+                                                        int C, int per_image, int pix_per_blk,
+                                                        int total_pix, float* __restrict__ part) {
+  __shared__ float red[2][NT * 8];
+  const int cg = C / 8;
+  const int lanes = NT / cg;
+  const int tid = threadIdx.x;
+  const int g = tid % cg, pl = tid / cg;
+  const int img = blockIdx.y;
+  const int64_t base = per_image ? (int64_t)img * HW : 0;
+  const int range = per_image ? HW : total_pix;
+  const int p0 = blockIdx.x * pix_per_blk, p1 = min(range, p0 + pix_per_blk);
+  // shift: the group's first pixel (keeps the one-pass variance well conditioned)
+  float K[8];
+  unpack8(*reinterpret_cast<const uint4*>(x + base * C + g * 8), K);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
+  if (pl < lanes) {
+    for (int p = p0 + pl; p < p1; p += lanes) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + (base + p) * C + g * 8), v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[i] - K[i];
+        s1[i] += d;
+        s2[i] += d * d;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    red[0][tid * 8 + i] = s1[i];
+    red[1][tid * 8 + i] = s2[i];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    const int gg = c / 8, ii = c % 8;
+    float a = 0.f, b = 0.f;
+    for (int l = 0; l < lanes; ++l) {
+      a += red[0][(l * cg + gg) * 8 + ii];
+      b += red[1][(l * cg + gg) * 8 + ii];
+    }
+    float* dst = part + ((int64_t)img * gridDim.x + blockIdx.x) * 2 * C;
+    dst[c] = a;
+    dst[C + c] = b;
+  }
+}
+
+// mode: 0 instance (train or eval: always batch statistics), 1 batch-train, 2 batch-eval, 3 none
+// one thread per (group image, channel)
+__global__ void norm_finalize_kernel(const float* __restrict__ part, const uint16_t* __restrict__ x,
+                                     int HW, int C, int groups_img, int nblk, int cnt, int mode,
+                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                     const float* __restrict__ cbias, float* __restrict__ rmean,
+                                     float* __restrict__ rvar, float momentum, float eps,
+                                     float* __restrict__ mean_out, float* __restrict__ invstd_out,
+                                     float* __restrict__ scale, float* __restrict__ shift, int nimg) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= groups_img * C) return;
+  const int gi = idx / C, c = idx % C;
+  const float b = cbias ? cbias[c] : 0.f;
+  float mean = 0.f, invstd = 1.f;
+  if (mode == 0 || mode == 1) {
+    double a = 0.0, q = 0.0;
+    for (int k = 0; k < nblk; ++k) {
+      const float* p = part + ((int64_t)gi * nblk + k) * 2 * C;
+      a += p[c];
+      q += p[C + c];
+    }
+    const float K = raft_bf16_to_f32(x[(int64_t)(mode == 0 ? gi : 0) * HW * C + c]);
+    const double m = a / cnt;
+    double var = q / cnt - m * m;
+    if (var < 0.0) var = 0.0;
+    mean = (float)(m + K);
+    invstd = (float)(1.0 / sqrt(var + (double)eps));
+    if (mode == 1 && rmean != nullptr) {
+      const double unb = cnt > 1 ? var * cnt / (cnt - 1) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * (mean + b);
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+    }
+  } else if (mode == 2) {
+    mean = rmean[c] - b;  // (x + b - rm) = (x - (rm - b))
+    invstd = 1.f / sqrtf(rvar[c] + eps);
+  } else {
+    mean = -b;  // y = x + b
+    invstd = 1.f;
+  }
+  const float gm = (mode == 1 || mode == 2) && gamma ? gamma[c] : 1.f;
+  const float bt = (mode == 1 || mode == 2) && beta ? beta[c] : 0.f;
+  mean_out[idx] = mean;
+  invstd_out[idx] = invstd;
+  // per-image scale/shift table [nimg][C] (instance: its own group; batch/none: shared)
+  for (int n = (mode == 0 ? gi : 0); n < (mode == 0 ? gi + 1 : nimg); ++n) {
+    scale[(int64_t)n * C + c] = gm * invstd;
+    shift[(int64_t)n * C + c] = bt - mean * gm * invstd;
+  }
+}
+
+// y = act(x*scale + shift) [+ res -> relu];  act: relu when relu != 0
+__global__ __launch_bounds__(NT) void norm_apply_kernel(const uint16_t* __restrict__ x,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, int HW,
+                                                        int C, int64_t nvec, int relu,
+                                                        const uint16_t* __restrict__ res,
+                                                        uint16_t* __restrict__ y) {
+  const int cg = C / 8;
+  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+    const int64_t pix = v / cg;
+    const int g = (int)(v - pix * cg);
+    const int n = (int)(pix / HW);
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), f);
+    const float* sc = scale + (int64_t)n * C + g * 8;
+    const float* sh = shift + (int64_t)n * C + g * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f[i] = f[i] * sc[i] + sh[i];
+      if (relu) f[i] = fmaxf(f[i], 0.f);
+    }
+    if (res) {
+      float r[8];
+      unpack8(*reinterpret_cast<const uint4*>(res + v * 8), r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = fmaxf(f[i] + r[i], 0.f);
+    }
+    *reinterpret_cast<uint4*>(y + v * 8) = pack8(f);
+  }
+}
+
+// out = relu(a + b)
+__global__ __launch_bounds__(NT) void add_relu_kernel(const uint16_t* __restrict__ a,
+                                                      const uint16_t* __restrict__ b,
+                                                      uint16_t* __restrict__ out, int64_t nvec) {
+  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+    float fa[8], fb[8];
+    unpack8(*reinterpret_cast<const uint4*>(a + v * 8), fa);
+    unpack8(*reinterpret_cast<const uint4*>(b + v * 8), fb);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = fmaxf(fa[i] + fb[i], 0.f);
+    *reinterpret_cast<uint4*>(out + v * 8) = pack8(fa);
+  }
+}
+
+// g = dy * [y > 0]   (the ReLU backward, also the block-end residual ReLU)
+__global__ __launch_bounds__(NT) void relu_mask_kernel(const uint16_t* __restrict__ dy,
+                                                       const uint16_t* __restrict__ y,
+                                                       uint16_t* __restrict__ g, int64_t nvec) {
+  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+    const uint4 d = *reinterpret_cast<const uint4*>(dy + v * 8);
+    const uint4 m = *reinterpret_cast<const uint4*>(y + v * 8);
+    const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, mw[4] = {m.x, m.y, m.z, m.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // bf16 > 0  <=>  sign bit clear and magnitude non-zero
+      const uint32_t lo = ((mw[i] & 0x8000u) == 0 && (mw[i] & 0x7fffu) != 0) ? 0xffffu : 0u;
+      const uint32_t hi = ((mw[i] & 0x80000000u) == 0 && (mw[i] & 0x7fff0000u) != 0) ? 0xffff0000u : 0u;
+      o[i] = dw[i] & (lo | hi);
+    }
+    *reinterpret_cast<uint4*>(g + v * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// backward partial sums per (group image, blk): sum g, sum g*xhat, sum xhat;
+// g = dy * [y > 0] when relu; xhat = (x - mean) * invstd
+__global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y, const uint16_t* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ invstd, int HW, int C, int per_image,
+    int pix_per_blk, int total_pix, int relu, float* __restrict__ part) {
+  __shared__ float red[3][NT * 8];
+  const int cg = C / 8;
+  const int lanes = NT / cg;
+  const int tid = threadIdx.x;
+  const int g = tid % cg, pl = tid / cg;
+  const int img = blockIdx.y;
+  const int64_t base = per_image ? (int64_t)img * HW : 0;
+  const int range = per_image ? HW : total_pix;
+  const int p0 = blockIdx.x * pix_per_blk, p1 = min(range, p0 + pix_per_blk);
+  float mu[8], is[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mu[i] = mean[(int64_t)(per_image ? img : 0) * C + g * 8 + i];
+    is[i] = invstd[(int64_t)(per_image ? img : 0) * C + g * 8 + i];
+  }
+  float sg[8], sgx[8], sx[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sg[i] = sgx[i] = sx[i] = 0.f;
+  if (pl < lanes) {
+    for (int p = p0 + pl; p < p1; p += lanes) {
+      const int64_t off = (base + p) * C + g * 8;
+      float d[8], xv[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + off), d);
+      unpack8(*reinterpret_cast<const uint4*>(x + off), xv);
+      if (relu) {
+        float yv[8];
+        unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xh = (xv[i] - mu[i]) * is[i];
+        sg[i] += d[i];
+        sgx[i] += d[i] * xh;
+        sx[i] += xh;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    red[0][tid * 8 + i] = sg[i];
+    red[1][tid * 8 + i] = sgx[i];
+    red[2][tid * 8 + i] = sx[i];
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    const int gg = c / 8, ii = c % 8;
+    float a = 0.f, b = 0.f, s = 0.f;
+    for (int l = 0; l < lanes; ++l) {
+      a += red[0][(l * cg + gg) * 8 + ii];
+      b += red[1][(l * cg + gg) * 8 + ii];
+      s += red[2][(l * cg + gg) * 8 + ii];
+    }
+    float* dst = part + ((int64_t)img * gridDim.x + blockIdx.x) * 3 * C;
+    dst[c] = a;
+    dst[C + c] = b;
+    dst[2 * C + c] = s;
+  }
+}
+
+// -> per (group image, c) coefficients dx = A*g + B*xhat + Cc, plus dgamma/dbeta/dcbias (summed
+// over images by the channel's thread for instance norm: one thread per channel here)
+__global__ void norm_bwd_finalize_kernel(const float* __restrict__ part, int C, int groups_img,
+                                         int nblk, int cnt, int mode,
+                                         const float* __restrict__ gamma,
+                                         const float* __restrict__ invstd,
+                                         float* __restrict__ coef, float* __restrict__ dgamma,
+                                         float* __restrict__ dbeta, float* __restrict__ dcbias) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float gm = (mode == 1 || mode == 2) && gamma ? gamma[c] : 1.f;
+  double dg = 0.0, db = 0.0, dcb = 0.0;
+  for (int gi = 0; gi < groups_img; ++gi) {
+    double sg = 0.0, sgx = 0.0, sx = 0.0;
+    for (int k = 0; k < nblk; ++k) {
+      const float* p = part + ((int64_t)gi * nblk + k) * 3 * C;
+      sg += p[c];
+      sgx += p[C + c];
+      sx += p[2 * C + c];
+    }
+    const float is = invstd[(int64_t)gi * C + c];
+    float A, B, Cc;
+    if (mode == 0 || mode == 1) {
+      const double mg = sg / cnt, mgx = sgx / cnt;
+      A = gm * is;
+      B = (float)(-gm * is * mgx);
+      Cc = (float)(-gm * is * mg);
+      // sum over the group of dx = A*sg + B*sx + C*cnt
+      dcb += A * sg + B * sx + (double)Cc * cnt;
+    } else {
+      A = gm * is;  // eval batch norm / none: an affine map
+      B = 0.f;
+      Cc = 0.f;
+      dcb += A * sg;
+    }
+    float* co = coef + ((int64_t)gi * C + c) * 3;
+    co[0] = A;
+    co[1] = B;
+    co[2] = Cc;
+    dg += sgx;
+    db += sg;
+  }
+  if (dgamma) dgamma[c] += (float)dg;
+  if (dbeta) dbeta[c] += (float)db;
+  if (dcbias) dcbias[c] += (float)dcb;
+}
+
+__global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y, const uint16_t* __restrict__ x,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ coef,
+    int HW, int C, int per_image, int64_t nvec, int relu, uint16_t* __restrict__ dx) {
+  const int cg = C / 8;
+  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+    const int64_t pix = v / cg;
+    const int g = (int)(v - pix * cg);
+    const int gi = per_image ? (int)(pix / HW) : 0;
+    float d[8], xv[8];
+    unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), d);
+    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
+    if (relu) {
+      float yv[8];
+      unpack8(*reinterpret_cast<const uint4*>(y + v * 8), yv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
+    }
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t k = (int64_t)gi * C + g * 8 + i;
+      const float xh = (xv[i] - mean[k]) * invstd[k];
+      o[i] = coef[k * 3] * d[i] + coef[k * 3 + 1] * xh + coef[k * 3 + 2];
+    }
+    *reinterpret_cast<uint4*>(dx + v * 8) = pack8(o);
+  }
+}
+
+unsigned grid_for(int64_t nvec) {
+  const int64_t b = (nvec + NT - 1) / NT;
+  return (unsigned)std::min<int64_t>(b, 256 * 16);
+}
+
+}  // namespace
+
+int encoder_norm_blocks(int64_t range, int C, int* pix_per_blk) {
+  // ~ one workgroup per 2 K pixel-rows of 8 channels -> enough blocks to fill the chip
+  const int cg = C / 8;
+  const int lanes = NT / cg;
+  int64_t ppb = (int64_t)lanes * 32;
+  if (ppb < 64) ppb = 64;
+  const int64_t nb = (range + ppb - 1) / ppb;
+  *pix_per_blk = (int)ppb;
+  return (int)nb;
+}
+
+void launch_norm_stats(const uint16_t* x, int N, int HW, int C, int per_image, float* part,
+                       int nblk, int pix_per_blk, hipStream_t stream) {
+  dim3 grid(nblk, per_image ? N : 1);
+  hipLaunchKernelGGL(norm_stats_kernel, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
+                     N * HW, part);
+}
+
+void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, int C, int mode,
+                          int nblk, const float* gamma, const float* beta, const float* cbias,
+                          float* rmean, float* rvar, float momentum, float eps, float* mean,
+                          float* invstd, float* scale, float* shift, hipStream_t stream) {
+  const int groups = mode == 0 ? N : 1;
+  const int cnt = mode == 0 ? HW : N * HW;
+  const int tot = groups * C;
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3((tot + 255) / 256), dim3(256), 0, stream, part, x, HW,
+                     C, groups, nblk, cnt, mode, gamma, beta, cbias, rmean, rvar, momentum, eps, mean,
+                     invstd, scale, shift, N);
+}
+
+void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift, int N, int HW,
+                       int C, int relu, const uint16_t* res, uint16_t* y, hipStream_t stream) {
+  const int64_t nvec = (int64_t)N * HW * C / 8;
+  hipLaunchKernelGGL(norm_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, x, scale, shift, HW,
+                     C, nvec, relu, res, y);
+}
+
+void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_t n,
+                     hipStream_t stream) {
+  const int64_t nvec = n / 8;
+  hipLaunchKernelGGL(add_relu_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, a, b, out, nvec);
+}
+
+void launch_relu_mask(const uint16_t* dy, const uint16_t* y, uint16_t* g, int64_t n,
+                      hipStream_t stream) {
+  const int64_t nvec = n / 8;
+  hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, y, g, nvec);
+}
+
+void launch_norm_bwd(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* mean,
+                     const float* invstd, int N, int HW, int C, int mode, int relu,
+                     const float* gamma, float* part, int nblk, int pix_per_blk, float* coef,
+                     float* dgamma, float* dbeta, float* dcbias, uint16_t* dx, hipStream_t stream) {
+  const int per_image = mode == 0 ? 1 : 0;
+  const int groups = per_image ? N : 1;
+  const int cnt = per_image ? HW : N * HW;
+  if (mode == 0 || mode == 1) {
+    dim3 grid(nblk, groups);
+    hipLaunchKernelGGL(norm_bwd_stats_kernel, grid, dim3(NT), 0, stream, dy, y, x, mean, invstd, HW, C,
+                       per_image, pix_per_blk, N * HW, relu, part);
+  } else {
+    // eval / none: only sum(g) and sum(g*xhat) are needed for the parameter grads
+    dim3 grid(nblk, 1);
+    hipLaunchKernelGGL(norm_bwd_stats_kernel, grid, dim3(NT), 0, stream, dy, y, x, mean, invstd, HW, C,
+                       0, pix_per_blk, N * HW, relu, part);
+  }
+  hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, stream, part, C,
+                     groups, nblk, cnt, mode, gamma, invstd, coef, dgamma, dbeta, dcbias);
+  const int64_t nvec = (int64_t)N * HW * C / 8;
+  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, y, x, mean,
+                     invstd, coef, HW, C, per_image, nvec, relu, dx);
+}

@@ -184,3 +184,23 @@ bool launch_convex_up_nhwc_fwd(const float* flow, const uint16_t* mask, float* o
 bool launch_convex_up_nhwc_bwd(const float* flow, const uint16_t* mask, const float* dout,
                                uint16_t* dmask, float* wbuf, float* dflow, int B, int H, int W,
                                hipStream_t stream);
+
+// ---- encoder norm + activation, NHWC bf16 (encoder_norm.hip)
+// mode: 0 instance, 1 batch (training statistics), 2 batch (running statistics), 3 none
+int encoder_norm_blocks(int64_t range, int C, int* pix_per_blk);
+void launch_norm_stats(const uint16_t* x, int N, int HW, int C, int per_image, float* part,
+                       int nblk, int pix_per_blk, hipStream_t stream);
+void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, int C, int mode,
+                          int nblk, const float* gamma, const float* beta, const float* cbias,
+                          float* rmean, float* rvar, float momentum, float eps, float* mean,
+                          float* invstd, float* scale, float* shift, hipStream_t stream);
+void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift, int N, int HW,
+                       int C, int relu, const uint16_t* res, uint16_t* y, hipStream_t stream);
+void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_t n,
+                     hipStream_t stream);
+void launch_relu_mask(const uint16_t* dy, const uint16_t* y, uint16_t* g, int64_t n,
+                      hipStream_t stream);
+void launch_norm_bwd(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* mean,
+                     const float* invstd, int N, int HW, int C, int mode, int relu,
+                     const float* gamma, float* part, int nblk, int pix_per_blk, float* coef,
+                     float* dgamma, float* dbeta, float* dcbias, uint16_t* dx, hipStream_t stream);

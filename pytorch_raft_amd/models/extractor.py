@@ -12,9 +12,10 @@ Behavioural parity with the reference encoders (`core/extractor.py:6-267`):
 State-dict schema is kept identical (`SURVEY.md` §2.5), including the strided residual block that
 registers the same norm module as both ``norm3`` and ``downsample.1`` (`core/extractor.py:26,44-45`).
 
-MI355X notes: the encoders are plain convolutions and stay on PyTorch-ROCm (MIOpen) under bf16
-autocast; ``to_channels_last()`` switches the weights to NHWC so MIOpen picks its NHWC implicit-GEMM
-solvers, which is the layout the rest of the HIP hot path consumes.
+MI355X notes: the convolutions stay on PyTorch-ROCm (MIOpen).  On the GPU under bf16 autocast the
+forward runs the channels-last fast path of ``pytorch_raft_amd.ops.encoder``: NHWC MIOpen convs
+without NCHW<->NHWC transposes, each norm + ReLU (and residual add + ReLU) one fused HIP autograd
+node, conv biases folded into the norms.
 """
 import torch
 import torch.nn as nn
@@ -135,11 +136,16 @@ class _Encoder(nn.Module):
         if batched:
             n = x[0].shape[0]
             x = torch.cat(x, dim=0)
-        x = self.relu1(self.norm1(self.conv1(x)))
-        x = self.layer3(self.layer2(self.layer1(x)))
-        x = self.conv2(x)
-        if self.training and self.dropout is not None:
-            x = self.dropout(x)
+        from ..ops import encoder as fast
+        if fast.fast_path_ok(self, x):
+            # channels-last MIOpen convs + fused HIP norm/ReLU/residual nodes (ops/encoder.py)
+            x = fast.encoder_forward(self, x)
+        else:
+            x = self.relu1(self.norm1(self.conv1(x)))
+            x = self.layer3(self.layer2(self.layer1(x)))
+            x = self.conv2(x)
+            if self.training and self.dropout is not None:
+                x = self.dropout(x)
         if batched:
             x = torch.split(x, [n, n], dim=0)
         return x

@@ -1,0 +1,163 @@
+"""Channels-last bf16 fast path of the RAFT encoders (fnet / cnet) on MI355X.
+
+Reference: `core/extractor.py:6-56` (ResidualBlock), `:60-116` (BottleneckBlock), `:118-267`
+(BasicEncoder / SmallEncoder forward).  Module tree, parameters and buffers are the nn.Module ones
+(checkpoint layout untouched); only the execution differs:
+
+* convolutions run as MIOpen NHWC bf16 convs (channels_last activations and weights -- no
+  NCHW<->NHWC transposes) WITHOUT their bias; the bias is folded into the following norm
+  (csrc/kernels/encoder_norm.hip), where it cancels for training-mode statistics and shifts the
+  eval-mode (frozen) BatchNorm.  Its gradient is computed exactly from the norm's backward sums;
+* every norm + ReLU is one autograd node with a hand-written forward (stats, finalize, apply) and
+  backward (sums, finalize, apply), replacing InstanceNorm-as-batch_norm, clamp, add and the
+  per-conv bias-gradient reductions of the eager graph;
+* the residual add + ReLU is one node.
+
+Used automatically by ``_Encoder.forward`` on the GPU under bf16 autocast (``fast_path_ok``).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _ext
+
+MODE_INSTANCE, MODE_BATCH_TRAIN, MODE_BATCH_EVAL, MODE_NONE = range(4)
+
+
+def _norm_mode(norm):
+    if isinstance(norm, nn.InstanceNorm2d):
+        if norm.affine or norm.track_running_stats:
+            return None
+        return MODE_INSTANCE
+    if isinstance(norm, nn.BatchNorm2d):
+        if norm.training or not norm.track_running_stats:
+            return MODE_BATCH_TRAIN
+        return MODE_BATCH_EVAL
+    if isinstance(norm, nn.Sequential) and len(norm) == 0:
+        return MODE_NONE
+    return None
+
+
+class _NormAct(torch.autograd.Function):
+    """y = act(norm(x + conv_bias)) on channels_last bf16; x is the bias-free conv output."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, cbias, norm, mode, relu):
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        rm = rv = None
+        momentum = 0.1
+        eps = 1e-5
+        if isinstance(norm, (nn.BatchNorm2d, nn.InstanceNorm2d)):
+            eps = norm.eps
+        if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and norm.track_running_stats:
+            rm, rv = norm.running_mean, norm.running_var
+            if mode == MODE_BATCH_TRAIN:
+                norm.num_batches_tracked.add_(1)
+                momentum = norm.momentum if norm.momentum is not None else \
+                    1.0 / float(norm.num_batches_tracked.item())
+        mean, invstd = _ext.ops().norm_fwd_(x, mode, int(relu), gamma, beta, cbias, rm, rv,
+                                            float(momentum), float(eps), None, y)
+        ctx.save_for_backward(x, y, mean, invstd, gamma)
+        ctx.mode = mode
+        ctx.relu = relu
+        ctx.has = (gamma is not None, beta is not None, cbias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, invstd, gamma = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        c = x.shape[1]
+        dev = x.device
+        dg = torch.zeros(c, device=dev) if ctx.has[0] else None
+        db = torch.zeros(c, device=dev) if ctx.has[1] else None
+        dc = torch.zeros(c, device=dev) if ctx.has[2] else None
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        _ext.ops().norm_bwd_(dy, y, x, mean, invstd, ctx.mode, int(ctx.relu), gamma, dg, db, dc, dx)
+        return dx, dg, db, dc, None, None, None
+
+
+class _AddRelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        a = a.contiguous(memory_format=torch.channels_last)
+        b = b.contiguous(memory_format=torch.channels_last)
+        out = torch.empty_like(a, memory_format=torch.channels_last)
+        _ext.ops().add_relu_(a, b, out)
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (out,) = ctx.saved_tensors
+        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        g = torch.empty_like(out, memory_format=torch.channels_last)
+        _ext.ops().relu_mask_(dout, out, g)
+        return g, g
+
+
+def _conv(x, conv, with_bias=False):
+    w = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    b = conv.bias.to(torch.bfloat16) if (with_bias and conv.bias is not None) else None
+    return F.conv2d(x, w, b, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+
+def conv_norm_act(x, conv, norm, relu=True):
+    mode = _norm_mode(norm)
+    y = _conv(x, conv)
+    y = y.contiguous(memory_format=torch.channels_last)
+    gamma = beta = None
+    if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and norm.affine:
+        gamma, beta = norm.weight, norm.bias
+    return _NormAct.apply(y, gamma, beta, conv.bias, norm, mode, relu)
+
+
+def residual_block(blk, x):
+    """`core/extractor.py:47-56` on the fast path."""
+    y = conv_norm_act(x, blk.conv1, blk.norm1)
+    y = conv_norm_act(y, blk.conv2, blk.norm2)
+    if blk.downsample is not None:
+        x = conv_norm_act(x, blk.downsample[0], blk.downsample[1], relu=False)
+    return _AddRelu.apply(x, y)
+
+
+def bottleneck_block(blk, x):
+    """`core/extractor.py:105-116` on the fast path."""
+    y = conv_norm_act(x, blk.conv1, blk.norm1)
+    y = conv_norm_act(y, blk.conv2, blk.norm2)
+    y = conv_norm_act(y, blk.conv3, blk.norm3)
+    if blk.downsample is not None:
+        x = conv_norm_act(x, blk.downsample[0], blk.downsample[1], relu=False)
+    return _AddRelu.apply(x, y)
+
+
+def fast_path_ok(enc, x):
+    """GPU + native library + bf16 autocast + supported norms; otherwise the eager path runs."""
+    if not (isinstance(x, torch.Tensor) and x.is_cuda and _ext.device_ok(x)):
+        return False
+    if not (torch.is_autocast_enabled('cuda') and
+            torch.get_autocast_dtype('cuda') == torch.bfloat16):
+        return False
+    if enc.training and enc.dropout is not None:
+        return False
+    if not _ext.gpu_path_enabled(required=False):
+        return False
+    for m in enc.modules():
+        if isinstance(m, (nn.GroupNorm,)):
+            return False
+        if isinstance(m, nn.InstanceNorm2d) and _norm_mode(m) is None:
+            return False
+    return True
+
+
+def encoder_forward(enc, x):
+    """`core/extractor.py:168-192` (both encoders): returns channels_last bf16 features."""
+    with torch.autocast('cuda', enabled=False):
+        x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        x = conv_norm_act(x, enc.conv1, enc.norm1)
+        block_fn = residual_block if enc.block.__name__ == 'ResidualBlock' else bottleneck_block
+        for layer in (enc.layer1, enc.layer2, enc.layer3):
+            for blk in layer:
+                x = block_fn(blk, x)
+        x = _conv(x, enc.conv2, with_bias=True)
+    return x

@@ -1,0 +1,67 @@
+"""Channels-last fused encoder path (ops/encoder.py + encoder_norm.hip) vs the eager encoder."""
+import pytest
+import torch
+
+from pytorch_raft_amd.models.extractor import BasicEncoder, SmallEncoder
+from pytorch_raft_amd.ops import encoder as fast
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _cos(a, b):
+    a, b = a.reshape(-1).double(), b.reshape(-1).double()
+    return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+
+
+@pytest.mark.parametrize('cls,norm,train', [
+    (BasicEncoder, 'instance', True), (BasicEncoder, 'batch', True), (BasicEncoder, 'batch', False),
+    (SmallEncoder, 'instance', True), (SmallEncoder, 'none', True)])
+def test_fast_encoder_matches_eager(ext_ops, cls, norm, train):
+    torch.manual_seed(0)
+    enc = cls(output_dim=256 if cls is BasicEncoder else 128, norm_fn=norm).to(DEV)
+    for m in enc.modules():  # non-trivial affine / conv biases / running stats
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+            m.running_mean.uniform_(-0.1, 0.1)
+            m.running_var.uniform_(0.8, 1.2)
+        if isinstance(m, torch.nn.Conv2d):
+            m.bias.data.uniform_(-0.1, 0.1)
+    enc.train(train)
+    x = torch.randn(4, 3, 96, 128, device=DEV)
+    state = {k: v.clone() for k, v in enc.state_dict().items()}
+    outs, grads, bufs = {}, {}, {}
+    for path in ('eager', 'fast'):
+        enc.load_state_dict(state)
+        enc.zero_grad(set_to_none=True)
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            if path == 'eager':
+                orig = fast.fast_path_ok
+                fast.fast_path_ok = lambda *a: False
+                try:
+                    y = enc(x)
+                finally:
+                    fast.fast_path_ok = orig
+            else:
+                assert fast.fast_path_ok(enc, x)
+                y = enc(x)
+        (y.float() * torch.linspace(-1, 1, y.numel(), device=DEV).view(y.shape)).sum().backward()
+        outs[path] = y.float()
+        grads[path] = {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None}
+        bufs[path] = {k: v.clone() for k, v in enc.state_dict().items() if 'running' in k}
+    assert _cos(outs['fast'], outs['eager']) > 0.999
+    rel = (outs['fast'] - outs['eager']).norm() / outs['eager'].norm()
+    assert rel < 3e-2, rel
+    for n, g in grads['eager'].items():
+        normed_bias = n != 'conv2.bias' and n.endswith(('conv1.bias', 'conv2.bias', 'conv3.bias',
+                                                             'downsample.0.bias'))
+        if normed_bias and norm != 'none' and not (norm == 'batch' and not train):
+            # exactly zero in exact arithmetic (the bias cancels in a batch-statistics norm)
+            assert grads['fast'][n].abs().max() < 1e-2
+            continue
+        assert n in grads['fast'], n
+        c = _cos(grads['fast'][n], g)
+        assert c > 0.99, (n, c)
+    for k, v in bufs['eager'].items():
+        torch.testing.assert_close(bufs['fast'][k], v, atol=2e-3, rtol=2e-2)
