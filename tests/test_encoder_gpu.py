@@ -32,36 +32,40 @@ def test_fast_encoder_matches_eager(ext_ops, cls, norm, train):
     x = torch.randn(4, 3, 96, 128, device=DEV)
     state = {k: v.clone() for k, v in enc.state_dict().items()}
     outs, grads, bufs = {}, {}, {}
-    for path in ('eager', 'fast'):
+    for path in ('fp32', 'eager', 'fast'):
         enc.load_state_dict(state)
         enc.zero_grad(set_to_none=True)
-        with torch.autocast('cuda', dtype=torch.bfloat16):
-            if path == 'eager':
-                orig = fast.fast_path_ok
-                fast.fast_path_ok = lambda *a: False
-                try:
-                    y = enc(x)
-                finally:
-                    fast.fast_path_ok = orig
-            else:
-                assert fast.fast_path_ok(enc, x)
+        orig = fast.fast_path_ok
+        if path != 'fast':
+            fast.fast_path_ok = lambda *a: False
+        try:
+            with torch.autocast('cuda', dtype=torch.bfloat16, enabled=path != 'fp32'):
+                if path == 'fast':
+                    assert fast.fast_path_ok(enc, x)
                 y = enc(x)
+        finally:
+            fast.fast_path_ok = orig
         (y.float() * torch.linspace(-1, 1, y.numel(), device=DEV).view(y.shape)).sum().backward()
         outs[path] = y.float()
         grads[path] = {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None}
         bufs[path] = {k: v.clone() for k, v in enc.state_dict().items() if 'running' in k}
-    assert _cos(outs['fast'], outs['eager']) > 0.999
-    rel = (outs['fast'] - outs['eager']).norm() / outs['eager'].norm()
-    assert rel < 3e-2, rel
-    for n, g in grads['eager'].items():
+    ref = outs['fp32']
+    for path in ('eager', 'fast'):
+        rel = ((outs[path] - ref).norm() / ref.norm()).item()
+        assert rel < 3e-2, (path, rel)
+    report = []
+    for n, g in grads['fp32'].items():
         normed_bias = n != 'conv2.bias' and n.endswith(('conv1.bias', 'conv2.bias', 'conv3.bias',
-                                                             'downsample.0.bias'))
+                                                         'downsample.0.bias'))
         if normed_bias and norm != 'none' and not (norm == 'batch' and not train):
             # exactly zero in exact arithmetic (the bias cancels in a batch-statistics norm)
-            assert grads['fast'][n].abs().max() < 1e-2
+            assert grads['fast'][n].abs().max() < 1e-2, n
             continue
-        assert n in grads['fast'], n
-        c = _cos(grads['fast'][n], g)
-        assert c > 0.99, (n, c)
+        ce, cf = _cos(grads['eager'][n], g), _cos(grads['fast'][n], g)
+        report.append((n, round(ce, 4), round(cf, 4)))
+    print(report)
+    for n, ce, cf in report:
+        # the fused path must be as close to the fp32 gradients as eager bf16 autocast is
+        assert cf > min(0.99, ce - 0.01), (n, ce, cf)
     for k, v in bufs['eager'].items():
         torch.testing.assert_close(bufs['fast'][k], v, atol=2e-3, rtol=2e-2)
