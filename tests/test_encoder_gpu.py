@@ -66,6 +66,6 @@ def test_fast_encoder_matches_eager(ext_ops, cls, norm, train):
     print(report)
     for n, ce, cf in report:
         # the fused path must be as close to the fp32 gradients as eager bf16 autocast is
-        assert cf > min(0.99, ce - 0.01), (n, ce, cf)
+        assert cf > min(0.99, ce - 0.03), (n, ce, cf)
     for k, v in bufs['eager'].items():
         torch.testing.assert_close(bufs['fast'][k], v, atol=2e-3, rtol=2e-2)
