@@ -4,7 +4,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -m pytest tests/test_encoder_gpu.py -q -s > gpurun_out/pytest_enc.log 2>&1
+timeout -k 10 300 python -m pytest tests/test_encoder_gpu.py -q > gpurun_out/pytest_enc.log 2>&1
 rc=$?; tail -15 gpurun_out/pytest_enc.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_all.log 2>&1
