@@ -789,7 +789,7 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
   Tensor part;
   if (mode <= 1) {
     nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
-    part = at::empty({groups, nblk, 2, C}, fo);
+    part = at::empty({groups * (nblk + 1) * 2 * C}, fo);  // partials + per-group sums
     launch_norm_stats(xp, (int)N, (int)HW, (int)C, mode == 0, part.data_ptr<float>(), nblk, ppb,
                       cur_stream());
   }
@@ -825,7 +825,7 @@ void norm_bwd_(const Tensor& dy, const Tensor& y, const Tensor& x, const Tensor&
   int ppb = 0;
   const int nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
   auto fo = x.options().dtype(at::kFloat);
-  Tensor part = at::empty({groups, nblk, 3, C}, fo);
+  Tensor part = at::empty({groups * (nblk + 1) * 3 * C}, fo);  // partials + per-group sums
   Tensor coef = at::empty({groups, C, 3}, fo);
   launch_norm_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr<at::BFloat16>()),
                   reinterpret_cast<const uint16_t*>(y.data_ptr<at::BFloat16>()),

@@ -90,6 +90,26 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
   }
 }
 
+// part [groups][nblk][S*C] -> sums [groups][S*C]: 4 lanes per column stride over the partials,
+// fixed-order LDS combine (deterministic); grid (groups, ceil(S*C / 64))
+__global__ __launch_bounds__(256) void partial_reduce_kernel(const float* __restrict__ part,
+                                                             int nblk, int SC,
+                                                             float* __restrict__ sums) {
+  __shared__ float red[4][64];
+  const int gi = blockIdx.x;
+  const int col = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int lane = threadIdx.x >> 6;
+  float a = 0.f;
+  if (col < SC)
+    for (int k = lane; k < nblk; k += 4) a += part[((int64_t)gi * nblk + k) * SC + col];
+  red[lane][threadIdx.x & 63] = a;
+  __syncthreads();
+  if (lane == 0 && col < SC) {
+    const int t = threadIdx.x & 63;
+    sums[(int64_t)gi * SC + col] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+  }
+}
+
 // mode: 0 instance (train or eval: always batch statistics), 1 batch-train, 2 batch-eval, 3 none
 // one thread per (group image, channel)
 __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint16_t* __restrict__ x,
@@ -105,12 +125,7 @@ __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint1
   const float b = cbias ? cbias[c] : 0.f;
   float mean = 0.f, invstd = 1.f;
   if (mode == 0 || mode == 1) {
-    double a = 0.0, q = 0.0;
-    for (int k = 0; k < nblk; ++k) {
-      const float* p = part + ((int64_t)gi * nblk + k) * 2 * C;
-      a += p[c];
-      q += p[C + c];
-    }
+    const double a = part[(int64_t)gi * 2 * C + c], q = part[(int64_t)gi * 2 * C + C + c];
     const float K = raft_bf16_to_f32(x[(int64_t)(mode == 0 ? gi : 0) * HW * C + c]);
     const double m = a / cnt;
     double var = q / cnt - m * m;
@@ -285,13 +300,8 @@ __global__ void norm_bwd_finalize_kernel(const float* __restrict__ part, int C, 
   const float gm = (mode == 1 || mode == 2) && gamma ? gamma[c] : 1.f;
   double dg = 0.0, db = 0.0, dcb = 0.0;
   for (int gi = 0; gi < groups_img; ++gi) {
-    double sg = 0.0, sgx = 0.0, sx = 0.0;
-    for (int k = 0; k < nblk; ++k) {
-      const float* p = part + ((int64_t)gi * nblk + k) * 3 * C;
-      sg += p[c];
-      sgx += p[C + c];
-      sx += p[2 * C + c];
-    }
+    const float* p = part + (int64_t)gi * 3 * C;
+    const double sg = p[c], sgx = p[C + c], sx = p[2 * C + c];
     const float is = invstd[(int64_t)gi * C + c];
     float A, B, Cc;
     if (mode == 0 || mode == 1) {
@@ -380,7 +390,14 @@ void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, i
   const int groups = mode == 0 ? N : 1;
   const int cnt = mode == 0 ? HW : N * HW;
   const int tot = groups * C;
-  hipLaunchKernelGGL(norm_finalize_kernel, dim3((tot + 255) / 256), dim3(256), 0, stream, part, x, HW,
+  // part holds nblk partials per group followed by room for the per-group sums
+  float* sums = nullptr;
+  if (mode <= 1) {
+    sums = const_cast<float*>(part) + (int64_t)groups * nblk * 2 * C;
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3(groups, (2 * C + 63) / 64), dim3(256), 0, stream,
+                       part, nblk, 2 * C, sums);
+  }
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
                      C, groups, nblk, cnt, mode, gamma, beta, cbias, rmean, rvar, momentum, eps, mean,
                      invstd, scale, shift, N);
 }
@@ -421,7 +438,10 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* y, const uint16_t* x, c
     hipLaunchKernelGGL(norm_bwd_stats_kernel, grid, dim3(NT), 0, stream, dy, y, x, mean, invstd, HW, C,
                        0, pix_per_blk, N * HW, relu, part);
   }
-  hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, stream, part, C,
+  float* sums = part + (int64_t)groups * nblk * 3 * C;
+  hipLaunchKernelGGL(partial_reduce_kernel, dim3(groups, (3 * C + 63) / 64), dim3(256), 0, stream,
+                     part, nblk, 3 * C, sums);
+  hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, stream, sums, C,
                      groups, nblk, cnt, mode, gamma, invstd, coef, dgamma, dbeta, dcbias);
   const int64_t nvec = (int64_t)N * HW * C / 8;
   hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, y, x, mean,
