@@ -125,6 +125,7 @@ struct ConvFwdArgs {
   int split;
   OSeg oseg[3];
   int noseg;
+  int nullmem;  // timing experiments only: operand loads read zeros (descriptor with 0 records)
 };
 
 // tile shape chosen per geometry: autotuned once (outside stream capture) and cached;
