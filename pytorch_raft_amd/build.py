@@ -52,7 +52,18 @@ def _run(cmd):
     return r.stdout
 
 
+def _up_to_date():
+    """Both libraries newer than every source / header: nothing to do (object files not needed,
+    so the build/ directory does not have to travel with the tree)."""
+    headers = glob.glob(os.path.join(CSRC, '**', '*.h'), recursive=True)
+    gpu_srcs = glob.glob(os.path.join(CSRC, 'kernels', '*.hip')) + [os.path.join(CSRC, 'bindings.cpp')]
+    cpu_srcs = glob.glob(os.path.join(CSRC, 'cpu', '*.cpp'))
+    return not _newer(OUT, gpu_srcs + headers) and not _newer(OUT_CPU, cpu_srcs + headers)
+
+
 def build(force=False, jobs=None, verbose=False):
+    if not force and _up_to_date():
+        return OUT
     os.makedirs(BUILD, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, '**', '*.h'), recursive=True)
     inc, tlib, abi = _torch_paths()

@@ -564,6 +564,9 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   a.cout = (int)cout;
   a.scale = (float)scale;
   a.split = (int)split;
+  // the epilogue picks the z / r half per 32-column MFMA tile
+  TORCH_CHECK(epi != EPI_GRU_ZR || (split % 32 == 0 && split > 0 && split < cout),
+              "GRU z|r split must be a multiple of 32");
   TORCH_CHECK(epi != EPI_DGRAD, "use conv_dgrad_ for the dgrad epilogue");
   const bool f32out = (epi == EPI_F32 || epi == EPI_ACC_F32 || epi == EPI_F32_NCHW);
   const int64_t need_out = (epi == EPI_GRU_ZR) ? 3 : (epi == EPI_GRU_Q ? 2 : 1);
@@ -586,6 +589,8 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   int* ostr[3] = {&a.out0_stride, &a.out1_stride, &a.out2_stride};
   for (size_t o = 0; o < outs.size(); ++o) {
     check_nhwc(outs[o], B, H, W, "conv output", f32out ? at::kFloat : at::kBFloat16);
+    TORCH_CHECK(outs[o].numel() * outs[o].element_size() < (int64_t(1) << 31),
+                "conv output exceeds the 2 GiB buffer-descriptor range");
     TORCH_CHECK(out_off[o] >= 0 && out_off[o] + out_ch[o] <= outs[o].size(3), "output slice out of range");
     *optr[o] = f32out ? (void*)(outs[o].data_ptr<float>() + out_off[o])
                       : (void*)(reinterpret_cast<uint16_t*>(outs[o].data_ptr<at::BFloat16>()) + out_off[o]);
@@ -597,6 +602,7 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   int* astr[2] = {&a.aux0_stride, &a.aux1_stride};
   for (size_t o = 0; o < aux.size(); ++o) {
     check_nhwc(aux[o], B, H, W, "conv aux", at::kBFloat16);
+    TORCH_CHECK(aux[o].numel() * 2 < (int64_t(1) << 31), "conv aux exceeds the 2 GiB buffer-descriptor range");
     const int64_t ch = (epi == EPI_GRU_ZR) ? cout - split : cout;
     TORCH_CHECK(aux_off[o] >= 0 && aux_off[o] + ch <= aux[o].size(3), "aux slice out of range");
     *aptr[o] = reinterpret_cast<const uint16_t*>(aux[o].data_ptr<at::BFloat16>()) + aux_off[o];
@@ -701,6 +707,10 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   for (size_t o = 0; o < outs.size(); ++o) {
     const bool relu_mode = outs[o].scalar_type() == at::kBFloat16;
     check_nhwc(outs[o], B, H, W, "dgrad output", relu_mode ? at::kBFloat16 : at::kFloat);
+    TORCH_CHECK(outs[o].numel() * outs[o].element_size() < (int64_t(1) << 31),
+                "dgrad output exceeds the 2 GiB buffer-descriptor range");
+    // the epilogue picks the output segment per 32-column MFMA tile
+    TORCH_CHECK(out_cnt[o] % 32 == 0, "dgrad output segments must be multiples of 32 channels");
     TORCH_CHECK(out_real[o] <= out_cnt[o] && out_off[o] >= 0 && out_off[o] + out_real[o] <= outs[o].size(3),
                 "dgrad output slice out of range");
     if (relu_mode) {
@@ -708,6 +718,7 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
       TORCH_CHECK(o < relu_y.size(), "bf16 dgrad output needs its relu output tensor");
       const Tensor& y = relu_y[o];
       check_nhwc(y, B, H, W, "relu output", at::kBFloat16);
+      TORCH_CHECK(y.numel() * 2 < (int64_t(1) << 31), "relu output exceeds the 2 GiB descriptor range");
       TORCH_CHECK(relu_off[o] >= 0 && relu_off[o] + out_real[o] <= y.size(3), "relu output slice out of range");
       TORCH_CHECK(!out_acc[o], "the relu-gated bf16 output cannot accumulate");
       a.oseg[o].ptr = nullptr;
