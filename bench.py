@@ -160,6 +160,8 @@ def main(argv=None):
         prof.__exit__(None, None, None)
         os.makedirs(a.profile, exist_ok=True)
         with open(os.path.join(a.profile, 'ops.txt'), 'w') as f:
+            f.write(prof.key_averages().table(sort_by='self_cuda_time_total', row_limit=80))
+            f.write('\n\n')
             f.write(prof.key_averages().table(sort_by='cuda_time_total', row_limit=60))
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if pdist.is_dist():

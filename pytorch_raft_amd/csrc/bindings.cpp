@@ -667,6 +667,76 @@ void conv_wgrad_(const Tensor& g, int64_t g_off, const std::vector<Tensor>& ins,
   launch_conv_wgrad(a, cout > 64 ? 128 : 64, cin_small != 0, dbp, cur_stream());
 }
 
+// Weight / bias gradient summed over several (grad, input) items of the same conv geometry -- the
+// GRU iterations of one step (shared weights): one launch, split-K over (item, pixel range).
+// gs[i] is item i's bf16 NHWC gradient; ins[i * nseg + s] its s-th input segment buffer.
+void conv_wgrad_multi_(const std::vector<Tensor>& gs, int64_t g_off, const std::vector<Tensor>& ins,
+                       const std::vector<int64_t>& in_off, const std::vector<int64_t>& in_cnt,
+                       int64_t kh, int64_t kw, int64_t ph, int64_t pw, int64_t cout,
+                       const Tensor& dw, const c10::optional<Tensor>& db, int64_t pix_per_split) {
+  const int64_t n = (int64_t)gs.size();
+  const int64_t nseg = (int64_t)in_off.size();
+  TORCH_CHECK(n >= 1 && n <= RAFT_WG_MAX_ITEMS, "1..", RAFT_WG_MAX_ITEMS, " items");
+  TORCH_CHECK(nseg >= 1 && nseg <= 3 && (int64_t)in_cnt.size() == nseg, "1..3 input segments");
+  TORCH_CHECK((int64_t)ins.size() == n * nseg, "ins must hold items x segments tensors");
+  const Tensor& g0 = gs[0];
+  const int64_t B = g0.size(0), H = g0.size(1), W = g0.size(2);
+  c10::DeviceGuard gd(g0.device());
+  ConvWgradArgs a{};
+  WgradItems it{};
+  it.n = (int)n;
+  a.g_stride = (int)g0.size(3);
+  a.nseg = (int)nseg;
+  int64_t cin_pad = 0;
+  for (int64_t s = 0; s < nseg; ++s) {
+    TORCH_CHECK(in_cnt[s] % 128 == 0 && in_off[s] % 8 == 0,
+                "multi-item wgrad: segments must be multiples of the 128-wide K tile");
+    a.seg[s].stride = (int)ins[s].size(3);
+    a.seg[s].cnt = (int)in_cnt[s];
+    cin_pad += in_cnt[s];
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    const Tensor& g = gs[i];
+    check_nhwc(g, B, H, W, "grad", at::kBFloat16);
+    TORCH_CHECK(g.size(3) == a.g_stride, "all items' grads must share a layout");
+    TORCH_CHECK(g_off >= 0 && g_off % 8 == 0 && g_off + (cout + 7) / 8 * 8 <= g.size(3),
+                "grad slice out of range (cout rounded up to 8 channels must fit the row)");
+    TORCH_CHECK(g.numel() * 2 < (int64_t(1) << 31), "grad exceeds the 2 GiB buffer-descriptor range");
+    it.g[i] = reinterpret_cast<const uint16_t*>(g.data_ptr<at::BFloat16>()) + g_off;
+    for (int64_t s = 0; s < nseg; ++s) {
+      const Tensor& x = ins[i * nseg + s];
+      check_nhwc(x, B, H, W, "wgrad input", at::kBFloat16);
+      TORCH_CHECK(x.size(3) == a.seg[s].stride, "all items' inputs must share a layout");
+      TORCH_CHECK(in_off[s] + in_cnt[s] <= x.size(3), "segment out of range");
+      TORCH_CHECK(x.numel() * 2 < (int64_t(1) << 31), "wgrad input exceeds the 2 GiB buffer-descriptor range");
+      it.seg[i][s] = reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>()) + in_off[s];
+    }
+  }
+  a.cin_pad = (int)cin_pad;
+  a.B = (int)B; a.H = (int)H; a.W = (int)W;
+  a.KH = (int)kh; a.KW = (int)kw; a.PH = (int)ph; a.PW = (int)pw;
+  a.cout = (int)cout;
+  check_cuda_f32(dw, "grad_weight");
+  const int64_t kpad = kh * kw * cin_pad;
+  TORCH_CHECK(kpad % 128 == 0, "multi-item wgrad needs packed K a multiple of 128");
+  TORCH_CHECK(dw.dim() == 2 && dw.size(0) == cout && dw.size(1) == kpad, "grad_weight must be (cout, kpad)");
+  a.dw = dw.data_ptr<float>();
+  a.kpad = (int)kpad;
+  const int64_t P = B * H * W;
+  a.pix_per_split = (int)std::max<int64_t>(64, (pix_per_split + 63) / 64 * 64);
+  a.splits_per_item = (int)((P + a.pix_per_split - 1) / a.pix_per_split);
+  TORCH_CHECK(W >= 2 && H * W >= 128, "multi-item wgrad needs W >= 2 and H*W >= 128");
+  a.w_magic = (uint32_t)(((uint64_t(1) << 32) + (uint64_t)W - 1) / (uint64_t)W);
+  TORCH_CHECK((int64_t)n * a.splits_per_item < 65536, "too many splits");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    check_cuda_f32(*db, "grad_bias");
+    TORCH_CHECK(db->numel() == cout, "grad_bias size");
+    dbp = db->data_ptr<float>();
+  }
+  TORCH_CHECK(launch_conv_wgrad_multi(a, it, cout > 64 ? 128 : 64, dbp, cur_stream()), "wgrad launch");
+}
+
 // Input gradient of a stride-1 "same" conv = the forward kernel on flipped/transposed packed
 // weights; the result's channels are scattered over up to 3 fp32 NHWC slices (store or +=).
 void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_off,
@@ -980,6 +1050,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("warp_fwd(Tensor img, Tensor flow, float sx, float bx, float sy, float by) -> Tensor");
   m.def("warp_bwd(Tensor img, Tensor flow, Tensor dout, float sx, float bx, float sy, float by) -> Tensor[]");
   m.def("conv_fwd_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, Tensor? bias, int kh, int kw, int ph, int pw, int cout, int cin_small, int epi, int bn, float scale, int split, Tensor(a!)[] outs, int[] out_off, Tensor[] aux, int[] aux_off) -> ()");
+  m.def("conv_wgrad_multi_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
   m.def("conv_wgrad_(Tensor g, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, int cin_small, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
 }
 
@@ -1003,6 +1074,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("warp_bwd", &warp_bwd);
   m.impl("conv_fwd_", &conv_fwd_);
   m.impl("conv_wgrad_", &conv_wgrad_);
+  m.impl("conv_wgrad_multi_", &conv_wgrad_multi_);
   m.impl("corr_lookup_nhwc_", &corr_lookup_nhwc_);
   m.impl("corr_window_grad", &corr_window_grad);
   m.impl("corr_window_reduce", &corr_window_reduce);

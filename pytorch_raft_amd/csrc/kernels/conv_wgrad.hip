@@ -269,6 +269,252 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(ConvWgradArgs a, floa
     }
 }
 
+// ------------------------------------------------------------------ multi-item LDS-DMA kernel
+// dW = sum over ITEMS (the GRU iterations of one training step: the weights are shared, so the
+// per-iteration weight gradients are summed) and pixels of G^T X.  Batching every iteration into
+// one launch makes the reduction 12x longer per output tile, so the split-K partials that leave
+// the chip as float atomics shrink 12x (they ran at the ~1.3 TB/s memory-side atomic rate).
+// Operands go global -> LDS by buffer_load ... lds (no staging VGPRs / ds_write pass).  LDS image:
+// [64 pixel rows][RB bytes] per operand, 16-B chunks XOR-swizzled per row on the SOURCE side so
+// the transposing ds_read_b64_tr_b16 fragment reads (16-lane group = 4 rows x 32 B) hit 16
+// distinct bank groups:  RB = 256: chunk ^= 4*(row & 3);  RB = 128: chunk ^= 4*((row >> 1) & 1).
+template <int RB>
+__device__ __forceinline__ int wg_swz(int row) {
+  return RB == 256 ? 4 * (row & 3) : 4 * ((row >> 1) & 1);
+}
+
+template <int N>
+__device__ __forceinline__ void wg_wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+// LDS-DMA issued from inline asm: hipcc does not know these writes LDS, so it cannot insert the
+// conservative `s_waitcnt vmcnt(0)` it otherwise places before every ds_read_b64_tr_b16 that
+// follows an LDS-DMA (which drained the next step's prefetch).  Completion is counted by hand
+// (wg_wait_vmcnt + barrier).  M0 is saved / restored inside the statement.
+__device__ __forceinline__ void wg_dma16(__amdgpu_buffer_rsrc_t r, uint32_t lds_addr, uint32_t voff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 4\n\t"
+      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds_addr), "v"(voff), "s"(r)
+      : "memory");
+}
+
+template <int BM>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_multi_kernel(ConvWgradArgs a, WgradItems it,
+                                                                 float* __restrict__ db) {
+  constexpr int BN = 128;
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int RBG = BM * 2, RBX = BN * 2;          // LDS row bytes
+  constexpr int CPRG = BM / 8, CPRX = BN / 8;        // 16-B chunks per row
+  constexpr int GCH = BKP * CPRG, XCH = BKP * CPRX;  // chunks per stage
+  static_assert(GCH % NT == 0 && XCH % NT == 0, "whole wave instructions");
+  constexpr int G_PER = GCH / NT, X_PER = XCH / NT;
+  constexpr int LPS = G_PER + X_PER;
+  constexpr int STAGE = (GCH + XCH) * 16;  // bytes
+  typedef __amdgpu_buffer_rsrc_t rsrc_t;
+  constexpr uint32_t OOB = 0x80000000u;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int HW = a.H * a.W;
+  const int P = a.B * HW;
+  const int ntile_n = (a.kpad + BN - 1) / BN;
+  const int tm = blockIdx.x / ntile_n, tn = blockIdx.x % ntile_n;
+  const int m0 = tm * BM, k0 = tn * BN;
+  const int item = blockIdx.y / a.splits_per_item;
+  const int p_begin = (blockIdx.y - item * a.splits_per_item) * a.pix_per_split;
+  const int p_end = min(P, p_begin + a.pix_per_split);
+  const int steps = (p_end - p_begin + BKP - 1) / BKP;
+  if (steps <= 0) return;  // uniform
+
+  auto mk = [](const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  };
+  const rsrc_t g_rs = mk(it.g[item], (uint32_t)P * a.g_stride * 2u);
+  rsrc_t seg_rs[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int qq = q < a.nseg ? q : 0;
+    seg_rs[q] = mk(it.seg[item][qq], (uint32_t)P * a.seg[qq].stride * 2u);
+  }
+
+  // G chunks: row r (pixel p_begin + r + 64 t), logical channel chunk lc (fixed per lane)
+  int g_row[G_PER];
+  uint32_t g_col[G_PER];  // byte offset of the chunk within a G row, or OOB
+#pragma unroll
+  for (int j = 0; j < G_PER; ++j) {
+    const int e = tid + j * NT;
+    const int row = e / CPRG, lc = (e % CPRG) ^ wg_swz<RBG>(row);
+    g_row[j] = row;
+    g_col[j] = m0 + lc * 8 < a.cout ? (uint32_t)(m0 + lc * 8) * 2u : OOB;
+  }
+  // X chunks: packed-K column decoded once, pixel walked incrementally
+  int x_dpix[X_PER], x_dy[X_PER], x_dx[X_PER], x_coff[X_PER], x_seg[X_PER];
+  int x_p[X_PER], x_y[X_PER], x_x[X_PER];
+  bool x_ok[X_PER];
+#pragma unroll
+  for (int j = 0; j < X_PER; ++j) {
+    const int e = tid + j * NT;
+    const int row = e / CPRX, lc = (e % CPRX) ^ wg_swz<RBX>(row);
+    const int kc = k0 + lc * 8;
+    x_ok[j] = kc < a.kpad;
+    const int tap = kc / a.cin_pad, c = kc - tap * a.cin_pad;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    x_dy[j] = kh - a.PH;
+    x_dx[j] = kw - a.PW;
+    x_dpix[j] = x_dy[j] * a.W + x_dx[j];
+    int sidx = 0, sbase = 0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (sidx + 1 < a.nseg && c >= sbase + a.seg[sidx].cnt) { sbase += a.seg[sidx].cnt; ++sidx; }
+    x_coff[j] = c - sbase;
+    x_seg[j] = sidx;
+    const int p = p_begin + row;
+    const int pp = p < P ? p : 0;
+    const int r = pp % HW;
+    x_p[j] = p;
+    x_y[j] = r / a.W;
+    x_x[j] = r - (r / a.W) * a.W;
+  }
+
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t*)smem;
+  const uint32_t wave_off = __builtin_amdgcn_readfirstlane(wave * 64 * 16);
+  auto issue = [&](int t, int buf) {
+    const uint32_t base = lds0 + buf * STAGE + wave_off;
+    const int pb = p_begin + t * BKP;
+#pragma unroll
+    for (int j = 0; j < G_PER; ++j) {
+      const int p = pb + g_row[j];
+      const uint32_t off = (p < p_end && g_col[j] != OOB) ? (uint32_t)p * a.g_stride * 2u + g_col[j] : OOB;
+      wg_dma16(g_rs, base + j * NT * 16, off);
+    }
+#pragma unroll
+    for (int j = 0; j < X_PER; ++j) {
+      const int p = x_p[j];
+      const int yy = x_y[j] + x_dy[j], xx = x_x[j] + x_dx[j];
+      const bool ok = x_ok[j] && p < p_end && (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+      // segment widths are multiples of the 128-wide K tile (host check): the segment is
+      // wave-uniform, so the descriptor select stays scalar (a per-lane descriptor would make
+      // hipcc wrap every DMA in a readfirstlane waterfall loop)
+      const int s = __builtin_amdgcn_readfirstlane(x_seg[j]);
+      const uint32_t off = (uint32_t)(((p + x_dpix[j]) * a.seg[s].stride + x_coff[j]) * 2);
+      const rsrc_t rs = s == 0 ? seg_rs[0] : (s == 1 ? seg_rs[1] : seg_rs[2]);
+      wg_dma16(rs, base + (GCH + j * NT) * 16, ok ? off : OOB);
+      // advance this chunk's pixel by BKP -- branch-free (a divergent wrap loop here made hipcc
+      // drain vmcnt(0) before it, i.e. wait for the DMAs just issued): q = (x + BKP) / W by a
+      // magic multiply (exact for (x + BKP) * W < 2^32), at most one image wrap (host: HW >= 128)
+      x_p[j] += BKP;
+      const uint32_t xn = (uint32_t)(x_x[j] + BKP);
+      const uint32_t qw = __umulhi(xn, a.w_magic);
+      int yn = x_y[j] + (int)qw;
+      yn = yn >= a.H ? yn - a.H : yn;
+      x_x[j] = (int)(xn - qw * (uint32_t)a.W);
+      x_y[j] = yn;
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int gi = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  const bool do_bias = db != nullptr && tn == 0;
+  // bias: thread sums 4 adjacent channels over 64 / (NT / (BM / 4)) rows per step
+  constexpr int BT = BM / 4;            // threads per row of the bias sweep
+  constexpr int BROWS = BKP / (NT / BT);
+  const int bcol = (tid % BT) * 4, brow0 = (tid / BT) * BROWS;
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+
+  auto rd_tr = [](const uint8_t* base, int rb_row_bytes, int swz, int row, int col) {
+    const int off = row * rb_row_bytes + (((col >> 3) ^ swz) << 4) + (col & 7) * 2;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(base + off));
+  };
+  auto compute = [&](int buf) {
+    const uint8_t* Gs = smem + buf * STAGE;
+    const uint8_t* Xs = Gs + GCH * 16;
+#pragma unroll
+    for (int s = 0; s < BKP / 16; ++s) {
+      bf16x8_t af[TM], bfr[TN];
+      const int row = s * 16 + (gi >> 1) * 8 + q;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int col = wm * WM + i * 32 + (gi & 1) * 16 + 4 * pp;
+        bf16x4_t lo = rd_tr(Gs, RBG, wg_swz<RBG>(row), row, col);
+        bf16x4_t hi = rd_tr(Gs, RBG, wg_swz<RBG>(row + 4), row + 4, col);
+        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WN + j * 32 + (gi & 1) * 16 + 4 * pp;
+        bf16x4_t lo = rd_tr(Xs, RBX, wg_swz<RBX>(row), row, col);
+        bf16x4_t hi = rd_tr(Xs, RBX, wg_swz<RBX>(row + 4), row + 4, col);
+        bfr[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int r = 0; r < BROWS; ++r) {
+        const int row = brow0 + r;
+        const int off = row * RBG + (((bcol >> 3) ^ wg_swz<RBG>(row)) << 4) + (bcol & 7) * 2;
+        const uint2 v = *reinterpret_cast<const uint2*>(Gs + off);
+        bsum[0] += __uint_as_float(v.x << 16);
+        bsum[1] += __uint_as_float(v.x & 0xffff0000u);
+        bsum[2] += __uint_as_float(v.y << 16);
+        bsum[3] += __uint_as_float(v.y & 0xffff0000u);
+      }
+    }
+  };
+
+  issue(0, 0);
+  for (int t = 0; t < steps; ++t) {
+    if (t + 1 < steps) {
+      issue(t + 1, (t + 1) & 1);
+      wg_wait_vmcnt<LPS>();
+    } else {
+      wg_wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    compute(t & 1);
+    __builtin_amdgcn_s_barrier();
+  }
+
+  if (do_bias) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (m0 + bcol + c < a.cout) atomicAdd(db + m0 + bcol + c, bsum[c]);
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int kc = k0 + wn * WN + j * 32 + (lane & 31);
+      if (kc >= a.kpad) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (n < a.cout) atomicAdd(a.dw + (int64_t)n * a.kpad + kc, acc[i][j][r]);
+      }
+    }
+}
+
 // db[n] = sum_p G[p][n]: each block sums a pixel range for 64 channels, then one atomic per channel
 __global__ __launch_bounds__(256) void col_sum_kernel(const uint16_t* __restrict__ g, int stride,
                                                       int cout, int P, int pix_per_block,
@@ -304,6 +550,17 @@ bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, float* db,
     if (smallc) hipLaunchKernelGGL((conv_wgrad_kernel<64, BN, true>), grid, dim3(NT), 0, stream, a, db);
     else hipLaunchKernelGGL((conv_wgrad_kernel<64, BN, false>), grid, dim3(NT), 0, stream, a, db);
   }
+  return true;
+}
+
+bool launch_conv_wgrad_multi(const ConvWgradArgs& a, const WgradItems& it, int bm, float* db,
+                             hipStream_t stream) {
+  constexpr int BN = 128;
+  const int tiles_n = (a.kpad + BN - 1) / BN;
+  dim3 grid(raft_cdiv(a.cout, bm) * tiles_n, it.n * a.splits_per_item);
+  if (bm == 128) hipLaunchKernelGGL((conv_wgrad_multi_kernel<128>), grid, dim3(NT), 0, stream, a, it, db);
+  else if (bm == 64) hipLaunchKernelGGL((conv_wgrad_multi_kernel<64>), grid, dim3(NT), 0, stream, a, it, db);
+  else return false;
   return true;
 }
 

@@ -146,7 +146,19 @@ struct ConvWgradArgs {
   float* dw;  // [cout][kpad] fp32, accumulated
   int kpad;
   int pix_per_split;
+  int splits_per_item;  // multi-item kernel: blockIdx.y = item * splits_per_item + split
+  uint32_t w_magic;     // ceil(2^32 / W): q = umulhi(n, w_magic) = n / W for n * W < 2^32
 };
+
+// the iterations of one step whose weight gradients are summed by one launch
+#define RAFT_WG_MAX_ITEMS 32
+struct WgradItems {
+  const uint16_t* g[RAFT_WG_MAX_ITEMS];       // dL/d(pre-activation), offset to channel 0
+  const uint16_t* seg[RAFT_WG_MAX_ITEMS][3];  // forward input segments, offset to first channel
+  int n;
+};
+bool launch_conv_wgrad_multi(const ConvWgradArgs& a, const WgradItems& it, int bm, float* db,
+                             hipStream_t stream);
 
 // db (nullable): fp32 bias gradient += column sums of G (fused)
 bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, float* db, hipStream_t stream);

@@ -108,6 +108,31 @@ def conv_wgrad(g, g_off, segs, ksize, pad, cout, dw, db=None, cin_small=0, pix_p
                     int(pad[1]), int(cout), int(cin_small), dw, db, int(pix_per_split))
 
 
+MAX_WG_ITEMS = 32
+
+
+def conv_wgrad_multi(items, g_off, in_off, in_cnt, ksize, pad, cout, dw, db=None,
+                     pix_per_split=None):
+    """dw / db += the weight / bias gradient summed over ``items`` = [(g, [input buffers])] of one
+    conv geometry (the GRU iterations of a step), in ONE launch.  Segment i of every item is
+    channels [in_off[i], in_off[i] + in_cnt[i]) of that item's i-th buffer."""
+    ops = _ext.ops()
+    n = len(items)
+    assert 1 <= n <= MAX_WG_ITEMS
+    if pix_per_split is None:
+        g0 = items[0][0]
+        p = g0.shape[0] * g0.shape[1] * g0.shape[2]
+        tiles = max(1, (cout + 127) // 128) * max(1, (dw.shape[1] + 127) // 128)
+        # >= ~3 resident rounds of workgroups over all items; each split's partial tile leaves
+        # the chip as fp32 atomics, so no more splits than that
+        per_item = max(1, (768 + tiles * n - 1) // (tiles * n))
+        pix_per_split = round_up((p + per_item - 1) // per_item, 64)
+    ins = [b for _, bufs in items for b in bufs]
+    ops.conv_wgrad_multi_([g for g, _ in items], int(g_off), ins, [int(o) for o in in_off],
+                          [int(c) for c in in_cnt], int(ksize[0]), int(ksize[1]), int(pad[0]),
+                          int(pad[1]), int(cout), dw, db, int(pix_per_split))
+
+
 def unpack_weight_grad(dw, cout, cin_real_segs, cin_pad_segs, ksize):
     """(cout, KH*KW*CinPad) packed gradient -> (Cout, Cin, KH, KW) module layout."""
     kh, kw = ksize

@@ -98,6 +98,9 @@ def flat_params(ub):
 class _Packed:
     """Per-step packed weights (bf16) + packed fp32 gradient accumulators."""
 
+    def defer_wgrad(self, name, g, g_off, segs):
+        self.pending.setdefault(name, []).append((g, g_off, segs))
+
     def __init__(self, params_by_layer, device, need_grad):
         self.w = {}
         self.wd = {}
@@ -105,6 +108,7 @@ class _Packed:
         self.kpad = {}
         self.dw = {}
         self.db = {}
+        self.pending = {}  # conv name -> [(g, g_off, segs)] awaiting the batched weight gradient
         with torch.no_grad():
             for s in SPECS:
                 ws = [w for w, _ in params_by_layer[s.name]]
@@ -145,6 +149,29 @@ class _Packed:
                     self.db[s.name] = torch.zeros(s.cout, device=device)
 
 
+def _flush_wgrad(pk):
+    """Weight gradients of every deferred (conv, iteration) item: one multi-item launch per conv
+    (the weights are shared by all iterations), per-item launches for the small-Cin conv."""
+    for name, items in pk.pending.items():
+        s = SPEC[name]
+        dw, db = pk.dw[name], pk.db[name]
+        same = all(it[1] == items[0][1] and [(o, c) for _, o, c in it[2]] ==
+                   [(o, c) for _, o, c in items[0][2]] for it in items)
+        if s.small or not same or any(c % 128 for _, _, c in items[0][2]):
+            for g, g_off, segs in items:
+                C.conv_wgrad(g, g_off, segs, s.k, s.pad, s.cout, dw, db,
+                             cin_small=2 if s.small else 0)
+            continue
+        g_off = items[0][1]
+        in_off = [o for _, o, _ in items[0][2]]
+        in_cnt = [c for _, _, c in items[0][2]]
+        for i in range(0, len(items), C.MAX_WG_ITEMS):
+            chunk = items[i:i + C.MAX_WG_ITEMS]
+            C.conv_wgrad_multi([(g, [b for b, _, _ in segs]) for g, _, segs in chunk], g_off,
+                               in_off, in_cnt, s.k, s.pad, s.cout, dw, db)
+    pk.pending = {}
+
+
 class _State:
     def __init__(self):
         self.packed = None
@@ -163,6 +190,7 @@ class _UpdateWeights(torch.autograd.Function):
     @staticmethod
     def backward(ctx, _tok):
         pk = ctx.state.packed
+        _flush_wgrad(pk)
         grads = []
         for s in SPECS:
             dw, db = pk.dw[s.name], pk.db[s.name]
@@ -256,9 +284,8 @@ class _UpdateIter(torch.autograd.Function):
         ops = _ext.ops()
 
         def wgrad(name, g, g_off, segs):
-            s = SPEC[name]
-            C.conv_wgrad(g, g_off, segs, s.k, s.pad, s.cout, pk.dw[name], pk.db[name],
-                         cin_small=2 if s.small else 0)
+            # deferred: summed over all iterations by one launch per conv (_Packed.flush_wgrad)
+            pk.defer_wgrad(name, g, g_off, segs)
 
         def dgrad(name, gsegs, outs, small=False, scale=1.0):
             """outs: list of (buffer fp32, offset, slot_cnt, real, acc) or, fusing the backward of a

@@ -2,8 +2,10 @@
 import re
 import sys
 
-CATS = [('ours conv fwd', r'conv_fwd_kernel<[^>]*, [0-57], (true|false)>'),
-        ('ours dgrad', r'conv_fwd_kernel<[^>]*, 6, '), ('ours wgrad', r'conv_wgrad'),
+CATS = [('ours conv fwd', r'conv_fwd_kernel<[^>]*, [0-57], (true|false)>|conv_fwd_glds_kernel<[^>]*, [0-57]>'),
+        ('ours dgrad', r'conv_fwd_kernel<[^>]*, 6, |conv_fwd_glds_kernel<[^>]*, 6>'),
+        ('ours wgrad', r'conv_wgrad'),
+        ('encoder norm', r'norm_(bwd_)?(stats|apply|finalize)|partial_reduce|add_relu|relu_mask'),
         ('miopen conv', r'igemm|grouped_conv|naive_conv|gemm|Conv'), ('transpose', r'transpose'),
         ('bn/norm', r'batch_norm|BatchNorm|InstanceNorm|instance_norm|welford|Norm'),
         ('reduce', r'reduce_kernel'),

@@ -4,7 +4,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py tests/test_update_hip_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_conv.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py tests/test_model_gpu.py tests/test_update_hip_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_conv.log 2>&1
 rc=$?; tail -4 gpurun_out/pytest_conv.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 200 python scripts/bench_conv.py > gpurun_out/bench_conv.log 2>&1 || exit $?

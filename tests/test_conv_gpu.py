@@ -192,3 +192,44 @@ def test_conv_dgrad_relu_gated_bf16(ext_ops):
                                    [cin], [cin], [0], [y], [32])
     torch.testing.assert_close(C.nchw(out[..., 8:8 + cin]).float(), ref, atol=2e-2, rtol=2e-2)
     assert torch.all(out[..., :8] == 7.0) and torch.all(out[..., 8 + cin:] == 7.0)
+
+
+@pytest.mark.parametrize('cin,cout,k,segs,g_off,pps', [
+    (256, 192, (3, 3), None, 0, None),
+    (384, 256, (1, 5), (128, 128, 128), 0, 128),
+    (128, 576, (1, 1), None, 0, None),
+    (256, 2, (3, 3), None, 0, 64),
+    (128, 64, (3, 3), None, 64, None),
+])
+def test_conv_wgrad_multi_items(ext_ops, cin, cout, k, segs, g_off, pps):
+    """One launch summing the weight gradient of several (grad, input) items (GRU iterations)."""
+    torch.manual_seed(7)
+    B, H, W = 2, 11, 19
+    n_items = 3
+    pad = (k[0] // 2, k[1] // 2)
+    w = torch.randn(cout, cin, *k, device=DEV, requires_grad=True)
+    b = torch.zeros(cout, device=DEV, requires_grad=True)
+    items = []
+    for _ in range(n_items):
+        x = torch.randn(B, cin, H, W, device=DEV).to(torch.bfloat16).float()
+        g = torch.randn(B, cout, H, W, device=DEV).to(torch.bfloat16).float()
+        F.conv2d(x, w, b, padding=pad).backward(g)
+        gb = torch.zeros(B, H, W, g_off + C.round_up(cout, 8), device=DEV, dtype=torch.bfloat16)
+        gb[..., g_off:g_off + cout] = C.nhwc(g)
+        if segs is None:
+            bufs = [C.nhwc(x)]
+        else:
+            bufs, o = [], 0
+            for c in segs:
+                bufs.append(C.nhwc(x[:, o:o + c]))
+                o += c
+        items.append((gb, bufs))
+    seg_cnt = [cin] if segs is None else list(segs)
+    dw = torch.zeros(cout, k[0] * k[1] * cin, device=DEV)
+    db = torch.zeros(cout, device=DEV)
+    C.conv_wgrad_multi(items, g_off, [0] * len(seg_cnt), seg_cnt, k, pad, cout, dw, db,
+                       pix_per_split=pps)
+    got = C.unpack_weight_grad(dw, cout, seg_cnt, seg_cnt, k)
+    scale = w.grad.abs().max().item()
+    torch.testing.assert_close(got, w.grad, atol=2e-3 * scale, rtol=1e-3)
+    torch.testing.assert_close(db, b.grad, atol=1e-3 * b.grad.abs().max().item(), rtol=1e-3)
