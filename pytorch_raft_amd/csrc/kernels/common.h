@@ -53,3 +53,35 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 static inline unsigned raft_cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+
+// ---- LDS-DMA (buffer_load ... lds) helpers shared by the MFMA conv kernels
+//
+// s_waitcnt vmcnt(N) with the other counters left alone (gfx9 encoding: vmcnt[3:0] + [15:14]).
+template <int N>
+__device__ __forceinline__ void raft_wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+// One 16-B-per-lane LDS-DMA: lane l's 16 bytes at voff land at LDS byte lds_addr + 16 l
+// (lds_addr wave-uniform).  Issued from inline asm so hipcc does not treat the following
+// ds_reads as dependent on it (it would otherwise insert `s_waitcnt vmcnt(0)` before the first
+// LDS read after any LDS-DMA, draining the prefetch pipeline); completion is counted by the
+// caller with raft_wait_vmcnt + a barrier.  M0 is saved and restored inside the statement.
+__device__ __forceinline__ void raft_dma16(__amdgpu_buffer_rsrc_t r, uint32_t lds_addr, uint32_t voff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 4\n\t"
+      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(lds_addr), "v"(voff), "s"(r)
+      : "memory");
+}
+
+// LDS byte address of a __shared__ object (for raft_dma16)
+__device__ __forceinline__ uint32_t raft_lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p;
+}

@@ -1,0 +1,204 @@
+// Shared device code of the implicit-GEMM conv kernels (conv_igemm.hip: register-staged kernel +
+// tile dispatch / autotune; conv_glds.hip: LDS-DMA pipelined kernel): LDS swizzle, buffer
+// descriptors, branch-free fused epilogues.
+#pragma once
+#include "common.h"
+#include "launchers.h"
+
+namespace conv_detail {
+
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+constexpr int BK = 64;   // K per pipeline step: one filter tap x 64 channels (128-B LDS rows)
+constexpr int NT = 256;
+
+// 16-B chunk `chunk` (0..7) of LDS row `row` (128 B).  A 256-B bank row holds two LDS rows; a
+// ds_read_b128 fragment read serves 16 lanes = 16 consecutive rows at one logical chunk per pass, so
+// the XOR key is (row >> 1) & 7: each row-parity class of the 16 rows lands on 8 distinct 16-B
+// slots and the pass is conflict-free (the ds_write_b128 tile stores stay conflict-free too).
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ ((row >> 1) & 7)); }
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr uint32_t OOB = 0x80000000u;  // voffset past every num_records: the load returns zeros
+
+__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 buf_load16(rsrc_t r, uint32_t voff) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+  return __builtin_bit_cast(uint4, v);
+}
+
+__device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + __expf(-v)); }
+__device__ __forceinline__ float tanhf_(float v) {
+  const float e = __expf(-2.f * fabsf(v));
+  const float t = (1.f - e) / (1.f + e);
+  return copysignf(t, v);
+}
+
+// ---------------------------------------------------------------- fused epilogue
+// Branch-free: every load and store goes through a range-checked buffer descriptor and invalid
+// rows / columns get an out-of-range offset (loads read 0, stores are dropped).  With no exec-
+// masked blocks around memory ops hipcc counts vmcnt exactly: one wait per 32x32 tile (for the
+// tile's aux / accumulate loads) instead of an `s_waitcnt vmcnt(0)` before EVERY store, which
+// serialized the 16-64 stores of a wave into dependent memory round trips.
+// Column-wise choices (GRU z vs r half, dgrad output segment) are made on the wave-uniform tile
+// column (segment / split boundaries are multiples of 32, checked on the host).
+__device__ __forceinline__ float bld_f32(rsrc_t r, uint32_t off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ float bld_bf16(rsrc_t r, uint32_t off) {
+  return raft_bf16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0));
+}
+__device__ __forceinline__ void bst_f32(rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bst_bf16(rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b16(raft_f32_to_bf16(v), r, off, 0, 0);
+}
+
+template <int TM, int TN, int WM, int WN, int EPI>
+__device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc)[TM][TN], int m0,
+                                              int n0, int wm, int wn, int lane, int P, int HW) {
+  constexpr bool F32OUT = EPI == EPI_F32 || EPI == EPI_ACC_F32 || EPI == EPI_F32_NCHW;
+  constexpr uint32_t ES = F32OUT ? 4u : 2u;
+  const rsrc_t bias_rs = make_rsrc(a.bias, a.bias ? (uint32_t)a.cout * 4u : 0u);
+  const uint32_t P_u = (uint32_t)P;
+  const rsrc_t nul = make_rsrc(nullptr, 0u);
+  rsrc_t o0 = nul, o1 = nul, o2 = nul, x0 = nul, x1 = nul;
+  if constexpr (EPI == EPI_F32_NCHW) {
+    o0 = make_rsrc(a.out0, P_u * (uint32_t)a.cout * 4u);
+  } else if constexpr (EPI != EPI_DGRAD) {
+    o0 = make_rsrc(a.out0, P_u * (uint32_t)a.out0_stride * ES);
+  }
+  if constexpr (EPI == EPI_GRU_ZR || EPI == EPI_GRU_Q) {
+    o1 = make_rsrc(a.out1, P_u * (uint32_t)a.out1_stride * 2u);
+    x0 = make_rsrc(a.aux0, P_u * (uint32_t)a.aux0_stride * 2u);
+  }
+  if constexpr (EPI == EPI_GRU_ZR) o2 = make_rsrc(a.out2, P_u * (uint32_t)a.out2_stride * 2u);
+  if constexpr (EPI == EPI_GRU_Q) x1 = make_rsrc(a.aux1, P_u * (uint32_t)a.aux1_stride * 2u);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int ncol0 = __builtin_amdgcn_readfirstlane(n0 + wn * WN + j * 32);
+      if (ncol0 >= a.cout) continue;  // wave-uniform
+      const int n = ncol0 + (lane & 31);
+      const bool nok = n < a.cout;
+      const float bias = bld_f32(bias_rs, nok ? (uint32_t)n * 4u : OOB);
+      int mrow[16];
+      bool ok[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        mrow[r] = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        ok[r] = nok && mrow[r] < P;
+      }
+      float v[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = (acc[i][j][r] + bias) * a.scale;
+
+      if constexpr (EPI == EPI_BF16 || EPI == EPI_RELU_BF16 || EPI == EPI_F32) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t off = ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * ES : OOB;
+          if constexpr (EPI == EPI_F32) bst_f32(o0, off, v[r]);
+          else bst_bf16(o0, off, EPI == EPI_RELU_BF16 ? fmaxf(v[r], 0.f) : v[r]);
+        }
+      } else if constexpr (EPI == EPI_ACC_F32) {
+        uint32_t off[16];
+        float pre[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          off[r] = ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 4u : OOB;
+          pre[r] = bld_f32(o0, off[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bst_f32(o0, off[r], pre[r] + v[r]);
+      } else if constexpr (EPI == EPI_F32_NCHW) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int b = mrow[r] / HW, yx = mrow[r] - b * HW;
+          bst_f32(o0, ok[r] ? (uint32_t)((b * a.cout + n) * HW + yx) * 4u : OOB, v[r]);
+        }
+      } else if constexpr (EPI == EPI_GRU_ZR) {
+        if (ncol0 < a.split) {  // z half
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            bst_bf16(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, sigmoidf_(v[r]));
+        } else {  // r half: r*h and r
+          const int c = n - a.split;
+          float h[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            h[r] = bld_bf16(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + c) * 2u : OOB);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float g = sigmoidf_(v[r]);
+            bst_bf16(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + c) * 2u : OOB, g * h[r]);
+            bst_bf16(o2, ok[r] ? (uint32_t)(mrow[r] * a.out2_stride + c) * 2u : OOB, g);
+          }
+        }
+      } else if constexpr (EPI == EPI_GRU_Q) {
+        float h[16], z[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          h[r] = bld_bf16(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + n) * 2u : OOB);
+          z[r] = bld_bf16(x1, ok[r] ? (uint32_t)(mrow[r] * a.aux1_stride + n) * 2u : OOB);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float q = tanhf_(v[r]);
+          bst_bf16(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, h[r] + z[r] * (q - h[r]));
+          bst_bf16(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + n) * 2u : OOB, q);
+        }
+      } else if constexpr (EPI == EPI_DGRAD) {
+        // output segment of this 32-column tile (uniform)
+        int s = 0, base = 0;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          if (s + 1 < a.noseg && ncol0 >= base + a.oseg[s].cnt) { base += a.oseg[s].cnt; ++s; }
+        const OSeg o = a.oseg[s];
+        const int c = n - base;
+        const bool cok = c < o.real;
+        if (o.ob != nullptr) {  // relu-gated bf16 gradient
+          const rsrc_t ob = make_rsrc(o.ob, P_u * (uint32_t)o.ob_stride * 2u);
+          const rsrc_t ry = make_rsrc(o.ry, P_u * (uint32_t)o.ry_stride * 2u);
+          float y[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            y[r] = bld_bf16(ry, ok[r] && cok ? (uint32_t)(mrow[r] * o.ry_stride + c) * 2u : OOB);
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            bst_bf16(ob, ok[r] && cok ? (uint32_t)(mrow[r] * o.ob_stride + c) * 2u : OOB,
+                     y[r] > 0.f ? v[r] : 0.f);
+        } else if (o.ptr != nullptr) {
+          const rsrc_t od = make_rsrc(o.ptr, P_u * (uint32_t)o.stride * 4u);
+          uint32_t off[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            off[r] = ok[r] && cok ? (uint32_t)(mrow[r] * o.stride + c) * 4u : OOB;
+          if (o.acc) {
+            float pre[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) pre[r] = bld_f32(od, off[r]);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bst_f32(od, off[r], pre[r] + v[r]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) bst_f32(od, off[r], v[r]);
+          }
+        }
+      }
+    }
+}
+
+
+template <int TM, int TN, int WVM>
+struct ConvTile {
+  static constexpr int WVN = 4 / WVM;
+  static constexpr int BM = 32 * TM * WVM, BN = 32 * TN * WVN;
+  static constexpr int LDS = 2 * (BM + BN) * 128;
+  static constexpr int OCC = LDS <= 65536 && TM * TN <= 4 ? 2 : 1;
+};
+
+}  // namespace conv_detail

@@ -1,0 +1,216 @@
+// LDS-DMA pipelined implicit-GEMM conv kernel (see conv_igemm.hip for the GEMM view, epilogues
+// and the tile-config dispatch).  Split into its own translation unit so the instantiations
+// (tile shapes x pipeline depths x epilogues) compile in parallel with conv_igemm.hip.
+#include "conv_common.h"
+
+namespace conv_detail {
+
+// ------------------------------------------------------------------ LDS-DMA variant
+// Same tiling / epilogues, but the A (input patch) and B (weight) tiles go global -> LDS with
+// buffer_load_dwordx4 ... lds: no staging VGPRs and no ds_write pass (on the register-staged
+// kernel the 13-cycle ds_write_b128 transfers cost as much LDS time as the fragment reads).
+// The DMA image is lane-linear (wave-uniform M0 base + 16 B x lane), so the XOR swizzle is
+// applied on the SOURCE side: the lane that lands in physical 16-B slot `pc` of row `row` loads
+// logical chunk pc ^ ((row >> 1) & 7); fragment reads use the same swz() as the register kernel.
+// Out-of-range taps / rows read as zeros through the range-checked descriptor (the DMA writes
+// the zeros).
+// NS-stage pipeline, ONE barrier per K step:  wait (counted vmcnt) for this wave's step-t DMAs
+// with the newer stages still in flight -> barrier (all waves' step-t data landed AND all waves
+// finished computing step t-1) -> issue step t+NS-1 into the buffer step t-1 used -> MFMAs on t.
+template <int TM, int TN, int WVM, int NS>
+struct GldsTile {
+  static constexpr int BM = 32 * TM * WVM, BN = 32 * TN * (4 / WVM);
+  static constexpr int STAGE_BYTES = (BM + BN) * 128;
+  static constexpr int LDS = NS * STAGE_BYTES;
+  static constexpr int OCC = (LDS <= 80 * 1024 && TM * TN <= 4) ? 2 : 1;
+};
+
+template <int TM, int TN, int WVM, int EPI, int NS>
+__global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd_glds_kernel(ConvFwdArgs a) {
+  using T = ConvTile<TM, TN, WVM>;
+  constexpr int BM = T::BM, BN = T::BN, WM = 32 * TM, WN = 32 * TN;
+  constexpr int WAVES_N = T::WVN;
+  constexpr int A_CHUNKS = BM * 8, B_CHUNKS = BN * 8;
+  static_assert(A_CHUNKS % NT == 0 && B_CHUNKS % NT == 0, "whole wave instructions per stage");
+  static_assert(NS >= 2 && NS <= 4, "2..4 pipeline stages");
+  constexpr int A_PER = A_CHUNKS / NT, B_PER = B_CHUNKS / NT;
+  constexpr int STAGE = A_CHUNKS + B_CHUNKS;  // 16-B slots per pipeline stage
+  constexpr int LPS = A_PER + B_PER;          // DMA instructions per thread per step
+
+  __shared__ __attribute__((aligned(16))) uint4 smem[NS * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int HW = a.H * a.W;
+  const int P = a.B * HW;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+
+  int a_pix[A_PER], a_y[A_PER], a_x[A_PER], a_lc[A_PER];
+#pragma unroll
+  for (int j = 0; j < A_PER; ++j) {
+    const int e = tid + j * NT;
+    const int row = e >> 3;
+    const int m = m0 + row;
+    const int mm = m < P ? m : 0;
+    const int r = mm % HW;
+    a_pix[j] = mm;
+    a_y[j] = m < P ? r / a.W : -(1 << 20);
+    a_x[j] = r % a.W;
+    a_lc[j] = ((e & 7) ^ ((row >> 1) & 7)) * 8;  // logical channel offset this lane fetches
+  }
+  uint32_t b_off[B_PER];
+#pragma unroll
+  for (int j = 0; j < B_PER; ++j) {
+    const int e = tid + j * NT;
+    const int row = e >> 3;
+    const int n = n0 + row;
+    const int lc = (e & 7) ^ ((row >> 1) & 7);
+    b_off[j] = n < a.cout ? (uint32_t)(((int64_t)n * a.kpad + lc * 8) * 2) : OOB;
+  }
+
+  const int nchunk = a.cin_pad / BK;
+  const int steps = a.KH * a.KW * nchunk;
+  rsrc_t seg_rs[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int qq = q < a.nseg ? q : 0;
+    seg_rs[q] = make_rsrc(a.seg[qq].ptr, (uint32_t)P * a.seg[qq].stride * 2u);
+  }
+  const rsrc_t w_rs = make_rsrc(a.wpk, (uint32_t)a.cout * a.kpad * 2u);
+  const uint32_t lds0 = raft_lds_addr(smem) + __builtin_amdgcn_readfirstlane(wave * 64 * 16);
+
+  auto issue = [&](int t, int buf) {
+    const int tap = t / nchunk, ch = t - tap * nchunk;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const int c0 = ch * BK;
+    int s = 0, sbase = 0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (s + 1 < a.nseg && c0 >= sbase + a.seg[s].cnt) { sbase += a.seg[s].cnt; ++s; }
+    const rsrc_t rs = s == 0 ? seg_rs[0] : (s == 1 ? seg_rs[1] : seg_rs[2]);
+    const int stride = a.seg[s].stride;
+    const int dy = kh - a.PH, dx = kw - a.PW;
+    const int dpix = dy * a.W + dx;
+    const int coff = c0 - sbase;
+    const uint32_t base = lds0 + (uint32_t)(buf * STAGE * 16);
+#pragma unroll
+    for (int j = 0; j < A_PER; ++j) {
+      const int yy = a_y[j] + dy, xx = a_x[j] + dx;
+      const bool ok = (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+      const uint32_t off = (uint32_t)(((a_pix[j] + dpix) * stride + coff + a_lc[j]) * 2);
+      raft_dma16(rs, base + j * NT * 16, ok ? off : OOB);
+    }
+    const uint32_t kb = (uint32_t)(t * BK * 2);
+#pragma unroll
+    for (int j = 0; j < B_PER; ++j)
+      raft_dma16(w_rs, base + (A_CHUNKS + j * NT) * 16, b_off[j] == OOB ? OOB : b_off[j] + kb);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto compute = [&](int buf) {
+    const uint4* As = smem + buf * STAGE;
+    const uint4* Bs = As + A_CHUNKS;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 32 + (lane & 31);
+        af[i] = __builtin_bit_cast(bf16x8_t, As[swz(row, kk * 2 + (lane >> 5))]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 32 + (lane & 31);
+        bfr[j] = __builtin_bit_cast(bf16x8_t, Bs[swz(row, kk * 2 + (lane >> 5))]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < steps) issue(s, s);
+  int cur = 0;  // buffer of step t
+  for (int t = 0; t < steps; ++t) {
+    // stages issued after step t that may stay in flight: min(NS - 2, steps - 1 - t)
+    const int newer = min(NS - 2, steps - 1 - t);
+    if (NS >= 4 && newer >= 2) raft_wait_vmcnt<(NS >= 4 ? 2 : 0) * LPS>();
+    else if (NS >= 3 && newer >= 1) raft_wait_vmcnt<(NS >= 3 ? 1 : 0) * LPS>();
+    else raft_wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (t + NS - 1 < steps) {
+      int nb = cur + NS - 1;
+      nb = nb >= NS ? nb - NS : nb;
+      issue(t + NS - 1, nb);
+    }
+    compute(cur);
+    cur = cur + 1 == NS ? 0 : cur + 1;
+  }
+
+  conv_epilogue<TM, TN, WM, WN, EPI>(a, acc, m0, n0, wm, wn, lane, P, HW);
+}
+
+
+template <int EPI, int TM, int TN, int WVM, int NS>
+void launch_one_glds(const ConvFwdArgs& a, hipStream_t stream) {
+  using T = ConvTile<TM, TN, WVM>;
+  const int P = a.B * a.H * a.W;
+  dim3 grid(raft_cdiv(P, T::BM), raft_cdiv(a.cout, T::BN));
+  hipLaunchKernelGGL((conv_fwd_glds_kernel<TM, TN, WVM, EPI, NS>), grid, dim3(NT), 0, stream, a);
+}
+
+template <int EPI>
+bool launch_glds_epi(const ConvFwdArgs& a, int idx, hipStream_t stream) {
+  switch (idx) {
+      case 10: launch_one_glds<EPI, 2, 2, 2, 2>(a, stream); return true;
+      case 11: launch_one_glds<EPI, 1, 2, 2, 2>(a, stream); return true;
+      case 12: launch_one_glds<EPI, 2, 1, 2, 2>(a, stream); return true;
+      case 13: launch_one_glds<EPI, 4, 2, 2, 2>(a, stream); return true;
+      case 14: launch_one_glds<EPI, 4, 2, 1, 2>(a, stream); return true;
+      case 15: launch_one_glds<EPI, 3, 2, 1, 2>(a, stream); return true;
+      case 16: launch_one_glds<EPI, 5, 1, 1, 2>(a, stream); return true;
+      case 17: launch_one_glds<EPI, 1, 1, 2, 2>(a, stream); return true;
+      case 18: launch_one_glds<EPI, 2, 2, 2, 4>(a, stream); return true;
+      case 19: launch_one_glds<EPI, 1, 2, 2, 3>(a, stream); return true;
+      case 20: launch_one_glds<EPI, 5, 1, 1, 4>(a, stream); return true;
+      case 21: launch_one_glds<EPI, 2, 1, 2, 4>(a, stream); return true;
+      case 22: launch_one_glds<EPI, 1, 1, 2, 4>(a, stream); return true;
+      case 23: launch_one_glds<EPI, 4, 2, 1, 3>(a, stream); return true;
+      case 24: launch_one_glds<EPI, 3, 1, 1, 4>(a, stream); return true;
+      case 25: launch_one_glds<EPI, 3, 1, 1, 2>(a, stream); return true;
+      case 26: launch_one_glds<EPI, 5, 2, 1, 2>(a, stream); return true;
+      case 27: launch_one_glds<EPI, 5, 2, 1, 3>(a, stream); return true;
+      case 28: launch_one_glds<EPI, 9, 1, 1, 2>(a, stream); return true;
+      case 29: launch_one_glds<EPI, 3, 3, 2, 2>(a, stream); return true;
+    default: return false;
+  }
+}
+
+}  // namespace conv_detail
+
+// config index -> LDS-DMA kernel launch (indices as in conv_igemm.hip's kCfgs table)
+bool launch_conv_glds(const ConvFwdArgs& a, int epi, int idx, hipStream_t stream) {
+  using namespace conv_detail;
+  switch (epi) {
+    case EPI_BF16: return launch_glds_epi<EPI_BF16>(a, idx, stream);
+    case EPI_RELU_BF16: return launch_glds_epi<EPI_RELU_BF16>(a, idx, stream);
+    case EPI_F32: return launch_glds_epi<EPI_F32>(a, idx, stream);
+    case EPI_ACC_F32: return launch_glds_epi<EPI_ACC_F32>(a, idx, stream);
+    case EPI_GRU_ZR: return launch_glds_epi<EPI_GRU_ZR>(a, idx, stream);
+    case EPI_GRU_Q: return launch_glds_epi<EPI_GRU_Q>(a, idx, stream);
+    case EPI_DGRAD: return launch_glds_epi<EPI_DGRAD>(a, idx, stream);
+    case EPI_F32_NCHW: return launch_glds_epi<EPI_F32_NCHW>(a, idx, stream);
+    default: return false;
+  }
+}

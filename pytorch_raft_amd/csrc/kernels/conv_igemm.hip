@@ -24,8 +24,7 @@
 //
 // dgrad reuses this kernel with flipped / transposed packed weights (stride-1 same padding is
 // self-adjoint up to the flip); wgrad lives in conv_wgrad.hip.
-#include "common.h"
-#include "launchers.h"
+#include "conv_common.h"
 
 #include <cmath>
 #include <cstdlib>
@@ -34,204 +33,14 @@
 #include <tuple>
 
 namespace {
-
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-constexpr int BK = 64;   // K per pipeline step: one filter tap x 64 channels (128-B LDS rows)
-constexpr int NT = 256;
-
-// 16-B chunk `chunk` (0..7) of LDS row `row` (128 B).  A 256-B bank row holds two LDS rows; a
-// ds_read_b128 fragment read serves 16 lanes = 16 consecutive rows at one logical chunk per pass, so
-// the XOR key is (row >> 1) & 7: each row-parity class of the 16 rows lands on 8 distinct 16-B
-// slots and the pass is conflict-free (the ds_write_b128 tile stores stay conflict-free too).
-__device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ ((row >> 1) & 7)); }
-
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-constexpr uint32_t OOB = 0x80000000u;  // voffset past every num_records: the load returns zeros
-
-__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ uint4 buf_load16(rsrc_t r, uint32_t voff) {
-  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
-  return __builtin_bit_cast(uint4, v);
-}
-
-__device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + __expf(-v)); }
-__device__ __forceinline__ float tanhf_(float v) {
-  const float e = __expf(-2.f * fabsf(v));
-  const float t = (1.f - e) / (1.f + e);
-  return copysignf(t, v);
-}
-
-// ---------------------------------------------------------------- fused epilogue
-// Branch-free: every load and store goes through a range-checked buffer descriptor and invalid
-// rows / columns get an out-of-range offset (loads read 0, stores are dropped).  With no exec-
-// masked blocks around memory ops hipcc counts vmcnt exactly: one wait per 32x32 tile (for the
-// tile's aux / accumulate loads) instead of an `s_waitcnt vmcnt(0)` before EVERY store, which
-// serialized the 16-64 stores of a wave into dependent memory round trips.
-// Column-wise choices (GRU z vs r half, dgrad output segment) are made on the wave-uniform tile
-// column (segment / split boundaries are multiples of 32, checked on the host).
-__device__ __forceinline__ float bld_f32(rsrc_t r, uint32_t off) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
-}
-__device__ __forceinline__ float bld_bf16(rsrc_t r, uint32_t off) {
-  return raft_bf16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0));
-}
-__device__ __forceinline__ void bst_f32(rsrc_t r, uint32_t off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
-}
-__device__ __forceinline__ void bst_bf16(rsrc_t r, uint32_t off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b16(raft_f32_to_bf16(v), r, off, 0, 0);
-}
-
-template <int TM, int TN, int WM, int WN, int EPI>
-__device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc)[TM][TN], int m0,
-                                              int n0, int wm, int wn, int lane, int P, int HW) {
-  constexpr bool F32OUT = EPI == EPI_F32 || EPI == EPI_ACC_F32 || EPI == EPI_F32_NCHW;
-  constexpr uint32_t ES = F32OUT ? 4u : 2u;
-  const rsrc_t bias_rs = make_rsrc(a.bias, a.bias ? (uint32_t)a.cout * 4u : 0u);
-  const uint32_t P_u = (uint32_t)P;
-  const rsrc_t nul = make_rsrc(nullptr, 0u);
-  rsrc_t o0 = nul, o1 = nul, o2 = nul, x0 = nul, x1 = nul;
-  if constexpr (EPI == EPI_F32_NCHW) {
-    o0 = make_rsrc(a.out0, P_u * (uint32_t)a.cout * 4u);
-  } else if constexpr (EPI != EPI_DGRAD) {
-    o0 = make_rsrc(a.out0, P_u * (uint32_t)a.out0_stride * ES);
-  }
-  if constexpr (EPI == EPI_GRU_ZR || EPI == EPI_GRU_Q) {
-    o1 = make_rsrc(a.out1, P_u * (uint32_t)a.out1_stride * 2u);
-    x0 = make_rsrc(a.aux0, P_u * (uint32_t)a.aux0_stride * 2u);
-  }
-  if constexpr (EPI == EPI_GRU_ZR) o2 = make_rsrc(a.out2, P_u * (uint32_t)a.out2_stride * 2u);
-  if constexpr (EPI == EPI_GRU_Q) x1 = make_rsrc(a.aux1, P_u * (uint32_t)a.aux1_stride * 2u);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int ncol0 = __builtin_amdgcn_readfirstlane(n0 + wn * WN + j * 32);
-      if (ncol0 >= a.cout) continue;  // wave-uniform
-      const int n = ncol0 + (lane & 31);
-      const bool nok = n < a.cout;
-      const float bias = bld_f32(bias_rs, nok ? (uint32_t)n * 4u : OOB);
-      int mrow[16];
-      bool ok[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        mrow[r] = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        ok[r] = nok && mrow[r] < P;
-      }
-      float v[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = (acc[i][j][r] + bias) * a.scale;
-
-      if constexpr (EPI == EPI_BF16 || EPI == EPI_RELU_BF16 || EPI == EPI_F32) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const uint32_t off = ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * ES : OOB;
-          if constexpr (EPI == EPI_F32) bst_f32(o0, off, v[r]);
-          else bst_bf16(o0, off, EPI == EPI_RELU_BF16 ? fmaxf(v[r], 0.f) : v[r]);
-        }
-      } else if constexpr (EPI == EPI_ACC_F32) {
-        uint32_t off[16];
-        float pre[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          off[r] = ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 4u : OOB;
-          pre[r] = bld_f32(o0, off[r]);
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) bst_f32(o0, off[r], pre[r] + v[r]);
-      } else if constexpr (EPI == EPI_F32_NCHW) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int b = mrow[r] / HW, yx = mrow[r] - b * HW;
-          bst_f32(o0, ok[r] ? (uint32_t)((b * a.cout + n) * HW + yx) * 4u : OOB, v[r]);
-        }
-      } else if constexpr (EPI == EPI_GRU_ZR) {
-        if (ncol0 < a.split) {  // z half
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            bst_bf16(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, sigmoidf_(v[r]));
-        } else {  // r half: r*h and r
-          const int c = n - a.split;
-          float h[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            h[r] = bld_bf16(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + c) * 2u : OOB);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float g = sigmoidf_(v[r]);
-            bst_bf16(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + c) * 2u : OOB, g * h[r]);
-            bst_bf16(o2, ok[r] ? (uint32_t)(mrow[r] * a.out2_stride + c) * 2u : OOB, g);
-          }
-        }
-      } else if constexpr (EPI == EPI_GRU_Q) {
-        float h[16], z[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          h[r] = bld_bf16(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + n) * 2u : OOB);
-          z[r] = bld_bf16(x1, ok[r] ? (uint32_t)(mrow[r] * a.aux1_stride + n) * 2u : OOB);
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float q = tanhf_(v[r]);
-          bst_bf16(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, h[r] + z[r] * (q - h[r]));
-          bst_bf16(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + n) * 2u : OOB, q);
-        }
-      } else if constexpr (EPI == EPI_DGRAD) {
-        // output segment of this 32-column tile (uniform)
-        int s = 0, base = 0;
-#pragma unroll
-        for (int q = 0; q < 2; ++q)
-          if (s + 1 < a.noseg && ncol0 >= base + a.oseg[s].cnt) { base += a.oseg[s].cnt; ++s; }
-        const OSeg o = a.oseg[s];
-        const int c = n - base;
-        const bool cok = c < o.real;
-        if (o.ob != nullptr) {  // relu-gated bf16 gradient
-          const rsrc_t ob = make_rsrc(o.ob, P_u * (uint32_t)o.ob_stride * 2u);
-          const rsrc_t ry = make_rsrc(o.ry, P_u * (uint32_t)o.ry_stride * 2u);
-          float y[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            y[r] = bld_bf16(ry, ok[r] && cok ? (uint32_t)(mrow[r] * o.ry_stride + c) * 2u : OOB);
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            bst_bf16(ob, ok[r] && cok ? (uint32_t)(mrow[r] * o.ob_stride + c) * 2u : OOB,
-                     y[r] > 0.f ? v[r] : 0.f);
-        } else if (o.ptr != nullptr) {
-          const rsrc_t od = make_rsrc(o.ptr, P_u * (uint32_t)o.stride * 4u);
-          uint32_t off[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            off[r] = ok[r] && cok ? (uint32_t)(mrow[r] * o.stride + c) * 4u : OOB;
-          if (o.acc) {
-            float pre[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) pre[r] = bld_f32(od, off[r]);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) bst_f32(od, off[r], pre[r] + v[r]);
-          } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) bst_f32(od, off[r], v[r]);
-          }
-        }
-      }
-    }
-}
-
+using namespace conv_detail;
 // Pipeline (per 64-deep K step, one barrier):  global loads for step t+2 are issued into one of
 // two register sets before the MFMAs of step t (two steps = ~1000+ MFMA cycles of latency cover),
 // the other set (step t+1, loaded one step earlier) is written to the idle LDS buffer after them.
 // Wave tile (32*TM) x (32*TN); WVM x (4/WVM) waves -> block tile BM x BN.  Larger wave tiles
 // cut LDS traffic per MFMA ((TM+TN)/(TM*TN) fragment reads per MFMA): at 2x2 the four SIMDs
 // already need the LDS's full 128 B/clk, so the big-M configs (4x2, 5x2) exist for that reason.
-template <int TM, int TN, int WVM>
-struct ConvTile {
-  static constexpr int WVN = 4 / WVM;
-  static constexpr int BM = 32 * TM * WVM, BN = 32 * TN * WVN;
-  static constexpr int LDS = 2 * (BM + BN) * 128;
-  static constexpr int OCC = LDS <= 65536 && TM * TN <= 4 ? 2 : 1;
-};
+
 
 template <int TM, int TN, int WVM, int EPI, bool SMALLC>
 __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_kernel(ConvFwdArgs a) {
@@ -419,161 +228,11 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
   conv_epilogue<TM, TN, WM, WN, EPI>(a, acc, m0, n0, wm, wn, lane, P, HW);
 }
 
-// ------------------------------------------------------------------ LDS-DMA variant
-// Same tiling / epilogues, but the A (input patch) and B (weight) tiles go global -> LDS with
-// buffer_load_dwordx4 ... lds: no staging VGPRs and no ds_write pass (on the register-staged
-// kernel the 13-cycle ds_write_b128 transfers cost as much LDS time as the fragment reads).
-// The DMA image is lane-linear (wave-uniform M0 base + 16 B x lane), so the XOR swizzle is
-// applied on the SOURCE side: the lane that lands in physical 16-B slot `pc` of row `row` loads
-// logical chunk pc ^ ((row >> 1) & 7); fragment reads use the same swz() as the register kernel.
-// Out-of-range taps / rows read as zeros through the range-checked descriptor (the DMA writes
-// the zeros).  Pipeline per K step: issue step t+1 into the other buffer, wait for this wave's
-// step-t DMAs with a counted vmcnt (step t+1 stays in flight), barrier, MFMAs, barrier.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-}
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-
-__device__ __forceinline__ void dma16(rsrc_t r, const uint4* lds_wave_base, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds_wave_base, 16, (int)voff, 0, 0, 0);
-}
-
-template <int TM, int TN, int WVM, int EPI>
-__global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_glds_kernel(ConvFwdArgs a) {
-  using T = ConvTile<TM, TN, WVM>;
-  constexpr int BM = T::BM, BN = T::BN, WM = 32 * TM, WN = 32 * TN;
-  constexpr int WAVES_N = T::WVN;
-  constexpr int A_CHUNKS = BM * 8, B_CHUNKS = BN * 8;
-  static_assert(A_CHUNKS % NT == 0 && B_CHUNKS % NT == 0, "whole wave instructions per stage");
-  constexpr int A_PER = A_CHUNKS / NT, B_PER = B_CHUNKS / NT;
-  constexpr int STAGE = A_CHUNKS + B_CHUNKS;  // 16-B slots per pipeline stage
-  constexpr int LPS = A_PER + B_PER;          // DMA instructions per thread per step
-
-  // ONE shared array (a second __shared__ object can make hipcc drain vmcnt before ds_reads)
-  __shared__ __attribute__((aligned(16))) uint4 smem[2 * STAGE];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int HW = a.H * a.W;
-  const int P = a.B * HW;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-
-  int a_pix[A_PER], a_y[A_PER], a_x[A_PER], a_lc[A_PER];
-#pragma unroll
-  for (int j = 0; j < A_PER; ++j) {
-    const int e = tid + j * NT;
-    const int row = e >> 3;
-    const int m = m0 + row;
-    const int mm = m < P ? m : 0;
-    const int r = mm % HW;
-    a_pix[j] = mm;
-    a_y[j] = m < P ? r / a.W : -(1 << 20);
-    a_x[j] = r % a.W;
-    a_lc[j] = ((e & 7) ^ ((row >> 1) & 7)) * 8;  // logical channel offset this lane fetches
-  }
-  uint32_t b_off[B_PER];
-#pragma unroll
-  for (int j = 0; j < B_PER; ++j) {
-    const int e = tid + j * NT;
-    const int row = e >> 3;
-    const int n = n0 + row;
-    const int lc = (e & 7) ^ ((row >> 1) & 7);
-    b_off[j] = n < a.cout ? (uint32_t)(((int64_t)n * a.kpad + lc * 8) * 2) : OOB;
-  }
-
-  const int nchunk = a.cin_pad / BK;
-  const int steps = a.KH * a.KW * nchunk;
-  rsrc_t seg_rs[3];
-#pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    const int qq = q < a.nseg ? q : 0;
-    seg_rs[q] = make_rsrc(a.seg[qq].ptr, (uint32_t)P * a.seg[qq].stride * 2u);
-  }
-  const rsrc_t w_rs = make_rsrc(a.wpk, (uint32_t)a.cout * a.kpad * 2u);
-
-  auto issue = [&](int t, int buf) {
-    const int tap = t / nchunk, ch = t - tap * nchunk;
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
-    const int c0 = ch * BK;
-    int s = 0, sbase = 0;
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      if (s + 1 < a.nseg && c0 >= sbase + a.seg[s].cnt) { sbase += a.seg[s].cnt; ++s; }
-    const rsrc_t rs = s == 0 ? seg_rs[0] : (s == 1 ? seg_rs[1] : seg_rs[2]);
-    const int stride = a.seg[s].stride;
-    const int dy = kh - a.PH, dx = kw - a.PW;
-    const int dpix = dy * a.W + dx;
-    const int coff = c0 - sbase;
-    const uint4* base = smem + buf * STAGE;
-#pragma unroll
-    for (int j = 0; j < A_PER; ++j) {
-      const int yy = a_y[j] + dy, xx = a_x[j] + dx;
-      const bool ok = (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
-      const uint32_t off = (uint32_t)(((a_pix[j] + dpix) * stride + coff + a_lc[j]) * 2);
-      dma16(rs, base + j * NT + wave * 64, ok ? off : OOB);
-    }
-    const uint32_t kb = (uint32_t)(t * BK * 2);
-#pragma unroll
-    for (int j = 0; j < B_PER; ++j)
-      dma16(w_rs, base + A_CHUNKS + j * NT + wave * 64, b_off[j] == OOB ? OOB : b_off[j] + kb);
-  };
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  auto compute = [&](int buf) {
-    const uint4* As = smem + buf * STAGE;
-    const uint4* Bs = As + A_CHUNKS;
-#pragma unroll
-    for (int kk = 0; kk < BK / 16; ++kk) {
-      bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * WM + i * 32 + (lane & 31);
-        af[i] = __builtin_bit_cast(bf16x8_t, As[swz(row, kk * 2 + (lane >> 5))]);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * WN + j * 32 + (lane & 31);
-        bfr[j] = __builtin_bit_cast(bf16x8_t, Bs[swz(row, kk * 2 + (lane >> 5))]);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  issue(0, 0);
-  for (int t = 0; t < steps; ++t) {
-    if (t + 1 < steps) {
-      issue(t + 1, (t + 1) & 1);
-      wait_vmcnt<LPS>();  // this wave's step-t DMAs landed; step t+1 stays in flight
-    } else {
-      wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_s_barrier();  // every wave's step-t DMAs landed
-    compute(t & 1);
-    __builtin_amdgcn_s_barrier();  // buffer t&1 free for step t+2
-  }
-
-  conv_epilogue<TM, TN, WM, WN, EPI>(a, acc, m0, n0, wm, wn, lane, P, HW);
-}
-
 // ------------------------------------------------------------------ tile configurations
 struct CfgDesc {
   int tm, tn, wvm, bm, bn;
   bool small_ok;
-  bool glds;  // LDS-DMA kernel (conv_fwd_glds_kernel)
+  int glds;  // 0: register-staged kernel; n: LDS-DMA kernel with n pipeline stages
 };
 // (keep in sync with the dispatch switch below)
 constexpr CfgDesc kCfgs[] = {
@@ -582,11 +241,18 @@ constexpr CfgDesc kCfgs[] = {
     {1, 1, 4, 128, 32, true, false},   {4, 2, 2, 256, 128, false, false},
     {5, 2, 1, 160, 256, false, false}, {5, 1, 1, 160, 128, false, false},
     {4, 2, 1, 128, 256, false, false}, {3, 2, 1, 96, 256, false, false},
-    // LDS-DMA variants
-    {2, 2, 2, 128, 128, false, true},  {1, 2, 2, 64, 128, false, true},
-    {2, 1, 2, 128, 64, false, true},   {4, 2, 2, 256, 128, false, true},
-    {4, 2, 1, 128, 256, false, true},  {3, 2, 1, 96, 256, false, true},
-    {5, 1, 1, 160, 128, false, true},  {1, 1, 2, 64, 64, false, true},
+    // LDS-DMA variants (last field: pipeline stages)
+    {2, 2, 2, 128, 128, false, 2},  {1, 2, 2, 64, 128, false, 2},
+    {2, 1, 2, 128, 64, false, 2},   {4, 2, 2, 256, 128, false, 2},
+    {4, 2, 1, 128, 256, false, 2},  {3, 2, 1, 96, 256, false, 2},
+    {5, 1, 1, 160, 128, false, 2},  {1, 1, 2, 64, 64, false, 2},
+    {2, 2, 2, 128, 128, false, 4},  {1, 2, 2, 64, 128, false, 3},
+    {5, 1, 1, 160, 128, false, 4},  {2, 1, 2, 128, 64, false, 4},
+    {1, 1, 2, 64, 64, false, 4},    {4, 2, 1, 128, 256, false, 3},
+    {3, 1, 1, 96, 128, false, 4},   {3, 1, 1, 96, 128, false, 2},
+    // one-round tiles for M = 34,224 (chairs, B = 12): 214 / 238 / 179 workgroups
+    {5, 2, 1, 160, 256, false, 2},  {5, 2, 1, 160, 256, false, 3},
+    {9, 1, 1, 288, 128, false, 2},  {3, 3, 2, 192, 192, false, 2},
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -598,13 +264,6 @@ void launch_one(const ConvFwdArgs& a, hipStream_t stream) {
   hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WVM, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
 }
 
-template <int EPI, int TM, int TN, int WVM>
-void launch_one_glds(const ConvFwdArgs& a, hipStream_t stream) {
-  using T = ConvTile<TM, TN, WVM>;
-  const int P = a.B * a.H * a.W;
-  dim3 grid(raft_cdiv(P, T::BM), raft_cdiv(a.cout, T::BN));
-  hipLaunchKernelGGL((conv_fwd_glds_kernel<TM, TN, WVM, EPI>), grid, dim3(NT), 0, stream, a);
-}
 
 template <int EPI, bool SMALLC>
 bool launch_cfg_idx(const ConvFwdArgs& a, int idx, hipStream_t stream) {
@@ -629,15 +288,9 @@ bool launch_cfg_idx(const ConvFwdArgs& a, int idx, hipStream_t stream) {
       case 7: launch_one<EPI, false, 5, 1, 1>(a, stream); return true;
       case 8: launch_one<EPI, false, 4, 2, 1>(a, stream); return true;
       case 9: launch_one<EPI, false, 3, 2, 1>(a, stream); return true;
-      case 10: launch_one_glds<EPI, 2, 2, 2>(a, stream); return true;
-      case 11: launch_one_glds<EPI, 1, 2, 2>(a, stream); return true;
-      case 12: launch_one_glds<EPI, 2, 1, 2>(a, stream); return true;
-      case 13: launch_one_glds<EPI, 4, 2, 2>(a, stream); return true;
-      case 14: launch_one_glds<EPI, 4, 2, 1>(a, stream); return true;
-      case 15: launch_one_glds<EPI, 3, 2, 1>(a, stream); return true;
-      case 16: launch_one_glds<EPI, 5, 1, 1>(a, stream); return true;
-      case 17: launch_one_glds<EPI, 1, 1, 2>(a, stream); return true;
-      default: return false;
+      default:
+        if (idx >= 0 && idx < kNumCfgs && kCfgs[idx].glds) return launch_conv_glds(a, EPI, idx, stream);
+        return false;
     }
   }
 }

@@ -283,29 +283,6 @@ __device__ __forceinline__ int wg_swz(int row) {
   return RB == 256 ? 4 * (row & 3) : 4 * ((row >> 1) & 1);
 }
 
-template <int N>
-__device__ __forceinline__ void wg_wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
-}
-
-// LDS-DMA issued from inline asm: hipcc does not know these writes LDS, so it cannot insert the
-// conservative `s_waitcnt vmcnt(0)` it otherwise places before every ds_read_b64_tr_b16 that
-// follows an LDS-DMA (which drained the next step's prefetch).  Completion is counted by hand
-// (wg_wait_vmcnt + barrier).  M0 is saved / restored inside the statement.
-__device__ __forceinline__ void wg_dma16(__amdgpu_buffer_rsrc_t r, uint32_t lds_addr, uint32_t voff) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 4\n\t"
-      "buffer_load_dwordx4 %2, %3, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(lds_addr), "v"(voff), "s"(r)
-      : "memory");
-}
-
 template <int BM>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_multi_kernel(ConvWgradArgs a, WgradItems it,
                                                                  float* __restrict__ db) {
@@ -386,7 +363,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_multi_kernel(ConvWgradArgs a
     x_x[j] = r - (r / a.W) * a.W;
   }
 
-  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) uint8_t*)smem;
+  const uint32_t lds0 = raft_lds_addr(smem);
   const uint32_t wave_off = __builtin_amdgcn_readfirstlane(wave * 64 * 16);
   auto issue = [&](int t, int buf) {
     const uint32_t base = lds0 + buf * STAGE + wave_off;
@@ -395,7 +372,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_multi_kernel(ConvWgradArgs a
     for (int j = 0; j < G_PER; ++j) {
       const int p = pb + g_row[j];
       const uint32_t off = (p < p_end && g_col[j] != OOB) ? (uint32_t)p * a.g_stride * 2u + g_col[j] : OOB;
-      wg_dma16(g_rs, base + j * NT * 16, off);
+      raft_dma16(g_rs, base + j * NT * 16, off);
     }
 #pragma unroll
     for (int j = 0; j < X_PER; ++j) {
@@ -408,7 +385,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_multi_kernel(ConvWgradArgs a
       const int s = __builtin_amdgcn_readfirstlane(x_seg[j]);
       const uint32_t off = (uint32_t)(((p + x_dpix[j]) * a.seg[s].stride + x_coff[j]) * 2);
       const rsrc_t rs = s == 0 ? seg_rs[0] : (s == 1 ? seg_rs[1] : seg_rs[2]);
-      wg_dma16(rs, base + (GCH + j * NT) * 16, ok ? off : OOB);
+      raft_dma16(rs, base + (GCH + j * NT) * 16, ok ? off : OOB);
       // advance this chunk's pixel by BKP -- branch-free (a divergent wrap loop here made hipcc
       // drain vmcnt(0) before it, i.e. wait for the DMAs just issued): q = (x + BKP) / W by a
       // magic multiply (exact for (x + BKP) * W < 2^32), at most one image wrap (host: HW >= 128)
@@ -487,9 +464,9 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_multi_kernel(ConvWgradArgs a
   for (int t = 0; t < steps; ++t) {
     if (t + 1 < steps) {
       issue(t + 1, (t + 1) & 1);
-      wg_wait_vmcnt<LPS>();
+      raft_wait_vmcnt<LPS>();
     } else {
-      wg_wait_vmcnt<0>();
+      raft_wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
     compute(t & 1);

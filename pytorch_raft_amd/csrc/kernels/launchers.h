@@ -131,6 +131,8 @@ struct ConvFwdArgs {
 // tile shape chosen per geometry: autotuned once (outside stream capture) and cached;
 // RAFT_CONV_CFG=<idx> forces a config, RAFT_CONV_AUTOTUNE=0 uses the analytic heuristic
 bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStream_t stream);
+// LDS-DMA kernel of config `idx` (conv_glds.hip); false for a non-LDS-DMA index
+bool launch_conv_glds(const ConvFwdArgs& a, int epi, int idx, hipStream_t stream);
 // rows of 12 ints: P H W KH KW cin cout small epi_class cfg BM BN
 int conv_tuned_table(int* out, int max_rows);
 

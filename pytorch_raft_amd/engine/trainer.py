@@ -42,6 +42,13 @@ class TrainState:
             self.sync = pdist.GradSync(model, bucket_mb=getattr(args, 'bucket_mb', 8.0),
                                        order=pdist.raft_grad_order)
         self.has_buffers = any(True for _ in model.buffers())
+        if device.type == 'cuda':
+            # optional: batched update-block weight gradients on a side stream, overlapped with
+            # the encoder backward (gradients land in .grad at the end of backward).  Measured
+            # neutral on MI355X at the chairs shape (the wgrad grids already fill every CU), so
+            # off unless args.wgrad_overlap is set.
+            from ..ops import update_hip
+            update_hip.set_wgrad_overlap(getattr(args, 'wgrad_overlap', False))
         self.nonfinite = torch.zeros((), device=device)
         self.total_steps = 0
 

@@ -109,6 +109,7 @@ class _Packed:
         self.dw = {}
         self.db = {}
         self.pending = {}  # conv name -> [(g, g_off, segs)] awaiting the batched weight gradient
+        self.device = device
         with torch.no_grad():
             for s in SPECS:
                 ws = [w for w, _ in params_by_layer[s.name]]
@@ -175,6 +176,8 @@ def _flush_wgrad(pk):
 class _State:
     def __init__(self):
         self.packed = None
+        self.overlap = False
+        self.params = []
 
 
 class _UpdateWeights(torch.autograd.Function):
@@ -189,26 +192,96 @@ class _UpdateWeights(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, _tok):
-        pk = ctx.state.packed
+        st = ctx.state
+        pk = st.packed
+        st.packed = None
+        if st.overlap and pk.device.type == 'cuda':
+            return _backward_overlapped(st, pk, ctx.n)
         _flush_wgrad(pk)
-        grads = []
-        for s in SPECS:
-            dw, db = pk.dw[s.name], pk.db[s.name]
-            if s.scale != 1.0:
-                dw = dw * s.scale
-                db = db * s.scale
-            if s.small:
-                wg = C.unpack_weight_grad_small(dw, s.cout, s.in_real[0], s.k)
-            else:
-                wg = C.unpack_weight_grad(dw, s.cout, s.in_real, s.in_pad, s.k)
-            n_parts = 2 if s.name in ('zr1', 'zr2', 'head') else 1
-            if n_parts == 1:
-                grads += [wg, db]
-            else:
-                h = s.cout // 2
-                grads += [wg[:h], db[:h], wg[h:], db[h:]]
-        ctx.state.packed = None
-        return (None, *grads)
+        return (None, *_unpack_grads(pk))
+
+
+def _unpack_grads(pk):
+    grads = []
+    for s in SPECS:
+        dw, db = pk.dw[s.name], pk.db[s.name]
+        if s.scale != 1.0:
+            dw = dw * s.scale
+            db = db * s.scale
+        if s.small:
+            wg = C.unpack_weight_grad_small(dw, s.cout, s.in_real[0], s.k)
+        else:
+            wg = C.unpack_weight_grad(dw, s.cout, s.in_real, s.in_pad, s.k)
+        n_parts = 2 if s.name in ('zr1', 'zr2', 'head') else 1
+        if n_parts == 1:
+            grads += [wg, db]
+        else:
+            h = s.cout // 2
+            grads += [wg[:h], db[:h], wg[h:], db[h:]]
+    return grads
+
+
+# ---------------------------------------------------------------- wgrad / encoder-backward overlap
+# The batched weight gradients (~15 % of a training step, MFMA-bound) depend on nothing the rest
+# of the backward produces, while the encoder backward that follows them (MIOpen convs + norm
+# passes) is mostly memory-bound.  With overlap enabled (set_wgrad_overlap; the trainer turns it
+# on) the flush runs on a side HIP stream concurrently with the rest of the backward, and the
+# update-block parameter gradients are written into ``.grad`` by an end-of-backward callback
+# after the main stream has joined the side stream -- so every consumer (optimizer, clip, RCCL
+# bucket sync, which launches never-hooked buckets in ``finish``) sees finished gradients.
+# Off by default: a plain autograd.grad() caller must get the gradients as return values.
+_OVERLAP = False
+_SIDE = {}
+
+
+def set_wgrad_overlap(enabled):
+    global _OVERLAP
+    _OVERLAP = bool(enabled)
+
+
+def _side_stream(dev):
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
+
+
+def _backward_overlapped(st, pk, n):
+    dev = pk.device
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(main)
+    # everything the side stream reads was allocated on the main stream: keep it from being
+    # recycled by main-stream allocations until the side stream is done with it
+    for items in pk.pending.values():
+        for g, _, segs in items:
+            g.record_stream(side)
+            for buf, _, _ in segs:
+                buf.record_stream(side)
+    for t in list(pk.dw.values()) + list(pk.db.values()):
+        t.record_stream(side)
+    params = st.params
+    with torch.cuda.stream(side):
+        _flush_wgrad(pk)
+        # .grad is assigned directly (no AccumulateGrad): match each parameter's strides, as
+        # AccumulateGrad's layout contract would (fused optimizers require it)
+        grads = [g if g.stride() == prm.stride() else torch.empty_like(prm).copy_(g)
+                 for prm, g in zip(params, _unpack_grads(pk))]
+
+    def _join():
+        main.wait_stream(side)
+        with torch.no_grad():
+            for prm, g in zip(params, grads):
+                if not prm.requires_grad:
+                    continue
+                g.record_stream(main)
+                if prm.grad is None:
+                    prm.grad = g
+                else:
+                    prm.grad.add_(g)
+
+    torch.autograd.Variable._execution_engine.queue_callback(_join)
+    return (None,) * (1 + n)
 
 
 def _bf16(shape, dev):
@@ -361,6 +434,8 @@ class HipUpdateBlock:
         self.state.ub = update_block
         params = flat_params(update_block)
         self.state.need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        self.state.params = params
+        self.state.overlap = _OVERLAP
         self.token = _UpdateWeights.apply(self.state, *params)
 
     def __call__(self, h, inp, corr, flow):

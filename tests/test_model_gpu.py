@@ -85,3 +85,28 @@ def test_alternate_training_grads_match_allpairs(ext_ops):
         grads[alt] = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
     rel = (grads[True] - grads[False]).norm() / grads[False].norm()
     assert rel < 2e-2, rel
+
+
+def test_wgrad_overlap_matches_inline(ext_ops):
+    """Side-stream weight-gradient flush (end-of-backward join) == in-graph gradients, up to the
+    run-to-run noise of the float-atomic split-K reductions (measured with overlap off twice)."""
+    from pytorch_raft_amd.ops import update_hip
+    from pytorch_raft_amd.ops.loss import sequence_loss
+    i1, i2, flow, valid = make_pair_batch(2, 128, 160, device=DEV)
+    runs = []
+    try:
+        for overlap in (False, False, True):
+            update_hip.set_wgrad_overlap(overlap)
+            m = _model('hip', mixed=True).train()
+            preds = m(i1, i2, iters=3)
+            loss, _ = sequence_loss(preds, flow, valid, 0.8, impl='hip')
+            loss.backward()
+            torch.cuda.synchronize()
+            runs.append([p.grad.clone() for p in m.update_block.parameters()])
+    finally:
+        update_hip.set_wgrad_overlap(False)
+    for a, a2, b in zip(*runs):
+        noise = (a - a2).abs().max().item()
+        scale = a.abs().max().item()
+        diff = (a - b).abs().max().item()
+        assert diff <= 4 * noise + 1e-4 * scale + 1e-7, (diff, noise, scale)
