@@ -146,7 +146,8 @@ Tensor corr_window_grad(const Tensor& coords, const Tensor& dout, int64_t levels
 
 // sum of all iterations' window gradients -> dcorr (B, N, N) = level-0 gradient * 1/sqrt(C)
 Tensor corr_window_reduce(const std::vector<Tensor>& coords, const std::vector<Tensor>& wgs,
-                          int64_t H, int64_t W, int64_t levels, int64_t radius, double inv_sqrt_c) {
+                          int64_t H, int64_t W, int64_t levels, int64_t radius, double inv_sqrt_c,
+                          bool out_bf16) {
   TORCH_CHECK(!coords.empty() && coords.size() == wgs.size() && coords.size() <= RAFT_MAX_WIN,
               "1..", RAFT_MAX_WIN, " iterations");
   const int64_t B = coords[0].size(0), N = H * W;
@@ -166,9 +167,9 @@ Tensor corr_window_reduce(const std::vector<Tensor>& coords, const std::vector<T
   const int lds = corr_window_reduce_lds_bytes((int)H, (int)W, (int)levels);
   TORCH_CHECK(lds <= 64 * 1024, "feature map too large for the LDS plane reduction");
   c10::DeviceGuard g(coords[0].device());
-  Tensor out = at::empty({B, N, N}, coords[0].options());
+  Tensor out = at::empty({B, N, N}, coords[0].options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
   TORCH_CHECK(launch_corr_window_reduce(wl, (int)levels, (int)B, (int)H, (int)W, (int)radius,
-                                        (float)inv_sqrt_c, out.data_ptr<float>(), cur_stream()),
+                                        (float)inv_sqrt_c, out.data_ptr(), out_bf16 ? 1 : 0, cur_stream()),
               "unsupported radius");
   return out;
 }
@@ -783,7 +784,15 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     TORCH_CHECK(out_cnt[o] % 32 == 0, "dgrad output segments must be multiples of 32 channels");
     TORCH_CHECK(out_real[o] <= out_cnt[o] && out_off[o] >= 0 && out_off[o] + out_real[o] <= outs[o].size(3),
                 "dgrad output slice out of range");
-    if (relu_mode) {
+    if (relu_mode && o < relu_off.size() && relu_off[o] < 0) {
+      // plain bf16 output (relu_off < 0: no ReLU gate)
+      TORCH_CHECK(!out_acc[o], "the bf16 dgrad output cannot accumulate");
+      a.oseg[o].ptr = nullptr;
+      a.oseg[o].ob = reinterpret_cast<uint16_t*>(outs[o].data_ptr<at::BFloat16>()) + out_off[o];
+      a.oseg[o].ob_stride = (int)outs[o].size(3);
+      a.oseg[o].ry = nullptr;
+      a.oseg[o].ry_stride = 0;
+    } else if (relu_mode) {
       // bf16 output = relu-gated gradient; relu_y[o] is the forward relu output of these channels
       TORCH_CHECK(o < relu_y.size(), "bf16 dgrad output needs its relu output tensor");
       const Tensor& y = relu_y[o];
@@ -1039,7 +1048,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout, bool nhwc=False) -> Tensor[]");
   m.def("corr_lookup_nhwc_(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
   m.def("corr_window_grad(Tensor coords, Tensor dout, int levels, int radius) -> Tensor");
-  m.def("corr_window_reduce(Tensor[] coords, Tensor[] wgs, int H, int W, int levels, int radius, float inv_sqrt_c) -> Tensor");
+  m.def("corr_window_reduce(Tensor[] coords, Tensor[] wgs, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16=False) -> Tensor");
   m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off) -> ()");
   m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale) -> ()");
   m.def("gru_q_bwd_(Tensor dh, Tensor z, Tensor q, Tensor hprev, Tensor(a!) dpre_q, Tensor(b!) dz, Tensor(c!) dhprev) -> ()");

@@ -160,7 +160,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
         const OSeg o = a.oseg[s];
         const int c = n - base;
         const bool cok = c < o.real;
-        if (o.ob != nullptr) {  // relu-gated bf16 gradient
+        if (o.ob != nullptr && o.ry == nullptr) {  // plain bf16 gradient
+          const rsrc_t ob = make_rsrc(o.ob, P_u * (uint32_t)o.ob_stride * 2u);
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            bst_bf16(ob, ok[r] && cok ? (uint32_t)(mrow[r] * o.ob_stride + c) * 2u : OOB, v[r]);
+        } else if (o.ob != nullptr) {  // relu-gated bf16 gradient
           const rsrc_t ob = make_rsrc(o.ob, P_u * (uint32_t)o.ob_stride * 2u);
           const rsrc_t ry = make_rsrc(o.ry, P_u * (uint32_t)o.ry_stride * 2u);
           float y[16];

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void corr_window_grad_kernel(const float* __re
 template <int R>
 __global__ __launch_bounds__(256) void corr_window_reduce_kernel(WinList wl_, int levels, int B, int H,
                                                                  int W, float inv_sqrt_c,
-                                                                 float* __restrict__ out) {
+                                                                 void* __restrict__ out, int out_bf16) {
   constexpr int D = 2 * R + 1, E = D + 1;
   extern __shared__ float planes[];
   const int N = H * W;
@@ -189,7 +189,8 @@ __global__ __launch_bounds__(256) void corr_window_reduce_kernel(WinList wl_, in
     }
     __syncthreads();
   }
-  float* O = out + ((int64_t)b * N + i) * N;
+  float* O = (float*)out + ((int64_t)b * N + i) * N;
+  uint16_t* Ob = (uint16_t*)out + ((int64_t)b * N + i) * N;
   for (int e = threadIdx.x; e < N; e += 256) {
     const int y = e / W, x = e % W;
     float v = planes[e];
@@ -199,7 +200,8 @@ __global__ __launch_bounds__(256) void corr_window_reduce_kernel(WinList wl_, in
       if (yl < hs[l] && xl < ws[l]) v += s * planes[off[l] + yl * ws[l] + xl];
       s *= 0.25f;
     }
-    O[e] = v * inv_sqrt_c;
+    if (out_bf16) Ob[e] = raft_f32_to_bf16(v * inv_sqrt_c);
+    else O[e] = v * inv_sqrt_c;
   }
 }
 
@@ -239,11 +241,11 @@ int corr_window_reduce_lds_bytes(int H, int W, int levels) {
 }
 
 bool launch_corr_window_reduce(const WinList& wl, int levels, int B, int H, int W, int radius,
-                               float inv_sqrt_c, float* out, hipStream_t stream) {
+                               float inv_sqrt_c, void* out, int out_bf16, hipStream_t stream) {
   const int lds = corr_window_reduce_lds_bytes(H, W, levels);
   dim3 grid((unsigned)(B * H * W));
-  if (radius == 4) hipLaunchKernelGGL(corr_window_reduce_kernel<4>, grid, dim3(256), lds, stream, wl, levels, B, H, W, inv_sqrt_c, out);
-  else if (radius == 3) hipLaunchKernelGGL(corr_window_reduce_kernel<3>, grid, dim3(256), lds, stream, wl, levels, B, H, W, inv_sqrt_c, out);
+  if (radius == 4) hipLaunchKernelGGL(corr_window_reduce_kernel<4>, grid, dim3(256), lds, stream, wl, levels, B, H, W, inv_sqrt_c, out, out_bf16);
+  else if (radius == 3) hipLaunchKernelGGL(corr_window_reduce_kernel<3>, grid, dim3(256), lds, stream, wl, levels, B, H, W, inv_sqrt_c, out, out_bf16);
   else return false;
   return true;
 }

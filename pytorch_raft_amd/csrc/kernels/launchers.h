@@ -190,8 +190,9 @@ bool launch_corr_lookup_tile(const float* const* lvl, const int* hs, const int* 
 bool launch_corr_window_grad(const float* coords, const uint16_t* dout, int cbuf, float* wg, int B,
                              int H, int W, int levels, int radius, hipStream_t stream);
 int corr_window_reduce_lds_bytes(int H, int W, int levels);
+// out: (B, N, N) fp32, or bf16 when out_bf16 (mixed-precision backward GEMMs)
 bool launch_corr_window_reduce(const WinList& wl, int levels, int B, int H, int W, int radius,
-                               float inv_sqrt_c, float* out, hipStream_t stream);
+                               float inv_sqrt_c, void* out, int out_bf16, hipStream_t stream);
 
 // ---- NHWC convex upsample (upsample.hip)
 bool launch_convex_up_nhwc_fwd(const float* flow, const uint16_t* mask, float* out, int B, int H,

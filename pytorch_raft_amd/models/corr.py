@@ -122,7 +122,10 @@ class CorrBlock:
         self.radius = radius
         self.hip = _use_hip(fmap1, impl)
         if self.hip:
-            self.volume = corr_ops.AllPairsVolume(fmap1.float(), fmap2.float(), num_levels)
+            # precision='bf16' (mixed precision): the volume and lookups stay fp32, the backward
+            # GEMMs take a bf16 dcorr (the fmaps are bf16 encoder outputs, exact in bf16)
+            self.volume = corr_ops.AllPairsVolume(fmap1.float(), fmap2.float(), num_levels,
+                                                  bf16_backward=(precision == 'bf16'))
             self.corr_pyramid = None
         else:
             self.corr_pyramid = torch_corr_pyramid(fmap1, fmap2, num_levels)

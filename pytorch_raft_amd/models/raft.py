@@ -114,7 +114,8 @@ class RAFT(nn.Module):
                                          impl=self.corr_impl,
                                          precision='bf16' if self.args.mixed_precision else 'fp32')
         else:
-            corr_fn = CorrBlock(fmap1, fmap2, radius=self.args.corr_radius, impl=self.corr_impl)
+            corr_fn = CorrBlock(fmap1, fmap2, radius=self.args.corr_radius, impl=self.corr_impl,
+                                precision='bf16' if self.args.mixed_precision else 'fp32')
 
         with self._autocast(dev):
             cnet = self.cnet(image1)

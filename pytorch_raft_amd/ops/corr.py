@@ -35,6 +35,7 @@ class _State:
         self.grad_f1 = None
         self.windows = []
         self.radius = None
+        self.bf16_bwd = False
 
 
 class _AllPairsBuild(torch.autograd.Function):
@@ -56,21 +57,28 @@ class _AllPairsBuild(torch.autograd.Function):
             return None, None, None, None
         b, c, h, w = fmap1.shape
         dcorr = None
+        # mixed precision, window path only: dcorr in bf16 and bf16 GEMMs (fp32 accumulation);
+        # the fmaps are bf16 encoder outputs, so only the dcorr rounding differs from fp32
+        bf16 = st.bf16_bwd and st.grad is None and bool(st.windows)
         if st.grad is not None:
             dcorr = _ext.ops().corr_pyr_grad_reduce(st.grad, 1.0 / math.sqrt(c))  # (B, N, N)
         if st.windows:
             dw = _ext.ops().corr_window_reduce([x[0] for x in st.windows], [x[1] for x in st.windows],
-                                               h, w, len(st.pyramid), st.radius, 1.0 / math.sqrt(c))
+                                               h, w, len(st.pyramid), st.radius, 1.0 / math.sqrt(c),
+                                               bf16)
             dcorr = dw if dcorr is None else dcorr + dw
         st.grad = None
         st.windows = []
         st.pyramid = None
         f1 = fmap1.view(b, c, h * w)
         f2 = fmap2.view(b, c, h * w)
-        # dF1 = F2 dC^T, dF2 = F1 dC  (library GEMMs: plain fp32 bmm)
+        if bf16:
+            f1 = f1.to(torch.bfloat16)
+            f2 = f2.to(torch.bfloat16)
+        # dF1 = F2 dC^T, dF2 = F1 dC  (library GEMMs)
         g1 = torch.bmm(f2, dcorr.transpose(1, 2)).view(b, c, h, w)
         g2 = torch.bmm(f1, dcorr).view(b, c, h, w)
-        return g1, g2, None, None
+        return g1.float(), g2.float(), None, None
 
 
 class _AllPairsLookup(torch.autograd.Function):
@@ -99,7 +107,8 @@ class _AllPairsLookupNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, token, coords, radius, state, cbuf):
         b, _, h, w = coords.shape
-        out = torch.zeros(b, h, w, cbuf, device=coords.device, dtype=torch.bfloat16)
+        # the tile kernel writes every channel of each pixel row, padding included
+        out = torch.empty(b, h, w, cbuf, device=coords.device, dtype=torch.bfloat16)
         _ext.ops().corr_lookup_nhwc_(state.pyramid, coords, radius, out)
         ctx.state = state
         ctx.radius = radius
@@ -134,8 +143,9 @@ def _window_reduce_fits(h, w, levels):
 
 
 class AllPairsVolume:
-    def __init__(self, fmap1, fmap2, num_levels=4):
+    def __init__(self, fmap1, fmap2, num_levels=4, bf16_backward=False):
         self.state = _State()
+        self.state.bf16_bwd = bool(bf16_backward)
         self.levels = num_levels
         self.token = _AllPairsBuild.apply(fmap1.contiguous(), fmap2.contiguous(), num_levels,
                                           self.state)

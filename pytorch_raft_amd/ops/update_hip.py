@@ -303,7 +303,7 @@ class _UpdateIter(torch.autograd.Function):
         B, H, W, _ = h.shape
         dev = h.device
         sh = (B, H, W)
-        flowb = torch.zeros(*sh, 8, device=dev, dtype=torch.bfloat16)
+        flowb = _bf16(sh + (8,), dev)  # flow_prep writes all 8 channels
         mf = _bf16(sh + (128,), dev)
         ops = _ext.ops()
         ops.flow_prep_(flow, flowb, mf, 126)
@@ -365,7 +365,9 @@ class _UpdateIter(torch.autograd.Function):
             ReLU, (buffer bf16, offset, slot_cnt, real, 0, relu_out, relu_out_offset)."""
             s = SPEC[name]
             ry = [o[5] if len(o) > 5 else o[0] for o in outs]
-            roff = [int(o[6]) if len(o) > 5 else 0 for o in outs]
+            # relu offset -1 marks a plain (ungated) bf16 output
+            roff = [int(o[6]) if len(o) > 5 else (-1 if o[0].dtype == torch.bfloat16 else 0)
+                    for o in outs]
             ops.conv_dgrad_([g[0] for g in gsegs], [g[1] for g in gsegs], [g[2] for g in gsegs],
                             pk.wd[name], s.k[0], s.k[1], s.pad[0], s.pad[1], 2 if small else 0,
                             float(scale), [o[0] for o in outs], [o[1] for o in outs],
@@ -381,7 +383,7 @@ class _UpdateIter(torch.autograd.Function):
         wgrad('m2', gmask, 0, [(fm, 256, 256)])
         dgrad('m2', [(gmask, 0, 576)], [(dpre_head, 256, 256, 256, 0, fm, 256)], scale=0.25)
         # ---- flow head conv2 -> delta
-        gd = torch.zeros(*sh, 8, device=dev, dtype=torch.bfloat16)
+        gd = _bf16(sh + (8,), dev)  # flow_prep writes all 8 channels
         ops.flow_prep_(gdelta.contiguous().float(), gd, None, 0)
         wgrad('fh2', gd, 0, [(fm, 0, 256)])
         dgrad('fh2', [(gd, 0, 8)], [(dpre_head, 0, 256, 256, 0, fm, 0)], small=True)
@@ -390,8 +392,9 @@ class _UpdateIter(torch.autograd.Function):
         dh = gh.float().contiguous() if gh is not None else _f32(sh + (HD,), dev, zero=True)
         dgrad('head', [(dpre_head, 0, 512)], [(dh, 0, HD, HD, 1)])
 
-        dinp = _f32(sh + (HD,), dev, zero=True)
-        dmf = _f32(sh + (128,), dev, zero=True)
+        dinp = _f32(sh + (HD,), dev)
+        dmf = _f32(sh + (128,), dev)
+        first = 1  # the first dgrad into dinp / dmf (q2's) stores: no zero fill
         for tag, (hin, z, rh, r, q) in (('2', (h1, z2, rh2, r2, q2)), ('1', (h0, z1, rh1, r1, q1))):
             dpre_q = _bf16(sh + (HD,), dev)
             dz = _f32(sh + (HD,), dev)
@@ -400,7 +403,8 @@ class _UpdateIter(torch.autograd.Function):
             wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)])
             drh = _f32(sh + (HD,), dev)
             dgrad('q' + tag, [(dpre_q, 0, HD)],
-                  [(drh, 0, HD, HD, 0), (dinp, 0, HD, HD, 1), (dmf, 0, 128, 128, 1)])
+                  [(drh, 0, HD, HD, 0), (dinp, 0, HD, HD, 1 - first), (dmf, 0, 128, 128, 1 - first)])
+            first = 0
             dpre_zr = _bf16(sh + (2 * HD,), dev)
             ops.gru_zr_bwd_(drh, dz, z, r, hin, dpre_zr, dhp)
             wgrad('zr' + tag, dpre_zr, 0, [(hin, 0, HD), (inp, 0, HD), (mf, 0, 128)])
@@ -421,7 +425,8 @@ class _UpdateIter(torch.autograd.Function):
         dgrad('f2', [(dpre_cf, 192, 64)], [(dpre_f1, 0, 128, 128, 0, f1, 0)])
         wgrad('f1', dpre_f1, 0, [(flowb, 0, 8)])
         wgrad('c1', dpre_c1, 0, [(corr, 0, CORR_BUF)])
-        dcorr = _f32(sh + (CORR_BUF,), dev)
+        # bf16 (the dtype of the corr input): autograd would otherwise cast an fp32 gradient
+        dcorr = _bf16(sh + (CORR_BUF,), dev)
         dgrad('c1', [(dpre_c1, 0, 256)], [(dcorr, 0, CORR_BUF, 324, 0)])  # slots 324.. unused
         return (torch.zeros((), device=dev), dh, dinp, dcorr, None, None)
 

@@ -4,7 +4,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py tests/test_model_gpu.py tests/test_update_hip_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_iter.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py tests/test_model_gpu.py tests/test_update_hip_gpu.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_iter.log 2>&1
 rc=$?; tail -4 gpurun_out/pytest_iter.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 if [ -n "$PMC_LAYER" ]; then bash scripts/gpu_pmc_conv2.sh $PMC_LAYER $PMC_CFGS || exit $?; fi

@@ -50,8 +50,9 @@ def _returns():
         b, _, h, w = coords.shape
         return torch.zeros(b, h * w, levels, 2 * r + 2, 2 * r + 2)
 
-    def win_reduce(coords, wgs, h, w, levels, r, s):
-        return torch.zeros(coords[0].shape[0], h * w, h * w)
+    def win_reduce(coords, wgs, h, w, levels, r, s, bf16=False):
+        return torch.zeros(coords[0].shape[0], h * w, h * w,
+                           dtype=torch.bfloat16 if bf16 else torch.float32)
 
     return {'corr_build': corr_build, 'corr_lookup_fwd': lookup, 'corr_pyr_grad_reduce': reduce,
             'corr_window_grad': win_grad, 'corr_window_reduce': win_reduce,

@@ -196,8 +196,9 @@ def test_lookup_deterministic(ext_ops):
     assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
 
 
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
 @pytest.mark.parametrize('hw', [(16, 20), (13, 19), (46, 62)])
-def test_lookup_nhwc_window_backward(ext_ops, hw):
+def test_lookup_nhwc_window_backward(ext_ops, hw, precision):
     """bf16 NHWC lookup (fused update-block input) + compact window backward vs grid_sample."""
     h, w = hw
     b, c, radius = 2, 256, 4
@@ -215,7 +216,7 @@ def test_lookup_nhwc_window_backward(ext_ops, hw):
     g1_ref, g2_ref = f1.grad.clone(), f2.grad.clone()
     f1.grad = f2.grad = None
 
-    blk = CorrBlock(f1, f2, num_levels=levels, radius=radius, impl='hip')
+    blk = CorrBlock(f1, f2, num_levels=levels, radius=radius, impl='hip', precision=precision)
     loss = 0
     for co, go in zip(coords, gouts):
         out = blk.lookup_nhwc(co, 384)
@@ -226,8 +227,10 @@ def test_lookup_nhwc_window_backward(ext_ops, hw):
         assert torch.all(out[..., nc:] == 0)
         loss = loss + (out.float() * go.float()).sum()
     loss.backward()
-    torch.testing.assert_close(f1.grad, g1_ref, atol=3e-3, rtol=3e-3)
-    torch.testing.assert_close(f2.grad, g2_ref, atol=3e-3, rtol=3e-3)
+    # bf16: dcorr rounded to bf16 before the (fp32-accumulating) backward GEMMs
+    tol = 3e-3 if precision == 'fp32' else 1e-2 * max(g1_ref.abs().max().item(), 1.0)
+    torch.testing.assert_close(f1.grad, g1_ref, atol=tol, rtol=3e-3 if precision == 'fp32' else 2e-2)
+    torch.testing.assert_close(f2.grad, g2_ref, atol=tol, rtol=3e-3 if precision == 'fp32' else 2e-2)
 
 
 @pytest.mark.parametrize('hw', [(8, 9), (46, 62)])
