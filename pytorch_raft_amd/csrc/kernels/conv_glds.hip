@@ -114,27 +114,34 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // fragments of k-slice kk+1 are read from LDS before the MFMAs of slice kk (two register sets),
+  // so each ds_read has a whole slice of MFMAs to land instead of one or two
   auto compute = [&](int buf) {
     const uint4* As = smem + buf * STAGE;
     const uint4* Bs = As + A_CHUNKS;
-#pragma unroll
-    for (int kk = 0; kk < BK / 16; ++kk) {
-      bf16x8_t af[TM], bfr[TN];
+    bf16x8_t af[2][TM], bfr[2][TN];
+    auto rd = [&](int kk, int set) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WM + i * 32 + (lane & 31);
-        af[i] = __builtin_bit_cast(bf16x8_t, As[swz(row, kk * 2 + (lane >> 5))]);
+        af[set][i] = __builtin_bit_cast(bf16x8_t, As[swz(row, kk * 2 + (lane >> 5))]);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WN + j * 32 + (lane & 31);
-        bfr[j] = __builtin_bit_cast(bf16x8_t, Bs[swz(row, kk * 2 + (lane >> 5))]);
+        bfr[set][j] = __builtin_bit_cast(bf16x8_t, Bs[swz(row, kk * 2 + (lane >> 5))]);
       }
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const int cur = kk & 1;
+      if (kk + 1 < BK / 16) rd(kk + 1, cur ^ 1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[cur][i], bfr[cur][j], acc[i][j], 0, 0, 0);
     }
   };
 

@@ -18,6 +18,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 namespace {
 
 struct PyrC4 {
@@ -91,6 +93,99 @@ __global__ __launch_bounds__(256) void corr_lookup_tile_kernel(PyrC4 pyr, const 
     *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i) * cbuf + ch * 8) =
         make_uint4(v[0] | ((uint32_t)v[1] << 16), v[2] | ((uint32_t)v[3] << 16),
                    v[4] | ((uint32_t)v[5] << 16), v[6] | ((uint32_t)v[7] << 16));
+  }
+}
+
+// Window-staged lookup (the launcher's kernel): the (2r+2)^2 integer window of every (pixel,
+// level) is first gathered into LDS with lanes running along the window rows (each row is 2r+2
+// consecutive floats of the pixel's correlation plane: a few wide requests per wave instead of a
+// scalar load per lane per tap), all loads of a level issued before any is consumed (range-checked
+// buffer loads: out-of-plane window cells read 0 with no branch).  The (2r+1)^2 bilinear taps are
+// then interpolated from LDS into the bf16 pixel-row tile, which is streamed out as above.
+constexpr int TPW = 32;  // pixels per workgroup
+
+template <int R>
+__global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const float* __restrict__ coords,
+                                                              uint16_t* __restrict__ out, int cbuf,
+                                                              int B, int H, int W, int levels) {
+  constexpr int D = 2 * R + 1, E = D + 1, EE = E * E, DD = D * D;
+  constexpr int ROW = (4 * DD + 7) / 8 * 8;
+  constexpr int PER = (TPW * EE + 255) / 256;  // window cells per thread per level
+  constexpr uint32_t OOB = 0x80000000u;
+  __shared__ float win[TPW * 4 * EE];
+  __shared__ float cxy[TPW * 4 * 2];
+  __shared__ __attribute__((aligned(16))) uint16_t tile[TPW * ROW];
+  const int N = H * W;
+  const int tiles = (N + TPW - 1) / TPW;
+  const int b = blockIdx.x / tiles;
+  const int i0 = (blockIdx.x % tiles) * TPW;
+  const int tid = threadIdx.x;
+  if (tid < TPW * 4) {  // level-scaled lookup centre per (pixel, level)
+    const int px = tid >> 2, l = tid & 3;
+    const int i = min(i0 + px, N - 1);
+    const float inv = 1.0f / (float)(1 << l);
+    cxy[tid * 2] = clampc(coords[((int64_t)b * 2) * N + i] * inv);
+    cxy[tid * 2 + 1] = clampc(coords[((int64_t)b * 2 + 1) * N + i] * inv);
+  }
+  __syncthreads();
+  for (int l = 0; l < levels; ++l) {
+    const int hl = pyr.h[l], wl = pyr.w[l];
+    const uint32_t plane = (uint32_t)(hl * wl);
+    // this workgroup's planes of level l: pixels i0 .. i0+TPW-1 of image b
+    const float* base = pyr.lvl[l] + ((int64_t)b * N + i0) * plane;
+    const uint32_t nplanes = (uint32_t)min(TPW, N - i0);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(base), (short)0, (int)(nplanes * plane * 4u), 0x00020000);
+    float v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = tid + k * 256;
+      const int px = e / EE, rc = e - px * EE, r = rc / E, c = rc - r * E;
+      uint32_t off = OOB;
+      if (e < TPW * EE) {
+        const float cx = cxy[(px * 4 + l) * 2], cy = cxy[(px * 4 + l) * 2 + 1];
+        const int gx = (int)floorf(cx) - R + c, gy = (int)floorf(cy) - R + r;
+        if ((unsigned)gy < (unsigned)hl && (unsigned)gx < (unsigned)wl)
+          off = ((uint32_t)px * plane + (uint32_t)(gy * wl + gx)) * 4u;
+      }
+      v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = tid + k * 256;
+      if (e < TPW * EE) {
+        const int px = e / EE, rc = e - px * EE;
+        win[(px * 4 + l) * EE + rc] = v[k];
+      }
+    }
+  }
+  __syncthreads();
+  const int ctot = levels * DD;
+  for (int it = tid; it < TPW * ctot; it += 256) {
+    const int px = it / ctot, ch = it - px * ctot;
+    const int l = ch / DD, t = ch - l * DD, ix = t / D, iy = t - ix * D;
+    const float cx = cxy[(px * 4 + l) * 2], cy = cxy[(px * 4 + l) * 2 + 1];
+    const float ax = cx - floorf(cx), ay = cy - floorf(cy);
+    const float* w = win + (px * 4 + l) * EE + iy * E + ix;
+    const float top = (1.f - ax) * w[0] + ax * w[1];
+    const float bot = (1.f - ax) * w[E] + ax * w[E + 1];
+    tile[px * ROW + ch] = raft_f32_to_bf16((1.f - ay) * top + ay * bot);
+  }
+  __syncthreads();
+  const int chunks = cbuf / 8;
+  for (int e = tid; e < TPW * chunks; e += 256) {
+    const int px = e / chunks, ch = e % chunks;
+    const int i = i0 + px;
+    if (i >= N) continue;
+    uint16_t q8[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = ch * 8 + q;
+      q8[q] = c < ctot ? tile[px * ROW + c] : (uint16_t)0;
+    }
+    *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i) * cbuf + ch * 8) =
+        make_uint4(q8[0] | ((uint32_t)q8[1] << 16), q8[2] | ((uint32_t)q8[3] << 16),
+                   q8[4] | ((uint32_t)q8[5] << 16), q8[6] | ((uint32_t)q8[7] << 16));
   }
 }
 
@@ -217,9 +312,20 @@ bool launch_corr_lookup_tile(const float* const* lvl, const int* hs, const int* 
     p.w[l] = l < levels ? ws[l] : 0;
   }
   const int N = H * W;
-  dim3 grid((unsigned)(B * ((N + TP - 1) / TP)));
-  if (radius == 4) hipLaunchKernelGGL(corr_lookup_tile_kernel<4>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-  else if (radius == 3) hipLaunchKernelGGL(corr_lookup_tile_kernel<3>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+  static const bool legacy = [] {
+    const char* e = getenv("RAFT_LOOKUP_LEGACY");
+    return e && e[0] == '1';
+  }();
+  if (legacy) {
+    dim3 grid((unsigned)(B * ((N + TP - 1) / TP)));
+    if (radius == 4) hipLaunchKernelGGL(corr_lookup_tile_kernel<4>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+    else if (radius == 3) hipLaunchKernelGGL(corr_lookup_tile_kernel<3>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+    else return false;
+    return true;
+  }
+  dim3 grid((unsigned)(B * ((N + TPW - 1) / TPW)));
+  if (radius == 4) hipLaunchKernelGGL(corr_lookup_win_kernel<4>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+  else if (radius == 3) hipLaunchKernelGGL(corr_lookup_win_kernel<3>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
   else return false;
   return true;
 }
