@@ -175,7 +175,8 @@ class RAFT(nn.Module):
             coords1 = coords1.detach()
             corr = corr_fn.lookup_nhwc(coords1, CORR_BUF)
             flow = coords1 - coords0
-            h, delta_flow, up_mask = hub(h, x, corr, flow)
+            last = itr == iters - 1
+            h, delta_flow, up_mask = hub(h, x, corr, flow, need_mask=last or not test_mode)
             coords1 = coords1 + delta_flow
             if test_mode and itr < iters - 1:
                 continue

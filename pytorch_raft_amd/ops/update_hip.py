@@ -292,6 +292,64 @@ def _f32(shape, dev, zero=False):
     return (torch.zeros if zero else torch.empty)(*shape, device=dev, dtype=torch.float32)
 
 
+def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
+    """Forward of one fused iteration; returns (h2, delta, mask, saved tensors).
+
+    ``need_mask=False`` (inference iterations whose flow is not upsampled) computes only the
+    flow-head half of the fused head conv and skips the mask conv: ~20 % of the iteration."""
+    B, H, W, _ = h.shape
+    dev = h.device
+    sh = (B, H, W)
+    flowb = _bf16(sh + (8,), dev)  # flow_prep writes all 8 channels
+    mf = _bf16(sh + (128,), dev)
+    ops = _ext.ops()
+    ops.flow_prep_(flow, flowb, mf, 126)
+    c1 = _bf16(sh + (256,), dev)
+    cf = _bf16(sh + (256,), dev)
+    f1 = _bf16(sh + (128,), dev)
+
+    def conv(name, segs, epi, outs, offs, aux=(), aux_offs=(), split=0, cout=None):
+        s = SPEC[name]
+        cout = cout or s.cout
+        w, b = pk.w[name], pk.b[name]
+        if cout != s.cout:  # leading output rows of a fused conv (packed rows are cout-major)
+            w, b = w[:C.round_up(cout, 128)], b[:cout]
+        C.conv_fwd(segs, w, b, s.k, s.pad, cout, epi, outs, offs, aux,
+                   aux_offs, scale=s.scale, split=split, cin_small=2 if s.small else 0)
+
+    conv('c1', [(corr, 0, CORR_BUF)], C.EPI_RELU_BF16, [c1], [0])
+    conv('c2', [(c1, 0, 256)], C.EPI_RELU_BF16, [cf], [0])
+    conv('f1', [(flowb, 0, 8)], C.EPI_RELU_BF16, [f1], [0])
+    conv('f2', [(f1, 0, 128)], C.EPI_RELU_BF16, [cf], [192])
+    conv('conv', [(cf, 0, 256)], C.EPI_RELU_BF16, [mf], [0])
+    gates = {}
+    hin = h
+    for tag in ('1', '2'):
+        z, rh, r = _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev)
+        conv('zr' + tag, [(hin, 0, HD), (inp, 0, HD), (mf, 0, 128)], C.EPI_GRU_ZR, [z, rh, r],
+             [0, 0, 0], aux=[hin], aux_offs=[0], split=HD)
+        hn, q = _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev)
+        conv('q' + tag, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)], C.EPI_GRU_Q, [hn, q], [0, 0],
+             aux=[hin, z], aux_offs=[0, 0])
+        gates[tag] = (hin, z, rh, r, q)
+        hin = hn
+    h2 = hin
+    delta = torch.empty(B, 2, H, W, device=dev, dtype=torch.float32)
+    if need_mask:
+        fm = _bf16(sh + (512,), dev)
+        conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0])
+        conv('fh2', [(fm, 0, 256)], C.EPI_F32_NCHW, [delta], [0])
+        mask = _bf16(sh + (576,), dev)
+        conv('m2', [(fm, 256, 256)], C.EPI_BF16, [mask], [0])
+    else:
+        fm = _bf16(sh + (256,), dev)
+        conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0], cout=256)
+        conv('fh2', [(fm, 0, 256)], C.EPI_F32_NCHW, [delta], [0])
+        mask = None
+    g1, g2 = gates['1'], gates['2']
+    return h2, delta, mask, (corr, flowb, c1, cf, f1, mf, inp, *g1, *g2, h2, fm)
+
+
 class _UpdateIter(torch.autograd.Function):
     """One GRU iteration.  Inputs: token, h (B,H,W,128) bf16, inp (B,H,W,128) bf16,
     corr (B,H,W,CORR_BUF) bf16, flow (B,2,H,W) fp32.  Outputs: h', delta (B,2,H,W) fp32,
@@ -299,50 +357,9 @@ class _UpdateIter(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, token, h, inp, corr, flow, state):
-        pk = state.packed
-        B, H, W, _ = h.shape
-        dev = h.device
-        sh = (B, H, W)
-        flowb = _bf16(sh + (8,), dev)  # flow_prep writes all 8 channels
-        mf = _bf16(sh + (128,), dev)
-        ops = _ext.ops()
-        ops.flow_prep_(flow, flowb, mf, 126)
-        c1 = _bf16(sh + (256,), dev)
-        cf = _bf16(sh + (256,), dev)
-        f1 = _bf16(sh + (128,), dev)
-
-        def conv(name, segs, epi, outs, offs, aux=(), aux_offs=(), split=0):
-            s = SPEC[name]
-            C.conv_fwd(segs, pk.w[name], pk.b[name], s.k, s.pad, s.cout, epi, outs, offs, aux,
-                       aux_offs, scale=s.scale, split=split, cin_small=2 if s.small else 0)
-
-        conv('c1', [(corr, 0, CORR_BUF)], C.EPI_RELU_BF16, [c1], [0])
-        conv('c2', [(c1, 0, 256)], C.EPI_RELU_BF16, [cf], [0])
-        conv('f1', [(flowb, 0, 8)], C.EPI_RELU_BF16, [f1], [0])
-        conv('f2', [(f1, 0, 128)], C.EPI_RELU_BF16, [cf], [192])
-        conv('conv', [(cf, 0, 256)], C.EPI_RELU_BF16, [mf], [0])
-        gates = {}
-        hin = h
-        for tag in ('1', '2'):
-            z, rh, r = _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev)
-            conv('zr' + tag, [(hin, 0, HD), (inp, 0, HD), (mf, 0, 128)], C.EPI_GRU_ZR, [z, rh, r],
-                 [0, 0, 0], aux=[hin], aux_offs=[0], split=HD)
-            hn, q = _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev)
-            conv('q' + tag, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)], C.EPI_GRU_Q, [hn, q], [0, 0],
-                 aux=[hin, z], aux_offs=[0, 0])
-            gates[tag] = (hin, z, rh, r, q)
-            hin = hn
-        h2 = hin
-        fm = _bf16(sh + (512,), dev)
-        conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0])
-        delta = torch.empty(B, 2, H, W, device=dev, dtype=torch.float32)
-        conv('fh2', [(fm, 0, 256)], C.EPI_F32_NCHW, [delta], [0])
-        mask = _bf16(sh + (576,), dev)
-        conv('m2', [(fm, 256, 256)], C.EPI_BF16, [mask], [0])
-
+        h2, delta, mask, saved = _iter_forward(state.packed, h, inp, corr, flow)
         ctx.state = state
-        g1, g2 = gates['1'], gates['2']
-        ctx.save_for_backward(corr, flowb, c1, cf, f1, mf, inp, *g1, *g2, h2, fm)
+        ctx.save_for_backward(*saved)
         return h2, delta, mask
 
     @staticmethod
@@ -443,7 +460,12 @@ class HipUpdateBlock:
         self.state.overlap = _OVERLAP
         self.token = _UpdateWeights.apply(self.state, *params)
 
-    def __call__(self, h, inp, corr, flow):
+    def __call__(self, h, inp, corr, flow, need_mask=True):
+        """-> (h', delta, mask).  Without gradients (inference) the iteration runs outside
+        autograd and ``need_mask=False`` skips the mask head (mask is then None)."""
+        if not self.state.need_grad and not torch.is_grad_enabled():
+            h2, delta, mask, _ = _iter_forward(self.state.packed, h, inp, corr, flow, need_mask)
+            return h2, delta, mask
         return _UpdateIter.apply(self.token, h, inp, corr, flow, self.state)
 
 
