@@ -324,9 +324,10 @@ __global__ void norm_bwd_finalize_kernel(const float* __restrict__ part, int C, 
     dg += sgx;
     db += sg;
   }
-  if (dgamma) dgamma[c] += (float)dg;
-  if (dbeta) dbeta[c] += (float)db;
-  if (dcbias) dcbias[c] += (float)dcb;
+  // plain stores: one thread owns each channel (the outputs need no zero fill)
+  if (dgamma) dgamma[c] = (float)dg;
+  if (dbeta) dbeta[c] = (float)db;
+  if (dcbias) dcbias[c] = (float)dcb;
 }
 
 __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(

@@ -177,6 +177,20 @@ void launch_gru_zr_bwd(const float* drh, const float* dz, const uint16_t* z, con
 void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int slot_stride, int B,
                       int HW, hipStream_t stream);
 
+// ---- flow_head.conv2 (3x3, 256 -> 2): fwd / dgrad (+ReLU gate) / multi-item wgrad (flow_head2.hip)
+#define RAFT_FH2_MAX_ITEMS 32
+struct Fh2Items {
+  const float* gout[RAFT_FH2_MAX_ITEMS];    // (B,2,H,W) fp32 output gradient per iteration
+  const uint16_t* in[RAFT_FH2_MAX_ITEMS];   // (B,H,W,cs) bf16 input (channels 0..255 used)
+  int n;
+};
+bool launch_fh2_fwd(const uint16_t* in, int cs, const float* w, const float* bias, float* out, int B,
+                    int H, int W, hipStream_t stream);
+bool launch_fh2_dgrad(const float* gout, const float* w, const uint16_t* fm, int fs, uint16_t* dx,
+                      int ds, int B, int H, int W, hipStream_t stream);
+bool launch_fh2_wgrad(const Fh2Items& it, int cs, int B, int H, int W, float* dw, float* db,
+                      hipStream_t stream);
+
 // ---- NHWC lookup tile + window-compact backward (corr_window.hip)
 #define RAFT_MAX_WIN 32
 struct WinList {

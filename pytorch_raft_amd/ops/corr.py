@@ -97,7 +97,7 @@ class _AllPairsLookup(torch.autograd.Function):
         if st.grad is None:
             st.grad = [torch.zeros_like(p) for p in st.pyramid]
         _ext.ops().corr_lookup_bwd_(st.grad, coords, dout.contiguous().float(), ctx.radius)
-        return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None
+        return None, None, None, None
 
 
 class _AllPairsLookupNHWC(torch.autograd.Function):
@@ -131,7 +131,7 @@ class _AllPairsLookupNHWC(torch.autograd.Function):
             if st.grad is None:
                 st.grad = [torch.zeros_like(p) for p in st.pyramid]
             _ext.ops().corr_lookup_bwd_(st.grad, coords, dout.float().contiguous(), ctx.radius)
-        return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None, None
+        return None, None, None, None, None
 
 
 def _window_reduce_fits(h, w, levels):
@@ -235,7 +235,7 @@ class _OTFLookup(torch.autograd.Function):
     def backward(ctx, dout):
         (coords,) = ctx.saved_tensors
         _otf_backward(ctx.state, coords, dout.float().permute(0, 2, 3, 1), ctx.radius)
-        return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None
+        return None, None, None, None
 
 
 class _OTFLookupNHWC(torch.autograd.Function):
@@ -264,7 +264,7 @@ class _OTFLookupNHWC(torch.autograd.Function):
             st.radius = ctx.radius
         else:
             _otf_backward(st, coords, dout, ctx.radius)
-        return torch.zeros((), device=dout.device, dtype=torch.float32), None, None, None, None
+        return None, None, None, None, None
 
 
 class OnTheFlyVolume:

@@ -69,9 +69,10 @@ class _NormAct(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         c = x.shape[1]
         dev = x.device
-        dg = torch.zeros(c, device=dev) if ctx.has[0] else None
-        db = torch.zeros(c, device=dev) if ctx.has[1] else None
-        dc = torch.zeros(c, device=dev) if ctx.has[2] else None
+        # written (not accumulated) by the finalize kernel: no zero fill
+        dg = torch.empty(c, device=dev) if ctx.has[0] else None
+        db = torch.empty(c, device=dev) if ctx.has[1] else None
+        dc = torch.empty(c, device=dev) if ctx.has[2] else None
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         _ext.ops().norm_bwd_(dy, y, x, mean, invstd, ctx.mode, int(ctx.relu), gamma, dg, db, dc, dx)
         return dx, dg, db, dc, None, None, None

@@ -109,6 +109,7 @@ class _Packed:
         self.dw = {}
         self.db = {}
         self.pending = {}  # conv name -> [(g, g_off, segs)] awaiting the batched weight gradient
+        self.fh2_items = []  # (fp32 delta gradient, head activations) per iteration
         self.device = device
         with torch.no_grad():
             for s in SPECS:
@@ -123,28 +124,28 @@ class _Packed:
                     self.w[s.name] = C.pack_weight(w, s.in_real, s.in_pad)
                 self.kpad[s.name] = self.w[s.name].shape[1]
                 self.b[s.name] = b.float().contiguous()
-                if need_grad and s.name != 'f1':
+                if s.name == 'fh2':
+                    # 256 -> 2 conv: dedicated VALU kernels read the module's fp32 weights
+                    self.w32 = w.contiguous()
+                    self.b32 = self.b[s.name]
+                if need_grad and s.name not in ('f1', 'fh2'):
                     # adjoint conv: inputs = this layer's output channels, outputs = its inputs
-                    if s.name == 'fh2':
-                        wt = w.flip(2, 3).transpose(0, 1).contiguous()  # (256, 2, 3, 3)
-                        self.wd[s.name] = C.pack_weight_small(wt)
-                    else:
-                        cout_pad = C.round_up(s.cout, 32)
-                        wt = w
-                        if cout_pad > s.cout:
-                            wt = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 0, 0, cout_pad - s.cout))
-                        wt = wt.flip(2, 3).transpose(0, 1).contiguous()  # (Cin, CoutPad, kh, kw)
-                        if sum(s.in_pad) > sum(s.in_real):
-                            # padded input slots become zero output rows of the adjoint
-                            parts, off = [], 0
-                            for r, p in zip(s.in_real, s.in_pad):
-                                part = wt[off:off + r]
-                                if p > r:
-                                    part = torch.nn.functional.pad(part, (0, 0, 0, 0, 0, 0, 0, p - r))
-                                parts.append(part)
-                                off += r
-                            wt = torch.cat(parts, 0)
-                        self.wd[s.name] = C.pack_weight(wt, [cout_pad], [cout_pad])
+                    cout_pad = C.round_up(s.cout, 32)
+                    wt = w
+                    if cout_pad > s.cout:
+                        wt = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 0, 0, cout_pad - s.cout))
+                    wt = wt.flip(2, 3).transpose(0, 1).contiguous()  # (Cin, CoutPad, kh, kw)
+                    if sum(s.in_pad) > sum(s.in_real):
+                        # padded input slots become zero output rows of the adjoint
+                        parts, off = [], 0
+                        for r, p in zip(s.in_real, s.in_pad):
+                            part = wt[off:off + r]
+                            if p > r:
+                                part = torch.nn.functional.pad(part, (0, 0, 0, 0, 0, 0, 0, p - r))
+                            parts.append(part)
+                            off += r
+                        wt = torch.cat(parts, 0)
+                    self.wd[s.name] = C.pack_weight(wt, [cout_pad], [cout_pad])
                 if need_grad:
                     self.dw[s.name] = torch.zeros(s.cout, self.kpad[s.name], device=device)
                     self.db[s.name] = torch.zeros(s.cout, device=device)
@@ -171,6 +172,12 @@ def _flush_wgrad(pk):
             C.conv_wgrad_multi([(g, [b for b, _, _ in segs]) for g, _, segs in chunk], g_off,
                                in_off, in_cnt, s.k, s.pad, s.cout, dw, db)
     pk.pending = {}
+    items = pk.fh2_items
+    for i in range(0, len(items), 32):
+        chunk = items[i:i + 32]
+        _ext.ops().fh2_wgrad_([g for g, _ in chunk], [x for _, x in chunk], pk.dw['fh2'],
+                              pk.db['fh2'])
+    pk.fh2_items = []
 
 
 class _State:
@@ -178,6 +185,8 @@ class _State:
         self.packed = None
         self.overlap = False
         self.params = []
+        self.n_iter = 0        # iterations issued through this block (forward order)
+        self.dinp_acc = None   # fp32 gradient w.r.t. the context input, summed over iterations
 
 
 class _UpdateWeights(torch.autograd.Function):
@@ -338,13 +347,13 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
     if need_mask:
         fm = _bf16(sh + (512,), dev)
         conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0])
-        conv('fh2', [(fm, 0, 256)], C.EPI_F32_NCHW, [delta], [0])
+        ops.fh2_fwd_(fm, pk.w32, pk.b32, delta)
         mask = _bf16(sh + (576,), dev)
         conv('m2', [(fm, 256, 256)], C.EPI_BF16, [mask], [0])
     else:
         fm = _bf16(sh + (256,), dev)
         conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0], cout=256)
-        conv('fh2', [(fm, 0, 256)], C.EPI_F32_NCHW, [delta], [0])
+        ops.fh2_fwd_(fm, pk.w32, pk.b32, delta)
         mask = None
     g1, g2 = gates['1'], gates['2']
     return h2, delta, mask, (corr, flowb, c1, cf, f1, mf, inp, *g1, *g2, h2, fm)
@@ -359,6 +368,8 @@ class _UpdateIter(torch.autograd.Function):
     def forward(ctx, token, h, inp, corr, flow, state):
         h2, delta, mask, saved = _iter_forward(state.packed, h, inp, corr, flow)
         ctx.state = state
+        ctx.itr = state.n_iter
+        state.n_iter += 1
         ctx.save_for_backward(*saved)
         return h2, delta, mask
 
@@ -399,19 +410,25 @@ class _UpdateIter(torch.autograd.Function):
         dpre_head = _bf16(sh + (512,), dev)
         wgrad('m2', gmask, 0, [(fm, 256, 256)])
         dgrad('m2', [(gmask, 0, 576)], [(dpre_head, 256, 256, 256, 0, fm, 256)], scale=0.25)
-        # ---- flow head conv2 -> delta
-        gd = _bf16(sh + (8,), dev)  # flow_prep writes all 8 channels
-        ops.flow_prep_(gdelta.contiguous().float(), gd, None, 0)
-        wgrad('fh2', gd, 0, [(fm, 0, 256)])
-        dgrad('fh2', [(gd, 0, 8)], [(dpre_head, 0, 256, 256, 0, fm, 0)], small=True)
+        # ---- flow head conv2 -> delta (VALU kernels; fp32 output gradient read directly)
+        gd = gdelta.contiguous().float()
+        pk.fh2_items.append((gd, fm))
+        ops.fh2_dgrad_(gd, pk.w32, fm, dpre_head)
         # ---- head
         wgrad('head', dpre_head, 0, [(h2, 0, HD)])
         dh = gh.float().contiguous() if gh is not None else _f32(sh + (HD,), dev, zero=True)
         dgrad('head', [(dpre_head, 0, 512)], [(dh, 0, HD, HD, 1)])
 
-        dinp = _f32(sh + (HD,), dev)
+        # inp is shared by every iteration: its gradient accumulates in ONE fp32 buffer across
+        # the iterations' backwards (11 -> 0, in that order since each needs the next one's dh)
+        # and is handed to autograd once, by iteration 0 -- instead of 12 bf16 casts + 11 adds
+        st = ctx.state
+        acc_inp = st.dinp_acc is not None
+        if not acc_inp:
+            st.dinp_acc = _f32(sh + (HD,), dev)
+        dinp = st.dinp_acc
         dmf = _f32(sh + (128,), dev)
-        first = 1  # the first dgrad into dinp / dmf (q2's) stores: no zero fill
+        first = 1  # the first dgrad into dmf (q2's) stores: no zero fill
         for tag, (hin, z, rh, r, q) in (('2', (h1, z2, rh2, r2, q2)), ('1', (h0, z1, rh1, r1, q1))):
             dpre_q = _bf16(sh + (HD,), dev)
             dz = _f32(sh + (HD,), dev)
@@ -420,8 +437,10 @@ class _UpdateIter(torch.autograd.Function):
             wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)])
             drh = _f32(sh + (HD,), dev)
             dgrad('q' + tag, [(dpre_q, 0, HD)],
-                  [(drh, 0, HD, HD, 0), (dinp, 0, HD, HD, 1 - first), (dmf, 0, 128, 128, 1 - first)])
+                  [(drh, 0, HD, HD, 0), (dinp, 0, HD, HD, int(acc_inp)),
+                   (dmf, 0, 128, 128, 1 - first)])
             first = 0
+            acc_inp = True
             dpre_zr = _bf16(sh + (2 * HD,), dev)
             ops.gru_zr_bwd_(drh, dz, z, r, hin, dpre_zr, dhp)
             wgrad('zr' + tag, dpre_zr, 0, [(hin, 0, HD), (inp, 0, HD), (mf, 0, 128)])
@@ -445,7 +464,12 @@ class _UpdateIter(torch.autograd.Function):
         # bf16 (the dtype of the corr input): autograd would otherwise cast an fp32 gradient
         dcorr = _bf16(sh + (CORR_BUF,), dev)
         dgrad('c1', [(dpre_c1, 0, 256)], [(dcorr, 0, CORR_BUF, 324, 0)])  # slots 324.. unused
-        return (torch.zeros((), device=dev), dh, dinp, dcorr, None, None)
+        if ctx.itr == 0:
+            st.dinp_acc = None
+        else:
+            dinp = None
+        # token: no gradient value (autograd still runs the weight node after every iteration)
+        return (None, dh, dinp, dcorr, None, None)
 
 
 class HipUpdateBlock:

@@ -77,3 +77,67 @@ def test_fused_train_step_bf16(ext_ops):
     losses = [st.step(i1, i2, flow, valid)[0].item() for _ in range(6)]
     assert st.check_finite()
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize('cs,shape', [(512, (2, 11, 13)), (256, (3, 46, 62)), (512, (1, 7, 70))])
+def test_flow_head2_kernels_match_fp32(ext_ops, cs, shape):
+    """flow_head.conv2 (3x3, 256 -> 2) fwd / ReLU-gated dgrad / multi-item wgrad vs torch fp32."""
+    import torch.nn.functional as F
+    B, H, W = shape
+    g = torch.Generator(device=DEV).manual_seed(3)
+    w = torch.randn(2, 256, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(2, device=DEV, generator=g)
+    fm = torch.relu(torch.randn(B, H, W, cs, device=DEV, generator=g)).to(torch.bfloat16)
+    x = fm[..., :256].float().permute(0, 3, 1, 2)
+    # forward
+    out = torch.empty(B, 2, H, W, device=DEV)
+    ext_ops.fh2_fwd_(fm, w, b, out)
+    ref = F.conv2d(x, w, b, padding=1)
+    torch.testing.assert_close(out, ref, atol=1e-3, rtol=1e-3)
+    # input gradient, gated by fm > 0, written into channels 0..255 of a cs-wide buffer
+    gout = torch.randn(B, 2, H, W, device=DEV, generator=g)
+    dx = torch.full((B, H, W, cs), 7.0, device=DEV, dtype=torch.bfloat16)
+    ext_ops.fh2_dgrad_(gout, w, fm, dx)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, b, padding=1).backward(gout)
+    dref = (xr.grad * (x > 0)).permute(0, 2, 3, 1)
+    torch.testing.assert_close(dx[..., :256].float(), dref, atol=2e-2, rtol=1e-2)
+    if cs > 256:
+        assert (dx[..., 256:] == 7.0).all(), 'wrote past channel 255'
+    # weight / bias gradient summed over 3 items, accumulated into existing values
+    gouts = [gout, gout * 0.5, -gout]
+    ins = [fm, fm, (fm.float() * 0.25).to(torch.bfloat16)]
+    dw = torch.ones(2, 9 * 256, device=DEV)
+    db = torch.ones(2, device=DEV)
+    ext_ops.fh2_wgrad_(gouts, ins, dw, db)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    for go, xi in zip(gouts, ins):
+        F.conv2d(xi[..., :256].float().permute(0, 3, 1, 2), wr, br, padding=1).backward(go)
+    dw_ref = wr.grad.permute(0, 2, 3, 1).reshape(2, 9 * 256) + 1.0  # k = tap * 256 + c
+    torch.testing.assert_close(dw, dw_ref, atol=1e-2, rtol=1e-3)
+    torch.testing.assert_close(db, br.grad + 1.0, atol=1e-3, rtol=1e-4)
+
+
+def test_inference_mask_skip_and_graph_match_eager(ext_ops):
+    """Test-mode forward without the non-final mask heads, eager and hipGraph-replayed, equals
+    the training-path forward (every iteration computes its mask)."""
+    from pytorch_raft_amd.engine.inference import FlowInference
+    torch.manual_seed(0)
+    m = _model('hip').eval()
+    i1, i2, _, _ = make_pair_batch(2, 124, 156, device=DEV)   # padded to 128 x 160
+    with torch.no_grad():
+        full = m(*[torch.nn.functional.pad(t, (2, 2, 2, 2), mode='replicate') for t in (i1, i2)],
+                 iters=5)
+    ref_up = full[-1][..., 2:-2, 2:-2]
+    eager = FlowInference(m, iters=5)
+    lo_e, up_e = eager(i1, i2)
+    # the flow-only head conv may run a different tile config than the fused 512-wide one
+    torch.testing.assert_close(up_e, ref_up, atol=5e-2, rtol=1e-3)
+    graphed = FlowInference(m, iters=5, graph=True)
+    lo_g, up_g = graphed(i1, i2)
+    lo_g2, up_g2 = graphed(i2, i1)          # replay with new inputs
+    lo_e2, up_e2 = eager(i2, i1)
+    torch.testing.assert_close(up_g, up_e, atol=0, rtol=0)
+    torch.testing.assert_close(up_g2, up_e2, atol=0, rtol=0)
+    torch.testing.assert_close(lo_g2, lo_e2, atol=0, rtol=0)
