@@ -90,24 +90,41 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
   }
 }
 
-// part [groups][nblk][S*C] -> sums [groups][S*C]: 4 lanes per column stride over the partials,
-// fixed-order LDS combine (deterministic); grid (groups, ceil(S*C / 64))
+// part [groups][nblk][S*C] -> sums [groups][S*C]: LANES lanes per column stride over the partials,
+// fixed-order LDS combine (deterministic); block = (256 / LANES) columns x LANES lanes,
+// grid (groups, ceil(S*C / (256 / LANES))).  16 lanes for the long batch-norm partial lists
+// (hundreds of blocks over all images), 4 for the per-image ones.
+template <int LANES>
 __global__ __launch_bounds__(256) void partial_reduce_kernel(const float* __restrict__ part,
                                                              int nblk, int SC,
                                                              float* __restrict__ sums) {
-  __shared__ float red[4][64];
+  constexpr int COLS = 256 / LANES;
+  __shared__ float red[LANES][COLS];
   const int gi = blockIdx.x;
-  const int col = blockIdx.y * 64 + (threadIdx.x & 63);
-  const int lane = threadIdx.x >> 6;
+  const int t = threadIdx.x % COLS;
+  const int col = blockIdx.y * COLS + t;
+  const int lane = threadIdx.x / COLS;
   float a = 0.f;
   if (col < SC)
-    for (int k = lane; k < nblk; k += 4) a += part[((int64_t)gi * nblk + k) * SC + col];
-  red[lane][threadIdx.x & 63] = a;
+    for (int k = lane; k < nblk; k += LANES) a += part[((int64_t)gi * nblk + k) * SC + col];
+  red[lane][t] = a;
   __syncthreads();
   if (lane == 0 && col < SC) {
-    const int t = threadIdx.x & 63;
-    sums[(int64_t)gi * SC + col] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    float s = 0.f;
+#pragma unroll
+    for (int l = 0; l < LANES; ++l) s += red[l][t];
+    sums[(int64_t)gi * SC + col] = s;
   }
+}
+
+void launch_partial_reduce(const float* part, int groups, int nblk, int SC, float* sums,
+                           hipStream_t stream) {
+  if (nblk > 64)
+    hipLaunchKernelGGL(partial_reduce_kernel<16>, dim3(groups, (SC + 15) / 16), dim3(256), 0, stream,
+                       part, nblk, SC, sums);
+  else
+    hipLaunchKernelGGL(partial_reduce_kernel<4>, dim3(groups, (SC + 63) / 64), dim3(256), 0, stream,
+                       part, nblk, SC, sums);
 }
 
 // mode: 0 instance (train or eval: always batch statistics), 1 batch-train, 2 batch-eval, 3 none
@@ -287,47 +304,54 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
   }
 }
 
-// -> per (group image, c) coefficients dx = A*g + B*xhat + Cc, plus dgamma/dbeta/dcbias (summed
-// over images by the channel's thread for instance norm: one thread per channel here)
-__global__ void norm_bwd_finalize_kernel(const float* __restrict__ part, int C, int groups_img,
-                                         int nblk, int cnt, int mode,
-                                         const float* __restrict__ gamma,
-                                         const float* __restrict__ invstd,
-                                         float* __restrict__ coef, float* __restrict__ dgamma,
-                                         float* __restrict__ dbeta, float* __restrict__ dcbias) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const float gm = (mode == 1 || mode == 2) && gamma ? gamma[c] : 1.f;
+// -> per (group image, c) coefficients dx = A*g + B*xhat + Cc, plus dgamma/dbeta/dcbias summed
+// over the groups: block = 64 channels x 4 group lanes (fixed-order LDS combine, deterministic)
+__global__ __launch_bounds__(256) void norm_bwd_finalize_kernel(
+    const float* __restrict__ part, int C, int groups_img, int nblk, int cnt, int mode,
+    const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ coef,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dcbias) {
+  __shared__ double red[3][4][64];
+  const int t = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + t;
   double dg = 0.0, db = 0.0, dcb = 0.0;
-  for (int gi = 0; gi < groups_img; ++gi) {
-    const float* p = part + (int64_t)gi * 3 * C;
-    const double sg = p[c], sgx = p[C + c], sx = p[2 * C + c];
-    const float is = invstd[(int64_t)gi * C + c];
-    float A, B, Cc;
-    if (mode == 0 || mode == 1) {
-      const double mg = sg / cnt, mgx = sgx / cnt;
-      A = gm * is;
-      B = (float)(-gm * is * mgx);
-      Cc = (float)(-gm * is * mg);
-      // sum over the group of dx = A*sg + B*sx + C*cnt
-      dcb += A * sg + B * sx + (double)Cc * cnt;
-    } else {
-      A = gm * is;  // eval batch norm / none: an affine map
-      B = 0.f;
-      Cc = 0.f;
-      dcb += A * sg;
+  if (c < C) {
+    const float gm = (mode == 1 || mode == 2) && gamma ? gamma[c] : 1.f;
+    for (int gi = lane; gi < groups_img; gi += 4) {
+      const float* p = part + (int64_t)gi * 3 * C;
+      const double sg = p[c], sgx = p[C + c], sx = p[2 * C + c];
+      const float is = invstd[(int64_t)gi * C + c];
+      float A, B, Cc;
+      if (mode == 0 || mode == 1) {
+        const double mg = sg / cnt, mgx = sgx / cnt;
+        A = gm * is;
+        B = (float)(-gm * is * mgx);
+        Cc = (float)(-gm * is * mg);
+        // sum over the group of dx = A*sg + B*sx + C*cnt
+        dcb += A * sg + B * sx + (double)Cc * cnt;
+      } else {
+        A = gm * is;  // eval batch norm / none: an affine map
+        B = 0.f;
+        Cc = 0.f;
+        dcb += A * sg;
+      }
+      float* co = coef + ((int64_t)gi * C + c) * 3;
+      co[0] = A;
+      co[1] = B;
+      co[2] = Cc;
+      dg += sgx;
+      db += sg;
     }
-    float* co = coef + ((int64_t)gi * C + c) * 3;
-    co[0] = A;
-    co[1] = B;
-    co[2] = Cc;
-    dg += sgx;
-    db += sg;
   }
-  // plain stores: one thread owns each channel (the outputs need no zero fill)
-  if (dgamma) dgamma[c] = (float)dg;
-  if (dbeta) dbeta[c] = (float)db;
-  if (dcbias) dcbias[c] = (float)dcb;
+  red[0][lane][t] = dg;
+  red[1][lane][t] = db;
+  red[2][lane][t] = dcb;
+  __syncthreads();
+  if (lane == 0 && c < C) {
+    // plain stores: one thread owns each channel (the outputs need no zero fill)
+    if (dgamma) dgamma[c] = (float)((red[0][0][t] + red[0][1][t]) + (red[0][2][t] + red[0][3][t]));
+    if (dbeta) dbeta[c] = (float)((red[1][0][t] + red[1][1][t]) + (red[1][2][t] + red[1][3][t]));
+    if (dcbias) dcbias[c] = (float)((red[2][0][t] + red[2][1][t]) + (red[2][2][t] + red[2][3][t]));
+  }
 }
 
 __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
@@ -395,8 +419,7 @@ void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, i
   float* sums = nullptr;
   if (mode <= 1) {
     sums = const_cast<float*>(part) + (int64_t)groups * nblk * 2 * C;
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3(groups, (2 * C + 63) / 64), dim3(256), 0, stream,
-                       part, nblk, 2 * C, sums);
+    launch_partial_reduce(part, groups, nblk, 2 * C, sums, stream);
   }
   hipLaunchKernelGGL(norm_finalize_kernel, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
                      C, groups, nblk, cnt, mode, gamma, beta, cbias, rmean, rvar, momentum, eps, mean,
@@ -440,9 +463,8 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* y, const uint16_t* x, c
                        0, pix_per_blk, N * HW, relu, part);
   }
   float* sums = part + (int64_t)groups * nblk * 3 * C;
-  hipLaunchKernelGGL(partial_reduce_kernel, dim3(groups, (3 * C + 63) / 64), dim3(256), 0, stream,
-                     part, nblk, 3 * C, sums);
-  hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, stream, sums, C,
+  launch_partial_reduce(part, groups, nblk, 3 * C, sums, stream);
+  hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, sums, C,
                      groups, nblk, cnt, mode, gamma, invstd, coef, dgamma, dbeta, dcbias);
   const int64_t nvec = (int64_t)N * HW * C / 8;
   hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, y, x, mean,

@@ -30,7 +30,7 @@ def pick_bn(cout):
     return 64
 
 
-def pack_weight(w, seg_real, seg_pad, npad_mult=128):
+def pack_weight(w, seg_real, seg_pad, npad_mult=128, dtype=torch.bfloat16):
     """(Cout, Cin, KH, KW) -> (Npad, KH*KW*sum(seg_pad)) bf16.
 
     ``seg_real[i]`` input channels of the module map to a ``seg_pad[i]``-wide slot in the packed K.
@@ -50,16 +50,16 @@ def pack_weight(w, seg_real, seg_pad, npad_mult=128):
     npad = round_up(cout, npad_mult)
     if npad > cout:
         wp = F.pad(wp, (0, 0, 0, npad - cout))
-    return wp.to(torch.bfloat16).contiguous()
+    return wp.to(dtype).contiguous()
 
 
-def pack_weight_small(w, npad_mult=128):
+def pack_weight_small(w, npad_mult=128, dtype=torch.bfloat16):
     """Dense-K packing for tiny Cin: k = tap*Cin + c, padded to a multiple of 64 (one K step)."""
     cout, cin, kh, kw = w.shape
     wp = w.permute(0, 2, 3, 1).reshape(cout, kh * kw * cin)
     kp = round_up(kh * kw * cin, 64)
     wp = F.pad(wp, (0, kp - kh * kw * cin, 0, round_up(cout, npad_mult) - cout))
-    return wp.to(torch.bfloat16).contiguous()
+    return wp.to(dtype).contiguous()
 
 
 def pack_weight_dgrad(w, out_real, out_pad, npad_mult=128):

@@ -97,8 +97,77 @@ class _AddRelu(torch.autograd.Function):
         return g, g
 
 
+class _CastWeightsCL(torch.autograd.Function):
+    """All conv weights of an encoder -> bf16 channels_last views of ONE buffer, and back.
+
+    Per conv, ``weight.to(bf16).contiguous(channels_last)`` and the backward cast of its bf16
+    gradient are 2-3 tiny kernels each (~100 launches per step for both encoders).  Here the
+    forward is cat -> permuting gather -> cast and the backward cat -> cast -> inverse gather, with
+    the index maps built once per weight geometry."""
+
+    @staticmethod
+    def forward(ctx, maps, *ws):
+        perm, inv, shapes = maps
+        flat = torch.cat([w.reshape(-1) for w in ws])
+        packed = flat.index_select(0, perm).to(torch.bfloat16)
+        outs, off = [], 0
+        for (co, ci, kh, kw) in shapes:
+            n = co * ci * kh * kw
+            outs.append(packed[off:off + n].view(co, kh, kw, ci).permute(0, 3, 1, 2))
+            off += n
+        ctx.maps = maps
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        perm, inv, shapes = ctx.maps
+        parts = []
+        for g, (co, ci, kh, kw) in zip(gs, shapes):
+            if g is None:
+                g = torch.zeros(co, ci, kh, kw, device=perm.device, dtype=torch.bfloat16)
+            parts.append(g.permute(0, 2, 3, 1).reshape(-1))
+        flat = torch.cat(parts).float().index_select(0, inv)
+        grads, off = [], 0
+        for (co, ci, kh, kw) in shapes:
+            n = co * ci * kh * kw
+            grads.append(flat[off:off + n].view(co, ci, kh, kw))
+            off += n
+        return (None, *grads)
+
+
+_MAPS = {}
+
+
+def _cast_maps(shapes, device):
+    key = (tuple(shapes), str(device))
+    if key not in _MAPS:
+        perm, off = [], 0
+        for (co, ci, kh, kw) in shapes:
+            n = co * ci * kh * kw
+            # packed (co, kh, kw, ci) position -> flat NCHW (co, ci, kh, kw) element
+            perm.append(torch.arange(n).view(co, ci, kh, kw).permute(0, 2, 3, 1).reshape(-1) + off)
+            off += n
+        perm = torch.cat(perm)
+        inv = torch.empty_like(perm)
+        inv[perm] = torch.arange(perm.numel())
+        _MAPS[key] = (perm.to(device), inv.to(device), list(shapes))
+    return _MAPS[key]
+
+
+def cast_conv_weights(convs):
+    """{conv: bf16 channels_last weight} for a list of nn.Conv2d, one batched cast node."""
+    ws = [c.weight for c in convs]
+    maps = _cast_maps([tuple(w.shape) for w in ws], ws[0].device)
+    return dict(zip(convs, _CastWeightsCL.apply(maps, *ws)))
+
+
+_WEIGHTS = {}   # conv -> bf16 channels_last weight for the encoder forward in flight
+
+
 def _conv(x, conv, with_bias=False):
-    w = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = _WEIGHTS.get(conv)
+    if w is None:
+        w = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     b = conv.bias.to(torch.bfloat16) if (with_bias and conv.bias is not None) else None
     return F.conv2d(x, w, b, conv.stride, conv.padding, conv.dilation, conv.groups)
 
@@ -154,11 +223,20 @@ def fast_path_ok(enc, x):
 def encoder_forward(enc, x):
     """`core/extractor.py:168-192` (both encoders): returns channels_last bf16 features."""
     with torch.autocast('cuda', enabled=False):
-        x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        x = conv_norm_act(x, enc.conv1, enc.norm1)
-        block_fn = residual_block if enc.block.__name__ == 'ResidualBlock' else bottleneck_block
-        for layer in (enc.layer1, enc.layer2, enc.layer3):
-            for blk in layer:
-                x = block_fn(blk, x)
-        x = _conv(x, enc.conv2, with_bias=True)
+        convs = [m for m in enc.modules() if isinstance(m, nn.Conv2d)]
+        _WEIGHTS.update(cast_conv_weights(convs))
+        try:
+            return _encoder_body(enc, x)
+        finally:
+            _WEIGHTS.clear()
+
+
+def _encoder_body(enc, x):
+    x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = conv_norm_act(x, enc.conv1, enc.norm1)
+    block_fn = residual_block if enc.block.__name__ == 'ResidualBlock' else bottleneck_block
+    for layer in (enc.layer1, enc.layer2, enc.layer3):
+        for blk in layer:
+            x = block_fn(blk, x)
+    x = _conv(x, enc.conv2, with_bias=True)
     return x

@@ -95,60 +95,145 @@ def flat_params(ub):
     return out
 
 
+def _pack_layers(params_by_layer, need_grad, dtype):
+    """Kernel-layout weights of every fused conv: ({name: forward [Npad][K]}, {name: adjoint
+    [Npad'][K']}, {name: bias}).  Runs on real parameters or on index tensors (``_PackPlan``)."""
+    w_out, wd_out, b_out = {}, {}, {}
+    for s in SPECS:
+        ws = [w for w, _ in params_by_layer[s.name]]
+        bs = [b for _, b in params_by_layer[s.name]]
+        w = ws[0] if len(ws) == 1 else torch.cat(ws, 0)
+        b_out[s.name] = bs[0] if len(bs) == 1 else torch.cat(bs, 0)
+        if s.small:
+            w_out[s.name] = C.pack_weight_small(w, dtype=dtype)
+        else:
+            w_out[s.name] = C.pack_weight(w, s.in_real, s.in_pad, dtype=dtype)
+        if need_grad and s.name not in ('f1', 'fh2'):
+            # adjoint conv: inputs = this layer's output channels, outputs = its inputs
+            cout_pad = C.round_up(s.cout, 32)
+            wt = w
+            if cout_pad > s.cout:
+                wt = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 0, 0, cout_pad - s.cout))
+            wt = wt.flip(2, 3).transpose(0, 1).contiguous()  # (Cin, CoutPad, kh, kw)
+            if sum(s.in_pad) > sum(s.in_real):
+                # padded input slots become zero output rows of the adjoint
+                parts, off = [], 0
+                for r, p in zip(s.in_real, s.in_pad):
+                    part = wt[off:off + r]
+                    if p > r:
+                        part = torch.nn.functional.pad(part, (0, 0, 0, 0, 0, 0, 0, p - r))
+                    parts.append(part)
+                    off += r
+                wt = torch.cat(parts, 0)
+            wd_out[s.name] = C.pack_weight(wt, [cout_pad], [cout_pad], dtype=dtype)
+    return w_out, wd_out, b_out
+
+
+class _PackPlan:
+    """Index maps that turn the 24 update-block parameters into every packed weight (forward and
+    adjoint, bf16) with ONE gather + cast, and the packed fp32 weight/bias gradients back into
+    the parameters' layout with one gather -- instead of ~100 small pad / permute / flip / cat /
+    cast kernels per training step.  Built once per parameter geometry by running the packing
+    code on index tensors (float64 holds the element ids exactly; 0 marks zero padding)."""
+
+    def __init__(self, ub, need_grad, device):
+        params = flat_params(ub)
+        self.numels = [p.numel() for p in params]
+        self.shapes = [tuple(p.shape) for p in params]
+        total = sum(self.numels)
+        ids, off = [], 0
+        for p in params:
+            ids.append((torch.arange(p.numel(), dtype=torch.float64) + off + 1).view(p.shape))
+            off += p.numel()
+        it = iter(ids)
+        by_layer = {s.name: [(next(it), next(it)) for _ in module_params(ub)[s.name]]
+                    for s in SPECS}
+        w_idx, wd_idx, b_idx = _pack_layers(by_layer, need_grad, torch.float64)
+        # gather index: element id - 1; padding (id 0) -> the zero slot appended after the params
+        self.views = []       # (kind, name, shape) in gather order
+        parts = []
+        for kind, d in (('w', w_idx), ('wd', wd_idx)):
+            for s in SPECS:
+                if s.name in d:
+                    t = d[s.name]
+                    self.views.append((kind, s.name, tuple(t.shape)))
+                    parts.append(t.reshape(-1))
+        gidx = torch.cat(parts).round().long() - 1
+        gidx[gidx < 0] = total
+        self.widx = gidx.to(device)
+        self.bshapes = [(s.name, b_idx[s.name].numel()) for s in SPECS]
+        self.bidx = (torch.cat([b_idx[s.name].reshape(-1) for s in SPECS]).round().long() - 1).to(device)
+        self.kpad = {s.name: w_idx[s.name].shape[1] for s in SPECS}
+        # gradient buffer: per layer dw (cout, kpad) then db (cout), concatenated in SPECS order;
+        # uidx[e] = the buffer position holding parameter element e's gradient
+        uidx = torch.full((total,), -1, dtype=torch.long)
+        self.dw_views = []
+        pos = 0
+        for s in SPECS:
+            ids_w = w_idx[s.name][:s.cout].round().long() - 1        # (cout, kpad)
+            n = ids_w.numel()
+            m = ids_w.reshape(-1) >= 0
+            uidx[ids_w.reshape(-1)[m]] = torch.arange(pos, pos + n)[m]
+            self.dw_views.append((s.name, 'w', pos, (s.cout, self.kpad[s.name])))
+            pos += n
+            ids_b = b_idx[s.name].round().long() - 1
+            uidx[ids_b] = torch.arange(pos, pos + s.cout)
+            self.dw_views.append((s.name, 'b', pos, (s.cout,)))
+            pos += s.cout
+        assert (uidx >= 0).all(), 'every parameter element must have a gradient slot'
+        self.dw_total = pos
+        self.uidx = uidx.to(device)
+
+
+def _plan(ub, need_grad, device):
+    key = (need_grad, str(device), tuple(tuple(p.shape) for p in flat_params(ub)))
+    cache = ub.__dict__.setdefault('_raft_pack_plans', {})
+    if key not in cache:
+        cache[key] = _PackPlan(ub, need_grad, device)
+    return cache[key]
+
+
 class _Packed:
     """Per-step packed weights (bf16) + packed fp32 gradient accumulators."""
 
     def defer_wgrad(self, name, g, g_off, segs):
         self.pending.setdefault(name, []).append((g, g_off, segs))
 
-    def __init__(self, params_by_layer, device, need_grad):
+    def __init__(self, ub, params, device, need_grad):
         self.w = {}
         self.wd = {}
         self.b = {}
-        self.kpad = {}
         self.dw = {}
         self.db = {}
         self.pending = {}  # conv name -> [(g, g_off, segs)] awaiting the batched weight gradient
         self.fh2_items = []  # (fp32 delta gradient, head activations) per iteration
         self.device = device
+        plan = self.plan = _plan(ub, need_grad, device)
+        self.kpad = plan.kpad
         with torch.no_grad():
-            for s in SPECS:
-                ws = [w for w, _ in params_by_layer[s.name]]
-                bs = [b for _, b in params_by_layer[s.name]]
-                w = ws[0] if len(ws) == 1 else torch.cat(ws, 0)
-                b = bs[0] if len(bs) == 1 else torch.cat(bs, 0)
-                w = w.float()
-                if s.small:
-                    self.w[s.name] = C.pack_weight_small(w)
-                else:
-                    self.w[s.name] = C.pack_weight(w, s.in_real, s.in_pad)
-                self.kpad[s.name] = self.w[s.name].shape[1]
-                self.b[s.name] = b.float().contiguous()
-                if s.name == 'fh2':
-                    # 256 -> 2 conv: dedicated VALU kernels read the module's fp32 weights
-                    self.w32 = w.contiguous()
-                    self.b32 = self.b[s.name]
-                if need_grad and s.name not in ('f1', 'fh2'):
-                    # adjoint conv: inputs = this layer's output channels, outputs = its inputs
-                    cout_pad = C.round_up(s.cout, 32)
-                    wt = w
-                    if cout_pad > s.cout:
-                        wt = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 0, 0, cout_pad - s.cout))
-                    wt = wt.flip(2, 3).transpose(0, 1).contiguous()  # (Cin, CoutPad, kh, kw)
-                    if sum(s.in_pad) > sum(s.in_real):
-                        # padded input slots become zero output rows of the adjoint
-                        parts, off = [], 0
-                        for r, p in zip(s.in_real, s.in_pad):
-                            part = wt[off:off + r]
-                            if p > r:
-                                part = torch.nn.functional.pad(part, (0, 0, 0, 0, 0, 0, 0, p - r))
-                            parts.append(part)
-                            off += r
-                        wt = torch.cat(parts, 0)
-                    self.wd[s.name] = C.pack_weight(wt, [cout_pad], [cout_pad])
-                if need_grad:
-                    self.dw[s.name] = torch.zeros(s.cout, self.kpad[s.name], device=device)
-                    self.db[s.name] = torch.zeros(s.cout, device=device)
+            flat = torch.cat([p.detach().float().reshape(-1) for p in params] +
+                             [torch.zeros(1, device=device)])
+            packed = flat.index_select(0, plan.widx).to(torch.bfloat16)
+            off = 0
+            for kind, name, shape in plan.views:
+                n = shape[0] * shape[1]
+                (self.w if kind == 'w' else self.wd)[name] = packed[off:off + n].view(shape)
+                off += n
+            bias = flat.index_select(0, plan.bidx)
+            off = 0
+            for name, n in plan.bshapes:
+                self.b[name] = bias[off:off + n]
+                off += n
+            # 256 -> 2 conv: dedicated VALU kernels read the module's fp32 weights
+            fh = ub.flow_head.conv2
+            self.w32 = fh.weight.detach().float().contiguous()
+            self.b32 = self.b['fh2']
+            if need_grad:
+                self.dwflat = torch.zeros(plan.dw_total, device=device)
+                for name, kind, pos, shape in plan.dw_views:
+                    n = shape[0] * (shape[1] if len(shape) > 1 else 1)
+                    (self.dw if kind == 'w' else self.db)[name] = \
+                        self.dwflat[pos:pos + n].view(shape)
 
 
 def _flush_wgrad(pk):
@@ -192,9 +277,7 @@ class _State:
 class _UpdateWeights(torch.autograd.Function):
     @staticmethod
     def forward(ctx, state, *params):
-        ub = state.ub
-        by_layer = module_params(ub)
-        state.packed = _Packed(by_layer, params[0].device, need_grad=state.need_grad)
+        state.packed = _Packed(state.ub, params, params[0].device, need_grad=state.need_grad)
         ctx.state = state
         ctx.n = len(params)
         return params[0].new_zeros(())
@@ -211,22 +294,17 @@ class _UpdateWeights(torch.autograd.Function):
 
 
 def _unpack_grads(pk):
-    grads = []
+    """Packed fp32 gradients -> one tensor per parameter (module layout), one gather."""
     for s in SPECS:
-        dw, db = pk.dw[s.name], pk.db[s.name]
         if s.scale != 1.0:
-            dw = dw * s.scale
-            db = db * s.scale
-        if s.small:
-            wg = C.unpack_weight_grad_small(dw, s.cout, s.in_real[0], s.k)
-        else:
-            wg = C.unpack_weight_grad(dw, s.cout, s.in_real, s.in_pad, s.k)
-        n_parts = 2 if s.name in ('zr1', 'zr2', 'head') else 1
-        if n_parts == 1:
-            grads += [wg, db]
-        else:
-            h = s.cout // 2
-            grads += [wg[:h], db[:h], wg[h:], db[h:]]
+            pk.dw[s.name].mul_(s.scale)
+            pk.db[s.name].mul_(s.scale)
+    plan = pk.plan
+    g = pk.dwflat.index_select(0, plan.uidx)
+    grads, off = [], 0
+    for n, shape in zip(plan.numels, plan.shapes):
+        grads.append(g[off:off + n].view(shape))
+        off += n
     return grads
 
 

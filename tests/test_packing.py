@@ -1,0 +1,70 @@
+"""CPU checks of the one-gather weight packing (fused update block) and the batched encoder
+weight cast: both must equal the per-layer reference formulation exactly."""
+import argparse
+
+import torch
+import torch.nn as nn
+
+from pytorch_raft_amd import RAFT
+from pytorch_raft_amd.ops import conv as C
+from pytorch_raft_amd.ops import update_hip as U
+from pytorch_raft_amd.ops.encoder import cast_conv_weights
+
+
+def _ub():
+    torch.manual_seed(0)
+    return RAFT(argparse.Namespace(small=False, mixed_precision=True)).update_block
+
+
+def test_pack_plan_matches_direct_packing():
+    ub = _ub()
+    params = U.flat_params(ub)
+    pk = U._Packed(ub, params, torch.device('cpu'), need_grad=True)
+    with torch.no_grad():
+        w, wd, b = U._pack_layers(U.module_params(ub), True, torch.bfloat16)
+    for name in w:
+        assert torch.equal(pk.w[name], w[name]), name
+        assert torch.equal(pk.b[name], b[name].float()), name
+        assert pk.kpad[name] == w[name].shape[1]
+    assert set(pk.wd) == set(wd)
+    for name in wd:
+        assert torch.equal(pk.wd[name], wd[name]), name
+
+
+def test_unpack_grads_matches_per_layer_unpack():
+    ub = _ub()
+    params = U.flat_params(ub)
+    pk = U._Packed(ub, params, torch.device('cpu'), need_grad=True)
+    g = torch.Generator().manual_seed(1)
+    pk.dwflat.copy_(torch.randn(pk.dwflat.shape, generator=g))
+    ref = []
+    for s in U.SPECS:
+        dw, db = pk.dw[s.name] * s.scale, pk.db[s.name] * s.scale
+        if s.small:
+            wg = C.unpack_weight_grad_small(dw, s.cout, s.in_real[0], s.k)
+        else:
+            wg = C.unpack_weight_grad(dw, s.cout, s.in_real, s.in_pad, s.k)
+        if s.name in ('zr1', 'zr2', 'head'):
+            h = s.cout // 2
+            ref += [wg[:h], db[:h], wg[h:], db[h:]]
+        else:
+            ref += [wg, db]
+    got = U._unpack_grads(pk)
+    assert len(got) == len(ref) == len(params)
+    for a, r, p in zip(got, ref, params):
+        assert a.shape == p.shape
+        assert torch.equal(a, r)
+
+
+def test_batched_encoder_weight_cast():
+    convs = [nn.Conv2d(3, 8, 7), nn.Conv2d(8, 16, 1), nn.Conv2d(16, 4, 3)]
+    m = cast_conv_weights(convs)
+    for c in convs:
+        w = m[c]
+        assert w.is_contiguous(memory_format=torch.channels_last)
+        assert torch.equal(w.float(), c.weight.to(torch.bfloat16).float())
+    loss = sum((m[c].float() ** 2).sum() * (i + 1) for i, c in enumerate(convs))
+    loss.backward()
+    for i, c in enumerate(convs):
+        ref = 2 * (i + 1) * c.weight.to(torch.bfloat16).float()
+        torch.testing.assert_close(c.weight.grad, ref, rtol=1e-2, atol=1e-3)

