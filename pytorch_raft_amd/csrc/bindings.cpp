@@ -1102,6 +1102,27 @@ void fh2_wgrad_(const std::vector<Tensor>& gouts, const std::vector<Tensor>& ins
               "fh2_wgrad: inputs need >= 256 channels, a multiple of 8");
 }
 
+// patch (B,H,W,128) bf16 = 7x7 neighbourhood of the flow (tap-major, 2 ch; 98..127 zero);
+// optionally slot[..., off:off+2] = flow
+void f1_patch_(const Tensor& flow, const Tensor& patch, const c10::optional<Tensor>& slot,
+               int64_t slot_off) {
+  check_cuda_f32(flow, "flow");
+  TORCH_CHECK(flow.dim() == 4 && flow.size(1) == 2, "flow must be (B,2,H,W)");
+  const int64_t B = flow.size(0), H = flow.size(2), W = flow.size(3);
+  check_nhwc(patch, B, H, W, "patch", at::kBFloat16);
+  TORCH_CHECK(patch.size(3) == 128, "patch must have 128 channels");
+  uint16_t* sp = nullptr;
+  int ss = 0;
+  if (slot.has_value() && slot->defined()) {
+    check_nhwc(*slot, B, H, W, "slot", at::kBFloat16);
+    TORCH_CHECK(slot_off >= 0 && slot_off + 2 <= slot->size(3), "slot range");
+    sp = bf16m(*slot) + slot_off;
+    ss = (int)slot->size(3);
+  }
+  c10::DeviceGuard gd(flow.device());
+  launch_f1_patch(flow.data_ptr<float>(), bf16m(patch), sp, ss, (int)B, (int)H, (int)W, cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(raft_amd, m) {
@@ -1133,6 +1154,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("warp_bwd(Tensor img, Tensor flow, Tensor dout, float sx, float bx, float sy, float by) -> Tensor[]");
   m.def("conv_fwd_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, Tensor? bias, int kh, int kw, int ph, int pw, int cout, int cin_small, int epi, int bn, float scale, int split, Tensor(a!)[] outs, int[] out_off, Tensor[] aux, int[] aux_off) -> ()");
   m.def("conv_wgrad_multi_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
+  m.def("f1_patch_(Tensor flow, Tensor(a!) patch, Tensor(b!)? slot, int slot_off) -> ()");
   m.def("fh2_fwd_(Tensor inp, Tensor w, Tensor b, Tensor(a!) out) -> ()");
   m.def("fh2_dgrad_(Tensor gout, Tensor w, Tensor fm, Tensor(a!) dx) -> ()");
   m.def("fh2_wgrad_(Tensor[] gouts, Tensor[] ins, Tensor(a!) dw, Tensor(b!)? db) -> ()");
@@ -1149,6 +1171,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("corr_otf_window_bwd_", &corr_otf_window_bwd_);
   m.impl("norm_fwd_", &norm_fwd_);
   m.impl("norm_bwd_", &norm_bwd_);
+  m.impl("f1_patch_", &f1_patch_);
   m.impl("fh2_fwd_", &fh2_fwd_);
   m.impl("fh2_dgrad_", &fh2_dgrad_);
   m.impl("fh2_wgrad_", &fh2_wgrad_);

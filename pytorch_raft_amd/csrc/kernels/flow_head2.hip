@@ -6,11 +6,11 @@
 // dgrad per iteration at the chairs shape, and the padded batched wgrad ~0.4 ms per step).  Here
 // each direction is one bandwidth-shaped VALU kernel over NHWC bf16 activations:
 //
-//   fwd    thread = (pixel, 64-channel quarter), 9 taps x 8 16-B loads, weights broadcast from LDS,
-//          4-way LDS combine, fp32 NCHW delta (+bias)                                    (wave64)
-//   dgrad  thread = (pixel, 8-channel group), its 144 weights held in VGPRs for the whole launch,
-//          18 broadcast loads of the fp32 NCHW output gradient per pixel, ReLU gate from fm,
-//          one 16-B bf16 store                                                 (adjoint, zero pad)
+//   fwd    thread = (pixel, 8-channel group): 9 coalesced 16-B loads, 72 v_dot2_f32_bf16 against
+//          its bf16-pair weights held in VGPRs, 32-lane shuffle reduction, fp32 NCHW delta (+bias)
+//   dgrad  thread = (pixel, 8-channel group): the two output-gradient channels of each tap form a
+//          bf16 pair, dot2 against (W0[c], W1[c]) pairs in VGPRs, ReLU gate from fm, one 16-B
+//          bf16 store                                                          (adjoint, zero pad)
 //   wgrad  thread = (output row, 8-channel group), a 3x3 window of 16-B input vectors slides along
 //          x (3 new loads per pixel), 144 fp32 accumulators, LDS combine over the 8 row lanes,
 //          one fp32 atomic per (weight, workgroup); all GRU iterations of a step in one launch.
@@ -33,110 +33,148 @@ __device__ __forceinline__ void bf16x8_to_f32(const uint4 v, float (&f)[8]) {
   }
 }
 
-// grid (ceil(W/64), H, B), block 256: lane = pixel, wave = channel quarter
+typedef __bf16 __attribute__((ext_vector_type(2))) bf16x2_t;
+
+__device__ __forceinline__ bf16x2_t as_bf2(uint32_t u) { return __builtin_bit_cast(bf16x2_t, u); }
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+  return (uint32_t)raft_f32_to_bf16(lo) | ((uint32_t)raft_f32_to_bf16(hi) << 16);
+}
+__device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(as_bf2(a), as_bf2(b), c, false);
+}
+
+// out[b,o,y,x] = bias[o] + sum_{t,c} in[b, y+ky-1, x+kx-1, c] * W[o][c][t]
+// block 256 = 8 pixel lanes x 32 channel groups (8 channels = 4 bf16 pairs each); a wave reads two
+// pixels' 512 contiguous bytes per tap; the thread's 72 bf16-pair weights stay in VGPRs; products
+// by v_dot2_f32_bf16; 32-lane shuffle reduction; two pixels per thread per step for ILP
 __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict__ in, int cs,
                                                       const float* __restrict__ w,
                                                       const float* __restrict__ bias,
-                                                      float* __restrict__ out, int H, int W) {
-  __shared__ float2 wl[9 * FH_C];
-  __shared__ float2 red[4][64];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < 9 * FH_C; i += 256) {
-    const int t = i / FH_C, c = i - t * FH_C;
-    wl[i] = make_float2(w[c * 9 + t], w[(FH_C + c) * 9 + t]);
-  }
-  __syncthreads();
-  const int px = tid & 63, q = tid >> 6;
-  const int b = blockIdx.z, y = blockIdx.y, x = blockIdx.x * 64 + px;
-  float a0 = 0.f, a1 = 0.f;
-  if (x < W) {
+                                                      float* __restrict__ out, int B, int H,
+                                                      int W) {
+  const int g = threadIdx.x & 31, pl = threadIdx.x >> 5;
+  uint32_t wp[2][9][4];
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const int yy = y + ky - 1;
-      if (yy < 0 || yy >= H) continue;
+  for (int o = 0; o < 2; ++o)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int xx = x + kx - 1;
-        if (xx < 0 || xx >= W) continue;
-        const uint16_t* p = in + ((int64_t)(b * H + yy) * W + xx) * cs + q * 64;
-        const float2* wt = wl + (ky * 3 + kx) * FH_C + q * 64;
-        uint4 v[8];
+    for (int t = 0; t < 9; ++t)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const uint4*>(p + j * 8);
+      for (int j = 0; j < 4; ++j) {
+        const int c = g * 8 + 2 * j;
+        wp[o][t][j] = pack_bf2(w[(o * FH_C + c) * 9 + t], w[(o * FH_C + c + 1) * 9 + t]);
+      }
+  const float b0 = bias[0], b1 = bias[1];
+  const int64_t hw = (int64_t)H * W, P = (int64_t)B * hw;
+  const int64_t step = (int64_t)gridDim.x * 16;
+  for (int64_t p0 = (int64_t)blockIdx.x * 16 + pl; p0 < P; p0 += step) {
+    uint4 v[2][9];
+    int64_t pp[2];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float f[8];
-          bf16x8_to_f32(v[j], f);
+    for (int k = 0; k < 2; ++k) {
+      const int64_t p = p0 + k * 8;
+      pp[k] = p;
+      const int b = (int)(min(p, P - 1) / hw);
+      const int yx = (int)(min(p, P - 1) - (int64_t)b * hw);
+      const int y = yx / W, x = yx - y * W;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const float2 ww = wt[j * 8 + i];
-            a0 = fmaf(f[i], ww.x, a0);
-            a1 = fmaf(f[i], ww.y, a1);
-          }
-        }
+      for (int t = 0; t < 9; ++t) {
+        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+        const bool ok = p < P && yy >= 0 && yy < H && xx >= 0 && xx < W;
+        v[k][t] = ok ? *reinterpret_cast<const uint4*>(in + ((int64_t)(b * H + yy) * W + xx) * cs + g * 8)
+                     : make_uint4(0, 0, 0, 0);
       }
     }
-  }
-  red[q][px] = make_float2(a0, a1);
-  __syncthreads();
-  if (q == 0 && x < W) {
-    const float2 r0 = red[0][px], r1 = red[1][px], r2 = red[2][px], r3 = red[3][px];
-    const int64_t hw = (int64_t)H * W, o = (int64_t)y * W + x;
-    out[(int64_t)b * 2 * hw + o] = ((r0.x + r1.x) + (r2.x + r3.x)) + bias[0];
-    out[(int64_t)b * 2 * hw + hw + o] = ((r0.y + r1.y) + (r2.y + r3.y)) + bias[1];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const uint32_t d[4] = {v[k][t].x, v[k][t].y, v[k][t].z, v[k][t].w};
+        a0 = dot2(d[0], wp[0][t][0], a0);
+        a1 = dot2(d[0], wp[1][t][0], a1);
+        a2 = dot2(d[1], wp[0][t][1], a2);
+        a3 = dot2(d[1], wp[1][t][1], a3);
+        a0 = dot2(d[2], wp[0][t][2], a0);
+        a1 = dot2(d[2], wp[1][t][2], a1);
+        a2 = dot2(d[3], wp[0][t][3], a2);
+        a3 = dot2(d[3], wp[1][t][3], a3);
+      }
+      float s0 = a0 + a2, s1 = a1 + a3;
+#pragma unroll
+      for (int m = 16; m > 0; m >>= 1) {
+        s0 += __shfl_xor(s0, m, 32);
+        s1 += __shfl_xor(s1, m, 32);
+      }
+      const int64_t p = pp[k];
+      if (g == 0 && p < P) {
+        const int64_t b = p / hw, yx = p - b * hw;
+        out[b * 2 * hw + yx] = s0 + b0;
+        out[b * 2 * hw + hw + yx] = s1 + b1;
+      }
+    }
   }
 }
 
 // dx[b,y,x,c] = [fm > 0] * sum_{ky,kx,o} gout[b,o,y-ky+1,x-kx+1] * W[o][c][ky][kx]
-// block 256 = 8 pixel lanes x 32 channel groups; grid-stride over pixels
+// block 256 = 8 pixel lanes x 32 channel groups; per channel the two output channels form one
+// bf16 pair: s[c] += dot2((g0, g1), (W0[c], W1[c])) with the 72 weight pairs held in VGPRs;
+// two pixels per thread per step; grid-stride over pixels
 __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict__ gout,
                                                         const float* __restrict__ w,
                                                         const uint16_t* __restrict__ fm, int fs,
                                                         uint16_t* __restrict__ dx, int ds, int B,
                                                         int H, int W) {
   const int g = threadIdx.x & 31, pl = threadIdx.x >> 5;
-  float wr[9][2][8];
+  uint32_t wp[9][8];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int o = 0; o < 2; ++o)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) wr[t][o][i] = w[(o * FH_C + g * 8 + i) * 9 + t];
+    for (int i = 0; i < 8; ++i)
+      wp[t][i] = pack_bf2(w[(g * 8 + i) * 9 + t], w[(FH_C + g * 8 + i) * 9 + t]);
   const int64_t hw = (int64_t)H * W, P = (int64_t)B * hw;
-  for (int64_t p = (int64_t)blockIdx.x * 8 + pl; p < P; p += (int64_t)gridDim.x * 8) {
-    const int b = (int)(p / hw);
-    const int yx = (int)(p - (int64_t)b * hw);
-    const int y = yx / W, x = yx - y * W;
-    const float* g0 = gout + (int64_t)b * 2 * hw;
-    float s[8];
+  const int64_t step = (int64_t)gridDim.x * 16;
+  for (int64_t p0 = (int64_t)blockIdx.x * 16 + pl; p0 < P; p0 += step) {
+    uint32_t gp[2][9];
+    uint4 m[2];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] = 0.f;
+    for (int k = 0; k < 2; ++k) {
+      const int64_t p = min(p0 + k * 8, P - 1);
+      const int b = (int)(p / hw);
+      const int yx = (int)(p - (int64_t)b * hw);
+      const int y = yx / W, x = yx - y * W;
+      const float* g0 = gout + (int64_t)b * 2 * hw;
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const int yy = y - ky + 1;
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const int xx = x - kx + 1;
+      for (int t = 0; t < 9; ++t) {
+        const int yy = y - t / 3 + 1, xx = x - t % 3 + 1;
         const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
         const int64_t o = ok ? (int64_t)yy * W + xx : 0;
-        const float d0 = ok ? g0[o] : 0.f, d1 = ok ? g0[hw + o] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          s[i] = fmaf(d0, wr[ky * 3 + kx][0][i], fmaf(d1, wr[ky * 3 + kx][1][i], s[i]));
+        gp[k][t] = ok ? pack_bf2(g0[o], g0[hw + o]) : 0u;
       }
+      m[k] = *reinterpret_cast<const uint4*>(fm + p * fs + g * 8);
     }
-    const uint4 m = *reinterpret_cast<const uint4*>(fm + p * fs + g * 8);
-    const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
-    uint32_t ov[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool lo = (mw[k] & 0x8000u) == 0 && (mw[k] & 0x7fffu) != 0;
-      const bool hi = (mw[k] & 0x80000000u) == 0 && (mw[k] & 0x7fff0000u) != 0;
-      const uint32_t a = lo ? raft_f32_to_bf16(s[2 * k]) : 0u;
-      const uint32_t c = hi ? raft_f32_to_bf16(s[2 * k + 1]) : 0u;
-      ov[k] = a | (c << 16);
+    for (int k = 0; k < 2; ++k) {
+      const int64_t p = p0 + k * 8;
+      float s[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[i] = dot2(gp[k][t], wp[t][i], s[i]);
+      const uint32_t mw[4] = {m[k].x, m[k].y, m[k].z, m[k].w};
+      uint32_t ov[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool lo = (mw[q] & 0x8000u) == 0 && (mw[q] & 0x7fffu) != 0;
+        const bool hi = (mw[q] & 0x80000000u) == 0 && (mw[q] & 0x7fff0000u) != 0;
+        const uint32_t a = lo ? raft_f32_to_bf16(s[2 * q]) : 0u;
+        const uint32_t c = hi ? raft_f32_to_bf16(s[2 * q + 1]) : 0u;
+        ov[q] = a | (c << 16);
+      }
+      if (p < P)
+        *reinterpret_cast<uint4*>(dx + p * ds + g * 8) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
     }
-    *reinterpret_cast<uint4*>(dx + p * ds + g * 8) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
   }
 }
 
@@ -235,8 +273,11 @@ __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int
 bool launch_fh2_fwd(const uint16_t* in, int cs, const float* w, const float* bias, float* out, int B,
                     int H, int W, hipStream_t stream) {
   if (cs % 8 != 0 || cs < FH_C) return false;
-  dim3 grid(raft_cdiv(W, 64), H, B);
-  hipLaunchKernelGGL(fh2_fwd_kernel, grid, dim3(256), 0, stream, in, cs, w, bias, out, H, W);
+  const int64_t P = (int64_t)B * H * W;
+  // weights are built once per thread: ~4 two-pixel steps per thread, >= 2 blocks per CU
+  const int64_t blocks = std::max<int64_t>(512, std::min<int64_t>((P + 63) / 64, 2048));
+  hipLaunchKernelGGL(fh2_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, in, cs, w, bias,
+                     out, B, H, W);
   return true;
 }
 
@@ -244,8 +285,7 @@ bool launch_fh2_dgrad(const float* gout, const float* w, const uint16_t* fm, int
                       int ds, int B, int H, int W, hipStream_t stream) {
   if (fs % 8 != 0 || ds % 8 != 0 || fs < FH_C || ds < FH_C) return false;
   const int64_t P = (int64_t)B * H * W;
-  // ~4 pixels per pixel lane: weights are loaded once per thread, so keep blocks few but >= 2/CU
-  const int64_t blocks = std::max<int64_t>(512, std::min<int64_t>((P + 31) / 32, 2048));
+  const int64_t blocks = std::max<int64_t>(512, std::min<int64_t>((P + 63) / 64, 2048));
   hipLaunchKernelGGL(fh2_dgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, gout, w, fm, fs,
                      dx, ds, B, H, W);
   return true;

@@ -176,6 +176,9 @@ void launch_gru_zr_bwd(const float* drh, const float* dz, const uint16_t* z, con
                        hipStream_t stream);
 void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int slot_stride, int B,
                       int HW, hipStream_t stream);
+// (B,2,H,W) fp32 flow -> (B,H,W,128) bf16 7x7 patch (tap-major, 2 ch), + optional flow slot
+void launch_f1_patch(const float* flow, uint16_t* patch, uint16_t* slot, int slot_stride, int B, int H,
+                     int W, hipStream_t stream);
 
 // ---- flow_head.conv2 (3x3, 256 -> 2): fwd / dgrad (+ReLU gate) / multi-item wgrad (flow_head2.hip)
 #define RAFT_FH2_MAX_ITEMS 32

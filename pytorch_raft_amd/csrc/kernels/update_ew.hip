@@ -86,6 +86,48 @@ __global__ __launch_bounds__(256) void flow_prep_kernel(const float* __restrict_
   }
 }
 
+// Motion-encoder convf1 (7x7, 2 -> 128, pad 3) as a 1x1 conv: patch[p][t*2 + c] = flow_c at tap t
+// of pixel p (t = ky*7 + kx; zero outside the map), channels 98..127 zero.  The dense-K packed
+// weight of the small-Cin path has exactly this K order, so the forward and the batched
+// weight gradient both run through the regular MFMA kernels.  Also writes the flow into the
+// motion-feature slot (`core/update.py:96`, cat([out, flow])).
+// thread = (pixel, 8-channel chunk of 16)
+__global__ __launch_bounds__(256) void f1_patch_kernel(const float* __restrict__ flow,
+                                                       uint16_t* __restrict__ patch,
+                                                       uint16_t* __restrict__ slot, int slot_stride,
+                                                       int B, int H, int W) {
+  const int64_t HW = (int64_t)H * W;
+  const int64_t total = (int64_t)B * HW * 16;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = t >> 4;
+    const int chunk = (int)(t & 15);
+    const int64_t b = p / HW;
+    const int yx = (int)(p - b * HW);
+    const int y = yx / W, x = yx - y * W;
+    const float* fx = flow + b * 2 * HW;
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tap = chunk * 4 + j;
+      uint32_t v = 0u;
+      if (tap < 49) {
+        const int yy = y + tap / 7 - 3, xx = x + tap % 7 - 3;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+          const int64_t o = (int64_t)yy * W + xx;
+          v = (uint32_t)raft_f32_to_bf16(fx[o]) | ((uint32_t)raft_f32_to_bf16(fx[HW + o]) << 16);
+        }
+      }
+      w[j] = v;
+    }
+    *reinterpret_cast<uint4*>(patch + p * 128 + chunk * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+    if (slot != nullptr && chunk == 0) {
+      slot[p * slot_stride] = raft_f32_to_bf16(fx[yx]);
+      slot[p * slot_stride + 1] = raft_f32_to_bf16(fx[HW + yx]);
+    }
+  }
+}
+
 inline unsigned ew_blocks(int64_t total) {
   return (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 16);
 }
@@ -116,4 +158,11 @@ void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int sl
   const int64_t total = (int64_t)B * HW;
   hipLaunchKernelGGL(flow_prep_kernel, dim3(raft_cdiv(total, 256)), dim3(256), 0, stream, flow, flowb,
                      slot, slot_stride, B, HW);
+}
+
+void launch_f1_patch(const float* flow, uint16_t* patch, uint16_t* slot, int slot_stride, int B, int H,
+                     int W, hipStream_t stream) {
+  const int64_t total = (int64_t)B * H * W * 16;
+  hipLaunchKernelGGL(f1_patch_kernel, dim3(ew_blocks(total)), dim3(256), 0, stream, flow, patch, slot,
+                     slot_stride, B, H, W);
 }

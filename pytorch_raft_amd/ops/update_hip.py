@@ -10,12 +10,13 @@ This module runs one iteration as ONE autograd node built from the hand-written 
 forward (12 MFMA implicit-GEMM convs + 1 prep kernel, NHWC bf16, fp32 accumulation)::
 
     corr(384, from the lookup kernel) -c1(1x1,relu)-> c1(256) -c2(3x3,relu)-> cf[0:192]
-    flow -prep-> flowb(8) -f1(7x7,relu, dense-K small-Cin path)-> f1(128) -f2(3x3,relu)-> cf[192:256]
+    flow -patch-> 7x7x2 im2col(128) -f1(as 1x1, relu)-> f1(128) -f2(3x3,relu)-> cf[192:256]
     cf -conv(3x3,relu)-> mf[0:126] ; mf[126:128] = flow
     [h | inp | mf] -zr1(1x5, sigmoid epilogue)-> z1, r1, r1*h
     [r1*h | inp | mf] -q1(1x5, tanh + GRU-update epilogue)-> h1, q1         (same for 5x1 -> h2)
     h2 -head(3x3, relu; flow_head.conv1 | mask.0 fused N=512)-> fm(512)
-    fm[0:256] -f2(3x3)-> delta (fp32, NCHW)     fm[256:512] -mask.2(1x1, x0.25)-> mask (NHWC bf16)
+    fm[0:256] -fh2(3x3, VALU dot2 kernel)-> delta (fp32, NCHW)
+    fm[256:512] -mask.2(1x1, x0.25)-> mask (NHWC bf16)
 
 backward: bf16 pre-activation gradients from fused elementwise kernels (relu / GRU gate algebra),
 dgrad = the same conv kernel on flipped/transposed weights writing fp32 gradients into channel
@@ -38,8 +39,12 @@ CORR_BUF = 384  # lookup taps (4 x 81 = 324) zero-padded to a multiple of the co
 class _LayerSpec:
     """Geometry of one conv of the fused block."""
 
-    def __init__(self, name, cout, ksize, in_real, in_pad, small=False, relu=False, scale=1.0):
+    def __init__(self, name, cout, ksize, in_real, in_pad, small=False, relu=False, scale=1.0,
+                 patch=False):
         self.name = name
+        # patch: the conv runs as a 1x1 conv over a tap-major im2col patch buffer whose K order is
+        # the dense-K packing of the small-Cin weight (convf1: 7x7x2 -> 98 of 128 channels)
+        self.patch = patch
         self.cout = cout
         self.k = ksize
         self.pad = (ksize[0] // 2, ksize[1] // 2)
@@ -53,7 +58,7 @@ class _LayerSpec:
 SPECS = [
     _LayerSpec('c1', 256, (1, 1), [324], [CORR_BUF]),
     _LayerSpec('c2', 192, (3, 3), [256], [256]),
-    _LayerSpec('f1', 128, (7, 7), [2], [8], small=True),
+    _LayerSpec('f1', 128, (7, 7), [2], [8], small=True, patch=True),
     _LayerSpec('f2', 64, (3, 3), [128], [128]),
     _LayerSpec('conv', 126, (3, 3), [256], [256]),
     _LayerSpec('zr1', 256, (1, 5), [128, 128, 128], [128, 128, 128]),
@@ -238,16 +243,17 @@ class _Packed:
 
 def _flush_wgrad(pk):
     """Weight gradients of every deferred (conv, iteration) item: one multi-item launch per conv
-    (the weights are shared by all iterations), per-item launches for the small-Cin conv."""
+    (the weights are shared by all iterations; convf1 as a 1x1 conv over its patch buffers),
+    the flow-head conv2 by its own VALU kernel."""
     for name, items in pk.pending.items():
         s = SPEC[name]
         dw, db = pk.dw[name], pk.db[name]
+        k, pad, small = ((1, 1), (0, 0), False) if s.patch else (s.k, s.pad, s.small)
         same = all(it[1] == items[0][1] and [(o, c) for _, o, c in it[2]] ==
                    [(o, c) for _, o, c in items[0][2]] for it in items)
-        if s.small or not same or any(c % 128 for _, _, c in items[0][2]):
+        if small or not same or any(c % 128 for _, _, c in items[0][2]):
             for g, g_off, segs in items:
-                C.conv_wgrad(g, g_off, segs, s.k, s.pad, s.cout, dw, db,
-                             cin_small=2 if s.small else 0)
+                C.conv_wgrad(g, g_off, segs, k, pad, s.cout, dw, db, cin_small=2 if small else 0)
             continue
         g_off = items[0][1]
         in_off = [o for _, o, _ in items[0][2]]
@@ -255,7 +261,7 @@ def _flush_wgrad(pk):
         for i in range(0, len(items), C.MAX_WG_ITEMS):
             chunk = items[i:i + C.MAX_WG_ITEMS]
             C.conv_wgrad_multi([(g, [b for b, _, _ in segs]) for g, _, segs in chunk], g_off,
-                               in_off, in_cnt, s.k, s.pad, s.cout, dw, db)
+                               in_off, in_cnt, k, pad, s.cout, dw, db)
     pk.pending = {}
     items = pk.fh2_items
     for i in range(0, len(items), 32):
@@ -387,10 +393,10 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
     B, H, W, _ = h.shape
     dev = h.device
     sh = (B, H, W)
-    flowb = _bf16(sh + (8,), dev)  # flow_prep writes all 8 channels
+    patch = _bf16(sh + (128,), dev)  # f1_patch writes all 128 channels
     mf = _bf16(sh + (128,), dev)
     ops = _ext.ops()
-    ops.flow_prep_(flow, flowb, mf, 126)
+    ops.f1_patch_(flow, patch, mf, 126)
     c1 = _bf16(sh + (256,), dev)
     cf = _bf16(sh + (256,), dev)
     f1 = _bf16(sh + (128,), dev)
@@ -401,12 +407,13 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
         w, b = pk.w[name], pk.b[name]
         if cout != s.cout:  # leading output rows of a fused conv (packed rows are cout-major)
             w, b = w[:C.round_up(cout, 128)], b[:cout]
-        C.conv_fwd(segs, w, b, s.k, s.pad, cout, epi, outs, offs, aux,
-                   aux_offs, scale=s.scale, split=split, cin_small=2 if s.small else 0)
+        k, pad, small = ((1, 1), (0, 0), False) if s.patch else (s.k, s.pad, s.small)
+        C.conv_fwd(segs, w, b, k, pad, cout, epi, outs, offs, aux,
+                   aux_offs, scale=s.scale, split=split, cin_small=2 if small else 0)
 
     conv('c1', [(corr, 0, CORR_BUF)], C.EPI_RELU_BF16, [c1], [0])
     conv('c2', [(c1, 0, 256)], C.EPI_RELU_BF16, [cf], [0])
-    conv('f1', [(flowb, 0, 8)], C.EPI_RELU_BF16, [f1], [0])
+    conv('f1', [(patch, 0, 128)], C.EPI_RELU_BF16, [f1], [0])
     conv('f2', [(f1, 0, 128)], C.EPI_RELU_BF16, [cf], [192])
     conv('conv', [(cf, 0, 256)], C.EPI_RELU_BF16, [mf], [0])
     gates = {}
@@ -434,7 +441,7 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
         ops.fh2_fwd_(fm, pk.w32, pk.b32, delta)
         mask = None
     g1, g2 = gates['1'], gates['2']
-    return h2, delta, mask, (corr, flowb, c1, cf, f1, mf, inp, *g1, *g2, h2, fm)
+    return h2, delta, mask, (corr, patch, c1, cf, f1, mf, inp, *g1, *g2, h2, fm)
 
 
 class _UpdateIter(torch.autograd.Function):
@@ -454,7 +461,7 @@ class _UpdateIter(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gh, gdelta, gmask):
         pk = ctx.state.packed
-        (corr, flowb, c1, cf, f1, mf, inp, h0, z1, rh1, r1, q1, h1, z2, rh2, r2, q2, h2, fm) = \
+        (corr, patch, c1, cf, f1, mf, inp, h0, z1, rh1, r1, q1, h1, z2, rh2, r2, q2, h2, fm) = \
             ctx.saved_tensors
         B, H, W, _ = h2.shape
         P = B * H * W
@@ -537,7 +544,7 @@ class _UpdateIter(torch.autograd.Function):
         dgrad('c2', [(dpre_cf, 0, 192)], [(dpre_c1, 0, 256, 256, 0, c1, 0)])
         dpre_f1 = _bf16(sh + (128,), dev)
         dgrad('f2', [(dpre_cf, 192, 64)], [(dpre_f1, 0, 128, 128, 0, f1, 0)])
-        wgrad('f1', dpre_f1, 0, [(flowb, 0, 8)])
+        wgrad('f1', dpre_f1, 0, [(patch, 0, 128)])
         wgrad('c1', dpre_c1, 0, [(corr, 0, CORR_BUF)])
         # bf16 (the dtype of the corr input): autograd would otherwise cast an fp32 gradient
         dcorr = _bf16(sh + (CORR_BUF,), dev)

@@ -75,8 +75,9 @@ def test_dry_run_fused_training_step(alternate):
         loss, metrics = sequence_loss(preds, flow, valid, 0.8)
         loss.backward()
     names = set(ops.calls)
-    assert {'conv_fwd_', 'conv_dgrad_', 'conv_wgrad_', 'gru_q_bwd_', 'gru_zr_bwd_', 'relu_bwd_',
-            'flow_prep_', 'convex_up_fwd', 'convex_up_bwd', 'seq_loss_fwd'} <= names, names
+    assert {'conv_fwd_', 'conv_dgrad_', 'conv_wgrad_multi_', 'gru_q_bwd_', 'gru_zr_bwd_',
+            'relu_bwd_', 'f1_patch_', 'fh2_fwd_', 'fh2_dgrad_', 'fh2_wgrad_', 'convex_up_fwd',
+            'convex_up_bwd', 'seq_loss_fwd'} <= names, names
     if not alternate:
         assert {'corr_build', 'corr_lookup_nhwc_', 'corr_window_grad', 'corr_window_reduce'} <= names
     else:

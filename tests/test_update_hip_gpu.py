@@ -93,7 +93,8 @@ def test_flow_head2_kernels_match_fp32(ext_ops, cs, shape):
     out = torch.empty(B, 2, H, W, device=DEV)
     ext_ops.fh2_fwd_(fm, w, b, out)
     ref = F.conv2d(x, w, b, padding=1)
-    torch.testing.assert_close(out, ref, atol=1e-3, rtol=1e-3)
+    # bf16 weights (v_dot2_f32_bf16), fp32 accumulation: ~0.2 % relative per product
+    torch.testing.assert_close(out, ref, atol=3e-2, rtol=1e-2)
     # input gradient, gated by fm > 0, written into channels 0..255 of a cs-wide buffer
     gout = torch.randn(B, 2, H, W, device=DEV, generator=g)
     dx = torch.full((B, H, W, cs), 7.0, device=DEV, dtype=torch.bfloat16)
@@ -144,3 +145,20 @@ def test_inference_mask_skip_and_graph_match_eager(ext_ops):
     assert swap > 0.1, swap
     for a, b in ((up_g, up_e), (up_g2, up_e2), (lo_g2, lo_e2)):
         assert (a - b).abs().max().item() < 0.05 * swap
+
+
+def test_f1_patch_matches_unfold(ext_ops):
+    """convf1 im2col: patch[..., t*2 + c] = flow_c at 7x7 tap t (zero padded), 98.. zero; the
+    flow is also written into the motion-feature slot."""
+    import torch.nn.functional as F
+    B, H, W = 2, 9, 13
+    flow = torch.randn(B, 2, H, W, device=DEV) * 4
+    patch = torch.full((B, H, W, 128), 5.0, device=DEV, dtype=torch.bfloat16)
+    slot = torch.zeros(B, H, W, 128, device=DEV, dtype=torch.bfloat16)
+    ext_ops.f1_patch_(flow, patch, slot, 126)
+    u = F.unfold(flow, 7, padding=3).view(B, 2, 49, H, W)        # (c, tap)
+    ref = u.permute(0, 3, 4, 2, 1).reshape(B, H, W, 98).to(torch.bfloat16)
+    assert torch.equal(patch[..., :98], ref)
+    assert (patch[..., 98:] == 0).all()
+    assert torch.equal(slot[..., 126:], flow.permute(0, 2, 3, 1).to(torch.bfloat16))
+    assert (slot[..., :126] == 0).all()
