@@ -7,12 +7,14 @@
 // each direction is one bandwidth-shaped VALU kernel over NHWC bf16 activations:
 //
 //   fwd    thread = (pixel, 8-channel group): 9 coalesced 16-B loads, 72 v_dot2_f32_bf16 against
-//          its bf16-pair weights held in VGPRs, 32-lane shuffle reduction, fp32 NCHW delta (+bias)
+//          bf16-pair weights staged once per block in LDS, 32-lane shuffle reduction, fp32 NCHW
+//          delta (+bias)
 //   dgrad  thread = (pixel, 8-channel group): the two output-gradient channels of each tap form a
-//          bf16 pair, dot2 against (W0[c], W1[c]) pairs in VGPRs, ReLU gate from fm, one 16-B
+//          bf16 pair, dot2 against (W0[c], W1[c]) pairs from LDS, ReLU gate from fm, one 16-B
 //          bf16 store                                                          (adjoint, zero pad)
-//   wgrad  thread = (output row, 8-channel group), a 3x3 window of 16-B input vectors slides along
-//          x (3 new loads per pixel), 144 fp32 accumulators, LDS combine over the 8 row lanes,
+//   wgrad  thread = (output row, 8-channel group), a 3x6 window of 16-B input vectors slides along
+//          x in blocks of 4 pixels (12 loads in flight per block), 144 fp32 accumulators, LDS
+//          combine over the 8 row lanes,
 //          one fp32 atomic per (weight, workgroup); all GRU iterations of a step in one launch.
 //
 // Weights: the module's fp32 (2, 256, 3, 3) tensor; weight gradient in the packed layout of the
@@ -45,34 +47,31 @@ __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
 
 // out[b,o,y,x] = bias[o] + sum_{t,c} in[b, y+ky-1, x+kx-1, c] * W[o][c][t]
 // block 256 = 8 pixel lanes x 32 channel groups (8 channels = 4 bf16 pairs each); a wave reads two
-// pixels' 512 contiguous bytes per tap; the thread's 72 bf16-pair weights stay in VGPRs; products
-// by v_dot2_f32_bf16; 32-lane shuffle reduction; two pixels per thread per step for ILP
+// pixels' 512 contiguous bytes per tap.  The weights are staged ONCE per block into LDS as bf16
+// pairs [t][o][c/2] (coalesced global reads) and read back as 16-B vectors; products by
+// v_dot2_f32_bf16; 32-lane shuffle reduction; grid-stride over NPIX-pixel steps
+template <int NPIX>
 __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict__ in, int cs,
                                                       const float* __restrict__ w,
                                                       const float* __restrict__ bias,
                                                       float* __restrict__ out, int B, int H,
                                                       int W) {
+  __shared__ uint32_t wl[9 * 2 * (FH_C / 2)];
+  for (int e = threadIdx.x; e < 9 * 2 * (FH_C / 2); e += 256) {
+    // e = (t * 2 + o) * 128 + cp ; source W[o][c][t] with c = 2 cp, 2 cp + 1
+    const int cp = e & 127, to = e >> 7, o = to & 1, t = to >> 1;
+    wl[e] = pack_bf2(w[(o * FH_C + 2 * cp) * 9 + t], w[(o * FH_C + 2 * cp + 1) * 9 + t]);
+  }
+  __syncthreads();
   const int g = threadIdx.x & 31, pl = threadIdx.x >> 5;
-  uint32_t wp[2][9][4];
-#pragma unroll
-  for (int o = 0; o < 2; ++o)
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = g * 8 + 2 * j;
-        wp[o][t][j] = pack_bf2(w[(o * FH_C + c) * 9 + t], w[(o * FH_C + c + 1) * 9 + t]);
-      }
   const float b0 = bias[0], b1 = bias[1];
   const int64_t hw = (int64_t)H * W, P = (int64_t)B * hw;
-  const int64_t step = (int64_t)gridDim.x * 16;
-  for (int64_t p0 = (int64_t)blockIdx.x * 16 + pl; p0 < P; p0 += step) {
-    uint4 v[2][9];
-    int64_t pp[2];
+  const int64_t step = (int64_t)gridDim.x * 8 * NPIX;
+  for (int64_t p0 = (int64_t)blockIdx.x * 8 * NPIX + pl; p0 < P; p0 += step) {
+    uint4 v[NPIX][9];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < NPIX; ++k) {
       const int64_t p = p0 + k * 8;
-      pp[k] = p;
       const int b = (int)(min(p, P - 1) / hw);
       const int yx = (int)(min(p, P - 1) - (int64_t)b * hw);
       const int y = yx / W, x = yx - y * W;
@@ -84,28 +83,36 @@ __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict
                      : make_uint4(0, 0, 0, 0);
       }
     }
+    float a[NPIX][4];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int k = 0; k < NPIX; ++k)
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const uint32_t d[4] = {v[k][t].x, v[k][t].y, v[k][t].z, v[k][t].w};
-        a0 = dot2(d[0], wp[0][t][0], a0);
-        a1 = dot2(d[0], wp[1][t][0], a1);
-        a2 = dot2(d[1], wp[0][t][1], a2);
-        a3 = dot2(d[1], wp[1][t][1], a3);
-        a0 = dot2(d[2], wp[0][t][2], a0);
-        a1 = dot2(d[2], wp[1][t][2], a1);
-        a2 = dot2(d[3], wp[0][t][3], a2);
-        a3 = dot2(d[3], wp[1][t][3], a3);
+      for (int j = 0; j < 4; ++j) a[k][j] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const uint4 w0 = *reinterpret_cast<const uint4*>(wl + (t * 2 + 0) * 128 + g * 4);
+      const uint4 w1 = *reinterpret_cast<const uint4*>(wl + (t * 2 + 1) * 128 + g * 4);
+#pragma unroll
+      for (int k = 0; k < NPIX; ++k) {
+        a[k][0] = dot2(v[k][t].x, w0.x, a[k][0]);
+        a[k][1] = dot2(v[k][t].x, w1.x, a[k][1]);
+        a[k][2] = dot2(v[k][t].y, w0.y, a[k][2]);
+        a[k][3] = dot2(v[k][t].y, w1.y, a[k][3]);
+        a[k][0] = dot2(v[k][t].z, w0.z, a[k][0]);
+        a[k][1] = dot2(v[k][t].z, w1.z, a[k][1]);
+        a[k][2] = dot2(v[k][t].w, w0.w, a[k][2]);
+        a[k][3] = dot2(v[k][t].w, w1.w, a[k][3]);
       }
-      float s0 = a0 + a2, s1 = a1 + a3;
+    }
+#pragma unroll
+    for (int k = 0; k < NPIX; ++k) {
+      float s0 = a[k][0] + a[k][2], s1 = a[k][1] + a[k][3];
 #pragma unroll
       for (int m = 16; m > 0; m >>= 1) {
         s0 += __shfl_xor(s0, m, 32);
         s1 += __shfl_xor(s1, m, 32);
       }
-      const int64_t p = pp[k];
+      const int64_t p = p0 + k * 8;
       if (g == 0 && p < P) {
         const int64_t b = p / hw, yx = p - b * hw;
         out[b * 2 * hw + yx] = s0 + b0;
@@ -117,20 +124,20 @@ __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict
 
 // dx[b,y,x,c] = [fm > 0] * sum_{ky,kx,o} gout[b,o,y-ky+1,x-kx+1] * W[o][c][ky][kx]
 // block 256 = 8 pixel lanes x 32 channel groups; per channel the two output channels form one
-// bf16 pair: s[c] += dot2((g0, g1), (W0[c], W1[c])) with the 72 weight pairs held in VGPRs;
-// two pixels per thread per step; grid-stride over pixels
+// bf16 pair: s[c] += dot2((g0, g1), (W0[c], W1[c])), the pairs staged once per block in LDS as
+// [t][c] and read as 16-B vectors; two pixels per thread per step; grid-stride over pixels
 __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict__ gout,
                                                         const float* __restrict__ w,
                                                         const uint16_t* __restrict__ fm, int fs,
                                                         uint16_t* __restrict__ dx, int ds, int B,
                                                         int H, int W) {
+  __shared__ uint32_t wl[9 * FH_C];
+  for (int e = threadIdx.x; e < 9 * FH_C; e += 256) {
+    const int c = e & (FH_C - 1), t = e >> 8;
+    wl[e] = pack_bf2(w[c * 9 + t], w[(FH_C + c) * 9 + t]);
+  }
+  __syncthreads();
   const int g = threadIdx.x & 31, pl = threadIdx.x >> 5;
-  uint32_t wp[9][8];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-      wp[t][i] = pack_bf2(w[(g * 8 + i) * 9 + t], w[(FH_C + g * 8 + i) * 9 + t]);
   const int64_t hw = (int64_t)H * W, P = (int64_t)B * hw;
   const int64_t step = (int64_t)gridDim.x * 16;
   for (int64_t p0 = (int64_t)blockIdx.x * 16 + pl; p0 < P; p0 += step) {
@@ -148,28 +155,37 @@ __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict_
         const int yy = y - t / 3 + 1, xx = x - t % 3 + 1;
         const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
         const int64_t o = ok ? (int64_t)yy * W + xx : 0;
-        gp[k][t] = ok ? pack_bf2(g0[o], g0[hw + o]) : 0u;
+        const float d0 = g0[o], d1 = g0[hw + o];
+        gp[k][t] = ok ? pack_bf2(d0, d1) : 0u;
       }
       m[k] = *reinterpret_cast<const uint4*>(fm + p * fs + g * 8);
+    }
+    float s[2][8];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[k][i] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const uint4 wa = *reinterpret_cast<const uint4*>(wl + t * FH_C + g * 8);
+      const uint4 wb = *reinterpret_cast<const uint4*>(wl + t * FH_C + g * 8 + 4);
+      const uint32_t wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[k][i] = dot2(gp[k][t], wv[i], s[k][i]);
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int64_t p = p0 + k * 8;
-      float s[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s[i] = 0.f;
-#pragma unroll
-      for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) s[i] = dot2(gp[k][t], wp[t][i], s[i]);
       const uint32_t mw[4] = {m[k].x, m[k].y, m[k].z, m[k].w};
       uint32_t ov[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const bool lo = (mw[q] & 0x8000u) == 0 && (mw[q] & 0x7fffu) != 0;
         const bool hi = (mw[q] & 0x80000000u) == 0 && (mw[q] & 0x7fff0000u) != 0;
-        const uint32_t a = lo ? raft_f32_to_bf16(s[2 * q]) : 0u;
-        const uint32_t c = hi ? raft_f32_to_bf16(s[2 * q + 1]) : 0u;
+        const uint32_t a = lo ? raft_f32_to_bf16(s[k][2 * q]) : 0u;
+        const uint32_t c = hi ? raft_f32_to_bf16(s[k][2 * q + 1]) : 0u;
         ov[q] = a | (c << 16);
       }
       if (p < P)
@@ -203,42 +219,52 @@ __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int
     if (y >= H) continue;
     const uint16_t* in = it.in[item] + (int64_t)b * hw * cs + g * 8;
     const float* go = it.gout[item] + (int64_t)b * 2 * hw + (int64_t)y * W;
-    // window columns (x-1, x, x+1) of rows (y-1, y, y+1); column -1 is zero padding
-    uint4 win[3][3];
+    // window columns (xb-1 .. xb+4) of rows (y-1, y, y+1) for a block of 4 output pixels xb..xb+3:
+    // the 12 loads of a block's new columns are issued together (one round trip per 4 pixels)
+    uint4 win[3][6];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      win[r][0] = make_uint4(0, 0, 0, 0);
+      win[r][0] = make_uint4(0, 0, 0, 0);  // column -1: zero padding
       const int yy = y + r - 1;
       win[r][1] = (yy >= 0 && yy < H) ? *reinterpret_cast<const uint4*>(in + ((int64_t)yy * W) * cs)
                                       : make_uint4(0, 0, 0, 0);
     }
-    for (int x = 0; x < W; ++x) {
+    for (int xb = 0; xb < W; xb += 4) {
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int yy = y + r - 1;
-        win[r][2] = (yy >= 0 && yy < H && x + 1 < W)
-                        ? *reinterpret_cast<const uint4*>(in + ((int64_t)yy * W + x + 1) * cs)
-                        : make_uint4(0, 0, 0, 0);
-      }
-      const float d0 = go[x], d1 = go[hw + x];
-      bs0 += d0;
-      bs1 += d1;
 #pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          float f[8];
-          bf16x8_to_f32(win[r][k], f);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            acc[0][r * 3 + k][i] = fmaf(d0, f[i], acc[0][r * 3 + k][i]);
-            acc[1][r * 3 + k][i] = fmaf(d1, f[i], acc[1][r * 3 + k][i]);
-          }
+        for (int j = 0; j < 4; ++j) {
+          const int xx = xb + 1 + j;
+          win[r][2 + j] = (yy >= 0 && yy < H && xx < W)
+                              ? *reinterpret_cast<const uint4*>(in + ((int64_t)yy * W + xx) * cs)
+                              : make_uint4(0, 0, 0, 0);
         }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int x = xb + j;
+        const bool ok = x < W;
+        const float d0 = ok ? go[x] : 0.f, d1 = ok ? go[hw + x] : 0.f;
+        bs0 += d0;
+        bs1 += d1;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            float f[8];
+            bf16x8_to_f32(win[r][j + k], f);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              acc[0][r * 3 + k][i] = fmaf(d0, f[i], acc[0][r * 3 + k][i]);
+              acc[1][r * 3 + k][i] = fmaf(d1, f[i], acc[1][r * 3 + k][i]);
+            }
+          }
+      }
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
-        win[r][0] = win[r][1];
-        win[r][1] = win[r][2];
+        win[r][0] = win[r][4];
+        win[r][1] = win[r][5];
       }
     }
   }
@@ -276,7 +302,7 @@ bool launch_fh2_fwd(const uint16_t* in, int cs, const float* w, const float* bia
   const int64_t P = (int64_t)B * H * W;
   // weights are built once per thread: ~4 two-pixel steps per thread, >= 2 blocks per CU
   const int64_t blocks = std::max<int64_t>(512, std::min<int64_t>((P + 63) / 64, 2048));
-  hipLaunchKernelGGL(fh2_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, in, cs, w, bias,
+  hipLaunchKernelGGL(fh2_fwd_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, stream, in, cs, w, bias,
                      out, B, H, W);
   return true;
 }

@@ -124,8 +124,11 @@ def conv_wgrad_multi(items, g_off, in_off, in_cnt, ksize, pad, cout, dw, db=None
         p = g0.shape[0] * g0.shape[1] * g0.shape[2]
         tiles = max(1, (cout + 127) // 128) * max(1, (dw.shape[1] + 127) // 128)
         # >= ~3 resident rounds of workgroups over all items; each split's partial tile leaves
-        # the chip as fp32 atomics, so no more splits than that
+        # the chip as fp32 atomics, so no more splits than that -- and at most ~48 partial tiles
+        # land on the same dw tile (a 768-way same-address atomic pile-up made the K=128 convf1
+        # weight gradient 20x slower than its MFMA work)
         per_item = max(1, (768 + tiles * n - 1) // (tiles * n))
+        per_item = max(1, min(per_item, 48 // n))
         pix_per_split = round_up((p + per_item - 1) // per_item, 64)
     ins = [b for _, bufs in items for b in bufs]
     ops.conv_wgrad_multi_([g for g, _ in items], int(g_off), ins, [int(o) for o in in_off],
