@@ -1030,48 +1030,49 @@ void flow_prep_(const Tensor& flow, const Tensor& flowb, const c10::optional<Ten
 }
 
 // ------------------------------------------------------------------ flow_head.conv2 (256 -> 2)
-void check_fh2_w(const Tensor& w, const Tensor& b) {
-  check_cuda_f32(w, "fh2 weight");
-  check_cuda_f32(b, "fh2 bias");
-  TORCH_CHECK(w.dim() == 4 && w.size(0) == 2 && w.size(1) == 256 && w.size(2) == 3 && w.size(3) == 3,
-              "fh2 weight must be (2,256,3,3)");
-  TORCH_CHECK(b.numel() == 2, "fh2 bias must have 2 elements");
+// Weights arrive as bf16 pair tables built by the update block's packing gather:
+// wf = W[o][c][t] as [t][o][c] (2304 bf16), wd = W[o][c][t] as [t][c][o] (4608 bf16).
+const uint32_t* fh2_pairs(const Tensor& t, int64_t n, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kBFloat16, name,
+              " must be a contiguous bf16 GPU tensor");
+  TORCH_CHECK(t.numel() == n, name, " must hold ", n, " elements");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-B aligned");
+  return reinterpret_cast<const uint32_t*>(t.data_ptr<at::BFloat16>());
 }
 
 // out (B,2,H,W) fp32 = conv3x3(in[..., 0:256]) + bias
-void fh2_fwd_(const Tensor& in, const Tensor& w, const Tensor& b, const Tensor& out) {
+void fh2_fwd_(const Tensor& in, const Tensor& wf, const Tensor& b, const Tensor& out) {
   TORCH_CHECK(in.dim() == 4, "in must be (B,H,W,C)");
   const int64_t B = in.size(0), H = in.size(1), W = in.size(2), cs = in.size(3);
   check_nhwc(in, B, H, W, "fh2 in", at::kBFloat16);
-  check_fh2_w(w, b);
+  const uint32_t* wp = fh2_pairs(wf, 9 * 2 * 256, "fh2 wf");
+  check_cuda_f32(b, "fh2 bias");
+  TORCH_CHECK(b.numel() == 2, "fh2 bias must have 2 elements");
   check_cuda_f32(out, "fh2 out");
   TORCH_CHECK(out.dim() == 4 && out.size(0) == B && out.size(1) == 2 && out.size(2) == H &&
               out.size(3) == W, "fh2 out must be (B,2,H,W)");
   c10::DeviceGuard gd(in.device());
-  TORCH_CHECK(launch_fh2_fwd(bf16p(in), (int)cs, w.data_ptr<float>(), b.data_ptr<float>(),
-                             out.data_ptr<float>(), (int)B, (int)H, (int)W, cur_stream()),
+  TORCH_CHECK(launch_fh2_fwd(bf16p(in), (int)cs, wp, b.data_ptr<float>(), out.data_ptr<float>(),
+                             (int)B, (int)H, (int)W, cur_stream()),
               "fh2_fwd: input needs >= 256 channels, a multiple of 8");
 }
 
 // dx[..., 0:256] (bf16) = [fm[..., 0:256] > 0] * conv3x3^T(gout)
-void fh2_dgrad_(const Tensor& gout, const Tensor& w, const Tensor& fm, const Tensor& dx) {
+void fh2_dgrad_(const Tensor& gout, const Tensor& wd, const Tensor& fm, const Tensor& dx) {
   check_cuda_f32(gout, "fh2 gout");
   TORCH_CHECK(gout.dim() == 4 && gout.size(1) == 2, "gout must be (B,2,H,W)");
   const int64_t B = gout.size(0), H = gout.size(2), W = gout.size(3);
   check_nhwc(fm, B, H, W, "fh2 fm", at::kBFloat16);
   check_nhwc(dx, B, H, W, "fh2 dx", at::kBFloat16);
-  TORCH_CHECK(w.dim() == 4 && w.size(0) == 2 && w.size(1) == 256, "fh2 weight must be (2,256,3,3)");
-  check_cuda_f32(w, "fh2 weight");
+  const uint32_t* wp = fh2_pairs(wd, 9 * 256 * 2, "fh2 wd");
   c10::DeviceGuard gd(gout.device());
-  TORCH_CHECK(launch_fh2_dgrad(gout.data_ptr<float>(), w.data_ptr<float>(), bf16p(fm),
-                               (int)fm.size(3), bf16m(dx), (int)dx.size(3), (int)B, (int)H, (int)W,
-                               cur_stream()),
+  TORCH_CHECK(launch_fh2_dgrad(gout.data_ptr<float>(), wp, bf16p(fm), (int)fm.size(3), bf16m(dx),
+                               (int)dx.size(3), (int)B, (int)H, (int)W, cur_stream()),
               "fh2_dgrad: fm / dx need >= 256 channels, multiples of 8");
 }
 
-// dw (2, 9*256) fp32 += sum over items of the packed weight gradient; db (2) += bias gradient
-void fh2_wgrad_(const std::vector<Tensor>& gouts, const std::vector<Tensor>& ins, const Tensor& dw,
-                const c10::optional<Tensor>& db) {
+// part (G, 2*2304 + 2) fp32 <- per-workgroup partial [dw (o, t*256 + c) | db] sums over all items
+void fh2_wgrad_(const std::vector<Tensor>& gouts, const std::vector<Tensor>& ins, const Tensor& part) {
   const int64_t n = (int64_t)gouts.size();
   TORCH_CHECK(n >= 1 && n <= RAFT_FH2_MAX_ITEMS && (int64_t)ins.size() == n, "1..",
               RAFT_FH2_MAX_ITEMS, " (gout, in) items");
@@ -1088,17 +1089,13 @@ void fh2_wgrad_(const std::vector<Tensor>& gouts, const std::vector<Tensor>& ins
     it.gout[i] = gouts[i].data_ptr<float>();
     it.in[i] = bf16p(ins[i]);
   }
-  check_cuda_f32(dw, "fh2 dw");
-  TORCH_CHECK(dw.numel() == 2 * 9 * 256, "fh2 dw must hold 2 x 2304 elements");
-  float* dbp = nullptr;
-  if (db.has_value() && db->defined()) {
-    check_cuda_f32(*db, "fh2 db");
-    TORCH_CHECK(db->numel() == 2, "fh2 db must have 2 elements");
-    dbp = db->data_ptr<float>();
-  }
-  c10::DeviceGuard gd(dw.device());
-  TORCH_CHECK(launch_fh2_wgrad(it, (int)cs, (int)B, (int)H, (int)W, dw.data_ptr<float>(), dbp,
-                               cur_stream()),
+  check_cuda_f32(part, "fh2 part");
+  TORCH_CHECK(part.dim() == 2 && part.size(1) == 2 * 9 * 256 + 2, "fh2 part must be (G, 4610)");
+  TORCH_CHECK(part.size(0) >= 1 && part.size(0) <= fh2_wgrad_units((int)n, (int)B, (int)H),
+              "fh2 part rows must be in [1, number of (item, image, 8-row) units]");
+  c10::DeviceGuard gd(part.device());
+  TORCH_CHECK(launch_fh2_wgrad(it, (int)cs, (int)B, (int)H, (int)W, part.data_ptr<float>(),
+                               (int)part.size(0), cur_stream()),
               "fh2_wgrad: inputs need >= 256 channels, a multiple of 8");
 }
 
@@ -1155,9 +1152,9 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("conv_fwd_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, Tensor? bias, int kh, int kw, int ph, int pw, int cout, int cin_small, int epi, int bn, float scale, int split, Tensor(a!)[] outs, int[] out_off, Tensor[] aux, int[] aux_off) -> ()");
   m.def("conv_wgrad_multi_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
   m.def("f1_patch_(Tensor flow, Tensor(a!) patch, Tensor(b!)? slot, int slot_off) -> ()");
-  m.def("fh2_fwd_(Tensor inp, Tensor w, Tensor b, Tensor(a!) out) -> ()");
-  m.def("fh2_dgrad_(Tensor gout, Tensor w, Tensor fm, Tensor(a!) dx) -> ()");
-  m.def("fh2_wgrad_(Tensor[] gouts, Tensor[] ins, Tensor(a!) dw, Tensor(b!)? db) -> ()");
+  m.def("fh2_fwd_(Tensor inp, Tensor wf, Tensor b, Tensor(a!) out) -> ()");
+  m.def("fh2_dgrad_(Tensor gout, Tensor wd, Tensor fm, Tensor(a!) dx) -> ()");
+  m.def("fh2_wgrad_(Tensor[] gouts, Tensor[] ins, Tensor(a!) part) -> ()");
   m.def("conv_wgrad_(Tensor g, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, int cin_small, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
 }
 

@@ -14,8 +14,8 @@
 //          bf16 store                                                          (adjoint, zero pad)
 //   wgrad  thread = (output row, 8-channel group), a 3x6 window of 16-B input vectors slides along
 //          x in blocks of 4 pixels (12 loads in flight per block), 144 fp32 accumulators, LDS
-//          combine over the 8 row lanes,
-//          one fp32 atomic per (weight, workgroup); all GRU iterations of a step in one launch.
+//          combine over the 8 row lanes, one partial row per workgroup (summed by the caller);
+//          all GRU iterations of a step in one launch.
 //
 // Weights: the module's fp32 (2, 256, 3, 3) tensor; weight gradient in the packed layout of the
 // fused block, dw[o][tap * 256 + c] (tap = ky * 3 + kx).
@@ -46,159 +46,111 @@ __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
 }
 
 // out[b,o,y,x] = bias[o] + sum_{t,c} in[b, y+ky-1, x+kx-1, c] * W[o][c][t]
-// block 256 = 8 pixel lanes x 32 channel groups (8 channels = 4 bf16 pairs each); a wave reads two
-// pixels' 512 contiguous bytes per tap.  The weights are staged ONCE per block into LDS as bf16
-// pairs [t][o][c/2] (coalesced global reads) and read back as 16-B vectors; products by
-// v_dot2_f32_bf16; 32-lane shuffle reduction; grid-stride over NPIX-pixel steps
-template <int NPIX>
+// thread = (pixel, 8-channel group = 4 bf16 pairs); block 256 = 8 pixels; one pixel per thread
+// and no loop, so every load of the launch is in flight at once (the kernel is latency-bound
+// otherwise).  wf: bf16 pairs [t][o][c/2] packed once per step; products by v_dot2_f32_bf16;
+// 32-lane shuffle reduction.
 __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict__ in, int cs,
-                                                      const float* __restrict__ w,
+                                                      const uint32_t* __restrict__ wf,
                                                       const float* __restrict__ bias,
                                                       float* __restrict__ out, int B, int H,
                                                       int W) {
-  __shared__ uint32_t wl[9 * 2 * (FH_C / 2)];
-  for (int e = threadIdx.x; e < 9 * 2 * (FH_C / 2); e += 256) {
-    // e = (t * 2 + o) * 128 + cp ; source W[o][c][t] with c = 2 cp, 2 cp + 1
-    const int cp = e & 127, to = e >> 7, o = to & 1, t = to >> 1;
-    wl[e] = pack_bf2(w[(o * FH_C + 2 * cp) * 9 + t], w[(o * FH_C + 2 * cp + 1) * 9 + t]);
-  }
-  __syncthreads();
-  const int g = threadIdx.x & 31, pl = threadIdx.x >> 5;
-  const float b0 = bias[0], b1 = bias[1];
+  const int g = threadIdx.x & 31;
   const int64_t hw = (int64_t)H * W, P = (int64_t)B * hw;
-  const int64_t step = (int64_t)gridDim.x * 8 * NPIX;
-  for (int64_t p0 = (int64_t)blockIdx.x * 8 * NPIX + pl; p0 < P; p0 += step) {
-    uint4 v[NPIX][9];
+  const int64_t p = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int64_t pc = min(p, P - 1);
+  const int b = (int)(pc / hw);
+  const int yx = (int)(pc - (int64_t)b * hw);
+  const int y = yx / W, x = yx - y * W;
+  uint4 v[9];
 #pragma unroll
-    for (int k = 0; k < NPIX; ++k) {
-      const int64_t p = p0 + k * 8;
-      const int b = (int)(min(p, P - 1) / hw);
-      const int yx = (int)(min(p, P - 1) - (int64_t)b * hw);
-      const int y = yx / W, x = yx - y * W;
+  for (int t = 0; t < 9; ++t) {
+    const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    v[t] = ok ? *reinterpret_cast<const uint4*>(in + ((int64_t)(b * H + yy) * W + xx) * cs + g * 8)
+              : make_uint4(0, 0, 0, 0);
+  }
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-        const bool ok = p < P && yy >= 0 && yy < H && xx >= 0 && xx < W;
-        v[k][t] = ok ? *reinterpret_cast<const uint4*>(in + ((int64_t)(b * H + yy) * W + xx) * cs + g * 8)
-                     : make_uint4(0, 0, 0, 0);
-      }
-    }
-    float a[NPIX][4];
+  for (int t = 0; t < 9; ++t) {
+    const uint4 w0 = *reinterpret_cast<const uint4*>(wf + (t * 2 + 0) * 128 + g * 4);
+    const uint4 w1 = *reinterpret_cast<const uint4*>(wf + (t * 2 + 1) * 128 + g * 4);
+    a0 = dot2(v[t].x, w0.x, a0);
+    a1 = dot2(v[t].x, w1.x, a1);
+    a2 = dot2(v[t].y, w0.y, a2);
+    a3 = dot2(v[t].y, w1.y, a3);
+    a0 = dot2(v[t].z, w0.z, a0);
+    a1 = dot2(v[t].z, w1.z, a1);
+    a2 = dot2(v[t].w, w0.w, a2);
+    a3 = dot2(v[t].w, w1.w, a3);
+  }
+  float s0 = a0 + a2, s1 = a1 + a3;
 #pragma unroll
-    for (int k = 0; k < NPIX; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) a[k][j] = 0.f;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const uint4 w0 = *reinterpret_cast<const uint4*>(wl + (t * 2 + 0) * 128 + g * 4);
-      const uint4 w1 = *reinterpret_cast<const uint4*>(wl + (t * 2 + 1) * 128 + g * 4);
-#pragma unroll
-      for (int k = 0; k < NPIX; ++k) {
-        a[k][0] = dot2(v[k][t].x, w0.x, a[k][0]);
-        a[k][1] = dot2(v[k][t].x, w1.x, a[k][1]);
-        a[k][2] = dot2(v[k][t].y, w0.y, a[k][2]);
-        a[k][3] = dot2(v[k][t].y, w1.y, a[k][3]);
-        a[k][0] = dot2(v[k][t].z, w0.z, a[k][0]);
-        a[k][1] = dot2(v[k][t].z, w1.z, a[k][1]);
-        a[k][2] = dot2(v[k][t].w, w0.w, a[k][2]);
-        a[k][3] = dot2(v[k][t].w, w1.w, a[k][3]);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < NPIX; ++k) {
-      float s0 = a[k][0] + a[k][2], s1 = a[k][1] + a[k][3];
-#pragma unroll
-      for (int m = 16; m > 0; m >>= 1) {
-        s0 += __shfl_xor(s0, m, 32);
-        s1 += __shfl_xor(s1, m, 32);
-      }
-      const int64_t p = p0 + k * 8;
-      if (g == 0 && p < P) {
-        const int64_t b = p / hw, yx = p - b * hw;
-        out[b * 2 * hw + yx] = s0 + b0;
-        out[b * 2 * hw + hw + yx] = s1 + b1;
-      }
-    }
+  for (int m = 16; m > 0; m >>= 1) {
+    s0 += __shfl_xor(s0, m, 32);
+    s1 += __shfl_xor(s1, m, 32);
+  }
+  if (g == 0 && p < P) {
+    out[(int64_t)b * 2 * hw + yx] = s0 + bias[0];
+    out[(int64_t)b * 2 * hw + hw + yx] = s1 + bias[1];
   }
 }
 
 // dx[b,y,x,c] = [fm > 0] * sum_{ky,kx,o} gout[b,o,y-ky+1,x-kx+1] * W[o][c][ky][kx]
-// block 256 = 8 pixel lanes x 32 channel groups; per channel the two output channels form one
-// bf16 pair: s[c] += dot2((g0, g1), (W0[c], W1[c])), the pairs staged once per block in LDS as
-// [t][c] and read as 16-B vectors; two pixels per thread per step; grid-stride over pixels
+// thread = (pixel, 8-channel group); one pixel per thread, no loop.  Per channel the two output
+// channels form one bf16 pair: s[c] += dot2((g0, g1), (W0[c], W1[c])), wd: pairs [t][c] packed
+// once per step.
 __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict__ gout,
-                                                        const float* __restrict__ w,
+                                                        const uint32_t* __restrict__ wd,
                                                         const uint16_t* __restrict__ fm, int fs,
                                                         uint16_t* __restrict__ dx, int ds, int B,
                                                         int H, int W) {
-  __shared__ uint32_t wl[9 * FH_C];
-  for (int e = threadIdx.x; e < 9 * FH_C; e += 256) {
-    const int c = e & (FH_C - 1), t = e >> 8;
-    wl[e] = pack_bf2(w[c * 9 + t], w[(FH_C + c) * 9 + t]);
-  }
-  __syncthreads();
-  const int g = threadIdx.x & 31, pl = threadIdx.x >> 5;
+  const int g = threadIdx.x & 31;
   const int64_t hw = (int64_t)H * W, P = (int64_t)B * hw;
-  const int64_t step = (int64_t)gridDim.x * 16;
-  for (int64_t p0 = (int64_t)blockIdx.x * 16 + pl; p0 < P; p0 += step) {
-    uint32_t gp[2][9];
-    uint4 m[2];
+  const int64_t p = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int64_t pc = min(p, P - 1);
+  const int b = (int)(pc / hw);
+  const int yx = (int)(pc - (int64_t)b * hw);
+  const int y = yx / W, x = yx - y * W;
+  const float* g0 = gout + (int64_t)b * 2 * hw;
+  uint32_t gp[9];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int64_t p = min(p0 + k * 8, P - 1);
-      const int b = (int)(p / hw);
-      const int yx = (int)(p - (int64_t)b * hw);
-      const int y = yx / W, x = yx - y * W;
-      const float* g0 = gout + (int64_t)b * 2 * hw;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int yy = y - t / 3 + 1, xx = x - t % 3 + 1;
-        const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
-        const int64_t o = ok ? (int64_t)yy * W + xx : 0;
-        const float d0 = g0[o], d1 = g0[hw + o];
-        gp[k][t] = ok ? pack_bf2(d0, d1) : 0u;
-      }
-      m[k] = *reinterpret_cast<const uint4*>(fm + p * fs + g * 8);
-    }
-    float s[2][8];
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s[k][i] = 0.f;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const uint4 wa = *reinterpret_cast<const uint4*>(wl + t * FH_C + g * 8);
-      const uint4 wb = *reinterpret_cast<const uint4*>(wl + t * FH_C + g * 8 + 4);
-      const uint32_t wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) s[k][i] = dot2(gp[k][t], wv[i], s[k][i]);
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int64_t p = p0 + k * 8;
-      const uint32_t mw[4] = {m[k].x, m[k].y, m[k].z, m[k].w};
-      uint32_t ov[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool lo = (mw[q] & 0x8000u) == 0 && (mw[q] & 0x7fffu) != 0;
-        const bool hi = (mw[q] & 0x80000000u) == 0 && (mw[q] & 0x7fff0000u) != 0;
-        const uint32_t a = lo ? raft_f32_to_bf16(s[k][2 * q]) : 0u;
-        const uint32_t c = hi ? raft_f32_to_bf16(s[k][2 * q + 1]) : 0u;
-        ov[q] = a | (c << 16);
-      }
-      if (p < P)
-        *reinterpret_cast<uint4*>(dx + p * ds + g * 8) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
-    }
+  for (int t = 0; t < 9; ++t) {
+    const int yy = y - t / 3 + 1, xx = x - t % 3 + 1;
+    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    const int64_t o = ok ? (int64_t)yy * W + xx : 0;
+    const float d0 = g0[o], d1 = g0[hw + o];
+    gp[t] = ok ? pack_bf2(d0, d1) : 0u;
   }
+  const uint4 m = *reinterpret_cast<const uint4*>(fm + pc * fs + g * 8);
+  float s[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = 0.f;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const uint4 wa = *reinterpret_cast<const uint4*>(wd + t * FH_C + g * 8);
+    const uint4 wb = *reinterpret_cast<const uint4*>(wd + t * FH_C + g * 8 + 4);
+    const uint32_t wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = dot2(gp[t], wv[i], s[i]);
+  }
+  const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
+  uint32_t ov[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const bool lo = (mw[q] & 0x8000u) == 0 && (mw[q] & 0x7fffu) != 0;
+    const bool hi = (mw[q] & 0x80000000u) == 0 && (mw[q] & 0x7fff0000u) != 0;
+    const uint32_t a = lo ? raft_f32_to_bf16(s[2 * q]) : 0u;
+    const uint32_t c = hi ? raft_f32_to_bf16(s[2 * q + 1]) : 0u;
+    ov[q] = a | (c << 16);
+  }
+  if (p < P) *reinterpret_cast<uint4*>(dx + p * ds + g * 8) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
 }
 
 // dw[o][t*256 + c] += sum_items sum_p gout[p][o] * in[p + off_t][c];  db[o] += sum gout[p][o]
 // block 256 = 8 row lanes x 32 channel groups; a unit = (item, image, 8-row block)
 __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int B, int H, int W,
-                                                        float* __restrict__ dw,
-                                                        float* __restrict__ db) {
+                                                        float* __restrict__ part) {
   __shared__ float red[8 * 32 * 73];  // 72 accumulators (+1 pad) per thread, one half at a time
   const int g = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int yblocks = (H + 7) / 8;
@@ -268,7 +220,9 @@ __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int
       }
     }
   }
-  // combine the 8 row lanes (fixed order), one output channel o per round
+  // combine the 8 row lanes (fixed order), one output channel o per round; each block writes its
+  // own partial row (summed over blocks by the caller: deterministic, no same-address atomics)
+  float* prow = part + (int64_t)blockIdx.x * (2 * 9 * FH_C + 2);
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
     float* mine = red + (rl * 32 + g) * 73;
@@ -284,45 +238,49 @@ __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int
       float s = 0.f;
 #pragma unroll
       for (int l = 0; l < 8; ++l) s += red[(l * 32 + gg) * 73 + t * 8 + i];
-      atomicAdd(dw + (int64_t)o * 9 * FH_C + e, s);
+      prow[o * 9 * FH_C + e] = s;
     }
     __syncthreads();
   }
-  if (db != nullptr && g == 0) {
-    atomicAdd(db, bs0);
-    atomicAdd(db + 1, bs1);
+  // bias sums: every (row lane, group 0) thread holds one row's; combine the 8 in LDS
+  if (g == 0) {
+    red[rl * 2] = bs0;
+    red[rl * 2 + 1] = bs1;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    float s = 0.f;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) s += red[l * 2 + threadIdx.x];
+    prow[2 * 9 * FH_C + threadIdx.x] = s;
   }
 }
 
 }  // namespace
 
-bool launch_fh2_fwd(const uint16_t* in, int cs, const float* w, const float* bias, float* out, int B,
-                    int H, int W, hipStream_t stream) {
+bool launch_fh2_fwd(const uint16_t* in, int cs, const uint32_t* wf, const float* bias, float* out,
+                    int B, int H, int W, hipStream_t stream) {
   if (cs % 8 != 0 || cs < FH_C) return false;
   const int64_t P = (int64_t)B * H * W;
-  // weights are built once per thread: ~4 two-pixel steps per thread, >= 2 blocks per CU
-  const int64_t blocks = std::max<int64_t>(512, std::min<int64_t>((P + 63) / 64, 2048));
-  hipLaunchKernelGGL(fh2_fwd_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, stream, in, cs, w, bias,
-                     out, B, H, W);
+  hipLaunchKernelGGL(fh2_fwd_kernel, dim3(raft_cdiv(P, 8)), dim3(256), 0, stream, in, cs, wf, bias, out,
+                     B, H, W);
   return true;
 }
 
-bool launch_fh2_dgrad(const float* gout, const float* w, const uint16_t* fm, int fs, uint16_t* dx,
+bool launch_fh2_dgrad(const float* gout, const uint32_t* wd, const uint16_t* fm, int fs, uint16_t* dx,
                       int ds, int B, int H, int W, hipStream_t stream) {
   if (fs % 8 != 0 || ds % 8 != 0 || fs < FH_C || ds < FH_C) return false;
   const int64_t P = (int64_t)B * H * W;
-  const int64_t blocks = std::max<int64_t>(512, std::min<int64_t>((P + 63) / 64, 2048));
-  hipLaunchKernelGGL(fh2_dgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, gout, w, fm, fs,
+  hipLaunchKernelGGL(fh2_dgrad_kernel, dim3(raft_cdiv(P, 8)), dim3(256), 0, stream, gout, wd, fm, fs,
                      dx, ds, B, H, W);
   return true;
 }
 
-bool launch_fh2_wgrad(const Fh2Items& it, int cs, int B, int H, int W, float* dw, float* db,
+int fh2_wgrad_units(int n, int B, int H) { return n * B * ((H + 7) / 8); }
+
+bool launch_fh2_wgrad(const Fh2Items& it, int cs, int B, int H, int W, float* part, int blocks,
                       hipStream_t stream) {
-  if (it.n < 1 || it.n > RAFT_FH2_MAX_ITEMS || cs % 8 != 0 || cs < FH_C) return false;
-  const int units = it.n * B * ((H + 7) / 8);
-  // ~2 workgroups per CU: each adds its 4608 partial sums with one fp32 atomic apiece
-  const int blocks = std::min(units, 512);
-  hipLaunchKernelGGL(fh2_wgrad_kernel, dim3(blocks), dim3(256), 0, stream, it, cs, B, H, W, dw, db);
+  if (it.n < 1 || it.n > RAFT_FH2_MAX_ITEMS || cs % 8 != 0 || cs < FH_C || blocks < 1) return false;
+  hipLaunchKernelGGL(fh2_wgrad_kernel, dim3(blocks), dim3(256), 0, stream, it, cs, B, H, W, part);
   return true;
 }

@@ -187,11 +187,14 @@ struct Fh2Items {
   const uint16_t* in[RAFT_FH2_MAX_ITEMS];   // (B,H,W,cs) bf16 input (channels 0..255 used)
   int n;
 };
-bool launch_fh2_fwd(const uint16_t* in, int cs, const float* w, const float* bias, float* out, int B,
-                    int H, int W, hipStream_t stream);
-bool launch_fh2_dgrad(const float* gout, const float* w, const uint16_t* fm, int fs, uint16_t* dx,
+// wf: bf16 pairs [t][o][c/2] (9*2*128 uint32); wd: bf16 pairs (W0[c], W1[c]) [t][c] (9*256 uint32)
+bool launch_fh2_fwd(const uint16_t* in, int cs, const uint32_t* wf, const float* bias, float* out,
+                    int B, int H, int W, hipStream_t stream);
+bool launch_fh2_dgrad(const float* gout, const uint32_t* wd, const uint16_t* fm, int fs, uint16_t* dx,
                       int ds, int B, int H, int W, hipStream_t stream);
-bool launch_fh2_wgrad(const Fh2Items& it, int cs, int B, int H, int W, float* dw, float* db,
+// part: (blocks, 2*2304 + 2) fp32 per-workgroup partial [dw | db] rows (fully written)
+int fh2_wgrad_units(int n, int B, int H);
+bool launch_fh2_wgrad(const Fh2Items& it, int cs, int B, int H, int W, float* part, int blocks,
                       hipStream_t stream);
 
 // ---- NHWC lookup tile + window-compact backward (corr_window.hip)

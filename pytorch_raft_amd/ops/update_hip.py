@@ -102,8 +102,10 @@ def flat_params(ub):
 
 def _pack_layers(params_by_layer, need_grad, dtype):
     """Kernel-layout weights of every fused conv: ({name: forward [Npad][K]}, {name: adjoint
-    [Npad'][K']}, {name: bias}).  Runs on real parameters or on index tensors (``_PackPlan``)."""
-    w_out, wd_out, b_out = {}, {}, {}
+    [Npad'][K']}, {name: bias}, {extra tables}).  Runs on real parameters or on index tensors
+    (``_PackPlan``).  Extras: flow_head.conv2's bf16 pair tables for its VALU kernels, forward
+    [t][o][c] and adjoint [t][c][o]."""
+    w_out, wd_out, b_out, x_out = {}, {}, {}, {}
     for s in SPECS:
         ws = [w for w, _ in params_by_layer[s.name]]
         bs = [b for _, b in params_by_layer[s.name]]
@@ -131,7 +133,10 @@ def _pack_layers(params_by_layer, need_grad, dtype):
                     off += r
                 wt = torch.cat(parts, 0)
             wd_out[s.name] = C.pack_weight(wt, [cout_pad], [cout_pad], dtype=dtype)
-    return w_out, wd_out, b_out
+        if s.name == 'fh2':
+            x_out['fh2f'] = w.permute(2, 3, 0, 1).reshape(18, 256).to(dtype)
+            x_out['fh2d'] = w.permute(2, 3, 1, 0).reshape(9, 512).to(dtype)
+    return w_out, wd_out, b_out, x_out
 
 
 class _PackPlan:
@@ -153,15 +158,15 @@ class _PackPlan:
         it = iter(ids)
         by_layer = {s.name: [(next(it), next(it)) for _ in module_params(ub)[s.name]]
                     for s in SPECS}
-        w_idx, wd_idx, b_idx = _pack_layers(by_layer, need_grad, torch.float64)
+        w_idx, wd_idx, b_idx, x_idx = _pack_layers(by_layer, need_grad, torch.float64)
         # gather index: element id - 1; padding (id 0) -> the zero slot appended after the params
         self.views = []       # (kind, name, shape) in gather order
         parts = []
-        for kind, d in (('w', w_idx), ('wd', wd_idx)):
-            for s in SPECS:
-                if s.name in d:
-                    t = d[s.name]
-                    self.views.append((kind, s.name, tuple(t.shape)))
+        for kind, d in (('w', w_idx), ('wd', wd_idx), ('x', x_idx)):
+            for name in [s.name for s in SPECS] + sorted(x_idx):
+                if name in d:
+                    t = d[name]
+                    self.views.append((kind, name, tuple(t.shape)))
                     parts.append(t.reshape(-1))
         gidx = torch.cat(parts).round().long() - 1
         gidx[gidx < 0] = total
@@ -207,6 +212,7 @@ class _Packed:
     def __init__(self, ub, params, device, need_grad):
         self.w = {}
         self.wd = {}
+        self.x = {}
         self.b = {}
         self.dw = {}
         self.db = {}
@@ -222,16 +228,15 @@ class _Packed:
             off = 0
             for kind, name, shape in plan.views:
                 n = shape[0] * shape[1]
-                (self.w if kind == 'w' else self.wd)[name] = packed[off:off + n].view(shape)
+                {'w': self.w, 'wd': self.wd, 'x': self.x}[kind][name] = packed[off:off + n].view(shape)
                 off += n
             bias = flat.index_select(0, plan.bidx)
             off = 0
             for name, n in plan.bshapes:
                 self.b[name] = bias[off:off + n]
                 off += n
-            # 256 -> 2 conv: dedicated VALU kernels read the module's fp32 weights
-            fh = ub.flow_head.conv2
-            self.w32 = fh.weight.detach().float().contiguous()
+            # 256 -> 2 conv: dedicated VALU kernels read bf16 pair tables
+            self.fh2_wf, self.fh2_wd = self.x['fh2f'], self.x['fh2d']
             self.b32 = self.b['fh2']
             if need_grad:
                 self.dwflat = torch.zeros(plan.dw_total, device=device)
@@ -266,8 +271,14 @@ def _flush_wgrad(pk):
     items = pk.fh2_items
     for i in range(0, len(items), 32):
         chunk = items[i:i + 32]
-        _ext.ops().fh2_wgrad_([g for g, _ in chunk], [x for _, x in chunk], pk.dw['fh2'],
-                              pk.db['fh2'])
+        g0 = chunk[0][0]
+        units = len(chunk) * g0.shape[0] * ((g0.shape[2] + 7) // 8)
+        # one partial [dw | db] row per workgroup, summed here (deterministic, no atomics)
+        part = torch.empty(min(units, 512), 2 * 9 * 256 + 2, device=g0.device)
+        _ext.ops().fh2_wgrad_([g for g, _ in chunk], [x for _, x in chunk], part)
+        ps = part.sum(0)
+        pk.dw['fh2'].add_(ps[:2 * 9 * 256].view(2, 9 * 256))
+        pk.db['fh2'].add_(ps[2 * 9 * 256:])
     pk.fh2_items = []
 
 
@@ -351,8 +362,10 @@ def _backward_overlapped(st, pk, n):
             g.record_stream(side)
             for buf, _, _ in segs:
                 buf.record_stream(side)
-    for t in list(pk.dw.values()) + list(pk.db.values()):
-        t.record_stream(side)
+    for g, x in pk.fh2_items:
+        g.record_stream(side)
+        x.record_stream(side)
+    pk.dwflat.record_stream(side)
     params = st.params
     with torch.cuda.stream(side):
         _flush_wgrad(pk)
@@ -432,13 +445,13 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
     if need_mask:
         fm = _bf16(sh + (512,), dev)
         conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0])
-        ops.fh2_fwd_(fm, pk.w32, pk.b32, delta)
+        ops.fh2_fwd_(fm, pk.fh2_wf, pk.b32, delta)
         mask = _bf16(sh + (576,), dev)
         conv('m2', [(fm, 256, 256)], C.EPI_BF16, [mask], [0])
     else:
         fm = _bf16(sh + (256,), dev)
         conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0], cout=256)
-        ops.fh2_fwd_(fm, pk.w32, pk.b32, delta)
+        ops.fh2_fwd_(fm, pk.fh2_wf, pk.b32, delta)
         mask = None
     g1, g2 = gates['1'], gates['2']
     return h2, delta, mask, (corr, patch, c1, cf, f1, mf, inp, *g1, *g2, h2, fm)
@@ -498,7 +511,7 @@ class _UpdateIter(torch.autograd.Function):
         # ---- flow head conv2 -> delta (VALU kernels; fp32 output gradient read directly)
         gd = gdelta.contiguous().float()
         pk.fh2_items.append((gd, fm))
-        ops.fh2_dgrad_(gd, pk.w32, fm, dpre_head)
+        ops.fh2_dgrad_(gd, pk.fh2_wd, fm, dpre_head)
         # ---- head
         wgrad('head', dpre_head, 0, [(h2, 0, HD)])
         dh = gh.float().contiguous() if gh is not None else _f32(sh + (HD,), dev, zero=True)

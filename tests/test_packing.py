@@ -21,7 +21,7 @@ def test_pack_plan_matches_direct_packing():
     params = U.flat_params(ub)
     pk = U._Packed(ub, params, torch.device('cpu'), need_grad=True)
     with torch.no_grad():
-        w, wd, b = U._pack_layers(U.module_params(ub), True, torch.bfloat16)
+        w, wd, b, x = U._pack_layers(U.module_params(ub), True, torch.bfloat16)
     for name in w:
         assert torch.equal(pk.w[name], w[name]), name
         assert torch.equal(pk.b[name], b[name].float()), name
@@ -29,6 +29,10 @@ def test_pack_plan_matches_direct_packing():
     assert set(pk.wd) == set(wd)
     for name in wd:
         assert torch.equal(pk.wd[name], wd[name]), name
+    fw = ub.flow_head.conv2.weight.detach().to(torch.bfloat16)
+    assert torch.equal(pk.fh2_wf.reshape(3, 3, 2, 256), fw.permute(2, 3, 0, 1))
+    assert torch.equal(pk.fh2_wd.reshape(3, 3, 256, 2), fw.permute(2, 3, 1, 0))
+    assert pk.fh2_wf.data_ptr() % 16 == 0 and pk.fh2_wd.data_ptr() % 16 == 0
 
 
 def test_unpack_grads_matches_per_layer_unpack():

@@ -91,14 +91,17 @@ def test_flow_head2_kernels_match_fp32(ext_ops, cs, shape):
     x = fm[..., :256].float().permute(0, 3, 1, 2)
     # forward
     out = torch.empty(B, 2, H, W, device=DEV)
-    ext_ops.fh2_fwd_(fm, w, b, out)
+    wb = w.to(torch.bfloat16)
+    wf = wb.permute(2, 3, 0, 1).contiguous()        # bf16 pair tables: [t][o][c]
+    wd = wb.permute(2, 3, 1, 0).contiguous()        # [t][c][o]
+    ext_ops.fh2_fwd_(fm, wf, b, out)
     ref = F.conv2d(x, w, b, padding=1)
     # bf16 weights (v_dot2_f32_bf16), fp32 accumulation: ~0.2 % relative per product
     torch.testing.assert_close(out, ref, atol=3e-2, rtol=1e-2)
     # input gradient, gated by fm > 0, written into channels 0..255 of a cs-wide buffer
     gout = torch.randn(B, 2, H, W, device=DEV, generator=g)
     dx = torch.full((B, H, W, cs), 7.0, device=DEV, dtype=torch.bfloat16)
-    ext_ops.fh2_dgrad_(gout, w, fm, dx)
+    ext_ops.fh2_dgrad_(gout, wd, fm, dx)
     xr = x.clone().requires_grad_(True)
     F.conv2d(xr, w, b, padding=1).backward(gout)
     dref = (xr.grad * (x > 0)).permute(0, 2, 3, 1)
@@ -108,9 +111,10 @@ def test_flow_head2_kernels_match_fp32(ext_ops, cs, shape):
     # weight / bias gradient summed over 3 items, accumulated into existing values
     gouts = [gout, gout * 0.5, -gout]
     ins = [fm, fm, (fm.float() * 0.25).to(torch.bfloat16)]
-    dw = torch.ones(2, 9 * 256, device=DEV)
-    db = torch.ones(2, device=DEV)
-    ext_ops.fh2_wgrad_(gouts, ins, dw, db)
+    part = torch.full((5, 2 * 9 * 256 + 2), float('nan'), device=DEV)
+    ext_ops.fh2_wgrad_(gouts, ins, part)                # every row fully written
+    ps = part.sum(0)
+    dw, db = ps[:-2].view(2, 9 * 256) + 1.0, ps[-2:] + 1.0
     wr = w.clone().requires_grad_(True)
     br = b.clone().requires_grad_(True)
     for go, xi in zip(gouts, ins):
