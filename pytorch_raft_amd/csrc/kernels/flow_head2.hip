@@ -12,8 +12,8 @@
 //   dgrad  thread = (pixel, 8-channel group): the two output-gradient channels of each tap form a
 //          bf16 pair, dot2 against (W0[c], W1[c]) pairs from LDS, ReLU gate from fm, one 16-B
 //          bf16 store                                                          (adjoint, zero pad)
-//   wgrad  thread = (output row, 8-channel group), a 3x6 window of 16-B input vectors slides along
-//          x in blocks of 4 pixels (12 loads in flight per block), 144 fp32 accumulators, LDS
+//   wgrad  thread = (output row, 8-channel group), a 3x4 window of 16-B input vectors slides along
+//          x in blocks of 2 pixels (6 loads in flight per block), 144 fp32 accumulators, LDS
 //          combine over the 8 row lanes, one partial row per workgroup (summed by the caller);
 //          all GRU iterations of a step in one launch.
 //
@@ -46,10 +46,11 @@ __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
 }
 
 // out[b,o,y,x] = bias[o] + sum_{t,c} in[b, y+ky-1, x+kx-1, c] * W[o][c][t]
-// thread = (pixel, 8-channel group = 4 bf16 pairs); block 256 = 8 pixels; one pixel per thread
-// and no loop, so every load of the launch is in flight at once (the kernel is latency-bound
-// otherwise).  wf: bf16 pairs [t][o][c/2] packed once per step; products by v_dot2_f32_bf16;
-// 32-lane shuffle reduction.
+// thread = (NPIX pixels, 8-channel group = 4 bf16 pairs); block 256 = 8 x NPIX pixels.  No loop:
+// every load (weights once, then all pixels' taps) is issued before the first use, so the launch
+// costs one memory round trip; NPIX > 1 divides the weight-table re-reads.  wf: bf16 pairs
+// [t][o][c/2] from the packing gather; products by v_dot2_f32_bf16; 32-lane shuffle reduction.
+template <int NPIX>
 __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict__ in, int cs,
                                                       const uint32_t* __restrict__ wf,
                                                       const float* __restrict__ bias,
@@ -57,49 +58,62 @@ __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict
                                                       int W) {
   const int g = threadIdx.x & 31;
   const int64_t hw = (int64_t)H * W, P = (int64_t)B * hw;
-  const int64_t p = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
-  const int64_t pc = min(p, P - 1);
-  const int b = (int)(pc / hw);
-  const int yx = (int)(pc - (int64_t)b * hw);
-  const int y = yx / W, x = yx - y * W;
-  uint4 v[9];
+  uint4 w0[9], w1[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
-    const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
-    v[t] = ok ? *reinterpret_cast<const uint4*>(in + ((int64_t)(b * H + yy) * W + xx) * cs + g * 8)
-              : make_uint4(0, 0, 0, 0);
+    w0[t] = *reinterpret_cast<const uint4*>(wf + (t * 2 + 0) * 128 + g * 4);
+    w1[t] = *reinterpret_cast<const uint4*>(wf + (t * 2 + 1) * 128 + g * 4);
   }
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  uint4 v[NPIX][9];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const uint4 w0 = *reinterpret_cast<const uint4*>(wf + (t * 2 + 0) * 128 + g * 4);
-    const uint4 w1 = *reinterpret_cast<const uint4*>(wf + (t * 2 + 1) * 128 + g * 4);
-    a0 = dot2(v[t].x, w0.x, a0);
-    a1 = dot2(v[t].x, w1.x, a1);
-    a2 = dot2(v[t].y, w0.y, a2);
-    a3 = dot2(v[t].y, w1.y, a3);
-    a0 = dot2(v[t].z, w0.z, a0);
-    a1 = dot2(v[t].z, w1.z, a1);
-    a2 = dot2(v[t].w, w0.w, a2);
-    a3 = dot2(v[t].w, w1.w, a3);
-  }
-  float s0 = a0 + a2, s1 = a1 + a3;
+  for (int k = 0; k < NPIX; ++k) {
+    const int64_t p = ((int64_t)blockIdx.x * NPIX + k) * 8 + (threadIdx.x >> 5);
+    const int64_t pc = min(p, P - 1);
+    const int b = (int)(pc / hw);
+    const int yx = (int)(pc - (int64_t)b * hw);
+    const int y = yx / W, x = yx - y * W;
 #pragma unroll
-  for (int m = 16; m > 0; m >>= 1) {
-    s0 += __shfl_xor(s0, m, 32);
-    s1 += __shfl_xor(s1, m, 32);
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      v[k][t] = ok ? *reinterpret_cast<const uint4*>(in + ((int64_t)(b * H + yy) * W + xx) * cs + g * 8)
+                   : make_uint4(0, 0, 0, 0);
+    }
   }
-  if (g == 0 && p < P) {
-    out[(int64_t)b * 2 * hw + yx] = s0 + bias[0];
-    out[(int64_t)b * 2 * hw + hw + yx] = s1 + bias[1];
+#pragma unroll
+  for (int k = 0; k < NPIX; ++k) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      a0 = dot2(v[k][t].x, w0[t].x, a0);
+      a1 = dot2(v[k][t].x, w1[t].x, a1);
+      a2 = dot2(v[k][t].y, w0[t].y, a2);
+      a3 = dot2(v[k][t].y, w1[t].y, a3);
+      a0 = dot2(v[k][t].z, w0[t].z, a0);
+      a1 = dot2(v[k][t].z, w1[t].z, a1);
+      a2 = dot2(v[k][t].w, w0[t].w, a2);
+      a3 = dot2(v[k][t].w, w1[t].w, a3);
+    }
+    float s0 = a0 + a2, s1 = a1 + a3;
+#pragma unroll
+    for (int m = 16; m > 0; m >>= 1) {
+      s0 += __shfl_xor(s0, m, 32);
+      s1 += __shfl_xor(s1, m, 32);
+    }
+    const int64_t p = ((int64_t)blockIdx.x * NPIX + k) * 8 + (threadIdx.x >> 5);
+    if (g == 0 && p < P) {
+      const int64_t b = p / hw, yx = p - b * hw;
+      out[b * 2 * hw + yx] = s0 + bias[0];
+      out[b * 2 * hw + hw + yx] = s1 + bias[1];
+    }
   }
 }
 
 // dx[b,y,x,c] = [fm > 0] * sum_{ky,kx,o} gout[b,o,y-ky+1,x-kx+1] * W[o][c][ky][kx]
-// thread = (pixel, 8-channel group); one pixel per thread, no loop.  Per channel the two output
-// channels form one bf16 pair: s[c] += dot2((g0, g1), (W0[c], W1[c])), wd: pairs [t][c] packed
-// once per step.
+// thread = (NPIX pixels, 8-channel group); all loads issued up front as in the forward.  Per
+// channel the two output channels form one bf16 pair: s[c] += dot2((g0, g1), (W0[c], W1[c])),
+// wd: pairs [t][c] from the packing gather.
+template <int NPIX>
 __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict__ gout,
                                                         const uint32_t* __restrict__ wd,
                                                         const uint16_t* __restrict__ fm, int fs,
@@ -107,44 +121,56 @@ __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict_
                                                         int H, int W) {
   const int g = threadIdx.x & 31;
   const int64_t hw = (int64_t)H * W, P = (int64_t)B * hw;
-  const int64_t p = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
-  const int64_t pc = min(p, P - 1);
-  const int b = (int)(pc / hw);
-  const int yx = (int)(pc - (int64_t)b * hw);
-  const int y = yx / W, x = yx - y * W;
-  const float* g0 = gout + (int64_t)b * 2 * hw;
-  uint32_t gp[9];
+  uint4 wa[9], wb[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
-    const int yy = y - t / 3 + 1, xx = x - t % 3 + 1;
-    const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
-    const int64_t o = ok ? (int64_t)yy * W + xx : 0;
-    const float d0 = g0[o], d1 = g0[hw + o];
-    gp[t] = ok ? pack_bf2(d0, d1) : 0u;
+    wa[t] = *reinterpret_cast<const uint4*>(wd + t * FH_C + g * 8);
+    wb[t] = *reinterpret_cast<const uint4*>(wd + t * FH_C + g * 8 + 4);
   }
-  const uint4 m = *reinterpret_cast<const uint4*>(fm + pc * fs + g * 8);
-  float s[8];
+  uint32_t gp[NPIX][9];
+  uint4 m[NPIX];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s[i] = 0.f;
+  for (int k = 0; k < NPIX; ++k) {
+    const int64_t p = ((int64_t)blockIdx.x * NPIX + k) * 8 + (threadIdx.x >> 5);
+    const int64_t pc = min(p, P - 1);
+    const int b = (int)(pc / hw);
+    const int yx = (int)(pc - (int64_t)b * hw);
+    const int y = yx / W, x = yx - y * W;
+    const float* g0 = gout + (int64_t)b * 2 * hw;
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const uint4 wa = *reinterpret_cast<const uint4*>(wd + t * FH_C + g * 8);
-    const uint4 wb = *reinterpret_cast<const uint4*>(wd + t * FH_C + g * 8 + 4);
-    const uint32_t wv[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] = dot2(gp[t], wv[i], s[i]);
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y - t / 3 + 1, xx = x - t % 3 + 1;
+      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      const int64_t o = ok ? (int64_t)yy * W + xx : 0;
+      const float d0 = g0[o], d1 = g0[hw + o];
+      gp[k][t] = ok ? pack_bf2(d0, d1) : 0u;
+    }
+    m[k] = *reinterpret_cast<const uint4*>(fm + pc * fs + g * 8);
   }
-  const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
-  uint32_t ov[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const bool lo = (mw[q] & 0x8000u) == 0 && (mw[q] & 0x7fffu) != 0;
-    const bool hi = (mw[q] & 0x80000000u) == 0 && (mw[q] & 0x7fff0000u) != 0;
-    const uint32_t a = lo ? raft_f32_to_bf16(s[2 * q]) : 0u;
-    const uint32_t c = hi ? raft_f32_to_bf16(s[2 * q + 1]) : 0u;
-    ov[q] = a | (c << 16);
+  for (int k = 0; k < NPIX; ++k) {
+    float s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const uint32_t wv[8] = {wa[t].x, wa[t].y, wa[t].z, wa[t].w, wb[t].x, wb[t].y, wb[t].z, wb[t].w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] = dot2(gp[k][t], wv[i], s[i]);
+    }
+    const uint32_t mw[4] = {m[k].x, m[k].y, m[k].z, m[k].w};
+    uint32_t ov[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool lo = (mw[q] & 0x8000u) == 0 && (mw[q] & 0x7fffu) != 0;
+      const bool hi = (mw[q] & 0x80000000u) == 0 && (mw[q] & 0x7fff0000u) != 0;
+      const uint32_t a = lo ? raft_f32_to_bf16(s[2 * q]) : 0u;
+      const uint32_t c = hi ? raft_f32_to_bf16(s[2 * q + 1]) : 0u;
+      ov[q] = a | (c << 16);
+    }
+    const int64_t p = ((int64_t)blockIdx.x * NPIX + k) * 8 + (threadIdx.x >> 5);
+    if (p < P) *reinterpret_cast<uint4*>(dx + p * ds + g * 8) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
   }
-  if (p < P) *reinterpret_cast<uint4*>(dx + p * ds + g * 8) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
 }
 
 // dw[o][t*256 + c] += sum_items sum_p gout[p][o] * in[p + off_t][c];  db[o] += sum gout[p][o]
@@ -171,9 +197,10 @@ __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int
     if (y >= H) continue;
     const uint16_t* in = it.in[item] + (int64_t)b * hw * cs + g * 8;
     const float* go = it.gout[item] + (int64_t)b * 2 * hw + (int64_t)y * W;
-    // window columns (xb-1 .. xb+4) of rows (y-1, y, y+1) for a block of 4 output pixels xb..xb+3:
-    // the 12 loads of a block's new columns are issued together (one round trip per 4 pixels)
-    uint4 win[3][6];
+    // window columns (xb-1 .. xb+XB) of rows (y-1, y, y+1) for a block of XB output pixels: the
+    // 3*XB loads of a block's new columns are issued together (one round trip per XB pixels)
+    constexpr int XB = 2;
+    uint4 win[3][XB + 2];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
       win[r][0] = make_uint4(0, 0, 0, 0);  // column -1: zero padding
@@ -181,12 +208,12 @@ __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int
       win[r][1] = (yy >= 0 && yy < H) ? *reinterpret_cast<const uint4*>(in + ((int64_t)yy * W) * cs)
                                       : make_uint4(0, 0, 0, 0);
     }
-    for (int xb = 0; xb < W; xb += 4) {
+    for (int xb = 0; xb < W; xb += XB) {
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int yy = y + r - 1;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < XB; ++j) {
           const int xx = xb + 1 + j;
           win[r][2 + j] = (yy >= 0 && yy < H && xx < W)
                               ? *reinterpret_cast<const uint4*>(in + ((int64_t)yy * W + xx) * cs)
@@ -194,7 +221,7 @@ __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int
         }
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < XB; ++j) {
         const int x = xb + j;
         const bool ok = x < W;
         const float d0 = ok ? go[x] : 0.f, d1 = ok ? go[hw + x] : 0.f;
@@ -215,8 +242,8 @@ __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int
       }
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
-        win[r][0] = win[r][4];
-        win[r][1] = win[r][5];
+        win[r][0] = win[r][XB];
+        win[r][1] = win[r][XB + 1];
       }
     }
   }
@@ -262,7 +289,7 @@ bool launch_fh2_fwd(const uint16_t* in, int cs, const uint32_t* wf, const float*
                     int B, int H, int W, hipStream_t stream) {
   if (cs % 8 != 0 || cs < FH_C) return false;
   const int64_t P = (int64_t)B * H * W;
-  hipLaunchKernelGGL(fh2_fwd_kernel, dim3(raft_cdiv(P, 8)), dim3(256), 0, stream, in, cs, wf, bias, out,
+  hipLaunchKernelGGL(fh2_fwd_kernel<2>, dim3(raft_cdiv(P, 16)), dim3(256), 0, stream, in, cs, wf, bias, out,
                      B, H, W);
   return true;
 }
@@ -271,7 +298,7 @@ bool launch_fh2_dgrad(const float* gout, const uint32_t* wd, const uint16_t* fm,
                       int ds, int B, int H, int W, hipStream_t stream) {
   if (fs % 8 != 0 || ds % 8 != 0 || fs < FH_C || ds < FH_C) return false;
   const int64_t P = (int64_t)B * H * W;
-  hipLaunchKernelGGL(fh2_dgrad_kernel, dim3(raft_cdiv(P, 8)), dim3(256), 0, stream, gout, wd, fm, fs,
+  hipLaunchKernelGGL(fh2_dgrad_kernel<4>, dim3(raft_cdiv(P, 32)), dim3(256), 0, stream, gout, wd, fm, fs,
                      dx, ds, B, H, W);
   return true;
 }
