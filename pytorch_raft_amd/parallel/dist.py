@@ -68,7 +68,10 @@ def init_distributed(backend=None, device=None, timeout_s=1800):
         torch.cuda.set_device(device)
     if ws > 1 and not is_dist():
         if backend is None:
-            backend = 'nccl' if device.type == 'cuda' else 'gloo'
+            # RAFT_DIST_BACKEND=gloo: rehearse the multi-rank GPU path with several ranks on ONE
+            # GPU (RCCL refuses two ranks per device); gloo reduces CUDA tensors via the host
+            backend = os.environ.get('RAFT_DIST_BACKEND') or \
+                ('nccl' if device.type == 'cuda' else 'gloo')
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         os.environ.setdefault('MASTER_PORT', '29511')
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))

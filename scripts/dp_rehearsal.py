@@ -1,0 +1,63 @@
+"""Multi-rank rehearsal of the data-parallel training path on ONE GPU.
+
+    RAFT_DIST_BACKEND=gloo python -m torch.distributed.run --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29561 scripts/dp_rehearsal.py
+
+Every rank runs the fused HIP training path on cuda:0 with its half of a batch; GradSync
+all-reduces the gradients (bucketed, side stream, post-accumulate-grad hooks).  Rank 0 then
+recomputes the full-batch gradient in a single process and checks that the averaged DP gradient
+matches it (BatchNorm frozen, as in every stage after chairs, so per-replica batch statistics do
+not enter).  RCCL refuses two ranks on one device, hence gloo (which reduces CUDA tensors through
+the host); the launch, hook, bucket and stream logic is the code the 8-GPU RCCL run executes.
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from pytorch_raft_amd import RAFT  # noqa: E402
+from pytorch_raft_amd.data.synthetic import make_pair_batch  # noqa: E402
+from pytorch_raft_amd.engine.trainer import TrainState  # noqa: E402
+from pytorch_raft_amd.parallel import dist as pdist  # noqa: E402
+
+
+def main():
+    dev = pdist.init_distributed()
+    rank, world = pdist.rank(), pdist.world_size()
+    args = argparse.Namespace(small=False, mixed_precision=True, corr_impl='hip', lr=4e-4,
+                              wdecay=1e-4, epsilon=1e-8, num_steps=100, iters=4, gamma=0.8,
+                              clip=1.0, add_noise=False, bucket_mb=2.0)
+    torch.manual_seed(0)
+    model = RAFT(args).to(dev).train()
+    model.freeze_bn()
+    pdist.broadcast_module(model)
+    i1, i2, flow, valid = make_pair_batch(2 * world, 128, 160, device=dev)
+    sl = slice(2 * rank, 2 * rank + 2)
+    st = TrainState(model, args, dev)
+    assert st.sync is not None and st.sync.enabled
+    st.optimizer.zero_grad(set_to_none=True)
+    st.sync.prepare()
+    loss, _ = st.forward_backward(i1[sl], i2[sl], flow[sl], valid[sl])
+    st.sync.finish()
+    g_dp = torch.cat([p.grad.reshape(-1).float() for p in model.parameters()])
+    if rank == 0:
+        torch.manual_seed(0)
+        ref = RAFT(argparse.Namespace(**vars(args))).to(dev).train()
+        ref.freeze_bn()
+        ref.load_state_dict(model.state_dict())
+        st1 = TrainState(ref, args, dev, sync=False)
+        st1.forward_backward(i1, i2, flow, valid)
+        g_full = torch.cat([p.grad.reshape(-1).float() for p in ref.parameters()])
+        rel = ((g_dp - g_full).norm() / g_full.norm()).item()
+        print('dp rehearsal: world=%d backend=%s buckets=%d rel_grad_err=%.3e loss=%.4f' %
+              (world, torch.distributed.get_backend(), len(st.sync.buckets), rel, loss.item()),
+              flush=True)
+        assert rel < 2e-2, rel
+    pdist.barrier(dev)
+    pdist.destroy()
+
+
+if __name__ == '__main__':
+    main()
