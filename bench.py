@@ -171,8 +171,12 @@ def main(argv=None):
     ok = st.check_finite()
     pairs = a.batch * world * a.steps
     value = pairs / elapsed
+    metric = METRIC
+    if (h, w) != (368, 496) or a.iters != 12 or a.small:
+        metric = 'training image-pairs/sec (whole node), RAFT%s %dx%d iters=%d, at %d MI355X' % (
+            '-small' if a.small else '', h, w, a.iters, world)
     res = {
-        'metric': METRIC,
+        'metric': metric,
         'value': round(value, 3),
         'unit': 'image-pairs/s',
         'n_gpus': world,
@@ -183,7 +187,7 @@ def main(argv=None):
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': a.precision,
-        'data': 'synthetic (random smooth texture pairs, 368x496, generated on device; random-init weights)',
+        'data': 'synthetic (random smooth texture pairs, %dx%d, generated on device; random-init weights)' % (h, w),
         'config': {
             'model': 'RAFT-small' if a.small else 'RAFT (full, 5.26M params)',
             'global_batch': a.batch * world,
