@@ -269,21 +269,48 @@ __global__ __launch_bounds__(256) void corr_window_reduce_kernel(WinList wl_, in
     }
   }
   for (int e = threadIdx.x; e < tot; e += 256) planes[e] = 0.f;
-  __syncthreads();
-  for (int k = 0; k < wl_.n; ++k) {
-    const float* C = wl_.coords[k];
-    const float* G = wl_.wg[k] + ((int64_t)b * N + i) * levels * E * E;
-    const float x = C[((int64_t)b * 2) * N + i], y = C[((int64_t)b * 2 + 1) * N + i];
-    for (int e = threadIdx.x; e < levels * E * E; e += 256) {
-      const int l = e / (E * E), yy = (e / E) % E, xx = e % E;
-      const float inv = 1.0f / (float)(1 << l);
-      const int xs = (int)floorf(clampc(x * inv)) - R, ys = (int)floorf(clampc(y * inv)) - R;
-      const int gy = ys + yy, gx = xs + xx;
-      if (gy >= 0 && gy < hs[l] && gx >= 0 && gx < ws[l])
-        planes[off[l] + gy * ws[l] + gx] += G[e];
+  // iterations are folded in a fixed order (deterministic), KC at a time: all of a chunk's
+  // coordinate and patch loads are issued before its first LDS add, so a workgroup waits for
+  // one memory round trip per chunk instead of one per iteration
+  constexpr int KC = 6;
+  constexpr int CPT = (4 * E * E + 255) / 256;  // window cells per thread (all levels)
+  const int cells = levels * E * E;
+  for (int k0 = 0; k0 < wl_.n; k0 += KC) {
+    float gv[KC][CPT];
+    int pos[KC][CPT];
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk) {
+      const int k = k0 + kk;
+      const bool kok = k < wl_.n;
+      const float* C = wl_.coords[kok ? k : 0];
+      const float* G = wl_.wg[kok ? k : 0] + ((int64_t)b * N + i) * levels * E * E;
+      const float x = C[((int64_t)b * 2) * N + i], y = C[((int64_t)b * 2 + 1) * N + i];
+#pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        const int e = threadIdx.x + q * 256;
+        pos[kk][q] = -1;
+        gv[kk][q] = 0.f;
+        if (kok && e < cells) {
+          const int l = e / (E * E), yy = (e / E) % E, xx = e % E;
+          const float inv = 1.0f / (float)(1 << l);
+          const int xs = (int)floorf(clampc(x * inv)) - R, ys = (int)floorf(clampc(y * inv)) - R;
+          const int gy = ys + yy, gx = xs + xx;
+          if (gy >= 0 && gy < hs[l] && gx >= 0 && gx < ws[l]) {
+            pos[kk][q] = off[l] + gy * ws[l] + gx;
+            gv[kk][q] = G[e];
+          }
+        }
+      }
     }
-    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk) {
+      __syncthreads();  // previous adds (and the zero fill) visible; one writer per cell per round
+#pragma unroll
+      for (int q = 0; q < CPT; ++q)
+        if (pos[kk][q] >= 0) planes[pos[kk][q]] += gv[kk][q];
+    }
   }
+  __syncthreads();
   float* O = (float*)out + ((int64_t)b * N + i) * N;
   uint16_t* Ob = (uint16_t*)out + ((int64_t)b * N + i) * N;
   for (int e = threadIdx.x; e < N; e += 256) {
