@@ -39,8 +39,6 @@ def parse(argv=None):
     ap.add_argument('--alternate_corr', action='store_true')
     ap.add_argument('--channels_last', action='store_true')
     ap.add_argument('--small', action='store_true')
-    ap.add_argument('--miopen_deterministic', action='store_true',
-                    help='torch.backends.cudnn.deterministic (MIOpen solvers without atomics)')
     ap.add_argument('--hipgraph', action='store_true',
                     help='capture forward+backward and the update as hipGraphs (measured slower than '
                          'the eager fused path on ROCm 7.0 torch; kept as an option)')
@@ -87,8 +85,6 @@ def main(argv=None):
     rank = pdist.rank()
     torch.manual_seed(1234 + rank)
     torch.backends.cudnn.benchmark = True
-    if a.miopen_deterministic:
-        torch.backends.cudnn.deterministic = True
 
     margs = argparse.Namespace(
         small=a.small, mixed_precision=a.precision != 'fp32',
