@@ -1029,6 +1029,41 @@ void flow_prep_(const Tensor& flow, const Tensor& flowb, const c10::optional<Ten
   launch_flow_prep(flow.data_ptr<float>(), bf16m(flowb), sp, ss, (int)B, (int)(H * W), cur_stream());
 }
 
+// dcorr level 0 (B, N, N) straight from the iterations' bf16 lookup-output gradients
+Tensor corr_tap_reduce(const std::vector<Tensor>& coords, const std::vector<Tensor>& douts,
+                       int64_t H, int64_t W, int64_t levels, int64_t radius, double inv_sqrt_c,
+                       bool out_bf16) {
+  TORCH_CHECK(!coords.empty() && coords.size() == douts.size() && coords.size() <= RAFT_MAX_WIN,
+              "1..", RAFT_MAX_WIN, " iterations");
+  TORCH_CHECK(radius == 3 || radius == 4, "radius must be 3 or 4");
+  TORCH_CHECK(levels >= 1 && levels <= 4, "1..4 levels");
+  const int64_t B = coords[0].size(0), N = H * W;
+  const int64_t D = 2 * radius + 1;
+  const int64_t cbuf = douts[0].size(-1);
+  TapList tl{};
+  for (size_t k = 0; k < coords.size(); ++k) {
+    check_cuda_f32(coords[k], "coords");
+    TORCH_CHECK(coords[k].dim() == 4 && coords[k].size(0) == B && coords[k].size(1) == 2 &&
+                    coords[k].size(2) == H && coords[k].size(3) == W,
+                "coords shape");
+    check_nhwc(douts[k], B, H, W, "tap gradient", at::kBFloat16);
+    TORCH_CHECK(douts[k].size(3) == cbuf && cbuf % 8 == 0 && cbuf >= levels * D * D,
+                "tap gradient rows must share a width >= levels*(2r+1)^2, multiple of 8");
+    tl.coords[k] = coords[k].data_ptr<float>();
+    tl.dout[k] = bf16p(douts[k]);
+  }
+  tl.n = (int)coords.size();
+  tl.cbuf = (int)cbuf;
+  const int lds = corr_tap_reduce_lds_bytes((int)H, (int)W, (int)levels, (int)radius);
+  TORCH_CHECK(lds <= 64 * 1024, "feature map too large for the LDS plane reduction");
+  c10::DeviceGuard g(coords[0].device());
+  Tensor out = at::empty({B, N, N}, coords[0].options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  TORCH_CHECK(launch_corr_tap_reduce(tl, (int)levels, (int)B, (int)H, (int)W, (int)radius,
+                                     (float)inv_sqrt_c, out.data_ptr(), out_bf16 ? 1 : 0, cur_stream()),
+              "unsupported radius / levels");
+  return out;
+}
+
 // ------------------------------------------------------------------ flow_head.conv2 (256 -> 2)
 // Weights arrive as bf16 pair tables built by the update block's packing gather:
 // wf = W[o][c][t] as [t][o][c] (2304 bf16), wd = W[o][c][t] as [t][c][o] (4608 bf16).
@@ -1152,6 +1187,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("conv_fwd_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, Tensor? bias, int kh, int kw, int ph, int pw, int cout, int cin_small, int epi, int bn, float scale, int split, Tensor(a!)[] outs, int[] out_off, Tensor[] aux, int[] aux_off) -> ()");
   m.def("conv_wgrad_multi_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
   m.def("f1_patch_(Tensor flow, Tensor(a!) patch, Tensor(b!)? slot, int slot_off) -> ()");
+  m.def("corr_tap_reduce(Tensor[] coords, Tensor[] douts, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16) -> Tensor");
   m.def("fh2_fwd_(Tensor inp, Tensor wf, Tensor b, Tensor(a!) out) -> ()");
   m.def("fh2_dgrad_(Tensor gout, Tensor wd, Tensor fm, Tensor(a!) dx) -> ()");
   m.def("fh2_wgrad_(Tensor[] gouts, Tensor[] ins, Tensor(a!) part) -> ()");
@@ -1169,6 +1205,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("norm_fwd_", &norm_fwd_);
   m.impl("norm_bwd_", &norm_bwd_);
   m.impl("f1_patch_", &f1_patch_);
+  m.impl("corr_tap_reduce", &corr_tap_reduce);
   m.impl("fh2_fwd_", &fh2_fwd_);
   m.impl("fh2_dgrad_", &fh2_dgrad_);
   m.impl("fh2_wgrad_", &fh2_wgrad_);

@@ -327,6 +327,105 @@ __global__ __launch_bounds__(256) void corr_window_reduce_kernel(WinList wl_, in
   }
 }
 
+// Fold straight from the lookup's tap gradients (no per-iteration compact window pass): the
+// workgroup of query pixel (b, i) stages, KC iterations at a time, the pixel's bf16 tap-gradient
+// rows (levels*(2r+1)^2 taps of the (B,H,W,cbuf) lookup-output gradient; 16-B loads, all issued
+// before use) in LDS, then every thread forms its window cells' bilinear adjoint (the same
+// arithmetic as corr_window_grad_kernel) and adds it into the level planes -- iterations in a
+// fixed order, one writer per cell per round (deterministic; bitwise the two-pass result).  Reads
+// ~0.77 KB per pixel-iteration instead of writing and re-reading a 1.6 KB fp32 window.
+template <int R>
+__global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int levels, int B, int H,
+                                                              int W, float inv_sqrt_c,
+                                                              void* __restrict__ out, int out_bf16) {
+  constexpr int D = 2 * R + 1, E = D + 1;
+  constexpr int KC = 6;
+  constexpr int CPT = (4 * E * E + 255) / 256;
+  extern __shared__ float planes[];
+  const int N = H * W;
+  const int b = blockIdx.x / N, i = blockIdx.x % N;
+  int hs[4], ws[4], off[4];
+  int tot = 0;
+  {
+    int h = H, w = W;
+    for (int l = 0; l < 4; ++l) {
+      hs[l] = h; ws[l] = w; off[l] = tot;
+      if (l < levels) tot += h * w;
+      h >>= 1; w >>= 1;
+    }
+  }
+  const int ctot = levels * D * D;
+  const int chunks = (ctot + 7) / 8;                    // 16-B pieces of one tap row
+  const int trow = chunks * 8;                          // bf16 per staged row
+  uint16_t* taps = reinterpret_cast<uint16_t*>(planes + ((tot + 3) & ~3));
+  for (int e = threadIdx.x; e < tot; e += 256) planes[e] = 0.f;
+  const int cells = levels * E * E;
+  for (int k0 = 0; k0 < tl.n; k0 += KC) {
+    const int kn = min(KC, tl.n - k0);
+    // one 16-B piece per thread: (kk, ch)
+    uint4 piece = make_uint4(0, 0, 0, 0);
+    const int kk_ld = threadIdx.x / chunks, ch = threadIdx.x % chunks;
+    const bool ld = kk_ld < kn;
+    if (ld)
+      piece = *reinterpret_cast<const uint4*>(tl.dout[k0 + kk_ld] + ((int64_t)b * N + i) * tl.cbuf + ch * 8);
+    float cx[KC], cy[KC];
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk) {
+      const float* C = tl.coords[k0 + (kk < kn ? kk : 0)];
+      cx[kk] = C[((int64_t)b * 2) * N + i];
+      cy[kk] = C[((int64_t)b * 2 + 1) * N + i];
+    }
+    __syncthreads();  // previous chunk's tap reads and plane adds done
+    if (ld) *reinterpret_cast<uint4*>(taps + kk_ld * trow + ch * 8) = piece;
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk) {
+      __syncthreads();  // staged taps + previous round's adds visible
+      if (kk >= kn) continue;
+      const uint16_t* T0 = taps + kk * trow;
+#pragma unroll
+      for (int q = 0; q < CPT; ++q) {
+        const int e = threadIdx.x + q * 256;
+        if (e >= cells) continue;
+        const int l = e / (E * E), yy = (e / E) % E, xx = e % E;
+        const float inv = 1.0f / (float)(1 << l);
+        const float fxc = clampc(cx[kk] * inv), fyc = clampc(cy[kk] * inv);
+        const float flx = floorf(fxc), fly = floorf(fyc);
+        const int gy = (int)fly - R + yy, gx = (int)flx - R + xx;
+        if (gy < 0 || gy >= hs[l] || gx < 0 || gx >= ws[l]) continue;
+        const float ax = fxc - flx, ay = fyc - fly;
+        const uint16_t* T = T0 + l * D * D;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int iy = yy - k;
+          if (iy < 0 || iy >= D) continue;
+          const float wy = k == 0 ? (1.f - ay) : ay;
+          float sx = 0.f;
+          if (xx < D) sx += (1.f - ax) * raft_bf16_to_f32(T[xx * D + iy]);
+          if (xx > 0) sx += ax * raft_bf16_to_f32(T[(xx - 1) * D + iy]);
+          acc += wy * sx;
+        }
+        planes[off[l] + gy * ws[l] + gx] += acc;
+      }
+    }
+  }
+  __syncthreads();
+  float* O = (float*)out + ((int64_t)b * N + i) * N;
+  uint16_t* Ob = (uint16_t*)out + ((int64_t)b * N + i) * N;
+  for (int e = threadIdx.x; e < N; e += 256) {
+    const int y = e / W, x = e % W;
+    float v = planes[e];
+    float s = 0.25f;
+    for (int l = 1; l < levels; ++l) {
+      const int yl = y >> l, xl = x >> l;
+      if (yl < hs[l] && xl < ws[l]) v += s * planes[off[l] + yl * ws[l] + xl];
+      s *= 0.25f;
+    }
+    if (out_bf16) Ob[e] = raft_f32_to_bf16(v * inv_sqrt_c);
+    else O[e] = v * inv_sqrt_c;
+  }
+}
+
 }  // namespace
 
 bool launch_corr_lookup_tile(const float* const* lvl, const int* hs, const int* ws, int levels,
@@ -379,6 +478,26 @@ bool launch_corr_window_reduce(const WinList& wl, int levels, int B, int H, int 
   dim3 grid((unsigned)(B * H * W));
   if (radius == 4) hipLaunchKernelGGL(corr_window_reduce_kernel<4>, grid, dim3(256), lds, stream, wl, levels, B, H, W, inv_sqrt_c, out, out_bf16);
   else if (radius == 3) hipLaunchKernelGGL(corr_window_reduce_kernel<3>, grid, dim3(256), lds, stream, wl, levels, B, H, W, inv_sqrt_c, out, out_bf16);
+  else return false;
+  return true;
+}
+
+int corr_tap_reduce_lds_bytes(int H, int W, int levels, int radius) {
+  int tot = 0, h = H, w = W;
+  for (int l = 0; l < levels; ++l) { tot += h * w; h >>= 1; w >>= 1; }
+  const int D = 2 * radius + 1;
+  const int trow = (levels * D * D + 7) / 8 * 8;
+  return ((tot + 3) & ~3) * 4 + 6 * trow * 2;
+}
+
+bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, int radius,
+                            float inv_sqrt_c, void* out, int out_bf16, hipStream_t stream) {
+  const int D = 2 * radius + 1;
+  if ((levels * D * D + 7) / 8 * 6 > 256) return false;  // one 16-B piece per thread per chunk
+  const int lds = corr_tap_reduce_lds_bytes(H, W, levels, radius);
+  dim3 grid((unsigned)(B * H * W));
+  if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_kernel<4>, grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16);
+  else if (radius == 3) hipLaunchKernelGGL(corr_tap_reduce_kernel<3>, grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16);
   else return false;
   return true;
 }

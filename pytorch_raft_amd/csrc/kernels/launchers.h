@@ -209,6 +209,15 @@ bool launch_corr_lookup_tile(const float* const* lvl, const int* hs, const int* 
                              int radius, hipStream_t stream);
 bool launch_corr_window_grad(const float* coords, const uint16_t* dout, int cbuf, float* wg, int B,
                              int H, int W, int levels, int radius, hipStream_t stream);
+struct TapList {
+  const float* coords[RAFT_MAX_WIN];   // (B,2,H,W) per iteration
+  const uint16_t* dout[RAFT_MAX_WIN];  // (B,H,W,cbuf) bf16 lookup-output gradient per iteration
+  int cbuf;
+  int n;
+};
+int corr_tap_reduce_lds_bytes(int H, int W, int levels, int radius);
+bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, int radius,
+                            float inv_sqrt_c, void* out, int out_bf16, hipStream_t stream);
 int corr_window_reduce_lds_bytes(int H, int W, int levels);
 // out: (B, N, N) fp32, or bf16 when out_bf16 (mixed-precision backward GEMMs)
 bool launch_corr_window_reduce(const WinList& wl, int levels, int B, int H, int W, int radius,

@@ -34,6 +34,7 @@ class _State:
         self.grad = None
         self.grad_f1 = None
         self.windows = []
+        self.taps = []       # (coords, bf16 NHWC lookup-output gradient) per iteration
         self.radius = None
         self.bf16_bwd = False
 
@@ -53,13 +54,13 @@ class _AllPairsBuild(torch.autograd.Function):
     def backward(ctx, _dtoken):
         st = ctx.state
         fmap1, fmap2 = ctx.saved_tensors
-        if st.grad is None and not st.windows:
+        if st.grad is None and not st.windows and not st.taps:
             return None, None, None, None
         b, c, h, w = fmap1.shape
         dcorr = None
         # mixed precision, window path only: dcorr in bf16 and bf16 GEMMs (fp32 accumulation);
         # the fmaps are bf16 encoder outputs, so only the dcorr rounding differs from fp32
-        bf16 = st.bf16_bwd and st.grad is None and bool(st.windows)
+        bf16 = st.bf16_bwd and st.grad is None and bool(st.windows or st.taps)
         if st.grad is not None:
             dcorr = _ext.ops().corr_pyr_grad_reduce(st.grad, 1.0 / math.sqrt(c))  # (B, N, N)
         if st.windows:
@@ -67,8 +68,14 @@ class _AllPairsBuild(torch.autograd.Function):
                                                h, w, len(st.pyramid), st.radius, 1.0 / math.sqrt(c),
                                                bf16)
             dcorr = dw if dcorr is None else dcorr + dw
+        if st.taps:
+            dt = _ext.ops().corr_tap_reduce([x[0] for x in st.taps], [x[1] for x in st.taps],
+                                            h, w, len(st.pyramid), st.radius, 1.0 / math.sqrt(c),
+                                            bf16)
+            dcorr = dt if dcorr is None else dcorr + dt
         st.grad = None
         st.windows = []
+        st.taps = []
         st.pyramid = None
         f1 = fmap1.view(b, c, h * w)
         f2 = fmap2.view(b, c, h * w)
@@ -121,11 +128,10 @@ class _AllPairsLookupNHWC(torch.autograd.Function):
         (coords,) = ctx.saved_tensors
         b, _, h, w = coords.shape
         levels = len(st.pyramid)
-        if _window_reduce_fits(h, w, levels) and len(st.windows) < 32:
-            # compact per-iteration window gradient; folded into dcorr once per step
-            wg = _ext.ops().corr_window_grad(coords, dout.to(torch.bfloat16).contiguous(), levels,
-                                             ctx.radius)
-            st.windows.append((coords, wg))
+        if _window_reduce_fits(h, w, levels) and len(st.taps) < 32 and dout.shape[-1] % 8 == 0:
+            # keep the iteration's bf16 tap gradient; all iterations are folded into dcorr once
+            # per step straight from these rows (corr_tap_reduce)
+            st.taps.append((coords, dout.to(torch.bfloat16).contiguous()))
             st.radius = ctx.radius
         else:
             if st.grad is None:

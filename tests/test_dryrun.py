@@ -50,12 +50,17 @@ def _returns():
         b, _, h, w = coords.shape
         return torch.zeros(b, h * w, levels, 2 * r + 2, 2 * r + 2)
 
+    def tap_reduce(coords, douts, h, w, levels, r, s, bf16=False):
+        return torch.zeros(coords[0].shape[0], h * w, h * w,
+                           dtype=torch.bfloat16 if bf16 else torch.float32)
+
     def win_reduce(coords, wgs, h, w, levels, r, s, bf16=False):
         return torch.zeros(coords[0].shape[0], h * w, h * w,
                            dtype=torch.bfloat16 if bf16 else torch.float32)
 
     return {'corr_build': corr_build, 'corr_lookup_fwd': lookup, 'corr_pyr_grad_reduce': reduce,
             'corr_window_grad': win_grad, 'corr_window_reduce': win_reduce,
+            'corr_tap_reduce': tap_reduce,
             'convex_up_fwd': cup_fwd, 'convex_up_bwd': cup_bwd, 'seq_loss_fwd': loss_fwd,
             'seq_loss_bwd': loss_bwd}
 
@@ -79,7 +84,7 @@ def test_dry_run_fused_training_step(alternate):
             'relu_bwd_', 'f1_patch_', 'fh2_fwd_', 'fh2_dgrad_', 'fh2_wgrad_', 'convex_up_fwd',
             'convex_up_bwd', 'seq_loss_fwd'} <= names, names
     if not alternate:
-        assert {'corr_build', 'corr_lookup_nhwc_', 'corr_window_grad', 'corr_window_reduce'} <= names
+        assert {'corr_build', 'corr_lookup_nhwc_', 'corr_tap_reduce'} <= names
     else:
         assert {'corr_otf_fwd_', 'corr_window_grad', 'corr_otf_window_bwd_'} <= names
     # every update-block parameter received a gradient through the fused backward

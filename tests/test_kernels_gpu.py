@@ -249,3 +249,21 @@ def test_convex_upsample_nhwc(ext_ops, hw):
     (out.float() * g).sum().backward()
     torch.testing.assert_close(flow.grad, gf_ref, atol=1e-3, rtol=1e-4)
     torch.testing.assert_close(mask.grad.float(), gm_ref, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize('radius,levels,hw', [(4, 4, (46, 62)), (3, 4, (24, 31)), (4, 3, (13, 19))])
+def test_tap_reduce_matches_window_path(ext_ops, radius, levels, hw):
+    """One-pass fold from the bf16 tap gradients == per-iteration compact windows + fold."""
+    h, w = hw
+    b = 2
+    D = 2 * radius + 1
+    coords = [_coords(b, h, w, seed=s) for s in range(7)]      # > one 6-iteration chunk
+    douts = [torch.randn(b, h, w, 384, device=DEV).to(torch.bfloat16) for _ in coords]
+    s = 1.0 / 16
+    wgs = [ext_ops.corr_window_grad(c, g, levels, radius) for c, g in zip(coords, douts)]
+    ref = ext_ops.corr_window_reduce(coords, wgs, h, w, levels, radius, s, False)
+    got = ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, False)
+    assert levels * D * D <= 384
+    torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-5)
+    got16 = ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, True)
+    torch.testing.assert_close(got16.float(), ref, atol=1e-2, rtol=1e-2)
