@@ -410,19 +410,30 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
     }
   }
   __syncthreads();
-  float* O = (float*)out + ((int64_t)b * N + i) * N;
-  uint16_t* Ob = (uint16_t*)out + ((int64_t)b * N + i) * N;
-  for (int e = threadIdx.x; e < N; e += 256) {
-    const int y = e / W, x = e % W;
+  // level-0 gradient row with the avg-pool adjoint of the coarser levels; two columns per thread
+  // (4-B stores of bf16 pairs when the row is 4-B aligned, i.e. N even)
+  const int64_t row = ((int64_t)b * N + i) * N;
+  auto cell = [&](int e) {
+    const int y = e / W, x = e - (e / W) * W;
     float v = planes[e];
-    float s = 0.25f;
+    float sc = 0.25f;
     for (int l = 1; l < levels; ++l) {
       const int yl = y >> l, xl = x >> l;
-      if (yl < hs[l] && xl < ws[l]) v += s * planes[off[l] + yl * ws[l] + xl];
-      s *= 0.25f;
+      if (yl < hs[l] && xl < ws[l]) v += sc * planes[off[l] + yl * ws[l] + xl];
+      sc *= 0.25f;
     }
-    if (out_bf16) Ob[e] = raft_f32_to_bf16(v * inv_sqrt_c);
-    else O[e] = v * inv_sqrt_c;
+    return v * inv_sqrt_c;
+  };
+  if (out_bf16 && (N & 1) == 0) {
+    uint32_t* Ob = reinterpret_cast<uint32_t*>((uint16_t*)out + row);
+    for (int e2 = threadIdx.x; e2 < N / 2; e2 += 256)
+      Ob[e2] = (uint32_t)raft_f32_to_bf16(cell(2 * e2)) | ((uint32_t)raft_f32_to_bf16(cell(2 * e2 + 1)) << 16);
+  } else if (out_bf16) {
+    uint16_t* Ob = (uint16_t*)out + row;
+    for (int e = threadIdx.x; e < N; e += 256) Ob[e] = raft_f32_to_bf16(cell(e));
+  } else {
+    float* O = (float*)out + row;
+    for (int e = threadIdx.x; e < N; e += 256) O[e] = cell(e);
   }
 }
 
