@@ -360,6 +360,17 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
   uint16_t* taps = reinterpret_cast<uint16_t*>(planes + ((tot + 3) & ~3));
   for (int e = threadIdx.x; e < tot; e += 256) planes[e] = 0.f;
   const int cells = levels * E * E;
+  // this thread's window cells: (level, row, column) decoded once, not per iteration
+  int cl[CPT], cyy[CPT], cxx[CPT];
+  float cinv[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    const int e = threadIdx.x + q * 256;
+    cl[q] = e < cells ? e / (E * E) : -1;
+    cyy[q] = (e / E) % E;
+    cxx[q] = e % E;
+    cinv[q] = cl[q] >= 0 ? 1.0f / (float)(1 << cl[q]) : 0.f;
+  }
   for (int k0 = 0; k0 < tl.n; k0 += KC) {
     const int kn = min(KC, tl.n - k0);
     // one 16-B piece per thread: (kk, ch)
@@ -384,11 +395,10 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
       const uint16_t* T0 = taps + kk * trow;
 #pragma unroll
       for (int q = 0; q < CPT; ++q) {
-        const int e = threadIdx.x + q * 256;
-        if (e >= cells) continue;
-        const int l = e / (E * E), yy = (e / E) % E, xx = e % E;
-        const float inv = 1.0f / (float)(1 << l);
-        const float fxc = clampc(cx[kk] * inv), fyc = clampc(cy[kk] * inv);
+        const int l = cl[q];
+        if (l < 0) continue;
+        const int yy = cyy[q], xx = cxx[q];
+        const float fxc = clampc(cx[kk] * cinv[q]), fyc = clampc(cy[kk] * cinv[q]);
         const float flx = floorf(fxc), fly = floorf(fyc);
         const int gy = (int)fly - R + yy, gx = (int)flx - R + xx;
         if (gy < 0 || gy >= hs[l] || gx < 0 || gx >= ws[l]) continue;
@@ -413,8 +423,9 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
   // level-0 gradient row with the avg-pool adjoint of the coarser levels; two columns per thread
   // (4-B stores of bf16 pairs when the row is 4-B aligned, i.e. N even)
   const int64_t row = ((int64_t)b * N + i) * N;
+  const float inv_w = 1.0f / (float)W;
   auto cell = [&](int e) {
-    const int y = e / W, x = e - (e / W) * W;
+    const int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W;  // exact for e < 2^22
     float v = planes[e];
     float sc = 0.25f;
     for (int l = 1; l < levels; ++l) {
