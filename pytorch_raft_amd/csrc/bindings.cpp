@@ -893,15 +893,15 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
 }
 
 // dx (bf16) and += parameter grads; y = the forward output when relu (mask), else ignored
-void norm_bwd_(const Tensor& dy, const Tensor& y, const Tensor& x, const Tensor& mean,
-               const Tensor& invstd, int64_t mode, int64_t relu, const c10::optional<Tensor>& gamma,
-               const c10::optional<Tensor>& dgamma, const c10::optional<Tensor>& dbeta,
-               const c10::optional<Tensor>& dcbias, const Tensor& dx) {
+void norm_bwd_(const Tensor& dy, const Tensor& x, const Tensor& mean, const Tensor& invstd,
+               int64_t mode, int64_t relu, const c10::optional<Tensor>& gamma,
+               const c10::optional<Tensor>& beta, const c10::optional<Tensor>& dgamma,
+               const c10::optional<Tensor>& dbeta, const c10::optional<Tensor>& dcbias,
+               const Tensor& dx) {
   check_cl_bf16(dy, "dy");
-  check_cl_bf16(y, "y");
   check_cl_bf16(x, "x");
   check_cl_bf16(dx, "dx");
-  TORCH_CHECK(dy.sizes() == x.sizes() && y.sizes() == x.sizes() && dx.sizes() == x.sizes(), "shapes");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dx.sizes() == x.sizes(), "shapes");
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   const int groups = mode == 0 ? (int)N : 1;
   check_cuda_f32(mean, "mean");
@@ -909,6 +909,7 @@ void norm_bwd_(const Tensor& dy, const Tensor& y, const Tensor& x, const Tensor&
   TORCH_CHECK(mean.numel() == groups * C && invstd.numel() == groups * C, "stat shapes");
   c10::DeviceGuard g(x.device());
   const float* gp = opt_f32(gamma, C, "gamma");
+  const float* bp = opt_f32(beta, C, "beta");
   float* dg = const_cast<float*>(opt_f32(dgamma, C, "dgamma"));
   float* db = const_cast<float*>(opt_f32(dbeta, C, "dbeta"));
   float* dc = const_cast<float*>(opt_f32(dcbias, C, "dcbias"));
@@ -918,9 +919,8 @@ void norm_bwd_(const Tensor& dy, const Tensor& y, const Tensor& x, const Tensor&
   Tensor part = at::empty({groups * (nblk + 1) * 3 * C}, fo);  // partials + per-group sums
   Tensor coef = at::empty({groups, C, 3}, fo);
   launch_norm_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr<at::BFloat16>()),
-                  reinterpret_cast<const uint16_t*>(y.data_ptr<at::BFloat16>()),
                   reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>()), mean.data_ptr<float>(),
-                  invstd.data_ptr<float>(), (int)N, (int)HW, (int)C, (int)mode, (int)relu, gp,
+                  invstd.data_ptr<float>(), (int)N, (int)HW, (int)C, (int)mode, (int)relu, gp, bp,
                   part.data_ptr<float>(), nblk, ppb, coef.data_ptr<float>(), dg, db, dc,
                   reinterpret_cast<uint16_t*>(dx.data_ptr<at::BFloat16>()), cur_stream());
 }
@@ -1166,7 +1166,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_otf_bwd_(Tensor f1, Tensor[] f2, Tensor coords, Tensor dout, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("conv_tune_table() -> int[]", &conv_tune_table);
   m.def("norm_fwd_(Tensor x, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor? cbias, Tensor(a!)? rmean, Tensor(b!)? rvar, float momentum, float eps, Tensor? res, Tensor(c!) y) -> Tensor[]");
-  m.def("norm_bwd_(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx) -> ()");
+  m.def("norm_bwd_(Tensor dy, Tensor x, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx) -> ()");
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] wgs, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");

@@ -12,8 +12,9 @@
 //             BatchNorm running-stat update; the conv bias is folded here too (it cancels in a
 //             training-mode norm, and shifts the eval-mode one), so the conv runs without bias
 //   apply     y = act(x * scale + shift) [+ residual, ReLU]     (16-B vectors, 8 channels/thread)
-//   backward  partial sums of g, g*xhat, xhat (g = dy masked by the ReLU) -> finalize -> one pass
-//             dx = A*g + B*xhat + C.  The conv-bias gradient falls out of the same sums.
+//   backward  partial sums of g, g*xhat, xhat (g = dy masked by the ReLU, the mask recomputed from
+//             x -- y is never read back) -> finalize -> one pass dx = A*g + B*xhat + C.  The
+//             conv-bias gradient falls out of the same sums.
 //
 // Channel counts are multiples of 8 up to 256; a thread owns one 16-B channel group of a pixel.
 #include "common.h"
@@ -37,6 +38,18 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
   for (int i = 0; i < 4; ++i)
     w[i] = (uint32_t)raft_f32_to_bf16(f[2 * i]) | ((uint32_t)raft_f32_to_bf16(f[2 * i + 1]) << 16);
   return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// The forward's per-(group, channel) affine of the normalised value, evaluated with exactly the
+// float expressions of norm_finalize_kernel (so a backward ReLU mask recomputed from x matches the
+// forward's y > 0 without reading y).
+__device__ __forceinline__ void norm_affine(int mode, const float* __restrict__ gamma,
+                                            const float* __restrict__ beta, int c, float mean,
+                                            float invstd, float& sc, float& sh) {
+  const float gm = (mode == 1 || mode == 2) && gamma ? gamma[c] : 1.f;
+  const float bt = (mode == 1 || mode == 2) && beta ? beta[c] : 0.f;
+  sc = gm * invstd;
+  sh = bt - mean * gm * invstd;
 }
 
 // grid.x = blocks per group-range, grid.y = image (instance) or 1 (batch: range = all images)
@@ -240,9 +253,10 @@ __global__ __launch_bounds__(NT) void relu_mask_kernel(const uint16_t* __restric
 // backward partial sums per (group image, blk): sum g, sum g*xhat, sum xhat;
 // g = dy * [y > 0] when relu; xhat = (x - mean) * invstd
 __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
-    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y, const uint16_t* __restrict__ x,
-    const float* __restrict__ mean, const float* __restrict__ invstd, int HW, int C, int per_image,
-    int pix_per_blk, int total_pix, int relu, float* __restrict__ part) {
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ beta,
+    int mode, int HW, int C, int per_image, int pix_per_blk, int total_pix, int relu,
+    float* __restrict__ part) {
   __shared__ float red[3][NT * 8];
   const int cg = C / 8;
   const int lanes = NT / cg;
@@ -252,11 +266,13 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
   const int64_t base = per_image ? (int64_t)img * HW : 0;
   const int range = per_image ? HW : total_pix;
   const int p0 = blockIdx.x * pix_per_blk, p1 = min(range, p0 + pix_per_blk);
-  float mu[8], is[8];
+  float mu[8], is[8], sc[8], sh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    mu[i] = mean[(int64_t)(per_image ? img : 0) * C + g * 8 + i];
-    is[i] = invstd[(int64_t)(per_image ? img : 0) * C + g * 8 + i];
+    const int c = g * 8 + i;
+    mu[i] = mean[(int64_t)(per_image ? img : 0) * C + c];
+    is[i] = invstd[(int64_t)(per_image ? img : 0) * C + c];
+    norm_affine(mode, gamma, beta, c, mu[i], is[i], sc[i], sh[i]);
   }
   float sg[8], sgx[8], sx[8];
 #pragma unroll
@@ -268,10 +284,9 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
       unpack8(*reinterpret_cast<const uint4*>(dy + off), d);
       unpack8(*reinterpret_cast<const uint4*>(x + off), xv);
       if (relu) {
-        float yv[8];
-        unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
+        // the forward ReLU mask, recomputed from x with the forward's own scale / shift
 #pragma unroll
-        for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
+        for (int i = 0; i < 8; ++i) d[i] = xv[i] * sc[i] + sh[i] > 0.f ? d[i] : 0.f;
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -355,9 +370,10 @@ __global__ __launch_bounds__(256) void norm_bwd_finalize_kernel(
 }
 
 __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
-    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y, const uint16_t* __restrict__ x,
-    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ coef,
-    int HW, int C, int per_image, int64_t nvec, int relu, uint16_t* __restrict__ dx) {
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ beta,
+    int mode, const float* __restrict__ coef, int HW, int C, int per_image, int64_t nvec, int relu,
+    uint16_t* __restrict__ dx) {
   const int cg = C / 8;
   for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
     const int64_t pix = v / cg;
@@ -366,17 +382,17 @@ __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     float d[8], xv[8];
     unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), d);
     unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
-    if (relu) {
-      float yv[8];
-      unpack8(*reinterpret_cast<const uint4*>(y + v * 8), yv);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
-    }
     float o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int64_t k = (int64_t)gi * C + g * 8 + i;
-      const float xh = (xv[i] - mean[k]) * invstd[k];
+      const float mu = mean[k], is = invstd[k];
+      if (relu) {
+        float sc, sh;
+        norm_affine(mode, gamma, beta, g * 8 + i, mu, is, sc, sh);
+        d[i] = xv[i] * sc + sh > 0.f ? d[i] : 0.f;
+      }
+      const float xh = (xv[i] - mu) * is;
       o[i] = coef[k * 3] * d[i] + coef[k * 3 + 1] * xh + coef[k * 3 + 2];
     }
     *reinterpret_cast<uint4*>(dx + v * 8) = pack8(o);
@@ -445,28 +461,28 @@ void launch_relu_mask(const uint16_t* dy, const uint16_t* y, uint16_t* g, int64_
   hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, y, g, nvec);
 }
 
-void launch_norm_bwd(const uint16_t* dy, const uint16_t* y, const uint16_t* x, const float* mean,
-                     const float* invstd, int N, int HW, int C, int mode, int relu,
-                     const float* gamma, float* part, int nblk, int pix_per_blk, float* coef,
+void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd,
+                     int N, int HW, int C, int mode, int relu, const float* gamma,
+                     const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
                      float* dgamma, float* dbeta, float* dcbias, uint16_t* dx, hipStream_t stream) {
   const int per_image = mode == 0 ? 1 : 0;
   const int groups = per_image ? N : 1;
   const int cnt = per_image ? HW : N * HW;
   if (mode == 0 || mode == 1) {
     dim3 grid(nblk, groups);
-    hipLaunchKernelGGL(norm_bwd_stats_kernel, grid, dim3(NT), 0, stream, dy, y, x, mean, invstd, HW, C,
-                       per_image, pix_per_blk, N * HW, relu, part);
+    hipLaunchKernelGGL(norm_bwd_stats_kernel, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, per_image, pix_per_blk, N * HW, relu, part);
   } else {
     // eval / none: only sum(g) and sum(g*xhat) are needed for the parameter grads
     dim3 grid(nblk, 1);
-    hipLaunchKernelGGL(norm_bwd_stats_kernel, grid, dim3(NT), 0, stream, dy, y, x, mean, invstd, HW, C,
-                       0, pix_per_blk, N * HW, relu, part);
+    hipLaunchKernelGGL(norm_bwd_stats_kernel, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, 0, pix_per_blk, N * HW, relu, part);
   }
   float* sums = part + (int64_t)groups * nblk * 3 * C;
   launch_partial_reduce(part, groups, nblk, 3 * C, sums, stream);
   hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, sums, C,
                      groups, nblk, cnt, mode, gamma, invstd, coef, dgamma, dbeta, dcbias);
   const int64_t nvec = (int64_t)N * HW * C / 8;
-  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, y, x, mean,
-                     invstd, coef, HW, C, per_image, nvec, relu, dx);
+  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, mean,
+                     invstd, gamma, beta, mode, coef, HW, C, per_image, nvec, relu, dx);
 }
