@@ -917,7 +917,7 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const Tensor& mean, const Tens
   const int nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
   auto fo = x.options().dtype(at::kFloat);
   Tensor part = at::empty({groups * (nblk + 1) * 3 * C}, fo);  // partials + per-group sums
-  Tensor coef = at::empty({groups, C, 3}, fo);
+  Tensor coef = at::empty({groups, C, 8}, fo);  // A, B', C', scale, shift (+pad) per (group, c)
   launch_norm_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr<at::BFloat16>()),
                   reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>()), mean.data_ptr<float>(),
                   invstd.data_ptr<float>(), (int)N, (int)HW, (int)C, (int)mode, (int)relu, gp, bp,

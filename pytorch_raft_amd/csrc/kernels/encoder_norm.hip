@@ -323,7 +323,8 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
 // over the groups: block = 64 channels x 4 group lanes (fixed-order LDS combine, deterministic)
 __global__ __launch_bounds__(256) void norm_bwd_finalize_kernel(
     const float* __restrict__ part, int C, int groups_img, int nblk, int cnt, int mode,
-    const float* __restrict__ gamma, const float* __restrict__ invstd, float* __restrict__ coef,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean,
+    const float* __restrict__ invstd, float* __restrict__ coef,
     float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dcbias) {
   __shared__ double red[3][4][64];
   const int t = threadIdx.x & 63, lane = threadIdx.x >> 6;
@@ -349,10 +350,14 @@ __global__ __launch_bounds__(256) void norm_bwd_finalize_kernel(
         Cc = 0.f;
         dcb += A * sg;
       }
-      float* co = coef + ((int64_t)gi * C + c) * 3;
-      co[0] = A;
-      co[1] = B;
-      co[2] = Cc;
+      // dx = A*g + B*xhat + Cc = A*g + (B*is)*x + (Cc - B*is*mean); sc / sh: the forward affine
+      // (the apply pass recomputes the ReLU mask from x with them)
+      const float mu = mean[(int64_t)gi * C + c];
+      float sc, sh;
+      norm_affine(mode, gamma, beta, c, mu, is, sc, sh);
+      float4* co = reinterpret_cast<float4*>(coef + ((int64_t)gi * C + c) * 8);
+      co[0] = make_float4(A, B * is, Cc - B * is * mu, sc);
+      co[1] = make_float4(sh, 0.f, 0.f, 0.f);
       dg += sgx;
       db += sg;
     }
@@ -370,10 +375,8 @@ __global__ __launch_bounds__(256) void norm_bwd_finalize_kernel(
 }
 
 __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
-    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const float* __restrict__ mean,
-    const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ beta,
-    int mode, const float* __restrict__ coef, int HW, int C, int per_image, int64_t nvec, int relu,
-    uint16_t* __restrict__ dx) {
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const float* __restrict__ coef,
+    int HW, int C, int per_image, int64_t nvec, int relu, uint16_t* __restrict__ dx) {
   const int cg = C / 8;
   for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
     const int64_t pix = v / cg;
@@ -382,18 +385,14 @@ __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     float d[8], xv[8];
     unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), d);
     unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
+    const float4* co = reinterpret_cast<const float4*>(coef + ((int64_t)gi * C + g * 8) * 8);
     float o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int64_t k = (int64_t)gi * C + g * 8 + i;
-      const float mu = mean[k], is = invstd[k];
-      if (relu) {
-        float sc, sh;
-        norm_affine(mode, gamma, beta, g * 8 + i, mu, is, sc, sh);
-        d[i] = xv[i] * sc + sh > 0.f ? d[i] : 0.f;
-      }
-      const float xh = (xv[i] - mu) * is;
-      o[i] = coef[k * 3] * d[i] + coef[k * 3 + 1] * xh + coef[k * 3 + 2];
+      const float4 k0 = co[2 * i];
+      // the forward ReLU mask, recomputed from x with the forward's own scale / shift
+      if (relu) d[i] = xv[i] * k0.w + co[2 * i + 1].x > 0.f ? d[i] : 0.f;
+      o[i] = k0.x * d[i] + k0.y * xv[i] + k0.z;
     }
     *reinterpret_cast<uint4*>(dx + v * 8) = pack8(o);
   }
@@ -481,8 +480,8 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, c
   float* sums = part + (int64_t)groups * nblk * 3 * C;
   launch_partial_reduce(part, groups, nblk, 3 * C, sums, stream);
   hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, sums, C,
-                     groups, nblk, cnt, mode, gamma, invstd, coef, dgamma, dbeta, dcbias);
+                     groups, nblk, cnt, mode, gamma, beta, mean, invstd, coef, dgamma, dbeta, dcbias);
   const int64_t nvec = (int64_t)N * HW * C / 8;
-  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, mean,
-                     invstd, gamma, beta, mode, coef, HW, C, per_image, nvec, relu, dx);
+  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, coef, HW,
+                     C, per_image, nvec, relu, dx);
 }
