@@ -185,7 +185,9 @@ __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint1
   }
 }
 
-// y = act(x*scale + shift) [+ res -> relu];  act: relu when relu != 0
+// y = act(x*scale + shift) [+ res -> relu];  act: relu when relu != 0.  Block size is a multiple
+// of the channel-group count: each thread keeps one channel group and reloads its scale / shift
+// only when the image changes.
 __global__ __launch_bounds__(NT) void norm_apply_kernel(const uint16_t* __restrict__ x,
                                                         const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int HW,
@@ -193,14 +195,23 @@ __global__ __launch_bounds__(NT) void norm_apply_kernel(const uint16_t* __restri
                                                         const uint16_t* __restrict__ res,
                                                         uint16_t* __restrict__ y) {
   const int cg = C / 8;
-  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  int cur = -1;
+  float sc[8], sh[8];
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nvec; v += step) {
     const int64_t pix = v / cg;
     const int g = (int)(v - pix * cg);
     const int n = (int)(pix / HW);
+    if (n != cur) {
+      cur = n;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        sc[i] = scale[(int64_t)n * C + g * 8 + i];
+        sh[i] = shift[(int64_t)n * C + g * 8 + i];
+      }
+    }
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(x + v * 8), f);
-    const float* sc = scale + (int64_t)n * C + g * 8;
-    const float* sh = shift + (int64_t)n * C + g * 8;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       f[i] = f[i] * sc[i] + sh[i];
@@ -374,25 +385,38 @@ __global__ __launch_bounds__(256) void norm_bwd_finalize_kernel(
   }
 }
 
+// block = (NT / cg) * cg threads, a multiple of the channel-group count: every thread keeps ONE
+// channel group for the whole grid-stride loop and re-reads its 8 channels' coefficients only
+// when the pixel's image (instance-norm group) changes
 __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const float* __restrict__ coef,
     int HW, int C, int per_image, int64_t nvec, int relu, uint16_t* __restrict__ dx) {
   const int cg = C / 8;
-  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+  const int64_t step = (int64_t)gridDim.x * blockDim.x;
+  int cur = -1;
+  float A[8], Bp[8], Cp[8], sc[8], sh[8];
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nvec; v += step) {
     const int64_t pix = v / cg;
     const int g = (int)(v - pix * cg);
     const int gi = per_image ? (int)(pix / HW) : 0;
+    if (gi != cur) {
+      cur = gi;
+      const float4* co = reinterpret_cast<const float4*>(coef + ((int64_t)gi * C + g * 8) * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float4 k0 = co[2 * i], k1 = co[2 * i + 1];
+        A[i] = k0.x; Bp[i] = k0.y; Cp[i] = k0.z; sc[i] = k0.w; sh[i] = k1.x;
+      }
+    }
     float d[8], xv[8];
     unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), d);
     unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
-    const float4* co = reinterpret_cast<const float4*>(coef + ((int64_t)gi * C + g * 8) * 8);
     float o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float4 k0 = co[2 * i];
       // the forward ReLU mask, recomputed from x with the forward's own scale / shift
-      if (relu) d[i] = xv[i] * k0.w + co[2 * i + 1].x > 0.f ? d[i] : 0.f;
-      o[i] = k0.x * d[i] + k0.y * xv[i] + k0.z;
+      if (relu) d[i] = xv[i] * sc[i] + sh[i] > 0.f ? d[i] : 0.f;
+      o[i] = A[i] * d[i] + Bp[i] * xv[i] + Cp[i];
     }
     *reinterpret_cast<uint4*>(dx + v * 8) = pack8(o);
   }
@@ -444,7 +468,8 @@ void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, i
 void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift, int N, int HW,
                        int C, int relu, const uint16_t* res, uint16_t* y, hipStream_t stream) {
   const int64_t nvec = (int64_t)N * HW * C / 8;
-  hipLaunchKernelGGL(norm_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, x, scale, shift, HW,
+  const int bt = (NT / (C / 8)) * (C / 8);  // multiple of the channel-group count
+  hipLaunchKernelGGL(norm_apply_kernel, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
                      C, nvec, relu, res, y);
 }
 
@@ -482,6 +507,7 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, c
   hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, sums, C,
                      groups, nblk, cnt, mode, gamma, beta, mean, invstd, coef, dgamma, dbeta, dcbias);
   const int64_t nvec = (int64_t)N * HW * C / 8;
-  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, coef, HW,
+  const int bt = (NT / (C / 8)) * (C / 8);  // multiple of the channel-group count
+  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(bt), 0, stream, dy, x, coef, HW,
                      C, per_image, nvec, relu, dx);
 }
