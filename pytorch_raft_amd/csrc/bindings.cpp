@@ -893,8 +893,8 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
 }
 
 // dx (bf16) and += parameter grads; y = the forward output when relu (mask), else ignored
-void norm_bwd_(const Tensor& dy, const Tensor& x, const Tensor& mean, const Tensor& invstd,
-               int64_t mode, int64_t relu, const c10::optional<Tensor>& gamma,
+void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y,
+               const Tensor& mean, const Tensor& invstd, int64_t mode, int64_t relu, const c10::optional<Tensor>& gamma,
                const c10::optional<Tensor>& beta, const c10::optional<Tensor>& dgamma,
                const c10::optional<Tensor>& dbeta, const c10::optional<Tensor>& dcbias,
                const Tensor& dx) {
@@ -918,8 +918,14 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const Tensor& mean, const Tens
   auto fo = x.options().dtype(at::kFloat);
   Tensor part = at::empty({groups * (nblk + 1) * 3 * C}, fo);  // partials + per-group sums
   Tensor coef = at::empty({groups, C, 8}, fo);  // A, B', C', scale, shift (+pad) per (group, c)
+  const uint16_t* yp = nullptr;
+  if (y.has_value() && y->defined()) {
+    check_cl_bf16(*y, "y");
+    TORCH_CHECK(y->sizes() == x.sizes(), "y shape");
+    yp = reinterpret_cast<const uint16_t*>(y->data_ptr<at::BFloat16>());
+  }
   launch_norm_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr<at::BFloat16>()),
-                  reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>()), mean.data_ptr<float>(),
+                  reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>()), yp, mean.data_ptr<float>(),
                   invstd.data_ptr<float>(), (int)N, (int)HW, (int)C, (int)mode, (int)relu, gp, bp,
                   part.data_ptr<float>(), nblk, ppb, coef.data_ptr<float>(), dg, db, dc,
                   reinterpret_cast<uint16_t*>(dx.data_ptr<at::BFloat16>()), cur_stream());
@@ -1166,7 +1172,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_otf_bwd_(Tensor f1, Tensor[] f2, Tensor coords, Tensor dout, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("conv_tune_table() -> int[]", &conv_tune_table);
   m.def("norm_fwd_(Tensor x, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor? cbias, Tensor(a!)? rmean, Tensor(b!)? rvar, float momentum, float eps, Tensor? res, Tensor(c!) y) -> Tensor[]");
-  m.def("norm_bwd_(Tensor dy, Tensor x, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx) -> ()");
+  m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx) -> ()");
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] wgs, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");

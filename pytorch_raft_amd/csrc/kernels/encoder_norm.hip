@@ -389,8 +389,9 @@ __global__ __launch_bounds__(256) void norm_bwd_finalize_kernel(
 // channel group for the whole grid-stride loop and re-reads its 8 channels' coefficients only
 // when the pixel's image (instance-norm group) changes
 __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
-    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const float* __restrict__ coef,
-    int HW, int C, int per_image, int64_t nvec, int relu, uint16_t* __restrict__ dx) {
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint16_t* __restrict__ y,
+    const float* __restrict__ coef, int HW, int C, int per_image, int64_t nvec, int relu,
+    uint16_t* __restrict__ dx) {
   const int cg = C / 8;
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
   int cur = -1;
@@ -411,13 +412,19 @@ __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     float d[8], xv[8];
     unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), d);
     unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
+    if (relu && y != nullptr) {
+      float yv[8];
+      unpack8(*reinterpret_cast<const uint4*>(y + v * 8), yv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
+    } else if (relu) {
+      // the forward ReLU mask, recomputed from x with the forward's own scale / shift
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = xv[i] * sc[i] + sh[i] > 0.f ? d[i] : 0.f;
+    }
     float o[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      // the forward ReLU mask, recomputed from x with the forward's own scale / shift
-      if (relu) d[i] = xv[i] * sc[i] + sh[i] > 0.f ? d[i] : 0.f;
-      o[i] = A[i] * d[i] + Bp[i] * xv[i] + Cp[i];
-    }
+    for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + Bp[i] * xv[i] + Cp[i];
     *reinterpret_cast<uint4*>(dx + v * 8) = pack8(o);
   }
 }
@@ -485,7 +492,8 @@ void launch_relu_mask(const uint16_t* dy, const uint16_t* y, uint16_t* g, int64_
   hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, y, g, nvec);
 }
 
-void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd,
+void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
+                     const float* invstd,
                      int N, int HW, int C, int mode, int relu, const float* gamma,
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
                      float* dgamma, float* dbeta, float* dcbias, uint16_t* dx, hipStream_t stream) {
@@ -508,6 +516,6 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, c
                      groups, nblk, cnt, mode, gamma, beta, mean, invstd, coef, dgamma, dbeta, dcbias);
   const int64_t nvec = (int64_t)N * HW * C / 8;
   const int bt = (NT / (C / 8)) * (C / 8);  // multiple of the channel-group count
-  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(bt), 0, stream, dy, x, coef, HW,
-                     C, per_image, nvec, relu, dx);
+  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(bt), 0, stream, dy, x, y, coef,
+                     HW, C, per_image, nvec, relu, dx);
 }

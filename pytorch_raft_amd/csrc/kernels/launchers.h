@@ -245,7 +245,9 @@ void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_
                      hipStream_t stream);
 void launch_relu_mask(const uint16_t* dy, const uint16_t* y, uint16_t* g, int64_t n,
                       hipStream_t stream);
-void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* invstd,
+// y (nullable): the forward output; when given, the ReLU mask is read from it, else recomputed
+void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
+                     const float* invstd,
                      int N, int HW, int C, int mode, int relu, const float* gamma,
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
                      float* dgamma, float* dbeta, float* dcbias, uint16_t* dx, hipStream_t stream);
