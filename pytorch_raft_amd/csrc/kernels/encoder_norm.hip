@@ -385,46 +385,34 @@ __global__ __launch_bounds__(256) void norm_bwd_finalize_kernel(
   }
 }
 
-// block = (NT / cg) * cg threads, a multiple of the channel-group count: every thread keeps ONE
-// channel group for the whole grid-stride loop and re-reads its 8 channels' coefficients only
-// when the pixel's image (instance-norm group) changes
+// dx = A*g + B'*x + C' with g = dy masked by the forward ReLU (read from y when given, else
+// recomputed from x with the forward's scale / shift); per-element coefficient reads (L1-resident
+// table) measured faster than per-thread register caching across the grid-stride loop
 __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint16_t* __restrict__ y,
     const float* __restrict__ coef, int HW, int C, int per_image, int64_t nvec, int relu,
     uint16_t* __restrict__ dx) {
   const int cg = C / 8;
-  const int64_t step = (int64_t)gridDim.x * blockDim.x;
-  int cur = -1;
-  float A[8], Bp[8], Cp[8], sc[8], sh[8];
-  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nvec; v += step) {
+  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
     const int64_t pix = v / cg;
     const int g = (int)(v - pix * cg);
     const int gi = per_image ? (int)(pix / HW) : 0;
-    if (gi != cur) {
-      cur = gi;
-      const float4* co = reinterpret_cast<const float4*>(coef + ((int64_t)gi * C + g * 8) * 8);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float4 k0 = co[2 * i], k1 = co[2 * i + 1];
-        A[i] = k0.x; Bp[i] = k0.y; Cp[i] = k0.z; sc[i] = k0.w; sh[i] = k1.x;
-      }
-    }
     float d[8], xv[8];
     unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), d);
     unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
+    const float* co = coef + ((int64_t)gi * C + g * 8) * 8;
     if (relu && y != nullptr) {
       float yv[8];
       unpack8(*reinterpret_cast<const uint4*>(y + v * 8), yv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
     } else if (relu) {
-      // the forward ReLU mask, recomputed from x with the forward's own scale / shift
 #pragma unroll
-      for (int i = 0; i < 8; ++i) d[i] = xv[i] * sc[i] + sh[i] > 0.f ? d[i] : 0.f;
+      for (int i = 0; i < 8; ++i) d[i] = xv[i] * co[i * 8 + 3] + co[i * 8 + 4] > 0.f ? d[i] : 0.f;
     }
     float o[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + Bp[i] * xv[i] + Cp[i];
+    for (int i = 0; i < 8; ++i) o[i] = co[i * 8] * d[i] + co[i * 8 + 1] * xv[i] + co[i * 8 + 2];
     *reinterpret_cast<uint4*>(dx + v * 8) = pack8(o);
   }
 }
@@ -515,7 +503,6 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
   hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, sums, C,
                      groups, nblk, cnt, mode, gamma, beta, mean, invstd, coef, dgamma, dbeta, dcbias);
   const int64_t nvec = (int64_t)N * HW * C / 8;
-  const int bt = (NT / (C / 8)) * (C / 8);  // multiple of the channel-group count
-  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(bt), 0, stream, dy, x, y, coef,
+  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
                      HW, C, per_image, nvec, relu, dx);
 }
