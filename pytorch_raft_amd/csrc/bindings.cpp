@@ -917,7 +917,7 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y
   const int nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
   auto fo = x.options().dtype(at::kFloat);
   Tensor part = at::empty({groups * (nblk + 1) * 3 * C}, fo);  // partials + per-group sums
-  Tensor coef = at::empty({groups, C, 8}, fo);  // A, B', C', scale, shift (+pad) per (group, c)
+  Tensor coef = at::empty({groups, 5, C}, fo);  // A, B', C', scale, shift per (group, c), SoA
   const uint16_t* yp = nullptr;
   if (y.has_value() && y->defined()) {
     check_cl_bf16(*y, "y");

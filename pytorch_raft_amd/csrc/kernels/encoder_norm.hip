@@ -366,9 +366,13 @@ __global__ __launch_bounds__(256) void norm_bwd_finalize_kernel(
       const float mu = mean[(int64_t)gi * C + c];
       float sc, sh;
       norm_affine(mode, gamma, beta, c, mu, is, sc, sh);
-      float4* co = reinterpret_cast<float4*>(coef + ((int64_t)gi * C + c) * 8);
-      co[0] = make_float4(A, B * is, Cc - B * is * mu, sc);
-      co[1] = make_float4(sh, 0.f, 0.f, 0.f);
+      // structure-of-arrays [group][field][C]: a thread's 8 channels of a field are 2 x 16 B
+      float* co = coef + (int64_t)gi * 5 * C + c;
+      co[0] = A;
+      co[C] = B * is;
+      co[2 * C] = Cc - B * is * mu;
+      co[3 * C] = sc;
+      co[4 * C] = sh;
       dg += sgx;
       db += sg;
     }
@@ -400,19 +404,30 @@ __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     float d[8], xv[8];
     unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), d);
     unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
-    const float* co = coef + ((int64_t)gi * C + g * 8) * 8;
+    const float* co = coef + (int64_t)gi * 5 * C + g * 8;
+    auto ld8 = [&](int f, float (&r)[8]) {
+      const float4 a = *reinterpret_cast<const float4*>(co + f * C);
+      const float4 b = *reinterpret_cast<const float4*>(co + f * C + 4);
+      r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w; r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+    };
     if (relu && y != nullptr) {
       float yv[8];
       unpack8(*reinterpret_cast<const uint4*>(y + v * 8), yv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
     } else if (relu) {
+      float sc[8], sh[8];
+      ld8(3, sc);
+      ld8(4, sh);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) d[i] = xv[i] * co[i * 8 + 3] + co[i * 8 + 4] > 0.f ? d[i] : 0.f;
+      for (int i = 0; i < 8; ++i) d[i] = xv[i] * sc[i] + sh[i] > 0.f ? d[i] : 0.f;
     }
-    float o[8];
+    float A[8], Bp[8], Cp[8], o[8];
+    ld8(0, A);
+    ld8(1, Bp);
+    ld8(2, Cp);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = co[i * 8] * d[i] + co[i * 8 + 1] * xv[i] + co[i * 8 + 2];
+    for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + Bp[i] * xv[i] + Cp[i];
     *reinterpret_cast<uint4*>(dx + v * 8) = pack8(o);
   }
 }
