@@ -57,9 +57,8 @@ class _NormAct(torch.autograd.Function):
                     1.0 / float(norm.num_batches_tracked.item())
         mean, invstd = _ext.ops().norm_fwd_(x, mode, int(relu), gamma, beta, cbias, rm, rv,
                                             float(momentum), float(eps), None, y)
-        # the backward's statistics pass recomputes the ReLU mask from x; its apply pass reads it
-        # from y (measured faster than recomputing it there)
-        ctx.save_for_backward(x, y, mean, invstd, gamma, beta)
+        # y is not kept: the backward recomputes the ReLU mask from x
+        ctx.save_for_backward(x, mean, invstd, gamma, beta)
         ctx.mode = mode
         ctx.relu = relu
         ctx.has = (gamma is not None, beta is not None, cbias is not None)
@@ -67,7 +66,7 @@ class _NormAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, mean, invstd, gamma, beta = ctx.saved_tensors
+        x, mean, invstd, gamma, beta = ctx.saved_tensors
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         c = x.shape[1]
         dev = x.device
@@ -76,7 +75,7 @@ class _NormAct(torch.autograd.Function):
         db = torch.empty(c, device=dev) if ctx.has[1] else None
         dc = torch.empty(c, device=dev) if ctx.has[2] else None
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        _ext.ops().norm_bwd_(dy, x, y, mean, invstd, ctx.mode, int(ctx.relu), gamma, beta, dg, db, dc,
+        _ext.ops().norm_bwd_(dy, x, None, mean, invstd, ctx.mode, int(ctx.relu), gamma, beta, dg, db, dc,
                              dx)
         return dx, dg, db, dc, None, None, None
 
