@@ -80,6 +80,49 @@ class _NormAct(torch.autograd.Function):
         return dx, dg, db, dc, None, None, None
 
 
+class _NormActAddRelu(torch.autograd.Function):
+    """out = relu(relu(norm(x + conv_bias)) + res): the second conv of a residual block, its norm,
+    ReLU, the residual add and the block-end ReLU as ONE node -- the apply pass adds the residual,
+    so the branch output is never written (`core/extractor.py:47-56`)."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, cbias, res, norm, mode):
+        out = torch.empty_like(x, memory_format=torch.channels_last)
+        rm = rv = None
+        momentum = 0.1
+        eps = 1e-5
+        if isinstance(norm, (nn.BatchNorm2d, nn.InstanceNorm2d)):
+            eps = norm.eps
+        if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and norm.track_running_stats:
+            rm, rv = norm.running_mean, norm.running_var
+            if mode == MODE_BATCH_TRAIN:
+                norm.num_batches_tracked.add_(1)
+                momentum = norm.momentum if norm.momentum is not None else \
+                    1.0 / float(norm.num_batches_tracked.item())
+        res = res.contiguous(memory_format=torch.channels_last)
+        mean, invstd = _ext.ops().norm_fwd_(x, mode, 1, gamma, beta, cbias, rm, rv, float(momentum),
+                                            float(eps), res, out)
+        ctx.save_for_backward(x, out, mean, invstd, gamma, beta)
+        ctx.mode = mode
+        ctx.has = (gamma is not None, beta is not None, cbias is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, out, mean, invstd, gamma, beta = ctx.saved_tensors
+        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        g = torch.empty_like(out, memory_format=torch.channels_last)
+        _ext.ops().relu_mask_(dout, out, g)          # block-end ReLU; g is also the residual's grad
+        c = x.shape[1]
+        dev = x.device
+        dg = torch.empty(c, device=dev) if ctx.has[0] else None
+        db = torch.empty(c, device=dev) if ctx.has[1] else None
+        dc = torch.empty(c, device=dev) if ctx.has[2] else None
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        _ext.ops().norm_bwd_(g, x, None, mean, invstd, ctx.mode, 1, gamma, beta, dg, db, dc, dx)
+        return dx, dg, db, dc, g, None, None
+
+
 class _AddRelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, b):
@@ -185,12 +228,16 @@ def conv_norm_act(x, conv, norm, relu=True):
 
 
 def residual_block(blk, x):
-    """`core/extractor.py:47-56` on the fast path."""
+    """`core/extractor.py:47-56` on the fast path (conv2 + norm2 + ReLU + add + ReLU fused)."""
     y = conv_norm_act(x, blk.conv1, blk.norm1)
-    y = conv_norm_act(y, blk.conv2, blk.norm2)
     if blk.downsample is not None:
         x = conv_norm_act(x, blk.downsample[0], blk.downsample[1], relu=False)
-    return _AddRelu.apply(x, y)
+    mode = _norm_mode(blk.norm2)
+    y2 = _conv(y, blk.conv2).contiguous(memory_format=torch.channels_last)
+    gamma = beta = None
+    if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and blk.norm2.affine:
+        gamma, beta = blk.norm2.weight, blk.norm2.bias
+    return _NormActAddRelu.apply(y2, gamma, beta, blk.conv2.bias, x, blk.norm2, mode)
 
 
 def bottleneck_block(blk, x):
