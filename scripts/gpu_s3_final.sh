@@ -1,0 +1,16 @@
+#!/bin/bash
+# end-of-session check: smoke, full GPU suite, default bench, steady-state profile
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; grep -E "smoke ok|Error" gpurun_out/smoke.log | tail -3
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -2 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 300 python bench.py > gpurun_out/bench_default.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_default.log | cut -c1-300
+bash scripts/gpu_profile.sh ${1:-final} > /dev/null && python scripts/categorize.py gpurun_out/${1:-final}_summary.txt > gpurun_out/${1:-final}_categories.txt
+cat gpurun_out/${1:-final}_categories.txt
