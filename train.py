@@ -95,6 +95,9 @@ def worker(args):
         device = torch.device('cuda', int(dev_env))
     device = pdist.init_distributed(device=device)
     rank, world = pdist.rank(), pdist.world_size()
+    if device.type == 'cuda':
+        # fixed crop size: let MIOpen time its encoder conv solvers once and keep the fastest
+        torch.backends.cudnn.benchmark = True
     torch.manual_seed(args.seed)
     np.random.seed(args.seed)
 
