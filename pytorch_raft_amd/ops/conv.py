@@ -9,6 +9,8 @@ optimizer step (``pack_weight``) to the kernel layout [Npad][KH*KW][CinPad] bf16
 segment's real channels are placed at its padded offset (e.g. the 324 correlation channels live in
 a 384-channel buffer whose tail is zero).  Segment widths are multiples of 64 = the kernel's K step.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -109,6 +111,8 @@ def conv_wgrad(g, g_off, segs, ksize, pad, cout, dw, db=None, cin_small=0, pix_p
 
 
 MAX_WG_ITEMS = 32
+# max partial tiles (items x K-splits) reduced into one weight-gradient tile by fp32 atomics
+_WG_FANIN = int(os.environ.get('RAFT_WG_FANIN', '48'))
 
 
 def conv_wgrad_multi(items, g_off, in_off, in_cnt, ksize, pad, cout, dw, db=None,
@@ -128,7 +132,7 @@ def conv_wgrad_multi(items, g_off, in_off, in_cnt, ksize, pad, cout, dw, db=None
         # land on the same dw tile (a 768-way same-address atomic pile-up made the K=128 convf1
         # weight gradient 20x slower than its MFMA work)
         per_item = max(1, (768 + tiles * n - 1) // (tiles * n))
-        per_item = max(1, min(per_item, 48 // n))
+        per_item = max(1, min(per_item, _WG_FANIN // n))
         pix_per_split = round_up((p + per_item - 1) // per_item, 64)
     ins = [b for _, bufs in items for b in bufs]
     ops.conv_wgrad_multi_([g for g, _ in items], int(g_off), ins, [int(o) for o in in_off],
