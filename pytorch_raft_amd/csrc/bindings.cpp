@@ -942,13 +942,19 @@ void add_relu_(const Tensor& a, const Tensor& b, const Tensor& out) {
                   reinterpret_cast<uint16_t*>(out.data_ptr<at::BFloat16>()), a.numel(), cur_stream());
 }
 
-void relu_mask_(const Tensor& dy, const Tensor& y, const Tensor& g) {
+void relu_mask_(const Tensor& dy, const Tensor& y, const Tensor& g, const c10::optional<Tensor>& dy2) {
   check_cl_bf16(dy, "dy");
   check_cl_bf16(y, "y");
   check_cl_bf16(g, "g");
   TORCH_CHECK(dy.sizes() == y.sizes() && g.sizes() == y.sizes(), "shapes");
+  const uint16_t* d2 = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    check_cl_bf16(*dy2, "dy2");
+    TORCH_CHECK(dy2->sizes() == y.sizes(), "dy2 shape");
+    d2 = reinterpret_cast<const uint16_t*>(dy2->data_ptr<at::BFloat16>());
+  }
   c10::DeviceGuard gd(y.device());
-  launch_relu_mask(reinterpret_cast<const uint16_t*>(dy.data_ptr<at::BFloat16>()),
+  launch_relu_mask(reinterpret_cast<const uint16_t*>(dy.data_ptr<at::BFloat16>()), d2,
                    reinterpret_cast<const uint16_t*>(y.data_ptr<at::BFloat16>()),
                    reinterpret_cast<uint16_t*>(g.data_ptr<at::BFloat16>()), y.numel(), cur_stream());
 }
@@ -1174,7 +1180,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("norm_fwd_(Tensor x, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor? cbias, Tensor(a!)? rmean, Tensor(b!)? rvar, float momentum, float eps, Tensor? res, Tensor(c!) y) -> Tensor[]");
   m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx) -> ()");
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
-  m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g) -> ()");
+  m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] wgs, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");
   m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout, bool nhwc=False) -> Tensor[]");

@@ -241,15 +241,31 @@ __global__ __launch_bounds__(NT) void add_relu_kernel(const uint16_t* __restrict
   }
 }
 
-// g = dy * [y > 0]   (the ReLU backward, also the block-end residual ReLU)
+// g = (dy [+ dy2]) * [y > 0]   (the ReLU backward, also the block-end residual ReLU)
 __global__ __launch_bounds__(NT) void relu_mask_kernel(const uint16_t* __restrict__ dy,
+                                                       const uint16_t* __restrict__ dy2,
                                                        const uint16_t* __restrict__ y,
                                                        uint16_t* __restrict__ g, int64_t nvec) {
   for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
-    const uint4 d = *reinterpret_cast<const uint4*>(dy + v * 8);
     const uint4 m = *reinterpret_cast<const uint4*>(y + v * 8);
-    const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, mw[4] = {m.x, m.y, m.z, m.w};
+    const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
     uint32_t o[4];
+    if (dy2 != nullptr) {
+      // g = (dy + dy2) * [y > 0]: the residual-branch gradient folded in (no separate add pass)
+      float a[8], b[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), a);
+      unpack8(*reinterpret_cast<const uint4*>(dy2 + v * 8), b);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t yw = (i & 1) ? (mw[i >> 1] >> 16) : (mw[i >> 1] & 0xffffu);
+        a[i] = ((yw & 0x8000u) == 0 && (yw & 0x7fffu) != 0) ? a[i] + b[i] : 0.f;
+      }
+      const uint4 r = pack8(a);
+      *reinterpret_cast<uint4*>(g + v * 8) = r;
+      continue;
+    }
+    const uint4 d = *reinterpret_cast<const uint4*>(dy + v * 8);
+    const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       // bf16 > 0  <=>  sign bit clear and magnitude non-zero
@@ -489,10 +505,10 @@ void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_
   hipLaunchKernelGGL(add_relu_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, a, b, out, nvec);
 }
 
-void launch_relu_mask(const uint16_t* dy, const uint16_t* y, uint16_t* g, int64_t n,
+void launch_relu_mask(const uint16_t* dy, const uint16_t* dy2, const uint16_t* y, uint16_t* g, int64_t n,
                       hipStream_t stream) {
   const int64_t nvec = n / 8;
-  hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, y, g, nvec);
+  hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, dy2, y, g, nvec);
 }
 
 void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,

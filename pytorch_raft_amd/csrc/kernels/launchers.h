@@ -243,7 +243,8 @@ void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift
                        int C, int relu, const uint16_t* res, uint16_t* y, hipStream_t stream);
 void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_t n,
                      hipStream_t stream);
-void launch_relu_mask(const uint16_t* dy, const uint16_t* y, uint16_t* g, int64_t n,
+// g = (dy [+ dy2]) * [y > 0]; dy2 nullable
+void launch_relu_mask(const uint16_t* dy, const uint16_t* dy2, const uint16_t* y, uint16_t* g, int64_t n,
                       hipStream_t stream);
 // y (nullable): the forward output; when given, the ReLU mask is read from it, else recomputed
 void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,

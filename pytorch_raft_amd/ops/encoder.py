@@ -86,8 +86,10 @@ class _NormActAddRelu(torch.autograd.Function):
     so the branch output is never written (`core/extractor.py:47-56`)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, cbias, res, norm, mode):
+    def forward(ctx, x, gamma, beta, cbias, res, norm, mode, holder, res_holder):
         out = torch.empty_like(x, memory_format=torch.channels_last)
+        ctx.holder = holder          # receives the NEXT block's residual gradient (see backward)
+        ctx.res_holder = res_holder  # this block's residual comes from such a block: stash into it
         rm = rv = None
         momentum = 0.1
         eps = 1e-5
@@ -112,7 +114,11 @@ class _NormActAddRelu(torch.autograd.Function):
         x, out, mean, invstd, gamma, beta = ctx.saved_tensors
         dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         g = torch.empty_like(out, memory_format=torch.channels_last)
-        _ext.ops().relu_mask_(dout, out, g)          # block-end ReLU; g is also the residual's grad
+        # an identity-residual consumer of this block's output left its gradient in the stash
+        # instead of handing it to autograd: fold it into the ReLU-mask pass (no bf16 add kernel).
+        # It always runs first -- this node waits for every consumer of its output.
+        stash = ctx.holder.pop('g', None)
+        _ext.ops().relu_mask_(dout, out, g, stash)   # block-end ReLU; g is also the residual's grad
         c = x.shape[1]
         dev = x.device
         dg = torch.empty(c, device=dev) if ctx.has[0] else None
@@ -120,7 +126,11 @@ class _NormActAddRelu(torch.autograd.Function):
         dc = torch.empty(c, device=dev) if ctx.has[2] else None
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         _ext.ops().norm_bwd_(g, x, None, mean, invstd, ctx.mode, 1, gamma, beta, dg, db, dc, dx)
-        return dx, dg, db, dc, g, None, None
+        gres = g
+        if ctx.res_holder is not None:
+            ctx.res_holder['g'] = g
+            gres = None
+        return dx, dg, db, dc, gres, None, None, None, None
 
 
 class _AddRelu(torch.autograd.Function):
@@ -237,7 +247,18 @@ def residual_block(blk, x):
     gamma = beta = None
     if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and blk.norm2.affine:
         gamma, beta = blk.norm2.weight, blk.norm2.bias
-    return _NormActAddRelu.apply(y2, gamma, beta, blk.conv2.bias, x, blk.norm2, mode)
+    # identity shortcut from a previous fused block: its gradient goes through that block's stash
+    res_holder = _HOLDERS.get(id(x)) if blk.downsample is None else None
+    if res_holder is not None and res_holder[0] is not x:
+        res_holder = None
+    holder = {}
+    out = _NormActAddRelu.apply(y2, gamma, beta, blk.conv2.bias, x, blk.norm2, mode, holder,
+                                res_holder[1] if res_holder is not None else None)
+    _HOLDERS[id(out)] = (out, holder)
+    return out
+
+
+_HOLDERS = {}  # id(block output) -> (output, its gradient stash), for the encoder forward in flight
 
 
 def bottleneck_block(blk, x):
@@ -278,6 +299,7 @@ def encoder_forward(enc, x):
             return _encoder_body(enc, x)
         finally:
             _WEIGHTS.clear()
+            _HOLDERS.clear()
 
 
 def _encoder_body(enc, x):
