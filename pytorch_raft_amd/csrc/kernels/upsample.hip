@@ -210,54 +210,80 @@ __global__ __launch_bounds__(256) void convex_up_nhwc_fwd_kernel(const float* __
   O[64 * HW + o] = o1 * inv;
 }
 
+// 16 lanes per cell, 4 consecutive sub-pixels per lane (4 cells per wave): the mask / dmask rows
+// move as 8-B pieces, dout as 16-B pieces, and the 18 neighbour-weight sums are reduced over the
+// lane's 4 sub-pixels in registers first, leaving 4 shuffle steps per sum (was 6 over 64 lanes).
 __global__ __launch_bounds__(256) void convex_up_nhwc_bwd_kernel(const float* __restrict__ flow,
                                                                  const uint16_t* __restrict__ mask,
                                                                  const float* __restrict__ dout,
                                                                  uint16_t* __restrict__ dmask,
                                                                  float* __restrict__ wbuf, int B,
                                                                  int H, int W) {
-  const int s = threadIdx.x & 63;
-  const int64_t cell = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int q = threadIdx.x & 15;
+  const int64_t cell = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int64_t HW = (int64_t)H * W;
-  if (cell >= (int64_t)B * HW) return;  // whole wave exits together (cell is wave-uniform)
+  if (cell >= (int64_t)B * HW) return;  // a 16-lane group exits together (cell is group-uniform)
   const int64_t b = cell / HW;
   const int yx = (int)(cell - b * HW), y = yx / W, x = yx % W;
   float nf[9][2];
   cell_flows(flow + b * 2 * HW, HW, y, x, H, W, nf);
-  const uint16_t* M = mask + cell * 576;
-  float p[9], mx = -INFINITY;
+  const uint16_t* M = mask + cell * 576 + 4 * q;
+  float p[9][4], mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    p[k] = raft_bf16_to_f32(M[k * 64 + s]);
-    mx = fmaxf(mx, p[k]);
-  }
-  float den = 0.f;
+    const uint2 v = *reinterpret_cast<const uint2*>(M + k * 64);
+    p[k][0] = __uint_as_float(v.x << 16);
+    p[k][1] = __uint_as_float(v.x & 0xffff0000u);
+    p[k][2] = __uint_as_float(v.y << 16);
+    p[k][3] = __uint_as_float(v.y & 0xffff0000u);
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    p[k] = __expf(p[k] - mx);
-    den += p[k];
+    for (int j = 0; j < 4; ++j) mx[j] = fmaxf(mx[j], p[k][j]);
   }
-  const float inv = 1.f / den;
+  float den[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      p[k][j] = __expf(p[k][j] - mx[j]);
+      den[j] += p[k][j];
+    }
   const int64_t W8 = 8 * (int64_t)W;
-  const int64_t o = (int64_t)(8 * y + (s >> 3)) * W8 + 8 * x + (s & 7);
+  const int64_t o = (int64_t)(8 * y + (q >> 1)) * W8 + 8 * x + (q & 1) * 4;
   const float* DO = dout + b * 2 * 64 * HW;
-  const float d0 = DO[o], d1 = DO[64 * HW + o];
-  float g[9], dot = 0.f;
+  const float4 da = *reinterpret_cast<const float4*>(DO + o);
+  const float4 db = *reinterpret_cast<const float4*>(DO + 64 * HW + o);
+  const float d0[4] = {da.x, da.y, da.z, da.w}, d1[4] = {db.x, db.y, db.z, db.w};
+  float g[9][4], dot[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    p[k] *= inv;
-    g[k] = d0 * nf[k][0] + d1 * nf[k][1];
-    dot += p[k] * g[k];
+  for (int j = 0; j < 4; ++j) {
+    const float inv = 1.f / den[j];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      p[k][j] *= inv;
+      g[k][j] = d0[j] * nf[k][0] + d1[j] * nf[k][1];
+      dot[j] += p[k][j] * g[k][j];
+    }
   }
-  uint16_t* DM = dmask + cell * 576;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) DM[k * 64 + s] = raft_f32_to_bf16(p[k] * (g[k] - dot));
-  // neighbour weights W[k][c] = sum_s p_k d_c, reduced across the wave
+  uint16_t* DM = dmask + cell * 576 + 4 * q;
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    const float w0 = wave_sum(p[k] * d0);
-    const float w1 = wave_sum(p[k] * d1);
-    if (s == 0) {
+    uint32_t lo = (uint32_t)raft_f32_to_bf16(p[k][0] * (g[k][0] - dot[0])) |
+                  ((uint32_t)raft_f32_to_bf16(p[k][1] * (g[k][1] - dot[1])) << 16);
+    uint32_t hi = (uint32_t)raft_f32_to_bf16(p[k][2] * (g[k][2] - dot[2])) |
+                  ((uint32_t)raft_f32_to_bf16(p[k][3] * (g[k][3] - dot[3])) << 16);
+    *reinterpret_cast<uint2*>(DM + k * 64) = make_uint2(lo, hi);
+  }
+  // neighbour weights W[k][c] = sum_s p_k d_c: the lane's 4 sub-pixels, then its 16-lane group
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    float w0 = (p[k][0] * d0[0] + p[k][1] * d0[1]) + (p[k][2] * d0[2] + p[k][3] * d0[3]);
+    float w1 = (p[k][0] * d1[0] + p[k][1] * d1[1]) + (p[k][2] * d1[2] + p[k][3] * d1[3]);
+#pragma unroll
+    for (int m = 8; m > 0; m >>= 1) {
+      w0 += __shfl_xor(w0, m, 16);
+      w1 += __shfl_xor(w1, m, 16);
+    }
+    if (q == 0) {
       wbuf[(b * 18 + 2 * k) * HW + yx] = w0;
       wbuf[(b * 18 + 2 * k + 1) * HW + yx] = w1;
     }
@@ -278,7 +304,7 @@ bool launch_convex_up_nhwc_bwd(const float* flow, const uint16_t* mask, const fl
                                uint16_t* dmask, float* wbuf, float* dflow, int B, int H, int W,
                                hipStream_t stream) {
   const int64_t cells = (int64_t)B * H * W;
-  hipLaunchKernelGGL(convex_up_nhwc_bwd_kernel, dim3(raft_cdiv(cells, 4)), dim3(256), 0, stream,
+  hipLaunchKernelGGL(convex_up_nhwc_bwd_kernel, dim3(raft_cdiv(cells, 16)), dim3(256), 0, stream,
                      flow, mask, dout, dmask, wbuf, B, H, W);
   hipLaunchKernelGGL(convex_up_bwd_flow_kernel, dim3(raft_cdiv(cells, 256)), dim3(256), 0, stream,
                      wbuf, dflow, B, H, W);
