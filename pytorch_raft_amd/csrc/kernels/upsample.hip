@@ -175,39 +175,52 @@ __device__ __forceinline__ void cell_flows(const float* F, int64_t HW, int y, in
   }
 }
 
+// 16 lanes per cell, 4 consecutive sub-pixels per lane (4 cells per wave): 8-B mask reads,
+// 16-B output stores
 __global__ __launch_bounds__(256) void convex_up_nhwc_fwd_kernel(const float* __restrict__ flow,
                                                                  const uint16_t* __restrict__ mask,
                                                                  float* __restrict__ out, int B,
                                                                  int H, int W) {
-  const int s = threadIdx.x & 63;
-  const int64_t cell = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int q = threadIdx.x & 15;
+  const int64_t cell = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int64_t HW = (int64_t)H * W;
   if (cell >= (int64_t)B * HW) return;
   const int64_t b = cell / HW;
   const int yx = (int)(cell - b * HW), y = yx / W, x = yx % W;
   float nf[9][2];
   cell_flows(flow + b * 2 * HW, HW, y, x, H, W, nf);
-  const uint16_t* M = mask + cell * 576;
-  float m[9], mx = -INFINITY;
+  const uint16_t* M = mask + cell * 576 + 4 * q;
+  float m[9][4], mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    m[k] = raft_bf16_to_f32(M[k * 64 + s]);
-    mx = fmaxf(mx, m[k]);
-  }
-  float den = 0.f, o0 = 0.f, o1 = 0.f;
+    const uint2 v = *reinterpret_cast<const uint2*>(M + k * 64);
+    m[k][0] = __uint_as_float(v.x << 16);
+    m[k][1] = __uint_as_float(v.x & 0xffff0000u);
+    m[k][2] = __uint_as_float(v.y << 16);
+    m[k][3] = __uint_as_float(v.y & 0xffff0000u);
 #pragma unroll
-  for (int k = 0; k < 9; ++k) {
-    const float e = __expf(m[k] - mx);
-    den += e;
-    o0 += e * nf[k][0];
-    o1 += e * nf[k][1];
+    for (int j = 0; j < 4; ++j) mx[j] = fmaxf(mx[j], m[k][j]);
   }
-  const float inv = 1.f / den;
+  float o0[4], o1[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float den = 0.f, a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const float e = __expf(m[k][j] - mx[j]);
+      den += e;
+      a0 += e * nf[k][0];
+      a1 += e * nf[k][1];
+    }
+    const float inv = 1.f / den;
+    o0[j] = a0 * inv;
+    o1[j] = a1 * inv;
+  }
   const int64_t W8 = 8 * (int64_t)W;
-  const int64_t o = (int64_t)(8 * y + (s >> 3)) * W8 + 8 * x + (s & 7);
+  const int64_t o = (int64_t)(8 * y + (q >> 1)) * W8 + 8 * x + (q & 1) * 4;
   float* O = out + b * 2 * 64 * HW;
-  O[o] = o0 * inv;
-  O[64 * HW + o] = o1 * inv;
+  *reinterpret_cast<float4*>(O + o) = make_float4(o0[0], o0[1], o0[2], o0[3]);
+  *reinterpret_cast<float4*>(O + 64 * HW + o) = make_float4(o1[0], o1[1], o1[2], o1[3]);
 }
 
 // 16 lanes per cell, 4 consecutive sub-pixels per lane (4 cells per wave): the mask / dmask rows
@@ -295,7 +308,7 @@ __global__ __launch_bounds__(256) void convex_up_nhwc_bwd_kernel(const float* __
 bool launch_convex_up_nhwc_fwd(const float* flow, const uint16_t* mask, float* out, int B, int H,
                                int W, hipStream_t stream) {
   const int64_t cells = (int64_t)B * H * W;
-  hipLaunchKernelGGL(convex_up_nhwc_fwd_kernel, dim3(raft_cdiv(cells, 4)), dim3(256), 0, stream,
+  hipLaunchKernelGGL(convex_up_nhwc_fwd_kernel, dim3(raft_cdiv(cells, 16)), dim3(256), 0, stream,
                      flow, mask, out, B, H, W);
   return true;
 }
