@@ -362,6 +362,10 @@ int mask_kind(const Tensor& m) {
   return m.scalar_type() == at::kBFloat16 ? 1 : 0;
 }
 
+// the NHWC vector kernels move the mask / dmask in 8-B and flow / dout / out in 16-B accesses:
+// a contiguous view with an odd storage offset (a narrowed tensor) takes the scalar kernels
+bool aligned16(const Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; }
+
 // mask is (B,576,H,W) contiguous (nhwc=false) or (B,H,W,576) contiguous (nhwc=true)
 void check_mask(const Tensor& mask, int64_t B, int64_t H, int64_t W, bool nhwc) {
   TORCH_CHECK(mask.is_cuda() && mask.is_contiguous(), "mask must be a contiguous GPU tensor");
@@ -380,7 +384,7 @@ Tensor convex_up_fwd(const Tensor& flow, const Tensor& mask, bool nhwc) {
   c10::DeviceGuard g(flow.device());
   Tensor out = at::empty({B, 2, 8 * H, 8 * W}, flow.options());
   const int64_t HW = H * W;
-  if (nhwc && mask_kind(mask) == 1) {
+  if (nhwc && mask_kind(mask) == 1 && aligned16(flow) && aligned16(mask) && aligned16(out)) {
     launch_convex_up_nhwc_fwd(flow.data_ptr<float>(),
                               reinterpret_cast<const uint16_t*>(mask.data_ptr<at::BFloat16>()),
                               out.data_ptr<float>(), (int)B, (int)H, (int)W, cur_stream());
@@ -406,7 +410,8 @@ std::vector<Tensor> convex_up_bwd(const Tensor& flow, const Tensor& mask, const 
   Tensor dflow = at::empty_like(flow);
   Tensor wbuf = at::empty({B, 18, H, W}, flow.options());
   const int64_t HW = H * W;
-  if (nhwc && mask_kind(mask) == 1) {
+  if (nhwc && mask_kind(mask) == 1 && aligned16(flow) && aligned16(mask) && aligned16(dout) &&
+      aligned16(dmask) && aligned16(dflow)) {
     launch_convex_up_nhwc_bwd(flow.data_ptr<float>(),
                               reinterpret_cast<const uint16_t*>(mask.data_ptr<at::BFloat16>()),
                               dout.data_ptr<float>(),

@@ -32,6 +32,35 @@ from .augmentor import FlowAugmentor, SparseFlowAugmentor
 
 _REPO = osp.dirname(osp.dirname(osp.dirname(osp.abspath(__file__))))
 
+# Worker RNG seed = _WORKER_SEED_BASE + worker id.  The reference seeds worker k with k
+# (`core/datasets.py:45-51`), which under one-process-per-GPU data parallelism would give worker k
+# of EVERY rank the same crop / flip / jitter / eraser stream; ``fetch_dataloader`` sets the base to
+# rank * num_workers inside each worker (``_seed_worker``) so every (rank, worker) pair is distinct.
+_WORKER_SEED_BASE = 0
+
+
+class _seed_worker:
+    """Picklable DataLoader ``worker_init_fn``: records this rank's seed base in the worker."""
+
+    def __init__(self, base):
+        self.base = int(base)
+
+    def __call__(self, worker_id):
+        global _WORKER_SEED_BASE
+        _WORKER_SEED_BASE = self.base
+
+
+def per_rank_batch(global_batch, world, rank=0):
+    """Per-rank batch for a GLOBAL ``--batch_size`` (reference DataParallel semantics).  A batch
+    that does not divide by the world size is rounded down; rank 0 says so, since the effective
+    global batch (and with it the gradient scale per step) differs from the one asked for."""
+    per = max(1, global_batch // world)
+    if per * world != global_batch and rank == 0:
+        import warnings
+        warnings.warn('--batch_size %d is not divisible by %d ranks: training with %d pairs per rank '
+                      '(effective global batch %d)' % (global_batch, world, per, per * world))
+    return per
+
 
 class FlowDataset(data.Dataset):
     def __init__(self, aug_params=None, sparse=False):
@@ -63,9 +92,10 @@ class FlowDataset(data.Dataset):
         if not self.init_seed:
             info = torch.utils.data.get_worker_info()
             if info is not None:
-                torch.manual_seed(info.id)
-                np.random.seed(info.id)
-                random.seed(info.id)
+                seed = _WORKER_SEED_BASE + info.id
+                torch.manual_seed(seed)
+                np.random.seed(seed)
+                random.seed(seed)
                 self.init_seed = True
 
         index = index % len(self.image_list)
@@ -223,14 +253,16 @@ def build_train_dataset(args, TRAIN_DS='C+T+K+S+H'):
 def fetch_dataloader(args, TRAIN_DS='C+T+K+S+H', rank=0, world=1, num_workers=4):
     """Per-stage training loader.  ``args.batch_size`` is the GLOBAL batch (reference semantics)."""
     ds = build_train_dataset(args, TRAIN_DS)
-    per_rank = max(1, args.batch_size // world)
+    per_rank = per_rank_batch(args.batch_size, world, rank)
     sampler = None
     if world > 1:
         sampler = torch.utils.data.distributed.DistributedSampler(ds, num_replicas=world, rank=rank,
                                                                   shuffle=True, drop_last=True)
     loader = data.DataLoader(ds, batch_size=per_rank, pin_memory=torch.cuda.is_available(),
                              shuffle=sampler is None, sampler=sampler, num_workers=num_workers,
-                             drop_last=True, persistent_workers=num_workers > 0)
+                             drop_last=True, persistent_workers=num_workers > 0,
+                             worker_init_fn=_seed_worker(rank * max(1, num_workers)))
     if rank == 0:
-        print('Training with %d image pairs' % len(ds))
+        print('Training with %d image pairs (global batch %d = %d ranks x %d)'
+              % (len(ds), per_rank * world, world, per_rank))
     return loader

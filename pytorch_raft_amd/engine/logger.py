@@ -3,7 +3,9 @@
 Same console format -- ``[{step:6d}, {lr:10.7f}] m1, m2, ...`` with metric names sorted -- and the same
 cadence (printed when ``total_steps % SUM_FREQ == SUM_FREQ - 1``).  Differences, all MI355X-driven:
 
-* metrics are pushed as device tensors and summed on the device; the host syncs once per window;
+* metrics are pushed as device tensors and summed on the device; the host syncs once per window,
+  after ONE all-reduce that averages the window's sums over the data-parallel ranks (the
+  reference's DataParallel loss/metrics are computed on the gathered global batch);
 * TensorBoard is used if importable, otherwise scalars go to ``runs/<name>/scalars.jsonl``;
 * throughput (image pairs / s) is reported alongside the loss metrics.
 """
@@ -56,9 +58,18 @@ class Logger:
 
     def _flush(self):
         keys = sorted(self.running.keys())
-        vals = torch.stack([self.running[k].detach().float().reshape(()) for k in keys]).cpu().tolist()
+        vals = torch.stack([self.running[k].detach().float().reshape(()) for k in keys])
+        # every rank pushes its own shard's metrics: average them over ranks (SURVEY §2.4 "metrics
+        # all-reduced on device every SUM_FREQ steps") -- one small collective per window, and
+        # every rank calls _flush at the same step, so the collective is matched
+        world = 1
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
+            world = torch.distributed.get_world_size()
+            if world > 1:
+                torch.distributed.all_reduce(vals)
+        vals = (vals / world).cpu().tolist()
         means = [v / self.sum_freq for v in vals]
-        lr = self.scheduler.get_last_lr()[0] if self.scheduler is not None else 0.0
+        lr = float(self.scheduler.get_last_lr()[0]) if self.scheduler is not None else 0.0
         line = '[{:6d}, {:10.7f}] '.format(self.total_steps + 1, lr)
         line += ('{:10.4f}, ' * len(means)).format(*means)
         dt = time.time() - self._t0

@@ -15,6 +15,8 @@ Reference: `core/extractor.py:6-56` (ResidualBlock), `:60-116` (BottleneckBlock)
 
 Used automatically by ``_Encoder.forward`` on the GPU under bf16 autocast (``fast_path_ok``).
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -248,7 +250,7 @@ def residual_block(blk, x):
     if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and blk.norm2.affine:
         gamma, beta = blk.norm2.weight, blk.norm2.bias
     # identity shortcut from a previous fused block: its gradient goes through that block's stash
-    res_holder = _HOLDERS.get(id(x)) if blk.downsample is None else None
+    res_holder = _HOLDERS.get(id(x)) if (blk.downsample is None and _STASH) else None
     if res_holder is not None and res_holder[0] is not x:
         res_holder = None
     holder = {}
@@ -258,7 +260,15 @@ def residual_block(blk, x):
     return out
 
 
-_HOLDERS = {}  # id(block output) -> (output, its gradient stash), for the encoder forward in flight
+# id(block output) -> (output, its gradient stash), for the encoder forward in flight.
+# Restriction of the stash: the identity-residual gradient of a fused block's output reaches its
+# producer through the stash, not through autograd, so a tensor hook on an intermediate block
+# output, or ``autograd.grad(..., inputs=[block_out])``, sees the gradient WITHOUT the shortcut
+# term.  Parameter gradients and the encoder-input gradient are exact (the producer node always
+# runs after all consumers of its output).  ``RAFT_ENCODER_STASH=0`` in the environment keeps
+# the shortcut gradient in the autograd graph when intermediate activation gradients are needed.
+_HOLDERS = {}
+_STASH = os.environ.get('RAFT_ENCODER_STASH', '1') != '0'
 
 
 def bottleneck_block(blk, x):

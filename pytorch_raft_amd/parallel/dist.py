@@ -206,7 +206,6 @@ class GradSync:
         ref = b.params[0]
         dev = ref.device
         dtype = self.comm_dtype or ref.dtype
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in b.params]
         s = self._comm_stream(dev)
         if s is not None:
             s.wait_stream(torch.cuda.current_stream(dev))
@@ -216,7 +215,17 @@ class GradSync:
         with ctx:
             if b.flat is None or b.flat.dtype != dtype or b.flat.device != dev:
                 b.flat = torch.empty(b.numel, dtype=dtype, device=dev)
-            torch.cat([g.reshape(-1).to(dtype) for g in grads], out=b.flat)
+            # parameters without a gradient this step contribute zeros: fill their slice of the
+            # flat buffer directly on the comm stream (no main-stream temporaries for it to race)
+            off = 0
+            for p in b.params:
+                n = p.numel()
+                dst = b.flat[off:off + n]
+                if p.grad is None:
+                    dst.zero_()
+                else:
+                    dst.copy_(p.grad.reshape(-1))
+                off += n
             b.flat.div_(self.world)
             b.work = dist.all_reduce(b.flat, async_op=True)
 

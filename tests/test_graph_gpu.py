@@ -1,0 +1,91 @@
+"""hipGraph-captured training step (``engine.trainer.GraphedTrainStep``) vs the eager step.
+
+The graphed step must be the SAME training step: same loss trajectory from the same initial
+state (capture warm-up rolled back), finite gradients equal to the eager ones, and the host cost
+of a step reduced to the replays.  Reference loop: `train.py:161-181`, `core/raft.py:122-139`.
+"""
+import argparse
+import time
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _args(**kw):
+    a = dict(small=False, mixed_precision=True, amp_dtype='bfloat16', alternate_corr=False,
+             dropout=0.0, corr_impl='auto', lr=4e-4, wdecay=1e-4, epsilon=1e-8, num_steps=1000,
+             iters=4, gamma=0.8, clip=1.0, add_noise=False)
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+def _model(args, dev, sd=None):
+    from pytorch_raft_amd.models.raft import RAFT
+    torch.manual_seed(7)
+    m = RAFT(args).to(dev).train()
+    if sd is not None:
+        m.load_state_dict(sd)
+    return m
+
+
+@pytest.mark.parametrize('alt', [False, True])
+def test_graph_step_matches_eager(ext_ops, alt):
+    from pytorch_raft_amd.engine.trainer import TrainState, GraphedTrainStep
+    from pytorch_raft_amd.data.synthetic import device_batches
+    dev = torch.device('cuda', 0)
+    args = _args(alternate_corr=alt)
+    m = _model(args, dev)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    batches = device_batches(4, 128, 192, dev, count=3, seed=3)
+
+    def eager_run():
+        mm = _model(_args(alternate_corr=alt), dev, sd)
+        st = TrainState(mm, _args(alternate_corr=alt), dev)
+        losses = [float(st.step(*batches[k])[0].detach()) for k in range(3)]
+        return losses, torch.cat([p.detach().reshape(-1) for p in mm.parameters()]), st
+
+    eager, w_e1, st = eager_run()
+    _, w_e2, _ = eager_run()   # run-to-run noise of the eager step (MIOpen atomics, bf16)
+
+    m2 = _model(_args(alternate_corr=alt), dev, sd)
+    st2 = TrainState(m2, _args(alternate_corr=alt), dev, graph_ready=True)
+    g = GraphedTrainStep(st2, batches[0], warmup=2)
+    # roll-back: weights are the initial ones again
+    for n, p in m2.named_parameters():
+        assert torch.equal(p.detach(), sd[n]), n
+    graph = [float(g.step(*batches[k])[0].detach()) for k in range(3)]
+    torch.cuda.synchronize()
+    assert g.check_finite()
+    for a, b in zip(eager, graph):
+        assert abs(a - b) <= 2e-3 * abs(a), (eager, graph)
+    w0 = torch.cat([sd[n].reshape(-1) for n, _ in m2.named_parameters()])
+    w_g = torch.cat([p.detach().reshape(-1) for p in m2.parameters()])
+    upd = float((w_e1 - w0).norm())
+    noise = float((w_e2 - w_e1).norm()) / upd
+    err = float((w_g - w_e1).norm()) / upd
+    # the graphed trajectory is as close to eager as eager is to itself
+    assert err <= max(3 * noise, 1e-3), (err, noise)
+    # the scheduler advanced exactly 3 steps in both runs
+    assert st.scheduler.last_epoch == st2.scheduler.last_epoch
+
+
+def test_graph_step_host_cost(ext_ops):
+    from pytorch_raft_amd.engine.trainer import TrainState, GraphedTrainStep
+    from pytorch_raft_amd.data.synthetic import device_batches
+    dev = torch.device('cuda', 0)
+    args = _args(iters=12)
+    m = _model(args, dev)
+    batches = device_batches(2, 128, 192, dev, count=2, seed=5)
+    st = TrainState(m, args, dev, graph_ready=True)
+    g = GraphedTrainStep(st, batches[0], warmup=1)
+    g.step(*batches[1])
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for k in range(5):
+        g.step(*batches[k % 2])
+    host = (time.perf_counter() - t) / 5
+    torch.cuda.synchronize()
+    # eager issues ~1000 launches per step (> 10 ms of host time); two graph replays are ~1 ms
+    assert host < 5e-3, host

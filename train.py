@@ -12,7 +12,7 @@ Differences (additive only):
 * new: ``--alternate_corr`` (differentiable on-the-fly correlation), ``--corr_impl``,
   ``--synthetic`` (no dataset needed), ``--resume`` (optimizer/scheduler/step sidecar),
   ``--val_freq``, ``--sum_freq``, ``--num_workers``, ``--channels_last``, ``--profile``,
-  ``--checkpoint_dir``.
+  ``--checkpoint_dir``, ``--hipgraph`` (graph-replayed training step).
 """
 import argparse
 import os
@@ -75,13 +75,16 @@ def build_parser():
     p.add_argument('--seed', type=int, default=1234)
     p.add_argument('--profile', type=str, default=None, help='write a torch.profiler trace here')
     p.add_argument('--cpu', action='store_true', help='force CPU (gloo) training')
+    p.add_argument('--hipgraph', action='store_true',
+                   help='replay each training step as two hipGraphs (bf16 on a GPU; fixed crop)')
     return p
 
 
 def _synthetic_loader(args, rank, world):
     from pytorch_raft_amd.data.synthetic import SyntheticPairs
     ds = SyntheticPairs(size=tuple(args.image_size), length=max(64, args.batch_size * 8), seed=rank)
-    per_rank = max(1, args.batch_size // world)
+    from pytorch_raft_amd.data.datasets import per_rank_batch
+    per_rank = per_rank_batch(args.batch_size, world, rank)
     return torch.utils.data.DataLoader(ds, batch_size=per_rank, shuffle=True, drop_last=True,
                                        num_workers=0)
 
@@ -98,7 +101,7 @@ def worker(args):
     if device.type == 'cuda':
         # fixed crop size: let MIOpen time its encoder conv solvers once and keep the fastest
         torch.backends.cudnn.benchmark = True
-    torch.manual_seed(args.seed)
+    torch.manual_seed(args.seed)  # identical init on every rank (weights are also broadcast)
     np.random.seed(args.seed)
 
     model = RAFT(args)
@@ -113,6 +116,10 @@ def worker(args):
     if args.stage != 'chairs':
         model.freeze_bn()
     pdist.broadcast_module(model)
+    # after the weights are in sync, every rank draws its own device-side noise / dropout stream
+    # (one DataParallel process would draw different numbers for each replica's slice)
+    torch.manual_seed(args.seed + rank)
+    np.random.seed(args.seed + rank)
 
     if args.synthetic or args.stage is None:
         loader = _synthetic_loader(args, rank, world)
@@ -120,13 +127,16 @@ def worker(args):
         from pytorch_raft_amd.data.datasets import fetch_dataloader
         loader = fetch_dataloader(args, rank=rank, world=world, num_workers=args.num_workers)
 
-    st = TrainState(model, args, device)
+    use_graph = (args.hipgraph and device.type == 'cuda' and args.mixed_precision
+                 and args.amp_dtype == 'bfloat16')
+    st = TrainState(model, args, device, graph_ready=use_graph)
+    stepper = st  # replaced by the graphed step at the first batch (capture needs its shapes)
     total_steps = 0
     if args.resume and args.restore_ckpt is not None:
         s = ckpt.load_training_state(args.restore_ckpt, st.optimizer, st.scheduler, st.scaler)
         if s is not None:
             total_steps = int(s['step'])
-    per_rank = max(1, args.batch_size // world)
+    per_rank = max(1, args.batch_size // world)  # per_rank_batch() already warned on rank 0
     logger = Logger(model, st.scheduler, logdir=args.logdir or os.path.join('runs', args.name),
                     sum_freq=args.sum_freq, enabled=(rank == 0), pairs_per_step=per_rank * world)
     logger.total_steps = total_steps
@@ -148,7 +158,10 @@ def worker(args):
             loader.sampler.set_epoch(epoch)
         for data_blob in loader:
             image1, image2, flow, valid = [x.to(device, non_blocking=True) for x in data_blob]
-            loss, metrics = st.step(image1, image2, flow, valid)
+            if use_graph and stepper is st:
+                from pytorch_raft_amd.engine.trainer import GraphedTrainStep
+                stepper = GraphedTrainStep(st, (image1, image2, flow, valid), warmup=2)
+            loss, metrics = stepper.step(image1, image2, flow, valid)
             logger.push({k: v for k, v in metrics.items() if k != 'loss'})
             if prof is not None:
                 prof.step()
