@@ -74,6 +74,40 @@ std::vector<Tensor> corr_build(const Tensor& f1, const Tensor& f2, int64_t level
   return out;
 }
 
+// bf16 fmaps in NHWC memory, (B,H,W,C) contiguous (the channels_last encoder outputs, permuted)
+std::vector<Tensor> corr_build_bf16(const Tensor& f1, const Tensor& f2, int64_t levels) {
+  TORCH_CHECK(f1.is_cuda() && f2.is_cuda() && f1.scalar_type() == at::kBFloat16 &&
+                  f2.scalar_type() == at::kBFloat16 && f1.is_contiguous() && f2.is_contiguous(),
+              "fmaps must be contiguous bf16 (B,H,W,C) GPU tensors");
+  TORCH_CHECK(f1.dim() == 4 && f1.sizes() == f2.sizes(), "fmap1/fmap2 must be equal (B,H,W,C)");
+  TORCH_CHECK(levels >= 1 && levels <= 4, "levels must be 1..4");
+  const int64_t B = f1.size(0), H = f1.size(1), W = f1.size(2), C = f1.size(3);
+  TORCH_CHECK(C % 16 == 0 && C > 0, "channels must be a multiple of 16");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(f1.data_ptr()) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(f2.data_ptr()) & 15) == 0,
+              "fmaps must be 16-B aligned");
+  c10::DeviceGuard g(f1.device());
+  const int64_t N = H * W;
+  std::vector<Tensor> out;
+  std::vector<float*> ptr;
+  std::vector<int> hs, ws;
+  int64_t h = H, w = W;
+  auto fopt = f1.options().dtype(at::kFloat);
+  for (int64_t l = 0; l < levels; ++l) {
+    TORCH_CHECK(h >= 1 && w >= 1, "feature map too small for ", levels, " pyramid levels");
+    out.push_back(at::empty({B, N, h, w}, fopt));
+    ptr.push_back(out.back().data_ptr<float>());
+    hs.push_back((int)h);
+    ws.push_back((int)w);
+    h /= 2;
+    w /= 2;
+  }
+  launch_corr_build_bf16(reinterpret_cast<const uint16_t*>(f1.data_ptr()),
+                         reinterpret_cast<const uint16_t*>(f2.data_ptr()), ptr.data(), hs.data(),
+                         ws.data(), (int)B, (int)C, (int)H, (int)W, (int)levels, cur_stream());
+  return out;
+}
+
 Tensor corr_lookup_fwd(const std::vector<Tensor>& pyr, const Tensor& coords, int64_t radius) {
   check_cuda_f32(coords, "coords");
   TORCH_CHECK(coords.dim() == 4 && coords.size(1) == 2, "coords must be (B,2,H,W)");
@@ -1187,6 +1221,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] wgs, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
+  m.def("corr_build_bf16(Tensor f1, Tensor f2, int levels) -> Tensor[]");
   m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");
   m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout, bool nhwc=False) -> Tensor[]");
   m.def("corr_lookup_nhwc_(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
@@ -1228,6 +1263,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("fh2_wgrad_", &fh2_wgrad_);
   m.impl("add_relu_", &add_relu_);
   m.impl("relu_mask_", &relu_mask_);
+  m.impl("corr_build_bf16", &corr_build_bf16);
   m.impl("convex_up_fwd", &convex_up_fwd);
   m.impl("convex_up_bwd", &convex_up_bwd);
   m.impl("seq_loss_fwd", &seq_loss_fwd);

@@ -157,6 +157,163 @@ __global__ __launch_bounds__(NT) void corr_build_kernel(const float* __restrict_
   }
 }
 
+// ------------------------------------------------------------------ bf16 NHWC variant
+// Mixed precision: the fmaps are the encoders' bf16 outputs, so a bf16 MFMA with fp32 accumulation
+// (v_mfma_f32_32x32x16_bf16, 16x the f32-MFMA rate) forms exactly the products the reference's fp32
+// matmul forms from them; only the summation order differs.  Both operands are channel-contiguous
+// (NHWC), which is exactly the MFMA fragment layout (8 consecutive K values per lane): fragments go
+// global -> registers as 16-B loads (L2-resident fmaps), no LDS staging.
+//
+// Tile: 64 query pixels i x one 8-row x 64-column band of target pixels j.  Wave w owns target rows
+// y0+2w, y0+2w+1 (2 i-tiles x 4 j-tiles of 32x32).  The band is 8-row / 64-column aligned, so:
+//   level 0 -> stored from the accumulators (32 lanes = 32 consecutive x: 128-B row segments);
+//   level 1 -> the wave's own two rows summed in registers + the neighbour lane (x pair);
+//   levels 2, 3 -> from a 32 KB LDS image of level 1.
+// Floor pooling for odd sizes holds: a level-l cell is written only if it is inside the level-l map,
+// and every such cell's footprint is inside level 0 (h_l = floor(h_{l-1} / 2)).
+constexpr int BB_I = 64, BB_Y = 8, BB_X = 64;
+
+__global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(const uint16_t* __restrict__ f1,
+                                                                 const uint16_t* __restrict__ f2,
+                                                                 Pyr4 out, int C, int H, int W,
+                                                                 int levels, float scale,
+                                                                 int tiles_i, int bands_y,
+                                                                 int tiles_x) {
+  __shared__ float P1[BB_I][4][32 + 1];
+  __shared__ float P2[BB_I][2][16 + 1];
+
+  const int N = H * W;
+  const int b = blockIdx.y;
+  int t = blockIdx.x;
+  const int tx = t % tiles_x;
+  t /= tiles_x;
+  const int by = t % bands_y;
+  const int ti0 = t / bands_y;
+  const int i0 = ti0 * BB_I, y0 = by * BB_Y, x0 = tx * BB_X;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l32 = lane & 31, kh = (lane >> 5) * 8;
+
+  // fragment row pointers (element offsets); out-of-range rows read a valid row, masked to zero
+  const uint16_t* arow[2];
+  bool aok[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int i = i0 + 32 * a + l32;
+    aok[a] = i < N;
+    arow[a] = f1 + ((int64_t)b * N + (aok[a] ? i : 0)) * C + kh;
+  }
+  const uint16_t* brow[4];
+  bool bok[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int y = y0 + 2 * wave + (j >> 1), x = x0 + 32 * (j & 1) + l32;
+    bok[j] = y < H && x < W;
+    brow[j] = f2 + ((int64_t)b * N + (bok[j] ? y * W + x : 0)) * C + kh;
+  }
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][j][r] = 0.f;
+
+  const bf16x8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  bf16x8 fa[2][2], fb[2][4];
+  auto load = [&](int k, int s) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      fa[s][a] = *reinterpret_cast<const bf16x8*>(arow[a] + k);
+      if (!aok[a]) fa[s][a] = zero;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      fb[s][j] = *reinterpret_cast<const bf16x8*>(brow[j] + k);
+      if (!bok[j]) fb[s][j] = zero;
+    }
+  };
+  load(0, 0);
+  const int ksteps = C / 16;
+  for (int kk = 0; kk < ksteps; kk += 2) {
+    if (kk + 1 < ksteps) load((kk + 1) * 16, 1);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[a][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][a], fb[0][j], acc[a][j], 0, 0, 0);
+    if (kk + 1 >= ksteps) break;
+    if (kk + 2 < ksteps) load((kk + 2) * 16, 0);
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[a][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][a], fb[1][j], acc[a][j], 0, 0, 0);
+  }
+
+  // ---- level 0 straight from the accumulators; level 1 from the wave's row pair
+  float* L0 = out.lvl[0];
+  const int h1 = out.h[1], w1 = out.w[1];
+  float* L1 = out.lvl[1];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int il = 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int i = i0 + il;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int y = y0 + 2 * wave + (j >> 1), x = x0 + 32 * (j & 1) + l32;
+        if (i < N && y < H && x < W) L0[(((int64_t)b * N + i) * H + y) * W + x] = acc[a][j][r] * scale;
+      }
+      if (levels > 1) {
+#pragma unroll
+        for (int xh = 0; xh < 2; ++xh) {
+          const float top = acc[a][xh][r] * scale, bot = acc[a][2 + xh][r] * scale;
+          // ((y,x) + (y,x+1)) + ((y+1,x) + (y+1,x+1)), as avg_pool2d sums a 2x2 window
+          const float rt = top + __shfl_xor(top, 1, 64);
+          const float rb = bot + __shfl_xor(bot, 1, 64);
+          const float v = (rt + rb) * 0.25f;
+          if (!(l32 & 1)) {
+            const int Xl = 16 * xh + (l32 >> 1);
+            const int Y = (y0 >> 1) + wave, X = (x0 >> 1) + Xl;
+            P1[il][wave][Xl] = v;
+            if (i < N && Y < h1 && X < w1) L1[(((int64_t)b * N + i) * h1 + Y) * w1 + X] = v;
+          }
+        }
+      }
+    }
+  }
+  if (levels <= 2) return;  // uniform
+  __syncthreads();
+  {
+    float* L2 = out.lvl[2];
+    const int h2 = out.h[2], w2 = out.w[2];
+    for (int e = threadIdx.x; e < BB_I * 2 * 16; e += 256) {
+      const int il = e >> 5, c = e & 31;
+      const int Yl = c >> 4, Xl = c & 15;
+      const float* r0 = &P1[il][2 * Yl][2 * Xl];
+      const float* r1 = &P1[il][2 * Yl + 1][2 * Xl];
+      const float v = ((r0[0] + r0[1]) + (r1[0] + r1[1])) * 0.25f;
+      P2[il][Yl][Xl] = v;
+      const int i = i0 + il, Y = (y0 >> 2) + Yl, X = (x0 >> 2) + Xl;
+      if (i < N && Y < h2 && X < w2) L2[(((int64_t)b * N + i) * h2 + Y) * w2 + X] = v;
+    }
+  }
+  __syncthreads();
+  if (levels > 3) {
+    float* L3 = out.lvl[3];
+    const int h3 = out.h[3], w3 = out.w[3];
+    for (int e = threadIdx.x; e < BB_I * 8; e += 256) {
+      const int il = e >> 3, Xl = e & 7;
+      const float v = ((P2[il][0][2 * Xl] + P2[il][0][2 * Xl + 1]) +
+                       (P2[il][1][2 * Xl] + P2[il][1][2 * Xl + 1])) * 0.25f;
+      const int i = i0 + il, Y = y0 >> 3, X = (x0 >> 3) + Xl;
+      if (i < N && Y < h3 && X < w3) L3[(((int64_t)b * N + i) * h3 + Y) * w3 + X] = v;
+    }
+  }
+}
+
 // dL0 = (G0 + 1/4 up(G1) + 1/16 up(G2) + 1/64 up(G3)) / sqrt(C)   (avg-pool adjoint chain)
 __global__ __launch_bounds__(256) void corr_pyr_grad_reduce_kernel(Pyr4 g, float* __restrict__ out,
                                                                    int64_t planes, int levels,
@@ -196,6 +353,23 @@ void launch_corr_build(const float* f1, const float* f2, float* const* lvl, cons
   dim3 grid(tiles_i * tiles_j, B);
   hipLaunchKernelGGL(corr_build_kernel, grid, dim3(NT), 0, stream, f1, f2, p, C, H, W, levels,
                      sqrtf((float)C), tiles_x, tiles_j);
+}
+
+void launch_corr_build_bf16(const uint16_t* f1, const uint16_t* f2, float* const* lvl, const int* hs,
+                            const int* ws, int B, int C, int H, int W, int levels,
+                            hipStream_t stream) {
+  Pyr4 p;
+  for (int l = 0; l < 4; ++l) {
+    p.lvl[l] = l < levels ? lvl[l] : nullptr;
+    p.h[l] = l < levels ? hs[l] : 0;
+    p.w[l] = l < levels ? ws[l] : 0;
+  }
+  const int N = H * W;
+  const int tiles_i = (int)raft_cdiv(N, BB_I), bands_y = (int)raft_cdiv(H, BB_Y);
+  const int tiles_x = (int)raft_cdiv(W, BB_X);
+  dim3 grid(tiles_i * bands_y * tiles_x, B);
+  hipLaunchKernelGGL(corr_build_bf16_kernel, grid, dim3(256), 0, stream, f1, f2, p, C, H, W,
+                     levels, 1.0f / sqrtf((float)C), tiles_i, bands_y, tiles_x);
 }
 
 void launch_corr_pyr_grad_reduce(float* const* glvl, const int* hs, const int* ws, int64_t planes,

@@ -13,9 +13,10 @@ multi-tensor kernel.  Two execution modes:
 * HIP-graph (``GraphedTrainStep``): RAFT issues thousands of small kernels per step (12 GRU
   iterations forward + backward), so on MI355X the eager step is launch-bound.  The whole
   forward + loss + backward is captured once into a hipGraph (torch.cuda.CUDAGraph == hipGraph on
-  ROCm) and replayed; gradients land in ONE flat buffer (``p.grad`` are views into it), which is
-  all-reduced with a single RCCL call outside the graph, and the clip + fused-AdamW update is a
-  second graph.  The learning rate lives in a device tensor so the OneCycle schedule keeps working
+  ROCm) and replayed; with several ranks the graph packs the gradients into ONE flat buffer,
+  which is all-reduced with a single RCCL call between the replays, and the unpack + clip +
+  fused-AdamW update is a second graph.  The learning rate lives in a device tensor so the
+  OneCycle schedule keeps working
   under replay.
 
 A device-side non-finite flag is accumulated for failure detection and checked at logging cadence.
@@ -120,12 +121,15 @@ class GraphedTrainStep:
         model = st.model
         self.params = [p for p in model.parameters() if p.requires_grad]
         numel = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(numel, device=st.device, dtype=torch.float32)
-        off = 0
+        # Gradients: .grad is None when backward starts, so every AccumulateGrad hands its
+        # incoming gradient over (no zero fill, no add kernel per parameter -- 143 of them when
+        # .grad were views of one persistent buffer).  Captured, those tensors live in the graph
+        # pool at fixed addresses.  With world > 1 the graph ends by packing them into ``flat``
+        # (one cat), which is all-reduced between the two replays and unpacked by the update graph.
+        self.flat = torch.zeros(numel, device=st.device, dtype=torch.float32) if self.world > 1 else None
+        self.grads = None
         for p in self.params:
-            n = p.numel()
-            p.grad = self.flat[off:off + n].view_as(p)
-            off += n
+            p.grad = None
         # learning rate as a device tensor (fused AdamW reads it in-graph)
         self.lr = []
         for g in st.optimizer.param_groups:
@@ -197,20 +201,38 @@ class GraphedTrainStep:
             t.fill_(float(v))
             g['lr'] = t
         st.nonfinite.copy_(snap['nonfinite'])
-        self.flat.zero_()
         torch.cuda.synchronize(st.device)
 
     def _fwd_bwd(self):
-        self.flat.zero_()
-        return self.st.forward_backward(*self.static)
+        for p in self.params:
+            p.grad = None
+        out = self.st.forward_backward(*self.static)
+        for p in self.params:
+            if p.grad is None:  # no gradient this step (keeps the optimizer's tensor list fixed)
+                p.grad = torch.zeros_like(p)
+        self.grads = [p.grad for p in self.params]
+        if self.flat is not None:
+            torch.cat([g.reshape(-1) for g in self.grads], out=self.flat)
+        return out
 
     def _post(self):
         if self.world > 1:
             dist.all_reduce(self.flat)
-            self.flat.div_(self.world)
+
+    def _unpack(self):
+        if self.flat is None:
+            return
+        views, off = [], 0
+        for g in self.grads:
+            n = g.numel()
+            views.append(self.flat[off:off + n].view_as(g))
+            off += n
+        torch._foreach_copy_(self.grads, views)
+        torch._foreach_mul_(self.grads, 1.0 / self.world)
 
     def _update_graphable(self, loss):
         st = self.st
+        self._unpack()
         clip_grad_norm_(self.params, st.args.clip)
         st.optimizer.step()
         st.nonfinite += (~torch.isfinite(loss.detach())).float()

@@ -1,7 +1,7 @@
 """Multi-rank rehearsal of the data-parallel training path on ONE GPU.
 
     RAFT_DIST_BACKEND=gloo python -m torch.distributed.run --nproc-per-node 2 \
-        --master-addr 127.0.0.1 --master-port 29561 scripts/dp_rehearsal.py
+        --master-addr 127.0.0.1 --master-port 29561 scripts/dp_rehearsal.py [--graph]
 
 Every rank runs the fused HIP training path on cuda:0 with its half of a batch; GradSync
 all-reduces the gradients (bucketed, side stream, post-accumulate-grad hooks).  Rank 0 then
@@ -23,7 +23,42 @@ from pytorch_raft_amd.engine.trainer import TrainState  # noqa: E402
 from pytorch_raft_amd.parallel import dist as pdist  # noqa: E402
 
 
+def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl):
+    """The graphed step's DP path: g_fb replay -> flat all-reduce -> g_up replay."""
+    from pytorch_raft_amd.engine.trainer import GraphedTrainStep
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    st = TrainState(model, args, dev, graph_ready=True)
+    assert st.sync is None
+    g = GraphedTrainStep(st, (i1[sl], i2[sl], flow[sl], valid[sl]), warmup=1)
+    g.g_fb.replay()
+    g._post()
+    torch.cuda.synchronize()
+    g_dp = (g.flat / world).float()
+    # two full steps: every rank must hold bit-identical weights afterwards
+    for _ in range(2):
+        g.step(i1[sl], i2[sl], flow[sl], valid[sl])
+    torch.cuda.synchronize()
+    w = torch.cat([p.detach().reshape(-1).float() for p in model.parameters()])
+    ws = [torch.empty_like(w) for _ in range(world)]
+    torch.distributed.all_gather(ws, w)
+    same = all(torch.equal(ws[0], x) for x in ws)
+    if rank == 0:
+        torch.manual_seed(0)
+        ref = RAFT(argparse.Namespace(**vars(args))).to(dev).train()
+        ref.freeze_bn()
+        ref.load_state_dict(sd)
+        st1 = TrainState(ref, args, dev, sync=False)
+        st1.forward_backward(i1, i2, flow, valid)
+        g_full = torch.cat([p.grad.reshape(-1).float() for p in ref.parameters()])
+        rel = ((g_dp - g_full).norm() / g_full.norm()).item()
+        print('dp rehearsal (hipgraph): world=%d backend=%s rel_grad_err=%.3e ranks_identical=%s' %
+              (world, torch.distributed.get_backend(), rel, same), flush=True)
+        assert rel < 2e-2, rel
+        assert same, 'weights diverged across ranks'
+
+
 def main():
+    graph = '--graph' in sys.argv
     dev = pdist.init_distributed()
     rank, world = pdist.rank(), pdist.world_size()
     args = argparse.Namespace(small=False, mixed_precision=True, corr_impl='hip', lr=4e-4,
@@ -35,6 +70,11 @@ def main():
     pdist.broadcast_module(model)
     i1, i2, flow, valid = make_pair_batch(2 * world, 128, 160, device=dev)
     sl = slice(2 * rank, 2 * rank + 2)
+    if graph:
+        graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl)
+        pdist.barrier(dev)
+        pdist.destroy()
+        return
     st = TrainState(model, args, dev)
     assert st.sync is not None and st.sync.enabled
     st.optimizer.zero_grad(set_to_none=True)
