@@ -122,13 +122,18 @@ class CorrBlock:
         self.radius = radius
         self.hip = _use_hip(fmap1, impl)
         if self.hip:
-            # precision='bf16' (mixed precision): the volume and lookups stay fp32, the backward
-            # GEMMs take a bf16 dcorr (the fmaps are bf16 encoder outputs, exact in bf16)
-            self.volume = corr_ops.AllPairsVolume(fmap1.float(), fmap2.float(), num_levels,
+            # precision='bf16' (mixed precision): bf16 fmaps (the encoder outputs, exact in bf16)
+            # go to the bf16-MFMA build as they are; the pyramid and lookups stay fp32 and the
+            # backward GEMMs take a bf16 dcorr.  fp32 fmaps use the exact-f32 MFMA build.
+            if precision == 'bf16' and fmap1.dtype == torch.bfloat16 and fmap1.shape[1] % 16 == 0:
+                f1, f2 = fmap1, fmap2
+            else:
+                f1, f2 = fmap1.float().contiguous(), fmap2.float().contiguous()
+            self.volume = corr_ops.AllPairsVolume(f1, f2, num_levels,
                                                   bf16_backward=(precision == 'bf16'))
             self.corr_pyramid = None
         else:
-            self.corr_pyramid = torch_corr_pyramid(fmap1, fmap2, num_levels)
+            self.corr_pyramid = torch_corr_pyramid(fmap1.float(), fmap2.float(), num_levels)
 
     def __call__(self, coords):
         if self.hip:

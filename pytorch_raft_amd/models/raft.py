@@ -106,8 +106,11 @@ class RAFT(nn.Module):
 
         with self._autocast(dev):
             fmap1, fmap2 = self.fnet([image1, image2])
-        fmap1 = fmap1.float().contiguous()
-        fmap2 = fmap2.float().contiguous()
+        if not (self._bf16_corr_ok(fmap1) and not self.args.alternate_corr):
+            # the reference runs the correlation in fp32 (`core/raft.py:102-103`); the bf16 HIP
+            # build takes the bf16 encoder outputs as they are (same products, fp32 accumulation)
+            fmap1 = fmap1.float().contiguous()
+            fmap2 = fmap2.float().contiguous()
         if self.args.alternate_corr:
             # mixed precision: bf16 MFMA operands; fp32 model: split-bf16 (fp32-accurate) forward
             corr_fn = AlternateCorrBlock(fmap1, fmap2, radius=self.args.corr_radius,
@@ -150,6 +153,10 @@ class RAFT(nn.Module):
         if test_mode:
             return coords1 - coords0, flow_up
         return flow_predictions
+
+    def _bf16_corr_ok(self, fmap):
+        return (fmap.dtype == torch.bfloat16 and self.corr_impl != 'torch' and
+                bool(self.args.mixed_precision) and _ext.device_ok(fmap))
 
     # ------------------------------------------------------------------ fused HIP update path
     def _use_fused_update(self, img):

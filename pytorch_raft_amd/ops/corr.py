@@ -39,15 +39,28 @@ class _State:
         self.bf16_bwd = False
 
 
+def _nhwc_bf16(f):
+    """(B,C,H,W) bf16 (channels_last memory, as the encoders produce it) -> (B,H,W,C) contiguous."""
+    return f.permute(0, 2, 3, 1).contiguous()
+
+
 class _AllPairsBuild(torch.autograd.Function):
     @staticmethod
     def forward(ctx, fmap1, fmap2, levels, state):
         ops = _ext.ops()
-        pyr = ops.corr_build(fmap1, fmap2, levels)
+        ctx.nhwc = fmap1.dtype == torch.bfloat16
+        if ctx.nhwc:
+            # mixed precision: bf16 MFMA straight from the NHWC encoder outputs (no fp32 copy)
+            f1, f2 = _nhwc_bf16(fmap1), _nhwc_bf16(fmap2)
+            pyr = ops.corr_build_bf16(f1, f2, levels)
+            ctx.save_for_backward(f1, f2)
+        else:
+            pyr = ops.corr_build(fmap1, fmap2, levels)
+            ctx.save_for_backward(fmap1, fmap2)
         state.pyramid = pyr
         ctx.state = state
-        ctx.save_for_backward(fmap1, fmap2)
-        token = fmap1.new_zeros(())
+        ctx.shape = tuple(fmap1.shape)
+        token = fmap1.new_zeros((), dtype=torch.float32)
         return token
 
     @staticmethod
@@ -56,11 +69,11 @@ class _AllPairsBuild(torch.autograd.Function):
         fmap1, fmap2 = ctx.saved_tensors
         if st.grad is None and not st.windows and not st.taps:
             return None, None, None, None
-        b, c, h, w = fmap1.shape
+        b, c, h, w = ctx.shape
         dcorr = None
         # mixed precision, window path only: dcorr in bf16 and bf16 GEMMs (fp32 accumulation);
         # the fmaps are bf16 encoder outputs, so only the dcorr rounding differs from fp32
-        bf16 = st.bf16_bwd and st.grad is None and bool(st.windows or st.taps)
+        bf16 = (st.bf16_bwd or ctx.nhwc) and st.grad is None and bool(st.windows or st.taps)
         if st.grad is not None:
             dcorr = _ext.ops().corr_pyr_grad_reduce(st.grad, 1.0 / math.sqrt(c))  # (B, N, N)
         if st.windows:
@@ -77,6 +90,15 @@ class _AllPairsBuild(torch.autograd.Function):
         st.windows = []
         st.taps = []
         st.pyramid = None
+        if ctx.nhwc:
+            # (B,N,C) operands: dF1 = dC F2, dF2 = dC^T F1 -> NHWC results, returned as
+            # channels_last (B,C,H,W) bf16 like the encoder outputs they flow back into
+            dcorr = dcorr.to(torch.bfloat16)
+            f1n = fmap1.view(b, h * w, c)
+            f2n = fmap2.view(b, h * w, c)
+            g1 = torch.bmm(dcorr, f2n).view(b, h, w, c).permute(0, 3, 1, 2)
+            g2 = torch.bmm(dcorr.transpose(1, 2), f1n).view(b, h, w, c).permute(0, 3, 1, 2)
+            return g1, g2, None, None
         f1 = fmap1.view(b, c, h * w)
         f2 = fmap2.view(b, c, h * w)
         if bf16:

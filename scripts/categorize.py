@@ -27,4 +27,4 @@ for line in open(sys.argv[1]):
         tot['other'] = tot.get('other', 0) + ms
 for c, v in sorted(tot.items(), key=lambda x: -x[1]):
     print('%-15s %7.2f' % (c, v))
-print('%-15s %7.2f' % ('total(top70)', sum(tot.values())))
+print('%-15s %7.2f' % ('total', sum(tot.values())))

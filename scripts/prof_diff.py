@@ -24,5 +24,5 @@ for k, (t, c) in b.items():
 tot = sum(r[0] for r in rows)
 print('steady-state kernel time per step: %.3f ms over %d steps (sum of kernel durations)' % (tot / 1e6 / steps, steps))
 print('%7s %8s %9s %10s  %s' % ('pct', 'calls/st', 'avg_us', 'ms/step', 'kernel'))
-for t, c, k in sorted(rows, reverse=True)[:70]:
+for t, c, k in sorted(rows, reverse=True)[:400]:
     print('%6.2f%% %8.1f %9.1f %10.3f  %s' % (100 * t / tot, c / steps, t / c / 1e3, t / 1e6 / steps, k[:140]))

@@ -25,6 +25,10 @@ def _returns():
             h, w = h // 2, w // 2
         return out
 
+    def corr_build_bf16(f1, f2, levels):
+        b, h, w, c = f1.shape
+        return corr_build(f1.permute(0, 3, 1, 2), f2, levels)
+
     def lookup(pyr, coords, r):
         b, _, h, w = coords.shape
         return torch.zeros(b, len(pyr) * (2 * r + 1) ** 2, h, w)
@@ -58,7 +62,7 @@ def _returns():
         return torch.zeros(coords[0].shape[0], h * w, h * w,
                            dtype=torch.bfloat16 if bf16 else torch.float32)
 
-    return {'corr_build': corr_build, 'corr_lookup_fwd': lookup, 'corr_pyr_grad_reduce': reduce,
+    return {'corr_build': corr_build, 'corr_build_bf16': corr_build_bf16, 'corr_lookup_fwd': lookup, 'corr_pyr_grad_reduce': reduce,
             'corr_window_grad': win_grad, 'corr_window_reduce': win_reduce,
             'corr_tap_reduce': tap_reduce,
             'convex_up_fwd': cup_fwd, 'convex_up_bwd': cup_bwd, 'seq_loss_fwd': loss_fwd,

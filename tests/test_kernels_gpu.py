@@ -39,6 +39,48 @@ def test_corr_build_matches_torch(ext_ops, shape):
         torch.testing.assert_close(g, r, atol=2e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize('shape', [(2, 256, 16, 20), (2, 256, 46, 62), (1, 128, 13, 19),
+                                   (1, 256, 11, 70), (1, 256, 55, 128)])
+def test_corr_build_bf16_matches_torch(ext_ops, shape):
+    """bf16-MFMA build from NHWC bf16 fmaps vs the fp32 pyramid of the same (bf16-valued) maps:
+    identical products, fp32 accumulation in another order.  Odd sizes exercise floor pooling,
+    W > 64 the multi-band column tiling."""
+    b, c, h, w = shape
+    f1 = torch.randn(b, h, w, c, device=DEV).to(torch.bfloat16)
+    f2 = torch.randn(b, h, w, c, device=DEV).to(torch.bfloat16)
+    levels = 4 if min(h, w) >= 8 else 3
+    got = ext_ops.corr_build_bf16(f1, f2, levels)
+    ref = torch_corr_pyramid(f1.permute(0, 3, 1, 2).float(), f2.permute(0, 3, 1, 2).float(), levels)
+    for g, r in zip(got, ref):
+        r = r.view(b, h * w, *r.shape[-2:])
+        assert g.shape == r.shape
+        torch.testing.assert_close(g, r, atol=2e-4, rtol=1e-4)
+
+
+def test_corrblock_bf16_fmaps_fwd_bwd(ext_ops):
+    """Mixed-precision CorrBlock: bf16 channels_last fmaps in (as the encoders produce them),
+    fp32 lookups out, bf16 fmap gradients back (bf16 dcorr: ~1e-2 relative)."""
+    b, c, h, w = 2, 256, 23, 30
+    g = torch.Generator(device='cpu').manual_seed(1)
+    f1 = torch.randn(b, c, h, w, generator=g).to(DEV, torch.bfloat16)
+    f2 = torch.randn(b, c, h, w, generator=g).to(DEV, torch.bfloat16)
+    f1 = f1.contiguous(memory_format=torch.channels_last).requires_grad_()
+    f2 = f2.contiguous(memory_format=torch.channels_last).requires_grad_()
+    coords = _coords(b, h, w, spread=3.0)
+    r1 = f1.detach().float().requires_grad_()
+    r2 = f2.detach().float().requires_grad_()
+    ref = torch_corr_lookup(torch_corr_pyramid(r1, r2, 4), coords, 4)
+    blk = CorrBlock(f1, f2, num_levels=4, radius=4, impl='hip', precision='bf16')
+    out = blk.lookup_nhwc(coords, 384)[..., :324].permute(0, 3, 1, 2).float()
+    assert _rel(out, ref) < 5e-3
+    gout = torch.randn_like(ref)
+    (ref * gout).sum().backward()
+    (out * gout).sum().backward()
+    assert f1.grad.dtype == torch.bfloat16 and f1.grad.shape == f1.shape
+    assert _rel(f1.grad.float(), r1.grad) < 2e-2
+    assert _rel(f2.grad.float(), r2.grad) < 2e-2
+
+
 @pytest.mark.parametrize('radius,c', [(4, 256), (3, 128)])
 @pytest.mark.parametrize('hw', [(16, 20), (13, 19)])
 def test_lookup_fwd_bwd_matches_grid_sample(ext_ops, radius, c, hw):

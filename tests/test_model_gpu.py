@@ -108,10 +108,12 @@ def test_wgrad_overlap_matches_inline(ext_ops):
     # MIOpen's encoder convs are not bitwise reproducible from run to run (solver choice), which
     # moves every update-block gradient by up to ~1 % between identical runs; a lost or stale
     # weight-gradient contribution on the side stream would be far larger than that
+    # (norm-wise: a near-cancelling fp32 atomic sum such as a tiny bias gradient can move by a few
+    # % of its max element when only the atomics' order changes)
     for a, a2, b in zip(*runs):
-        noise = (a - a2).abs().max().item()
-        scale = a.abs().max().item()
-        diff = (a - b).abs().max().item()
+        noise = (a - a2).norm().item()
+        scale = a.norm().item()
+        diff = (a - b).norm().item()
         assert diff <= 4 * noise + 3e-2 * scale + 1e-7, (diff, noise, scale)
         cos = torch.nn.functional.cosine_similarity(a.reshape(1, -1), b.reshape(1, -1)).item()
         assert cos > 0.999, cos
