@@ -126,12 +126,18 @@ def main(argv=None):
 
     host_issue = []
 
+    last_note = [time.perf_counter()]
+
     def run(n):
         for k in range(n):
             i1, i2, fl, va = batches[k % len(batches)]
             t_issue = time.perf_counter()
             stepper.step(i1, i2, fl, va)
             host_issue.append(time.perf_counter() - t_issue)
+            if rank == 0 and time.perf_counter() - last_note[0] > 20.0:
+                # liveness for long (fp32 / stock) runs; stdout stays the single JSON line
+                print('bench: step %d/%d issued' % (k + 1, n), file=sys.stderr, flush=True)
+                last_note[0] = time.perf_counter()
 
     run(a.warmup)
     if device.type == 'cuda':

@@ -288,6 +288,7 @@ class _State:
         self.overlap = False
         self.params = []
         self.n_iter = 0        # iterations issued through this block (forward order)
+        self.next_bwd = None   # iteration whose backward must run next (strictly n_iter-1 .. 0)
         self.dinp_acc = None   # fp32 gradient w.r.t. the context input, summed over iterations
 
 
@@ -302,6 +303,12 @@ class _UpdateWeights(torch.autograd.Function):
     @staticmethod
     def backward(ctx, _tok):
         st = ctx.state
+        if st.dinp_acc is not None:
+            # the context gradient is handed to autograd by iteration 0's backward; a partial
+            # backward (autograd.grad over a subset of the iterations) would silently drop it
+            raise RuntimeError('fused update block: the backward must run through every GRU '
+                               'iteration down to iteration 0 (partial autograd.grad over the '
+                               'iterations is not supported; use update_impl="torch")')
         pk = st.packed
         st.packed = None
         if st.overlap and pk.device.type == 'cuda':
@@ -473,7 +480,17 @@ class _UpdateIter(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gh, gdelta, gmask):
-        pk = ctx.state.packed
+        st = ctx.state
+        # the shared context gradient is accumulated across the iterations' backwards in one
+        # buffer (see below), which needs them strictly in reverse order n-1 .. 0
+        if st.next_bwd is None:
+            # iterations after the last one that received a gradient never run their backward
+            st.next_bwd = ctx.itr
+        if ctx.itr != st.next_bwd:
+            raise RuntimeError('fused update block: iteration %d backward ran out of order '
+                               '(expected %d)' % (ctx.itr, st.next_bwd))
+        st.next_bwd -= 1
+        pk = st.packed
         (corr, patch, c1, cf, f1, mf, inp, h0, z1, rh1, r1, q1, h1, z2, rh2, r2, q2, h2, fm) = \
             ctx.saved_tensors
         B, H, W, _ = h2.shape
@@ -520,7 +537,6 @@ class _UpdateIter(torch.autograd.Function):
         # inp is shared by every iteration: its gradient accumulates in ONE fp32 buffer across
         # the iterations' backwards (11 -> 0, in that order since each needs the next one's dh)
         # and is handed to autograd once, by iteration 0 -- instead of 12 bf16 casts + 11 adds
-        st = ctx.state
         acc_inp = st.dinp_acc is not None
         if not acc_inp:
             st.dinp_acc = _f32(sh + (HD,), dev)
@@ -564,6 +580,7 @@ class _UpdateIter(torch.autograd.Function):
         dgrad('c1', [(dpre_c1, 0, 256)], [(dcorr, 0, CORR_BUF, 324, 0)])  # slots 324.. unused
         if ctx.itr == 0:
             st.dinp_acc = None
+            st.next_bwd = None
         else:
             dinp = None
         # token: no gradient value (autograd still runs the weight node after every iteration)

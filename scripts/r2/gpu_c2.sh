@@ -1,0 +1,18 @@
+#!/bin/bash
+set -o pipefail
+cd "$(dirname "$0")/../.."
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_update_hip_gpu.py tests/test_kernels_gpu.py -m gpu -x -q --timeout 280 --timeout-method thread > gpurun_out/c2_pytest.log 2>&1
+rc=$?
+tail -4 gpurun_out/c2_pytest.log
+if [ $rc -ne 0 ]; then grep -E "Error|assert|FAILED|bad" gpurun_out/c2_pytest.log | head -30; fi
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --alternate_corr > gpurun_out/c2_bench_alt.log 2>&1 || exit 1
+grep metric gpurun_out/c2_bench_alt.log | cut -c1-300
+timeout -k 10 600 python bench.py --steps 50 --warmup 10 --impl torch > gpurun_out/c2_stock_bf16.log 2>&1 || exit 1
+grep metric gpurun_out/c2_stock_bf16.log | cut -c1-300
+timeout -k 10 900 python bench.py --steps 50 --warmup 10 --impl torch --precision fp32 > gpurun_out/c2_stock_fp32.log 2>&1 || exit 1
+grep metric gpurun_out/c2_stock_fp32.log | cut -c1-300
+bash scripts/gpu_profile.sh c2alt --alternate_corr > /dev/null 2>&1
+python scripts/categorize.py gpurun_out/c2alt_summary.txt > gpurun_out/c2alt_categories.txt 2>&1
+head -12 gpurun_out/c2alt_summary.txt | cut -c1-200; cat gpurun_out/c2alt_categories.txt

@@ -309,3 +309,27 @@ def test_tap_reduce_matches_window_path(ext_ops, radius, levels, hw):
     torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-5)
     got16 = ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, True)
     torch.testing.assert_close(got16.float(), ref, atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize('convention', ['reference', 'exact'])
+@pytest.mark.parametrize('shape', [(1, 3, 37, 53), (2, 3, 64, 96)])
+def test_warp_sampler_matches_grid_sample(ext_ops, convention, shape):
+    """sampler.hip (demo warping, reference `demo_warp.py:27-56`) vs F.grid_sample: forward and
+    both gradients, with flows that push samples off the image (zero padding)."""
+    from pytorch_raft_amd.ops.sampler import warp_image, torch_warp
+    b, c, h, w = shape
+    g = torch.Generator(device='cpu').manual_seed(11)
+    x = (torch.rand(shape, generator=g) * 255).to(DEV).requires_grad_(True)
+    flo = (torch.randn(b, 2, h, w, generator=g) * 6).to(DEV)
+    flo[:, 0, :, :4] -= 20.0      # off the left edge
+    flo = flo.requires_grad_(True)
+    out = warp_image(x, flo, convention=convention, impl='hip')
+    x2 = x.detach().clone().requires_grad_(True)
+    f2 = flo.detach().clone().requires_grad_(True)
+    ref = torch_warp(x2, f2, convention)
+    torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-4)
+    gout = torch.randn_like(ref)
+    (out * gout).sum().backward()
+    (ref * gout).sum().backward()
+    torch.testing.assert_close(x.grad, x2.grad, atol=2e-3, rtol=1e-4)
+    torch.testing.assert_close(flo.grad, f2.grad, atol=5e-2, rtol=1e-3)

@@ -166,3 +166,85 @@ def test_f1_patch_matches_unfold(ext_ops):
     assert (patch[..., 98:] == 0).all()
     assert torch.equal(slot[..., 126:], flow.permute(0, 2, 3, 1).to(torch.bfloat16))
     assert (slot[..., :126] == 0).all()
+
+
+def test_fused_iterations_match_eager_bf16_same_precision(ext_ops):
+    """The fused HIP update block (bf16 activations, fp32 MFMA accumulation) vs the eager
+    BasicUpdateBlock under bf16 autocast (`core/update.py:114-136`) -- the same precision -- and
+    both vs an fp32 eager oracle, chained over 3 GRU iterations.
+
+    * forward: per-iteration h / delta / mask within 1e-2 (norm-relative) of eager bf16;
+    * backward: every parameter gradient and the h0 / inp / corr gradients at least as close to
+      the fp32 oracle as eager bf16 autocast is (x1.5 + 1e-2 slack).  Eager autocast rounds every
+      intermediate gradient to bf16 while the fused backward keeps the accumulating gradients
+      (dh, d inp, d motion features) in fp32, so eager bf16 itself sits several % from fp32 on
+      the deepest (motion-encoder) gradients -- a bound of 1e-2 against eager bf16 would test
+      eager's rounding, not the kernels."""
+    from pytorch_raft_amd.models.update import BasicUpdateBlock
+    from pytorch_raft_amd.ops.update_hip import HipUpdateBlock, CORR_BUF
+    args = argparse.Namespace(corr_levels=4, corr_radius=4)
+    torch.manual_seed(0)
+    ub = BasicUpdateBlock(args, hidden_dim=128).to(DEV)
+    B, H, W, T = 2, 23, 31, 3
+    g = torch.Generator(device=DEV).manual_seed(5)
+    h0 = torch.tanh(torch.randn(B, 128, H, W, device=DEV, generator=g)).to(torch.bfloat16)
+    inp = torch.relu(torch.randn(B, 128, H, W, device=DEV, generator=g)).to(torch.bfloat16)
+    corrs = [torch.randn(B, 324, H, W, device=DEV, generator=g).to(torch.bfloat16) for _ in range(T)]
+    flows = [torch.randn(B, 2, H, W, device=DEV, generator=g) * 3 for _ in range(T)]
+    Rh = [torch.randn(B, 128, H, W, device=DEV, generator=g) for _ in range(T)]
+    Rd = [torch.randn(B, 2, H, W, device=DEV, generator=g) for _ in range(T)]
+    Rm = [torch.randn(B, 576, H, W, device=DEV, generator=g) for _ in range(T)]
+
+    def run(mode):
+        ub.zero_grad(set_to_none=True)
+        dt = torch.float32 if mode == 'fp32' else torch.bfloat16
+        h = h0.to(dt).requires_grad_(True)
+        x = inp.to(dt).requires_grad_(True)
+        cs = [c.to(dt).requires_grad_(True) for c in corrs]
+        outs, loss = [], 0.0
+        if mode == 'fused':
+            hub = HipUpdateBlock(ub)
+            hh = h.permute(0, 2, 3, 1).contiguous()
+            xx = x.permute(0, 2, 3, 1).contiguous()
+            for t in range(T):
+                cb = torch.nn.functional.pad(cs[t].permute(0, 2, 3, 1), (0, CORR_BUF - 324))
+                hh, delta, mask = hub(hh, xx, cb.contiguous(), flows[t])
+                outs.append((hh.permute(0, 3, 1, 2).float(), delta.float(),
+                             mask.permute(0, 3, 1, 2).float()))
+        else:
+            hh = h
+            for t in range(T):
+                with torch.autocast('cuda', dtype=torch.bfloat16, enabled=(mode == 'bf16')):
+                    hh, mask, delta = ub(hh, x, cs[t], flows[t])
+                outs.append((hh.float(), delta.float(), mask.float()))
+        for t, (hn, d, mk) in enumerate(outs):
+            loss = loss + (hn * Rh[t]).sum() + (d * Rd[t]).sum() + (mk * Rm[t]).sum()
+        loss.backward()
+        grads = {n: p.grad.detach().float().clone() for n, p in ub.named_parameters()}
+        grads['d_h0'] = h.grad.float()
+        grads['d_inp'] = x.grad.float()
+        for t in range(T):
+            grads['d_corr%d' % t] = cs[t].grad.float()
+        return outs, grads
+
+    o_32, g_32 = run('fp32')
+    o_bf, g_bf = run('bf16')
+    o_fu, g_fu = run('fused')
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+    bad, report = [], []
+    for t in range(T):
+        for k, name in enumerate(('h', 'delta', 'mask')):
+            r = rel(o_fu[t][k], o_bf[t][k])
+            report.append(('iter%d.%s vs eager-bf16' % (t, name), round(r, 5)))
+            if r > 1e-2:
+                bad.append(report[-1])
+    for n in g_32:
+        e_fu, e_bf = rel(g_fu[n], g_32[n]), rel(g_bf[n], g_32[n])
+        report.append((n, 'fused %.4f / eager-bf16 %.4f vs fp32' % (e_fu, e_bf)))
+        if e_fu > 1.5 * e_bf + 1e-2:
+            bad.append(report[-1])
+    print('\n'.join('%s: %s' % r for r in report))
+    assert not bad, '\n'.join('%s: %s' % r for r in bad)
