@@ -91,7 +91,8 @@ def build(force=False, jobs=None, verbose=False):
         jobs_list.append([HIPCC] + flags + ['-c', bsrc, '-o', bobj])
 
     # ---- CPU helper library (data pipeline)
-    cpu_srcs = sorted(glob.glob(os.path.join(CSRC, 'cpu', '*.cpp')))
+    cpu_srcs = sorted(f for f in glob.glob(os.path.join(CSRC, 'cpu', '*.cpp'))
+                      if not f.endswith('sanitize_main.cpp'))
     cpu_objs = []
     for src in cpu_srcs:
         obj = os.path.join(BUILD, 'cpu_' + os.path.basename(src) + '.o')
@@ -118,12 +119,41 @@ def build(force=False, jobs=None, verbose=False):
     return OUT
 
 
+SANITIZE_FLAGS = ['-fsanitize=address,undefined,float-cast-overflow', '-fno-sanitize-recover=all',
+                  '-fno-omit-frame-pointer', '-g', '-O1', '-std=c++17']
+
+
+def build_sanitized(run=True):
+    """Host-code sanitizer build: csrc/cpu/*.cpp + the csrc/cpu/sanitize_main.cpp driver linked into
+    one ASan/UBSan executable (no GPU code involved), optionally run.  Returns (path, output)."""
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, 'cpu', '*.cpp')))
+    exe = os.path.join(BUILD, 'imgproc_sanitize')
+    if _newer(exe, srcs + glob.glob(os.path.join(CSRC, 'cpu', '*.h'))):
+        _run(['g++'] + SANITIZE_FLAGS + srcs + ['-o', exe])
+    out = ''
+    if run:
+        env = dict(os.environ, ASAN_OPTIONS='detect_leaks=1:abort_on_error=0',
+                   UBSAN_OPTIONS='print_stacktrace=1')
+        r = subprocess.run([exe], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+        out = r.stdout
+        if r.returncode != 0:
+            raise RuntimeError('sanitizer run failed (%d):\n%s' % (r.returncode, out))
+    return exe, out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--force', action='store_true')
     ap.add_argument('-j', type=int, default=None)
     ap.add_argument('-v', action='store_true')
+    ap.add_argument('--sanitize', action='store_true',
+                    help='build + run the ASan/UBSan executable of the CPU image runtime')
     a = ap.parse_args(argv)
+    if a.sanitize:
+        exe, out = build_sanitized()
+        print(out.strip())
+        return
     out = build(force=a.force, jobs=a.j, verbose=a.v)
     print('built', out)
 

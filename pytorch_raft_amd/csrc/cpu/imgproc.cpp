@@ -63,6 +63,12 @@ void raft_remap_linear_f32(const float* src, int h, int w, int c, const float* m
         for (int k = 0; k < c; ++k) out[k] = 0.f;
         continue;
       }
+      // a coordinate beyond the +-1 pixel border samples only zeros; clamping first keeps the
+      // float -> int conversion defined for any finite map value (UBSan float-cast-overflow)
+      if (mx <= -1.f || my <= -1.f || mx >= (float)w || my >= (float)h) {
+        for (int k = 0; k < c; ++k) out[k] = 0.f;
+        continue;
+      }
       const int x0 = (int)std::floor(mx), y0 = (int)std::floor(my);
       const float ax = mx - x0, ay = my - y0;
       float wts[4] = {(1 - ax) * (1 - ay), ax * (1 - ay), (1 - ax) * ay, ax * ay};
