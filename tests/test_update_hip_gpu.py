@@ -198,9 +198,9 @@ def test_fused_iterations_match_eager_bf16_same_precision(ext_ops):
     def run(mode):
         ub.zero_grad(set_to_none=True)
         dt = torch.float32 if mode == 'fp32' else torch.bfloat16
-        h = h0.to(dt).requires_grad_(True)
-        x = inp.to(dt).requires_grad_(True)
-        cs = [c.to(dt).requires_grad_(True) for c in corrs]
+        h = h0.detach().to(dt).clone().requires_grad_(True)
+        x = inp.detach().to(dt).clone().requires_grad_(True)
+        cs = [c.detach().to(dt).clone().requires_grad_(True) for c in corrs]
         outs, loss = [], 0.0
         if mode == 'fused':
             hub = HipUpdateBlock(ub)
