@@ -24,6 +24,9 @@ sys.path.insert(0, HERE)
 
 METRIC = ('training image-pairs/sec (whole node), RAFT FlyingChairs 368x496 iters=12, '
           'at 1/2/4/8 MI355X')
+# stock PyTorch-ROCm execution of the reference semantics on one MI355X (bf16
+# autocast, batch 12, 10 warm-up / 50 timed steps) -- scaled ideally to N GPUs for vs_baseline
+STOCK_BF16_PAIRS_PER_GPU = 113.19
 
 
 def parse(argv=None):
@@ -206,7 +209,8 @@ def main(argv=None):
         'ms_per_step': round(1000.0 * elapsed / a.steps, 3),
         'higher_is_better': True,
         'scaling': 'weak',
-        'vs_baseline': None,
+        'vs_baseline': (round(value / (STOCK_BF16_PAIRS_PER_GPU * world), 3)
+                        if metric == METRIC else None),
         'dtype': a.precision,
         'data': 'synthetic (random smooth texture pairs, %dx%d, generated on device; random-init weights)' % (h, w),
         'config': {
