@@ -49,6 +49,8 @@ def parse(argv=None):
                     help='issue every kernel eagerly (RCCL buckets overlapped with backward)')
     ap.add_argument('--profile', type=str, default=None, help='torch.profiler trace dir')
     ap.add_argument('--json_out', type=str, default=None)
+    ap.add_argument('--trace_markers', action='store_true',
+                    help='launch a marker spin kernel right before and after the timed steps')
     ap.add_argument('--roctx_region', action='store_true',
                     help='bracket the timed steps with roctxProfilerResume/Pause '
                          '(use with rocprofv3 --selected-regions)')
@@ -172,12 +174,20 @@ def main(argv=None):
     roctx = _roctx() if a.roctx_region else None
     if roctx is not None:
         roctx.roctxProfilerResume(0)
+    if a.trace_markers and device.type == 'cuda':
+        # a tiny spin kernel on each side of the timed steps: scripts/prof_diff.py --markers
+        # aggregates exactly the kernels between them in a plain --kernel-trace
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(a.steps)
     if device.type == 'cuda':
         torch.cuda.synchronize()
     pdist.barrier(device)
     elapsed = time.perf_counter() - t0
+    if a.trace_markers and device.type == 'cuda':
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     if roctx is not None:
         roctx.roctxProfilerPause(0)
     if prof is not None:

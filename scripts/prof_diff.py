@@ -2,6 +2,7 @@
 
 usage: prof_diff.py <dir_warm_only> <dir_warm_plus_steps> <steps>
        prof_diff.py --single <dir_of_timed_region_trace> <steps>
+       prof_diff.py --markers <dir_of_full_trace> <steps>   (bench.py --trace_markers)
 """
 import csv, glob, os, sys
 
@@ -16,7 +17,23 @@ def load(d):
     return out
 
 
-if sys.argv[1] == '--single':   # one trace restricted to the timed region (roctx selected regions)
+def load_between_markers(d):
+    """Kernels dispatched between the last two marker spin kernels (bench.py --trace_markers)."""
+    f = glob.glob(os.path.join(d, '**', '*kernel_trace.csv'), recursive=True)
+    rows = sorted(csv.DictReader(open(f[0])), key=lambda r: int(r['Start_Timestamp']))
+    marks = [i for i, r in enumerate(rows) if 'spin' in r['Kernel_Name'].lower() or 'sleep' in r['Kernel_Name'].lower()]
+    assert len(marks) >= 2, 'no marker kernels in the trace'
+    i0, i1 = marks[-2], marks[-1]
+    out = {}
+    for r in rows[i0 + 1:i1]:
+        t, c = out.get(r['Kernel_Name'], (0.0, 0))
+        out[r['Kernel_Name']] = (t + int(r['End_Timestamp']) - int(r['Start_Timestamp']), c + 1)
+    return out
+
+
+if sys.argv[1] == '--markers':
+    a, b, steps = {}, load_between_markers(sys.argv[2]), int(sys.argv[3])
+elif sys.argv[1] == '--single':   # one trace restricted to the timed region (roctx selected regions)
     a, b, steps = {}, load(sys.argv[2]), int(sys.argv[3])
 else:
     a, b, steps = load(sys.argv[1]), load(sys.argv[2]), int(sys.argv[3])

@@ -1,0 +1,79 @@
+"""Per-kernel PMC summary of a profiled training step (three rocprofv3 --pmc passes).
+
+usage: pmc_summary.py <pass1_dir> <pass2_dir> <pass3_dir> <steps>
+Columns (per kernel name, summed over its dispatches per step):
+  ms      kernel time (kernel trace of pass 1)
+  mfma%   SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x duration x 2.4 GHz): share of the chip's bf16
+          MFMA peak the kernel's matrix pipes were busy (at max clock)
+  wait%   SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers)
+  inst%   SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (issue stalls)
+  ldsbc   SQ_LDS_BANK_CONFLICT cycles per dispatch (x1e3)
+  rdGB wrGB  HBM-side bytes: FETCH_SIZE x 2 (gfx950 reports half of a wide streaming read,
+          MI355X_MICROARCH.md) and WRITE_SIZE, per step
+  TB/s    (rd + wr) / ms
+"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+
+def counters(d):
+    f = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
+    out = defaultdict(lambda: defaultdict(float))
+    calls = defaultdict(set)
+    if not f:
+        return out, calls
+    ids = window_ids(d)
+    for r in csv.DictReader(open(f[0])):
+        if r.get('Dispatch_Id') not in ids:
+            continue
+        k = r['Kernel_Name']
+        out[k][r['Counter_Name']] += float(r['Counter_Value'])
+        calls[k].add(r.get('Dispatch_Id', r.get('Correlation_Id', '')))
+    return out, calls
+
+
+def _window(d):
+    """kernel-trace rows between the last two marker spin kernels (bench.py --trace_markers)"""
+    f = glob.glob(os.path.join(d, '**', '*kernel_trace.csv'), recursive=True)
+    rows = sorted(csv.DictReader(open(f[0])), key=lambda r: int(r['Start_Timestamp']))
+    marks = [i for i, r in enumerate(rows) if 'spin' in r['Kernel_Name'].lower() or 'sleep' in r['Kernel_Name'].lower()]
+    return rows[marks[-2] + 1:marks[-1]]
+
+
+def durations(d):
+    out = defaultdict(float)
+    for r in _window(d):
+        out[r['Kernel_Name']] += (float(r['End_Timestamp']) - float(r['Start_Timestamp'])) * 1e-6
+    return out
+
+
+def window_ids(d):
+    return {r.get('Dispatch_Id') for r in _window(d)}
+
+
+c1, n1 = counters(sys.argv[1])
+c2, _ = counters(sys.argv[2])
+c3, _ = counters(sys.argv[3])
+dur = durations(sys.argv[1])
+steps = int(sys.argv[4])
+rows = []
+for k, ms in dur.items():
+    ms /= steps
+    a = c1.get(k, {})
+    wc = a.get('SQ_WAVE_CYCLES', 0.0) or 1.0
+    mfma = a.get('SQ_VALU_MFMA_BUSY_CYCLES', 0.0) / steps / (1024 * ms * 1e-3 * 2.4e9) if ms > 0 else 0
+    rd = c2.get(k, {}).get('FETCH_SIZE', 0.0) * 2 / steps / 1e6   # KB -> GB
+    wr = c3.get(k, {}).get('WRITE_SIZE', 0.0) / steps / 1e6
+    rows.append((ms, k, 100 * mfma, 100 * a.get('SQ_WAIT_ANY', 0) / wc, 100 * a.get('SQ_WAIT_INST_ANY', 0) / wc,
+                 a.get('SQ_LDS_BANK_CONFLICT', 0) / max(1, len(n1.get(k, ()))) / 1e3, rd, wr,
+                 (rd + wr) / ms if ms > 0 else 0))
+rows.sort(reverse=True)
+tot = sum(r[0] for r in rows)
+print('timed-region kernel time per step: %.3f ms; HBM rd %.2f GB, wr %.2f GB per step' % (
+    tot, sum(r[6] for r in rows), sum(r[7] for r in rows)))
+print('%8s %6s %6s %6s %8s %7s %7s %6s  %s' % ('ms', 'mfma%', 'wait%', 'inst%', 'ldsbc_k', 'rdGB', 'wrGB', 'TB/s', 'kernel'))
+for r in rows[:60]:
+    print('%8.3f %6.1f %6.1f %6.1f %8.1f %7.3f %7.3f %6.2f  %s' % (r[0], r[2], r[3], r[4], r[5], r[6], r[7], r[8], r[1][:110]))
