@@ -202,6 +202,7 @@ def main(argv=None):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t.item())
     peak = torch.cuda.max_memory_allocated(device) / 2 ** 30 if device.type == 'cuda' else 0.0
+    nonfinite_steps = float(st.nonfinite.item())
     ok = st.check_finite()
     pairs = a.batch * world * a.steps
     value = pairs / elapsed
@@ -237,6 +238,7 @@ def main(argv=None):
         },
         'peak_hbm_gib_rank0': round(peak, 2),
         'loss_finite': ok,
+        'nonfinite_steps': nonfinite_steps,
         # host time to issue one step (asynchronous launches); ~= ms_per_step means host-bound
         'host_issue_ms': round(1000.0 * sum(host_issue[-a.steps:]) / max(1, a.steps), 3),
     }

@@ -103,31 +103,40 @@ class TrainState:
 
 
 class GraphedTrainStep:
-    """hipGraph-captured training step around a ``TrainState`` built with ``graph_ready=True``.
+    """hipGraph-replayed training step around a ``TrainState`` built with ``graph_ready=True``.
+
+    What is captured: the launch-bound recurrent part -- correlation volume, the 12 GRU
+    iterations forward AND backward (the fused update block's ~900 kernels), convex upsampling and
+    the sequence loss (``RAFT.decode`` + ``sequence_loss`` + backward to the encoder outputs) --
+    and the parameter update (grad clip + fused AdamW).  What runs eagerly: the two encoders,
+    forward and backward (``RAFT.encode``, ~100 large MIOpen convolutions + fused norm nodes).
+    MIOpen's strided-convolution backward solvers are not replay-safe (replay 0 matches eager
+    bit for bit, later replays read stale workspace / output state: profiles/r2/graph_cmp_*.log),
+    and the encoders are not launch-bound anyway, so keeping them out of the graph costs nothing.
+
+    Per step: eager encode -> copy the four encoder outputs into the graph's static leaves ->
+    replay g_dec (fills the update-block .grad and the leaves' .grad) -> eager encoder backward
+    from the leaves' gradients (accumulating into persistent encoder .grad buffers) -> (ranks > 1:
+    one flat RCCL all-reduce) -> replay g_up.
 
     The warm-up steps needed before capture (MIOpen solver search, allocator, lazy optimizer
     state) are real training steps; their effect on the weights, BN statistics, optimizer moments
-    and LR schedule is rolled back after capture, so the first replay is step 0 of the run and a
-    graphed run follows the same trajectory as an eager one (``tests/test_graph_gpu.py``).
-    Host cost per step is one replay of each graph (~0.4 ms) instead of ~1000 kernel launches
-    through Python and autograd (~16-20 ms of host time per step on MI355X).
+    and LR schedule is rolled back after capture, so the first replayed step is step 0 of the run
+    and a graphed run follows the eager trajectory (``tests/test_graph_gpu.py``).
     """
 
-    def __init__(self, st, example, warmup=3):
+    def __init__(self, st, example, warmup=2):
         assert st.device.type == 'cuda', 'graph capture needs a GPU'
         assert not st.scaler.is_enabled(), 'use bf16 autocast (no GradScaler) with graph capture'
         self.st = st
         self.world = pdist.world_size()
         model = st.model
-        self.params = [p for p in model.parameters() if p.requires_grad]
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        self.params = [p for _, p in named]
+        self.dec_params = [p for n, p in named if n.startswith('update_block')]
+        self.enc_params = [p for n, p in named if not n.startswith('update_block')]
         numel = sum(p.numel() for p in self.params)
-        # Gradients: .grad is None when backward starts, so every AccumulateGrad hands its
-        # incoming gradient over (no zero fill, no add kernel per parameter -- 143 of them when
-        # .grad were views of one persistent buffer).  Captured, those tensors live in the graph
-        # pool at fixed addresses.  With world > 1 the graph ends by packing them into ``flat``
-        # (one cat), which is all-reduced between the two replays and unpacked by the update graph.
         self.flat = torch.zeros(numel, device=st.device, dtype=torch.float32) if self.world > 1 else None
-        self.grads = None
         for p in self.params:
             p.grad = None
         # learning rate as a device tensor (fused AdamW reads it in-graph)
@@ -136,35 +145,135 @@ class GraphedTrainStep:
             t = torch.tensor(float(g['lr']), device=st.device, dtype=torch.float32)
             g['lr'] = t
             self.lr.append(t)
-        self.static = [t.clone() for t in example]
 
-        # warm-up AND capture on ONE side stream: autograd runs each parameter's AccumulateGrad
-        # on the stream its node was first used on, so a warm-up on another stream would leave
-        # the gradient accumulation outside the captured stream (the grads of a replay are then
-        # never written into ``flat``)
         stream = torch.cuda.Stream(device=st.device)
         self.stream = stream
         snap = self._snapshot()
         stream.wait_stream(torch.cuda.current_stream(st.device))
         with torch.cuda.stream(stream):
-            for _ in range(warmup):  # MIOpen find / allocator warm-up; these are real steps
-                loss, _ = self._fwd_bwd()
-                self._post()
-                self._update_graphable(loss)
-                self._sched()
-                del loss
+            # static leaves of the decode graph, shaped / strided like the encoder outputs
+            with torch.no_grad():
+                feats = model.encode(example[0], example[1])
+            self.sfeat = [f.detach().clone().requires_grad_(True) for f in feats]
+            self.sflow = example[2].detach().clone()
+            self.svalid = example[3].detach().clone()
+            del feats
+            for _ in range(warmup):  # MIOpen find / autotune / allocator warm-up: real steps
+                self._step_body(*example, graphs=False)
         torch.cuda.current_stream(st.device).wait_stream(stream)
         torch.cuda.synchronize(st.device)
+        # persistent encoder gradient buffers (eager backward accumulates into them in place)
+        for p in self.enc_params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        self.enc_grads = [p.grad for p in self.enc_params]
 
-        self.g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_fb, stream=stream):
-            self.loss, self.metrics = self._fwd_bwd()
+        self.g_dec = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_dec, stream=stream):
+            self.loss, self.metrics = self._decode()
+        for p in self.dec_params:
+            if p.grad is None:  # no gradient this step: keep the optimizer's tensor list fixed
+                p.grad = torch.zeros_like(p)
+        self.grads = [p.grad for p in self.params]
         self.g_up = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_up, pool=self.g_fb.pool(), stream=stream):
+        with torch.cuda.graph(self.g_up, stream=stream):
             self._update_graphable(self.loss)
         self.warmup_steps = warmup
         self._restore(snap)
 
+    # ---------------------------------------------------------------- pieces of one step
+    def _decode(self):
+        """The captured part: decode + loss + backward to the static leaves / update block."""
+        st = self.st
+        for p in self.dec_params:
+            p.grad = None
+        for s in self.sfeat:
+            s.grad = None
+        preds = st.model.decode(*self.sfeat, iters=st.args.iters)
+        loss, metrics = sequence_loss(preds, self.sflow, self.svalid, st.args.gamma)
+        loss.backward()
+        return loss, metrics
+
+    def _encode_and_stage(self, image1, image2, flow, valid):
+        st = self.st
+        if getattr(st.args, 'add_noise', False):
+            image1, image2 = st.add_noise(image1, image2)
+        feats = st.model.encode(image1, image2)
+        with torch.no_grad():
+            for s, f in zip(self.sfeat, feats):
+                s.copy_(f)
+            if self.sflow.data_ptr() != flow.data_ptr():
+                self.sflow.copy_(flow, non_blocking=True)
+            if self.svalid.data_ptr() != valid.data_ptr():
+                self.svalid.copy_(valid, non_blocking=True)
+        return feats
+
+    def _encoder_backward(self, feats):
+        torch.autograd.backward(list(feats), [s.grad for s in self.sfeat])
+
+    def _step_body(self, image1, image2, flow, valid, graphs=True):
+        st = self.st
+        if graphs:
+            torch._foreach_zero_(self.enc_grads)
+        else:
+            for p in self.params:
+                p.grad = None
+        if st.has_buffers and self.world > 1:
+            pdist.broadcast_buffers(st.model)  # DataParallel semantics: replica 0's BN stats
+        feats = self._encode_and_stage(image1, image2, flow, valid)
+        if graphs:
+            self.g_dec.replay()
+            loss = self.loss
+        else:
+            loss, _ = self._decode()
+        self._encoder_backward(feats)
+        del feats
+        if not graphs:
+            for p in self.params:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            self.grads = [p.grad for p in self.params]
+        self._post()
+        if graphs:
+            self.g_up.replay()
+        else:
+            self._update_graphable(loss)
+        self._sched()
+        return loss
+
+    def _post(self):
+        if self.world > 1:
+            torch.cat([p.grad.reshape(-1) for p in self.params], out=self.flat)
+            dist.all_reduce(self.flat)
+
+    def _unpack(self):
+        if self.flat is None:
+            return
+        views, off = [], 0
+        for g in self.grads:
+            n = g.numel()
+            views.append(self.flat[off:off + n].view_as(g))
+            off += n
+        torch._foreach_copy_(self.grads, views)
+        torch._foreach_mul_(self.grads, 1.0 / self.world)
+
+    def _update_graphable(self, loss):
+        st = self.st
+        self._unpack()
+        clip_grad_norm_(self.params, st.args.clip)
+        st.optimizer.step()
+        st.nonfinite += (~torch.isfinite(loss.detach())).float()
+
+    def _sched(self):
+        st = self.st
+        st.scheduler.step()
+        for g, t in zip(st.optimizer.param_groups, self.lr):
+            v = g['lr']
+            if not torch.is_tensor(v):
+                t.fill_(float(v))
+                g['lr'] = t
+
+    # ---------------------------------------------------------------- warm-up roll-back
     @torch.no_grad()
     def _snapshot(self):
         st = self.st
@@ -203,60 +312,10 @@ class GraphedTrainStep:
         st.nonfinite.copy_(snap['nonfinite'])
         torch.cuda.synchronize(st.device)
 
-    def _fwd_bwd(self):
-        for p in self.params:
-            p.grad = None
-        out = self.st.forward_backward(*self.static)
-        for p in self.params:
-            if p.grad is None:  # no gradient this step (keeps the optimizer's tensor list fixed)
-                p.grad = torch.zeros_like(p)
-        self.grads = [p.grad for p in self.params]
-        if self.flat is not None:
-            torch.cat([g.reshape(-1) for g in self.grads], out=self.flat)
-        return out
-
-    def _post(self):
-        if self.world > 1:
-            dist.all_reduce(self.flat)
-
-    def _unpack(self):
-        if self.flat is None:
-            return
-        views, off = [], 0
-        for g in self.grads:
-            n = g.numel()
-            views.append(self.flat[off:off + n].view_as(g))
-            off += n
-        torch._foreach_copy_(self.grads, views)
-        torch._foreach_mul_(self.grads, 1.0 / self.world)
-
-    def _update_graphable(self, loss):
-        st = self.st
-        self._unpack()
-        clip_grad_norm_(self.params, st.args.clip)
-        st.optimizer.step()
-        st.nonfinite += (~torch.isfinite(loss.detach())).float()
-
-    def _sched(self):
-        st = self.st
-        st.scheduler.step()
-        for g, t in zip(st.optimizer.param_groups, self.lr):
-            v = g['lr']
-            if not torch.is_tensor(v):
-                t.fill_(float(v))
-                g['lr'] = t
-
+    # ---------------------------------------------------------------- public
     def step(self, image1, image2, flow, valid):
         st = self.st
-        for s, x in zip(self.static, (image1, image2, flow, valid)):
-            if s.data_ptr() != x.data_ptr():
-                s.copy_(x, non_blocking=True)
-        if st.has_buffers and self.world > 1:
-            pdist.broadcast_buffers(st.model)
-        self.g_fb.replay()
-        self._post()
-        self.g_up.replay()
-        self._sched()
+        self._step_body(image1, image2, flow, valid, graphs=True)
         st.total_steps += 1
         metrics = dict(self.metrics)
         metrics['loss'] = self.loss.detach()

@@ -95,6 +95,14 @@ class RAFT(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward(self, image1, image2, iters=12, flow_init=None, upsample=True, test_mode=False):
+        feats = self.encode(image1, image2)
+        return self.decode(*feats, iters=iters, flow_init=flow_init, test_mode=test_mode)
+
+    def encode(self, image1, image2):
+        """Feature + context encoders (`core/raft.py:89-114`): -> (fmap1, fmap2, net, inp).
+
+        Split from ``decode`` so the hipGraph training step can replay the launch-bound recurrent
+        part while the encoders (a few large MIOpen convolutions) run eagerly."""
         image1 = (2 * (image1 / 255.0) - 1.0).contiguous()
         image2 = (2 * (image2 / 255.0) - 1.0).contiguous()
         hdim, cdim = self.hidden_dim, self.context_dim
@@ -103,9 +111,17 @@ class RAFT(nn.Module):
         if cl:
             image1 = image1.contiguous(memory_format=torch.channels_last)
             image2 = image2.contiguous(memory_format=torch.channels_last)
-
         with self._autocast(dev):
             fmap1, fmap2 = self.fnet([image1, image2])
+        with self._autocast(dev):
+            cnet = self.cnet(image1)
+            net, inp = torch.split(cnet, [hdim, cdim], dim=1)
+            net = torch.tanh(net)
+            inp = torch.relu(inp)
+        return fmap1, fmap2, net, inp
+
+    def decode(self, fmap1, fmap2, net, inp, iters=12, flow_init=None, test_mode=False):
+        """Correlation volume + GRU iterations + upsampling (`core/raft.py:102-144`)."""
         if not (self._bf16_corr_ok(fmap1) and not self.args.alternate_corr):
             # the reference runs the correlation in fp32 (`core/raft.py:102-103`); the bf16 HIP
             # build takes the bf16 encoder outputs as they are (same products, fp32 accumulation)
@@ -119,18 +135,14 @@ class RAFT(nn.Module):
         else:
             corr_fn = CorrBlock(fmap1, fmap2, radius=self.args.corr_radius, impl=self.corr_impl,
                                 precision='bf16' if self.args.mixed_precision else 'fp32')
-
-        with self._autocast(dev):
-            cnet = self.cnet(image1)
-            net, inp = torch.split(cnet, [hdim, cdim], dim=1)
-            net = torch.tanh(net)
-            inp = torch.relu(inp)
-
-        coords0, coords1 = self.initialize_flow(image1)
+        dev = fmap1.device
+        b, _, h8, w8 = fmap1.shape
+        coords0 = coords_grid(b, h8, w8, device=dev)
+        coords1 = coords_grid(b, h8, w8, device=dev)
         if flow_init is not None:
             coords1 = coords1 + flow_init
 
-        if self._use_fused_update(image1):
+        if self._use_fused_update(fmap1):
             return self._iterate_fused(net, inp, corr_fn, coords0, coords1, iters, test_mode)
 
         flow_predictions = []
@@ -160,9 +172,10 @@ class RAFT(nn.Module):
 
     # ------------------------------------------------------------------ fused HIP update path
     def _use_fused_update(self, img):
-        """Fused MFMA update block: GPU, full model, bf16 mixed precision (its compute dtype)."""
+        """Fused MFMA update block (full and small model): GPU, bf16 mixed precision (its
+        compute dtype)."""
         impl = _get(self.args, 'update_impl', 'auto')
-        if impl == 'torch' or self.corr_impl == 'torch' or self.args.small or not _ext.device_ok(img):
+        if impl == 'torch' or self.corr_impl == 'torch' or not _ext.device_ok(img):
             return False
         if not (self.args.mixed_precision and self.amp_dtype == torch.bfloat16):
             if impl == 'hip':
@@ -171,7 +184,32 @@ class RAFT(nn.Module):
         from ..ops import update_hip
         return update_hip.available(required=(impl == 'hip'))
 
+    def _iterate_fused_small(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
+        """RAFT-small: fused ConvGRU iterations (ops/update_hip_small.py), upflow8 output."""
+        from ..ops.update_hip_small import HipSmallUpdateBlock, CORR_BUF_SMALL, HDP
+        hub = HipSmallUpdateBlock(self.update_block)
+        h = torch.nn.functional.pad(net.to(torch.bfloat16).permute(0, 2, 3, 1),
+                                    (0, HDP - net.shape[1])).contiguous()
+        x = inp.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+        flow_predictions = []
+        flow_up = None
+        for itr in range(iters):
+            coords1 = coords1.detach()
+            corr = corr_fn.lookup_nhwc(coords1, CORR_BUF_SMALL)
+            flow = coords1 - coords0
+            h, delta_flow = hub(h, x, corr, flow)
+            coords1 = coords1 + delta_flow
+            if test_mode and itr < iters - 1:
+                continue
+            flow_up = upflow8(coords1 - coords0)
+            flow_predictions.append(flow_up)
+        if test_mode:
+            return coords1 - coords0, flow_up
+        return flow_predictions
+
     def _iterate_fused(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
+        if self.args.small:
+            return self._iterate_fused_small(net, inp, corr_fn, coords0, coords1, iters, test_mode)
         from ..ops.update_hip import HipUpdateBlock, CORR_BUF
         hub = HipUpdateBlock(self.update_block)
         h = net.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()

@@ -221,6 +221,55 @@ def cast_conv_weights(convs):
 _WEIGHTS = {}   # conv -> bf16 channels_last weight for the encoder forward in flight
 
 
+class _Head1x1(torch.autograd.Function):
+    """The encoders' final 1x1 conv (`core/extractor.py:185`, 128 -> 256 with bias) on the
+    MFMA implicit-GEMM kernels of the update block (NHWC bf16, fp32 accumulation): forward with
+    the bias epilogue, input gradient by the same kernel on the transposed weight, weight / bias
+    gradient by the split-K wgrad kernel.  Replaces MIOpen's 1x1 solvers, one of which produced
+    inf weight gradients under hipGraph replay (profiles/r2/graph_cmp_cnet_conv2.log)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        from . import conv as C
+        B, cin, H, W = x.shape
+        cout = weight.shape[0]
+        xn = x.permute(0, 2, 3, 1)                     # channels_last memory: a view, no copy
+        if not xn.is_contiguous():
+            xn = xn.contiguous()
+        w2 = weight.reshape(cout, cin)
+        wpk = C.pack_weight(weight, [cin], [cin])       # (Npad, cin) bf16
+        out = torch.empty(B, H, W, cout, device=x.device, dtype=torch.bfloat16)
+        C.conv_fwd([(xn, 0, cin)], wpk, bias.float().contiguous(), (1, 1), (0, 0), cout,
+                   C.EPI_BF16, [out], [0])
+        ctx.save_for_backward(xn, w2)
+        return out.permute(0, 3, 1, 2)                  # (B, cout, H, W), channels_last strides
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import conv as C
+        xn, w2 = ctx.saved_tensors
+        B, H, W, cin = xn.shape
+        cout = w2.shape[0]
+        g = dy.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()   # (B, H, W, cout)
+        dx = torch.empty(B, H, W, cin, device=xn.device, dtype=torch.bfloat16)
+        wd = C.pack_weight(w2.t().contiguous().view(cin, cout, 1, 1), [cout], [cout])
+        _ext.ops().conv_dgrad_([g], [0], [cout], wd, 1, 1, 0, 0, 0, 1.0, [dx], [0], [cin], [cin],
+                               [0], [dx], [-1])
+        dw = torch.zeros(cout, cin, device=xn.device)
+        db = torch.zeros(cout, device=xn.device)
+        C.conv_wgrad(g, 0, [(xn, 0, cin)], (1, 1), (0, 0), cout, dw, db)
+        return dx.permute(0, 3, 1, 2), dw.view(cout, cin, 1, 1), db
+
+
+def _head_ok(x, conv):
+    return (conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.bias is not None
+            and conv.in_channels % 64 == 0 and conv.out_channels % 32 == 0 and x.is_cuda
+            and _HEAD_NATIVE)
+
+
+_HEAD_NATIVE = os.environ.get('RAFT_ENCODER_HEAD_NATIVE', '1') != '0'
+
+
 def _conv(x, conv, with_bias=False):
     w = _WEIGHTS.get(conv)
     if w is None:
@@ -304,6 +353,8 @@ def encoder_forward(enc, x):
     """`core/extractor.py:168-192` (both encoders): returns channels_last bf16 features."""
     with torch.autocast('cuda', enabled=False):
         convs = [m for m in enc.modules() if isinstance(m, nn.Conv2d)]
+        if _head_ok(x, enc.conv2):
+            convs = [c for c in convs if c is not enc.conv2]  # runs on _Head1x1 (fp32 weight)
         _WEIGHTS.update(cast_conv_weights(convs))
         try:
             return _encoder_body(enc, x)
@@ -319,5 +370,7 @@ def _encoder_body(enc, x):
     for layer in (enc.layer1, enc.layer2, enc.layer3):
         for blk in layer:
             x = block_fn(blk, x)
+    if _head_ok(x, enc.conv2):
+        return _Head1x1.apply(x, enc.conv2.weight, enc.conv2.bias)
     x = _conv(x, enc.conv2, with_bias=True)
     return x

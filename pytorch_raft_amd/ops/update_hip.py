@@ -40,8 +40,15 @@ class _LayerSpec:
     """Geometry of one conv of the fused block."""
 
     def __init__(self, name, cout, ksize, in_real, in_pad, small=False, relu=False, scale=1.0,
-                 patch=False):
+                 patch=False, row_pad=None, adj_pad=None, adj_off=0):
         self.name = name
+        # row_pad: per source module, its output rows are zero-padded to this many (a hidden width
+        # of 96 carried in 128-channel buffers); adj_pad / adj_off: K width of the adjoint (dgrad)
+        # conv's input segment and where this layer's output channels sit inside it (the adjoint
+        # input must be a multiple of 64 channels wide)
+        self.row_pad = row_pad
+        self.adj_pad = adj_pad
+        self.adj_off = adj_off
         # patch: the conv runs as a 1x1 conv over a tap-major im2col patch buffer whose K order is
         # the dense-K packing of the small-Cin weight (convf1: 7x7x2 -> 98 of 128 channels)
         self.patch = patch
@@ -72,6 +79,23 @@ SPECS = [
 SPEC = {s.name: s for s in SPECS}
 
 
+class Design:
+    """A fused update block: its layer specs and where their parameters live in the module."""
+
+    def __init__(self, specs, module_params):
+        self.specs = specs
+        self.spec = {s.name: s for s in specs}
+        self.module_params = module_params
+
+    def flat_params(self, ub):
+        mp = self.module_params(ub)
+        out = []
+        for s in self.specs:
+            for w, b in mp[s.name]:
+                out += [w, b]
+        return out
+
+
 def module_params(ub):
     """(weight, bias) tensors of each fused layer, in SPECS order, from a BasicUpdateBlock."""
     e, g, fh, mk = ub.encoder, ub.gru, ub.flow_head, ub.mask
@@ -91,36 +115,38 @@ def module_params(ub):
     }
 
 
-def flat_params(ub):
-    mp = module_params(ub)
-    out = []
-    for s in SPECS:
-        for w, b in mp[s.name]:
-            out += [w, b]
-    return out
+FULL = Design(SPECS, module_params)
 
 
-def _pack_layers(params_by_layer, need_grad, dtype):
+def flat_params(ub, design=FULL):
+    return design.flat_params(ub)
+
+
+def _pack_layers(params_by_layer, need_grad, dtype, design=FULL):
     """Kernel-layout weights of every fused conv: ({name: forward [Npad][K]}, {name: adjoint
     [Npad'][K']}, {name: bias}, {extra tables}).  Runs on real parameters or on index tensors
     (``_PackPlan``).  Extras: flow_head.conv2's bf16 pair tables for its VALU kernels, forward
     [t][o][c] and adjoint [t][c][o]."""
     w_out, wd_out, b_out, x_out = {}, {}, {}, {}
-    for s in SPECS:
+    F_ = torch.nn.functional
+    for s in design.specs:
         ws = [w for w, _ in params_by_layer[s.name]]
         bs = [b for _, b in params_by_layer[s.name]]
+        if s.row_pad is not None:
+            ws = [F_.pad(w, (0, 0, 0, 0, 0, 0, 0, s.row_pad - w.shape[0])) for w in ws]
+            bs = [F_.pad(b, (0, s.row_pad - b.shape[0])) for b in bs]
         w = ws[0] if len(ws) == 1 else torch.cat(ws, 0)
         b_out[s.name] = bs[0] if len(bs) == 1 else torch.cat(bs, 0)
         if s.small:
             w_out[s.name] = C.pack_weight_small(w, dtype=dtype)
         else:
             w_out[s.name] = C.pack_weight(w, s.in_real, s.in_pad, dtype=dtype)
-        if need_grad and s.name not in ('f1', 'fh2'):
+        if need_grad and not s.patch and not (design is FULL and s.name == 'fh2'):
             # adjoint conv: inputs = this layer's output channels, outputs = its inputs
-            cout_pad = C.round_up(s.cout, 32)
+            cout_pad = s.adj_pad or C.round_up(s.cout, 32)
             wt = w
             if cout_pad > s.cout:
-                wt = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 0, 0, cout_pad - s.cout))
+                wt = F_.pad(w, (0, 0, 0, 0, 0, 0, s.adj_off, cout_pad - s.cout - s.adj_off))
             wt = wt.flip(2, 3).transpose(0, 1).contiguous()  # (Cin, CoutPad, kh, kw)
             if sum(s.in_pad) > sum(s.in_real):
                 # padded input slots become zero output rows of the adjoint
@@ -133,7 +159,7 @@ def _pack_layers(params_by_layer, need_grad, dtype):
                     off += r
                 wt = torch.cat(parts, 0)
             wd_out[s.name] = C.pack_weight(wt, [cout_pad], [cout_pad], dtype=dtype)
-        if s.name == 'fh2':
+        if design is FULL and s.name == 'fh2':
             x_out['fh2f'] = w.permute(2, 3, 0, 1).reshape(18, 256).to(dtype)
             x_out['fh2d'] = w.permute(2, 3, 1, 0).reshape(9, 512).to(dtype)
     return w_out, wd_out, b_out, x_out
@@ -146,8 +172,10 @@ class _PackPlan:
     cast kernels per training step.  Built once per parameter geometry by running the packing
     code on index tensors (float64 holds the element ids exactly; 0 marks zero padding)."""
 
-    def __init__(self, ub, need_grad, device):
-        params = flat_params(ub)
+    def __init__(self, ub, need_grad, device, design=FULL):
+        SPECS = design.specs
+        module_params = design.module_params
+        params = design.flat_params(ub)
         self.numels = [p.numel() for p in params]
         self.shapes = [tuple(p.shape) for p in params]
         total = sum(self.numels)
@@ -158,7 +186,7 @@ class _PackPlan:
         it = iter(ids)
         by_layer = {s.name: [(next(it), next(it)) for _ in module_params(ub)[s.name]]
                     for s in SPECS}
-        w_idx, wd_idx, b_idx, x_idx = _pack_layers(by_layer, need_grad, torch.float64)
+        w_idx, wd_idx, b_idx, x_idx = _pack_layers(by_layer, need_grad, torch.float64, design)
         # gather index: element id - 1; padding (id 0) -> the zero slot appended after the params
         self.views = []       # (kind, name, shape) in gather order
         parts = []
@@ -172,7 +200,9 @@ class _PackPlan:
         gidx[gidx < 0] = total
         self.widx = gidx.to(device)
         self.bshapes = [(s.name, b_idx[s.name].numel()) for s in SPECS]
-        self.bidx = (torch.cat([b_idx[s.name].reshape(-1) for s in SPECS]).round().long() - 1).to(device)
+        bidx = torch.cat([b_idx[s.name].reshape(-1) for s in SPECS]).round().long() - 1
+        bidx[bidx < 0] = total   # padded rows (row_pad) read the zero slot
+        self.bidx = bidx.to(device)
         self.kpad = {s.name: w_idx[s.name].shape[1] for s in SPECS}
         # gradient buffer: per layer dw (cout, kpad) then db (cout), concatenated in SPECS order;
         # uidx[e] = the buffer position holding parameter element e's gradient
@@ -187,7 +217,8 @@ class _PackPlan:
             self.dw_views.append((s.name, 'w', pos, (s.cout, self.kpad[s.name])))
             pos += n
             ids_b = b_idx[s.name].round().long() - 1
-            uidx[ids_b] = torch.arange(pos, pos + s.cout)
+            mb = ids_b >= 0   # padded output rows (row_pad) have no parameter
+            uidx[ids_b[mb]] = torch.arange(pos, pos + s.cout)[mb]
             self.dw_views.append((s.name, 'b', pos, (s.cout,)))
             pos += s.cout
         assert (uidx >= 0).all(), 'every parameter element must have a gradient slot'
@@ -195,11 +226,11 @@ class _PackPlan:
         self.uidx = uidx.to(device)
 
 
-def _plan(ub, need_grad, device):
-    key = (need_grad, str(device), tuple(tuple(p.shape) for p in flat_params(ub)))
+def _plan(ub, need_grad, device, design=FULL):
+    key = (need_grad, str(device), tuple(tuple(p.shape) for p in design.flat_params(ub)))
     cache = ub.__dict__.setdefault('_raft_pack_plans', {})
     if key not in cache:
-        cache[key] = _PackPlan(ub, need_grad, device)
+        cache[key] = _PackPlan(ub, need_grad, device, design)
     return cache[key]
 
 
@@ -209,7 +240,8 @@ class _Packed:
     def defer_wgrad(self, name, g, g_off, segs):
         self.pending.setdefault(name, []).append((g, g_off, segs))
 
-    def __init__(self, ub, params, device, need_grad):
+    def __init__(self, ub, params, device, need_grad, design=FULL):
+        self.design = design
         self.w = {}
         self.wd = {}
         self.x = {}
@@ -219,7 +251,7 @@ class _Packed:
         self.pending = {}  # conv name -> [(g, g_off, segs)] awaiting the batched weight gradient
         self.fh2_items = []  # (fp32 delta gradient, head activations) per iteration
         self.device = device
-        plan = self.plan = _plan(ub, need_grad, device)
+        plan = self.plan = _plan(ub, need_grad, device, design)
         self.kpad = plan.kpad
         with torch.no_grad():
             flat = torch.cat([p.detach().float().reshape(-1) for p in params] +
@@ -236,7 +268,8 @@ class _Packed:
                 self.b[name] = bias[off:off + n]
                 off += n
             # 256 -> 2 conv: dedicated VALU kernels read bf16 pair tables
-            self.fh2_wf, self.fh2_wd = self.x['fh2f'], self.x['fh2d']
+            if design is FULL:
+                self.fh2_wf, self.fh2_wd = self.x['fh2f'], self.x['fh2d']
             self.b32 = self.b['fh2']
             if need_grad:
                 self.dwflat = torch.zeros(plan.dw_total, device=device)
@@ -251,7 +284,7 @@ def _flush_wgrad(pk):
     (the weights are shared by all iterations; convf1 as a 1x1 conv over its patch buffers),
     the flow-head conv2 by its own VALU kernel."""
     for name, items in pk.pending.items():
-        s = SPEC[name]
+        s = pk.design.spec[name]
         dw, db = pk.dw[name], pk.db[name]
         k, pad, small = ((1, 1), (0, 0), False) if s.patch else (s.k, s.pad, s.small)
         same = all(it[1] == items[0][1] and [(o, c) for _, o, c in it[2]] ==
@@ -290,12 +323,14 @@ class _State:
         self.n_iter = 0        # iterations issued through this block (forward order)
         self.next_bwd = None   # iteration whose backward must run next (strictly n_iter-1 .. 0)
         self.dinp_acc = None   # fp32 gradient w.r.t. the context input, summed over iterations
+        self.design = FULL
 
 
 class _UpdateWeights(torch.autograd.Function):
     @staticmethod
     def forward(ctx, state, *params):
-        state.packed = _Packed(state.ub, params, params[0].device, need_grad=state.need_grad)
+        state.packed = _Packed(state.ub, params, params[0].device, need_grad=state.need_grad,
+                               design=state.design)
         ctx.state = state
         ctx.n = len(params)
         return params[0].new_zeros(())
@@ -319,7 +354,7 @@ class _UpdateWeights(torch.autograd.Function):
 
 def _unpack_grads(pk):
     """Packed fp32 gradients -> one tensor per parameter (module layout), one gather."""
-    for s in SPECS:
+    for s in pk.design.specs:
         if s.scale != 1.0:
             pk.dw[s.name].mul_(s.scale)
             pk.db[s.name].mul_(s.scale)

@@ -1,0 +1,210 @@
+"""Fused HIP update block of RAFT-small: SmallMotionEncoder + ConvGRU (3x3) + FlowHead.
+
+Reference: `core/update.py:16-31` (ConvGRU), `:62-77` (SmallMotionEncoder), `:99-112`
+(SmallUpdateBlock), `core/raft.py:133-139` (upflow8 instead of the convex mask).  One GRU
+iteration is ONE autograd node built from the same gfx950 kernels as the full block
+(``ops/update_hip.py``): implicit-GEMM bf16 MFMA convs with fused epilogues, hand-written
+backward (dgrad on flipped weights, batched weight gradients per step).
+
+Layout: every activation is an NHWC bf16 buffer whose width is a multiple of 64 (the conv's K
+step).  The small model's odd widths are carried in padded buffers whose pad channels are exact
+zeros, with the padding folded into the packed weights:
+
+* hidden state h: 96 real channels in 128.  convz / convr / convq rows are zero-padded to 128
+  (``row_pad``), so the padded gate channels evaluate to z = r = 0.5, q = tanh(0) = 0 and the GRU
+  epilogue writes h' = 0 there -- the pads stay zero through every iteration;
+* corr: 4 x 49 = 196 taps in 256 (the lookup zero-fills the tail);
+* motion features: [cor 96 | flo 32] in one 128-wide buffer (both convs write their slice), then
+  [conv 80 | flow 2 | 0 ...] in 128;
+* flow_head.conv2 (128 -> 2) runs as a 32-wide-N MFMA conv writing the fp32 NCHW delta.
+
+The backward keeps the accumulating gradients (dh, d inp, d motion) in fp32 and feeds bf16
+pre-activation gradients to the dgrad / wgrad kernels, like the full block.
+"""
+import torch
+
+from . import _ext
+from . import conv as C
+from . import update_hip as _UH
+from .update_hip import _LayerSpec, Design, _UpdateWeights, _State, _bf16, _f32
+
+HDP = 128        # padded hidden width (96 real)
+CORR_BUF_SMALL = 256  # 196 lookup taps zero-padded to a multiple of the K step
+
+SMALL_SPECS = [
+    _LayerSpec('c1', 96, (1, 1), [196], [CORR_BUF_SMALL], adj_pad=128),
+    _LayerSpec('f1', 64, (7, 7), [2], [8], small=True, patch=True),
+    _LayerSpec('f2', 32, (3, 3), [64], [64], adj_pad=64, adj_off=32),
+    _LayerSpec('conv', 80, (3, 3), [128], [128], adj_pad=128),
+    _LayerSpec('zr', 256, (3, 3), [96, 64, 82], [HDP, 64, 128], row_pad=HDP),
+    _LayerSpec('q', 128, (3, 3), [96, 64, 82], [HDP, 64, 128], row_pad=HDP),
+    _LayerSpec('fh1', 128, (3, 3), [96], [HDP]),
+    _LayerSpec('fh2', 2, (3, 3), [128], [128], adj_pad=64),
+]
+
+
+def small_module_params(ub):
+    e, g, fh = ub.encoder, ub.gru, ub.flow_head
+    return {
+        'c1': [(e.convc1.weight, e.convc1.bias)],
+        'f1': [(e.convf1.weight, e.convf1.bias)],
+        'f2': [(e.convf2.weight, e.convf2.bias)],
+        'conv': [(e.conv.weight, e.conv.bias)],
+        'zr': [(g.convz.weight, g.convz.bias), (g.convr.weight, g.convr.bias)],
+        'q': [(g.convq.weight, g.convq.bias)],
+        'fh1': [(fh.conv1.weight, fh.conv1.bias)],
+        'fh2': [(fh.conv2.weight, fh.conv2.bias)],
+    }
+
+
+SMALL = Design(SMALL_SPECS, small_module_params)
+
+
+def _zeros_bf16(shape, dev):
+    return torch.zeros(*shape, device=dev, dtype=torch.bfloat16)
+
+
+def _conv(pk, name, segs, epi, outs, offs, aux=(), aux_offs=(), split=0):
+    s = SMALL.spec[name]
+    k, pad, small = ((1, 1), (0, 0), False) if s.patch else (s.k, s.pad, s.small)
+    C.conv_fwd(segs, pk.w[name], pk.b[name], k, pad, s.cout, epi, outs, offs, aux, aux_offs,
+               scale=s.scale, split=split, cin_small=2 if small else 0)
+
+
+def _iter_forward(pk, h, inp, corr, flow):
+    """h (B,H,W,128) bf16 [96 real], inp (B,H,W,64) bf16, corr (B,H,W,256) bf16 [196 real],
+    flow (B,2,H,W) fp32 -> (h', delta (B,2,H,W) fp32, saved tensors)."""
+    B, H, W, _ = h.shape
+    dev = h.device
+    sh = (B, H, W)
+    ops = _ext.ops()
+    patch = _bf16(sh + (128,), dev)
+    mf = _zeros_bf16(sh + (128,), dev)        # [conv 80 | flow 2 | zeros]
+    ops.f1_patch_(flow, patch, mf, 80)
+    cf = _bf16(sh + (128,), dev)              # [cor 96 | flo 32]
+    f1 = _bf16(sh + (64,), dev)
+    _conv(pk, 'c1', [(corr, 0, CORR_BUF_SMALL)], C.EPI_RELU_BF16, [cf], [0])
+    _conv(pk, 'f1', [(patch, 0, 128)], C.EPI_RELU_BF16, [f1], [0])
+    _conv(pk, 'f2', [(f1, 0, 64)], C.EPI_RELU_BF16, [cf], [96])
+    _conv(pk, 'conv', [(cf, 0, 128)], C.EPI_RELU_BF16, [mf], [0])
+    z, rh, r = _bf16(sh + (HDP,), dev), _bf16(sh + (HDP,), dev), _bf16(sh + (HDP,), dev)
+    segs = [(h, 0, HDP), (inp, 0, 64), (mf, 0, 128)]
+    _conv(pk, 'zr', segs, C.EPI_GRU_ZR, [z, rh, r], [0, 0, 0], aux=[h], aux_offs=[0], split=HDP)
+    hn, q = _bf16(sh + (HDP,), dev), _bf16(sh + (HDP,), dev)
+    _conv(pk, 'q', [(rh, 0, HDP), (inp, 0, 64), (mf, 0, 128)], C.EPI_GRU_Q, [hn, q], [0, 0],
+          aux=[h, z], aux_offs=[0, 0])
+    fm = _bf16(sh + (128,), dev)
+    _conv(pk, 'fh1', [(hn, 0, HDP)], C.EPI_RELU_BF16, [fm], [0])
+    delta = torch.empty(B, 2, H, W, device=dev, dtype=torch.float32)
+    _conv(pk, 'fh2', [(fm, 0, 128)], C.EPI_F32_NCHW, [delta], [0])
+    return hn, delta, (corr, patch, cf, f1, mf, inp, h, z, rh, r, q, hn, fm)
+
+
+class _SmallUpdateIter(torch.autograd.Function):
+    """One ConvGRU iteration of RAFT-small (inputs as ``_iter_forward``) -> (h', delta)."""
+
+    @staticmethod
+    def forward(ctx, token, h, inp, corr, flow, state):
+        hn, delta, saved = _iter_forward(state.packed, h, inp, corr, flow)
+        ctx.state = state
+        ctx.itr = state.n_iter
+        state.n_iter += 1
+        ctx.save_for_backward(*saved)
+        return hn, delta
+
+    @staticmethod
+    def backward(ctx, gh, gdelta):
+        st = ctx.state
+        if st.next_bwd is None:
+            st.next_bwd = ctx.itr
+        if ctx.itr != st.next_bwd:
+            raise RuntimeError('fused update block: iteration %d backward ran out of order '
+                               '(expected %d)' % (ctx.itr, st.next_bwd))
+        st.next_bwd -= 1
+        pk = st.packed
+        corr, patch, cf, f1, mf, inp, h, z, rh, r, q, hn, fm = ctx.saved_tensors
+        B, H, W, _ = hn.shape
+        dev = hn.device
+        sh = (B, H, W)
+        ops = _ext.ops()
+
+        def dgrad(name, gsegs, outs, scale=1.0):
+            s = SMALL.spec[name]
+            ry = [o[5] if len(o) > 5 else o[0] for o in outs]
+            roff = [int(o[6]) if len(o) > 5 else (-1 if o[0].dtype == torch.bfloat16 else 0)
+                    for o in outs]
+            ops.conv_dgrad_([g[0] for g in gsegs], [g[1] for g in gsegs], [g[2] for g in gsegs],
+                            pk.wd[name], s.k[0], s.k[1], s.pad[0], s.pad[1], 0, float(scale),
+                            [o[0] for o in outs], [o[1] for o in outs], [o[2] for o in outs],
+                            [o[3] for o in outs], [o[4] for o in outs], ry, roff)
+
+        # ---- flow head: conv2 (128 -> 2) as an MFMA conv on a 64-wide bf16 gradient
+        g2 = _zeros_bf16(sh + (64,), dev)
+        g2[..., :2] = gdelta.permute(0, 2, 3, 1)
+        pk.defer_wgrad('fh2', g2, 0, [(fm, 0, 128)])
+        dpre_fm = _zeros_bf16(sh + (128,), dev)
+        dgrad('fh2', [(g2, 0, 64)], [(dpre_fm, 0, 128, 128, 0, fm, 0)])
+        pk.defer_wgrad('fh1', dpre_fm, 0, [(hn, 0, HDP)])
+        dh = gh.float().contiguous() if gh is not None else _f32(sh + (HDP,), dev, zero=True)
+        dgrad('fh1', [(dpre_fm, 0, 128)], [(dh, 0, HDP, 96, 1)])
+        # ---- ConvGRU (pads: every gradient buffer is zero beyond the 96 real channels)
+        acc_inp = st.dinp_acc is not None
+        if not acc_inp:
+            st.dinp_acc = _f32(sh + (64,), dev)
+        dinp = st.dinp_acc
+        dmf = _f32(sh + (128,), dev, zero=True)
+        dpre_q = _bf16(sh + (HDP,), dev)
+        dz = _f32(sh + (HDP,), dev)
+        dhp = _f32(sh + (HDP,), dev)
+        ops.gru_q_bwd_(dh, z, q, h, dpre_q, dz, dhp)
+        pk.defer_wgrad('q', dpre_q, 0, [(rh, 0, HDP), (inp, 0, 64), (mf, 0, 128)])
+        drh = _f32(sh + (HDP,), dev, zero=True)
+        dgrad('q', [(dpre_q, 0, HDP)],
+              [(drh, 0, HDP, 96, 0), (dinp, 0, 64, 64, int(acc_inp)), (dmf, 0, 128, 82, 1)])
+        dpre_zr = _bf16(sh + (2 * HDP,), dev)
+        ops.gru_zr_bwd_(drh, dz, z, r, h, dpre_zr, dhp)
+        pk.defer_wgrad('zr', dpre_zr, 0, [(h, 0, HDP), (inp, 0, 64), (mf, 0, 128)])
+        dgrad('zr', [(dpre_zr, 0, 2 * HDP)],
+              [(dhp, 0, HDP, 96, 1), (dinp, 0, 64, 64, 1), (dmf, 0, 128, 82, 1)])
+        # ---- motion encoder
+        dpre_conv = _zeros_bf16(sh + (128,), dev)
+        ops.relu_bwd_(dmf, 0, mf, 0, dpre_conv, 0, 80, 1.0)
+        pk.defer_wgrad('conv', dpre_conv, 0, [(cf, 0, 128)])
+        dpre_cf = _bf16(sh + (128,), dev)
+        dgrad('conv', [(dpre_conv, 0, 128)], [(dpre_cf, 0, 128, 128, 0, cf, 0)])
+        pk.defer_wgrad('c1', dpre_cf, 0, [(corr, 0, CORR_BUF_SMALL)])
+        pk.defer_wgrad('f2', dpre_cf, 96, [(f1, 0, 64)])
+        dpre_f1 = _bf16(sh + (64,), dev)
+        # f2's outputs are channels 96..127 of dpre_cf: the adjoint reads [64, 128) with the
+        # layer's rows at offset 32 of it (adj_off), c1's rows at [0, 96) of [0, 128)
+        dgrad('f2', [(dpre_cf, 64, 64)], [(dpre_f1, 0, 64, 64, 0, f1, 0)])
+        pk.defer_wgrad('f1', dpre_f1, 0, [(patch, 0, 128)])
+        dcorr = _bf16(sh + (CORR_BUF_SMALL,), dev)
+        dgrad('c1', [(dpre_cf, 0, 128)], [(dcorr, 0, CORR_BUF_SMALL, 196, 0)])
+        if ctx.itr == 0:
+            st.dinp_acc = None
+            st.next_bwd = None
+        else:
+            dinp = None
+        return (None, dhp, dinp, dcorr, None, None)
+
+
+class HipSmallUpdateBlock:
+    """Drives the fused iterations for one forward pass of a SmallUpdateBlock."""
+
+    def __init__(self, update_block):
+        self.state = _State()
+        self.state.ub = update_block
+        self.state.design = SMALL
+        params = SMALL.flat_params(update_block)
+        self.state.need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        self.state.params = params
+        self.state.overlap = _UH._OVERLAP
+        self.token = _UpdateWeights.apply(self.state, *params)
+
+    def __call__(self, h, inp, corr, flow):
+        """-> (h', delta)"""
+        if not self.state.need_grad and not torch.is_grad_enabled():
+            hn, delta, _ = _iter_forward(self.state.packed, h, inp, corr, flow)
+            return hn, delta
+        return _SmallUpdateIter.apply(self.token, h, inp, corr, flow, self.state)

@@ -24,13 +24,17 @@ from pytorch_raft_amd.parallel import dist as pdist  # noqa: E402
 
 
 def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl):
-    """The graphed step's DP path: g_fb replay -> flat all-reduce -> g_up replay."""
+    """The graphed step's DP path: eager encoders + g_dec replay -> flat all-reduce -> g_up."""
     from pytorch_raft_amd.engine.trainer import GraphedTrainStep
     sd = {k: v.clone() for k, v in model.state_dict().items()}
     st = TrainState(model, args, dev, graph_ready=True)
     assert st.sync is None
     g = GraphedTrainStep(st, (i1[sl], i2[sl], flow[sl], valid[sl]), warmup=1)
-    g.g_fb.replay()
+    # one step up to the all-reduce: eager encoders + replayed decode + eager encoder backward
+    torch._foreach_zero_(g.enc_grads)
+    feats = g._encode_and_stage(i1[sl], i2[sl], flow[sl], valid[sl])
+    g.g_dec.replay()
+    g._encoder_backward(feats)
     g._post()
     torch.cuda.synchronize()
     g_dp = (g.flat / world).float()

@@ -97,6 +97,28 @@ def test_dry_run_fused_training_step(alternate):
             assert p.grad is not None and p.grad.shape == p.shape, n
 
 
+def test_dry_run_small_model_training_step():
+    """RAFT-small through the fused ConvGRU path (ops/update_hip_small.py): schema-checked ops,
+    every update-block parameter gets a gradient of its own shape."""
+    from pytorch_raft_amd import RAFT
+    from pytorch_raft_amd.ops.loss import sequence_loss
+    from pytorch_raft_amd.data.synthetic import make_pair_batch
+    args = argparse.Namespace(small=True, mixed_precision=True, corr_impl='hip', update_impl='hip')
+    torch.manual_seed(0)
+    m = RAFT(args).train()
+    i1, i2, flow, valid = make_pair_batch(2, 128, 160)
+    with _ext.dry_run(_returns()) as ops:
+        preds = m(i1, i2, iters=2)
+        loss, _ = sequence_loss(preds, flow, valid, 0.8)
+        loss.backward()
+    names = set(ops.calls)
+    assert {'conv_fwd_', 'conv_dgrad_', 'conv_wgrad_', 'gru_q_bwd_', 'gru_zr_bwd_', 'relu_bwd_',
+            'f1_patch_', 'corr_lookup_nhwc_'} <= names, names
+    for n, p in m.named_parameters():
+        if n.startswith('update_block'):
+            assert p.grad is not None and p.grad.shape == p.shape, n
+
+
 def test_dry_run_inference():
     from pytorch_raft_amd import RAFT
     args = argparse.Namespace(small=False, mixed_precision=True, corr_impl='hip', update_impl='hip')

@@ -69,3 +69,28 @@ def test_fast_encoder_matches_eager(ext_ops, cls, norm, train):
         assert cf > min(0.99, ce - 0.05), (n, ce, cf)
     for k, v in bufs['eager'].items():
         torch.testing.assert_close(bufs['fast'][k], v, atol=2e-3, rtol=2e-2)
+
+
+def test_native_head_1x1_matches_conv2d(ext_ops):
+    """Encoder head 1x1 conv on the MFMA kernels (ops/encoder.py _Head1x1) vs F.conv2d in fp32 on
+    the same bf16 operands: output and all three gradients."""
+    from pytorch_raft_amd.ops.encoder import _Head1x1
+    g = torch.Generator(device='cpu').manual_seed(2)
+    x = torch.randn(3, 128, 23, 31, generator=g).to('cuda', torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    w = (torch.randn(256, 128, 1, 1, generator=g) * 0.05).cuda().requires_grad_(True)
+    b = torch.randn(256, generator=g).cuda().requires_grad_(True)
+    y = _Head1x1.apply(x, w, b)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(xr, wr, br)
+    assert y.shape == ref.shape and y.dtype == torch.bfloat16
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=1e-2)
+    gy = torch.randn(ref.shape, generator=g).cuda()
+    (y.float() * gy).sum().backward()
+    (ref * gy.to(torch.bfloat16).float()).sum().backward()
+    rel = lambda a, r: ((a.float() - r).norm() / r.norm()).item()
+    assert rel(x.grad, xr.grad) < 1e-2
+    assert rel(w.grad, wr.grad) < 1e-2
+    assert rel(b.grad, br.grad) < 1e-3

@@ -72,20 +72,28 @@ def test_graph_step_matches_eager(ext_ops, alt):
 
 
 def test_graph_step_host_cost(ext_ops):
+    """The replayed part removes ~900 Python/autograd launches per step: the graphed step's host
+    time must be at most half the eager step's (encoders stay eager: ~100 launches)."""
     from pytorch_raft_amd.engine.trainer import TrainState, GraphedTrainStep
     from pytorch_raft_amd.data.synthetic import device_batches
     dev = torch.device('cuda', 0)
     args = _args(iters=12)
-    m = _model(args, dev)
     batches = device_batches(2, 128, 192, dev, count=2, seed=5)
-    st = TrainState(m, args, dev, graph_ready=True)
-    g = GraphedTrainStep(st, batches[0], warmup=1)
-    g.step(*batches[1])
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    for k in range(5):
-        g.step(*batches[k % 2])
-    host = (time.perf_counter() - t) / 5
-    torch.cuda.synchronize()
-    # eager issues ~1000 launches per step (> 10 ms of host time); two graph replays are ~1 ms
-    assert host < 5e-3, host
+
+    def host_time(stepper):
+        stepper.step(*batches[1])
+        torch.cuda.synchronize()
+        tot = 0.0
+        for k in range(5):
+            t = time.perf_counter()
+            stepper.step(*batches[k % 2])       # issue time only (asynchronous launches)
+            tot += time.perf_counter() - t
+            torch.cuda.synchronize()            # idle queue before the next issue
+        return tot / 5
+
+    m = _model(args, dev)
+    eager = host_time(TrainState(m, args, dev))
+    m2 = _model(args, dev)
+    g = GraphedTrainStep(TrainState(m2, args, dev, graph_ready=True), batches[0], warmup=1)
+    graphed = host_time(g)
+    assert graphed < 0.5 * eager, (graphed, eager)

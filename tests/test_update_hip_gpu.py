@@ -248,3 +248,35 @@ def test_fused_iterations_match_eager_bf16_same_precision(ext_ops):
             bad.append(report[-1])
     print('\n'.join('%s: %s' % r for r in report))
     assert not bad, '\n'.join('%s: %s' % r for r in bad)
+
+
+def test_small_model_fused_matches_eager_bf16(ext_ops):
+    """RAFT-small on the fused ConvGRU path (ops/update_hip_small.py) vs the eager small model
+    under bf16 autocast (`core/update.py:16-31,62-77,99-112`): same loss, flow and gradients
+    within bf16 tolerance, and the fused path is the one that ran."""
+    from pytorch_raft_amd.ops import update_hip_small
+    i1, i2, flow, valid = make_pair_batch(2, 128, 160, device=DEV)
+    outs = {}
+    for impl in ('torch', 'hip'):
+        args = argparse.Namespace(small=True, mixed_precision=True, corr_impl='hip',
+                                  update_impl=impl)
+        torch.manual_seed(0)
+        m = RAFT(args).to(DEV).train()
+        assert m._use_fused_update(i1) == (impl == 'hip')
+        preds = m(i1, i2, iters=3)
+        loss, _ = sequence_loss(preds, flow, valid, 0.8)
+        loss.backward()
+        outs[impl] = (loss.item(), preds[-1].detach(),
+                      {n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    (le, fe, ge), (lh, fh, gh) = outs['torch'], outs['hip']
+    assert abs(lh - le) < 0.02 * abs(le), (lh, le)
+    assert _cos(fh, fe) > 0.995
+    bad = [(n, _cos(gh[n], g)) for n, g in ge.items()
+           if n.startswith('update_block') and _cos(gh[n], g) < 0.98]
+    assert not bad, bad
+    # eval / test mode through the fused path
+    m.eval()
+    with torch.no_grad():
+        lo, up = m(i1, i2, iters=4, test_mode=True)
+    assert up.shape == (2, 2, 128, 160) and torch.isfinite(up).all()
+    assert update_hip_small.SMALL.spec['zr'].row_pad == 128
