@@ -132,9 +132,12 @@ class GraphedTrainStep:
         self.world = pdist.world_size()
         model = st.model
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
-        self.params = [p for _, p in named]
         self.dec_params = [p for n, p in named if n.startswith('update_block')]
         self.enc_params = [p for n, p in named if not n.startswith('update_block')]
+        # flat gradient layout [update block | encoders]: the update-block half is final after the
+        # decode replay and is all-reduced while the eager encoder backward runs
+        self.params = self.dec_params + self.enc_params
+        self.n_dec = sum(p.numel() for p in self.dec_params)
         numel = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(numel, device=st.device, dtype=torch.float32) if self.world > 1 else None
         for p in self.params:
@@ -226,14 +229,21 @@ class GraphedTrainStep:
             loss = self.loss
         else:
             loss, _ = self._decode()
+            for p in self.dec_params:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+        work = self._post_part(self.dec_params, 0)      # overlaps the encoder backward
         self._encoder_backward(feats)
         del feats
         if not graphs:
-            for p in self.params:
+            for p in self.enc_params:
                 if p.grad is None:
                     p.grad = torch.zeros_like(p)
             self.grads = [p.grad for p in self.params]
-        self._post()
+        work2 = self._post_part(self.enc_params, self.n_dec)
+        for w in (work, work2):
+            if w is not None:
+                w.wait()
         if graphs:
             self.g_up.replay()
         else:
@@ -241,10 +251,19 @@ class GraphedTrainStep:
         self._sched()
         return loss
 
+    def _post_part(self, params, off):
+        """Pack ``params``' gradients into their slice of ``flat`` and start its all-reduce."""
+        if self.world <= 1:
+            return None
+        n = sum(p.numel() for p in params)
+        part = self.flat[off:off + n]
+        torch.cat([p.grad.reshape(-1) for p in params], out=part)
+        return dist.all_reduce(part, async_op=True)
+
     def _post(self):
-        if self.world > 1:
-            torch.cat([p.grad.reshape(-1) for p in self.params], out=self.flat)
-            dist.all_reduce(self.flat)
+        for w in (self._post_part(self.dec_params, 0), self._post_part(self.enc_params, self.n_dec)):
+            if w is not None:
+                w.wait()
 
     def _unpack(self):
         if self.flat is None:

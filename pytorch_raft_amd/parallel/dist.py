@@ -183,6 +183,9 @@ class GradSync:
         self.stream = None
         self.enabled = self.world > 1
         self.hooks = []
+        # overlap evidence: (bucket index, gradients finalised so far) at each bucket launch
+        self.hooks_fired = 0
+        self.launch_log = []
         if self.enabled:
             for p in params:
                 self.hooks.append(p.register_post_accumulate_grad_hook(self._hook))
@@ -195,6 +198,8 @@ class GradSync:
         return self.stream
 
     def prepare(self):
+        self.hooks_fired = 0
+        self.launch_log = []
         for b in self.buckets:
             b.pending = len(b.params)
             b.work = None
@@ -230,9 +235,11 @@ class GradSync:
             b.work = dist.all_reduce(b.flat, async_op=True)
 
     def _hook(self, p):
+        self.hooks_fired += 1
         b = self.bucket_of[p]
         b.pending -= 1
         if b.pending == 0 and not b.launched:
+            self.launch_log.append((self.buckets.index(b), self.hooks_fired))
             self._launch(b)
 
     @torch.no_grad()

@@ -37,7 +37,12 @@ def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl):
     g._encoder_backward(feats)
     g._post()
     torch.cuda.synchronize()
-    g_dp = (g.flat / world).float()
+    # flat is [update block | encoders]: back to model parameter order for the comparison
+    views, off = {}, 0
+    for p in g.params:
+        views[p] = g.flat[off:off + p.numel()]
+        off += p.numel()
+    g_dp = (torch.cat([views[p] for p in model.parameters()]) / world).float()
     # two full steps: every rank must hold bit-identical weights afterwards
     for _ in range(2):
         g.step(i1[sl], i2[sl], flow[sl], valid[sl])
