@@ -777,6 +777,103 @@ void conv_wgrad_multi_(const std::vector<Tensor>& gs, int64_t g_off, const std::
   TORCH_CHECK(launch_conv_wgrad_multi(a, it, cout > 64 ? 128 : 64, dbp, cur_stream()), "wgrad launch");
 }
 
+// Tap-fused multi-item weight gradient (conv_wgrad_taps.hip): same contract as conv_wgrad_multi_
+// (dw / db accumulated), segments only need to be multiples of 64 channels.
+void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::vector<Tensor>& ins,
+                      const std::vector<int64_t>& in_off, const std::vector<int64_t>& in_cnt,
+                      int64_t kh, int64_t kw, int64_t ph, int64_t pw, int64_t cout,
+                      const Tensor& dw, const c10::optional<Tensor>& db, int64_t splits) {
+  const int64_t n = (int64_t)gs.size();
+  const int64_t nseg = (int64_t)in_off.size();
+  TORCH_CHECK(n >= 1 && n <= RAFT_WG_MAX_ITEMS, "1..", RAFT_WG_MAX_ITEMS, " items");
+  TORCH_CHECK(nseg >= 1 && nseg <= 3 && (int64_t)in_cnt.size() == nseg, "1..3 input segments");
+  TORCH_CHECK((int64_t)ins.size() == n * nseg, "ins must hold items x segments tensors");
+  TORCH_CHECK((kh == 1 && kw == 1) || (kh == 1 && kw == 5) || (kh == 5 && kw == 1) ||
+                  (kh == 3 && kw == 3),
+              "tap-fused wgrad supports 1x1, 1x5, 5x1 and 3x3 kernels");
+  const Tensor& g0 = gs[0];
+  const int64_t B = g0.size(0), H = g0.size(1), W = g0.size(2);
+  c10::DeviceGuard gd(g0.device());
+  ConvWgradArgs a{};
+  WgradItems it{};
+  WgradTapArgs ta{};
+  it.n = (int)n;
+  a.g_stride = (int)g0.size(3);
+  a.nseg = (int)nseg;
+  int64_t cin_pad = 0;
+  ta.n_ci = 0;
+  for (int64_t s = 0; s < nseg; ++s) {
+    TORCH_CHECK(in_cnt[s] % 64 == 0 && in_off[s] % 8 == 0,
+                "tap-fused wgrad: segments must be multiples of 64 channels");
+    a.seg[s].stride = (int)ins[s].size(3);
+    a.seg[s].cnt = (int)in_cnt[s];
+    for (int64_t c = 0; c < in_cnt[s]; c += 64) {
+      TORCH_CHECK(ta.n_ci < RAFT_WG_MAX_CI_CHUNKS, "too many input channels");
+      ta.ci_seg[ta.n_ci] = (int)s;
+      ta.ci_off[ta.n_ci] = (int)c;
+      ta.ci_k[ta.n_ci] = (int)(cin_pad + c);
+      ++ta.n_ci;
+    }
+    cin_pad += in_cnt[s];
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    const Tensor& g = gs[i];
+    check_nhwc(g, B, H, W, "grad", at::kBFloat16);
+    TORCH_CHECK(g.size(3) == a.g_stride, "all items' grads must share a layout");
+    TORCH_CHECK(g_off >= 0 && g_off % 8 == 0 && g_off + (cout + 7) / 8 * 8 <= g.size(3),
+                "grad slice out of range (cout rounded up to 8 channels must fit the row)");
+    TORCH_CHECK(g.numel() * 2 < (int64_t(1) << 31), "grad exceeds the 2 GiB buffer-descriptor range");
+    it.g[i] = reinterpret_cast<const uint16_t*>(g.data_ptr<at::BFloat16>()) + g_off;
+    for (int64_t s = 0; s < nseg; ++s) {
+      const Tensor& x = ins[i * nseg + s];
+      check_nhwc(x, B, H, W, "wgrad input", at::kBFloat16);
+      TORCH_CHECK(x.size(3) == a.seg[s].stride, "all items' inputs must share a layout");
+      TORCH_CHECK(in_off[s] + in_cnt[s] <= x.size(3), "segment out of range");
+      TORCH_CHECK(x.numel() * 2 < (int64_t(1) << 31), "wgrad input exceeds the 2 GiB buffer-descriptor range");
+      it.seg[i][s] = reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>()) + in_off[s];
+    }
+  }
+  a.cin_pad = (int)cin_pad;
+  a.B = (int)B; a.H = (int)H; a.W = (int)W;
+  a.KH = (int)kh; a.KW = (int)kw; a.PH = (int)ph; a.PW = (int)pw;
+  a.cout = (int)cout;
+  check_cuda_f32(dw, "grad_weight");
+  const int64_t kpad = kh * kw * cin_pad;
+  TORCH_CHECK(dw.dim() == 2 && dw.size(0) == cout && dw.size(1) == kpad, "grad_weight must be (cout, kpad)");
+  TORCH_CHECK(kpad % 4 == 0, "packed K must be a multiple of 4");
+  a.dw = dw.data_ptr<float>();
+  a.kpad = (int)kpad;
+  ta.n_co = (int)((cout + 127) / 128);
+  ta.tiles_x = (int)((W + 7) / 8);
+  ta.tiles_per_img = (int)(((H + 7) / 8) * ta.tiles_x);
+  ta.chunks_per_item = (int)(B * ta.tiles_per_img);
+  ta.total_chunks = (int)(n * ta.chunks_per_item);
+  if (splits <= 0) {
+    // one full round of equal-sized workgroups (resident per CU: 1 for 3x3 -- 9 x 2 accumulator
+    // tiles fill the register file --, 2 for the 5-tap convs, 3 for 1x1); every extra split
+    // costs a cout x kpad fp32 partial written and re-read
+    const int64_t per_cu = kh * kw == 9 ? 1 : (kh * kw == 5 ? 2 : 3);
+    const int64_t pairs = (int64_t)ta.n_co * ta.n_ci;
+    splits = std::max<int64_t>(1, std::min<int64_t>(256 * per_cu / pairs, ta.total_chunks / 8));
+  }
+  ta.chunks_per_split = (int)((ta.total_chunks + splits - 1) / splits);
+  ta.splits = (int)((ta.total_chunks + ta.chunks_per_split - 1) / ta.chunks_per_split);
+  TORCH_CHECK(ta.splits < 65536, "too many splits");
+  auto fo = dw.options();
+  Tensor wpart = at::empty({(int64_t)ta.splits * cout * kpad}, fo);
+  ta.w_part = wpart.data_ptr<float>();
+  float* dbp = nullptr;
+  Tensor bpart;
+  if (db.has_value() && db->defined()) {
+    check_cuda_f32(*db, "grad_bias");
+    TORCH_CHECK(db->numel() == cout, "grad_bias size");
+    dbp = db->data_ptr<float>();
+    bpart = at::empty({(int64_t)ta.splits * cout}, fo);
+    ta.db_part = bpart.data_ptr<float>();
+  }
+  TORCH_CHECK(launch_conv_wgrad_taps(a, it, ta, dbp, cur_stream()), "tap wgrad launch");
+}
+
 // Input gradient of a stride-1 "same" conv = the forward kernel on flipped/transposed packed
 // weights; the result's channels are scattered over up to 3 fp32 NHWC slices (store or +=).
 void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_off,
@@ -1222,6 +1319,8 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] wgs, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("corr_build_bf16(Tensor f1, Tensor f2, int levels) -> Tensor[]");
+  m.def("conv_wgrad_taps_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, "
+        "int kw, int ph, int pw, int cout, Tensor dw, Tensor? db, int splits=0) -> ()");
   m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");
   m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout, bool nhwc=False) -> Tensor[]");
   m.def("corr_lookup_nhwc_(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
@@ -1264,6 +1363,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("add_relu_", &add_relu_);
   m.impl("relu_mask_", &relu_mask_);
   m.impl("corr_build_bf16", &corr_build_bf16);
+  m.impl("conv_wgrad_taps_", &conv_wgrad_taps_);
   m.impl("convex_up_fwd", &convex_up_fwd);
   m.impl("convex_up_bwd", &convex_up_bwd);
   m.impl("seq_loss_fwd", &seq_loss_fwd);

@@ -73,7 +73,27 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
 #pragma unroll
   for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
   if (pl < lanes) {
-    for (int p = p0 + pl; p < p1; p += lanes) {
+    // 4 pixels per round with all four 16-B loads issued first: one outstanding load per
+    // thread left this pass latency-bound at ~3 TB/s
+    int p = p0 + pl;
+    for (; p + 3 * lanes < p1; p += 4 * lanes) {
+      uint4 raw[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        raw[u] = *reinterpret_cast<const uint4*>(x + (base + p + u * lanes) * C + g * 8);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float v[8];
+        unpack8(raw[u], v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float d = v[i] - K[i];
+          s1[i] += d;
+          s2[i] += d * d;
+        }
+      }
+    }
+    for (; p < p1; p += lanes) {
       float v[8];
       unpack8(*reinterpret_cast<const uint4*>(x + (base + p) * C + g * 8), v);
 #pragma unroll
@@ -304,24 +324,40 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
   float sg[8], sgx[8], sx[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) sg[i] = sgx[i] = sx[i] = 0.f;
+  auto accum = [&](const uint4& rd, const uint4& rx) {
+    float d[8], xv[8];
+    unpack8(rd, d);
+    unpack8(rx, xv);
+    if (relu) {
+      // the forward ReLU mask, recomputed from x with the forward's own scale / shift
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = xv[i] * sc[i] + sh[i] > 0.f ? d[i] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float xh = (xv[i] - mu[i]) * is[i];
+      sg[i] += d[i];
+      sgx[i] += d[i] * xh;
+      sx[i] += xh;
+    }
+  };
   if (pl < lanes) {
-    for (int p = p0 + pl; p < p1; p += lanes) {
+    // 4 pixels (8 loads) in flight per round (see norm_stats_kernel)
+    int p = p0 + pl;
+    for (; p + 3 * lanes < p1; p += 4 * lanes) {
+      uint4 rd[4], rx[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t off = (base + p + u * lanes) * C + g * 8;
+        rd[u] = *reinterpret_cast<const uint4*>(dy + off);
+        rx[u] = *reinterpret_cast<const uint4*>(x + off);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) accum(rd[u], rx[u]);
+    }
+    for (; p < p1; p += lanes) {
       const int64_t off = (base + p) * C + g * 8;
-      float d[8], xv[8];
-      unpack8(*reinterpret_cast<const uint4*>(dy + off), d);
-      unpack8(*reinterpret_cast<const uint4*>(x + off), xv);
-      if (relu) {
-        // the forward ReLU mask, recomputed from x with the forward's own scale / shift
-#pragma unroll
-        for (int i = 0; i < 8; ++i) d[i] = xv[i] * sc[i] + sh[i] > 0.f ? d[i] : 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float xh = (xv[i] - mu[i]) * is[i];
-        sg[i] += d[i];
-        sgx[i] += d[i] * xh;
-        sx[i] += xh;
-      }
+      accum(*reinterpret_cast<const uint4*>(dy + off), *reinterpret_cast<const uint4*>(x + off));
     }
   }
 #pragma unroll

@@ -166,6 +166,22 @@ struct WgradItems {
 bool launch_conv_wgrad_multi(const ConvWgradArgs& a, const WgradItems& it, int bm, float* db,
                              hipStream_t stream);
 
+// tap-fused multi-item weight gradient (conv_wgrad_taps.hip): workgroup = (128 Cout) x (64 Cin) x
+// all taps over a range of 8x8-pixel chunks; partial tiles go to a workspace and are reduced
+#define RAFT_WG_MAX_CI_CHUNKS 16
+struct WgradTapArgs {
+  int n_ci;                              // 64-wide Cin chunks
+  int ci_seg[RAFT_WG_MAX_CI_CHUNKS];     // input segment of each chunk
+  int ci_off[RAFT_WG_MAX_CI_CHUNKS];     // channel offset inside the segment
+  int ci_k[RAFT_WG_MAX_CI_CHUNKS];       // packed-K column of the chunk's first channel (tap 0)
+  int n_co;                              // 128-wide Cout tiles
+  int tiles_x, tiles_per_img, chunks_per_item, total_chunks, chunks_per_split, splits;
+  float* w_part;                         // [splits][cout][kpad]
+  float* db_part;                        // [splits][cout] or null
+};
+bool launch_conv_wgrad_taps(const ConvWgradArgs& a, const WgradItems& it, const WgradTapArgs& ta,
+                            float* db, hipStream_t stream);
+
 // db (nullable): fp32 bias gradient += column sums of G (fused)
 bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, float* db, hipStream_t stream);
 void launch_col_sum(const uint16_t* g, int stride, int cout, int P, float* db, hipStream_t stream);

@@ -107,17 +107,18 @@ class GraphedTrainStep:
 
     What is captured: the launch-bound recurrent part -- correlation volume, the 12 GRU
     iterations forward AND backward (the fused update block's ~900 kernels), convex upsampling and
-    the sequence loss (``RAFT.decode`` + ``sequence_loss`` + backward to the encoder outputs) --
-    and the parameter update (grad clip + fused AdamW).  What runs eagerly: the two encoders,
-    forward and backward (``RAFT.encode``, ~100 large MIOpen convolutions + fused norm nodes).
+    the sequence loss (``RAFT.decode`` + ``sequence_loss`` + backward to the encoder outputs).
+    What runs eagerly: the two encoders, forward and backward (``RAFT.encode``, ~100 large MIOpen
+    convolutions + fused norm nodes), and the parameter update (a few multi-tensor kernels).
     MIOpen's strided-convolution backward solvers are not replay-safe (replay 0 matches eager
     bit for bit, later replays read stale workspace / output state: profiles/r2/graph_cmp_*.log),
     and the encoders are not launch-bound anyway, so keeping them out of the graph costs nothing.
 
     Per step: eager encode -> copy the four encoder outputs into the graph's static leaves ->
-    replay g_dec (fills the update-block .grad and the leaves' .grad) -> eager encoder backward
-    from the leaves' gradients (accumulating into persistent encoder .grad buffers) -> (ranks > 1:
-    one flat RCCL all-reduce) -> replay g_up.
+    replay g_dec (fills the update-block .grad and the leaves' .grad) -> (ranks > 1: RCCL
+    all-reduce of the update-block gradients starts) -> eager encoder backward from the leaves'
+    gradients -> (all-reduce of the encoder gradients) -> clip + fused AdamW (multi-tensor
+    kernels, eager).
 
     The warm-up steps needed before capture (MIOpen solver search, allocator, lazy optimizer
     state) are real training steps; their effect on the weights, BN statistics, optimizer moments
@@ -165,22 +166,14 @@ class GraphedTrainStep:
                 self._step_body(*example, graphs=False)
         torch.cuda.current_stream(st.device).wait_stream(stream)
         torch.cuda.synchronize(st.device)
-        # persistent encoder gradient buffers (eager backward accumulates into them in place)
-        for p in self.enc_params:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-        self.enc_grads = [p.grad for p in self.enc_params]
 
         self.g_dec = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_dec, stream=stream):
             self.loss, self.metrics = self._decode()
         for p in self.dec_params:
-            if p.grad is None:  # no gradient this step: keep the optimizer's tensor list fixed
+            if p.grad is None:  # no gradient this step (fixed tensors for the replays)
                 p.grad = torch.zeros_like(p)
-        self.grads = [p.grad for p in self.params]
-        self.g_up = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_up, stream=stream):
-            self._update_graphable(self.loss)
+        self.dec_grads = [p.grad for p in self.dec_params]
         self.warmup_steps = warmup
         self._restore(snap)
 
@@ -216,11 +209,10 @@ class GraphedTrainStep:
 
     def _step_body(self, image1, image2, flow, valid, graphs=True):
         st = self.st
-        if graphs:
-            torch._foreach_zero_(self.enc_grads)
-        else:
-            for p in self.params:
-                p.grad = None
+        # encoder gradients are handed over by AccumulateGrad each step (no zero fill, no add
+        # kernel per parameter); the update-block gradients live in the decode graph's pool
+        for p in (self.enc_params if graphs else self.params):
+            p.grad = None
         if st.has_buffers and self.world > 1:
             pdist.broadcast_buffers(st.model)  # DataParallel semantics: replica 0's BN stats
         feats = self._encode_and_stage(image1, image2, flow, valid)
@@ -235,19 +227,17 @@ class GraphedTrainStep:
         work = self._post_part(self.dec_params, 0)      # overlaps the encoder backward
         self._encoder_backward(feats)
         del feats
-        if not graphs:
-            for p in self.enc_params:
-                if p.grad is None:
-                    p.grad = torch.zeros_like(p)
-            self.grads = [p.grad for p in self.params]
+        for p in self.enc_params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        self.grads = [p.grad for p in self.params]
         work2 = self._post_part(self.enc_params, self.n_dec)
         for w in (work, work2):
             if w is not None:
                 w.wait()
-        if graphs:
-            self.g_up.replay()
-        else:
-            self._update_graphable(loss)
+        # clip + fused AdamW: a handful of multi-tensor launches, issued eagerly (the encoder
+        # gradients are fresh tensors every step)
+        self._update_graphable(loss)
         self._sched()
         return loss
 

@@ -115,6 +115,27 @@ MAX_WG_ITEMS = 32
 _WG_FANIN = int(os.environ.get('RAFT_WG_FANIN', '48'))
 
 
+# weight-gradient kernel of the fused update blocks: 'taps' = tap-fused (conv_wgrad_taps.hip, one
+# workgroup per (128 Cout x 64 Cin) owns every tap, halo tiles in LDS), 'tile' = packed-K tiles
+_WG_IMPL = os.environ.get('RAFT_WGRAD_IMPL', 'taps')
+_TAP_KERNELS = {(1, 1), (1, 5), (5, 1), (3, 3)}
+
+
+def _taps_ok(in_off, in_cnt, ksize):
+    return (_WG_IMPL == 'taps' and tuple(ksize) in _TAP_KERNELS
+            and all(c % 64 == 0 for c in in_cnt) and all(o % 8 == 0 for o in in_off)
+            and sum(int(c) for c in in_cnt) // 64 <= 16)
+
+
+def conv_wgrad_taps(items, g_off, in_off, in_cnt, ksize, pad, cout, dw, db=None, splits=0):
+    """Tap-fused variant of :func:`conv_wgrad_multi` (segments must be multiples of 64 channels).
+    Partial tiles of the ``splits`` chunk ranges are reduced deterministically (no atomics)."""
+    ins = [b for _, bufs in items for b in bufs]
+    _ext.ops().conv_wgrad_taps_([g for g, _ in items], int(g_off), ins, [int(o) for o in in_off],
+                                [int(c) for c in in_cnt], int(ksize[0]), int(ksize[1]),
+                                int(pad[0]), int(pad[1]), int(cout), dw, db, int(splits))
+
+
 def conv_wgrad_multi(items, g_off, in_off, in_cnt, ksize, pad, cout, dw, db=None,
                      pix_per_split=None):
     """dw / db += the weight / bias gradient summed over ``items`` = [(g, [input buffers])] of one
@@ -123,6 +144,12 @@ def conv_wgrad_multi(items, g_off, in_off, in_cnt, ksize, pad, cout, dw, db=None
     ops = _ext.ops()
     n = len(items)
     assert 1 <= n <= MAX_WG_ITEMS
+    if pix_per_split is None and _taps_ok(in_off, in_cnt, ksize):
+        ins = [b for _, bufs in items for b in bufs]
+        ops.conv_wgrad_taps_([g for g, _ in items], int(g_off), ins, [int(o) for o in in_off],
+                             [int(c) for c in in_cnt], int(ksize[0]), int(ksize[1]), int(pad[0]),
+                             int(pad[1]), int(cout), dw, db, 0)
+        return
     if pix_per_split is None:
         g0 = items[0][0]
         p = g0.shape[0] * g0.shape[1] * g0.shape[2]

@@ -289,7 +289,10 @@ def _flush_wgrad(pk):
         k, pad, small = ((1, 1), (0, 0), False) if s.patch else (s.k, s.pad, s.small)
         same = all(it[1] == items[0][1] and [(o, c) for _, o, c in it[2]] ==
                    [(o, c) for _, o, c in items[0][2]] for it in items)
-        if small or not same or any(c % 128 for _, _, c in items[0][2]):
+        cnts = [c for _, _, c in items[0][2]]
+        offs = [o for _, o, _ in items[0][2]]
+        batched = C._taps_ok(offs, cnts, k) or not any(c % 128 for c in cnts)
+        if small or not same or not batched:
             for g, g_off, segs in items:
                 C.conv_wgrad(g, g_off, segs, k, pad, s.cout, dw, db, cin_small=2 if small else 0)
             continue

@@ -24,17 +24,21 @@ from pytorch_raft_amd.parallel import dist as pdist  # noqa: E402
 
 
 def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl):
-    """The graphed step's DP path: eager encoders + g_dec replay -> flat all-reduce -> g_up."""
+    """The graphed step's DP path: eager encoders + g_dec replay -> flat all-reduce -> update."""
     from pytorch_raft_amd.engine.trainer import GraphedTrainStep
     sd = {k: v.clone() for k, v in model.state_dict().items()}
     st = TrainState(model, args, dev, graph_ready=True)
     assert st.sync is None
     g = GraphedTrainStep(st, (i1[sl], i2[sl], flow[sl], valid[sl]), warmup=1)
     # one step up to the all-reduce: eager encoders + replayed decode + eager encoder backward
-    torch._foreach_zero_(g.enc_grads)
+    for p in g.enc_params:
+        p.grad = None
     feats = g._encode_and_stage(i1[sl], i2[sl], flow[sl], valid[sl])
     g.g_dec.replay()
     g._encoder_backward(feats)
+    for p in g.enc_params:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
     g._post()
     torch.cuda.synchronize()
     # flat is [update block | encoders]: back to model parameter order for the comparison

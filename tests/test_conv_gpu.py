@@ -233,3 +233,55 @@ def test_conv_wgrad_multi_items(ext_ops, cin, cout, k, segs, g_off, pps):
     scale = w.grad.abs().max().item()
     torch.testing.assert_close(got, w.grad, atol=2e-3 * scale, rtol=1e-3)
     torch.testing.assert_close(db, b.grad, atol=1e-3 * b.grad.abs().max().item(), rtol=1e-3)
+
+
+@pytest.mark.parametrize('cin,cout,k,segs,g_off,splits', [
+    (256, 192, (3, 3), None, 0, 0),
+    (384, 256, (1, 5), (128, 128, 128), 0, 0),
+    (384, 256, (5, 1), (128, 256), 0, 3),
+    (128, 576, (1, 1), None, 0, 0),
+    (128, 64, (3, 3), None, 64, 1),
+    (192, 126, (3, 3), (64, 128), 0, 0),
+    (64, 80, (3, 3), None, 0, 0),
+])
+def test_conv_wgrad_taps(ext_ops, cin, cout, k, segs, g_off, splits):
+    """Tap-fused weight gradient (halo tiles, all taps per workgroup, deterministic split reduce)
+    vs the fp32 PyTorch conv weight/bias gradient, summed over 3 items."""
+    torch.manual_seed(11)
+    B, H, W = 2, 13, 21
+    pad = (k[0] // 2, k[1] // 2)
+    w = torch.randn(cout, cin, *k, device=DEV, requires_grad=True)
+    b = torch.zeros(cout, device=DEV, requires_grad=True)
+    items = []
+    for _ in range(3):
+        x = torch.randn(B, cin, H, W, device=DEV).to(torch.bfloat16).float()
+        g = torch.randn(B, cout, H, W, device=DEV).to(torch.bfloat16).float()
+        F.conv2d(x, w, b, padding=pad).backward(g)
+        gb = torch.full((B, H, W, g_off + C.round_up(cout, 8)), 3.0, device=DEV,
+                        dtype=torch.bfloat16)
+        gb[..., g_off:g_off + cout] = C.nhwc(g)
+        if cout % 8:  # channels past cout inside the last 8-wide chunk are ignored
+            gb[..., g_off + cout:] = 5.0
+        if segs is None:
+            bufs = [C.nhwc(x)]
+        else:
+            bufs, o = [], 0
+            for c in segs:
+                bufs.append(C.nhwc(x[:, o:o + c]))
+                o += c
+        items.append((gb, bufs))
+    seg_cnt = [cin] if segs is None else list(segs)
+    dw = torch.ones(cout, k[0] * k[1] * cin, device=DEV)   # accumulates into existing values
+    db = torch.ones(cout, device=DEV)
+    C.conv_wgrad_taps(items, g_off, [0] * len(seg_cnt), seg_cnt, k, pad, cout, dw, db,
+                      splits=splits)
+    got = C.unpack_weight_grad(dw - 1.0, cout, seg_cnt, seg_cnt, k)
+    scale = w.grad.abs().max().item()
+    torch.testing.assert_close(got, w.grad, atol=2e-3 * scale, rtol=1e-3)
+    torch.testing.assert_close(db - 1.0, b.grad, atol=1e-3 * b.grad.abs().max().item(), rtol=1e-3)
+    # deterministic: a second run gives bit-identical results
+    dw2 = torch.ones_like(dw)
+    db2 = torch.ones_like(db)
+    C.conv_wgrad_taps(items, g_off, [0] * len(seg_cnt), seg_cnt, k, pad, cout, dw2, db2,
+                      splits=splits)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
