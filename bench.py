@@ -40,6 +40,8 @@ def parse(argv=None):
     ap.add_argument('--impl', choices=['hip', 'torch'], default='hip')
     ap.add_argument('--precision', choices=['bf16', 'fp16', 'fp32'], default='bf16')
     ap.add_argument('--alternate_corr', action='store_true')
+    ap.add_argument('--max_flow', type=float, default=20.0,
+                    help='synthetic ground-truth flow magnitude (px)')
     ap.add_argument('--channels_last', action='store_true')
     ap.add_argument('--small', action='store_true')
     ap.add_argument('--hipgraph', action='store_true', default=True,
@@ -136,7 +138,7 @@ def main(argv=None):
     st = TrainState(model, margs, device, graph_ready=use_graph)
 
     h, w = a.size
-    batches = device_batches(a.batch, h, w, device, count=2, seed=17 * rank)
+    batches = device_batches(a.batch, h, w, device, count=2, seed=17 * rank, max_flow=a.max_flow)
 
     if use_graph:
         from pytorch_raft_amd.engine.trainer import GraphedTrainStep

@@ -32,6 +32,10 @@ def main(argv=None):
     ap.add_argument('--impl', choices=['hip', 'torch'], default='hip')
     ap.add_argument('--precision', choices=['bf16', 'fp32'], default='bf16')
     ap.add_argument('--small', action='store_true')
+    ap.add_argument('--flow_init_px', type=float, default=0.0,
+                    help='warm-start flow magnitude (px at 1/8 res x 8): large lookup coordinates')
+    ap.add_argument('--discontinuous', action='store_true',
+                    help='flow_init piecewise constant on 4x4-cell blocks (motion boundaries)')
     a = ap.parse_args(argv)
 
     import torch
@@ -51,14 +55,27 @@ def main(argv=None):
     i1 = torch.rand(a.batch, 3, h, w, device=dev, generator=g) * 255
     i2 = torch.roll(i1, shifts=(3, -5), dims=(2, 3)).contiguous()
 
+    finit = None
+    if a.flow_init_px > 0:
+        ph, pw = (h + 7) // 8, (w + 7) // 8
+        if a.discontinuous:
+            lo = torch.rand(a.batch, 2, (ph + 3) // 4, (pw + 3) // 4, device=dev, generator=g)
+            finit = torch.nn.functional.interpolate(lo, scale_factor=4, mode='nearest')[..., :ph, :pw]
+        else:
+            lo = torch.rand(a.batch, 2, max(ph // 8, 2), max(pw // 8, 2), device=dev, generator=g)
+            finit = torch.nn.functional.interpolate(lo, size=(ph, pw), mode='bilinear',
+                                                    align_corners=False)
+        # flow at 1/8 resolution is in 1/8-res pixels: +-P full-res px = +-P/8 cells
+        finit = ((finit * 2 - 1) * (a.flow_init_px / 8.0)).contiguous()
+
     for _ in range(a.warmup):
-        out = runner(i1, i2)
+        out = runner(i1, i2, finit)
     if dev.type == 'cuda':
         torch.cuda.synchronize()
         torch.cuda.reset_peak_memory_stats()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        out = runner(i1, i2)
+        out = runner(i1, i2, finit)
     if dev.type == 'cuda':
         torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -80,7 +97,8 @@ def main(argv=None):
         'config': {'model': 'RAFT-small' if a.small else 'RAFT (full)', 'batch': a.batch,
                    'image_size': [h, w], 'padded': [(h + 7) // 8 * 8, (w + 7) // 8 * 8],
                    'iters': a.iters, 'impl': a.impl, 'hipgraph': runner.graph,
-                   'corr': 'alternate(on-the-fly)' if a.alternate_corr else 'all-pairs'},
+                   'corr': 'alternate(on-the-fly)' if a.alternate_corr else 'all-pairs',
+                   'flow_init_px': a.flow_init_px, 'discontinuous': a.discontinuous},
         'out_shape': list(flow_up.shape),
         'peak_hbm_gib': round(peak, 2),
         'finite': finite,

@@ -52,7 +52,7 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-static inline unsigned raft_cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+static inline __host__ __device__ unsigned raft_cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
 // ---- LDS-DMA (buffer_load ... lds) helpers shared by the MFMA conv kernels
 //

@@ -29,6 +29,20 @@ __device__ __forceinline__ uint4 buf_load16(rsrc_t r, uint32_t voff) {
   return __builtin_bit_cast(uint4, v);
 }
 
+// XCD-aware tile order for a 1-D grid padded to a multiple of 8: the dispatcher deals
+// consecutive workgroups round-robin over the 8 XCDs, so logical tile L = (id % 8) * (grid / 8) +
+// id / 8 gives every XCD a contiguous run of tiles: the N tiles of one M tile (same input rows)
+// and neighbouring M tiles (shared halo rows of the shifted taps) meet in the same L2.
+// Returns false for the padding workgroups.
+__device__ __forceinline__ bool conv_tile_coords(int n_m, int n_n, int& mt, int& nt) {
+  const int L = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+  if (L >= n_m * n_n) return false;
+  mt = L / n_n;
+  nt = L - mt * n_n;
+  return true;
+}
+inline int conv_grid_1d(int n_m, int n_n) { return (n_m * n_n + 7) / 8 * 8; }
+
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.f / (1.f + __expf(-v)); }
 __device__ __forceinline__ float tanhf_(float v) {
   const float e = __expf(-2.f * fabsf(v));

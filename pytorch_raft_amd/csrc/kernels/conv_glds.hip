@@ -3,6 +3,10 @@
 // (tile shapes x pipeline depths x epilogues) compile in parallel with conv_igemm.hip.
 #include "conv_common.h"
 
+#ifndef RAFT_CONV_UPFRONT
+#define RAFT_CONV_UPFRONT 1
+#endif
+
 namespace conv_detail {
 
 // ------------------------------------------------------------------ LDS-DMA variant
@@ -36,6 +40,7 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
   constexpr int A_PER = A_CHUNKS / NT, B_PER = B_CHUNKS / NT;
   constexpr int STAGE = A_CHUNKS + B_CHUNKS;  // 16-B slots per pipeline stage
   constexpr int LPS = A_PER + B_PER;          // DMA instructions per thread per step
+  constexpr bool UPFRONT = RAFT_CONV_UPFRONT && TM * TN >= 4;
 
   __shared__ __attribute__((aligned(16))) uint4 smem[NS * STAGE];
 
@@ -43,7 +48,9 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int HW = a.H * a.W;
   const int P = a.B * HW;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int mt, nt;
+  if (!conv_tile_coords(raft_cdiv(P, BM), raft_cdiv(a.cout, BN), mt, nt)) return;
+  const int m0 = mt * BM, n0 = nt * BN;
 
   int a_pix[A_PER], a_y[A_PER], a_x[A_PER], a_lc[A_PER];
 #pragma unroll
@@ -68,8 +75,12 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
     b_off[j] = n < a.cout ? (uint32_t)(((int64_t)n * a.kpad + lc * 8) * 2) : OOB;
   }
 
+  // K loop channel-chunk-major, taps inner: the KH*KW shifted reads of one 64-channel slice of
+  // the A rows follow each other while those rows are still in L2 (tap-major order re-fetched
+  // the whole tile per tap: ~10x the input's bytes went to MALL / HBM on the 1x5 / 5x1 convs)
   const int nchunk = a.cin_pad / BK;
-  const int steps = a.KH * a.KW * nchunk;
+  const int ntap = a.KH * a.KW;
+  const int steps = ntap * nchunk;
   rsrc_t seg_rs[3];
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
@@ -80,7 +91,7 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
   const uint32_t lds0 = raft_lds_addr(smem) + __builtin_amdgcn_readfirstlane(wave * 64 * 16);
 
   auto issue = [&](int t, int buf) {
-    const int tap = t / nchunk, ch = t - tap * nchunk;
+    const int ch = t / ntap, tap = t - ch * ntap;
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
     const int c0 = ch * BK;
     int s = 0, sbase = 0;
@@ -100,7 +111,7 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
       const uint32_t off = (uint32_t)(((a_pix[j] + dpix) * stride + coff + a_lc[j]) * 2);
       raft_dma16(rs, base + j * NT * 16, ok ? off : OOB);
     }
-    const uint32_t kb = (uint32_t)(t * BK * 2);
+    const uint32_t kb = (uint32_t)((tap * a.cin_pad + c0) * 2);
 #pragma unroll
     for (int j = 0; j < B_PER; ++j)
       raft_dma16(w_rs, base + (A_CHUNKS + j * NT) * 16, b_off[j] == OOB ? OOB : b_off[j] + kb);
@@ -113,6 +124,39 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // All fragments of the step are read up front (4 k-slices x (TM + TN) ds_reads) and the group
+  // barriers pin that order: the MFMAs of slice kk wait (counted lgkmcnt) only for their own
+  // reads while the later slices' reads are in flight.  Left to itself hipcc sank every read to
+  // just before its first MFMA with lgkmcnt(1) waits, exposing the LDS latency ~10x per step at
+  // one wave per SIMD (profiles/r2: 29% MFMA busy on the 5x2 tile).
+  auto compute_upfront = [&](int buf) {
+    const uint4* As = smem + buf * STAGE;
+    const uint4* Bs = As + A_CHUNKS;
+    bf16x8_t af[BK / 16][TM], bfr[BK / 16][TN];
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 32 + (lane & 31);
+        bfr[kk][j] = __builtin_bit_cast(bf16x8_t, Bs[swz(row, kk * 2 + (lane >> 5))]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 32 + (lane & 31);
+        af[kk][i] = __builtin_bit_cast(bf16x8_t, As[swz(row, kk * 2 + (lane >> 5))]);
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, (BK / 16) * (TM + TN), 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, (BK / 16) * TM * TN, 0);
+  };
 
   // fragments of k-slice kk+1 are read from LDS before the MFMAs of slice kk (two register sets),
   // so each ds_read has a whole slice of MFMAs to land instead of one or two
@@ -161,7 +205,8 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
       nb = nb >= NS ? nb - NS : nb;
       issue(t + NS - 1, nb);
     }
-    compute(cur);
+    if constexpr (UPFRONT) compute_upfront(cur);
+    else compute(cur);
     cur = cur + 1 == NS ? 0 : cur + 1;
   }
 
@@ -173,7 +218,7 @@ template <int EPI, int TM, int TN, int WVM, int NS>
 void launch_one_glds(const ConvFwdArgs& a, hipStream_t stream) {
   using T = ConvTile<TM, TN, WVM>;
   const int P = a.B * a.H * a.W;
-  dim3 grid(raft_cdiv(P, T::BM), raft_cdiv(a.cout, T::BN));
+  dim3 grid(conv_grid_1d(raft_cdiv(P, T::BM), raft_cdiv(a.cout, T::BN)));
   hipLaunchKernelGGL((conv_fwd_glds_kernel<TM, TN, WVM, EPI, NS>), grid, dim3(NT), 0, stream, a);
 }
 

@@ -59,7 +59,9 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int HW = a.H * a.W;
   const int P = a.B * HW;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int mt, nt;
+  if (!conv_tile_coords(raft_cdiv(P, BM), raft_cdiv(a.cout, BN), mt, nt)) return;
+  const int m0 = mt * BM, n0 = nt * BN;
 
   // per-thread A rows (fixed over the K loop): chunk e -> row e>>3, 16-B column e&7;
   // (pixel index, y, x) with y = -2^20 marking rows past P
@@ -76,7 +78,8 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
   }
 
   const int nchunk = SMALLC ? 0 : a.cin_pad / BK;
-  const int steps = SMALLC ? a.kpad / BK : a.KH * a.KW * nchunk;
+  const int ntap = a.KH * a.KW;
+  const int steps = SMALLC ? a.kpad / BK : ntap * nchunk;   // channel-chunk-major (conv_glds.hip)
   // buffer descriptors: out-of-range offsets (padding taps, rows past P, weight rows past cout)
   // read as zeros with no branch and no register pre-zeroing
   rsrc_t seg_rs[3];
@@ -89,7 +92,7 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
 
   auto load = [&](int t, uint4 (&ra)[A_PER], uint4 (&rb)[B_PER]) {
     if constexpr (!SMALLC) {
-      const int tap = t / nchunk, ch = t - tap * nchunk;
+      const int ch = t / ntap, tap = t - ch * ntap;
       const int kh = tap / a.KW, kw = tap - kh * a.KW;
       const int c0 = ch * BK;
       int s = 0, sbase = 0;
@@ -140,7 +143,12 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
       const int e = tid + j * NT;
       const int n = n0 + (e >> 3);
       // rows past cout read as zeros (range-checked descriptor); the packed tensor may end there
-      const uint32_t off = (uint32_t)(((int64_t)n * a.kpad + t * BK + (e & 7) * 8) * 2);
+      int kcol = t * BK;
+      if constexpr (!SMALLC) {
+        const int ch = t / ntap, tap = t - ch * ntap;
+        kcol = tap * a.cin_pad + ch * BK;
+      }
+      const uint32_t off = (uint32_t)(((int64_t)n * a.kpad + kcol + (e & 7) * 8) * 2);
       rb[j] = buf_load16(w_rs, e < B_CHUNKS ? off : OOB);
     }
   };
@@ -260,7 +268,7 @@ template <int EPI, bool SMALLC, int TM, int TN, int WVM>
 void launch_one(const ConvFwdArgs& a, hipStream_t stream) {
   using T = ConvTile<TM, TN, WVM>;
   const int P = a.B * a.H * a.W;
-  dim3 grid(raft_cdiv(P, T::BM), raft_cdiv(a.cout, T::BN));
+  dim3 grid(conv_grid_1d(raft_cdiv(P, T::BM), raft_cdiv(a.cout, T::BN)));
   hipLaunchKernelGGL((conv_fwd_kernel<TM, TN, WVM, EPI, SMALLC>), grid, dim3(NT), 0, stream, a);
 }
 

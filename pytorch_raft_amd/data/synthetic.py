@@ -51,5 +51,6 @@ class SyntheticPairs(torch.utils.data.Dataset):
         return i1[0], i2[0], f[0], v[0]
 
 
-def device_batches(batch, h, w, device, count=2, seed=0):
-    return [make_pair_batch(batch, h, w, device=device, seed=seed + k) for k in range(count)]
+def device_batches(batch, h, w, device, count=2, seed=0, max_flow=20.0):
+    return [make_pair_batch(batch, h, w, device=device, seed=seed + k, max_flow=max_flow)
+            for k in range(count)]
