@@ -40,6 +40,8 @@ def parse(argv=None):
     ap.add_argument('--impl', choices=['hip', 'torch'], default='hip')
     ap.add_argument('--precision', choices=['bf16', 'fp16', 'fp32'], default='bf16')
     ap.add_argument('--alternate_corr', action='store_true')
+    ap.add_argument('--corr_mode', choices=['auto', 'allpairs', 'onthefly'], default='auto',
+                    help="auto: all-pairs while the pyramid fits RAFT_CORR_BUDGET_GB, else on-the-fly")
     ap.add_argument('--max_flow', type=float, default=20.0,
                     help='synthetic ground-truth flow magnitude (px)')
     ap.add_argument('--channels_last', action='store_true')
@@ -114,7 +116,7 @@ def main(argv=None):
     margs = argparse.Namespace(
         small=a.small, mixed_precision=a.precision != 'fp32',
         amp_dtype='float16' if a.precision == 'fp16' else 'bfloat16',
-        alternate_corr=a.alternate_corr, dropout=0.0,
+        alternate_corr=a.alternate_corr, dropout=0.0, corr_mode=a.corr_mode,
         corr_impl='torch' if a.impl == 'torch' else 'auto',
         channels_last=a.channels_last,
         lr=4e-4, wdecay=1e-4, epsilon=1e-8, num_steps=100000, iters=a.iters, gamma=0.8,
@@ -217,6 +219,9 @@ def main(argv=None):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t.item())
     peak = torch.cuda.max_memory_allocated(device) / 2 ** 30 if device.type == 'cuda' else 0.0
+    # a hipGraph replay allocates nothing (its private pool was sized at capture): the reserved
+    # peak is the footprint that includes the graphed decode's buffers
+    reserved = torch.cuda.max_memory_reserved(device) / 2 ** 30 if device.type == 'cuda' else 0.0
     nonfinite_steps = float(st.nonfinite.item())
     ok = st.check_finite()
     pairs = a.batch * world * a.steps
@@ -248,10 +253,11 @@ def main(argv=None):
             'iters': a.iters,
             'parallelism': 'dp%d' % world,
             'impl': a.impl,
-            'corr': 'alternate(on-the-fly)' if a.alternate_corr else 'all-pairs',
+            'corr': getattr(model, 'last_corr', None), 'corr_mode': a.corr_mode,
             'hipgraph': use_graph,
         },
         'peak_hbm_gib_rank0': round(peak, 2),
+        'peak_reserved_gib_rank0': round(reserved, 2),
         'loss_finite': ok,
         'nonfinite_steps': nonfinite_steps,
         # host time to issue one step on an idle queue (3 extra untimed steps); vs ms_per_step

@@ -29,6 +29,8 @@ def main(argv=None):
     ap.add_argument('--size', type=int, nargs=2, default=[436, 1024])
     ap.add_argument('--graph', action='store_true', help='capture the forward as one hipGraph')
     ap.add_argument('--alternate_corr', action='store_true')
+    ap.add_argument('--corr_mode', choices=['auto', 'allpairs', 'onthefly'], default='auto',
+                    help="auto: all-pairs while the pyramid fits RAFT_CORR_BUDGET_GB, else on-the-fly")
     ap.add_argument('--impl', choices=['hip', 'torch'], default='hip')
     ap.add_argument('--precision', choices=['bf16', 'fp32'], default='bf16')
     ap.add_argument('--small', action='store_true')
@@ -45,6 +47,7 @@ def main(argv=None):
     dev = torch.device('cuda', 0) if torch.cuda.is_available() else torch.device('cpu')
     margs = argparse.Namespace(small=a.small, mixed_precision=a.precision == 'bf16',
                                amp_dtype='bfloat16', alternate_corr=a.alternate_corr, dropout=0.0,
+                               corr_mode=a.corr_mode,
                                corr_impl='torch' if a.impl == 'torch' else 'auto')
     torch.manual_seed(1234)
     model = RAFT(margs).to(dev).eval()
@@ -72,7 +75,6 @@ def main(argv=None):
         out = runner(i1, i2, finit)
     if dev.type == 'cuda':
         torch.cuda.synchronize()
-        torch.cuda.reset_peak_memory_stats()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         out = runner(i1, i2, finit)
@@ -81,7 +83,15 @@ def main(argv=None):
     el = time.perf_counter() - t0
     flow_low, flow_up = out
     finite = bool(torch.isfinite(flow_up).all().item())
+    # allocator peak over warm-up + timed steps (a graph replay allocates nothing: its pool was
+    # sized during capture, which max_memory_reserved covers) and the device's own used bytes
     peak = torch.cuda.max_memory_allocated(dev) / 2 ** 30 if dev.type == 'cuda' else 0.0
+    reserved = torch.cuda.max_memory_reserved(dev) / 2 ** 30 if dev.type == 'cuda' else 0.0
+    if dev.type == 'cuda':
+        free, total = torch.cuda.mem_get_info(dev)
+        used = (total - free) / 2 ** 30
+    else:
+        used, total = 0.0, 0
     res = {
         'metric': 'inference image-pairs/sec (1 GPU), RAFT Sintel %dx%d iters=%d test_mode' % (h, w, a.iters),
         'value': round(a.batch * a.steps / el, 3),
@@ -97,10 +107,13 @@ def main(argv=None):
         'config': {'model': 'RAFT-small' if a.small else 'RAFT (full)', 'batch': a.batch,
                    'image_size': [h, w], 'padded': [(h + 7) // 8 * 8, (w + 7) // 8 * 8],
                    'iters': a.iters, 'impl': a.impl, 'hipgraph': runner.graph,
-                   'corr': 'alternate(on-the-fly)' if a.alternate_corr else 'all-pairs',
+                   'corr': getattr(model, 'last_corr', None), 'corr_mode': a.corr_mode,
                    'flow_init_px': a.flow_init_px, 'discontinuous': a.discontinuous},
         'out_shape': list(flow_up.shape),
         'peak_hbm_gib': round(peak, 2),
+        'peak_reserved_gib': round(reserved, 2),
+        'device_used_gib': round(used, 2),
+        'device_total_gib': round(total / 2 ** 30, 1),
         'finite': finite,
     }
     print(json.dumps(res), flush=True)

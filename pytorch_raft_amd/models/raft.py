@@ -14,10 +14,21 @@ MI355X-specific extensions (all optional ``args`` attributes, defaults chosen fo
 * ``amp_dtype``   autocast dtype for ``mixed_precision`` -- 'bfloat16' (default; MI355X MFMA native)
                   or 'float16' (reference behaviour on CUDA)
 * ``channels_last`` run the encoders in NHWC (MIOpen's NHWC implicit-GEMM solvers)
+* ``corr_mode``   'auto' (default) | 'allpairs' | 'onthefly'.  ``alternate_corr=True`` (the
+                  reference flag, `core/raft.py:105-108`) always selects the on-the-fly block.
+                  'auto' is memory-aware: the all-pairs pyramid (B x (HW/64)^2 x 4/3 elements) is
+                  used while it fits in ``RAFT_CORR_BUDGET_GB`` (default: a quarter of the GPU's
+                  HBM, 72 GB on MI355X), the O(HW) on-the-fly correlation beyond that.  Both give
+                  the same values; all-pairs is the faster of the two at every batch that fits
+                  (profiles/r2/sweep: 395 vs 358 training pairs/s at batch 12, 325 vs 317
+                  inference pairs/s at Sintel batch 64), on-the-fly is what makes batch-1024
+                  Sintel inference or 4K frames fit.
 
 In test mode the convex upsampling runs only after the last iteration (the reference computes and
 discards it every iteration, `core/raft.py:133-142`); outputs are identical.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -31,6 +42,20 @@ from ..ops import _ext
 
 def _get(args, name, default):
     return getattr(args, name, default)
+
+
+_BUDGET = {}
+
+
+def corr_budget_bytes(device):
+    """HBM the all-pairs pyramid may take before 'auto' switches to on-the-fly correlation."""
+    env = os.environ.get('RAFT_CORR_BUDGET_GB')
+    if env:
+        return float(env) * 2 ** 30
+    key = (device.type, device.index)
+    if key not in _BUDGET:
+        _BUDGET[key] = 0.25 * torch.cuda.get_device_properties(device).total_memory
+    return _BUDGET[key]
 
 
 class RAFT(nn.Module):
@@ -122,12 +147,14 @@ class RAFT(nn.Module):
 
     def decode(self, fmap1, fmap2, net, inp, iters=12, flow_init=None, test_mode=False):
         """Correlation volume + GRU iterations + upsampling (`core/raft.py:102-144`)."""
-        if not (self._bf16_corr_ok(fmap1) and not self.args.alternate_corr):
+        otf = self._use_onthefly(fmap1)
+        self.last_corr = 'on-the-fly' if otf else 'all-pairs'
+        if not (self._bf16_corr_ok(fmap1) and not otf):
             # the reference runs the correlation in fp32 (`core/raft.py:102-103`); the bf16 HIP
             # build takes the bf16 encoder outputs as they are (same products, fp32 accumulation)
             fmap1 = fmap1.float().contiguous()
             fmap2 = fmap2.float().contiguous()
-        if self.args.alternate_corr:
+        if otf:
             # mixed precision: bf16 MFMA operands; fp32 model: split-bf16 (fp32-accurate) forward
             corr_fn = AlternateCorrBlock(fmap1, fmap2, radius=self.args.corr_radius,
                                          impl=self.corr_impl,
@@ -165,6 +192,19 @@ class RAFT(nn.Module):
         if test_mode:
             return coords1 - coords0, flow_up
         return flow_predictions
+
+    def _use_onthefly(self, fmap):
+        """Correlation block choice (see ``corr_mode`` in the module docstring)."""
+        mode = _get(self.args, 'corr_mode', 'auto')
+        if self.args.alternate_corr or mode == 'onthefly':
+            return True
+        if mode == 'allpairs' or fmap.device.type != 'cuda':
+            return False
+        b, _, h, w = fmap.shape
+        n = h * w
+        esz = 2 if self._bf16_corr_ok(fmap) else 4
+        pyramid = b * n * n * esz * (1 + 1 / 4 + 1 / 16 + 1 / 64)
+        return pyramid > corr_budget_bytes(fmap.device)
 
     def _bf16_corr_ok(self, fmap):
         return (fmap.dtype == torch.bfloat16 and self.corr_impl != 'torch' and

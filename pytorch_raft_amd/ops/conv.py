@@ -73,7 +73,22 @@ def pack_weight_dgrad(w, out_real, out_pad, npad_mult=128):
 
 def conv_fwd(segs, wpk, bias, ksize, pad, cout, epi, outs, out_offs, aux=(), aux_offs=(),
              scale=1.0, split=0, cin_small=0, bn=None):
-    """Launch the implicit-GEMM conv.  ``segs`` = [(buffer, offset, count)], ``outs`` buffers."""
+    """Launch the implicit-GEMM conv.  ``segs`` = [(buffer, offset, count)], ``outs`` buffers.
+
+    The kernels address every operand through a 32-bit buffer descriptor (range-checked loads
+    give the zero padding for free), so one launch covers < 2 GiB per buffer; larger batches
+    (e.g. Sintel-size inference at batch 512+) are issued as batch slices."""
+    limit = 1 << 31
+    big = max(t.numel() * t.element_size() for t in [s[0] for s in segs] + list(outs) + list(aux))
+    if big >= limit:
+        b = segs[0][0].shape[0]
+        step = max(1, (limit - 1) * b // big)
+        for b0 in range(0, b, step):
+            sl = slice(b0, min(b, b0 + step))
+            conv_fwd([(t[sl], o, c) for t, o, c in segs], wpk, bias, ksize, pad, cout, epi,
+                     [t[sl] for t in outs], out_offs, [t[sl] for t in aux], aux_offs, scale,
+                     split, cin_small, bn)
+        return
     ops = _ext.ops()
     ins = [s[0] for s in segs]
     ops.conv_fwd_(ins, [int(s[1]) for s in segs], [int(s[2]) for s in segs], wpk, bias,

@@ -117,3 +117,18 @@ def test_wgrad_overlap_matches_inline(ext_ops):
         assert diff <= 4 * noise + 3e-2 * scale + 1e-7, (diff, noise, scale)
         cos = torch.nn.functional.cosine_similarity(a.reshape(1, -1), b.reshape(1, -1)).item()
         assert cos > 0.999, cos
+
+
+def test_auto_corr_mode_switches_on_budget(ext_ops, monkeypatch):
+    """corr_mode='auto': all-pairs while the pyramid fits the HBM budget, on-the-fly past it --
+    same flow either way (the two blocks compute the same windows)."""
+    i1, i2, _, _ = make_pair_batch(2, 128, 160, device=DEV)
+    m = _model('hip').eval()
+    with torch.no_grad():
+        lo_ap, up_ap = m(i1, i2, iters=4, test_mode=True)
+        assert m.last_corr == 'all-pairs'
+        monkeypatch.setenv('RAFT_CORR_BUDGET_GB', '1e-6')   # 1 KiB: any pyramid exceeds it
+        lo_ot, up_ot = m(i1, i2, iters=4, test_mode=True)
+        assert m.last_corr == 'on-the-fly'
+    torch.testing.assert_close(lo_ot, lo_ap, atol=2e-3, rtol=1e-3)
+    torch.testing.assert_close(up_ot, up_ap, atol=2e-2, rtol=1e-3)
