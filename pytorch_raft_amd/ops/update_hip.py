@@ -27,6 +27,8 @@ Weights are packed once per forward pass by ``_UpdateWeights`` whose backward (r
 after every iteration's backward) unpacks the accumulated packed gradients into the nn.Conv2d
 ``.grad`` tensors -- the checkpoint layout is unchanged.
 """
+import os
+
 import torch
 
 from . import _ext
@@ -435,6 +437,49 @@ def _backward_overlapped(st, pk, n):
     return (None,) * (1 + n)
 
 
+# ---------------------------------------------------------------- independent branches
+# Each conv of an iteration is small (34k pixels at batch 12) and latency-bound, so two
+# independent chains run concurrently on a second HIP stream and fill the CUs the other leaves
+# idle: forward -- motion encoder flow branch (f1 -> f2) || correlation branch (c1 -> c2), mask
+# conv m2 || flow-head conv fh2; backward -- m2 dgrad || fh2 dgrad, f2 dgrad || c2 -> c1 dgrad.
+# Every buffer the branch touches is allocated on the main stream before the fork and stays
+# referenced until after the join, so the caching allocator never hands it out while the branch
+# runs.  Captured into the training hipGraph as parallel branches.
+# OFF by default (RAFT_UPDATE_BRANCHES=1 enables it): measured 381-383 vs 397-398 pairs/s
+# without -- co-running convs slow each other more than the overlap gains (kernel sum per step
+# 31.0 -> 33.0 ms: the XCD-local tile order and L2 reuse of each conv are lost when two grids
+# share the XCDs).
+_BRANCHES = os.environ.get('RAFT_UPDATE_BRANCHES', '0') == '1'
+_BRANCH = {}
+
+
+class _Branch:
+    def __init__(self, dev):
+        self.side = None
+        if _BRANCHES and dev.type == 'cuda':
+            key = dev.index if dev.index is not None else torch.cuda.current_device()
+            if key not in _BRANCH:
+                _BRANCH[key] = torch.cuda.Stream(device=dev)
+            self.side = _BRANCH[key]
+            self.main = torch.cuda.current_stream(dev)
+            self.side.wait_stream(self.main)
+
+    def __enter__(self):
+        if self.side is not None:
+            self._ctx = torch.cuda.stream(self.side)
+            self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.side is not None:
+            self._ctx.__exit__(*exc)
+        return False
+
+    def join(self):
+        if self.side is not None:
+            self.main.wait_stream(self.side)
+
+
 def _bf16(shape, dev):
     return torch.empty(*shape, device=dev, dtype=torch.bfloat16)
 
@@ -469,10 +514,13 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
         C.conv_fwd(segs, w, b, k, pad, cout, epi, outs, offs, aux,
                    aux_offs, scale=s.scale, split=split, cin_small=2 if small else 0)
 
+    br = _Branch(dev)
+    with br:
+        conv('f1', [(patch, 0, 128)], C.EPI_RELU_BF16, [f1], [0])
+        conv('f2', [(f1, 0, 128)], C.EPI_RELU_BF16, [cf], [192])
     conv('c1', [(corr, 0, CORR_BUF)], C.EPI_RELU_BF16, [c1], [0])
     conv('c2', [(c1, 0, 256)], C.EPI_RELU_BF16, [cf], [0])
-    conv('f1', [(patch, 0, 128)], C.EPI_RELU_BF16, [f1], [0])
-    conv('f2', [(f1, 0, 128)], C.EPI_RELU_BF16, [cf], [192])
+    br.join()
     conv('conv', [(cf, 0, 256)], C.EPI_RELU_BF16, [mf], [0])
     gates = {}
     hin = h
@@ -490,9 +538,12 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
     if need_mask:
         fm = _bf16(sh + (512,), dev)
         conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0])
-        ops.fh2_fwd_(fm, pk.fh2_wf, pk.b32, delta)
         mask = _bf16(sh + (576,), dev)
-        conv('m2', [(fm, 256, 256)], C.EPI_BF16, [mask], [0])
+        br = _Branch(dev)
+        with br:
+            conv('m2', [(fm, 256, 256)], C.EPI_BF16, [mask], [0])
+        ops.fh2_fwd_(fm, pk.fh2_wf, pk.b32, delta)
+        br.join()
     else:
         fm = _bf16(sh + (256,), dev)
         conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0], cout=256)
@@ -561,12 +612,15 @@ class _UpdateIter(torch.autograd.Function):
             gmask = gmask.to(torch.bfloat16)
         # the head's ReLU backward is fused into both dgrad epilogues (bf16 pre-activation grads)
         dpre_head = _bf16(sh + (512,), dev)
-        wgrad('m2', gmask, 0, [(fm, 256, 256)])
-        dgrad('m2', [(gmask, 0, 576)], [(dpre_head, 256, 256, 256, 0, fm, 256)], scale=0.25)
-        # ---- flow head conv2 -> delta (VALU kernels; fp32 output gradient read directly)
         gd = gdelta.contiguous().float()
+        wgrad('m2', gmask, 0, [(fm, 256, 256)])
+        br = _Branch(dev)
+        with br:
+            dgrad('m2', [(gmask, 0, 576)], [(dpre_head, 256, 256, 256, 0, fm, 256)], scale=0.25)
+        # ---- flow head conv2 -> delta (VALU kernels; fp32 output gradient read directly)
         pk.fh2_items.append((gd, fm))
         ops.fh2_dgrad_(gd, pk.fh2_wd, fm, dpre_head)
+        br.join()
         # ---- head
         wgrad('head', dpre_head, 0, [(h2, 0, HD)])
         dh = gh.float().contiguous() if gh is not None else _f32(sh + (HD,), dev, zero=True)
@@ -608,14 +662,17 @@ class _UpdateIter(torch.autograd.Function):
         wgrad('c2', dpre_cf, 0, [(c1, 0, 256)])
         wgrad('f2', dpre_cf, 192, [(f1, 0, 128)])
         dpre_c1 = _bf16(sh + (256,), dev)
-        dgrad('c2', [(dpre_cf, 0, 192)], [(dpre_c1, 0, 256, 256, 0, c1, 0)])
         dpre_f1 = _bf16(sh + (128,), dev)
-        dgrad('f2', [(dpre_cf, 192, 64)], [(dpre_f1, 0, 128, 128, 0, f1, 0)])
-        wgrad('f1', dpre_f1, 0, [(patch, 0, 128)])
-        wgrad('c1', dpre_c1, 0, [(corr, 0, CORR_BUF)])
         # bf16 (the dtype of the corr input): autograd would otherwise cast an fp32 gradient
         dcorr = _bf16(sh + (CORR_BUF,), dev)
+        br = _Branch(dev)
+        with br:   # f2's input gradient only feeds f1's (deferred) weight gradient
+            dgrad('f2', [(dpre_cf, 192, 64)], [(dpre_f1, 0, 128, 128, 0, f1, 0)])
+        dgrad('c2', [(dpre_cf, 0, 192)], [(dpre_c1, 0, 256, 256, 0, c1, 0)])
         dgrad('c1', [(dpre_c1, 0, 256)], [(dcorr, 0, CORR_BUF, 324, 0)])  # slots 324.. unused
+        br.join()
+        wgrad('f1', dpre_f1, 0, [(patch, 0, 128)])
+        wgrad('c1', dpre_c1, 0, [(corr, 0, CORR_BUF)])
         if ctx.itr == 0:
             st.dinp_acc = None
             st.next_bwd = None
