@@ -803,8 +803,9 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
   int64_t cin_pad = 0;
   ta.n_ci = 0;
   for (int64_t s = 0; s < nseg; ++s) {
-    TORCH_CHECK(in_cnt[s] % 64 == 0 && in_off[s] % 8 == 0,
-                "tap-fused wgrad: segments must be multiples of 64 channels");
+    // 64-channel chunks; the last segment may end in a 32-channel tail (the encoders' 96)
+    TORCH_CHECK(in_off[s] % 8 == 0 && (in_cnt[s] % 64 == 0 || (s == nseg - 1 && in_cnt[s] % 32 == 0)),
+                "tap-fused wgrad: segments must be multiples of 64 channels (last: of 32)");
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
     for (int64_t c = 0; c < in_cnt[s]; c += 64) {
@@ -812,6 +813,7 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
       ta.ci_seg[ta.n_ci] = (int)s;
       ta.ci_off[ta.n_ci] = (int)c;
       ta.ci_k[ta.n_ci] = (int)(cin_pad + c);
+      ta.ci_cnt[ta.n_ci] = (int)std::min<int64_t>(64, in_cnt[s] - c);
       ++ta.n_ci;
     }
     cin_pad += in_cnt[s];
@@ -843,7 +845,8 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
   TORCH_CHECK(kpad % 4 == 0, "packed K must be a multiple of 4");
   a.dw = dw.data_ptr<float>();
   a.kpad = (int)kpad;
-  ta.n_co = (int)((cout + 127) / 128);
+  ta.bm = (kh == 3 && kw == 3 && cout <= 64) ? 64 : 128;
+  ta.n_co = (int)((cout + ta.bm - 1) / ta.bm);
   ta.tiles_x = (int)((W + 7) / 8);
   ta.tiles_per_img = (int)(((H + 7) / 8) * ta.tiles_x);
   ta.chunks_per_item = (int)(B * ta.tiles_per_img);
@@ -852,7 +855,7 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
     // one full round of equal-sized workgroups (resident per CU: 1 for 3x3 -- 9 x 2 accumulator
     // tiles fill the register file --, 2 for the 5-tap convs, 3 for 1x1); every extra split
     // costs a cout x kpad fp32 partial written and re-read
-    const int64_t per_cu = kh * kw == 9 ? 1 : (kh * kw == 5 ? 2 : 3);
+    const int64_t per_cu = kh * kw == 9 ? (ta.bm == 64 ? 2 : 1) : (kh * kw == 5 ? 2 : 3);
     const int64_t pairs = (int64_t)ta.n_co * ta.n_ci;
     splits = std::max<int64_t>(1, std::min<int64_t>(256 * per_cu / pairs, ta.total_chunks / 8));
   }

@@ -29,7 +29,6 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4_t;
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
-constexpr int BM = 128;           // Cout per workgroup (2 x 64)
 constexpr int BC = 64;            // Cin per workgroup
 constexpr int TP = 8;             // pixel tile edge (8 x 8 = 64 pixels per chunk)
 constexpr uint32_t OOB = 0x80000000u;
@@ -38,35 +37,42 @@ __device__ __forceinline__ rsrc_t mk_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-// LDS images: G rows 256 B (128 co), X rows 128 B (64 ci); XOR swizzle of the 16-B chunk index
+// LDS images: G rows 256 B (128 co) or 128 B (64 co), X rows 128 B (64 ci); XOR swizzle of the
+// 16-B chunk index by row
 __device__ __forceinline__ int swz_g(int row) { return 4 * (row & 3); }
 __device__ __forceinline__ int swz_x(int row) { return 4 * ((row >> 1) & 1); }
+template <int ROWB>
+__device__ __forceinline__ int swz_rows(int row) { return ROWB == 256 ? swz_g(row) : swz_x(row); }
 
-// TG tap groups: 4 x TG waves; wave (tg, wm, wn) owns taps [tg*TPG, +TPG) of Cout [wm*64, +64) x
-// Cin [wn*32, +32).  TG = 2 for 3x3 keeps 2 x 5 accumulator tiles per wave (2 waves per SIMD
-// instead of 1 wave holding all 18: the second wave hides the first one's LDS / barrier waits).
-template <int KH, int KW, int TG>
+// Workgroup = BMT Cout (64 or 128) x 64 Cin x all taps.  TG tap groups x (BMT / 64) x 2 waves;
+// wave (tg, wm, wn) owns taps [tg*TPG, +TPG) of Cout [wm*64, +64) x Cin [wn*32, +32).  TG = 2
+// for 3x3 at BMT = 128 keeps 2 x 5 accumulator tiles per wave (2 waves per SIMD instead of 1
+// wave holding all 18: the second wave hides the first one's LDS / barrier waits); BMT = 64
+// (Cout <= 64: the encoders' 64-channel layers, the motion encoder's f2) uses TG = 3.
+template <int KH, int KW, int TG, int BMT>
 struct TapGeo {
-  static constexpr int NT = 256 * TG;
+  static constexpr int WMW = BMT / 64;                // waves along Cout
+  static constexpr int NT = 64 * WMW * 2 * TG;
+  static constexpr int GRB = BMT * 2;                 // G row bytes
+  static constexpr int G_CPR = BMT / 8;               // 16-B chunks per G row
   static constexpr int T = KH * KW;
   static constexpr int TPG = (T + TG - 1) / TG;      // taps per group
   static constexpr int HWD = TP + KW - 1;            // halo width
   static constexpr int HALO = (TP + KH - 1) * HWD;   // halo rows (pixels)
-  static constexpr int G_CH = 64 * (BM / 8);         // 16-B chunks of the G tile (1024)
+  static constexpr int G_CH = 64 * G_CPR;            // 16-B chunks of the G tile
   static constexpr int X_CH = HALO * (BC / 8);
-  static constexpr int G_PER = G_CH / NT;            // DMA instructions per thread
+  static constexpr int G_PER = (G_CH + NT - 1) / NT;  // DMA instructions per thread
   static constexpr int X_PER = (X_CH + NT - 1) / NT;
-  static constexpr int G_BYTES = G_CH * 16;
+  static constexpr int G_BYTES = G_PER * NT * 16;    // lane-linear DMA images (rounded up)
   static constexpr int X_BYTES = X_PER * NT * 16;    // lane-linear DMA image (rounded up)
   static constexpr int STAGE = G_BYTES + X_BYTES;
 };
 
-template <int KH, int KW, int TG>
-__global__ __launch_bounds__(256 * TG, 1) void conv_wgrad_taps_kernel(ConvWgradArgs a,
-                                                                      WgradItems it,
-                                                                      WgradTapArgs ta) {
-  using Geo = TapGeo<KH, KW, TG>;
-  constexpr int NT = Geo::NT;
+template <int KH, int KW, int TG, int BMT>
+__global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_taps_kernel(
+    ConvWgradArgs a, WgradItems it, WgradTapArgs ta) {
+  using Geo = TapGeo<KH, KW, TG, BMT>;
+  constexpr int NT = Geo::NT, GRB = Geo::GRB, G_CPR = Geo::G_CPR, WMW = Geo::WMW;
   constexpr int T = Geo::T, TPG = Geo::TPG, HWD = Geo::HWD, HALO = Geo::HALO;
   constexpr int G_PER = Geo::G_PER, X_PER = Geo::X_PER, LPS = G_PER + X_PER;
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * Geo::STAGE];
@@ -82,7 +88,8 @@ __global__ __launch_bounds__(256 * TG, 1) void conv_wgrad_taps_kernel(ConvWgradA
   if (L >= pairs * ta.splits) return;            // grid padded to a multiple of 8
   const int pair = L % pairs;
   const int ci_chunk = pair % ta.n_ci;
-  const int m0 = (pair / ta.n_ci) * BM;
+  const int m0 = (pair / ta.n_ci) * BMT;
+  const int ci_cnt = ta.ci_cnt[ci_chunk];         // valid channels of this chunk (64 or 32)
   const int sidx = ta.ci_seg[ci_chunk];           // input segment of this Cin chunk (uniform)
   const int coff = ta.ci_off[ci_chunk];           // channel offset inside that segment
   const int kbase = ta.ci_k[ci_chunk];            // first packed-K column of this chunk (tap 0)
@@ -93,15 +100,16 @@ __global__ __launch_bounds__(256 * TG, 1) void conv_wgrad_taps_kernel(ConvWgradA
   const bool do_bias = ta.db_part != nullptr && ci_chunk == 0;
   const int stride = a.seg[sidx].stride;
 
-  // DMA slots: G chunk e = tid + j*NT -> (pixel row e>>4, physical 16-B chunk e&15)
+  // DMA slots: G chunk e = tid + j*NT -> (pixel row e / G_CPR, physical 16-B chunk e % G_CPR);
+  // slots past the tile (rounding of the lane-linear image) load nothing
   int g_row[G_PER];
   uint32_t g_col[G_PER];
 #pragma unroll
   for (int j = 0; j < G_PER; ++j) {
     const int e = tid + j * NT;
-    const int row = e >> 4, lc = (e & 15) ^ swz_g(row);
-    g_row[j] = row;
-    g_col[j] = m0 + lc * 8 < a.cout ? (uint32_t)(m0 + lc * 8) * 2u : OOB;
+    const int row = e / G_CPR, lc = (e % G_CPR) ^ swz_rows<GRB>(row);
+    g_row[j] = row < 64 ? row : 0;
+    g_col[j] = (row < 64 && m0 + lc * 8 < a.cout) ? (uint32_t)(m0 + lc * 8) * 2u : OOB;
   }
   int x_hy[X_PER], x_hx[X_PER];
   uint32_t x_col[X_PER];
@@ -145,8 +153,8 @@ __global__ __launch_bounds__(256 * TG, 1) void conv_wgrad_taps_kernel(ConvWgradA
 
   // wave (tg, wm, wn): per 16-pixel k-step 2 G fragments (shared by the group's taps) + TPG X
   // fragments for 2 TPG MFMAs
-  const int tg = __builtin_amdgcn_readfirstlane(wave >> 2);
-  const int wm = (wave >> 1) & 1, wn = wave & 1;
+  const int tg = __builtin_amdgcn_readfirstlane(wave / (2 * WMW));
+  const int wm = (wave >> 1) % WMW, wn = wave & 1;
   const int t0 = tg * TPG;
   f32x16 acc[TPG][2];
 #pragma unroll
@@ -176,8 +184,8 @@ __global__ __launch_bounds__(256 * TG, 1) void conv_wgrad_taps_kernel(ConvWgradA
       bf16x8_t af[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const bf16x4_t lo = rd_tr(Gs, 256, swz_g(k), k, a_col + 32 * i);
-        const bf16x4_t hi = rd_tr(Gs, 256, swz_g(k + 4), k + 4, a_col + 32 * i);
+        const bf16x4_t lo = rd_tr(Gs, GRB, swz_rows<GRB>(k), k, a_col + 32 * i);
+        const bf16x4_t hi = rd_tr(Gs, GRB, swz_rows<GRB>(k + 4), k + 4, a_col + 32 * i);
         af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
       if (bias_wave) {
@@ -219,14 +227,18 @@ __global__ __launch_bounds__(256 * TG, 1) void conv_wgrad_taps_kernel(ConvWgradA
     }
   }
 
-  // partial tile -> workspace [split][cout][kpad]: 32 lanes = 32 consecutive Cin = 128-B rows
+  // partial tile -> workspace [split][cout][kpad]: 32 lanes = 32 consecutive Cin = 128-B rows.
+  // A 32-channel tail chunk (Cin = 96) stores only its wn = 0 half: the packed K has no padding
+  // there, so the other half's columns belong to the next tap.
   float* part = ta.w_part + (int64_t)split * a.cout * a.kpad;
+  const bool ci_ok = wn * 32 < ci_cnt;
 #pragma unroll
   for (int tt = 0; tt < TPG; ++tt)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int t = t0 + tt;
       if (TPG * TG != T && t >= T) break;
+      if (!ci_ok) break;
       const int kc = t * a.cin_pad + kbase + wn * 32 + (lane & 31);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -300,22 +312,25 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __r
   }
 }
 
-template <int KH, int KW, int TG>
+template <int KH, int KW, int TG, int BMT>
 void launch_taps(const ConvWgradArgs& a, const WgradItems& it, const WgradTapArgs& ta,
                  hipStream_t stream) {
   dim3 grid((ta.n_co * ta.n_ci * ta.splits + 7) / 8 * 8);
-  hipLaunchKernelGGL((conv_wgrad_taps_kernel<KH, KW, TG>), grid, dim3(256 * TG), 0, stream, a,
-                     it, ta);
+  hipLaunchKernelGGL((conv_wgrad_taps_kernel<KH, KW, TG, BMT>), grid,
+                     dim3(TapGeo<KH, KW, TG, BMT>::NT), 0, stream, a, it, ta);
 }
 
 }  // namespace
 
 bool launch_conv_wgrad_taps(const ConvWgradArgs& a, const WgradItems& it, const WgradTapArgs& ta,
                             float* db, hipStream_t stream) {
-  if (a.KH == 1 && a.KW == 1) launch_taps<1, 1, 1>(a, it, ta, stream);
-  else if (a.KH == 1 && a.KW == 5) launch_taps<1, 5, 1>(a, it, ta, stream);
-  else if (a.KH == 5 && a.KW == 1) launch_taps<5, 1, 1>(a, it, ta, stream);
-  else if (a.KH == 3 && a.KW == 3) launch_taps<3, 3, 2>(a, it, ta, stream);
+  if (ta.bm == 64) {
+    if (a.KH == 3 && a.KW == 3) launch_taps<3, 3, 3, 64>(a, it, ta, stream);
+    else return false;
+  } else if (a.KH == 1 && a.KW == 1) launch_taps<1, 1, 1, 128>(a, it, ta, stream);
+  else if (a.KH == 1 && a.KW == 5) launch_taps<1, 5, 1, 128>(a, it, ta, stream);
+  else if (a.KH == 5 && a.KW == 1) launch_taps<5, 1, 1, 128>(a, it, ta, stream);
+  else if (a.KH == 3 && a.KW == 3) launch_taps<3, 3, 2, 128>(a, it, ta, stream);
   else return false;
   const int64_t n = (int64_t)a.cout * a.kpad;
   const bool bias = ta.db_part != nullptr && db != nullptr;

@@ -174,7 +174,9 @@ struct WgradTapArgs {
   int ci_seg[RAFT_WG_MAX_CI_CHUNKS];     // input segment of each chunk
   int ci_off[RAFT_WG_MAX_CI_CHUNKS];     // channel offset inside the segment
   int ci_k[RAFT_WG_MAX_CI_CHUNKS];       // packed-K column of the chunk's first channel (tap 0)
-  int n_co;                              // 128-wide Cout tiles
+  int ci_cnt[RAFT_WG_MAX_CI_CHUNKS];     // valid channels of the chunk (64, or a 32 tail)
+  int bm;                                // Cout tile: 128, or 64 (3x3 with Cout <= 64)
+  int n_co;                              // Cout tiles
   int tiles_x, tiles_per_img, chunks_per_item, total_chunks, chunks_per_split, splits;
   float* w_part;                         // [splits][cout][kpad]
   float* db_part;                        // [splits][cout] or null

@@ -270,10 +270,56 @@ def _head_ok(x, conv):
 _HEAD_NATIVE = os.environ.get('RAFT_ENCODER_HEAD_NATIVE', '1') != '0'
 
 
+class _Conv3x3WgradNative(torch.autograd.Function):
+    """Stride-1 3x3 "same" encoder conv (the residual blocks' stride-1 convs, `core/extractor.py
+    :22-23`): forward and input gradient on MIOpen, weight gradient on the tap-fused MFMA kernel
+    (csrc/kernels/conv_wgrad_taps.hip -- one workgroup per Cout x 64-Cin slab owns all 9 taps over
+    8x8-pixel halo tiles).  Replaces MIOpen's backward-weights solvers and their zero-fill / cast
+    passes (SubTensorOp kernels) for these convs."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return F.conv2d(x, w, None, 1, 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import conv as C
+        x, w = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(
+                dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            co, ci = w.shape[:2]
+            dwp = torch.zeros(co, 9 * ci, device=x.device, dtype=torch.float32)
+            C.conv_wgrad_taps([(dy.permute(0, 2, 3, 1), [x.permute(0, 2, 3, 1)])], 0, [0], [ci],
+                              (3, 3), (1, 1), co, dwp, None)
+            # packed (co, kh, kw, ci) -> (co, ci, kh, kw) with channels_last strides (= w's)
+            dw = dwp.view(co, 3, 3, ci).permute(0, 3, 1, 2).to(w.dtype)
+        return dx, dw
+
+
+_WGRAD_NATIVE = os.environ.get('RAFT_ENCODER_WGRAD_NATIVE', '1') != '0'
+
+
+def _wgrad_native_ok(x, conv):
+    return (_WGRAD_NATIVE and conv.kernel_size == (3, 3) and conv.stride == (1, 1)
+            and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
+            and conv.in_channels % 32 == 0 and conv.out_channels % 8 == 0
+            and conv.in_channels <= 1024 and x.is_cuda and x.dtype == torch.bfloat16
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and x.numel() * 2 < 2 ** 31 and x.shape[0] * x.shape[2] * x.shape[3] * conv.out_channels * 2 < 2 ** 31)
+
+
 def _conv(x, conv, with_bias=False):
     w = _WEIGHTS.get(conv)
     if w is None:
         w = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    if not with_bias and _wgrad_native_ok(x, conv) and torch.is_grad_enabled() and \
+            (x.requires_grad or w.requires_grad):
+        return _Conv3x3WgradNative.apply(x, w)
     b = conv.bias.to(torch.bfloat16) if (with_bias and conv.bias is not None) else None
     return F.conv2d(x, w, b, conv.stride, conv.padding, conv.dilation, conv.groups)
 

@@ -243,6 +243,9 @@ def test_conv_wgrad_multi_items(ext_ops, cin, cout, k, segs, g_off, pps):
     (128, 64, (3, 3), None, 64, 1),
     (192, 126, (3, 3), (64, 128), 0, 0),
     (64, 80, (3, 3), None, 0, 0),
+    (96, 64, (3, 3), None, 0, 0),        # 64-wide Cout tile, 32-channel Cin tail
+    (96, 96, (3, 3), None, 0, 5),        # Cin tail at 128-wide Cout tiles
+    (64, 48, (3, 3), None, 8, 0),
 ])
 def test_conv_wgrad_taps(ext_ops, cin, cout, k, segs, g_off, splits):
     """Tap-fused weight gradient (halo tiles, all taps per workgroup, deterministic split reduce)

@@ -94,3 +94,29 @@ def test_native_head_1x1_matches_conv2d(ext_ops):
     assert rel(x.grad, xr.grad) < 1e-2
     assert rel(w.grad, wr.grad) < 1e-2
     assert rel(b.grad, br.grad) < 1e-3
+
+
+@pytest.mark.parametrize('cin,cout', [(64, 64), (96, 96), (128, 128), (96, 64), (64, 128)])
+def test_native_wgrad_3x3_matches_conv2d(ext_ops, cin, cout):
+    """Stride-1 3x3 encoder conv with the tap-fused weight gradient (Cout <= 64 -> 64-wide Cout
+    tiles; Cin = 96 -> a 32-channel tail chunk) vs the autograd of F.conv2d at the same bf16
+    inputs (fp32 reference of the products)."""
+    torch.manual_seed(3)
+    x = torch.randn(3, cin, 37, 45, device=DEV).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) * 0.05).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    dy = torch.randn(3, cout, 37, 45, device=DEV).to(torch.bfloat16)
+    dy = dy.contiguous(memory_format=torch.channels_last)
+    y = fast._Conv3x3WgradNative.apply(x, w)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, None, 1, 1)
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    s = wr.grad.abs().max().item()
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=1e-2 * s, rtol=1e-2)
+    assert w.grad.dtype == torch.bfloat16 and w.grad.shape == w.shape
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=3e-2 * xr.grad.abs().max().item(),
+                               rtol=2e-2)
