@@ -885,8 +885,10 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
                  const std::vector<Tensor>& outs, const std::vector<int64_t>& out_off,
                  const std::vector<int64_t>& out_cnt, const std::vector<int64_t>& out_real,
                  const std::vector<int64_t>& out_acc, const std::vector<Tensor>& relu_y,
-                 const std::vector<int64_t>& relu_off) {
+                 const std::vector<int64_t>& relu_off, const std::vector<int64_t>& gate_mode,
+                 const std::vector<Tensor>& gate_t) {
   TORCH_CHECK(relu_y.size() == relu_off.size(), "relu spec mismatch");
+  TORCH_CHECK(gate_mode.empty() || gate_mode.size() == outs.size(), "gate spec mismatch");
   TORCH_CHECK(!ins.empty() && ins.size() <= 3 && !outs.empty() && outs.size() <= 3, "1..3 segments");
   TORCH_CHECK(in_off.size() == ins.size() && in_cnt.size() == ins.size(), "input spec mismatch");
   TORCH_CHECK(out_off.size() == outs.size() && out_cnt.size() == outs.size() &&
@@ -953,8 +955,59 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     a.oseg[o].cnt = (int)out_cnt[o];
     a.oseg[o].real = (int)out_real[o];
     a.oseg[o].acc = (int)out_acc[o];
+    a.oseg[o].gate = 0;
     cout += out_cnt[o];
   }
+  // fused ConvGRU gate backward (see OSeg): 7 tensors per gated segment, in segment order:
+  // z, q|r, h (bf16), dz (fp32, gate 2), d-pre (bf16), dz out (fp32, gate 1), dh (fp32)
+  size_t gt = 0;
+  for (size_t o = 0; o < gate_mode.size(); ++o) {
+    const int mode = (int)gate_mode[o];
+    if (mode == 0) continue;
+    TORCH_CHECK(mode == 1 || mode == 2, "gate mode must be 0, 1 or 2");
+    TORCH_CHECK(gt + 7 <= gate_t.size(), "gate tensors missing");
+    TORCH_CHECK(outs[o].scalar_type() == at::kFloat, "gated dgrad segment must be fp32");
+    TORCH_CHECK(mode == 2 || out_acc[o], "q-gate segment reads the accumulated state gradient");
+    const int real = (int)out_real[o];
+    const Tensor& z = gate_t[gt + 0];
+    const Tensor& qr = gate_t[gt + 1];
+    const Tensor& h = gate_t[gt + 2];
+    const Tensor& gin = gate_t[gt + 3];
+    const Tensor& gbo = gate_t[gt + 4];
+    const Tensor& gf0 = gate_t[gt + 5];
+    const Tensor& gf1 = gate_t[gt + 6];
+    gt += 7;
+    for (const Tensor* t : {&z, &qr, &h}) {
+      check_nhwc(*t, B, H, W, "gate input", at::kBFloat16);
+      TORCH_CHECK(t->size(3) == z.size(3) && t->size(3) >= real, "gate inputs must share a layout");
+      TORCH_CHECK(t->numel() * 2 < (int64_t(1) << 31), "gate input exceeds the 2 GiB descriptor range");
+    }
+    check_nhwc(gbo, B, H, W, "gate output", at::kBFloat16);
+    TORCH_CHECK(gbo.size(3) >= (mode == 2 ? 2 * real : real), "gate d-pre output too narrow");
+    check_nhwc(gf1, B, H, W, "gate state gradient", at::kFloat);
+    TORCH_CHECK(gf1.size(3) >= real && gf1.numel() * 4 < (int64_t(1) << 31), "gate state gradient");
+    a.oseg[o].gate = mode;
+    a.oseg[o].ga0 = reinterpret_cast<const uint16_t*>(z.data_ptr<at::BFloat16>());
+    a.oseg[o].ga1 = reinterpret_cast<const uint16_t*>(qr.data_ptr<at::BFloat16>());
+    a.oseg[o].ga2 = reinterpret_cast<const uint16_t*>(h.data_ptr<at::BFloat16>());
+    a.oseg[o].ga_stride = (int)z.size(3);
+    a.oseg[o].gb = reinterpret_cast<uint16_t*>(gbo.data_ptr<at::BFloat16>());
+    a.oseg[o].gb_stride = (int)gbo.size(3);
+    a.oseg[o].gf1 = gf1.data_ptr<float>();
+    a.oseg[o].gf_stride = (int)gf1.size(3);
+    if (mode == 1) {
+      check_nhwc(gf0, B, H, W, "gate dz output", at::kFloat);
+      TORCH_CHECK(gf0.size(3) == gf1.size(3), "gate fp32 outputs must share a layout");
+      a.oseg[o].gf0 = gf0.data_ptr<float>();
+      a.oseg[o].gin = nullptr;
+    } else {
+      check_nhwc(gin, B, H, W, "gate dz input", at::kFloat);
+      TORCH_CHECK(gin.size(3) == gf1.size(3), "gate fp32 inputs must share a layout");
+      a.oseg[o].gin = gin.data_ptr<float>();
+      a.oseg[o].gf0 = nullptr;
+    }
+  }
+  TORCH_CHECK(gt == gate_t.size(), "unused gate tensors");
   a.cout = (int)cout;
   const int bn = (cout % 128 == 0) ? 128 : 64;
   TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == at::kBFloat16 && wpk.dim() == 2,
@@ -966,7 +1019,11 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   a.kpad = (int)wpk.size(1);
   a.bias = nullptr;
   a.scale = (float)scale;
-  TORCH_CHECK(launch_conv_fwd(a, EPI_DGRAD, bn, cin_small != 0, cur_stream()), "dgrad launch");
+  bool any_gate = false;
+  for (int o = 0; o < a.noseg; ++o) any_gate = any_gate || a.oseg[o].gate != 0;
+  TORCH_CHECK(!(any_gate && cin_small), "gated dgrad needs the 64-channel K path");
+  TORCH_CHECK(launch_conv_fwd(a, any_gate ? EPI_DGRAD_GATE : EPI_DGRAD, bn, cin_small != 0, cur_stream()),
+              "dgrad launch");
 }
 
 // ------------------------------------------------------------------ encoder norm + activation
@@ -1329,7 +1386,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_lookup_nhwc_(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
   m.def("corr_window_grad(Tensor coords, Tensor dout, int levels, int radius) -> Tensor");
   m.def("corr_window_reduce(Tensor[] coords, Tensor[] wgs, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16=False) -> Tensor");
-  m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off) -> ()");
+  m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off, int[] gate_mode, Tensor[] gate_t) -> ()");
   m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale) -> ()");
   m.def("gru_q_bwd_(Tensor dh, Tensor z, Tensor q, Tensor hprev, Tensor(a!) dpre_q, Tensor(b!) dz, Tensor(c!) dhprev) -> ()");
   m.def("gru_zr_bwd_(Tensor drh, Tensor dz, Tensor z, Tensor r, Tensor hprev, Tensor(a!) dpre_zr, Tensor(b!) dhprev) -> ()");

@@ -82,7 +82,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
   rsrc_t o0 = nul, o1 = nul, o2 = nul, x0 = nul, x1 = nul;
   if constexpr (EPI == EPI_F32_NCHW) {
     o0 = make_rsrc(a.out0, P_u * (uint32_t)a.cout * 4u);
-  } else if constexpr (EPI != EPI_DGRAD) {
+  } else if constexpr (EPI != EPI_DGRAD && EPI != EPI_DGRAD_GATE) {
     o0 = make_rsrc(a.out0, P_u * (uint32_t)a.out0_stride * ES);
   }
   if constexpr (EPI == EPI_GRU_ZR || EPI == EPI_GRU_Q) {
@@ -165,7 +165,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
           bst_bf16(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, h[r] + z[r] * (q - h[r]));
           bst_bf16(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + n) * 2u : OOB, q);
         }
-      } else if constexpr (EPI == EPI_DGRAD) {
+      } else if constexpr (EPI == EPI_DGRAD || EPI == EPI_DGRAD_GATE) {
         // output segment of this 32-column tile (uniform)
         int s = 0, base = 0;
 #pragma unroll
@@ -174,7 +174,79 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
         const OSeg o = a.oseg[s];
         const int c = n - base;
         const bool cok = c < o.real;
-        if (o.ob != nullptr && o.ry == nullptr) {  // plain bf16 gradient
+        bool gated = false;
+        if constexpr (EPI == EPI_DGRAD_GATE) {
+          gated = o.gate != 0;
+          if (o.gate == 1) {  // ConvGRU q-gate backward on the final state gradient
+            const rsrc_t od = make_rsrc(o.ptr, P_u * (uint32_t)o.stride * 4u);
+            const uint32_t ab = P_u * (uint32_t)o.ga_stride * 2u;
+            const rsrc_t rz = make_rsrc(o.ga0, ab), rq = make_rsrc(o.ga1, ab), rh = make_rsrc(o.ga2, ab);
+            const rsrc_t gb = make_rsrc(o.gb, P_u * (uint32_t)o.gb_stride * 2u);
+            const rsrc_t f0 = make_rsrc(o.gf0, P_u * (uint32_t)o.gf_stride * 4u);
+            const rsrc_t f1 = make_rsrc(o.gf1, P_u * (uint32_t)o.gf_stride * 4u);
+#pragma unroll
+            for (int h8 = 0; h8 < 16; h8 += 8) {   // 8 rows at a time: bounded live registers
+              float pre[8], zz[8], qq[8], hh[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int r = h8 + u;
+                const bool e = ok[r] && cok;
+                pre[u] = bld_f32(od, e ? (uint32_t)(mrow[r] * o.stride + c) * 4u : OOB);
+                const uint32_t oa = e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB;
+                zz[u] = bld_bf16(rz, oa);
+                qq[u] = bld_bf16(rq, oa);
+                hh[u] = bld_bf16(rh, oa);
+              }
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int r = h8 + u;
+                const bool e = ok[r] && cok;
+                const float g = pre[u] + v[r];
+                bst_bf16(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB,
+                         g * zz[u] * (1.f - qq[u] * qq[u]));
+                const uint32_t of = e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB;
+                bst_f32(f0, of, g * (qq[u] - hh[u]));
+                bst_f32(f1, of, g * (1.f - zz[u]));
+              }
+            }
+          } else if (o.gate == 2) {  // ConvGRU z / r gate backward on d(r*h)
+            const uint32_t ab = P_u * (uint32_t)o.ga_stride * 2u;
+            const rsrc_t rz = make_rsrc(o.ga0, ab), rr = make_rsrc(o.ga1, ab), rh = make_rsrc(o.ga2, ab);
+            const rsrc_t gi = make_rsrc(o.gin, P_u * (uint32_t)o.gf_stride * 4u);
+            const rsrc_t gb = make_rsrc(o.gb, P_u * (uint32_t)o.gb_stride * 2u);
+            const rsrc_t f1 = make_rsrc(o.gf1, P_u * (uint32_t)o.gf_stride * 4u);
+#pragma unroll
+            for (int h8 = 0; h8 < 16; h8 += 8) {
+              float dz[8], zz[8], rv[8], hh[8], dh[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int r = h8 + u;
+                const bool e = ok[r] && cok;
+                const uint32_t oa = e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB;
+                const uint32_t of = e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB;
+                dz[u] = bld_f32(gi, of);
+                dh[u] = bld_f32(f1, of);
+                zz[u] = bld_bf16(rz, oa);
+                rv[u] = bld_bf16(rr, oa);
+                hh[u] = bld_bf16(rh, oa);
+              }
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int r = h8 + u;
+                const bool e = ok[r] && cok;
+                const uint32_t ob = e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB;
+                bst_bf16(gb, ob, dz[u] * zz[u] * (1.f - zz[u]));
+                bst_bf16(gb, e ? ob + (uint32_t)o.real * 2u : OOB,
+                         v[r] * hh[u] * rv[u] * (1.f - rv[u]));
+                bst_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB,
+                        dh[u] + v[r] * rv[u]);
+              }
+            }
+          }
+        }
+        if (gated) {
+          // the gate epilogue consumed this segment's values
+        } else if (o.ob != nullptr && o.ry == nullptr) {  // plain bf16 gradient
           const rsrc_t ob = make_rsrc(o.ob, P_u * (uint32_t)o.ob_stride * 2u);
 #pragma unroll
           for (int r = 0; r < 16; ++r)

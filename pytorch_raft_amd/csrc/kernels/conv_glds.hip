@@ -262,6 +262,7 @@ bool launch_conv_glds(const ConvFwdArgs& a, int epi, int idx, hipStream_t stream
     case EPI_GRU_ZR: return launch_glds_epi<EPI_GRU_ZR>(a, idx, stream);
     case EPI_GRU_Q: return launch_glds_epi<EPI_GRU_Q>(a, idx, stream);
     case EPI_DGRAD: return launch_glds_epi<EPI_DGRAD>(a, idx, stream);
+    case EPI_DGRAD_GATE: return launch_glds_epi<EPI_DGRAD_GATE>(a, idx, stream);
     case EPI_F32_NCHW: return launch_glds_epi<EPI_F32_NCHW>(a, idx, stream);
     default: return false;
   }

@@ -312,6 +312,7 @@ bool launch_epi_idx(const ConvFwdArgs& a, int epi, int idx, bool smallc, hipStre
     RAFT_EPI_CASE(EPI_F32)
     RAFT_EPI_CASE(EPI_ACC_F32)
     RAFT_EPI_CASE(EPI_DGRAD)
+    case EPI_DGRAD_GATE: return !smallc && launch_cfg_idx<EPI_DGRAD_GATE, false>(a, idx, stream);
     RAFT_EPI_CASE(EPI_F32_NCHW)
     case EPI_GRU_ZR: return !smallc && launch_cfg_idx<EPI_GRU_ZR, false>(a, idx, stream);
     case EPI_GRU_Q: return !smallc && launch_cfg_idx<EPI_GRU_Q, false>(a, idx, stream);
@@ -420,7 +421,8 @@ int choose_cfg(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   }();
   const int P = a.B * a.H * a.W;
   if (forced >= 0 && forced < kNumCfgs && cfg_allowed(forced, a.cout, smallc, epi)) return forced;
-  const bool f32out = epi == EPI_F32 || epi == EPI_ACC_F32 || epi == EPI_DGRAD || epi == EPI_F32_NCHW;
+  const bool f32out = epi == EPI_F32 || epi == EPI_ACC_F32 || epi == EPI_DGRAD ||
+                      epi == EPI_DGRAD_GATE || epi == EPI_F32_NCHW;
   const int eclass = f32out ? 1 : ((epi == EPI_GRU_ZR || epi == EPI_GRU_Q) ? 2 : 0);
   const TuneKey key{P, a.H, a.W, a.KH, a.KW, smallc ? a.cin_small : a.cin_pad, a.cout, (int)smallc,
                     eclass};

@@ -83,6 +83,8 @@ enum ConvEpilogue {
   EPI_GRU_Q = 5,      // q = tanh; out0 = aux0 + aux1 * (q - aux0) (h'), out1 = q
   EPI_DGRAD = 6,      // output channels split over oseg[] fp32 buffers (store or accumulate)
   EPI_F32_NCHW = 7,   // out0 f32 NCHW (B, cout, H, W)
+  EPI_DGRAD_GATE = 8, // EPI_DGRAD + the fused ConvGRU gate backward (OSeg.gate); its own
+                      // instantiation: the gate math's registers stay out of the plain dgrads
 };
 
 struct Seg {
@@ -103,6 +105,23 @@ struct OSeg {
   int ob_stride;
   const uint16_t* ry;
   int ry_stride;
+  // fused ConvGRU gate backward on an fp32 segment (gate != 0; the segment itself is not
+  // stored), per element (pixel, channel c < real) with v the dgrad value:
+  //  gate 1 -- q gate on the state gradient: g = *ptr + v (the final dh);
+  //            gb[c] = bf16(g z (1 - q^2)) (d pre-q), gf0[c] = g (q - h) (dz), gf1[c] = g (1 - z)
+  //  gate 2 -- z / r gates on d(r*h): gb[c] = bf16(gin[c] z (1 - z)), gb[real + c] =
+  //            bf16(v h r (1 - r)), gf1[c] += v r                 (ga0, ga1, ga2 = z, q|r, h)
+  int gate;
+  const uint16_t* ga0;
+  const uint16_t* ga1;
+  const uint16_t* ga2;
+  int ga_stride;
+  const float* gin;
+  uint16_t* gb;
+  int gb_stride;
+  float* gf0;
+  float* gf1;
+  int gf_stride;
 };
 
 struct ConvFwdArgs {

@@ -254,7 +254,7 @@ class _Head1x1(torch.autograd.Function):
         dx = torch.empty(B, H, W, cin, device=xn.device, dtype=torch.bfloat16)
         wd = C.pack_weight(w2.t().contiguous().view(cin, cout, 1, 1), [cout], [cout])
         _ext.ops().conv_dgrad_([g], [0], [cout], wd, 1, 1, 0, 0, 0, 1.0, [dx], [0], [cin], [cin],
-                               [0], [dx], [-1])
+                               [0], [dx], [-1], [], [])
         dw = torch.zeros(cout, cin, device=xn.device)
         db = torch.zeros(cout, device=xn.device)
         C.conv_wgrad(g, 0, [(xn, 0, cin)], (1, 1), (0, 0), cout, dw, db)

@@ -450,6 +450,9 @@ def _backward_overlapped(st, pk, n):
 # 31.0 -> 33.0 ms: the XCD-local tile order and L2 reuse of each conv are lost when two grids
 # share the XCDs).
 _BRANCHES = os.environ.get('RAFT_UPDATE_BRANCHES', '0') == '1'
+# ConvGRU gate backward (gru_q_bwd / gru_zr_bwd) fused into the dgrad epilogues (OSeg.gate);
+# RAFT_GRU_GATES_FUSED=0 runs the separate elementwise kernels
+_GATES_FUSED = os.environ.get('RAFT_GRU_GATES_FUSED', '1') != '0'
 _BRANCH = {}
 
 
@@ -592,19 +595,27 @@ class _UpdateIter(torch.autograd.Function):
             # deferred: summed over all iterations by one launch per conv (_Packed.flush_wgrad)
             pk.defer_wgrad(name, g, g_off, segs)
 
-        def dgrad(name, gsegs, outs, small=False, scale=1.0):
+        def dgrad(name, gsegs, outs, small=False, scale=1.0, gates=None):
             """outs: list of (buffer fp32, offset, slot_cnt, real, acc) or, fusing the backward of a
-            ReLU, (buffer bf16, offset, slot_cnt, real, 0, relu_out, relu_out_offset)."""
+            ReLU, (buffer bf16, offset, slot_cnt, real, 0, relu_out, relu_out_offset).
+            gates: per output, None or (mode, [z, q|r, h, dz_in, d_pre, dz_out, dh]) -- the ConvGRU
+            gate backward fused into that fp32 segment's epilogue (OSeg in launchers.h)."""
             s = SPEC[name]
             ry = [o[5] if len(o) > 5 else o[0] for o in outs]
             # relu offset -1 marks a plain (ungated) bf16 output
             roff = [int(o[6]) if len(o) > 5 else (-1 if o[0].dtype == torch.bfloat16 else 0)
                     for o in outs]
+            gmode, gt = [], []
+            if gates is not None:
+                for gspec in gates:
+                    gmode.append(0 if gspec is None else gspec[0])
+                    if gspec is not None:
+                        gt.extend(gspec[1])
             ops.conv_dgrad_([g[0] for g in gsegs], [g[1] for g in gsegs], [g[2] for g in gsegs],
                             pk.wd[name], s.k[0], s.k[1], s.pad[0], s.pad[1], 2 if small else 0,
                             float(scale), [o[0] for o in outs], [o[1] for o in outs],
                             [o[2] for o in outs], [o[3] for o in outs], [o[4] for o in outs],
-                            ry, roff)
+                            ry, roff, gmode, gt)
 
         # ---- mask head (mask = 0.25 * conv(fm[256:]))
         gmask = gmask.contiguous()
@@ -624,7 +635,20 @@ class _UpdateIter(torch.autograd.Function):
         # ---- head
         wgrad('head', dpre_head, 0, [(h2, 0, HD)])
         dh = gh.float().contiguous() if gh is not None else _f32(sh + (HD,), dev, zero=True)
-        dgrad('head', [(dpre_head, 0, 512)], [(dh, 0, HD, HD, 1)])
+        halves = (('2', (h1, z2, rh2, r2, q2)), ('1', (h0, z1, rh1, r1, q1)))
+
+        def qgate(half):
+            """q-gate backward of a GRU half-step, fused into the epilogue of the dgrad that
+            finalises its output-state gradient: -> (spec, (d pre-q bf16, dz, dh of its input))."""
+            hin, z, _, _, q = half
+            bufs = (_bf16(sh + (HD,), dev), _f32(sh + (HD,), dev), _f32(sh + (HD,), dev))
+            return (1, [z, q, hin, z, bufs[0], bufs[1], bufs[2]]), bufs
+
+        if _GATES_FUSED:
+            gspec, nxt = qgate(halves[0][1])
+            dgrad('head', [(dpre_head, 0, 512)], [(dh, 0, HD, HD, 1)], gates=[gspec])
+        else:
+            dgrad('head', [(dpre_head, 0, 512)], [(dh, 0, HD, HD, 1)])
 
         # inp is shared by every iteration: its gradient accumulates in ONE fp32 buffer across
         # the iterations' backwards (11 -> 0, in that order since each needs the next one's dh)
@@ -635,23 +659,39 @@ class _UpdateIter(torch.autograd.Function):
         dinp = st.dinp_acc
         dmf = _f32(sh + (128,), dev)
         first = 1  # the first dgrad into dmf (q2's) stores: no zero fill
-        for tag, (hin, z, rh, r, q) in (('2', (h1, z2, rh2, r2, q2)), ('1', (h0, z1, rh1, r1, q1))):
-            dpre_q = _bf16(sh + (HD,), dev)
-            dz = _f32(sh + (HD,), dev)
-            dhp = _f32(sh + (HD,), dev)
-            ops.gru_q_bwd_(dh, z, q, hin, dpre_q, dz, dhp)
-            wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)])
-            drh = _f32(sh + (HD,), dev)
-            dgrad('q' + tag, [(dpre_q, 0, HD)],
-                  [(drh, 0, HD, HD, 0), (dinp, 0, HD, HD, int(acc_inp)),
-                   (dmf, 0, 128, 128, 1 - first)])
+        for k, (tag, (hin, z, rh, r, q)) in enumerate(halves):
+            if _GATES_FUSED:
+                # the q gate ran in the epilogue of the previous dgrad (head / zr2); the z / r
+                # gates run in this q dgrad's d(r*h) epilogue, d(r*h) itself is never stored
+                dpre_q, dz, dhp = nxt
+                wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)])
+                dpre_zr = _bf16(sh + (2 * HD,), dev)
+                dgrad('q' + tag, [(dpre_q, 0, HD)],
+                      [(dhp, 0, HD, HD, 0), (dinp, 0, HD, HD, int(acc_inp)),
+                       (dmf, 0, 128, 128, 1 - first)],
+                      gates=[(2, [z, r, hin, dz, dpre_zr, dz, dhp]), None, None])
+            else:
+                dpre_q = _bf16(sh + (HD,), dev)
+                dz = _f32(sh + (HD,), dev)
+                dhp = _f32(sh + (HD,), dev)
+                ops.gru_q_bwd_(dh, z, q, hin, dpre_q, dz, dhp)
+                wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)])
+                drh = _f32(sh + (HD,), dev)
+                dgrad('q' + tag, [(dpre_q, 0, HD)],
+                      [(drh, 0, HD, HD, 0), (dinp, 0, HD, HD, int(acc_inp)),
+                       (dmf, 0, 128, 128, 1 - first)])
+                dpre_zr = _bf16(sh + (2 * HD,), dev)
+                ops.gru_zr_bwd_(drh, dz, z, r, hin, dpre_zr, dhp)
             first = 0
             acc_inp = True
-            dpre_zr = _bf16(sh + (2 * HD,), dev)
-            ops.gru_zr_bwd_(drh, dz, z, r, hin, dpre_zr, dhp)
             wgrad('zr' + tag, dpre_zr, 0, [(hin, 0, HD), (inp, 0, HD), (mf, 0, 128)])
-            dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)],
-                  [(dhp, 0, HD, HD, 1), (dinp, 0, HD, HD, 1), (dmf, 0, 128, 128, 1)])
+            zr_outs = [(dhp, 0, HD, HD, 1), (dinp, 0, HD, HD, 1), (dmf, 0, 128, 128, 1)]
+            if _GATES_FUSED and k == 0:
+                # dhp is now the final gradient of half-step 1's output: its q gate here
+                gspec, nxt = qgate(halves[1][1])
+                dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)], zr_outs, gates=[gspec, None, None])
+            else:
+                dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)], zr_outs)
             dh = dhp
         # ---- motion encoder
         dpre_conv = _bf16(sh + (128,), dev)

@@ -136,7 +136,7 @@ class _SmallUpdateIter(torch.autograd.Function):
             ops.conv_dgrad_([g[0] for g in gsegs], [g[1] for g in gsegs], [g[2] for g in gsegs],
                             pk.wd[name], s.k[0], s.k[1], s.pad[0], s.pad[1], 0, float(scale),
                             [o[0] for o in outs], [o[1] for o in outs], [o[2] for o in outs],
-                            [o[3] for o in outs], [o[4] for o in outs], ry, roff)
+                            [o[3] for o in outs], [o[4] for o in outs], ry, roff, [], [])
 
         # ---- flow head: conv2 (128 -> 2) as an MFMA conv on a 64-wide bf16 gradient
         g2 = _zeros_bf16(sh + (64,), dev)

@@ -189,7 +189,7 @@ def test_conv_dgrad_relu_gated_bf16(ext_ops):
     out = torch.full((B, H, W, cin + 16), 7.0, device=DEV, dtype=torch.bfloat16)
     wd = C.pack_weight_dgrad(w, [cout], [cout])
     torch.ops.raft_amd.conv_dgrad_([C.nhwc(g)], [0], [cout], wd, 3, 3, 1, 1, 0, 1.0, [out], [8],
-                                   [cin], [cin], [0], [y], [32])
+                                   [cin], [cin], [0], [y], [32], [], [])
     torch.testing.assert_close(C.nchw(out[..., 8:8 + cin]).float(), ref, atol=2e-2, rtol=2e-2)
     assert torch.all(out[..., :8] == 7.0) and torch.all(out[..., 8 + cin:] == 7.0)
 

@@ -84,7 +84,7 @@ def test_dry_run_fused_training_step(alternate):
         loss, metrics = sequence_loss(preds, flow, valid, 0.8)
         loss.backward()
     names = set(ops.calls)
-    assert {'conv_fwd_', 'conv_dgrad_', 'conv_wgrad_taps_', 'gru_q_bwd_', 'gru_zr_bwd_',
+    assert {'conv_fwd_', 'conv_dgrad_', 'conv_wgrad_taps_',
             'relu_bwd_', 'f1_patch_', 'fh2_fwd_', 'fh2_dgrad_', 'fh2_wgrad_', 'convex_up_fwd',
             'convex_up_bwd', 'seq_loss_fwd'} <= names, names
     if not alternate:
