@@ -383,6 +383,13 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   t.out0 = g_scratch;
   t.out0_stride = (a.cout + 255) / 256 * 256;
   t.noseg = 0;
+  // store-only epilogues are timed as they will run (the GRU gate epilogues cost registers and
+  // bytes the fp32 scratch epilogue does not): their outputs are rewritten by the real launch
+  // that follows; accumulating epilogues (ACC_F32, DGRAD) are timed on the fp32 scratch
+  const bool real_epi = epi == EPI_BF16 || epi == EPI_RELU_BF16 || epi == EPI_GRU_ZR ||
+                        epi == EPI_GRU_Q || epi == EPI_F32 || epi == EPI_F32_NCHW;
+  const ConvFwdArgs& ta = real_epi ? a : t;
+  const int te = real_epi ? epi : EPI_F32;
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -390,13 +397,13 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   float best_ms = 1e30f;
   for (int i = 0; i < kNumCfgs; ++i) {
     if (!cfg_allowed(i, a.cout, smallc, epi)) continue;
-    launch_epi_idx(t, EPI_F32, i, smallc, stream);  // warm (code load, caches)
+    if (!launch_epi_idx(ta, te, i, smallc, stream)) continue;  // warm (code load, caches)
     // min over 3 trials of 2 launches: one noisy trial (clock ramp, a co-running stream) must
     // not flip the choice -- run-to-run step time varied by ~0.8 ms with single-trial timing
     float ms = 1e30f;
     for (int trial = 0; trial < 3; ++trial) {
       (void)hipEventRecord(e0, stream);
-      for (int r = 0; r < 2; ++r) launch_epi_idx(t, EPI_F32, i, smallc, stream);
+      for (int r = 0; r < 2; ++r) launch_epi_idx(ta, te, i, smallc, stream);
       (void)hipEventRecord(e1, stream);
       (void)hipEventSynchronize(e1);
       float tms = 0.f;
