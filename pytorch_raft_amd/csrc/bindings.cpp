@@ -75,7 +75,8 @@ std::vector<Tensor> corr_build(const Tensor& f1, const Tensor& f2, int64_t level
 }
 
 // bf16 fmaps in NHWC memory, (B,H,W,C) contiguous (the channels_last encoder outputs, permuted)
-std::vector<Tensor> corr_build_bf16(const Tensor& f1, const Tensor& f2, int64_t levels) {
+std::vector<Tensor> corr_build_bf16(const Tensor& f1, const Tensor& f2, int64_t levels,
+                                    bool pyr_bf16) {
   TORCH_CHECK(f1.is_cuda() && f2.is_cuda() && f1.scalar_type() == at::kBFloat16 &&
                   f2.scalar_type() == at::kBFloat16 && f1.is_contiguous() && f2.is_contiguous(),
               "fmaps must be contiguous bf16 (B,H,W,C) GPU tensors");
@@ -89,14 +90,14 @@ std::vector<Tensor> corr_build_bf16(const Tensor& f1, const Tensor& f2, int64_t 
   c10::DeviceGuard g(f1.device());
   const int64_t N = H * W;
   std::vector<Tensor> out;
-  std::vector<float*> ptr;
+  std::vector<void*> ptr;
   std::vector<int> hs, ws;
   int64_t h = H, w = W;
-  auto fopt = f1.options().dtype(at::kFloat);
+  auto fopt = f1.options().dtype(pyr_bf16 ? at::kBFloat16 : at::kFloat);
   for (int64_t l = 0; l < levels; ++l) {
     TORCH_CHECK(h >= 1 && w >= 1, "feature map too small for ", levels, " pyramid levels");
     out.push_back(at::empty({B, N, h, w}, fopt));
-    ptr.push_back(out.back().data_ptr<float>());
+    ptr.push_back(out.back().data_ptr());
     hs.push_back((int)h);
     ws.push_back((int)w);
     h /= 2;
@@ -104,7 +105,8 @@ std::vector<Tensor> corr_build_bf16(const Tensor& f1, const Tensor& f2, int64_t 
   }
   launch_corr_build_bf16(reinterpret_cast<const uint16_t*>(f1.data_ptr()),
                          reinterpret_cast<const uint16_t*>(f2.data_ptr()), ptr.data(), hs.data(),
-                         ws.data(), (int)B, (int)C, (int)H, (int)W, (int)levels, cur_stream());
+                         ws.data(), (int)B, (int)C, (int)H, (int)W, (int)levels, pyr_bf16,
+                         cur_stream());
   return out;
 }
 
@@ -137,7 +139,26 @@ void corr_lookup_nhwc_(const std::vector<Tensor>& pyr, const Tensor& coords, int
   TORCH_CHECK(radius == 3 || radius == 4, "radius must be 3 or 4");
   c10::DeviceGuard g(coords.device());
   const int64_t B = coords.size(0), H = coords.size(2), W = coords.size(3);
-  Levels L = levels_of(pyr, B * H * W, "pyramid");
+  // fp32 or bf16 pyramid (corr_build_bf16 with pyr_bf16)
+  const bool pyr_bf16 = !pyr.empty() && pyr[0].scalar_type() == at::kBFloat16;
+  std::vector<Tensor> pyr32;
+  std::vector<const void*> cp;
+  Levels L;
+  if (pyr_bf16) {
+    TORCH_CHECK(pyr.size() <= 4, "pyramid: 1..4 levels required");
+    for (const auto& t : pyr) {
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kBFloat16 && t.dim() == 4,
+                  "bf16 pyramid levels must be contiguous (B, N, h, w)");
+      TORCH_CHECK(t.size(0) * t.size(1) == B * H * W, "pyramid plane count mismatch");
+      TORCH_CHECK(t.numel() * 2 < (int64_t(1) << 40), "pyramid level too large");
+      cp.push_back(t.data_ptr());
+      L.h.push_back((int)t.size(2));
+      L.w.push_back((int)t.size(3));
+    }
+  } else {
+    L = levels_of(pyr, B * H * W, "pyramid");
+    for (auto* q : L.ptr) cp.push_back(q);
+  }
   TORCH_CHECK(L.h[0] == H && L.w[0] == W, "pyramid level 0 must match coords grid");
   const int64_t D = 2 * radius + 1;
   const int levels = (int)pyr.size();
@@ -147,12 +168,12 @@ void corr_lookup_nhwc_(const std::vector<Tensor>& pyr, const Tensor& coords, int
               "out must be a contiguous bf16 (B,H,W,C>=L*D*D) buffer");
   const int64_t Cb = out.size(3);
   TORCH_CHECK(Cb % 8 == 0, "out channels must be a multiple of 8");
-  std::vector<const float*> cp(L.ptr.begin(), L.ptr.end());
   // LDS-tiled kernel writes whole pixel rows including the zero padding
   TORCH_CHECK(launch_corr_lookup_tile(cp.data(), L.h.data(), L.w.data(), levels,
                                       coords.data_ptr<float>(),
                                       reinterpret_cast<uint16_t*>(out.data_ptr<at::BFloat16>()),
-                                      (int)Cb, (int)B, (int)H, (int)W, (int)radius, cur_stream()),
+                                      (int)Cb, (int)B, (int)H, (int)W, (int)radius, pyr_bf16,
+                                      cur_stream()),
               "unsupported radius");
 }
 
@@ -839,11 +860,15 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
   a.B = (int)B; a.H = (int)H; a.W = (int)W;
   a.KH = (int)kh; a.KW = (int)kw; a.PH = (int)ph; a.PW = (int)pw;
   a.cout = (int)cout;
-  check_cuda_f32(dw, "grad_weight");
+  // fp32 dw: accumulated (+=); bf16 dw: stored (the encoders' bf16 weight gradients)
+  const bool dw_bf16 = dw.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(dw.is_cuda() && dw.is_contiguous() && (dw_bf16 || dw.scalar_type() == at::kFloat),
+              "grad_weight must be a contiguous fp32 or bf16 GPU tensor");
   const int64_t kpad = kh * kw * cin_pad;
   TORCH_CHECK(dw.dim() == 2 && dw.size(0) == cout && dw.size(1) == kpad, "grad_weight must be (cout, kpad)");
   TORCH_CHECK(kpad % 4 == 0, "packed K must be a multiple of 4");
-  a.dw = dw.data_ptr<float>();
+  a.dw = dw_bf16 ? nullptr : dw.data_ptr<float>();
+  ta.dw_bf16 = dw_bf16 ? reinterpret_cast<uint16_t*>(dw.data_ptr<at::BFloat16>()) : nullptr;
   a.kpad = (int)kpad;
   ta.bm = (kh == 3 && kw == 3 && cout <= 64) ? 64 : 128;
   ta.n_co = (int)((cout + ta.bm - 1) / ta.bm);
@@ -862,7 +887,7 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
   ta.chunks_per_split = (int)((ta.total_chunks + splits - 1) / splits);
   ta.splits = (int)((ta.total_chunks + ta.chunks_per_split - 1) / ta.chunks_per_split);
   TORCH_CHECK(ta.splits < 65536, "too many splits");
-  auto fo = dw.options();
+  auto fo = dw.options().dtype(at::kFloat);
   Tensor wpart = at::empty({(int64_t)ta.splits * cout * kpad}, fo);
   ta.w_part = wpart.data_ptr<float>();
   float* dbp = nullptr;
@@ -1378,7 +1403,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] wgs, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
-  m.def("corr_build_bf16(Tensor f1, Tensor f2, int levels) -> Tensor[]");
+  m.def("corr_build_bf16(Tensor f1, Tensor f2, int levels, bool pyr_bf16=False) -> Tensor[]");
   m.def("conv_wgrad_taps_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, "
         "int kw, int ph, int pw, int cout, Tensor dw, Tensor? db, int splits=0) -> ()");
   m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");

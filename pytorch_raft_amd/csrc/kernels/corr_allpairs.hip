@@ -17,6 +17,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int BI = 64;   // query pixels per workgroup
@@ -24,6 +26,9 @@ constexpr int TJ = 8;    // target block is TJ x TJ on the fmap2 grid
 constexpr int BJ = TJ * TJ;
 constexpr int KC = 32;   // channels per LDS stage
 constexpr int NT = 256;  // threads
+
+__device__ __forceinline__ void pyr_st(float* p, float v) { *p = v; }
+__device__ __forceinline__ void pyr_st(uint16_t* p, float v) { *p = raft_f32_to_bf16(v); }
 
 struct Pyr4 {
   float* lvl[4];
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(NT) void corr_build_kernel(const float* __restrict_
       float v = (((row0[0] + row0[1]) + row1[0]) + row1[1]) * 0.25f;
       P2[ii][c] = v;
       int i = i0 + ii, Y = (y0 >> 2) + cy, X = (x0 >> 2) + cx;
-      if (i < N && Y < h2 && X < w2) L2[(((int64_t)b * N + i) * h2 + Y) * w2 + X] = v;
+      if (i < N && Y < h2 && X < w2) pyr_st(&L2[(((int64_t)b * N + i) * h2 + Y) * w2 + X], v);
     }
   }
   __syncthreads();
@@ -152,7 +157,7 @@ __global__ __launch_bounds__(NT) void corr_build_kernel(const float* __restrict_
     for (int ii = tid; ii < BI; ii += NT) {
       float v = (((P2[ii][0] + P2[ii][1]) + P2[ii][2]) + P2[ii][3]) * 0.25f;
       int i = i0 + ii, Y = y0 >> 3, X = x0 >> 3;
-      if (i < N && Y < h3 && X < w3) L3[(((int64_t)b * N + i) * h3 + Y) * w3 + X] = v;
+      if (i < N && Y < h3 && X < w3) pyr_st(&L3[(((int64_t)b * N + i) * h3 + Y) * w3 + X], v);
     }
   }
 }
@@ -173,9 +178,19 @@ __global__ __launch_bounds__(NT) void corr_build_kernel(const float* __restrict_
 // and every such cell's footprint is inside level 0 (h_l = floor(h_{l-1} / 2)).
 constexpr int BB_I = 64, BB_Y = 8, BB_X = 64;
 
+// pyramid element type: fp32, or bf16 for the NHWC lookup of the fused update block (half the
+// bytes of the ~0.5 GB volume the per-iteration window gathers read at chairs / B = 12)
+template <typename T>
+struct PyrO {
+  T* lvl[4];
+  int h[4];
+  int w[4];
+};
+
+template <typename OutT>
 __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(const uint16_t* __restrict__ f1,
                                                                  const uint16_t* __restrict__ f2,
-                                                                 Pyr4 out, int C, int H, int W,
+                                                                 PyrO<OutT> out, int C, int H, int W,
                                                                  int levels, float scale,
                                                                  int tiles_i, int bands_y,
                                                                  int tiles_x) {
@@ -252,9 +267,9 @@ __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(const uint16_t*
   }
 
   // ---- level 0 straight from the accumulators; level 1 from the wave's row pair
-  float* L0 = out.lvl[0];
+  OutT* L0 = out.lvl[0];
   const int h1 = out.h[1], w1 = out.w[1];
-  float* L1 = out.lvl[1];
+  OutT* L1 = out.lvl[1];
 #pragma unroll
   for (int a = 0; a < 2; ++a) {
 #pragma unroll
@@ -264,7 +279,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(const uint16_t*
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int y = y0 + 2 * wave + (j >> 1), x = x0 + 32 * (j & 1) + l32;
-        if (i < N && y < H && x < W) L0[(((int64_t)b * N + i) * H + y) * W + x] = acc[a][j][r] * scale;
+        if (i < N && y < H && x < W) pyr_st(&L0[(((int64_t)b * N + i) * H + y) * W + x], acc[a][j][r] * scale);
       }
       if (levels > 1) {
 #pragma unroll
@@ -278,7 +293,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(const uint16_t*
             const int Xl = 16 * xh + (l32 >> 1);
             const int Y = (y0 >> 1) + wave, X = (x0 >> 1) + Xl;
             P1[il][wave][Xl] = v;
-            if (i < N && Y < h1 && X < w1) L1[(((int64_t)b * N + i) * h1 + Y) * w1 + X] = v;
+            if (i < N && Y < h1 && X < w1) pyr_st(&L1[(((int64_t)b * N + i) * h1 + Y) * w1 + X], v);
           }
         }
       }
@@ -287,7 +302,7 @@ __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(const uint16_t*
   if (levels <= 2) return;  // uniform
   __syncthreads();
   {
-    float* L2 = out.lvl[2];
+    OutT* L2 = out.lvl[2];
     const int h2 = out.h[2], w2 = out.w[2];
     for (int e = threadIdx.x; e < BB_I * 2 * 16; e += 256) {
       const int il = e >> 5, c = e & 31;
@@ -297,19 +312,19 @@ __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(const uint16_t*
       const float v = ((r0[0] + r0[1]) + (r1[0] + r1[1])) * 0.25f;
       P2[il][Yl][Xl] = v;
       const int i = i0 + il, Y = (y0 >> 2) + Yl, X = (x0 >> 2) + Xl;
-      if (i < N && Y < h2 && X < w2) L2[(((int64_t)b * N + i) * h2 + Y) * w2 + X] = v;
+      if (i < N && Y < h2 && X < w2) pyr_st(&L2[(((int64_t)b * N + i) * h2 + Y) * w2 + X], v);
     }
   }
   __syncthreads();
   if (levels > 3) {
-    float* L3 = out.lvl[3];
+    OutT* L3 = out.lvl[3];
     const int h3 = out.h[3], w3 = out.w[3];
     for (int e = threadIdx.x; e < BB_I * 8; e += 256) {
       const int il = e >> 3, Xl = e & 7;
       const float v = ((P2[il][0][2 * Xl] + P2[il][0][2 * Xl + 1]) +
                        (P2[il][1][2 * Xl] + P2[il][1][2 * Xl + 1])) * 0.25f;
       const int i = i0 + il, Y = y0 >> 3, X = (x0 >> 3) + Xl;
-      if (i < N && Y < h3 && X < w3) L3[(((int64_t)b * N + i) * h3 + Y) * w3 + X] = v;
+      if (i < N && Y < h3 && X < w3) pyr_st(&L3[(((int64_t)b * N + i) * h3 + Y) * w3 + X], v);
     }
   }
 }
@@ -355,21 +370,26 @@ void launch_corr_build(const float* f1, const float* f2, float* const* lvl, cons
                      sqrtf((float)C), tiles_x, tiles_j);
 }
 
-void launch_corr_build_bf16(const uint16_t* f1, const uint16_t* f2, float* const* lvl, const int* hs,
-                            const int* ws, int B, int C, int H, int W, int levels,
+void launch_corr_build_bf16(const uint16_t* f1, const uint16_t* f2, void* const* lvl, const int* hs,
+                            const int* ws, int B, int C, int H, int W, int levels, bool pyr_bf16,
                             hipStream_t stream) {
-  Pyr4 p;
-  for (int l = 0; l < 4; ++l) {
-    p.lvl[l] = l < levels ? lvl[l] : nullptr;
-    p.h[l] = l < levels ? hs[l] : 0;
-    p.w[l] = l < levels ? ws[l] : 0;
-  }
   const int N = H * W;
   const int tiles_i = (int)raft_cdiv(N, BB_I), bands_y = (int)raft_cdiv(H, BB_Y);
   const int tiles_x = (int)raft_cdiv(W, BB_X);
   dim3 grid(tiles_i * bands_y * tiles_x, B);
-  hipLaunchKernelGGL(corr_build_bf16_kernel, grid, dim3(256), 0, stream, f1, f2, p, C, H, W,
-                     levels, 1.0f / sqrtf((float)C), tiles_i, bands_y, tiles_x);
+  auto go = [&](auto* tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    PyrO<T> p;
+    for (int l = 0; l < 4; ++l) {
+      p.lvl[l] = l < levels ? static_cast<T*>(lvl[l]) : nullptr;
+      p.h[l] = l < levels ? hs[l] : 0;
+      p.w[l] = l < levels ? ws[l] : 0;
+    }
+    hipLaunchKernelGGL(corr_build_bf16_kernel<T>, grid, dim3(256), 0, stream, f1, f2, p, C, H, W,
+                       levels, 1.0f / sqrtf((float)C), tiles_i, bands_y, tiles_x);
+  };
+  if (pyr_bf16) go((uint16_t*)nullptr);
+  else go((float*)nullptr);
 }
 
 void launch_corr_pyr_grad_reduce(float* const* glvl, const int* hs, const int* ws, int64_t planes,

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void corr_lookup_tile_kernel(PyrC4 pyr, const 
 // then interpolated from LDS into the bf16 pixel-row tile, which is streamed out as above.
 constexpr int TPW = 32;  // pixels per workgroup
 
-template <int R>
+template <int R, bool BF>
 __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const float* __restrict__ coords,
                                                               uint16_t* __restrict__ out, int cbuf,
                                                               int B, int H, int W, int levels) {
@@ -131,11 +131,13 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
   for (int l = 0; l < levels; ++l) {
     const int hl = pyr.h[l], wl = pyr.w[l];
     const uint32_t plane = (uint32_t)(hl * wl);
-    // this workgroup's planes of level l: pixels i0 .. i0+TPW-1 of image b
-    const float* base = pyr.lvl[l] + ((int64_t)b * N + i0) * plane;
+    // this workgroup's planes of level l: pixels i0 .. i0+TPW-1 of image b (fp32 or bf16 cells)
+    constexpr uint32_t ES = BF ? 2u : 4u;
+    const char* base = reinterpret_cast<const char*>(pyr.lvl[l]) +
+                       ((int64_t)b * N + i0) * (int64_t)plane * ES;
     const uint32_t nplanes = (uint32_t)min(TPW, N - i0);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(base), (short)0, (int)(nplanes * plane * 4u), 0x00020000);
+        const_cast<char*>(base), (short)0, (int)(nplanes * plane * ES), 0x00020000);
     float v[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -146,9 +148,12 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
         const float cx = cxy[(px * 4 + l) * 2], cy = cxy[(px * 4 + l) * 2 + 1];
         const int gx = (int)floorf(cx) - R + c, gy = (int)floorf(cy) - R + r;
         if ((unsigned)gy < (unsigned)hl && (unsigned)gx < (unsigned)wl)
-          off = ((uint32_t)px * plane + (uint32_t)(gy * wl + gx)) * 4u;
+          off = ((uint32_t)px * plane + (uint32_t)(gy * wl + gx)) * ES;
       }
-      v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+      if constexpr (BF)
+        v[k] = raft_bf16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0));
+      else
+        v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -450,12 +455,12 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
 
 }  // namespace
 
-bool launch_corr_lookup_tile(const float* const* lvl, const int* hs, const int* ws, int levels,
+bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* ws, int levels,
                              const float* coords, uint16_t* out, int cbuf, int B, int H, int W,
-                             int radius, hipStream_t stream) {
+                             int radius, bool pyr_bf16, hipStream_t stream) {
   PyrC4 p;
   for (int l = 0; l < 4; ++l) {
-    p.lvl[l] = l < levels ? lvl[l] : nullptr;
+    p.lvl[l] = l < levels ? static_cast<const float*>(lvl[l]) : nullptr;
     p.h[l] = l < levels ? hs[l] : 0;
     p.w[l] = l < levels ? ws[l] : 0;
   }
@@ -464,7 +469,7 @@ bool launch_corr_lookup_tile(const float* const* lvl, const int* hs, const int* 
     const char* e = getenv("RAFT_LOOKUP_LEGACY");
     return e && e[0] == '1';
   }();
-  if (legacy) {
+  if (legacy && !pyr_bf16) {
     dim3 grid((unsigned)(B * ((N + TP - 1) / TP)));
     if (radius == 4) hipLaunchKernelGGL(corr_lookup_tile_kernel<4>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
     else if (radius == 3) hipLaunchKernelGGL(corr_lookup_tile_kernel<3>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
@@ -472,8 +477,10 @@ bool launch_corr_lookup_tile(const float* const* lvl, const int* hs, const int* 
     return true;
   }
   dim3 grid((unsigned)(B * ((N + TPW - 1) / TPW)));
-  if (radius == 4) hipLaunchKernelGGL(corr_lookup_win_kernel<4>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-  else if (radius == 3) hipLaunchKernelGGL(corr_lookup_win_kernel<3>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+  if (radius == 4 && pyr_bf16) hipLaunchKernelGGL((corr_lookup_win_kernel<4, true>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+  else if (radius == 4) hipLaunchKernelGGL((corr_lookup_win_kernel<4, false>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+  else if (radius == 3 && pyr_bf16) hipLaunchKernelGGL((corr_lookup_win_kernel<3, true>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+  else if (radius == 3) hipLaunchKernelGGL((corr_lookup_win_kernel<3, false>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
   else return false;
   return true;
 }

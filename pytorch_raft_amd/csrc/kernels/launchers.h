@@ -16,8 +16,8 @@ struct PredPtrsMut {
 void launch_corr_build(const float* f1, const float* f2, float* const* lvl, const int* hs,
                        const int* ws, int B, int C, int H, int W, int levels, hipStream_t stream);
 // bf16 NHWC fmaps (B,H,W,C), C % 16 == 0
-void launch_corr_build_bf16(const uint16_t* f1, const uint16_t* f2, float* const* lvl, const int* hs,
-                            const int* ws, int B, int C, int H, int W, int levels,
+void launch_corr_build_bf16(const uint16_t* f1, const uint16_t* f2, void* const* lvl, const int* hs,
+                            const int* ws, int B, int C, int H, int W, int levels, bool pyr_bf16,
                             hipStream_t stream);
 void launch_corr_pyr_grad_reduce(float* const* glvl, const int* hs, const int* ws, int64_t planes,
                                  int levels, float inv_sqrt_c, float* out, hipStream_t stream);
@@ -199,6 +199,7 @@ struct WgradTapArgs {
   int tiles_x, tiles_per_img, chunks_per_item, total_chunks, chunks_per_split, splits;
   float* w_part;                         // [splits][cout][kpad]
   float* db_part;                        // [splits][cout] or null
+  uint16_t* dw_bf16;                     // non-null: dW stored as bf16 here (no accumulate)
 };
 bool launch_conv_wgrad_taps(const ConvWgradArgs& a, const WgradItems& it, const WgradTapArgs& ta,
                             float* db, hipStream_t stream);
@@ -245,9 +246,9 @@ struct WinList {
   const float* wg[RAFT_MAX_WIN];      // (B,N,L,E,E) per iteration
   int n;
 };
-bool launch_corr_lookup_tile(const float* const* lvl, const int* hs, const int* ws, int levels,
+bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* ws, int levels,
                              const float* coords, uint16_t* out, int cbuf, int B, int H, int W,
-                             int radius, hipStream_t stream);
+                             int radius, bool pyr_bf16, hipStream_t stream);
 bool launch_corr_window_grad(const float* coords, const uint16_t* dout, int cbuf, float* wg, int B,
                              int H, int W, int levels, int radius, hipStream_t stream);
 struct TapList {

@@ -117,7 +117,10 @@ def _use_hip(t, impl):
 class CorrBlock:
     """All-pairs correlation pyramid with a (2r+1)^2 window lookup per level."""
 
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, impl='auto', precision='fp32'):
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, impl='auto', precision='fp32',
+                 nhwc_lookup=False):
+        """``nhwc_lookup``: every lookup goes through ``lookup_nhwc`` (the fused update block),
+        so the pyramid may be stored in bf16 under mixed precision."""
         self.num_levels = num_levels
         self.radius = radius
         self.hip = _use_hip(fmap1, impl)
@@ -129,8 +132,9 @@ class CorrBlock:
                 f1, f2 = fmap1, fmap2
             else:
                 f1, f2 = fmap1.float().contiguous(), fmap2.float().contiguous()
-            self.volume = corr_ops.AllPairsVolume(f1, f2, num_levels,
-                                                  bf16_backward=(precision == 'bf16'))
+            self.volume = corr_ops.AllPairsVolume(
+                f1, f2, num_levels, bf16_backward=(precision == 'bf16'),
+                bf16_pyramid=bool(nhwc_lookup) and precision == 'bf16')
             self.corr_pyramid = None
         else:
             self.corr_pyramid = torch_corr_pyramid(fmap1.float(), fmap2.float(), num_levels)
@@ -161,7 +165,10 @@ def _to_nhwc_padded(corr, cbuf):
 class AlternateCorrBlock:
     """On-the-fly correlation: O(HW * r^2) memory instead of O((HW)^2); differentiable."""
 
-    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, impl='auto', precision='fp32'):
+    def __init__(self, fmap1, fmap2, num_levels=4, radius=4, impl='auto', precision='fp32',
+                 nhwc_lookup=False):
+        """``nhwc_lookup``: every lookup goes through ``lookup_nhwc`` (the fused update block),
+        so the pyramid may be stored in bf16 under mixed precision."""
         self.num_levels = num_levels
         self.radius = radius
         self.hip = _use_hip(fmap1, impl)

@@ -161,7 +161,8 @@ class RAFT(nn.Module):
                                          precision='bf16' if self.args.mixed_precision else 'fp32')
         else:
             corr_fn = CorrBlock(fmap1, fmap2, radius=self.args.corr_radius, impl=self.corr_impl,
-                                precision='bf16' if self.args.mixed_precision else 'fp32')
+                                precision='bf16' if self.args.mixed_precision else 'fp32',
+                                nhwc_lookup=self._use_fused_update(fmap1))
         dev = fmap1.device
         b, _, h8, w8 = fmap1.shape
         coords0 = coords_grid(b, h8, w8, device=dev)

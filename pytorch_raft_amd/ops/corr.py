@@ -37,6 +37,7 @@ class _State:
         self.taps = []       # (coords, bf16 NHWC lookup-output gradient) per iteration
         self.radius = None
         self.bf16_bwd = False
+        self.pyr_bf16 = False  # bf16 pyramid: NHWC (bf16-output) lookups only
 
 
 def _nhwc_bf16(f):
@@ -50,9 +51,10 @@ class _AllPairsBuild(torch.autograd.Function):
         ops = _ext.ops()
         ctx.nhwc = fmap1.dtype == torch.bfloat16
         if ctx.nhwc:
-            # mixed precision: bf16 MFMA straight from the NHWC encoder outputs (no fp32 copy)
+            # mixed precision: bf16 MFMA straight from the NHWC encoder outputs (no fp32 copy);
+            # a bf16 pyramid when only the NHWC lookup (fused update block, bf16 output) reads it
             f1, f2 = _nhwc_bf16(fmap1), _nhwc_bf16(fmap2)
-            pyr = ops.corr_build_bf16(f1, f2, levels)
+            pyr = ops.corr_build_bf16(f1, f2, levels, bool(state.pyr_bf16))
             ctx.save_for_backward(f1, f2)
         else:
             pyr = ops.corr_build(fmap1, fmap2, levels)
@@ -171,9 +173,12 @@ def _window_reduce_fits(h, w, levels):
 
 
 class AllPairsVolume:
-    def __init__(self, fmap1, fmap2, num_levels=4, bf16_backward=False):
+    def __init__(self, fmap1, fmap2, num_levels=4, bf16_backward=False, bf16_pyramid=False):
         self.state = _State()
         self.state.bf16_bwd = bool(bf16_backward)
+        # the window lookup writes bf16 taps anyway: a bf16 pyramid halves the bytes its
+        # per-iteration gathers pull (~0.5 GB fp32 volume at chairs / batch 12)
+        self.state.pyr_bf16 = bool(bf16_pyramid) and fmap1.dtype == torch.bfloat16
         self.levels = num_levels
         self.token = _AllPairsBuild.apply(fmap1.contiguous(), fmap2.contiguous(), num_levels,
                                           self.state)
@@ -183,6 +188,8 @@ class AllPairsVolume:
         return self.state.pyramid
 
     def lookup(self, coords, radius):
+        if self.state.pyr_bf16:
+            raise RuntimeError('bf16 pyramid: only the NHWC lookup (lookup_nhwc) reads it')
         return _AllPairsLookup.apply(self.token, coords.contiguous().float(), radius, self.state)
 
     def lookup_nhwc(self, coords, radius, cbuf):

@@ -293,11 +293,12 @@ class _Conv3x3WgradNative(torch.autograd.Function):
                 dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])[0]
         if ctx.needs_input_grad[1]:
             co, ci = w.shape[:2]
-            dwp = torch.zeros(co, 9 * ci, device=x.device, dtype=torch.float32)
+            # bf16 stored straight by the split reduce (no zero fill, no cast kernel)
+            dwp = torch.empty(co, 9 * ci, device=x.device, dtype=torch.bfloat16)
             C.conv_wgrad_taps([(dy.permute(0, 2, 3, 1), [x.permute(0, 2, 3, 1)])], 0, [0], [ci],
                               (3, 3), (1, 1), co, dwp, None)
             # packed (co, kh, kw, ci) -> (co, ci, kh, kw) with channels_last strides (= w's)
-            dw = dwp.view(co, 3, 3, ci).permute(0, 3, 1, 2).to(w.dtype)
+            dw = dwp.view(co, 3, 3, ci).permute(0, 3, 1, 2)
         return dx, dw
 
 

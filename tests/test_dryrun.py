@@ -25,7 +25,7 @@ def _returns():
             h, w = h // 2, w // 2
         return out
 
-    def corr_build_bf16(f1, f2, levels):
+    def corr_build_bf16(f1, f2, levels, pyr_bf16=False):
         b, h, w, c = f1.shape
         return corr_build(f1.permute(0, 3, 1, 2), f2, levels)
 

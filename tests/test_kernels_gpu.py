@@ -57,6 +57,28 @@ def test_corr_build_bf16_matches_torch(ext_ops, shape):
         torch.testing.assert_close(g, r, atol=2e-4, rtol=1e-4)
 
 
+@pytest.mark.parametrize('shape', [(2, 256, 46, 62), (1, 128, 13, 19)])
+def test_corr_build_bf16_pyramid_and_lookup(ext_ops, shape):
+    """bf16 pyramid (the fused path's storage): every level is the bf16 rounding of the fp32
+    build, and the NHWC window lookup reading it matches the lookup of the fp32 pyramid to bf16
+    resolution."""
+    b, c, h, w = shape
+    f1 = torch.randn(b, h, w, c, device=DEV).to(torch.bfloat16)
+    f2 = torch.randn(b, h, w, c, device=DEV).to(torch.bfloat16)
+    levels = 4 if min(h, w) >= 8 else 3
+    p32 = ext_ops.corr_build_bf16(f1, f2, levels, False)
+    p16 = ext_ops.corr_build_bf16(f1, f2, levels, True)
+    for a, q in zip(p16, p32):
+        assert a.dtype == torch.bfloat16 and a.shape == q.shape
+        torch.testing.assert_close(a.float(), q.to(torch.bfloat16).float(), atol=0, rtol=0)
+    coords = _coords(b, h, w, spread=6.0)
+    o32 = torch.zeros(b, h, w, 384, device=DEV, dtype=torch.bfloat16)
+    o16 = torch.zeros_like(o32)
+    ext_ops.corr_lookup_nhwc_(p32, coords, 4 if levels == 4 else 3, o32)
+    ext_ops.corr_lookup_nhwc_(p16, coords, 4 if levels == 4 else 3, o16)
+    assert _rel(o16.float(), o32.float()) < 1e-2
+
+
 def test_corrblock_bf16_fmaps_fwd_bwd(ext_ops):
     """Mixed-precision CorrBlock: bf16 channels_last fmaps in (as the encoders produce them),
     fp32 lookups out, bf16 fmap gradients back (bf16 dcorr: ~1e-2 relative)."""
