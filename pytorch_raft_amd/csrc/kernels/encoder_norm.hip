@@ -76,13 +76,13 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
     // 4 pixels per round with all four 16-B loads issued first: one outstanding load per
     // thread left this pass latency-bound at ~3 TB/s
     int p = p0 + pl;
-    for (; p + 3 * lanes < p1; p += 4 * lanes) {
-      uint4 raw[4];
+    for (; p + 7 * lanes < p1; p += 8 * lanes) {
+      uint4 raw[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u)
         raw[u] = *reinterpret_cast<const uint4*>(x + (base + p + u * lanes) * C + g * 8);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         float v[8];
         unpack8(raw[u], v);
 #pragma unroll
@@ -110,16 +110,33 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
     red[1][tid * 8 + i] = s2[i];
   }
   __syncthreads();
-  for (int c = tid; c < C; c += NT) {
-    const int gg = c / 8, ii = c % 8;
+  // block combine: Q = NT / C threads per channel each sum every Q-th lane row, then one
+  // thread per channel adds the Q partials (fixed order: deterministic)
+  {
+    __shared__ float red2[2][NT];
+    const int Q = NT / C;
+    const int c = tid % C, q = tid / C;
     float a = 0.f, b = 0.f;
-    for (int l = 0; l < lanes; ++l) {
-      a += red[0][(l * cg + gg) * 8 + ii];
-      b += red[1][(l * cg + gg) * 8 + ii];
+    if (q < Q) {
+      const int gg = c / 8, ii = c % 8;
+      for (int l = q; l < lanes; l += Q) {
+        a += red[0][(l * cg + gg) * 8 + ii];
+        b += red[1][(l * cg + gg) * 8 + ii];
+      }
+      red2[0][q * C + c] = a;
+      red2[1][q * C + c] = b;
     }
-    float* dst = part + ((int64_t)img * gridDim.x + blockIdx.x) * 2 * C;
-    dst[c] = a;
-    dst[C + c] = b;
+    __syncthreads();
+    if (tid < C) {
+      float sa = 0.f, sb = 0.f;
+      for (int k = 0; k < Q; ++k) {
+        sa += red2[0][k * C + tid];
+        sb += red2[1][k * C + tid];
+      }
+      float* dst = part + ((int64_t)img * gridDim.x + blockIdx.x) * 2 * C;
+      dst[tid] = sa;
+      dst[C + tid] = sb;
+    }
   }
 }
 
@@ -344,16 +361,16 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
   if (pl < lanes) {
     // 4 pixels (8 loads) in flight per round (see norm_stats_kernel)
     int p = p0 + pl;
-    for (; p + 3 * lanes < p1; p += 4 * lanes) {
-      uint4 rd[4], rx[4];
+    for (; p + 7 * lanes < p1; p += 8 * lanes) {
+      uint4 rd[8], rx[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const int64_t off = (base + p + u * lanes) * C + g * 8;
         rd[u] = *reinterpret_cast<const uint4*>(dy + off);
         rx[u] = *reinterpret_cast<const uint4*>(x + off);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) accum(rd[u], rx[u]);
+      for (int u = 0; u < 8; ++u) accum(rd[u], rx[u]);
     }
     for (; p < p1; p += lanes) {
       const int64_t off = (base + p) * C + g * 8;
@@ -367,18 +384,35 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
     red[2][tid * 8 + i] = sx[i];
   }
   __syncthreads();
-  for (int c = tid; c < C; c += NT) {
-    const int gg = c / 8, ii = c % 8;
-    float a = 0.f, b = 0.f, s = 0.f;
-    for (int l = 0; l < lanes; ++l) {
-      a += red[0][(l * cg + gg) * 8 + ii];
-      b += red[1][(l * cg + gg) * 8 + ii];
-      s += red[2][(l * cg + gg) * 8 + ii];
+  {
+    __shared__ float red2[3][NT];
+    const int Q = NT / C;
+    const int c = tid % C, q = tid / C;
+    if (q < Q) {
+      const int gg = c / 8, ii = c % 8;
+      float a = 0.f, b = 0.f, s = 0.f;
+      for (int l = q; l < lanes; l += Q) {
+        a += red[0][(l * cg + gg) * 8 + ii];
+        b += red[1][(l * cg + gg) * 8 + ii];
+        s += red[2][(l * cg + gg) * 8 + ii];
+      }
+      red2[0][q * C + c] = a;
+      red2[1][q * C + c] = b;
+      red2[2][q * C + c] = s;
     }
-    float* dst = part + ((int64_t)img * gridDim.x + blockIdx.x) * 3 * C;
-    dst[c] = a;
-    dst[C + c] = b;
-    dst[2 * C + c] = s;
+    __syncthreads();
+    if (tid < C) {
+      float sa = 0.f, sb = 0.f, ss = 0.f;
+      for (int k = 0; k < Q; ++k) {
+        sa += red2[0][k * C + tid];
+        sb += red2[1][k * C + tid];
+        ss += red2[2][k * C + tid];
+      }
+      float* dst = part + ((int64_t)img * gridDim.x + blockIdx.x) * 3 * C;
+      dst[tid] = sa;
+      dst[C + tid] = sb;
+      dst[2 * C + tid] = ss;
+    }
   }
 }
 
