@@ -617,7 +617,15 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   TORCH_CHECK(wpk.size(0) >= ((cout + bn - 1) / bn) * bn, "packed weight has too few rows");
   a.wpk = reinterpret_cast<const uint16_t*>(wpk.data_ptr<at::BFloat16>());
   a.kpad = (int)wpk.size(1);
-  if (bias.has_value() && bias->defined()) {
+  if (bias.has_value() && bias->defined() && bias->dim() == 4) {
+    // per-pixel bias map (B,H,W,>=cout) fp32: the precomputed context part of a ConvGRU conv
+    TORCH_CHECK(epi == EPI_GRU_ZR || epi == EPI_GRU_Q, "a per-pixel bias map needs a GRU epilogue");
+    check_nhwc(*bias, B, H, W, "bias map", at::kFloat);
+    TORCH_CHECK(bias->size(3) >= cout, "bias map has too few channels");
+    TORCH_CHECK(bias->numel() * 4 < (int64_t(1) << 31), "bias map exceeds the 2 GiB buffer-descriptor range");
+    a.bmap = bias->data_ptr<float>();
+    a.bmap_stride = (int)bias->size(3);
+  } else if (bias.has_value() && bias->defined()) {
     check_cuda_f32(*bias, "bias");
     TORCH_CHECK(bias->numel() >= cout, "bias too short");
     a.bias = bias->data_ptr<float>();
@@ -1242,6 +1250,36 @@ void gru_zr_bwd_(const Tensor& drh, const Tensor& dz, const Tensor& z, const Ten
                     bf16m(dpre_zr), dhprev.data_ptr<float>(), (int)P, (int)hd, cur_stream());
 }
 
+// out = sum(ins) (+ carry): n <= RAFT_SUM_MAX same-shape contiguous bf16 tensors, fp32 accumulation,
+// out bf16 or fp32 of the same shape
+void sum_bf16_(const std::vector<Tensor>& ins, const c10::optional<Tensor>& carry, const Tensor& out) {
+  TORCH_CHECK(!ins.empty() && ins.size() <= RAFT_SUM_MAX, "1..", RAFT_SUM_MAX, " summands");
+  const int64_t numel = out.numel();
+  TORCH_CHECK(numel % 8 == 0, "sum_bf16_: numel must be a multiple of 8");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() &&
+                  (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
+              "sum_bf16_: out must be a contiguous bf16 / fp32 GPU tensor");
+  BfPtrs p{};
+  for (size_t k = 0; k < ins.size(); ++k) {
+    TORCH_CHECK(ins[k].is_cuda() && ins[k].is_contiguous() && ins[k].scalar_type() == at::kBFloat16 &&
+                    ins[k].numel() == numel && ins[k].device() == out.device(),
+                "sum_bf16_: summands must be contiguous bf16 tensors of the output's size");
+    p.p[k] = bf16p(ins[k]);
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(p.p[k]) % 16 == 0, "sum_bf16_: summands must be 16-byte aligned");
+  }
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "sum_bf16_: out must be 16-byte aligned");
+  const float* cp = nullptr;
+  if (carry.has_value() && carry->defined()) {
+    check_cuda_f32(*carry, "carry");
+    TORCH_CHECK(carry->numel() == numel, "carry size");
+    cp = carry->data_ptr<float>();
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(cp) % 16 == 0, "sum_bf16_: carry must be 16-byte aligned");
+  }
+  c10::DeviceGuard gd(out.device());
+  launch_sum_bf16(p, (int)ins.size(), cp, out.data_ptr(), out.scalar_type() == at::kFloat, numel,
+                  cur_stream());
+}
+
 // flow (B,2,H,W) fp32 -> flowb (B,H,W,8) bf16 [fx, fy, 0...]; optionally slot[..., off:off+2] = flow
 void flow_prep_(const Tensor& flow, const Tensor& flowb, const c10::optional<Tensor>& slot,
                 int64_t slot_off) {
@@ -1415,6 +1453,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale) -> ()");
   m.def("gru_q_bwd_(Tensor dh, Tensor z, Tensor q, Tensor hprev, Tensor(a!) dpre_q, Tensor(b!) dz, Tensor(c!) dhprev) -> ()");
   m.def("gru_zr_bwd_(Tensor drh, Tensor dz, Tensor z, Tensor r, Tensor hprev, Tensor(a!) dpre_zr, Tensor(b!) dhprev) -> ()");
+  m.def("sum_bf16_(Tensor[] ins, Tensor? carry, Tensor(a!) out) -> ()");
   m.def("flow_prep_(Tensor flow, Tensor(a!) flowb, Tensor(b!)? slot, int slot_off) -> ()");
   m.def("seq_loss_fwd(Tensor[] preds, Tensor gt, Tensor valid, float gamma, float max_flow) -> Tensor");
   m.def("seq_loss_bwd(Tensor[] preds, Tensor gt, Tensor valid, Tensor dloss, float gamma, float max_flow) -> Tensor[]");
@@ -1466,4 +1505,5 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("gru_q_bwd_", &gru_q_bwd_);
   m.impl("gru_zr_bwd_", &gru_zr_bwd_);
   m.impl("flow_prep_", &flow_prep_);
+  m.impl("sum_bf16_", &sum_bf16_);
 }

@@ -110,6 +110,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
       float v[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = (acc[i][j][r] + bias) * a.scale;
+      if constexpr (EPI == EPI_GRU_ZR || EPI == EPI_GRU_Q) {
+        if (a.bmap != nullptr) {  // uniform
+          const rsrc_t bm = make_rsrc(a.bmap, P_u * (uint32_t)a.bmap_stride * 4u);
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            v[r] += bld_f32(bm, ok[r] ? (uint32_t)(mrow[r] * a.bmap_stride + n) * 4u : OOB);
+        }
+      }
 
       if constexpr (EPI == EPI_BF16 || EPI == EPI_RELU_BF16 || EPI == EPI_F32) {
 #pragma unroll

@@ -133,6 +133,10 @@ struct ConvFwdArgs {
   const uint16_t* wpk;  // packed weights [Npad][kpad] bf16
   int kpad;
   const float* bias;    // may be null
+  // GRU epilogues: per-pixel fp32 bias map [P][bmap_stride] added instead of `bias` (the
+  // iteration-invariant context part of the ConvGRU convs, precomputed once per forward)
+  const float* bmap;
+  int bmap_stride;
   int cout;
   void* out0;
   int out0_stride;
@@ -218,6 +222,13 @@ void launch_gru_zr_bwd(const float* drh, const float* dz, const uint16_t* z, con
                        hipStream_t stream);
 void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int slot_stride, int B,
                       int HW, hipStream_t stream);
+// out (bf16 or fp32) = sum of n <= RAFT_SUM_MAX bf16 tensors (+ fp32 carry); numel % 8 == 0
+#define RAFT_SUM_MAX 32
+struct BfPtrs {
+  const uint16_t* p[RAFT_SUM_MAX];
+};
+void launch_sum_bf16(const BfPtrs& ins, int n, const float* carry, void* out, bool out_f32,
+                     int64_t numel, hipStream_t stream);
 // (B,2,H,W) fp32 flow -> (B,H,W,128) bf16 7x7 patch (tap-major, 2 ch), + optional flow slot
 void launch_f1_patch(const float* flow, uint16_t* patch, uint16_t* slot, int slot_stride, int B, int H,
                      int W, hipStream_t stream);

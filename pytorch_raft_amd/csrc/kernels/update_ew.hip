@@ -128,11 +128,60 @@ __global__ __launch_bounds__(256) void f1_patch_kernel(const float* __restrict__
   }
 }
 
+// out = sum_k in[k] (+ carry), fp32 accumulation, 8 elements (16 B of bf16) per thread per step.
+// The ConvGRU context input is the same tensor in every iteration, so the context part of each
+// GRU conv's input / weight gradient is linear in the iterations' pre-activation gradients:
+// one conv over their sum replaces one per iteration (ops/update_hip.py).
+__global__ __launch_bounds__(256) void sum_bf16_kernel(BfPtrs ins, int n, const float* __restrict__ carry,
+                                                       void* __restrict__ out, int out_f32,
+                                                       int64_t total8) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total8;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    float acc[8];
+    if (carry != nullptr) {
+      const float4 c0 = reinterpret_cast<const float4*>(carry)[2 * t];
+      const float4 c1 = reinterpret_cast<const float4*>(carry)[2 * t + 1];
+      acc[0] = c0.x; acc[1] = c0.y; acc[2] = c0.z; acc[3] = c0.w;
+      acc[4] = c1.x; acc[5] = c1.y; acc[6] = c1.z; acc[7] = c1.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    }
+    for (int k = 0; k < n; ++k) {
+      const uint4 v = reinterpret_cast<const uint4*>(ins.p[k])[t];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += __uint_as_float(w[j] << 16);
+        acc[2 * j + 1] += __uint_as_float(w[j] & 0xffff0000u);
+      }
+    }
+    if (out_f32) {
+      float4* o = reinterpret_cast<float4*>(out) + 2 * t;
+      o[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      o[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    } else {
+      uint32_t w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        w[j] = (uint32_t)raft_f32_to_bf16(acc[2 * j]) | ((uint32_t)raft_f32_to_bf16(acc[2 * j + 1]) << 16);
+      reinterpret_cast<uint4*>(out)[t] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
 inline unsigned ew_blocks(int64_t total) {
   return (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 16);
 }
 
 }  // namespace
+
+void launch_sum_bf16(const BfPtrs& ins, int n, const float* carry, void* out, bool out_f32,
+                     int64_t numel, hipStream_t stream) {
+  const int64_t total8 = numel / 8;
+  hipLaunchKernelGGL(sum_bf16_kernel, dim3(ew_blocks(total8)), dim3(256), 0, stream, ins, n, carry, out,
+                     out_f32 ? 1 : 0, total8);
+}
 
 void launch_relu_bwd(const float* g, int gs, const uint16_t* y, int ys, uint16_t* out, int os, int P,
                      int C, float scale, hipStream_t stream) {

@@ -17,6 +17,7 @@ _LOCK = threading.Lock()
 _STATE = {'loaded': None, 'error': None}
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_PKG_DIR, '_C.so')
+SUM_MAX = 32  # summands per sum_bf16_ launch (RAFT_SUM_MAX in csrc/kernels/launchers.h)
 
 
 def _try_load():

@@ -79,13 +79,15 @@ def conv_fwd(segs, wpk, bias, ksize, pad, cout, epi, outs, out_offs, aux=(), aux
     give the zero padding for free), so one launch covers < 2 GiB per buffer; larger batches
     (e.g. Sintel-size inference at batch 512+) are issued as batch slices."""
     limit = 1 << 31
-    big = max(t.numel() * t.element_size() for t in [s[0] for s in segs] + list(outs) + list(aux))
+    bmap = bias is not None and bias.dim() == 4   # per-pixel bias map (GRU epilogues)
+    big = max(t.numel() * t.element_size() for t in [s[0] for s in segs] + list(outs) + list(aux)
+              + ([bias] if bmap else []))
     if big >= limit:
         b = segs[0][0].shape[0]
         step = max(1, (limit - 1) * b // big)
         for b0 in range(0, b, step):
             sl = slice(b0, min(b, b0 + step))
-            conv_fwd([(t[sl], o, c) for t, o, c in segs], wpk, bias, ksize, pad, cout, epi,
+            conv_fwd([(t[sl], o, c) for t, o, c in segs], wpk, bias[sl] if bmap else bias, ksize, pad, cout, epi,
                      [t[sl] for t in outs], out_offs, [t[sl] for t in aux], aux_offs, scale,
                      split, cin_small, bn)
         return

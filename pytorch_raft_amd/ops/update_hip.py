@@ -42,8 +42,12 @@ class _LayerSpec:
     """Geometry of one conv of the fused block."""
 
     def __init__(self, name, cout, ksize, in_real, in_pad, small=False, relu=False, scale=1.0,
-                 patch=False, row_pad=None, adj_pad=None, adj_off=0):
+                 patch=False, row_pad=None, adj_pad=None, adj_off=0, in_sel=None, no_bias=False):
         self.name = name
+        # in_sel: [(start, count)] input-channel ranges of the module weight this conv uses (one
+        # module conv split over two fused convs); no_bias: the module bias belongs to the other
+        self.in_sel = in_sel
+        self.no_bias = no_bias
         # row_pad: per source module, its output rows are zero-padded to this many (a hidden width
         # of 96 carried in 128-channel buffers); adj_pad / adj_off: K width of the adjoint (dgrad)
         # conv's input segment and where this layer's output channels sit inside it (the adjoint
@@ -64,20 +68,32 @@ class _LayerSpec:
         self.scale = scale
 
 
+_HM = [(0, HD), (2 * HD, 128)]   # [h | mf] channels of a ConvGRU conv's module weight
+_CTX = [(HD, HD)]                # its context (inp) channels
+
 SPECS = [
     _LayerSpec('c1', 256, (1, 1), [324], [CORR_BUF]),
     _LayerSpec('c2', 192, (3, 3), [256], [256]),
     _LayerSpec('f1', 128, (7, 7), [2], [8], small=True, patch=True),
     _LayerSpec('f2', 64, (3, 3), [128], [128]),
     _LayerSpec('conv', 126, (3, 3), [256], [256]),
-    _LayerSpec('zr1', 256, (1, 5), [128, 128, 128], [128, 128, 128]),
-    _LayerSpec('q1', 128, (1, 5), [128, 128, 128], [128, 128, 128]),
-    _LayerSpec('zr2', 256, (5, 1), [128, 128, 128], [128, 128, 128]),
-    _LayerSpec('q2', 128, (5, 1), [128, 128, 128], [128, 128, 128]),
+    # ConvGRU convs over [h | inp | mf]: the per-iteration conv reads [h | mf] only; the context
+    # part (inp: the same tensor in every iteration) is the '<name>i' conv, run ONCE per forward
+    # into a per-pixel fp32 bias map, and once per backward on the iterations' summed
+    # pre-activation gradients (linearity: sum_t conv_T(g_t) = conv_T(sum_t g_t))
+    _LayerSpec('zr1', 256, (1, 5), [128, 128], [128, 128], in_sel=_HM, no_bias=True),
+    _LayerSpec('q1', 128, (1, 5), [128, 128], [128, 128], in_sel=_HM, no_bias=True),
+    _LayerSpec('zr2', 256, (5, 1), [128, 128], [128, 128], in_sel=_HM, no_bias=True),
+    _LayerSpec('q2', 128, (5, 1), [128, 128], [128, 128], in_sel=_HM, no_bias=True),
     _LayerSpec('head', 512, (3, 3), [128], [128]),
     _LayerSpec('fh2', 2, (3, 3), [256], [256]),
     _LayerSpec('m2', 576, (1, 1), [256], [256], scale=0.25),
+    _LayerSpec('zr1i', 256, (1, 5), [128], [128], in_sel=_CTX),
+    _LayerSpec('q1i', 128, (1, 5), [128], [128], in_sel=_CTX),
+    _LayerSpec('zr2i', 256, (5, 1), [128], [128], in_sel=_CTX),
+    _LayerSpec('q2i', 128, (5, 1), [128], [128], in_sel=_CTX),
 ]
+GRU_CONVS = ('zr1', 'q1', 'zr2', 'q2')
 SPEC = {s.name: s for s in SPECS}
 
 
@@ -90,10 +106,14 @@ class Design:
         self.module_params = module_params
 
     def flat_params(self, ub):
+        """Module parameters in spec order, each once (a module conv may feed two specs)."""
         mp = self.module_params(ub)
-        out = []
+        out, seen = [], set()
         for s in self.specs:
             for w, b in mp[s.name]:
+                if id(w) in seen:
+                    continue
+                seen.add(id(w))
                 out += [w, b]
         return out
 
@@ -114,6 +134,10 @@ def module_params(ub):
         'head': [(fh.conv1.weight, fh.conv1.bias), (mk[0].weight, mk[0].bias)],
         'fh2': [(fh.conv2.weight, fh.conv2.bias)],
         'm2': [(mk[2].weight, mk[2].bias)],
+        'zr1i': [(g.convz1.weight, g.convz1.bias), (g.convr1.weight, g.convr1.bias)],
+        'q1i': [(g.convq1.weight, g.convq1.bias)],
+        'zr2i': [(g.convz2.weight, g.convz2.bias), (g.convr2.weight, g.convr2.bias)],
+        'q2i': [(g.convq2.weight, g.convq2.bias)],
     }
 
 
@@ -134,6 +158,10 @@ def _pack_layers(params_by_layer, need_grad, dtype, design=FULL):
     for s in design.specs:
         ws = [w for w, _ in params_by_layer[s.name]]
         bs = [b for _, b in params_by_layer[s.name]]
+        if s.in_sel is not None:
+            ws = [torch.cat([w[:, a:a + n] for a, n in s.in_sel], 1) for w in ws]
+        if s.no_bias:
+            bs = [torch.zeros_like(b) for b in bs]
         if s.row_pad is not None:
             ws = [F_.pad(w, (0, 0, 0, 0, 0, 0, 0, s.row_pad - w.shape[0])) for w in ws]
             bs = [F_.pad(b, (0, s.row_pad - b.shape[0])) for b in bs]
@@ -185,8 +213,8 @@ class _PackPlan:
         for p in params:
             ids.append((torch.arange(p.numel(), dtype=torch.float64) + off + 1).view(p.shape))
             off += p.numel()
-        it = iter(ids)
-        by_layer = {s.name: [(next(it), next(it)) for _ in module_params(ub)[s.name]]
+        idmap = {id(p): t for p, t in zip(params, ids)}
+        by_layer = {s.name: [(idmap[id(w)], idmap[id(b)]) for w, b in module_params(ub)[s.name]]
                     for s in SPECS}
         w_idx, wd_idx, b_idx, x_idx = _pack_layers(by_layer, need_grad, torch.float64, design)
         # gather index: element id - 1; padding (id 0) -> the zero slot appended after the params
@@ -252,6 +280,8 @@ class _Packed:
         self.db = {}
         self.pending = {}  # conv name -> [(g, g_off, segs)] awaiting the batched weight gradient
         self.fh2_items = []  # (fp32 delta gradient, head activations) per iteration
+        self.ctx = None      # GRU conv -> fp32 (B,H,W,cout) context bias map (see ctx_maps)
+        self.ctx_key = None
         self.device = device
         plan = self.plan = _plan(ub, need_grad, device, design)
         self.kpad = plan.kpad
@@ -328,6 +358,7 @@ class _State:
         self.n_iter = 0        # iterations issued through this block (forward order)
         self.next_bwd = None   # iteration whose backward must run next (strictly n_iter-1 .. 0)
         self.dinp_acc = None   # fp32 gradient w.r.t. the context input, summed over iterations
+        self.ctx_g = {}        # GRU conv -> its pre-activation gradients of the iterations run
         self.design = FULL
 
 
@@ -343,7 +374,7 @@ class _UpdateWeights(torch.autograd.Function):
     @staticmethod
     def backward(ctx, _tok):
         st = ctx.state
-        if st.dinp_acc is not None:
+        if st.dinp_acc is not None or st.ctx_g:
             # the context gradient is handed to autograd by iteration 0's backward; a partial
             # backward (autograd.grad over a subset of the iterations) would silently drop it
             raise RuntimeError('fused update block: the backward must run through every GRU '
@@ -491,6 +522,43 @@ def _f32(shape, dev, zero=False):
     return (torch.zeros if zero else torch.empty)(*shape, device=dev, dtype=torch.float32)
 
 
+def ctx_maps(pk, inp):
+    """Context part of the four ConvGRU convs, conv(inp, W_inp) + bias as fp32 (B,H,W,cout)
+    maps -- computed once per forward pass (the iterations share ``inp``) and added by the
+    iterations' GRU epilogues."""
+    key = (inp.data_ptr(), tuple(inp.shape), inp._version)
+    if pk.ctx is not None:
+        if key != pk.ctx_key:
+            raise RuntimeError('fused update block: every iteration of a forward pass must take '
+                               'the same context tensor')
+        return pk.ctx
+    B, H, W, _ = inp.shape
+    pk.ctx = {}
+    for name in GRU_CONVS:
+        s = SPEC[name + 'i']
+        m = torch.empty(B, H, W, s.cout, device=inp.device, dtype=torch.float32)
+        C.conv_fwd([(inp, 0, HD)], pk.w[s.name], pk.b[s.name], s.k, s.pad, s.cout, C.EPI_F32,
+                   [m], [0])
+        pk.ctx[name] = m
+    pk.ctx_key = key
+    return pk.ctx
+
+
+def _sum_bf16(gs):
+    """bf16 sum (fp32 accumulation) of same-shape bf16 tensors."""
+    ops = _ext.ops()
+    out = torch.empty_like(gs[0])
+    n = _ext.SUM_MAX
+    if len(gs) <= n:
+        ops.sum_bf16_(gs, None, out)
+        return out
+    carry = torch.empty(gs[0].shape, device=gs[0].device, dtype=torch.float32)
+    ops.sum_bf16_(gs[:n], None, carry)
+    for i in range(n, len(gs), n):
+        ops.sum_bf16_(gs[i:i + n], carry, out if i + n >= len(gs) else carry)
+    return out
+
+
 def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
     """Forward of one fused iteration; returns (h2, delta, mask, saved tensors).
 
@@ -507,10 +575,10 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
     cf = _bf16(sh + (256,), dev)
     f1 = _bf16(sh + (128,), dev)
 
-    def conv(name, segs, epi, outs, offs, aux=(), aux_offs=(), split=0, cout=None):
+    def conv(name, segs, epi, outs, offs, aux=(), aux_offs=(), split=0, cout=None, bias=None):
         s = SPEC[name]
         cout = cout or s.cout
-        w, b = pk.w[name], pk.b[name]
+        w, b = pk.w[name], (pk.b[name] if bias is None else bias)
         if cout != s.cout:  # leading output rows of a fused conv (packed rows are cout-major)
             w, b = w[:C.round_up(cout, 128)], b[:cout]
         k, pad, small = ((1, 1), (0, 0), False) if s.patch else (s.k, s.pad, s.small)
@@ -527,13 +595,14 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
     conv('conv', [(cf, 0, 256)], C.EPI_RELU_BF16, [mf], [0])
     gates = {}
     hin = h
+    ctx = ctx_maps(pk, inp)
     for tag in ('1', '2'):
         z, rh, r = _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev)
-        conv('zr' + tag, [(hin, 0, HD), (inp, 0, HD), (mf, 0, 128)], C.EPI_GRU_ZR, [z, rh, r],
-             [0, 0, 0], aux=[hin], aux_offs=[0], split=HD)
+        conv('zr' + tag, [(hin, 0, HD), (mf, 0, 128)], C.EPI_GRU_ZR, [z, rh, r],
+             [0, 0, 0], aux=[hin], aux_offs=[0], split=HD, bias=ctx['zr' + tag])
         hn, q = _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev)
-        conv('q' + tag, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)], C.EPI_GRU_Q, [hn, q], [0, 0],
-             aux=[hin, z], aux_offs=[0, 0])
+        conv('q' + tag, [(rh, 0, HD), (mf, 0, 128)], C.EPI_GRU_Q, [hn, q], [0, 0],
+             aux=[hin, z], aux_offs=[0, 0], bias=ctx['q' + tag])
         gates[tag] = (hin, z, rh, r, q)
         hin = hn
     h2 = hin
@@ -650,13 +719,11 @@ class _UpdateIter(torch.autograd.Function):
         else:
             dgrad('head', [(dpre_head, 0, 512)], [(dh, 0, HD, HD, 1)])
 
-        # inp is shared by every iteration: its gradient accumulates in ONE fp32 buffer across
-        # the iterations' backwards (11 -> 0, in that order since each needs the next one's dh)
-        # and is handed to autograd once, by iteration 0 -- instead of 12 bf16 casts + 11 adds
-        acc_inp = st.dinp_acc is not None
-        if not acc_inp:
-            st.dinp_acc = _f32(sh + (HD,), dev)
-        dinp = st.dinp_acc
+        # inp is shared by every iteration: the GRU convs' context parts get their input / weight
+        # gradients once, from the iterations' summed pre-activation gradients, after the last
+        # iteration's backward (11 -> 0, in that order since each needs the next one's dh); the
+        # context gradient is handed to autograd by iteration 0
+        ctx_g = st.ctx_g
         dmf = _f32(sh + (128,), dev)
         first = 1  # the first dgrad into dmf (q2's) stores: no zero fill
         for k, (tag, (hin, z, rh, r, q)) in enumerate(halves):
@@ -664,32 +731,31 @@ class _UpdateIter(torch.autograd.Function):
                 # the q gate ran in the epilogue of the previous dgrad (head / zr2); the z / r
                 # gates run in this q dgrad's d(r*h) epilogue, d(r*h) itself is never stored
                 dpre_q, dz, dhp = nxt
-                wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)])
+                wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (mf, 0, 128)])
                 dpre_zr = _bf16(sh + (2 * HD,), dev)
                 dgrad('q' + tag, [(dpre_q, 0, HD)],
-                      [(dhp, 0, HD, HD, 0), (dinp, 0, HD, HD, int(acc_inp)),
-                       (dmf, 0, 128, 128, 1 - first)],
-                      gates=[(2, [z, r, hin, dz, dpre_zr, dz, dhp]), None, None])
+                      [(dhp, 0, HD, HD, 0), (dmf, 0, 128, 128, 1 - first)],
+                      gates=[(2, [z, r, hin, dz, dpre_zr, dz, dhp]), None])
             else:
                 dpre_q = _bf16(sh + (HD,), dev)
                 dz = _f32(sh + (HD,), dev)
                 dhp = _f32(sh + (HD,), dev)
                 ops.gru_q_bwd_(dh, z, q, hin, dpre_q, dz, dhp)
-                wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (inp, 0, HD), (mf, 0, 128)])
+                wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (mf, 0, 128)])
                 drh = _f32(sh + (HD,), dev)
                 dgrad('q' + tag, [(dpre_q, 0, HD)],
-                      [(drh, 0, HD, HD, 0), (dinp, 0, HD, HD, int(acc_inp)),
-                       (dmf, 0, 128, 128, 1 - first)])
+                      [(drh, 0, HD, HD, 0), (dmf, 0, 128, 128, 1 - first)])
                 dpre_zr = _bf16(sh + (2 * HD,), dev)
                 ops.gru_zr_bwd_(drh, dz, z, r, hin, dpre_zr, dhp)
             first = 0
-            acc_inp = True
-            wgrad('zr' + tag, dpre_zr, 0, [(hin, 0, HD), (inp, 0, HD), (mf, 0, 128)])
-            zr_outs = [(dhp, 0, HD, HD, 1), (dinp, 0, HD, HD, 1), (dmf, 0, 128, 128, 1)]
+            ctx_g.setdefault('q' + tag, []).append(dpre_q)
+            ctx_g.setdefault('zr' + tag, []).append(dpre_zr)
+            wgrad('zr' + tag, dpre_zr, 0, [(hin, 0, HD), (mf, 0, 128)])
+            zr_outs = [(dhp, 0, HD, HD, 1), (dmf, 0, 128, 128, 1)]
             if _GATES_FUSED and k == 0:
                 # dhp is now the final gradient of half-step 1's output: its q gate here
                 gspec, nxt = qgate(halves[1][1])
-                dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)], zr_outs, gates=[gspec, None, None])
+                dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)], zr_outs, gates=[gspec, None])
             else:
                 dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)], zr_outs)
             dh = dhp
@@ -713,11 +779,17 @@ class _UpdateIter(torch.autograd.Function):
         br.join()
         wgrad('f1', dpre_f1, 0, [(patch, 0, 128)])
         wgrad('c1', dpre_c1, 0, [(corr, 0, CORR_BUF)])
+        dinp = None
         if ctx.itr == 0:
-            st.dinp_acc = None
+            # context input / weight gradients of the four GRU convs on the summed gradients
+            dinp = _f32(sh + (HD,), dev)
+            for j, name in enumerate(GRU_CONVS):
+                gsum = _sum_bf16(ctx_g.pop(name))
+                cnt = gsum.shape[-1]
+                dgrad(name + 'i', [(gsum, 0, cnt)], [(dinp, 0, HD, HD, int(j > 0))])
+                wgrad(name + 'i', gsum, 0, [(inp, 0, HD)])
+            st.ctx_g = {}
             st.next_bwd = None
-        else:
-            dinp = None
         # token: no gradient value (autograd still runs the weight node after every iteration)
         return (None, dh, dinp, dcorr, None, None)
 

@@ -41,13 +41,30 @@ def test_unpack_grads_matches_per_layer_unpack():
     pk = U._Packed(ub, params, torch.device('cpu'), need_grad=True)
     g = torch.Generator().manual_seed(1)
     pk.dwflat.copy_(torch.randn(pk.dwflat.shape, generator=g))
-    ref = []
+    # per spec: module-layout gradient of the input channels it owns (in_sel), bias if it has one
+    parts = {}
     for s in U.SPECS:
         dw, db = pk.dw[s.name] * s.scale, pk.db[s.name] * s.scale
         if s.small:
             wg = C.unpack_weight_grad_small(dw, s.cout, s.in_real[0], s.k)
         else:
             wg = C.unpack_weight_grad(dw, s.cout, s.in_real, s.in_pad, s.k)
+        base = s.name[:-1] if s.name.endswith('i') else s.name
+        sel = s.in_sel or [(0, wg.shape[1])]
+        full = parts.setdefault(base, [None, None])
+        if full[0] is None:  # split GRU convs: module weight over [h | inp | mf] = 384
+            full[0] = torch.zeros(s.cout, 3 * U.HD if s.in_sel else wg.shape[1], *s.k)
+        off = 0
+        for a, n in sel:
+            full[0][:, a:a + n] = wg[:, off:off + n]
+            off += n
+        if not s.no_bias:
+            full[1] = db
+    ref = []
+    for s in U.SPECS:
+        if s.name not in parts:
+            continue
+        wg, db = parts[s.name]
         if s.name in ('zr1', 'zr2', 'head'):
             h = s.cout // 2
             ref += [wg[:h], db[:h], wg[h:], db[h:]]
