@@ -25,6 +25,7 @@
 // dgrad reuses this kernel with flipped / transposed packed weights (stride-1 same padding is
 // self-adjoint up to the flip); wgrad lives in conv_wgrad.hip.
 #include "conv_common.h"
+#include "conv_halo.h"
 
 #include <cmath>
 #include <cstdlib>
@@ -240,8 +241,9 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
 struct CfgDesc {
   int tm, tn, wvm, bm, bn;
   bool small_ok;
-  int glds;  // 0: register-staged kernel; n: LDS-DMA kernel with n pipeline stages
+  int glds;  // 0: register-staged kernel; n: LDS-DMA kernel with n pipeline stages; HALO
 };
+constexpr int HALO = 9;
 // (keep in sync with the dispatch switch below)
 constexpr CfgDesc kCfgs[] = {
     {2, 2, 2, 128, 128, true, false},  {1, 2, 2, 64, 128, true, false},
@@ -261,6 +263,9 @@ constexpr CfgDesc kCfgs[] = {
     // one-round tiles for M = 34,224 (chairs, B = 12): 214 / 238 / 179 workgroups
     {5, 2, 1, 160, 256, false, 2},  {5, 2, 1, 160, 256, false, 3},
     {9, 1, 1, 288, 128, false, 2},  {3, 3, 2, 192, 192, false, 2},
+    // halo-tile kernel (conv_halo.h; glds = HALO): A image per channel chunk, B straight to VGPRs
+    {5, 1, 1, 160, 128, false, HALO}, {5, 2, 1, 160, 256, false, HALO},
+    {4, 2, 1, 128, 256, false, HALO}, {2, 2, 2, 128, 128, false, HALO},
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -297,6 +302,8 @@ bool launch_cfg_idx(const ConvFwdArgs& a, int idx, hipStream_t stream) {
       case 8: launch_one<EPI, false, 4, 2, 1>(a, stream); return true;
       case 9: launch_one<EPI, false, 3, 2, 1>(a, stream); return true;
       default:
+        if (idx >= 0 && idx < kNumCfgs && kCfgs[idx].glds == HALO)
+          return launch_conv_halo(a, EPI, kCfgs[idx].tm, kCfgs[idx].tn, kCfgs[idx].wvm, stream);
         if (idx >= 0 && idx < kNumCfgs && kCfgs[idx].glds) return launch_conv_glds(a, EPI, idx, stream);
         return false;
     }
@@ -321,6 +328,14 @@ bool launch_epi_idx(const ConvFwdArgs& a, int epi, int idx, bool smallc, hipStre
 #undef RAFT_EPI_CASE
 }
 
+bool halo_disabled() {
+  static const bool off = [] {
+    const char* e = getenv("RAFT_CONV_HALO");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
 bool glds_disabled() {
   static const bool off = [] {
     const char* e = getenv("RAFT_CONV_GLDS");
@@ -333,6 +348,7 @@ bool cfg_allowed(int idx, int cout, bool smallc, int epi) {
   const CfgDesc& c = kCfgs[idx];
   if (smallc && !c.small_ok) return false;
   if (c.glds && glds_disabled()) return false;
+  if (c.glds == HALO && halo_disabled()) return false;
   if (idx == 6 && (epi == EPI_GRU_ZR || epi == EPI_GRU_Q)) return false;
   const int npad = (cout + 31) / 32 * 32;
   return c.bn <= 2 * npad || c.bn <= 32;  // no config more than half empty in N
@@ -417,7 +433,10 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   return best;
 }
 
+int g_forced_cfg = -1;
+
 int choose_cfg(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
+  if (g_forced_cfg >= 0) return g_forced_cfg;
   static const int forced = [] {
     const char* e = getenv("RAFT_CONV_CFG");
     return e ? atoi(e) : -1;
@@ -461,6 +480,8 @@ bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStre
   }
   return launch_epi_idx(a, epi, idx, smallc, stream);
 }
+
+void conv_set_forced_cfg(int idx) { g_forced_cfg = idx < kNumCfgs ? idx : -1; }
 
 int conv_tuned_table(int* out, int max_rows) {
   std::lock_guard<std::mutex> lk(g_tune_mu);

@@ -162,6 +162,8 @@ bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStre
 bool launch_conv_glds(const ConvFwdArgs& a, int epi, int idx, hipStream_t stream);
 // rows of 12 ints: P H W KH KW cin cout small epi_class cfg BM BN
 int conv_tuned_table(int* out, int max_rows);
+// tests: run every following conv launch with config `idx` (-1: back to the tuned choice)
+void conv_set_forced_cfg(int idx);
 
 struct ConvWgradArgs {
   const uint16_t* g;  // dL/d(pre-activation), NHWC bf16, offset to channel 0

@@ -7,7 +7,7 @@ import torch  # noqa: E402
 
 from pytorch_raft_amd.ops import conv as C  # noqa: E402
 
-SH = {'zr': (384, 256, (1, 5)), 'q': (384, 128, (5, 1)), 'c2': (256, 192, (3, 3)),
+SH = {'zr': (384, 256, (1, 5)), 'zr2': (256, 256, (1, 5)), 'q': (384, 128, (5, 1)), 'c2': (256, 192, (3, 3)),
       'head': (128, 512, (3, 3)), 'conv': (256, 126, (3, 3)), 'm2': (256, 576, (1, 1))}
 name = sys.argv[1]
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 20

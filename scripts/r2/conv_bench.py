@@ -13,10 +13,10 @@ GEOS = [  # name, cout, k, cin segs
     ('c2', 192, (3, 3), [256]),
     ('f2', 64, (3, 3), [128]),
     ('conv', 126, (3, 3), [256]),
-    ('zr1', 256, (1, 5), [128, 128, 128]),
-    ('q1', 128, (1, 5), [128, 128, 128]),
-    ('zr2', 256, (5, 1), [128, 128, 128]),
-    ('q2', 128, (5, 1), [128, 128, 128]),
+    ('zr1', 256, (1, 5), [128, 128]),   # [h | mf]: the context part is hoisted (update_hip.py)
+    ('q1', 128, (1, 5), [128, 128]),
+    ('zr2', 256, (5, 1), [128, 128]),
+    ('q2', 128, (5, 1), [128, 128]),
     ('head', 512, (3, 3), [128]),
     ('m2', 576, (1, 1), [256]),
 ]

@@ -288,3 +288,77 @@ def test_conv_wgrad_taps(ext_ops, cin, cout, k, segs, g_off, splits):
     C.conv_wgrad_taps(items, g_off, [0] * len(seg_cnt), seg_cnt, k, pad, cout, dw2, db2,
                       splits=splits)
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+HALO_CFGS = (30, 31, 32, 33)   # conv_igemm.hip kCfgs: the halo-tile kernel (conv_halo.h)
+
+
+@pytest.mark.parametrize('cfg', HALO_CFGS)
+@pytest.mark.parametrize('segs,cout,k,hw', [
+    ([256], 192, (3, 3), (13, 21)),
+    ([128, 128], 256, (1, 5), (13, 21)),
+    ([128, 128], 128, (5, 1), (11, 62)),    # 5x1 at W = 62: the largest (16-piece) A image
+    ([384], 256, (1, 1), (9, 17)),
+    ([128], 126, (3, 3), (46, 62)),
+])
+def test_conv_halo_fwd(ext_ops, cfg, segs, cout, k, hw):
+    """Halo-tile kernel forced for every tile shape: fwd vs an fp32 conv of the bf16 operands,
+    across image / batch boundaries (rows whose shifted neighbour leaves the image read zeros)."""
+    torch.manual_seed(5)
+    B, (H, W) = 2, hw
+    cin = sum(segs)
+    xs = [torch.randn(B, c, H, W, device=DEV) for c in segs]
+    w = torch.randn(cout, cin, *k, device=DEV) / (cin * k[0] * k[1]) ** 0.5
+    b = torch.randn(cout, device=DEV)
+    pad = (k[0] // 2, k[1] // 2)
+    ref = _ref(torch.cat(xs, 1), w, b, pad)
+    bufs = [C.nhwc(x) for x in xs]
+    wpk = C.pack_weight(w, segs, segs)
+    out = torch.zeros(B, H, W, cout + 2, device=DEV)
+    torch.ops.raft_amd.conv_set_forced_cfg(cfg)
+    try:
+        C.conv_fwd([(t, 0, c) for t, c in zip(bufs, segs)], wpk, b, k, pad, cout, C.EPI_F32,
+                   [out], [0])
+        torch.cuda.synchronize()
+    finally:
+        torch.ops.raft_amd.conv_set_forced_cfg(-1)
+    torch.testing.assert_close(C.nchw(out[..., :cout]), ref, atol=2e-3 * max(1.0, ref.abs().max().item()),
+                               rtol=2e-3)
+    assert torch.all(out[..., cout:] == 0)
+
+
+@pytest.mark.parametrize('cfg', HALO_CFGS)
+def test_conv_halo_gru_and_dgrad(ext_ops, cfg):
+    """Halo kernel under the GRU gate epilogue (with a per-pixel bias map) and the multi-segment
+    dgrad epilogue (fp32 store + accumulate), against the register / LDS-DMA kernels' results."""
+    torch.manual_seed(6)
+    B, H, W, hd = 2, 10, 14, 128
+    h = C.nhwc(torch.randn(B, hd, H, W, device=DEV).tanh())
+    x = C.nhwc(torch.randn(B, 128, H, W, device=DEV))
+    wzr = torch.randn(2 * hd, 2 * hd, 1, 5, device=DEV) / 40
+    bmap = torch.randn(B, H, W, 2 * hd, device=DEV) * 0.1
+    wpk = C.pack_weight(wzr, [hd, 128], [hd, 128])
+    g = C.nhwc(torch.randn(B, 2 * hd, H, W, device=DEV))
+    wd = C.pack_weight_dgrad(wzr, [2 * hd], [2 * hd])
+    zb = torch.zeros(2 * hd, device=DEV)
+
+    def run():
+        z, rh, r = (torch.empty(B, H, W, hd, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+        C.conv_fwd([(h, 0, hd), (x, 0, 128)], wpk, bmap, (1, 5), (0, 2), 2 * hd, C.EPI_GRU_ZR,
+                   [z, rh, r], [0, 0, 0], aux=[h], aux_offs=[0], split=hd)
+        dh = torch.randn(B, H, W, hd, device=DEV, generator=torch.Generator(DEV).manual_seed(7))
+        dx = torch.empty(B, H, W, 128, device=DEV)
+        torch.ops.raft_amd.conv_dgrad_(
+            [g], [0], [2 * hd], wd, 1, 5, 0, 2, 0, 1.0, [dh, dx], [0, 0], [hd, 128], [hd, 128],
+            [1, 0], [dh, dx], [0, 0], [], [])
+        torch.cuda.synchronize()
+        return z.float(), rh.float(), r.float(), dh, dx
+
+    want = run()
+    torch.ops.raft_amd.conv_set_forced_cfg(cfg)
+    try:
+        got = run()
+    finally:
+        torch.ops.raft_amd.conv_set_forced_cfg(-1)
+    for name, a_, b_ in zip(('z', 'rh', 'r', 'dh', 'dx'), got, want):
+        torch.testing.assert_close(a_, b_, atol=2e-2, rtol=1e-2, msg=lambda m: name + ': ' + m)
