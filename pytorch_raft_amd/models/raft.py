@@ -38,6 +38,7 @@ from .corr import CorrBlock, AlternateCorrBlock
 from ..utils.utils import coords_grid, upflow8
 from ..ops.upsample import convex_upsample
 from ..ops import _ext
+from ..ops import conv_fp32
 
 
 def _get(args, name, default):
@@ -175,11 +176,12 @@ class RAFT(nn.Module):
 
         flow_predictions = []
         flow_up = None
+        fp32_mfma = self._use_fp32_mfma(fmap1)
         for itr in range(iters):
             coords1 = coords1.detach()
             corr = corr_fn(coords1)
             flow = coords1 - coords0
-            with self._autocast(dev):
+            with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
                 net, up_mask, delta_flow = self.update_block(net, inp, corr, flow)
             coords1 = coords1 + delta_flow
             if test_mode and itr < iters - 1:
@@ -212,6 +214,13 @@ class RAFT(nn.Module):
                 bool(self.args.mixed_precision) and _ext.device_ok(fmap))
 
     # ------------------------------------------------------------------ fused HIP update path
+    def _use_fp32_mfma(self, img):
+        """fp32 model on a GPU: the update-block convs run as split-bf16 MFMA convs
+        (ops/conv_fp32.py, ~2^-16 relative to fp32) instead of MIOpen fp32 convs."""
+        impl = _get(self.args, 'update_impl', 'auto')
+        return (impl != 'torch' and self.corr_impl != 'torch' and not self.args.mixed_precision
+                and _ext.device_ok(img) and _ext.gpu_path_enabled())
+
     def _use_fused_update(self, img):
         """Fused MFMA update block (full and small model): GPU, bf16 mixed precision (its
         compute dtype)."""

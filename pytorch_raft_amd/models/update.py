@@ -23,6 +23,19 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 
+class MfmaConv2d(nn.Conv2d):
+    """nn.Conv2d (same parameters and state-dict keys) whose fp32 GPU forward runs on the bf16
+    MFMA conv kernels as a split-bf16 product (``ops/conv_fp32.py``) while an fp32 model's update
+    block is active (``conv_fp32.enabled()``); everything else is the plain nn.Conv2d path."""
+
+    def forward(self, x):
+        from ..ops import conv_fp32
+        if (conv_fp32.active_for(x, self.weight) and self.stride == (1, 1) and
+                self.dilation == (1, 1) and self.groups == 1 and self.padding_mode == 'zeros'):
+            return conv_fp32.conv2d(x, self.weight, self.bias, self.padding)
+        return super().forward(x)
+
+
 def _gru_gate_update(h, z, q):
     # h' = (1-z) h + z q  written as one lerp (same value, one fewer temporary)
     return torch.lerp(h, q, z)
@@ -31,8 +44,8 @@ def _gru_gate_update(h, z, q):
 class FlowHead(nn.Module):
     def __init__(self, input_dim=128, hidden_dim=256):
         super().__init__()
-        self.conv1 = nn.Conv2d(input_dim, hidden_dim, 3, padding=1)
-        self.conv2 = nn.Conv2d(hidden_dim, 2, 3, padding=1)
+        self.conv1 = MfmaConv2d(input_dim, hidden_dim, 3, padding=1)
+        self.conv2 = MfmaConv2d(hidden_dim, 2, 3, padding=1)
         self.relu = nn.ReLU(inplace=True)
 
     def forward(self, x):
@@ -45,9 +58,9 @@ class ConvGRU(nn.Module):
     def __init__(self, hidden_dim=128, input_dim=192 + 128):
         super().__init__()
         cin = hidden_dim + input_dim
-        self.convz = nn.Conv2d(cin, hidden_dim, 3, padding=1)
-        self.convr = nn.Conv2d(cin, hidden_dim, 3, padding=1)
-        self.convq = nn.Conv2d(cin, hidden_dim, 3, padding=1)
+        self.convz = MfmaConv2d(cin, hidden_dim, 3, padding=1)
+        self.convr = MfmaConv2d(cin, hidden_dim, 3, padding=1)
+        self.convq = MfmaConv2d(cin, hidden_dim, 3, padding=1)
 
     def forward(self, h, x):
         hx = torch.cat([h, x], dim=1)
@@ -63,12 +76,12 @@ class SepConvGRU(nn.Module):
     def __init__(self, hidden_dim=128, input_dim=192 + 128):
         super().__init__()
         cin = hidden_dim + input_dim
-        self.convz1 = nn.Conv2d(cin, hidden_dim, (1, 5), padding=(0, 2))
-        self.convr1 = nn.Conv2d(cin, hidden_dim, (1, 5), padding=(0, 2))
-        self.convq1 = nn.Conv2d(cin, hidden_dim, (1, 5), padding=(0, 2))
-        self.convz2 = nn.Conv2d(cin, hidden_dim, (5, 1), padding=(2, 0))
-        self.convr2 = nn.Conv2d(cin, hidden_dim, (5, 1), padding=(2, 0))
-        self.convq2 = nn.Conv2d(cin, hidden_dim, (5, 1), padding=(2, 0))
+        self.convz1 = MfmaConv2d(cin, hidden_dim, (1, 5), padding=(0, 2))
+        self.convr1 = MfmaConv2d(cin, hidden_dim, (1, 5), padding=(0, 2))
+        self.convq1 = MfmaConv2d(cin, hidden_dim, (1, 5), padding=(0, 2))
+        self.convz2 = MfmaConv2d(cin, hidden_dim, (5, 1), padding=(2, 0))
+        self.convr2 = MfmaConv2d(cin, hidden_dim, (5, 1), padding=(2, 0))
+        self.convq2 = MfmaConv2d(cin, hidden_dim, (5, 1), padding=(2, 0))
 
     @staticmethod
     def _half_step(h, x, cz, cr, cq):
@@ -88,10 +101,10 @@ class SmallMotionEncoder(nn.Module):
     def __init__(self, args):
         super().__init__()
         cor_planes = args.corr_levels * (2 * args.corr_radius + 1) ** 2
-        self.convc1 = nn.Conv2d(cor_planes, 96, 1, padding=0)
-        self.convf1 = nn.Conv2d(2, 64, 7, padding=3)
-        self.convf2 = nn.Conv2d(64, 32, 3, padding=1)
-        self.conv = nn.Conv2d(128, 80, 3, padding=1)
+        self.convc1 = MfmaConv2d(cor_planes, 96, 1, padding=0)
+        self.convf1 = MfmaConv2d(2, 64, 7, padding=3)
+        self.convf2 = MfmaConv2d(64, 32, 3, padding=1)
+        self.conv = MfmaConv2d(128, 80, 3, padding=1)
 
     def forward(self, flow, corr):
         cor = F.relu(self.convc1(corr))
@@ -104,11 +117,11 @@ class BasicMotionEncoder(nn.Module):
     def __init__(self, args):
         super().__init__()
         cor_planes = args.corr_levels * (2 * args.corr_radius + 1) ** 2
-        self.convc1 = nn.Conv2d(cor_planes, 256, 1, padding=0)
-        self.convc2 = nn.Conv2d(256, 192, 3, padding=1)
-        self.convf1 = nn.Conv2d(2, 128, 7, padding=3)
-        self.convf2 = nn.Conv2d(128, 64, 3, padding=1)
-        self.conv = nn.Conv2d(64 + 192, 128 - 2, 3, padding=1)
+        self.convc1 = MfmaConv2d(cor_planes, 256, 1, padding=0)
+        self.convc2 = MfmaConv2d(256, 192, 3, padding=1)
+        self.convf1 = MfmaConv2d(2, 128, 7, padding=3)
+        self.convf2 = MfmaConv2d(128, 64, 3, padding=1)
+        self.conv = MfmaConv2d(64 + 192, 128 - 2, 3, padding=1)
 
     def forward(self, flow, corr):
         cor = F.relu(self.convc2(F.relu(self.convc1(corr))))
@@ -140,9 +153,9 @@ class BasicUpdateBlock(nn.Module):
         self.gru = SepConvGRU(hidden_dim=hidden_dim, input_dim=128 + hidden_dim)
         self.flow_head = FlowHead(hidden_dim, hidden_dim=256)
         self.mask = nn.Sequential(
-            nn.Conv2d(128, 256, 3, padding=1),
+            MfmaConv2d(128, 256, 3, padding=1),
             nn.ReLU(inplace=True),
-            nn.Conv2d(256, 64 * 9, 1, padding=0))
+            MfmaConv2d(256, 64 * 9, 1, padding=0))
 
     def forward(self, net, inp, corr, flow, upsample=True):
         motion = self.encoder(flow, corr)

@@ -1,0 +1,118 @@
+"""fp32 convolutions of the update block on the bf16 MFMA kernels (split-bf16, 3 products).
+
+The reference's paper schedule trains in fp32 (`train_standard.sh`, no `--mixed_precision`):
+every update-block conv (`core/update.py`) is then an fp32 NCHW conv.  gfx950's matrix cores
+have no fast fp32 path (the fp32 MFMA rate is 1/8 of bf16), so an fp32 operand is carried as
+an exact-to-2^-16 pair ``x = x_hi + x_lo`` of bf16 values and the conv as three bf16 products
+
+    conv(x, w) ~= conv(x_hi, w_hi) + conv(x_lo, w_hi) + conv(x_hi, w_lo)      (fp32 accumulation)
+
+(the dropped ``x_lo * w_lo`` term and the bf16 rounding of the residuals are ~2^-16 relative,
+the same scheme the fp32 correlation kernels use).  The three products are ONE launch of the
+implicit-GEMM conv kernel: the input buffer is NHWC ``[x_hi | x_lo]`` (each half padded to a
+multiple of 64 channels), read as the virtual concat ``[x_hi, x_lo, x_hi]`` against packed
+weights ``[w_hi, w_hi, w_lo]``.  The input gradient is the same construction on the split
+output gradient and the flipped / transposed weights; the weight gradient is two launches of the
+weight-gradient kernel (``g_hi x [x_hi | x_lo]`` and ``g_lo x x_hi``).
+
+Used by :class:`pytorch_raft_amd.models.update.MfmaConv2d` (every update-block conv with >= 32
+input channels) while an fp32 model runs on a GPU; bf16 autocast takes the fused update block.
+"""
+import contextlib
+import os
+
+import torch
+
+from . import _ext
+from . import conv as C
+
+_ACTIVE = {'on': False}
+# RAFT_FP32_MFMA=0: fp32 models keep MIOpen fp32 convs in the update block (A/B measurements)
+_ENV_ON = os.environ.get('RAFT_FP32_MFMA', '1') != '0'
+
+
+@contextlib.contextmanager
+def enabled(on=True):
+    """Route MfmaConv2d modules through the split-bf16 MFMA conv inside the block."""
+    prev = _ACTIVE['on']
+    _ACTIVE['on'] = bool(on)
+    try:
+        yield
+    finally:
+        _ACTIVE['on'] = prev
+
+
+def active_for(x, weight):
+    return (_ACTIVE['on'] and _ENV_ON and x.is_cuda and x.dtype == torch.float32 and
+            weight.dtype == torch.float32 and x.dim() == 4 and weight.shape[1] >= 32 and
+            not torch.is_autocast_enabled())
+
+
+def _split_nhwc(x, cpad):
+    """(B, C, H, W) fp32 -> (B, H, W, 2 cpad) bf16 [hi | lo] (zero padded)."""
+    b, c, h, w = x.shape
+    xn = x.permute(0, 2, 3, 1)
+    hi = xn.to(torch.bfloat16)
+    buf = torch.zeros(b, h, w, 2 * cpad, device=x.device, dtype=torch.bfloat16)
+    buf[..., :c] = hi
+    buf[..., cpad:cpad + c] = (xn - hi.float()).to(torch.bfloat16)
+    return buf
+
+
+def _pack3(w, cpad):
+    """(Cout, Cin, kh, kw) fp32 -> packed [w_hi | w_hi | w_lo] over three cpad-wide segments."""
+    cin = w.shape[1]
+    wh = w.to(torch.bfloat16).float()
+    w3 = torch.cat([wh, wh, w - wh], dim=1)
+    return C.pack_weight(w3, [cin] * 3, [cpad] * 3)
+
+
+class _SplitConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, pad):
+        x = x.contiguous()
+        b, cin, h, w = x.shape
+        cout, _, kh, kw = weight.shape
+        cp = C.round_up(cin, 64)
+        xs = _split_nhwc(x, cp)
+        out = torch.empty(b, cout, h, w, device=x.device, dtype=torch.float32)
+        C.conv_fwd([(xs, 0, cp), (xs, cp, cp), (xs, 0, cp)], _pack3(weight, cp),
+                   None if bias is None else bias.contiguous(), (kh, kw), pad, cout,
+                   C.EPI_F32_NCHW, [out], [0])
+        ctx.save_for_backward(xs, weight)
+        ctx.pad, ctx.cin, ctx.has_bias = pad, cin, bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        xs, weight = ctx.saved_tensors
+        g = g.contiguous()
+        b, cout, h, w = g.shape
+        cin, pad = ctx.cin, ctx.pad
+        _, _, kh, kw = weight.shape
+        cp = xs.shape[-1] // 2
+        cop = C.round_up(cout, 64)
+        gs = _split_nhwc(g, cop)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wt = weight.flip(2, 3).transpose(0, 1).contiguous()   # adjoint: (Cin, Cout, kh, kw)
+            dx = torch.empty(b, cin, h, w, device=g.device, dtype=torch.float32)
+            C.conv_fwd([(gs, 0, cop), (gs, cop, cop), (gs, 0, cop)], _pack3(wt, cop), None,
+                       (kh, kw), pad, cin, C.EPI_F32_NCHW, [dx], [0])
+        if ctx.needs_input_grad[1]:
+            k = kh * kw
+            d1 = torch.zeros(cout, k * 2 * cp, device=g.device)    # g_hi x [x_hi | x_lo]
+            C.conv_wgrad(gs, 0, [(xs, 0, cp), (xs, cp, cp)], (kh, kw), pad, cout, d1)
+            d2 = torch.zeros(cout, k * cp, device=g.device)        # g_lo x x_hi
+            C.conv_wgrad(gs, cop, [(xs, 0, cp)], (kh, kw), pad, cout, d2)
+            g1 = C.unpack_weight_grad(d1, cout, [cin, cin], [cp, cp], (kh, kw))
+            dw = g1[:, :cin] + g1[:, cin:] + C.unpack_weight_grad(d2, cout, [cin], [cp], (kh, kw))
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = g.sum((0, 2, 3))
+        return dx, dw, db, None
+
+
+def conv2d(x, weight, bias, padding):
+    """fp32 conv2d (stride 1, 'same'-style padding) on the split-bf16 MFMA kernels."""
+    _ext.gpu_path_enabled(required=True)
+    return _SplitConv.apply(x, weight, bias, tuple(int(p) for p in padding))
