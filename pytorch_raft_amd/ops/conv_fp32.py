@@ -15,8 +15,10 @@ weights ``[w_hi, w_hi, w_lo]``.  The input gradient is the same construction on 
 output gradient and the flipped / transposed weights; the weight gradient is two launches of the
 weight-gradient kernel (``g_hi x [x_hi | x_lo]`` and ``g_lo x x_hi``).
 
-Used by :class:`pytorch_raft_amd.models.update.MfmaConv2d` (every update-block conv with >= 32
-input channels) while an fp32 model runs on a GPU; bf16 autocast takes the fused update block.
+Used by :class:`pytorch_raft_amd.models.update.MfmaConv2d` (every update-block conv; convf1's 2
+input channels ride in a 64-channel slot) while an fp32 model runs on a GPU, so the decode of an
+fp32 step has no MIOpen call left and is captured in the training hipGraph like the bf16 one;
+bf16 autocast takes the fused update block.
 """
 import contextlib
 import os
@@ -44,8 +46,7 @@ def enabled(on=True):
 
 def active_for(x, weight):
     return (_ACTIVE['on'] and _ENV_ON and x.is_cuda and x.dtype == torch.float32 and
-            weight.dtype == torch.float32 and x.dim() == 4 and weight.shape[1] >= 32 and
-            not torch.is_autocast_enabled())
+            weight.dtype == torch.float32 and x.dim() == 4 and not torch.is_autocast_enabled())
 
 
 def _split_nhwc(x, cpad):

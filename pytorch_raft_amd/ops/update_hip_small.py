@@ -31,16 +31,24 @@ from .update_hip import _LayerSpec, Design, _UpdateWeights, _State, _bf16, _f32
 HDP = 128        # padded hidden width (96 real)
 CORR_BUF_SMALL = 256  # 196 lookup taps zero-padded to a multiple of the K step
 
+_HM_S = [(0, 96), (160, 82)]   # [h | mf] input channels of the small ConvGRU's module weights
+_CTX_S = [(96, 64)]            # its context (inp) channels
+
 SMALL_SPECS = [
     _LayerSpec('c1', 96, (1, 1), [196], [CORR_BUF_SMALL], adj_pad=128),
     _LayerSpec('f1', 64, (7, 7), [2], [8], small=True, patch=True),
     _LayerSpec('f2', 32, (3, 3), [64], [64], adj_pad=64, adj_off=32),
     _LayerSpec('conv', 80, (3, 3), [128], [128], adj_pad=128),
-    _LayerSpec('zr', 256, (3, 3), [96, 64, 82], [HDP, 64, 128], row_pad=HDP),
-    _LayerSpec('q', 128, (3, 3), [96, 64, 82], [HDP, 64, 128], row_pad=HDP),
+    # ConvGRU over [h | inp | mf]: per iteration [h | mf]; the context part (inp, the same in
+    # every iteration) runs once per forward / backward as '<name>i' (see ops/update_hip.py)
+    _LayerSpec('zr', 256, (3, 3), [96, 82], [HDP, 128], row_pad=HDP, in_sel=_HM_S, no_bias=True),
+    _LayerSpec('q', 128, (3, 3), [96, 82], [HDP, 128], row_pad=HDP, in_sel=_HM_S, no_bias=True),
     _LayerSpec('fh1', 128, (3, 3), [96], [HDP]),
     _LayerSpec('fh2', 2, (3, 3), [128], [128], adj_pad=64),
+    _LayerSpec('zri', 256, (3, 3), [64], [64], row_pad=HDP, in_sel=_CTX_S),
+    _LayerSpec('qi', 128, (3, 3), [64], [64], row_pad=HDP, in_sel=_CTX_S),
 ]
+GRU_S = ('zr', 'q')
 
 
 def small_module_params(ub):
@@ -52,6 +60,8 @@ def small_module_params(ub):
         'conv': [(e.conv.weight, e.conv.bias)],
         'zr': [(g.convz.weight, g.convz.bias), (g.convr.weight, g.convr.bias)],
         'q': [(g.convq.weight, g.convq.bias)],
+        'zri': [(g.convz.weight, g.convz.bias), (g.convr.weight, g.convr.bias)],
+        'qi': [(g.convq.weight, g.convq.bias)],
         'fh1': [(fh.conv1.weight, fh.conv1.bias)],
         'fh2': [(fh.conv2.weight, fh.conv2.bias)],
     }
@@ -64,11 +74,29 @@ def _zeros_bf16(shape, dev):
     return torch.zeros(*shape, device=dev, dtype=torch.bfloat16)
 
 
-def _conv(pk, name, segs, epi, outs, offs, aux=(), aux_offs=(), split=0):
+def _conv(pk, name, segs, epi, outs, offs, aux=(), aux_offs=(), split=0, bias=None):
     s = SMALL.spec[name]
     k, pad, small = ((1, 1), (0, 0), False) if s.patch else (s.k, s.pad, s.small)
-    C.conv_fwd(segs, pk.w[name], pk.b[name], k, pad, s.cout, epi, outs, offs, aux, aux_offs,
-               scale=s.scale, split=split, cin_small=2 if small else 0)
+    C.conv_fwd(segs, pk.w[name], pk.b[name] if bias is None else bias, k, pad, s.cout, epi, outs,
+               offs, aux, aux_offs, scale=s.scale, split=split, cin_small=2 if small else 0)
+
+
+def _ctx_maps(pk, inp):
+    """conv(inp, W_inp) + bias of the ConvGRU convs, fp32 (B,H,W,cout), once per forward pass."""
+    key = (inp.data_ptr(), tuple(inp.shape), inp._version)
+    if pk.ctx is not None:
+        if key != pk.ctx_key:
+            raise RuntimeError('fused update block: every iteration of a forward pass must take '
+                               'the same context tensor')
+        return pk.ctx
+    b, h, w, _ = inp.shape
+    pk.ctx = {}
+    for name in GRU_S:
+        m = torch.empty(b, h, w, SMALL.spec[name + 'i'].cout, device=inp.device, dtype=torch.float32)
+        _conv(pk, name + 'i', [(inp, 0, 64)], C.EPI_F32, [m], [0])
+        pk.ctx[name] = m
+    pk.ctx_key = key
+    return pk.ctx
 
 
 def _iter_forward(pk, h, inp, corr, flow):
@@ -88,11 +116,12 @@ def _iter_forward(pk, h, inp, corr, flow):
     _conv(pk, 'f2', [(f1, 0, 64)], C.EPI_RELU_BF16, [cf], [96])
     _conv(pk, 'conv', [(cf, 0, 128)], C.EPI_RELU_BF16, [mf], [0])
     z, rh, r = _bf16(sh + (HDP,), dev), _bf16(sh + (HDP,), dev), _bf16(sh + (HDP,), dev)
-    segs = [(h, 0, HDP), (inp, 0, 64), (mf, 0, 128)]
-    _conv(pk, 'zr', segs, C.EPI_GRU_ZR, [z, rh, r], [0, 0, 0], aux=[h], aux_offs=[0], split=HDP)
+    ctx = _ctx_maps(pk, inp)
+    _conv(pk, 'zr', [(h, 0, HDP), (mf, 0, 128)], C.EPI_GRU_ZR, [z, rh, r], [0, 0, 0], aux=[h],
+          aux_offs=[0], split=HDP, bias=ctx['zr'])
     hn, q = _bf16(sh + (HDP,), dev), _bf16(sh + (HDP,), dev)
-    _conv(pk, 'q', [(rh, 0, HDP), (inp, 0, 64), (mf, 0, 128)], C.EPI_GRU_Q, [hn, q], [0, 0],
-          aux=[h, z], aux_offs=[0, 0])
+    _conv(pk, 'q', [(rh, 0, HDP), (mf, 0, 128)], C.EPI_GRU_Q, [hn, q], [0, 0],
+          aux=[h, z], aux_offs=[0, 0], bias=ctx['q'])
     fm = _bf16(sh + (128,), dev)
     _conv(pk, 'fh1', [(hn, 0, HDP)], C.EPI_RELU_BF16, [fm], [0])
     delta = torch.empty(B, 2, H, W, device=dev, dtype=torch.float32)
@@ -147,25 +176,22 @@ class _SmallUpdateIter(torch.autograd.Function):
         pk.defer_wgrad('fh1', dpre_fm, 0, [(hn, 0, HDP)])
         dh = gh.float().contiguous() if gh is not None else _f32(sh + (HDP,), dev, zero=True)
         dgrad('fh1', [(dpre_fm, 0, 128)], [(dh, 0, HDP, 96, 1)])
-        # ---- ConvGRU (pads: every gradient buffer is zero beyond the 96 real channels)
-        acc_inp = st.dinp_acc is not None
-        if not acc_inp:
-            st.dinp_acc = _f32(sh + (64,), dev)
-        dinp = st.dinp_acc
+        # ---- ConvGRU (pads: every gradient buffer is zero beyond the 96 real channels); the
+        # context part's input / weight gradients come once from the summed gradients (below)
         dmf = _f32(sh + (128,), dev, zero=True)
         dpre_q = _bf16(sh + (HDP,), dev)
         dz = _f32(sh + (HDP,), dev)
         dhp = _f32(sh + (HDP,), dev)
         ops.gru_q_bwd_(dh, z, q, h, dpre_q, dz, dhp)
-        pk.defer_wgrad('q', dpre_q, 0, [(rh, 0, HDP), (inp, 0, 64), (mf, 0, 128)])
+        pk.defer_wgrad('q', dpre_q, 0, [(rh, 0, HDP), (mf, 0, 128)])
         drh = _f32(sh + (HDP,), dev, zero=True)
-        dgrad('q', [(dpre_q, 0, HDP)],
-              [(drh, 0, HDP, 96, 0), (dinp, 0, 64, 64, int(acc_inp)), (dmf, 0, 128, 82, 1)])
+        dgrad('q', [(dpre_q, 0, HDP)], [(drh, 0, HDP, 96, 0), (dmf, 0, 128, 82, 1)])
         dpre_zr = _bf16(sh + (2 * HDP,), dev)
         ops.gru_zr_bwd_(drh, dz, z, r, h, dpre_zr, dhp)
-        pk.defer_wgrad('zr', dpre_zr, 0, [(h, 0, HDP), (inp, 0, 64), (mf, 0, 128)])
-        dgrad('zr', [(dpre_zr, 0, 2 * HDP)],
-              [(dhp, 0, HDP, 96, 1), (dinp, 0, 64, 64, 1), (dmf, 0, 128, 82, 1)])
+        pk.defer_wgrad('zr', dpre_zr, 0, [(h, 0, HDP), (mf, 0, 128)])
+        dgrad('zr', [(dpre_zr, 0, 2 * HDP)], [(dhp, 0, HDP, 96, 1), (dmf, 0, 128, 82, 1)])
+        st.ctx_g.setdefault('q', []).append(dpre_q)
+        st.ctx_g.setdefault('zr', []).append(dpre_zr)
         # ---- motion encoder
         dpre_conv = _zeros_bf16(sh + (128,), dev)
         ops.relu_bwd_(dmf, 0, mf, 0, dpre_conv, 0, 80, 1.0)
@@ -181,11 +207,15 @@ class _SmallUpdateIter(torch.autograd.Function):
         pk.defer_wgrad('f1', dpre_f1, 0, [(patch, 0, 128)])
         dcorr = _bf16(sh + (CORR_BUF_SMALL,), dev)
         dgrad('c1', [(dpre_cf, 0, 128)], [(dcorr, 0, CORR_BUF_SMALL, 196, 0)])
+        dinp = None
         if ctx.itr == 0:
-            st.dinp_acc = None
+            dinp = _f32(sh + (64,), dev)
+            for j, name in enumerate(GRU_S):
+                gsum = _UH._sum_bf16(st.ctx_g.pop(name))
+                dgrad(name + 'i', [(gsum, 0, gsum.shape[-1])], [(dinp, 0, 64, 64, int(j > 0))])
+                pk.defer_wgrad(name + 'i', gsum, 0, [(inp, 0, 64)])
+            st.ctx_g = {}
             st.next_bwd = None
-        else:
-            dinp = None
         return (None, dhp, dinp, dcorr, None, None)
 
 

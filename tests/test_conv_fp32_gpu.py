@@ -19,7 +19,7 @@ def _rel(a, b):
 
 @pytest.mark.parametrize('cin,cout,k', [
     (384, 256, (1, 5)), (384, 128, (5, 1)), (256, 192, (3, 3)), (128, 64, (3, 3)),
-    (324, 256, (1, 1)), (256, 2, (3, 3)), (256, 576, (1, 1)), (146, 96, (3, 3)),
+    (324, 256, (1, 1)), (256, 2, (3, 3)), (256, 576, (1, 1)), (146, 96, (3, 3)), (2, 128, (7, 7)),
 ])
 def test_split_bf16_conv_matches_fp64(ext_ops, cin, cout, k):
     torch.manual_seed(0)

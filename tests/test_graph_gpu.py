@@ -30,27 +30,28 @@ def _model(args, dev, sd=None):
     return m
 
 
-@pytest.mark.parametrize('alt', [False, True])
-def test_graph_step_matches_eager(ext_ops, alt):
+@pytest.mark.parametrize('alt,mixed', [(False, True), (True, True), (False, False)])
+def test_graph_step_matches_eager(ext_ops, alt, mixed):
+    """bf16 (fused update block) and fp32 (split-bf16 MFMA update-block convs) steps."""
     from pytorch_raft_amd.engine.trainer import TrainState, GraphedTrainStep
     from pytorch_raft_amd.data.synthetic import device_batches
     dev = torch.device('cuda', 0)
-    args = _args(alternate_corr=alt)
+    args = _args(alternate_corr=alt, mixed_precision=mixed)
     m = _model(args, dev)
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     batches = device_batches(4, 128, 192, dev, count=3, seed=3)
 
     def eager_run():
-        mm = _model(_args(alternate_corr=alt), dev, sd)
-        st = TrainState(mm, _args(alternate_corr=alt), dev)
+        mm = _model(_args(alternate_corr=alt, mixed_precision=mixed), dev, sd)
+        st = TrainState(mm, _args(alternate_corr=alt, mixed_precision=mixed), dev)
         losses = [float(st.step(*batches[k])[0].detach()) for k in range(3)]
         return losses, torch.cat([p.detach().reshape(-1) for p in mm.parameters()]), st
 
     eager, w_e1, st = eager_run()
     _, w_e2, _ = eager_run()   # run-to-run noise of the eager step (MIOpen atomics, bf16)
 
-    m2 = _model(_args(alternate_corr=alt), dev, sd)
-    st2 = TrainState(m2, _args(alternate_corr=alt), dev, graph_ready=True)
+    m2 = _model(_args(alternate_corr=alt, mixed_precision=mixed), dev, sd)
+    st2 = TrainState(m2, _args(alternate_corr=alt, mixed_precision=mixed), dev, graph_ready=True)
     g = GraphedTrainStep(st2, batches[0], warmup=2)
     # roll-back: weights are the initial ones again
     for n, p in m2.named_parameters():
