@@ -174,14 +174,20 @@ class RAFT(nn.Module):
         if self._use_fused_update(fmap1):
             return self._iterate_fused(net, inp, corr_fn, coords0, coords1, iters, test_mode)
 
+        # fp32 model: split-bf16 MFMA update-block convs for this decode (the iterations share the
+        # packed split weights)
+        with conv_fp32.enabled(self._use_fp32_mfma(fmap1)):
+            return self._iterate_eager(net, inp, corr_fn, coords0, coords1, iters, test_mode)
+
+    def _iterate_eager(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
+        dev = coords0.device
         flow_predictions = []
         flow_up = None
-        fp32_mfma = self._use_fp32_mfma(fmap1)
         for itr in range(iters):
             coords1 = coords1.detach()
             corr = corr_fn(coords1)
             flow = coords1 - coords0
-            with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
+            with self._autocast(dev):
                 net, up_mask, delta_flow = self.update_block(net, inp, corr, flow)
             coords1 = coords1 + delta_flow
             if test_mode and itr < iters - 1:

@@ -33,11 +33,17 @@ _ACTIVE = {'on': False}
 _ENV_ON = os.environ.get('RAFT_FP32_MFMA', '1') != '0'
 
 
+# packed [w_hi | w_hi | w_lo] weights of the current decode (forward and adjoint), keyed by the
+# parameter storage and version: the 12 iterations share them; cleared when a decode begins
+_PACKED = {}
+
+
 @contextlib.contextmanager
 def enabled(on=True):
-    """Route MfmaConv2d modules through the split-bf16 MFMA conv inside the block."""
+    """Route MfmaConv2d modules through the split-bf16 MFMA conv inside the block (one decode)."""
     prev = _ACTIVE['on']
     _ACTIVE['on'] = bool(on)
+    _PACKED.clear()
     try:
         yield
     finally:
@@ -68,6 +74,26 @@ def _pack3(w, cpad):
     return C.pack_weight(w3, [cin] * 3, [cpad] * 3)
 
 
+def _wgrad(gs, g_off, xs, offs, cnts, k, pad, cout, dw):
+    """dw += weight gradient: the tap-fused kernel (the fused block's) where it applies (1x1,
+    3x3, 1x5, 5x1), the tile kernel otherwise (convf1's 7x7)."""
+    if C._taps_ok(offs, cnts, k):
+        C.conv_wgrad_multi([(gs, [xs] * len(offs))], g_off, offs, cnts, k, pad, cout, dw)
+    else:
+        C.conv_wgrad(gs, g_off, [(xs, o, c) for o, c in zip(offs, cnts)], k, pad, cout, dw)
+
+
+def _packed(weight, cpad, adjoint):
+    key = (weight.data_ptr(), weight._version, tuple(weight.shape), cpad, adjoint)
+    w = _PACKED.get(key)
+    if w is None:
+        src = weight.detach()
+        if adjoint:
+            src = src.flip(2, 3).transpose(0, 1).contiguous()   # (Cin, Cout, kh, kw)
+        w = _PACKED[key] = _pack3(src, cpad)
+    return w
+
+
 class _SplitConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, pad):
@@ -77,7 +103,7 @@ class _SplitConv(torch.autograd.Function):
         cp = C.round_up(cin, 64)
         xs = _split_nhwc(x, cp)
         out = torch.empty(b, cout, h, w, device=x.device, dtype=torch.float32)
-        C.conv_fwd([(xs, 0, cp), (xs, cp, cp), (xs, 0, cp)], _pack3(weight, cp),
+        C.conv_fwd([(xs, 0, cp), (xs, cp, cp), (xs, 0, cp)], _packed(weight, cp, False),
                    None if bias is None else bias.contiguous(), (kh, kw), pad, cout,
                    C.EPI_F32_NCHW, [out], [0])
         ctx.save_for_backward(xs, weight)
@@ -96,16 +122,15 @@ class _SplitConv(torch.autograd.Function):
         gs = _split_nhwc(g, cop)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            wt = weight.flip(2, 3).transpose(0, 1).contiguous()   # adjoint: (Cin, Cout, kh, kw)
             dx = torch.empty(b, cin, h, w, device=g.device, dtype=torch.float32)
-            C.conv_fwd([(gs, 0, cop), (gs, cop, cop), (gs, 0, cop)], _pack3(wt, cop), None,
+            C.conv_fwd([(gs, 0, cop), (gs, cop, cop), (gs, 0, cop)], _packed(weight, cop, True), None,
                        (kh, kw), pad, cin, C.EPI_F32_NCHW, [dx], [0])
         if ctx.needs_input_grad[1]:
             k = kh * kw
             d1 = torch.zeros(cout, k * 2 * cp, device=g.device)    # g_hi x [x_hi | x_lo]
-            C.conv_wgrad(gs, 0, [(xs, 0, cp), (xs, cp, cp)], (kh, kw), pad, cout, d1)
+            _wgrad(gs, 0, xs, [0, cp], [cp, cp], (kh, kw), pad, cout, d1)
             d2 = torch.zeros(cout, k * cp, device=g.device)        # g_lo x x_hi
-            C.conv_wgrad(gs, cop, [(xs, 0, cp)], (kh, kw), pad, cout, d2)
+            _wgrad(gs, cop, xs, [0], [cp], (kh, kw), pad, cout, d2)
             g1 = C.unpack_weight_grad(d1, cout, [cin, cin], [cp, cp], (kh, kw))
             dw = g1[:, :cin] + g1[:, cin:] + C.unpack_weight_grad(d2, cout, [cin], [cp], (kh, kw))
         if ctx.has_bias and ctx.needs_input_grad[2]:
