@@ -24,9 +24,12 @@ sys.path.insert(0, HERE)
 
 METRIC = ('training image-pairs/sec (whole node), RAFT FlyingChairs 368x496 iters=12, '
           'at 1/2/4/8 MI355X')
-# stock PyTorch-ROCm execution of the reference semantics on one MI355X (bf16
-# autocast, batch 12, 10 warm-up / 50 timed steps) -- scaled ideally to N GPUs for vs_baseline
-STOCK_BF16_PAIRS_PER_GPU = 113.19
+# stock PyTorch-ROCm execution of the reference semantics on one MI355X (batch 12,
+# 368x496, iters 12, 10 warm-up / 50 timed steps), per compute dtype -- scaled ideally to N GPUs
+# for vs_baseline.  A run is compared only with the stock run of ITS dtype at the headline
+# config (per-GPU batch 12); any other config reports vs_baseline = null.
+STOCK_PAIRS_PER_GPU = {'bf16': 113.19, 'fp32': 66.85}
+HEADLINE_BATCH = 12
 
 
 def parse(argv=None):
@@ -232,6 +235,16 @@ def main(argv=None):
     if (h, w) != (368, 496) or a.iters != 12 or a.small:
         metric = 'training image-pairs/sec (whole node), RAFT%s %dx%d iters=%d, at %d MI355X' % (
             '-small' if a.small else '', h, w, a.iters, world)
+    extra = []
+    if a.precision != 'bf16':
+        extra.append(a.precision)
+    if a.batch != HEADLINE_BATCH:
+        extra.append('per-GPU batch %d' % a.batch)
+    if extra:
+        metric += ' [%s]' % ', '.join(extra)
+    base = STOCK_PAIRS_PER_GPU.get(a.precision)
+    headline = ((h, w) == (368, 496) and a.iters == 12 and not a.small
+                and a.batch == HEADLINE_BATCH and base is not None)
     res = {
         'metric': metric,
         'value': round(value, 3),
@@ -242,8 +255,7 @@ def main(argv=None):
         'ms_per_step': round(1000.0 * elapsed / a.steps, 3),
         'higher_is_better': True,
         'scaling': 'weak',
-        'vs_baseline': (round(value / (STOCK_BF16_PAIRS_PER_GPU * world), 3)
-                        if metric == METRIC else None),
+        'vs_baseline': round(value / (base * world), 3) if headline else None,
         'dtype': a.precision,
         'data': 'synthetic (random smooth texture pairs, %dx%d, generated on device; random-init weights)' % (h, w),
         'config': {

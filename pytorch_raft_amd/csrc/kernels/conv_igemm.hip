@@ -385,6 +385,34 @@ std::mutex g_tune_mu;
 float* g_scratch = nullptr;
 size_t g_scratch_bytes = 0;
 
+// byte range [lo, hi) of a per-pixel NHWC buffer (P rows of `stride` elements of `esz` bytes)
+struct Range { uintptr_t lo, hi; };
+inline Range nhwc_range(const void* p, int P, int stride, int esz) {
+  const uintptr_t lo = (uintptr_t)p;
+  return Range{lo, p ? lo + (uintptr_t)P * (uintptr_t)stride * (uintptr_t)esz : lo};
+}
+inline bool ranges_meet(Range x, Range y) { return x.lo < x.hi && y.lo < y.hi && x.lo < y.hi && y.lo < x.hi; }
+
+bool outputs_overlap_inputs(const ConvFwdArgs& a, int epi) {
+  const int P = a.B * a.H * a.W;
+  const bool f32 = epi == EPI_F32 || epi == EPI_F32_NCHW;
+  Range outs[3] = {nhwc_range(a.out0, P, epi == EPI_F32_NCHW ? a.cout : a.out0_stride, f32 ? 4 : 2),
+                   nhwc_range(a.out1, P, a.out1_stride, 2), nhwc_range(a.out2, P, a.out2_stride, 2)};
+  const int nout = epi == EPI_GRU_ZR ? 3 : (epi == EPI_GRU_Q ? 2 : 1);
+  Range ins[6];
+  int nin = 0;
+  for (int q = 0; q < a.nseg && q < 3; ++q) ins[nin++] = nhwc_range(a.seg[q].ptr, P, a.seg[q].stride, 2);
+  if (epi == EPI_GRU_ZR || epi == EPI_GRU_Q) {
+    ins[nin++] = nhwc_range(a.aux0, P, a.aux0_stride, 2);
+    if (epi == EPI_GRU_Q) ins[nin++] = nhwc_range(a.aux1, P, a.aux1_stride, 2);
+    if (a.bmap) ins[nin++] = nhwc_range(a.bmap, P, a.bmap_stride, 4);
+  }
+  for (int o = 0; o < nout; ++o)
+    for (int i = 0; i < nin; ++i)
+      if (ranges_meet(outs[o], ins[i])) return true;
+  return false;
+}
+
 // Time every allowed config on the real operands (output into a private scratch buffer
 // through the fp32 epilogue) and cache the fastest.  Runs only outside stream capture.
 int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
@@ -402,8 +430,11 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   // store-only epilogues are timed as they will run (the GRU gate epilogues cost registers and
   // bytes the fp32 scratch epilogue does not): their outputs are rewritten by the real launch
   // that follows; accumulating epilogues (ACC_F32, DGRAD) are timed on the fp32 scratch
-  const bool real_epi = epi == EPI_BF16 || epi == EPI_RELU_BF16 || epi == EPI_GRU_ZR ||
-                        epi == EPI_GRU_Q || epi == EPI_F32 || epi == EPI_F32_NCHW;
+  bool real_epi = epi == EPI_BF16 || epi == EPI_RELU_BF16 || epi == EPI_GRU_ZR ||
+                  epi == EPI_GRU_Q || epi == EPI_F32 || epi == EPI_F32_NCHW;
+  // ... but only while no output overlaps an operand the launches read (an in-place GRU state
+  // update, say): repeated candidate launches would then read their own outputs
+  if (real_epi && outputs_overlap_inputs(a, epi)) real_epi = false;
   const ConvFwdArgs& ta = real_epi ? a : t;
   const int te = real_epi ? epi : EPI_F32;
   hipEvent_t e0, e1;

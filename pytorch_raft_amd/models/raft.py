@@ -137,6 +137,10 @@ class RAFT(nn.Module):
         if cl:
             image1 = image1.contiguous(memory_format=torch.channels_last)
             image2 = image2.contiguous(memory_format=torch.channels_last)
+        # corr_impl='torch' = stock reference-semantics ops everywhere (the baseline): no HIP
+        # encoder kernels either
+        native = self.corr_impl != 'torch'
+        self.fnet.allow_native = self.cnet.allow_native = native
         with self._autocast(dev):
             fmap1, fmap2 = self.fnet([image1, image2])
         with self._autocast(dev):

@@ -34,20 +34,22 @@ _ENV_ON = os.environ.get('RAFT_FP32_MFMA', '1') != '0'
 
 
 # packed [w_hi | w_hi | w_lo] weights of the current decode (forward and adjoint), keyed by the
-# parameter storage and version: the 12 iterations share them; cleared when a decode begins
-_PACKED = {}
+# parameter storage and version: the 12 iterations share them.  One dict per decode
+# (``enabled()`` scope), referenced by that decode's autograd nodes: it lives until their
+# backward has run and the graph is freed, never across decodes (no stale pack can be served
+# to a later tensor that reuses a freed weight's storage).
 
 
 @contextlib.contextmanager
 def enabled(on=True):
     """Route MfmaConv2d modules through the split-bf16 MFMA conv inside the block (one decode)."""
-    prev = _ACTIVE['on']
+    prev = _ACTIVE['on'], _ACTIVE.get('packed')
     _ACTIVE['on'] = bool(on)
-    _PACKED.clear()
+    _ACTIVE['packed'] = {}
     try:
         yield
     finally:
-        _ACTIVE['on'] = prev
+        _ACTIVE['on'], _ACTIVE['packed'] = prev
 
 
 def active_for(x, weight):
@@ -83,14 +85,14 @@ def _wgrad(gs, g_off, xs, offs, cnts, k, pad, cout, dw):
         C.conv_wgrad(gs, g_off, [(xs, o, c) for o, c in zip(offs, cnts)], k, pad, cout, dw)
 
 
-def _packed(weight, cpad, adjoint):
+def _packed(cache, weight, cpad, adjoint):
     key = (weight.data_ptr(), weight._version, tuple(weight.shape), cpad, adjoint)
-    w = _PACKED.get(key)
+    w = cache.get(key)
     if w is None:
         src = weight.detach()
         if adjoint:
             src = src.flip(2, 3).transpose(0, 1).contiguous()   # (Cin, Cout, kh, kw)
-        w = _PACKED[key] = _pack3(src, cpad)
+        w = cache[key] = _pack3(src, cpad)
     return w
 
 
@@ -103,7 +105,10 @@ class _SplitConv(torch.autograd.Function):
         cp = C.round_up(cin, 64)
         xs = _split_nhwc(x, cp)
         out = torch.empty(b, cout, h, w, device=x.device, dtype=torch.float32)
-        C.conv_fwd([(xs, 0, cp), (xs, cp, cp), (xs, 0, cp)], _packed(weight, cp, False),
+        cache = _ACTIVE.get('packed')
+        cache = {} if cache is None else cache
+        ctx.packed = cache
+        C.conv_fwd([(xs, 0, cp), (xs, cp, cp), (xs, 0, cp)], _packed(cache, weight, cp, False),
                    None if bias is None else bias.contiguous(), (kh, kw), pad, cout,
                    C.EPI_F32_NCHW, [out], [0])
         ctx.save_for_backward(xs, weight)
@@ -123,7 +128,7 @@ class _SplitConv(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty(b, cin, h, w, device=g.device, dtype=torch.float32)
-            C.conv_fwd([(gs, 0, cop), (gs, cop, cop), (gs, 0, cop)], _packed(weight, cop, True), None,
+            C.conv_fwd([(gs, 0, cop), (gs, cop, cop), (gs, 0, cop)], _packed(ctx.packed, weight, cop, True), None,
                        (kh, kw), pad, cin, C.EPI_F32_NCHW, [dx], [0])
         if ctx.needs_input_grad[1]:
             k = kh * kw

@@ -180,8 +180,15 @@ class AllPairsVolume:
         # per-iteration gathers pull (~0.5 GB fp32 volume at chairs / batch 12)
         self.state.pyr_bf16 = bool(bf16_pyramid) and fmap1.dtype == torch.bfloat16
         self.levels = num_levels
-        self.token = _AllPairsBuild.apply(fmap1.contiguous(), fmap2.contiguous(), num_levels,
-                                          self.state)
+        # bf16 encoder outputs are channels_last: kept as they are, so _nhwc_bf16's permute is
+        # already contiguous (a plain .contiguous() here made an NCHW copy that _nhwc_bf16 then
+        # permuted back: two full copies of each fmap per step)
+        if fmap1.dtype == torch.bfloat16:
+            fmap1 = fmap1.contiguous(memory_format=torch.channels_last)
+            fmap2 = fmap2.contiguous(memory_format=torch.channels_last)
+        else:
+            fmap1, fmap2 = fmap1.contiguous(), fmap2.contiguous()
+        self.token = _AllPairsBuild.apply(fmap1, fmap2, num_levels, self.state)
 
     @property
     def pyramid(self):

@@ -378,7 +378,11 @@ def bottleneck_block(blk, x):
 
 
 def fast_path_ok(enc, x):
-    """GPU + native library + bf16 autocast + supported norms; otherwise the eager path runs."""
+    """GPU + native library + bf16 autocast + supported norms; otherwise the eager path runs.
+    ``enc.allow_native = False`` (set by RAFT for ``corr_impl='torch'``, the stock-ops baseline)
+    forces the eager MIOpen / ATen encoder."""
+    if not getattr(enc, 'allow_native', True):
+        return False
     if not (isinstance(x, torch.Tensor) and x.is_cuda and _ext.device_ok(x)):
         return False
     if not (torch.is_autocast_enabled('cuda') and

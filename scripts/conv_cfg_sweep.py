@@ -6,7 +6,7 @@ import torch
 
 sys.path.insert(0, '.')
 from pytorch_raft_amd.ops import conv as C  # noqa: E402
-from scripts.r2.conv_bench import GEOS, timeit  # noqa: E402
+from scripts.conv_bench import GEOS, timeit  # noqa: E402
 
 
 def main():

@@ -1,8 +1,8 @@
 #!/bin/bash
 # PMC counters of one graphed training step (timed region only), 3 passes (SQ, FETCH, WRITE).
-# -> gpurun_out/pmc_<tag>_<pass>/ ; summarised by scripts/r2/pmc_summary.py
+# -> gpurun_out/pmc_<tag>_<pass>/ ; summarised by scripts/pmc_summary.py
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 TAG=${1:-step}; shift
 mkdir -p gpurun_out
@@ -15,5 +15,5 @@ for P in "$P1" "$P2" "$P3"; do
   timeout -s KILL 240 rocprofv3 --pmc $P --kernel-trace --output-format csv -d /tmp/pmc_${TAG}_$i -o run -- python bench.py --steps 2 --warmup 2 --trace_markers "$@" > gpurun_out/pmc_${TAG}_$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmc_${TAG}_$i.log; exit 1; }
   echo "pass $i ok"
 done
-python scripts/r2/pmc_summary.py /tmp/pmc_${TAG}_1 /tmp/pmc_${TAG}_2 /tmp/pmc_${TAG}_3 2 > gpurun_out/pmc_${TAG}_summary.txt 2>&1
+python scripts/pmc_summary.py /tmp/pmc_${TAG}_1 /tmp/pmc_${TAG}_2 /tmp/pmc_${TAG}_3 2 > gpurun_out/pmc_${TAG}_summary.txt 2>&1
 head -60 gpurun_out/pmc_${TAG}_summary.txt

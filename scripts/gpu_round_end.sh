@@ -1,7 +1,7 @@
 #!/bin/bash
 # final tree check: every GPU test + smoke() + one bench run
 set -o pipefail
-cd "$(dirname "$0")/../.."
+cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 280 --timeout-method thread > gpurun_out/final_pytest.log 2>&1
