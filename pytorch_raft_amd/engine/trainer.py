@@ -11,13 +11,15 @@ multi-tensor kernel.  Two execution modes:
 * eager (``TrainState.step``): gradients are all-reduced over RCCL in buckets overlapped with
   backward on a side HIP stream (``parallel.dist.GradSync``);
 * HIP-graph (``GraphedTrainStep``): RAFT issues thousands of small kernels per step (12 GRU
-  iterations forward + backward), so on MI355X the eager step is launch-bound.  The whole
-  forward + loss + backward is captured once into a hipGraph (torch.cuda.CUDAGraph == hipGraph on
-  ROCm) and replayed; with several ranks the graph packs the gradients into ONE flat buffer,
-  which is all-reduced with a single RCCL call between the replays, and the unpack + clip +
-  fused-AdamW update is a second graph.  The learning rate lives in a device tensor so the
-  OneCycle schedule keeps working
-  under replay.
+  iterations forward + backward), so on MI355X the eager step is launch-bound.  The recurrent
+  part -- correlation, the GRU iterations forward AND backward, upsampling and the loss -- is
+  captured once into a hipGraph (torch.cuda.CUDAGraph == hipGraph on ROCm) and replayed; the
+  encoders (large MIOpen convolutions) and the clip + fused-AdamW update run eagerly around it.
+  With several ranks the update-block gradients (final after the replay) go out as ONE flat RCCL
+  all-reduce that overlaps the eager encoder backward, and the encoder gradients are bucketed
+  (``GradSync``: post-accumulate-grad hooks launch each bucket on a side stream while the rest of
+  the encoder backward runs).  The learning rate lives in a device tensor so the OneCycle
+  schedule keeps working under replay.
 
 A device-side non-finite flag is accumulated for failure detection and checked at logging cadence.
 """
@@ -115,10 +117,11 @@ class GraphedTrainStep:
     and the encoders are not launch-bound anyway, so keeping them out of the graph costs nothing.
 
     Per step: eager encode -> copy the four encoder outputs into the graph's static leaves ->
-    replay g_dec (fills the update-block .grad and the leaves' .grad) -> (ranks > 1: RCCL
-    all-reduce of the update-block gradients starts) -> eager encoder backward from the leaves'
-    gradients -> (all-reduce of the encoder gradients) -> clip + fused AdamW (multi-tensor
-    kernels, eager).
+    replay g_dec (fills the update-block .grad and the leaves' .grad) -> (ranks > 1: ONE flat
+    RCCL all-reduce of the update-block gradients starts) -> eager encoder backward from the
+    leaves' gradients, whose post-accumulate-grad hooks launch the encoder gradient buckets
+    (``GradSync``, side stream) as each bucket's last gradient lands -> wait for all of them ->
+    clip + fused AdamW (multi-tensor kernels, eager).
 
     The warm-up steps needed before capture (MIOpen solver search, allocator, lazy optimizer
     state) are real training steps; their effect on the weights, BN statistics, optimizer moments
@@ -135,12 +138,17 @@ class GraphedTrainStep:
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
         self.dec_params = [p for n, p in named if n.startswith('update_block')]
         self.enc_params = [p for n, p in named if not n.startswith('update_block')]
-        # flat gradient layout [update block | encoders]: the update-block half is final after the
-        # decode replay and is all-reduced while the eager encoder backward runs
+        # ranks > 1: the update-block gradients are final after the decode replay and go out as
+        # one flat all-reduce while the eager encoder backward runs; the encoder gradients are
+        # all-reduced in buckets launched by post-accumulate-grad hooks during that backward
         self.params = self.dec_params + self.enc_params
         self.n_dec = sum(p.numel() for p in self.dec_params)
-        numel = sum(p.numel() for p in self.params)
-        self.flat = torch.zeros(numel, device=st.device, dtype=torch.float32) if self.world > 1 else None
+        self.flat = (torch.zeros(self.n_dec, device=st.device, dtype=torch.float32)
+                     if self.world > 1 else None)
+        self.enc_sync = None
+        if self.world > 1:
+            self.enc_sync = pdist.GradSync(model, bucket_mb=getattr(st.args, 'enc_bucket_mb', 2.0),
+                                           order=pdist.raft_grad_order, params=self.enc_params)
         for p in self.params:
             p.grad = None
         # learning rate as a device tensor (fused AdamW reads it in-graph)
@@ -207,7 +215,8 @@ class GraphedTrainStep:
     def _encoder_backward(self, feats):
         torch.autograd.backward(list(feats), [s.grad for s in self.sfeat])
 
-    def _step_body(self, image1, image2, flow, valid, graphs=True):
+    def _forward_backward_sync(self, image1, image2, flow, valid, graphs=True):
+        """Forward + backward of one step; on return every gradient is the all-rank mean."""
         st = self.st
         # encoder gradients are handed over by AccumulateGrad each step (no zero fill, no add
         # kernel per parameter); the update-block gradients live in the decode graph's pool
@@ -224,51 +233,49 @@ class GraphedTrainStep:
             for p in self.dec_params:
                 if p.grad is None:
                     p.grad = torch.zeros_like(p)
-        work = self._post_part(self.dec_params, 0)      # overlaps the encoder backward
+        work = self._allreduce_dec()                 # overlaps the encoder backward
+        if self.enc_sync is not None:
+            self.enc_sync.prepare()
         self._encoder_backward(feats)
         del feats
+        if self.enc_sync is not None:
+            self.enc_sync.finish()                   # buckets with no gradient go out as zeros
         for p in self.enc_params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
+        if work is not None:
+            work.wait()
+            self._unpack()
         self.grads = [p.grad for p in self.params]
-        work2 = self._post_part(self.enc_params, self.n_dec)
-        for w in (work, work2):
-            if w is not None:
-                w.wait()
+        return loss
+
+    def _step_body(self, image1, image2, flow, valid, graphs=True):
+        loss = self._forward_backward_sync(image1, image2, flow, valid, graphs)
         # clip + fused AdamW: a handful of multi-tensor launches, issued eagerly (the encoder
         # gradients are fresh tensors every step)
         self._update_graphable(loss)
         self._sched()
         return loss
 
-    def _post_part(self, params, off):
-        """Pack ``params``' gradients into their slice of ``flat`` and start its all-reduce."""
+    def _allreduce_dec(self):
+        """Pack the update-block gradients into ``flat`` and start its (sum) all-reduce."""
         if self.world <= 1:
             return None
-        n = sum(p.numel() for p in params)
-        part = self.flat[off:off + n]
-        torch.cat([p.grad.reshape(-1) for p in params], out=part)
-        return dist.all_reduce(part, async_op=True)
-
-    def _post(self):
-        for w in (self._post_part(self.dec_params, 0), self._post_part(self.enc_params, self.n_dec)):
-            if w is not None:
-                w.wait()
+        torch.cat([p.grad.reshape(-1) for p in self.dec_params], out=self.flat)
+        return dist.all_reduce(self.flat, async_op=True)
 
     def _unpack(self):
-        if self.flat is None:
-            return
+        grads = [p.grad for p in self.dec_params]
         views, off = [], 0
-        for g in self.grads:
+        for g in grads:
             n = g.numel()
             views.append(self.flat[off:off + n].view_as(g))
             off += n
-        torch._foreach_copy_(self.grads, views)
-        torch._foreach_mul_(self.grads, 1.0 / self.world)
+        torch._foreach_copy_(grads, views)
+        torch._foreach_mul_(grads, 1.0 / self.world)
 
     def _update_graphable(self, loss):
         st = self.st
-        self._unpack()
         clip_grad_norm_(self.params, st.args.clip)
         st.optimizer.step()
         st.nonfinite += (~torch.isfinite(loss.detach())).float()

@@ -157,10 +157,15 @@ class GradSync:
         sync.finish()            # waits, writes averaged grads back (any unfinished bucket too)
     """
 
-    def __init__(self, module, bucket_mb=8.0, comm_dtype=None, order=None):
+    def __init__(self, module, bucket_mb=8.0, comm_dtype=None, order=None, params=None):
+        """``params``: sync only these parameters of ``module`` (default: all that require grad);
+        ``order(module, params)`` returns them in the order their gradients become final."""
         self.world = world_size()
         self.comm_dtype = comm_dtype
-        params = [p for p in module.parameters() if p.requires_grad]
+        if params is None:
+            params = [p for p in module.parameters() if p.requires_grad]
+        else:
+            params = [p for p in params if p.requires_grad]
         if order is not None:
             params = order(module, params)
         else:

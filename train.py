@@ -75,8 +75,14 @@ def build_parser():
     p.add_argument('--seed', type=int, default=1234)
     p.add_argument('--profile', type=str, default=None, help='write a torch.profiler trace here')
     p.add_argument('--cpu', action='store_true', help='force CPU (gloo) training')
-    p.add_argument('--hipgraph', action='store_true',
-                   help='replay each training step as two hipGraphs (bf16 on a GPU; fixed crop)')
+    p.add_argument('--hipgraph', dest='hipgraph', action='store_true', default=True,
+                   help='(default on a GPU) replay the recurrent part of each step -- correlation, '
+                        'GRU iterations fwd+bwd, upsampling, loss -- as one hipGraph; encoders and '
+                        'the update run eagerly around it (fixed crop; bf16 or fp32)')
+    p.add_argument('--eager', '--no_hipgraph', dest='hipgraph', action='store_false',
+                   help='issue every kernel of the step eagerly')
+    p.add_argument('--enc_bucket_mb', type=float, default=2.0,
+                   help='graphed step, ranks > 1: encoder gradient bucket size (MB)')
     return p
 
 
@@ -127,8 +133,9 @@ def worker(args):
         from pytorch_raft_amd.data.datasets import fetch_dataloader
         loader = fetch_dataloader(args, rank=rank, world=world, num_workers=args.num_workers)
 
-    use_graph = (args.hipgraph and device.type == 'cuda' and args.mixed_precision
-                 and args.amp_dtype == 'bfloat16')
+    # fp16 autocast needs the GradScaler's host-side inf checks: that step runs eagerly
+    use_graph = (args.hipgraph and device.type == 'cuda' and
+                 not (args.mixed_precision and args.amp_dtype == 'float16'))
     st = TrainState(model, args, device, graph_ready=use_graph)
     stepper = st  # replaced by the graphed step at the first batch (capture needs its shapes)
     total_steps = 0
