@@ -244,6 +244,7 @@ struct CfgDesc {
   int glds;  // 0: register-staged kernel; n: LDS-DMA kernel with n pipeline stages; HALO
 };
 constexpr int HALO = 9;
+constexpr int V3 = 10;  // pipelined register-staged kernel (conv_v3.h)
 // (keep in sync with the dispatch switch below)
 constexpr CfgDesc kCfgs[] = {
     {2, 2, 2, 128, 128, true, false},  {1, 2, 2, 64, 128, true, false},
@@ -266,6 +267,10 @@ constexpr CfgDesc kCfgs[] = {
     // halo-tile kernel (conv_halo.h; glds = HALO): A image per channel chunk, B straight to VGPRs
     {5, 1, 1, 160, 128, false, HALO}, {5, 2, 1, 160, 256, false, HALO},
     {4, 2, 1, 128, 256, false, HALO}, {2, 2, 2, 128, 128, false, HALO},
+    // v3 kernel (conv_v3.h; glds = V3): MFMAs right after the barrier, A register-staged two steps
+    // ahead, B straight to VGPRs, two workgroups per CU where the registers allow
+    {5, 1, 1, 160, 128, false, V3}, {3, 1, 1, 96, 128, false, V3},
+    {5, 2, 1, 160, 256, false, V3}, {3, 2, 1, 96, 256, false, V3},
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -302,6 +307,8 @@ bool launch_cfg_idx(const ConvFwdArgs& a, int idx, hipStream_t stream) {
       case 8: launch_one<EPI, false, 4, 2, 1>(a, stream); return true;
       case 9: launch_one<EPI, false, 3, 2, 1>(a, stream); return true;
       default:
+        if (idx >= 0 && idx < kNumCfgs && kCfgs[idx].glds == V3)
+          return launch_conv_v3(a, EPI, kCfgs[idx].tm, kCfgs[idx].tn, stream);
         if (idx >= 0 && idx < kNumCfgs && kCfgs[idx].glds == HALO)
           return launch_conv_halo(a, EPI, kCfgs[idx].tm, kCfgs[idx].tn, kCfgs[idx].wvm, stream);
         if (idx >= 0 && idx < kNumCfgs && kCfgs[idx].glds) return launch_conv_glds(a, EPI, idx, stream);
@@ -336,6 +343,14 @@ bool halo_disabled() {
   return off;
 }
 
+bool v3_disabled() {
+  static const bool off = [] {
+    const char* e = getenv("RAFT_CONV_V3");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
 bool glds_disabled() {
   static const bool off = [] {
     const char* e = getenv("RAFT_CONV_GLDS");
@@ -349,6 +364,10 @@ bool cfg_allowed(int idx, int cout, bool smallc, int epi) {
   if (smallc && !c.small_ok) return false;
   if (c.glds && glds_disabled()) return false;
   if (c.glds == HALO && halo_disabled()) return false;
+  if (c.glds == V3 && v3_disabled()) return false;
+  // v3's wide tiles do not offer the gate epilogues (they spill there): an autotune timed on the
+  // fp32 scratch epilogue must not pick a config the real epilogue cannot launch
+  if (c.glds == V3 && c.tn == 2 && (epi == EPI_GRU_ZR || epi == EPI_DGRAD_GATE)) return false;
   if (idx == 6 && (epi == EPI_GRU_ZR || epi == EPI_GRU_Q)) return false;
   const int npad = (cout + 31) / 32 * 32;
   return c.bn <= 2 * npad || c.bn <= 32;  // no config more than half empty in N

@@ -160,6 +160,8 @@ struct ConvFwdArgs {
 bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStream_t stream);
 // LDS-DMA kernel of config `idx` (conv_glds.hip); false for a non-LDS-DMA index
 bool launch_conv_glds(const ConvFwdArgs& a, int epi, int idx, hipStream_t stream);
+// v3 kernel (conv_v3.hip) of tile (tm, tn); false if the geometry / epilogue is not offered
+bool launch_conv_v3(const ConvFwdArgs& a, int epi, int tm, int tn, hipStream_t stream);
 // rows of 12 ints: P H W KH KW cin cout small epi_class cfg BM BN
 int conv_tuned_table(int* out, int max_rows);
 // tests: run every following conv launch with config `idx` (-1: back to the tuned choice)
