@@ -66,7 +66,12 @@ def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl):
         # one eager single-process step of the global batch from the same weights
         ref.load_state_dict(sd)
         st2 = TrainState(ref, args, dev, sync=False)
-        st2.step(i1, i2, flow, valid)
+        # TrainState.step would broadcast BN buffers (a collective) from rank 0 alone: the
+        # single-process step is spelled out instead
+        st2.optimizer.zero_grad(set_to_none=True)
+        loss2, _ = st2.forward_backward(i1, i2, flow, valid)
+        st2.apply_update(loss2)
+        st2.scheduler.step()
         torch.cuda.synchronize()
         wr = torch.cat([p.detach().reshape(-1).float() for p in ref.parameters()])
         d_dp, d_ref = w1 - w0, wr - w0

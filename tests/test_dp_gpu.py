@@ -28,7 +28,7 @@ def test_dp_rehearsal(ext_ops, mode):
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
            '--master-addr', '127.0.0.1', '--master-port', str(_port()),
            os.path.join(ROOT, 'scripts', 'dp_rehearsal.py')] + (['--graph'] if mode == 'graph' else [])
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=160)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert 'dp rehearsal' in out, out[-2000:]
