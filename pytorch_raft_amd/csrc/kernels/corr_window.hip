@@ -109,10 +109,14 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
                                                               uint16_t* __restrict__ out, int cbuf,
                                                               int B, int H, int W, int levels) {
   constexpr int D = 2 * R + 1, E = D + 1, EE = E * E, DD = D * D;
+  // window rows padded to an odd stride in LDS: the interpolation reads of consecutive taps (iy
+  // fastest) are one row apart, and a stride of E = 10 floats put them on 16 banks (2-way
+  // conflicts on every read)
+  constexpr int WRS = E + 1, EES = E * WRS;
   constexpr int ROW = (4 * DD + 7) / 8 * 8;
   constexpr int PER = (TPW * EE + 255) / 256;  // window cells per thread per level
   constexpr uint32_t OOB = 0x80000000u;
-  __shared__ float win[TPW * 4 * EE];
+  __shared__ float win[TPW * 4 * EES];
   __shared__ float cxy[TPW * 4 * 2];
   __shared__ __attribute__((aligned(16))) uint16_t tile[TPW * ROW];
   const int N = H * W;
@@ -159,8 +163,8 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
     for (int k = 0; k < PER; ++k) {
       const int e = tid + k * 256;
       if (e < TPW * EE) {
-        const int px = e / EE, rc = e - px * EE;
-        win[(px * 4 + l) * EE + rc] = v[k];
+        const int px = e / EE, rc = e - px * EE, r = rc / E, c = rc - r * E;
+        win[(px * 4 + l) * EES + r * WRS + c] = v[k];
       }
     }
   }
@@ -171,9 +175,9 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
     const int l = ch / DD, t = ch - l * DD, ix = t / D, iy = t - ix * D;
     const float cx = cxy[(px * 4 + l) * 2], cy = cxy[(px * 4 + l) * 2 + 1];
     const float ax = cx - floorf(cx), ay = cy - floorf(cy);
-    const float* w = win + (px * 4 + l) * EE + iy * E + ix;
+    const float* w = win + (px * 4 + l) * EES + iy * WRS + ix;
     const float top = (1.f - ax) * w[0] + ax * w[1];
-    const float bot = (1.f - ax) * w[E] + ax * w[E + 1];
+    const float bot = (1.f - ax) * w[WRS] + ax * w[WRS + 1];
     tile[px * ROW + ch] = raft_f32_to_bf16((1.f - ay) * top + ay * bot);
   }
   __syncthreads();
@@ -182,15 +186,20 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
     const int px = e / chunks, ch = e % chunks;
     const int i = i0 + px;
     if (i >= N) continue;
-    uint16_t q8[8];
+    uint4 o;
+    if (ch * 8 + 8 <= ctot) {  // whole 16-B piece of taps: one LDS read (ROW % 8 == 0)
+      o = *reinterpret_cast<const uint4*>(tile + px * ROW + ch * 8);
+    } else {
+      uint16_t q8[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int c = ch * 8 + q;
-      q8[q] = c < ctot ? tile[px * ROW + c] : (uint16_t)0;
+      for (int q = 0; q < 8; ++q) {
+        const int c = ch * 8 + q;
+        q8[q] = c < ctot ? tile[px * ROW + c] : (uint16_t)0;
+      }
+      o = make_uint4(q8[0] | ((uint32_t)q8[1] << 16), q8[2] | ((uint32_t)q8[3] << 16),
+                     q8[4] | ((uint32_t)q8[5] << 16), q8[6] | ((uint32_t)q8[7] << 16));
     }
-    *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i) * cbuf + ch * 8) =
-        make_uint4(q8[0] | ((uint32_t)q8[1] << 16), q8[2] | ((uint32_t)q8[3] << 16),
-                   q8[4] | ((uint32_t)q8[5] << 16), q8[6] | ((uint32_t)q8[7] << 16));
+    *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i) * cbuf + ch * 8) = o;
   }
 }
 
