@@ -28,7 +28,7 @@ METRIC = ('training image-pairs/sec (whole node), RAFT FlyingChairs 368x496 iter
 # 368x496, iters 12, 10 warm-up / 50 timed steps), per compute dtype -- scaled ideally to N GPUs
 # for vs_baseline.  A run is compared only with the stock run of ITS dtype at the headline
 # config (per-GPU batch 12); any other config reports vs_baseline = null.
-STOCK_PAIRS_PER_GPU = {'bf16': 113.19, 'fp32': 66.85}
+STOCK_PAIRS_PER_GPU = {'bf16': 102.705, 'fp32': 66.85}
 HEADLINE_BATCH = 12
 
 
