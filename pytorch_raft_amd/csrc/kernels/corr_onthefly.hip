@@ -329,6 +329,12 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
   __shared__ float dwin[MULTI ? 1 : TP * NP];
   __shared__ int gx[NIT][TP], gy[NIT][TP];
   __shared__ Geo geo;
+  // MULTI: per pixel, the sum over the iterations of its window gradients on a UG x UG grid at
+  // the union of its windows (the windows of one pixel move only a few positions over a step),
+  // so building a dS chunk element is one LDS read instead of a global read per iteration
+  constexpr int UG = 15, UGG = UG * UG;
+  __shared__ float ugrid[MULTI ? TP * UGG : 1];
+  __shared__ int uxy[MULTI ? 2 * TP + 1 : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int t = blockIdx.x;
@@ -404,6 +410,49 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
       }
       __syncthreads();
     }
+    bool ufits = false;
+    if constexpr (MULTI) {
+      // union origin of each pixel's windows; the fast path needs every pixel's union <= UG^2
+      if (wave == 0) {
+        int mnx = 0x7fffffff, mxx = -0x7fffffff, mny = 0x7fffffff, mxy = -0x7fffffff;
+        for (int it = 0; it < wl.n; ++it) {
+          const int x0 = gx[it][lane], y0 = gy[it][lane];
+          if (x0 > -(1 << 27)) {
+            mnx = min(mnx, x0);
+            mxx = max(mxx, x0);
+            mny = min(mny, y0);
+            mxy = max(mxy, y0);
+          }
+        }
+        const bool none = mnx > mxx;
+        const bool fit = none || (mxx - mnx + E <= UG && mxy - mny + E <= UG);
+        uxy[lane] = none ? -(1 << 28) : mnx;
+        uxy[TP + lane] = none ? -(1 << 28) : mny;
+        const bool all = __builtin_amdgcn_read_exec() == __ballot(fit);
+        if (lane == 0) uxy[2 * TP] = all ? 1 : 0;
+      }
+      __syncthreads();
+      ufits = uxy[2 * TP] != 0;
+      if (ufits) {
+        for (int e = tid; e < TP * UGG; e += NT) ugrid[e] = 0.f;
+        __syncthreads();
+        // each thread owns the same (pixel, cell) set in every iteration: no two threads add to
+        // one grid cell, and one thread's adds run in iteration order (deterministic)
+        for (int it = 0; it < wl.n; ++it) {
+          for (int e = tid; e < TP * NP; e += NT) {
+            const int p = e / NP, qq = e - (e / NP) * NP;
+            const int x0 = gx[it][p], y0 = gy[it][p];
+            if (x0 <= -(1 << 27)) continue;
+            const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
+            if (py >= H || px >= W) continue;
+            const int64_t wrow = (((int64_t)b * HW + py * W + px) * levels + l) * NP;
+            const int cy = y0 - uxy[TP + p] + qq / E, cxg = x0 - uxy[p] + qq % E;
+            ugrid[p * UGG + cy * UG + cxg] += wl.wg[it][wrow + qq];
+          }
+        }
+        __syncthreads();
+      }
+    }
     const int bx0 = geo.box[0], by0 = geo.box[1], bw = geo.box[2], bh = geo.box[3];
     const int U = bw * bh;
     const int nchunk = (U + NCH - 1) / NCH;
@@ -420,12 +469,18 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
         if (pos < U) {
           const int iy = by0 + pos / bw, ix = bx0 + pos % bw;
           if constexpr (MULTI) {
-            const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
-            const int64_t wrow = (((int64_t)b * HW + py * W + px) * levels + l) * NP;
-            for (int it = 0; it < wl.n; ++it) {  // fixed order -> deterministic
-              const int rx = ix - gx[it][p], ry = iy - gy[it][p];
-              if ((unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E)
-                v += wl.wg[it][wrow + ry * E + rx];
+            if (ufits) {
+              const int rx = ix - uxy[p], ry = iy - uxy[TP + p];
+              if ((unsigned)rx < (unsigned)UG && (unsigned)ry < (unsigned)UG)
+                v = ugrid[p * UGG + ry * UG + rx];
+            } else {  // a pixel's windows spread wider than the grid: sum from global memory
+              const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
+              const int64_t wrow = (((int64_t)b * HW + py * W + px) * levels + l) * NP;
+              for (int it = 0; it < wl.n; ++it) {  // fixed order -> deterministic
+                const int rx = ix - gx[it][p], ry = iy - gy[it][p];
+                if ((unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E)
+                  v += wl.wg[it][wrow + ry * E + rx];
+              }
             }
             v *= isc;
           } else {

@@ -172,16 +172,26 @@ def test_onthefly_matches_allpairs(ext_ops, radius, c, hw, spread, precision):
     assert _rel(f2.grad, g2_ref) < 1e-2
 
 
+@pytest.mark.parametrize('drift', [False, True])
 @pytest.mark.parametrize('hw', [(46, 62), (13, 19)])
-def test_onthefly_nhwc_bf16(ext_ops, hw):
+def test_onthefly_nhwc_bf16(ext_ops, hw, drift):
     """Fused-path lookups (bf16 NHWC) over 3 iterations; backward = window-compact gradients
-    folded by ONE corr_otf_window_bwd_ launch.  Also checks it is deterministic in dF1."""
+    folded by ONE corr_otf_window_bwd_ launch.  Also checks it is deterministic in dF1.
+    drift=True moves each pixel's window by a pixel or two per iteration (as RAFT's refinement
+    does), so every tile takes the union-grid path of the backward; drift=False scatters the
+    windows independently, so level 0 mostly falls back to the per-iteration sum."""
     h, w = hw
     b, c, radius = 2, 256, 4
     levels = 4 if min(h, w) >= 16 else 3
     f1 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
     f2 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
-    coords = [_coords(b, h, w, spread=2.0 + s, seed=5 + s) for s in range(3)]
+    if drift:
+        c0 = _coords(b, h, w, spread=3.0, seed=5)
+        g = torch.Generator(device='cpu').manual_seed(9)
+        coords = [c0 + 0.6 * s * torch.randn(c0.shape, generator=g).clamp(-1.5, 1.5).to(DEV)
+                  for s in range(3)]
+    else:
+        coords = [_coords(b, h, w, spread=2.0 + s, seed=5 + s) for s in range(3)]
     nc = levels * 81
     pyr = torch_corr_pyramid(f1, f2, levels)
     gouts = [torch.randn(b, h, w, 384, device=DEV) for _ in coords]
