@@ -18,6 +18,8 @@ constexpr int NT = 256;
 // slots and the pass is conflict-free (the ds_write_b128 tile stores stay conflict-free too).
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk ^ ((row >> 1) & 7)); }
 
+__device__ __forceinline__ bf16x8_t zero_frag8() { return __builtin_bit_cast(bf16x8_t, make_uint4(0, 0, 0, 0)); }
+
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr uint32_t OOB = 0x80000000u;  // voffset past every num_records: the load returns zeros
 

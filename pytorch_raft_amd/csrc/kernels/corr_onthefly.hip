@@ -434,21 +434,36 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
       __syncthreads();
       ufits = uxy[2 * TP] != 0;
       if (ufits) {
-        for (int e = tid; e < TP * UGG; e += NT) ugrid[e] = 0.f;
-        __syncthreads();
-        // each thread owns the same (pixel, cell) set in every iteration: no two threads add to
-        // one grid cell, and one thread's adds run in iteration order (deterministic)
-        for (int it = 0; it < wl.n; ++it) {
-          for (int e = tid; e < TP * NP; e += NT) {
-            const int p = e / NP, qq = e - (e / NP) * NP;
-            const int x0 = gx[it][p], y0 = gy[it][p];
-            if (x0 <= -(1 << 27)) continue;
-            const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
-            if (py >= H || px >= W) continue;
+        // gather: a thread owns a (pixel, grid cell) and sums, in iteration order, the window
+        // gradient entries of every iteration whose window covers that cell (one writer per cell:
+        // no zero pass, no read-modify-write races, deterministic).  The iterations' loads are
+        // issued in batches of 8 independent reads so they are in flight together.
+        for (int e = tid; e < TP * UGG; e += NT) {
+          const int p = e / UGG, cell = e - p * UGG;
+          const int cgy = cell / UG, cgx = cell - cgy * UG;
+          const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
+          float s = 0.f;
+          if (py < H && px < W) {
             const int64_t wrow = (((int64_t)b * HW + py * W + px) * levels + l) * NP;
-            const int cy = y0 - uxy[TP + p] + qq / E, cxg = x0 - uxy[p] + qq % E;
-            ugrid[p * UGG + cy * UG + cxg] += wl.wg[it][wrow + qq];
+            const int ux = uxy[p] + cgx, uy = uxy[TP + p] + cgy;
+            for (int i0 = 0; i0 < wl.n; i0 += 8) {
+              float v[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int it = i0 + u;
+                v[u] = 0.f;
+                if (it < wl.n) {  // uniform
+                  const int x0 = gx[it][p];  // -(1 << 28): this iteration's window misses the map
+                  const int rx = ux - x0, ry = uy - gy[it][p];
+                  if (x0 > -(1 << 27) && (unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E)
+                    v[u] = wl.wg[it][wrow + ry * E + rx];
+                }
+              }
+#pragma unroll
+              for (int u = 0; u < 8; ++u) s += v[u];
+            }
           }
+          ugrid[e] = s;
         }
         __syncthreads();
       }
