@@ -305,6 +305,66 @@ class _Conv3x3WgradNative(torch.autograd.Function):
 _WGRAD_NATIVE = os.environ.get('RAFT_ENCODER_WGRAD_NATIVE', '1') != '0'
 
 
+def _conv3x3_native_fwd(x, w):
+    from . import conv as C
+    B, ci, H, W = x.shape
+    co = w.shape[0]
+    xn = x.permute(0, 2, 3, 1)                     # channels_last memory: a view
+    wpk = w.permute(0, 2, 3, 1).reshape(co, 9 * ci)
+    out = torch.empty(B, H, W, co, device=x.device, dtype=torch.bfloat16)
+    C.conv_fwd([(xn, 0, ci)], wpk, None, (3, 3), (1, 1), co, C.EPI_BF16, [out], [0])
+    return out.permute(0, 3, 1, 2)
+
+
+class _Conv3x3Native(torch.autograd.Function):
+    """Stride-1 3x3 "same" encoder conv with 64-multiple channel counts (`core/extractor.py:22-23`:
+    layer1's 64-channel and layer3's 128-channel residual convs) entirely on the MFMA kernels:
+    forward = the update block's implicit-GEMM conv (bf16 epilogue), input gradient = the same
+    kernel on the flipped / transposed weight, weight gradient = the tap-fused kernel.  MIOpen
+    took 1.6-4.5x longer per call on these shapes (profiles/r3/enc_conv_miopen_vs_mfma.txt) and
+    zero-filled every input-gradient buffer before its solver ran (SubTensorOpWithScalar1d).
+
+    The channels_last bf16 weight (co, kh, kw, ci in memory) IS the kernels' packed layout
+    [co][tap * ci + c]: the forward packs nothing."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return _conv3x3_native_fwd(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import conv as C
+        x, w = ctx.saved_tensors
+        co, ci = w.shape[:2]
+        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        gn = dy.permute(0, 2, 3, 1)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            B, _, H, W = x.shape
+            # adjoint weight W'[c][tap'][o] = W[o][c][flip(tap')], in the kernels' packed layout
+            wd = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+            wd = wd.permute(0, 2, 3, 1).reshape(ci, 9 * co)
+            dxn = torch.empty(B, H, W, ci, device=x.device, dtype=torch.bfloat16)
+            _ext.ops().conv_dgrad_([gn], [0], [co], wd, 3, 3, 1, 1, 0, 1.0, [dxn], [0], [ci], [ci],
+                                   [0], [dxn], [-1], [], [])
+            dx = dxn.permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            dwp = torch.empty(co, 9 * ci, device=x.device, dtype=torch.bfloat16)
+            C.conv_wgrad_taps([(gn, [x.permute(0, 2, 3, 1)])], 0, [0], [ci], (3, 3), (1, 1), co,
+                              dwp, None)
+            dw = dwp.view(co, 3, 3, ci).permute(0, 3, 1, 2)
+        return dx, dw
+
+
+_CONV_NATIVE = os.environ.get('RAFT_ENCODER_CONV_NATIVE', '1') != '0'
+
+
+def _conv_native_ok(x, conv):
+    return (_CONV_NATIVE and _wgrad_native_ok(x, conv) and conv.in_channels % 64 == 0
+            and conv.out_channels % 64 == 0 and conv.out_channels <= 1024)
+
+
 def _wgrad_native_ok(x, conv):
     return (_WGRAD_NATIVE and conv.kernel_size == (3, 3) and conv.stride == (1, 1)
             and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
@@ -318,6 +378,10 @@ def _conv(x, conv, with_bias=False):
     w = _WEIGHTS.get(conv)
     if w is None:
         w = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    if not with_bias and _conv_native_ok(x, conv) and w.is_contiguous(memory_format=torch.channels_last):
+        if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
+            return _Conv3x3Native.apply(x, w)
+        return _conv3x3_native_fwd(x, w)
     if not with_bias and _wgrad_native_ok(x, conv) and torch.is_grad_enabled() and \
             (x.requires_grad or w.requires_grad):
         return _Conv3x3WgradNative.apply(x, w)

@@ -120,3 +120,33 @@ def test_native_wgrad_3x3_matches_conv2d(ext_ops, cin, cout):
     assert w.grad.dtype == torch.bfloat16 and w.grad.shape == w.shape
     torch.testing.assert_close(x.grad.float(), xr.grad, atol=3e-2 * xr.grad.abs().max().item(),
                                rtol=2e-2)
+
+
+@pytest.mark.parametrize('cin,cout', [(64, 64), (128, 128), (64, 128)])
+def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout):
+    """Stride-1 3x3 encoder conv entirely on the MFMA kernels (forward implicit GEMM, input
+    gradient on the flipped weight, tap-fused weight gradient) vs the fp32 autograd of F.conv2d at
+    the same bf16 inputs, across image and batch borders."""
+    torch.manual_seed(4)
+    x = torch.randn(3, cin, 37, 45, device=DEV).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) * 0.05).to(torch.bfloat16)
+    w = w.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    dy = torch.randn(3, cout, 37, 45, device=DEV).to(torch.bfloat16)
+    dy = dy.contiguous(memory_format=torch.channels_last)
+    y = fast._Conv3x3Native.apply(x, w)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, None, 1, 1)
+    yr.backward(dy.float())
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    s = wr.grad.abs().max().item()
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=1e-2 * s, rtol=1e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=3e-2 * xr.grad.abs().max().item(),
+                               rtol=2e-2)
+    # no-grad path (inference) gives the same forward
+    with torch.no_grad():
+        y2 = fast._conv3x3_native_fwd(x.detach(), w.detach())
+    assert torch.equal(y2, y.detach())
