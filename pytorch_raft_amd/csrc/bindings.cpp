@@ -373,27 +373,34 @@ void corr_otf_bwd_(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor
               "on-the-fly corr supports radius 3/4 with C = 128/256");
 }
 
-// every iteration's gradient at once: coords[k] (B,2,H,W), wgs[k] (B,N,L,E,E) from corr_window_grad
+// every iteration's gradient at once: coords[k] (B,2,H,W) and douts[k] (B,H,W,cbuf) bf16, the
+// gradient of iteration k's NHWC lookup output (taps in channels [0, L*(2r+1)^2))
 void corr_otf_window_bwd_(const Tensor& f1, const std::vector<Tensor>& f2,
-                          const std::vector<Tensor>& coords, const std::vector<Tensor>& wgs,
+                          const std::vector<Tensor>& coords, const std::vector<Tensor>& douts,
                           const Tensor& df1, const std::vector<Tensor>& df2, int64_t radius) {
-  TORCH_CHECK(!coords.empty() && coords.size() == wgs.size() && coords.size() <= RAFT_MAX_WIN,
+  TORCH_CHECK(!coords.empty() && coords.size() == douts.size() && coords.size() <= RAFT_MAX_WIN,
               "1..", RAFT_MAX_WIN, " iterations");
   otf_common_checks(f1, coords[0], radius);
   const int64_t B = f1.size(0), H = f1.size(1), W = f1.size(2), C = f1.size(3);
-  const int64_t levels = (int64_t)f2.size(), E = 2 * radius + 2;
+  const int64_t levels = (int64_t)f2.size(), D = 2 * radius + 1;
   check_cuda_f32(df1, "grad_fmap1");
   TORCH_CHECK(df1.sizes() == f1.sizes(), "grad_fmap1 must be (B,H,W,C)");
   TORCH_CHECK(f2.size() == df2.size(), "level count mismatch");
   WinList wl{};
+  const int64_t cbuf = douts[0].dim() == 4 ? douts[0].size(3) : 0;
   for (size_t k = 0; k < coords.size(); ++k) {
     check_cuda_f32(coords[k], "coords");
-    check_cuda_f32(wgs[k], "window grad");
     TORCH_CHECK(coords[k].sizes() == coords[0].sizes(), "coords shape");
-    TORCH_CHECK(wgs[k].numel() == B * H * W * levels * E * E, "window grad shape");
+    TORCH_CHECK(douts[k].is_cuda() && douts[k].is_contiguous() && douts[k].scalar_type() == at::kBFloat16 &&
+                    douts[k].dim() == 4 && douts[k].size(0) == B && douts[k].size(1) == H &&
+                    douts[k].size(2) == W && douts[k].size(3) == cbuf,
+                "tap gradients must be contiguous bf16 (B,H,W,Cbuf) tensors of one shape");
     wl.coords[k] = coords[k].data_ptr<float>();
-    wl.wg[k] = wgs[k].data_ptr<float>();
+    wl.dout[k] = reinterpret_cast<const uint16_t*>(douts[k].data_ptr<at::BFloat16>());
   }
+  // the kernel stages 16-B pieces of the 8-aligned span of every level's taps
+  TORCH_CHECK(cbuf % 8 == 0 && cbuf >= (levels * D * D + 7) / 8 * 8, "tap gradient Cbuf too small");
+  wl.cbuf = (int)cbuf;
   wl.n = (int)coords.size();
   c10::DeviceGuard g(f1.device());
   Bf16Levels L = otf_levels(f2, B, C, H, W);
@@ -1441,7 +1448,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx) -> ()");
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
-  m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] wgs, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
+  m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] douts, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("corr_build_bf16(Tensor f1, Tensor f2, int levels, bool pyr_bf16=False) -> Tensor[]");
   m.def("conv_wgrad_taps_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, "
         "int kw, int ph, int pw, int cout, Tensor dw, Tensor? db, int splits=0) -> ()");

@@ -308,10 +308,30 @@ __device__ __forceinline__ void tile_geometry_multi(int (*gx)[TP], int (*gy)[TP]
   }
 }
 
+// Window-gradient cell (rx, ry) in [0, 2r+2)^2 of one lookup: the bilinear adjoint of its
+// (2r+1)^2 bf16 tap gradients T (x-offset-major, tap ix*D + iy; ax, ay = the lookup centre's
+// fractions), in the expression order of corr_window_grad_kernel.
+template <int R>
+__device__ __forceinline__ float win_cell(const uint16_t* T, int rx, int ry, float ax, float ay) {
+  constexpr int D = 2 * R + 1;
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int iy = ry - k;
+    if (iy < 0 || iy >= D) continue;
+    const float wy = k == 0 ? (1.f - ay) : ay;
+    float s = 0.f;
+    if (rx < D) s += (1.f - ax) * raft_bf16_to_f32(T[rx * D + iy]);
+    if (rx > 0) s += ax * raft_bf16_to_f32(T[(rx - 1) * D + iy]);
+    acc += wy * s;
+  }
+  return acc;
+}
+
 // MULTI = false: one lookup's gradient, dout (B,H,W,dstride) -> bilinear adjoint in LDS.
-// MULTI = true : every iteration of the step at once from compact window gradients
-//                wg_it (B,N,L,E,E) (corr_window_grad_kernel), so the fmap2 box GEMMs and the
-//                dF2 atomics run once per step over the union box instead of once per iteration.
+// MULTI = true : every iteration of the step at once, straight from the iterations' bf16 tap
+//                gradients (WinList dout / coords), so the fmap2 box GEMMs and the dF2 atomics
+//                run once per step over the union box instead of once per iteration.
 template <int R, int C, typename TD, bool MULTI>
 __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
     const uint16_t* __restrict__ f1, OtfLvls lv, const float* __restrict__ coords,
@@ -335,6 +355,7 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
   constexpr int UG = 15, UGG = UG * UG;
   __shared__ float ugrid[MULTI ? TP * UGG : 1];
   __shared__ int uxy[MULTI ? 2 * TP + 1 : 1];
+  __shared__ float pax[2][MULTI ? TP : 1], pay[2][MULTI ? TP : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int t = blockIdx.x;
@@ -434,36 +455,61 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
       __syncthreads();
       ufits = uxy[2 * TP] != 0;
       if (ufits) {
-        // gather: a thread owns a (pixel, grid cell) and sums, in iteration order, the window
-        // gradient entries of every iteration whose window covers that cell (one writer per cell:
-        // no zero pass, no read-modify-write races, deterministic).  The iterations' loads are
-        // issued in batches of 8 independent reads so they are in flight together.
-        for (int e = tid; e < TP * UGG; e += NT) {
-          const int p = e / UGG, cell = e - p * UGG;
-          const int cgy = cell / UG, cgx = cell - cgy * UG;
-          const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
-          float s = 0.f;
-          if (py < H && px < W) {
-            const int64_t wrow = (((int64_t)b * HW + py * W + px) * levels + l) * NP;
-            const int ux = uxy[p] + cgx, uy = uxy[TP + p] + cgy;
-            for (int i0 = 0; i0 < wl.n; i0 += 8) {
-              float v[8];
-#pragma unroll
-              for (int u = 0; u < 8; ++u) {
-                const int it = i0 + u;
-                v[u] = 0.f;
-                if (it < wl.n) {  // uniform
-                  const int x0 = gx[it][p];  // -(1 << 28): this iteration's window misses the map
-                  const int rx = ux - x0, ry = uy - gy[it][p];
-                  if (x0 > -(1 << 27) && (unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E)
-                    v[u] = wl.wg[it][wrow + ry * E + rx];
-                }
-              }
-#pragma unroll
-              for (int u = 0; u < 8; ++u) s += v[u];
-            }
+        // Per iteration (fixed order), each window cell of each pixel adds the bilinear adjoint of
+        // up to 4 of its bf16 tap gradients into the pixel's union grid: within one iteration the
+        // cells of a pixel's window are distinct grid cells (one writer each), and a barrier
+        // separates the iterations -- deterministic, no atomics.  The 64 pixels' level-l taps of
+        // iteration it+1 (16-B pieces of the 8-aligned span around l*D*D) are staged in LDS (the
+        // fmap2 chunk buffer, free here; two slots) while iteration it's cells are added: the
+        // window gradients never go through global memory.
+        constexpr int TROW = ((DD + 7 + 7) / 8) * 8;  // staged taps per pixel (8-aligned span)
+        // two slots (stage it+1 during it) where the chunk buffer holds them (C = 256), else one
+        constexpr int NSLOT = 2 * TP * TROW <= NCH * RS ? 2 : 1;
+        static_assert(TP * TROW <= NCH * RS, "a tap slot fits the chunk buffer");
+        const int t0 = (l * DD) & ~7, tpieces = ((l * DD + DD + 7) & ~7) / 8 - t0 / 8;
+        const float inv = 1.f / (float)(1 << l);
+        auto stage = [&](int it) {
+          uint16_t* Ts = Bs + (it % NSLOT) * TP * TROW;
+          for (int e = tid; e < TP * tpieces; e += NT) {
+            const int p = e / tpieces, q = e - p * tpieces;
+            const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (py < H && px < W)
+              v = *reinterpret_cast<const uint4*>(wl.dout[it] + ((int64_t)b * HW + py * W + px) * wl.cbuf + t0 + q * 8);
+            *reinterpret_cast<uint4*>(Ts + p * TROW + q * 8) = v;
           }
-          ugrid[e] = s;
+          if (tid < TP) {
+            const int py = ty * TPX + tid / TPX, px = tx * TPX + tid % TPX;
+            float ax = 0.f, ay = 0.f;
+            if (py < H && px < W) {
+              const int64_t ci = (int64_t)b * 2 * HW + py * W + px;
+              const float cx = clampc(wl.coords[it][ci] * inv), cy = clampc(wl.coords[it][ci + HW] * inv);
+              ax = cx - floorf(cx);
+              ay = cy - floorf(cy);
+            }
+            pax[it % NSLOT][tid] = ax;
+            pay[it % NSLOT][tid] = ay;
+          }
+        };
+        for (int e = tid; e < TP * UGG; e += NT) ugrid[e] = 0.f;
+        if (NSLOT == 2 && wl.n > 0) stage(0);
+        for (int it = 0; it < wl.n; ++it) {
+          __syncthreads();  // iteration it-1's adds done (its slot is free); 2 slots: it staged
+          if (NSLOT == 1) {
+            stage(it);
+            __syncthreads();
+          } else if (it + 1 < wl.n) {
+            stage(it + 1);
+          }
+          const uint16_t* Ts = Bs + (it % NSLOT) * TP * TROW + (l * DD - t0);
+          for (int e = tid; e < TP * NP; e += NT) {
+            const int p = e / NP, qq = e - p * NP;
+            const int x0 = gx[it][p];  // -(1 << 28): this iteration's window misses the map
+            if (x0 <= -(1 << 27)) continue;
+            const int ry = qq / E, rx = qq - ry * E;
+            const int cy = gy[it][p] - uxy[TP + p] + ry, cxg = x0 - uxy[p] + rx;
+            ugrid[p * UGG + cy * UG + cxg] += win_cell<R>(Ts + p * TROW, rx, ry, pax[it % NSLOT][p], pay[it % NSLOT][p]);
+          }
         }
         __syncthreads();
       }
@@ -488,13 +534,18 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
               const int rx = ix - uxy[p], ry = iy - uxy[TP + p];
               if ((unsigned)rx < (unsigned)UG && (unsigned)ry < (unsigned)UG)
                 v = ugrid[p * UGG + ry * UG + rx];
-            } else {  // a pixel's windows spread wider than the grid: sum from global memory
+            } else {  // a pixel's windows spread wider than the grid: from the global taps
               const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
-              const int64_t wrow = (((int64_t)b * HW + py * W + px) * levels + l) * NP;
+              const int64_t pix = (int64_t)b * HW + py * W + px;
+              const int64_t ci = (int64_t)b * 2 * HW + py * W + px;
+              const float inv = 1.f / (float)(1 << l);
               for (int it = 0; it < wl.n; ++it) {  // fixed order -> deterministic
                 const int rx = ix - gx[it][p], ry = iy - gy[it][p];
-                if ((unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E)
-                  v += wl.wg[it][wrow + ry * E + rx];
+                if ((unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E) {
+                  const float cx = clampc(wl.coords[it][ci] * inv), cy = clampc(wl.coords[it][ci + HW] * inv);
+                  v += win_cell<R>(wl.dout[it] + pix * wl.cbuf + l * DD, rx, ry, cx - floorf(cx),
+                                   cy - floorf(cy));
+                }
               }
             }
             v *= isc;

@@ -257,8 +257,10 @@ bool launch_fh2_wgrad(const Fh2Items& it, int cs, int B, int H, int W, float* pa
 // ---- NHWC lookup tile + window-compact backward (corr_window.hip)
 #define RAFT_MAX_WIN 32
 struct WinList {
-  const float* coords[RAFT_MAX_WIN];  // (B,2,H,W) per iteration
-  const float* wg[RAFT_MAX_WIN];      // (B,N,L,E,E) per iteration
+  const float* coords[RAFT_MAX_WIN];   // (B,2,H,W) per iteration
+  const float* wg[RAFT_MAX_WIN];       // (B,N,L,E,E) per iteration (corr_window_reduce)
+  const uint16_t* dout[RAFT_MAX_WIN];  // (B,H,W,cbuf) bf16 tap gradients (on-the-fly backward)
+  int cbuf;
   int n;
 };
 bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* ws, int levels,

@@ -298,11 +298,10 @@ class _OTFLookupNHWC(torch.autograd.Function):
         st = ctx.state
         (coords,) = ctx.saved_tensors
         if len(st.windows) < 32 and dout.shape[-1] % 8 == 0:
-            # compact per-iteration window gradient; the MFMA box GEMMs + dF2 atomics then run ONCE
-            # per step over all iterations (build node backward) instead of once per iteration
-            wg = _ext.ops().corr_window_grad(coords, dout.to(torch.bfloat16).contiguous(),
-                                             len(st.f2), ctx.radius)
-            st.windows.append((coords, wg))
+            # the iteration's bf16 tap gradient is kept; the MFMA box GEMMs + dF2 atomics then run
+            # ONCE per step over all iterations (build node backward) instead of once per
+            # iteration, forming each pixel's window gradients from the taps in LDS
+            st.windows.append((coords, dout.to(torch.bfloat16).contiguous()))
             st.radius = ctx.radius
         else:
             _otf_backward(st, coords, dout, ctx.radius)

@@ -9,7 +9,7 @@ CATS = [('ours conv fwd', r'conv_fwd_kernel<[^>]*, [0-57], (true|false)>|conv_fw
         ('encoder norm', r'norm_(bwd_)?(stats|apply|finalize)|partial_reduce|add_relu|relu_mask'),
         ('miopen conv', r'igemm|grouped_conv|naive_conv|gemm|Conv'), ('transpose', r'transpose'),
         ('bn/norm', r'batch_norm|BatchNorm|InstanceNorm|instance_norm|welford|Norm'),
-        ('reduce', r'reduce_kernel'),
+        ('corr', r'corr_'), ('reduce', r'reduce_kernel'),
         ('elementwise', r'elementwise|vectorized|SubTensor|OpTensor|Cast|copy_kernel|unrolled'),
         ('corr', r'corr_'), ('upsample', r'convex'), ('update ew', r'relu_bwd|gru_|flow_prep'),
         ('copy', r'copyBuffer'), ('loss', r'seq_loss'), ('adam', r'adam|Adam|multi_tensor')]

@@ -90,7 +90,7 @@ def test_dry_run_fused_training_step(alternate):
     if not alternate:
         assert {'corr_build', 'corr_lookup_nhwc_', 'corr_tap_reduce'} <= names
     else:
-        assert {'corr_otf_fwd_', 'corr_window_grad', 'corr_otf_window_bwd_'} <= names
+        assert {'corr_otf_fwd_', 'corr_otf_window_bwd_'} <= names
     # every update-block parameter received a gradient through the fused backward
     for n, p in m.named_parameters():
         if n.startswith('update_block'):
