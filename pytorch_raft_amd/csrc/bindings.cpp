@@ -446,9 +446,8 @@ Tensor convex_up_fwd(const Tensor& flow, const Tensor& mask, bool nhwc) {
   c10::DeviceGuard g(flow.device());
   Tensor out = at::empty({B, 2, 8 * H, 8 * W}, flow.options());
   const int64_t HW = H * W;
-  if (nhwc && mask_kind(mask) == 1 && aligned16(flow) && aligned16(mask) && aligned16(out)) {
-    launch_convex_up_nhwc_fwd(flow.data_ptr<float>(),
-                              reinterpret_cast<const uint16_t*>(mask.data_ptr<at::BFloat16>()),
+  if (nhwc && mask.is_contiguous() && aligned16(flow) && aligned16(mask) && aligned16(out)) {
+    launch_convex_up_nhwc_fwd(flow.data_ptr<float>(), mask.data_ptr(), mask_kind(mask),
                               out.data_ptr<float>(), (int)B, (int)H, (int)W, cur_stream());
     return out;
   }
@@ -472,14 +471,11 @@ std::vector<Tensor> convex_up_bwd(const Tensor& flow, const Tensor& mask, const 
   Tensor dflow = at::empty_like(flow);
   Tensor wbuf = at::empty({B, 18, H, W}, flow.options());
   const int64_t HW = H * W;
-  if (nhwc && mask_kind(mask) == 1 && aligned16(flow) && aligned16(mask) && aligned16(dout) &&
-      aligned16(dmask) && aligned16(dflow)) {
-    launch_convex_up_nhwc_bwd(flow.data_ptr<float>(),
-                              reinterpret_cast<const uint16_t*>(mask.data_ptr<at::BFloat16>()),
-                              dout.data_ptr<float>(),
-                              reinterpret_cast<uint16_t*>(dmask.data_ptr<at::BFloat16>()),
-                              wbuf.data_ptr<float>(), dflow.data_ptr<float>(), (int)B, (int)H,
-                              (int)W, cur_stream());
+  if (nhwc && mask.is_contiguous() && dmask.is_contiguous() && aligned16(flow) && aligned16(mask) &&
+      aligned16(dout) && aligned16(dmask) && aligned16(dflow)) {
+    launch_convex_up_nhwc_bwd(flow.data_ptr<float>(), mask.data_ptr(), mask_kind(mask),
+                              dout.data_ptr<float>(), dmask.data_ptr(), wbuf.data_ptr<float>(),
+                              dflow.data_ptr<float>(), (int)B, (int)H, (int)W, cur_stream());
     return {dflow, dmask};
   }
   launch_convex_up_bwd(flow.data_ptr<float>(), mask.data_ptr(), mask_kind(mask), 576 * HW,
@@ -1205,6 +1201,18 @@ void check_pc(const Tensor& t, int64_t P, int64_t C, at::ScalarType st, const ch
 }
 
 // out[:, o_off:o_off+C] (bf16) = g[:, g_off:g_off+C] * scale * [y[:, y_off:] > 0]
+void split_hilo_(const Tensor& x, const Tensor& out) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4, "x: fp32 (B,C,H,W)");
+  const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  check_nhwc(out, B, H, W, "split_hilo out", at::kBFloat16);
+  const int64_t cp = out.size(3) / 2;
+  TORCH_CHECK(out.size(3) % 2 == 0 && cp % 8 == 0 && cp >= C, "out must be (B,H,W,2cp), cp >= C, cp % 8 == 0");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 31) && out.numel() < (int64_t(1) << 31), "split_hilo: tensor too large");
+  c10::DeviceGuard gd(x.device());
+  launch_split_hilo(x.data_ptr<float>(), x.stride(0), x.stride(1), x.stride(2), x.stride(3), (int)B,
+                    (int)C, (int)H, (int)W, (int)cp, bf16m(out), cur_stream());
+}
+
 void relu_bwd_(const Tensor& g, int64_t g_off, const c10::optional<Tensor>& y, int64_t y_off,
                const Tensor& out, int64_t o_off, int64_t C, double scale) {
   TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.scalar_type() == at::kFloat && g.dim() == 4, "g: fp32 NHWC");
@@ -1458,6 +1466,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_window_grad(Tensor coords, Tensor dout, int levels, int radius) -> Tensor");
   m.def("corr_window_reduce(Tensor[] coords, Tensor[] wgs, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16=False) -> Tensor");
   m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off, int[] gate_mode, Tensor[] gate_t) -> ()");
+  m.def("split_hilo_(Tensor x, Tensor(a!) out) -> ()");
   m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale) -> ()");
   m.def("gru_q_bwd_(Tensor dh, Tensor z, Tensor q, Tensor hprev, Tensor(a!) dpre_q, Tensor(b!) dz, Tensor(c!) dhprev) -> ()");
   m.def("gru_zr_bwd_(Tensor drh, Tensor dz, Tensor z, Tensor r, Tensor hprev, Tensor(a!) dpre_zr, Tensor(b!) dhprev) -> ()");
@@ -1510,6 +1519,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("corr_window_reduce", &corr_window_reduce);
   m.impl("conv_dgrad_", &conv_dgrad_);
   m.impl("relu_bwd_", &relu_bwd_);
+  m.impl("split_hilo_", &split_hilo_);
   m.impl("gru_q_bwd_", &gru_q_bwd_);
   m.impl("gru_zr_bwd_", &gru_zr_bwd_);
   m.impl("flow_prep_", &flow_prep_);

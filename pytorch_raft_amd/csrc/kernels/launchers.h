@@ -217,6 +217,9 @@ bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, float* db, h
 void launch_col_sum(const uint16_t* g, int stride, int cout, int P, float* db, hipStream_t stream);
 
 // ---- fused update-block elementwise kernels (update_ew.hip)
+// fp32 (B,C,H,W) any strides -> (B,H,W,2cp) bf16 [hi | lo], zero padded (ops/conv_fp32.py)
+void launch_split_hilo(const float* x, int64_t sb, int64_t sc, int64_t sh, int64_t sw, int B, int C,
+                       int H, int W, int cp, uint16_t* out, hipStream_t stream);
 void launch_relu_bwd(const float* g, int gs, const uint16_t* y, int ys, uint16_t* out, int os, int P,
                      int C, float scale, hipStream_t stream);
 void launch_gru_q_bwd(const float* dh, const uint16_t* z, const uint16_t* q, const uint16_t* hprev,
@@ -283,11 +286,11 @@ bool launch_corr_window_reduce(const WinList& wl, int levels, int B, int H, int 
                                float inv_sqrt_c, void* out, int out_bf16, hipStream_t stream);
 
 // ---- NHWC convex upsample (upsample.hip)
-bool launch_convex_up_nhwc_fwd(const float* flow, const uint16_t* mask, float* out, int B, int H,
-                               int W, hipStream_t stream);
-bool launch_convex_up_nhwc_bwd(const float* flow, const uint16_t* mask, const float* dout,
-                               uint16_t* dmask, float* wbuf, float* dflow, int B, int H, int W,
-                               hipStream_t stream);
+bool launch_convex_up_nhwc_fwd(const float* flow, const void* mask, int mask_is_bf16, float* out,
+                               int B, int H, int W, hipStream_t stream);
+bool launch_convex_up_nhwc_bwd(const float* flow, const void* mask, int mask_is_bf16,
+                               const float* dout, void* dmask, float* wbuf, float* dflow, int B,
+                               int H, int W, hipStream_t stream);
 
 // ---- encoder norm + activation, NHWC bf16 (encoder_norm.hip)
 // mode: 0 instance, 1 batch (training statistics), 2 batch (running statistics), 3 none

@@ -170,6 +170,56 @@ __global__ __launch_bounds__(256) void sum_bf16_kernel(BfPtrs ins, int n, const 
   }
 }
 
+// fp32 (B, C, H, W) tensor of any strides -> NHWC bf16 pair buffer [x_hi | x_lo] (B, H, W, 2 cp),
+// x_hi = bf16(x), x_lo = bf16(x - x_hi), channels [C, cp) of both halves zero: the operand image of
+// the split-bf16 fp32 convs (ops/conv_fp32.py).  A workgroup moves a 64-pixel x 64-channel tile
+// through LDS, read with lanes along whichever of pixels / channels is contiguous in the input,
+// written as 16-B vectors of 8 channels (8 consecutive lanes = one pixel's 128-B row).
+__global__ __launch_bounds__(256) void split_hilo_kernel(const float* __restrict__ x, int64_t sb,
+                                                         int64_t sc, int64_t sh, int64_t sw, int B,
+                                                         int C, int H, int W, int cp,
+                                                         uint16_t* __restrict__ out,
+                                                         int chan_fast) {
+  __shared__ float tile[64][65];
+  const int HW = H * W;
+  const int64_t P = (int64_t)B * HW;
+  const int64_t p0 = (int64_t)blockIdx.x * 64;
+  const int c0 = blockIdx.y * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int pl = chan_fast ? i / 64 : i % 64, cl = chan_fast ? i % 64 : i / 64;
+    const int64_t p = p0 + pl;
+    const int c = c0 + cl;
+    float v = 0.f;
+    if (p < P && c < C) {
+      const int b = (int)(p / HW), r = (int)(p - (int64_t)b * HW), y = r / W, xx = r - y * W;
+      v = x[b * sb + c * sc + y * sh + xx * sw];
+    }
+    tile[cl][pl] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 8; i += 256) {
+    const int pl = i / 8, g = i % 8;
+    const int64_t p = p0 + pl;
+    const int c = c0 + g * 8;
+    if (p >= P || c >= cp) continue;
+    float f[8], lo[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      f[k] = tile[g * 8 + k][pl];
+      lo[k] = f[k] - raft_bf16_to_f32(raft_f32_to_bf16(f[k]));
+    }
+    uint32_t wh[4], wl[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      wh[k] = (uint32_t)raft_f32_to_bf16(f[2 * k]) | ((uint32_t)raft_f32_to_bf16(f[2 * k + 1]) << 16);
+      wl[k] = (uint32_t)raft_f32_to_bf16(lo[2 * k]) | ((uint32_t)raft_f32_to_bf16(lo[2 * k + 1]) << 16);
+    }
+    uint16_t* o = out + p * (2 * cp) + c;
+    *reinterpret_cast<uint4*>(o) = make_uint4(wh[0], wh[1], wh[2], wh[3]);
+    *reinterpret_cast<uint4*>(o + cp) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+  }
+}
+
 inline unsigned ew_blocks(int64_t total) {
   return (unsigned)std::min<int64_t>((total + 255) / 256, 256 * 16);
 }
@@ -214,4 +264,12 @@ void launch_f1_patch(const float* flow, uint16_t* patch, uint16_t* slot, int slo
   const int64_t total = (int64_t)B * H * W * 16;
   hipLaunchKernelGGL(f1_patch_kernel, dim3(ew_blocks(total)), dim3(256), 0, stream, flow, patch, slot,
                      slot_stride, B, H, W);
+}
+
+void launch_split_hilo(const float* x, int64_t sb, int64_t sc, int64_t sh, int64_t sw, int B, int C,
+                       int H, int W, int cp, uint16_t* out, hipStream_t stream) {
+  const int64_t P = (int64_t)B * H * W;
+  dim3 grid((unsigned)raft_cdiv(P, 64), (unsigned)raft_cdiv(cp, 64));
+  hipLaunchKernelGGL(split_hilo_kernel, grid, dim3(256), 0, stream, x, sb, sc, sh, sw, B, C, H, W, cp,
+                     out, sc == 1 ? 1 : 0);
 }

@@ -175,10 +175,33 @@ __device__ __forceinline__ void cell_flows(const float* F, int64_t HW, int y, in
   }
 }
 
-// 16 lanes per cell, 4 consecutive sub-pixels per lane (4 cells per wave): 8-B mask reads,
-// 16-B output stores
+// 4 consecutive mask channels of a NHWC row: bf16 (8-B access) or fp32 (16-B access; the fp32
+// model's mask head writes NHWC fp32)
+__device__ __forceinline__ void mask_ld4(const uint16_t* p, float (&v)[4]) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  v[0] = __uint_as_float(u.x << 16);
+  v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16);
+  v[3] = __uint_as_float(u.y & 0xffff0000u);
+}
+__device__ __forceinline__ void mask_ld4(const float* p, float (&v)[4]) {
+  const float4 u = *reinterpret_cast<const float4*>(p);
+  v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
+}
+__device__ __forceinline__ void mask_st4(uint16_t* p, const float (&v)[4]) {
+  *reinterpret_cast<uint2*>(p) =
+      make_uint2((uint32_t)raft_f32_to_bf16(v[0]) | ((uint32_t)raft_f32_to_bf16(v[1]) << 16),
+                 (uint32_t)raft_f32_to_bf16(v[2]) | ((uint32_t)raft_f32_to_bf16(v[3]) << 16));
+}
+__device__ __forceinline__ void mask_st4(float* p, const float (&v)[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// 16 lanes per cell, 4 consecutive sub-pixels per lane (4 cells per wave): 8-B (bf16) / 16-B
+// (fp32) mask reads, 16-B output stores
+template <typename TM>
 __global__ __launch_bounds__(256) void convex_up_nhwc_fwd_kernel(const float* __restrict__ flow,
-                                                                 const uint16_t* __restrict__ mask,
+                                                                 const TM* __restrict__ mask,
                                                                  float* __restrict__ out, int B,
                                                                  int H, int W) {
   const int q = threadIdx.x & 15;
@@ -189,15 +212,11 @@ __global__ __launch_bounds__(256) void convex_up_nhwc_fwd_kernel(const float* __
   const int yx = (int)(cell - b * HW), y = yx / W, x = yx % W;
   float nf[9][2];
   cell_flows(flow + b * 2 * HW, HW, y, x, H, W, nf);
-  const uint16_t* M = mask + cell * 576 + 4 * q;
+  const TM* M = mask + cell * 576 + 4 * q;
   float m[9][4], mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    const uint2 v = *reinterpret_cast<const uint2*>(M + k * 64);
-    m[k][0] = __uint_as_float(v.x << 16);
-    m[k][1] = __uint_as_float(v.x & 0xffff0000u);
-    m[k][2] = __uint_as_float(v.y << 16);
-    m[k][3] = __uint_as_float(v.y & 0xffff0000u);
+    mask_ld4(M + k * 64, m[k]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) mx[j] = fmaxf(mx[j], m[k][j]);
   }
@@ -226,10 +245,11 @@ __global__ __launch_bounds__(256) void convex_up_nhwc_fwd_kernel(const float* __
 // 16 lanes per cell, 4 consecutive sub-pixels per lane (4 cells per wave): the mask / dmask rows
 // move as 8-B pieces, dout as 16-B pieces, and the 18 neighbour-weight sums are reduced over the
 // lane's 4 sub-pixels in registers first, leaving 4 shuffle steps per sum (was 6 over 64 lanes).
+template <typename TM>
 __global__ __launch_bounds__(256) void convex_up_nhwc_bwd_kernel(const float* __restrict__ flow,
-                                                                 const uint16_t* __restrict__ mask,
+                                                                 const TM* __restrict__ mask,
                                                                  const float* __restrict__ dout,
-                                                                 uint16_t* __restrict__ dmask,
+                                                                 TM* __restrict__ dmask,
                                                                  float* __restrict__ wbuf, int B,
                                                                  int H, int W) {
   const int q = threadIdx.x & 15;
@@ -240,15 +260,11 @@ __global__ __launch_bounds__(256) void convex_up_nhwc_bwd_kernel(const float* __
   const int yx = (int)(cell - b * HW), y = yx / W, x = yx % W;
   float nf[9][2];
   cell_flows(flow + b * 2 * HW, HW, y, x, H, W, nf);
-  const uint16_t* M = mask + cell * 576 + 4 * q;
+  const TM* M = mask + cell * 576 + 4 * q;
   float p[9][4], mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    const uint2 v = *reinterpret_cast<const uint2*>(M + k * 64);
-    p[k][0] = __uint_as_float(v.x << 16);
-    p[k][1] = __uint_as_float(v.x & 0xffff0000u);
-    p[k][2] = __uint_as_float(v.y << 16);
-    p[k][3] = __uint_as_float(v.y & 0xffff0000u);
+    mask_ld4(M + k * 64, p[k]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) mx[j] = fmaxf(mx[j], p[k][j]);
   }
@@ -277,14 +293,12 @@ __global__ __launch_bounds__(256) void convex_up_nhwc_bwd_kernel(const float* __
       dot[j] += p[k][j] * g[k][j];
     }
   }
-  uint16_t* DM = dmask + cell * 576 + 4 * q;
+  TM* DM = dmask + cell * 576 + 4 * q;
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    uint32_t lo = (uint32_t)raft_f32_to_bf16(p[k][0] * (g[k][0] - dot[0])) |
-                  ((uint32_t)raft_f32_to_bf16(p[k][1] * (g[k][1] - dot[1])) << 16);
-    uint32_t hi = (uint32_t)raft_f32_to_bf16(p[k][2] * (g[k][2] - dot[2])) |
-                  ((uint32_t)raft_f32_to_bf16(p[k][3] * (g[k][3] - dot[3])) << 16);
-    *reinterpret_cast<uint2*>(DM + k * 64) = make_uint2(lo, hi);
+    const float dm[4] = {p[k][0] * (g[k][0] - dot[0]), p[k][1] * (g[k][1] - dot[1]),
+                         p[k][2] * (g[k][2] - dot[2]), p[k][3] * (g[k][3] - dot[3])};
+    mask_st4(DM + k * 64, dm);
   }
   // neighbour weights W[k][c] = sum_s p_k d_c: the lane's 4 sub-pixels, then its 16-lane group
 #pragma unroll
@@ -305,20 +319,30 @@ __global__ __launch_bounds__(256) void convex_up_nhwc_bwd_kernel(const float* __
 
 }  // namespace
 
-bool launch_convex_up_nhwc_fwd(const float* flow, const uint16_t* mask, float* out, int B, int H,
-                               int W, hipStream_t stream) {
+bool launch_convex_up_nhwc_fwd(const float* flow, const void* mask, int mask_is_bf16, float* out,
+                               int B, int H, int W, hipStream_t stream) {
   const int64_t cells = (int64_t)B * H * W;
-  hipLaunchKernelGGL(convex_up_nhwc_fwd_kernel, dim3(raft_cdiv(cells, 16)), dim3(256), 0, stream,
-                     flow, mask, out, B, H, W);
+  if (mask_is_bf16)
+    hipLaunchKernelGGL(convex_up_nhwc_fwd_kernel<uint16_t>, dim3(raft_cdiv(cells, 16)), dim3(256), 0,
+                       stream, flow, static_cast<const uint16_t*>(mask), out, B, H, W);
+  else
+    hipLaunchKernelGGL(convex_up_nhwc_fwd_kernel<float>, dim3(raft_cdiv(cells, 16)), dim3(256), 0,
+                       stream, flow, static_cast<const float*>(mask), out, B, H, W);
   return true;
 }
 
-bool launch_convex_up_nhwc_bwd(const float* flow, const uint16_t* mask, const float* dout,
-                               uint16_t* dmask, float* wbuf, float* dflow, int B, int H, int W,
-                               hipStream_t stream) {
+bool launch_convex_up_nhwc_bwd(const float* flow, const void* mask, int mask_is_bf16,
+                               const float* dout, void* dmask, float* wbuf, float* dflow, int B,
+                               int H, int W, hipStream_t stream) {
   const int64_t cells = (int64_t)B * H * W;
-  hipLaunchKernelGGL(convex_up_nhwc_bwd_kernel, dim3(raft_cdiv(cells, 16)), dim3(256), 0, stream,
-                     flow, mask, dout, dmask, wbuf, B, H, W);
+  if (mask_is_bf16)
+    hipLaunchKernelGGL(convex_up_nhwc_bwd_kernel<uint16_t>, dim3(raft_cdiv(cells, 16)), dim3(256), 0,
+                       stream, flow, static_cast<const uint16_t*>(mask), dout,
+                       static_cast<uint16_t*>(dmask), wbuf, B, H, W);
+  else
+    hipLaunchKernelGGL(convex_up_nhwc_bwd_kernel<float>, dim3(raft_cdiv(cells, 16)), dim3(256), 0,
+                       stream, flow, static_cast<const float*>(mask), dout, static_cast<float*>(dmask),
+                       wbuf, B, H, W);
   hipLaunchKernelGGL(convex_up_bwd_flow_kernel, dim3(raft_cdiv(cells, 256)), dim3(256), 0, stream,
                      wbuf, dflow, B, H, W);
   return true;

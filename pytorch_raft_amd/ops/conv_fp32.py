@@ -43,13 +43,14 @@ _ENV_ON = os.environ.get('RAFT_FP32_MFMA', '1') != '0'
 @contextlib.contextmanager
 def enabled(on=True):
     """Route MfmaConv2d modules through the split-bf16 MFMA conv inside the block (one decode)."""
-    prev = _ACTIVE['on'], _ACTIVE.get('packed')
+    prev = _ACTIVE['on'], _ACTIVE.get('packed'), _ACTIVE.get('mods')
     _ACTIVE['on'] = bool(on)
     _ACTIVE['packed'] = {}
+    _ACTIVE['mods'] = {}   # module -> _ModState of this decode (weight token, deferred wgrad)
     try:
         yield
     finally:
-        _ACTIVE['on'], _ACTIVE['packed'] = prev
+        _ACTIVE['on'], _ACTIVE['packed'], _ACTIVE['mods'] = prev
 
 
 def active_for(x, weight):
@@ -57,14 +58,25 @@ def active_for(x, weight):
             weight.dtype == torch.float32 and x.dim() == 4 and not torch.is_autocast_enabled())
 
 
-def _split_nhwc(x, cpad):
-    """(B, C, H, W) fp32 -> (B, H, W, 2 cpad) bf16 [hi | lo] (zero padded)."""
+def _split_nhwc_torch(x, cpad):
+    """Reference formulation of :func:`_split_nhwc` (CPU tensors; the kernel's oracle)."""
     b, c, h, w = x.shape
     xn = x.permute(0, 2, 3, 1)
     hi = xn.to(torch.bfloat16)
     buf = torch.zeros(b, h, w, 2 * cpad, device=x.device, dtype=torch.bfloat16)
     buf[..., :c] = hi
     buf[..., cpad:cpad + c] = (xn - hi.float()).to(torch.bfloat16)
+    return buf
+
+
+def _split_nhwc(x, cpad):
+    """(B, C, H, W) fp32 (any strides) -> (B, H, W, 2 cpad) bf16 [hi | lo] (zero padded): on the
+    GPU ONE pass of the split_hilo kernel (LDS-tiled transpose when x is NCHW)."""
+    if not x.is_cuda:
+        return _split_nhwc_torch(x, cpad)
+    b, c, h, w = x.shape
+    buf = torch.empty(b, h, w, 2 * cpad, device=x.device, dtype=torch.bfloat16)
+    _ext.ops().split_hilo_(x, buf)
     return buf
 
 
@@ -96,29 +108,157 @@ def _packed(cache, weight, cpad, adjoint):
     return w
 
 
+class _ModState:
+    """One MfmaConv2d module within one decode: its detached parameters, their split packs, and
+    the (split output gradient, split input) pairs of every call, whose weight / bias gradients
+    are computed in ONE batched launch pair when the module's token node runs (after the last
+    call's backward) instead of per iteration."""
+
+    def __init__(self, weight, bias, pad, cache):
+        self.weight = weight.detach()
+        self.bias = None if bias is None else bias.detach()
+        self.pad = pad
+        self.cache = cache
+        self.items = []
+        self.tok = None
+
+
+class _WeightSink(torch.autograd.Function):
+    """Token standing for a module's weight and bias in the decode: every call takes it as input
+    (returning no gradient for it), so its backward runs once, after all of them."""
+
+    @staticmethod
+    def forward(ctx, st, weight, bias):
+        ctx.st = st
+        ctx.has_bias = bias is not None
+        return weight.new_zeros(())
+
+    @staticmethod
+    def backward(ctx, _g):
+        st = ctx.st
+        dw, db = _flush_wgrad(st)
+        st.items = []
+        return None, dw, (db if ctx.has_bias else None)
+
+
+def _flush_wgrad(st):
+    cout, cin, kh, kw = st.weight.shape
+    dev = st.weight.device
+    if not st.items:
+        return torch.zeros_like(st.weight), torch.zeros(cout, device=dev)
+    k = kh * kw
+    cp = st.items[0][1].shape[-1] // 2
+    cop = st.items[0][0].shape[-1] // 2
+    d1 = torch.zeros(cout, k * 2 * cp, device=dev)    # g_hi x [x_hi | x_lo]
+    d2 = torch.zeros(cout, k * cp, device=dev)        # g_lo x x_hi
+    db = torch.zeros(cout, device=dev)                # sum(g_hi) + sum(g_lo)
+    if C._taps_ok([0, cp], [cp, cp], (kh, kw)):
+        for i in range(0, len(st.items), C.MAX_WG_ITEMS):
+            chunk = st.items[i:i + C.MAX_WG_ITEMS]
+            C.conv_wgrad_multi([(gs, [xs, xs]) for gs, xs in chunk], 0, [0, cp], [cp, cp], (kh, kw),
+                               st.pad, cout, d1, db)
+            C.conv_wgrad_multi([(gs, [xs]) for gs, xs in chunk], cop, [0], [cp], (kh, kw), st.pad,
+                               cout, d2, db)
+    else:  # convf1's 7x7 over a 64-channel slot: the tile kernel, per item
+        for gs, xs in st.items:
+            C.conv_wgrad(gs, 0, [(xs, 0, cp), (xs, cp, cp)], (kh, kw), st.pad, cout, d1, db)
+            C.conv_wgrad(gs, cop, [(xs, 0, cp)], (kh, kw), st.pad, cout, d2, db)
+    g1 = C.unpack_weight_grad(d1, cout, [cin, cin], [cp, cp], (kh, kw))
+    dw = g1[:, :cin] + g1[:, cin:] + C.unpack_weight_grad(d2, cout, [cin], [cp], (kh, kw))
+    return dw, db
+
+
+def _split_conv_fwd(x, weight, bias, pad, cache):
+    b, cin, h, w = x.shape
+    cout, _, kh, kw = weight.shape
+    cp = C.round_up(cin, 64)
+    xs = _split_nhwc(x, cp)
+    # NHWC fp32 output (row-contiguous epilogue stores), handed on as a channels_last tensor: the
+    # next conv's split then reads it channel-contiguous
+    out = torch.empty(b, cout, h, w, device=x.device, dtype=torch.float32,
+                      memory_format=torch.channels_last)
+    C.conv_fwd([(xs, 0, cp), (xs, cp, cp), (xs, 0, cp)], _packed(cache, weight, cp, False),
+               None if bias is None else bias.contiguous(), (kh, kw), pad, cout,
+               C.EPI_F32, [out.permute(0, 2, 3, 1)], [0])
+    return out, xs
+
+
+class _SplitConvTok(torch.autograd.Function):
+    """Split-bf16 conv of one call: forward, input gradient here; the weight / bias gradient is
+    deferred to the module's token node (_WeightSink)."""
+
+    @staticmethod
+    def forward(ctx, x, tok, st):
+        out, xs = _split_conv_fwd(x, st.weight, st.bias, st.pad, st.cache)
+        ctx.save_for_backward(xs)
+        ctx.st = st
+        ctx.cin = x.shape[1]
+        return out   # not a view: the update block applies in-place ReLUs to it
+
+    @staticmethod
+    def backward(ctx, g):
+        (xs,) = ctx.saved_tensors
+        st = ctx.st
+        b, cout, h, w = g.shape
+        cin = ctx.cin
+        _, _, kh, kw = st.weight.shape
+        cop = C.round_up(cout, 64)
+        gs = _split_nhwc(g, cop)
+        st.items.append((gs, xs))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(b, cin, h, w, device=g.device, dtype=torch.float32,
+                             memory_format=torch.channels_last)
+            C.conv_fwd([(gs, 0, cop), (gs, cop, cop), (gs, 0, cop)], _packed(st.cache, st.weight, cop, True),
+                       None, (kh, kw), st.pad, cin, C.EPI_F32, [dx.permute(0, 2, 3, 1)], [0])
+        return dx, None, None
+
+
+def module_conv2d(mod, x):
+    """MfmaConv2d forward while the split path is active: per decode, a module's calls share one
+    weight token (batched weight gradients) and its packed split weights."""
+    _ext.gpu_path_enabled(required=True)
+    pad = tuple(int(p) for p in mod.padding)
+    cache = _ACTIVE.get('packed')
+    cache = {} if cache is None else cache
+    need_w = mod.weight.requires_grad or (mod.bias is not None and mod.bias.requires_grad)
+    if not (torch.is_grad_enabled() and (need_w or x.requires_grad)):
+        return _split_conv_fwd(x, mod.weight.detach(), None if mod.bias is None else mod.bias.detach(),
+                               pad, cache)[0]
+    mods = _ACTIVE.get('mods')
+    if mods is None:   # outside an enabled() scope (tests): a token per call
+        mods = {}
+    st = mods.get(id(mod))
+    if st is None:
+        st = mods[id(mod)] = _ModState(mod.weight, mod.bias, pad, cache)
+        st.tok = _WeightSink.apply(st, mod.weight, mod.bias)
+    return _SplitConvTok.apply(x, st.tok, st)
+
+
 class _SplitConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, pad):
-        x = x.contiguous()
         b, cin, h, w = x.shape
         cout, _, kh, kw = weight.shape
         cp = C.round_up(cin, 64)
         xs = _split_nhwc(x, cp)
-        out = torch.empty(b, cout, h, w, device=x.device, dtype=torch.float32)
+        # NHWC fp32 output (row-contiguous epilogue stores), handed on as a channels_last tensor:
+        # the next conv's split then reads it channel-contiguous
+        out = torch.empty(b, cout, h, w, device=x.device, dtype=torch.float32,
+                          memory_format=torch.channels_last)
         cache = _ACTIVE.get('packed')
         cache = {} if cache is None else cache
         ctx.packed = cache
         C.conv_fwd([(xs, 0, cp), (xs, cp, cp), (xs, 0, cp)], _packed(cache, weight, cp, False),
                    None if bias is None else bias.contiguous(), (kh, kw), pad, cout,
-                   C.EPI_F32_NCHW, [out], [0])
+                   C.EPI_F32, [out.permute(0, 2, 3, 1)], [0])
         ctx.save_for_backward(xs, weight)
         ctx.pad, ctx.cin, ctx.has_bias = pad, cin, bias is not None
-        return out
+        return out   # not a view: the update block applies in-place ReLUs to it
 
     @staticmethod
     def backward(ctx, g):
         xs, weight = ctx.saved_tensors
-        g = g.contiguous()
         b, cout, h, w = g.shape
         cin, pad = ctx.cin, ctx.pad
         _, _, kh, kw = weight.shape
@@ -127,9 +267,10 @@ class _SplitConv(torch.autograd.Function):
         gs = _split_nhwc(g, cop)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.empty(b, cin, h, w, device=g.device, dtype=torch.float32)
+            dx = torch.empty(b, cin, h, w, device=g.device, dtype=torch.float32,
+                             memory_format=torch.channels_last)
             C.conv_fwd([(gs, 0, cop), (gs, cop, cop), (gs, 0, cop)], _packed(ctx.packed, weight, cop, True), None,
-                       (kh, kw), pad, cin, C.EPI_F32_NCHW, [dx], [0])
+                       (kh, kw), pad, cin, C.EPI_F32, [dx.permute(0, 2, 3, 1)], [0])
         if ctx.needs_input_grad[1]:
             k = kh * kw
             d1 = torch.zeros(cout, k * 2 * cp, device=g.device)    # g_hi x [x_hi | x_lo]

@@ -38,6 +38,10 @@ def convex_upsample(flow, mask, impl='auto', nhwc=False):
     """``mask`` is (B,576,H,W), or (B,H,W,576) with ``nhwc=True`` (the fused update block's layout)."""
     if impl != 'torch' and _ext.device_ok(flow) and _ext.gpu_path_enabled(required=(impl == 'hip')):
         out_dtype = torch.promote_types(flow.dtype, mask.dtype)
+        if (not nhwc and mask.dim() == 4 and not mask.is_contiguous() and
+                mask.is_contiguous(memory_format=torch.channels_last)):
+            # channels_last mask (the fp32 model's NHWC conv outputs): the NHWC kernel, no copy
+            mask, nhwc = mask.permute(0, 2, 3, 1), True
         out = _ConvexUpsample.apply(flow, mask, nhwc)
         return out if out_dtype == torch.float32 else out.to(out_dtype)
     if nhwc:

@@ -1,0 +1,11 @@
+#!/bin/bash
+# large-batch training sweep (HBM headroom): per-GPU batch 96 / 192 / 384, all-pairs vs on-the-fly
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+mkdir -p gpurun_out/sweep
+for cfg in "96 allpairs" "96 onthefly" "192 allpairs" "192 onthefly" "384 onthefly"; do
+  set -- $cfg
+  timeout -k 10 300 python bench.py --batch $1 --corr_mode $2 --steps 10 --warmup 3 > gpurun_out/sweep/train_b$1_$2.log 2>&1 || { tail -3 gpurun_out/sweep/train_b$1_$2.log; exit 1; }
+  echo "b$1 $2: $(grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*\|"peak_hbm_gib_rank0": [0-9.]*\|"peak_reserved_gib_rank0": [0-9.]*' gpurun_out/sweep/train_b$1_$2.log | tr '\n' ' ')"
+done

@@ -307,22 +307,32 @@ def test_lookup_nhwc_window_backward(ext_ops, hw, precision):
     torch.testing.assert_close(f2.grad, g2_ref, atol=tol, rtol=3e-3 if precision == 'fp32' else 2e-2)
 
 
+@pytest.mark.parametrize('mask_dtype', [torch.bfloat16, torch.float32, 'channels_last'])
 @pytest.mark.parametrize('hw', [(8, 9), (46, 62)])
-def test_convex_upsample_nhwc(ext_ops, hw):
+def test_convex_upsample_nhwc(ext_ops, hw, mask_dtype):
+    """NHWC mask: bf16 (fused bf16 block), fp32 (B,H,W,576), and an fp32 channels_last
+    (B,576,H,W) tensor -- the fp32 model's mask head output, routed to the NHWC kernel."""
     h, w = hw
     b = 2
     flow = torch.randn(b, 2, h, w, device=DEV, requires_grad=True)
-    mask = (3 * torch.randn(b, h, w, 576, device=DEV)).to(torch.bfloat16).requires_grad_(True)
-    ref = torch_convex_upsample(flow, mask.float().permute(0, 3, 1, 2))
+    m = 3 * torch.randn(b, h, w, 576, device=DEV)
+    if mask_dtype == 'channels_last':
+        mask = m.permute(0, 3, 1, 2).requires_grad_(True)   # (B,576,H,W), channels_last strides
+        nhwc, ref_mask = False, mask
+    else:
+        mask = m.to(mask_dtype).requires_grad_(True)
+        nhwc, ref_mask = True, mask.float().permute(0, 3, 1, 2)
+    ref = torch_convex_upsample(flow, ref_mask)
     g = torch.randn_like(ref)
     (ref * g).sum().backward()
     gf_ref, gm_ref = flow.grad.clone(), mask.grad.clone().float()
     flow.grad = mask.grad = None
-    out = convex_upsample(flow, mask, impl='hip', nhwc=True)
+    out = convex_upsample(flow, mask, impl='hip', nhwc=nhwc)
     torch.testing.assert_close(out.float(), ref, atol=1e-4, rtol=1e-4)
     (out.float() * g).sum().backward()
     torch.testing.assert_close(flow.grad, gf_ref, atol=1e-3, rtol=1e-4)
-    torch.testing.assert_close(mask.grad.float(), gm_ref, atol=2e-2, rtol=2e-2)
+    tol = 2e-2 if mask_dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(mask.grad.float(), gm_ref, atol=tol, rtol=tol)
 
 
 @pytest.mark.parametrize('radius,levels,hw', [(4, 4, (46, 62)), (3, 4, (24, 31)), (4, 3, (13, 19))])
