@@ -1201,6 +1201,30 @@ void check_pc(const Tensor& t, int64_t P, int64_t C, at::ScalarType st, const ch
 }
 
 // out[:, o_off:o_off+C] (bf16) = g[:, g_off:g_off+C] * scale * [y[:, y_off:] > 0]
+// stride-1 3x3 conv, 64 -> 64 channels, NHWC bf16 (the encoders' layer1; forward, or the input
+// gradient with the adjoint weight pack)
+void conv_enc64_(const Tensor& x, const Tensor& wpk, const Tensor& out) {
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 64, "x must be (B,H,W,64)");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2);
+  check_nhwc(x, B, H, W, "conv_enc64 input", at::kBFloat16);
+  check_nhwc(out, B, H, W, "conv_enc64 output", at::kBFloat16);
+  TORCH_CHECK(out.size(3) == 64, "out must be (B,H,W,64)");
+  TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == at::kBFloat16 &&
+                  wpk.dim() == 2 && wpk.size(0) == 64 && wpk.size(1) == 9 * 64,
+              "packed weight must be a contiguous bf16 (64, 576) tensor");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 31), "conv_enc64: input too large");
+  c10::DeviceGuard gd(x.device());
+  static const int cus = [] {
+    hipDeviceProp_t p{};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
+  }();
+  TORCH_CHECK(launch_conv_enc64(bf16p(x), bf16p(wpk), bf16m(out), (int)B, (int)H, (int)W, cus,
+                                cur_stream()),
+              "conv_enc64 launch failed");
+}
+
 void split_hilo_(const Tensor& x, const Tensor& out) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.dim() == 4, "x: fp32 (B,C,H,W)");
   const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -1467,6 +1491,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_window_reduce(Tensor[] coords, Tensor[] wgs, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16=False) -> Tensor");
   m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off, int[] gate_mode, Tensor[] gate_t) -> ()");
   m.def("split_hilo_(Tensor x, Tensor(a!) out) -> ()");
+  m.def("conv_enc64_(Tensor x, Tensor wpk, Tensor(a!) out) -> ()");
   m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale) -> ()");
   m.def("gru_q_bwd_(Tensor dh, Tensor z, Tensor q, Tensor hprev, Tensor(a!) dpre_q, Tensor(b!) dz, Tensor(c!) dhprev) -> ()");
   m.def("gru_zr_bwd_(Tensor drh, Tensor dz, Tensor z, Tensor r, Tensor hprev, Tensor(a!) dpre_zr, Tensor(b!) dhprev) -> ()");
@@ -1520,6 +1545,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("conv_dgrad_", &conv_dgrad_);
   m.impl("relu_bwd_", &relu_bwd_);
   m.impl("split_hilo_", &split_hilo_);
+  m.impl("conv_enc64_", &conv_enc64_);
   m.impl("gru_q_bwd_", &gru_q_bwd_);
   m.impl("gru_zr_bwd_", &gru_zr_bwd_);
   m.impl("flow_prep_", &flow_prep_);

@@ -1,0 +1,170 @@
+// Stride-1 3x3 conv for the encoders' 64 -> 64-channel layers (`core/extractor.py:22-23`, layer1 of
+// both encoders at 1/2 resolution: 184 x 248 for chairs, 12-24 images) -- forward and input
+// gradient (the same conv on the flipped / transposed weight), NHWC bf16, fp32 accumulation.
+//
+// Why a kernel of its own: at Cin = 64 the implicit GEMM has K = 9 x 64 = 576, i.e. 9 K steps, and
+// the general kernels (conv_glds.hip) re-fetch their A tile for every tap through LDS-DMA: 6 DMA
+// pieces per thread per 8 MFMAs per wave, ~110 us per call at ~20 % MFMA use (profiles/r3).
+// Here a workgroup is persistent and
+//   * keeps the whole weight matrix in LDS (64 x 576 bf16, rows padded to 1168 B: conflict-free
+//     fragment reads), loaded once;
+//   * works on 2-D tiles of 8 x 16 output pixels: the tile's 10 x 18 input halo (all 64 channels,
+//     144-B padded rows) is loaded ONCE and every tap reads its shifted rows from it -- 1.4x the
+//     tile's bytes instead of 9x;
+//   * stages the halo through registers two tiles ahead (two tiles' loads, ~46 KB per CU, in
+//     flight while a tile's 72 MFMAs per wave run);
+//   * writes the output tile through LDS as 16-B rows (per-lane 2-B stores of the MFMA layout
+//     were store-issue bound: ~115 us per call either way, profiles/r3/c2_kernel_summary.txt).
+// 4 waves as 2 (pixels) x 2 (channels): a wave owns 64 pixels (4 tile rows) x 32 channels.
+#include "common.h"
+#include "launchers.h"
+
+namespace {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+constexpr int TH = 8, TW = 16;                 // output tile
+constexpr int HH = TH + 2, HWD = TW + 2;       // halo tile
+constexpr int HROWS = HH * HWD;                // 180 halo pixels
+constexpr int AROW = 144;                      // LDS bytes per halo pixel (128 + 16 pad)
+constexpr int BROW = 1168;                     // LDS bytes per weight row (1152 + 16 pad)
+constexpr int KTOT = 9 * 64;
+constexpr int NTH = 256;
+constexpr int APIECES = HROWS * 8;             // 16-B pieces of a halo tile
+constexpr int APER = (APIECES + NTH - 1) / NTH;  // 6 per thread
+constexpr int ABUF = HROWS * AROW;             // 25,920 B
+constexpr int BBUF = 64 * BROW;                // 74,752 B
+constexpr int OROW = 144;                      // LDS bytes per staged output pixel (128 + 16 pad)
+constexpr int OBUF = TH * TW * OROW;           // 18,432 B
+
+__global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ wpk,
+                                                            uint16_t* __restrict__ out, int B,
+                                                            int H, int W, int tiles_y,
+                                                            int tiles_x) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * ABUF + BBUF + OBUF];
+  char* As = smem;                 // 2 halo buffers
+  char* Bs = smem + 2 * ABUF;      // weights
+  char* Os = Bs + BBUF;            // output tile staging (bf16 [pixel][channel])
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntiles = B * tiles_y * tiles_x;
+
+  // weights [n][tap * 64 + c] -> padded LDS rows (once per workgroup)
+  for (int e = tid; e < 64 * (KTOT / 8); e += NTH) {
+    const int n = e / (KTOT / 8), q = e - n * (KTOT / 8);
+    *reinterpret_cast<uint4*>(Bs + n * BROW + q * 16) =
+        *reinterpret_cast<const uint4*>(wpk + (int64_t)n * KTOT + q * 8);
+  }
+
+  // halo piece e = tid + j * NTH of tile t -> registers (zeros outside the image)
+  auto load_a = [&](int t, uint4 (&areg)[APER]) {
+    const int b = t / (tiles_y * tiles_x), r = t - b * tiles_y * tiles_x;
+    const int y0 = (r / tiles_x) * TH - 1, x0 = (r % tiles_x) * TW - 1;
+#pragma unroll
+    for (int j = 0; j < APER; ++j) {
+      const int e = tid + j * NTH;
+      const int hp = e >> 3, q = e & 7;
+      const int yy = y0 + hp / HWD, xx = x0 + hp % HWD;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (e < APIECES && t < ntiles && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+        v = *reinterpret_cast<const uint4*>(x + (((int64_t)b * H + yy) * W + xx) * 64 + q * 8);
+      areg[j] = v;
+    }
+  };
+  auto store_a = [&](int buf, const uint4 (&areg)[APER]) {
+#pragma unroll
+    for (int j = 0; j < APER; ++j) {
+      const int e = tid + j * NTH;
+      if (e < APIECES)
+        *reinterpret_cast<uint4*>(As + buf * ABUF + (e >> 3) * AROW + (e & 7) * 16) = areg[j];
+    }
+  };
+
+  // this lane's A rows: fragment i covers tile rows wm*4 + 2i + (lane&31)/16, column lane & 15
+  int hbase[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int tr = wm * 4 + 2 * i + ((lane & 31) >> 4), tc = lane & 15;
+    hbase[i] = (tr * HWD + tc) * AROW + (lane >> 5) * 16;
+  }
+  const int bbase = (wn * 32 + (lane & 31)) * BROW + (lane >> 5) * 16;
+
+  // two tiles of halo loads in flight per thread (HBM latency x bandwidth per CU needs ~2 tiles'
+  // 23 KB): registers R0 / R1 alternate; the loop is unrolled by two so both stay static
+  uint4 R0[APER], R1[APER];
+  const int G = gridDim.x;
+  load_a(blockIdx.x, R0);
+  load_a(blockIdx.x + G, R1);
+  auto tile = [&](int t, int buf, uint4 (&R)[APER]) {
+    store_a(buf, R);
+    __syncthreads();  // halo (and, first time, weights) visible; the other buffer is free
+    load_a(t + 2 * G, R);  // two tiles ahead, in flight during this tile and the next
+
+    f32x16 acc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    const char* Ab = As + buf * ABUF;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int shift = ((tap / 3) * HWD + tap % 3) * AROW;
+      bf16x8_t af[4][2], bfr[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        bfr[kk] = *reinterpret_cast<const bf16x8_t*>(Bs + bbase + (tap * 64 + kk * 16) * 2);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          af[kk][i] = *reinterpret_cast<const bf16x8_t*>(Ab + hbase[i] + shift + kk * 32);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bfr[kk], acc[i], 0, 0, 0);
+    }
+
+    // epilogue: the accumulators go to an LDS [pixel][channel] bf16 tile, then out as 16-B rows
+    // of 8 channels (4 stores per thread instead of 32 scattered 2-B stores per lane, whose issue
+    // set the tile time); pixels past the image edge dropped
+    const int n = wn * 32 + (lane & 31);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int p = wm * 64 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
+        *reinterpret_cast<uint16_t*>(Os + p * OROW + n * 2) = raft_f32_to_bf16(acc[i][rr]);
+      }
+    __syncthreads();  // staged tile complete (the next tile's stores come after its own barrier)
+    const int b = t / (tiles_y * tiles_x), r = t - b * tiles_y * tiles_x;
+    const int ty0 = (r / tiles_x) * TH, tx0 = (r % tiles_x) * TW;
+#pragma unroll
+    for (int j = 0; j < TH * TW * 8 / NTH; ++j) {
+      const int e = tid + j * NTH;
+      const int p = e >> 3, q = e & 7;
+      const int yy = ty0 + p / TW, xx = tx0 + p % TW;
+      if (yy < H && xx < W)
+        *reinterpret_cast<uint4*>(out + (((int64_t)b * H + yy) * W + xx) * 64 + q * 8) =
+            *reinterpret_cast<const uint4*>(Os + p * OROW + q * 16);
+    }
+  };
+  for (int t = blockIdx.x; t < ntiles; t += 2 * G) {
+    tile(t, 0, R0);
+    if (t + G < ntiles) tile(t + G, 1, R1);
+  }
+}
+
+}  // namespace
+
+// persistent grid: one workgroup per CU (144 KB of LDS each), capped by the tile count
+bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, int B, int H, int W,
+                       int grid_cap, hipStream_t stream) {
+  const int ty = (H + TH - 1) / TH, tx = (W + TW - 1) / TW;
+  const int ntiles = B * ty * tx;
+  if (ntiles <= 0) return true;
+  const int grid = ntiles < grid_cap ? ntiles : grid_cap;
+  hipLaunchKernelGGL(conv_enc64_kernel, dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B, H, W, ty,
+                     tx);
+  return true;
+}

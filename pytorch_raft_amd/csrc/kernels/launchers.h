@@ -217,6 +217,9 @@ bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, float* db, h
 void launch_col_sum(const uint16_t* g, int stride, int cout, int P, float* db, hipStream_t stream);
 
 // ---- fused update-block elementwise kernels (update_ew.hip)
+// stride-1 3x3 64 -> 64 NHWC bf16 conv (conv_enc64.hip); wpk = (64, 9*64) packed [n][tap*64 + c]
+bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, int B, int H, int W,
+                       int grid_cap, hipStream_t stream);
 // fp32 (B,C,H,W) any strides -> (B,H,W,2cp) bf16 [hi | lo], zero padded (ops/conv_fp32.py)
 void launch_split_hilo(const float* x, int64_t sb, int64_t sc, int64_t sh, int64_t sw, int B, int C,
                        int H, int W, int cp, uint16_t* out, hipStream_t stream);

@@ -305,15 +305,27 @@ class _Conv3x3WgradNative(torch.autograd.Function):
 _WGRAD_NATIVE = os.environ.get('RAFT_ENCODER_WGRAD_NATIVE', '1') != '0'
 
 
-def _conv3x3_native_fwd(x, w):
+_ENC64 = os.environ.get('RAFT_ENC64', '1') != '0'
+
+
+def _conv3x3_nhwc(xn, wpk, ci, co):
+    """NHWC bf16 stride-1 3x3 conv with a packed [co][tap * ci + c] weight: 64 -> 64 channels on
+    the persistent 2-D halo-tile kernel (conv_enc64.hip), anything else on the implicit GEMM."""
     from . import conv as C
-    B, ci, H, W = x.shape
-    co = w.shape[0]
+    B, H, W, _ = xn.shape
+    out = torch.empty(B, H, W, co, device=xn.device, dtype=torch.bfloat16)
+    if _ENC64 and ci == 64 and co == 64:
+        _ext.ops().conv_enc64_(xn, wpk, out)
+    else:
+        C.conv_fwd([(xn, 0, ci)], wpk, None, (3, 3), (1, 1), co, C.EPI_BF16, [out], [0])
+    return out
+
+
+def _conv3x3_native_fwd(x, w):
+    ci, co = x.shape[1], w.shape[0]
     xn = x.permute(0, 2, 3, 1)                     # channels_last memory: a view
     wpk = w.permute(0, 2, 3, 1).reshape(co, 9 * ci)
-    out = torch.empty(B, H, W, co, device=x.device, dtype=torch.bfloat16)
-    C.conv_fwd([(xn, 0, ci)], wpk, None, (3, 3), (1, 1), co, C.EPI_BF16, [out], [0])
-    return out.permute(0, 3, 1, 2)
+    return _conv3x3_nhwc(xn, wpk, ci, co).permute(0, 3, 1, 2)
 
 
 class _Conv3x3Native(torch.autograd.Function):
@@ -345,10 +357,13 @@ class _Conv3x3Native(torch.autograd.Function):
             # adjoint weight W'[c][tap'][o] = W[o][c][flip(tap')], in the kernels' packed layout
             wd = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
             wd = wd.permute(0, 2, 3, 1).reshape(ci, 9 * co)
-            dxn = torch.empty(B, H, W, ci, device=x.device, dtype=torch.bfloat16)
-            _ext.ops().conv_dgrad_([gn], [0], [co], wd, 3, 3, 1, 1, 0, 1.0, [dxn], [0], [ci], [ci],
-                                   [0], [dxn], [-1], [], [])
-            dx = dxn.permute(0, 3, 1, 2)
+            if _ENC64 and ci == 64 and co == 64:
+                dx = _conv3x3_nhwc(gn, wd, co, ci).permute(0, 3, 1, 2)
+            else:
+                dxn = torch.empty(B, H, W, ci, device=x.device, dtype=torch.bfloat16)
+                _ext.ops().conv_dgrad_([gn], [0], [co], wd, 3, 3, 1, 1, 0, 1.0, [dxn], [0], [ci],
+                                       [ci], [0], [dxn], [-1], [], [])
+                dx = dxn.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             dwp = torch.empty(co, 9 * ci, device=x.device, dtype=torch.bfloat16)
             C.conv_wgrad_taps([(gn, [x.permute(0, 2, 3, 1)])], 0, [0], [ci], (3, 3), (1, 1), co,

@@ -4,6 +4,7 @@ import sys
 
 CATS = [('ours conv fwd', r'conv_fwd_kernel<[^>]*, [0-57], (true|false)>|conv_fwd_(glds|halo|v3)_kernel<\d+, \d+, \d+, [0-57], \d+>|fh2_fwd'),
         ('ours dgrad', r'conv_fwd_kernel<[^>]*, [68], |conv_fwd_(glds|halo|v3)_kernel<\d+, \d+, \d+, [68], \d+>|fh2_dgrad'),
+        ('ours conv fwd', r'conv_enc64'),
         ('ours wgrad', r'fh2_wgrad'),
         ('ours wgrad', r'conv_wgrad'),
         ('encoder norm', r'norm_(bwd_)?(stats|apply|finalize)|partial_reduce|add_relu|relu_mask'),

@@ -1,0 +1,20 @@
+#!/bin/bash
+# encoder tests + bench + step profile, then the large-batch runs and the fp32 bench
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+TAG=${1:-combo2}
+mkdir -p gpurun_out/miopen_db
+[ -d miopen_db ] && cp -r miopen_db/. gpurun_out/miopen_db/
+export MIOPEN_USER_DB_PATH=$PWD/gpurun_out/miopen_db
+timeout -k 10 300 python -u -m pytest tests/test_encoder_gpu.py tests/test_model_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1
+rc=$?; tail -n 2 gpurun_out/${TAG}_pytest.log; if [ $rc -ne 0 ]; then grep -E "^E |FAILED" gpurun_out/${TAG}_pytest.log | head -20; exit $rc; fi
+timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench.log 2>&1 || { tail -3 gpurun_out/${TAG}_bench.log; exit 1; }
+grep metric gpurun_out/${TAG}_bench.log | cut -c1-330
+bash scripts/gpu_profile.sh ${TAG} > /dev/null 2>&1 || exit 1
+python scripts/categorize.py gpurun_out/${TAG}_summary.txt > gpurun_out/${TAG}_categories.txt
+cat gpurun_out/${TAG}_categories.txt
+grep enc64 gpurun_out/${TAG}_summary.txt | cut -c1-120
+timeout -k 10 900 python bench.py --precision fp32 --warmup 3 --steps 10 > gpurun_out/${TAG}_fp32_bench.log 2>&1 || { tail -5 gpurun_out/${TAG}_fp32_bench.log; exit 1; }
+grep metric gpurun_out/${TAG}_fp32_bench.log | cut -c1-300
+SWEEP_CFGS="192:allpairs 384:onthefly" bash scripts/gpu_batch_sweep.sh

@@ -122,17 +122,20 @@ def test_native_wgrad_3x3_matches_conv2d(ext_ops, cin, cout):
                                rtol=2e-2)
 
 
-@pytest.mark.parametrize('cin,cout', [(64, 64), (128, 128), (64, 128)])
-def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout):
-    """Stride-1 3x3 encoder conv entirely on the MFMA kernels (forward implicit GEMM, input
-    gradient on the flipped weight, tap-fused weight gradient) vs the fp32 autograd of F.conv2d at
-    the same bf16 inputs, across image and batch borders."""
+@pytest.mark.parametrize('cin,cout,hw', [(64, 64, (37, 45)), (64, 64, (8, 16)), (64, 64, (19, 70)),
+                                         (128, 128, (37, 45)), (64, 128, (37, 45))])
+def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout, hw):
+    """Stride-1 3x3 encoder conv entirely on the MFMA kernels (forward implicit GEMM -- or, 64 -> 64,
+    the persistent 2-D halo-tile kernel --, input gradient on the flipped weight, tap-fused weight
+    gradient) vs the fp32 autograd of F.conv2d at the same bf16 inputs, across image and batch
+    borders and partial 8 x 16 tiles."""
     torch.manual_seed(4)
-    x = torch.randn(3, cin, 37, 45, device=DEV).to(torch.bfloat16)
+    h, wd = hw
+    x = torch.randn(3, cin, h, wd, device=DEV).to(torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
     w = (torch.randn(cout, cin, 3, 3, device=DEV) * 0.05).to(torch.bfloat16)
     w = w.contiguous(memory_format=torch.channels_last).requires_grad_(True)
-    dy = torch.randn(3, cout, 37, 45, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(3, cout, h, wd, device=DEV).to(torch.bfloat16)
     dy = dy.contiguous(memory_format=torch.channels_last)
     y = fast._Conv3x3Native.apply(x, w)
     assert y.is_contiguous(memory_format=torch.channels_last)
