@@ -90,6 +90,12 @@ def _heartbeat(period=30.0):
             print('bench: alive %.0f s' % (time.perf_counter() - t0), file=sys.stderr, flush=True)
 
     threading.Thread(target=beat, daemon=True).start()
+    # RAFT_STACK_DUMP=<s>: every <s> seconds also print every thread's Python stack (where a
+    # slow first step spends its time, without a debugger)
+    dump = float(os.environ.get('RAFT_STACK_DUMP', '0') or 0)
+    if dump > 0:
+        import faulthandler
+        faulthandler.dump_traceback_later(dump, repeat=True, file=sys.stderr)
 
 
 def main(argv=None):
