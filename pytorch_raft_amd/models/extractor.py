@@ -17,6 +17,8 @@ forward runs the channels-last fast path of ``pytorch_raft_amd.ops.encoder``: NH
 without NCHW<->NHWC transposes, each norm + ReLU (and residual add + ReLU) one fused HIP autograd
 node, conv biases folded into the norms.
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -131,11 +133,38 @@ class _Encoder(nn.Module):
         self.in_planes = dim
         return nn.Sequential(first, second)
 
+    def _chunk_images(self, x):
+        """Images per call so that the largest activation (the stem output at 1/2 resolution)
+        stays under 2 GiB -- the int32 byte-offset range of MIOpen's kernels and of our buffer
+        descriptors.  Past it MIOpen falls back to solvers that did not finish one batch-192
+        training step (384 fnet images, a 2.24 GB stem output) in 10 minutes (profiles/r3/cfg).
+        Only per-image norms may be chunked: batch norm couples the images (0 = no chunking)."""
+        if self.norm_fn == 'batch':
+            return 0
+        limit = int(os.environ.get('RAFT_ENC_CHUNK_BYTES', str(2 ** 31 - 1)))
+        es = 2 if torch.is_autocast_enabled(x.device.type) else x.element_size()
+        per_img = self.widths[0] * ((x.shape[2] + 1) // 2) * ((x.shape[3] + 1) // 2) * es
+        n = max(1, limit // per_img)
+        return n if x.shape[0] > n else 0
+
     def forward(self, x):
         batched = isinstance(x, (list, tuple))
         if batched:
             n = x[0].shape[0]
             x = torch.cat(x, dim=0)
+        chunk = self._chunk_images(x)
+        if chunk:
+            # equal chunks (the same kernel configs for every chunk)
+            k = -(-x.shape[0] // chunk)
+            size = -(-x.shape[0] // k)
+            x = torch.cat([self._run(c) for c in torch.split(x, size, dim=0)], dim=0)
+        else:
+            x = self._run(x)
+        if batched:
+            x = torch.split(x, [n, n], dim=0)
+        return x
+
+    def _run(self, x):
         from ..ops import encoder as fast
         if fast.fast_path_ok(self, x):
             # channels-last MIOpen convs + fused HIP norm/ReLU/residual nodes (ops/encoder.py)
@@ -146,8 +175,6 @@ class _Encoder(nn.Module):
             x = self.conv2(x)
             if self.training and self.dropout is not None:
                 x = self.dropout(x)
-        if batched:
-            x = torch.split(x, [n, n], dim=0)
         return x
 
 

@@ -1,0 +1,44 @@
+"""Encoders with per-image norms run huge batches in image chunks (the stem output must stay under
+the 2 GiB byte-offset range, models/extractor.py:_chunk_images).  Chunked == unchunked, forward and
+backward, on the CPU (fp32) with a tiny limit; batch norm is never chunked."""
+import pytest
+import torch
+
+from pytorch_raft_amd.models.extractor import BasicEncoder, SmallEncoder
+
+
+@pytest.mark.parametrize('cls,dim', [(BasicEncoder, 256), (SmallEncoder, 128)])
+def test_instance_norm_encoder_chunked_matches_whole(monkeypatch, cls, dim):
+    torch.manual_seed(0)
+    enc = cls(output_dim=dim, norm_fn='instance').train()
+    x1 = torch.randn(3, 3, 32, 40, requires_grad=True)
+    x2 = torch.randn(3, 3, 32, 40, requires_grad=True)
+    f1, f2 = enc([x1, x2])
+    (f1.square().mean() + f2.mean()).backward()
+    ref = [f1.detach(), f2.detach(), x1.grad.clone(), x2.grad.clone(),
+           enc.conv1.weight.grad.clone()]
+    enc.zero_grad()
+    x1.grad = x2.grad = None
+    per_img = enc.widths[0] * 16 * 20 * 4
+    monkeypatch.setenv('RAFT_ENC_CHUNK_BYTES', str(2 * per_img + 1))  # 2 images per call
+    assert enc._chunk_images(torch.cat([x1, x2])) == 2
+    g1, g2 = enc([x1, x2])
+    (g1.square().mean() + g2.mean()).backward()
+    got = [g1.detach(), g2.detach(), x1.grad, x2.grad, enc.conv1.weight.grad]
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
+
+
+def test_batch_norm_encoder_never_chunked(monkeypatch):
+    enc = BasicEncoder(output_dim=256, norm_fn='batch')
+    monkeypatch.setenv('RAFT_ENC_CHUNK_BYTES', '1')
+    assert enc._chunk_images(torch.randn(8, 3, 32, 40)) == 0
+
+
+def test_default_limit_keeps_headline_batches_whole():
+    # chairs 368x496, bf16 stem: 5.84 MB per image -> 367 images per call; batch 96 (192 fnet
+    # images) stays one call, batch 192 (384) becomes two calls of 192
+    enc = BasicEncoder(output_dim=256, norm_fn='instance')
+    with torch.autocast('cpu', dtype=torch.bfloat16):
+        assert enc._chunk_images(torch.empty(1, 3, 368, 496).expand(192, -1, -1, -1)) == 0
+        assert enc._chunk_images(torch.empty(1, 3, 368, 496).expand(384, -1, -1, -1)) == 367
