@@ -49,6 +49,8 @@ def parse(argv=None):
                     help='synthetic ground-truth flow magnitude (px)')
     ap.add_argument('--channels_last', action='store_true')
     ap.add_argument('--small', action='store_true')
+    ap.add_argument('--freeze_bn', action='store_true',
+                    help='frozen context-encoder batch norm (train.py stages after chairs)')
     ap.add_argument('--hipgraph', action='store_true', default=True,
                     help='(default) replay forward+backward and the update as two hipGraphs: the '
                          'host cost of a step drops from ~1000 Python/autograd launches to 2 replays')
@@ -135,6 +137,8 @@ def main(argv=None):
     if a.channels_last:
         model = model.to(memory_format=torch.channels_last)
     model.train()
+    if a.freeze_bn:
+        model.freeze_bn()
     pdist.broadcast_module(model)
     if a.impl == 'torch':
         import pytorch_raft_amd.ops.loss as L
@@ -249,7 +253,7 @@ def main(argv=None):
     if extra:
         metric += ' [%s]' % ', '.join(extra)
     base = STOCK_PAIRS_PER_GPU.get(a.precision)
-    headline = ((h, w) == (368, 496) and a.iters == 12 and not a.small
+    headline = ((h, w) == (368, 496) and a.iters == 12 and not a.small and not a.freeze_bn
                 and a.batch == HEADLINE_BATCH and base is not None)
     res = {
         'metric': metric,
@@ -275,6 +279,7 @@ def main(argv=None):
             'impl': a.impl,
             'corr': getattr(model, 'last_corr', None), 'corr_mode': a.corr_mode,
             'hipgraph': use_graph,
+            'freeze_bn': a.freeze_bn,
         },
         'peak_hbm_gib_rank0': round(peak, 2),
         'peak_reserved_gib_rank0': round(reserved, 2),

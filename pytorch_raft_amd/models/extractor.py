@@ -138,8 +138,10 @@ class _Encoder(nn.Module):
         stays under 2 GiB -- the int32 byte-offset range of MIOpen's kernels and of our buffer
         descriptors.  Past it MIOpen falls back to solvers that did not finish one batch-192
         training step (384 fnet images, a 2.24 GB stem output) in 10 minutes (profiles/r3/cfg).
-        Only per-image norms may be chunked: batch norm couples the images (0 = no chunking)."""
-        if self.norm_fn == 'batch':
+        Only per-image norms may be chunked: batch norm in training mode couples the images
+        (0 = no chunking); frozen batch norm (`freeze_bn`, every stage after chairs) is per-image."""
+        if self.norm_fn == 'batch' and any(
+                m.training for m in self.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)):
             return 0
         limit = int(os.environ.get('RAFT_ENC_CHUNK_BYTES', str(2 ** 31 - 1)))
         es = 2 if torch.is_autocast_enabled(x.device.type) else x.element_size()

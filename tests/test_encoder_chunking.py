@@ -29,10 +29,17 @@ def test_instance_norm_encoder_chunked_matches_whole(monkeypatch, cls, dim):
         torch.testing.assert_close(a, b, atol=1e-5, rtol=1e-5)
 
 
-def test_batch_norm_encoder_never_chunked(monkeypatch):
-    enc = BasicEncoder(output_dim=256, norm_fn='batch')
+def test_batch_norm_encoder_chunked_only_when_frozen(monkeypatch):
+    torch.manual_seed(1)
+    enc = BasicEncoder(output_dim=256, norm_fn='batch').train()
     monkeypatch.setenv('RAFT_ENC_CHUNK_BYTES', '1')
-    assert enc._chunk_images(torch.randn(8, 3, 32, 40)) == 0
+    x = torch.randn(4, 3, 32, 40)
+    assert enc._chunk_images(x) == 0  # training-mode batch statistics couple the images
+    enc.eval()  # frozen statistics: per-image, chunkable (one image per call here)
+    assert enc._chunk_images(x) == 1
+    got = enc(x)
+    monkeypatch.setenv('RAFT_ENC_CHUNK_BYTES', str(2 ** 31 - 1))
+    torch.testing.assert_close(got, enc(x), atol=1e-5, rtol=1e-5)
 
 
 def test_default_limit_keeps_headline_batches_whole():
