@@ -57,6 +57,9 @@ def parse(argv=None):
     ap.add_argument('--eager', '--no_hipgraph', dest='hipgraph', action='store_false',
                     help='issue every kernel eagerly (RCCL buckets overlapped with backward)')
     ap.add_argument('--profile', type=str, default=None, help='torch.profiler trace dir')
+    ap.add_argument('--profile_stack', action='store_true',
+                    help='with --profile: record Python stacks and write stacks.txt (ops grouped by '
+                         'the source lines that issued them; use with --eager to see the decode)')
     ap.add_argument('--json_out', type=str, default=None)
     ap.add_argument('--trace_markers', action='store_true',
                     help='launch a marker spin kernel right before and after the timed steps')
@@ -188,7 +191,8 @@ def main(argv=None):
     prof = None
     if a.profile and rank == 0:
         from torch.profiler import profile, ProfilerActivity
-        prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=False)
+        prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=False,
+                       with_stack=a.profile_stack)
         prof.__enter__()
     roctx = _roctx() if a.roctx_region else None
     if roctx is not None:
@@ -216,6 +220,10 @@ def main(argv=None):
             f.write(prof.key_averages().table(sort_by='self_cuda_time_total', row_limit=80))
             f.write('\n\n')
             f.write(prof.key_averages().table(sort_by='cuda_time_total', row_limit=60))
+        if a.profile_stack:
+            with open(os.path.join(a.profile, 'stacks.txt'), 'w') as f:
+                f.write(prof.key_averages(group_by_stack_n=7).table(
+                    sort_by='self_cuda_time_total', row_limit=400, max_name_column_width=60))
     # host cost of issuing one step on an idle queue (outside the timed region): in the timed
     # loop the host runs ahead until the HIP queue is full, so per-step issue time there is
     # back-pressure, not host work

@@ -1476,6 +1476,13 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_otf_bwd_(Tensor f1, Tensor[] f2, Tensor coords, Tensor dout, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("conv_tune_table() -> int[]", &conv_tune_table);
   m.def("conv_set_forced_cfg(int idx) -> ()", [](int64_t idx) { conv_set_forced_cfg((int)idx); });
+  m.def("conv_set_autotune(int mode) -> ()", [](int64_t mode) { conv_set_autotune((int)mode); });
+  m.def("conv_autotune_runs() -> int", []() -> int64_t { return conv_autotune_runs(); });
+  m.def("conv_tune_import(int[] rows) -> int", [](std::vector<int64_t> rows) -> int64_t {
+    TORCH_CHECK(rows.size() % 12 == 0, "tuned table rows have 12 entries");
+    std::vector<int> r(rows.begin(), rows.end());
+    return conv_import_tuned(r.data(), (int)(r.size() / 12));
+  });
   m.def("norm_fwd_(Tensor x, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor? cbias, Tensor(a!)? rmean, Tensor(b!)? rvar, float momentum, float eps, Tensor? res, Tensor(c!) y) -> Tensor[]");
   m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx) -> ()");
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");

@@ -244,7 +244,6 @@ struct CfgDesc {
   int glds;  // 0: register-staged kernel; n: LDS-DMA kernel with n pipeline stages; HALO
 };
 constexpr int HALO = 9;
-constexpr int V3 = 10;  // pipelined register-staged kernel (conv_v3.h)
 // (keep in sync with the dispatch switch below)
 constexpr CfgDesc kCfgs[] = {
     {2, 2, 2, 128, 128, true, false},  {1, 2, 2, 64, 128, true, false},
@@ -267,10 +266,6 @@ constexpr CfgDesc kCfgs[] = {
     // halo-tile kernel (conv_halo.h; glds = HALO): A image per channel chunk, B straight to VGPRs
     {5, 1, 1, 160, 128, false, HALO}, {5, 2, 1, 160, 256, false, HALO},
     {4, 2, 1, 128, 256, false, HALO}, {2, 2, 2, 128, 128, false, HALO},
-    // v3 kernel (conv_v3.h; glds = V3): MFMAs right after the barrier, A register-staged two steps
-    // ahead, B straight to VGPRs, two workgroups per CU where the registers allow
-    {5, 1, 1, 160, 128, false, V3}, {3, 1, 1, 96, 128, false, V3},
-    {5, 2, 1, 160, 256, false, V3}, {3, 2, 1, 96, 256, false, V3},
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
@@ -307,8 +302,6 @@ bool launch_cfg_idx(const ConvFwdArgs& a, int idx, hipStream_t stream) {
       case 8: launch_one<EPI, false, 4, 2, 1>(a, stream); return true;
       case 9: launch_one<EPI, false, 3, 2, 1>(a, stream); return true;
       default:
-        if (idx >= 0 && idx < kNumCfgs && kCfgs[idx].glds == V3)
-          return launch_conv_v3(a, EPI, kCfgs[idx].tm, kCfgs[idx].tn, stream);
         if (idx >= 0 && idx < kNumCfgs && kCfgs[idx].glds == HALO)
           return launch_conv_halo(a, EPI, kCfgs[idx].tm, kCfgs[idx].tn, kCfgs[idx].wvm, stream);
         if (idx >= 0 && idx < kNumCfgs && kCfgs[idx].glds) return launch_conv_glds(a, EPI, idx, stream);
@@ -343,14 +336,6 @@ bool halo_disabled() {
   return off;
 }
 
-bool v3_disabled() {
-  static const bool off = [] {
-    const char* e = getenv("RAFT_CONV_V3");
-    return e && e[0] == '0';
-  }();
-  return off;
-}
-
 bool glds_disabled() {
   static const bool off = [] {
     const char* e = getenv("RAFT_CONV_GLDS");
@@ -364,10 +349,6 @@ bool cfg_allowed(int idx, int cout, bool smallc, int epi) {
   if (smallc && !c.small_ok) return false;
   if (c.glds && glds_disabled()) return false;
   if (c.glds == HALO && halo_disabled()) return false;
-  if (c.glds == V3 && v3_disabled()) return false;
-  // v3's wide tiles do not offer the gate epilogues (they spill there): an autotune timed on the
-  // fp32 scratch epilogue must not pick a config the real epilogue cannot launch
-  if (c.glds == V3 && c.tn == 2 && (epi == EPI_GRU_ZR || epi == EPI_DGRAD_GATE)) return false;
   if (idx == 6 && (epi == EPI_GRU_ZR || epi == EPI_GRU_Q)) return false;
   const int npad = (cout + 31) / 32 * 32;
   return c.bn <= 2 * npad || c.bn <= 32;  // no config more than half empty in N
@@ -484,6 +465,8 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
 }
 
 int g_forced_cfg = -1;
+int g_autotune_override = -1;  // -1: RAFT_CONV_AUTOTUNE decides; 0 / 1: off / on (data parallel)
+int g_autotune_runs = 0;
 
 int choose_cfg(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   if (g_forced_cfg >= 0) return g_forced_cfg;
@@ -508,7 +491,11 @@ int choose_cfg(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(stream, &cs);
   int idx = -1;
-  if (tune && cs == hipStreamCaptureStatusNone) idx = autotune(a, epi, smallc, stream);
+  const bool tune_now = g_autotune_override >= 0 ? g_autotune_override == 1 : tune;
+  if (tune_now && cs == hipStreamCaptureStatusNone) {
+    idx = autotune(a, epi, smallc, stream);
+    ++g_autotune_runs;
+  }
   if (idx < 0) idx = heuristic_cfg(P, a.cout, smallc, epi);
   if (cs == hipStreamCaptureStatusNone) g_tuned[key] = idx;
   return idx;
@@ -528,10 +515,29 @@ bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStre
     t.nullmem = 1;
     return launch_epi_idx(t, epi, idx, smallc, stream);
   }
-  return launch_epi_idx(a, epi, idx, smallc, stream);
+  if (launch_epi_idx(a, epi, idx, smallc, stream)) return true;
+  // a cached pick is shared by the epilogues of one class (TuneKey.f32out); should it not offer
+  // this epilogue, the analytic register-staged choice (every epilogue instantiated) runs instead
+  return launch_epi_idx(a, epi, heuristic_cfg(a.B * a.H * a.W, a.cout, smallc, epi), smallc, stream);
 }
 
 void conv_set_forced_cfg(int idx) { g_forced_cfg = idx < kNumCfgs ? idx : -1; }
+
+void conv_set_autotune(int mode) { g_autotune_override = mode < 0 ? -1 : (mode ? 1 : 0); }
+
+int conv_autotune_runs() { return g_autotune_runs; }
+
+int conv_import_tuned(const int* rows, int n) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  int done = 0;
+  for (int i = 0; i < n; ++i) {
+    const int* r = rows + 12 * i;
+    if (r[9] < 0 || r[9] >= kNumCfgs) continue;  // a table from another build: keep our choice
+    g_tuned[TuneKey{r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], r[8]}] = r[9];
+    ++done;
+  }
+  return done;
+}
 
 int conv_tuned_table(int* out, int max_rows) {
   std::lock_guard<std::mutex> lk(g_tune_mu);

@@ -160,12 +160,15 @@ struct ConvFwdArgs {
 bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStream_t stream);
 // LDS-DMA kernel of config `idx` (conv_glds.hip); false for a non-LDS-DMA index
 bool launch_conv_glds(const ConvFwdArgs& a, int epi, int idx, hipStream_t stream);
-// v3 kernel (conv_v3.hip) of tile (tm, tn); false if the geometry / epilogue is not offered
-bool launch_conv_v3(const ConvFwdArgs& a, int epi, int tm, int tn, hipStream_t stream);
 // rows of 12 ints: P H W KH KW cin cout small epi_class cfg BM BN
 int conv_tuned_table(int* out, int max_rows);
 // tests: run every following conv launch with config `idx` (-1: back to the tuned choice)
 void conv_set_forced_cfg(int idx);
+// data parallel: ranks > 0 skip the autotune (mode 0) and import rank 0's table (rows as
+// conv_tuned_table), so every rank runs the same kernels; -1 restores RAFT_CONV_AUTOTUNE
+void conv_set_autotune(int mode);
+int conv_autotune_runs();
+int conv_import_tuned(const int* rows, int n);
 
 struct ConvWgradArgs {
   const uint16_t* g;  // dL/d(pre-activation), NHWC bf16, offset to channel 0

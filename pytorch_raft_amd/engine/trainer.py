@@ -170,6 +170,8 @@ class GraphedTrainStep:
             self.sflow = example[2].detach().clone()
             self.svalid = example[3].detach().clone()
             del feats
+            if self.world > 1:
+                self._tune_on_rank0(example)
             for _ in range(warmup):  # MIOpen find / autotune / allocator warm-up: real steps
                 self._step_body(*example, graphs=False)
         torch.cuda.current_stream(st.device).wait_stream(stream)
@@ -184,6 +186,36 @@ class GraphedTrainStep:
         self.dec_grads = [p.grad for p in self.dec_params]
         self.warmup_steps = warmup
         self._restore(snap)
+
+    def _tune_on_rank0(self, example):
+        """Kernel choices are made ONCE, on rank 0, and every rank runs them: rank 0 runs a
+        forward + backward alone (no collectives) while the others wait -- it autotunes the
+        conv tiles and MIOpen's find writes its choices to the shared user find-db -- then the
+        tuned tile table is broadcast and imported, and the other ranks pre-warm with autotune
+        off (their MIOpen finds hit rank 0's db records).  Identical kernels mean identical
+        reduction orders on every rank, and the tuning cost is paid once per node.  Effects on
+        the weights / BN statistics are rolled back with the warm-up steps."""
+        ops = torch.ops.raft_amd
+        me = pdist.rank()
+        if me != 0:
+            ops.conv_set_autotune(0)
+        if me == 0:
+            self._prewarm(example)
+        pdist.barrier(self.st.device)
+        pdist.share_conv_tuning(self.st.device)
+        if me != 0:
+            self._prewarm(example)
+        self.autotune_runs = int(ops.conv_autotune_runs())
+        pdist.barrier(self.st.device)
+
+    def _prewarm(self, example):
+        feats = self.st.model.encode(example[0], example[1])
+        preds = self.st.model.decode(*feats, iters=self.st.args.iters)
+        loss, _ = sequence_loss(preds, example[2], example[3], self.st.args.gamma)
+        loss.backward()
+        del feats, preds, loss
+        for p in self.params:
+            p.grad = None
 
     # ---------------------------------------------------------------- pieces of one step
     def _decode(self):

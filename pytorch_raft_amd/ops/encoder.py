@@ -218,9 +218,6 @@ def cast_conv_weights(convs):
     return dict(zip(convs, _CastWeightsCL.apply(maps, *ws)))
 
 
-_WEIGHTS = {}   # conv -> bf16 channels_last weight for the encoder forward in flight
-
-
 class _Head1x1(torch.autograd.Function):
     """The encoders' final 1x1 conv (`core/extractor.py:185`, 128 -> 256 with bias) on the
     MFMA implicit-GEMM kernels of the update block (NHWC bf16, fp32 accumulation): forward with
@@ -389,8 +386,8 @@ def _wgrad_native_ok(x, conv):
             and x.numel() * 2 < 2 ** 31 and x.shape[0] * x.shape[2] * x.shape[3] * conv.out_channels * 2 < 2 ** 31)
 
 
-def _conv(x, conv, with_bias=False):
-    w = _WEIGHTS.get(conv)
+def _conv(ps, x, conv, with_bias=False):
+    w = ps.weights.get(conv)
     if w is None:
         w = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     if not with_bias and _conv_native_ok(x, conv) and w.is_contiguous(memory_format=torch.channels_last):
@@ -404,9 +401,9 @@ def _conv(x, conv, with_bias=False):
     return F.conv2d(x, w, b, conv.stride, conv.padding, conv.dilation, conv.groups)
 
 
-def conv_norm_act(x, conv, norm, relu=True):
+def conv_norm_act(ps, x, conv, norm, relu=True):
     mode = _norm_mode(norm)
-    y = _conv(x, conv)
+    y = _conv(ps, x, conv)
     y = y.contiguous(memory_format=torch.channels_last)
     gamma = beta = None
     if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and norm.affine:
@@ -414,45 +411,44 @@ def conv_norm_act(x, conv, norm, relu=True):
     return _NormAct.apply(y, gamma, beta, conv.bias, norm, mode, relu)
 
 
-def residual_block(blk, x):
+def residual_block(ps, blk, x):
     """`core/extractor.py:47-56` on the fast path (conv2 + norm2 + ReLU + add + ReLU fused)."""
-    y = conv_norm_act(x, blk.conv1, blk.norm1)
+    y = conv_norm_act(ps, x, blk.conv1, blk.norm1)
     if blk.downsample is not None:
-        x = conv_norm_act(x, blk.downsample[0], blk.downsample[1], relu=False)
+        x = conv_norm_act(ps, x, blk.downsample[0], blk.downsample[1], relu=False)
     mode = _norm_mode(blk.norm2)
-    y2 = _conv(y, blk.conv2).contiguous(memory_format=torch.channels_last)
+    y2 = _conv(ps, y, blk.conv2).contiguous(memory_format=torch.channels_last)
     gamma = beta = None
     if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and blk.norm2.affine:
         gamma, beta = blk.norm2.weight, blk.norm2.bias
     # identity shortcut from a previous fused block: its gradient goes through that block's stash
-    res_holder = _HOLDERS.get(id(x)) if (blk.downsample is None and _STASH) else None
+    res_holder = ps.holders.get(id(x)) if (blk.downsample is None and _STASH) else None
     if res_holder is not None and res_holder[0] is not x:
         res_holder = None
     holder = {}
     out = _NormActAddRelu.apply(y2, gamma, beta, blk.conv2.bias, x, blk.norm2, mode, holder,
                                 res_holder[1] if res_holder is not None else None)
-    _HOLDERS[id(out)] = (out, holder)
+    ps.holders[id(out)] = (out, holder)
     return out
 
 
-# id(block output) -> (output, its gradient stash), for the encoder forward in flight.
+# _Pass.holders: id(block output) -> (output, its gradient stash), for ONE encoder forward.
 # Restriction of the stash: the identity-residual gradient of a fused block's output reaches its
 # producer through the stash, not through autograd, so a tensor hook on an intermediate block
 # output, or ``autograd.grad(..., inputs=[block_out])``, sees the gradient WITHOUT the shortcut
 # term.  Parameter gradients and the encoder-input gradient are exact (the producer node always
 # runs after all consumers of its output).  ``RAFT_ENCODER_STASH=0`` in the environment keeps
 # the shortcut gradient in the autograd graph when intermediate activation gradients are needed.
-_HOLDERS = {}
 _STASH = os.environ.get('RAFT_ENCODER_STASH', '1') != '0'
 
 
-def bottleneck_block(blk, x):
+def bottleneck_block(ps, blk, x):
     """`core/extractor.py:105-116` on the fast path."""
-    y = conv_norm_act(x, blk.conv1, blk.norm1)
-    y = conv_norm_act(y, blk.conv2, blk.norm2)
-    y = conv_norm_act(y, blk.conv3, blk.norm3)
+    y = conv_norm_act(ps, x, blk.conv1, blk.norm1)
+    y = conv_norm_act(ps, y, blk.conv2, blk.norm2)
+    y = conv_norm_act(ps, y, blk.conv3, blk.norm3)
     if blk.downsample is not None:
-        x = conv_norm_act(x, blk.downsample[0], blk.downsample[1], relu=False)
+        x = conv_norm_act(ps, x, blk.downsample[0], blk.downsample[1], relu=False)
     return _AddRelu.apply(x, y)
 
 
@@ -479,28 +475,33 @@ def fast_path_ok(enc, x):
     return True
 
 
+class _Pass:
+    """State of ONE encoder forward: the batched bf16 weight casts and the residual-gradient
+    stashes.  Passed down explicitly (no module globals), so encoder forwards running
+    concurrently on two streams or threads, or re-entrantly, cannot see each other's state."""
+
+    def __init__(self, weights):
+        self.weights = weights   # conv -> bf16 channels_last weight
+        self.holders = {}        # id(block output) -> (output, its gradient stash)
+
+
 def encoder_forward(enc, x):
     """`core/extractor.py:168-192` (both encoders): returns channels_last bf16 features."""
     with torch.autocast('cuda', enabled=False):
         convs = [m for m in enc.modules() if isinstance(m, nn.Conv2d)]
         if _head_ok(x, enc.conv2):
             convs = [c for c in convs if c is not enc.conv2]  # runs on _Head1x1 (fp32 weight)
-        _WEIGHTS.update(cast_conv_weights(convs))
-        try:
-            return _encoder_body(enc, x)
-        finally:
-            _WEIGHTS.clear()
-            _HOLDERS.clear()
+        return _encoder_body(_Pass(cast_conv_weights(convs)), enc, x)
 
 
-def _encoder_body(enc, x):
+def _encoder_body(ps, enc, x):
     x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    x = conv_norm_act(x, enc.conv1, enc.norm1)
+    x = conv_norm_act(ps, x, enc.conv1, enc.norm1)
     block_fn = residual_block if enc.block.__name__ == 'ResidualBlock' else bottleneck_block
     for layer in (enc.layer1, enc.layer2, enc.layer3):
         for blk in layer:
-            x = block_fn(blk, x)
+            x = block_fn(ps, blk, x)
     if _head_ok(x, enc.conv2):
         return _Head1x1.apply(x, enc.conv2.weight, enc.conv2.bias)
-    x = _conv(x, enc.conv2, with_bias=True)
+    x = _conv(ps, x, enc.conv2, with_bias=True)
     return x

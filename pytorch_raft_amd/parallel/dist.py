@@ -126,6 +126,35 @@ def _broadcast_coalesced(tensors, src):
             off += n
 
 
+def conv_tuning_table():
+    """This process's autotuned conv configs: (n, 12) int64 rows (key, config, tile); empty
+    without the native library."""
+    try:
+        rows = torch.ops.raft_amd.conv_tune_table()
+    except (AttributeError, RuntimeError):
+        return torch.zeros(0, 12, dtype=torch.int64)
+    return torch.tensor(rows, dtype=torch.int64).view(-1, 12)
+
+
+def share_conv_tuning(device, src=0):
+    """Rank ``src``'s autotuned conv configs -> every rank (broadcast, then imported into the
+    native tile cache), so all ranks launch identical kernels with identical reduction orders.
+    Returns the number of rows imported on this rank (0 on ``src``)."""
+    if not is_dist():
+        return 0
+    dev = device if dist.get_backend() == 'nccl' else torch.device('cpu')
+    table = conv_tuning_table() if rank() == src else torch.zeros(0, 12, dtype=torch.int64)
+    n = torch.tensor([table.shape[0]], dtype=torch.int64, device=dev)
+    dist.broadcast(n, src)
+    buf = table.to(dev) if rank() == src else torch.zeros(int(n.item()), 12, dtype=torch.int64,
+                                                          device=dev)
+    if int(n.item()) > 0:
+        dist.broadcast(buf, src)
+    if rank() == src or int(n.item()) == 0:
+        return 0
+    return int(torch.ops.raft_amd.conv_tune_import(buf.cpu().reshape(-1).tolist()))
+
+
 @torch.no_grad()
 def all_reduce_mean(t):
     if is_dist():

@@ -1,7 +1,12 @@
 """Multi-rank rehearsal of the data-parallel training path on ONE GPU.
 
     RAFT_DIST_BACKEND=gloo python -m torch.distributed.run --nproc-per-node 2 \
-        --master-addr 127.0.0.1 --master-port 29561 scripts/dp_rehearsal.py [--graph]
+        --master-addr 127.0.0.1 --master-port 29561 scripts/dp_rehearsal.py [--graph] [--fp32]
+
+``--fp32``: the fp32 model (the reference's default precision, `train_standard.sh`): the DP
+gradient must then match the full-batch one to rel 1e-4 (what remains is summation order), which
+pins the all-reduce arithmetic itself rather than bf16 noise.  Without a RAFT_DIST_BACKEND the
+ranks use RCCL, one GPU each (needs as many visible GPUs as ranks).
 
 Every rank runs the fused HIP training path on cuda:0 with its half of a batch; GradSync
 all-reduces the gradients (bucketed, side stream, post-accumulate-grad hooks).  Rank 0 then
@@ -23,7 +28,7 @@ from pytorch_raft_amd.engine.trainer import TrainState  # noqa: E402
 from pytorch_raft_amd.parallel import dist as pdist  # noqa: E402
 
 
-def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl):
+def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl, fp32=False):
     """The graphed step's DP path: eager encoders + g_dec replay -> one flat all-reduce of the
     update-block gradients overlapping the eager encoder backward, whose post-accumulate-grad
     hooks launch the encoder gradient buckets -> clip + fused AdamW."""
@@ -33,6 +38,12 @@ def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl):
     assert st.sync is None
     g = GraphedTrainStep(st, (i1[sl], i2[sl], flow[sl], valid[sl]), warmup=1)
     assert g.enc_sync is not None and len(g.enc_sync.buckets) > 1
+    # kernel choices made once on rank 0: identical tile tables, no autotune on the other ranks
+    tab = pdist.conv_tuning_table().tolist()
+    tabs = [None] * world
+    torch.distributed.all_gather_object(tabs, (sorted(map(tuple, tab)), g.autotune_runs))
+    tables_same = all(t[0] == tabs[0][0] for t in tabs) and len(tabs[0][0]) > 0
+    runs = [t[1] for t in tabs]
     # one step up to the averaged gradients (weights untouched)
     g._forward_backward_sync(i1[sl], i2[sl], flow[sl], valid[sl], graphs=True)
     torch.cuda.synchronize()
@@ -82,21 +93,31 @@ def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl):
         rel_w = ((d_dp - d_ref).norm() / d_ref.norm()).item()
         cos_w = torch.nn.functional.cosine_similarity(d_dp[None], d_ref[None]).item()
         print('resolved gradient entries: %.4f' % resolved.float().mean().item(), flush=True)
-        print('dp rehearsal (hipgraph): world=%d backend=%s enc_buckets=%d launched_during_'
-              'backward=%d rel_grad_err=%.3e step_delta_rel=%.3e step_delta_cos=%.5f '
-              'ranks_identical=%s' %
-              (world, torch.distributed.get_backend(), len(g.enc_sync.buckets), launched_early,
-               rel, rel_w, cos_w, same), flush=True)
-        assert rel < 2e-2, rel
-        assert cos_w > 0.98 and rel_w < 0.2, (cos_w, rel_w)
+        print('dp rehearsal (hipgraph%s): world=%d backend=%s enc_buckets=%d launched_during_'
+              'backward=%d rel_grad_err=%.3e step_delta_rel=%.3e step_delta_cos=%.6f '
+              'ranks_identical=%s tuned_tables_identical=%s autotune_runs=%s' %
+              (', fp32' if fp32 else '', world, torch.distributed.get_backend(),
+               len(g.enc_sync.buckets), launched_early, rel, rel_w, cos_w, same, tables_same,
+               runs), flush=True)
+        if fp32:
+            # fp32: summation order only (split-bf16 update-block products are ~2^-16 exact)
+            assert rel < 1e-4, rel
+            assert cos_w > 0.99999 and rel_w < 1e-3, (cos_w, rel_w)
+        else:
+            # bf16: observed rel_grad_err ~3e-3, step delta rel ~0.12 / cos ~0.993 (round 3)
+            assert rel < 1e-2, rel
+            assert cos_w > 0.99 and rel_w < 0.15, (cos_w, rel_w)
         assert same, 'weights diverged across ranks'
+        assert tables_same, 'ranks run different conv kernels'
+        assert all(r == 0 for r in runs[1:]), ('ranks > 0 must not autotune', runs)
 
 
 def main():
     graph = '--graph' in sys.argv
+    fp32 = '--fp32' in sys.argv
     dev = pdist.init_distributed()
     rank, world = pdist.rank(), pdist.world_size()
-    args = argparse.Namespace(small=False, mixed_precision=True, corr_impl='hip', lr=4e-4,
+    args = argparse.Namespace(small=False, mixed_precision=not fp32, corr_impl='hip', lr=4e-4,
                               wdecay=1e-4, epsilon=1e-8, num_steps=100, iters=4, gamma=0.8,
                               clip=1.0, add_noise=False, bucket_mb=2.0, enc_bucket_mb=1.0)
     torch.manual_seed(0)
@@ -106,7 +127,7 @@ def main():
     i1, i2, flow, valid = make_pair_batch(2 * world, 128, 160, device=dev)
     sl = slice(2 * rank, 2 * rank + 2)
     if graph:
-        graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl)
+        graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl, fp32)
         pdist.barrier(dev)
         pdist.destroy()
         return
@@ -126,10 +147,10 @@ def main():
         st1.forward_backward(i1, i2, flow, valid)
         g_full = torch.cat([p.grad.reshape(-1).float() for p in ref.parameters()])
         rel = ((g_dp - g_full).norm() / g_full.norm()).item()
-        print('dp rehearsal: world=%d backend=%s buckets=%d rel_grad_err=%.3e loss=%.4f' %
-              (world, torch.distributed.get_backend(), len(st.sync.buckets), rel, loss.item()),
-              flush=True)
-        assert rel < 2e-2, rel
+        print('dp rehearsal%s: world=%d backend=%s buckets=%d rel_grad_err=%.3e loss=%.4f' %
+              (' (fp32)' if fp32 else '', world, torch.distributed.get_backend(),
+               len(st.sync.buckets), rel, loss.item()), flush=True)
+        assert rel < (1e-4 if fp32 else 1e-2), rel
     pdist.barrier(dev)
     pdist.destroy()
 

@@ -291,12 +291,10 @@ def test_conv_wgrad_taps(ext_ops, cin, cout, k, segs, g_off, splits):
 
 
 HALO_CFGS = (30, 31, 32, 33)   # conv_igemm.hip kCfgs: the halo-tile kernel (conv_halo.h)
-V3_CFGS = (34, 35, 36, 37)     # the pipelined v3 kernel (conv_v3.h): 5x1, 3x1, 5x2, 3x2 tiles
-# v3's 5x2 tile does not offer the GRU-gate epilogue (it would spill)
-GATE_CFGS = HALO_CFGS + (34, 35, 37)
+GATE_CFGS = HALO_CFGS
 
 
-@pytest.mark.parametrize('cfg', HALO_CFGS + V3_CFGS)
+@pytest.mark.parametrize('cfg', HALO_CFGS)
 @pytest.mark.parametrize('segs,cout,k,hw', [
     ([256], 192, (3, 3), (13, 21)),
     ([128, 128], 256, (1, 5), (13, 21)),
@@ -305,7 +303,7 @@ GATE_CFGS = HALO_CFGS + (34, 35, 37)
     ([128], 126, (3, 3), (46, 62)),
 ])
 def test_conv_halo_fwd(ext_ops, cfg, segs, cout, k, hw):
-    """Halo-tile and v3 kernels forced for every tile shape: fwd vs an fp32 conv of the bf16 operands,
+    """Halo-tile kernels forced for every tile shape: fwd vs an fp32 conv of the bf16 operands,
     across image / batch boundaries (rows whose shifted neighbour leaves the image read zeros)."""
     torch.manual_seed(5)
     B, (H, W) = 2, hw
@@ -332,7 +330,7 @@ def test_conv_halo_fwd(ext_ops, cfg, segs, cout, k, hw):
 
 @pytest.mark.parametrize('cfg', GATE_CFGS)
 def test_conv_halo_gru_and_dgrad(ext_ops, cfg):
-    """Halo / v3 kernels under the GRU gate epilogue (with a per-pixel bias map) and the multi-segment
+    """Halo kernels under the GRU gate epilogue (with a per-pixel bias map) and the multi-segment
     dgrad epilogue (fp32 store + accumulate), against the register / LDS-DMA kernels' results."""
     torch.manual_seed(6)
     B, H, W, hd = 2, 10, 14, 128

@@ -22,14 +22,41 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize('mode', ['eager', 'graph'])
-def test_dp_rehearsal(ext_ops, mode):
-    env = dict(os.environ, RAFT_DIST_BACKEND='gloo', MASTER_ADDR='127.0.0.1')
+def _run(mode, precision, backend):
+    env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    if backend == 'gloo':
+        env['RAFT_DIST_BACKEND'] = 'gloo'
+    else:
+        env.pop('RAFT_DIST_BACKEND', None)
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
            '--master-addr', '127.0.0.1', '--master-port', str(_port()),
-           os.path.join(ROOT, 'scripts', 'dp_rehearsal.py')] + (['--graph'] if mode == 'graph' else [])
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=160)
+           os.path.join(ROOT, 'scripts', 'dp_rehearsal.py')] + \
+        (['--graph'] if mode == 'graph' else []) + (['--fp32'] if precision == 'fp32' else [])
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+
+
+@pytest.mark.parametrize('precision', ['bf16', 'fp32'])
+@pytest.mark.parametrize('mode', ['eager', 'graph'])
+def test_dp_rehearsal(ext_ops, mode, precision):
+    """fp32 pins the all-reduce math (DP gradient == full-batch gradient to 1e-4); the graphed
+    mode also checks that rank 0's kernel choices are the ones every rank runs."""
+    r = _run(mode, precision, 'gloo')
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert 'dp rehearsal' in out, out[-2000:]
     print([l for l in out.splitlines() if 'dp rehearsal' in l][0])
+
+
+@pytest.mark.parametrize('precision', ['bf16', 'fp32'])
+def test_dp_rccl_two_gpus(ext_ops, precision):
+    """The same graphed DP step over RCCL, one GPU per rank: needs >= 2 visible GPUs (the driver's
+    multi-GPU node; skipped on a one-GPU box)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip('needs 2 GPUs for an RCCL rehearsal')
+    r = _run('graph', precision, 'nccl')
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    line = [l for l in out.splitlines() if 'dp rehearsal' in l][0]
+    assert 'backend=nccl' in line and 'ranks_identical=True' in line, line
+    print(line)

@@ -138,3 +138,71 @@ def test_auto_corr_mode_switches_on_budget(ext_ops, monkeypatch):
         assert m.last_corr == 'on-the-fly'
     torch.testing.assert_close(lo_ot, lo_ap, atol=2e-3, rtol=1e-3)
     torch.testing.assert_close(up_ot, up_ap, atol=2e-2, rtol=1e-3)
+
+
+def _fp16_args(**kw):
+    a = dict(small=False, mixed_precision=True, amp_dtype='float16', corr_impl='hip', lr=4e-4,
+             wdecay=1e-4, epsilon=1e-8, num_steps=100, iters=3, gamma=0.8, clip=1.0,
+             add_noise=False)
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+def test_fp16_gradscaler_grads_match_fp32(ext_ops):
+    """The reference's --mixed_precision (`train.py:154,175-181`): fp16 autocast + GradScaler.
+    Unscaled fp16 gradients vs the fp32 model's on the same weights (BN frozen: no batch-stat
+    coupling), and the fp16 path must not lose to bf16 (more mantissa, same step)."""
+    from pytorch_raft_amd.ops.loss import sequence_loss
+    i1, i2, flow, valid = make_pair_batch(2, 128, 160, device=DEV)
+    grads = {}
+    for prec in ('fp32', 'fp16', 'bf16'):
+        args = _fp16_args(mixed_precision=prec != 'fp32',
+                          amp_dtype='float16' if prec == 'fp16' else 'bfloat16')
+        torch.manual_seed(0)
+        m = RAFT(args).to(DEV).train()
+        m.freeze_bn()
+        scaler = torch.amp.GradScaler('cuda', init_scale=2.0 ** 12, enabled=prec == 'fp16')
+        preds = m(i1, i2, iters=3)
+        loss, _ = sequence_loss(preds, flow, valid, 0.8)
+        scaler.scale(loss).backward()
+        g = torch.cat([p.grad.reshape(-1).float() for p in m.parameters()])
+        if prec == 'fp16':
+            g = g / scaler.get_scale()
+        grads[prec] = g
+    ref = grads['fp32']
+    rel16 = ((grads['fp16'] - ref).norm() / ref.norm()).item()
+    rel_bf = ((grads['bf16'] - ref).norm() / ref.norm()).item()
+    print('rel grad err vs fp32: fp16 %.3e  bf16 %.3e' % (rel16, rel_bf))
+    assert torch.isfinite(grads['fp16']).all()
+    assert rel16 < 2e-2, rel16
+    assert rel16 < 1.5 * rel_bf + 1e-3, (rel16, rel_bf)
+
+
+def test_fp16_train_step_gradscaler(ext_ops):
+    """fp16 TrainState steps: loss scaling, unscale before clip, device-side found-inf skip (fused
+    AdamW takes found_inf / no host sync) and the scale update.  A 2^40 initial scale overflows
+    the fp16 gradients: that step must leave the weights untouched and halve the scale; later
+    steps train normally."""
+    from pytorch_raft_amd.engine.trainer import TrainState
+    args = _fp16_args()
+    torch.manual_seed(0)
+    m = RAFT(args).to(DEV).train()
+    st = TrainState(m, args, torch.device(DEV))
+    assert st.scaler.is_enabled()
+    st.scaler = torch.amp.GradScaler('cuda', init_scale=2.0 ** 40, growth_interval=1000)
+    i1, i2, flow, valid = make_pair_batch(2, 128, 160, device=DEV)
+    w0 = torch.cat([p.detach().reshape(-1).clone() for p in m.parameters()])
+    st.step(i1, i2, flow, valid)
+    w1 = torch.cat([p.detach().reshape(-1).clone() for p in m.parameters()])
+    assert torch.equal(w0, w1), 'overflowed step must be skipped'
+    assert st.scaler.get_scale() < 2.0 ** 40
+    losses = []
+    for _ in range(60):
+        loss, _ = st.step(i1, i2, flow, valid)
+        if st.scaler.get_scale() < 2.0 ** 20:
+            losses.append(loss.item())
+        if len(losses) >= 4:
+            break
+    w2 = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    assert not torch.equal(w1, w2), 'no step was taken once the scale came down'
+    assert all(l == l for l in losses) and losses[-1] < losses[0] * 1.5, losses
