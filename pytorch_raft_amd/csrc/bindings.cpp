@@ -599,13 +599,19 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   int64_t cin_pad = 0;
   for (size_t s = 0; s < ins.size(); ++s) {
     check_nhwc(ins[s], B, H, W, "conv input", at::kBFloat16);
-    TORCH_CHECK(in_off[s] >= 0 && in_off[s] + in_cnt[s] <= ins[s].size(3), "segment out of range");
+    // a segment may run past the tensor's last channel (a 96-channel tensor in a 128-channel K
+    // slot): the kernels read the channels that are not there as zeros
+    const int64_t present = std::min<int64_t>(in_cnt[s], ins[s].size(3) - in_off[s]);
+    TORCH_CHECK(in_off[s] >= 0 && present > 0 && present % 8 == 0 &&
+                    (present == in_cnt[s] || cin_small == 0),
+                "segment out of range");
     TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
     if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 64 == 0, "segment channels must be a multiple of 64");
     TORCH_CHECK(ins[s].numel() * 2 < (int64_t(1) << 31), "conv input exceeds the 2 GiB buffer-descriptor range");
     a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
+    a.seg[s].real = (int)present;
     cin_pad += in_cnt[s];
   }
   a.cin_pad = (int)cin_pad;
@@ -684,9 +690,9 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
 }
 
 std::vector<int64_t> conv_tune_table() {
-  std::vector<int> buf(12 * 512);
+  std::vector<int> buf(13 * 512);
   const int n = conv_tuned_table(buf.data(), 512);
-  return std::vector<int64_t>(buf.begin(), buf.begin() + 12 * n);
+  return std::vector<int64_t>(buf.begin(), buf.begin() + 13 * n);
 }
 
 // dw (cout, kpad) fp32 += sum_p g[p][:cout] (x) im2col(ins)[p][:]; db (cout) fp32 += colsum(g)
@@ -717,6 +723,7 @@ void conv_wgrad_(const Tensor& g, int64_t g_off, const std::vector<Tensor>& ins,
     a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
+    a.seg[s].real = (int)in_cnt[s];
     cin_pad += in_cnt[s];
   }
   a.cin_pad = (int)cin_pad;
@@ -765,6 +772,7 @@ void conv_wgrad_multi_(const std::vector<Tensor>& gs, int64_t g_off, const std::
                 "multi-item wgrad: segments must be multiples of the 128-wide K tile");
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
+    a.seg[s].real = (int)in_cnt[s];
     cin_pad += in_cnt[s];
   }
   for (int64_t i = 0; i < n; ++i) {
@@ -840,6 +848,7 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
                 "tap-fused wgrad: segments must be multiples of 64 channels (last: of 32)");
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
+    a.seg[s].real = (int)in_cnt[s];
     for (int64_t c = 0; c < in_cnt[s]; c += 64) {
       TORCH_CHECK(ta.n_ci < RAFT_WG_MAX_CI_CHUNKS, "too many input channels");
       ta.ci_seg[ta.n_ci] = (int)s;
@@ -937,13 +946,19 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   int64_t cin_pad = 0;
   for (size_t s = 0; s < ins.size(); ++s) {
     check_nhwc(ins[s], B, H, W, "dgrad input", at::kBFloat16);
-    TORCH_CHECK(in_off[s] >= 0 && in_off[s] + in_cnt[s] <= ins[s].size(3), "segment out of range");
+    // a segment may run past the tensor's last channel (a 96-channel tensor in a 128-channel K
+    // slot): the kernels read the channels that are not there as zeros
+    const int64_t present = std::min<int64_t>(in_cnt[s], ins[s].size(3) - in_off[s]);
+    TORCH_CHECK(in_off[s] >= 0 && present > 0 && present % 8 == 0 &&
+                    (present == in_cnt[s] || cin_small == 0),
+                "segment out of range");
     TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
     if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 64 == 0, "segment channels must be a multiple of 64");
     TORCH_CHECK(ins[s].numel() * 2 < (int64_t(1) << 31), "conv input exceeds the 2 GiB buffer-descriptor range");
     a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
+    a.seg[s].real = (int)present;
     cin_pad += in_cnt[s];
   }
   a.cin_pad = (int)cin_pad;
@@ -1478,10 +1493,11 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("conv_set_forced_cfg(int idx) -> ()", [](int64_t idx) { conv_set_forced_cfg((int)idx); });
   m.def("conv_set_autotune(int mode) -> ()", [](int64_t mode) { conv_set_autotune((int)mode); });
   m.def("conv_autotune_runs() -> int", []() -> int64_t { return conv_autotune_runs(); });
+  m.def("phase_mark() -> ()", []() { launch_phase_marker(cur_stream()); });
   m.def("conv_tune_import(int[] rows) -> int", [](std::vector<int64_t> rows) -> int64_t {
-    TORCH_CHECK(rows.size() % 12 == 0, "tuned table rows have 12 entries");
+    TORCH_CHECK(rows.size() % 13 == 0, "tuned table rows have 13 entries");
     std::vector<int> r(rows.begin(), rows.end());
-    return conv_import_tuned(r.data(), (int)(r.size() / 12));
+    return conv_import_tuned(r.data(), (int)(r.size() / 13));
   });
   m.def("norm_fwd_(Tensor x, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor? cbias, Tensor(a!)? rmean, Tensor(b!)? rvar, float momentum, float eps, Tensor? res, Tensor(c!) y) -> Tensor[]");
   m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx) -> ()");

@@ -103,11 +103,13 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
     const int dy = kh - a.PH, dx = kw - a.PW;
     const int dpix = dy * a.W + dx;
     const int coff = c0 - sbase;
+    const int creal = a.seg[s].real;
     const uint32_t base = lds0 + (uint32_t)(buf * STAGE * 16);
 #pragma unroll
     for (int j = 0; j < A_PER; ++j) {
       const int yy = a_y[j] + dy, xx = a_x[j] + dx;
-      const bool ok = (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+      const bool ok = (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W &&
+                      coff + a_lc[j] < creal;
       const uint32_t off = (uint32_t)(((a_pix[j] + dpix) * stride + coff + a_lc[j]) * 2);
       raft_dma16(rs, base + j * NT * 16, ok ? off : OOB);
     }

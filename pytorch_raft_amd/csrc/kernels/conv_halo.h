@@ -97,6 +97,7 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_halo_kernel(ConvFwdArgs a) {
     const rsrc_t rs = s == 0 ? seg_rs[0] : (s == 1 ? seg_rs[1] : seg_rs[2]);
     const int stride = a.seg[s].stride;
     const int coff = c0 - sbase;
+    const int creal = a.seg[s].real;
     const uint32_t base = lds0 + (uint32_t)((c & 1) * ABUF) + wave_off;
     // thread slot g = j * NT + tid of the image -> (row g / 9, 16-B slot g % 9; slot 8 = pad)
 #pragma unroll
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_halo_kernel(ConvFwdArgs a) {
       const int g = j * NT + tid;
       const int row = g / 9, slot = g - row * 9;
       const int q = m0 - HL + row;
-      const bool ok = real && slot < 8 && q >= 0 && q < P;
+      const bool ok = real && slot < 8 && q >= 0 && q < P && coff + slot * 8 < creal;
       raft_dma16(rs, base + j * NT * 16, ok ? (uint32_t)((q * stride + coff + slot * 8) * 2) : OOB);
     }
   };

@@ -105,11 +105,13 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
       const int dy = kh - a.PH, dx = kw - a.PW;
       const int dpix = dy * a.W + dx;
       const int coff = c0 - sbase;
+      const int creal = a.seg[s].real;
 #pragma unroll
       for (int j = 0; j < A_PER; ++j) {
         const int e = tid + j * NT;
         const int yy = a_y[j] + dy, xx = a_x[j] + dx;
-        const bool ok = (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W;
+        const bool ok = (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W &&
+                        coff + (e & 7) * 8 < creal;
         const uint32_t off = (uint32_t)(((a_pix[j] + dpix) * stride + coff + (e & 7) * 8) * 2);
         ra[j] = buf_load16(rs, ok ? off : OOB);
       }
@@ -374,10 +376,10 @@ int heuristic_cfg(int P, int cout, bool smallc, int epi) {
 }
 
 struct TuneKey {
-  int P, H, W, KH, KW, cin, cout, small, f32out;
+  int P, H, W, KH, KW, cin, cout, small, f32out, creal;
   bool operator<(const TuneKey& o) const {
-    return std::tie(P, H, W, KH, KW, cin, cout, small, f32out) <
-           std::tie(o.P, o.H, o.W, o.KH, o.KW, o.cin, o.cout, o.small, o.f32out);
+    return std::tie(P, H, W, KH, KW, cin, cout, small, f32out, creal) <
+           std::tie(o.P, o.H, o.W, o.KH, o.KW, o.cin, o.cout, o.small, o.f32out, o.creal);
   }
 };
 std::map<TuneKey, int> g_tuned;
@@ -483,8 +485,10 @@ int choose_cfg(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   const bool f32out = epi == EPI_F32 || epi == EPI_ACC_F32 || epi == EPI_DGRAD ||
                       epi == EPI_DGRAD_GATE || epi == EPI_F32_NCHW;
   const int eclass = f32out ? 1 : ((epi == EPI_GRU_ZR || epi == EPI_GRU_Q) ? 2 : 0);
+  int creal = 0;
+  for (int q = 0; q < a.nseg && q < 3; ++q) creal += a.seg[q].real;
   const TuneKey key{P, a.H, a.W, a.KH, a.KW, smallc ? a.cin_small : a.cin_pad, a.cout, (int)smallc,
-                    eclass};
+                    eclass, creal};
   std::lock_guard<std::mutex> lk(g_tune_mu);
   auto it = g_tuned.find(key);
   if (it != g_tuned.end()) return it->second;
@@ -531,9 +535,9 @@ int conv_import_tuned(const int* rows, int n) {
   std::lock_guard<std::mutex> lk(g_tune_mu);
   int done = 0;
   for (int i = 0; i < n; ++i) {
-    const int* r = rows + 12 * i;
+    const int* r = rows + 13 * i;
     if (r[9] < 0 || r[9] >= kNumCfgs) continue;  // a table from another build: keep our choice
-    g_tuned[TuneKey{r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], r[8]}] = r[9];
+    g_tuned[TuneKey{r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], r[8], r[12]}] = r[9];
     ++done;
   }
   return done;
@@ -546,9 +550,9 @@ int conv_tuned_table(int* out, int max_rows) {
     if (n >= max_rows) break;
     const TuneKey& k = kv.first;
     const CfgDesc& c = kCfgs[kv.second];
-    const int row[12] = {k.P, k.H, k.W, k.KH, k.KW, k.cin, k.cout, k.small, k.f32out, kv.second,
-                         c.bm, c.bn};
-    for (int i = 0; i < 12; ++i) out[n * 12 + i] = row[i];
+    const int row[13] = {k.P, k.H, k.W, k.KH, k.KW, k.cin, k.cout, k.small, k.f32out, kv.second,
+                         c.bm, c.bn, k.creal};
+    for (int i = 0; i < 13; ++i) out[n * 13 + i] = row[i];
     ++n;
   }
   return n;

@@ -18,6 +18,7 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -200,6 +201,145 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
                      q8[4] | ((uint32_t)q8[5] << 16), q8[6] | ((uint32_t)q8[7] << 16));
     }
     *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i) * cbuf + ch * 8) = o;
+  }
+}
+
+// Row-vector lookup (bf16 pyramid; the launcher's default): the window of a (pixel, level) is
+// 2r+2 rows of 2r+2 consecutive bf16 cells of the pixel's correlation plane.  Phase 1 fetches
+// every window row as whole ALIGNED 16-B pieces (2, or 3 when the row straddles a third piece) --
+// 2-3 vector loads per row instead of 2r+2 two-byte gathers, all of a thread's rows in flight at
+// once -- and parks them raw in LDS; phase 2 reads the row cells at the row's start offset inside
+// its pieces (LDS indexing is free), masks cells outside the plane and interpolates the (2r+1)^2
+// taps into the bf16 pixel-row tile; phase 3 streams the tile out as 16-B pixel-row pieces.
+constexpr int TPV = 16;  // pixels per workgroup (42 KB LDS: three workgroups per CU)
+
+template <int R>
+__global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const float* __restrict__ coords,
+                                                               uint16_t* __restrict__ out, int cbuf,
+                                                               int B, int H, int W, int levels) {
+  constexpr int D = 2 * R + 1, E = D + 1;
+  constexpr int ROWT = (4 * D * D + 7) / 8 * 8;
+  constexpr uint32_t OOB = 0x80000000u;
+  __shared__ __attribute__((aligned(16))) uint4 rows[TPV * 4 * E * 3];
+  __shared__ float cxy[TPV * 4 * 2];
+  __shared__ __attribute__((aligned(16))) uint16_t tile[TPV * ROWT];
+  const int N = H * W;
+  const int tiles = (N + TPV - 1) / TPV;
+  const int b = blockIdx.x / tiles;
+  const int i0 = (blockIdx.x % tiles) * TPV;
+  const int tid = threadIdx.x;
+  const int npx = min(TPV, N - i0);
+  if (tid < TPV * 4) {
+    const int px = tid >> 2, l = tid & 3;
+    const int i = min(i0 + px, N - 1);
+    const float inv = 1.0f / (float)(1 << l);
+    cxy[tid * 2] = clampc(coords[((int64_t)b * 2) * N + i] * inv);
+    cxy[tid * 2 + 1] = clampc(coords[((int64_t)b * 2 + 1) * N + i] * inv);
+  }
+  // per level: a 16-B aligned base at or below this workgroup's first plane; `dl` = elements
+  // between that base and the first plane (0..7)
+  __amdgpu_buffer_rsrc_t rs[4];
+  int dl[4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    const int ll = l < levels ? l : 0;
+    const int64_t plane = (int64_t)pyr.h[ll] * pyr.w[ll];
+    const int64_t first = ((int64_t)b * N + i0) * plane;  // element index of the first plane
+    const int64_t abase = first & ~(int64_t)7;
+    dl[l] = (int)(first - abase);
+    const uint16_t* base = reinterpret_cast<const uint16_t*>(pyr.lvl[ll]) + abase;
+    const uint32_t bytes = (uint32_t)((dl[l] + (int64_t)npx * plane) * 2);
+    rs[l] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), (short)0, (int)bytes,
+                                             0x00020000);
+  }
+  __syncthreads();
+  // ---- phase 1: every window row's aligned 16-B pieces -> LDS (all loads before any store)
+  constexpr int ITEMS = TPV * 4 * E;
+  constexpr int PER = (ITEMS + 255) / 256;
+  uint4 v[PER][3];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + k * 256;
+    const int px = e / (4 * E), rem = e - px * (4 * E), l = rem / E, r = rem - l * E;
+    uint32_t o0 = OOB, o1 = OOB, o2 = OOB;
+    int lq = 0;
+    if (e < ITEMS && px < npx && l < levels) {
+      lq = l;
+      const int hl = pyr.h[l], wl = pyr.w[l];
+      const float cx = cxy[(px * 4 + l) * 2], cy = cxy[(px * 4 + l) * 2 + 1];
+      const int xs = (int)floorf(cx) - R, gy = (int)floorf(cy) - R + r;
+      if ((unsigned)gy < (unsigned)hl) {
+        const int er = dl[l] + px * hl * wl + gy * wl + xs;  // element offset of the row start
+        const int q0 = er >> 3;  // floor: er < 0 only before the first plane (cells masked)
+        o0 = q0 >= 0 ? (uint32_t)q0 * 16u : OOB;
+        o1 = q0 + 1 >= 0 ? (uint32_t)(q0 + 1) * 16u : OOB;
+        o2 = (er & 7) + E > 16 && q0 + 2 >= 0 ? (uint32_t)(q0 + 2) * 16u : OOB;
+      }
+    }
+    const __amdgpu_buffer_rsrc_t r0 = lq == 0 ? rs[0] : (lq == 1 ? rs[1] : (lq == 2 ? rs[2] : rs[3]));
+    v[k][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r0, o0, 0, 0));
+    v[k][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r0, o1, 0, 0));
+    v[k][2] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r0, o2, 0, 0));
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int e = tid + k * 256;
+    if (e < ITEMS) {
+      rows[e * 3] = v[k][0];
+      rows[e * 3 + 1] = v[k][1];
+      rows[e * 3 + 2] = v[k][2];
+    }
+  }
+  __syncthreads();
+  // ---- phase 2: (pixel, level, window row iy) -> the 2r+1 taps of that row
+  const int items2 = TPV * levels * D;
+  for (int it = tid; it < items2; it += 256) {
+    const int px = it / (levels * D), rem = it - px * (levels * D), l = rem / D, iy = rem - l * D;
+    const int hl = pyr.h[l], wl = pyr.w[l];
+    const float cx = cxy[(px * 4 + l) * 2], cy = cxy[(px * 4 + l) * 2 + 1];
+    const float fx = floorf(cx), fy = floorf(cy);
+    const float ax = cx - fx, ay = cy - fy;
+    const int xs = (int)fx - R, ys = (int)fy - R;
+    float hr[2][D];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int r = iy + k, gy = ys + r;
+      const bool rowok = (unsigned)gy < (unsigned)hl;
+      const int er = dl[l] + px * hl * wl + gy * wl + xs;
+      const uint16_t* src = reinterpret_cast<const uint16_t*>(rows + ((px * 4 + l) * E + r) * 3) + (er & 7);
+      float c[E];
+#pragma unroll
+      for (int xx = 0; xx < E; ++xx) {
+        const int gx = xs + xx;
+        c[xx] = (rowok && (unsigned)gx < (unsigned)wl) ? raft_bf16_to_f32(src[xx]) : 0.f;
+      }
+#pragma unroll
+      for (int ix = 0; ix < D; ++ix) hr[k][ix] = (1.f - ax) * c[ix] + ax * c[ix + 1];
+    }
+    uint16_t* T = tile + px * ROWT + l * D * D;
+#pragma unroll
+    for (int ix = 0; ix < D; ++ix) T[ix * D + iy] = raft_f32_to_bf16((1.f - ay) * hr[0][ix] + ay * hr[1][ix]);
+  }
+  __syncthreads();
+  // ---- phase 3: whole 16-B pieces of the (B,H,W,cbuf) rows, zero padding included
+  const int ctot = levels * D * D;
+  const int chunks = cbuf / 8;
+  for (int e = tid; e < npx * chunks; e += 256) {
+    const int px = e / chunks, ch = e - px * chunks;
+    uint4 o;
+    if (ch * 8 + 8 <= ctot) {
+      o = *reinterpret_cast<const uint4*>(tile + px * ROWT + ch * 8);
+    } else {
+      uint16_t q8[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int c = ch * 8 + q;
+        q8[q] = c < ctot ? tile[px * ROWT + c] : (uint16_t)0;
+      }
+      o = make_uint4(q8[0] | ((uint32_t)q8[1] << 16), q8[2] | ((uint32_t)q8[3] << 16),
+                     q8[4] | ((uint32_t)q8[5] << 16), q8[6] | ((uint32_t)q8[7] << 16));
+    }
+    *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i0 + px) * cbuf + ch * 8) = o;
   }
 }
 
@@ -462,6 +602,116 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
   }
 }
 
+// Wave-per-query-pixel fold (the launcher's default): the same per-cell arithmetic and iteration
+// order as corr_tap_reduce_kernel (bitwise the same dC), but each WAVE owns one query pixel's
+// level planes in its own LDS slice, so there is no workgroup barrier at all: a wave's LDS
+// operations execute in issue order, which orders the iterations' read-modify-writes and makes
+// the staged tap row visible to the wave's other lanes.  The next iteration's tap row is in
+// flight (registers) while the current one is folded.  Plane zero fill and the level-0 row
+// write-out are 16-B / 4-B vector operations.  ~17 KB of LDS per wave at chairs (1/8 = 46 x 62).
+template <int R>
+__global__ __launch_bounds__(256) void corr_tap_reduce_wave_kernel(TapList tl, int levels, int B, int H,
+                                                                   int W, float inv_sqrt_c,
+                                                                   void* __restrict__ out, int out_bf16,
+                                                                   int wave_bytes) {
+  constexpr int D = 2 * R + 1, E = D + 1;
+  constexpr int CPL = (4 * E * E + 63) / 64;  // window cells per lane (all levels)
+  extern __shared__ float lds_all[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int N = H * W;
+  const int64_t q = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (q >= (int64_t)B * N) return;  // no workgroup barrier below: waves retire independently
+  const int b = (int)(q / N), i = (int)(q - (int64_t)b * N);
+  float* planes = lds_all + wv * (wave_bytes / 4);
+  int hs[4], ws[4], off[4];
+  int tot = 0;
+  {
+    int h = H, w = W;
+    for (int l = 0; l < 4; ++l) {
+      hs[l] = h; ws[l] = w; off[l] = tot;
+      if (l < levels) tot += h * w;
+      h >>= 1; w >>= 1;
+    }
+  }
+  const int tot4 = (tot + 3) & ~3;
+  const int ctot = levels * D * D;
+  const int chunks = (ctot + 7) / 8;
+  const int trow = chunks * 8;
+  uint16_t* taps = reinterpret_cast<uint16_t*>(planes + tot4);  // [2][trow] double buffer
+  for (int e = lane; e < tot4 / 4; e += 64) reinterpret_cast<uint4*>(planes)[e] = make_uint4(0, 0, 0, 0);
+  int cl[CPL], cyy[CPL], cxx[CPL];
+  float cinv[CPL];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k) {
+    const int e = lane + k * 64;
+    cl[k] = e < levels * E * E ? e / (E * E) : -1;
+    cyy[k] = (e / E) % E;
+    cxx[k] = e % E;
+    cinv[k] = cl[k] >= 0 ? 1.0f / (float)(1 << cl[k]) : 0.f;
+  }
+  const int64_t prow = ((int64_t)b * N + i) * tl.cbuf;
+  uint4 piece = make_uint4(0, 0, 0, 0);
+  if (lane < chunks) piece = *reinterpret_cast<const uint4*>(tl.dout[0] + prow + lane * 8);
+  for (int k = 0; k < tl.n; ++k) {
+    const float* C = tl.coords[k];
+    const float cx = C[((int64_t)b * 2) * N + i], cy = C[((int64_t)b * 2 + 1) * N + i];
+    uint16_t* T0 = taps + (k & 1) * trow;
+    if (lane < chunks) reinterpret_cast<uint4*>(T0)[lane] = piece;
+    if (k + 1 < tl.n && lane < chunks)
+      piece = *reinterpret_cast<const uint4*>(tl.dout[k + 1] + prow + lane * 8);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int l = cl[c];
+      if (l < 0) continue;
+      const int yy = cyy[c], xx = cxx[c];
+      const float fxc = clampc(cx * cinv[c]), fyc = clampc(cy * cinv[c]);
+      const float flx = floorf(fxc), fly = floorf(fyc);
+      const int gy = (int)fly - R + yy, gx = (int)flx - R + xx;
+      if (gy < 0 || gy >= hs[l] || gx < 0 || gx >= ws[l]) continue;
+      const float ax = fxc - flx, ay = fyc - fly;
+      const uint16_t* T = T0 + l * D * D;
+      float acc = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int iy = yy - kk;
+        if (iy < 0 || iy >= D) continue;
+        const float wy = kk == 0 ? (1.f - ay) : ay;
+        float sx = 0.f;
+        if (xx < D) sx += (1.f - ax) * raft_bf16_to_f32(T[xx * D + iy]);
+        if (xx > 0) sx += ax * raft_bf16_to_f32(T[(xx - 1) * D + iy]);
+        acc += wy * sx;
+      }
+      planes[off[l] + gy * ws[l] + gx] += acc;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  const int64_t row = ((int64_t)b * N + i) * N;
+  const float inv_w = 1.0f / (float)W;
+  auto cell = [&](int e) {
+    const int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W;  // exact for e < 2^22
+    float v = planes[e];
+    float sc = 0.25f;
+    for (int l = 1; l < levels; ++l) {
+      const int yl = y >> l, xl = x >> l;
+      if (yl < hs[l] && xl < ws[l]) v += sc * planes[off[l] + yl * ws[l] + xl];
+      sc *= 0.25f;
+    }
+    return v * inv_sqrt_c;
+  };
+  if (out_bf16 && (N & 1) == 0) {
+    uint32_t* Ob = reinterpret_cast<uint32_t*>((uint16_t*)out + row);
+    for (int e2 = lane; e2 < N / 2; e2 += 64)
+      Ob[e2] = (uint32_t)raft_f32_to_bf16(cell(2 * e2)) | ((uint32_t)raft_f32_to_bf16(cell(2 * e2 + 1)) << 16);
+  } else if (out_bf16) {
+    uint16_t* Ob = (uint16_t*)out + row;
+    for (int e = lane; e < N; e += 64) Ob[e] = raft_f32_to_bf16(cell(e));
+  } else {
+    float* O = (float*)out + row;
+    for (int e = lane; e < N; e += 64) O[e] = cell(e);
+  }
+}
+
 }  // namespace
 
 bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* ws, int levels,
@@ -483,6 +733,16 @@ bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* w
     if (radius == 4) hipLaunchKernelGGL(corr_lookup_tile_kernel<4>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
     else if (radius == 3) hipLaunchKernelGGL(corr_lookup_tile_kernel<3>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
     else return false;
+    return true;
+  }
+  static const bool v1 = [] {
+    const char* e = getenv("RAFT_LOOKUP_V1");
+    return e && e[0] == '1';
+  }();
+  if (pyr_bf16 && !v1 && (radius == 4 || radius == 3)) {
+    dim3 grid((unsigned)(B * ((N + TPV - 1) / TPV)));
+    if (radius == 4) hipLaunchKernelGGL(corr_lookup_rows_kernel<4>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+    else hipLaunchKernelGGL(corr_lookup_rows_kernel<3>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
     return true;
   }
   dim3 grid((unsigned)(B * ((N + TPW - 1) / TPW)));
@@ -532,6 +792,23 @@ bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, 
                             float inv_sqrt_c, void* out, int out_bf16, hipStream_t stream) {
   const int D = 2 * radius + 1;
   if ((levels * D * D + 7) / 8 * 6 > 256) return false;  // one 16-B piece per thread per chunk
+  static const bool v1 = [] {
+    const char* e = getenv("RAFT_TAPRED_V1");
+    return e && e[0] == '1';
+  }();
+  if (!v1 && (radius == 4 || radius == 3)) {
+    // one wave per query pixel: its level planes + a double-buffered tap row in its LDS slice
+    int tot = 0, h = H, w = W;
+    for (int l = 0; l < levels; ++l) { tot += h * w; h >>= 1; w >>= 1; }
+    const int trow = (levels * D * D + 7) / 8 * 8;
+    const int wave_bytes = (((tot + 3) & ~3) * 4 + 2 * trow * 2 + 15) & ~15;
+    const int wpb = std::max(1, std::min(4, (64 * 1024) / wave_bytes));
+    const int64_t P = (int64_t)B * H * W;
+    dim3 grid((unsigned)((P + wpb - 1) / wpb));
+    if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<4>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, wave_bytes);
+    else hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<3>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, wave_bytes);
+    return true;
+  }
   const int lds = corr_tap_reduce_lds_bytes(H, W, levels, radius);
   dim3 grid((unsigned)(B * H * W));
   if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_kernel<4>, grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16);

@@ -8,13 +8,14 @@
 //
 //   stats     per (image, channel) [instance] or per channel [batch] shifted sums  sum(x-K),
 //             sum((x-K)^2) -> per-workgroup partials (deterministic, no atomics)
-//   finalize  partials -> mean / invstd, the affine fold into one scale/shift per (image, channel),
+//   finalize  partials reduced (same launch) -> mean / invstd, the affine fold into one scale/shift per (image, channel),
 //             BatchNorm running-stat update; the conv bias is folded here too (it cancels in a
 //             training-mode norm, and shifts the eval-mode one), so the conv runs without bias
 //   apply     y = act(x * scale + shift) [+ residual, ReLU]     (16-B vectors, 8 channels/thread)
 //   backward  partial sums of g, g*xhat, xhat (g = dy masked by the ReLU, the mask recomputed from
-//             x -- y is never read back) -> finalize -> one pass dx = A*g + B*xhat + C.  The
-//             conv-bias gradient falls out of the same sums.
+//             x -- y is never read back) -> reduce + finalize (one launch) -> one pass
+//             dx = A*g + B*xhat + C, whose first workgroup also sums the parameter gradients over
+//             the groups.  The conv-bias gradient falls out of the same sums.
 //
 // Channel counts are multiples of 8 up to 256; a thread owns one 16-B channel group of a pixel.
 #include "common.h"
@@ -140,45 +141,9 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
   }
 }
 
-// part [groups][nblk][S*C] -> sums [groups][S*C]: LANES lanes per column stride over the partials,
-// fixed-order LDS combine (deterministic); block = (256 / LANES) columns x LANES lanes,
-// grid (groups, ceil(S*C / (256 / LANES))).  16 lanes for the long batch-norm partial lists
-// (hundreds of blocks over all images), 4 for the per-image ones.
-template <int LANES>
-__global__ __launch_bounds__(256) void partial_reduce_kernel(const float* __restrict__ part,
-                                                             int nblk, int SC,
-                                                             float* __restrict__ sums) {
-  constexpr int COLS = 256 / LANES;
-  __shared__ float red[LANES][COLS];
-  const int gi = blockIdx.x;
-  const int t = threadIdx.x % COLS;
-  const int col = blockIdx.y * COLS + t;
-  const int lane = threadIdx.x / COLS;
-  float a = 0.f;
-  if (col < SC)
-    for (int k = lane; k < nblk; k += LANES) a += part[((int64_t)gi * nblk + k) * SC + col];
-  red[lane][t] = a;
-  __syncthreads();
-  if (lane == 0 && col < SC) {
-    float s = 0.f;
-#pragma unroll
-    for (int l = 0; l < LANES; ++l) s += red[l][t];
-    sums[(int64_t)gi * SC + col] = s;
-  }
-}
-
-void launch_partial_reduce(const float* part, int groups, int nblk, int SC, float* sums,
-                           hipStream_t stream) {
-  if (nblk > 64)
-    hipLaunchKernelGGL(partial_reduce_kernel<16>, dim3(groups, (SC + 15) / 16), dim3(256), 0, stream,
-                       part, nblk, SC, sums);
-  else
-    hipLaunchKernelGGL(partial_reduce_kernel<4>, dim3(groups, (SC + 63) / 64), dim3(256), 0, stream,
-                       part, nblk, SC, sums);
-}
-
 // mode: 0 instance (train or eval: always batch statistics), 1 batch-train, 2 batch-eval, 3 none
-// one thread per (group image, channel)
+// one thread per (group image, channel); the training-statistics modes run
+// norm_reduce_finalize_kernel instead
 __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint16_t* __restrict__ x,
                                      int HW, int C, int groups_img, int nblk, int cnt, int mode,
                                      const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -216,6 +181,63 @@ __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint1
   mean_out[idx] = mean;
   invstd_out[idx] = invstd;
   // per-image scale/shift table [nimg][C] (instance: its own group; batch/none: shared)
+  for (int n = (mode == 0 ? gi : 0); n < (mode == 0 ? gi + 1 : nimg); ++n) {
+    scale[(int64_t)n * C + c] = gm * invstd;
+    shift[(int64_t)n * C + c] = bt - mean * gm * invstd;
+  }
+}
+
+// Partial reduce + finalize of the training statistics in ONE launch: block = COLS channels x
+// LANES lanes of one group (grid (groups, ceil(C / COLS))); the lanes stride over the group's
+// per-workgroup partials, a fixed-order LDS combine (deterministic), then lane 0 finalizes its
+// (group, channel).  16 lanes for the long batch-norm partial lists, 4 for per-image ones.
+template <int LANES>
+__global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(
+    const float* __restrict__ part, int nblk, const uint16_t* __restrict__ x, int HW, int C,
+    int cnt, int mode, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ cbias, float* __restrict__ rmean, float* __restrict__ rvar,
+    float momentum, float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out,
+    float* __restrict__ scale, float* __restrict__ shift, int nimg) {
+  constexpr int COLS = 256 / LANES;
+  __shared__ float red[2][LANES][COLS];
+  const int gi = blockIdx.x;
+  const int t = threadIdx.x % COLS, lane = threadIdx.x / COLS;
+  const int c = blockIdx.y * COLS + t;
+  const int SC = 2 * C;
+  float a = 0.f, q = 0.f;
+  if (c < C)
+    for (int k = lane; k < nblk; k += LANES) {
+      const float* pk = part + ((int64_t)gi * nblk + k) * SC;
+      a += pk[c];
+      q += pk[C + c];
+    }
+  red[0][lane][t] = a;
+  red[1][lane][t] = q;
+  __syncthreads();
+  if (lane != 0 || c >= C) return;
+  float sa = 0.f, sq = 0.f;
+#pragma unroll
+  for (int l = 0; l < LANES; ++l) {
+    sa += red[0][l][t];
+    sq += red[1][l][t];
+  }
+  const float b = cbias ? cbias[c] : 0.f;
+  const double m = (double)sa / cnt;
+  double var = (double)sq / cnt - m * m;
+  if (var < 0.0) var = 0.0;
+  const float K = raft_bf16_to_f32(x[(int64_t)(mode == 0 ? gi : 0) * HW * C + c]);
+  const float mean = (float)(m + K);
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  if (mode == 1 && rmean != nullptr) {
+    const double unb = cnt > 1 ? var * cnt / (cnt - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (mean + b);
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+  }
+  const float gm = mode == 1 && gamma ? gamma[c] : 1.f;
+  const float bt = mode == 1 && beta ? beta[c] : 0.f;
+  const int idx = gi * C + c;
+  mean_out[idx] = mean;
+  invstd_out[idx] = invstd;
   for (int n = (mode == 0 ? gi : 0); n < (mode == 0 ? gi + 1 : nimg); ++n) {
     scale[(int64_t)n * C + c] = gm * invstd;
     shift[(int64_t)n * C + c] = bt - mean * gm * invstd;
@@ -416,63 +438,71 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
   }
 }
 
-// -> per (group image, c) coefficients dx = A*g + B*xhat + Cc, plus dgamma/dbeta/dcbias summed
-// over the groups: block = 64 channels x 4 group lanes (fixed-order LDS combine, deterministic)
-__global__ __launch_bounds__(256) void norm_bwd_finalize_kernel(
-    const float* __restrict__ part, int C, int groups_img, int nblk, int cnt, int mode,
+// Backward partial reduce + per-group finalize in ONE launch: block =
+// COLS channels x LANES lanes of one group (grid (groups, ceil(C / COLS))); lanes stride over the
+// group's partials, fixed-order LDS combine, then lane 0 writes the group's coefficients and its
+// contributions (sum g*xhat, sum g, conv-bias term) to pg [groups][3][C]; the apply kernel's
+// first workgroup sums pg over the groups (fixed order) into dgamma / dbeta / dcbias.
+template <int LANES>
+__global__ __launch_bounds__(256) void norm_bwd_reduce_finalize_kernel(
+    const float* __restrict__ part, int nblk, int C, int cnt, int mode,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean,
-    const float* __restrict__ invstd, float* __restrict__ coef,
-    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dcbias) {
-  __shared__ double red[3][4][64];
-  const int t = threadIdx.x & 63, lane = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + t;
-  double dg = 0.0, db = 0.0, dcb = 0.0;
-  if (c < C) {
-    const float gm = (mode == 1 || mode == 2) && gamma ? gamma[c] : 1.f;
-    for (int gi = lane; gi < groups_img; gi += 4) {
-      const float* p = part + (int64_t)gi * 3 * C;
-      const double sg = p[c], sgx = p[C + c], sx = p[2 * C + c];
-      const float is = invstd[(int64_t)gi * C + c];
-      float A, B, Cc;
-      if (mode == 0 || mode == 1) {
-        const double mg = sg / cnt, mgx = sgx / cnt;
-        A = gm * is;
-        B = (float)(-gm * is * mgx);
-        Cc = (float)(-gm * is * mg);
-        // sum over the group of dx = A*sg + B*sx + C*cnt
-        dcb += A * sg + B * sx + (double)Cc * cnt;
-      } else {
-        A = gm * is;  // eval batch norm / none: an affine map
-        B = 0.f;
-        Cc = 0.f;
-        dcb += A * sg;
-      }
-      // dx = A*g + B*xhat + Cc = A*g + (B*is)*x + (Cc - B*is*mean); sc / sh: the forward affine
-      // (the apply pass recomputes the ReLU mask from x with them)
-      const float mu = mean[(int64_t)gi * C + c];
-      float sc, sh;
-      norm_affine(mode, gamma, beta, c, mu, is, sc, sh);
-      // structure-of-arrays [group][field][C]: a thread's 8 channels of a field are 2 x 16 B
-      float* co = coef + (int64_t)gi * 5 * C + c;
-      co[0] = A;
-      co[C] = B * is;
-      co[2 * C] = Cc - B * is * mu;
-      co[3 * C] = sc;
-      co[4 * C] = sh;
-      dg += sgx;
-      db += sg;
+    const float* __restrict__ invstd, float* __restrict__ coef, float* __restrict__ pg) {
+  constexpr int COLS = 256 / LANES;
+  __shared__ float red[3][LANES][COLS];
+  const int gi = blockIdx.x;
+  const int t = threadIdx.x % COLS, lane = threadIdx.x / COLS;
+  const int c = blockIdx.y * COLS + t;
+  float a = 0.f, b = 0.f, s = 0.f;
+  if (c < C)
+    for (int k = lane; k < nblk; k += LANES) {
+      const float* pk = part + ((int64_t)gi * nblk + k) * 3 * C;
+      a += pk[c];
+      b += pk[C + c];
+      s += pk[2 * C + c];
     }
-  }
-  red[0][lane][t] = dg;
-  red[1][lane][t] = db;
-  red[2][lane][t] = dcb;
+  red[0][lane][t] = a;
+  red[1][lane][t] = b;
+  red[2][lane][t] = s;
   __syncthreads();
-  if (lane == 0 && c < C) {
-    // plain stores: one thread owns each channel (the outputs need no zero fill)
-    if (dgamma) dgamma[c] = (float)((red[0][0][t] + red[0][1][t]) + (red[0][2][t] + red[0][3][t]));
-    if (dbeta) dbeta[c] = (float)((red[1][0][t] + red[1][1][t]) + (red[1][2][t] + red[1][3][t]));
-    if (dcbias) dcbias[c] = (float)((red[2][0][t] + red[2][1][t]) + (red[2][2][t] + red[2][3][t]));
+  if (lane != 0 || c >= C) return;
+  float fsg = 0.f, fsgx = 0.f, fsx = 0.f;
+#pragma unroll
+  for (int l = 0; l < LANES; ++l) {
+    fsg += red[0][l][t];
+    fsgx += red[1][l][t];
+    fsx += red[2][l][t];
   }
+  const double sg = fsg, sgx = fsgx, sx = fsx;
+  const float gm = (mode == 1 || mode == 2) && gamma ? gamma[c] : 1.f;
+  const float is = invstd[(int64_t)gi * C + c];
+  float A, B, Cc;
+  double dcb;
+  if (mode == 0 || mode == 1) {
+    const double mg = sg / cnt, mgx = sgx / cnt;
+    A = gm * is;
+    B = (float)(-gm * is * mgx);
+    Cc = (float)(-gm * is * mg);
+    dcb = A * sg + B * sx + (double)Cc * cnt;
+  } else {
+    A = gm * is;
+    B = 0.f;
+    Cc = 0.f;
+    dcb = A * sg;
+  }
+  const float mu = mean[(int64_t)gi * C + c];
+  float sc, sh;
+  norm_affine(mode, gamma, beta, c, mu, is, sc, sh);
+  float* co = coef + (int64_t)gi * 5 * C + c;
+  co[0] = A;
+  co[C] = B * is;
+  co[2 * C] = Cc - B * is * mu;
+  co[3 * C] = sc;
+  co[4 * C] = sh;
+  float* q = pg + (int64_t)gi * 3 * C + c;
+  q[0] = fsgx;
+  q[C] = fsg;
+  q[2 * C] = (float)dcb;
 }
 
 // dx = A*g + B'*x + C' with g = dy masked by the forward ReLU (read from y when given, else
@@ -481,8 +511,24 @@ __global__ __launch_bounds__(256) void norm_bwd_finalize_kernel(
 __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint16_t* __restrict__ y,
     const float* __restrict__ coef, int HW, int C, int per_image, int64_t nvec, int relu,
-    uint16_t* __restrict__ dx) {
+    uint16_t* __restrict__ dx, const float* __restrict__ pg, int groups, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float* __restrict__ dcbias) {
   const int cg = C / 8;
+  if (pg != nullptr && blockIdx.x == 0) {
+    // parameter gradients: the groups' contributions summed in a fixed order
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      double dg = 0.0, db = 0.0, dcb = 0.0;
+      for (int gi = 0; gi < groups; ++gi) {
+        const float* q = pg + (int64_t)gi * 3 * C + c;
+        dg += q[0];
+        db += q[C];
+        dcb += q[2 * C];
+      }
+      if (dgamma) dgamma[c] = (float)dg;
+      if (dbeta) dbeta[c] = (float)db;
+      if (dcbias) dcbias[c] = (float)dcb;
+    }
+  }
   for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
     const int64_t pix = v / cg;
     const int g = (int)(v - pix * cg);
@@ -550,12 +596,19 @@ void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, i
   const int groups = mode == 0 ? N : 1;
   const int cnt = mode == 0 ? HW : N * HW;
   const int tot = groups * C;
-  // part holds nblk partials per group followed by room for the per-group sums
-  float* sums = nullptr;
   if (mode <= 1) {
-    sums = const_cast<float*>(part) + (int64_t)groups * nblk * 2 * C;
-    launch_partial_reduce(part, groups, nblk, 2 * C, sums, stream);
+    // training statistics: partial reduce + finalize in one launch
+    if (nblk > 64)
+      hipLaunchKernelGGL(norm_reduce_finalize_kernel<16>, dim3(groups, (C + 15) / 16), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
+    else
+      hipLaunchKernelGGL(norm_reduce_finalize_kernel<4>, dim3(groups, (C + 63) / 64), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
+    return;
   }
+  float* sums = nullptr;
   hipLaunchKernelGGL(norm_finalize_kernel, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
                      C, groups, nblk, cnt, mode, gamma, beta, cbias, rmean, rvar, momentum, eps, mean,
                      invstd, scale, shift, N);
@@ -599,11 +652,16 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
     hipLaunchKernelGGL(norm_bwd_stats_kernel, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
                        beta, mode, HW, C, 0, pix_per_blk, N * HW, relu, part);
   }
-  float* sums = part + (int64_t)groups * nblk * 3 * C;
-  launch_partial_reduce(part, groups, nblk, 3 * C, sums, stream);
-  hipLaunchKernelGGL(norm_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, stream, sums, C,
-                     groups, nblk, cnt, mode, gamma, beta, mean, invstd, coef, dgamma, dbeta, dcbias);
+  // per-group sums + coefficients in one launch; pg (the groups' parameter-gradient terms) sits
+  // after the partials in `part`
+  float* pg = part + (int64_t)groups * nblk * 3 * C;
+  if (nblk > 64)
+    hipLaunchKernelGGL(norm_bwd_reduce_finalize_kernel<16>, dim3(groups, (C + 15) / 16), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
+  else
+    hipLaunchKernelGGL(norm_bwd_reduce_finalize_kernel<4>, dim3(groups, (C + 63) / 64), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
   const int64_t nvec = (int64_t)N * HW * C / 8;
   hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
-                     HW, C, per_image, nvec, relu, dx);
+                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias);
 }

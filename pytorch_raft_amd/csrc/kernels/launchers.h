@@ -91,6 +91,9 @@ struct Seg {
   const uint16_t* ptr;  // bf16 NHWC base, already offset to the segment's first channel
   int stride;           // elements between consecutive pixels
   int cnt;              // channels (multiple of 32 unless SMALLC)
+  int real;             // channels present (<= cnt, multiple of 8): the forward / dgrad kernels
+                        // read the rest of the segment's K slot as zeros (a 96-channel tensor
+                        // runs with a 128-channel K slot whose padded weights are zero)
 };
 
 struct OSeg {
@@ -160,7 +163,7 @@ struct ConvFwdArgs {
 bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStream_t stream);
 // LDS-DMA kernel of config `idx` (conv_glds.hip); false for a non-LDS-DMA index
 bool launch_conv_glds(const ConvFwdArgs& a, int epi, int idx, hipStream_t stream);
-// rows of 12 ints: P H W KH KW cin cout small epi_class cfg BM BN
+// rows of 13 ints: P H W KH KW cin cout small epi_class cfg BM BN channels-present
 int conv_tuned_table(int* out, int max_rows);
 // tests: run every following conv launch with config `idx` (-1: back to the tuned choice)
 void conv_set_forced_cfg(int idx);
@@ -220,6 +223,8 @@ bool launch_conv_wgrad(const ConvWgradArgs& a, int bm, bool smallc, float* db, h
 void launch_col_sum(const uint16_t* g, int stride, int cout, int P, float* db, hipStream_t stream);
 
 // ---- fused update-block elementwise kernels (update_ew.hip)
+// empty kernel `raft_phase_marker_kernel` (trace phase boundaries, scripts/prof_diff.py --phases)
+void launch_phase_marker(hipStream_t stream);
 // stride-1 3x3 64 -> 64 NHWC bf16 conv (conv_enc64.hip); wpk = (64, 9*64) packed [n][tap*64 + c]
 bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, int B, int H, int W,
                        int grid_cap, hipStream_t stream);

@@ -23,12 +23,20 @@ multi-tensor kernel.  Two execution modes:
 
 A device-side non-finite flag is accumulated for failure detection and checked at logging cadence.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
 from ..ops.loss import sequence_loss
 from ..parallel import dist as pdist
 from .optim import fetch_optimizer, clip_grad_norm_
+
+
+# RAFT_PHASE_MARKS=1: an empty marker kernel before and after each decode replay, so a kernel
+# trace splits into encoder forward / decode (update block, correlation, loss) / encoder backward +
+# update (scripts/prof_diff.py --phases, scripts/categorize.py)
+_PHASE_MARKS = os.environ.get('RAFT_PHASE_MARKS', '0') == '1'
 
 
 class TrainState:
@@ -258,7 +266,11 @@ class GraphedTrainStep:
             pdist.broadcast_buffers(st.model)  # DataParallel semantics: replica 0's BN stats
         feats = self._encode_and_stage(image1, image2, flow, valid)
         if graphs:
+            if _PHASE_MARKS:
+                torch.ops.raft_amd.phase_mark()
             self.g_dec.replay()
+            if _PHASE_MARKS:
+                torch.ops.raft_amd.phase_mark()
             loss = self.loss
         else:
             loss, _ = self._decode()

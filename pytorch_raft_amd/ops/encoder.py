@@ -54,7 +54,8 @@ class _NormAct(torch.autograd.Function):
         if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and norm.track_running_stats:
             rm, rv = norm.running_mean, norm.running_var
             if mode == MODE_BATCH_TRAIN:
-                norm.num_batches_tracked.add_(1)
+                # num_batches_tracked: incremented for every batch norm of the encoder at once
+                # (one multi-tensor add in encoder_forward)
                 momentum = norm.momentum if norm.momentum is not None else \
                     1.0 / float(norm.num_batches_tracked.item())
         mean, invstd = _ext.ops().norm_fwd_(x, mode, int(relu), gamma, beta, cbias, rm, rv,
@@ -100,7 +101,8 @@ class _NormActAddRelu(torch.autograd.Function):
         if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and norm.track_running_stats:
             rm, rv = norm.running_mean, norm.running_var
             if mode == MODE_BATCH_TRAIN:
-                norm.num_batches_tracked.add_(1)
+                # num_batches_tracked: incremented for every batch norm of the encoder at once
+                # (one multi-tensor add in encoder_forward)
                 momentum = norm.momentum if norm.momentum is not None else \
                     1.0 / float(norm.num_batches_tracked.item())
         res = res.contiguous(memory_format=torch.channels_last)
@@ -160,26 +162,36 @@ class _CastWeightsCL(torch.autograd.Function):
     Per conv, ``weight.to(bf16).contiguous(channels_last)`` and the backward cast of its bf16
     gradient are 2-3 tiny kernels each (~100 launches per step for both encoders).  Here the
     forward is cat -> permuting gather -> cast and the backward cat -> cast -> inverse gather, with
-    the index maps built once per weight geometry."""
+    the index maps built once per weight geometry.  The same gather also lays out, for every
+    native stride-1 3x3 conv, the ADJOINT weight (flipped taps, Cin <-> Cout: the input-gradient
+    conv's packed [ci][tap * co' + o] operand) and -- when Cin is not a multiple of 64 (the 96-
+    channel convs) -- a forward pack with 64-aligned K slots [co][tap * ci' + c] whose padded
+    entries read a zero element; the backward then runs no per-conv flip / transpose / pad
+    kernels.  Those extra outputs carry no gradient."""
 
     @staticmethod
     def forward(ctx, maps, *ws):
-        perm, inv, shapes = maps
-        flat = torch.cat([w.reshape(-1) for w in ws])
+        perm, inv, shapes, extra = maps
+        flat = torch.cat([w.reshape(-1) for w in ws] + [ws[0].new_zeros(1)])
         packed = flat.index_select(0, perm).to(torch.bfloat16)
         outs, off = [], 0
         for (co, ci, kh, kw) in shapes:
             n = co * ci * kh * kw
             outs.append(packed[off:off + n].view(co, kh, kw, ci).permute(0, 3, 1, 2))
             off += n
+        ext = []
+        for _, rows, cols in extra:
+            ext.append(packed[off:off + rows * cols].view(rows, cols))
+            off += rows * cols
         ctx.maps = maps
-        return tuple(outs)
+        ctx.mark_non_differentiable(*ext)
+        return tuple(outs) + tuple(ext)
 
     @staticmethod
     def backward(ctx, *gs):
-        perm, inv, shapes = ctx.maps
+        perm, inv, shapes, extra = ctx.maps
         parts = []
-        for g, (co, ci, kh, kw) in zip(gs, shapes):
+        for g, (co, ci, kh, kw) in zip(gs[:len(shapes)], shapes):
             if g is None:
                 g = torch.zeros(co, ci, kh, kw, device=perm.device, dtype=torch.bfloat16)
             parts.append(g.permute(0, 2, 3, 1).reshape(-1))
@@ -195,27 +207,74 @@ class _CastWeightsCL(torch.autograd.Function):
 _MAPS = {}
 
 
-def _cast_maps(shapes, device):
-    key = (tuple(shapes), str(device))
+def _kslot(c):
+    return (c + 63) // 64 * 64
+
+
+def _native_geom(conv):
+    """Static geometry of a conv the native 3x3 path can run (the input-dependent checks come
+    at call time, ``_conv_native_ok``): stride-1 'same' 3x3 with 32-multiple channel counts."""
+    return (conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.in_channels % 32 == 0
+            and conv.out_channels % 32 == 0 and conv.out_channels <= 1024
+            and conv.in_channels <= 1024)
+
+
+def _cast_maps(shapes, device, native=()):
+    key = (tuple(shapes), str(device), tuple(native))
     if key not in _MAPS:
-        perm, off = [], 0
+        perm, off, offs = [], 0, []
         for (co, ci, kh, kw) in shapes:
             n = co * ci * kh * kw
             # packed (co, kh, kw, ci) position -> flat NCHW (co, ci, kh, kw) element
             perm.append(torch.arange(n).view(co, ci, kh, kw).permute(0, 2, 3, 1).reshape(-1) + off)
+            offs.append(off)
             off += n
+        n_fwd = off
+        zero = n_fwd  # index of the appended zero element
+        extra = []    # ('adj' | 'fwd', rows, cols) per extra output, in output order
+        for j in native:
+            co, ci, kh, kw = shapes[j]
+            idx = torch.arange(co * ci * kh * kw).view(co, ci, kh, kw) + offs[j]
+            # adjoint W'[c][tap'][o] = W[o][c][flip(tap')]: packed (ci, kh, kw, co'), o >= co zero
+            adj = idx.flip(2, 3).permute(1, 2, 3, 0)
+            cop = _kslot(co)
+            if cop > co:
+                adj = torch.cat([adj, torch.full((ci, kh, kw, cop - co), zero)], 3)
+            perm.append(adj.reshape(-1))
+            extra.append(('adj', ci, kh * kw * cop))
+        for j in native:
+            co, ci, kh, kw = shapes[j]
+            cip = _kslot(ci)
+            if cip == ci:
+                continue  # the channels_last weight IS the packed forward operand
+            idx = torch.arange(co * ci * kh * kw).view(co, ci, kh, kw).permute(0, 2, 3, 1) + offs[j]
+            fwd = torch.cat([idx, torch.full((co, kh, kw, cip - ci), zero)], 3)
+            perm.append(fwd.reshape(-1))
+            extra.append(('fwd', co, kh * kw * cip))
         perm = torch.cat(perm)
-        inv = torch.empty_like(perm)
-        inv[perm] = torch.arange(perm.numel())
-        _MAPS[key] = (perm.to(device), inv.to(device), list(shapes))
+        inv = torch.empty(n_fwd, dtype=torch.long)
+        inv[perm[:n_fwd]] = torch.arange(n_fwd)
+        _MAPS[key] = (perm.to(device), inv.to(device), list(shapes), tuple(extra))
     return _MAPS[key]
 
 
 def cast_conv_weights(convs):
-    """{conv: bf16 channels_last weight} for a list of nn.Conv2d, one batched cast node."""
+    """({conv: bf16 channels_last weight}, {conv: packed bf16 adjoint weight}, {conv: packed
+    bf16 forward weight with 64-aligned K slots, when Cin % 64 != 0}) for a list of nn.Conv2d,
+    one batched cast node."""
     ws = [c.weight for c in convs]
-    maps = _cast_maps([tuple(w.shape) for w in ws], ws[0].device)
-    return dict(zip(convs, _CastWeightsCL.apply(maps, *ws)))
+    native = tuple(j for j, c in enumerate(convs) if _native_geom(c))
+    maps = _cast_maps([tuple(w.shape) for w in ws], ws[0].device, native)
+    outs = _CastWeightsCL.apply(maps, *ws)
+    ext = outs[len(convs):]
+    adj = {convs[j]: ext[k] for k, j in enumerate(native)}
+    fwd, k = {}, len(native)
+    for j in native:
+        if _kslot(convs[j].in_channels) != convs[j].in_channels:
+            fwd[convs[j]] = ext[k]
+            k += 1
+    return dict(zip(convs, outs[:len(convs)])), adj, fwd
 
 
 class _Head1x1(torch.autograd.Function):
@@ -306,23 +365,28 @@ _ENC64 = os.environ.get('RAFT_ENC64', '1') != '0'
 
 
 def _conv3x3_nhwc(xn, wpk, ci, co):
-    """NHWC bf16 stride-1 3x3 conv with a packed [co][tap * ci + c] weight: 64 -> 64 channels on
-    the persistent 2-D halo-tile kernel (conv_enc64.hip), anything else on the implicit GEMM."""
+    """NHWC bf16 stride-1 3x3 conv with a packed [co][tap * ci' + c] weight (ci' = ci rounded up
+    to 64; the K slot past ci reads zeros): 64 -> 64 channels on the persistent 2-D halo-tile
+    kernel (conv_enc64.hip), anything else on the implicit GEMM."""
     from . import conv as C
     B, H, W, _ = xn.shape
     out = torch.empty(B, H, W, co, device=xn.device, dtype=torch.bfloat16)
     if _ENC64 and ci == 64 and co == 64:
         _ext.ops().conv_enc64_(xn, wpk, out)
     else:
-        C.conv_fwd([(xn, 0, ci)], wpk, None, (3, 3), (1, 1), co, C.EPI_BF16, [out], [0])
+        C.conv_fwd([(xn, 0, _kslot(ci))], wpk, None, (3, 3), (1, 1), co, C.EPI_BF16, [out], [0],
+                   bn=32)
     return out
 
 
-def _conv3x3_native_fwd(x, w):
+def _conv3x3_native_fwd(x, w, wf=None):
     ci, co = x.shape[1], w.shape[0]
     xn = x.permute(0, 2, 3, 1)                     # channels_last memory: a view
-    wpk = w.permute(0, 2, 3, 1).reshape(co, 9 * ci)
-    return _conv3x3_nhwc(xn, wpk, ci, co).permute(0, 3, 1, 2)
+    if wf is None:
+        wf = w.permute(0, 2, 3, 1).reshape(co, 9 * ci)
+        if _kslot(ci) != ci:
+            wf = torch.nn.functional.pad(wf.view(co, 9, ci), (0, _kslot(ci) - ci)).reshape(co, -1)
+    return _conv3x3_nhwc(xn, wf, ci, co).permute(0, 3, 1, 2)
 
 
 class _Conv3x3Native(torch.autograd.Function):
@@ -337,44 +401,46 @@ class _Conv3x3Native(torch.autograd.Function):
     [co][tap * ci + c]: the forward packs nothing."""
 
     @staticmethod
-    def forward(ctx, x, w):
-        ctx.save_for_backward(x, w)
-        return _conv3x3_native_fwd(x, w)
+    def forward(ctx, x, w, wd=None, wf=None):
+        ctx.save_for_backward(x, w, wd)
+        return _conv3x3_native_fwd(x, w, wf)
 
     @staticmethod
     def backward(ctx, dy):
         from . import conv as C
-        x, w = ctx.saved_tensors
+        x, w, wd = ctx.saved_tensors
         co, ci = w.shape[:2]
         dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         gn = dy.permute(0, 2, 3, 1)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             B, _, H, W = x.shape
-            # adjoint weight W'[c][tap'][o] = W[o][c][flip(tap')], in the kernels' packed layout
-            wd = w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
-            wd = wd.permute(0, 2, 3, 1).reshape(ci, 9 * co)
+            if wd is None:
+                # adjoint weight W'[c][tap'][o] = W[o][c][flip(tap')], in the kernels' packed
+                # layout (normally laid out by the batched weight cast, _CastWeightsCL)
+                wd = C.pack_weight(w.flip(2, 3).transpose(0, 1), [co], [_kslot(co)], npad_mult=1)
             if _ENC64 and ci == 64 and co == 64:
                 dx = _conv3x3_nhwc(gn, wd, co, ci).permute(0, 3, 1, 2)
             else:
                 dxn = torch.empty(B, H, W, ci, device=x.device, dtype=torch.bfloat16)
-                _ext.ops().conv_dgrad_([gn], [0], [co], wd, 3, 3, 1, 1, 0, 1.0, [dxn], [0], [ci],
-                                       [ci], [0], [dxn], [-1], [], [])
+                _ext.ops().conv_dgrad_([gn], [0], [_kslot(co)], wd, 3, 3, 1, 1, 0, 1.0, [dxn], [0],
+                                       [ci], [ci], [0], [dxn], [-1], [], [])
                 dx = dxn.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             dwp = torch.empty(co, 9 * ci, device=x.device, dtype=torch.bfloat16)
             C.conv_wgrad_taps([(gn, [x.permute(0, 2, 3, 1)])], 0, [0], [ci], (3, 3), (1, 1), co,
                               dwp, None)
             dw = dwp.view(co, 3, 3, ci).permute(0, 3, 1, 2)
-        return dx, dw
+        return dx, dw, None, None
 
 
 _CONV_NATIVE = os.environ.get('RAFT_ENCODER_CONV_NATIVE', '1') != '0'
 
 
 def _conv_native_ok(x, conv):
-    return (_CONV_NATIVE and _wgrad_native_ok(x, conv) and conv.in_channels % 64 == 0
-            and conv.out_channels % 64 == 0 and conv.out_channels <= 1024)
+    # 32-multiple channel counts: a 96-channel operand runs in a 128-channel K slot (the kernels
+    # read the missing channels as zeros; the packed weights are zero there)
+    return (_CONV_NATIVE and _wgrad_native_ok(x, conv) and _native_geom(conv))
 
 
 def _wgrad_native_ok(x, conv):
@@ -392,8 +458,8 @@ def _conv(ps, x, conv, with_bias=False):
         w = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     if not with_bias and _conv_native_ok(x, conv) and w.is_contiguous(memory_format=torch.channels_last):
         if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
-            return _Conv3x3Native.apply(x, w)
-        return _conv3x3_native_fwd(x, w)
+            return _Conv3x3Native.apply(x, w, ps.adjoint.get(conv), ps.fwdpack.get(conv))
+        return _conv3x3_native_fwd(x, w, ps.fwdpack.get(conv))
     if not with_bias and _wgrad_native_ok(x, conv) and torch.is_grad_enabled() and \
             (x.requires_grad or w.requires_grad):
         return _Conv3x3WgradNative.apply(x, w)
@@ -480,8 +546,10 @@ class _Pass:
     stashes.  Passed down explicitly (no module globals), so encoder forwards running
     concurrently on two streams or threads, or re-entrantly, cannot see each other's state."""
 
-    def __init__(self, weights):
+    def __init__(self, weights, adjoint, fwdpack):
         self.weights = weights   # conv -> bf16 channels_last weight
+        self.adjoint = adjoint   # conv -> packed bf16 adjoint weight (native 3x3 convs)
+        self.fwdpack = fwdpack   # conv -> packed forward weight, 64-aligned K slots (Cin 96)
         self.holders = {}        # id(block output) -> (output, its gradient stash)
 
 
@@ -491,7 +559,13 @@ def encoder_forward(enc, x):
         convs = [m for m in enc.modules() if isinstance(m, nn.Conv2d)]
         if _head_ok(x, enc.conv2):
             convs = [c for c in convs if c is not enc.conv2]  # runs on _Head1x1 (fp32 weight)
-        return _encoder_body(_Pass(cast_conv_weights(convs)), enc, x)
+        counters = [m.num_batches_tracked for m in enc.modules()
+                    if isinstance(m, nn.BatchNorm2d) and _norm_mode(m) == MODE_BATCH_TRAIN
+                    and m.track_running_stats and m.num_batches_tracked is not None]
+        if counters:
+            with torch.no_grad():
+                torch._foreach_add_(counters, 1)
+        return _encoder_body(_Pass(*cast_conv_weights(convs)), enc, x)
 
 
 def _encoder_body(ps, enc, x):

@@ -127,13 +127,13 @@ def _broadcast_coalesced(tensors, src):
 
 
 def conv_tuning_table():
-    """This process's autotuned conv configs: (n, 12) int64 rows (key, config, tile); empty
+    """This process's autotuned conv configs: (n, 13) int64 rows (key, config, tile); empty
     without the native library."""
     try:
         rows = torch.ops.raft_amd.conv_tune_table()
     except (AttributeError, RuntimeError):
-        return torch.zeros(0, 12, dtype=torch.int64)
-    return torch.tensor(rows, dtype=torch.int64).view(-1, 12)
+        return torch.zeros(0, 13, dtype=torch.int64)
+    return torch.tensor(rows, dtype=torch.int64).view(-1, 13)
 
 
 def share_conv_tuning(device, src=0):
@@ -143,10 +143,10 @@ def share_conv_tuning(device, src=0):
     if not is_dist():
         return 0
     dev = device if dist.get_backend() == 'nccl' else torch.device('cpu')
-    table = conv_tuning_table() if rank() == src else torch.zeros(0, 12, dtype=torch.int64)
+    table = conv_tuning_table() if rank() == src else torch.zeros(0, 13, dtype=torch.int64)
     n = torch.tensor([table.shape[0]], dtype=torch.int64, device=dev)
     dist.broadcast(n, src)
-    buf = table.to(dev) if rank() == src else torch.zeros(int(n.item()), 12, dtype=torch.int64,
+    buf = table.to(dev) if rank() == src else torch.zeros(int(n.item()), 13, dtype=torch.int64,
                                                           device=dev)
     if int(n.item()) > 0:
         dist.broadcast(buf, src)

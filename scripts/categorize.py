@@ -2,8 +2,8 @@
 import re
 import sys
 
-CATS = [('ours conv fwd', r'conv_fwd_kernel<[^>]*, [0-57], (true|false)>|conv_fwd_(glds|halo|v3)_kernel<\d+, \d+, \d+, [0-57], \d+>|fh2_fwd'),
-        ('ours dgrad', r'conv_fwd_kernel<[^>]*, [68], |conv_fwd_(glds|halo|v3)_kernel<\d+, \d+, \d+, [68], \d+>|fh2_dgrad'),
+CATS = [('ours conv fwd', r'conv_fwd_kernel<[^>]*, [0-57], (true|false)>|conv_fwd_(glds|halo)_kernel<\d+, \d+, \d+, [0-57], \d+>|fh2_fwd'),
+        ('ours dgrad', r'conv_fwd_kernel<[^>]*, [68], |conv_fwd_(glds|halo)_kernel<\d+, \d+, \d+, [68], \d+>|fh2_dgrad'),
         ('ours conv fwd', r'conv_enc64'),
         ('ours wgrad', r'fh2_wgrad'),
         ('ours wgrad', r'conv_wgrad'),
@@ -15,13 +15,23 @@ CATS = [('ours conv fwd', r'conv_fwd_kernel<[^>]*, [0-57], (true|false)>|conv_fw
         ('corr', r'corr_'), ('upsample', r'convex'), ('update ew', r'relu_bwd|gru_|flow_prep'),
         ('copy', r'copyBuffer'), ('loss', r'seq_loss'), ('adam', r'adam|Adam|multi_tensor')]
 tot = {}
+phase_tot = {}
 for line in open(sys.argv[1]):
     if not re.match(r'\s*[\d.]+%', line):
         continue
     parts = line.split(None, 4)
     ms, name = float(parts[3]), parts[4]
+    # prof_diff.py --phases prefixes '[decode] ' / '[encoder] ': our conv kernels serve both the
+    # update block (decode) and the encoders, so their categories are split by phase
+    m = re.match(r'\[(decode|encoder)\] (.*)', name)
+    phase = None
+    if m:
+        phase, name = m.group(1), m.group(2)
+        phase_tot[phase] = phase_tot.get(phase, 0) + ms
     for c, pat in CATS:
         if re.search(pat, name):
+            if phase and c.startswith('ours'):
+                c = c.replace('ours', 'update-block' if phase == 'decode' else 'encoder')
             tot[c] = tot.get(c, 0) + ms
             break
     else:
@@ -29,3 +39,5 @@ for line in open(sys.argv[1]):
 for c, v in sorted(tot.items(), key=lambda x: -x[1]):
     print('%-15s %7.2f' % (c, v))
 print('%-15s %7.2f' % ('total', sum(tot.values())))
+for p, v in sorted(phase_tot.items()):
+    print('%-15s %7.2f' % ('phase ' + p, v))

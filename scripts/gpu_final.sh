@@ -4,6 +4,12 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 TAG=${1:-final}
+mkdir -p gpurun_out
+# liveness for long steps (MIOpen searches, multi-process tests): the per-step timeouts below
+# bound real hangs
+(while sleep 50; do date +%T >> gpurun_out/heartbeat.txt; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 mkdir -p gpurun_out/miopen_db
 [ -d miopen_db ] && cp -r miopen_db/. gpurun_out/miopen_db/
 export MIOPEN_USER_DB_PATH=$PWD/gpurun_out/miopen_db

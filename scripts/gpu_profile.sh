@@ -9,9 +9,9 @@ export TMPDIR=/tmp
 TAG=${1:-prof}; shift
 mkdir -p gpurun_out
 K=4
-timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d /tmp/prof_${TAG} -o run -- python bench.py --steps $K --warmup 3 --trace_markers "$@" > gpurun_out/${TAG}_prof_bench.log 2>&1
+RAFT_PHASE_MARKS=1 timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d /tmp/prof_${TAG} -o run -- python bench.py --steps $K --warmup 3 --trace_markers "$@" > gpurun_out/${TAG}_prof_bench.log 2>&1
 rc=$?
 echo "rocprof rc=$rc"
-python scripts/prof_diff.py --markers /tmp/prof_${TAG} $K > gpurun_out/${TAG}_summary.txt 2>&1
+python scripts/prof_diff.py --phases /tmp/prof_${TAG} $K > gpurun_out/${TAG}_summary.txt 2>&1
 head -40 gpurun_out/${TAG}_summary.txt | cut -c1-180
 exit $rc

@@ -4,6 +4,11 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+# liveness for long steps (MIOpen searches, multi-process tests): the per-step timeouts below
+# bound real hangs
+(while sleep 50; do date +%T >> gpurun_out/heartbeat.txt; done) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 TAG=${1:-quick}
 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_model_gpu.py -x -q --timeout 200 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?; tail -2 gpurun_out/${TAG}_pytest.log; if [ $rc -ne 0 ]; then grep -E "^E |FAILED" gpurun_out/${TAG}_pytest.log | head -20; exit $rc; fi

@@ -3,6 +3,7 @@
 usage: prof_diff.py <dir_warm_only> <dir_warm_plus_steps> <steps>
        prof_diff.py --single <dir_of_timed_region_trace> <steps>
        prof_diff.py --markers <dir_of_full_trace> <steps>   (bench.py --trace_markers)
+       prof_diff.py --phases <dir_of_full_trace> <steps>    (+ RAFT_PHASE_MARKS=1: [decode] / [encoder])
 """
 import csv, glob, os, sys
 
@@ -31,7 +32,32 @@ def load_between_markers(d):
     return out
 
 
-if sys.argv[1] == '--markers':
+def load_phases(d):
+    """As load_between_markers, with every kernel name prefixed by its phase: the decode replay
+    (correlation, update block, upsampling, loss; forward + backward) is bracketed by
+    raft_phase_marker_kernel launches (RAFT_PHASE_MARKS=1) -> '[decode] '; everything else
+    (encoders forward / backward, clip, optimizer) -> '[encoder] '."""
+    f = glob.glob(os.path.join(d, '**', '*kernel_trace.csv'), recursive=True)
+    rows = sorted(csv.DictReader(open(f[0])), key=lambda r: int(r['Start_Timestamp']))
+    marks = [i for i, r in enumerate(rows) if 'spin' in r['Kernel_Name'].lower() or 'sleep' in r['Kernel_Name'].lower()]
+    assert len(marks) >= 2, 'no marker kernels in the trace'
+    i0, i1 = marks[-2], marks[-1]
+    out = {}
+    decode = False
+    for r in rows[i0 + 1:i1]:
+        name = r['Kernel_Name']
+        if 'raft_phase_marker' in name:
+            decode = not decode
+            continue
+        key = '[%s] %s' % ('decode' if decode else 'encoder', name)
+        t, c = out.get(key, (0.0, 0))
+        out[key] = (t + int(r['End_Timestamp']) - int(r['Start_Timestamp']), c + 1)
+    return out
+
+
+if sys.argv[1] == '--phases':
+    a, b, steps = {}, load_phases(sys.argv[2]), int(sys.argv[3])
+elif sys.argv[1] == '--markers':
     a, b, steps = {}, load_between_markers(sys.argv[2]), int(sys.argv[3])
 elif sys.argv[1] == '--single':   # one trace restricted to the timed region (roctx selected regions)
     a, b, steps = {}, load(sys.argv[2]), int(sys.argv[3])

@@ -24,6 +24,10 @@ def _port():
 
 def _run(mode, precision, backend):
     env = dict(os.environ, MASTER_ADDR='127.0.0.1')
+    if precision == 'fp32':
+        # immediate-mode MIOpen solvers: no per-shape fp32 benchmark search (minutes on a fresh
+        # box, and several batch shapes run here); the check compares gradients, not speed
+        env.setdefault('MIOPEN_FIND_MODE', 'FAST')
     if backend == 'gloo':
         env['RAFT_DIST_BACKEND'] = 'gloo'
     else:
@@ -32,14 +36,15 @@ def _run(mode, precision, backend):
            '--master-addr', '127.0.0.1', '--master-port', str(_port()),
            os.path.join(ROOT, 'scripts', 'dp_rehearsal.py')] + \
         (['--graph'] if mode == 'graph' else []) + (['--fp32'] if precision == 'fp32' else [])
-    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
 
 
 @pytest.mark.parametrize('precision', ['bf16', 'fp32'])
 @pytest.mark.parametrize('mode', ['eager', 'graph'])
 def test_dp_rehearsal(ext_ops, mode, precision):
-    """fp32 pins the all-reduce math (DP gradient == full-batch gradient to 1e-4); the graphed
-    mode also checks that rank 0's kernel choices are the ones every rank runs."""
+    """fp32 pins the all-reduce math (DP gradient == mean of the ranks' same-shape single-process
+    gradients to 1e-5, full-batch gradient to 1e-3); the graphed mode also checks that rank 0's
+    kernel choices are the ones every rank runs."""
     r = _run(mode, precision, 'gloo')
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]

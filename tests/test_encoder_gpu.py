@@ -123,8 +123,10 @@ def test_native_wgrad_3x3_matches_conv2d(ext_ops, cin, cout):
 
 
 @pytest.mark.parametrize('cin,cout,hw', [(64, 64, (37, 45)), (64, 64, (8, 16)), (64, 64, (19, 70)),
-                                         (128, 128, (37, 45)), (64, 128, (37, 45))])
-def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout, hw):
+                                         (128, 128, (37, 45)), (64, 128, (37, 45)),
+                                         (96, 96, (23, 31)), (64, 96, (11, 19)), (96, 128, (9, 14))])
+@pytest.mark.parametrize('packed', [False, True])
+def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout, hw, packed):
     """Stride-1 3x3 encoder conv entirely on the MFMA kernels (forward implicit GEMM -- or, 64 -> 64,
     the persistent 2-D halo-tile kernel --, input gradient on the flipped weight, tap-fused weight
     gradient) vs the fp32 autograd of F.conv2d at the same bf16 inputs, across image and batch
@@ -137,7 +139,16 @@ def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout, hw):
     w = w.contiguous(memory_format=torch.channels_last).requires_grad_(True)
     dy = torch.randn(3, cout, h, wd, device=DEV).to(torch.bfloat16)
     dy = dy.contiguous(memory_format=torch.channels_last)
-    y = fast._Conv3x3Native.apply(x, w)
+    wd = wf = None
+    if packed:
+        # the batched cast's adjoint / padded forward packs (96-channel K slots read zeros)
+        conv = torch.nn.Conv2d(cin, cout, 3, padding=1).to(DEV)
+        with torch.no_grad():
+            conv.weight.copy_(w.float())
+        _, adj, fwd = fast.cast_conv_weights([conv])
+        wd, wf = adj[conv], fwd.get(conv)
+        assert (wf is not None) == (cin % 64 != 0)
+    y = fast._Conv3x3Native.apply(x, w, wd, wf)
     assert y.is_contiguous(memory_format=torch.channels_last)
     y.backward(dy)
     xr = x.detach().float().requires_grad_(True)
@@ -151,5 +162,5 @@ def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout, hw):
                                rtol=2e-2)
     # no-grad path (inference) gives the same forward
     with torch.no_grad():
-        y2 = fast._conv3x3_native_fwd(x.detach(), w.detach())
+        y2 = fast._conv3x3_native_fwd(x.detach(), w.detach(), wf)
     assert torch.equal(y2, y.detach())

@@ -79,6 +79,29 @@ def test_corr_build_bf16_pyramid_and_lookup(ext_ops, shape):
     assert _rel(o16.float(), o32.float()) < 1e-2
 
 
+@pytest.mark.parametrize('shape,radius,spread', [((2, 256, 46, 62), 4, 6.0), ((1, 128, 13, 19), 3, 6.0),
+                                                  ((2, 64, 23, 30), 4, 40.0), ((3, 32, 11, 17), 4, 2.0)])
+def test_lookup_rows_bf16_vs_oracle(ext_ops, shape, radius, spread):
+    """Row-vector NHWC lookup on the bf16 pyramid (aligned 16-B row pieces, plane-edge masking)
+    vs the grid_sample oracle on the same bf16 values: equal up to the bf16 rounding of the
+    output; the zero-padded channels stay exactly zero."""
+    b, c, h, w = shape
+    f1 = torch.randn(b, h, w, c, device=DEV).to(torch.bfloat16)
+    f2 = torch.randn(b, h, w, c, device=DEV).to(torch.bfloat16)
+    levels = 4 if min(h, w) >= 8 else 3
+    pyr = ext_ops.corr_build_bf16(f1, f2, levels, True)
+    coords = _coords(b, h, w, spread=spread, seed=3)
+    out = torch.full((b, h, w, 384), 7.0, device=DEV, dtype=torch.bfloat16)
+    ext_ops.corr_lookup_nhwc_(pyr, coords, radius, out)
+    ref = torch_corr_lookup([p.float().reshape(b * h * w, 1, *p.shape[-2:]) for p in pyr],
+                            coords, radius)
+    ctot = levels * (2 * radius + 1) ** 2
+    got = out[..., :ctot].permute(0, 3, 1, 2).float()
+    err = (got - ref).abs()
+    assert (err <= ref.abs() * 2.0 ** -8 + 1e-6).all(), err.max().item()
+    assert (out[..., ctot:] == 0).all()
+
+
 def test_corrblock_bf16_fmaps_fwd_bwd(ext_ops):
     """Mixed-precision CorrBlock: bf16 channels_last fmaps in (as the encoders produce them),
     fp32 lookups out, bf16 fmap gradients back (bf16 dcorr: ~1e-2 relative)."""
@@ -351,6 +374,8 @@ def test_tap_reduce_matches_window_path(ext_ops, radius, levels, hw):
     torch.testing.assert_close(got, ref, atol=1e-5, rtol=1e-5)
     got16 = ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, True)
     torch.testing.assert_close(got16.float(), ref, atol=1e-2, rtol=1e-2)
+    # fixed fold order: bitwise reproducible
+    assert torch.equal(ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, False), got)
 
 
 @pytest.mark.parametrize('convention', ['reference', 'exact'])

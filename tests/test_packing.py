@@ -78,12 +78,24 @@ def test_unpack_grads_matches_per_layer_unpack():
 
 
 def test_batched_encoder_weight_cast():
-    convs = [nn.Conv2d(3, 8, 7), nn.Conv2d(8, 16, 1), nn.Conv2d(16, 4, 3)]
-    m = cast_conv_weights(convs)
+    convs = [nn.Conv2d(3, 8, 7), nn.Conv2d(8, 16, 1), nn.Conv2d(16, 4, 3),
+             nn.Conv2d(64, 128, 3, padding=1), nn.Conv2d(96, 96, 3, padding=1)]
+    m, adj, fwd = cast_conv_weights(convs)
     for c in convs:
         w = m[c]
         assert w.is_contiguous(memory_format=torch.channels_last)
         assert torch.equal(w.float(), c.weight.to(torch.bfloat16).float())
+    # the adjoint (input-gradient) weight of the native 3x3 convs: W'[c][tap'][o] = W[o][c][flip],
+    # K slots of 64-multiples (zeros past Cout); a padded forward pack where Cin % 64 != 0
+    assert list(adj) == [convs[3], convs[4]] and list(fwd) == [convs[4]]
+    w = convs[3].weight.to(torch.bfloat16)
+    ref = w.flip(2, 3).permute(1, 2, 3, 0).reshape(64, 9 * 128)
+    assert torch.equal(adj[convs[3]], ref) and not adj[convs[3]].requires_grad
+    w = convs[4].weight.to(torch.bfloat16)
+    ref = torch.nn.functional.pad(w.flip(2, 3).permute(1, 2, 3, 0), (0, 32)).reshape(96, 9 * 128)
+    assert torch.equal(adj[convs[4]], ref)
+    ref = torch.nn.functional.pad(w.permute(0, 2, 3, 1), (0, 32)).reshape(96, 9 * 128)
+    assert torch.equal(fwd[convs[4]], ref)
     loss = sum((m[c].float() ** 2).sum() * (i + 1) for i, c in enumerate(convs))
     loss.backward()
     for i, c in enumerate(convs):
