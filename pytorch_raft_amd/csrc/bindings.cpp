@@ -341,6 +341,37 @@ void corr_otf_fwd_(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor
               "on-the-fly corr supports radius 3/4 with C = 128/256");
 }
 
+// deterministic on-the-fly dF2 (default; RAFT_OTF_DF2_ATOMIC=1: float atomics): per-tile slab
+// rows sized for a union box of up to 32 x 32 positions at level 0 (~20 x 20 at chairs), 24 x 24
+// above; a box past that capacity falls back to atomics for its tile
+struct OtfSlabs {
+  std::vector<Tensor> keep;
+  std::vector<float*> ptr;
+  std::vector<int> cap;
+  Tensor boxes;
+  bool on = false;
+  OtfSlabs(const Bf16Levels& L, int64_t levels, int64_t B, int64_t H, int64_t W, int64_t C,
+           const at::TensorOptions& fo) {
+    static const bool atomic_df2 = [] {
+      const char* e = getenv("RAFT_OTF_DF2_ATOMIC");
+      return e && e[0] == '1';
+    }();
+    if (atomic_df2) return;
+    on = true;
+    const int tiles = otf_tiles((int)B, (int)H, (int)W);
+    for (int64_t l = 0; l < levels; ++l) {
+      const int plane = L.h[l] * L.w[l];
+      cap.push_back(std::min(plane, l == 0 ? 1024 : 576));
+      keep.push_back(at::empty({(int64_t)tiles * cap.back() * C}, fo));
+      ptr.push_back(keep.back().data_ptr<float>());
+    }
+    boxes = at::empty({(int64_t)tiles * 16}, fo.dtype(at::kInt));
+  }
+  float* const* slab() const { return on ? ptr.data() : nullptr; }
+  const int* caps() const { return on ? cap.data() : nullptr; }
+  int* box() { return on ? boxes.data_ptr<int>() : nullptr; }
+};
+
 void corr_otf_bwd_(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor& coords,
                    const Tensor& dout, const Tensor& df1, const std::vector<Tensor>& df2,
                    int64_t radius) {
@@ -364,12 +395,13 @@ void corr_otf_bwd_(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor
     TORCH_CHECK(df2[l].sizes() == f2[l].sizes(), "grad fmap2 level shape mismatch");
     gp.push_back(df2[l].data_ptr<float>());
   }
+  OtfSlabs sl(L, (int64_t)f2.size(), B, H, W, C, df1.options());
   TORCH_CHECK(launch_corr_otf_bwd(reinterpret_cast<const uint16_t*>(f1.data_ptr()), L.ptr.data(),
                                   L.h.data(), L.w.data(), (int)f2.size(),
                                   coords.data_ptr<float>(), dout.data_ptr(),
                                   dout.scalar_type() == at::kBFloat16, (int)dout.size(3),
                                   df1.data_ptr<float>(), gp.data(), (int)B, (int)C, (int)H, (int)W,
-                                  (int)radius, cur_stream()),
+                                  (int)radius, sl.slab(), sl.caps(), sl.box(), cur_stream()),
               "on-the-fly corr supports radius 3/4 with C = 128/256");
 }
 
@@ -410,10 +442,12 @@ void corr_otf_window_bwd_(const Tensor& f1, const std::vector<Tensor>& f2,
     TORCH_CHECK(df2[l].sizes() == f2[l].sizes(), "grad fmap2 level shape mismatch");
     gp.push_back(df2[l].data_ptr<float>());
   }
+  OtfSlabs sl(L, levels, B, H, W, C, df1.options());
   TORCH_CHECK(launch_corr_otf_window_bwd(reinterpret_cast<const uint16_t*>(f1.data_ptr()),
                                          L.ptr.data(), L.h.data(), L.w.data(), (int)levels, wl,
                                          df1.data_ptr<float>(), gp.data(), (int)B, (int)C, (int)H,
-                                         (int)W, (int)radius, cur_stream()),
+                                         (int)W, (int)radius, sl.slab(), sl.caps(), sl.box(),
+                                         cur_stream()),
               "on-the-fly corr supports radius 3/4 with C = 128/256");
 }
 
@@ -623,7 +657,8 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
               "packed weight must be a contiguous bf16 (Npad, Kpad) tensor");
   const int64_t kneed = cin_small ? ((kh * kw * cin_small + 63) / 64) * 64 : kh * kw * cin_pad;
   TORCH_CHECK(wpk.size(1) == kneed, "packed weight K mismatch: ", wpk.size(1), " vs ", kneed);
-  TORCH_CHECK(wpk.size(0) >= ((cout + bn - 1) / bn) * bn, "packed weight has too few rows");
+  // rows past cout are never read (range-checked descriptors in every kernel)
+  TORCH_CHECK(wpk.size(0) >= cout, "packed weight has too few rows");
   a.wpk = reinterpret_cast<const uint16_t*>(wpk.data_ptr<at::BFloat16>());
   a.kpad = (int)wpk.size(1);
   if (bias.has_value() && bias->defined() && bias->dim() == 4) {
@@ -1065,7 +1100,7 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
               "packed weight must be a contiguous bf16 (Npad, Kpad) tensor");
   const int64_t kneed = cin_small ? ((kh * kw * cin_small + 63) / 64) * 64 : kh * kw * cin_pad;
   TORCH_CHECK(wpk.size(1) == kneed, "packed dgrad weight K mismatch: ", wpk.size(1), " vs ", kneed);
-  TORCH_CHECK(wpk.size(0) >= ((cout + bn - 1) / bn) * bn, "packed dgrad weight has too few rows");
+  TORCH_CHECK(wpk.size(0) >= cout, "packed dgrad weight has too few rows");
   a.wpk = reinterpret_cast<const uint16_t*>(wpk.data_ptr<at::BFloat16>());
   a.kpad = (int)wpk.size(1);
   a.bias = nullptr;

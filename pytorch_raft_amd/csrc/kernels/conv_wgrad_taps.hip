@@ -23,6 +23,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 namespace {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -68,14 +70,21 @@ struct TapGeo {
   static constexpr int STAGE = G_BYTES + X_BYTES;
 };
 
-template <int KH, int KW, int TG, int BMT>
+// NS: LDS pipeline stages.  The 128-Cout 3x3 kernel runs one workgroup per CU (its accumulators
+// fill the register file), so a chunk's DMA has to land behind the MFMAs of NS - 1 earlier chunks:
+// with two stages the ~1300-cycle chunk of MFMAs did not cover the global -> LDS latency (39% MFMA
+// busy, profiles/r2/pmc_step_final.txt).  The other kernels keep two stages and two or three
+// resident workgroups per CU instead.
+template <int KH, int KW, int TG, int BMT, int NS>
 __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_taps_kernel(
     ConvWgradArgs a, WgradItems it, WgradTapArgs ta) {
   using Geo = TapGeo<KH, KW, TG, BMT>;
   constexpr int NT = Geo::NT, GRB = Geo::GRB, G_CPR = Geo::G_CPR, WMW = Geo::WMW;
   constexpr int T = Geo::T, TPG = Geo::TPG, HWD = Geo::HWD, HALO = Geo::HALO;
   constexpr int G_PER = Geo::G_PER, X_PER = Geo::X_PER, LPS = G_PER + X_PER;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * Geo::STAGE];
+  static_assert(NS >= 2 && NS <= 4, "2..4 pipeline stages");
+  static_assert(NS * Geo::STAGE <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NS * Geo::STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int HW = a.H * a.W;
@@ -212,18 +221,42 @@ __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_t
     }
   };
 
-  if (nsteps > 0) {
-    issue(c_begin, 0);
-    for (int t = 0; t < nsteps; ++t) {
-      if (t + 1 < nsteps) {
-        issue(c_begin + t + 1, (t + 1) & 1);
-        raft_wait_vmcnt<LPS>();
-      } else {
-        raft_wait_vmcnt<0>();
+  if constexpr (NS == 2) {
+    if (nsteps > 0) {
+      issue(c_begin, 0);
+      for (int t = 0; t < nsteps; ++t) {
+        if (t + 1 < nsteps) {
+          issue(c_begin + t + 1, (t + 1) & 1);
+          raft_wait_vmcnt<LPS>();
+        } else {
+          raft_wait_vmcnt<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+        compute(t & 1);
+        __builtin_amdgcn_s_barrier();
       }
+    }
+  } else {
+    // NS-stage ring, ONE barrier per chunk: wait (counted vmcnt) for this wave's chunk-t DMAs with
+    // the newer stages still in flight -> barrier (every wave's chunk-t data landed AND every wave
+    // finished computing chunk t-1) -> issue chunk t+NS-1 into the buffer chunk t-1 used -> MFMAs
+#pragma unroll
+    for (int q = 0; q < NS - 1; ++q)
+      if (q < nsteps) issue(c_begin + q, q);
+    int cur = 0;
+    for (int t = 0; t < nsteps; ++t) {
+      const int newer = min(NS - 2, nsteps - 1 - t);
+      if (NS >= 4 && newer >= 2) raft_wait_vmcnt<(NS >= 4 ? 2 : 0) * LPS>();
+      else if (newer >= 1) raft_wait_vmcnt<LPS>();
+      else raft_wait_vmcnt<0>();
       __builtin_amdgcn_s_barrier();
-      compute(t & 1);
-      __builtin_amdgcn_s_barrier();
+      if (t + NS - 1 < nsteps) {
+        int nb = cur + NS - 1;
+        nb = nb >= NS ? nb - NS : nb;
+        issue(c_begin + t + NS - 1, nb);
+      }
+      compute(cur);
+      cur = cur + 1 == NS ? 0 : cur + 1;
     }
   }
 
@@ -321,26 +354,42 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __r
   }
 }
 
-template <int KH, int KW, int TG, int BMT>
+template <int KH, int KW, int TG, int BMT, int NS>
 void launch_taps(const ConvWgradArgs& a, const WgradItems& it, const WgradTapArgs& ta,
                  hipStream_t stream) {
   dim3 grid((ta.n_co * ta.n_ci * ta.splits + 7) / 8 * 8);
-  hipLaunchKernelGGL((conv_wgrad_taps_kernel<KH, KW, TG, BMT>), grid,
+  hipLaunchKernelGGL((conv_wgrad_taps_kernel<KH, KW, TG, BMT, NS>), grid,
                      dim3(TapGeo<KH, KW, TG, BMT>::NT), 0, stream, a, it, ta);
+}
+
+int taps_stages_3x3() {
+  static const int ns = [] {
+    const char* e = getenv("RAFT_WGRAD_STAGES");  // A/B: 2 = the round-3 pipeline
+    const int v = e ? atoi(e) : 4;
+    return v == 2 || v == 3 ? v : 4;
+  }();
+  return ns;
 }
 
 }  // namespace
 
 bool launch_conv_wgrad_taps(const ConvWgradArgs& a, const WgradItems& it, const WgradTapArgs& ta,
                             float* db, hipStream_t stream) {
+  const int ns = taps_stages_3x3();
   if (ta.bm == 64) {
-    if (a.KH == 3 && a.KW == 3) launch_taps<3, 3, 3, 64>(a, it, ta, stream);
+    // two resident workgroups per CU (6 waves, 60 KB each) cover each other's DMA latency
+    if (a.KH == 3 && a.KW == 3) launch_taps<3, 3, 3, 64, 2>(a, it, ta, stream);
     else return false;
-  } else if (a.KH == 1 && a.KW == 1) launch_taps<1, 1, 1, 128>(a, it, ta, stream);
-  else if (a.KH == 1 && a.KW == 5) launch_taps<1, 5, 1, 128>(a, it, ta, stream);
-  else if (a.KH == 5 && a.KW == 1) launch_taps<5, 1, 1, 128>(a, it, ta, stream);
-  else if (a.KH == 3 && a.KW == 3) launch_taps<3, 3, 2, 128>(a, it, ta, stream);
-  else return false;
+  } else if (a.KH == 1 && a.KW == 1) launch_taps<1, 1, 1, 128, 2>(a, it, ta, stream);
+  else if (a.KH == 1 && a.KW == 5) launch_taps<1, 5, 1, 128, 2>(a, it, ta, stream);
+  else if (a.KH == 5 && a.KW == 1) launch_taps<5, 1, 1, 128, 2>(a, it, ta, stream);
+  else if (a.KH == 3 && a.KW == 3) {
+    if (ns == 4) launch_taps<3, 3, 2, 128, 4>(a, it, ta, stream);
+    else if (ns == 3) launch_taps<3, 3, 2, 128, 3>(a, it, ta, stream);
+    else launch_taps<3, 3, 2, 128, 2>(a, it, ta, stream);
+  } else {
+    return false;
+  }
   const int64_t n = (int64_t)a.cout * a.kpad;
   const bool bias = ta.db_part != nullptr && db != nullptr;
   const unsigned blocks = (unsigned)((n / 4 + 15) / 16 + (bias ? (a.cout + 15) / 16 : 0));

@@ -42,6 +42,13 @@ struct OtfLvls {
   float* g2[4];
   int h[4];
   int w[4];
+  // deterministic dF2 (backward): a tile's box gradient goes to its private slab rows
+  // slab[l][tile][cap[l]][C] and its box to boxes[tile][l] (bw = 0: not slabbed -- an empty box,
+  // or one past the capacity, whose rows went out as float atomics instead); the reduce kernel
+  // then sums the overlapping tiles' rows per fmap2 position in tile order
+  float* slab[4];
+  int cap[4];
+  int* boxes;
 };
 
 __device__ __forceinline__ float clampc(float v) { return fminf(fmaxf(v, -1.0e6f), 1.0e6f); }
@@ -519,6 +526,15 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
     const int nchunk = (U + NCH - 1) / NCH;
     const uint16_t* F2 = lv.f2[l] + (int64_t)b * hl * wl_ * C;
     float* G2 = lv.g2[l] + (int64_t)b * hl * wl_ * C;
+    const bool slabbed = lv.slab[l] != nullptr && U > 0 && U <= lv.cap[l];
+    float* S2 = slabbed ? lv.slab[l] + (int64_t)blockIdx.x * lv.cap[l] * C : nullptr;
+    if (lv.boxes != nullptr && tid == 0) {
+      int* bx = lv.boxes + ((int64_t)blockIdx.x * 4 + l) * 4;
+      bx[0] = bx0;
+      bx[1] = by0;
+      bx[2] = slabbed ? bw : 0;
+      bx[3] = slabbed ? bh : 0;
+    }
     if (nchunk > 0) ld.load(F2, wl_, bx0, by0, bw, U, 0, tid);
     for (int c = 0; c < nchunk; ++c) {
       ld.store(Bs, RS, tid);
@@ -602,10 +618,16 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
         for (int r = 0; r < 16; ++r) {
           const int pos = c * NCH + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           if (pos >= U) continue;
-          const int iy = by0 + pos / bw, ix = bx0 + pos % bw;
-          float* dst = G2 + ((int64_t)iy * wl_ + ix) * C + wave * WC + (lane & 31);
+          if (slabbed) {  // plain 128-B row stores into this tile's slab rows
+            float* dst = S2 + (int64_t)pos * C + wave * WC + (lane & 31);
 #pragma unroll
-          for (int j = 0; j < TN; ++j) atomicAdd(dst + j * 32, g2[i][j][r]);
+            for (int j = 0; j < TN; ++j) dst[j * 32] = g2[i][j][r];
+          } else {
+            const int iy = by0 + pos / bw, ix = bx0 + pos % bw;
+            float* dst = G2 + ((int64_t)iy * wl_ + ix) * C + wave * WC + (lane & 31);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) atomicAdd(dst + j * 32, g2[i][j][r]);
+          }
         }
       __syncthreads();
     }
@@ -633,8 +655,62 @@ OtfLvls make_lvls(const uint16_t* const* f2, float* const* g2, const int* hs, co
     p.g2[l] = (g2 && l < levels) ? g2[l] : nullptr;
     p.h[l] = l < levels ? hs[l] : 0;
     p.w[l] = l < levels ? ws[l] : 0;
+    p.slab[l] = nullptr;
+    p.cap[l] = 0;
   }
+  p.boxes = nullptr;
   return p;
+}
+
+// dF2 of one level, deterministic: workgroup = an 8 x 8 block of fmap2 positions x 64 channels;
+// thread = 4 positions x 4 channels (float4).  The query tiles of the same image are visited in
+// tile order; a tile whose slabbed box covers a position contributes that slab row.  The sum is
+// added to the level gradient (which may already hold atomically-added unslabbed boxes).
+template <int C>
+__global__ __launch_bounds__(256) void corr_otf_df2_reduce_kernel(const float* __restrict__ slab, int cap,
+                                                                  const int* __restrict__ boxes, int l,
+                                                                  int tiles_img, int hl, int wl,
+                                                                  float* __restrict__ g2) {
+  const int ptx = (wl + 7) / 8, pty = (hl + 7) / 8;
+  int t = blockIdx.x;
+  const int bx = t % ptx;
+  t /= ptx;
+  const int by = t % pty;
+  const int b = t / pty;
+  const int c0 = blockIdx.y * 64 + (threadIdx.x & 15) * 4;
+  const int pr = threadIdx.x >> 4;
+  float4 acc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int y0 = by * 8, x0 = bx * 8;
+  for (int q = 0; q < tiles_img; ++q) {
+    const int64_t T = (int64_t)b * tiles_img + q;
+    const int4 box = *reinterpret_cast<const int4*>(boxes + (T * 4 + l) * 4);
+    const int bw = box.z, bh = box.w;
+    if (bw == 0) continue;  // uniform
+    if (box.x > x0 + 7 || box.x + bw <= x0 || box.y > y0 + 7 || box.y + bh <= y0) continue;
+    const float* S = slab + T * cap * C + c0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = pr + 16 * k;
+      const int py = y0 + (p >> 3), px = x0 + (p & 7);
+      const int ry = py - box.y, rx = px - box.x;
+      if ((unsigned)ry < (unsigned)bh && (unsigned)rx < (unsigned)bw) {
+        const float4 v = *reinterpret_cast<const float4*>(S + (int64_t)(ry * bw + rx) * C);
+        acc[k].x += v.x; acc[k].y += v.y; acc[k].z += v.z; acc[k].w += v.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int p = pr + 16 * k;
+    const int py = y0 + (p >> 3), px = x0 + (p & 7);
+    if (py >= hl || px >= wl) continue;
+    float4* dst = reinterpret_cast<float4*>(g2 + (((int64_t)b * hl + py) * wl + px) * C + c0);
+    float4 o = *dst;
+    o.x += acc[k].x; o.y += acc[k].y; o.z += acc[k].z; o.w += acc[k].w;
+    *dst = o;
+  }
 }
 
 }  // namespace
@@ -674,11 +750,24 @@ bool launch_corr_otf_fwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
 #undef FWD
 }
 
+void launch_df2_reduce(float* const* slab, const int* cap, const int* boxes, int levels,
+                       const int* hs, const int* ws, int tiles_img, int B, int C, float* const* df2lvl,
+                       hipStream_t stream);
+
 bool launch_corr_otf_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const int* hs,
                          const int* ws, int levels, const float* coords, const void* dout,
                          int dout_bf16, int dstride, float* df1, float* const* df2lvl, int B,
-                         int C, int H, int W, int radius, hipStream_t stream) {
-  const OtfLvls p = make_lvls(f2lvl, df2lvl, hs, ws, levels);
+                         int C, int H, int W, int radius, float* const* slab, const int* cap,
+                         int* boxes, hipStream_t stream) {
+  if (!((radius == 4 || radius == 3) && (C == 128 || C == 256))) return false;
+  OtfLvls p = make_lvls(f2lvl, df2lvl, hs, ws, levels);
+  if (slab != nullptr) {
+    for (int l = 0; l < levels; ++l) {
+      p.slab[l] = slab[l];
+      p.cap[l] = cap[l];
+    }
+    p.boxes = boxes;
+  }
   const int tx = (W + TPX - 1) / TPX, ty = (H + TPX - 1) / TPX;
   const dim3 grid((unsigned)(B * tx * ty));
   const float isc = 1.f / sqrtf((float)C);
@@ -689,23 +778,64 @@ bool launch_corr_otf_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
                      coords, (const TD*)dout, dstride, none, df1, B, H, W, levels, tx, ty, isc)
 #define BWD_BF16(RR, CC) BWD(RR, CC, uint16_t)
 #define BWD_F32(RR, CC) BWD(RR, CC, float)
-  if (dout_bf16) OTF_CASES(BWD_BF16);
-  OTF_CASES(BWD_F32);
+  if (dout_bf16) {
+    if (radius == 4 && C == 256) BWD_BF16(4, 256);
+    else if (radius == 3 && C == 128) BWD_BF16(3, 128);
+    else if (radius == 4 && C == 128) BWD_BF16(4, 128);
+    else BWD_BF16(3, 256);
+  } else {
+    if (radius == 4 && C == 256) BWD_F32(4, 256);
+    else if (radius == 3 && C == 128) BWD_F32(3, 128);
+    else if (radius == 4 && C == 128) BWD_F32(4, 128);
+    else BWD_F32(3, 256);
+  }
 #undef BWD
+  if (slab != nullptr) launch_df2_reduce(slab, cap, boxes, levels, hs, ws, tx * ty, B, C, df2lvl, stream);
+  return true;
 }
+
+void launch_df2_reduce(float* const* slab, const int* cap, const int* boxes, int levels,
+                       const int* hs, const int* ws, int tiles_img, int B, int C, float* const* df2lvl,
+                       hipStream_t stream) {
+  for (int l = 0; l < levels; ++l) {
+    const dim3 rg((unsigned)(B * ((hs[l] + 7) / 8) * ((ws[l] + 7) / 8)), (unsigned)(C / 64));
+    if (C == 256)
+      hipLaunchKernelGGL(corr_otf_df2_reduce_kernel<256>, rg, dim3(256), 0, stream, slab[l], cap[l],
+                         boxes, l, tiles_img, hs[l], ws[l], df2lvl[l]);
+    else
+      hipLaunchKernelGGL(corr_otf_df2_reduce_kernel<128>, rg, dim3(256), 0, stream, slab[l], cap[l],
+                         boxes, l, tiles_img, hs[l], ws[l], df2lvl[l]);
+  }
+}
+
+int otf_tiles(int B, int H, int W) { return B * ((W + TPX - 1) / TPX) * ((H + TPX - 1) / TPX); }
 
 bool launch_corr_otf_window_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const int* hs,
                                 const int* ws, int levels, const WinList& wl, float* df1,
                                 float* const* df2lvl, int B, int C, int H, int W, int radius,
+                                float* const* slab, const int* cap, int* boxes,
                                 hipStream_t stream) {
   if (wl.n < 1 || wl.n > RAFT_MAX_WIN) return false;
-  const OtfLvls p = make_lvls(f2lvl, df2lvl, hs, ws, levels);
+  if (!((radius == 4 || radius == 3) && (C == 128 || C == 256))) return false;
+  OtfLvls p = make_lvls(f2lvl, df2lvl, hs, ws, levels);
+  if (slab != nullptr) {
+    for (int l = 0; l < levels; ++l) {
+      p.slab[l] = slab[l];
+      p.cap[l] = cap[l];
+    }
+    p.boxes = boxes;
+  }
   const int tx = (W + TPX - 1) / TPX, ty = (H + TPX - 1) / TPX;
   const dim3 grid((unsigned)(B * tx * ty));
   const float isc = 1.f / sqrtf((float)C);
 #define BWDW(RR, CC)                                                                           \
   hipLaunchKernelGGL((corr_otf_bwd_kernel<RR, CC, float, true>), grid, dim3(NT), 0, stream, f1, \
                      p, nullptr, (const float*)nullptr, 0, wl, df1, B, H, W, levels, tx, ty, isc)
-  OTF_CASES(BWDW);
+  if (radius == 4 && C == 256) BWDW(4, 256);
+  else if (radius == 3 && C == 128) BWDW(3, 128);
+  else if (radius == 4 && C == 128) BWDW(4, 128);
+  else BWDW(3, 256);
 #undef BWDW
+  if (slab != nullptr) launch_df2_reduce(slab, cap, boxes, levels, hs, ws, tx * ty, B, C, df2lvl, stream);
+  return true;
 }

@@ -213,6 +213,18 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
 // taps into the bf16 pixel-row tile; phase 3 streams the tile out as 16-B pixel-row pieces.
 constexpr int TPV = 16;  // pixels per workgroup (42 KB LDS: three workgroups per CU)
 
+// one aligned 16-B piece; a piece that runs past the range end (the last rows of the range's
+// last plane) is read as four range-checked dwords: a 16-B load that is only partly in range
+// returns zeros for all of it, in-range bytes included
+__device__ __forceinline__ uint4 piece16(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t lim) {
+  if (off == 0x80000000u || off + 16u <= lim)
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  return make_uint4(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0),
+                    __builtin_amdgcn_raw_buffer_load_b32(r, off + 4u, 0, 0),
+                    __builtin_amdgcn_raw_buffer_load_b32(r, off + 8u, 0, 0),
+                    __builtin_amdgcn_raw_buffer_load_b32(r, off + 12u, 0, 0));
+}
+
 template <int R>
 __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const float* __restrict__ coords,
                                                                uint16_t* __restrict__ out, int cbuf,
@@ -240,6 +252,7 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
   // between that base and the first plane (0..7)
   __amdgpu_buffer_rsrc_t rs[4];
   int dl[4];
+  uint32_t nbytes[4];
 #pragma unroll
   for (int l = 0; l < 4; ++l) {
     const int ll = l < levels ? l : 0;
@@ -249,22 +262,28 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
     dl[l] = (int)(first - abase);
     const uint16_t* base = reinterpret_cast<const uint16_t*>(pyr.lvl[ll]) + abase;
     const uint32_t bytes = (uint32_t)((dl[l] + (int64_t)npx * plane) * 2);
+    nbytes[l] = bytes;
     rs[l] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), (short)0, (int)bytes,
                                              0x00020000);
   }
   __syncthreads();
-  // ---- phase 1: every window row's aligned 16-B pieces -> LDS (all loads before any store)
-  constexpr int ITEMS = TPV * 4 * E;
+  // ---- phase 1: every window row's aligned 16-B pieces -> LDS (all loads before any store).
+  // Items are level-major in 64-aligned per-level ranges, so every wave reads ONE level: the
+  // buffer resource stays wave-uniform (a lane-varying descriptor costs a waterfall loop)
+  constexpr int IPL = (TPV * E + 63) / 64 * 64;  // items per level (padded)
+  constexpr int ITEMS = 4 * IPL;
   constexpr int PER = (ITEMS + 255) / 256;
   uint4 v[PER][3];
+  int slot[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const int e = tid + k * 256;
-    const int px = e / (4 * E), rem = e - px * (4 * E), l = rem / E, r = rem - l * E;
+    const int l = __builtin_amdgcn_readfirstlane(e / IPL), rem = e - l * IPL;
+    const int px = rem / E, r = rem - px * E;
+    slot[k] = rem < TPV * E && l < 4 ? (px * 4 + l) * E + r : -1;
     uint32_t o0 = OOB, o1 = OOB, o2 = OOB;
-    int lq = 0;
-    if (e < ITEMS && px < npx && l < levels) {
-      lq = l;
+    const int lq = l < levels ? l : 0;
+    if (rem < TPV * E && px < npx && l < levels) {
       const int hl = pyr.h[l], wl = pyr.w[l];
       const float cx = cxy[(px * 4 + l) * 2], cy = cxy[(px * 4 + l) * 2 + 1];
       const int xs = (int)floorf(cx) - R, gy = (int)floorf(cy) - R + r;
@@ -277,17 +296,17 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
       }
     }
     const __amdgpu_buffer_rsrc_t r0 = lq == 0 ? rs[0] : (lq == 1 ? rs[1] : (lq == 2 ? rs[2] : rs[3]));
-    v[k][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r0, o0, 0, 0));
-    v[k][1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r0, o1, 0, 0));
-    v[k][2] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r0, o2, 0, 0));
+    const uint32_t lim = nbytes[lq];
+    v[k][0] = piece16(r0, o0, lim);
+    v[k][1] = piece16(r0, o1, lim);
+    v[k][2] = piece16(r0, o2, lim);
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
-    const int e = tid + k * 256;
-    if (e < ITEMS) {
-      rows[e * 3] = v[k][0];
-      rows[e * 3 + 1] = v[k][1];
-      rows[e * 3 + 2] = v[k][2];
+    if (slot[k] >= 0) {
+      rows[slot[k] * 3] = v[k][0];
+      rows[slot[k] * 3 + 1] = v[k][1];
+      rows[slot[k] * 3 + 2] = v[k][2];
     }
   }
   __syncthreads();

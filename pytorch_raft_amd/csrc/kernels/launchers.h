@@ -39,13 +39,18 @@ bool launch_corr_otf_fwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
 bool launch_corr_otf_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const int* hs,
                          const int* ws, int levels, const float* coords, const void* dout,
                          int dout_bf16, int dstride, float* df1, float* const* df2lvl, int B,
-                         int C, int H, int W, int radius, hipStream_t stream);
+                         int C, int H, int W, int radius, float* const* slab, const int* cap,
+                         int* boxes, hipStream_t stream);
 
 // all iterations of a step at once from compact window gradients (see corr_window.hip)
 struct WinList;
+// slab / cap / boxes (nullable): deterministic dF2 -- per-tile slab rows [tile][cap[l]][C] fp32
+// per level, boxes [tiles][4][4] int, then a fixed-order reduce (corr_otf_df2_reduce_kernel)
+int otf_tiles(int B, int H, int W);
 bool launch_corr_otf_window_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const int* hs,
                                 const int* ws, int levels, const WinList& wl, float* df1,
                                 float* const* df2lvl, int B, int C, int H, int W, int radius,
+                                float* const* slab, const int* cap, int* boxes,
                                 hipStream_t stream);
 
 // ---- convex upsample (upsample.hip)

@@ -39,6 +39,11 @@ from .optim import fetch_optimizer, clip_grad_norm_
 _PHASE_MARKS = os.environ.get('RAFT_PHASE_MARKS', '0') == '1'
 
 
+def _phase_mark():
+    from ..ops import _ext
+    _ext.ops().phase_mark()
+
+
 class TrainState:
     def __init__(self, model, args, device, sync=True, graph_ready=False):
         self.model = model
@@ -171,6 +176,9 @@ class GraphedTrainStep:
         snap = self._snapshot()
         stream.wait_stream(torch.cuda.current_stream(st.device))
         with torch.cuda.stream(stream):
+            if self.world > 1:
+                # before any other launch: every kernel choice is made on rank 0
+                self._tune_on_rank0(example)
             # static leaves of the decode graph, shaped / strided like the encoder outputs
             with torch.no_grad():
                 feats = model.encode(example[0], example[1])
@@ -178,8 +186,6 @@ class GraphedTrainStep:
             self.sflow = example[2].detach().clone()
             self.svalid = example[3].detach().clone()
             del feats
-            if self.world > 1:
-                self._tune_on_rank0(example)
             for _ in range(warmup):  # MIOpen find / autotune / allocator warm-up: real steps
                 self._step_body(*example, graphs=False)
         torch.cuda.current_stream(st.device).wait_stream(stream)
@@ -203,7 +209,8 @@ class GraphedTrainStep:
         off (their MIOpen finds hit rank 0's db records).  Identical kernels mean identical
         reduction orders on every rank, and the tuning cost is paid once per node.  Effects on
         the weights / BN statistics are rolled back with the warm-up steps."""
-        ops = torch.ops.raft_amd
+        from ..ops import _ext
+        ops = _ext.ops()   # loads the native library (nothing ran yet)
         me = pdist.rank()
         if me != 0:
             ops.conv_set_autotune(0)
@@ -217,11 +224,19 @@ class GraphedTrainStep:
         pdist.barrier(self.st.device)
 
     def _prewarm(self, example):
-        feats = self.st.model.encode(example[0], example[1])
-        preds = self.st.model.decode(*feats, iters=self.st.args.iters)
-        loss, _ = sequence_loss(preds, example[2], example[3], self.st.args.gamma)
-        loss.backward()
-        del feats, preds, loss
+        # a purely local pass: the encoder buckets' all-reduce hooks must not fire (the other
+        # ranks are not in a collective)
+        if self.enc_sync is not None:
+            self.enc_sync.paused = True
+        try:
+            feats = self.st.model.encode(example[0], example[1])
+            preds = self.st.model.decode(*feats, iters=self.st.args.iters)
+            loss, _ = sequence_loss(preds, example[2], example[3], self.st.args.gamma)
+            loss.backward()
+            del feats, preds, loss
+        finally:
+            if self.enc_sync is not None:
+                self.enc_sync.paused = False
         for p in self.params:
             p.grad = None
 
@@ -267,10 +282,10 @@ class GraphedTrainStep:
         feats = self._encode_and_stage(image1, image2, flow, valid)
         if graphs:
             if _PHASE_MARKS:
-                torch.ops.raft_amd.phase_mark()
+                _phase_mark()
             self.g_dec.replay()
             if _PHASE_MARKS:
-                torch.ops.raft_amd.phase_mark()
+                _phase_mark()
             loss = self.loss
         else:
             loss, _ = self._decode()

@@ -130,8 +130,9 @@ def conv_tuning_table():
     """This process's autotuned conv configs: (n, 13) int64 rows (key, config, tile); empty
     without the native library."""
     try:
-        rows = torch.ops.raft_amd.conv_tune_table()
-    except (AttributeError, RuntimeError):
+        from ..ops import _ext
+        rows = _ext.ops().conv_tune_table()
+    except (AttributeError, RuntimeError, ImportError, OSError):
         return torch.zeros(0, 13, dtype=torch.int64)
     return torch.tensor(rows, dtype=torch.int64).view(-1, 13)
 
@@ -152,7 +153,8 @@ def share_conv_tuning(device, src=0):
         dist.broadcast(buf, src)
     if rank() == src or int(n.item()) == 0:
         return 0
-    return int(torch.ops.raft_amd.conv_tune_import(buf.cpu().reshape(-1).tolist()))
+    from ..ops import _ext
+    return int(_ext.ops().conv_tune_import(buf.cpu().reshape(-1).tolist()))
 
 
 @torch.no_grad()
@@ -216,6 +218,7 @@ class GradSync:
                 self.bucket_of[p] = b
         self.stream = None
         self.enabled = self.world > 1
+        self.paused = False
         self.hooks = []
         # overlap evidence: (bucket index, gradients finalised so far) at each bucket launch
         self.hooks_fired = 0
@@ -269,6 +272,8 @@ class GradSync:
             b.work = dist.all_reduce(b.flat, async_op=True)
 
     def _hook(self, p):
+        if self.paused:  # a local pass with no collective partner (rank-0 kernel tuning)
+            return
         self.hooks_fired += 1
         b = self.bucket_of[p]
         b.pending -= 1

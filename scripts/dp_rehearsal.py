@@ -27,6 +27,7 @@ from pytorch_raft_amd import RAFT  # noqa: E402
 from pytorch_raft_amd.data.synthetic import make_pair_batch  # noqa: E402
 from pytorch_raft_amd.engine.trainer import TrainState  # noqa: E402
 from pytorch_raft_amd.parallel import dist as pdist  # noqa: E402
+from pytorch_raft_amd.ops import _ext  # noqa: E402
 
 
 def single_grad(args, sd, dev, i1, i2, flow, valid):
@@ -63,7 +64,8 @@ def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl, fp32=Fals
     # kernel choices made once on rank 0: identical tile tables, no autotune on the other ranks
     tab = pdist.conv_tuning_table().tolist()
     tabs = [None] * world
-    torch.distributed.all_gather_object(tabs, (sorted(map(tuple, tab)), g.autotune_runs))
+    torch.distributed.all_gather_object(tabs, (sorted(map(tuple, tab)),
+                                               int(_ext.ops().conv_autotune_runs())))
     tables_same = all(t[0] == tabs[0][0] for t in tabs) and len(tabs[0][0]) > 0
     runs = [t[1] for t in tabs]
     # one step up to the averaged gradients (weights untouched)

@@ -34,14 +34,15 @@ def parse(d):
     f = glob.glob(os.path.join(d, '**', '*kernel_trace.csv'), recursive=True)[0]
     rows = list(csv.DictReader(open(f)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    ours = [r for r in rows if 'anonymous namespace' in r['Kernel_Name']]
+    ours = [r for r in rows if 'anonymous namespace' in r['Kernel_Name'] or
+            'conv_detail' in r['Kernel_Name']]
     # last third = the last iteration
     n = len(ours) // 3
     tot = 0.0
     for r in ours[-n:]:
         us = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
         tot += us
-        print('%8.1f  %s' % (us, r['Kernel_Name'][:110]))
+        print('%8.1f  %s' % (us, r['Kernel_Name'][:150]))
     print('total %.1f us' % tot)
 
 
