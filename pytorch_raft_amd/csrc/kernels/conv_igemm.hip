@@ -25,6 +25,8 @@
 // dgrad reuses this kernel with flipped / transposed packed weights (stride-1 same padding is
 // self-adjoint up to the flip); wgrad lives in conv_wgrad.hip.
 #include "conv_common.h"
+
+#include <type_traits>
 #include "conv_halo.h"
 
 #include <cmath>
@@ -386,6 +388,16 @@ std::map<TuneKey, int> g_tuned;
 std::mutex g_tune_mu;
 float* g_scratch = nullptr;
 size_t g_scratch_bytes = 0;
+void* g_scratch2 = nullptr;   // redirected outputs of input-gradient convs under autotune
+size_t g_scratch2_bytes = 0;
+
+bool tune_real_dgrad() {
+  static const bool on = [] {
+    const char* e = getenv("RAFT_TUNE_REAL_DGRAD");  // 0: time dgrads on the fp32 scratch store
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 // byte range [lo, hi) of a per-pixel NHWC buffer (P rows of `stride` elements of `esz` bytes)
 struct Range { uintptr_t lo, hi; };
@@ -429,6 +441,44 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   t.out0 = g_scratch;
   t.out0_stride = (a.cout + 255) / 256 * 256;
   t.noseg = 0;
+  // input-gradient convs: timed with their REAL epilogue (the fused GRU gate backward moves as
+  // many bytes as its GEMM), every written / read-modify-written pointer redirected into scratch
+  const bool dgrad_real = (epi == EPI_DGRAD || epi == EPI_DGRAD_GATE) && tune_real_dgrad();
+  ConvFwdArgs td = a;
+  if (dgrad_real) {
+    size_t tot = 0;
+    auto sz = [&](const void* p, int stride, int esz) {
+      return p ? ((size_t)P * stride * esz + 255) / 256 * 256 : (size_t)0;
+    };
+    for (int o = 0; o < a.noseg; ++o) {
+      const OSeg& q = a.oseg[o];
+      tot += sz(q.ptr, q.stride, 4) + sz(q.ob, q.ob_stride, 2) + sz(q.gb, q.gb_stride, 2) +
+             sz(q.gf0, q.gf_stride, 4) + sz(q.gf1, q.gf_stride, 4);
+    }
+    if (tot > g_scratch2_bytes) {
+      if (g_scratch2) (void)hipFree(g_scratch2);
+      if (hipMalloc(&g_scratch2, tot) != hipSuccess) { g_scratch2 = nullptr; g_scratch2_bytes = 0; tot = 0; }
+      else g_scratch2_bytes = tot;
+    }
+    if (g_scratch2 != nullptr && tot > 0) {
+      char* cur = static_cast<char*>(g_scratch2);
+      auto take = [&](auto* p, int stride, int esz) {
+        using T = std::remove_pointer_t<std::remove_reference_t<decltype(p)>>;
+        if (!p) return p;
+        T* r = reinterpret_cast<T*>(cur);
+        cur += sz(p, stride, esz);
+        return r;
+      };
+      for (int o = 0; o < a.noseg; ++o) {
+        OSeg& q = td.oseg[o];
+        q.ptr = take(q.ptr, q.stride, 4);
+        q.ob = take(q.ob, q.ob_stride, 2);
+        q.gb = take(q.gb, q.gb_stride, 2);
+        q.gf0 = take(q.gf0, q.gf_stride, 4);
+        q.gf1 = take(q.gf1, q.gf_stride, 4);
+      }
+    }
+  }
   // store-only epilogues are timed as they will run (the GRU gate epilogues cost registers and
   // bytes the fp32 scratch epilogue does not): their outputs are rewritten by the real launch
   // that follows; accumulating epilogues (ACC_F32, DGRAD) are timed on the fp32 scratch
@@ -437,8 +487,9 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   // ... but only while no output overlaps an operand the launches read (an in-place GRU state
   // update, say): repeated candidate launches would then read their own outputs
   if (real_epi && outputs_overlap_inputs(a, epi)) real_epi = false;
-  const ConvFwdArgs& ta = real_epi ? a : t;
-  const int te = real_epi ? epi : EPI_F32;
+  const bool dgr = dgrad_real && g_scratch2 != nullptr;
+  const ConvFwdArgs& ta = dgr ? td : (real_epi ? a : t);
+  const int te = (real_epi || dgr) ? epi : EPI_F32;
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -483,8 +534,11 @@ int choose_cfg(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   const int P = a.B * a.H * a.W;
   if (forced >= 0 && forced < kNumCfgs && cfg_allowed(forced, a.cout, smallc, epi)) return forced;
   const bool f32out = epi == EPI_F32 || epi == EPI_ACC_F32 || epi == EPI_DGRAD ||
-                      epi == EPI_DGRAD_GATE || epi == EPI_F32_NCHW;
-  const int eclass = f32out ? 1 : ((epi == EPI_GRU_ZR || epi == EPI_GRU_Q) ? 2 : 0);
+                      epi == EPI_F32_NCHW;
+  // the gated input-gradient convs tune apart from the plain ones of the same geometry (their
+  // epilogue is timed for real)
+  const int eclass = epi == EPI_DGRAD_GATE ? 3
+                     : (f32out ? 1 : ((epi == EPI_GRU_ZR || epi == EPI_GRU_Q) ? 2 : 0));
   int creal = 0;
   for (int q = 0; q < a.nseg && q < 3; ++q) creal += a.seg[q].real;
   const TuneKey key{P, a.H, a.W, a.KH, a.KW, smallc ? a.cin_small : a.cin_pad, a.cout, (int)smallc,

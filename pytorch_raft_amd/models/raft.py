@@ -253,18 +253,20 @@ class RAFT(nn.Module):
         x = inp.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
         flow_predictions = []
         flow_up = None
+        flow = coords1 - coords0
         for itr in range(iters):
             coords1 = coords1.detach()
             corr = corr_fn.lookup_nhwc(coords1, CORR_BUF_SMALL)
-            flow = coords1 - coords0
+            flow = flow.detach()   # = coords1 - coords0 (see _iterate_fused)
             h, delta_flow = hub(h, x, corr, flow)
             coords1 = coords1 + delta_flow
+            flow = coords1 - coords0
             if test_mode and itr < iters - 1:
                 continue
-            flow_up = upflow8(coords1 - coords0)
+            flow_up = upflow8(flow)
             flow_predictions.append(flow_up)
         if test_mode:
-            return coords1 - coords0, flow_up
+            return flow, flow_up
         return flow_predictions
 
     def _iterate_fused(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
@@ -276,17 +278,21 @@ class RAFT(nn.Module):
         x = inp.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
         flow_predictions = []
         flow_up = None
+        flow = coords1 - coords0
         for itr in range(iters):
             coords1 = coords1.detach()
             corr = corr_fn.lookup_nhwc(coords1, CORR_BUF)
-            flow = coords1 - coords0
+            # flow = coords1 - coords0 of the detached coords: the previous iteration's upsampling
+            # input, detached (same values; one subtraction kernel per iteration instead of two)
+            flow = flow.detach()
             last = itr == iters - 1
             h, delta_flow, up_mask = hub(h, x, corr, flow, need_mask=last or not test_mode)
             coords1 = coords1 + delta_flow
+            flow = coords1 - coords0
             if test_mode and itr < iters - 1:
                 continue
-            flow_up = convex_upsample(coords1 - coords0, up_mask, nhwc=True)
+            flow_up = convex_upsample(flow, up_mask, nhwc=True)
             flow_predictions.append(flow_up)
         if test_mode:
-            return coords1 - coords0, flow_up
+            return flow, flow_up
         return flow_predictions

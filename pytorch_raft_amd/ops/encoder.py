@@ -452,7 +452,29 @@ def _wgrad_native_ok(x, conv):
             and x.numel() * 2 < 2 ** 31 and x.shape[0] * x.shape[2] * x.shape[3] * conv.out_channels * 2 < 2 ** 31)
 
 
+# int32 byte-offset range of MIOpen's kernels and of our buffer descriptors
+_CONV_BYTES = int(os.environ.get('RAFT_CONV_CHUNK_BYTES', str(2 ** 31 - 1)))
+
+
 def _conv(ps, x, conv, with_bias=False):
+    """One encoder conv; batches whose input or output passes 2 GiB run as equal image chunks
+    (a conv is per-image; the batch norm that couples the images runs on the whole batch, so a
+    training-mode batch-norm encoder -- the chairs stage -- no longer caps the per-GPU batch)."""
+    n, _, h, w = x.shape
+    sh, sw = conv.stride
+    ho = (h + 2 * conv.padding[0] - conv.dilation[0] * (conv.kernel_size[0] - 1) - 1) // sh + 1
+    wo = (w + 2 * conv.padding[1] - conv.dilation[1] * (conv.kernel_size[1] - 1) - 1) // sw + 1
+    per = max(x[0].numel(), conv.out_channels * ho * wo) * 2
+    if n > 1 and n * per > _CONV_BYTES:
+        k = max(1, _CONV_BYTES // per)
+        parts = -(-n // k)
+        size = -(-n // parts)   # equal chunks: the same kernel choices for every chunk
+        outs = [_conv_one(ps, c, conv, with_bias) for c in torch.split(x, size, dim=0)]
+        return torch.cat(outs, dim=0).contiguous(memory_format=torch.channels_last)
+    return _conv_one(ps, x, conv, with_bias)
+
+
+def _conv_one(ps, x, conv, with_bias=False):
     w = ps.weights.get(conv)
     if w is None:
         w = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)

@@ -20,6 +20,8 @@ for c in "$@"; do
   case $c in
     fp16) run fp16 500 --precision fp16 ;;
     fp32) run fp32 900 --precision fp32 ;;
+    fp32cl) run fp32cl 900 --precision fp32 --channels_last ;;
+    b384) MIOPEN_FIND_MODE=2 run train_b384_bn 900 --batch 384 --steps 3 --warmup 2 ;;
     kitti_ap) run kitti_ap 500 --size 288 960 --iters 24 --corr_mode allpairs ;;
     kitti_otf) run kitti_otf 500 --size 288 960 --iters 24 --corr_mode onthefly ;;
     chairs_otf) run chairs_otf 400 --corr_mode onthefly ;;

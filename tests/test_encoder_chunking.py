@@ -49,3 +49,31 @@ def test_default_limit_keeps_headline_batches_whole():
     with torch.autocast('cpu', dtype=torch.bfloat16):
         assert enc._chunk_images(torch.empty(1, 3, 368, 496).expand(192, -1, -1, -1)) == 0
         assert enc._chunk_images(torch.empty(1, 3, 368, 496).expand(384, -1, -1, -1)) == 367
+
+
+@pytest.mark.parametrize('stride,k', [(1, 3), (2, 3), (2, 7), (2, 1)])
+def test_fast_path_conv_chunks_oversized_batches(monkeypatch, stride, k):
+    """A training-mode batch-norm encoder cannot be chunked as a whole; instead each conv whose
+    input or output passes the 2 GiB offset range runs as equal image chunks (ops/encoder.py:
+    _conv) -- same output and gradients as one call (CPU, bf16 channels_last, tiny limit)."""
+    from pytorch_raft_amd.ops import encoder as fast
+    torch.manual_seed(2)
+    conv = torch.nn.Conv2d(8, 16, k, stride=stride, padding=k // 2)
+    x = torch.randn(5, 8, 12, 14).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    ps = fast._Pass({}, {}, {})
+    y0 = fast._conv(ps, x, conv)
+    g = torch.randn_like(y0)
+    (y0.float() * g).sum().backward()
+    ref = (y0.detach().clone(), x.grad.clone(), conv.weight.grad.clone())
+    x.grad = None
+    conv.weight.grad = None
+    monkeypatch.setattr(fast, '_CONV_BYTES', 2 * 16 * 12 * 14 * 2)   # two images per call
+    y1 = fast._conv(ps, x, conv)
+    assert y1.is_contiguous(memory_format=torch.channels_last)
+    (y1.float() * g).sum().backward()
+    torch.testing.assert_close(y1, ref[0], atol=0, rtol=0)
+    torch.testing.assert_close(x.grad, ref[1], atol=0, rtol=0)
+    # the weight gradient sums per-chunk bf16 gradients (autograd accumulation): bf16 rounding
+    scale = ref[2].abs().max().item()
+    torch.testing.assert_close(conv.weight.grad, ref[2], atol=2e-2 * scale, rtol=0)

@@ -82,13 +82,14 @@ def test_corr_build_bf16_pyramid_and_lookup(ext_ops, shape):
 @pytest.mark.parametrize('shape,radius,spread', [((2, 256, 46, 62), 4, 6.0), ((1, 128, 13, 19), 3, 6.0),
                                                   ((2, 64, 23, 30), 4, 40.0), ((3, 32, 11, 17), 4, 2.0)])
 def test_lookup_rows_bf16_vs_oracle(ext_ops, shape, radius, spread):
-    """Row-vector NHWC lookup on the bf16 pyramid (aligned 16-B row pieces, plane-edge masking)
-    vs the grid_sample oracle on the same bf16 values: equal up to the bf16 rounding of the
-    output; the zero-padded channels stay exactly zero."""
+    """Row-vector NHWC lookup on the bf16 pyramid (aligned 16-B row pieces, plane-edge masking,
+    dword reads for the pieces at a workgroup range's end) vs the grid_sample oracle on the same
+    bf16 values: equal up to the bf16 rounding of the output; the padded channels stay zero."""
     b, c, h, w = shape
     f1 = torch.randn(b, h, w, c, device=DEV).to(torch.bfloat16)
     f2 = torch.randn(b, h, w, c, device=DEV).to(torch.bfloat16)
-    levels = 4 if min(h, w) >= 8 else 3
+    # the oracle's align_corners normalisation divides by (size - 1): every level >= 2 x 2
+    levels = 4 if min(h, w) >= 16 else 3
     pyr = ext_ops.corr_build_bf16(f1, f2, levels, True)
     coords = _coords(b, h, w, spread=spread, seed=3)
     out = torch.full((b, h, w, 384), 7.0, device=DEV, dtype=torch.bfloat16)
@@ -98,7 +99,10 @@ def test_lookup_rows_bf16_vs_oracle(ext_ops, shape, radius, spread):
     ctot = levels * (2 * radius + 1) ** 2
     got = out[..., :ctot].permute(0, 3, 1, 2).float()
     err = (got - ref).abs()
-    assert (err <= ref.abs() * 2.0 ** -8 + 1e-6).all(), err.max().item()
+    # bf16 output rounding (<= 2^-8 relative) + the oracle's own coordinate normalisation
+    # (grid_sample maps x -> [-1, 1] -> x: ~1e-6 px, i.e. ~1e-5 absolute on the taps)
+    bound = ref.abs() * 2.0 ** -8 + 1e-4 * ref.abs().max()
+    assert (err <= bound).all(), ((err - bound).max().item(), err.max().item())
     assert (out[..., ctot:] == 0).all()
 
 
