@@ -1050,10 +1050,10 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   for (size_t o = 0; o < gate_mode.size(); ++o) {
     const int mode = (int)gate_mode[o];
     if (mode == 0) continue;
-    TORCH_CHECK(mode == 1 || mode == 2, "gate mode must be 0, 1 or 2");
+    TORCH_CHECK(mode >= 1 && mode <= 3, "gate mode must be 0..3");
     TORCH_CHECK(gt + 7 <= gate_t.size(), "gate tensors missing");
     TORCH_CHECK(outs[o].scalar_type() == at::kFloat, "gated dgrad segment must be fp32");
-    TORCH_CHECK(mode == 2 || out_acc[o], "q-gate segment reads the accumulated state gradient");
+    TORCH_CHECK(mode == 2 || out_acc[o], "q-gate / relu segments read the accumulated gradient");
     const int real = (int)out_real[o];
     const Tensor& z = gate_t[gt + 0];
     const Tensor& qr = gate_t[gt + 1];
@@ -1081,7 +1081,10 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     a.oseg[o].gb_stride = (int)gbo.size(3);
     a.oseg[o].gf1 = gf1.data_ptr<float>();
     a.oseg[o].gf_stride = (int)gf1.size(3);
-    if (mode == 1) {
+    if (mode == 3) {  // gf1: the accumulated fp32 gradient; z: the ReLU output; gb: the result
+      a.oseg[o].gf0 = nullptr;
+      a.oseg[o].gin = nullptr;
+    } else if (mode == 1) {
       check_nhwc(gf0, B, H, W, "gate dz output", at::kFloat);
       TORCH_CHECK(gf0.size(3) == gf1.size(3), "gate fp32 outputs must share a layout");
       a.oseg[o].gf0 = gf0.data_ptr<float>();

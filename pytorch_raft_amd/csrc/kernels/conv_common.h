@@ -219,6 +219,29 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
                 bst_f32(f1, of, g * (1.f - zz[u]));
               }
             }
+          } else if (o.gate == 3) {  // last accumulation + ReLU backward: gb = bf16([y > 0](pre + v))
+            const uint32_t ab = P_u * (uint32_t)o.ga_stride * 2u;
+            const rsrc_t ry = make_rsrc(o.ga0, ab);
+            const rsrc_t f1 = make_rsrc(o.gf1, P_u * (uint32_t)o.gf_stride * 4u);
+            const rsrc_t gb = make_rsrc(o.gb, P_u * (uint32_t)o.gb_stride * 2u);
+#pragma unroll
+            for (int h8 = 0; h8 < 16; h8 += 8) {
+              float pre[8], yv[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int r = h8 + u;
+                const bool e = ok[r] && cok;
+                pre[u] = bld_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB);
+                yv[u] = bld_bf16(ry, e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB);
+              }
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int r = h8 + u;
+                const bool e = ok[r] && cok;
+                bst_bf16(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB,
+                         yv[u] > 0.f ? pre[u] + v[r] : 0.f);
+              }
+            }
           } else if (o.gate == 2) {  // ConvGRU z / r gate backward on d(r*h)
             const uint32_t ab = P_u * (uint32_t)o.ga_stride * 2u;
             const rsrc_t rz = make_rsrc(o.ga0, ab), rr = make_rsrc(o.ga1, ab), rh = make_rsrc(o.ga2, ab);

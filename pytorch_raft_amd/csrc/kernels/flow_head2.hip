@@ -22,6 +22,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int FH_C = 256;
@@ -173,6 +175,87 @@ __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict_
   }
 }
 
+// Tiled variant (the launcher's kernel): a workgroup owns a 4 x 16 pixel tile; the tile's 6 x 18
+// halo of the two fp32 output-gradient planes is staged once in LDS as bf16 pairs (the rounding
+// fh2_dgrad_kernel applies), so a tap is one broadcast LDS read instead of two scattered global
+// loads per lane (the 72 gathers per thread made the per-pixel kernel ~4x slower than its bytes).
+// thread = 8-channel group (tid & 31) x 8 of the tile's pixels.
+constexpr int DTH = 4, DTW = 16;
+__global__ __launch_bounds__(256) void fh2_dgrad_tile_kernel(const float* __restrict__ gout,
+                                                             const uint32_t* __restrict__ wd,
+                                                             const uint16_t* __restrict__ fm, int fs,
+                                                             uint16_t* __restrict__ dx, int ds, int B,
+                                                             int H, int W, int tiles_y, int tiles_x) {
+  constexpr int HH = DTH + 2, HW_ = DTW + 2;
+  __shared__ uint32_t gp[HH * HW_];
+  const int g = threadIdx.x & 31;
+  int t = blockIdx.x;
+  const int tx = t % tiles_x;
+  t /= tiles_x;
+  const int ty = t % tiles_y;
+  const int b = t / tiles_y;
+  const int y0 = ty * DTH, x0 = tx * DTW;
+  const int64_t hw = (int64_t)H * W;
+  const float* g0 = gout + (int64_t)b * 2 * hw;
+  for (int e = threadIdx.x; e < HH * HW_; e += 256) {
+    const int yy = y0 - 1 + e / HW_, xx = x0 - 1 + e % HW_;
+    uint32_t v = 0u;
+    if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
+      const int64_t o = (int64_t)yy * W + xx;
+      v = pack_bf2(g0[o], g0[hw + o]);
+    }
+    gp[e] = v;
+  }
+  uint4 wa[9], wb[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    wa[k] = *reinterpret_cast<const uint4*>(wd + k * FH_C + g * 8);
+    wb[k] = *reinterpret_cast<const uint4*>(wd + k * FH_C + g * 8 + 4);
+  }
+  constexpr int NP = DTH * DTW / 8;  // pixels per thread
+  uint4 m[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int p = (threadIdx.x >> 5) + 8 * k;
+    const int yy = y0 + p / DTW, xx = x0 + p % DTW;
+    m[k] = (yy < H && xx < W)
+               ? *reinterpret_cast<const uint4*>(fm + (((int64_t)b * H + yy) * W + xx) * fs + g * 8)
+               : make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int p = (threadIdx.x >> 5) + 8 * k;
+    const int py = p / DTW, px = p % DTW;
+    float s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      // tap (ky, kx) of the adjoint: gout at (y - ky + 1, x - kx + 1) = halo (py + 2 - ky, px + 2 - kx)
+      const uint32_t gv = gp[(py + 2 - tap / 3) * HW_ + px + 2 - tap % 3];
+      const uint32_t wv[8] = {wa[tap].x, wa[tap].y, wa[tap].z, wa[tap].w,
+                              wb[tap].x, wb[tap].y, wb[tap].z, wb[tap].w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] = dot2(gv, wv[i], s[i]);
+    }
+    const uint32_t mw[4] = {m[k].x, m[k].y, m[k].z, m[k].w};
+    uint32_t ov[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool lo = (mw[q] & 0x8000u) == 0 && (mw[q] & 0x7fffu) != 0;
+      const bool hi = (mw[q] & 0x80000000u) == 0 && (mw[q] & 0x7fff0000u) != 0;
+      const uint32_t a = lo ? raft_f32_to_bf16(s[2 * q]) : 0u;
+      const uint32_t c = hi ? raft_f32_to_bf16(s[2 * q + 1]) : 0u;
+      ov[q] = a | (c << 16);
+    }
+    const int yy = y0 + py, xx = x0 + px;
+    if (yy < H && xx < W)
+      *reinterpret_cast<uint4*>(dx + (((int64_t)b * H + yy) * W + xx) * ds + g * 8) =
+          make_uint4(ov[0], ov[1], ov[2], ov[3]);
+  }
+}
+
 // dw[o][t*256 + c] += sum_items sum_p gout[p][o] * in[p + off_t][c];  db[o] += sum gout[p][o]
 // block 256 = 8 row lanes x 32 channel groups; a unit = (item, image, 8-row block)
 __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int B, int H, int W,
@@ -297,6 +380,16 @@ bool launch_fh2_fwd(const uint16_t* in, int cs, const uint32_t* wf, const float*
 bool launch_fh2_dgrad(const float* gout, const uint32_t* wd, const uint16_t* fm, int fs, uint16_t* dx,
                       int ds, int B, int H, int W, hipStream_t stream) {
   if (fs % 8 != 0 || ds % 8 != 0 || fs < FH_C || ds < FH_C) return false;
+  static const bool v1 = [] {
+    const char* e = getenv("RAFT_FH2_DGRAD_V1");
+    return e && e[0] == '1';
+  }();
+  if (!v1) {
+    const int ty = (H + DTH - 1) / DTH, tx = (W + DTW - 1) / DTW;
+    hipLaunchKernelGGL(fh2_dgrad_tile_kernel, dim3((unsigned)(B * ty * tx)), dim3(256), 0, stream,
+                       gout, wd, fm, fs, dx, ds, B, H, W, ty, tx);
+    return true;
+  }
   const int64_t P = (int64_t)B * H * W;
   hipLaunchKernelGGL(fh2_dgrad_kernel<4>, dim3(raft_cdiv(P, 32)), dim3(256), 0, stream, gout, wd, fm, fs,
                      dx, ds, B, H, W);

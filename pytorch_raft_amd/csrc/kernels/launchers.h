@@ -119,6 +119,8 @@ struct OSeg {
   //            gb[c] = bf16(g z (1 - q^2)) (d pre-q), gf0[c] = g (q - h) (dz), gf1[c] = g (1 - z)
   //  gate 2 -- z / r gates on d(r*h): gb[c] = bf16(gin[c] z (1 - z)), gb[real + c] =
   //            bf16(v h r (1 - r)), gf1[c] += v r                 (ga0, ga1, ga2 = z, q|r, h)
+  //  gate 3 -- the last accumulation into an fp32 gradient + the backward of the ReLU that
+  //            produced this conv's input (ga0 = its output y): gb[c] = bf16([y > 0](gf1[c] + v))
   int gate;
   const uint16_t* ga0;
   const uint16_t* ga1;

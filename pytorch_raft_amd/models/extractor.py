@@ -12,15 +12,19 @@ Behavioural parity with the reference encoders (`core/extractor.py:6-267`):
 State-dict schema is kept identical (`SURVEY.md` §2.5), including the strided residual block that
 registers the same norm module as both ``norm3`` and ``downsample.1`` (`core/extractor.py:26,44-45`).
 
-MI355X notes: the convolutions stay on PyTorch-ROCm (MIOpen).  On the GPU under bf16 autocast the
-forward runs the channels-last fast path of ``pytorch_raft_amd.ops.encoder``: NHWC MIOpen convs
-without NCHW<->NHWC transposes, each norm + ReLU (and residual add + ReLU) one fused HIP autograd
-node, conv biases folded into the norms.
+MI355X notes: on the GPU under bf16 autocast the forward runs the channels-last fast path of
+``pytorch_raft_amd.ops.encoder``: the stride-1 convs on our MFMA implicit-GEMM kernels, the strided
+ones on NHWC MIOpen convs, each norm + ReLU (and residual add + ReLU) one fused HIP autograd node,
+conv biases folded into the norms.  An fp32 model (the reference's default schedule) runs its
+stride-1 convs as split-bf16 MFMA products (``MfmaConv2d`` -> ``ops/conv_fp32.py``, ~2^-16
+relative) while ``conv_fp32.enabled()`` is active; only the three strided convs stay on MIOpen.
 """
 import os
 
 import torch
 import torch.nn as nn
+
+from .update import MfmaConv2d
 
 
 def make_norm(kind, channels, groups=None):
@@ -42,8 +46,8 @@ class ResidualBlock(nn.Module):
 
     def __init__(self, in_planes, planes, norm_fn='group', stride=1):
         super().__init__()
-        self.conv1 = nn.Conv2d(in_planes, planes, kernel_size=3, padding=1, stride=stride)
-        self.conv2 = nn.Conv2d(planes, planes, kernel_size=3, padding=1)
+        self.conv1 = MfmaConv2d(in_planes, planes, kernel_size=3, padding=1, stride=stride)
+        self.conv2 = MfmaConv2d(planes, planes, kernel_size=3, padding=1)
         self.relu = nn.ReLU(inplace=True)
         g = planes // 8
         self.norm1 = make_norm(norm_fn, planes, g)
@@ -54,7 +58,7 @@ class ResidualBlock(nn.Module):
             # the same module object under two names -> both key sets appear in state_dict
             self.norm3 = make_norm(norm_fn, planes, g)
             self.downsample = nn.Sequential(
-                nn.Conv2d(in_planes, planes, kernel_size=1, stride=stride), self.norm3)
+                MfmaConv2d(in_planes, planes, kernel_size=1, stride=stride), self.norm3)
 
     def forward(self, x):
         y = self.relu(self.norm1(self.conv1(x)))
@@ -70,9 +74,9 @@ class BottleneckBlock(nn.Module):
     def __init__(self, in_planes, planes, norm_fn='group', stride=1):
         super().__init__()
         mid = planes // 4
-        self.conv1 = nn.Conv2d(in_planes, mid, kernel_size=1, padding=0)
-        self.conv2 = nn.Conv2d(mid, mid, kernel_size=3, padding=1, stride=stride)
-        self.conv3 = nn.Conv2d(mid, planes, kernel_size=1, padding=0)
+        self.conv1 = MfmaConv2d(in_planes, mid, kernel_size=1, padding=0)
+        self.conv2 = MfmaConv2d(mid, mid, kernel_size=3, padding=1, stride=stride)
+        self.conv3 = MfmaConv2d(mid, planes, kernel_size=1, padding=0)
         self.relu = nn.ReLU(inplace=True)
         g = planes // 8
         self.norm1 = make_norm(norm_fn, mid, g)
@@ -83,7 +87,7 @@ class BottleneckBlock(nn.Module):
         else:
             self.norm4 = make_norm(norm_fn, planes, g)
             self.downsample = nn.Sequential(
-                nn.Conv2d(in_planes, planes, kernel_size=1, stride=stride), self.norm4)
+                MfmaConv2d(in_planes, planes, kernel_size=1, stride=stride), self.norm4)
 
     def forward(self, x):
         y = self.relu(self.norm1(self.conv1(x)))
@@ -105,14 +109,14 @@ class _Encoder(nn.Module):
         self.norm_fn = norm_fn
         stem = self.widths[0]
         self.norm1 = make_norm(norm_fn, stem, 8)
-        self.conv1 = nn.Conv2d(3, stem, kernel_size=7, stride=2, padding=3)
+        self.conv1 = MfmaConv2d(3, stem, kernel_size=7, stride=2, padding=3)
         self.relu1 = nn.ReLU(inplace=True)
 
         self.in_planes = stem
         self.layer1 = self._make_layer(self.widths[1], stride=1)
         self.layer2 = self._make_layer(self.widths[2], stride=2)
         self.layer3 = self._make_layer(self.widths[3], stride=2)
-        self.conv2 = nn.Conv2d(self.widths[3], output_dim, kernel_size=1)
+        self.conv2 = MfmaConv2d(self.widths[3], output_dim, kernel_size=1)
         self.dropout = nn.Dropout2d(p=dropout) if dropout > 0 else None
         self._init_weights()
 

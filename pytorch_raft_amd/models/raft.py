@@ -40,6 +40,9 @@ from ..ops.upsample import convex_upsample
 from ..ops import _ext
 from ..ops import conv_fp32
 
+# RAFT_FP32_ENC_MFMA=0: an fp32 model's encoders keep MIOpen fp32 convs (A/B measurements)
+_FP32_ENC_MFMA = os.environ.get('RAFT_FP32_ENC_MFMA', '1') != '0'
+
 
 def _get(args, name, default):
     return getattr(args, name, default)
@@ -141,9 +144,12 @@ class RAFT(nn.Module):
         # encoder kernels either
         native = self.corr_impl != 'torch'
         self.fnet.allow_native = self.cnet.allow_native = native
-        with self._autocast(dev):
+        # fp32 model: the encoders' stride-1 convs run as split-bf16 MFMA convs (one scope per
+        # encoder call, so each conv's deferred weight gradient covers exactly that call)
+        fp32_mfma = native and self._use_fp32_mfma(image1) and _FP32_ENC_MFMA
+        with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
             fmap1, fmap2 = self.fnet([image1, image2])
-        with self._autocast(dev):
+        with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
             cnet = self.cnet(image1)
             net, inp = torch.split(cnet, [hdim, cdim], dim=1)
             net = torch.tanh(net)

@@ -31,7 +31,8 @@ class MfmaConv2d(nn.Conv2d):
     def forward(self, x):
         from ..ops import conv_fp32
         if (conv_fp32.active_for(x, self.weight) and self.stride == (1, 1) and
-                self.dilation == (1, 1) and self.groups == 1 and self.padding_mode == 'zeros'):
+                self.dilation == (1, 1) and self.groups == 1 and self.padding_mode == 'zeros' and
+                conv_fp32.fits(x, self.out_channels)):
             return conv_fp32.module_conv2d(self, x)
         return super().forward(x)
 

@@ -1,4 +1,5 @@
-"""fp32 convolutions of the update block on the bf16 MFMA kernels (split-bf16, 3 products).
+"""fp32 convolutions (update block + stride-1 encoder convs) on the bf16 MFMA kernels (split-bf16,
+3 products).
 
 The reference's paper schedule trains in fp32 (`train_standard.sh`, no `--mixed_precision`):
 every update-block conv (`core/update.py`) is then an fp32 NCHW conv.  gfx950's matrix cores
@@ -56,6 +57,15 @@ def enabled(on=True):
 def active_for(x, weight):
     return (_ACTIVE['on'] and _ENV_ON and x.is_cuda and x.dtype == torch.float32 and
             weight.dtype == torch.float32 and x.dim() == 4 and not torch.is_autocast_enabled())
+
+
+def fits(x, cout):
+    """The split operands ([hi | lo] bf16 NHWC, 2 x the 64-padded channels) and the fp32 output
+    stay inside the kernels' 32-bit buffer-descriptor range; larger calls keep MIOpen."""
+    b, cin, h, w = x.shape
+    pix = b * h * w
+    return (pix * 4 * max(C.round_up(cin, 64), C.round_up(cout, 64)) < 2 ** 31 and
+            pix * 4 * cout < 2 ** 31)
 
 
 def _split_nhwc_torch(x, cpad):

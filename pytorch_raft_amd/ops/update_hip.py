@@ -756,12 +756,19 @@ class _UpdateIter(torch.autograd.Function):
                 # dhp is now the final gradient of half-step 1's output: its q gate here
                 gspec, nxt = qgate(halves[1][1])
                 dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)], zr_outs, gates=[gspec, None])
+            elif _GATES_FUSED:
+                # the last accumulation into dmf: the motion-encoder ReLU backward (its forward
+                # output is mf) in this epilogue -> bf16 d pre-activation, dmf is never re-read
+                dpre_conv = _bf16(sh + (128,), dev)
+                dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)], zr_outs,
+                      gates=[None, (3, [mf, mf, mf, dmf, dpre_conv, dmf, dmf])])
             else:
                 dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)], zr_outs)
             dh = dhp
         # ---- motion encoder
-        dpre_conv = _bf16(sh + (128,), dev)
-        ops.relu_bwd_(dmf, 0, mf, 0, dpre_conv, 0, 128, 1.0)
+        if not _GATES_FUSED:
+            dpre_conv = _bf16(sh + (128,), dev)
+            ops.relu_bwd_(dmf, 0, mf, 0, dpre_conv, 0, 128, 1.0)
         wgrad('conv', dpre_conv, 0, [(cf, 0, 256)])
         dpre_cf = _bf16(sh + (256,), dev)
         dgrad('conv', [(dpre_conv, 0, 128)], [(dpre_cf, 0, 256, 256, 0, cf, 0)])

@@ -142,3 +142,38 @@ def test_fp32_training_trajectory_split_vs_miopen(ext_ops):
         if n.startswith('update_block'):
             # biases: few entries of small norm, where one sign-flipped AdamW step shows most
             assert _rel(wa[n], wb[n]) < (2e-3 if wb[n].dim() > 1 else 1e-2), n
+
+
+@pytest.mark.parametrize('norm', ['instance', 'batch'])
+def test_fp32_encoder_split_vs_fp64(ext_ops, norm):
+    """fp32 BasicEncoder (fnet: instance norm, cnet: batch norm): with ``conv_fp32.enabled()`` its
+    stride-1 convs (12 of 15) run as split-bf16 MFMA products.  Output, input gradient and every
+    parameter gradient are compared with an fp64 CPU run of the same module: the split encoder's
+    error stays within 4x the MIOpen fp32 encoder's own error (plus a 2^-16-scale floor)."""
+    import copy
+    from pytorch_raft_amd.models.extractor import BasicEncoder
+    torch.manual_seed(0)
+    enc = BasicEncoder(output_dim=256, norm_fn=norm).to(DEV).train()
+    x0 = torch.randn(3, 3, 96, 128, device=DEV)
+    gout = torch.randn(3, 256, 12, 16, device=DEV)
+
+    def run(m, x, g, on=False):
+        m.zero_grad(set_to_none=True)
+        x = x.clone().requires_grad_(True)
+        with conv_fp32.enabled(on):
+            y = m(x)
+        (y * g).sum().backward()
+        return {'out': y.detach().double().cpu(), 'dx': x.grad.detach().double().cpu(),
+                **{n: p.grad.detach().double().cpu() for n, p in m.named_parameters()}}
+
+    ref = run(copy.deepcopy(enc).double().cpu(), x0.double().cpu(), gout.double().cpu())
+    split = run(enc, x0, gout, True)
+    miop = run(enc, x0, gout, False)
+    errs = []
+    for n in ref:
+        if n.endswith('.bias') and n != 'conv2.bias' and ('conv' in n or 'downsample.0' in n):
+            continue   # a conv bias feeding a norm has an exactly-zero gradient (rounding noise)
+        es, em = _rel(split[n], ref[n]), _rel(miop[n], ref[n])
+        errs.append((n, es, em))
+        assert es <= 4 * em + 3e-5, (n, es, em)
+    print('\n'.join('%-28s split %.2e  miopen %.2e' % e for e in errs))

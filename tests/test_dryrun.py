@@ -10,7 +10,7 @@ import os
 import pytest
 import torch
 
-from pytorch_raft_amd.ops import _ext
+from pytorch_raft_amd.ops import _ext, update_hip
 
 if not os.path.exists(_ext.LIB_PATH):
     pytest.skip('native library not built', allow_module_level=True)
@@ -85,8 +85,10 @@ def test_dry_run_fused_training_step(alternate):
         loss.backward()
     names = set(ops.calls)
     assert {'conv_fwd_', 'conv_dgrad_', 'conv_wgrad_taps_',
-            'relu_bwd_', 'f1_patch_', 'fh2_fwd_', 'fh2_dgrad_', 'fh2_wgrad_', 'convex_up_fwd',
+            'f1_patch_', 'fh2_fwd_', 'fh2_dgrad_', 'fh2_wgrad_', 'convex_up_fwd',
             'convex_up_bwd', 'seq_loss_fwd'} <= names, names
+    # the motion encoder's ReLU backward rides in the last input-gradient conv's epilogue (gate 3)
+    assert ('relu_bwd_' in names) == (not update_hip._GATES_FUSED)
     if not alternate:
         assert {'corr_build', 'corr_lookup_nhwc_', 'corr_tap_reduce'} <= names
     else:
