@@ -261,7 +261,10 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
     const int64_t abase = first & ~(int64_t)7;
     dl[l] = (int)(first - abase);
     const uint16_t* base = reinterpret_cast<const uint16_t*>(pyr.lvl[ll]) + abase;
-    const uint32_t bytes = (uint32_t)((dl[l] + (int64_t)npx * plane) * 2);
+    // rounded up to whole dwords: a dword read only partly inside num_records returns zero, so
+    // an odd element count would lose the last plane's last element (the allocation is padded,
+    // the extra bytes are masked cells)
+    const uint32_t bytes = (uint32_t)(((dl[l] + (int64_t)npx * plane) * 2 + 3) & ~(int64_t)3);
     nbytes[l] = bytes;
     rs[l] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), (short)0, (int)bytes,
                                              0x00020000);
@@ -625,14 +628,49 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
 // order as corr_tap_reduce_kernel (bitwise the same dC), but each WAVE owns one query pixel's
 // level planes in its own LDS slice, so there is no workgroup barrier at all: a wave's LDS
 // operations execute in issue order, which orders the iterations' read-modify-writes and makes
-// the staged tap row visible to the wave's other lanes.  The next iteration's tap row is in
-// flight (registers) while the current one is folded.  Plane zero fill and the level-0 row
-// write-out are 16-B / 4-B vector operations.  ~17 KB of LDS per wave at chairs (1/8 = 46 x 62).
+// the staged tap rows visible to the wave's other lanes.
+//  * Latency: the coordinates and tap rows of the next TG iterations are loaded (wave-uniform
+//    coordinate loads, one 16-B tap piece per lane and iteration) while the current TG are folded;
+//    a dependent global load per iteration made the first version of this kernel 3x slower than
+//    the workgroup-per-pixel one.
+//  * Banks: a half-wave's 32 window cells span ~3 rows of 10; level rows of >= 16 cells are padded
+//    to a stride = 10 (mod 32) so those rows land on disjoint banks (unpadded, a 62-cell row stride
+//    = -2 (mod 32) put them 3-way on the same banks: 25 M conflict cycles per step).
+//  * Write-out: two columns per lane (8-B plane reads, one coarse-level read per pair, 4-B bf16
+//    pair stores) when W is even.
+constexpr int TG = 2;  // iterations per prefetch group
+struct TapGeo {
+  int ps[4];   // padded row stride of each level plane (floats)
+  int off[4];  // offset of each level plane in the wave's slice (floats)
+  int tot4;    // plane floats (16-B multiple)
+  int wave_floats;
+};
+
+TapGeo tap_geo(int H, int W, int levels, int radius) {
+  TapGeo g{};
+  int h = H, w = W, tot = 0;
+  for (int l = 0; l < 4; ++l) {
+    int ps = w;
+    if (w >= 16) {
+      ps = w + ((10 - w) % 32 + 32) % 32;
+    }
+    g.ps[l] = ps;
+    g.off[l] = tot;
+    if (l < levels) tot += ((h * ps + 1) & ~1);  // even: the next level's plane stays 8-B aligned
+    h >>= 1;
+    w >>= 1;
+  }
+  g.tot4 = (tot + 3) & ~3;
+  const int D = 2 * radius + 1;
+  const int trow = (levels * D * D + 7) / 8 * 8;
+  g.wave_floats = g.tot4 + TG * trow / 2;
+  return g;
+}
+
 template <int R>
-__global__ __launch_bounds__(256) void corr_tap_reduce_wave_kernel(TapList tl, int levels, int B, int H,
-                                                                   int W, float inv_sqrt_c,
-                                                                   void* __restrict__ out, int out_bf16,
-                                                                   int wave_bytes) {
+__global__ __launch_bounds__(256) void corr_tap_reduce_wave_kernel(TapList tl, TapGeo tg, int levels, int B,
+                                                                   int H, int W, float inv_sqrt_c,
+                                                                   void* __restrict__ out, int out_bf16) {
   constexpr int D = 2 * R + 1, E = D + 1;
   constexpr int CPL = (4 * E * E + 63) / 64;  // window cells per lane (all levels)
   extern __shared__ float lds_all[];
@@ -641,88 +679,129 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_wave_kernel(TapList tl, i
   const int64_t q = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
   if (q >= (int64_t)B * N) return;  // no workgroup barrier below: waves retire independently
   const int b = (int)(q / N), i = (int)(q - (int64_t)b * N);
-  float* planes = lds_all + wv * (wave_bytes / 4);
-  int hs[4], ws[4], off[4];
-  int tot = 0;
+  float* planes = lds_all + wv * tg.wave_floats;
+  int hs[4], ws[4];
   {
     int h = H, w = W;
     for (int l = 0; l < 4; ++l) {
-      hs[l] = h; ws[l] = w; off[l] = tot;
-      if (l < levels) tot += h * w;
+      hs[l] = h; ws[l] = w;
       h >>= 1; w >>= 1;
     }
   }
-  const int tot4 = (tot + 3) & ~3;
   const int ctot = levels * D * D;
   const int chunks = (ctot + 7) / 8;
   const int trow = chunks * 8;
-  uint16_t* taps = reinterpret_cast<uint16_t*>(planes + tot4);  // [2][trow] double buffer
-  for (int e = lane; e < tot4 / 4; e += 64) reinterpret_cast<uint4*>(planes)[e] = make_uint4(0, 0, 0, 0);
-  int cl[CPL], cyy[CPL], cxx[CPL];
+  uint16_t* taps = reinterpret_cast<uint16_t*>(planes + tg.tot4);  // [TG][trow]
+  const int64_t prow = ((int64_t)b * N + i) * tl.cbuf;
+  const int64_t cix = (int64_t)b * 2 * N + i;
+  // prefetch group 0 before the zero fill
+  uint4 pc[TG];
+  float ncx[TG], ncy[TG];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < TG; ++j) {
+      const int k = min(k0 + j, tl.n - 1);
+      const float* C = tl.coords[k];
+      ncx[j] = C[cix];
+      ncy[j] = C[cix + N];
+      pc[j] = lane < chunks ? *reinterpret_cast<const uint4*>(tl.dout[k] + prow + lane * 8)
+                            : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (tl.n > 0) fetch(0);
+  for (int e = lane; e < tg.tot4 / 4; e += 64) reinterpret_cast<uint4*>(planes)[e] = make_uint4(0, 0, 0, 0);
+  int cbase[CPL], cgy[CPL], cgx[CPL], cps[CPL], cl[CPL];
   float cinv[CPL];
 #pragma unroll
   for (int k = 0; k < CPL; ++k) {
     const int e = lane + k * 64;
-    cl[k] = e < levels * E * E ? e / (E * E) : -1;
-    cyy[k] = (e / E) % E;
-    cxx[k] = e % E;
-    cinv[k] = cl[k] >= 0 ? 1.0f / (float)(1 << cl[k]) : 0.f;
+    const int l = e < levels * E * E ? e / (E * E) : -1;
+    cl[k] = l;
+    const int ll = l < 0 ? 0 : l;
+    cgy[k] = (e / E) % E;
+    cgx[k] = e % E;
+    // (selects, not a dynamic index into the kernel-argument struct)
+    cps[k] = ll == 0 ? tg.ps[0] : ll == 1 ? tg.ps[1] : ll == 2 ? tg.ps[2] : tg.ps[3];
+    cbase[k] = ll == 0 ? tg.off[0] : ll == 1 ? tg.off[1] : ll == 2 ? tg.off[2] : tg.off[3];
+    cinv[k] = 1.0f / (float)(1 << ll);
   }
-  const int64_t prow = ((int64_t)b * N + i) * tl.cbuf;
-  uint4 piece = make_uint4(0, 0, 0, 0);
-  if (lane < chunks) piece = *reinterpret_cast<const uint4*>(tl.dout[0] + prow + lane * 8);
-  for (int k = 0; k < tl.n; ++k) {
-    const float* C = tl.coords[k];
-    const float cx = C[((int64_t)b * 2) * N + i], cy = C[((int64_t)b * 2 + 1) * N + i];
-    uint16_t* T0 = taps + (k & 1) * trow;
-    if (lane < chunks) reinterpret_cast<uint4*>(T0)[lane] = piece;
-    if (k + 1 < tl.n && lane < chunks)
-      piece = *reinterpret_cast<const uint4*>(tl.dout[k + 1] + prow + lane * 8);
+  for (int k0 = 0; k0 < tl.n; k0 += TG) {
+    float cx[TG], cy[TG];
+#pragma unroll
+    for (int j = 0; j < TG; ++j) {
+      if (lane < chunks) reinterpret_cast<uint4*>(taps + j * trow)[lane] = pc[j];
+      cx[j] = ncx[j];
+      cy[j] = ncy[j];
+    }
+    if (k0 + TG < tl.n) fetch(k0 + TG);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-      const int l = cl[c];
-      if (l < 0) continue;
-      const int yy = cyy[c], xx = cxx[c];
-      const float fxc = clampc(cx * cinv[c]), fyc = clampc(cy * cinv[c]);
-      const float flx = floorf(fxc), fly = floorf(fyc);
-      const int gy = (int)fly - R + yy, gx = (int)flx - R + xx;
-      if (gy < 0 || gy >= hs[l] || gx < 0 || gx >= ws[l]) continue;
-      const float ax = fxc - flx, ay = fyc - fly;
-      const uint16_t* T = T0 + l * D * D;
-      float acc = 0.f;
+    for (int j = 0; j < TG; ++j) {
+      if (k0 + j >= tl.n) break;
+      const uint16_t* T0 = taps + j * trow;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int iy = yy - kk;
-        if (iy < 0 || iy >= D) continue;
-        const float wy = kk == 0 ? (1.f - ay) : ay;
-        float sx = 0.f;
-        if (xx < D) sx += (1.f - ax) * raft_bf16_to_f32(T[xx * D + iy]);
-        if (xx > 0) sx += ax * raft_bf16_to_f32(T[(xx - 1) * D + iy]);
-        acc += wy * sx;
+      for (int c = 0; c < CPL; ++c) {
+        const int l = cl[c];
+        if (l < 0) continue;
+        const int yy = cgy[c], xx = cgx[c];
+        const float fxc = clampc(cx[j] * cinv[c]), fyc = clampc(cy[j] * cinv[c]);
+        const float flx = floorf(fxc), fly = floorf(fyc);
+        const int gy = (int)fly - R + yy, gx = (int)flx - R + xx;
+        if (gy < 0 || gy >= (H >> l) || gx < 0 || gx >= (W >> l)) continue;
+        const float ax = fxc - flx, ay = fyc - fly;
+        const uint16_t* T = T0 + l * D * D;
+        float acc = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const int iy = yy - kk;
+          if (iy < 0 || iy >= D) continue;
+          const float wy = kk == 0 ? (1.f - ay) : ay;
+          float sx = 0.f;
+          if (xx < D) sx += (1.f - ax) * raft_bf16_to_f32(T[xx * D + iy]);
+          if (xx > 0) sx += ax * raft_bf16_to_f32(T[(xx - 1) * D + iy]);
+          acc += wy * sx;
+        }
+        planes[cbase[c] + gy * cps[c] + gx] += acc;
       }
-      planes[off[l] + gy * ws[l] + gx] += acc;
     }
     __builtin_amdgcn_wave_barrier();
   }
   const int64_t row = ((int64_t)b * N + i) * N;
   const float inv_w = 1.0f / (float)W;
+  if (out_bf16 && (W & 1) == 0) {
+    // pairs (x, x+1), x even: one coarse-level read serves both columns
+    uint32_t* Ob = reinterpret_cast<uint32_t*>((uint16_t*)out + row);
+    for (int e2 = lane; e2 < N / 2; e2 += 64) {
+      const int e = 2 * e2;
+      const int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W;
+      const float2 p0 = *reinterpret_cast<const float2*>(planes + y * tg.ps[0] + x);
+      float v0 = p0.x, v1 = p0.y;
+      float sc = 0.25f;
+      for (int l = 1; l < levels; ++l) {
+        const int yl = y >> l, xl = x >> l;
+        if (yl < hs[l] && xl < ws[l]) {
+          const float c = sc * planes[tg.off[l] + yl * tg.ps[l] + xl];
+          v0 += c;
+          v1 += c;
+        }
+        sc *= 0.25f;
+      }
+      Ob[e2] = (uint32_t)raft_f32_to_bf16(v0 * inv_sqrt_c) | ((uint32_t)raft_f32_to_bf16(v1 * inv_sqrt_c) << 16);
+    }
+    return;
+  }
   auto cell = [&](int e) {
     const int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W;  // exact for e < 2^22
-    float v = planes[e];
+    float v = planes[y * tg.ps[0] + x];
     float sc = 0.25f;
     for (int l = 1; l < levels; ++l) {
       const int yl = y >> l, xl = x >> l;
-      if (yl < hs[l] && xl < ws[l]) v += sc * planes[off[l] + yl * ws[l] + xl];
+      if (yl < hs[l] && xl < ws[l]) v += sc * planes[tg.off[l] + yl * tg.ps[l] + xl];
       sc *= 0.25f;
     }
     return v * inv_sqrt_c;
   };
-  if (out_bf16 && (N & 1) == 0) {
-    uint32_t* Ob = reinterpret_cast<uint32_t*>((uint16_t*)out + row);
-    for (int e2 = lane; e2 < N / 2; e2 += 64)
-      Ob[e2] = (uint32_t)raft_f32_to_bf16(cell(2 * e2)) | ((uint32_t)raft_f32_to_bf16(cell(2 * e2 + 1)) << 16);
-  } else if (out_bf16) {
+  if (out_bf16) {
     uint16_t* Ob = (uint16_t*)out + row;
     for (int e = lane; e < N; e += 64) Ob[e] = raft_f32_to_bf16(cell(e));
   } else {
@@ -816,17 +895,23 @@ bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, 
     return e && e[0] == '1';
   }();
   if (!v1 && (radius == 4 || radius == 3)) {
-    // one wave per query pixel: its level planes + a double-buffered tap row in its LDS slice
-    int tot = 0, h = H, w = W;
-    for (int l = 0; l < levels; ++l) { tot += h * w; h >>= 1; w >>= 1; }
-    const int trow = (levels * D * D + 7) / 8 * 8;
-    const int wave_bytes = (((tot + 3) & ~3) * 4 + 2 * trow * 2 + 15) & ~15;
-    const int wpb = std::max(1, std::min(4, (64 * 1024) / wave_bytes));
+    // one wave per query pixel: its (padded) level planes + TG staged tap rows in its LDS slice;
+    // waves per workgroup chosen for the most resident waves per CU (160 KB, <= 64 KB a group)
+    const TapGeo tg = tap_geo(H, W, levels, radius);
+    const int wave_bytes = tg.wave_floats * 4;
+    int wpb = 1, best = 0;
+    for (int c = 1; c <= 4; ++c) {
+      if (c * wave_bytes > 64 * 1024) break;
+      const int waves = c * ((160 * 1024) / (c * wave_bytes));
+      if (waves >= best) { best = waves; wpb = c; }
+    }
     const int64_t P = (int64_t)B * H * W;
     dim3 grid((unsigned)((P + wpb - 1) / wpb));
-    if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<4>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, wave_bytes);
-    else hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<3>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, wave_bytes);
-    return true;
+    if (best == 0) {
+      // planes past 64 KB: the workgroup-per-pixel kernel below
+    } else if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<4>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, tg, levels, B, H, W, inv_sqrt_c, out, out_bf16);
+    else hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<3>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, tg, levels, B, H, W, inv_sqrt_c, out, out_bf16);
+    if (best > 0) return true;
   }
   const int lds = corr_tap_reduce_lds_bytes(H, W, levels, radius);
   dim3 grid((unsigned)(B * H * W));

@@ -44,7 +44,10 @@ def test_hip_training_grads_match_torch(ext_ops):
         grads[impl] = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
     a, b = grads['torch'], grads['hip']
     rel = (a - b).norm() / a.norm()
-    assert rel < 1e-3, rel
+    # fp32 model: the HIP path runs the update block AND the encoders' stride-1 convs as split-bf16
+    # products (~4e-6 per conv); the encoders' early-layer gradients amplify a forward
+    # perturbation of that size ~1000x even in fp64 (profiles/r4/fp32_encoder_conditioning.txt)
+    assert rel < 3e-3, rel
 
 
 def test_train_step_bf16_runs(ext_ops):
