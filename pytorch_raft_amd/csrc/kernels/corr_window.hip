@@ -624,7 +624,7 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
   }
 }
 
-// Wave-per-query-pixel fold (the launcher's default): the same per-cell arithmetic and iteration
+// Wave-per-query-pixel fold (opt-in, RAFT_TAPRED_WAVE=1): the same per-cell arithmetic and iteration
 // order as corr_tap_reduce_kernel (bitwise the same dC), but each WAVE owns one query pixel's
 // level planes in its own LDS slice, so there is no workgroup barrier at all: a wave's LDS
 // operations execute in issue order, which orders the iterations' read-modify-writes and makes
@@ -890,11 +890,14 @@ bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, 
                             float inv_sqrt_c, void* out, int out_bf16, hipStream_t stream) {
   const int D = 2 * radius + 1;
   if ((levels * D * D + 7) / 8 * 6 > 256) return false;  // one 16-B piece per thread per chunk
-  static const bool v1 = [] {
-    const char* e = getenv("RAFT_TAPRED_V1");
+  // the wave-per-pixel kernel holds 2 waves per SIMD (20 KB of planes per wave) and measured
+  // 684 vs 532 us for the workgroup-per-pixel kernel at the chairs shape
+  // (profiles/r4/tapred_variants.txt): opt-in with RAFT_TAPRED_WAVE=1
+  static const bool wave = [] {
+    const char* e = getenv("RAFT_TAPRED_WAVE");
     return e && e[0] == '1';
   }();
-  if (!v1 && (radius == 4 || radius == 3)) {
+  if (wave && (radius == 4 || radius == 3)) {
     // one wave per query pixel: its (padded) level planes + TG staged tap rows in its LDS slice;
     // waves per workgroup chosen for the most resident waves per CU (160 KB, <= 64 KB a group)
     const TapGeo tg = tap_geo(H, W, levels, radius);

@@ -1,6 +1,6 @@
 """Time the correlation fold (corr_tap_reduce: tap gradients of every iteration -> dense bf16 dC)
 at the chairs training shape (B=12, 46x62, 4 levels, r=4, 12 iterations).  The kernel variant
-follows RAFT_TAPRED_V1 (1 = workgroup per pixel, default = wave per pixel); prints us per call
+follows RAFT_TAPRED_WAVE (1 = wave per pixel, default = workgroup per pixel); prints us per call
 and a checksum so the variants can be compared bit for bit."""
 import sys
 
