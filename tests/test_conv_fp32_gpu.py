@@ -144,53 +144,79 @@ def test_fp32_training_trajectory_split_vs_miopen(ext_ops):
             assert _rel(wa[n], wb[n]) < (2e-3 if wb[n].dim() > 1 else 1e-2), n
 
 
+def _emulated_split_conv(x, w, b, pad):
+    """fp64 emulation of the split-bf16 forward (3 products of bf16-rounded hi / lo parts)."""
+    def bf(t):
+        return t.float().to(torch.bfloat16).double()
+    xh, wh = bf(x), bf(w)
+    xl, wl = bf(x - xh), bf(w - wh)
+    y = (F.conv2d(xh, wh, None, padding=pad) + F.conv2d(xl, wh, None, padding=pad) +
+         F.conv2d(xh, wl, None, padding=pad))
+    return y + b.view(1, -1, 1, 1)
+
+
+class _EmuSplit(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, pad):
+        ctx.save_for_backward(x, w)
+        ctx.pad = pad
+        return _emulated_split_conv(x, w, b, pad)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        return (torch.nn.grad.conv2d_input(x.shape, w, g, padding=ctx.pad),
+                torch.nn.grad.conv2d_weight(x, w.shape, g, padding=ctx.pad), g.sum((0, 2, 3)), None)
+
+
 @pytest.mark.parametrize('norm', ['instance', 'batch'])
 def test_fp32_encoder_split_vs_fp64(ext_ops, norm):
     """fp32 BasicEncoder (fnet: instance norm, cnet: batch norm): with ``conv_fp32.enabled()`` its
     stride-1 convs (12 of 15) run as split-bf16 MFMA products.  Output, input gradient and every
     parameter gradient are compared with an fp64 CPU run of the same module.
 
-    The encoder's gradients at init are ill-conditioned in the FORWARD activations: 4e-6 relative
-    noise on the stride-1 conv outputs moves the input gradient by ~6e-3 in exact arithmetic
-    (profiles/r4/fp32_encoder_conditioning.txt), while each split conv is at ~4e-6 given the
-    gradient it receives.  So the bound per tensor is 4x the larger of MIOpen fp32's own error and
-    that fp64 sensitivity (measured here for the same module and inputs); the output itself must
-    stay within 1e-4."""
+    The encoder's gradients at init are very sensitive to the forward's rounding: the split-bf16
+    forward ALONE, emulated in fp64 with exact backward convs, moves the input gradient by ~7e-3
+    (an fp32 forward by ~2e-7; profiles/r4/fp32_encoder_conditioning.txt), while every split conv
+    is at ~4e-6 given the gradient it receives.  So the GPU run is bounded per tensor by 3x the
+    larger of MIOpen fp32's error and that emulation's (computed here for the same module and
+    inputs): the kernels implement the scheme, the scheme's own sensitivity is documented.  The
+    output itself must stay within 1e-4."""
     import copy
+    from pytorch_raft_amd.models import update as U
     from pytorch_raft_amd.models.extractor import BasicEncoder
     torch.manual_seed(0)
     enc = BasicEncoder(output_dim=256, norm_fn=norm).to(DEV).train()
     x0 = torch.randn(3, 3, 96, 128, device=DEV)
     gout = torch.randn(3, 256, 12, 16, device=DEV)
 
-    def run(m, x, g, on=False, noise=0.0):
+    def run(m, x, g, on=False, emulate=False):
         m.zero_grad(set_to_none=True)
         x = x.clone().requires_grad_(True)
-        hooks = []
-        if noise:
-            gen = torch.Generator().manual_seed(5)
-
-            def fh(mod, inp, out):
-                return out + noise * out.abs().mean() * torch.randn(out.shape, generator=gen,
-                                                                    dtype=out.dtype)
-            hooks = [mm.register_forward_hook(fh) for mm in m.modules()
-                     if isinstance(mm, torch.nn.Conv2d) and mm.stride == (1, 1)]
-        with conv_fp32.enabled(on):
-            y = m(x)
+        orig = U.MfmaConv2d.forward
+        if emulate:
+            def fwd(self, xx):
+                if self.stride == (1, 1):
+                    return _EmuSplit.apply(xx, self.weight, self.bias, self.padding)
+                return torch.nn.Conv2d.forward(self, xx)
+            U.MfmaConv2d.forward = fwd
+        try:
+            with conv_fp32.enabled(on):
+                y = m(x)
+        finally:
+            U.MfmaConv2d.forward = orig
         (y * g).sum().backward()
-        for h in hooks:
-            h.remove()
         return {'out': y.detach().double().cpu(), 'dx': x.grad.detach().double().cpu(),
                 **{n: p.grad.detach().double().cpu() for n, p in m.named_parameters()}}
 
     m64 = copy.deepcopy(enc).double().cpu()
     ref = run(m64, x0.double().cpu(), gout.double().cpu())
-    pert = run(m64, x0.double().cpu(), gout.double().cpu(), noise=4e-6)
+    emu = run(m64, x0.double().cpu(), gout.double().cpu(), emulate=True)
     split = run(enc, x0, gout, True)
     miop = run(enc, x0, gout, False)
     assert _rel(split['out'], ref['out']) < 1e-4
     for n in ref:
         if n.endswith('.bias') and n != 'conv2.bias' and ('conv' in n or 'downsample.0' in n):
             continue   # a conv bias feeding a norm has an exactly-zero gradient (rounding noise)
-        es, em, ec = _rel(split[n], ref[n]), _rel(miop[n], ref[n]), _rel(pert[n], ref[n])
-        assert es <= 4 * max(em, ec) + 3e-5, (n, es, em, ec)
+        es, em, ee = _rel(split[n], ref[n]), _rel(miop[n], ref[n]), _rel(emu[n], ref[n])
+        assert es <= 3 * max(em, ee) + 3e-5, (n, es, em, ee)
