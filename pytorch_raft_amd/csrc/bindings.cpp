@@ -1421,8 +1421,11 @@ Tensor corr_tap_reduce(const std::vector<Tensor>& coords, const std::vector<Tens
   TORCH_CHECK(lds <= 64 * 1024, "feature map too large for the LDS plane reduction");
   c10::DeviceGuard g(coords[0].device());
   Tensor out = at::empty({B, N, N}, coords[0].options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  // overflow list of the union-box fold (count + pixel indices)
+  Tensor list = at::empty({1 + B * N}, coords[0].options().dtype(at::kInt));
   TORCH_CHECK(launch_corr_tap_reduce(tl, (int)levels, (int)B, (int)H, (int)W, (int)radius,
-                                     (float)inv_sqrt_c, out.data_ptr(), out_bf16 ? 1 : 0, cur_stream()),
+                                     (float)inv_sqrt_c, out.data_ptr(), out_bf16 ? 1 : 0,
+                                     list.data_ptr<int>(), cur_stream()),
               "unsupported radius / levels");
   return out;
 }

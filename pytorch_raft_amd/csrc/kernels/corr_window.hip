@@ -513,13 +513,19 @@ __global__ __launch_bounds__(256) void corr_window_reduce_kernel(WinList wl_, in
 template <int R>
 __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int levels, int B, int H,
                                                               int W, float inv_sqrt_c,
-                                                              void* __restrict__ out, int out_bf16) {
+                                                              void* __restrict__ out, int out_bf16,
+                                                              const int* __restrict__ list) {
   constexpr int D = 2 * R + 1, E = D + 1;
   constexpr int KC = 6;
   constexpr int CPT = (4 * E * E + 255) / 256;
   extern __shared__ float planes[];
   const int N = H * W;
-  const int b = blockIdx.x / N, i = blockIdx.x % N;
+  // list != nullptr: the pixels the box kernel could not take (list[0] = count, then the pixel
+  // indices), grid-strided; otherwise one pixel per workgroup
+  const int nitems = list != nullptr ? list[0] : B * N;
+  for (int w = blockIdx.x; w < nitems; w += (list != nullptr ? gridDim.x : nitems)) {
+  const int q = list != nullptr ? list[1 + w] : w;
+  const int b = q / N, i = q % N;
   int hs[4], ws[4], off[4];
   int tot = 0;
   {
@@ -622,9 +628,11 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
     float* O = (float*)out + row;
     for (int e = threadIdx.x; e < N; e += 256) O[e] = cell(e);
   }
+  __syncthreads();  // the next listed pixel reuses the planes
+  }
 }
 
-// Wave-per-query-pixel fold (opt-in, RAFT_TAPRED_WAVE=1): the same per-cell arithmetic and iteration
+// Wave-per-query-pixel fold (opt-in, RAFT_TAPRED=2): the same per-cell arithmetic and iteration
 // order as corr_tap_reduce_kernel (bitwise the same dC), but each WAVE owns one query pixel's
 // level planes in its own LDS slice, so there is no workgroup barrier at all: a wave's LDS
 // operations execute in issue order, which orders the iterations' read-modify-writes and makes
@@ -810,6 +818,216 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_wave_kernel(TapList tl, T
   }
 }
 
+
+// Union-box fold (the launcher's default, W even): one WAVE per query pixel whose level planes
+// are held only over the union box of its windows across the step's iterations (<= 24 x 24 cells
+// per level: 5.4 KB per wave at chairs instead of the full 15 KB planes, ~5 waves per SIMD), so
+// the zero fill and the LDS footprint shrink and the write-out reads the boxes.
+//  * fold: lane = (level, window column rx) in 16-lane rows; a lane takes its tap column from the
+//    staged tap row (5 dword reads), the column to its left from lane - 1 (DPP row shift), and
+//    adds its 2r+2 window cells (x- then y-interpolated, the same bilinear adjoint as the other
+//    folds) down the column: ~2.5 LDS operations per cell instead of 6.
+//  * iterations in order, one writer per cell and iteration, waves never share planes: no
+//    barrier, deterministic.
+//  * a pixel whose windows spread past a 24 x 24 box at some level is appended to `list` and
+//    folded afterwards by corr_tap_reduce_kernel (list mode).
+constexpr int BOXC = 24;   // box side cap (cells)
+struct BoxGeo {
+  int cap[4];    // floats reserved per level box
+  int off[4];
+  int wave_floats;
+};
+
+BoxGeo box_geo(int H, int W, int levels, int radius) {
+  BoxGeo g{};
+  int h = H, w = W, tot = 0;
+  for (int l = 0; l < 4; ++l) {
+    const int c = l < levels ? (std::min(BOXC * BOXC, h * w) + 3) & ~3 : 0;
+    g.cap[l] = c;
+    g.off[l] = tot;
+    tot += c;
+    h >>= 1;
+    w >>= 1;
+  }
+  const int D = 2 * radius + 1;
+  const int trow = (levels * D * D + 7) / 8 * 8;
+  g.wave_floats = tot + 2 * trow / 2;
+  return g;
+}
+
+template <int R>
+__global__ __launch_bounds__(256) void corr_tap_fold_box_kernel(TapList tl, BoxGeo bg, int levels, int B,
+                                                                int H, int W, float inv_sqrt_c,
+                                                                uint16_t* __restrict__ out, int* __restrict__ list) {
+  constexpr int D = 2 * R + 1, E = D + 1;
+  extern __shared__ float lds_all[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int N = H * W;
+  const int q = blockIdx.x * (blockDim.x >> 6) + wv;
+  if (q >= B * N) return;  // no workgroup barrier below
+  const int b = q / N, i = q - b * N;
+  float* box = lds_all + wv * bg.wave_floats;
+  const int ctot = levels * D * D;
+  const int chunks = (ctot + 7) / 8;
+  const int trow = chunks * 8;
+  uint16_t* taps = reinterpret_cast<uint16_t*>(box + (bg.wave_floats - trow));  // [2][trow]
+  const int n = tl.n;
+  const int64_t prow = ((int64_t)b * N + i) * tl.cbuf;
+  // iteration k's coordinates in lane k (k < n <= 32)
+  float cxv = 0.f, cyv = 0.f;
+  if (lane < n) {
+    const float* C = tl.coords[lane];
+    cxv = C[(int64_t)b * 2 * N + i];
+    cyv = C[(int64_t)b * 2 * N + N + i];
+  }
+  // tap rows of the next BPF iterations in flight (registers) while one is folded
+  constexpr int BPF = 4;
+  uint4 piece[BPF];
+#pragma unroll
+  for (int j = 0; j < BPF; ++j)
+    piece[j] = (lane < chunks && j < n) ? *reinterpret_cast<const uint4*>(tl.dout[j] + prow + lane * 8)
+                                        : make_uint4(0, 0, 0, 0);
+  // this lane's level / column and its level's plane
+  const int ll = lane >> 4, rx = lane & 15;
+  const bool lact = ll < levels;
+  const int hl = H >> ll, wl = W >> ll;
+  const float inv = 1.0f / (float)(1 << ll);
+  // union box of the level's windows (every lane of the level computes the same box)
+  int mnx = 0x7fffffff, mxx = -0x7fffffff, mny = 0x7fffffff, mxy = -0x7fffffff;
+  for (int k = 0; k < n; ++k) {
+    const float cx = clampc(__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxv), k)) * inv);
+    const float cy = clampc(__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cyv), k)) * inv);
+    const int x0 = (int)floorf(cx) - R, y0 = (int)floorf(cy) - R;
+    if (x0 <= wl - 1 && x0 + E - 1 >= 0 && y0 <= hl - 1 && y0 + E - 1 >= 0) {
+      mnx = min(mnx, x0);
+      mxx = max(mxx, x0 + E - 1);
+      mny = min(mny, y0);
+      mxy = max(mxy, y0 + E - 1);
+    }
+  }
+  int bx0 = max(mnx, 0), by0 = max(mny, 0);
+  const int bx1 = min(mxx, wl - 1), by1 = min(mxy, hl - 1);
+  if (ll == 0) bx0 &= ~1;  // level 0: even origin and width -> 8-B pair reads in the write-out
+  int bw = bx1 >= bx0 ? bx1 - bx0 + 1 : 0, bh = by1 >= by0 ? by1 - by0 + 1 : 0;
+  if (ll == 0) bw = (bw + 1) & ~1;
+  if (bw == 0 || bh == 0) bw = bh = 0;
+  const bool over = lact && (bw > BOXC || bh > BOXC);
+  if (__builtin_amdgcn_read_exec() & __ballot(over)) {
+    if (lane == 0) {
+      const int slot = atomicAdd(list, 1);
+      list[1 + slot] = q;
+    }
+    return;
+  }
+  // level boxes' geometry from their lanes (uniform); zero only the boxes' cells
+  int gbx[4], gby[4], gbw[4], gbh[4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    gbx[l] = __builtin_amdgcn_readlane(bx0, l * 16);
+    gby[l] = __builtin_amdgcn_readlane(by0, l * 16);
+    gbw[l] = __builtin_amdgcn_readlane(bw, l * 16);
+    gbh[l] = __builtin_amdgcn_readlane(bh, l * 16);
+  }
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    if (l >= levels) break;
+    const int n4 = (gbw[l] * gbh[l] + 3) >> 2;  // <= cap / 4 (caps are multiples of 4)
+    uint4* z = reinterpret_cast<uint4*>(box + bg.off[l]);
+    for (int e = lane; e < n4; e += 64) z[e] = make_uint4(0, 0, 0, 0);
+  }
+  float* mybox = box + (ll == 0 ? bg.off[0] : ll == 1 ? bg.off[1] : ll == 2 ? bg.off[2] : bg.off[3]);
+  const bool colact = lact && rx < E;
+  for (int k0 = 0; k0 < n; k0 += BPF) {
+#pragma unroll
+  for (int j = 0; j < BPF; ++j) {
+    const int k = k0 + j;
+    if (k >= n) break;
+    uint16_t* T0 = taps + (k & 1) * trow;
+    if (lane < chunks) reinterpret_cast<uint4*>(T0)[lane] = piece[j];
+    if (k + BPF < n && lane < chunks)
+      piece[j] = *reinterpret_cast<const uint4*>(tl.dout[k + BPF] + prow + lane * 8);
+    __builtin_amdgcn_wave_barrier();
+    const float cx = clampc(__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cxv), k)) * inv);
+    const float cy = clampc(__builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cyv), k)) * inv);
+    const float flx = floorf(cx), fly = floorf(cy);
+    const float ax = cx - flx, ay = cy - fly;
+    const int gx = (int)flx - R + rx, gy0 = (int)fly - R;
+    // tap column rx (zero past the last tap column) -> fp32, 9 values
+    float tc[D];
+    {
+      const int start = (lact ? ll : 0) * D * D + min(rx, D - 1) * D;
+      const uint32_t* Tw = reinterpret_cast<const uint32_t*>(T0) + (start >> 1);
+      uint32_t wd[(D + 2) / 2];
+#pragma unroll
+      for (int u = 0; u < (D + 2) / 2; ++u) wd[u] = Tw[u];
+      const int sh = start & 1;
+#pragma unroll
+      for (int t = 0; t < D; ++t) {
+        const int idx = t + sh;
+        const uint32_t h16 = (wd[idx >> 1] >> ((idx & 1) * 16)) & 0xffffu;
+        tc[t] = (rx < D) ? raft_bf16_to_f32((uint16_t)h16) : 0.f;
+      }
+    }
+    // the column to the left (lane - 1 of the same 16-lane row; zero for rx = 0)
+    float tl_[D];
+#pragma unroll
+    for (int t = 0; t < D; ++t)
+      tl_[t] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, tc[t]),
+                                                                      0x111, 0xf, 0xf, false));
+    if (colact && gx >= bx0 && gx < bx0 + bw) {
+      float hx[D];
+#pragma unroll
+      for (int t = 0; t < D; ++t) {
+        float sx = 0.f;
+        if (rx < D) sx += (1.f - ax) * tc[t];
+        if (rx > 0) sx += ax * tl_[t];
+        hx[t] = sx;
+      }
+      float* colp = mybox + (gx - bx0);
+#pragma unroll
+      for (int ry = 0; ry < E; ++ry) {
+        const int gy = gy0 + ry;
+        if (gy < by0 || gy >= by0 + bh) continue;
+        float acc = 0.f;
+        if (ry < D) acc += (1.f - ay) * hx[ry];
+        if (ry > 0) acc += ay * hx[ry - 1];
+        colp[(gy - by0) * bw] += acc;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  }
+  uint32_t* Ob = reinterpret_cast<uint32_t*>(out + ((int64_t)b * N + i) * N);
+  const float inv_w = 1.0f / (float)W;
+  for (int e2 = lane; e2 < N / 2; e2 += 64) {
+    const int e = 2 * e2;
+    const int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W;
+    float v0 = 0.f, v1 = 0.f;
+    {
+      const int yy = y - gby[0], xx = x - gbx[0];
+      if ((unsigned)yy < (unsigned)gbh[0] && (unsigned)xx < (unsigned)gbw[0]) {
+        const float2 p = *reinterpret_cast<const float2*>(box + bg.off[0] + yy * gbw[0] + xx);
+        v0 = p.x;
+        v1 = p.y;
+      }
+    }
+    float sc = 0.25f;
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+      if (l < levels) {
+        const int yy = (y >> l) - gby[l], xx = (x >> l) - gbx[l];
+        if ((unsigned)yy < (unsigned)gbh[l] && (unsigned)xx < (unsigned)gbw[l]) {
+          const float c = sc * box[bg.off[l] + yy * gbw[l] + xx];
+          v0 += c;
+          v1 += c;
+        }
+      }
+      sc *= 0.25f;
+    }
+    Ob[e2] = (uint32_t)raft_f32_to_bf16(v0 * inv_sqrt_c) | ((uint32_t)raft_f32_to_bf16(v1 * inv_sqrt_c) << 16);
+  }
+}
+
 }  // namespace
 
 bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* ws, int levels,
@@ -887,17 +1105,32 @@ int corr_tap_reduce_lds_bytes(int H, int W, int levels, int radius) {
 }
 
 bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, int radius,
-                            float inv_sqrt_c, void* out, int out_bf16, hipStream_t stream) {
+                            float inv_sqrt_c, void* out, int out_bf16, int* list, hipStream_t stream) {
   const int D = 2 * radius + 1;
   if ((levels * D * D + 7) / 8 * 6 > 256) return false;  // one 16-B piece per thread per chunk
-  // the wave-per-pixel kernel holds 2 waves per SIMD (20 KB of planes per wave) and measured
-  // 684 vs 532 us for the workgroup-per-pixel kernel at the chairs shape
-  // (profiles/r4/tapred_variants.txt): opt-in with RAFT_TAPRED_WAVE=1
-  static const bool wave = [] {
-    const char* e = getenv("RAFT_TAPRED_WAVE");
-    return e && e[0] == '1';
+  if (radius != 3 && radius != 4) return false;
+  static const int mode = [] {  // 0 = box (default), 1 = workgroup per pixel, 2 = wave per pixel
+    const char* e = getenv("RAFT_TAPRED");
+    return e ? atoi(e) : 0;
   }();
-  if (wave && (radius == 4 || radius == 3)) {
+  const int64_t P = (int64_t)B * H * W;
+  const int lds = corr_tap_reduce_lds_bytes(H, W, levels, radius);
+  if (mode == 0 && out_bf16 && (W & 1) == 0 && list != nullptr && tl.n <= 32 &&
+      (levels * D * D + 7) / 8 <= 64) {
+    const BoxGeo bg = box_geo(H, W, levels, radius);
+    const int wpb = 4;
+    (void)hipMemsetAsync(list, 0, sizeof(int), stream);
+    dim3 grid((unsigned)((P + wpb - 1) / wpb));
+    const size_t sh = (size_t)wpb * bg.wave_floats * 4;
+    if (radius == 4) hipLaunchKernelGGL(corr_tap_fold_box_kernel<4>, grid, dim3(64 * wpb), sh, stream, tl, bg, levels, B, H, W, inv_sqrt_c, (uint16_t*)out, list);
+    else hipLaunchKernelGGL(corr_tap_fold_box_kernel<3>, grid, dim3(64 * wpb), sh, stream, tl, bg, levels, B, H, W, inv_sqrt_c, (uint16_t*)out, list);
+    // the pixels whose windows spread past the box cap (usually none): grid-strided over the list
+    dim3 g2((unsigned)std::min<int64_t>(P, 1024));
+    if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_kernel<4>, g2, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)list);
+    else hipLaunchKernelGGL(corr_tap_reduce_kernel<3>, g2, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)list);
+    return true;
+  }
+  if (mode == 2) {
     // one wave per query pixel: its (padded) level planes + TG staged tap rows in its LDS slice;
     // waves per workgroup chosen for the most resident waves per CU (160 KB, <= 64 KB a group)
     const TapGeo tg = tap_geo(H, W, levels, radius);
@@ -908,18 +1141,15 @@ bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, 
       const int waves = c * ((160 * 1024) / (c * wave_bytes));
       if (waves >= best) { best = waves; wpb = c; }
     }
-    const int64_t P = (int64_t)B * H * W;
-    dim3 grid((unsigned)((P + wpb - 1) / wpb));
-    if (best == 0) {
-      // planes past 64 KB: the workgroup-per-pixel kernel below
-    } else if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<4>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, tg, levels, B, H, W, inv_sqrt_c, out, out_bf16);
-    else hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<3>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, tg, levels, B, H, W, inv_sqrt_c, out, out_bf16);
-    if (best > 0) return true;
+    if (best > 0) {
+      dim3 grid((unsigned)((P + wpb - 1) / wpb));
+      if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<4>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, tg, levels, B, H, W, inv_sqrt_c, out, out_bf16);
+      else hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<3>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, tg, levels, B, H, W, inv_sqrt_c, out, out_bf16);
+      return true;
+    }
   }
-  const int lds = corr_tap_reduce_lds_bytes(H, W, levels, radius);
-  dim3 grid((unsigned)(B * H * W));
-  if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_kernel<4>, grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16);
-  else if (radius == 3) hipLaunchKernelGGL(corr_tap_reduce_kernel<3>, grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16);
-  else return false;
+  dim3 grid((unsigned)P);
+  if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_kernel<4>, grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)nullptr);
+  else hipLaunchKernelGGL(corr_tap_reduce_kernel<3>, grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)nullptr);
   return true;
 }

@@ -296,8 +296,9 @@ struct TapList {
   int n;
 };
 int corr_tap_reduce_lds_bytes(int H, int W, int levels, int radius);
+// list: (1 + B*H*W) ints of scratch for the box fold's overflow list (nullptr: no box fold)
 bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, int radius,
-                            float inv_sqrt_c, void* out, int out_bf16, hipStream_t stream);
+                            float inv_sqrt_c, void* out, int out_bf16, int* list, hipStream_t stream);
 int corr_window_reduce_lds_bytes(int H, int W, int levels);
 // out: (B, N, N) fp32, or bf16 when out_bf16 (mixed-precision backward GEMMs)
 bool launch_corr_window_reduce(const WinList& wl, int levels, int B, int H, int W, int radius,

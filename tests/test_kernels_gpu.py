@@ -387,6 +387,33 @@ def test_tap_reduce_matches_window_path(ext_ops, radius, levels, hw):
     assert torch.equal(ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, False), got)
 
 
+@pytest.mark.parametrize('radius,levels,hw,drift', [(4, 4, (46, 62), 0.7), (3, 4, (24, 32), 0.7),
+                                                     (4, 3, (14, 20), 0.7), (4, 4, (46, 62), 3.0)])
+def test_tap_reduce_box_path(ext_ops, radius, levels, hw, drift):
+    """Union-box fold (the default for bf16 dC at even W): windows that drift a little per
+    iteration (the training case) fit the 24 x 24 boxes; drift 3.0 pushes some pixels past the cap
+    onto the listed workgroup-per-pixel fold.  Both == the window path up to the bf16 output
+    rounding, and bitwise reproducible."""
+    h, w = hw
+    b = 2
+    g = torch.Generator(device='cpu').manual_seed(4)
+    ys, xs = torch.meshgrid(torch.arange(h).float(), torch.arange(w).float(), indexing='ij')
+    c = torch.stack([xs, ys])[None].repeat(b, 1, 1, 1) + 4 * torch.randn(b, 2, h, w, generator=g)
+    coords = []
+    for _ in range(12):
+        c = c + drift * torch.randn(b, 2, h, w, generator=g)
+        coords.append(c.clone().to(DEV))
+    coords[3][:, :, 0, 0] = -50.0      # one iteration's window leaves the map
+    douts = [torch.randn(b, h, w, 384, device=DEV).to(torch.bfloat16) for _ in coords]
+    s = 1.0 / 16
+    wgs = [ext_ops.corr_window_grad(cc, gg, levels, radius) for cc, gg in zip(coords, douts)]
+    ref = ext_ops.corr_window_reduce(coords, wgs, h, w, levels, radius, s, False)
+    got = ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, True)
+    err = (got.float() - ref).abs()
+    assert (err <= ref.abs() * 2.0 ** -8 + 1e-6).all(), err.max().item()
+    assert torch.equal(ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, True), got)
+
+
 @pytest.mark.parametrize('convention', ['reference', 'exact'])
 @pytest.mark.parametrize('shape', [(1, 3, 37, 53), (2, 3, 64, 96)])
 def test_warp_sampler_matches_grid_sample(ext_ops, convention, shape):
