@@ -374,7 +374,7 @@ struct OtfSlabs {
 
 void corr_otf_bwd_(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor& coords,
                    const Tensor& dout, const Tensor& df1, const std::vector<Tensor>& df2,
-                   int64_t radius) {
+                   int64_t radius, int64_t dslo) {
   otf_common_checks(f1, coords, radius);
   const int64_t B = f1.size(0), H = f1.size(1), W = f1.size(2), C = f1.size(3);
   check_cuda_f32(df1, "grad_fmap1");
@@ -401,7 +401,8 @@ void corr_otf_bwd_(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor
                                   coords.data_ptr<float>(), dout.data_ptr(),
                                   dout.scalar_type() == at::kBFloat16, (int)dout.size(3),
                                   df1.data_ptr<float>(), gp.data(), (int)B, (int)C, (int)H, (int)W,
-                                  (int)radius, sl.slab(), sl.caps(), sl.box(), cur_stream()),
+                                  (int)radius, sl.slab(), sl.caps(), sl.box(), (int)dslo,
+                                  cur_stream()),
               "on-the-fly corr supports radius 3/4 with C = 128/256");
 }
 
@@ -1529,7 +1530,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_lookup_bwd_(Tensor(a!)[] gpyr, Tensor coords, Tensor dout, int radius) -> ()");
   m.def("corr_pyr_grad_reduce(Tensor[] gpyr, float inv_sqrt_c) -> Tensor");
   m.def("corr_otf_fwd_(Tensor f1, Tensor[] f2, Tensor coords, int radius, Tensor(a!) out, Tensor[] lo) -> ()");
-  m.def("corr_otf_bwd_(Tensor f1, Tensor[] f2, Tensor coords, Tensor dout, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
+  m.def("corr_otf_bwd_(Tensor f1, Tensor[] f2, Tensor coords, Tensor dout, Tensor(a!) df1, Tensor(b!)[] df2, int radius, int dslo=0) -> ()");
   m.def("conv_tune_table() -> int[]", &conv_tune_table);
   m.def("conv_set_forced_cfg(int idx) -> ()", [](int64_t idx) { conv_set_forced_cfg((int)idx); });
   m.def("conv_set_autotune(int mode) -> ()", [](int64_t mode) { conv_set_autotune((int)mode); });

@@ -49,6 +49,9 @@ struct OtfLvls {
   float* slab[4];
   int cap[4];
   int* boxes;
+  // 1: the dS operand is the bf16 RESIDUAL of the window gradient, v - bf16(v) (the fp32-accurate
+  // backward: passes (dS_hi, F_hi) + (dS_lo, F_hi) + (dS_hi, F_lo) accumulate into the gradients)
+  int dslo;
 };
 
 __device__ __forceinline__ float clampc(float v) { return fminf(fmaxf(v, -1.0e6f), 1.0e6f); }
@@ -571,6 +574,7 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
               v = dwin[p * NP + ry * E + rx];
           }
         }
+        if (lv.dslo) v -= raft_bf16_to_f32(raft_f32_to_bf16(v));
         dS[p * SS + n] = raft_f32_to_bf16(v);
       }
       __syncthreads();
@@ -659,6 +663,7 @@ OtfLvls make_lvls(const uint16_t* const* f2, float* const* g2, const int* hs, co
     p.cap[l] = 0;
   }
   p.boxes = nullptr;
+  p.dslo = 0;
   return p;
 }
 
@@ -758,9 +763,10 @@ bool launch_corr_otf_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
                          const int* ws, int levels, const float* coords, const void* dout,
                          int dout_bf16, int dstride, float* df1, float* const* df2lvl, int B,
                          int C, int H, int W, int radius, float* const* slab, const int* cap,
-                         int* boxes, hipStream_t stream) {
+                         int* boxes, int dslo, hipStream_t stream) {
   if (!((radius == 4 || radius == 3) && (C == 128 || C == 256))) return false;
   OtfLvls p = make_lvls(f2lvl, df2lvl, hs, ws, levels);
+  p.dslo = dslo;
   if (slab != nullptr) {
     for (int l = 0; l < levels; ++l) {
       p.slab[l] = slab[l];

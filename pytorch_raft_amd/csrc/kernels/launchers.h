@@ -40,7 +40,7 @@ bool launch_corr_otf_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
                          const int* ws, int levels, const float* coords, const void* dout,
                          int dout_bf16, int dstride, float* df1, float* const* df2lvl, int B,
                          int C, int H, int W, int radius, float* const* slab, const int* cap,
-                         int* boxes, hipStream_t stream);
+                         int* boxes, int dslo, hipStream_t stream);
 
 // all iterations of a step at once from compact window gradients (see corr_window.hip)
 struct WinList;

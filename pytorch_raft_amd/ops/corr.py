@@ -258,7 +258,17 @@ def _otf_backward(st, coords, dout, radius):
     _otf_alloc_grads(st)
     if dout.dtype not in (torch.float32, torch.bfloat16):
         dout = dout.float()
-    _ext.ops().corr_otf_bwd_(st.f1, st.f2, coords, dout.contiguous(), st.grad_f1, st.grad, radius)
+    dout = dout.contiguous()
+    ops = _ext.ops()
+    ops.corr_otf_bwd_(st.f1, st.f2, coords, dout, st.grad_f1, st.grad, radius)
+    if st.precision == 'fp32' and st.lo:
+        # fp32-accurate backward (the reference's alt_cuda_corr backward is fp32): with the window
+        # gradient dS = dS_hi + dS_lo and F = F_hi + F_lo (bf16 parts), dF1 = dS F2 and
+        # dF2 = dS^T F1 are the three bf16 products hi*hi (above) + lo(dS)*hi + hi*lo(F), each a
+        # pass of the same MFMA kernel accumulating into the gradients (~2^-16 relative; the
+        # dropped lo*lo term is ~2^-18)
+        ops.corr_otf_bwd_(st.f1, st.f2, coords, dout, st.grad_f1, st.grad, radius, 1)
+        ops.corr_otf_bwd_(st.lo[0], st.lo[1:], coords, dout, st.grad_f1, st.grad, radius)
 
 
 class _OTFLookup(torch.autograd.Function):
@@ -309,8 +319,8 @@ class _OTFLookupNHWC(torch.autograd.Function):
 
 
 class OnTheFlyVolume:
-    """precision: 'bf16' (MFMA operands bf16, fp32 accumulation) or 'fp32' (split-bf16 forward,
-    ~2^-16 relative error; the backward always uses bf16 operands with fp32 accumulation)."""
+    """precision: 'bf16' (MFMA operands bf16, fp32 accumulation) or 'fp32' (split-bf16 forward
+    AND backward, ~2^-16 relative error: three bf16 products per product, fp32 accumulation)."""
 
     def __init__(self, fmap1, fmap2_pyramid, precision='fp32'):
         assert precision in ('bf16', 'fp32'), precision
