@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
 // once -- and parks them raw in LDS; phase 2 reads the row cells at the row's start offset inside
 // its pieces (LDS indexing is free), masks cells outside the plane and interpolates the (2r+1)^2
 // taps into the bf16 pixel-row tile; phase 3 streams the tile out as 16-B pixel-row pieces.
-constexpr int TPV = 16;  // pixels per workgroup (42 KB LDS: three workgroups per CU)
+// pixels per workgroup: the TPVK template parameter (16: 42 KB LDS, three workgroups per CU; 8: 21 KB)
 
 // one aligned 16-B piece; a piece that runs past the range end (the last rows of the range's
 // last plane) is read as four range-checked dwords: a 16-B load that is only partly in range
@@ -225,23 +225,23 @@ __device__ __forceinline__ uint4 piece16(__amdgpu_buffer_rsrc_t r, uint32_t off,
                     __builtin_amdgcn_raw_buffer_load_b32(r, off + 12u, 0, 0));
 }
 
-template <int R>
+template <int R, int TPVK>
 __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const float* __restrict__ coords,
                                                                uint16_t* __restrict__ out, int cbuf,
                                                                int B, int H, int W, int levels) {
   constexpr int D = 2 * R + 1, E = D + 1;
   constexpr int ROWT = (4 * D * D + 7) / 8 * 8;
   constexpr uint32_t OOB = 0x80000000u;
-  __shared__ __attribute__((aligned(16))) uint4 rows[TPV * 4 * E * 3];
-  __shared__ float cxy[TPV * 4 * 2];
-  __shared__ __attribute__((aligned(16))) uint16_t tile[TPV * ROWT];
+  __shared__ __attribute__((aligned(16))) uint4 rows[TPVK * 4 * E * 3];
+  __shared__ float cxy[TPVK * 4 * 2];
+  __shared__ __attribute__((aligned(16))) uint16_t tile[TPVK * ROWT];
   const int N = H * W;
-  const int tiles = (N + TPV - 1) / TPV;
+  const int tiles = (N + TPVK - 1) / TPVK;
   const int b = blockIdx.x / tiles;
-  const int i0 = (blockIdx.x % tiles) * TPV;
+  const int i0 = (blockIdx.x % tiles) * TPVK;
   const int tid = threadIdx.x;
-  const int npx = min(TPV, N - i0);
-  if (tid < TPV * 4) {
+  const int npx = min(TPVK, N - i0);
+  if (tid < TPVK * 4) {
     const int px = tid >> 2, l = tid & 3;
     const int i = min(i0 + px, N - 1);
     const float inv = 1.0f / (float)(1 << l);
@@ -273,7 +273,7 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
   // ---- phase 1: every window row's aligned 16-B pieces -> LDS (all loads before any store).
   // Items are level-major in 64-aligned per-level ranges, so every wave reads ONE level: the
   // buffer resource stays wave-uniform (a lane-varying descriptor costs a waterfall loop)
-  constexpr int IPL = (TPV * E + 63) / 64 * 64;  // items per level (padded)
+  constexpr int IPL = (TPVK * E + 63) / 64 * 64;  // items per level (padded)
   constexpr int ITEMS = 4 * IPL;
   constexpr int PER = (ITEMS + 255) / 256;
   uint4 v[PER][3];
@@ -283,10 +283,10 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
     const int e = tid + k * 256;
     const int l = __builtin_amdgcn_readfirstlane(e / IPL), rem = e - l * IPL;
     const int px = rem / E, r = rem - px * E;
-    slot[k] = rem < TPV * E && l < 4 ? (px * 4 + l) * E + r : -1;
+    slot[k] = rem < TPVK * E && l < 4 ? (px * 4 + l) * E + r : -1;
     uint32_t o0 = OOB, o1 = OOB, o2 = OOB;
     const int lq = l < levels ? l : 0;
-    if (rem < TPV * E && px < npx && l < levels) {
+    if (rem < TPVK * E && px < npx && l < levels) {
       const int hl = pyr.h[l], wl = pyr.w[l];
       const float cx = cxy[(px * 4 + l) * 2], cy = cxy[(px * 4 + l) * 2 + 1];
       const int xs = (int)floorf(cx) - R, gy = (int)floorf(cy) - R + r;
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
   }
   __syncthreads();
   // ---- phase 2: (pixel, level, window row iy) -> the 2r+1 taps of that row
-  const int items2 = TPV * levels * D;
+  const int items2 = TPVK * levels * D;
   for (int it = tid; it < items2; it += 256) {
     const int px = it / (levels * D), rem = it - px * (levels * D), l = rem / D, iy = rem - l * D;
     const int hl = pyr.h[l], wl = pyr.w[l];
@@ -1056,9 +1056,25 @@ bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* w
     return e && e[0] == '1';
   }();
   if (pyr_bf16 && !v1 && (radius == 4 || radius == 3)) {
-    dim3 grid((unsigned)(B * ((N + TPV - 1) / TPV)));
-    if (radius == 4) hipLaunchKernelGGL(corr_lookup_rows_kernel<4>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-    else hipLaunchKernelGGL(corr_lookup_rows_kernel<3>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+    // pixels per workgroup (RAFT_LOOKUP_TPV): 4 (default, 10.5 KB LDS) -- 27.7 / 28.8 / 34.7 us
+    // per call for 4 / 8 / 16 at chairs (profiles/r4/lookup_tpv.txt): more workgroups in flight
+    // per CU keep more window-row loads outstanding
+    static const int tpv = [] {
+      const char* e = getenv("RAFT_LOOKUP_TPV");
+      const int v = e ? atoi(e) : 4;
+      return v == 8 || v == 16 ? v : 4;
+    }();
+    dim3 grid((unsigned)(B * ((N + tpv - 1) / tpv)));
+    if (tpv == 4) {
+      if (radius == 4) hipLaunchKernelGGL((corr_lookup_rows_kernel<4, 4>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+      else hipLaunchKernelGGL((corr_lookup_rows_kernel<3, 4>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+    } else if (tpv == 8) {
+      if (radius == 4) hipLaunchKernelGGL((corr_lookup_rows_kernel<4, 8>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+      else hipLaunchKernelGGL((corr_lookup_rows_kernel<3, 8>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+    } else {
+      if (radius == 4) hipLaunchKernelGGL((corr_lookup_rows_kernel<4, 16>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+      else hipLaunchKernelGGL((corr_lookup_rows_kernel<3, 16>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+    }
     return true;
   }
   dim3 grid((unsigned)(B * ((N + TPW - 1) / TPW)));

@@ -3,6 +3,10 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 O=gpurun_out/diag; mkdir -p $O
-timeout -k 10 500 python -u -m pytest -q --timeout 200 --timeout-method thread tests/test_conv_fp32_gpu.py tests/test_graph_gpu.py > $O/pytest_fix.log 2>&1
-rc=$?; tail -n 1 $O/pytest_fix.log; grep -E "^E  .*Error|FAILED" $O/pytest_fix.log | head
+for t in 4 8; do
+  RAFT_LOOKUP_TPV=$t timeout -k 10 120 python -u scripts/bench_lookup.py > $O/lookup_$t.txt 2>&1 || { tail -5 $O/lookup_$t.txt; exit 1; }
+  echo "tpv $t: $(grep us $O/lookup_$t.txt)"
+done
+RAFT_LOOKUP_TPV=4 timeout -k 10 300 python -u -m pytest -q -x --timeout 200 --timeout-method thread tests/test_kernels_gpu.py -k "lookup" > $O/pytest_lookup8.log 2>&1
+rc=$?; tail -n 1 $O/pytest_lookup8.log; grep -E "^E  .*Error|FAILED" $O/pytest_lookup8.log | head
 exit $rc
