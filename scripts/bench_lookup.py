@@ -1,5 +1,6 @@
-"""Time the bf16 NHWC pyramid lookup (corr_lookup_nhwc_) at the chairs training shape (B=12,
-46x62, 4 levels, r=4); RAFT_LOOKUP_TPV=8|16 picks the pixels per workgroup.  Prints us per call
+"""Time the bf16 all-pairs pyramid build (corr_build_bf16) and the NHWC
+pyramid lookup (corr_lookup_nhwc_; RAFT_LOOKUP_TPV=4|8|16 pixels per workgroup) at the chairs
+training shape (B=12, 46x62, 4 levels, r=4).  Prints us per call
 and a checksum (variants must agree bit for bit)."""
 import sys
 
@@ -21,6 +22,16 @@ def main():
     out = torch.empty(b, h, w, 384, device='cuda', dtype=torch.bfloat16)
     for _ in range(3):
         ops.corr_lookup_nhwc_(pyr, coords, 4, out)
+        pyr = ops.corr_build_bf16(f1, f2, 4, True)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        pyr = ops.corr_build_bf16(f1, f2, 4, True)
+    e1.record()
+    torch.cuda.synchronize()
+    print('corr_build_bf16 %.1f us/call  checksum %.6f' % (e0.elapsed_time(e1) * 100,
+                                                          sum(float(p.float().sum()) for p in pyr)), flush=True)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     n = 20
