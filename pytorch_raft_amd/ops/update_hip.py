@@ -357,6 +357,8 @@ class _State:
         self.params = []
         self.n_iter = 0        # iterations issued through this block (forward order)
         self.next_bwd = None   # iteration whose backward must run next (strictly n_iter-1 .. 0)
+        self.dh_carry = None   # fp32 gradient of the next-to-run iteration's output state
+        self.zero_h = None     # bf16 scalar zero, broadcast as the stand-in h gradient
         self.dinp_acc = None   # fp32 gradient w.r.t. the context input, summed over iterations
         self.ctx_g = {}        # GRU conv -> its pre-activation gradients of the iterations run
         self.design = FULL
@@ -637,6 +639,9 @@ class _UpdateIter(torch.autograd.Function):
         ctx.itr = state.n_iter
         state.n_iter += 1
         ctx.save_for_backward(*saved)
+        # an output nobody differentiates arrives as None, not as a zero-filled tensor (the
+        # recurrent state's gradient comes through state.dh_carry, see backward)
+        ctx.set_materialize_grads(False)
         return h2, delta, mask
 
     @staticmethod
@@ -687,6 +692,10 @@ class _UpdateIter(torch.autograd.Function):
                             ry, roff, gmode, gt)
 
         # ---- mask head (mask = 0.25 * conv(fm[256:]))
+        if gmask is None:
+            gmask = _bf16(sh + (576,), dev).zero_()
+        if gdelta is None:
+            gdelta = torch.zeros(B, 2, H, W, device=dev, dtype=torch.float32)
         gmask = gmask.contiguous()
         if gmask.dtype != torch.bfloat16:
             gmask = gmask.to(torch.bfloat16)
@@ -703,7 +712,16 @@ class _UpdateIter(torch.autograd.Function):
         br.join()
         # ---- head
         wgrad('head', dpre_head, 0, [(h2, 0, HD)])
-        dh = gh.float().contiguous() if gh is not None else _f32(sh + (HD,), dev, zero=True)
+        # the recurrent state's gradient: the next iteration's backward hands it over in fp32
+        # (state.dh_carry) instead of through autograd, which would round it to h's bf16 dtype
+        # and back (two conversion kernels per iteration and a bf16 rounding of dh)
+        carry, st.dh_carry = st.dh_carry, None
+        if gh is not None and st.zero_h is not None and gh.data_ptr() == st.zero_h.data_ptr():
+            gh = None   # the stand-in zero of a carried gradient (below)
+        if gh is not None:
+            dh = gh.float().contiguous() if carry is None else carry.add_(gh)
+        else:
+            dh = carry if carry is not None else _f32(sh + (HD,), dev, zero=True)
         halves = (('2', (h1, z2, rh2, r2, q2)), ('1', (h0, z1, rh1, r1, q1)))
 
         def qgate(half):
@@ -798,6 +816,14 @@ class _UpdateIter(torch.autograd.Function):
             st.ctx_g = {}
             st.next_bwd = None
         # token: no gradient value (autograd still runs the weight node after every iteration)
+        if ctx.itr > 0:
+            # h came from iteration itr-1, whose backward runs next (strict order, checked above):
+            # autograd gets a broadcast zero of h's shape and dtype (no memory, no kernel) so it
+            # still runs that backward, which takes the real fp32 gradient from dh_carry
+            st.dh_carry = dh
+            if st.zero_h is None:
+                st.zero_h = torch.zeros((), device=dev, dtype=torch.bfloat16)
+            return (None, st.zero_h.expand(B, H, W, h0.shape[-1]), dinp, dcorr, None, None)
         return (None, dh, dinp, dcorr, None, None)
 
 
