@@ -7,7 +7,10 @@ CATS = [('ours conv fwd', r'conv_fwd_kernel<[^>]*, [0-57], (true|false)>|conv_fw
         ('ours conv fwd', r'conv_enc64'),
         ('ours wgrad', r'fh2_wgrad'),
         ('ours wgrad', r'conv_wgrad'),
-        ('encoder norm', r'norm_(bwd_)?(stats|apply|finalize)|partial_reduce|add_relu|relu_mask'),
+        ('encoder norm', r'norm_(bwd_)?(stats|apply|finalize|reduce_finalize)|partial_reduce|add_relu|relu_mask'),
+        # hipBLASLt: the two GEMMs of the all-pairs correlation backward (dF1 = dC F2, dF2 = dC^T F1)
+        ('corr gemm', r'Cijk_'),
+        ('update ew', r'f1_patch|sum_bf16'),
         ('miopen conv', r'igemm|grouped_conv|naive_conv|gemm|Conv'), ('transpose', r'transpose'),
         ('bn/norm', r'batch_norm|BatchNorm|InstanceNorm|instance_norm|welford|Norm'),
         ('corr', r'corr_'), ('reduce', r'reduce_kernel'),
