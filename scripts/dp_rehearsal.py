@@ -108,10 +108,12 @@ def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl, fp32=Fals
         st2.scheduler.step()
         torch.cuda.synchronize()
         wr = torch.cat([p.detach().reshape(-1).float() for p in ref.parameters()])
-        # AdamW's first step is ~lr * sign(g): it is compared where the gradient's sign is resolved
-        # (|g| above 4x the DP-vs-full discrepancy); the rest is bf16 noise whose sign varies
-        # run to run with the autotuned kernels' reduction order
-        resolved = g_full.abs() > 4 * (g_dp - g_full).abs()
+        # AdamW's first step is lr * g / (|g| + eps) ~ lr * sign(g): it is compared where the
+        # gradient's sign is resolved (|g| above 4x the DP-vs-full discrepancy) and |g| >> eps
+        # (around |g| ~ eps = 1e-8 the step still depends on |g| itself, and the per-rank vs
+        # global loss normalisation moves such entries by O(1) of their size); the rest is
+        # rounding noise whose sign varies run to run with the kernels' reduction order
+        resolved = (g_full.abs() > 4 * (g_dp - g_full).abs()) & (g_full.abs() > 100 * args.epsilon)
         d_dp, d_ref = (w1 - w0)[resolved], (wr - w0)[resolved]
         rel_w = ((d_dp - d_ref).norm() / d_ref.norm()).item()
         cos_w = torch.nn.functional.cosine_similarity(d_dp[None], d_ref[None]).item()
@@ -126,8 +128,9 @@ def graph_mode(model, args, dev, rank, world, i1, i2, flow, valid, sl, fp32=Fals
         if fp32:
             assert cos_w > 0.9999 and rel_w < 1e-2, (cos_w, rel_w)
         else:
-            # bf16: observed step delta rel ~0.12 / cos ~0.993 (round 3)
-            assert cos_w > 0.99 and rel_w < 0.15, (cos_w, rel_w)
+            # bf16: observed step delta rel 1.2e-3 / cos 0.999999 at 4 ranks once entries with
+            # |g| ~ eps are excluded (round 3's 0.12 / 0.993 came from those)
+            assert cos_w > 0.9995 and rel_w < 3e-2, (cos_w, rel_w)
         assert same, 'weights diverged across ranks'
         assert tables_same, 'ranks run different conv kernels'
         assert all(r == 0 for r in runs[1:]), ('ranks > 0 must not autotune', runs)
