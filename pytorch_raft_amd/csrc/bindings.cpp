@@ -663,13 +663,16 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   a.wpk = reinterpret_cast<const uint16_t*>(wpk.data_ptr<at::BFloat16>());
   a.kpad = (int)wpk.size(1);
   if (bias.has_value() && bias->defined() && bias->dim() == 4) {
-    // per-pixel bias map (B,H,W,>=cout) fp32: the precomputed context part of a ConvGRU conv
+    // per-pixel bias map (B,H,W,>=cout) fp32 or bf16: the precomputed context part of a ConvGRU conv
     TORCH_CHECK(epi == EPI_GRU_ZR || epi == EPI_GRU_Q, "a per-pixel bias map needs a GRU epilogue");
-    check_nhwc(*bias, B, H, W, "bias map", at::kFloat);
+    const bool bm16 = bias->scalar_type() == at::kBFloat16;
+    check_nhwc(*bias, B, H, W, "bias map", bm16 ? at::kBFloat16 : at::kFloat);
     TORCH_CHECK(bias->size(3) >= cout, "bias map has too few channels");
-    TORCH_CHECK(bias->numel() * 4 < (int64_t(1) << 31), "bias map exceeds the 2 GiB buffer-descriptor range");
-    a.bmap = bias->data_ptr<float>();
+    TORCH_CHECK(bias->numel() * bias->element_size() < (int64_t(1) << 31),
+                "bias map exceeds the 2 GiB buffer-descriptor range");
+    a.bmap = reinterpret_cast<const float*>(bias->data_ptr());
     a.bmap_stride = (int)bias->size(3);
+    a.bmap_bf16 = bm16 ? 1 : 0;
   } else if (bias.has_value() && bias->defined()) {
     check_cuda_f32(*bias, "bias");
     TORCH_CHECK(bias->numel() >= cout, "bias too short");

@@ -113,7 +113,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = (acc[i][j][r] + bias) * a.scale;
       if constexpr (EPI == EPI_GRU_ZR || EPI == EPI_GRU_Q) {
-        if (a.bmap != nullptr) {  // uniform
+        if (a.bmap != nullptr && a.bmap_bf16) {  // uniform
+          const rsrc_t bm = make_rsrc(a.bmap, P_u * (uint32_t)a.bmap_stride * 2u);
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            v[r] += bld_bf16(bm, ok[r] ? (uint32_t)(mrow[r] * a.bmap_stride + n) * 2u : OOB);
+        } else if (a.bmap != nullptr) {
           const rsrc_t bm = make_rsrc(a.bmap, P_u * (uint32_t)a.bmap_stride * 4u);
 #pragma unroll
           for (int r = 0; r < 16; ++r)

@@ -419,7 +419,7 @@ bool outputs_overlap_inputs(const ConvFwdArgs& a, int epi) {
   if (epi == EPI_GRU_ZR || epi == EPI_GRU_Q) {
     ins[nin++] = nhwc_range(a.aux0, P, a.aux0_stride, 2);
     if (epi == EPI_GRU_Q) ins[nin++] = nhwc_range(a.aux1, P, a.aux1_stride, 2);
-    if (a.bmap) ins[nin++] = nhwc_range(a.bmap, P, a.bmap_stride, 4);
+    if (a.bmap) ins[nin++] = nhwc_range(a.bmap, P, a.bmap_stride, a.bmap_bf16 ? 2 : 4);
   }
   for (int o = 0; o < nout; ++o)
     for (int i = 0; i < nin; ++i)

@@ -147,6 +147,7 @@ struct ConvFwdArgs {
   // iteration-invariant context part of the ConvGRU convs, precomputed once per forward)
   const float* bmap;
   int bmap_stride;
+  int bmap_bf16;        // 1: the bias map is bf16 (bmap points at uint16 data)
   int cout;
   void* out0;
   int out0_stride;

@@ -280,7 +280,7 @@ class _Packed:
         self.db = {}
         self.pending = {}  # conv name -> [(g, g_off, segs)] awaiting the batched weight gradient
         self.fh2_items = []  # (fp32 delta gradient, head activations) per iteration
-        self.ctx = None      # GRU conv -> fp32 (B,H,W,cout) context bias map (see ctx_maps)
+        self.ctx = None      # GRU conv -> bf16 (B,H,W,cout) context bias map (see ctx_maps)
         self.ctx_key = None
         self.device = device
         plan = self.plan = _plan(ub, need_grad, device, design)
@@ -524,10 +524,15 @@ def _f32(shape, dev, zero=False):
     return (torch.zeros if zero else torch.empty)(*shape, device=dev, dtype=torch.float32)
 
 
+# RAFT_CTX_BF16=0: fp32 context maps (A/B; bf16 halves the maps' per-iteration reads -- 1.5 KB per
+# pixel and iteration -- at the rounding the GRU pre-activations see anyway)
+_CTX_BF16 = os.environ.get('RAFT_CTX_BF16', '1') != '0'
+
+
 def ctx_maps(pk, inp):
-    """Context part of the four ConvGRU convs, conv(inp, W_inp) + bias as fp32 (B,H,W,cout)
-    maps -- computed once per forward pass (the iterations share ``inp``) and added by the
-    iterations' GRU epilogues."""
+    """Context part of the four ConvGRU convs, conv(inp, W_inp) + bias as bf16 (fp32 with
+    RAFT_CTX_BF16=0) (B,H,W,cout) maps -- computed once per forward pass (the iterations share
+    ``inp``) and added by the iterations' GRU epilogues."""
     key = (inp.data_ptr(), tuple(inp.shape), inp._version)
     if pk.ctx is not None:
         if key != pk.ctx_key:
@@ -538,9 +543,10 @@ def ctx_maps(pk, inp):
     pk.ctx = {}
     for name in GRU_CONVS:
         s = SPEC[name + 'i']
-        m = torch.empty(B, H, W, s.cout, device=inp.device, dtype=torch.float32)
-        C.conv_fwd([(inp, 0, HD)], pk.w[s.name], pk.b[s.name], s.k, s.pad, s.cout, C.EPI_F32,
-                   [m], [0])
+        m = torch.empty(B, H, W, s.cout, device=inp.device,
+                        dtype=torch.bfloat16 if _CTX_BF16 else torch.float32)
+        C.conv_fwd([(inp, 0, HD)], pk.w[s.name], pk.b[s.name], s.k, s.pad, s.cout,
+                   C.EPI_BF16 if _CTX_BF16 else C.EPI_F32, [m], [0])
         pk.ctx[name] = m
     pk.ctx_key = key
     return pk.ctx
