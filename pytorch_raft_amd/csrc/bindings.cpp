@@ -1396,6 +1396,59 @@ void flow_prep_(const Tensor& flow, const Tensor& flowb, const c10::optional<Ten
   launch_flow_prep(flow.data_ptr<float>(), bf16m(flowb), sp, ss, (int)B, (int)(H * W), cur_stream());
 }
 
+// AdamW over lists of fp32 tensors with the global-norm gradient clip folded in (adamw.hip);
+// returns the device pair [clip coefficient, total gradient norm]
+Tensor adamw_step_(const std::vector<Tensor>& params, const std::vector<Tensor>& grads,
+                   const std::vector<Tensor>& exp_avg, const std::vector<Tensor>& exp_avg_sq,
+                   const c10::optional<Tensor>& lr_t, double lr, double beta1, double beta2,
+                   double eps, double wd, double bc1, double bc2, double max_norm) {
+  const size_t T = params.size();
+  TORCH_CHECK(T > 0 && grads.size() == T && exp_avg.size() == T && exp_avg_sq.size() == T,
+              "adamw: tensor lists must have the same length");
+  const auto dev = params[0].device();
+  for (size_t i = 0; i < T; ++i)
+    for (const Tensor* t : {&params[i], &grads[i], &exp_avg[i], &exp_avg_sq[i]}) {
+      TORCH_CHECK(t->is_cuda() && t->device() == dev && t->scalar_type() == at::kFloat &&
+                      t->is_contiguous() && t->numel() == params[i].numel(),
+                  "adamw: contiguous fp32 tensors of equal size on one GPU");
+    }
+  const int64_t CH = adam_chunk_elems();
+  const int64_t tab_bytes = (int64_t)T * (int64_t)sizeof(AdamTensor);
+  Tensor host = at::empty({tab_bytes + (int64_t)(T + 1) * 4},
+                          at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  AdamTensor* ht = reinterpret_cast<AdamTensor*>(host.data_ptr<uint8_t>());
+  int* hc = reinterpret_cast<int*>(host.data_ptr<uint8_t>() + tab_bytes);
+  hc[0] = 0;
+  for (size_t i = 0; i < T; ++i) {
+    ht[i] = AdamTensor{params[i].data_ptr<float>(), grads[i].data_ptr<float>(),
+                       exp_avg[i].data_ptr<float>(), exp_avg_sq[i].data_ptr<float>(),
+                       params[i].numel()};
+    const int64_t nc = (params[i].numel() + CH - 1) / CH;
+    TORCH_CHECK((int64_t)hc[i] + nc < (int64_t(1) << 30), "adamw: too many chunks");
+    hc[i + 1] = hc[i] + (int)nc;
+  }
+  const int nchunks = hc[T];
+  c10::DeviceGuard g(dev);
+  // pinned source + stream-ordered copy: no host sync (the caching host allocator keeps the
+  // block until the copy has run)
+  Tensor dtab = host.to(dev, /*non_blocking=*/true);
+  Tensor out = at::empty({(int64_t)nchunks + 2}, params[0].options());
+  const float* lrp = nullptr;
+  if (lr_t.has_value() && lr_t->defined()) {
+    TORCH_CHECK(lr_t->is_cuda() && lr_t->device() == dev && lr_t->scalar_type() == at::kFloat &&
+                    lr_t->numel() == 1,
+                "adamw: lr tensor must be a one-element fp32 tensor on the parameters' GPU");
+    lrp = lr_t->data_ptr<float>();
+  }
+  if (nchunks > 0)
+    launch_adamw_multi(reinterpret_cast<const AdamTensor*>(dtab.data_ptr<uint8_t>()),
+                       reinterpret_cast<const int*>(dtab.data_ptr<uint8_t>() + tab_bytes), (int)T,
+                       nchunks, lrp, (float)lr, beta1, beta2, (float)eps, (float)wd,
+                       (float)bc1, (float)bc2, (float)max_norm, out.data_ptr<float>(),
+                       out.data_ptr<float>() + nchunks, cur_stream());
+  return out.narrow(0, nchunks, 2);
+}
+
 // dcorr level 0 (B, N, N) straight from the iterations' bf16 lookup-output gradients
 Tensor corr_tap_reduce(const std::vector<Tensor>& coords, const std::vector<Tensor>& douts,
                        int64_t H, int64_t W, int64_t levels, int64_t radius, double inv_sqrt_c,
@@ -1572,6 +1625,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("conv_fwd_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, Tensor? bias, int kh, int kw, int ph, int pw, int cout, int cin_small, int epi, int bn, float scale, int split, Tensor(a!)[] outs, int[] out_off, Tensor[] aux, int[] aux_off) -> ()");
   m.def("conv_wgrad_multi_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
   m.def("f1_patch_(Tensor flow, Tensor(a!) patch, Tensor(b!)? slot, int slot_off) -> ()");
+  m.def("adamw_step_(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, Tensor? lr_t, float lr, float beta1, float beta2, float eps, float wd, float bc1, float bc2, float max_norm) -> Tensor");
   m.def("corr_tap_reduce(Tensor[] coords, Tensor[] douts, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16) -> Tensor");
   m.def("fh2_fwd_(Tensor inp, Tensor wf, Tensor b, Tensor(a!) out) -> ()");
   m.def("fh2_dgrad_(Tensor gout, Tensor wd, Tensor fm, Tensor(a!) dx) -> ()");
@@ -1590,6 +1644,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("norm_fwd_", &norm_fwd_);
   m.impl("norm_bwd_", &norm_bwd_);
   m.impl("f1_patch_", &f1_patch_);
+  m.impl("adamw_step_", &adamw_step_);
   m.impl("corr_tap_reduce", &corr_tap_reduce);
   m.impl("fh2_fwd_", &fh2_fwd_);
   m.impl("fh2_dgrad_", &fh2_dgrad_);

@@ -334,3 +334,18 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
                      int N, int HW, int C, int mode, int relu, const float* gamma,
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
                      float* dgamma, float* dbeta, float* dcbias, uint16_t* dx, hipStream_t stream);
+
+// ---- multi-tensor AdamW + global-norm clip (adamw.hip)
+struct AdamTensor {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int64_t numel;
+};
+int adam_chunk_elems();
+// tab / cum: device tables (T tensors, cum[T] = nchunks); part: nchunks floats; coef: 2 floats
+// (clip coefficient, total norm); max_norm <= 0: no clipping
+void launch_adamw_multi(const AdamTensor* tab, const int* cum, int T, int nchunks, const float* lr_dev,
+                        float lr_host, double b1, double b2, float eps, float wd, float bc1, float bc2,
+                        float max_norm, float* part, float* coef, hipStream_t stream);

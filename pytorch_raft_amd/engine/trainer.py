@@ -30,7 +30,7 @@ import torch.distributed as dist
 
 from ..ops.loss import sequence_loss
 from ..parallel import dist as pdist
-from .optim import fetch_optimizer, clip_grad_norm_
+from .optim import fetch_optimizer, clip_grad_norm_, clip_and_step
 
 
 # RAFT_PHASE_MARKS=1: an empty marker kernel before and after each decode replay, so a kernel
@@ -49,9 +49,10 @@ class TrainState:
         self.model = model
         self.args = args
         self.device = device
-        self.optimizer, self.scheduler = fetch_optimizer(args, model, capturable=graph_ready)
         amp_fp16 = bool(getattr(args, 'mixed_precision', False)) and \
             getattr(args, 'amp_dtype', 'bfloat16') in ('float16', 'fp16')
+        self.optimizer, self.scheduler = fetch_optimizer(args, model, capturable=graph_ready,
+                                                         amp_fp16=amp_fp16)
         self.scaler = torch.amp.GradScaler('cuda', enabled=amp_fp16 and device.type == 'cuda')
         self.sync = None
         if sync and pdist.world_size() > 1 and not graph_ready:
@@ -85,10 +86,7 @@ class TrainState:
         return loss, metrics
 
     def apply_update(self, loss):
-        self.scaler.unscale_(self.optimizer)
-        clip_grad_norm_(self.model.parameters(), self.args.clip)
-        self.scaler.step(self.optimizer)
-        self.scaler.update()
+        clip_and_step(self.optimizer, self.model.parameters(), self.args.clip, self.scaler)
         self.nonfinite += (~torch.isfinite(loss.detach())).float()
 
     def step(self, image1, image2, flow, valid):
@@ -335,8 +333,7 @@ class GraphedTrainStep:
 
     def _update_graphable(self, loss):
         st = self.st
-        clip_grad_norm_(self.params, st.args.clip)
-        st.optimizer.step()
+        clip_and_step(st.optimizer, self.params, st.args.clip)
         st.nonfinite += (~torch.isfinite(loss.detach())).float()
 
     def _sched(self):
