@@ -1269,7 +1269,7 @@ void conv_enc64_(const Tensor& x, const Tensor& wpk, const Tensor& out) {
   TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == at::kBFloat16 &&
                   wpk.dim() == 2 && wpk.size(0) == 64 && wpk.size(1) == 9 * 64,
               "packed weight must be a contiguous bf16 (64, 576) tensor");
-  TORCH_CHECK(x.numel() < (int64_t(1) << 31), "conv_enc64: input too large");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 31) && H * W * 128 < (int64_t(1) << 31), "conv_enc64: input too large");
   c10::DeviceGuard gd(x.device());
   static const int cus = [] {
     hipDeviceProp_t p{};

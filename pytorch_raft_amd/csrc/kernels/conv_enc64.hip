@@ -9,19 +9,27 @@
 //   * keeps the whole weight matrix in LDS (64 x 576 bf16, rows padded to 1168 B: conflict-free
 //     fragment reads), loaded once;
 //   * works on 2-D tiles of 8 x 16 output pixels: the tile's 10 x 18 input halo (all 64 channels,
-//     144-B padded rows) is loaded ONCE and every tap reads its shifted rows from it -- 1.4x the
-//     tile's bytes instead of 9x;
-//   * stages the halo through registers two tiles ahead (two tiles' loads, ~46 KB per CU, in
-//     flight while a tile's 72 MFMAs per wave run);
+//     144-B padded pixels, 2816-B padded rows: bank-conflict-free fragment reads) is loaded ONCE
+//     and every tap reads its shifted rows from it -- 1.4x the tile's bytes instead of 9x;
+//   * stages the halo through registers three tiles ahead (buffer loads, zeros outside the image,
+//     no branches) while a tile's 72 MFMAs per wave run, the K loop reading the next tap's
+//     fragments ahead of the current tap's MFMAs;
 //   * writes the output tile through LDS as 16-B rows (per-lane 2-B stores of the MFMA layout
 //     were store-issue bound: ~115 us per call either way, profiles/r3/c2_kernel_summary.txt).
 // 4 waves as 2 (pixels) x 2 (channels): a wave owns 64 pixels (4 tile rows) x 32 channels.
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 namespace {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t mk_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
 
 constexpr int TH = 8, TW = 16;                 // output tile
 constexpr int HH = TH + 2, HWD = TW + 2;       // halo tile
@@ -30,13 +38,30 @@ constexpr int AROW = 144;                      // LDS bytes per halo pixel (128 
 constexpr int BROW = 1168;                     // LDS bytes per weight row (1152 + 16 pad)
 constexpr int KTOT = 9 * 64;
 constexpr int NTH = 256;
+constexpr uint32_t OOB = 0x80000000u;          // buffer offset past any descriptor's range
 constexpr int APIECES = HROWS * 8;             // 16-B pieces of a halo tile
 constexpr int APER = (APIECES + NTH - 1) / NTH;  // 6 per thread
-constexpr int ABUF = HROWS * AROW;             // 25,920 B
+// halo rows of 18 pixels padded to 2816 B = 704 dwords, a multiple of the 64 banks: a fragment
+// read (ds_read_b128, 16-lane groups spanning two tile rows) then covers all 64 banks once.  With
+// unpadded 2592-B rows (648 dwords = 8 mod 64) every A-fragment read was 2-way conflicted and the
+// LDS array, at 4 waves x (8 A x 8 + 4 B x 4) cycles per tap, outran the tap's 8 MFMAs (256).
+constexpr int AROWB = 2816;
+constexpr int ABUF = 11 * AROWB;               // 10 halo rows + the spare pieces, 30,976 B
 constexpr int BBUF = 64 * BROW;                // 74,752 B
 constexpr int OROW = 144;                      // LDS bytes per staged output pixel (128 + 16 pad)
 constexpr int OBUF = TH * TW * OROW;           // 18,432 B
 
+// LDS offset of halo pixel hp (row-major over the 10 x 18 halo; hp >= 180: spare row 10)
+__device__ __forceinline__ int hoff(int hp) { return (hp / HWD) * AROWB + (hp % HWD) * AROW; }
+
+// PIPE: the K loop reads the next tap's 12 fragments (4 weight + 8 halo, ds_read_b128) before
+// the current tap's 8 MFMAs, fenced by scheduling barriers.  Left to itself the compiler issued
+// each MFMA pair's reads just before it and waited on them (lgkmcnt(0..2) ahead of every second
+// MFMA), exposing the LDS latency at one wave per SIMD.  PIPE = false keeps that schedule (A/B).
+// NSET: register sets of halo loads in flight (tiles ahead).  One workgroup per CU moves a tile's
+// 24.6 KB halo per ~3.7 us, so at HBM latency under load the loads in flight, not the MFMAs, set
+// the pace: 3 sets keep ~74 KB per CU outstanding instead of ~49 KB.
+template <bool PIPE, int NSET>
 __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ wpk,
                                                             uint16_t* __restrict__ out, int B,
@@ -61,23 +86,40 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
   auto load_a = [&](int t, uint4 (&areg)[APER]) {
     const int b = t / (tiles_y * tiles_x), r = t - b * tiles_y * tiles_x;
     const int y0 = (r / tiles_x) * TH - 1, x0 = (r % tiles_x) * TW - 1;
+    if constexpr (PIPE) {
+      // branch-free: per-image buffer descriptor, out-of-image pieces (and tiles past the end:
+      // zero-sized descriptor) read as zeros -- no control flow, so the wait before this
+      // register set's LDS store counts only its own loads, not the next tile's
+      const rsrc_t rs = mk_rsrc(x + (int64_t)b * H * W * 64, t < ntiles ? (uint32_t)H * W * 128 : 0u);
 #pragma unroll
-    for (int j = 0; j < APER; ++j) {
-      const int e = tid + j * NTH;
-      const int hp = e >> 3, q = e & 7;
-      const int yy = y0 + hp / HWD, xx = x0 + hp % HWD;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (e < APIECES && t < ntiles && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
-        v = *reinterpret_cast<const uint4*>(x + (((int64_t)b * H + yy) * W + xx) * 64 + q * 8);
-      areg[j] = v;
+      for (int j = 0; j < APER; ++j) {
+        const int e = tid + j * NTH;
+        const int hp = e >> 3, q = e & 7;
+        const int yy = y0 + hp / HWD, xx = x0 + hp % HWD;
+        const bool in = e < APIECES && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const uint32_t off = in ? (uint32_t)((yy * W + xx) * 128 + q * 16) : OOB;
+        areg[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < APER; ++j) {
+        const int e = tid + j * NTH;
+        const int hp = e >> 3, q = e & 7;
+        const int yy = y0 + hp / HWD, xx = x0 + hp % HWD;
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (e < APIECES && t < ntiles && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+          v = *reinterpret_cast<const uint4*>(x + (((int64_t)b * H + yy) * W + xx) * 64 + q * 8);
+        areg[j] = v;
+      }
     }
   };
   auto store_a = [&](int buf, const uint4 (&areg)[APER]) {
 #pragma unroll
     for (int j = 0; j < APER; ++j) {
       const int e = tid + j * NTH;
-      if (e < APIECES)
-        *reinterpret_cast<uint4*>(As + buf * ABUF + (e >> 3) * AROW + (e & 7) * 16) = areg[j];
+      // PIPE: pieces past the halo land in the buffer's spare rows (no branch)
+      if (PIPE || e < APIECES)
+        *reinterpret_cast<uint4*>(As + buf * ABUF + hoff(e >> 3) + (e & 7) * 16) = areg[j];
     }
   };
 
@@ -86,20 +128,21 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int tr = wm * 4 + 2 * i + ((lane & 31) >> 4), tc = lane & 15;
-    hbase[i] = (tr * HWD + tc) * AROW + (lane >> 5) * 16;
+    hbase[i] = tr * AROWB + tc * AROW + (lane >> 5) * 16;
   }
   const int bbase = (wn * 32 + (lane & 31)) * BROW + (lane >> 5) * 16;
 
   // two tiles of halo loads in flight per thread (HBM latency x bandwidth per CU needs ~2 tiles'
   // 23 KB): registers R0 / R1 alternate; the loop is unrolled by two so both stay static
-  uint4 R0[APER], R1[APER];
+  uint4 R0[APER], R1[APER], R2[APER];
   const int G = gridDim.x;
   load_a(blockIdx.x, R0);
   load_a(blockIdx.x + G, R1);
+  if constexpr (NSET == 3) load_a(blockIdx.x + 2 * G, R2);
   auto tile = [&](int t, int buf, uint4 (&R)[APER]) {
     store_a(buf, R);
     __syncthreads();  // halo (and, first time, weights) visible; the other buffer is free
-    load_a(t + 2 * G, R);  // two tiles ahead, in flight during this tile and the next
+    load_a(t + NSET * G, R);  // NSET tiles ahead, in flight during this tile and the next ones
 
     f32x16 acc[2];
 #pragma unroll
@@ -107,10 +150,8 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
     const char* Ab = As + buf * ABUF;
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int shift = ((tap / 3) * HWD + tap % 3) * AROW;
-      bf16x8_t af[4][2], bfr[4];
+    auto frags = [&](int tap, bf16x8_t (&af)[4][2], bf16x8_t (&bfr)[4]) {
+      const int shift = (tap / 3) * AROWB + (tap % 3) * AROW;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         bfr[kk] = *reinterpret_cast<const bf16x8_t*>(Bs + bbase + (tap * 64 + kk * 16) * 2);
@@ -118,11 +159,31 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
         for (int i = 0; i < 2; ++i)
           af[kk][i] = *reinterpret_cast<const bf16x8_t*>(Ab + hbase[i] + shift + kk * 32);
       }
+    };
+    auto mma = [&](const bf16x8_t (&af)[4][2], const bf16x8_t (&bfr)[4]) {
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
           acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bfr[kk], acc[i], 0, 0, 0);
+    };
+    if constexpr (PIPE) {
+      bf16x8_t af[2][4][2], bfr[2][4];
+      frags(0, af[0], bfr[0]);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        if (tap + 1 < 9) frags(tap + 1, af[(tap + 1) & 1], bfr[(tap + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(af[tap & 1], bfr[tap & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        bf16x8_t af[4][2], bfr[4];
+        frags(tap, af, bfr);
+        mma(af, bfr);
+      }
     }
 
     // epilogue: the accumulators go to an LDS [pixel][channel] bf16 tile, then out as 16-B rows
@@ -139,32 +200,61 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
     __syncthreads();  // staged tile complete (the next tile's stores come after its own barrier)
     const int b = t / (tiles_y * tiles_x), r = t - b * tiles_y * tiles_x;
     const int ty0 = (r / tiles_x) * TH, tx0 = (r % tiles_x) * TW;
+    const rsrc_t ro = mk_rsrc(out + (int64_t)b * H * W * 64, (uint32_t)H * W * 128);
 #pragma unroll
     for (int j = 0; j < TH * TW * 8 / NTH; ++j) {
       const int e = tid + j * NTH;
       const int p = e >> 3, q = e & 7;
       const int yy = ty0 + p / TW, xx = tx0 + p % TW;
-      if (yy < H && xx < W)
-        *reinterpret_cast<uint4*>(out + (((int64_t)b * H + yy) * W + xx) * 64 + q * 8) =
-            *reinterpret_cast<const uint4*>(Os + p * OROW + q * 16);
+      const uint4 v = *reinterpret_cast<const uint4*>(Os + p * OROW + q * 16);
+      if constexpr (PIPE) {
+        // pixels past the image edge: out-of-range offset, the store is dropped (no branch)
+        const uint32_t off = yy < H && xx < W ? (uint32_t)((yy * W + xx) * 128 + q * 16) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                               ro, off, 0, 0);
+      } else if (yy < H && xx < W) {
+        *reinterpret_cast<uint4*>(out + (((int64_t)b * H + yy) * W + xx) * 64 + q * 8) = v;
+      }
     }
   };
-  for (int t = blockIdx.x; t < ntiles; t += 2 * G) {
-    tile(t, 0, R0);
-    if (t + G < ntiles) tile(t + G, 1, R1);
+  if constexpr (NSET == 2) {
+    for (int t = blockIdx.x; t < ntiles; t += 2 * G) {
+      tile(t, 0, R0);
+      if (t + G < ntiles) tile(t + G, 1, R1);
+    }
+  } else {
+    // three register sets, two LDS buffers: the buffer index alternates at run time
+    int k = 0;
+    for (int t = blockIdx.x; t < ntiles; t += 3 * G, k += 3) {
+      tile(t, k & 1, R0);
+      if (t + G < ntiles) tile(t + G, (k + 1) & 1, R1);
+      if (t + 2 * G < ntiles) tile(t + 2 * G, k & 1, R2);
+    }
   }
 }
 
 }  // namespace
 
-// persistent grid: one workgroup per CU (144 KB of LDS each), capped by the tile count
+// persistent grid: one workgroup per CU (152 KB of LDS each), capped by the tile count
 bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, int B, int H, int W,
                        int grid_cap, hipStream_t stream) {
   const int ty = (H + TH - 1) / TH, tx = (W + TW - 1) / TW;
   const int ntiles = B * ty * tx;
   if (ntiles <= 0) return true;
   const int grid = ntiles < grid_cap ? ntiles : grid_cap;
-  hipLaunchKernelGGL(conv_enc64_kernel, dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B, H, W, ty,
-                     tx);
+  static const int variant = [] {
+    // A/B: 1 = the compiler-scheduled K loop, 2 = pipelined K loop without the overlap
+    const char* e = getenv("RAFT_ENC64_V1");
+    return e ? atoi(e) : 0;
+  }();
+  if (variant == 1)
+    hipLaunchKernelGGL((conv_enc64_kernel<false, 2>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B, H,
+                       W, ty, tx);
+  else if (variant == 2)
+    hipLaunchKernelGGL((conv_enc64_kernel<true, 2>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B, H,
+                       W, ty, tx);
+  else
+    hipLaunchKernelGGL((conv_enc64_kernel<true, 3>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B, H,
+                       W, ty, tx);
   return true;
 }
