@@ -343,7 +343,10 @@ void corr_otf_fwd_(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor
 
 // deterministic on-the-fly dF2 (default; RAFT_OTF_DF2_ATOMIC=1: float atomics): per-tile slab
 // rows sized for a union box of up to 32 x 32 positions at level 0 (~20 x 20 at chairs), 24 x 24
-// above; a box past that capacity falls back to atomics for its tile
+// above; a box past that capacity falls back to atomics for its tile.  The scratch grows with the
+// pixel count (~170 KB per query pixel at C = 256) while on-the-fly correlation is what runs when
+// the all-pairs pyramid does not fit, so it is bounded: past RAFT_OTF_SLAB_GB (default 8) the
+// whole call takes the atomic dF2 path instead of allocating more
 struct OtfSlabs {
   std::vector<Tensor> keep;
   std::vector<float*> ptr;
@@ -356,13 +359,23 @@ struct OtfSlabs {
       const char* e = getenv("RAFT_OTF_DF2_ATOMIC");
       return e && e[0] == '1';
     }();
+    const char* eb = getenv("RAFT_OTF_SLAB_GB");   // read per call (tests lower it)
+    const double budget = (eb ? atof(eb) : 8.0) * 1e9;
     if (atomic_df2) return;
-    on = true;
     const int tiles = otf_tiles((int)B, (int)H, (int)W);
+    double bytes = 0.0;
     for (int64_t l = 0; l < levels; ++l) {
       const int plane = L.h[l] * L.w[l];
       cap.push_back(std::min(plane, l == 0 ? 1024 : 576));
-      keep.push_back(at::empty({(int64_t)tiles * cap.back() * C}, fo));
+      bytes += (double)tiles * cap.back() * C * 4.0;
+    }
+    if (bytes > budget) {
+      cap.clear();
+      return;
+    }
+    on = true;
+    for (int64_t l = 0; l < levels; ++l) {
+      keep.push_back(at::empty({(int64_t)tiles * cap[l] * C}, fo));
       ptr.push_back(keep.back().data_ptr<float>());
     }
     boxes = at::empty({(int64_t)tiles * 16}, fo.dtype(at::kInt));
@@ -970,8 +983,9 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
                  const std::vector<int64_t>& out_cnt, const std::vector<int64_t>& out_real,
                  const std::vector<int64_t>& out_acc, const std::vector<Tensor>& relu_y,
                  const std::vector<int64_t>& relu_off, const std::vector<int64_t>& gate_mode,
-                 const std::vector<Tensor>& gate_t) {
+                 const std::vector<Tensor>& gate_t, const std::vector<int64_t>& out_kcin) {
   TORCH_CHECK(relu_y.size() == relu_off.size(), "relu spec mismatch");
+  TORCH_CHECK(out_kcin.empty() || out_kcin.size() == outs.size(), "K-prefix spec mismatch");
   TORCH_CHECK(gate_mode.empty() || gate_mode.size() == outs.size(), "gate spec mismatch");
   TORCH_CHECK(!ins.empty() && ins.size() <= 3 && !outs.empty() && outs.size() <= 3, "1..3 segments");
   TORCH_CHECK(in_off.size() == ins.size() && in_cnt.size() == ins.size(), "input spec mismatch");
@@ -1048,32 +1062,35 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     a.oseg[o].gate = 0;
     cout += out_cnt[o];
   }
-  // fused ConvGRU gate backward (see OSeg): 7 tensors per gated segment, in segment order:
-  // z, q|r, h (bf16), dz (fp32, gate 2), d-pre (bf16), dz out (fp32, gate 1), dh (fp32)
+  // fused ConvGRU gate backward (see OSeg): 6 tensors per gated segment, in segment order:
+  // ga0, ga1, ga2 (bf16: z, q, h | -, r, h | y), gb (bf16), gz (bf16, gate 1), gf1 (fp32)
   size_t gt = 0;
   for (size_t o = 0; o < gate_mode.size(); ++o) {
     const int mode = (int)gate_mode[o];
     if (mode == 0) continue;
     TORCH_CHECK(mode >= 1 && mode <= 3, "gate mode must be 0..3");
-    TORCH_CHECK(gt + 7 <= gate_t.size(), "gate tensors missing");
+    TORCH_CHECK(gt + 6 <= gate_t.size(), "gate tensors missing");
     TORCH_CHECK(outs[o].scalar_type() == at::kFloat, "gated dgrad segment must be fp32");
     TORCH_CHECK(mode == 2 || out_acc[o], "q-gate / relu segments read the accumulated gradient");
     const int real = (int)out_real[o];
     const Tensor& z = gate_t[gt + 0];
     const Tensor& qr = gate_t[gt + 1];
     const Tensor& h = gate_t[gt + 2];
-    const Tensor& gin = gate_t[gt + 3];
-    const Tensor& gbo = gate_t[gt + 4];
-    const Tensor& gf0 = gate_t[gt + 5];
-    const Tensor& gf1 = gate_t[gt + 6];
-    gt += 7;
+    const Tensor& gbo = gate_t[gt + 3];
+    const Tensor& gzo = gate_t[gt + 4];
+    const Tensor& gf1 = gate_t[gt + 5];
+    gt += 6;
     for (const Tensor* t : {&z, &qr, &h}) {
       check_nhwc(*t, B, H, W, "gate input", at::kBFloat16);
       TORCH_CHECK(t->size(3) == z.size(3) && t->size(3) >= real, "gate inputs must share a layout");
       TORCH_CHECK(t->numel() * 2 < (int64_t(1) << 31), "gate input exceeds the 2 GiB descriptor range");
     }
-    check_nhwc(gbo, B, H, W, "gate output", at::kBFloat16);
+    for (const Tensor* t : {&gbo, &gzo}) {
+      check_nhwc(*t, B, H, W, "gate output", at::kBFloat16);
+      TORCH_CHECK(t->numel() * 2 < (int64_t(1) << 31), "gate output exceeds the 2 GiB descriptor range");
+    }
     TORCH_CHECK(gbo.size(3) >= (mode == 2 ? 2 * real : real), "gate d-pre output too narrow");
+    TORCH_CHECK(mode != 1 || gzo.size(3) >= real, "gate d-pre-z output too narrow");
     check_nhwc(gf1, B, H, W, "gate state gradient", at::kFloat);
     TORCH_CHECK(gf1.size(3) >= real && gf1.numel() * 4 < (int64_t(1) << 31), "gate state gradient");
     a.oseg[o].gate = mode;
@@ -1083,22 +1100,23 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     a.oseg[o].ga_stride = (int)z.size(3);
     a.oseg[o].gb = reinterpret_cast<uint16_t*>(gbo.data_ptr<at::BFloat16>());
     a.oseg[o].gb_stride = (int)gbo.size(3);
+    a.oseg[o].gz = reinterpret_cast<uint16_t*>(gzo.data_ptr<at::BFloat16>());
+    a.oseg[o].gz_stride = (int)gzo.size(3);
     a.oseg[o].gf1 = gf1.data_ptr<float>();
     a.oseg[o].gf_stride = (int)gf1.size(3);
-    if (mode == 3) {  // gf1: the accumulated fp32 gradient; z: the ReLU output; gb: the result
-      a.oseg[o].gf0 = nullptr;
-      a.oseg[o].gin = nullptr;
-    } else if (mode == 1) {
-      check_nhwc(gf0, B, H, W, "gate dz output", at::kFloat);
-      TORCH_CHECK(gf0.size(3) == gf1.size(3), "gate fp32 outputs must share a layout");
-      a.oseg[o].gf0 = gf0.data_ptr<float>();
-      a.oseg[o].gin = nullptr;
-    } else {
-      check_nhwc(gin, B, H, W, "gate dz input", at::kFloat);
-      TORCH_CHECK(gin.size(3) == gf1.size(3), "gate fp32 inputs must share a layout");
-      a.oseg[o].gin = gin.data_ptr<float>();
-      a.oseg[o].gf0 = nullptr;
-    }
+  }
+  // per-segment K prefixes: a prefix must end on an input-segment boundary (multiple of 64)
+  a.kprefix = 0;
+  for (size_t o = 0; o < out_kcin.size(); ++o) {
+    const int64_t kc = out_kcin[o];
+    if (kc == 0 || kc == cin_pad) continue;
+    int64_t acc = 0;
+    bool on_boundary = false;
+    for (size_t s2 = 0; s2 < ins.size(); ++s2) { acc += in_cnt[s2]; on_boundary = on_boundary || acc == kc; }
+    TORCH_CHECK(kc > 0 && kc < cin_pad && kc % 64 == 0 && on_boundary && cin_small == 0,
+                "out_kcin must end on an input segment boundary");
+    a.oseg[o].kcin = (int)kc;
+    a.kprefix = 1;
   }
   TORCH_CHECK(gt == gate_t.size(), "unused gate tensors");
   a.cout = (int)cout;
@@ -1452,7 +1470,7 @@ Tensor adamw_step_(const std::vector<Tensor>& params, const std::vector<Tensor>&
 // dcorr level 0 (B, N, N) straight from the iterations' bf16 lookup-output gradients
 Tensor corr_tap_reduce(const std::vector<Tensor>& coords, const std::vector<Tensor>& douts,
                        int64_t H, int64_t W, int64_t levels, int64_t radius, double inv_sqrt_c,
-                       bool out_bf16) {
+                       bool out_bf16, int64_t pitch_mult) {
   TORCH_CHECK(!coords.empty() && coords.size() == douts.size() && coords.size() <= RAFT_MAX_WIN,
               "1..", RAFT_MAX_WIN, " iterations");
   TORCH_CHECK(radius == 3 || radius == 4, "radius must be 3 or 4");
@@ -1474,10 +1492,14 @@ Tensor corr_tap_reduce(const std::vector<Tensor>& coords, const std::vector<Tens
   }
   tl.n = (int)coords.size();
   tl.cbuf = (int)cbuf;
+  // row pitch: N, or N rounded up to pitch_mult (zero columns: the MFMA backward GEMMs' K padding)
+  TORCH_CHECK(pitch_mult >= 0 && pitch_mult % 2 == 0, "pitch_mult must be even");
+  const int64_t ldo = pitch_mult > 0 ? (N + pitch_mult - 1) / pitch_mult * pitch_mult : N;
+  tl.ldo = (int)ldo;
   const int lds = corr_tap_reduce_lds_bytes((int)H, (int)W, (int)levels, (int)radius);
   TORCH_CHECK(lds <= 64 * 1024, "feature map too large for the LDS plane reduction");
   c10::DeviceGuard g(coords[0].device());
-  Tensor out = at::empty({B, N, N}, coords[0].options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  Tensor out = at::empty({B, N, ldo}, coords[0].options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
   // overflow list of the union-box fold (count + pixel indices)
   Tensor list = at::empty({1 + B * N}, coords[0].options().dtype(at::kInt));
   TORCH_CHECK(launch_corr_tap_reduce(tl, (int)levels, (int)B, (int)H, (int)W, (int)radius,
@@ -1485,6 +1507,31 @@ Tensor corr_tap_reduce(const std::vector<Tensor>& coords, const std::vector<Tens
                                      list.data_ptr<int>(), cur_stream()),
               "unsupported radius / levels");
   return out;
+}
+
+// feature-map gradients of the all-pairs correlation: dc (B, N, ldc) bf16 from corr_tap_reduce
+// with pitch_mult 64, f1 / f2 (B, H, W, C) bf16 -> [dF1 = dC F2, dF2 = dC^T F1] as (B, H, W, C)
+std::vector<Tensor> corr_bwd_fmaps(const Tensor& dc, const Tensor& f1, const Tensor& f2) {
+  TORCH_CHECK(f1.dim() == 4 && f1.sizes() == f2.sizes(), "fmaps must be (B, H, W, C) of one shape");
+  const int64_t B = f1.size(0), H = f1.size(1), W = f1.size(2), C = f1.size(3), N = H * W;
+  check_nhwc(f1, B, H, W, "fmap1", at::kBFloat16);
+  check_nhwc(f2, B, H, W, "fmap2", at::kBFloat16);
+  TORCH_CHECK(dc.is_cuda() && dc.is_contiguous() && dc.scalar_type() == at::kBFloat16 && dc.dim() == 3 &&
+                  dc.size(0) == B && dc.size(1) == N && dc.size(2) >= N && dc.size(2) % 64 == 0,
+              "dcorr must be a contiguous bf16 (B, N, ldc) tensor, ldc a multiple of 64 >= N");
+  TORCH_CHECK(C % 128 == 0, "channels must be a multiple of 128");
+  const int64_t ldc = dc.size(2);
+  TORCH_CHECK(N * ldc * 2 < (int64_t(1) << 31) && C * ldc * 2 < (int64_t(1) << 31) &&
+                  N * C * 2 < (int64_t(1) << 31),
+              "per-image operands exceed the 2 GiB buffer-descriptor range");
+  c10::DeviceGuard g(dc.device());
+  Tensor f2t = at::empty({B, C, ldc}, dc.options());
+  Tensor g1 = at::empty({B, H, W, C}, dc.options());
+  Tensor g2 = at::empty({B, H, W, C}, dc.options());
+  TORCH_CHECK(launch_corr_bwd_fmaps(bf16p(dc), (int)ldc, bf16p(f1), bf16p(f2), bf16m(f2t), bf16m(g1),
+                                    bf16m(g2), (int)B, (int)N, (int)C, cur_stream()),
+              "corr backward GEMM launch");
+  return {g1, g2};
 }
 
 // ------------------------------------------------------------------ flow_head.conv2 (256 -> 2)
@@ -1610,7 +1657,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_lookup_nhwc_(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
   m.def("corr_window_grad(Tensor coords, Tensor dout, int levels, int radius) -> Tensor");
   m.def("corr_window_reduce(Tensor[] coords, Tensor[] wgs, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16=False) -> Tensor");
-  m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off, int[] gate_mode, Tensor[] gate_t) -> ()");
+  m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off, int[] gate_mode, Tensor[] gate_t, int[] out_kcin=[]) -> ()");
   m.def("split_hilo_(Tensor x, Tensor(a!) out) -> ()");
   m.def("conv_enc64_(Tensor x, Tensor wpk, Tensor(a!) out) -> ()");
   m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale) -> ()");
@@ -1626,7 +1673,8 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("conv_wgrad_multi_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
   m.def("f1_patch_(Tensor flow, Tensor(a!) patch, Tensor(b!)? slot, int slot_off) -> ()");
   m.def("adamw_step_(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, Tensor? lr_t, float lr, float beta1, float beta2, float eps, float wd, float bc1, float bc2, float max_norm) -> Tensor");
-  m.def("corr_tap_reduce(Tensor[] coords, Tensor[] douts, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16) -> Tensor");
+  m.def("corr_tap_reduce(Tensor[] coords, Tensor[] douts, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16, int pitch_mult=0) -> Tensor");
+  m.def("corr_bwd_fmaps(Tensor dc, Tensor f1, Tensor f2) -> Tensor[]");
   m.def("fh2_fwd_(Tensor inp, Tensor wf, Tensor b, Tensor(a!) out) -> ()");
   m.def("fh2_dgrad_(Tensor gout, Tensor wd, Tensor fm, Tensor(a!) dx) -> ()");
   m.def("fh2_wgrad_(Tensor[] gouts, Tensor[] ins, Tensor(a!) part) -> ()");
@@ -1646,6 +1694,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("f1_patch_", &f1_patch_);
   m.impl("adamw_step_", &adamw_step_);
   m.impl("corr_tap_reduce", &corr_tap_reduce);
+  m.impl("corr_bwd_fmaps", &corr_bwd_fmaps);
   m.impl("fh2_fwd_", &fh2_fwd_);
   m.impl("fh2_dgrad_", &fh2_dgrad_);
   m.impl("fh2_wgrad_", &fh2_wgrad_);

@@ -73,6 +73,22 @@ __device__ __forceinline__ void bst_bf16(rsrc_t r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b16(raft_f32_to_bf16(v), r, off, 0, 0);
 }
 
+// 64-channel K chunks of the workgroup whose N tile is [n0, n0 + BN): all of cin_pad unless the
+// output segments it overlaps all read a K prefix (OSeg.kcin); then the longest of those prefixes
+__device__ __forceinline__ int tile_nchunk(const ConvFwdArgs& a, int n0, int BN) {
+  if (!a.kprefix) return a.cin_pad / BK;
+  int base = 0, kc = 0;
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    if (s < a.noseg) {
+      const int hi = base + a.oseg[s].cnt;
+      if (base < n0 + BN && hi > n0) kc = max(kc, a.oseg[s].kcin > 0 ? a.oseg[s].kcin : a.cin_pad);
+      base = hi;
+    }
+  }
+  return (kc > 0 ? kc : a.cin_pad) / BK;
+}
+
 template <int TM, int TN, int WM, int WN, int EPI>
 __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc)[TM][TN], int m0,
                                               int n0, int wm, int wn, int lane, int P, int HW) {
@@ -192,12 +208,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
         bool gated = false;
         if constexpr (EPI == EPI_DGRAD_GATE) {
           gated = o.gate != 0;
-          if (o.gate == 1) {  // ConvGRU q-gate backward on the final state gradient
+          if (o.gate == 1) {  // ConvGRU q / z gate backward on the final state gradient
             const rsrc_t od = make_rsrc(o.ptr, P_u * (uint32_t)o.stride * 4u);
             const uint32_t ab = P_u * (uint32_t)o.ga_stride * 2u;
             const rsrc_t rz = make_rsrc(o.ga0, ab), rq = make_rsrc(o.ga1, ab), rh = make_rsrc(o.ga2, ab);
             const rsrc_t gb = make_rsrc(o.gb, P_u * (uint32_t)o.gb_stride * 2u);
-            const rsrc_t f0 = make_rsrc(o.gf0, P_u * (uint32_t)o.gf_stride * 4u);
+            const rsrc_t gz = make_rsrc(o.gz, P_u * (uint32_t)o.gz_stride * 2u);
             const rsrc_t f1 = make_rsrc(o.gf1, P_u * (uint32_t)o.gf_stride * 4u);
 #pragma unroll
             for (int h8 = 0; h8 < 16; h8 += 8) {   // 8 rows at a time: bounded live registers
@@ -219,9 +235,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
                 const float g = pre[u] + v[r];
                 bst_bf16(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB,
                          g * zz[u] * (1.f - qq[u] * qq[u]));
-                const uint32_t of = e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB;
-                bst_f32(f0, of, g * (qq[u] - hh[u]));
-                bst_f32(f1, of, g * (1.f - zz[u]));
+                const float dz = g * (qq[u] - hh[u]);
+                bst_bf16(gz, e ? (uint32_t)(mrow[r] * o.gz_stride + c) * 2u : OOB,
+                         dz * zz[u] * (1.f - zz[u]));
+                bst_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB, g * (1.f - zz[u]));
               }
             }
           } else if (o.gate == 3) {  // last accumulation + ReLU backward: gb = bf16([y > 0](pre + v))
@@ -247,24 +264,20 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
                          yv[u] > 0.f ? pre[u] + v[r] : 0.f);
               }
             }
-          } else if (o.gate == 2) {  // ConvGRU z / r gate backward on d(r*h)
+          } else if (o.gate == 2) {  // ConvGRU r gate backward on d(r*h)
             const uint32_t ab = P_u * (uint32_t)o.ga_stride * 2u;
-            const rsrc_t rz = make_rsrc(o.ga0, ab), rr = make_rsrc(o.ga1, ab), rh = make_rsrc(o.ga2, ab);
-            const rsrc_t gi = make_rsrc(o.gin, P_u * (uint32_t)o.gf_stride * 4u);
+            const rsrc_t rr = make_rsrc(o.ga1, ab), rh = make_rsrc(o.ga2, ab);
             const rsrc_t gb = make_rsrc(o.gb, P_u * (uint32_t)o.gb_stride * 2u);
             const rsrc_t f1 = make_rsrc(o.gf1, P_u * (uint32_t)o.gf_stride * 4u);
 #pragma unroll
             for (int h8 = 0; h8 < 16; h8 += 8) {
-              float dz[8], zz[8], rv[8], hh[8], dh[8];
+              float rv[8], hh[8], dh[8];
 #pragma unroll
               for (int u = 0; u < 8; ++u) {
                 const int r = h8 + u;
                 const bool e = ok[r] && cok;
                 const uint32_t oa = e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB;
-                const uint32_t of = e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB;
-                dz[u] = bld_f32(gi, of);
-                dh[u] = bld_f32(f1, of);
-                zz[u] = bld_bf16(rz, oa);
+                dh[u] = bld_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB);
                 rv[u] = bld_bf16(rr, oa);
                 hh[u] = bld_bf16(rh, oa);
               }
@@ -272,9 +285,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
               for (int u = 0; u < 8; ++u) {
                 const int r = h8 + u;
                 const bool e = ok[r] && cok;
-                const uint32_t ob = e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB;
-                bst_bf16(gb, ob, dz[u] * zz[u] * (1.f - zz[u]));
-                bst_bf16(gb, e ? ob + (uint32_t)o.real * 2u : OOB,
+                bst_bf16(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + o.real + c) * 2u : OOB,
                          v[r] * hh[u] * rv[u] * (1.f - rv[u]));
                 bst_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB,
                         dh[u] + v[r] * rv[u]);

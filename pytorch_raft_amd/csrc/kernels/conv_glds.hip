@@ -78,7 +78,7 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
   // K loop channel-chunk-major, taps inner: the KH*KW shifted reads of one 64-channel slice of
   // the A rows follow each other while those rows are still in L2 (tap-major order re-fetched
   // the whole tile per tap: ~10x the input's bytes went to MALL / HBM on the 1x5 / 5x1 convs)
-  const int nchunk = a.cin_pad / BK;
+  const int nchunk = tile_nchunk(a, n0, BN);
   const int ntap = a.KH * a.KW;
   const int steps = ntap * nchunk;
   rsrc_t seg_rs[3];

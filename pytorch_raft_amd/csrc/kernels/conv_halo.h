@@ -82,7 +82,7 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_halo_kernel(ConvFwdArgs a) {
     const int qq = q < a.nseg ? q : 0;
     seg_rs[q] = make_rsrc(a.seg[qq].ptr, (uint32_t)P * a.seg[qq].stride * 2u);
   }
-  const int nchunk = a.cin_pad / BK;
+  const int nchunk = tile_nchunk(a, n0, BN);
   const int ntap = a.KH * a.KW;
   const int steps = ntap * nchunk;
   const uint32_t wave_off = __builtin_amdgcn_readfirstlane(wave * 64 * 16);

@@ -80,7 +80,7 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
     a_x[j] = r % a.W;
   }
 
-  const int nchunk = SMALLC ? 0 : a.cin_pad / BK;
+  const int nchunk = SMALLC ? 0 : tile_nchunk(a, n0, BN);
   const int ntap = a.KH * a.KW;
   const int steps = SMALLC ? a.kpad / BK : ntap * nchunk;   // channel-chunk-major (conv_glds.hip)
   // buffer descriptors: out-of-range offsets (padding taps, rows past P, weight rows past cout)
@@ -453,7 +453,7 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
     for (int o = 0; o < a.noseg; ++o) {
       const OSeg& q = a.oseg[o];
       tot += sz(q.ptr, q.stride, 4) + sz(q.ob, q.ob_stride, 2) + sz(q.gb, q.gb_stride, 2) +
-             sz(q.gf0, q.gf_stride, 4) + sz(q.gf1, q.gf_stride, 4);
+             sz(q.gz, q.gz_stride, 2) + sz(q.gf1, q.gf_stride, 4);
     }
     if (tot > g_scratch2_bytes) {
       if (g_scratch2) (void)hipFree(g_scratch2);
@@ -474,7 +474,7 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
         q.ptr = take(q.ptr, q.stride, 4);
         q.ob = take(q.ob, q.ob_stride, 2);
         q.gb = take(q.gb, q.gb_stride, 2);
-        q.gf0 = take(q.gf0, q.gf_stride, 4);
+        q.gz = take(q.gz, q.gz_stride, 2);
         q.gf1 = take(q.gf1, q.gf_stride, 4);
       }
     }

@@ -604,7 +604,8 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
   __syncthreads();
   // level-0 gradient row with the avg-pool adjoint of the coarser levels; two columns per thread
   // (4-B stores of bf16 pairs when the row is 4-B aligned, i.e. N even)
-  const int64_t row = ((int64_t)b * N + i) * N;
+  const int ldo = tl.ldo;
+  const int64_t row = ((int64_t)b * N + i) * ldo;
   const float inv_w = 1.0f / (float)W;
   auto cell = [&](int e) {
     const int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W;  // exact for e < 2^22
@@ -619,14 +620,16 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
   };
   if (out_bf16 && (N & 1) == 0) {
     uint32_t* Ob = reinterpret_cast<uint32_t*>((uint16_t*)out + row);
-    for (int e2 = threadIdx.x; e2 < N / 2; e2 += 256)
-      Ob[e2] = (uint32_t)raft_f32_to_bf16(cell(2 * e2)) | ((uint32_t)raft_f32_to_bf16(cell(2 * e2 + 1)) << 16);
+    for (int e2 = threadIdx.x; e2 < ldo / 2; e2 += 256)
+      Ob[e2] = 2 * e2 < N ? (uint32_t)raft_f32_to_bf16(cell(2 * e2)) |
+                                ((uint32_t)raft_f32_to_bf16(cell(2 * e2 + 1)) << 16)
+                          : 0u;
   } else if (out_bf16) {
     uint16_t* Ob = (uint16_t*)out + row;
-    for (int e = threadIdx.x; e < N; e += 256) Ob[e] = raft_f32_to_bf16(cell(e));
+    for (int e = threadIdx.x; e < ldo; e += 256) Ob[e] = e < N ? raft_f32_to_bf16(cell(e)) : (uint16_t)0;
   } else {
     float* O = (float*)out + row;
-    for (int e = threadIdx.x; e < N; e += 256) O[e] = cell(e);
+    for (int e = threadIdx.x; e < ldo; e += 256) O[e] = e < N ? cell(e) : 0.f;
   }
   __syncthreads();  // the next listed pixel reuses the planes
   }
@@ -774,11 +777,13 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_wave_kernel(TapList tl, T
     }
     __builtin_amdgcn_wave_barrier();
   }
-  const int64_t row = ((int64_t)b * N + i) * N;
+  const int ldo = tl.ldo;
+  const int64_t row = ((int64_t)b * N + i) * ldo;
   const float inv_w = 1.0f / (float)W;
   if (out_bf16 && (W & 1) == 0) {
     // pairs (x, x+1), x even: one coarse-level read serves both columns
     uint32_t* Ob = reinterpret_cast<uint32_t*>((uint16_t*)out + row);
+    for (int e2 = N / 2 + lane; e2 < ldo / 2; e2 += 64) Ob[e2] = 0u;
     for (int e2 = lane; e2 < N / 2; e2 += 64) {
       const int e = 2 * e2;
       const int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W;
@@ -811,10 +816,10 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_wave_kernel(TapList tl, T
   };
   if (out_bf16) {
     uint16_t* Ob = (uint16_t*)out + row;
-    for (int e = lane; e < N; e += 64) Ob[e] = raft_f32_to_bf16(cell(e));
+    for (int e = lane; e < ldo; e += 64) Ob[e] = e < N ? raft_f32_to_bf16(cell(e)) : (uint16_t)0;
   } else {
     float* O = (float*)out + row;
-    for (int e = lane; e < N; e += 64) O[e] = cell(e);
+    for (int e = lane; e < ldo; e += 64) O[e] = e < N ? cell(e) : 0.f;
   }
 }
 
@@ -997,8 +1002,9 @@ __global__ __launch_bounds__(256) void corr_tap_fold_box_kernel(TapList tl, BoxG
     __builtin_amdgcn_wave_barrier();
   }
   }
-  uint32_t* Ob = reinterpret_cast<uint32_t*>(out + ((int64_t)b * N + i) * N);
+  uint32_t* Ob = reinterpret_cast<uint32_t*>(out + ((int64_t)b * N + i) * tl.ldo);
   const float inv_w = 1.0f / (float)W;
+  for (int e2 = N / 2 + lane; e2 < tl.ldo / 2; e2 += 64) Ob[e2] = 0u;
   for (int e2 = lane; e2 < N / 2; e2 += 64) {
     const int e = 2 * e2;
     const int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W;

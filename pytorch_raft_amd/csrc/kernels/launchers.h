@@ -115,10 +115,11 @@ struct OSeg {
   int ry_stride;
   // fused ConvGRU gate backward on an fp32 segment (gate != 0; the segment itself is not
   // stored), per element (pixel, channel c < real) with v the dgrad value:
-  //  gate 1 -- q gate on the state gradient: g = *ptr + v (the final dh);
-  //            gb[c] = bf16(g z (1 - q^2)) (d pre-q), gf0[c] = g (q - h) (dz), gf1[c] = g (1 - z)
-  //  gate 2 -- z / r gates on d(r*h): gb[c] = bf16(gin[c] z (1 - z)), gb[real + c] =
-  //            bf16(v h r (1 - r)), gf1[c] += v r                 (ga0, ga1, ga2 = z, q|r, h)
+  //  gate 1 -- q / z gates on the state gradient g = *ptr + v (the final dh of a half-step):
+  //            gb[c] = bf16(g z (1 - q^2)) (d pre-q), gz[c] = bf16(g (q - h) z (1 - z)) (d pre-z),
+  //            gf1[c] = g (1 - z)                                   (ga0, ga1, ga2 = z, q, h)
+  //  gate 2 -- r gate on d(r*h) = v: gb[real + c] = bf16(v h r (1 - r)), gf1[c] += v r
+  //                                                               (ga1, ga2 = r, h)
   //  gate 3 -- the last accumulation into an fp32 gradient + the backward of the ReLU that
   //            produced this conv's input (ga0 = its output y): gb[c] = bf16([y > 0](gf1[c] + v))
   int gate;
@@ -126,12 +127,16 @@ struct OSeg {
   const uint16_t* ga1;
   const uint16_t* ga2;
   int ga_stride;
-  const float* gin;
   uint16_t* gb;
   int gb_stride;
-  float* gf0;
+  uint16_t* gz;
+  int gz_stride;
   float* gf1;
   int gf_stride;
+  // K prefix: this segment's columns read only the first kcin input channels (the rest of the
+  // packed K is zero for them); 0 = all.  A workgroup whose N tile lies in such segments runs
+  // only those K steps (one launch = two GEMMs sharing M and the leading K)
+  int kcin;
 };
 
 struct ConvFwdArgs {
@@ -163,6 +168,7 @@ struct ConvFwdArgs {
   int split;
   OSeg oseg[3];
   int noseg;
+  int kprefix;  // 1: some output segment has kcin != 0 (per-tile K steps, tile_nchunk)
   int nullmem;  // timing experiments only: operand loads read zeros (descriptor with 0 records)
 };
 
@@ -295,11 +301,19 @@ struct TapList {
   const uint16_t* dout[RAFT_MAX_WIN];  // (B,H,W,cbuf) bf16 lookup-output gradient per iteration
   int cbuf;
   int n;
+  int ldo;  // row pitch of the (B, N, ldo) output (elements, >= N, even for bf16 when N is);
+            // columns N..ldo-1 are written as zeros (the MFMA backward GEMMs' K padding)
 };
 int corr_tap_reduce_lds_bytes(int H, int W, int levels, int radius);
 // list: (1 + B*H*W) ints of scratch for the box fold's overflow list (nullptr: no box fold)
 bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, int radius,
                             float inv_sqrt_c, void* out, int out_bf16, int* list, hipStream_t stream);
+// all-pairs feature-map gradients (corr_bwd.hip): dc (B, N, ldc) bf16 from the fold (ldc % 64 ==
+// 0, zero columns past N), f1 / f2 (B, N, C) bf16 NHWC, f2t scratch (B, C, ldc);
+// g1 = dC F2, g2 = dC^T F1 as (B, N, C) bf16.  False for an unsupported geometry (C % 128 != 0)
+bool launch_corr_bwd_fmaps(const uint16_t* dc, int ldc, const uint16_t* f1, const uint16_t* f2,
+                           uint16_t* f2t, uint16_t* g1, uint16_t* g2, int B, int N, int C,
+                           hipStream_t stream);
 int corr_window_reduce_lds_bytes(int H, int W, int levels);
 // out: (B, N, N) fp32, or bf16 when out_bf16 (mixed-precision backward GEMMs)
 bool launch_corr_window_reduce(const WinList& wl, int levels, int B, int H, int W, int radius,

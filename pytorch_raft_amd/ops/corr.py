@@ -16,11 +16,17 @@ Design (MI355X-first, see `SURVEY.md` §7.4 item 3):
   tile's fmap2 bounding box) with the same token scheme for d(fmap1), d(fmap2 levels).
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
 
 from . import _ext
+
+
+# RAFT_CORR_BWD_GEMM=0: the feature-map gradients of the all-pairs correlation on torch.bmm
+# (hipBLASLt) instead of the MFMA kernel of corr_bwd.hip (A/B, tests)
+_NATIVE_BWD_GEMM = os.environ.get('RAFT_CORR_BWD_GEMM', '1') != '0'
 
 
 def available(required=False):
@@ -83,15 +89,22 @@ class _AllPairsBuild(torch.autograd.Function):
                                                h, w, len(st.pyramid), st.radius, 1.0 / math.sqrt(c),
                                                bf16)
             dcorr = dw if dcorr is None else dcorr + dw
+        # mixed precision, tap path only: the fold writes dC with rows padded to 64 columns and
+        # the two feature-map GEMMs run on the hand-written MFMA kernel (corr_bwd.hip)
+        native_gemm = (ctx.nhwc and bf16 and dcorr is None and bool(st.taps) and c % 128 == 0
+                       and _NATIVE_BWD_GEMM)
         if st.taps:
             dt = _ext.ops().corr_tap_reduce([x[0] for x in st.taps], [x[1] for x in st.taps],
                                             h, w, len(st.pyramid), st.radius, 1.0 / math.sqrt(c),
-                                            bf16)
+                                            bf16, 64 if native_gemm else 0)
             dcorr = dt if dcorr is None else dcorr + dt
         st.grad = None
         st.windows = []
         st.taps = []
         st.pyramid = None
+        if native_gemm:
+            g1, g2 = _ext.ops().corr_bwd_fmaps(dcorr, fmap1, fmap2)
+            return g1.permute(0, 3, 1, 2), g2.permute(0, 3, 1, 2), None, None
         if ctx.nhwc:
             # (B,N,C) operands: dF1 = dC F2, dF2 = dC^T F1 -> NHWC results, returned as
             # channels_last (B,C,H,W) bf16 like the encoder outputs they flow back into

@@ -154,6 +154,7 @@ def _pack_layers(params_by_layer, need_grad, dtype, design=FULL):
     (``_PackPlan``).  Extras: flow_head.conv2's bf16 pair tables for its VALU kernels, forward
     [t][o][c] and adjoint [t][c][o]."""
     w_out, wd_out, b_out, x_out = {}, {}, {}, {}
+    w_mod = {}   # per layer: the module weight as the fused conv sees it (in_sel / row_pad applied)
     F_ = torch.nn.functional
     for s in design.specs:
         ws = [w for w, _ in params_by_layer[s.name]]
@@ -166,12 +167,13 @@ def _pack_layers(params_by_layer, need_grad, dtype, design=FULL):
             ws = [F_.pad(w, (0, 0, 0, 0, 0, 0, 0, s.row_pad - w.shape[0])) for w in ws]
             bs = [F_.pad(b, (0, s.row_pad - b.shape[0])) for b in bs]
         w = ws[0] if len(ws) == 1 else torch.cat(ws, 0)
+        w_mod[s.name] = w
         b_out[s.name] = bs[0] if len(bs) == 1 else torch.cat(bs, 0)
         if s.small:
             w_out[s.name] = C.pack_weight_small(w, dtype=dtype)
         else:
             w_out[s.name] = C.pack_weight(w, s.in_real, s.in_pad, dtype=dtype)
-        if need_grad and not s.patch and not (design is FULL and s.name == 'fh2'):
+        if need_grad and not s.patch and not (design is FULL and s.name in _NO_ADJOINT):
             # adjoint conv: inputs = this layer's output channels, outputs = its inputs
             cout_pad = s.adj_pad or C.round_up(s.cout, 32)
             wt = w
@@ -192,7 +194,30 @@ def _pack_layers(params_by_layer, need_grad, dtype, design=FULL):
         if design is FULL and s.name == 'fh2':
             x_out['fh2f'] = w.permute(2, 3, 0, 1).reshape(18, 256).to(dtype)
             x_out['fh2d'] = w.permute(2, 3, 1, 0).reshape(9, 512).to(dtype)
+    if need_grad and design is FULL:
+        for tag in ('1', '2'):
+            x_out['zrq' + tag] = _zrq_adjoint(w_mod['zr' + tag], w_mod['q' + tag], dtype)
     return w_out, wd_out, b_out, x_out
+
+
+# layers whose plain adjoint is never packed: fh2 runs on its own VALU kernels, the z|r convs'
+# input gradient is part of the combined z|r + q adjoint (_zrq_adjoint)
+_NO_ADJOINT = ('fh2', 'zr1', 'zr2')
+
+
+def _zrq_adjoint(w_zr, w_q, dtype):
+    """Input gradient of a GRU half-step's z|r conv AND the motion-feature part of its q conv as
+    ONE conv: inputs [d pre-z|r (256) | d pre-q (128)], outputs [dh (128) | d mf (128)].  The q
+    conv reads [r*h | mf]; the gradient of r*h takes the gate path (OSeg gate 2), so the dh rows
+    are zero over the d pre-q columns and their output tiles run only the K prefix of d pre-z|r
+    (OSeg.kcin).  d mf gets both convs' contributions in one fp32 MFMA accumulation: no
+    read-modify-write pass of the fp32 motion-feature gradient between the two convs
+    (`core/update.py:45-60`)."""
+    a_zr = w_zr.flip(2, 3).transpose(0, 1)             # (256 [h | mf], 256 [z | r], kh, kw)
+    a_q = w_q.flip(2, 3).transpose(0, 1).clone()        # (256 [rh | mf], 128, kh, kw)
+    a_q[:HD] = 0                                        # 0 = padding in the index-tensor plans
+    wt = torch.cat([a_zr, a_q], 1).contiguous()         # (256, 384, kh, kw)
+    return C.pack_weight(wt, [3 * HD], [3 * HD], dtype=dtype)
 
 
 class _PackPlan:
@@ -675,11 +700,13 @@ class _UpdateIter(torch.autograd.Function):
             # deferred: summed over all iterations by one launch per conv (_Packed.flush_wgrad)
             pk.defer_wgrad(name, g, g_off, segs)
 
-        def dgrad(name, gsegs, outs, small=False, scale=1.0, gates=None):
+        def dgrad(name, gsegs, outs, small=False, scale=1.0, gates=None, wpk=None, kcin=None):
             """outs: list of (buffer fp32, offset, slot_cnt, real, acc) or, fusing the backward of a
             ReLU, (buffer bf16, offset, slot_cnt, real, 0, relu_out, relu_out_offset).
-            gates: per output, None or (mode, [z, q|r, h, dz_in, d_pre, dz_out, dh]) -- the ConvGRU
-            gate backward fused into that fp32 segment's epilogue (OSeg in launchers.h)."""
+            gates: per output, None or (mode, [a0, a1, a2, d_pre, d_pre_z, dh]) -- the ConvGRU
+            gate backward fused into that fp32 segment's epilogue (OSeg in launchers.h).
+            wpk: packed adjoint weight (default: the layer's); kcin: per output, the input-channel
+            prefix it reads (0 = all)."""
             s = SPEC[name]
             ry = [o[5] if len(o) > 5 else o[0] for o in outs]
             # relu offset -1 marks a plain (ungated) bf16 output
@@ -692,10 +719,11 @@ class _UpdateIter(torch.autograd.Function):
                     if gspec is not None:
                         gt.extend(gspec[1])
             ops.conv_dgrad_([g[0] for g in gsegs], [g[1] for g in gsegs], [g[2] for g in gsegs],
-                            pk.wd[name], s.k[0], s.k[1], s.pad[0], s.pad[1], 2 if small else 0,
+                            pk.wd[name] if wpk is None else wpk, s.k[0], s.k[1], s.pad[0],
+                            s.pad[1], 2 if small else 0,
                             float(scale), [o[0] for o in outs], [o[1] for o in outs],
                             [o[2] for o in outs], [o[3] for o in outs], [o[4] for o in outs],
-                            ry, roff, gmode, gt)
+                            ry, roff, gmode, gt, list(kcin or []))
 
         # ---- mask head (mask = 0.25 * conv(fm[256:]))
         if gmask is None:
@@ -731,11 +759,12 @@ class _UpdateIter(torch.autograd.Function):
         halves = (('2', (h1, z2, rh2, r2, q2)), ('1', (h0, z1, rh1, r1, q1)))
 
         def qgate(half):
-            """q-gate backward of a GRU half-step, fused into the epilogue of the dgrad that
-            finalises its output-state gradient: -> (spec, (d pre-q bf16, dz, dh of its input))."""
+            """q / z gate backward of a GRU half-step, fused into the epilogue of the dgrad that
+            finalises its output-state gradient: -> (spec, (d pre-q, d pre-z|r, dh of its input));
+            the r half of d pre-z|r is written by the q dgrad's epilogue (gate 2)."""
             hin, z, _, _, q = half
-            bufs = (_bf16(sh + (HD,), dev), _f32(sh + (HD,), dev), _f32(sh + (HD,), dev))
-            return (1, [z, q, hin, z, bufs[0], bufs[1], bufs[2]]), bufs
+            bufs = (_bf16(sh + (HD,), dev), _bf16(sh + (2 * HD,), dev), _f32(sh + (HD,), dev))
+            return (1, [z, q, hin, bufs[0], bufs[1], bufs[2]]), bufs
 
         if _GATES_FUSED:
             gspec, nxt = qgate(halves[0][1])
@@ -749,17 +778,15 @@ class _UpdateIter(torch.autograd.Function):
         # context gradient is handed to autograd by iteration 0
         ctx_g = st.ctx_g
         dmf = _f32(sh + (128,), dev)
-        first = 1  # the first dgrad into dmf (q2's) stores: no zero fill
         for k, (tag, (hin, z, rh, r, q)) in enumerate(halves):
             if _GATES_FUSED:
-                # the q gate ran in the epilogue of the previous dgrad (head / zr2); the z / r
-                # gates run in this q dgrad's d(r*h) epilogue, d(r*h) itself is never stored
-                dpre_q, dz, dhp = nxt
+                # the q / z gates ran in the epilogue of the previous dgrad (head / z|r+q); the r
+                # gate runs in this q dgrad's d(r*h) epilogue, d(r*h) itself is never stored
+                dpre_q, dpre_zr, dhp = nxt
                 wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (mf, 0, 128)])
-                dpre_zr = _bf16(sh + (2 * HD,), dev)
-                dgrad('q' + tag, [(dpre_q, 0, HD)],
-                      [(dhp, 0, HD, HD, 0), (dmf, 0, 128, 128, 1 - first)],
-                      gates=[(2, [z, r, hin, dz, dpre_zr, dz, dhp]), None])
+                dgrad('q' + tag, [(dpre_q, 0, HD)], [(dhp, 0, HD, HD, 0)],
+                      gates=[(2, [r, r, hin, dpre_zr, dpre_zr, dhp])],
+                      wpk=pk.wd['q' + tag][:HD])
             else:
                 dpre_q = _bf16(sh + (HD,), dev)
                 dz = _f32(sh + (HD,), dev)
@@ -767,27 +794,29 @@ class _UpdateIter(torch.autograd.Function):
                 ops.gru_q_bwd_(dh, z, q, hin, dpre_q, dz, dhp)
                 wgrad('q' + tag, dpre_q, 0, [(rh, 0, HD), (mf, 0, 128)])
                 drh = _f32(sh + (HD,), dev)
-                dgrad('q' + tag, [(dpre_q, 0, HD)],
-                      [(drh, 0, HD, HD, 0), (dmf, 0, 128, 128, 1 - first)])
+                dgrad('q' + tag, [(dpre_q, 0, HD)], [(drh, 0, HD, HD, 0)],
+                      wpk=pk.wd['q' + tag][:HD])
                 dpre_zr = _bf16(sh + (2 * HD,), dev)
                 ops.gru_zr_bwd_(drh, dz, z, r, hin, dpre_zr, dhp)
-            first = 0
             ctx_g.setdefault('q' + tag, []).append(dpre_q)
             ctx_g.setdefault('zr' + tag, []).append(dpre_zr)
             wgrad('zr' + tag, dpre_zr, 0, [(hin, 0, HD), (mf, 0, 128)])
-            zr_outs = [(dhp, 0, HD, HD, 1), (dmf, 0, 128, 128, 1)]
+            # one conv for dh (z|r adjoint, K prefix) and d mf (z|r + q adjoints)
+            zsegs = [(dpre_zr, 0, 2 * HD), (dpre_q, 0, HD)]
+            zw, zk = pk.x['zrq' + tag], [2 * HD, 0]
+            zr_outs = [(dhp, 0, HD, HD, 1), (dmf, 0, 128, 128, k)]
             if _GATES_FUSED and k == 0:
-                # dhp is now the final gradient of half-step 1's output: its q gate here
+                # dhp is now the final gradient of half-step 1's output: its q / z gates here
                 gspec, nxt = qgate(halves[1][1])
-                dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)], zr_outs, gates=[gspec, None])
+                dgrad('zr' + tag, zsegs, zr_outs, gates=[gspec, None], wpk=zw, kcin=zk)
             elif _GATES_FUSED:
                 # the last accumulation into dmf: the motion-encoder ReLU backward (its forward
                 # output is mf) in this epilogue -> bf16 d pre-activation, dmf is never re-read
                 dpre_conv = _bf16(sh + (128,), dev)
-                dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)], zr_outs,
-                      gates=[None, (3, [mf, mf, mf, dmf, dpre_conv, dmf, dmf])])
+                dgrad('zr' + tag, zsegs, zr_outs,
+                      gates=[None, (3, [mf, mf, mf, dpre_conv, dpre_conv, dmf])], wpk=zw, kcin=zk)
             else:
-                dgrad('zr' + tag, [(dpre_zr, 0, 2 * HD)], zr_outs)
+                dgrad('zr' + tag, zsegs, zr_outs, wpk=zw, kcin=zk)
             dh = dhp
         # ---- motion encoder
         if not _GATES_FUSED:

@@ -250,6 +250,42 @@ def test_onthefly_nhwc_bf16(ext_ops, hw, drift):
         assert torch.equal(runs[0][1], runs[1][1])
 
 
+def test_onthefly_slab_budget_falls_back_to_atomics(ext_ops, monkeypatch):
+    """The deterministic dF2 scratch (per-tile slab rows, ~170 KB per query pixel) is bounded by
+    RAFT_OTF_SLAB_GB: past it the call takes the float-atomic dF2 path, with the same gradients
+    up to summation order and no slab allocation (peak memory stays at the fmaps' scale)."""
+    b, c, h, w, radius, levels = 2, 256, 46, 62, 4, 4
+    g = torch.Generator(device='cpu').manual_seed(3)
+    f1 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    f2 = torch.randn(b, c, h, w, device=DEV, requires_grad=True)
+    c0 = _coords(b, h, w, spread=3.0, seed=5)
+    coords = [c0 + 0.5 * torch.randn(c0.shape, generator=g).clamp(-1, 1).to(DEV) for _ in range(3)]
+    gouts = [torch.randn(b, h, w, 384, device=DEV) for _ in coords]
+
+    def run():
+        f1.grad = f2.grad = None
+        blk = AlternateCorrBlock(f1, f2, num_levels=levels, radius=radius, impl='hip',
+                                 precision='bf16')
+        outs = [blk.lookup_nhwc(co, 384) for co in coords]
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        sum((o.float() * gg).sum() for o, gg in zip(outs, gouts)).backward()
+        torch.cuda.synchronize()
+        return f1.grad.clone(), f2.grad.clone(), torch.cuda.max_memory_allocated() - base
+
+    g1_s, g2_s, peak_slab = run()
+    monkeypatch.setenv('RAFT_OTF_SLAB_GB', '0.001')
+    g1_a, g2_a, peak_atomic = run()
+    assert _rel(g1_a, g1_s) < 1e-5 and _rel(g2_a, g2_s) < 1e-4
+    caps, hh, ww = 0, h, w
+    for lvl in range(levels):
+        caps += min(hh * ww, 1024 if lvl == 0 else 576)
+        hh, ww = hh // 2, ww // 2
+    slab_bytes = b * ((h + 7) // 8) * ((w + 7) // 8) * caps * c * 4
+    assert peak_atomic < peak_slab - 0.5 * slab_bytes, (peak_atomic, peak_slab, slab_bytes)
+
+
 @pytest.mark.parametrize('mask_dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('hw', [(8, 9), (46, 62), (5, 70)])
 def test_convex_upsample_fwd_bwd(ext_ops, mask_dtype, hw):
@@ -415,6 +451,51 @@ def test_tap_reduce_box_path(ext_ops, radius, levels, hw, drift):
     err = (got.float() - ref).abs()
     assert (err <= ref.abs() * 2.0 ** -8 + 1e-6).all(), err.max().item()
     assert torch.equal(ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, True), got)
+
+
+@pytest.mark.parametrize('radius,levels,hw,bf16', [(4, 4, (46, 62), True), (4, 4, (23, 31), True),
+                                                   (3, 4, (24, 31), False), (4, 3, (13, 19), True)])
+def test_tap_reduce_padded_pitch(ext_ops, radius, levels, hw, bf16):
+    """pitch_mult: every fold variant (box at even W, workgroup / listed at odd W) writes rows of
+    round_up(N, 64) with the same first N columns and zero padding."""
+    h, w = hw
+    b, n = 2, hw[0] * hw[1]
+    coords = [_coords(b, h, w, seed=s) for s in range(5)]
+    douts = [torch.randn(b, h, w, 384, device=DEV).to(torch.bfloat16) for _ in coords]
+    s = 1.0 / 16
+    ref = ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, bf16)
+    got = ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, bf16, 64)
+    ld = (n + 63) // 64 * 64
+    assert got.shape == (b, n, ld)
+    assert torch.equal(got[..., :n], ref)
+    assert (got[..., n:] == 0).all()
+
+
+@pytest.mark.parametrize('b,hw,c', [(2, (46, 62), 256), (3, (7, 9), 128), (1, (23, 31), 256)])
+def test_corr_bwd_fmaps_matches_fp32(ext_ops, b, hw, c):
+    """corr_bwd.hip: dF1 = dC F2 and dF2 = dC^T F1 (the all-pairs correlation's feature-map
+    gradients, `core/corr.py:52-60`) on bf16 operands vs fp32 matmuls of the same bf16 values,
+    with a padded dC pitch (odd N: padded K and M tails)."""
+    h, w = hw
+    n = h * w
+    ld = (n + 63) // 64 * 64
+    g = torch.Generator(device=DEV).manual_seed(11)
+    dc = torch.zeros(b, n, ld, device=DEV, dtype=torch.bfloat16)
+    dc[..., :n] = torch.randn(b, n, n, device=DEV, generator=g).to(torch.bfloat16)
+    f1 = torch.randn(b, h, w, c, device=DEV, generator=g).to(torch.bfloat16)
+    f2 = torch.randn(b, h, w, c, device=DEV, generator=g).to(torch.bfloat16)
+    g1, g2 = ext_ops.corr_bwd_fmaps(dc, f1, f2)
+    d = dc[..., :n].float()
+    r1 = torch.bmm(d, f2.float().view(b, n, c)).view(b, h, w, c)
+    r2 = torch.bmm(d.transpose(1, 2), f1.float().view(b, n, c)).view(b, h, w, c)
+    for got, ref in ((g1, r1), (g2, r2)):
+        assert got.shape == ref.shape and got.dtype == torch.bfloat16
+        # fp32 accumulation, one bf16 rounding of the result
+        err = (got.float() - ref).abs().max().item()
+        assert err <= 2.0 ** -7 * ref.abs().max().item(), err
+    # deterministic: no atomics
+    g1b, g2b = ext_ops.corr_bwd_fmaps(dc, f1, f2)
+    assert torch.equal(g1, g1b) and torch.equal(g2, g2b)
 
 
 @pytest.mark.parametrize('convention', ['reference', 'exact'])
