@@ -152,9 +152,11 @@ def main(argv=None):
             return _orig(*x, **k)
         import pytorch_raft_amd.engine.trainer as T
         T.sequence_loss = _torch_loss
-    # the graphed step replays the decode (bf16: fused update block; fp32: split-bf16 MFMA convs,
-    # no MIOpen call); fp16 steps (GradScaler) run eagerly
-    use_graph = (device.type == 'cuda' and a.hipgraph and a.impl == 'hip' and a.precision != 'fp16')
+    # the graphed step replays the decode (bf16 / fp16: fused update block, fp16 with the
+    # device-side GradScaler inside the fused AdamW step; fp32: split-bf16 MFMA convs, no MIOpen
+    # call)
+    use_graph = device.type == 'cuda' and a.hipgraph and a.impl == 'hip'
+
     st = TrainState(model, margs, device, graph_ready=use_graph)
 
     h, w = a.size

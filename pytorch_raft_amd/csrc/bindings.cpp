@@ -162,18 +162,19 @@ void corr_lookup_nhwc_(const std::vector<Tensor>& pyr, const Tensor& coords, int
   TORCH_CHECK(L.h[0] == H && L.w[0] == W, "pyramid level 0 must match coords grid");
   const int64_t D = 2 * radius + 1;
   const int levels = (int)pyr.size();
-  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.scalar_type() == at::kBFloat16 &&
+  const bool f16 = out.scalar_type() == at::kHalf;
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && (f16 || out.scalar_type() == at::kBFloat16) &&
                   out.dim() == 4 && out.size(0) == B && out.size(1) == H && out.size(2) == W &&
                   out.size(3) >= levels * D * D,
-              "out must be a contiguous bf16 (B,H,W,C>=L*D*D) buffer");
+              "out must be a contiguous bf16 / fp16 (B,H,W,C>=L*D*D) buffer");
+  TORCH_CHECK(!(f16 && pyr_bf16), "fp16 taps come from the fp32 pyramid");
   const int64_t Cb = out.size(3);
   TORCH_CHECK(Cb % 8 == 0, "out channels must be a multiple of 8");
   // LDS-tiled kernel writes whole pixel rows including the zero padding
   TORCH_CHECK(launch_corr_lookup_tile(cp.data(), L.h.data(), L.w.data(), levels,
-                                      coords.data_ptr<float>(),
-                                      reinterpret_cast<uint16_t*>(out.data_ptr<at::BFloat16>()),
+                                      coords.data_ptr<float>(), reinterpret_cast<uint16_t*>(out.data_ptr()),
                                       (int)Cb, (int)B, (int)H, (int)W, (int)radius, pyr_bf16,
-                                      cur_stream()),
+                                      f16 ? 1 : 0, cur_stream()),
               "unsupported radius");
 }
 
@@ -466,10 +467,12 @@ void corr_otf_window_bwd_(const Tensor& f1, const std::vector<Tensor>& f2,
 }
 
 // ------------------------------------------------------------------ convex upsample
+// 0 fp32, 1 bf16, 2 fp16 (fp16 masks: the NHWC fused-path kernels only)
 int mask_kind(const Tensor& m) {
-  TORCH_CHECK(m.scalar_type() == at::kFloat || m.scalar_type() == at::kBFloat16,
-              "mask must be float32 or bfloat16");
-  return m.scalar_type() == at::kBFloat16 ? 1 : 0;
+  TORCH_CHECK(m.scalar_type() == at::kFloat || m.scalar_type() == at::kBFloat16 ||
+                  m.scalar_type() == at::kHalf,
+              "mask must be float32, bfloat16 or float16");
+  return m.scalar_type() == at::kBFloat16 ? 1 : (m.scalar_type() == at::kHalf ? 2 : 0);
 }
 
 // the NHWC vector kernels move the mask / dmask in 8-B and flow / dout / out in 16-B accesses:
@@ -499,6 +502,7 @@ Tensor convex_up_fwd(const Tensor& flow, const Tensor& mask, bool nhwc) {
                               out.data_ptr<float>(), (int)B, (int)H, (int)W, cur_stream());
     return out;
   }
+  TORCH_CHECK(mask_kind(mask) != 2, "fp16 masks need the aligned NHWC layout");
   launch_convex_up_fwd(flow.data_ptr<float>(), mask.data_ptr(), mask_kind(mask), 576 * HW,
                        nhwc ? 1 : HW, nhwc ? 576 : 1, out.data_ptr<float>(), (int)B, (int)H,
                        (int)W, cur_stream());
@@ -526,6 +530,7 @@ std::vector<Tensor> convex_up_bwd(const Tensor& flow, const Tensor& mask, const 
                               dflow.data_ptr<float>(), (int)B, (int)H, (int)W, cur_stream());
     return {dflow, dmask};
   }
+  TORCH_CHECK(mask_kind(mask) != 2, "fp16 masks need the aligned NHWC layout");
   launch_convex_up_bwd(flow.data_ptr<float>(), mask.data_ptr(), mask_kind(mask), 576 * HW,
                        nhwc ? 1 : HW, nhwc ? 576 : 1, dout.data_ptr<float>(), dmask.data_ptr(),
                        wbuf.data_ptr<float>(), dflow.data_ptr<float>(), (int)B, (int)H, (int)W,
@@ -631,6 +636,15 @@ void check_nhwc(const Tensor& t, int64_t B, int64_t H, int64_t W, const char* na
               " must be (B,H,W,C) matching the conv geometry");
 }
 
+// 16-bit operand type of the MFMA kernels: bf16 (default) or fp16 (fp16 autocast)
+at::ScalarType op16(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf,
+              "16-bit operands must be bfloat16 or float16, got ", t.scalar_type());
+  return t.scalar_type();
+}
+const uint16_t* u16(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* u16m(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
 void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_off,
                const std::vector<int64_t>& in_cnt, const Tensor& wpk,
                const c10::optional<Tensor>& bias, int64_t kh, int64_t kw, int64_t ph, int64_t pw,
@@ -643,10 +657,12 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   const int64_t B = ins[0].size(0), H = ins[0].size(1), W = ins[0].size(2);
   c10::DeviceGuard g(ins[0].device());
   ConvFwdArgs a{};
+  const at::ScalarType st = op16(ins[0]);
+  TORCH_CHECK(!epi_f16((int)epi), "pass the epilogue kind; fp16 follows the operand dtype");
   a.nseg = (int)ins.size();
   int64_t cin_pad = 0;
   for (size_t s = 0; s < ins.size(); ++s) {
-    check_nhwc(ins[s], B, H, W, "conv input", at::kBFloat16);
+    check_nhwc(ins[s], B, H, W, "conv input", st);
     // a segment may run past the tensor's last channel (a 96-channel tensor in a 128-channel K
     // slot): the kernels read the channels that are not there as zeros
     const int64_t present = std::min<int64_t>(in_cnt[s], ins[s].size(3) - in_off[s]);
@@ -656,7 +672,7 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
     TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
     if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 64 == 0, "segment channels must be a multiple of 64");
     TORCH_CHECK(ins[s].numel() * 2 < (int64_t(1) << 31), "conv input exceeds the 2 GiB buffer-descriptor range");
-    a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
+    a.seg[s].ptr = u16(ins[s]) + in_off[s];
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
     a.seg[s].real = (int)present;
@@ -667,19 +683,19 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   if (cin_small) TORCH_CHECK(ins.size() == 1 && cin_small <= in_cnt[0], "small-Cin path takes one segment");
   a.B = (int)B; a.H = (int)H; a.W = (int)W;
   a.KH = (int)kh; a.KW = (int)kw; a.PH = (int)ph; a.PW = (int)pw;
-  TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == at::kBFloat16 && wpk.dim() == 2,
-              "packed weight must be a contiguous bf16 (Npad, Kpad) tensor");
+  TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == st && wpk.dim() == 2,
+              "packed weight must be a contiguous (Npad, Kpad) tensor of the operand dtype");
   const int64_t kneed = cin_small ? ((kh * kw * cin_small + 63) / 64) * 64 : kh * kw * cin_pad;
   TORCH_CHECK(wpk.size(1) == kneed, "packed weight K mismatch: ", wpk.size(1), " vs ", kneed);
   // rows past cout are never read (range-checked descriptors in every kernel)
   TORCH_CHECK(wpk.size(0) >= cout, "packed weight has too few rows");
-  a.wpk = reinterpret_cast<const uint16_t*>(wpk.data_ptr<at::BFloat16>());
+  a.wpk = u16(wpk);
   a.kpad = (int)wpk.size(1);
   if (bias.has_value() && bias->defined() && bias->dim() == 4) {
     // per-pixel bias map (B,H,W,>=cout) fp32 or bf16: the precomputed context part of a ConvGRU conv
     TORCH_CHECK(epi == EPI_GRU_ZR || epi == EPI_GRU_Q, "a per-pixel bias map needs a GRU epilogue");
-    const bool bm16 = bias->scalar_type() == at::kBFloat16;
-    check_nhwc(*bias, B, H, W, "bias map", bm16 ? at::kBFloat16 : at::kFloat);
+    const bool bm16 = bias->scalar_type() != at::kFloat;
+    check_nhwc(*bias, B, H, W, "bias map", bm16 ? st : at::kFloat);
     TORCH_CHECK(bias->size(3) >= cout, "bias map has too few channels");
     TORCH_CHECK(bias->numel() * bias->element_size() < (int64_t(1) << 31),
                 "bias map exceeds the 2 GiB buffer-descriptor range");
@@ -691,6 +707,8 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
     TORCH_CHECK(bias->numel() >= cout, "bias too short");
     a.bias = bias->data_ptr<float>();
   }
+  const int ef16 = st == at::kHalf ? EPI_F16 : 0;
+  TORCH_CHECK(!ef16 || cin_small == 0, "fp16 operands: no small-Cin path");
   a.cout = (int)cout;
   a.scale = (float)scale;
   a.split = (int)split;
@@ -718,12 +736,12 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   void** optr[3] = {&a.out0, &a.out1, &a.out2};
   int* ostr[3] = {&a.out0_stride, &a.out1_stride, &a.out2_stride};
   for (size_t o = 0; o < outs.size(); ++o) {
-    check_nhwc(outs[o], B, H, W, "conv output", f32out ? at::kFloat : at::kBFloat16);
+    check_nhwc(outs[o], B, H, W, "conv output", f32out ? at::kFloat : st);
     TORCH_CHECK(outs[o].numel() * outs[o].element_size() < (int64_t(1) << 31),
                 "conv output exceeds the 2 GiB buffer-descriptor range");
     TORCH_CHECK(out_off[o] >= 0 && out_off[o] + out_ch[o] <= outs[o].size(3), "output slice out of range");
     *optr[o] = f32out ? (void*)(outs[o].data_ptr<float>() + out_off[o])
-                      : (void*)(reinterpret_cast<uint16_t*>(outs[o].data_ptr<at::BFloat16>()) + out_off[o]);
+                      : (void*)(u16m(outs[o]) + out_off[o]);
     *ostr[o] = (int)outs[o].size(3);
   }
   const int64_t need_aux = (epi == EPI_GRU_ZR) ? 1 : (epi == EPI_GRU_Q ? 2 : 0);
@@ -731,14 +749,14 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   const uint16_t** aptr[2] = {&a.aux0, &a.aux1};
   int* astr[2] = {&a.aux0_stride, &a.aux1_stride};
   for (size_t o = 0; o < aux.size(); ++o) {
-    check_nhwc(aux[o], B, H, W, "conv aux", at::kBFloat16);
+    check_nhwc(aux[o], B, H, W, "conv aux", st);
     TORCH_CHECK(aux[o].numel() * 2 < (int64_t(1) << 31), "conv aux exceeds the 2 GiB buffer-descriptor range");
     const int64_t ch = (epi == EPI_GRU_ZR) ? cout - split : cout;
     TORCH_CHECK(aux_off[o] >= 0 && aux_off[o] + ch <= aux[o].size(3), "aux slice out of range");
-    *aptr[o] = reinterpret_cast<const uint16_t*>(aux[o].data_ptr<at::BFloat16>()) + aux_off[o];
+    *aptr[o] = u16(aux[o]) + aux_off[o];
     *astr[o] = (int)aux[o].size(3);
   }
-  TORCH_CHECK(launch_conv_fwd(a, (int)epi, (int)bn, cin_small != 0, cur_stream()), "bad epilogue");
+  TORCH_CHECK(launch_conv_fwd(a, (int)epi | ef16, (int)bn, cin_small != 0, cur_stream()), "bad epilogue");
 }
 
 std::vector<int64_t> conv_tune_table() {
@@ -887,6 +905,8 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
   const int64_t B = g0.size(0), H = g0.size(1), W = g0.size(2);
   c10::DeviceGuard gd(g0.device());
   ConvWgradArgs a{};
+  const at::ScalarType st = op16(gs.at(0));
+  a.f16 = st == at::kHalf ? 1 : 0;
   WgradItems it{};
   WgradTapArgs ta{};
   it.n = (int)n;
@@ -913,19 +933,19 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
   }
   for (int64_t i = 0; i < n; ++i) {
     const Tensor& g = gs[i];
-    check_nhwc(g, B, H, W, "grad", at::kBFloat16);
+    check_nhwc(g, B, H, W, "grad", st);
     TORCH_CHECK(g.size(3) == a.g_stride, "all items' grads must share a layout");
     TORCH_CHECK(g_off >= 0 && g_off % 8 == 0 && g_off + (cout + 7) / 8 * 8 <= g.size(3),
                 "grad slice out of range (cout rounded up to 8 channels must fit the row)");
     TORCH_CHECK(g.numel() * 2 < (int64_t(1) << 31), "grad exceeds the 2 GiB buffer-descriptor range");
-    it.g[i] = reinterpret_cast<const uint16_t*>(g.data_ptr<at::BFloat16>()) + g_off;
+    it.g[i] = u16(g) + g_off;
     for (int64_t s = 0; s < nseg; ++s) {
       const Tensor& x = ins[i * nseg + s];
-      check_nhwc(x, B, H, W, "wgrad input", at::kBFloat16);
+      check_nhwc(x, B, H, W, "wgrad input", st);
       TORCH_CHECK(x.size(3) == a.seg[s].stride, "all items' inputs must share a layout");
       TORCH_CHECK(in_off[s] + in_cnt[s] <= x.size(3), "segment out of range");
       TORCH_CHECK(x.numel() * 2 < (int64_t(1) << 31), "wgrad input exceeds the 2 GiB buffer-descriptor range");
-      it.seg[i][s] = reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>()) + in_off[s];
+      it.seg[i][s] = u16(x) + in_off[s];
     }
   }
   a.cin_pad = (int)cin_pad;
@@ -995,10 +1015,12 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   const int64_t B = ins[0].size(0), H = ins[0].size(1), W = ins[0].size(2);
   c10::DeviceGuard g(ins[0].device());
   ConvFwdArgs a{};
+  const at::ScalarType st = op16(ins[0]);
+  const int ef16 = st == at::kHalf ? EPI_F16 : 0;
   a.nseg = (int)ins.size();
   int64_t cin_pad = 0;
   for (size_t s = 0; s < ins.size(); ++s) {
-    check_nhwc(ins[s], B, H, W, "dgrad input", at::kBFloat16);
+    check_nhwc(ins[s], B, H, W, "dgrad input", st);
     // a segment may run past the tensor's last channel (a 96-channel tensor in a 128-channel K
     // slot): the kernels read the channels that are not there as zeros
     const int64_t present = std::min<int64_t>(in_cnt[s], ins[s].size(3) - in_off[s]);
@@ -1008,7 +1030,7 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     TORCH_CHECK(in_off[s] % 8 == 0 && ins[s].size(3) % 8 == 0, "segments must be 16-byte aligned");
     if (cin_small == 0) TORCH_CHECK(in_cnt[s] % 64 == 0, "segment channels must be a multiple of 64");
     TORCH_CHECK(ins[s].numel() * 2 < (int64_t(1) << 31), "conv input exceeds the 2 GiB buffer-descriptor range");
-    a.seg[s].ptr = reinterpret_cast<const uint16_t*>(ins[s].data_ptr<at::BFloat16>()) + in_off[s];
+    a.seg[s].ptr = u16(ins[s]) + in_off[s];
     a.seg[s].stride = (int)ins[s].size(3);
     a.seg[s].cnt = (int)in_cnt[s];
     a.seg[s].real = (int)present;
@@ -1021,8 +1043,8 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   int64_t cout = 0;
   a.noseg = (int)outs.size();
   for (size_t o = 0; o < outs.size(); ++o) {
-    const bool relu_mode = outs[o].scalar_type() == at::kBFloat16;
-    check_nhwc(outs[o], B, H, W, "dgrad output", relu_mode ? at::kBFloat16 : at::kFloat);
+    const bool relu_mode = outs[o].scalar_type() != at::kFloat;
+    check_nhwc(outs[o], B, H, W, "dgrad output", relu_mode ? st : at::kFloat);
     TORCH_CHECK(outs[o].numel() * outs[o].element_size() < (int64_t(1) << 31),
                 "dgrad output exceeds the 2 GiB buffer-descriptor range");
     // the epilogue picks the output segment per 32-column MFMA tile
@@ -1033,7 +1055,7 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
       // plain bf16 output (relu_off < 0: no ReLU gate)
       TORCH_CHECK(!out_acc[o], "the bf16 dgrad output cannot accumulate");
       a.oseg[o].ptr = nullptr;
-      a.oseg[o].ob = reinterpret_cast<uint16_t*>(outs[o].data_ptr<at::BFloat16>()) + out_off[o];
+      a.oseg[o].ob = u16m(outs[o]) + out_off[o];
       a.oseg[o].ob_stride = (int)outs[o].size(3);
       a.oseg[o].ry = nullptr;
       a.oseg[o].ry_stride = 0;
@@ -1041,14 +1063,14 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
       // bf16 output = relu-gated gradient; relu_y[o] is the forward relu output of these channels
       TORCH_CHECK(o < relu_y.size(), "bf16 dgrad output needs its relu output tensor");
       const Tensor& y = relu_y[o];
-      check_nhwc(y, B, H, W, "relu output", at::kBFloat16);
+      check_nhwc(y, B, H, W, "relu output", st);
       TORCH_CHECK(y.numel() * 2 < (int64_t(1) << 31), "relu output exceeds the 2 GiB descriptor range");
       TORCH_CHECK(relu_off[o] >= 0 && relu_off[o] + out_real[o] <= y.size(3), "relu output slice out of range");
       TORCH_CHECK(!out_acc[o], "the relu-gated bf16 output cannot accumulate");
       a.oseg[o].ptr = nullptr;
-      a.oseg[o].ob = reinterpret_cast<uint16_t*>(outs[o].data_ptr<at::BFloat16>()) + out_off[o];
+      a.oseg[o].ob = u16m(outs[o]) + out_off[o];
       a.oseg[o].ob_stride = (int)outs[o].size(3);
-      a.oseg[o].ry = reinterpret_cast<const uint16_t*>(y.data_ptr<at::BFloat16>()) + relu_off[o];
+      a.oseg[o].ry = u16(y) + relu_off[o];
       a.oseg[o].ry_stride = (int)y.size(3);
     } else {
       a.oseg[o].ptr = outs[o].data_ptr<float>() + out_off[o];
@@ -1081,12 +1103,12 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     const Tensor& gf1 = gate_t[gt + 5];
     gt += 6;
     for (const Tensor* t : {&z, &qr, &h}) {
-      check_nhwc(*t, B, H, W, "gate input", at::kBFloat16);
+      check_nhwc(*t, B, H, W, "gate input", st);
       TORCH_CHECK(t->size(3) == z.size(3) && t->size(3) >= real, "gate inputs must share a layout");
       TORCH_CHECK(t->numel() * 2 < (int64_t(1) << 31), "gate input exceeds the 2 GiB descriptor range");
     }
     for (const Tensor* t : {&gbo, &gzo}) {
-      check_nhwc(*t, B, H, W, "gate output", at::kBFloat16);
+      check_nhwc(*t, B, H, W, "gate output", st);
       TORCH_CHECK(t->numel() * 2 < (int64_t(1) << 31), "gate output exceeds the 2 GiB descriptor range");
     }
     TORCH_CHECK(gbo.size(3) >= (mode == 2 ? 2 * real : real), "gate d-pre output too narrow");
@@ -1094,13 +1116,13 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     check_nhwc(gf1, B, H, W, "gate state gradient", at::kFloat);
     TORCH_CHECK(gf1.size(3) >= real && gf1.numel() * 4 < (int64_t(1) << 31), "gate state gradient");
     a.oseg[o].gate = mode;
-    a.oseg[o].ga0 = reinterpret_cast<const uint16_t*>(z.data_ptr<at::BFloat16>());
-    a.oseg[o].ga1 = reinterpret_cast<const uint16_t*>(qr.data_ptr<at::BFloat16>());
-    a.oseg[o].ga2 = reinterpret_cast<const uint16_t*>(h.data_ptr<at::BFloat16>());
+    a.oseg[o].ga0 = u16(z);
+    a.oseg[o].ga1 = u16(qr);
+    a.oseg[o].ga2 = u16(h);
     a.oseg[o].ga_stride = (int)z.size(3);
-    a.oseg[o].gb = reinterpret_cast<uint16_t*>(gbo.data_ptr<at::BFloat16>());
+    a.oseg[o].gb = u16m(gbo);
     a.oseg[o].gb_stride = (int)gbo.size(3);
-    a.oseg[o].gz = reinterpret_cast<uint16_t*>(gzo.data_ptr<at::BFloat16>());
+    a.oseg[o].gz = u16m(gzo);
     a.oseg[o].gz_stride = (int)gzo.size(3);
     a.oseg[o].gf1 = gf1.data_ptr<float>();
     a.oseg[o].gf_stride = (int)gf1.size(3);
@@ -1121,19 +1143,20 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   TORCH_CHECK(gt == gate_t.size(), "unused gate tensors");
   a.cout = (int)cout;
   const int bn = (cout % 128 == 0) ? 128 : 64;
-  TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == at::kBFloat16 && wpk.dim() == 2,
-              "packed weight must be a contiguous bf16 (Npad, Kpad) tensor");
+  TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == st && wpk.dim() == 2,
+              "packed weight must be a contiguous (Npad, Kpad) tensor of the operand dtype");
   const int64_t kneed = cin_small ? ((kh * kw * cin_small + 63) / 64) * 64 : kh * kw * cin_pad;
   TORCH_CHECK(wpk.size(1) == kneed, "packed dgrad weight K mismatch: ", wpk.size(1), " vs ", kneed);
   TORCH_CHECK(wpk.size(0) >= cout, "packed dgrad weight has too few rows");
-  a.wpk = reinterpret_cast<const uint16_t*>(wpk.data_ptr<at::BFloat16>());
+  a.wpk = u16(wpk);
   a.kpad = (int)wpk.size(1);
   a.bias = nullptr;
   a.scale = (float)scale;
   bool any_gate = false;
   for (int o = 0; o < a.noseg; ++o) any_gate = any_gate || a.oseg[o].gate != 0;
   TORCH_CHECK(!(any_gate && cin_small), "gated dgrad needs the 64-channel K path");
-  TORCH_CHECK(launch_conv_fwd(a, any_gate ? EPI_DGRAD_GATE : EPI_DGRAD, bn, cin_small != 0, cur_stream()),
+  TORCH_CHECK(!ef16 || cin_small == 0, "fp16 operands: no small-Cin path");
+  TORCH_CHECK(launch_conv_fwd(a, (any_gate ? EPI_DGRAD_GATE : EPI_DGRAD) | ef16, bn, cin_small != 0, cur_stream()),
               "dgrad launch");
 }
 
@@ -1371,14 +1394,14 @@ void sum_bf16_(const std::vector<Tensor>& ins, const c10::optional<Tensor>& carr
   const int64_t numel = out.numel();
   TORCH_CHECK(numel % 8 == 0, "sum_bf16_: numel must be a multiple of 8");
   TORCH_CHECK(out.is_cuda() && out.is_contiguous() &&
-                  (out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat),
-              "sum_bf16_: out must be a contiguous bf16 / fp32 GPU tensor");
+                  (out.scalar_type() == op16(ins[0]) || out.scalar_type() == at::kFloat),
+              "sum_bf16_: out must be a contiguous GPU tensor of the summands' dtype or fp32");
   BfPtrs p{};
   for (size_t k = 0; k < ins.size(); ++k) {
-    TORCH_CHECK(ins[k].is_cuda() && ins[k].is_contiguous() && ins[k].scalar_type() == at::kBFloat16 &&
+    TORCH_CHECK(ins[k].is_cuda() && ins[k].is_contiguous() && ins[k].scalar_type() == ins[0].scalar_type() &&
                     ins[k].numel() == numel && ins[k].device() == out.device(),
-                "sum_bf16_: summands must be contiguous bf16 tensors of the output's size");
-    p.p[k] = bf16p(ins[k]);
+                "sum_bf16_: summands must be contiguous 16-bit tensors of one dtype and the output's size");
+    p.p[k] = u16(ins[k]);
     TORCH_CHECK(reinterpret_cast<uintptr_t>(p.p[k]) % 16 == 0, "sum_bf16_: summands must be 16-byte aligned");
   }
   TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "sum_bf16_: out must be 16-byte aligned");
@@ -1391,7 +1414,7 @@ void sum_bf16_(const std::vector<Tensor>& ins, const c10::optional<Tensor>& carr
   }
   c10::DeviceGuard gd(out.device());
   launch_sum_bf16(p, (int)ins.size(), cp, out.data_ptr(), out.scalar_type() == at::kFloat, numel,
-                  cur_stream());
+                  ins[0].scalar_type() == at::kHalf, cur_stream());
 }
 
 // flow (B,2,H,W) fp32 -> flowb (B,H,W,8) bf16 [fx, fy, 0...]; optionally slot[..., off:off+2] = flow
@@ -1416,55 +1439,91 @@ void flow_prep_(const Tensor& flow, const Tensor& flowb, const c10::optional<Ten
 
 // AdamW over lists of fp32 tensors with the global-norm gradient clip folded in (adamw.hip);
 // returns the device pair [clip coefficient, total gradient norm]
+// One AdamW step over every parameter group (global-norm clip over all of them), with the fp16
+// GradScaler folded in: inv_scale (1/S, device) unscales the gradients inside the kernels, and an
+// overflow (non-finite norm) skips the whole step on the device and sets found_inf.  Per group g:
+// lr_t[g] (a one-element fp32 device tensor, or an empty tensor for the host value lr[g]),
+// beta1/beta2/eps/wd[g]; per tensor: its group index and its device step counter (fp32, 1 elem).
+// Returns (gradient multiplier, total unscaled norm, found_inf) as a 3-element device tensor.
 Tensor adamw_step_(const std::vector<Tensor>& params, const std::vector<Tensor>& grads,
                    const std::vector<Tensor>& exp_avg, const std::vector<Tensor>& exp_avg_sq,
-                   const c10::optional<Tensor>& lr_t, double lr, double beta1, double beta2,
-                   double eps, double wd, double bc1, double bc2, double max_norm) {
+                   const std::vector<Tensor>& steps, const std::vector<int64_t>& group_of,
+                   const std::vector<Tensor>& lr_t, const std::vector<double>& lr,
+                   const std::vector<double>& beta1, const std::vector<double>& beta2,
+                   const std::vector<double>& eps, const std::vector<double>& wd, double max_norm,
+                   const c10::optional<Tensor>& inv_scale, const c10::optional<Tensor>& found_inf,
+                   bool write_grad) {
   const size_t T = params.size();
-  TORCH_CHECK(T > 0 && grads.size() == T && exp_avg.size() == T && exp_avg_sq.size() == T,
+  TORCH_CHECK(T > 0 && grads.size() == T && exp_avg.size() == T && exp_avg_sq.size() == T &&
+                  steps.size() == T && group_of.size() == T,
               "adamw: tensor lists must have the same length");
+  const size_t G = lr.size();
+  TORCH_CHECK(G >= 1 && lr_t.size() == G && beta1.size() == G && beta2.size() == G &&
+                  eps.size() == G && wd.size() == G,
+              "adamw: per-group hyper-parameter lists must have the same length");
   const auto dev = params[0].device();
-  for (size_t i = 0; i < T; ++i)
+  for (size_t i = 0; i < T; ++i) {
     for (const Tensor* t : {&params[i], &grads[i], &exp_avg[i], &exp_avg_sq[i]}) {
       TORCH_CHECK(t->is_cuda() && t->device() == dev && t->scalar_type() == at::kFloat &&
                       t->is_contiguous() && t->numel() == params[i].numel(),
                   "adamw: contiguous fp32 tensors of equal size on one GPU");
     }
+    TORCH_CHECK(steps[i].is_cuda() && steps[i].device() == dev && steps[i].scalar_type() == at::kFloat &&
+                    steps[i].numel() == 1,
+                "adamw: step counters must be one-element fp32 tensors on the parameters' GPU");
+    TORCH_CHECK(group_of[i] >= 0 && group_of[i] < (int64_t)G, "adamw: group index out of range");
+  }
+  auto dev_scalar = [&](const c10::optional<Tensor>& t, const char* name) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->device() == dev && t->scalar_type() == at::kFloat && t->numel() == 1,
+                "adamw: ", name, " must be a one-element fp32 tensor on the parameters' GPU");
+    return t->data_ptr<float>();
+  };
+  const float* isp = dev_scalar(inv_scale, "inv_scale");
+  float* fip = dev_scalar(found_inf, "found_inf");
   const int64_t CH = adam_chunk_elems();
   const int64_t tab_bytes = (int64_t)T * (int64_t)sizeof(AdamTensor);
-  Tensor host = at::empty({tab_bytes + (int64_t)(T + 1) * 4},
-                          at::TensorOptions().dtype(at::kByte).pinned_memory(true));
-  AdamTensor* ht = reinterpret_cast<AdamTensor*>(host.data_ptr<uint8_t>());
-  int* hc = reinterpret_cast<int*>(host.data_ptr<uint8_t>() + tab_bytes);
+  const int64_t grp_off = (tab_bytes + (int64_t)(T + 1) * 4 + 15) / 16 * 16;
+  const int64_t grp_bytes = (int64_t)G * (int64_t)sizeof(AdamGroup);
+  Tensor host = at::empty({grp_off + grp_bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  uint8_t* hb = host.data_ptr<uint8_t>();
+  AdamTensor* ht = reinterpret_cast<AdamTensor*>(hb);
+  int* hc = reinterpret_cast<int*>(hb + tab_bytes);
+  AdamGroup* hg = reinterpret_cast<AdamGroup*>(hb + grp_off);
   hc[0] = 0;
   for (size_t i = 0; i < T; ++i) {
     ht[i] = AdamTensor{params[i].data_ptr<float>(), grads[i].data_ptr<float>(),
                        exp_avg[i].data_ptr<float>(), exp_avg_sq[i].data_ptr<float>(),
-                       params[i].numel()};
+                       params[i].numel(), steps[i].data_ptr<float>(), (int)group_of[i]};
     const int64_t nc = (params[i].numel() + CH - 1) / CH;
     TORCH_CHECK((int64_t)hc[i] + nc < (int64_t(1) << 30), "adamw: too many chunks");
     hc[i + 1] = hc[i] + (int)nc;
+  }
+  for (size_t g = 0; g < G; ++g) {
+    const float* lp = nullptr;
+    if (lr_t[g].defined() && lr_t[g].numel() > 0) {
+      TORCH_CHECK(lr_t[g].is_cuda() && lr_t[g].device() == dev && lr_t[g].scalar_type() == at::kFloat &&
+                      lr_t[g].numel() == 1,
+                  "adamw: lr tensor must be a one-element fp32 tensor on the parameters' GPU");
+      lp = lr_t[g].data_ptr<float>();
+    }
+    // 1 - beta in double, like torch (1 - 0.999 from a float-rounded beta is 1.3e-5 off)
+    hg[g] = AdamGroup{lp, (float)lr[g], (float)wd[g], (float)beta1[g], (float)beta2[g],
+                      (float)(1.0 - beta1[g]), (float)(1.0 - beta2[g]), (float)eps[g]};
   }
   const int nchunks = hc[T];
   c10::DeviceGuard g(dev);
   // pinned source + stream-ordered copy: no host sync (the caching host allocator keeps the
   // block until the copy has run)
   Tensor dtab = host.to(dev, /*non_blocking=*/true);
-  Tensor out = at::empty({(int64_t)nchunks + 2}, params[0].options());
-  const float* lrp = nullptr;
-  if (lr_t.has_value() && lr_t->defined()) {
-    TORCH_CHECK(lr_t->is_cuda() && lr_t->device() == dev && lr_t->scalar_type() == at::kFloat &&
-                    lr_t->numel() == 1,
-                "adamw: lr tensor must be a one-element fp32 tensor on the parameters' GPU");
-    lrp = lr_t->data_ptr<float>();
-  }
-  if (nchunks > 0)
-    launch_adamw_multi(reinterpret_cast<const AdamTensor*>(dtab.data_ptr<uint8_t>()),
-                       reinterpret_cast<const int*>(dtab.data_ptr<uint8_t>() + tab_bytes), (int)T,
-                       nchunks, lrp, (float)lr, beta1, beta2, (float)eps, (float)wd,
-                       (float)bc1, (float)bc2, (float)max_norm, out.data_ptr<float>(),
-                       out.data_ptr<float>() + nchunks, cur_stream());
-  return out.narrow(0, nchunks, 2);
+  Tensor out = at::empty({(int64_t)nchunks + 3}, params[0].options());
+  uint8_t* db = dtab.data_ptr<uint8_t>();
+  const bool need_norm = max_norm > 0.0 || isp != nullptr;
+  launch_adamw_multi(reinterpret_cast<const AdamTensor*>(db), reinterpret_cast<const int*>(db + tab_bytes),
+                     (int)T, nchunks, reinterpret_cast<const AdamGroup*>(db + grp_off), (float)max_norm,
+                     isp, need_norm ? 1 : 0, write_grad ? 1 : 0, out.data_ptr<float>(),
+                     out.data_ptr<float>() + nchunks, fip, cur_stream());
+  return out.narrow(0, nchunks, 3);
 }
 
 // dcorr level 0 (B, N, N) straight from the iterations' bf16 lookup-output gradients
@@ -1484,14 +1543,17 @@ Tensor corr_tap_reduce(const std::vector<Tensor>& coords, const std::vector<Tens
     TORCH_CHECK(coords[k].dim() == 4 && coords[k].size(0) == B && coords[k].size(1) == 2 &&
                     coords[k].size(2) == H && coords[k].size(3) == W,
                 "coords shape");
-    check_nhwc(douts[k], B, H, W, "tap gradient", at::kBFloat16);
+    check_nhwc(douts[k], B, H, W, "tap gradient", douts[0].scalar_type());
+    TORCH_CHECK(douts[k].scalar_type() == at::kBFloat16 || douts[k].scalar_type() == at::kHalf,
+                "tap gradients must be bf16 or fp16");
     TORCH_CHECK(douts[k].size(3) == cbuf && cbuf % 8 == 0 && cbuf >= levels * D * D,
                 "tap gradient rows must share a width >= levels*(2r+1)^2, multiple of 8");
     tl.coords[k] = coords[k].data_ptr<float>();
-    tl.dout[k] = bf16p(douts[k]);
+    tl.dout[k] = u16(douts[k]);
   }
   tl.n = (int)coords.size();
   tl.cbuf = (int)cbuf;
+  tl.tf16 = douts[0].scalar_type() == at::kHalf ? 1 : 0;
   // row pitch: N, or N rounded up to pitch_mult (zero columns: the MFMA backward GEMMs' K padding)
   TORCH_CHECK(pitch_mult >= 0 && pitch_mult % 2 == 0, "pitch_mult must be even");
   const int64_t ldo = pitch_mult > 0 ? (N + pitch_mult - 1) / pitch_mult * pitch_mult : N;
@@ -1537,28 +1599,29 @@ std::vector<Tensor> corr_bwd_fmaps(const Tensor& dc, const Tensor& f1, const Ten
 // ------------------------------------------------------------------ flow_head.conv2 (256 -> 2)
 // Weights arrive as bf16 pair tables built by the update block's packing gather:
 // wf = W[o][c][t] as [t][o][c] (2304 bf16), wd = W[o][c][t] as [t][c][o] (4608 bf16).
-const uint32_t* fh2_pairs(const Tensor& t, int64_t n, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kBFloat16, name,
-              " must be a contiguous bf16 GPU tensor");
+const uint32_t* fh2_pairs(const Tensor& t, int64_t n, const char* name, at::ScalarType st) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == st, name,
+              " must be a contiguous GPU tensor of the activation dtype");
   TORCH_CHECK(t.numel() == n, name, " must hold ", n, " elements");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-B aligned");
-  return reinterpret_cast<const uint32_t*>(t.data_ptr<at::BFloat16>());
+  return reinterpret_cast<const uint32_t*>(t.data_ptr());
 }
 
 // out (B,2,H,W) fp32 = conv3x3(in[..., 0:256]) + bias
 void fh2_fwd_(const Tensor& in, const Tensor& wf, const Tensor& b, const Tensor& out) {
   TORCH_CHECK(in.dim() == 4, "in must be (B,H,W,C)");
   const int64_t B = in.size(0), H = in.size(1), W = in.size(2), cs = in.size(3);
-  check_nhwc(in, B, H, W, "fh2 in", at::kBFloat16);
-  const uint32_t* wp = fh2_pairs(wf, 9 * 2 * 256, "fh2 wf");
+  const at::ScalarType st = op16(in);
+  check_nhwc(in, B, H, W, "fh2 in", st);
+  const uint32_t* wp = fh2_pairs(wf, 9 * 2 * 256, "fh2 wf", st);
   check_cuda_f32(b, "fh2 bias");
   TORCH_CHECK(b.numel() == 2, "fh2 bias must have 2 elements");
   check_cuda_f32(out, "fh2 out");
   TORCH_CHECK(out.dim() == 4 && out.size(0) == B && out.size(1) == 2 && out.size(2) == H &&
               out.size(3) == W, "fh2 out must be (B,2,H,W)");
   c10::DeviceGuard gd(in.device());
-  TORCH_CHECK(launch_fh2_fwd(bf16p(in), (int)cs, wp, b.data_ptr<float>(), out.data_ptr<float>(),
-                             (int)B, (int)H, (int)W, cur_stream()),
+  TORCH_CHECK(launch_fh2_fwd(u16(in), (int)cs, wp, b.data_ptr<float>(), out.data_ptr<float>(),
+                             (int)B, (int)H, (int)W, st == at::kHalf, cur_stream()),
               "fh2_fwd: input needs >= 256 channels, a multiple of 8");
 }
 
@@ -1567,12 +1630,13 @@ void fh2_dgrad_(const Tensor& gout, const Tensor& wd, const Tensor& fm, const Te
   check_cuda_f32(gout, "fh2 gout");
   TORCH_CHECK(gout.dim() == 4 && gout.size(1) == 2, "gout must be (B,2,H,W)");
   const int64_t B = gout.size(0), H = gout.size(2), W = gout.size(3);
-  check_nhwc(fm, B, H, W, "fh2 fm", at::kBFloat16);
-  check_nhwc(dx, B, H, W, "fh2 dx", at::kBFloat16);
-  const uint32_t* wp = fh2_pairs(wd, 9 * 256 * 2, "fh2 wd");
+  const at::ScalarType st = op16(fm);
+  check_nhwc(fm, B, H, W, "fh2 fm", st);
+  check_nhwc(dx, B, H, W, "fh2 dx", st);
+  const uint32_t* wp = fh2_pairs(wd, 9 * 256 * 2, "fh2 wd", st);
   c10::DeviceGuard gd(gout.device());
-  TORCH_CHECK(launch_fh2_dgrad(gout.data_ptr<float>(), wp, bf16p(fm), (int)fm.size(3), bf16m(dx),
-                               (int)dx.size(3), (int)B, (int)H, (int)W, cur_stream()),
+  TORCH_CHECK(launch_fh2_dgrad(gout.data_ptr<float>(), wp, u16(fm), (int)fm.size(3), u16m(dx),
+                               (int)dx.size(3), (int)B, (int)H, (int)W, st == at::kHalf, cur_stream()),
               "fh2_dgrad: fm / dx need >= 256 channels, multiples of 8");
 }
 
@@ -1585,14 +1649,15 @@ void fh2_wgrad_(const std::vector<Tensor>& gouts, const std::vector<Tensor>& ins
   const int64_t cs = ins[0].size(3);
   Fh2Items it{};
   it.n = (int)n;
+  const at::ScalarType st = op16(ins[0]);
   for (int64_t i = 0; i < n; ++i) {
     check_cuda_f32(gouts[i], "fh2 gout");
     TORCH_CHECK(gouts[i].dim() == 4 && gouts[i].size(0) == B && gouts[i].size(1) == 2 &&
                 gouts[i].size(2) == H && gouts[i].size(3) == W, "all gouts must be (B,2,H,W)");
-    check_nhwc(ins[i], B, H, W, "fh2 wgrad input", at::kBFloat16);
+    check_nhwc(ins[i], B, H, W, "fh2 wgrad input", st);
     TORCH_CHECK(ins[i].size(3) == cs, "all items' inputs must share a layout");
     it.gout[i] = gouts[i].data_ptr<float>();
-    it.in[i] = bf16p(ins[i]);
+    it.in[i] = u16(ins[i]);
   }
   check_cuda_f32(part, "fh2 part");
   TORCH_CHECK(part.dim() == 2 && part.size(1) == 2 * 9 * 256 + 2, "fh2 part must be (G, 4610)");
@@ -1600,7 +1665,7 @@ void fh2_wgrad_(const std::vector<Tensor>& gouts, const std::vector<Tensor>& ins
   TORCH_CHECK(part.size(0) >= 1 && part.size(0) <= 65535, "fh2 part needs 1..65535 rows");
   c10::DeviceGuard gd(part.device());
   TORCH_CHECK(launch_fh2_wgrad(it, (int)cs, (int)B, (int)H, (int)W, part.data_ptr<float>(),
-                               (int)part.size(0), cur_stream()),
+                               (int)part.size(0), st == at::kHalf, cur_stream()),
               "fh2_wgrad: inputs need >= 256 channels, a multiple of 8");
 }
 
@@ -1611,18 +1676,20 @@ void f1_patch_(const Tensor& flow, const Tensor& patch, const c10::optional<Tens
   check_cuda_f32(flow, "flow");
   TORCH_CHECK(flow.dim() == 4 && flow.size(1) == 2, "flow must be (B,2,H,W)");
   const int64_t B = flow.size(0), H = flow.size(2), W = flow.size(3);
-  check_nhwc(patch, B, H, W, "patch", at::kBFloat16);
+  const at::ScalarType st = op16(patch);
+  check_nhwc(patch, B, H, W, "patch", st);
   TORCH_CHECK(patch.size(3) == 128, "patch must have 128 channels");
   uint16_t* sp = nullptr;
   int ss = 0;
   if (slot.has_value() && slot->defined()) {
-    check_nhwc(*slot, B, H, W, "slot", at::kBFloat16);
+    check_nhwc(*slot, B, H, W, "slot", st);
     TORCH_CHECK(slot_off >= 0 && slot_off + 2 <= slot->size(3), "slot range");
-    sp = bf16m(*slot) + slot_off;
+    sp = u16m(*slot) + slot_off;
     ss = (int)slot->size(3);
   }
   c10::DeviceGuard gd(flow.device());
-  launch_f1_patch(flow.data_ptr<float>(), bf16m(patch), sp, ss, (int)B, (int)H, (int)W, cur_stream());
+  launch_f1_patch(flow.data_ptr<float>(), u16m(patch), sp, ss, (int)B, (int)H, (int)W, st == at::kHalf,
+                  cur_stream());
 }
 
 }  // namespace
@@ -1672,7 +1739,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("conv_fwd_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, Tensor? bias, int kh, int kw, int ph, int pw, int cout, int cin_small, int epi, int bn, float scale, int split, Tensor(a!)[] outs, int[] out_off, Tensor[] aux, int[] aux_off) -> ()");
   m.def("conv_wgrad_multi_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
   m.def("f1_patch_(Tensor flow, Tensor(a!) patch, Tensor(b!)? slot, int slot_off) -> ()");
-  m.def("adamw_step_(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, Tensor(c!)[] exp_avg_sq, Tensor? lr_t, float lr, float beta1, float beta2, float eps, float wd, float bc1, float bc2, float max_norm) -> Tensor");
+  m.def("adamw_step_(Tensor(a!)[] params, Tensor(b!)[] grads, Tensor(c!)[] exp_avg, Tensor(d!)[] exp_avg_sq, Tensor(e!)[] steps, int[] group_of, Tensor[] lr_t, float[] lr, float[] beta1, float[] beta2, float[] eps, float[] wd, float max_norm, Tensor? inv_scale=None, Tensor(f!)? found_inf=None, bool write_grad=False) -> Tensor");
   m.def("corr_tap_reduce(Tensor[] coords, Tensor[] douts, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16, int pitch_mult=0) -> Tensor");
   m.def("corr_bwd_fmaps(Tensor dc, Tensor f1, Tensor f2) -> Tensor[]");
   m.def("fh2_fwd_(Tensor inp, Tensor wf, Tensor b, Tensor(a!) out) -> ()");

@@ -1,15 +1,22 @@
-// Multi-tensor AdamW with the global-norm gradient clip folded in (the training step's update:
-// reference `train.py:158-181` -- clip_grad_norm_(1.0), AdamW(lr, wd, eps), OneCycle lr).
+// Multi-tensor AdamW with the global-norm gradient clip and the fp16 GradScaler's unscale /
+// overflow skip folded in (the training step's update: reference `train.py:158-181` --
+// scaler.unscale_, clip_grad_norm_(1.0), scaler.step(AdamW(lr, wd, eps)), OneCycle lr).
 //
 // torch's fused AdamW spent 4 multi-tensor launches x ~72 us on RAFT's 5.3 M parameters in ~150
 // tensors (a few thousand elements per workgroup, most of the GPU idle) plus two launches for the
-// foreach clip.  Here every tensor is cut into CH-element chunks, one workgroup per chunk over
-// all tensors at once (~1.4 K workgroups), in three launches:
+// foreach clip.  Here every tensor of every parameter group is cut into CH-element chunks, one
+// workgroup per chunk over all tensors at once (~1.4 K workgroups), in three launches:
 //   1. sum of squares of the gradients per chunk (fixed-order block reduction, no atomics);
-//   2. one workgroup: total norm in fixed chunk order -> clip coefficient min(1, max/(norm+1e-6));
+//   2. one workgroup: total norm over ALL groups in fixed chunk order, unscaled by the
+//      GradScaler's 1/S -> clip coefficient min(1, max/(norm+1e-6)) / S, found_inf = the norm is
+//      not finite (an inf / nan anywhere makes the sum of squares non-finite); on a finite step
+//      every tensor's device step counter advances (a skipped step leaves the moments, the
+//      parameters and the step counts untouched, as torch's GradScaler.step does);
 //   3. the AdamW update with the clipped gradient (torch's non-amsgrad AdamW arithmetic:
 //      p *= 1 - lr wd;  m = lerp(m, g, 1-b1);  v = b2 v + (1-b2) g^2;
-//      p -= (lr / bc1) m / (sqrt(v) / sqrt(bc2) + eps)).
+//      p -= (lr / bc1) m / (sqrt(v) / sqrt(bc2) + eps)), bias corrections from the tensor's own
+//      step count, hyper-parameters from its group; optionally the clipped, unscaled gradient is
+//      written back to .grad (what clip_grad_norm_ / unscale_ leave there).
 // Tensor pointers come in a small device table (the gradients are new allocations every step);
 // a workgroup finds its tensor by binary search over the cumulative chunk counts.
 #include "common.h"
@@ -62,42 +69,64 @@ __global__ __launch_bounds__(ADAM_NT) void adam_sumsq_kernel(AdamTab tab, float*
   if (threadIdx.x == 0) part[c] = s;
 }
 
-// coef[0] = clip coefficient, coef[1] = total norm
-__global__ __launch_bounds__(ADAM_NT) void adam_clip_kernel(const float* __restrict__ part, int nchunks,
-                                                            float max_norm, float* __restrict__ coef) {
+// coef[0] = gradient multiplier (clip coefficient / S), coef[1] = total (unscaled) norm,
+// coef[2] = found_inf (1: skip the step); the tensors' step counters advance on a finite step
+__global__ __launch_bounds__(ADAM_NT) void adam_clip_kernel(AdamTab tab, const float* __restrict__ part,
+                                                            int nchunks, float max_norm,
+                                                            const float* __restrict__ inv_scale,
+                                                            float* __restrict__ coef,
+                                                            float* __restrict__ found_inf) {
   __shared__ float red[ADAM_NT];
+  __shared__ int fin;
   float s = 0.f;
-  for (int c = threadIdx.x; c < nchunks; c += ADAM_NT) s += part[c];
+  if (part != nullptr)
+    for (int c = threadIdx.x; c < nchunks; c += ADAM_NT) s += part[c];
   red[threadIdx.x] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
     float tot = 0.f;
     for (int i = 0; i < ADAM_NT; ++i) tot += red[i];
-    const float norm = sqrtf(tot);
-    coef[0] = fminf(1.f, max_norm / (norm + 1e-6f));
+    const float is = inv_scale != nullptr ? inv_scale[0] : 1.f;
+    const float norm = sqrtf(tot) * is;
+    const bool finite = isfinite(norm);
+    const float k = max_norm > 0.f ? fminf(1.f, max_norm / (norm + 1e-6f)) : 1.f;
+    coef[0] = k * is;
     coef[1] = norm;
+    coef[2] = finite ? 0.f : 1.f;
+    if (found_inf != nullptr) found_inf[0] = finite ? 0.f : 1.f;
+    fin = finite ? 1 : 0;
   }
+  __syncthreads();
+  if (fin)
+    for (int i = threadIdx.x; i < tab.T; i += ADAM_NT) tab.t[i].step[0] += 1.f;
 }
 
-__global__ __launch_bounds__(ADAM_NT) void adam_update_kernel(AdamTab tab, const float* __restrict__ lr_dev,
-                                                              float lr_host, float b1, float b2, float omb1,
-                                                              float omb2, float eps,
-                                                              float wd, float bc1, float bc2_sqrt,
-                                                              const float* __restrict__ coef) {
+__global__ __launch_bounds__(ADAM_NT) void adam_update_kernel(AdamTab tab, const AdamGroup* __restrict__ grp,
+                                                              const float* __restrict__ coef,
+                                                              int write_grad) {
+  if (coef[2] != 0.f) return;   // overflow: the whole step is skipped
   const int c = blockIdx.x;
   const int ti = find_tensor(tab.cum, tab.T, c);
   const AdamTensor t = tab.t[ti];
+  const AdamGroup gp = grp[t.group];
   const int64_t s0 = (int64_t)(c - tab.cum[ti]) * ADAM_CH;
   const int64_t n = min((int64_t)ADAM_CH, t.numel - s0);
-  const float lr = lr_dev != nullptr ? lr_dev[0] : lr_host;
-  const float k = coef != nullptr ? coef[0] : 1.f;
-  const float decay = 1.f - lr * wd, step = lr / bc1;
+  const float lr = gp.lr_dev != nullptr ? gp.lr_dev[0] : gp.lr;
+  const float k = coef[0];
+  // bias corrections of this tensor's own step count (already advanced by the clip kernel); in
+  // double like torch's host-side 1 - beta ** step
+  const double st = (double)t.step[0];
+  const float bc1 = (float)(1.0 - pow((double)gp.b1, st));
+  const float bc2_sqrt = sqrtf((float)(1.0 - pow((double)gp.b2, st)));
+  const float decay = 1.f - lr * gp.wd, step = lr / bc1;
+  const float b2 = gp.b2, omb1 = gp.omb1, omb2 = gp.omb2, eps = gp.eps;
   float* p = t.p + s0;
-  const float* g = t.g + s0;
+  float* g = t.g + s0;
   float* m = t.m + s0;
   float* v = t.v + s0;
   for (int64_t e = threadIdx.x; e < n; e += ADAM_NT) {
     const float gg = g[e] * k;
+    if (write_grad) g[e] = gg;
     const float mm = m[e] + omb1 * (gg - m[e]);  // lerp(m, g, 1 - b1)
     const float vv = b2 * v[e] + omb2 * gg * gg;
     m[e] = mm;
@@ -111,16 +140,14 @@ __global__ __launch_bounds__(ADAM_NT) void adam_update_kernel(AdamTab tab, const
 
 int adam_chunk_elems() { return ADAM_CH; }
 
-void launch_adamw_multi(const AdamTensor* tab, const int* cum, int T, int nchunks, const float* lr_dev,
-                        float lr_host, double b1, double b2, float eps, float wd, float bc1, float bc2,
-                        float max_norm, float* part, float* coef, hipStream_t stream) {
-  // 1 - beta in double, like torch (1 - 0.999 from a float-rounded beta is 1.3e-5 off)
+void launch_adamw_multi(const AdamTensor* tab, const int* cum, int T, int nchunks, const AdamGroup* groups,
+                        float max_norm, const float* inv_scale, int need_norm, int write_grad,
+                        float* part, float* coef, float* found_inf, hipStream_t stream) {
   AdamTab at{tab, cum, T};
-  if (max_norm > 0.f) {
+  if (need_norm)
     hipLaunchKernelGGL(adam_sumsq_kernel, dim3((unsigned)nchunks), dim3(ADAM_NT), 0, stream, at, part);
-    hipLaunchKernelGGL(adam_clip_kernel, dim3(1), dim3(ADAM_NT), 0, stream, part, nchunks, max_norm, coef);
-  }
-  hipLaunchKernelGGL(adam_update_kernel, dim3((unsigned)nchunks), dim3(ADAM_NT), 0, stream, at, lr_dev,
-                     lr_host, (float)b1, (float)b2, (float)(1.0 - b1), (float)(1.0 - b2), eps, wd, bc1,
-                     sqrtf(bc2), max_norm > 0.f ? coef : nullptr);
+  hipLaunchKernelGGL(adam_clip_kernel, dim3(1), dim3(ADAM_NT), 0, stream, at, need_norm ? part : nullptr,
+                     nchunks, max_norm, inv_scale, coef, found_inf);
+  hipLaunchKernelGGL(adam_update_kernel, dim3((unsigned)nchunks), dim3(ADAM_NT), 0, stream, at, groups,
+                     coef, write_grad);
 }

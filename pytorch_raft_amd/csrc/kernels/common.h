@@ -26,6 +26,29 @@ __device__ __forceinline__ uint16_t raft_f32_to_bf16(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// ---- 16-bit MFMA operand type: bf16 (F16 = false) or fp16 (fp16 autocast).  Operands travel as
+// 16-bit bit containers; only the MFMA instruction and the conversions know the type.
+typedef __bf16 raft_v8bf16 __attribute__((ext_vector_type(8)));
+typedef _Float16 raft_v8f16 __attribute__((ext_vector_type(8)));
+template <bool F16>
+__device__ __forceinline__ f32x16 raft_mfma32(raft_v8bf16 a, raft_v8bf16 b, f32x16 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(raft_v8f16, a),
+                                                 __builtin_bit_cast(raft_v8f16, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <bool F16>
+__device__ __forceinline__ float raft_h2f(uint16_t v) {
+  if constexpr (F16) return (float)__builtin_bit_cast(_Float16, v);
+  else return raft_bf16_to_f32(v);
+}
+template <bool F16>
+__device__ __forceinline__ uint16_t raft_f2h(float v) {
+  if constexpr (F16) return __builtin_bit_cast(uint16_t, (_Float16)v);
+  else return raft_f32_to_bf16(v);
+}
+
 template <typename T> struct Ld;
 template <> struct Ld<float> {
   __device__ __forceinline__ static float get(const float* p, int64_t i) { return p[i]; }

@@ -20,6 +20,14 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * 8 + (chunk
 
 __device__ __forceinline__ bf16x8_t zero_frag8() { return __builtin_bit_cast(bf16x8_t, make_uint4(0, 0, 0, 0)); }
 
+// 16-bit operand type (common.h): fragments travel as bf16x8_t bit containers
+template <bool F16>
+__device__ __forceinline__ f32x16 mfma16(bf16x8_t a, bf16x8_t b, f32x16 c) { return raft_mfma32<F16>(a, b, c); }
+template <bool F16>
+__device__ __forceinline__ float cvt16(uint16_t v) { return raft_h2f<F16>(v); }
+template <bool F16>
+__device__ __forceinline__ uint16_t pack16(float v) { return raft_f2h<F16>(v); }
+
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 constexpr uint32_t OOB = 0x80000000u;  // voffset past every num_records: the load returns zeros
 
@@ -63,14 +71,16 @@ __device__ __forceinline__ float tanhf_(float v) {
 __device__ __forceinline__ float bld_f32(rsrc_t r, uint32_t off) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
+template <bool F16 = false>
 __device__ __forceinline__ float bld_bf16(rsrc_t r, uint32_t off) {
-  return raft_bf16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0));
+  return cvt16<F16>(__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0));
 }
 __device__ __forceinline__ void bst_f32(rsrc_t r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
 }
+template <bool F16 = false>
 __device__ __forceinline__ void bst_bf16(rsrc_t r, uint32_t off, float v) {
-  __builtin_amdgcn_raw_buffer_store_b16(raft_f32_to_bf16(v), r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b16(pack16<F16>(v), r, off, 0, 0);
 }
 
 // 64-channel K chunks of the workgroup whose N tile is [n0, n0 + BN): all of cin_pad unless the
@@ -92,23 +102,25 @@ __device__ __forceinline__ int tile_nchunk(const ConvFwdArgs& a, int n0, int BN)
 template <int TM, int TN, int WM, int WN, int EPI>
 __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc)[TM][TN], int m0,
                                               int n0, int wm, int wn, int lane, int P, int HW) {
-  constexpr bool F32OUT = EPI == EPI_F32 || EPI == EPI_ACC_F32 || EPI == EPI_F32_NCHW;
+  constexpr bool F16 = epi_f16(EPI);
+  constexpr int E = epi_kind(EPI);
+  constexpr bool F32OUT = E == EPI_F32 || E == EPI_ACC_F32 || E == EPI_F32_NCHW;
   constexpr uint32_t ES = F32OUT ? 4u : 2u;
   const rsrc_t bias_rs = make_rsrc(a.bias, a.bias ? (uint32_t)a.cout * 4u : 0u);
   const uint32_t P_u = (uint32_t)P;
   const rsrc_t nul = make_rsrc(nullptr, 0u);
   rsrc_t o0 = nul, o1 = nul, o2 = nul, x0 = nul, x1 = nul;
-  if constexpr (EPI == EPI_F32_NCHW) {
+  if constexpr (E == EPI_F32_NCHW) {
     o0 = make_rsrc(a.out0, P_u * (uint32_t)a.cout * 4u);
-  } else if constexpr (EPI != EPI_DGRAD && EPI != EPI_DGRAD_GATE) {
+  } else if constexpr (E != EPI_DGRAD && E != EPI_DGRAD_GATE) {
     o0 = make_rsrc(a.out0, P_u * (uint32_t)a.out0_stride * ES);
   }
-  if constexpr (EPI == EPI_GRU_ZR || EPI == EPI_GRU_Q) {
+  if constexpr (E == EPI_GRU_ZR || E == EPI_GRU_Q) {
     o1 = make_rsrc(a.out1, P_u * (uint32_t)a.out1_stride * 2u);
     x0 = make_rsrc(a.aux0, P_u * (uint32_t)a.aux0_stride * 2u);
   }
-  if constexpr (EPI == EPI_GRU_ZR) o2 = make_rsrc(a.out2, P_u * (uint32_t)a.out2_stride * 2u);
-  if constexpr (EPI == EPI_GRU_Q) x1 = make_rsrc(a.aux1, P_u * (uint32_t)a.aux1_stride * 2u);
+  if constexpr (E == EPI_GRU_ZR) o2 = make_rsrc(a.out2, P_u * (uint32_t)a.out2_stride * 2u);
+  if constexpr (E == EPI_GRU_Q) x1 = make_rsrc(a.aux1, P_u * (uint32_t)a.aux1_stride * 2u);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -128,12 +140,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
       float v[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) v[r] = (acc[i][j][r] + bias) * a.scale;
-      if constexpr (EPI == EPI_GRU_ZR || EPI == EPI_GRU_Q) {
+      if constexpr (E == EPI_GRU_ZR || E == EPI_GRU_Q) {
         if (a.bmap != nullptr && a.bmap_bf16) {  // uniform
           const rsrc_t bm = make_rsrc(a.bmap, P_u * (uint32_t)a.bmap_stride * 2u);
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            v[r] += bld_bf16(bm, ok[r] ? (uint32_t)(mrow[r] * a.bmap_stride + n) * 2u : OOB);
+            v[r] += bld_bf16<F16>(bm, ok[r] ? (uint32_t)(mrow[r] * a.bmap_stride + n) * 2u : OOB);
         } else if (a.bmap != nullptr) {
           const rsrc_t bm = make_rsrc(a.bmap, P_u * (uint32_t)a.bmap_stride * 4u);
 #pragma unroll
@@ -142,14 +154,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
         }
       }
 
-      if constexpr (EPI == EPI_BF16 || EPI == EPI_RELU_BF16 || EPI == EPI_F32) {
+      if constexpr (E == EPI_BF16 || E == EPI_RELU_BF16 || E == EPI_F32) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const uint32_t off = ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * ES : OOB;
-          if constexpr (EPI == EPI_F32) bst_f32(o0, off, v[r]);
-          else bst_bf16(o0, off, EPI == EPI_RELU_BF16 ? fmaxf(v[r], 0.f) : v[r]);
+          if constexpr (E == EPI_F32) bst_f32(o0, off, v[r]);
+          else bst_bf16<F16>(o0, off, E == EPI_RELU_BF16 ? fmaxf(v[r], 0.f) : v[r]);
         }
-      } else if constexpr (EPI == EPI_ACC_F32) {
+      } else if constexpr (E == EPI_ACC_F32) {
         uint32_t off[16];
         float pre[16];
 #pragma unroll
@@ -159,44 +171,44 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) bst_f32(o0, off[r], pre[r] + v[r]);
-      } else if constexpr (EPI == EPI_F32_NCHW) {
+      } else if constexpr (E == EPI_F32_NCHW) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int b = mrow[r] / HW, yx = mrow[r] - b * HW;
           bst_f32(o0, ok[r] ? (uint32_t)((b * a.cout + n) * HW + yx) * 4u : OOB, v[r]);
         }
-      } else if constexpr (EPI == EPI_GRU_ZR) {
+      } else if constexpr (E == EPI_GRU_ZR) {
         if (ncol0 < a.split) {  // z half
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            bst_bf16(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, sigmoidf_(v[r]));
+            bst_bf16<F16>(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, sigmoidf_(v[r]));
         } else {  // r half: r*h and r
           const int c = n - a.split;
           float h[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            h[r] = bld_bf16(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + c) * 2u : OOB);
+            h[r] = bld_bf16<F16>(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + c) * 2u : OOB);
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const float g = sigmoidf_(v[r]);
-            bst_bf16(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + c) * 2u : OOB, g * h[r]);
-            bst_bf16(o2, ok[r] ? (uint32_t)(mrow[r] * a.out2_stride + c) * 2u : OOB, g);
+            bst_bf16<F16>(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + c) * 2u : OOB, g * h[r]);
+            bst_bf16<F16>(o2, ok[r] ? (uint32_t)(mrow[r] * a.out2_stride + c) * 2u : OOB, g);
           }
         }
-      } else if constexpr (EPI == EPI_GRU_Q) {
+      } else if constexpr (E == EPI_GRU_Q) {
         float h[16], z[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          h[r] = bld_bf16(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + n) * 2u : OOB);
-          z[r] = bld_bf16(x1, ok[r] ? (uint32_t)(mrow[r] * a.aux1_stride + n) * 2u : OOB);
+          h[r] = bld_bf16<F16>(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + n) * 2u : OOB);
+          z[r] = bld_bf16<F16>(x1, ok[r] ? (uint32_t)(mrow[r] * a.aux1_stride + n) * 2u : OOB);
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float q = tanhf_(v[r]);
-          bst_bf16(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, h[r] + z[r] * (q - h[r]));
-          bst_bf16(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + n) * 2u : OOB, q);
+          bst_bf16<F16>(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, h[r] + z[r] * (q - h[r]));
+          bst_bf16<F16>(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + n) * 2u : OOB, q);
         }
-      } else if constexpr (EPI == EPI_DGRAD || EPI == EPI_DGRAD_GATE) {
+      } else if constexpr (E == EPI_DGRAD || E == EPI_DGRAD_GATE) {
         // output segment of this 32-column tile (uniform)
         int s = 0, base = 0;
 #pragma unroll
@@ -206,7 +218,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
         const int c = n - base;
         const bool cok = c < o.real;
         bool gated = false;
-        if constexpr (EPI == EPI_DGRAD_GATE) {
+        if constexpr (E == EPI_DGRAD_GATE) {
           gated = o.gate != 0;
           if (o.gate == 1) {  // ConvGRU q / z gate backward on the final state gradient
             const rsrc_t od = make_rsrc(o.ptr, P_u * (uint32_t)o.stride * 4u);
@@ -224,19 +236,19 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
                 const bool e = ok[r] && cok;
                 pre[u] = bld_f32(od, e ? (uint32_t)(mrow[r] * o.stride + c) * 4u : OOB);
                 const uint32_t oa = e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB;
-                zz[u] = bld_bf16(rz, oa);
-                qq[u] = bld_bf16(rq, oa);
-                hh[u] = bld_bf16(rh, oa);
+                zz[u] = bld_bf16<F16>(rz, oa);
+                qq[u] = bld_bf16<F16>(rq, oa);
+                hh[u] = bld_bf16<F16>(rh, oa);
               }
 #pragma unroll
               for (int u = 0; u < 8; ++u) {
                 const int r = h8 + u;
                 const bool e = ok[r] && cok;
                 const float g = pre[u] + v[r];
-                bst_bf16(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB,
+                bst_bf16<F16>(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB,
                          g * zz[u] * (1.f - qq[u] * qq[u]));
                 const float dz = g * (qq[u] - hh[u]);
-                bst_bf16(gz, e ? (uint32_t)(mrow[r] * o.gz_stride + c) * 2u : OOB,
+                bst_bf16<F16>(gz, e ? (uint32_t)(mrow[r] * o.gz_stride + c) * 2u : OOB,
                          dz * zz[u] * (1.f - zz[u]));
                 bst_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB, g * (1.f - zz[u]));
               }
@@ -254,13 +266,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
                 const int r = h8 + u;
                 const bool e = ok[r] && cok;
                 pre[u] = bld_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB);
-                yv[u] = bld_bf16(ry, e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB);
+                yv[u] = bld_bf16<F16>(ry, e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB);
               }
 #pragma unroll
               for (int u = 0; u < 8; ++u) {
                 const int r = h8 + u;
                 const bool e = ok[r] && cok;
-                bst_bf16(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB,
+                bst_bf16<F16>(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB,
                          yv[u] > 0.f ? pre[u] + v[r] : 0.f);
               }
             }
@@ -278,14 +290,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
                 const bool e = ok[r] && cok;
                 const uint32_t oa = e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB;
                 dh[u] = bld_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB);
-                rv[u] = bld_bf16(rr, oa);
-                hh[u] = bld_bf16(rh, oa);
+                rv[u] = bld_bf16<F16>(rr, oa);
+                hh[u] = bld_bf16<F16>(rh, oa);
               }
 #pragma unroll
               for (int u = 0; u < 8; ++u) {
                 const int r = h8 + u;
                 const bool e = ok[r] && cok;
-                bst_bf16(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + o.real + c) * 2u : OOB,
+                bst_bf16<F16>(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + o.real + c) * 2u : OOB,
                          v[r] * hh[u] * rv[u] * (1.f - rv[u]));
                 bst_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB,
                         dh[u] + v[r] * rv[u]);
@@ -299,17 +311,17 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
           const rsrc_t ob = make_rsrc(o.ob, P_u * (uint32_t)o.ob_stride * 2u);
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            bst_bf16(ob, ok[r] && cok ? (uint32_t)(mrow[r] * o.ob_stride + c) * 2u : OOB, v[r]);
+            bst_bf16<F16>(ob, ok[r] && cok ? (uint32_t)(mrow[r] * o.ob_stride + c) * 2u : OOB, v[r]);
         } else if (o.ob != nullptr) {  // relu-gated bf16 gradient
           const rsrc_t ob = make_rsrc(o.ob, P_u * (uint32_t)o.ob_stride * 2u);
           const rsrc_t ry = make_rsrc(o.ry, P_u * (uint32_t)o.ry_stride * 2u);
           float y[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            y[r] = bld_bf16(ry, ok[r] && cok ? (uint32_t)(mrow[r] * o.ry_stride + c) * 2u : OOB);
+            y[r] = bld_bf16<F16>(ry, ok[r] && cok ? (uint32_t)(mrow[r] * o.ry_stride + c) * 2u : OOB);
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            bst_bf16(ob, ok[r] && cok ? (uint32_t)(mrow[r] * o.ob_stride + c) * 2u : OOB,
+            bst_bf16<F16>(ob, ok[r] && cok ? (uint32_t)(mrow[r] * o.ob_stride + c) * 2u : OOB,
                      y[r] > 0.f ? v[r] : 0.f);
         } else if (o.ptr != nullptr) {
           const rsrc_t od = make_rsrc(o.ptr, P_u * (uint32_t)o.stride * 4u);

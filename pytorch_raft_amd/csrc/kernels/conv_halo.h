@@ -186,8 +186,8 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_halo_kernel(ConvFwdArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              af[kk][i], __builtin_bit_cast(bf16x8_t, bf[kk][j]), acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16<epi_f16(EPI)>(af[kk][i], __builtin_bit_cast(bf16x8_t, bf[kk][j]),
+                                           acc[i][j]);
     read_frags(ch, dy, dx, afn);
 #pragma unroll
     for (int u = 0; u < 4 * TM; ++u) {
@@ -253,11 +253,54 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_halo_kernel(ConvFwdArgs a) {
   conv_epilogue<TM, TN, WM, WN, EPI>(a, acc, m0, n0, wm, wn, lane, P, HW);
 }
 
-template <int NPA>
+template <int EPI, int TM, int TN, int WVM, int NPA>
+void launch_halo_one(const ConvFwdArgs& a, hipStream_t stream) {
+  constexpr int BM = 32 * TM * WVM, BN = 32 * TN * (4 / WVM);
+  const int P = a.B * a.H * a.W;
+  dim3 grid(conv_grid_1d(raft_cdiv(P, BM), raft_cdiv(a.cout, BN)));
+  hipLaunchKernelGGL((conv_fwd_halo_kernel<TM, TN, WVM, EPI, NPA>), grid, dim3(NT), 0, stream, a);
+}
+
+template <int EPI, int NPA>
+bool halo_cfg(const ConvFwdArgs& a, int tm, int tn, int wvm, hipStream_t s) {
+  if (tm == 5 && tn == 1 && wvm == 1) { launch_halo_one<EPI, 5, 1, 1, NPA>(a, s); return true; }
+  if (tm == 5 && tn == 2 && wvm == 1) { launch_halo_one<EPI, 5, 2, 1, NPA>(a, s); return true; }
+  if (tm == 4 && tn == 2 && wvm == 1) { launch_halo_one<EPI, 4, 2, 1, NPA>(a, s); return true; }
+  if (tm == 2 && tn == 2 && wvm == 2) { launch_halo_one<EPI, 2, 2, 2, NPA>(a, s); return true; }
+  return false;
+}
+
+// the epilogues the halo kernel serves, for one operand type (TY = 0 bf16, EPI_F16 fp16)
+template <int NPA, int TY>
+bool halo_switch(const ConvFwdArgs& a, int epi, int tm, int tn, int wvm, hipStream_t s) {
+  switch (epi_kind(epi)) {
+    case EPI_BF16: return halo_cfg<EPI_BF16 | TY, NPA>(a, tm, tn, wvm, s);
+    case EPI_RELU_BF16: return halo_cfg<EPI_RELU_BF16 | TY, NPA>(a, tm, tn, wvm, s);
+    case EPI_F32: return halo_cfg<EPI_F32 | TY, NPA>(a, tm, tn, wvm, s);
+    case EPI_GRU_ZR: return halo_cfg<EPI_GRU_ZR | TY, NPA>(a, tm, tn, wvm, s);
+    case EPI_GRU_Q: return halo_cfg<EPI_GRU_Q | TY, NPA>(a, tm, tn, wvm, s);
+    case EPI_DGRAD: return halo_cfg<EPI_DGRAD | TY, NPA>(a, tm, tn, wvm, s);
+    case EPI_DGRAD_GATE: return halo_cfg<EPI_DGRAD_GATE | TY, NPA>(a, tm, tn, wvm, s);
+    default: return false;
+  }
+}
+
+// one translation unit per (image size, operand type): conv_halo_<NPA>[_f16].hip
+template <int NPA, bool F16>
 bool launch_conv_halo_npa(const ConvFwdArgs& a, int epi, int tm, int tn, int wvm, hipStream_t stream);
-template <> bool launch_conv_halo_npa<6>(const ConvFwdArgs&, int, int, int, int, hipStream_t);
-template <> bool launch_conv_halo_npa<11>(const ConvFwdArgs&, int, int, int, int, hipStream_t);
-template <> bool launch_conv_halo_npa<16>(const ConvFwdArgs&, int, int, int, int, hipStream_t);
+#define RAFT_HALO_DECL(N)                                                                       \
+  template <> bool launch_conv_halo_npa<N, false>(const ConvFwdArgs&, int, int, int, int, hipStream_t); \
+  template <> bool launch_conv_halo_npa<N, true>(const ConvFwdArgs&, int, int, int, int, hipStream_t);
+RAFT_HALO_DECL(6)
+RAFT_HALO_DECL(11)
+RAFT_HALO_DECL(16)
+#undef RAFT_HALO_DECL
+#define RAFT_HALO_TU(N, F16)                                                                    \
+  template <>                                                                                   \
+  bool launch_conv_halo_npa<N, F16>(const ConvFwdArgs& a, int epi, int tm, int tn, int wvm,    \
+                                    hipStream_t s) {                                            \
+    return halo_switch<N, (F16) ? EPI_F16 : 0>(a, epi, tm, tn, wvm, s);                         \
+  }
 
 }  // namespace conv_detail
 

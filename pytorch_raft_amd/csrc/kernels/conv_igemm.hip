@@ -196,7 +196,7 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16<epi_f16(EPI)>(af[i], bfr[j], acc[i][j]);
     }
   };
 
@@ -284,7 +284,13 @@ void launch_one(const ConvFwdArgs& a, hipStream_t stream) {
 
 template <int EPI, bool SMALLC>
 bool launch_cfg_idx(const ConvFwdArgs& a, int idx, hipStream_t stream) {
-  if constexpr (SMALLC) {
+  if constexpr (epi_f16(EPI)) {
+    // fp16 operands: LDS-DMA and halo kernels only
+    if (SMALLC || idx < 0 || idx >= kNumCfgs || !kCfgs[idx].glds) return false;
+    if (kCfgs[idx].glds == HALO)
+      return launch_conv_halo(a, EPI, kCfgs[idx].tm, kCfgs[idx].tn, kCfgs[idx].wvm, stream);
+    return launch_conv_glds(a, EPI, idx, stream);
+  } else if constexpr (SMALLC) {
     switch (idx) {
       case 0: launch_one<EPI, true, 2, 2, 2>(a, stream); return true;
       case 1: launch_one<EPI, true, 1, 2, 2>(a, stream); return true;
@@ -327,6 +333,13 @@ bool launch_epi_idx(const ConvFwdArgs& a, int epi, int idx, bool smallc, hipStre
     RAFT_EPI_CASE(EPI_F32_NCHW)
     case EPI_GRU_ZR: return !smallc && launch_cfg_idx<EPI_GRU_ZR, false>(a, idx, stream);
     case EPI_GRU_Q: return !smallc && launch_cfg_idx<EPI_GRU_Q, false>(a, idx, stream);
+    case EPI_BF16 | EPI_F16: return launch_cfg_idx<EPI_BF16 | EPI_F16, false>(a, idx, stream);
+    case EPI_RELU_BF16 | EPI_F16: return launch_cfg_idx<EPI_RELU_BF16 | EPI_F16, false>(a, idx, stream);
+    case EPI_F32 | EPI_F16: return launch_cfg_idx<EPI_F32 | EPI_F16, false>(a, idx, stream);
+    case EPI_GRU_ZR | EPI_F16: return launch_cfg_idx<EPI_GRU_ZR | EPI_F16, false>(a, idx, stream);
+    case EPI_GRU_Q | EPI_F16: return launch_cfg_idx<EPI_GRU_Q | EPI_F16, false>(a, idx, stream);
+    case EPI_DGRAD | EPI_F16: return launch_cfg_idx<EPI_DGRAD | EPI_F16, false>(a, idx, stream);
+    case EPI_DGRAD_GATE | EPI_F16: return launch_cfg_idx<EPI_DGRAD_GATE | EPI_F16, false>(a, idx, stream);
     default: return false;
   }
 #undef RAFT_EPI_CASE
@@ -350,10 +363,11 @@ bool glds_disabled() {
 
 bool cfg_allowed(int idx, int cout, bool smallc, int epi) {
   const CfgDesc& c = kCfgs[idx];
+  if (epi_f16(epi) && (smallc || !c.glds)) return false;  // fp16: LDS-DMA / halo kernels only
   if (smallc && !c.small_ok) return false;
   if (c.glds && glds_disabled()) return false;
   if (c.glds == HALO && halo_disabled()) return false;
-  if (idx == 6 && (epi == EPI_GRU_ZR || epi == EPI_GRU_Q)) return false;
+  if (idx == 6 && (epi_kind(epi) == EPI_GRU_ZR || epi_kind(epi) == EPI_GRU_Q)) return false;
   const int npad = (cout + 31) / 32 * 32;
   return c.bn <= 2 * npad || c.bn <= 32;  // no config more than half empty in N
 }
@@ -361,10 +375,11 @@ bool cfg_allowed(int idx, int cout, bool smallc, int epi) {
 // Analytic fallback (stream capture / autotune disabled): rounds of workgroups x tile cost,
 // with the 2x2-wave tiles' LDS-bandwidth penalty.
 int heuristic_cfg(int P, int cout, bool smallc, int epi) {
+  const bool f16 = epi_f16(epi);  // fp16: the 2-stage LDS-DMA configs stand in
   double best = 1e30;
-  int bi = 0;
+  int bi = f16 ? 17 : 0;
   for (int i = 0; i < kNumCfgs; ++i) {
-    if (!cfg_allowed(i, cout, smallc, epi) || kCfgs[i].glds) continue;
+    if (!cfg_allowed(i, cout, smallc, epi) || (f16 ? kCfgs[i].glds != 2 : kCfgs[i].glds != 0)) continue;
     const CfgDesc& c = kCfgs[i];
     const int tiles = raft_cdiv(P, c.bm) * raft_cdiv(cout, c.bn);
     const int occ = (2 * (c.bm + c.bn) * 128 <= 65536 && c.tm * c.tn <= 4) ? 2 : 1;
@@ -407,7 +422,8 @@ inline Range nhwc_range(const void* p, int P, int stride, int esz) {
 }
 inline bool ranges_meet(Range x, Range y) { return x.lo < x.hi && y.lo < y.hi && x.lo < y.hi && y.lo < x.hi; }
 
-bool outputs_overlap_inputs(const ConvFwdArgs& a, int epi) {
+bool outputs_overlap_inputs(const ConvFwdArgs& a, int epi_any) {
+  const int epi = epi_kind(epi_any);
   const int P = a.B * a.H * a.W;
   const bool f32 = epi == EPI_F32 || epi == EPI_F32_NCHW;
   Range outs[3] = {nhwc_range(a.out0, P, epi == EPI_F32_NCHW ? a.cout : a.out0_stride, f32 ? 4 : 2),
@@ -443,7 +459,8 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   t.noseg = 0;
   // input-gradient convs: timed with their REAL epilogue (the fused GRU gate backward moves as
   // many bytes as its GEMM), every written / read-modify-written pointer redirected into scratch
-  const bool dgrad_real = (epi == EPI_DGRAD || epi == EPI_DGRAD_GATE) && tune_real_dgrad();
+  const int ek = epi_kind(epi);
+  const bool dgrad_real = (ek == EPI_DGRAD || ek == EPI_DGRAD_GATE) && tune_real_dgrad();
   ConvFwdArgs td = a;
   if (dgrad_real) {
     size_t tot = 0;
@@ -482,14 +499,14 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   // store-only epilogues are timed as they will run (the GRU gate epilogues cost registers and
   // bytes the fp32 scratch epilogue does not): their outputs are rewritten by the real launch
   // that follows; accumulating epilogues (ACC_F32, DGRAD) are timed on the fp32 scratch
-  bool real_epi = epi == EPI_BF16 || epi == EPI_RELU_BF16 || epi == EPI_GRU_ZR ||
-                  epi == EPI_GRU_Q || epi == EPI_F32 || epi == EPI_F32_NCHW;
+  bool real_epi = ek == EPI_BF16 || ek == EPI_RELU_BF16 || ek == EPI_GRU_ZR ||
+                  ek == EPI_GRU_Q || ek == EPI_F32 || ek == EPI_F32_NCHW;
   // ... but only while no output overlaps an operand the launches read (an in-place GRU state
   // update, say): repeated candidate launches would then read their own outputs
   if (real_epi && outputs_overlap_inputs(a, epi)) real_epi = false;
   const bool dgr = dgrad_real && g_scratch2 != nullptr;
   const ConvFwdArgs& ta = dgr ? td : (real_epi ? a : t);
-  const int te = (real_epi || dgr) ? epi : EPI_F32;
+  const int te = (real_epi || dgr) ? epi : (EPI_F32 | (epi & EPI_F16));
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -533,12 +550,14 @@ int choose_cfg(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   }();
   const int P = a.B * a.H * a.W;
   if (forced >= 0 && forced < kNumCfgs && cfg_allowed(forced, a.cout, smallc, epi)) return forced;
-  const bool f32out = epi == EPI_F32 || epi == EPI_ACC_F32 || epi == EPI_DGRAD ||
-                      epi == EPI_F32_NCHW;
+  const int ek = epi_kind(epi);
+  const bool f32out = ek == EPI_F32 || ek == EPI_ACC_F32 || ek == EPI_DGRAD ||
+                      ek == EPI_F32_NCHW;
   // the gated input-gradient convs tune apart from the plain ones of the same geometry (their
-  // epilogue is timed for real)
-  const int eclass = epi == EPI_DGRAD_GATE ? 3
-                     : (f32out ? 1 : ((epi == EPI_GRU_ZR || epi == EPI_GRU_Q) ? 2 : 0));
+  // epilogue is timed for real); fp16 operands tune apart from bf16 (LDS-DMA / halo only)
+  const int eclass = (ek == EPI_DGRAD_GATE ? 3
+                      : (f32out ? 1 : ((ek == EPI_GRU_ZR || ek == EPI_GRU_Q) ? 2 : 0))) +
+                     (epi_f16(epi) ? 4 : 0);
   int creal = 0;
   for (int q = 0; q < a.nseg && q < 3; ++q) creal += a.seg[q].real;
   const TuneKey key{P, a.H, a.W, a.KH, a.KW, smallc ? a.cin_small : a.cin_pad, a.cout, (int)smallc,

@@ -75,7 +75,7 @@ struct TapGeo {
 // with two stages the ~1300-cycle chunk of MFMAs did not cover the global -> LDS latency (39% MFMA
 // busy, profiles/r2/pmc_step_final.txt).  The other kernels keep two stages and two or three
 // resident workgroups per CU instead.
-template <int KH, int KW, int TG, int BMT, int NS>
+template <int KH, int KW, int TG, int BMT, int NS, bool F16>
 __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_taps_kernel(
     ConvWgradArgs a, WgradItems it, WgradTapArgs ta) {
   using Geo = TapGeo<KH, KW, TG, BMT>;
@@ -201,7 +201,8 @@ __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_t
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) bsum[i] += (float)af[i][e];
+          for (int e = 0; e < 8; ++e)
+            bsum[i] += F16 ? (float)__builtin_bit_cast(raft_v8f16, af[i])[e] : (float)af[i][e];
       }
       const int ky0 = k >> 3, kx0 = k & 7;     // k and k + 4 share the tile row
 #pragma unroll
@@ -216,7 +217,7 @@ __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_t
         const bf16x8_t bfr = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          acc[tt][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr, acc[tt][i], 0, 0, 0);
+          acc[tt][i] = raft_mfma32<F16>(af[i], bfr, acc[tt][i]);
       }
     }
   };
@@ -358,8 +359,12 @@ template <int KH, int KW, int TG, int BMT, int NS>
 void launch_taps(const ConvWgradArgs& a, const WgradItems& it, const WgradTapArgs& ta,
                  hipStream_t stream) {
   dim3 grid((ta.n_co * ta.n_ci * ta.splits + 7) / 8 * 8);
-  hipLaunchKernelGGL((conv_wgrad_taps_kernel<KH, KW, TG, BMT, NS>), grid,
-                     dim3(TapGeo<KH, KW, TG, BMT>::NT), 0, stream, a, it, ta);
+  if (a.f16)
+    hipLaunchKernelGGL((conv_wgrad_taps_kernel<KH, KW, TG, BMT, NS, true>), grid,
+                       dim3(TapGeo<KH, KW, TG, BMT>::NT), 0, stream, a, it, ta);
+  else
+    hipLaunchKernelGGL((conv_wgrad_taps_kernel<KH, KW, TG, BMT, NS, false>), grid,
+                       dim3(TapGeo<KH, KW, TG, BMT>::NT), 0, stream, a, it, ta);
 }
 
 int taps_stages_3x3() {

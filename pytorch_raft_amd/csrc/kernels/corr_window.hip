@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void corr_lookup_tile_kernel(PyrC4 pyr, const 
 // then interpolated from LDS into the bf16 pixel-row tile, which is streamed out as above.
 constexpr int TPW = 32;  // pixels per workgroup
 
-template <int R, bool BF>
+template <int R, bool BF, bool OF16 = false>
 __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const float* __restrict__ coords,
                                                               uint16_t* __restrict__ out, int cbuf,
                                                               int B, int H, int W, int levels) {
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
     const float* w = win + (px * 4 + l) * EES + iy * WRS + ix;
     const float top = (1.f - ax) * w[0] + ax * w[1];
     const float bot = (1.f - ax) * w[WRS] + ax * w[WRS + 1];
-    tile[px * ROW + ch] = raft_f32_to_bf16((1.f - ay) * top + ay * bot);
+    tile[px * ROW + ch] = raft_f2h<OF16>((1.f - ay) * top + ay * bot);
   }
   __syncthreads();
   const int chunks = cbuf / 8;
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(256) void corr_window_reduce_kernel(WinList wl_, in
 // arithmetic as corr_window_grad_kernel) and adds it into the level planes -- iterations in a
 // fixed order, one writer per cell per round (deterministic; bitwise the two-pass result).  Reads
 // ~0.77 KB per pixel-iteration instead of writing and re-reading a 1.6 KB fp32 window.
-template <int R>
+template <int R, bool TF16 = false>
 __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int levels, int B, int H,
                                                               int W, float inv_sqrt_c,
                                                               void* __restrict__ out, int out_bf16,
@@ -593,8 +593,8 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
           if (iy < 0 || iy >= D) continue;
           const float wy = k == 0 ? (1.f - ay) : ay;
           float sx = 0.f;
-          if (xx < D) sx += (1.f - ax) * raft_bf16_to_f32(T[xx * D + iy]);
-          if (xx > 0) sx += ax * raft_bf16_to_f32(T[(xx - 1) * D + iy]);
+          if (xx < D) sx += (1.f - ax) * raft_h2f<TF16>(T[xx * D + iy]);
+          if (xx > 0) sx += ax * raft_h2f<TF16>(T[(xx - 1) * D + iy]);
           acc += wy * sx;
         }
         planes[off[l] + gy * ws[l] + gx] += acc;
@@ -678,7 +678,7 @@ TapGeo tap_geo(int H, int W, int levels, int radius) {
   return g;
 }
 
-template <int R>
+template <int R, bool TF16 = false>
 __global__ __launch_bounds__(256) void corr_tap_reduce_wave_kernel(TapList tl, TapGeo tg, int levels, int B,
                                                                    int H, int W, float inv_sqrt_c,
                                                                    void* __restrict__ out, int out_bf16) {
@@ -768,8 +768,8 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_wave_kernel(TapList tl, T
           if (iy < 0 || iy >= D) continue;
           const float wy = kk == 0 ? (1.f - ay) : ay;
           float sx = 0.f;
-          if (xx < D) sx += (1.f - ax) * raft_bf16_to_f32(T[xx * D + iy]);
-          if (xx > 0) sx += ax * raft_bf16_to_f32(T[(xx - 1) * D + iy]);
+          if (xx < D) sx += (1.f - ax) * raft_h2f<TF16>(T[xx * D + iy]);
+          if (xx > 0) sx += ax * raft_h2f<TF16>(T[(xx - 1) * D + iy]);
           acc += wy * sx;
         }
         planes[cbase[c] + gy * cps[c] + gx] += acc;
@@ -860,7 +860,7 @@ BoxGeo box_geo(int H, int W, int levels, int radius) {
   return g;
 }
 
-template <int R>
+template <int R, bool TF16 = false>
 __global__ __launch_bounds__(256) void corr_tap_fold_box_kernel(TapList tl, BoxGeo bg, int levels, int B,
                                                                 int H, int W, float inv_sqrt_c,
                                                                 uint16_t* __restrict__ out, int* __restrict__ list) {
@@ -970,7 +970,7 @@ __global__ __launch_bounds__(256) void corr_tap_fold_box_kernel(TapList tl, BoxG
       for (int t = 0; t < D; ++t) {
         const int idx = t + sh;
         const uint32_t h16 = (wd[idx >> 1] >> ((idx & 1) * 16)) & 0xffffu;
-        tc[t] = (rx < D) ? raft_bf16_to_f32((uint16_t)h16) : 0.f;
+        tc[t] = (rx < D) ? raft_h2f<TF16>((uint16_t)h16) : 0.f;
       }
     }
     // the column to the left (lane - 1 of the same 16-lane row; zero for rx = 0)
@@ -1038,7 +1038,7 @@ __global__ __launch_bounds__(256) void corr_tap_fold_box_kernel(TapList tl, BoxG
 
 bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* ws, int levels,
                              const float* coords, uint16_t* out, int cbuf, int B, int H, int W,
-                             int radius, bool pyr_bf16, hipStream_t stream) {
+                             int radius, bool pyr_bf16, int out_f16, hipStream_t stream) {
   PyrC4 p;
   for (int l = 0; l < 4; ++l) {
     p.lvl[l] = l < levels ? static_cast<const float*>(lvl[l]) : nullptr;
@@ -1046,6 +1046,15 @@ bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* w
     p.w[l] = l < levels ? ws[l] : 0;
   }
   const int N = H * W;
+  if (out_f16) {
+    // fp16 taps (fp16 autocast) from the fp32 pyramid of the reference's fp32 correlation
+    if (pyr_bf16) return false;
+    dim3 grid((unsigned)(B * ((N + TPW - 1) / TPW)));
+    if (radius == 4) hipLaunchKernelGGL((corr_lookup_win_kernel<4, false, true>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+    else if (radius == 3) hipLaunchKernelGGL((corr_lookup_win_kernel<3, false, true>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+    else return false;
+    return true;
+  }
   static const bool legacy = [] {
     const char* e = getenv("RAFT_LOOKUP_LEGACY");
     return e && e[0] == '1';
@@ -1137,6 +1146,14 @@ bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, 
   }();
   const int64_t P = (int64_t)B * H * W;
   const int lds = corr_tap_reduce_lds_bytes(H, W, levels, radius);
+  if (tl.tf16) {
+    // fp16 tap gradients (fp16 autocast; fp32 dC as the reference's fp32 correlation): the
+    // workgroup-per-pixel fold
+    dim3 grid((unsigned)P);
+    if (radius == 4) hipLaunchKernelGGL((corr_tap_reduce_kernel<4, true>), grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)nullptr);
+    else hipLaunchKernelGGL((corr_tap_reduce_kernel<3, true>), grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)nullptr);
+    return true;
+  }
   if (mode == 0 && out_bf16 && (W & 1) == 0 && list != nullptr && tl.n <= 32 &&
       (levels * D * D + 7) / 8 <= 64) {
     const BoxGeo bg = box_geo(H, W, levels, radius);

@@ -28,23 +28,31 @@ namespace {
 
 constexpr int FH_C = 256;
 
+// 16-bit operand helpers: bf16 (F16 = false) or fp16 (fp16 autocast: v_dot2_f32_f16)
+template <bool F16>
 __device__ __forceinline__ void bf16x8_to_f32(const uint4 v, float (&f)[8]) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    f[2 * i] = __uint_as_float(w[i] << 16);
-    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    f[2 * i] = raft_h2f<F16>((uint16_t)(w[i] & 0xffffu));
+    f[2 * i + 1] = raft_h2f<F16>((uint16_t)(w[i] >> 16));
   }
 }
 
 typedef __bf16 __attribute__((ext_vector_type(2))) bf16x2_t;
+typedef _Float16 __attribute__((ext_vector_type(2))) f16x2_t;
 
-__device__ __forceinline__ bf16x2_t as_bf2(uint32_t u) { return __builtin_bit_cast(bf16x2_t, u); }
+template <bool F16>
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)raft_f32_to_bf16(lo) | ((uint32_t)raft_f32_to_bf16(hi) << 16);
+  return (uint32_t)raft_f2h<F16>(lo) | ((uint32_t)raft_f2h<F16>(hi) << 16);
 }
+template <bool F16>
 __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
-  return __builtin_amdgcn_fdot2_f32_bf16(as_bf2(a), as_bf2(b), c, false);
+  if constexpr (F16)
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2_t, a), __builtin_bit_cast(f16x2_t, b), c, false);
+  else
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b),
+                                           c, false);
 }
 
 // out[b,o,y,x] = bias[o] + sum_{t,c} in[b, y+ky-1, x+kx-1, c] * W[o][c][t]
@@ -52,7 +60,7 @@ __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
 // every load (weights once, then all pixels' taps) is issued before the first use, so the launch
 // costs one memory round trip; NPIX > 1 divides the weight-table re-reads.  wf: bf16 pairs
 // [t][o][c/2] from the packing gather; products by v_dot2_f32_bf16; 32-lane shuffle reduction.
-template <int NPIX>
+template <int NPIX, bool F16>
 __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict__ in, int cs,
                                                       const uint32_t* __restrict__ wf,
                                                       const float* __restrict__ bias,
@@ -87,14 +95,14 @@ __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      a0 = dot2(v[k][t].x, w0[t].x, a0);
-      a1 = dot2(v[k][t].x, w1[t].x, a1);
-      a2 = dot2(v[k][t].y, w0[t].y, a2);
-      a3 = dot2(v[k][t].y, w1[t].y, a3);
-      a0 = dot2(v[k][t].z, w0[t].z, a0);
-      a1 = dot2(v[k][t].z, w1[t].z, a1);
-      a2 = dot2(v[k][t].w, w0[t].w, a2);
-      a3 = dot2(v[k][t].w, w1[t].w, a3);
+      a0 = dot2<F16>(v[k][t].x, w0[t].x, a0);
+      a1 = dot2<F16>(v[k][t].x, w1[t].x, a1);
+      a2 = dot2<F16>(v[k][t].y, w0[t].y, a2);
+      a3 = dot2<F16>(v[k][t].y, w1[t].y, a3);
+      a0 = dot2<F16>(v[k][t].z, w0[t].z, a0);
+      a1 = dot2<F16>(v[k][t].z, w1[t].z, a1);
+      a2 = dot2<F16>(v[k][t].w, w0[t].w, a2);
+      a3 = dot2<F16>(v[k][t].w, w1[t].w, a3);
     }
     float s0 = a0 + a2, s1 = a1 + a3;
 #pragma unroll
@@ -113,9 +121,9 @@ __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict
 
 // dx[b,y,x,c] = [fm > 0] * sum_{ky,kx,o} gout[b,o,y-ky+1,x-kx+1] * W[o][c][ky][kx]
 // thread = (NPIX pixels, 8-channel group); all loads issued up front as in the forward.  Per
-// channel the two output channels form one bf16 pair: s[c] += dot2((g0, g1), (W0[c], W1[c])),
+// channel the two output channels form one bf16 pair: s[c] += dot2<F16>((g0, g1), (W0[c], W1[c])),
 // wd: pairs [t][c] from the packing gather.
-template <int NPIX>
+template <int NPIX, bool F16>
 __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict__ gout,
                                                         const uint32_t* __restrict__ wd,
                                                         const uint16_t* __restrict__ fm, int fs,
@@ -145,7 +153,7 @@ __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict_
       const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
       const int64_t o = ok ? (int64_t)yy * W + xx : 0;
       const float d0 = g0[o], d1 = g0[hw + o];
-      gp[k][t] = ok ? pack_bf2(d0, d1) : 0u;
+      gp[k][t] = ok ? pack_bf2<F16>(d0, d1) : 0u;
     }
     m[k] = *reinterpret_cast<const uint4*>(fm + pc * fs + g * 8);
   }
@@ -158,7 +166,7 @@ __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict_
     for (int t = 0; t < 9; ++t) {
       const uint32_t wv[8] = {wa[t].x, wa[t].y, wa[t].z, wa[t].w, wb[t].x, wb[t].y, wb[t].z, wb[t].w};
 #pragma unroll
-      for (int i = 0; i < 8; ++i) s[i] = dot2(gp[k][t], wv[i], s[i]);
+      for (int i = 0; i < 8; ++i) s[i] = dot2<F16>(gp[k][t], wv[i], s[i]);
     }
     const uint32_t mw[4] = {m[k].x, m[k].y, m[k].z, m[k].w};
     uint32_t ov[4];
@@ -166,8 +174,8 @@ __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict_
     for (int q = 0; q < 4; ++q) {
       const bool lo = (mw[q] & 0x8000u) == 0 && (mw[q] & 0x7fffu) != 0;
       const bool hi = (mw[q] & 0x80000000u) == 0 && (mw[q] & 0x7fff0000u) != 0;
-      const uint32_t a = lo ? raft_f32_to_bf16(s[2 * q]) : 0u;
-      const uint32_t c = hi ? raft_f32_to_bf16(s[2 * q + 1]) : 0u;
+      const uint32_t a = lo ? raft_f2h<F16>(s[2 * q]) : 0u;
+      const uint32_t c = hi ? raft_f2h<F16>(s[2 * q + 1]) : 0u;
       ov[q] = a | (c << 16);
     }
     const int64_t p = ((int64_t)blockIdx.x * NPIX + k) * 8 + (threadIdx.x >> 5);
@@ -181,6 +189,7 @@ __global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict_
 // loads per lane (the 72 gathers per thread made the per-pixel kernel ~4x slower than its bytes).
 // thread = 8-channel group (tid & 31) x 8 of the tile's pixels.
 constexpr int DTH = 4, DTW = 16;
+template <bool F16>
 __global__ __launch_bounds__(256) void fh2_dgrad_tile_kernel(const float* __restrict__ gout,
                                                              const uint32_t* __restrict__ wd,
                                                              const uint16_t* __restrict__ fm, int fs,
@@ -202,7 +211,7 @@ __global__ __launch_bounds__(256) void fh2_dgrad_tile_kernel(const float* __rest
     uint32_t v = 0u;
     if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
       const int64_t o = (int64_t)yy * W + xx;
-      v = pack_bf2(g0[o], g0[hw + o]);
+      v = pack_bf2<F16>(g0[o], g0[hw + o]);
     }
     gp[e] = v;
   }
@@ -237,7 +246,7 @@ __global__ __launch_bounds__(256) void fh2_dgrad_tile_kernel(const float* __rest
       const uint32_t wv[8] = {wa[tap].x, wa[tap].y, wa[tap].z, wa[tap].w,
                               wb[tap].x, wb[tap].y, wb[tap].z, wb[tap].w};
 #pragma unroll
-      for (int i = 0; i < 8; ++i) s[i] = dot2(gv, wv[i], s[i]);
+      for (int i = 0; i < 8; ++i) s[i] = dot2<F16>(gv, wv[i], s[i]);
     }
     const uint32_t mw[4] = {m[k].x, m[k].y, m[k].z, m[k].w};
     uint32_t ov[4];
@@ -245,8 +254,8 @@ __global__ __launch_bounds__(256) void fh2_dgrad_tile_kernel(const float* __rest
     for (int q = 0; q < 4; ++q) {
       const bool lo = (mw[q] & 0x8000u) == 0 && (mw[q] & 0x7fffu) != 0;
       const bool hi = (mw[q] & 0x80000000u) == 0 && (mw[q] & 0x7fff0000u) != 0;
-      const uint32_t a = lo ? raft_f32_to_bf16(s[2 * q]) : 0u;
-      const uint32_t c = hi ? raft_f32_to_bf16(s[2 * q + 1]) : 0u;
+      const uint32_t a = lo ? raft_f2h<F16>(s[2 * q]) : 0u;
+      const uint32_t c = hi ? raft_f2h<F16>(s[2 * q + 1]) : 0u;
       ov[q] = a | (c << 16);
     }
     const int yy = y0 + py, xx = x0 + px;
@@ -258,6 +267,7 @@ __global__ __launch_bounds__(256) void fh2_dgrad_tile_kernel(const float* __rest
 
 // dw[o][t*256 + c] += sum_items sum_p gout[p][o] * in[p + off_t][c];  db[o] += sum gout[p][o]
 // block 256 = 8 row lanes x 32 channel groups; a unit = (item, image, 8-row block)
+template <bool F16>
 __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int B, int H, int W,
                                                         float* __restrict__ part) {
   __shared__ float red[8 * 32 * 73];  // 72 accumulators (+1 pad) per thread, one half at a time
@@ -315,7 +325,7 @@ __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int
 #pragma unroll
           for (int k = 0; k < 3; ++k) {
             float f[8];
-            bf16x8_to_f32(win[r][j + k], f);
+            bf16x8_to_f32<F16>(win[r][j + k], f);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
               acc[0][r * 3 + k][i] = fmaf(d0, f[i], acc[0][r * 3 + k][i]);
@@ -369,16 +379,20 @@ __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int
 }  // namespace
 
 bool launch_fh2_fwd(const uint16_t* in, int cs, const uint32_t* wf, const float* bias, float* out,
-                    int B, int H, int W, hipStream_t stream) {
+                    int B, int H, int W, int f16, hipStream_t stream) {
   if (cs % 8 != 0 || cs < FH_C) return false;
   const int64_t P = (int64_t)B * H * W;
-  hipLaunchKernelGGL(fh2_fwd_kernel<2>, dim3(raft_cdiv(P, 16)), dim3(256), 0, stream, in, cs, wf, bias, out,
-                     B, H, W);
+  if (f16)
+    hipLaunchKernelGGL((fh2_fwd_kernel<2, true>), dim3(raft_cdiv(P, 16)), dim3(256), 0, stream, in, cs, wf,
+                       bias, out, B, H, W);
+  else
+    hipLaunchKernelGGL((fh2_fwd_kernel<2, false>), dim3(raft_cdiv(P, 16)), dim3(256), 0, stream, in, cs, wf,
+                       bias, out, B, H, W);
   return true;
 }
 
 bool launch_fh2_dgrad(const float* gout, const uint32_t* wd, const uint16_t* fm, int fs, uint16_t* dx,
-                      int ds, int B, int H, int W, hipStream_t stream) {
+                      int ds, int B, int H, int W, int f16, hipStream_t stream) {
   if (fs % 8 != 0 || ds % 8 != 0 || fs < FH_C || ds < FH_C) return false;
   static const bool v1 = [] {
     const char* e = getenv("RAFT_FH2_DGRAD_V1");
@@ -386,21 +400,32 @@ bool launch_fh2_dgrad(const float* gout, const uint32_t* wd, const uint16_t* fm,
   }();
   if (!v1) {
     const int ty = (H + DTH - 1) / DTH, tx = (W + DTW - 1) / DTW;
-    hipLaunchKernelGGL(fh2_dgrad_tile_kernel, dim3((unsigned)(B * ty * tx)), dim3(256), 0, stream,
-                       gout, wd, fm, fs, dx, ds, B, H, W, ty, tx);
+    if (f16)
+      hipLaunchKernelGGL(fh2_dgrad_tile_kernel<true>, dim3((unsigned)(B * ty * tx)), dim3(256), 0, stream,
+                         gout, wd, fm, fs, dx, ds, B, H, W, ty, tx);
+    else
+      hipLaunchKernelGGL(fh2_dgrad_tile_kernel<false>, dim3((unsigned)(B * ty * tx)), dim3(256), 0, stream,
+                         gout, wd, fm, fs, dx, ds, B, H, W, ty, tx);
     return true;
   }
   const int64_t P = (int64_t)B * H * W;
-  hipLaunchKernelGGL(fh2_dgrad_kernel<4>, dim3(raft_cdiv(P, 32)), dim3(256), 0, stream, gout, wd, fm, fs,
-                     dx, ds, B, H, W);
+  if (f16)
+    hipLaunchKernelGGL((fh2_dgrad_kernel<4, true>), dim3(raft_cdiv(P, 32)), dim3(256), 0, stream, gout, wd,
+                       fm, fs, dx, ds, B, H, W);
+  else
+    hipLaunchKernelGGL((fh2_dgrad_kernel<4, false>), dim3(raft_cdiv(P, 32)), dim3(256), 0, stream, gout, wd,
+                       fm, fs, dx, ds, B, H, W);
   return true;
 }
 
 int fh2_wgrad_units(int n, int B, int H) { return n * B * ((H + 7) / 8); }
 
 bool launch_fh2_wgrad(const Fh2Items& it, int cs, int B, int H, int W, float* part, int blocks,
-                      hipStream_t stream) {
+                      int f16, hipStream_t stream) {
   if (it.n < 1 || it.n > RAFT_FH2_MAX_ITEMS || cs % 8 != 0 || cs < FH_C || blocks < 1) return false;
-  hipLaunchKernelGGL(fh2_wgrad_kernel, dim3(blocks), dim3(256), 0, stream, it, cs, B, H, W, part);
+  if (f16)
+    hipLaunchKernelGGL(fh2_wgrad_kernel<true>, dim3(blocks), dim3(256), 0, stream, it, cs, B, H, W, part);
+  else
+    hipLaunchKernelGGL(fh2_wgrad_kernel<false>, dim3(blocks), dim3(256), 0, stream, it, cs, B, H, W, part);
   return true;
 }

@@ -90,7 +90,14 @@ enum ConvEpilogue {
   EPI_F32_NCHW = 7,   // out0 f32 NCHW (B, cout, H, W)
   EPI_DGRAD_GATE = 8, // EPI_DGRAD + the fused ConvGRU gate backward (OSeg.gate); its own
                       // instantiation: the gate math's registers stay out of the plain dgrads
+  // operand-type flag OR-ed into an epilogue id: every 16-bit operand / output of the conv is
+  // fp16 (v_mfma_f32_32x32x16_f16; fp16 autocast) instead of bf16.  The names above say "BF16"
+  // for "16-bit operand type".  LDS-DMA and halo kernels only (the register-staged configs
+  // are bf16-only)
+  EPI_F16 = 16,
 };
+inline constexpr int epi_kind(int epi) { return epi & 15; }
+inline constexpr bool epi_f16(int epi) { return (epi & EPI_F16) != 0; }
 
 struct Seg {
   const uint16_t* ptr;  // bf16 NHWC base, already offset to the segment's first channel
@@ -201,6 +208,7 @@ struct ConvWgradArgs {
   int pix_per_split;
   int splits_per_item;  // multi-item kernel: blockIdx.y = item * splits_per_item + split
   uint32_t w_magic;     // ceil(2^32 / W): q = umulhi(n, w_magic) = n / W for n * W < 2^32
+  int f16;              // 1: fp16 operands (v_mfma_f32_32x32x16_f16), 0: bf16
 };
 
 // the iterations of one step whose weight gradients are summed by one launch
@@ -260,10 +268,10 @@ struct BfPtrs {
   const uint16_t* p[RAFT_SUM_MAX];
 };
 void launch_sum_bf16(const BfPtrs& ins, int n, const float* carry, void* out, bool out_f32,
-                     int64_t numel, hipStream_t stream);
+                     int64_t numel, int f16, hipStream_t stream);
 // (B,2,H,W) fp32 flow -> (B,H,W,128) bf16 7x7 patch (tap-major, 2 ch), + optional flow slot
 void launch_f1_patch(const float* flow, uint16_t* patch, uint16_t* slot, int slot_stride, int B, int H,
-                     int W, hipStream_t stream);
+                     int W, int f16, hipStream_t stream);
 
 // ---- flow_head.conv2 (3x3, 256 -> 2): fwd / dgrad (+ReLU gate) / multi-item wgrad (flow_head2.hip)
 #define RAFT_FH2_MAX_ITEMS 32
@@ -273,14 +281,15 @@ struct Fh2Items {
   int n;
 };
 // wf: bf16 pairs [t][o][c/2] (9*2*128 uint32); wd: bf16 pairs (W0[c], W1[c]) [t][c] (9*256 uint32)
+// f16: fp16 activations / weight pairs (v_dot2_f32_f16) instead of bf16
 bool launch_fh2_fwd(const uint16_t* in, int cs, const uint32_t* wf, const float* bias, float* out,
-                    int B, int H, int W, hipStream_t stream);
+                    int B, int H, int W, int f16, hipStream_t stream);
 bool launch_fh2_dgrad(const float* gout, const uint32_t* wd, const uint16_t* fm, int fs, uint16_t* dx,
-                      int ds, int B, int H, int W, hipStream_t stream);
+                      int ds, int B, int H, int W, int f16, hipStream_t stream);
 // part: (blocks, 2*2304 + 2) fp32 per-workgroup partial [dw | db] rows (fully written)
 int fh2_wgrad_units(int n, int B, int H);
 bool launch_fh2_wgrad(const Fh2Items& it, int cs, int B, int H, int W, float* part, int blocks,
-                      hipStream_t stream);
+                      int f16, hipStream_t stream);
 
 // ---- NHWC lookup tile + window-compact backward (corr_window.hip)
 #define RAFT_MAX_WIN 32
@@ -291,9 +300,10 @@ struct WinList {
   int cbuf;
   int n;
 };
+// out_f16: fp16 taps (fp32 pyramid only) instead of bf16
 bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* ws, int levels,
                              const float* coords, uint16_t* out, int cbuf, int B, int H, int W,
-                             int radius, bool pyr_bf16, hipStream_t stream);
+                             int radius, bool pyr_bf16, int out_f16, hipStream_t stream);
 bool launch_corr_window_grad(const float* coords, const uint16_t* dout, int cbuf, float* wg, int B,
                              int H, int W, int levels, int radius, hipStream_t stream);
 struct TapList {
@@ -303,6 +313,7 @@ struct TapList {
   int n;
   int ldo;  // row pitch of the (B, N, ldo) output (elements, >= N, even for bf16 when N is);
             // columns N..ldo-1 are written as zeros (the MFMA backward GEMMs' K padding)
+  int tf16; // 1: the tap gradients are fp16 (fp16 autocast), 0: bf16
 };
 int corr_tap_reduce_lds_bytes(int H, int W, int levels, int radius);
 // list: (1 + B*H*W) ints of scratch for the box fold's overflow list (nullptr: no box fold)
@@ -349,17 +360,25 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
                      float* dgamma, float* dbeta, float* dcbias, uint16_t* dx, hipStream_t stream);
 
-// ---- multi-tensor AdamW + global-norm clip (adamw.hip)
+// ---- multi-tensor AdamW + global-norm clip + GradScaler unscale / overflow skip (adamw.hip)
 struct AdamTensor {
   float* p;
-  const float* g;
+  float* g;
   float* m;
   float* v;
   int64_t numel;
+  float* step;  // device step counter of this tensor (advanced on every finite step)
+  int group;    // index into the AdamGroup table
+};
+struct AdamGroup {
+  const float* lr_dev;  // nullable: lr from the device (graph-ready schedule)
+  float lr, wd, b1, b2, omb1, omb2, eps;  // omb = 1 - beta computed in double on the host
 };
 int adam_chunk_elems();
-// tab / cum: device tables (T tensors, cum[T] = nchunks); part: nchunks floats; coef: 2 floats
-// (clip coefficient, total norm); max_norm <= 0: no clipping
-void launch_adamw_multi(const AdamTensor* tab, const int* cum, int T, int nchunks, const float* lr_dev,
-                        float lr_host, double b1, double b2, float eps, float wd, float bc1, float bc2,
-                        float max_norm, float* part, float* coef, hipStream_t stream);
+// tab / cum / groups: device tables (T tensors, cum[T] = nchunks); part: nchunks floats;
+// coef: 3 floats (gradient multiplier, total norm, found_inf); max_norm <= 0: no clipping;
+// inv_scale (nullable): 1 / GradScaler scale; need_norm: run the sum-of-squares pass (clipping or
+// overflow detection); found_inf (nullable): the GradScaler's flag, written
+void launch_adamw_multi(const AdamTensor* tab, const int* cum, int T, int nchunks, const AdamGroup* groups,
+                        float max_norm, const float* inv_scale, int need_norm, int write_grad,
+                        float* part, float* coef, float* found_inf, hipStream_t stream);

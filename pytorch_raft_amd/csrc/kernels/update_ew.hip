@@ -92,6 +92,7 @@ __global__ __launch_bounds__(256) void flow_prep_kernel(const float* __restrict_
 // weight gradient both run through the regular MFMA kernels.  Also writes the flow into the
 // motion-feature slot (`core/update.py:96`, cat([out, flow])).
 // thread = (pixel, 8-channel chunk of 16)
+template <bool F16>
 __global__ __launch_bounds__(256) void f1_patch_kernel(const float* __restrict__ flow,
                                                        uint16_t* __restrict__ patch,
                                                        uint16_t* __restrict__ slot, int slot_stride,
@@ -115,15 +116,15 @@ __global__ __launch_bounds__(256) void f1_patch_kernel(const float* __restrict__
         const int yy = y + tap / 7 - 3, xx = x + tap % 7 - 3;
         if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
           const int64_t o = (int64_t)yy * W + xx;
-          v = (uint32_t)raft_f32_to_bf16(fx[o]) | ((uint32_t)raft_f32_to_bf16(fx[HW + o]) << 16);
+          v = (uint32_t)raft_f2h<F16>(fx[o]) | ((uint32_t)raft_f2h<F16>(fx[HW + o]) << 16);
         }
       }
       w[j] = v;
     }
     *reinterpret_cast<uint4*>(patch + p * 128 + chunk * 8) = make_uint4(w[0], w[1], w[2], w[3]);
     if (slot != nullptr && chunk == 0) {
-      slot[p * slot_stride] = raft_f32_to_bf16(fx[yx]);
-      slot[p * slot_stride + 1] = raft_f32_to_bf16(fx[HW + yx]);
+      slot[p * slot_stride] = raft_f2h<F16>(fx[yx]);
+      slot[p * slot_stride + 1] = raft_f2h<F16>(fx[HW + yx]);
     }
   }
 }
@@ -132,6 +133,7 @@ __global__ __launch_bounds__(256) void f1_patch_kernel(const float* __restrict__
 // The ConvGRU context input is the same tensor in every iteration, so the context part of each
 // GRU conv's input / weight gradient is linear in the iterations' pre-activation gradients:
 // one conv over their sum replaces one per iteration (ops/update_hip.py).
+template <bool F16>
 __global__ __launch_bounds__(256) void sum_bf16_kernel(BfPtrs ins, int n, const float* __restrict__ carry,
                                                        void* __restrict__ out, int out_f32,
                                                        int64_t total8) {
@@ -152,8 +154,8 @@ __global__ __launch_bounds__(256) void sum_bf16_kernel(BfPtrs ins, int n, const 
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        acc[2 * j] += __uint_as_float(w[j] << 16);
-        acc[2 * j + 1] += __uint_as_float(w[j] & 0xffff0000u);
+        acc[2 * j] += raft_h2f<F16>((uint16_t)(w[j] & 0xffffu));
+        acc[2 * j + 1] += raft_h2f<F16>((uint16_t)(w[j] >> 16));
       }
     }
     if (out_f32) {
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(256) void sum_bf16_kernel(BfPtrs ins, int n, const 
       uint32_t w[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        w[j] = (uint32_t)raft_f32_to_bf16(acc[2 * j]) | ((uint32_t)raft_f32_to_bf16(acc[2 * j + 1]) << 16);
+        w[j] = (uint32_t)raft_f2h<F16>(acc[2 * j]) | ((uint32_t)raft_f2h<F16>(acc[2 * j + 1]) << 16);
       reinterpret_cast<uint4*>(out)[t] = make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
@@ -234,10 +236,14 @@ void launch_phase_marker(hipStream_t stream) {
 }
 
 void launch_sum_bf16(const BfPtrs& ins, int n, const float* carry, void* out, bool out_f32,
-                     int64_t numel, hipStream_t stream) {
+                     int64_t numel, int f16, hipStream_t stream) {
   const int64_t total8 = numel / 8;
-  hipLaunchKernelGGL(sum_bf16_kernel, dim3(ew_blocks(total8)), dim3(256), 0, stream, ins, n, carry, out,
-                     out_f32 ? 1 : 0, total8);
+  if (f16)
+    hipLaunchKernelGGL(sum_bf16_kernel<true>, dim3(ew_blocks(total8)), dim3(256), 0, stream, ins, n, carry,
+                       out, out_f32 ? 1 : 0, total8);
+  else
+    hipLaunchKernelGGL(sum_bf16_kernel<false>, dim3(ew_blocks(total8)), dim3(256), 0, stream, ins, n, carry,
+                       out, out_f32 ? 1 : 0, total8);
 }
 
 void launch_relu_bwd(const float* g, int gs, const uint16_t* y, int ys, uint16_t* out, int os, int P,
@@ -267,10 +273,14 @@ void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int sl
 }
 
 void launch_f1_patch(const float* flow, uint16_t* patch, uint16_t* slot, int slot_stride, int B, int H,
-                     int W, hipStream_t stream) {
+                     int W, int f16, hipStream_t stream) {
   const int64_t total = (int64_t)B * H * W * 16;
-  hipLaunchKernelGGL(f1_patch_kernel, dim3(ew_blocks(total)), dim3(256), 0, stream, flow, patch, slot,
-                     slot_stride, B, H, W);
+  if (f16)
+    hipLaunchKernelGGL(f1_patch_kernel<true>, dim3(ew_blocks(total)), dim3(256), 0, stream, flow, patch,
+                       slot, slot_stride, B, H, W);
+  else
+    hipLaunchKernelGGL(f1_patch_kernel<false>, dim3(ew_blocks(total)), dim3(256), 0, stream, flow, patch,
+                       slot, slot_stride, B, H, W);
 }
 
 void launch_split_hilo(const float* x, int64_t sb, int64_t sc, int64_t sh, int64_t sw, int B, int C,

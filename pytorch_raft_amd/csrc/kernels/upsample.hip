@@ -196,6 +196,19 @@ __device__ __forceinline__ void mask_st4(uint16_t* p, const float (&v)[4]) {
 __device__ __forceinline__ void mask_st4(float* p, const float (&v)[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
 }
+// fp16 mask (fp16 autocast)
+__device__ __forceinline__ void mask_ld4(const _Float16* p, float (&v)[4]) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  v[0] = raft_h2f<true>((uint16_t)(u.x & 0xffffu));
+  v[1] = raft_h2f<true>((uint16_t)(u.x >> 16));
+  v[2] = raft_h2f<true>((uint16_t)(u.y & 0xffffu));
+  v[3] = raft_h2f<true>((uint16_t)(u.y >> 16));
+}
+__device__ __forceinline__ void mask_st4(_Float16* p, const float (&v)[4]) {
+  *reinterpret_cast<uint2*>(p) =
+      make_uint2((uint32_t)raft_f2h<true>(v[0]) | ((uint32_t)raft_f2h<true>(v[1]) << 16),
+                 (uint32_t)raft_f2h<true>(v[2]) | ((uint32_t)raft_f2h<true>(v[3]) << 16));
+}
 
 // 16 lanes per cell, 4 consecutive sub-pixels per lane (4 cells per wave): 8-B (bf16) / 16-B
 // (fp32) mask reads, 16-B output stores
@@ -322,7 +335,10 @@ __global__ __launch_bounds__(256) void convex_up_nhwc_bwd_kernel(const float* __
 bool launch_convex_up_nhwc_fwd(const float* flow, const void* mask, int mask_is_bf16, float* out,
                                int B, int H, int W, hipStream_t stream) {
   const int64_t cells = (int64_t)B * H * W;
-  if (mask_is_bf16)
+  if (mask_is_bf16 == 2)   // mask kind: 0 fp32, 1 bf16, 2 fp16
+    hipLaunchKernelGGL(convex_up_nhwc_fwd_kernel<_Float16>, dim3(raft_cdiv(cells, 16)), dim3(256), 0,
+                       stream, flow, static_cast<const _Float16*>(mask), out, B, H, W);
+  else if (mask_is_bf16)
     hipLaunchKernelGGL(convex_up_nhwc_fwd_kernel<uint16_t>, dim3(raft_cdiv(cells, 16)), dim3(256), 0,
                        stream, flow, static_cast<const uint16_t*>(mask), out, B, H, W);
   else
@@ -335,7 +351,11 @@ bool launch_convex_up_nhwc_bwd(const float* flow, const void* mask, int mask_is_
                                const float* dout, void* dmask, float* wbuf, float* dflow, int B,
                                int H, int W, hipStream_t stream) {
   const int64_t cells = (int64_t)B * H * W;
-  if (mask_is_bf16)
+  if (mask_is_bf16 == 2)
+    hipLaunchKernelGGL(convex_up_nhwc_bwd_kernel<_Float16>, dim3(raft_cdiv(cells, 16)), dim3(256), 0,
+                       stream, flow, static_cast<const _Float16*>(mask), dout,
+                       static_cast<_Float16*>(dmask), wbuf, B, H, W);
+  else if (mask_is_bf16)
     hipLaunchKernelGGL(convex_up_nhwc_bwd_kernel<uint16_t>, dim3(raft_cdiv(cells, 16)), dim3(256), 0,
                        stream, flow, static_cast<const uint16_t*>(mask), dout,
                        static_cast<uint16_t*>(dmask), wbuf, B, H, W);

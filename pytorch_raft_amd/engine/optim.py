@@ -1,11 +1,11 @@
 """Optimizer + LR schedule (reference `fetch_optimizer`, `train.py:79-86`).
 
 AdamW(lr, weight_decay, eps) and OneCycleLR(max_lr=lr, total_steps=num_steps+100, pct_start=0.05,
-cycle_momentum=False, anneal_strategy='linear').  On GPU (no GradScaler) the update is
-:class:`FusedAdamW`: the global-norm gradient clip and AdamW over all ~150 parameter tensors in
-three launches of the native multi-tensor kernel (``csrc/kernels/adamw.hip``: one workgroup per
-4096-element chunk of any tensor).  torch's fused AdamW took 4 launches x ~72 us plus the foreach
-clip on RAFT's 5.3 M parameters.  With a GradScaler (fp16) or on the CPU it is torch's AdamW.
+cycle_momentum=False, anneal_strategy='linear').  On GPU the update is :class:`FusedAdamW`: the
+global-norm gradient clip, the fp16 GradScaler's unscale / overflow skip and AdamW over all ~150
+parameter tensors in three launches of the native multi-tensor kernel (``csrc/kernels/adamw.hip``:
+one workgroup per 4096-element chunk of any tensor).  torch's fused AdamW took 4 launches x ~72 us
+plus the foreach clip on RAFT's 5.3 M parameters.  On the CPU it is torch's AdamW.
 """
 import os
 
@@ -15,47 +15,76 @@ import torch.optim as optim
 
 class FusedAdamW(optim.Optimizer):
     """torch.optim.AdamW semantics (non-amsgrad, decoupled weight decay) on the native multi-tensor
-    kernel; ``step(max_norm=c)`` first clips the gradients' global 2-norm to ``c`` exactly as
-    ``torch.nn.utils.clip_grad_norm_`` does (coefficient min(1, c / (norm + 1e-6))), on the device,
-    without writing the clipped gradients back.  ``lr`` may be a float or a one-element device
-    tensor (the graph-ready step keeps it on the device; the LR scheduler fills it)."""
+    kernel.  ``step(max_norm=c, scaler=s)`` is, in one pass over the gradients of EVERY group,
+    ``s.unscale_(opt); clip_grad_norm_(all params, c); s.step(opt); s.update()``:
+
+    * the clip coefficient min(1, c / (norm + 1e-6)) comes from the global 2-norm over all groups
+      (as ``torch.nn.utils.clip_grad_norm_`` over all parameters), and the clipped (unscaled)
+      gradients are written back to ``.grad`` (``write_grad=False`` skips that store);
+    * with an enabled GradScaler the gradients are unscaled by 1/S inside the kernels, a
+      non-finite norm skips the whole step on the device (parameters, moments and step counts
+      untouched) and the scale is updated on the device (``torch._amp_update_scale_``): no host
+      sync, so the step can run inside a replayed training step;
+    * every tensor keeps its own device step counter (advanced only on finite steps), so tensors
+      that missed gradients on earlier steps get their own bias corrections, as in torch.
+
+    ``lr`` may be a float or a one-element device tensor (the graph-ready step keeps it on the
+    device; the LR scheduler fills it)."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.last_norm = None
 
     @torch.no_grad()
-    def step(self, closure=None, max_norm=None):
+    def step(self, closure=None, max_norm=None, scaler=None, write_grad=True):
         assert closure is None, 'FusedAdamW takes no closure'
         from ..ops import _ext
         ops = _ext.ops()
-        for group in self.param_groups:
-            ps, gs, ms, vs = [], [], [], []
+        ps, gs, ms, vs, steps, gof = [], [], [], [], [], []
+        lr_t, lrs, b1s, b2s, epss, wds = [], [], [], [], [], []
+        for gi, group in enumerate(self.param_groups):
             for p in group['params']:
                 if p.grad is None:
                     continue
                 st = self.state[p]
                 if not st:
-                    # a CPU tensor like torch's step counter: snapshots / roll-backs that treat
-                    # every tensor entry alike (GraphedTrainStep._restore) reset it too
-                    st['step'] = torch.zeros((), dtype=torch.float32)
+                    st['step'] = torch.zeros((), dtype=torch.float32, device=p.device)
                     st['exp_avg'] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                st['step'] += 1
+                elif st['step'].device != p.device or st['step'].dtype != torch.float32:
+                    st['step'] = st['step'].to(p.device, torch.float32)  # a loaded CPU counter
+                if not p.grad.is_contiguous():
+                    p.grad = p.grad.contiguous()
                 ps.append(p)
-                gs.append(p.grad.contiguous())
+                gs.append(p.grad)
                 ms.append(st['exp_avg'])
                 vs.append(st['exp_avg_sq'])
-            if not ps:
-                continue
-            b1, b2 = group['betas']
-            t = int(self.state[ps[0]]['step'].item())   # CPU tensor: no device sync
+                steps.append(st['step'])
+                gof.append(gi)
             lr = group['lr']
-            lr_t = lr if isinstance(lr, torch.Tensor) else None
-            self.last_norm = ops.adamw_step_(
-                ps, gs, ms, vs, lr_t, 0.0 if lr_t is not None else float(lr), b1, b2,
-                group['eps'], group['weight_decay'], 1.0 - b1 ** t, 1.0 - b2 ** t,
-                float(max_norm) if max_norm else 0.0)
+            is_t = isinstance(lr, torch.Tensor)
+            lr_t.append(lr if is_t else torch.empty(0))
+            lrs.append(0.0 if is_t else float(lr))
+            b1, b2 = group['betas']
+            b1s.append(float(b1))
+            b2s.append(float(b2))
+            epss.append(float(group['eps']))
+            wds.append(float(group['weight_decay']))
+        if not ps:
+            return None
+        inv = found = None
+        use_scaler = scaler is not None and scaler.is_enabled()
+        if use_scaler:
+            assert scaler._scale is not None, 'GradScaler.scale() must run before the step'
+            inv = scaler._scale.double().reciprocal().float()
+            found = torch.zeros(1, device=ps[0].device)
+        res = ops.adamw_step_(ps, gs, ms, vs, steps, gof, lr_t, lrs, b1s, b2s, epss, wds,
+                              float(max_norm) if max_norm else 0.0, inv, found, bool(write_grad))
+        self.last_norm = res[:2]
+        if use_scaler:
+            torch._amp_update_scale_(scaler._scale, scaler._growth_tracker, found,
+                                     scaler._growth_factor, scaler._backoff_factor,
+                                     scaler._growth_interval)
         return None
 
 
@@ -63,7 +92,7 @@ def _use_fused_adamw(params, amp_fp16):
     # RAFT_FUSED_ADAMW=0: torch's fused AdamW + foreach clip (A/B)
     if os.environ.get('RAFT_FUSED_ADAMW', '1') == '0':
         return False
-    if amp_fp16 or not params or not params[0].is_cuda:
+    if not params or not params[0].is_cuda:
         return False
     try:
         from ..ops import _ext
@@ -99,8 +128,8 @@ def fetch_optimizer(args, model, fused=None, capturable=False, amp_fp16=False):
 def clip_and_step(optimizer, parameters, max_norm, scaler=None):
     """Global-norm clip + optimizer step: folded into one native pass for FusedAdamW, otherwise
     torch's foreach clip (after the scaler's unscale) and the (scaler's) step."""
-    if isinstance(optimizer, FusedAdamW) and (scaler is None or not scaler.is_enabled()):
-        optimizer.step(max_norm=max_norm)
+    if isinstance(optimizer, FusedAdamW):
+        optimizer.step(max_norm=max_norm, scaler=scaler)
         return
     if scaler is not None:
         scaler.unscale_(optimizer)

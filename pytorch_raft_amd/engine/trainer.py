@@ -30,7 +30,7 @@ import torch.distributed as dist
 
 from ..ops.loss import sequence_loss
 from ..parallel import dist as pdist
-from .optim import fetch_optimizer, clip_grad_norm_, clip_and_step
+from .optim import fetch_optimizer, clip_grad_norm_, clip_and_step, FusedAdamW
 
 
 # RAFT_PHASE_MARKS=1: an empty marker kernel before and after each decode replay, so a kernel
@@ -142,7 +142,11 @@ class GraphedTrainStep:
 
     def __init__(self, st, example, warmup=2):
         assert st.device.type == 'cuda', 'graph capture needs a GPU'
-        assert not st.scaler.is_enabled(), 'use bf16 autocast (no GradScaler) with graph capture'
+        # fp16 autocast: the GradScaler's loss scale is a device tensor the captured backward
+        # multiplies by, and the unscale / overflow skip / scale update run on the device inside
+        # FusedAdamW's step (no host sync), so fp16 steps replay like bf16 ones
+        assert not st.scaler.is_enabled() or isinstance(st.optimizer, FusedAdamW), \
+            'graph capture with a GradScaler needs the device-side FusedAdamW step'
         self.st = st
         self.world = pdist.world_size()
         model = st.model
@@ -248,7 +252,7 @@ class GraphedTrainStep:
             s.grad = None
         preds = st.model.decode(*self.sfeat, iters=st.args.iters)
         loss, metrics = sequence_loss(preds, self.sflow, self.svalid, st.args.gamma)
-        loss.backward()
+        st.scaler.scale(loss).backward()   # fp16: times the device loss scale; else the loss
         return loss, metrics
 
     def _encode_and_stage(self, image1, image2, flow, valid):
@@ -333,7 +337,7 @@ class GraphedTrainStep:
 
     def _update_graphable(self, loss):
         st = self.st
-        clip_and_step(st.optimizer, self.params, st.args.clip)
+        clip_and_step(st.optimizer, self.params, st.args.clip, st.scaler)
         st.nonfinite += (~torch.isfinite(loss.detach())).float()
 
     def _sched(self):
@@ -354,8 +358,12 @@ class GraphedTrainStep:
             stt = st.optimizer.state.get(p)
             if stt:
                 opt_state[p] = {k: v.clone() if torch.is_tensor(v) else v for k, v in stt.items()}
+        scaler = None
+        if st.scaler.is_enabled() and st.scaler._scale is not None:
+            scaler = (st.scaler._scale.clone(), st.scaler._growth_tracker.clone())
         return dict(model={k: v.clone() for k, v in st.model.state_dict().items()},
-                    opt=opt_state, sched=st.scheduler.state_dict(), nonfinite=st.nonfinite.clone())
+                    opt=opt_state, sched=st.scheduler.state_dict(), nonfinite=st.nonfinite.clone(),
+                    scaler=scaler)
 
     @torch.no_grad()
     def _restore(self, snap):
@@ -382,6 +390,13 @@ class GraphedTrainStep:
             t.fill_(float(v))
             g['lr'] = t
         st.nonfinite.copy_(snap['nonfinite'])
+        if st.scaler.is_enabled() and st.scaler._scale is not None:
+            if snap['scaler'] is not None:
+                st.scaler._scale.copy_(snap['scaler'][0])
+                st.scaler._growth_tracker.copy_(snap['scaler'][1])
+            else:   # created by the warm-up steps: back to the initial scale
+                st.scaler._scale.fill_(st.scaler._init_scale)
+                st.scaler._growth_tracker.zero_()
         torch.cuda.synchronize(st.device)
 
     # ---------------------------------------------------------------- public

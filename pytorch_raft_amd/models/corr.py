@@ -144,19 +144,20 @@ class CorrBlock:
             return self.volume.lookup(coords, self.radius)
         return torch_corr_lookup(self.corr_pyramid, coords, self.radius)
 
-    def lookup_nhwc(self, coords, cbuf):
-        """bf16 (B,H,W,cbuf) zero-padded taps for the fused HIP update block."""
+    def lookup_nhwc(self, coords, cbuf, dtype=torch.bfloat16):
+        """(B,H,W,cbuf) zero-padded taps for the fused HIP update block, in its operand dtype
+        (bf16, or fp16 under fp16 autocast: written from the fp32 pyramid)."""
         if self.hip:
-            return self.volume.lookup_nhwc(coords, self.radius, cbuf)
-        return _to_nhwc_padded(self(coords), cbuf)
+            return self.volume.lookup_nhwc(coords, self.radius, cbuf, dtype)
+        return _to_nhwc_padded(self(coords), cbuf, dtype)
 
     @staticmethod
     def corr(fmap1, fmap2):
         return torch_corr_volume(fmap1, fmap2)
 
 
-def _to_nhwc_padded(corr, cbuf):
-    x = corr.permute(0, 2, 3, 1).to(torch.bfloat16)
+def _to_nhwc_padded(corr, cbuf, dtype=torch.bfloat16):
+    x = corr.permute(0, 2, 3, 1).to(dtype)
     if cbuf > x.shape[-1]:
         x = F.pad(x, (0, cbuf - x.shape[-1]))
     return x.contiguous()
@@ -186,8 +187,10 @@ class AlternateCorrBlock:
             return self.volume.lookup(coords, self.radius)
         return torch_onthefly_corr(self.pyramid2, self.fmap1, coords, self.radius)
 
-    def lookup_nhwc(self, coords, cbuf):
-        """bf16 (B,H,W,cbuf) zero-padded taps for the fused HIP update block."""
+    def lookup_nhwc(self, coords, cbuf, dtype=torch.bfloat16):
+        """(B,H,W,cbuf) zero-padded taps for the fused HIP update block (bf16 MFMA taps; an fp16
+        update block gets them converted)."""
         if self.hip:
-            return self.volume.lookup_nhwc(coords, self.radius, cbuf)
-        return _to_nhwc_padded(self(coords), cbuf)
+            out = self.volume.lookup_nhwc(coords, self.radius, cbuf)
+            return out if out.dtype == dtype else out.to(dtype)
+        return _to_nhwc_padded(self(coords), cbuf, dtype)

@@ -165,15 +165,17 @@ class RAFT(nn.Module):
             # build takes the bf16 encoder outputs as they are (same products, fp32 accumulation)
             fmap1 = fmap1.float().contiguous()
             fmap2 = fmap2.float().contiguous()
+        # bf16 mixed precision: bf16 MFMA correlation; fp32 model and fp16 autocast: the
+        # reference's fp32 correlation (`core/raft.py:102-107`, outside autocast)
+        corr_prec = 'bf16' if (self.args.mixed_precision and self.amp_dtype == torch.bfloat16) \
+            else 'fp32'
         if otf:
-            # mixed precision: bf16 MFMA operands; fp32 model: split-bf16 (fp32-accurate) forward
+            # bf16: bf16 MFMA operands; fp32: split-bf16 (fp32-accurate) forward and backward
             corr_fn = AlternateCorrBlock(fmap1, fmap2, radius=self.args.corr_radius,
-                                         impl=self.corr_impl,
-                                         precision='bf16' if self.args.mixed_precision else 'fp32')
+                                         impl=self.corr_impl, precision=corr_prec)
         else:
             corr_fn = CorrBlock(fmap1, fmap2, radius=self.args.corr_radius, impl=self.corr_impl,
-                                precision='bf16' if self.args.mixed_precision else 'fp32',
-                                nhwc_lookup=self._use_fused_update(fmap1))
+                                precision=corr_prec, nhwc_lookup=self._use_fused_update(fmap1))
         dev = fmap1.device
         b, _, h8, w8 = fmap1.shape
         coords0 = coords_grid(b, h8, w8, device=dev)
@@ -238,14 +240,17 @@ class RAFT(nn.Module):
                 and _ext.device_ok(img) and _ext.gpu_path_enabled())
 
     def _use_fused_update(self, img):
-        """Fused MFMA update block (full and small model): GPU, bf16 mixed precision (its
-        compute dtype)."""
+        """Fused MFMA update block: GPU and mixed precision -- bf16 (full and small model) or
+        fp16 autocast (full model; the operand dtype of the conv kernels' MFMAs)."""
         impl = _get(self.args, 'update_impl', 'auto')
         if impl == 'torch' or self.corr_impl == 'torch' or not _ext.device_ok(img):
             return False
-        if not (self.args.mixed_precision and self.amp_dtype == torch.bfloat16):
+        ok = self.args.mixed_precision and (
+            self.amp_dtype == torch.bfloat16 or (self.amp_dtype == torch.float16 and not self.args.small))
+        if not ok:
             if impl == 'hip':
-                raise ValueError("update_impl='hip' needs mixed_precision with amp_dtype='bfloat16'")
+                raise ValueError("update_impl='hip' needs mixed precision (bf16, or fp16 for the "
+                                 "full model)")
             return False
         from ..ops import update_hip
         return update_hip.available(required=(impl == 'hip'))
@@ -279,15 +284,16 @@ class RAFT(nn.Module):
         if self.args.small:
             return self._iterate_fused_small(net, inp, corr_fn, coords0, coords1, iters, test_mode)
         from ..ops.update_hip import HipUpdateBlock, CORR_BUF
-        hub = HipUpdateBlock(self.update_block)
-        h = net.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
-        x = inp.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+        adt = self.amp_dtype   # operand dtype of the fused block: bf16, or fp16 autocast
+        hub = HipUpdateBlock(self.update_block, dtype=adt)
+        h = net.to(adt).permute(0, 2, 3, 1).contiguous()
+        x = inp.to(adt).permute(0, 2, 3, 1).contiguous()
         flow_predictions = []
         flow_up = None
         flow = coords1 - coords0
         for itr in range(iters):
             coords1 = coords1.detach()
-            corr = corr_fn.lookup_nhwc(coords1, CORR_BUF)
+            corr = corr_fn.lookup_nhwc(coords1, CORR_BUF, adt)
             # flow = coords1 - coords0 of the detached coords: the previous iteration's upsampling
             # input, detached (same values; one subtraction kernel per iteration instead of two)
             flow = flow.detach()

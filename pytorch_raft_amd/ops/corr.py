@@ -149,10 +149,11 @@ class _AllPairsLookupNHWC(torch.autograd.Function):
     the fused update block's first 1x1 conv (no NCHW->NHWC transpose, no fp32->bf16 cast kernel)."""
 
     @staticmethod
-    def forward(ctx, token, coords, radius, state, cbuf):
+    def forward(ctx, token, coords, radius, state, cbuf, dtype=torch.bfloat16):
         b, _, h, w = coords.shape
-        # the tile kernel writes every channel of each pixel row, padding included
-        out = torch.empty(b, h, w, cbuf, device=coords.device, dtype=torch.bfloat16)
+        # the tile kernel writes every channel of each pixel row, padding included; fp16 taps
+        # (fp16 autocast) come from an fp32 pyramid
+        out = torch.empty(b, h, w, cbuf, device=coords.device, dtype=dtype)
         _ext.ops().corr_lookup_nhwc_(state.pyramid, coords, radius, out)
         ctx.state = state
         ctx.radius = radius
@@ -166,15 +167,17 @@ class _AllPairsLookupNHWC(torch.autograd.Function):
         b, _, h, w = coords.shape
         levels = len(st.pyramid)
         if _window_reduce_fits(h, w, levels) and len(st.taps) < 32 and dout.shape[-1] % 8 == 0:
-            # keep the iteration's bf16 tap gradient; all iterations are folded into dcorr once
-            # per step straight from these rows (corr_tap_reduce)
-            st.taps.append((coords, dout.to(torch.bfloat16).contiguous()))
+            # keep the iteration's 16-bit tap gradient (bf16, or fp16 under fp16 autocast); all
+            # iterations are folded into dcorr once per step straight from these rows
+            # (corr_tap_reduce)
+            td = dout.dtype if dout.dtype in (torch.bfloat16, torch.float16) else torch.bfloat16
+            st.taps.append((coords, dout.to(td).contiguous()))
             st.radius = ctx.radius
         else:
             if st.grad is None:
                 st.grad = [torch.zeros_like(p) for p in st.pyramid]
             _ext.ops().corr_lookup_bwd_(st.grad, coords, dout.float().contiguous(), ctx.radius)
-        return None, None, None, None, None
+        return None, None, None, None, None, None
 
 
 def _window_reduce_fits(h, w, levels):
@@ -212,9 +215,11 @@ class AllPairsVolume:
             raise RuntimeError('bf16 pyramid: only the NHWC lookup (lookup_nhwc) reads it')
         return _AllPairsLookup.apply(self.token, coords.contiguous().float(), radius, self.state)
 
-    def lookup_nhwc(self, coords, radius, cbuf):
+    def lookup_nhwc(self, coords, radius, cbuf, dtype=torch.bfloat16):
+        if dtype != torch.bfloat16 and self.state.pyr_bf16:
+            raise RuntimeError('bf16 pyramid: the NHWC lookup writes bf16 taps')
         return _AllPairsLookupNHWC.apply(self.token, coords.contiguous().float(), radius, self.state,
-                                         cbuf)
+                                         cbuf, dtype)
 
 
 def _pool_nhwc(x):

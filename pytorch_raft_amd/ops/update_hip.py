@@ -295,8 +295,9 @@ class _Packed:
     def defer_wgrad(self, name, g, g_off, segs):
         self.pending.setdefault(name, []).append((g, g_off, segs))
 
-    def __init__(self, ub, params, device, need_grad, design=FULL):
+    def __init__(self, ub, params, device, need_grad, design=FULL, dtype=torch.bfloat16):
         self.design = design
+        self.dtype = dtype   # operand dtype of the packed weights (bf16, or fp16 autocast)
         self.w = {}
         self.wd = {}
         self.x = {}
@@ -313,7 +314,7 @@ class _Packed:
         with torch.no_grad():
             flat = torch.cat([p.detach().float().reshape(-1) for p in params] +
                              [torch.zeros(1, device=device)])
-            packed = flat.index_select(0, plan.widx).to(torch.bfloat16)
+            packed = flat.index_select(0, plan.widx).to(dtype)
             off = 0
             for kind, name, shape in plan.views:
                 n = shape[0] * shape[1]
@@ -387,13 +388,14 @@ class _State:
         self.dinp_acc = None   # fp32 gradient w.r.t. the context input, summed over iterations
         self.ctx_g = {}        # GRU conv -> its pre-activation gradients of the iterations run
         self.design = FULL
+        self.dtype = torch.bfloat16  # operand dtype (fp16 under fp16 autocast)
 
 
 class _UpdateWeights(torch.autograd.Function):
     @staticmethod
     def forward(ctx, state, *params):
         state.packed = _Packed(state.ub, params, params[0].device, need_grad=state.need_grad,
-                               design=state.design)
+                               design=state.design, dtype=state.dtype)
         ctx.state = state
         ctx.n = len(params)
         return params[0].new_zeros(())
@@ -541,8 +543,9 @@ class _Branch:
             self.main.wait_stream(self.side)
 
 
-def _bf16(shape, dev):
-    return torch.empty(*shape, device=dev, dtype=torch.bfloat16)
+def _bf16(shape, dev, dt=torch.bfloat16):
+    """16-bit activation buffer: bf16, or fp16 under fp16 autocast (the operand dtype of a step)."""
+    return torch.empty(*shape, device=dev, dtype=dt)
 
 
 def _f32(shape, dev, zero=False):
@@ -569,7 +572,7 @@ def ctx_maps(pk, inp):
     for name in GRU_CONVS:
         s = SPEC[name + 'i']
         m = torch.empty(B, H, W, s.cout, device=inp.device,
-                        dtype=torch.bfloat16 if _CTX_BF16 else torch.float32)
+                        dtype=inp.dtype if _CTX_BF16 else torch.float32)
         C.conv_fwd([(inp, 0, HD)], pk.w[s.name], pk.b[s.name], s.k, s.pad, s.cout,
                    C.EPI_BF16 if _CTX_BF16 else C.EPI_F32, [m], [0])
         pk.ctx[name] = m
@@ -599,14 +602,15 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
     flow-head half of the fused head conv and skips the mask conv: ~20 % of the iteration."""
     B, H, W, _ = h.shape
     dev = h.device
+    dt = h.dtype   # operand dtype: bf16, or fp16 under fp16 autocast
     sh = (B, H, W)
-    patch = _bf16(sh + (128,), dev)  # f1_patch writes all 128 channels
-    mf = _bf16(sh + (128,), dev)
+    patch = _bf16(sh + (128,), dev, dt)  # f1_patch writes all 128 channels
+    mf = _bf16(sh + (128,), dev, dt)
     ops = _ext.ops()
     ops.f1_patch_(flow, patch, mf, 126)
-    c1 = _bf16(sh + (256,), dev)
-    cf = _bf16(sh + (256,), dev)
-    f1 = _bf16(sh + (128,), dev)
+    c1 = _bf16(sh + (256,), dev, dt)
+    cf = _bf16(sh + (256,), dev, dt)
+    f1 = _bf16(sh + (128,), dev, dt)
 
     def conv(name, segs, epi, outs, offs, aux=(), aux_offs=(), split=0, cout=None, bias=None):
         s = SPEC[name]
@@ -630,10 +634,10 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
     hin = h
     ctx = ctx_maps(pk, inp)
     for tag in ('1', '2'):
-        z, rh, r = _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev)
+        z, rh, r = _bf16(sh + (HD,), dev, dt), _bf16(sh + (HD,), dev, dt), _bf16(sh + (HD,), dev, dt)
         conv('zr' + tag, [(hin, 0, HD), (mf, 0, 128)], C.EPI_GRU_ZR, [z, rh, r],
              [0, 0, 0], aux=[hin], aux_offs=[0], split=HD, bias=ctx['zr' + tag])
-        hn, q = _bf16(sh + (HD,), dev), _bf16(sh + (HD,), dev)
+        hn, q = _bf16(sh + (HD,), dev, dt), _bf16(sh + (HD,), dev, dt)
         conv('q' + tag, [(rh, 0, HD), (mf, 0, 128)], C.EPI_GRU_Q, [hn, q], [0, 0],
              aux=[hin, z], aux_offs=[0, 0], bias=ctx['q' + tag])
         gates[tag] = (hin, z, rh, r, q)
@@ -641,16 +645,16 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
     h2 = hin
     delta = torch.empty(B, 2, H, W, device=dev, dtype=torch.float32)
     if need_mask:
-        fm = _bf16(sh + (512,), dev)
+        fm = _bf16(sh + (512,), dev, dt)
         conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0])
-        mask = _bf16(sh + (576,), dev)
+        mask = _bf16(sh + (576,), dev, dt)
         br = _Branch(dev)
         with br:
             conv('m2', [(fm, 256, 256)], C.EPI_BF16, [mask], [0])
         ops.fh2_fwd_(fm, pk.fh2_wf, pk.b32, delta)
         br.join()
     else:
-        fm = _bf16(sh + (256,), dev)
+        fm = _bf16(sh + (256,), dev, dt)
         conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0], cout=256)
         ops.fh2_fwd_(fm, pk.fh2_wf, pk.b32, delta)
         mask = None
@@ -693,6 +697,7 @@ class _UpdateIter(torch.autograd.Function):
         B, H, W, _ = h2.shape
         P = B * H * W
         dev = h2.device
+        dt = h2.dtype
         sh = (B, H, W)
         ops = _ext.ops()
 
@@ -710,7 +715,7 @@ class _UpdateIter(torch.autograd.Function):
             s = SPEC[name]
             ry = [o[5] if len(o) > 5 else o[0] for o in outs]
             # relu offset -1 marks a plain (ungated) bf16 output
-            roff = [int(o[6]) if len(o) > 5 else (-1 if o[0].dtype == torch.bfloat16 else 0)
+            roff = [int(o[6]) if len(o) > 5 else (-1 if o[0].dtype != torch.float32 else 0)
                     for o in outs]
             gmode, gt = [], []
             if gates is not None:
@@ -727,14 +732,14 @@ class _UpdateIter(torch.autograd.Function):
 
         # ---- mask head (mask = 0.25 * conv(fm[256:]))
         if gmask is None:
-            gmask = _bf16(sh + (576,), dev).zero_()
+            gmask = _bf16(sh + (576,), dev, dt).zero_()
         if gdelta is None:
             gdelta = torch.zeros(B, 2, H, W, device=dev, dtype=torch.float32)
         gmask = gmask.contiguous()
-        if gmask.dtype != torch.bfloat16:
-            gmask = gmask.to(torch.bfloat16)
+        if gmask.dtype != dt:
+            gmask = gmask.to(dt)
         # the head's ReLU backward is fused into both dgrad epilogues (bf16 pre-activation grads)
-        dpre_head = _bf16(sh + (512,), dev)
+        dpre_head = _bf16(sh + (512,), dev, dt)
         gd = gdelta.contiguous().float()
         wgrad('m2', gmask, 0, [(fm, 256, 256)])
         br = _Branch(dev)
@@ -763,7 +768,7 @@ class _UpdateIter(torch.autograd.Function):
             finalises its output-state gradient: -> (spec, (d pre-q, d pre-z|r, dh of its input));
             the r half of d pre-z|r is written by the q dgrad's epilogue (gate 2)."""
             hin, z, _, _, q = half
-            bufs = (_bf16(sh + (HD,), dev), _bf16(sh + (2 * HD,), dev), _f32(sh + (HD,), dev))
+            bufs = (_bf16(sh + (HD,), dev, dt), _bf16(sh + (2 * HD,), dev, dt), _f32(sh + (HD,), dev))
             return (1, [z, q, hin, bufs[0], bufs[1], bufs[2]]), bufs
 
         if _GATES_FUSED:
@@ -788,7 +793,7 @@ class _UpdateIter(torch.autograd.Function):
                       gates=[(2, [r, r, hin, dpre_zr, dpre_zr, dhp])],
                       wpk=pk.wd['q' + tag][:HD])
             else:
-                dpre_q = _bf16(sh + (HD,), dev)
+                dpre_q = _bf16(sh + (HD,), dev, dt)
                 dz = _f32(sh + (HD,), dev)
                 dhp = _f32(sh + (HD,), dev)
                 ops.gru_q_bwd_(dh, z, q, hin, dpre_q, dz, dhp)
@@ -796,7 +801,7 @@ class _UpdateIter(torch.autograd.Function):
                 drh = _f32(sh + (HD,), dev)
                 dgrad('q' + tag, [(dpre_q, 0, HD)], [(drh, 0, HD, HD, 0)],
                       wpk=pk.wd['q' + tag][:HD])
-                dpre_zr = _bf16(sh + (2 * HD,), dev)
+                dpre_zr = _bf16(sh + (2 * HD,), dev, dt)
                 ops.gru_zr_bwd_(drh, dz, z, r, hin, dpre_zr, dhp)
             ctx_g.setdefault('q' + tag, []).append(dpre_q)
             ctx_g.setdefault('zr' + tag, []).append(dpre_zr)
@@ -812,7 +817,7 @@ class _UpdateIter(torch.autograd.Function):
             elif _GATES_FUSED:
                 # the last accumulation into dmf: the motion-encoder ReLU backward (its forward
                 # output is mf) in this epilogue -> bf16 d pre-activation, dmf is never re-read
-                dpre_conv = _bf16(sh + (128,), dev)
+                dpre_conv = _bf16(sh + (128,), dev, dt)
                 dgrad('zr' + tag, zsegs, zr_outs,
                       gates=[None, (3, [mf, mf, mf, dpre_conv, dpre_conv, dmf])], wpk=zw, kcin=zk)
             else:
@@ -820,17 +825,17 @@ class _UpdateIter(torch.autograd.Function):
             dh = dhp
         # ---- motion encoder
         if not _GATES_FUSED:
-            dpre_conv = _bf16(sh + (128,), dev)
+            dpre_conv = _bf16(sh + (128,), dev, dt)
             ops.relu_bwd_(dmf, 0, mf, 0, dpre_conv, 0, 128, 1.0)
         wgrad('conv', dpre_conv, 0, [(cf, 0, 256)])
-        dpre_cf = _bf16(sh + (256,), dev)
+        dpre_cf = _bf16(sh + (256,), dev, dt)
         dgrad('conv', [(dpre_conv, 0, 128)], [(dpre_cf, 0, 256, 256, 0, cf, 0)])
         wgrad('c2', dpre_cf, 0, [(c1, 0, 256)])
         wgrad('f2', dpre_cf, 192, [(f1, 0, 128)])
-        dpre_c1 = _bf16(sh + (256,), dev)
-        dpre_f1 = _bf16(sh + (128,), dev)
+        dpre_c1 = _bf16(sh + (256,), dev, dt)
+        dpre_f1 = _bf16(sh + (128,), dev, dt)
         # bf16 (the dtype of the corr input): autograd would otherwise cast an fp32 gradient
-        dcorr = _bf16(sh + (CORR_BUF,), dev)
+        dcorr = _bf16(sh + (CORR_BUF,), dev, dt)
         br = _Branch(dev)
         with br:   # f2's input gradient only feeds f1's (deferred) weight gradient
             dgrad('f2', [(dpre_cf, 192, 64)], [(dpre_f1, 0, 128, 128, 0, f1, 0)])
@@ -857,7 +862,7 @@ class _UpdateIter(torch.autograd.Function):
             # still runs that backward, which takes the real fp32 gradient from dh_carry
             st.dh_carry = dh
             if st.zero_h is None:
-                st.zero_h = torch.zeros((), device=dev, dtype=torch.bfloat16)
+                st.zero_h = torch.zeros((), device=dev, dtype=dt)
             return (None, st.zero_h.expand(B, H, W, h0.shape[-1]), dinp, dcorr, None, None)
         return (None, dh, dinp, dcorr, None, None)
 
@@ -865,9 +870,10 @@ class _UpdateIter(torch.autograd.Function):
 class HipUpdateBlock:
     """Drives the fused iterations for one forward pass of a BasicUpdateBlock."""
 
-    def __init__(self, update_block):
+    def __init__(self, update_block, dtype=torch.bfloat16):
         self.state = _State()
         self.state.ub = update_block
+        self.state.dtype = dtype
         params = flat_params(update_block)
         self.state.need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         self.state.params = params

@@ -21,7 +21,8 @@ class _ConvexUpsample(torch.autograd.Function):
     def forward(ctx, flow, mask, nhwc):
         flow = flow.contiguous().float()
         mask = mask.contiguous()
-        if mask.dtype not in (torch.float32, torch.bfloat16):
+        # fp16 masks (fp16 autocast) run on the NHWC kernels only
+        if mask.dtype not in (torch.float32, torch.bfloat16) and not (nhwc and mask.dtype == torch.float16):
             mask = mask.float()
         ctx.save_for_backward(flow, mask)
         ctx.nhwc = nhwc

@@ -52,4 +52,13 @@ if [ -n "$PMC" ]; then
   python scripts/pmc_summary.py /tmp/pmc_${TAG}_1 /tmp/pmc_${TAG}_2 /tmp/pmc_${TAG}_3 2 > $O/pmc.txt 2>&1 || true
   head -3 $O/pmc.txt
 fi
+if [ -n "$AB" ]; then
+  # A/B on one box: alternating runs of the default build and the build under $AB (VAR=value)
+  step ab
+  for i in 1 2; do
+    timeout -k 10 300 env $AB python bench.py $BENCH_ARGS > $O/ab_alt_$i.log 2>&1 || { tail -3 $O/ab_alt_$i.log; exit 1; }
+    timeout -k 10 300 python bench.py $BENCH_ARGS > $O/ab_def_$i.log 2>&1 || { tail -3 $O/ab_def_$i.log; exit 1; }
+    echo "$AB: $(grep -o '"value": [0-9.]*' $O/ab_alt_$i.log)   default: $(grep -o '"value": [0-9.]*' $O/ab_def_$i.log)"
+  done
+fi
 step done

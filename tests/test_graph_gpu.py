@@ -30,13 +30,18 @@ def _model(args, dev, sd=None):
     return m
 
 
-@pytest.mark.parametrize('alt,mixed', [(False, True), (True, True), (False, False)])
-def test_graph_step_matches_eager(ext_ops, alt, mixed):
-    """bf16 (fused update block) and fp32 (split-bf16 MFMA update-block convs) steps."""
+@pytest.mark.parametrize('alt,prec', [(False, 'bf16'), (True, 'bf16'), (False, 'fp32'),
+                                      (False, 'fp16')])
+def test_graph_step_matches_eager(ext_ops, alt, prec):
+    """bf16 and fp16 (fused update block; fp16 with the GradScaler's loss scale in the captured
+    backward and its unscale / overflow skip / scale update in the device-side AdamW step) and
+    fp32 (split-bf16 MFMA update-block convs) steps."""
     from pytorch_raft_amd.engine.trainer import TrainState, GraphedTrainStep
     from pytorch_raft_amd.data.synthetic import device_batches
     dev = torch.device('cuda', 0)
-    args = _args(alternate_corr=alt, mixed_precision=mixed)
+    kw = dict(alternate_corr=alt, mixed_precision=prec != 'fp32',
+              amp_dtype='float16' if prec == 'fp16' else 'bfloat16')
+    args = _args(**kw)
     m = _model(args, dev)
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     batches = device_batches(4, 128, 192, dev, count=3, seed=3)
@@ -45,25 +50,39 @@ def test_graph_step_matches_eager(ext_ops, alt, mixed):
         return torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).detach().reshape(-1)
                           .float().clone() for p in mm.parameters()])
 
+    def moments(st, mm):
+        # first-moment state after step 1 = (1 - b1) x the clipped (unscaled) gradient: the
+        # optimizer-level check of the graphed path (bias correction, clip, unscale, lr)
+        return torch.cat([st.optimizer.state[p]['exp_avg'].reshape(-1).clone()
+                          if p in st.optimizer.state else torch.zeros(p.numel(), device=dev)
+                          for p in mm.parameters()])
+
     def eager_run():
-        mm = _model(_args(alternate_corr=alt, mixed_precision=mixed), dev, sd)
-        st = TrainState(mm, _args(alternate_corr=alt, mixed_precision=mixed), dev)
+        mm = _model(_args(**kw), dev, sd)
+        st = TrainState(mm, _args(**kw), dev)
         losses = [float(st.step(*batches[0])[0].detach())]
-        g1 = grads(mm)
+        g1, m1 = grads(mm), moments(st, mm)
         losses += [float(st.step(*batches[k])[0].detach()) for k in range(1, 3)]
-        return losses, torch.cat([p.detach().reshape(-1) for p in mm.parameters()]), st, g1
+        return losses, torch.cat([p.detach().reshape(-1) for p in mm.parameters()]), st, g1, m1
 
-    eager, w_e1, st, g_e1 = eager_run()
-    _, w_e2, _, g_e2 = eager_run()   # run-to-run noise of the eager step (MIOpen atomics, bf16)
+    eager, w_e1, st, g_e1, m_e1 = eager_run()
+    # run-to-run noise of the eager step (MIOpen atomics, bf16)
+    _, w_e2, _, g_e2, m_e2 = eager_run()
 
-    m2 = _model(_args(alternate_corr=alt, mixed_precision=mixed), dev, sd)
-    st2 = TrainState(m2, _args(alternate_corr=alt, mixed_precision=mixed), dev, graph_ready=True)
+    m2 = _model(_args(**kw), dev, sd)
+    st2 = TrainState(m2, _args(**kw), dev, graph_ready=True)
     g = GraphedTrainStep(st2, batches[0], warmup=2)
     # roll-back: weights are the initial ones again
     for n, p in m2.named_parameters():
         assert torch.equal(p.detach(), sd[n]), n
+    if prec == 'fp16':
+        assert st2.scaler.is_enabled() and float(st2.scaler.get_scale()) == st2.scaler._init_scale
+        assert m2._use_fused_update(batches[0][0]), 'fp16 must run the fused update block'
     graph = [float(g.step(*batches[0])[0].detach())]
-    g_g1 = grads(m2)
+    g_g1, m_g1 = grads(m2), moments(st2, m2)
+    mnoise = float((m_e2 - m_e1).norm() / m_e1.norm())
+    merr = float((m_g1 - m_e1).norm() / m_e1.norm())
+    assert merr <= max(3 * mnoise, 2e-3), (merr, mnoise)
     graph += [float(g.step(*batches[k])[0].detach()) for k in range(1, 3)]
     torch.cuda.synchronize()
     assert g.check_finite()
