@@ -952,15 +952,16 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
   a.B = (int)B; a.H = (int)H; a.W = (int)W;
   a.KH = (int)kh; a.KW = (int)kw; a.PH = (int)ph; a.PW = (int)pw;
   a.cout = (int)cout;
-  // fp32 dw: accumulated (+=); bf16 dw: stored (the encoders' bf16 weight gradients)
-  const bool dw_bf16 = dw.scalar_type() == at::kBFloat16;
+  // fp32 dw: accumulated (+=); bf16 / fp16 dw: stored (the encoders' 16-bit weight gradients)
+  const bool dw_bf16 = dw.scalar_type() == at::kBFloat16 || dw.scalar_type() == at::kHalf;
   TORCH_CHECK(dw.is_cuda() && dw.is_contiguous() && (dw_bf16 || dw.scalar_type() == at::kFloat),
-              "grad_weight must be a contiguous fp32 or bf16 GPU tensor");
+              "grad_weight must be a contiguous fp32, bf16 or fp16 GPU tensor");
   const int64_t kpad = kh * kw * cin_pad;
   TORCH_CHECK(dw.dim() == 2 && dw.size(0) == cout && dw.size(1) == kpad, "grad_weight must be (cout, kpad)");
   TORCH_CHECK(kpad % 4 == 0, "packed K must be a multiple of 4");
   a.dw = dw_bf16 ? nullptr : dw.data_ptr<float>();
-  ta.dw_bf16 = dw_bf16 ? reinterpret_cast<uint16_t*>(dw.data_ptr<at::BFloat16>()) : nullptr;
+  ta.dw_bf16 = dw_bf16 ? u16m(dw) : nullptr;
+  ta.dw_f16 = dw.scalar_type() == at::kHalf ? 1 : 0;
   a.kpad = (int)kpad;
   ta.bm = (kh == 3 && kw == 3 && cout <= 64) ? 64 : 128;
   ta.n_co = (int)((cout + ta.bm - 1) / ta.bm);
@@ -1161,10 +1162,11 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
 }
 
 // ------------------------------------------------------------------ encoder norm + activation
-// Tensors are NCHW-shaped channels_last bf16 (the memory is NHWC).
-void check_cl_bf16(const Tensor& t, const char* name) {
-  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 4, name,
-              ": must be a 4-D bf16 GPU tensor");
+// Tensors are NCHW-shaped channels_last bf16, or fp16 under fp16 autocast (the memory is NHWC);
+// every 16-bit tensor of one call has the dtype st of its first.
+void check_cl16(at::ScalarType st, const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == st && t.dim() == 4, name,
+              ": must be a 4-D GPU tensor of dtype ", st);
   TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name, ": must be channels_last");
   TORCH_CHECK(t.size(1) % 8 == 0 && t.size(1) <= 256, name, ": channels must be a multiple of 8, <= 256");
 }
@@ -1182,8 +1184,9 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
                               const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
                               double momentum, double eps, const c10::optional<Tensor>& res,
                               const Tensor& y) {
-  check_cl_bf16(x, "x");
-  check_cl_bf16(y, "y");
+  const at::ScalarType st = op16(x);
+  check_cl16(st, x, "x");
+  check_cl16(st, y, "y");
   TORCH_CHECK(y.sizes() == x.sizes(), "y shape");
   TORCH_CHECK(mode >= 0 && mode <= 3, "mode");
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
@@ -1196,29 +1199,29 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
   if (mode == 2) TORCH_CHECK(rm && rv, "eval batch norm needs running stats");
   const uint16_t* rp = nullptr;
   if (res.has_value() && res->defined()) {
-    check_cl_bf16(*res, "res");
+    check_cl16(st, *res, "res");
     TORCH_CHECK(res->sizes() == x.sizes(), "res shape");
-    rp = reinterpret_cast<const uint16_t*>(res->data_ptr<at::BFloat16>());
+    rp = u16(*res);
   }
   const int groups = mode == 0 ? (int)N : 1;
   auto fo = x.options().dtype(at::kFloat);
   Tensor mean = at::empty({groups, C}, fo), invstd = at::empty({groups, C}, fo);
   Tensor scale = at::empty({N, C}, fo), shift = at::empty({N, C}, fo);
-  const uint16_t* xp = reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>());
+  const uint16_t* xp = u16(x);
   int ppb = 0, nblk = 0;
   Tensor part;
   if (mode <= 1) {
     nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
     part = at::empty({groups * (nblk + 1) * 2 * C}, fo);  // partials + per-group sums
     launch_norm_stats(xp, (int)N, (int)HW, (int)C, mode == 0, part.data_ptr<float>(), nblk, ppb,
-                      cur_stream());
+                      st == at::kHalf, cur_stream());
   }
   launch_norm_finalize(mode <= 1 ? part.data_ptr<float>() : nullptr, xp, (int)N, (int)HW, (int)C,
                        (int)mode, nblk, gp, bp, cb, rm, rv, (float)momentum, (float)eps,
                        mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
-                       shift.data_ptr<float>(), cur_stream());
+                       shift.data_ptr<float>(), st == at::kHalf, cur_stream());
   launch_norm_apply(xp, scale.data_ptr<float>(), shift.data_ptr<float>(), (int)N, (int)HW, (int)C,
-                    (int)relu, rp, reinterpret_cast<uint16_t*>(y.data_ptr<at::BFloat16>()), cur_stream());
+                    (int)relu, rp, u16m(y), st == at::kHalf, cur_stream());
   return {mean, invstd};
 }
 
@@ -1227,10 +1230,12 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y
                const Tensor& mean, const Tensor& invstd, int64_t mode, int64_t relu, const c10::optional<Tensor>& gamma,
                const c10::optional<Tensor>& beta, const c10::optional<Tensor>& dgamma,
                const c10::optional<Tensor>& dbeta, const c10::optional<Tensor>& dcbias,
-               const Tensor& dx) {
-  check_cl_bf16(dy, "dy");
-  check_cl_bf16(x, "x");
-  check_cl_bf16(dx, "dx");
+               const Tensor& dx, const c10::optional<Tensor>& dy2, const c10::optional<Tensor>& yres,
+               const c10::optional<Tensor>& gout) {
+  const at::ScalarType st = op16(dy);
+  check_cl16(st, dy, "dy");
+  check_cl16(st, x, "x");
+  check_cl16(st, dx, "dx");
   TORCH_CHECK(dy.sizes() == x.sizes() && dx.sizes() == x.sizes(), "shapes");
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
   const int groups = mode == 0 ? (int)N : 1;
@@ -1250,43 +1255,63 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y
   Tensor coef = at::empty({groups, 5, C}, fo);  // A, B', C', scale, shift per (group, c), SoA
   const uint16_t* yp = nullptr;
   if (y.has_value() && y->defined()) {
-    check_cl_bf16(*y, "y");
+    check_cl16(st, *y, "y");
     TORCH_CHECK(y->sizes() == x.sizes(), "y shape");
-    yp = reinterpret_cast<const uint16_t*>(y->data_ptr<at::BFloat16>());
+    yp = u16(*y);
   }
-  launch_norm_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr<at::BFloat16>()),
-                  reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>()), yp, mean.data_ptr<float>(),
+  // fused block-end ReLU: g = (dy [+ dy2]) * [yres > 0] -> gout, the norm backward runs on g
+  const uint16_t *d2 = nullptr, *yr = nullptr;
+  uint16_t* go = nullptr;
+  if (yres.has_value() && yres->defined()) {
+    check_cl16(st, *yres, "yres");
+    TORCH_CHECK(gout.has_value() && gout->defined(), "yres needs gout");
+    check_cl16(st, *gout, "gout");
+    TORCH_CHECK(yres->sizes() == x.sizes() && gout->sizes() == x.sizes(), "yres / gout shape");
+    yr = u16(*yres);
+    go = u16m(*gout);
+    if (dy2.has_value() && dy2->defined()) {
+      check_cl16(st, *dy2, "dy2");
+      TORCH_CHECK(dy2->sizes() == x.sizes(), "dy2 shape");
+      d2 = u16(*dy2);
+    }
+  } else {
+    TORCH_CHECK(!(dy2.has_value() && dy2->defined()), "dy2 needs yres");
+  }
+  launch_norm_bwd(u16(dy),
+                  u16(x), yp, mean.data_ptr<float>(),
                   invstd.data_ptr<float>(), (int)N, (int)HW, (int)C, (int)mode, (int)relu, gp, bp,
                   part.data_ptr<float>(), nblk, ppb, coef.data_ptr<float>(), dg, db, dc,
-                  reinterpret_cast<uint16_t*>(dx.data_ptr<at::BFloat16>()), cur_stream());
+                  u16m(dx), d2, yr, go, st == at::kHalf, cur_stream());
 }
 
 void add_relu_(const Tensor& a, const Tensor& b, const Tensor& out) {
-  check_cl_bf16(a, "a");
-  check_cl_bf16(b, "b");
-  check_cl_bf16(out, "out");
+  const at::ScalarType st = op16(a);
+  check_cl16(st, a, "a");
+  check_cl16(st, b, "b");
+  check_cl16(st, out, "out");
   TORCH_CHECK(a.sizes() == b.sizes() && out.sizes() == a.sizes(), "shapes");
   c10::DeviceGuard g(a.device());
-  launch_add_relu(reinterpret_cast<const uint16_t*>(a.data_ptr<at::BFloat16>()),
-                  reinterpret_cast<const uint16_t*>(b.data_ptr<at::BFloat16>()),
-                  reinterpret_cast<uint16_t*>(out.data_ptr<at::BFloat16>()), a.numel(), cur_stream());
+  launch_add_relu(u16(a),
+                  u16(b),
+                  u16m(out), a.numel(), st == at::kHalf, cur_stream());
 }
 
 void relu_mask_(const Tensor& dy, const Tensor& y, const Tensor& g, const c10::optional<Tensor>& dy2) {
-  check_cl_bf16(dy, "dy");
-  check_cl_bf16(y, "y");
-  check_cl_bf16(g, "g");
+  const at::ScalarType st = op16(dy);
+  check_cl16(st, dy, "dy");
+  check_cl16(st, y, "y");
+  check_cl16(st, g, "g");
   TORCH_CHECK(dy.sizes() == y.sizes() && g.sizes() == y.sizes(), "shapes");
   const uint16_t* d2 = nullptr;
   if (dy2.has_value() && dy2->defined()) {
-    check_cl_bf16(*dy2, "dy2");
+    check_cl16(st, *dy2, "dy2");
     TORCH_CHECK(dy2->sizes() == y.sizes(), "dy2 shape");
-    d2 = reinterpret_cast<const uint16_t*>(dy2->data_ptr<at::BFloat16>());
+    d2 = u16(*dy2);
   }
   c10::DeviceGuard gd(y.device());
-  launch_relu_mask(reinterpret_cast<const uint16_t*>(dy.data_ptr<at::BFloat16>()), d2,
-                   reinterpret_cast<const uint16_t*>(y.data_ptr<at::BFloat16>()),
-                   reinterpret_cast<uint16_t*>(g.data_ptr<at::BFloat16>()), y.numel(), cur_stream());
+  launch_relu_mask(u16(dy), d2,
+                   u16(y),
+                   u16m(g), y.numel(), st == at::kHalf, cur_stream());
 }
 
 // ------------------------------------------------------------------ update-block elementwise
@@ -1304,12 +1329,13 @@ void check_pc(const Tensor& t, int64_t P, int64_t C, at::ScalarType st, const ch
 void conv_enc64_(const Tensor& x, const Tensor& wpk, const Tensor& out) {
   TORCH_CHECK(x.dim() == 4 && x.size(3) == 64, "x must be (B,H,W,64)");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2);
-  check_nhwc(x, B, H, W, "conv_enc64 input", at::kBFloat16);
-  check_nhwc(out, B, H, W, "conv_enc64 output", at::kBFloat16);
+  const at::ScalarType st = op16(x);
+  check_nhwc(x, B, H, W, "conv_enc64 input", st);
+  check_nhwc(out, B, H, W, "conv_enc64 output", st);
   TORCH_CHECK(out.size(3) == 64, "out must be (B,H,W,64)");
-  TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == at::kBFloat16 &&
+  TORCH_CHECK(wpk.is_cuda() && wpk.is_contiguous() && wpk.scalar_type() == st &&
                   wpk.dim() == 2 && wpk.size(0) == 64 && wpk.size(1) == 9 * 64,
-              "packed weight must be a contiguous bf16 (64, 576) tensor");
+              "packed weight must be a contiguous (64, 576) tensor of the operand dtype");
   TORCH_CHECK(x.numel() < (int64_t(1) << 31) && H * W * 128 < (int64_t(1) << 31), "conv_enc64: input too large");
   c10::DeviceGuard gd(x.device());
   static const int cus = [] {
@@ -1318,8 +1344,8 @@ void conv_enc64_(const Tensor& x, const Tensor& wpk, const Tensor& out) {
     (void)hipGetDevice(&dev);
     return hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
   }();
-  TORCH_CHECK(launch_conv_enc64(bf16p(x), bf16p(wpk), bf16m(out), (int)B, (int)H, (int)W, cus,
-                                cur_stream()),
+  TORCH_CHECK(launch_conv_enc64(u16(x), u16(wpk), u16m(out), (int)B, (int)H, (int)W, cus,
+                                st == at::kHalf, cur_stream()),
               "conv_enc64 launch failed");
 }
 
@@ -1712,7 +1738,7 @@ TORCH_LIBRARY(raft_amd, m) {
     return conv_import_tuned(r.data(), (int)(r.size() / 13));
   });
   m.def("norm_fwd_(Tensor x, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor? cbias, Tensor(a!)? rmean, Tensor(b!)? rvar, float momentum, float eps, Tensor? res, Tensor(c!) y) -> Tensor[]");
-  m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx) -> ()");
+  m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx, Tensor? dy2=None, Tensor? yres=None, Tensor(e!)? gout=None) -> ()");
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] douts, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");

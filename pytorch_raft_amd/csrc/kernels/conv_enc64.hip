@@ -61,7 +61,7 @@ __device__ __forceinline__ int hoff(int hp) { return (hp / HWD) * AROWB + (hp % 
 // NSET: register sets of halo loads in flight (tiles ahead).  One workgroup per CU moves a tile's
 // 24.6 KB halo per ~3.7 us, so at HBM latency under load the loads in flight, not the MFMAs, set
 // the pace: 3 sets keep ~74 KB per CU outstanding instead of ~49 KB.
-template <bool PIPE, int NSET>
+template <bool PIPE, int NSET, bool F16 = false>
 __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ wpk,
                                                             uint16_t* __restrict__ out, int B,
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
       for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bfr[kk], acc[i], 0, 0, 0);
+          acc[i] = raft_mfma32<F16>(af[kk][i], bfr[kk], acc[i]);
     };
     if constexpr (PIPE) {
       bf16x8_t af[2][4][2], bfr[2][4];
@@ -195,7 +195,7 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
         const int p = wm * 64 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
-        *reinterpret_cast<uint16_t*>(Os + p * OROW + n * 2) = raft_f32_to_bf16(acc[i][rr]);
+        *reinterpret_cast<uint16_t*>(Os + p * OROW + n * 2) = raft_f2h<F16>(acc[i][rr]);
       }
     __syncthreads();  // staged tile complete (the next tile's stores come after its own barrier)
     const int b = t / (tiles_y * tiles_x), r = t - b * tiles_y * tiles_x;
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
 
 // persistent grid: one workgroup per CU (152 KB of LDS each), capped by the tile count
 bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, int B, int H, int W,
-                       int grid_cap, hipStream_t stream) {
+                       int grid_cap, int f16, hipStream_t stream) {
   const int ty = (H + TH - 1) / TH, tx = (W + TW - 1) / TW;
   const int ntiles = B * ty * tx;
   if (ntiles <= 0) return true;
@@ -247,6 +247,11 @@ bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, in
     const char* e = getenv("RAFT_ENC64_V1");
     return e ? atoi(e) : 0;
   }();
+  if (f16) {   // fp16 operands (fp16 autocast): the default schedule
+    hipLaunchKernelGGL((conv_enc64_kernel<true, 3, true>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B,
+                       H, W, ty, tx);
+    return true;
+  }
   if (variant == 1)
     hipLaunchKernelGGL((conv_enc64_kernel<false, 2>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B, H,
                        W, ty, tx);

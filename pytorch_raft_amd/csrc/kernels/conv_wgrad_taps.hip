@@ -293,14 +293,15 @@ __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_t
 // dw[i] += sum_s part[s][i]: 16 float4 columns x 16 split groups per workgroup (split group g
 // sums splits g, g + 16, ... with 4 loads in flight), then a fixed-order LDS combine over the
 // groups: deterministic, and ~splits/16 dependent load rounds instead of splits
-// dw_bf16 != null: store bf16(sum) there instead (no fp32 read-modify-write; the encoders'
+// dw_bf16 != null: store bf16(sum) (fp16 when dw_f16) there instead (no fp32 read-modify-write; the encoders'
 // bf16 weight gradients, packed (co, tap, ci) = the channels_last weight layout)
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part,
                                                                 int splits, int64_t n,
                                                                 float* __restrict__ dw,
                                                                 const float* __restrict__ bpart,
                                                                 int cout, float* __restrict__ db,
-                                                                uint16_t* __restrict__ dw_bf16) {
+                                                                uint16_t* __restrict__ dw_bf16,
+                                                                int dw_f16) {
   __shared__ float4 red[16][17];
   const int col = threadIdx.x & 15, grp = threadIdx.x >> 4;
   const int64_t n4 = n / 4;
@@ -345,7 +346,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __r
       const float4 r = red[g][col];
       t.x += r.x; t.y += r.y; t.z += r.z; t.w += r.w;
     }
-    if (dw_bf16) {
+    if (dw_bf16 && dw_f16) {
+      const uint32_t lo = (uint32_t)raft_f2h<true>(t.x) | ((uint32_t)raft_f2h<true>(t.y) << 16);
+      const uint32_t hi = (uint32_t)raft_f2h<true>(t.z) | ((uint32_t)raft_f2h<true>(t.w) << 16);
+      reinterpret_cast<uint2*>(dw_bf16)[v] = make_uint2(lo, hi);
+    } else if (dw_bf16) {
       const uint32_t lo = (uint32_t)raft_f32_to_bf16(t.x) | ((uint32_t)raft_f32_to_bf16(t.y) << 16);
       const uint32_t hi = (uint32_t)raft_f32_to_bf16(t.z) | ((uint32_t)raft_f32_to_bf16(t.w) << 16);
       reinterpret_cast<uint2*>(dw_bf16)[v] = make_uint2(lo, hi);
@@ -399,7 +404,7 @@ bool launch_conv_wgrad_taps(const ConvWgradArgs& a, const WgradItems& it, const 
   const bool bias = ta.db_part != nullptr && db != nullptr;
   const unsigned blocks = (unsigned)((n / 4 + 15) / 16 + (bias ? (a.cout + 15) / 16 : 0));
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, stream, ta.w_part,
-                     ta.splits, n, a.dw, bias ? ta.db_part : nullptr, a.cout, db, ta.dw_bf16);
+                     ta.splits, n, a.dw, bias ? ta.db_part : nullptr, a.cout, db, ta.dw_bf16, ta.dw_f16);
   return true;
 }
 

@@ -25,19 +25,27 @@ namespace {
 
 constexpr int NT = 256;
 
+// 8 x 16-bit (bf16, or fp16 under fp16 autocast: F16) <-> fp32
+template <bool F16>
 __device__ __forceinline__ void unpack8(uint4 v, float (&f)[8]) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    f[2 * i] = __uint_as_float(w[i] << 16);
-    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    if constexpr (F16) {
+      f[2 * i] = raft_h2f<true>((uint16_t)(w[i] & 0xffffu));
+      f[2 * i + 1] = raft_h2f<true>((uint16_t)(w[i] >> 16));
+    } else {
+      f[2 * i] = __uint_as_float(w[i] << 16);
+      f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
   }
 }
+template <bool F16>
 __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
   uint32_t w[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    w[i] = (uint32_t)raft_f32_to_bf16(f[2 * i]) | ((uint32_t)raft_f32_to_bf16(f[2 * i + 1]) << 16);
+    w[i] = (uint32_t)raft_f2h<F16>(f[2 * i]) | ((uint32_t)raft_f2h<F16>(f[2 * i + 1]) << 16);
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
@@ -55,6 +63,7 @@ __device__ __forceinline__ void norm_affine(int mode, const float* __restrict__ 
 
 // grid.x = blocks per group-range, grid.y = image (instance) or 1 (batch: range = all images)
 // partial layout [group_img][blk][2][C]
+template <bool F16>
 __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restrict__ x, int HW,
                                                         int C, int per_image, int pix_per_blk,
                                                         int total_pix, float* __restrict__ part) {
@@ -69,7 +78,7 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
   const int p0 = blockIdx.x * pix_per_blk, p1 = min(range, p0 + pix_per_blk);
   // shift: the group's first pixel (keeps the one-pass variance well conditioned)
   float K[8];
-  unpack8(*reinterpret_cast<const uint4*>(x + base * C + g * 8), K);
+  unpack8<F16>(*reinterpret_cast<const uint4*>(x + base * C + g * 8), K);
   float s1[8], s2[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
@@ -85,7 +94,7 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         float v[8];
-        unpack8(raw[u], v);
+        unpack8<F16>(raw[u], v);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const float d = v[i] - K[i];
@@ -96,7 +105,7 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
     }
     for (; p < p1; p += lanes) {
       float v[8];
-      unpack8(*reinterpret_cast<const uint4*>(x + (base + p) * C + g * 8), v);
+      unpack8<F16>(*reinterpret_cast<const uint4*>(x + (base + p) * C + g * 8), v);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float d = v[i] - K[i];
@@ -144,6 +153,7 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
 // mode: 0 instance (train or eval: always batch statistics), 1 batch-train, 2 batch-eval, 3 none
 // one thread per (group image, channel); the training-statistics modes run
 // norm_reduce_finalize_kernel instead
+template <bool F16>
 __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint16_t* __restrict__ x,
                                      int HW, int C, int groups_img, int nblk, int cnt, int mode,
                                      const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -158,7 +168,7 @@ __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint1
   float mean = 0.f, invstd = 1.f;
   if (mode == 0 || mode == 1) {
     const double a = part[(int64_t)gi * 2 * C + c], q = part[(int64_t)gi * 2 * C + C + c];
-    const float K = raft_bf16_to_f32(x[(int64_t)(mode == 0 ? gi : 0) * HW * C + c]);
+    const float K = raft_h2f<F16>(x[(int64_t)(mode == 0 ? gi : 0) * HW * C + c]);
     const double m = a / cnt;
     double var = q / cnt - m * m;
     if (var < 0.0) var = 0.0;
@@ -191,7 +201,7 @@ __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint1
 // LANES lanes of one group (grid (groups, ceil(C / COLS))); the lanes stride over the group's
 // per-workgroup partials, a fixed-order LDS combine (deterministic), then lane 0 finalizes its
 // (group, channel).  16 lanes for the long batch-norm partial lists, 4 for per-image ones.
-template <int LANES>
+template <int LANES, bool F16>
 __global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(
     const float* __restrict__ part, int nblk, const uint16_t* __restrict__ x, int HW, int C,
     int cnt, int mode, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -225,7 +235,7 @@ __global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(
   const double m = (double)sa / cnt;
   double var = (double)sq / cnt - m * m;
   if (var < 0.0) var = 0.0;
-  const float K = raft_bf16_to_f32(x[(int64_t)(mode == 0 ? gi : 0) * HW * C + c]);
+  const float K = raft_h2f<F16>(x[(int64_t)(mode == 0 ? gi : 0) * HW * C + c]);
   const float mean = (float)(m + K);
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   if (mode == 1 && rmean != nullptr) {
@@ -247,6 +257,7 @@ __global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(
 // y = act(x*scale + shift) [+ res -> relu];  act: relu when relu != 0.  Block size is a multiple
 // of the channel-group count: each thread keeps one channel group and reloads its scale / shift
 // only when the image changes.
+template <bool F16>
 __global__ __launch_bounds__(NT) void norm_apply_kernel(const uint16_t* __restrict__ x,
                                                         const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int HW,
@@ -270,7 +281,7 @@ __global__ __launch_bounds__(NT) void norm_apply_kernel(const uint16_t* __restri
       }
     }
     float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), f);
+    unpack8<F16>(*reinterpret_cast<const uint4*>(x + v * 8), f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       f[i] = f[i] * sc[i] + sh[i];
@@ -278,29 +289,31 @@ __global__ __launch_bounds__(NT) void norm_apply_kernel(const uint16_t* __restri
     }
     if (res) {
       float r[8];
-      unpack8(*reinterpret_cast<const uint4*>(res + v * 8), r);
+      unpack8<F16>(*reinterpret_cast<const uint4*>(res + v * 8), r);
 #pragma unroll
       for (int i = 0; i < 8; ++i) f[i] = fmaxf(f[i] + r[i], 0.f);
     }
-    *reinterpret_cast<uint4*>(y + v * 8) = pack8(f);
+    *reinterpret_cast<uint4*>(y + v * 8) = pack8<F16>(f);
   }
 }
 
 // out = relu(a + b)
+template <bool F16>
 __global__ __launch_bounds__(NT) void add_relu_kernel(const uint16_t* __restrict__ a,
                                                       const uint16_t* __restrict__ b,
                                                       uint16_t* __restrict__ out, int64_t nvec) {
   for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
     float fa[8], fb[8];
-    unpack8(*reinterpret_cast<const uint4*>(a + v * 8), fa);
-    unpack8(*reinterpret_cast<const uint4*>(b + v * 8), fb);
+    unpack8<F16>(*reinterpret_cast<const uint4*>(a + v * 8), fa);
+    unpack8<F16>(*reinterpret_cast<const uint4*>(b + v * 8), fb);
 #pragma unroll
     for (int i = 0; i < 8; ++i) fa[i] = fmaxf(fa[i] + fb[i], 0.f);
-    *reinterpret_cast<uint4*>(out + v * 8) = pack8(fa);
+    *reinterpret_cast<uint4*>(out + v * 8) = pack8<F16>(fa);
   }
 }
 
 // g = (dy [+ dy2]) * [y > 0]   (the ReLU backward, also the block-end residual ReLU)
+template <bool F16>
 __global__ __launch_bounds__(NT) void relu_mask_kernel(const uint16_t* __restrict__ dy,
                                                        const uint16_t* __restrict__ dy2,
                                                        const uint16_t* __restrict__ y,
@@ -312,14 +325,14 @@ __global__ __launch_bounds__(NT) void relu_mask_kernel(const uint16_t* __restric
     if (dy2 != nullptr) {
       // g = (dy + dy2) * [y > 0]: the residual-branch gradient folded in (no separate add pass)
       float a[8], b[8];
-      unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), a);
-      unpack8(*reinterpret_cast<const uint4*>(dy2 + v * 8), b);
+      unpack8<F16>(*reinterpret_cast<const uint4*>(dy + v * 8), a);
+      unpack8<F16>(*reinterpret_cast<const uint4*>(dy2 + v * 8), b);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const uint32_t yw = (i & 1) ? (mw[i >> 1] >> 16) : (mw[i >> 1] & 0xffffu);
         a[i] = ((yw & 0x8000u) == 0 && (yw & 0x7fffu) != 0) ? a[i] + b[i] : 0.f;
       }
-      const uint4 r = pack8(a);
+      const uint4 r = pack8<F16>(a);
       *reinterpret_cast<uint4*>(g + v * 8) = r;
       continue;
     }
@@ -336,13 +349,40 @@ __global__ __launch_bounds__(NT) void relu_mask_kernel(const uint16_t* __restric
   }
 }
 
+// bf16 > 0 per 16-bit half of a packed word: sign bit clear and magnitude non-zero
+__device__ __forceinline__ uint32_t pos_mask(uint32_t w) {
+  const uint32_t lo = ((w & 0x8000u) == 0 && (w & 0x7fffu) != 0) ? 0xffffu : 0u;
+  const uint32_t hi = ((w & 0x80000000u) == 0 && (w & 0x7fff0000u) != 0) ? 0xffff0000u : 0u;
+  return lo | hi;
+}
+
+// The block-end ReLU of a residual block (out = relu(branch + res)) folded into the norm
+// backward's statistics pass: g = (dy [+ dy2]) * [out > 0] is formed on load, written once (it
+// is also the residual's gradient and the apply pass's input) and summed -- the separate
+// relu_mask pass and its re-read of g are gone.
+template <bool F16>
+__device__ __forceinline__ uint4 block_end_grad(uint4 d, const uint16_t* dy2, int64_t off, uint4 o) {
+  if (dy2 != nullptr) {
+    float a[8], b[8];
+    unpack8<F16>(d, a);
+    unpack8<F16>(*reinterpret_cast<const uint4*>(dy2 + off), b);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] += b[i];
+    d = pack8<F16>(a);
+  }
+  return make_uint4(d.x & pos_mask(o.x), d.y & pos_mask(o.y), d.z & pos_mask(o.z), d.w & pos_mask(o.w));
+}
+
 // backward partial sums per (group image, blk): sum g, sum g*xhat, sum xhat;
-// g = dy * [y > 0] when relu; xhat = (x - mean) * invstd
+// g = dy * [y > 0] when relu; xhat = (x - mean) * invstd.  yres != null: dy is the block output's
+// gradient, g0 = (dy [+ dy2]) * [yres > 0] is formed first and stored to gout (see above)
+template <bool F16>
 __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ beta,
     int mode, int HW, int C, int per_image, int pix_per_blk, int total_pix, int relu,
-    float* __restrict__ part) {
+    float* __restrict__ part, const uint16_t* __restrict__ dy2, const uint16_t* __restrict__ yres,
+    uint16_t* __restrict__ gout) {
   __shared__ float red[3][NT * 8];
   const int cg = C / 8;
   const int lanes = NT / cg;
@@ -365,8 +405,8 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
   for (int i = 0; i < 8; ++i) sg[i] = sgx[i] = sx[i] = 0.f;
   auto accum = [&](const uint4& rd, const uint4& rx) {
     float d[8], xv[8];
-    unpack8(rd, d);
-    unpack8(rx, xv);
+    unpack8<F16>(rd, d);
+    unpack8<F16>(rx, xv);
     if (relu) {
       // the forward ReLU mask, recomputed from x with the forward's own scale / shift
 #pragma unroll
@@ -391,12 +431,25 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
         rd[u] = *reinterpret_cast<const uint4*>(dy + off);
         rx[u] = *reinterpret_cast<const uint4*>(x + off);
       }
+      if (yres != nullptr) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int64_t off = (base + p + u * lanes) * C + g * 8;
+          rd[u] = block_end_grad<F16>(rd[u], dy2, off, *reinterpret_cast<const uint4*>(yres + off));
+          *reinterpret_cast<uint4*>(gout + off) = rd[u];
+        }
+      }
 #pragma unroll
       for (int u = 0; u < 8; ++u) accum(rd[u], rx[u]);
     }
     for (; p < p1; p += lanes) {
       const int64_t off = (base + p) * C + g * 8;
-      accum(*reinterpret_cast<const uint4*>(dy + off), *reinterpret_cast<const uint4*>(x + off));
+      uint4 d = *reinterpret_cast<const uint4*>(dy + off);
+      if (yres != nullptr) {
+        d = block_end_grad<F16>(d, dy2, off, *reinterpret_cast<const uint4*>(yres + off));
+        *reinterpret_cast<uint4*>(gout + off) = d;
+      }
+      accum(d, *reinterpret_cast<const uint4*>(x + off));
     }
   }
 #pragma unroll
@@ -443,7 +496,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
 // group's partials, fixed-order LDS combine, then lane 0 writes the group's coefficients and its
 // contributions (sum g*xhat, sum g, conv-bias term) to pg [groups][3][C]; the apply kernel's
 // first workgroup sums pg over the groups (fixed order) into dgamma / dbeta / dcbias.
-template <int LANES>
+template <int LANES, bool F16>
 __global__ __launch_bounds__(256) void norm_bwd_reduce_finalize_kernel(
     const float* __restrict__ part, int nblk, int C, int cnt, int mode,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean,
@@ -508,6 +561,7 @@ __global__ __launch_bounds__(256) void norm_bwd_reduce_finalize_kernel(
 // dx = A*g + B'*x + C' with g = dy masked by the forward ReLU (read from y when given, else
 // recomputed from x with the forward's scale / shift); per-element coefficient reads (L1-resident
 // table) measured faster than per-thread register caching across the grid-stride loop
+template <bool F16>
 __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint16_t* __restrict__ y,
     const float* __restrict__ coef, int HW, int C, int per_image, int64_t nvec, int relu,
@@ -534,8 +588,8 @@ __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     const int g = (int)(v - pix * cg);
     const int gi = per_image ? (int)(pix / HW) : 0;
     float d[8], xv[8];
-    unpack8(*reinterpret_cast<const uint4*>(dy + v * 8), d);
-    unpack8(*reinterpret_cast<const uint4*>(x + v * 8), xv);
+    unpack8<F16>(*reinterpret_cast<const uint4*>(dy + v * 8), d);
+    unpack8<F16>(*reinterpret_cast<const uint4*>(x + v * 8), xv);
     const float* co = coef + (int64_t)gi * 5 * C + g * 8;
     auto ld8 = [&](int f, float (&r)[8]) {
       const float4 a = *reinterpret_cast<const float4*>(co + f * C);
@@ -544,7 +598,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     };
     if (relu && y != nullptr) {
       float yv[8];
-      unpack8(*reinterpret_cast<const uint4*>(y + v * 8), yv);
+      unpack8<F16>(*reinterpret_cast<const uint4*>(y + v * 8), yv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
     } else if (relu) {
@@ -560,7 +614,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     ld8(2, Cp);
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + Bp[i] * xv[i] + Cp[i];
-    *reinterpret_cast<uint4*>(dx + v * 8) = pack8(o);
+    *reinterpret_cast<uint4*>(dx + v * 8) = pack8<F16>(o);
   }
 }
 
@@ -583,85 +637,115 @@ int encoder_norm_blocks(int64_t range, int C, int* pix_per_blk) {
 }
 
 void launch_norm_stats(const uint16_t* x, int N, int HW, int C, int per_image, float* part,
-                       int nblk, int pix_per_blk, hipStream_t stream) {
+                       int nblk, int pix_per_blk, int f16, hipStream_t stream) {
   dim3 grid(nblk, per_image ? N : 1);
-  hipLaunchKernelGGL(norm_stats_kernel, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
+  if (f16) hipLaunchKernelGGL(norm_stats_kernel<true>, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
+                     N * HW, part);
+  else hipLaunchKernelGGL(norm_stats_kernel<false>, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
                      N * HW, part);
 }
 
 void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, int C, int mode,
                           int nblk, const float* gamma, const float* beta, const float* cbias,
                           float* rmean, float* rvar, float momentum, float eps, float* mean,
-                          float* invstd, float* scale, float* shift, hipStream_t stream) {
+                          float* invstd, float* scale, float* shift, int f16, hipStream_t stream) {
   const int groups = mode == 0 ? N : 1;
   const int cnt = mode == 0 ? HW : N * HW;
   const int tot = groups * C;
   if (mode <= 1) {
     // training statistics: partial reduce + finalize in one launch
-    if (nblk > 64)
-      hipLaunchKernelGGL(norm_reduce_finalize_kernel<16>, dim3(groups, (C + 15) / 16), dim3(256), 0,
+    if (nblk > 64) {
+      if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, true>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                          stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
                          momentum, eps, mean, invstd, scale, shift, N);
-    else
-      hipLaunchKernelGGL(norm_reduce_finalize_kernel<4>, dim3(groups, (C + 63) / 64), dim3(256), 0,
+      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, false>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                          stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
                          momentum, eps, mean, invstd, scale, shift, N);
+    } else {
+      if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, true>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
+      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, false>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
+    }
     return;
   }
   float* sums = nullptr;
-  hipLaunchKernelGGL(norm_finalize_kernel, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
+  if (f16) hipLaunchKernelGGL(norm_finalize_kernel<true>, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
+                     C, groups, nblk, cnt, mode, gamma, beta, cbias, rmean, rvar, momentum, eps, mean,
+                     invstd, scale, shift, N);
+  else hipLaunchKernelGGL(norm_finalize_kernel<false>, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
                      C, groups, nblk, cnt, mode, gamma, beta, cbias, rmean, rvar, momentum, eps, mean,
                      invstd, scale, shift, N);
 }
 
 void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift, int N, int HW,
-                       int C, int relu, const uint16_t* res, uint16_t* y, hipStream_t stream) {
+                       int C, int relu, const uint16_t* res, uint16_t* y, int f16, hipStream_t stream) {
   const int64_t nvec = (int64_t)N * HW * C / 8;
   const int bt = (NT / (C / 8)) * (C / 8);  // multiple of the channel-group count
-  hipLaunchKernelGGL(norm_apply_kernel, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
+  if (f16) hipLaunchKernelGGL(norm_apply_kernel<true>, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
+                     C, nvec, relu, res, y);
+  else hipLaunchKernelGGL(norm_apply_kernel<false>, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
                      C, nvec, relu, res, y);
 }
 
 void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_t n,
-                     hipStream_t stream) {
+                     int f16, hipStream_t stream) {
   const int64_t nvec = n / 8;
-  hipLaunchKernelGGL(add_relu_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, a, b, out, nvec);
+  if (f16) hipLaunchKernelGGL(add_relu_kernel<true>, dim3(grid_for(nvec)), dim3(NT), 0, stream, a, b, out, nvec);
+  else hipLaunchKernelGGL(add_relu_kernel<false>, dim3(grid_for(nvec)), dim3(NT), 0, stream, a, b, out, nvec);
 }
 
 void launch_relu_mask(const uint16_t* dy, const uint16_t* dy2, const uint16_t* y, uint16_t* g, int64_t n,
-                      hipStream_t stream) {
+                      int f16, hipStream_t stream) {
   const int64_t nvec = n / 8;
-  hipLaunchKernelGGL(relu_mask_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, dy2, y, g, nvec);
+  if (f16) hipLaunchKernelGGL(relu_mask_kernel<true>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, dy2, y, g, nvec);
+  else hipLaunchKernelGGL(relu_mask_kernel<false>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, dy2, y, g, nvec);
 }
 
 void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
                      const float* invstd,
                      int N, int HW, int C, int mode, int relu, const float* gamma,
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
-                     float* dgamma, float* dbeta, float* dcbias, uint16_t* dx, hipStream_t stream) {
+                     float* dgamma, float* dbeta, float* dcbias, uint16_t* dx,
+                     const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int f16, hipStream_t stream) {
   const int per_image = mode == 0 ? 1 : 0;
   const int groups = per_image ? N : 1;
   const int cnt = per_image ? HW : N * HW;
   if (mode == 0 || mode == 1) {
     dim3 grid(nblk, groups);
-    hipLaunchKernelGGL(norm_bwd_stats_kernel, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
-                       beta, mode, HW, C, per_image, pix_per_blk, N * HW, relu, part);
+    if (f16) hipLaunchKernelGGL(norm_bwd_stats_kernel<true>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, per_image, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
+    else hipLaunchKernelGGL(norm_bwd_stats_kernel<false>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, per_image, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
   } else {
     // eval / none: only sum(g) and sum(g*xhat) are needed for the parameter grads
     dim3 grid(nblk, 1);
-    hipLaunchKernelGGL(norm_bwd_stats_kernel, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
-                       beta, mode, HW, C, 0, pix_per_blk, N * HW, relu, part);
+    if (f16) hipLaunchKernelGGL(norm_bwd_stats_kernel<true>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, 0, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
+    else hipLaunchKernelGGL(norm_bwd_stats_kernel<false>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, 0, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
   }
+  // the block-end ReLU ran in the statistics pass: the apply pass reads its result
+  if (yres != nullptr) dy = gout;
   // per-group sums + coefficients in one launch; pg (the groups' parameter-gradient terms) sits
   // after the partials in `part`
   float* pg = part + (int64_t)groups * nblk * 3 * C;
-  if (nblk > 64)
-    hipLaunchKernelGGL(norm_bwd_reduce_finalize_kernel<16>, dim3(groups, (C + 15) / 16), dim3(256), 0,
+  if (nblk > 64) {
+    if (f16) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, true>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                        stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
-  else
-    hipLaunchKernelGGL(norm_bwd_reduce_finalize_kernel<4>, dim3(groups, (C + 63) / 64), dim3(256), 0,
+    else hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, false>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                        stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
+  } else {
+    if (f16) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<4, true>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
+    else hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<4, false>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
+  }
   const int64_t nvec = (int64_t)N * HW * C / 8;
-  hipLaunchKernelGGL(norm_bwd_apply_kernel, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
+  if (f16) hipLaunchKernelGGL(norm_bwd_apply_kernel<true>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
+                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias);
+  else hipLaunchKernelGGL(norm_bwd_apply_kernel<false>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
                      HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias);
 }

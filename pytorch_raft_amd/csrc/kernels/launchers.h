@@ -236,6 +236,7 @@ struct WgradTapArgs {
   float* w_part;                         // [splits][cout][kpad]
   float* db_part;                        // [splits][cout] or null
   uint16_t* dw_bf16;                     // non-null: dW stored as bf16 here (no accumulate)
+  int dw_f16;                            // ... as fp16 instead (fp16 autocast)
 };
 bool launch_conv_wgrad_taps(const ConvWgradArgs& a, const WgradItems& it, const WgradTapArgs& ta,
                             float* db, hipStream_t stream);
@@ -249,7 +250,7 @@ void launch_col_sum(const uint16_t* g, int stride, int cout, int P, float* db, h
 void launch_phase_marker(hipStream_t stream);
 // stride-1 3x3 64 -> 64 NHWC bf16 conv (conv_enc64.hip); wpk = (64, 9*64) packed [n][tap*64 + c]
 bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, int B, int H, int W,
-                       int grid_cap, hipStream_t stream);
+                       int grid_cap, int f16, hipStream_t stream);
 // fp32 (B,C,H,W) any strides -> (B,H,W,2cp) bf16 [hi | lo], zero padded (ops/conv_fp32.py)
 void launch_split_hilo(const float* x, int64_t sb, int64_t sc, int64_t sh, int64_t sw, int B, int C,
                        int H, int W, int cp, uint16_t* out, hipStream_t stream);
@@ -337,28 +338,32 @@ bool launch_convex_up_nhwc_bwd(const float* flow, const void* mask, int mask_is_
                                const float* dout, void* dmask, float* wbuf, float* dflow, int B,
                                int H, int W, hipStream_t stream);
 
-// ---- encoder norm + activation, NHWC bf16 (encoder_norm.hip)
+// ---- encoder norm + activation, NHWC bf16 / fp16 (f16) (encoder_norm.hip)
 // mode: 0 instance, 1 batch (training statistics), 2 batch (running statistics), 3 none
 int encoder_norm_blocks(int64_t range, int C, int* pix_per_blk);
 void launch_norm_stats(const uint16_t* x, int N, int HW, int C, int per_image, float* part,
-                       int nblk, int pix_per_blk, hipStream_t stream);
+                       int nblk, int pix_per_blk, int f16, hipStream_t stream);
 void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, int C, int mode,
                           int nblk, const float* gamma, const float* beta, const float* cbias,
                           float* rmean, float* rvar, float momentum, float eps, float* mean,
-                          float* invstd, float* scale, float* shift, hipStream_t stream);
+                          float* invstd, float* scale, float* shift, int f16, hipStream_t stream);
 void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift, int N, int HW,
-                       int C, int relu, const uint16_t* res, uint16_t* y, hipStream_t stream);
+                       int C, int relu, const uint16_t* res, uint16_t* y, int f16, hipStream_t stream);
 void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_t n,
-                     hipStream_t stream);
+                     int f16, hipStream_t stream);
 // g = (dy [+ dy2]) * [y > 0]; dy2 nullable
 void launch_relu_mask(const uint16_t* dy, const uint16_t* dy2, const uint16_t* y, uint16_t* g, int64_t n,
-                      hipStream_t stream);
+                      int f16, hipStream_t stream);
 // y (nullable): the forward output; when given, the ReLU mask is read from it, else recomputed
+// yres (nullable): dy is the gradient of a residual block's output relu(branch + res) = yres;
+// g = (dy [+ dy2]) * [yres > 0] is formed in the statistics pass and stored to gout (the
+// residual's gradient), and the norm backward runs on it (the block-end ReLU mask fused)
 void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
                      const float* invstd,
                      int N, int HW, int C, int mode, int relu, const float* gamma,
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
-                     float* dgamma, float* dbeta, float* dcbias, uint16_t* dx, hipStream_t stream);
+                     float* dgamma, float* dbeta, float* dcbias, uint16_t* dx,
+                     const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int f16, hipStream_t stream);
 
 // ---- multi-tensor AdamW + global-norm clip + GradScaler unscale / overflow skip (adamw.hip)
 struct AdamTensor {

@@ -221,7 +221,12 @@ class GraphedTrainStep:
         pdist.barrier(self.st.device)
         pdist.share_conv_tuning(self.st.device)
         if me != 0:
-            self._prewarm(example)
+            try:
+                self._prewarm(example)
+            finally:
+                # back to the environment's default: a geometry first seen later (another
+                # resolution, an eval pass) is tuned, as on rank 0
+                ops.conv_set_autotune(-1)
         self.autotune_runs = int(ops.conv_autotune_runs())
         pdist.barrier(self.st.device)
 

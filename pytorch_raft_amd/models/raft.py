@@ -12,7 +12,7 @@ MI355X-specific extensions (all optional ``args`` attributes, defaults chosen fo
 
 * ``corr_impl``   'auto' (HIP kernels on GPU, torch on CPU) | 'hip' | 'torch'
 * ``amp_dtype``   autocast dtype for ``mixed_precision`` -- 'bfloat16' (default; MI355X MFMA native)
-                  or 'float16' (reference behaviour on CUDA)
+                  or 'float16' (reference behaviour on CUDA; same fused HIP kernels, fp16 MFMA)
 * ``channels_last`` run the encoders in NHWC (MIOpen's NHWC implicit-GEMM solvers)
 * ``corr_mode``   'auto' (default) | 'allpairs' | 'onthefly'.  ``alternate_corr=True`` (the
                   reference flag, `core/raft.py:105-108`) always selects the on-the-fly block.
@@ -20,9 +20,9 @@ MI355X-specific extensions (all optional ``args`` attributes, defaults chosen fo
                   used while it fits in ``RAFT_CORR_BUDGET_GB`` (default: a quarter of the GPU's
                   HBM, 72 GB on MI355X), the O(HW) on-the-fly correlation beyond that.  Both give
                   the same values; all-pairs is the faster of the two at every batch that fits
-                  (profiles/r2/sweep: 395 vs 358 training pairs/s at batch 12, 325 vs 317
-                  inference pairs/s at Sintel batch 64), on-the-fly is what makes batch-1024
-                  Sintel inference or 4K frames fit.
+                  (profiles/r2/sweep measured the gap when it was last swept: training and
+                  Sintel inference both a few percent faster on all-pairs), on-the-fly is what
+                  makes batch-1024 Sintel inference or 4K frames fit.
 
 In test mode the convex upsampling runs only after the last iteration (the reference computes and
 discards it every iteration, `core/raft.py:133-142`); outputs are identical.

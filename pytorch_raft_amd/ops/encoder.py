@@ -13,7 +13,10 @@ Reference: `core/extractor.py:6-56` (ResidualBlock), `:60-116` (BottleneckBlock)
   per-conv bias-gradient reductions of the eager graph;
 * the residual add + ReLU is one node.
 
-Used automatically by ``_Encoder.forward`` on the GPU under bf16 autocast (``fast_path_ok``).
+Used automatically by ``_Encoder.forward`` on the GPU under bf16 or fp16 autocast
+(``fast_path_ok``; the reference's ``--mixed_precision`` is fp16 autocast, `core/raft.py:99`):
+activations, weights and weight gradients are in the autocast dtype, statistics and accumulation
+in fp32.
 """
 import os
 
@@ -24,6 +27,7 @@ import torch.nn.functional as F
 from . import _ext
 
 MODE_INSTANCE, MODE_BATCH_TRAIN, MODE_BATCH_EVAL, MODE_NONE = range(4)
+_DTYPES = (torch.bfloat16, torch.float16)
 
 
 def _norm_mode(norm):
@@ -41,7 +45,7 @@ def _norm_mode(norm):
 
 
 class _NormAct(torch.autograd.Function):
-    """y = act(norm(x + conv_bias)) on channels_last bf16; x is the bias-free conv output."""
+    """y = act(norm(x + conv_bias)) on channels_last bf16 / fp16; x is the bias-free conv output."""
 
     @staticmethod
     def forward(ctx, x, gamma, beta, cbias, norm, mode, relu):
@@ -70,7 +74,7 @@ class _NormAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, mean, invstd, gamma, beta = ctx.saved_tensors
-        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
         c = x.shape[1]
         dev = x.device
         # written (not accumulated) by the finalize kernel: no zero fill
@@ -116,20 +120,23 @@ class _NormActAddRelu(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         x, out, mean, invstd, gamma, beta = ctx.saved_tensors
-        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dout = dout.to(out.dtype).contiguous(memory_format=torch.channels_last)
         g = torch.empty_like(out, memory_format=torch.channels_last)
         # an identity-residual consumer of this block's output left its gradient in the stash
-        # instead of handing it to autograd: fold it into the ReLU-mask pass (no bf16 add kernel).
-        # It always runs first -- this node waits for every consumer of its output.
+        # instead of handing it to autograd: it is added where the block-end ReLU mask is applied
+        # (no bf16 add kernel).  It always runs first -- this node waits for every consumer of
+        # its output.
         stash = ctx.holder.pop('g', None)
-        _ext.ops().relu_mask_(dout, out, g, stash)   # block-end ReLU; g is also the residual's grad
         c = x.shape[1]
         dev = x.device
         dg = torch.empty(c, device=dev) if ctx.has[0] else None
         db = torch.empty(c, device=dev) if ctx.has[1] else None
         dc = torch.empty(c, device=dev) if ctx.has[2] else None
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        _ext.ops().norm_bwd_(g, x, None, mean, invstd, ctx.mode, 1, gamma, beta, dg, db, dc, dx)
+        # block-end ReLU fused into the norm backward's statistics pass: g = (dout [+ stash]) *
+        # [out > 0] is formed there and stored once (it is also the residual's gradient)
+        _ext.ops().norm_bwd_(dout, x, None, mean, invstd, ctx.mode, 1, gamma, beta, dg, db, dc, dx,
+                             stash, out, g)
         gres = g
         if ctx.res_holder is not None:
             ctx.res_holder['g'] = g
@@ -150,14 +157,15 @@ class _AddRelu(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         (out,) = ctx.saved_tensors
-        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dout = dout.to(out.dtype).contiguous(memory_format=torch.channels_last)
         g = torch.empty_like(out, memory_format=torch.channels_last)
         _ext.ops().relu_mask_(dout, out, g)
         return g, g
 
 
 class _CastWeightsCL(torch.autograd.Function):
-    """All conv weights of an encoder -> bf16 channels_last views of ONE buffer, and back.
+    """All conv weights of an encoder -> 16-bit (bf16 / fp16: the autocast dtype) channels_last
+    views of ONE buffer, and back.
 
     Per conv, ``weight.to(bf16).contiguous(channels_last)`` and the backward cast of its bf16
     gradient are 2-3 tiny kernels each (~100 launches per step for both encoders).  Here the
@@ -170,10 +178,10 @@ class _CastWeightsCL(torch.autograd.Function):
     kernels.  Those extra outputs carry no gradient."""
 
     @staticmethod
-    def forward(ctx, maps, *ws):
+    def forward(ctx, maps, dt, *ws):
         perm, inv, shapes, extra = maps
         flat = torch.cat([w.reshape(-1) for w in ws] + [ws[0].new_zeros(1)])
-        packed = flat.index_select(0, perm).to(torch.bfloat16)
+        packed = flat.index_select(0, perm).to(dt)
         outs, off = [], 0
         for (co, ci, kh, kw) in shapes:
             n = co * ci * kh * kw
@@ -184,6 +192,7 @@ class _CastWeightsCL(torch.autograd.Function):
             ext.append(packed[off:off + rows * cols].view(rows, cols))
             off += rows * cols
         ctx.maps = maps
+        ctx.dt = dt
         ctx.mark_non_differentiable(*ext)
         return tuple(outs) + tuple(ext)
 
@@ -193,7 +202,7 @@ class _CastWeightsCL(torch.autograd.Function):
         parts = []
         for g, (co, ci, kh, kw) in zip(gs[:len(shapes)], shapes):
             if g is None:
-                g = torch.zeros(co, ci, kh, kw, device=perm.device, dtype=torch.bfloat16)
+                g = torch.zeros(co, ci, kh, kw, device=perm.device, dtype=ctx.dt)
             parts.append(g.permute(0, 2, 3, 1).reshape(-1))
         flat = torch.cat(parts).float().index_select(0, inv)
         grads, off = [], 0
@@ -201,7 +210,7 @@ class _CastWeightsCL(torch.autograd.Function):
             n = co * ci * kh * kw
             grads.append(flat[off:off + n].view(co, ci, kh, kw))
             off += n
-        return (None, *grads)
+        return (None, None, *grads)
 
 
 _MAPS = {}
@@ -259,14 +268,14 @@ def _cast_maps(shapes, device, native=()):
     return _MAPS[key]
 
 
-def cast_conv_weights(convs):
-    """({conv: bf16 channels_last weight}, {conv: packed bf16 adjoint weight}, {conv: packed
-    bf16 forward weight with 64-aligned K slots, when Cin % 64 != 0}) for a list of nn.Conv2d,
-    one batched cast node."""
+def cast_conv_weights(convs, dt=torch.bfloat16):
+    """({conv: 16-bit channels_last weight}, {conv: packed adjoint weight}, {conv: packed forward
+    weight with 64-aligned K slots, when Cin % 64 != 0}) for a list of nn.Conv2d, one batched cast
+    node; ``dt`` = bf16 or fp16."""
     ws = [c.weight for c in convs]
     native = tuple(j for j, c in enumerate(convs) if _native_geom(c))
     maps = _cast_maps([tuple(w.shape) for w in ws], ws[0].device, native)
-    outs = _CastWeightsCL.apply(maps, *ws)
+    outs = _CastWeightsCL.apply(maps, dt, *ws)
     ext = outs[len(convs):]
     adj = {convs[j]: ext[k] for k, j in enumerate(native)}
     fwd, k = {}, len(native)
@@ -279,7 +288,7 @@ def cast_conv_weights(convs):
 
 class _Head1x1(torch.autograd.Function):
     """The encoders' final 1x1 conv (`core/extractor.py:185`, 128 -> 256 with bias) on the
-    MFMA implicit-GEMM kernels of the update block (NHWC bf16, fp32 accumulation): forward with
+    MFMA implicit-GEMM kernels of the update block (NHWC bf16 / fp16, fp32 accumulation): forward with
     the bias epilogue, input gradient by the same kernel on the transposed weight, weight / bias
     gradient by the split-K wgrad kernel.  Replaces MIOpen's 1x1 solvers, one of which produced
     inf weight gradients under hipGraph replay (profiles/r2/graph_cmp_cnet_conv2.log)."""
@@ -293,8 +302,8 @@ class _Head1x1(torch.autograd.Function):
         if not xn.is_contiguous():
             xn = xn.contiguous()
         w2 = weight.reshape(cout, cin)
-        wpk = C.pack_weight(weight, [cin], [cin])       # (Npad, cin) bf16
-        out = torch.empty(B, H, W, cout, device=x.device, dtype=torch.bfloat16)
+        wpk = C.pack_weight(weight, [cin], [cin], dtype=x.dtype)   # (Npad, cin) 16-bit
+        out = torch.empty(B, H, W, cout, device=x.device, dtype=x.dtype)
         C.conv_fwd([(xn, 0, cin)], wpk, bias.float().contiguous(), (1, 1), (0, 0), cout,
                    C.EPI_BF16, [out], [0])
         ctx.save_for_backward(xn, w2)
@@ -306,14 +315,19 @@ class _Head1x1(torch.autograd.Function):
         xn, w2 = ctx.saved_tensors
         B, H, W, cin = xn.shape
         cout = w2.shape[0]
-        g = dy.permute(0, 2, 3, 1).to(torch.bfloat16).contiguous()   # (B, H, W, cout)
-        dx = torch.empty(B, H, W, cin, device=xn.device, dtype=torch.bfloat16)
-        wd = C.pack_weight(w2.t().contiguous().view(cin, cout, 1, 1), [cout], [cout])
+        dt = xn.dtype
+        g = dy.permute(0, 2, 3, 1).to(dt).contiguous()   # (B, H, W, cout)
+        dx = torch.empty(B, H, W, cin, device=xn.device, dtype=dt)
+        wd = C.pack_weight(w2.t().contiguous().view(cin, cout, 1, 1), [cout], [cout], dtype=dt)
         _ext.ops().conv_dgrad_([g], [0], [cout], wd, 1, 1, 0, 0, 0, 1.0, [dx], [0], [cin], [cin],
                                [0], [dx], [-1], [], [])
         dw = torch.zeros(cout, cin, device=xn.device)
         db = torch.zeros(cout, device=xn.device)
-        C.conv_wgrad(g, 0, [(xn, 0, cin)], (1, 1), (0, 0), cout, dw, db)
+        if dt == torch.float16:
+            # the tile kernel (conv_wgrad.hip) is bf16-only; the tap-fused one takes fp16
+            C.conv_wgrad_taps([(g, [xn])], 0, [0], [cin], (1, 1), (0, 0), cout, dw, db)
+        else:
+            C.conv_wgrad(g, 0, [(xn, 0, cin)], (1, 1), (0, 0), cout, dw, db)
         return dx.permute(0, 3, 1, 2), dw.view(cout, cin, 1, 1), db
 
 
@@ -342,15 +356,15 @@ class _Conv3x3WgradNative(torch.autograd.Function):
     def backward(ctx, dy):
         from . import conv as C
         x, w = ctx.saved_tensors
-        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(
                 dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False])[0]
         if ctx.needs_input_grad[1]:
             co, ci = w.shape[:2]
-            # bf16 stored straight by the split reduce (no zero fill, no cast kernel)
-            dwp = torch.empty(co, 9 * ci, device=x.device, dtype=torch.bfloat16)
+            # 16-bit stored straight by the split reduce (no zero fill, no cast kernel)
+            dwp = torch.empty(co, 9 * ci, device=x.device, dtype=x.dtype)
             C.conv_wgrad_taps([(dy.permute(0, 2, 3, 1), [x.permute(0, 2, 3, 1)])], 0, [0], [ci],
                               (3, 3), (1, 1), co, dwp, None)
             # packed (co, kh, kw, ci) -> (co, ci, kh, kw) with channels_last strides (= w's)
@@ -365,12 +379,12 @@ _ENC64 = os.environ.get('RAFT_ENC64', '1') != '0'
 
 
 def _conv3x3_nhwc(xn, wpk, ci, co):
-    """NHWC bf16 stride-1 3x3 conv with a packed [co][tap * ci' + c] weight (ci' = ci rounded up
+    """NHWC 16-bit stride-1 3x3 conv with a packed [co][tap * ci' + c] weight (ci' = ci rounded up
     to 64; the K slot past ci reads zeros): 64 -> 64 channels on the persistent 2-D halo-tile
     kernel (conv_enc64.hip), anything else on the implicit GEMM."""
     from . import conv as C
     B, H, W, _ = xn.shape
-    out = torch.empty(B, H, W, co, device=xn.device, dtype=torch.bfloat16)
+    out = torch.empty(B, H, W, co, device=xn.device, dtype=xn.dtype)
     if _ENC64 and ci == 64 and co == 64:
         _ext.ops().conv_enc64_(xn, wpk, out)
     else:
@@ -410,7 +424,7 @@ class _Conv3x3Native(torch.autograd.Function):
         from . import conv as C
         x, w, wd = ctx.saved_tensors
         co, ci = w.shape[:2]
-        dy = dy.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
         gn = dy.permute(0, 2, 3, 1)
         dx = dw = None
         if ctx.needs_input_grad[0]:
@@ -418,16 +432,17 @@ class _Conv3x3Native(torch.autograd.Function):
             if wd is None:
                 # adjoint weight W'[c][tap'][o] = W[o][c][flip(tap')], in the kernels' packed
                 # layout (normally laid out by the batched weight cast, _CastWeightsCL)
-                wd = C.pack_weight(w.flip(2, 3).transpose(0, 1), [co], [_kslot(co)], npad_mult=1)
+                wd = C.pack_weight(w.flip(2, 3).transpose(0, 1), [co], [_kslot(co)], npad_mult=1,
+                                   dtype=x.dtype)
             if _ENC64 and ci == 64 and co == 64:
                 dx = _conv3x3_nhwc(gn, wd, co, ci).permute(0, 3, 1, 2)
             else:
-                dxn = torch.empty(B, H, W, ci, device=x.device, dtype=torch.bfloat16)
+                dxn = torch.empty(B, H, W, ci, device=x.device, dtype=x.dtype)
                 _ext.ops().conv_dgrad_([gn], [0], [_kslot(co)], wd, 3, 3, 1, 1, 0, 1.0, [dxn], [0],
                                        [ci], [ci], [0], [dxn], [-1], [], [])
                 dx = dxn.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
-            dwp = torch.empty(co, 9 * ci, device=x.device, dtype=torch.bfloat16)
+            dwp = torch.empty(co, 9 * ci, device=x.device, dtype=x.dtype)
             C.conv_wgrad_taps([(gn, [x.permute(0, 2, 3, 1)])], 0, [0], [ci], (3, 3), (1, 1), co,
                               dwp, None)
             dw = dwp.view(co, 3, 3, ci).permute(0, 3, 1, 2)
@@ -447,7 +462,7 @@ def _wgrad_native_ok(x, conv):
     return (_WGRAD_NATIVE and conv.kernel_size == (3, 3) and conv.stride == (1, 1)
             and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
             and conv.in_channels % 32 == 0 and conv.out_channels % 8 == 0
-            and conv.in_channels <= 1024 and x.is_cuda and x.dtype == torch.bfloat16
+            and conv.in_channels <= 1024 and x.is_cuda and x.dtype in _DTYPES
             and x.is_contiguous(memory_format=torch.channels_last)
             and x.numel() * 2 < 2 ** 31 and x.shape[0] * x.shape[2] * x.shape[3] * conv.out_channels * 2 < 2 ** 31)
 
@@ -477,7 +492,7 @@ def _conv(ps, x, conv, with_bias=False):
 def _conv_one(ps, x, conv, with_bias=False):
     w = ps.weights.get(conv)
     if w is None:
-        w = conv.weight.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        w = conv.weight.to(x.dtype).contiguous(memory_format=torch.channels_last)
     if not with_bias and _conv_native_ok(x, conv) and w.is_contiguous(memory_format=torch.channels_last):
         if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
             return _Conv3x3Native.apply(x, w, ps.adjoint.get(conv), ps.fwdpack.get(conv))
@@ -485,7 +500,7 @@ def _conv_one(ps, x, conv, with_bias=False):
     if not with_bias and _wgrad_native_ok(x, conv) and torch.is_grad_enabled() and \
             (x.requires_grad or w.requires_grad):
         return _Conv3x3WgradNative.apply(x, w)
-    b = conv.bias.to(torch.bfloat16) if (with_bias and conv.bias is not None) else None
+    b = conv.bias.to(x.dtype) if (with_bias and conv.bias is not None) else None
     return F.conv2d(x, w, b, conv.stride, conv.padding, conv.dilation, conv.groups)
 
 
@@ -541,7 +556,7 @@ def bottleneck_block(ps, blk, x):
 
 
 def fast_path_ok(enc, x):
-    """GPU + native library + bf16 autocast + supported norms; otherwise the eager path runs.
+    """GPU + native library + bf16 / fp16 autocast + supported norms; otherwise the eager path runs.
     ``enc.allow_native = False`` (set by RAFT for ``corr_impl='torch'``, the stock-ops baseline)
     forces the eager MIOpen / ATen encoder."""
     if not getattr(enc, 'allow_native', True):
@@ -549,7 +564,7 @@ def fast_path_ok(enc, x):
     if not (isinstance(x, torch.Tensor) and x.is_cuda and _ext.device_ok(x)):
         return False
     if not (torch.is_autocast_enabled('cuda') and
-            torch.get_autocast_dtype('cuda') == torch.bfloat16):
+            torch.get_autocast_dtype('cuda') in _DTYPES):
         return False
     if enc.training and enc.dropout is not None:
         return False
@@ -564,19 +579,21 @@ def fast_path_ok(enc, x):
 
 
 class _Pass:
-    """State of ONE encoder forward: the batched bf16 weight casts and the residual-gradient
+    """State of ONE encoder forward: the batched 16-bit weight casts and the residual-gradient
     stashes.  Passed down explicitly (no module globals), so encoder forwards running
     concurrently on two streams or threads, or re-entrantly, cannot see each other's state."""
 
     def __init__(self, weights, adjoint, fwdpack):
-        self.weights = weights   # conv -> bf16 channels_last weight
-        self.adjoint = adjoint   # conv -> packed bf16 adjoint weight (native 3x3 convs)
+        self.weights = weights   # conv -> 16-bit channels_last weight
+        self.adjoint = adjoint   # conv -> packed adjoint weight (native 3x3 convs)
         self.fwdpack = fwdpack   # conv -> packed forward weight, 64-aligned K slots (Cin 96)
         self.holders = {}        # id(block output) -> (output, its gradient stash)
 
 
 def encoder_forward(enc, x):
-    """`core/extractor.py:168-192` (both encoders): returns channels_last bf16 features."""
+    """`core/extractor.py:168-192` (both encoders): returns channels_last features in the
+    autocast dtype (bf16 / fp16)."""
+    dt = torch.get_autocast_dtype('cuda')
     with torch.autocast('cuda', enabled=False):
         convs = [m for m in enc.modules() if isinstance(m, nn.Conv2d)]
         if _head_ok(x, enc.conv2):
@@ -587,11 +604,11 @@ def encoder_forward(enc, x):
         if counters:
             with torch.no_grad():
                 torch._foreach_add_(counters, 1)
-        return _encoder_body(_Pass(*cast_conv_weights(convs)), enc, x)
+        return _encoder_body(_Pass(*cast_conv_weights(convs, dt)), enc, x, dt)
 
 
-def _encoder_body(ps, enc, x):
-    x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+def _encoder_body(ps, enc, x, dt=torch.bfloat16):
+    x = x.to(dt).contiguous(memory_format=torch.channels_last)
     x = conv_norm_act(ps, x, enc.conv1, enc.norm1)
     block_fn = residual_block if enc.block.__name__ == 'ResidualBlock' else bottleneck_block
     for layer in (enc.layer1, enc.layer2, enc.layer3):

@@ -14,10 +14,17 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
 
 
-@pytest.mark.parametrize('cls,norm,train', [
-    (BasicEncoder, 'instance', True), (BasicEncoder, 'batch', True), (BasicEncoder, 'batch', False),
-    (SmallEncoder, 'instance', True), (SmallEncoder, 'none', True)])
-def test_fast_encoder_matches_eager(ext_ops, cls, norm, train):
+H16 = torch.float16
+
+
+@pytest.mark.parametrize('cls,norm,train,dt', [
+    (BasicEncoder, 'instance', True, torch.bfloat16), (BasicEncoder, 'batch', True, torch.bfloat16),
+    (BasicEncoder, 'batch', False, torch.bfloat16), (SmallEncoder, 'instance', True, torch.bfloat16),
+    (SmallEncoder, 'none', True, torch.bfloat16),
+    # fp16 autocast (the reference's --mixed_precision): fp16 MFMA convs and fp16 norm kernels
+    (BasicEncoder, 'instance', True, H16), (BasicEncoder, 'batch', True, H16),
+    (SmallEncoder, 'instance', True, H16)])
+def test_fast_encoder_matches_eager(ext_ops, cls, norm, train, dt):
     torch.manual_seed(0)
     enc = cls(output_dim=256 if cls is BasicEncoder else 128, norm_fn=norm).to(DEV)
     for m in enc.modules():  # non-trivial affine / conv biases / running stats
@@ -39,10 +46,12 @@ def test_fast_encoder_matches_eager(ext_ops, cls, norm, train):
         if path != 'fast':
             fast.fast_path_ok = lambda *a: False
         try:
-            with torch.autocast('cuda', dtype=torch.bfloat16, enabled=path != 'fp32'):
+            with torch.autocast('cuda', dtype=dt, enabled=path != 'fp32'):
                 if path == 'fast':
                     assert fast.fast_path_ok(enc, x)
                 y = enc(x)
+                if path != 'fp32':
+                    assert y.dtype == dt
         finally:
             fast.fast_path_ok = orig
         (y.float() * torch.linspace(-1, 1, y.numel(), device=DEV).view(y.shape)).sum().backward()
@@ -71,25 +80,26 @@ def test_fast_encoder_matches_eager(ext_ops, cls, norm, train):
         torch.testing.assert_close(bufs['fast'][k], v, atol=2e-3, rtol=2e-2)
 
 
-def test_native_head_1x1_matches_conv2d(ext_ops):
+@pytest.mark.parametrize('dt', [torch.bfloat16, H16])
+def test_native_head_1x1_matches_conv2d(ext_ops, dt):
     """Encoder head 1x1 conv on the MFMA kernels (ops/encoder.py _Head1x1) vs F.conv2d in fp32 on
-    the same bf16 operands: output and all three gradients."""
+    the same 16-bit operands: output and all three gradients."""
     from pytorch_raft_amd.ops.encoder import _Head1x1
     g = torch.Generator(device='cpu').manual_seed(2)
-    x = torch.randn(3, 128, 23, 31, generator=g).to('cuda', torch.bfloat16)
+    x = torch.randn(3, 128, 23, 31, generator=g).to('cuda', dt)
     x = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
     w = (torch.randn(256, 128, 1, 1, generator=g) * 0.05).cuda().requires_grad_(True)
     b = torch.randn(256, generator=g).cuda().requires_grad_(True)
     y = _Head1x1.apply(x, w, b)
     xr = x.detach().float().requires_grad_(True)
-    wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+    wr = w.detach().to(dt).float().requires_grad_(True)
     br = b.detach().clone().requires_grad_(True)
     ref = torch.nn.functional.conv2d(xr, wr, br)
-    assert y.shape == ref.shape and y.dtype == torch.bfloat16
+    assert y.shape == ref.shape and y.dtype == dt
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=1e-2)
     gy = torch.randn(ref.shape, generator=g).cuda()
     (y.float() * gy).sum().backward()
-    (ref * gy.to(torch.bfloat16).float()).sum().backward()
+    (ref * gy.to(dt).float()).sum().backward()
     rel = lambda a, r: ((a.float() - r).norm() / r.norm()).item()
     assert rel(x.grad, xr.grad) < 1e-2
     assert rel(w.grad, wr.grad) < 1e-2
@@ -126,18 +136,19 @@ def test_native_wgrad_3x3_matches_conv2d(ext_ops, cin, cout):
                                          (128, 128, (37, 45)), (64, 128, (37, 45)),
                                          (96, 96, (23, 31)), (64, 96, (11, 19)), (96, 128, (9, 14))])
 @pytest.mark.parametrize('packed', [False, True])
-def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout, hw, packed):
+@pytest.mark.parametrize('dt', [torch.bfloat16, H16])
+def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout, hw, packed, dt):
     """Stride-1 3x3 encoder conv entirely on the MFMA kernels (forward implicit GEMM -- or, 64 -> 64,
     the persistent 2-D halo-tile kernel --, input gradient on the flipped weight, tap-fused weight
     gradient) vs the fp32 autograd of F.conv2d at the same bf16 inputs, across image and batch
     borders and partial 8 x 16 tiles."""
     torch.manual_seed(4)
     h, wd = hw
-    x = torch.randn(3, cin, h, wd, device=DEV).to(torch.bfloat16)
+    x = torch.randn(3, cin, h, wd, device=DEV).to(dt)
     x = x.contiguous(memory_format=torch.channels_last).requires_grad_(True)
-    w = (torch.randn(cout, cin, 3, 3, device=DEV) * 0.05).to(torch.bfloat16)
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) * 0.05).to(dt)
     w = w.contiguous(memory_format=torch.channels_last).requires_grad_(True)
-    dy = torch.randn(3, cout, h, wd, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(3, cout, h, wd, device=DEV).to(dt)
     dy = dy.contiguous(memory_format=torch.channels_last)
     wd = wf = None
     if packed:
@@ -145,11 +156,12 @@ def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout, hw, packed):
         conv = torch.nn.Conv2d(cin, cout, 3, padding=1).to(DEV)
         with torch.no_grad():
             conv.weight.copy_(w.float())
-        _, adj, fwd = fast.cast_conv_weights([conv])
+        _, adj, fwd = fast.cast_conv_weights([conv], dt)
         wd, wf = adj[conv], fwd.get(conv)
         assert (wf is not None) == (cin % 64 != 0)
     y = fast._Conv3x3Native.apply(x, w, wd, wf)
-    assert y.is_contiguous(memory_format=torch.channels_last)
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.dtype == dt
+    assert w.grad is None
     y.backward(dy)
     xr = x.detach().float().requires_grad_(True)
     wr = w.detach().float().requires_grad_(True)
@@ -158,6 +170,7 @@ def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout, hw, packed):
     torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
     s = wr.grad.abs().max().item()
     torch.testing.assert_close(w.grad.float(), wr.grad, atol=1e-2 * s, rtol=1e-2)
+    assert w.grad.dtype == dt
     torch.testing.assert_close(x.grad.float(), xr.grad, atol=3e-2 * xr.grad.abs().max().item(),
                                rtol=2e-2)
     # no-grad path (inference) gives the same forward
