@@ -133,7 +133,7 @@ Tensor corr_lookup_fwd(const std::vector<Tensor>& pyr, const Tensor& coords, int
 // writes bf16 taps into channels [0, L*D*D) of an NHWC (B,H,W,Cbuf) buffer (the fused update
 // block's correlation input); the caller owns the zero padding of the remaining channels
 void corr_lookup_nhwc_(const std::vector<Tensor>& pyr, const Tensor& coords, int64_t radius,
-                       const Tensor& out) {
+                       const Tensor& out, bool split) {
   check_cuda_f32(coords, "coords");
   TORCH_CHECK(coords.dim() == 4 && coords.size(1) == 2, "coords must be (B,2,H,W)");
   TORCH_CHECK(radius == 3 || radius == 4, "radius must be 3 or 4");
@@ -165,16 +165,18 @@ void corr_lookup_nhwc_(const std::vector<Tensor>& pyr, const Tensor& coords, int
   const bool f16 = out.scalar_type() == at::kHalf;
   TORCH_CHECK(out.is_cuda() && out.is_contiguous() && (f16 || out.scalar_type() == at::kBFloat16) &&
                   out.dim() == 4 && out.size(0) == B && out.size(1) == H && out.size(2) == W &&
-                  out.size(3) >= levels * D * D,
+                  out.size(3) >= (split ? 2 : 1) * levels * D * D,
               "out must be a contiguous bf16 / fp16 (B,H,W,C>=L*D*D) buffer");
   TORCH_CHECK(!(f16 && pyr_bf16), "fp16 taps come from the fp32 pyramid");
-  const int64_t Cb = out.size(3);
+  // split fp32 taps: [hi (C/2) | lo (C/2)] bf16 halves from the fp32 pyramid
+  TORCH_CHECK(!split || (!f16 && !pyr_bf16 && out.size(3) % 16 == 0), "split taps: bf16 halves, fp32 pyramid");
+  const int64_t Cb = split ? out.size(3) / 2 : out.size(3);
   TORCH_CHECK(Cb % 8 == 0, "out channels must be a multiple of 8");
   // LDS-tiled kernel writes whole pixel rows including the zero padding
   TORCH_CHECK(launch_corr_lookup_tile(cp.data(), L.h.data(), L.w.data(), levels,
                                       coords.data_ptr<float>(), reinterpret_cast<uint16_t*>(out.data_ptr()),
                                       (int)Cb, (int)B, (int)H, (int)W, (int)radius, pyr_bf16,
-                                      f16 ? 1 : 0, cur_stream()),
+                                      split ? 2 : (f16 ? 1 : 0), cur_stream()),
               "unsupported radius");
 }
 
@@ -659,13 +661,23 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
   ConvFwdArgs a{};
   const at::ScalarType st = op16(ins[0]);
   TORCH_CHECK(!epi_f16((int)epi), "pass the epilogue kind; fp16 follows the operand dtype");
+  // split fp32 (EPI_SPL): every 16-bit tensor holds [hi | lo] halves; segments, output and aux
+  // slices name hi-half channels, the kernels find the lo half at + size(3) / 2
+  const bool spl = epi_spl((int)epi);
+  epi = epi_kind((int)epi);
+  TORCH_CHECK(!spl || (st == at::kBFloat16 && cin_small == 0), "split fp32: bf16 pairs, no small-Cin path");
+  auto half = [&](const Tensor& t) -> int64_t {
+    if (!spl) return t.size(3);
+    TORCH_CHECK(t.size(3) % 16 == 0, "split fp32 tensors hold two 8-aligned halves");
+    return t.size(3) / 2;
+  };
   a.nseg = (int)ins.size();
   int64_t cin_pad = 0;
   for (size_t s = 0; s < ins.size(); ++s) {
     check_nhwc(ins[s], B, H, W, "conv input", st);
     // a segment may run past the tensor's last channel (a 96-channel tensor in a 128-channel K
     // slot): the kernels read the channels that are not there as zeros
-    const int64_t present = std::min<int64_t>(in_cnt[s], ins[s].size(3) - in_off[s]);
+    const int64_t present = std::min<int64_t>(in_cnt[s], half(ins[s]) - in_off[s]);
     TORCH_CHECK(in_off[s] >= 0 && present > 0 && present % 8 == 0 &&
                     (present == in_cnt[s] || cin_small == 0),
                 "segment out of range");
@@ -678,6 +690,8 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
     a.seg[s].real = (int)present;
     cin_pad += in_cnt[s];
   }
+  if (spl) cin_pad *= 3;  // K thirds [hi | lo | hi]
+  a.spl = spl ? 1 : 0;
   a.cin_pad = (int)cin_pad;
   a.cin_small = (int)cin_small;
   if (cin_small) TORCH_CHECK(ins.size() == 1 && cin_small <= in_cnt[0], "small-Cin path takes one segment");
@@ -728,7 +742,8 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
     a.out0 = o.data_ptr<float>();
     a.out0_stride = 0;
     TORCH_CHECK(aux.empty(), "no aux for the NCHW epilogue");
-    TORCH_CHECK(launch_conv_fwd(a, (int)epi, (int)bn, cin_small != 0, cur_stream()), "bad epilogue");
+    TORCH_CHECK(launch_conv_fwd(a, (int)epi | (spl ? EPI_SPL : 0), (int)bn, cin_small != 0, cur_stream()),
+                "bad epilogue");
     return;
   }
   const int64_t out_ch[3] = {epi == EPI_GRU_ZR ? split : cout, epi == EPI_GRU_ZR ? cout - split : cout,
@@ -739,7 +754,8 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
     check_nhwc(outs[o], B, H, W, "conv output", f32out ? at::kFloat : st);
     TORCH_CHECK(outs[o].numel() * outs[o].element_size() < (int64_t(1) << 31),
                 "conv output exceeds the 2 GiB buffer-descriptor range");
-    TORCH_CHECK(out_off[o] >= 0 && out_off[o] + out_ch[o] <= outs[o].size(3), "output slice out of range");
+    TORCH_CHECK(out_off[o] >= 0 && out_off[o] + out_ch[o] <= (f32out ? outs[o].size(3) : half(outs[o])),
+                "output slice out of range");
     *optr[o] = f32out ? (void*)(outs[o].data_ptr<float>() + out_off[o])
                       : (void*)(u16m(outs[o]) + out_off[o]);
     *ostr[o] = (int)outs[o].size(3);
@@ -752,11 +768,12 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
     check_nhwc(aux[o], B, H, W, "conv aux", st);
     TORCH_CHECK(aux[o].numel() * 2 < (int64_t(1) << 31), "conv aux exceeds the 2 GiB buffer-descriptor range");
     const int64_t ch = (epi == EPI_GRU_ZR) ? cout - split : cout;
-    TORCH_CHECK(aux_off[o] >= 0 && aux_off[o] + ch <= aux[o].size(3), "aux slice out of range");
+    TORCH_CHECK(aux_off[o] >= 0 && aux_off[o] + ch <= half(aux[o]), "aux slice out of range");
     *aptr[o] = u16(aux[o]) + aux_off[o];
     *astr[o] = (int)aux[o].size(3);
   }
-  TORCH_CHECK(launch_conv_fwd(a, (int)epi | ef16, (int)bn, cin_small != 0, cur_stream()), "bad epilogue");
+  TORCH_CHECK(launch_conv_fwd(a, (int)epi | ef16 | (spl ? EPI_SPL : 0), (int)bn, cin_small != 0, cur_stream()),
+              "bad epilogue");
 }
 
 std::vector<int64_t> conv_tune_table() {
@@ -892,12 +909,18 @@ void conv_wgrad_multi_(const std::vector<Tensor>& gs, int64_t g_off, const std::
 void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::vector<Tensor>& ins,
                       const std::vector<int64_t>& in_off, const std::vector<int64_t>& in_cnt,
                       int64_t kh, int64_t kw, int64_t ph, int64_t pw, int64_t cout,
-                      const Tensor& dw, const c10::optional<Tensor>& db, int64_t splits) {
-  const int64_t n = (int64_t)gs.size();
+                      const Tensor& dw, const c10::optional<Tensor>& db, int64_t splits,
+                      bool split) {
+  const int64_t n0 = (int64_t)gs.size();
+  // split fp32: g and the inputs are [hi | lo] pairs; dW = sum g_hi x_hi + g_lo x_hi + g_hi x_lo
+  // as three kernel items per item (the bias sum takes the first two: g_hi + g_lo)
+  const int64_t n = split ? 3 * n0 : n0;
   const int64_t nseg = (int64_t)in_off.size();
-  TORCH_CHECK(n >= 1 && n <= RAFT_WG_MAX_ITEMS, "1..", RAFT_WG_MAX_ITEMS, " items");
+  TORCH_CHECK(n0 >= 1 && n <= RAFT_WG_MAX_ITEMS, "1..", split ? RAFT_WG_MAX_ITEMS / 3 : RAFT_WG_MAX_ITEMS,
+              " items");
   TORCH_CHECK(nseg >= 1 && nseg <= 3 && (int64_t)in_cnt.size() == nseg, "1..3 input segments");
-  TORCH_CHECK((int64_t)ins.size() == n * nseg, "ins must hold items x segments tensors");
+  TORCH_CHECK((int64_t)ins.size() == n0 * nseg, "ins must hold items x segments tensors");
+  TORCH_CHECK(!split || op16(gs.at(0)) == at::kBFloat16, "split fp32: bf16 pairs");
   TORCH_CHECK((kh == 1 && kw == 1) || (kh == 1 && kw == 5) || (kh == 5 && kw == 1) ||
                   (kh == 3 && kw == 3),
               "tap-fused wgrad supports 1x1, 1x5, 5x1 and 3x3 kernels");
@@ -931,23 +954,37 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
     }
     cin_pad += in_cnt[s];
   }
-  for (int64_t i = 0; i < n; ++i) {
+  auto half = [&](const Tensor& t) -> int64_t {
+    if (!split) return t.size(3);
+    TORCH_CHECK(t.size(3) % 16 == 0, "split fp32 tensors hold two 8-aligned halves");
+    return t.size(3) / 2;
+  };
+  for (int64_t i = 0; i < n0; ++i) {
     const Tensor& g = gs[i];
     check_nhwc(g, B, H, W, "grad", st);
     TORCH_CHECK(g.size(3) == a.g_stride, "all items' grads must share a layout");
-    TORCH_CHECK(g_off >= 0 && g_off % 8 == 0 && g_off + (cout + 7) / 8 * 8 <= g.size(3),
+    TORCH_CHECK(g_off >= 0 && g_off % 8 == 0 && g_off + (cout + 7) / 8 * 8 <= half(g),
                 "grad slice out of range (cout rounded up to 8 channels must fit the row)");
     TORCH_CHECK(g.numel() * 2 < (int64_t(1) << 31), "grad exceeds the 2 GiB buffer-descriptor range");
     it.g[i] = u16(g) + g_off;
+    if (split) {
+      it.g[n0 + i] = u16(g) + g_off + g.size(3) / 2;   // g_lo x x_hi
+      it.g[2 * n0 + i] = u16(g) + g_off;               // g_hi x x_lo
+    }
     for (int64_t s = 0; s < nseg; ++s) {
       const Tensor& x = ins[i * nseg + s];
       check_nhwc(x, B, H, W, "wgrad input", st);
       TORCH_CHECK(x.size(3) == a.seg[s].stride, "all items' inputs must share a layout");
-      TORCH_CHECK(in_off[s] + in_cnt[s] <= x.size(3), "segment out of range");
+      TORCH_CHECK(in_off[s] + in_cnt[s] <= half(x), "segment out of range");
       TORCH_CHECK(x.numel() * 2 < (int64_t(1) << 31), "wgrad input exceeds the 2 GiB buffer-descriptor range");
       it.seg[i][s] = u16(x) + in_off[s];
+      if (split) {
+        it.seg[n0 + i][s] = u16(x) + in_off[s];
+        it.seg[2 * n0 + i][s] = u16(x) + in_off[s] + x.size(3) / 2;
+      }
     }
   }
+  ta.db_items = split ? (int)(2 * n0) : 0;
   a.cin_pad = (int)cin_pad;
   a.B = (int)B; a.H = (int)H; a.W = (int)W;
   a.KH = (int)kh; a.KW = (int)kw; a.PH = (int)ph; a.PW = (int)pw;
@@ -1004,7 +1041,7 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
                  const std::vector<int64_t>& out_cnt, const std::vector<int64_t>& out_real,
                  const std::vector<int64_t>& out_acc, const std::vector<Tensor>& relu_y,
                  const std::vector<int64_t>& relu_off, const std::vector<int64_t>& gate_mode,
-                 const std::vector<Tensor>& gate_t, const std::vector<int64_t>& out_kcin) {
+                 const std::vector<Tensor>& gate_t, const std::vector<int64_t>& out_kcin, bool split) {
   TORCH_CHECK(relu_y.size() == relu_off.size(), "relu spec mismatch");
   TORCH_CHECK(out_kcin.empty() || out_kcin.size() == outs.size(), "K-prefix spec mismatch");
   TORCH_CHECK(gate_mode.empty() || gate_mode.size() == outs.size(), "gate spec mismatch");
@@ -1018,13 +1055,20 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   ConvFwdArgs a{};
   const at::ScalarType st = op16(ins[0]);
   const int ef16 = st == at::kHalf ? EPI_F16 : 0;
+  // split fp32: 16-bit tensors hold [hi | lo] halves (see conv_fwd_); fp32 outputs are plain
+  TORCH_CHECK(!split || (st == at::kBFloat16 && cin_small == 0), "split fp32: bf16 pairs, no small-Cin path");
+  auto half = [&](const Tensor& t) -> int64_t {
+    if (!split) return t.size(3);
+    TORCH_CHECK(t.size(3) % 16 == 0, "split fp32 tensors hold two 8-aligned halves");
+    return t.size(3) / 2;
+  };
   a.nseg = (int)ins.size();
   int64_t cin_pad = 0;
   for (size_t s = 0; s < ins.size(); ++s) {
     check_nhwc(ins[s], B, H, W, "dgrad input", st);
     // a segment may run past the tensor's last channel (a 96-channel tensor in a 128-channel K
     // slot): the kernels read the channels that are not there as zeros
-    const int64_t present = std::min<int64_t>(in_cnt[s], ins[s].size(3) - in_off[s]);
+    const int64_t present = std::min<int64_t>(in_cnt[s], half(ins[s]) - in_off[s]);
     TORCH_CHECK(in_off[s] >= 0 && present > 0 && present % 8 == 0 &&
                     (present == in_cnt[s] || cin_small == 0),
                 "segment out of range");
@@ -1037,6 +1081,9 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     a.seg[s].real = (int)present;
     cin_pad += in_cnt[s];
   }
+  const int64_t cin_seg = cin_pad;  // K-prefix boundaries are in segment channels
+  if (split) cin_pad *= 3;           // K thirds [hi | lo | hi]
+  a.spl = split ? 1 : 0;
   a.cin_pad = (int)cin_pad;
   a.cin_small = (int)cin_small;
   a.B = (int)B; a.H = (int)H; a.W = (int)W;
@@ -1050,7 +1097,8 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
                 "dgrad output exceeds the 2 GiB buffer-descriptor range");
     // the epilogue picks the output segment per 32-column MFMA tile
     TORCH_CHECK(out_cnt[o] % 32 == 0, "dgrad output segments must be multiples of 32 channels");
-    TORCH_CHECK(out_real[o] <= out_cnt[o] && out_off[o] >= 0 && out_off[o] + out_real[o] <= outs[o].size(3),
+    TORCH_CHECK(out_real[o] <= out_cnt[o] && out_off[o] >= 0 &&
+                    out_off[o] + out_real[o] <= (relu_mode ? half(outs[o]) : outs[o].size(3)),
                 "dgrad output slice out of range");
     if (relu_mode && o < relu_off.size() && relu_off[o] < 0) {
       // plain bf16 output (relu_off < 0: no ReLU gate)
@@ -1066,7 +1114,7 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
       const Tensor& y = relu_y[o];
       check_nhwc(y, B, H, W, "relu output", st);
       TORCH_CHECK(y.numel() * 2 < (int64_t(1) << 31), "relu output exceeds the 2 GiB descriptor range");
-      TORCH_CHECK(relu_off[o] >= 0 && relu_off[o] + out_real[o] <= y.size(3), "relu output slice out of range");
+      TORCH_CHECK(relu_off[o] >= 0 && relu_off[o] + out_real[o] <= half(y), "relu output slice out of range");
       TORCH_CHECK(!out_acc[o], "the relu-gated bf16 output cannot accumulate");
       a.oseg[o].ptr = nullptr;
       a.oseg[o].ob = u16m(outs[o]) + out_off[o];
@@ -1105,15 +1153,15 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
     gt += 6;
     for (const Tensor* t : {&z, &qr, &h}) {
       check_nhwc(*t, B, H, W, "gate input", st);
-      TORCH_CHECK(t->size(3) == z.size(3) && t->size(3) >= real, "gate inputs must share a layout");
+      TORCH_CHECK(t->size(3) == z.size(3) && half(*t) >= real, "gate inputs must share a layout");
       TORCH_CHECK(t->numel() * 2 < (int64_t(1) << 31), "gate input exceeds the 2 GiB descriptor range");
     }
     for (const Tensor* t : {&gbo, &gzo}) {
       check_nhwc(*t, B, H, W, "gate output", st);
       TORCH_CHECK(t->numel() * 2 < (int64_t(1) << 31), "gate output exceeds the 2 GiB descriptor range");
     }
-    TORCH_CHECK(gbo.size(3) >= (mode == 2 ? 2 * real : real), "gate d-pre output too narrow");
-    TORCH_CHECK(mode != 1 || gzo.size(3) >= real, "gate d-pre-z output too narrow");
+    TORCH_CHECK(half(gbo) >= (mode == 2 ? 2 * real : real), "gate d-pre output too narrow");
+    TORCH_CHECK(mode != 1 || half(gzo) >= real, "gate d-pre-z output too narrow");
     check_nhwc(gf1, B, H, W, "gate state gradient", at::kFloat);
     TORCH_CHECK(gf1.size(3) >= real && gf1.numel() * 4 < (int64_t(1) << 31), "gate state gradient");
     a.oseg[o].gate = mode;
@@ -1132,11 +1180,13 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   a.kprefix = 0;
   for (size_t o = 0; o < out_kcin.size(); ++o) {
     const int64_t kc = out_kcin[o];
-    if (kc == 0 || kc == cin_pad) continue;
+    // split fp32: the K thirds interleave hi / lo, so a prefix is no longer contiguous -- the
+    // full K runs (the packed weight is zero past the prefix anyway)
+    if (kc == 0 || kc == cin_seg || split) continue;
     int64_t acc = 0;
     bool on_boundary = false;
     for (size_t s2 = 0; s2 < ins.size(); ++s2) { acc += in_cnt[s2]; on_boundary = on_boundary || acc == kc; }
-    TORCH_CHECK(kc > 0 && kc < cin_pad && kc % 64 == 0 && on_boundary && cin_small == 0,
+    TORCH_CHECK(kc > 0 && kc < cin_seg && kc % 64 == 0 && on_boundary && cin_small == 0,
                 "out_kcin must end on an input segment boundary");
     a.oseg[o].kcin = (int)kc;
     a.kprefix = 1;
@@ -1157,7 +1207,7 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
   for (int o = 0; o < a.noseg; ++o) any_gate = any_gate || a.oseg[o].gate != 0;
   TORCH_CHECK(!(any_gate && cin_small), "gated dgrad needs the 64-channel K path");
   TORCH_CHECK(!ef16 || cin_small == 0, "fp16 operands: no small-Cin path");
-  TORCH_CHECK(launch_conv_fwd(a, (any_gate ? EPI_DGRAD_GATE : EPI_DGRAD) | ef16, bn, cin_small != 0, cur_stream()),
+  TORCH_CHECK(launch_conv_fwd(a, (any_gate ? EPI_DGRAD_GATE : EPI_DGRAD) | ef16 | (split ? EPI_SPL : 0), bn, cin_small != 0, cur_stream()),
               "dgrad launch");
 }
 
@@ -1555,14 +1605,19 @@ Tensor adamw_step_(const std::vector<Tensor>& params, const std::vector<Tensor>&
 // dcorr level 0 (B, N, N) straight from the iterations' bf16 lookup-output gradients
 Tensor corr_tap_reduce(const std::vector<Tensor>& coords, const std::vector<Tensor>& douts,
                        int64_t H, int64_t W, int64_t levels, int64_t radius, double inv_sqrt_c,
-                       bool out_bf16, int64_t pitch_mult) {
-  TORCH_CHECK(!coords.empty() && coords.size() == douts.size() && coords.size() <= RAFT_MAX_WIN,
-              "1..", RAFT_MAX_WIN, " iterations");
+                       bool out_bf16, int64_t pitch_mult, bool split) {
+  // split fp32 tap gradients ([hi | lo] bf16 halves): the fold is linear in the taps, so each
+  // iteration enters twice -- its hi and its lo half -- with the same coordinates
+  const size_t rep = split ? 2 : 1;
+  TORCH_CHECK(!coords.empty() && coords.size() == douts.size() && rep * coords.size() <= RAFT_MAX_WIN,
+              "1..", RAFT_MAX_WIN / rep, " iterations");
   TORCH_CHECK(radius == 3 || radius == 4, "radius must be 3 or 4");
   TORCH_CHECK(levels >= 1 && levels <= 4, "1..4 levels");
   const int64_t B = coords[0].size(0), N = H * W;
   const int64_t D = 2 * radius + 1;
   const int64_t cbuf = douts[0].size(-1);
+  const int64_t cuse = split ? cbuf / 2 : cbuf;
+  TORCH_CHECK(!split || (cbuf % 16 == 0 && douts[0].scalar_type() == at::kBFloat16), "split taps: bf16 halves");
   TapList tl{};
   for (size_t k = 0; k < coords.size(); ++k) {
     check_cuda_f32(coords[k], "coords");
@@ -1572,12 +1627,14 @@ Tensor corr_tap_reduce(const std::vector<Tensor>& coords, const std::vector<Tens
     check_nhwc(douts[k], B, H, W, "tap gradient", douts[0].scalar_type());
     TORCH_CHECK(douts[k].scalar_type() == at::kBFloat16 || douts[k].scalar_type() == at::kHalf,
                 "tap gradients must be bf16 or fp16");
-    TORCH_CHECK(douts[k].size(3) == cbuf && cbuf % 8 == 0 && cbuf >= levels * D * D,
+    TORCH_CHECK(douts[k].size(3) == cbuf && cbuf % 8 == 0 && cuse >= levels * D * D,
                 "tap gradient rows must share a width >= levels*(2r+1)^2, multiple of 8");
-    tl.coords[k] = coords[k].data_ptr<float>();
-    tl.dout[k] = u16(douts[k]);
+    for (size_t h = 0; h < rep; ++h) {
+      tl.coords[rep * k + h] = coords[k].data_ptr<float>();
+      tl.dout[rep * k + h] = u16(douts[k]) + h * cuse;
+    }
   }
-  tl.n = (int)coords.size();
+  tl.n = (int)(rep * coords.size());
   tl.cbuf = (int)cbuf;
   tl.tf16 = douts[0].scalar_type() == at::kHalf ? 1 : 0;
   // row pitch: N, or N rounded up to pitch_mult (zero columns: the MFMA backward GEMMs' K padding)
@@ -1704,18 +1761,22 @@ void f1_patch_(const Tensor& flow, const Tensor& patch, const c10::optional<Tens
   const int64_t B = flow.size(0), H = flow.size(2), W = flow.size(3);
   const at::ScalarType st = op16(patch);
   check_nhwc(patch, B, H, W, "patch", st);
-  TORCH_CHECK(patch.size(3) == 128, "patch must have 128 channels");
+  // 256 channels: split fp32 [hi (128) | lo (128)] (the fp32 schedule); the slot likewise
+  TORCH_CHECK(patch.size(3) == 128 || (patch.size(3) == 256 && st == at::kBFloat16),
+              "patch must have 128 channels (256: split fp32 pairs)");
+  const bool spl = patch.size(3) == 256;
   uint16_t* sp = nullptr;
   int ss = 0;
   if (slot.has_value() && slot->defined()) {
     check_nhwc(*slot, B, H, W, "slot", st);
-    TORCH_CHECK(slot_off >= 0 && slot_off + 2 <= slot->size(3), "slot range");
+    TORCH_CHECK(slot_off >= 0 && slot_off + 2 <= (spl ? slot->size(3) / 2 : slot->size(3)), "slot range");
+    TORCH_CHECK(!spl || slot->size(3) % 2 == 0, "split slot: two halves");
     sp = u16m(*slot) + slot_off;
     ss = (int)slot->size(3);
   }
   c10::DeviceGuard gd(flow.device());
-  launch_f1_patch(flow.data_ptr<float>(), u16m(patch), sp, ss, (int)B, (int)H, (int)W, st == at::kHalf,
-                  cur_stream());
+  launch_f1_patch(flow.data_ptr<float>(), u16m(patch), sp, ss, (int)B, (int)H, (int)W,
+                  spl ? 2 : (st == at::kHalf ? 1 : 0), cur_stream());
 }
 
 }  // namespace
@@ -1744,13 +1805,13 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] douts, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("corr_build_bf16(Tensor f1, Tensor f2, int levels, bool pyr_bf16=False) -> Tensor[]");
   m.def("conv_wgrad_taps_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, "
-        "int kw, int ph, int pw, int cout, Tensor dw, Tensor? db, int splits=0) -> ()");
+        "int kw, int ph, int pw, int cout, Tensor dw, Tensor? db, int splits=0, bool split=False) -> ()");
   m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");
   m.def("convex_up_bwd(Tensor flow, Tensor mask, Tensor dout, bool nhwc=False) -> Tensor[]");
-  m.def("corr_lookup_nhwc_(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out) -> ()");
+  m.def("corr_lookup_nhwc_(Tensor[] pyr, Tensor coords, int radius, Tensor(a!) out, bool split=False) -> ()");
   m.def("corr_window_grad(Tensor coords, Tensor dout, int levels, int radius) -> Tensor");
   m.def("corr_window_reduce(Tensor[] coords, Tensor[] wgs, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16=False) -> Tensor");
-  m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off, int[] gate_mode, Tensor[] gate_t, int[] out_kcin=[]) -> ()");
+  m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off, int[] gate_mode, Tensor[] gate_t, int[] out_kcin=[], bool split=False) -> ()");
   m.def("split_hilo_(Tensor x, Tensor(a!) out) -> ()");
   m.def("conv_enc64_(Tensor x, Tensor wpk, Tensor(a!) out) -> ()");
   m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale) -> ()");
@@ -1766,7 +1827,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("conv_wgrad_multi_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
   m.def("f1_patch_(Tensor flow, Tensor(a!) patch, Tensor(b!)? slot, int slot_off) -> ()");
   m.def("adamw_step_(Tensor(a!)[] params, Tensor(b!)[] grads, Tensor(c!)[] exp_avg, Tensor(d!)[] exp_avg_sq, Tensor(e!)[] steps, int[] group_of, Tensor[] lr_t, float[] lr, float[] beta1, float[] beta2, float[] eps, float[] wd, float max_norm, Tensor? inv_scale=None, Tensor(f!)? found_inf=None, bool write_grad=False) -> Tensor");
-  m.def("corr_tap_reduce(Tensor[] coords, Tensor[] douts, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16, int pitch_mult=0) -> Tensor");
+  m.def("corr_tap_reduce(Tensor[] coords, Tensor[] douts, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16, int pitch_mult=0, bool split=False) -> Tensor");
   m.def("corr_bwd_fmaps(Tensor dc, Tensor f1, Tensor f2) -> Tensor[]");
   m.def("fh2_fwd_(Tensor inp, Tensor wf, Tensor b, Tensor(a!) out) -> ()");
   m.def("fh2_dgrad_(Tensor gout, Tensor wd, Tensor fm, Tensor(a!) dx) -> ()");

@@ -82,6 +82,22 @@ template <bool F16 = false>
 __device__ __forceinline__ void bst_bf16(rsrc_t r, uint32_t off, float v) {
   __builtin_amdgcn_raw_buffer_store_b16(pack16<F16>(v), r, off, 0, 0);
 }
+// 16-bit activation element of operand type OT (0 bf16, 1 fp16, 2 split: the fp32 value as a
+// bf16 pair, hi at channel c and lo = bf16(v - hi) at channel c + stride / 2 of the same pixel
+// row -- `lo` is that distance in bytes, i.e. the row stride in elements)
+template <int OT>
+__device__ __forceinline__ float ld16(rsrc_t r, uint32_t off, uint32_t lo) {
+  float v = cvt16<OT == 1>(__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0));
+  if constexpr (OT == 2) v += cvt16<false>(__builtin_amdgcn_raw_buffer_load_b16(r, off + lo, 0, 0));
+  return v;
+}
+template <int OT>
+__device__ __forceinline__ void st16(rsrc_t r, uint32_t off, uint32_t lo, float v) {
+  const uint16_t h = pack16<OT == 1>(v);
+  __builtin_amdgcn_raw_buffer_store_b16(h, r, off, 0, 0);
+  if constexpr (OT == 2)
+    __builtin_amdgcn_raw_buffer_store_b16(pack16<false>(v - cvt16<false>(h)), r, off + lo, 0, 0);
+}
 
 // 64-channel K chunks of the workgroup whose N tile is [n0, n0 + BN): all of cin_pad unless the
 // output segments it overlaps all read a K prefix (OSeg.kcin); then the longest of those prefixes
@@ -102,7 +118,7 @@ __device__ __forceinline__ int tile_nchunk(const ConvFwdArgs& a, int n0, int BN)
 template <int TM, int TN, int WM, int WN, int EPI>
 __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc)[TM][TN], int m0,
                                               int n0, int wm, int wn, int lane, int P, int HW) {
-  constexpr bool F16 = epi_f16(EPI);
+  constexpr int OT = epi_ot(EPI);
   constexpr int E = epi_kind(EPI);
   constexpr bool F32OUT = E == EPI_F32 || E == EPI_ACC_F32 || E == EPI_F32_NCHW;
   constexpr uint32_t ES = F32OUT ? 4u : 2u;
@@ -145,7 +161,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
           const rsrc_t bm = make_rsrc(a.bmap, P_u * (uint32_t)a.bmap_stride * 2u);
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            v[r] += bld_bf16<F16>(bm, ok[r] ? (uint32_t)(mrow[r] * a.bmap_stride + n) * 2u : OOB);
+            v[r] += ld16<OT>(bm, ok[r] ? (uint32_t)(mrow[r] * a.bmap_stride + n) * 2u : OOB, (uint32_t)a.bmap_stride);
         } else if (a.bmap != nullptr) {
           const rsrc_t bm = make_rsrc(a.bmap, P_u * (uint32_t)a.bmap_stride * 4u);
 #pragma unroll
@@ -159,7 +175,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
         for (int r = 0; r < 16; ++r) {
           const uint32_t off = ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * ES : OOB;
           if constexpr (E == EPI_F32) bst_f32(o0, off, v[r]);
-          else bst_bf16<F16>(o0, off, E == EPI_RELU_BF16 ? fmaxf(v[r], 0.f) : v[r]);
+          else st16<OT>(o0, off, (uint32_t)a.out0_stride, E == EPI_RELU_BF16 ? fmaxf(v[r], 0.f) : v[r]);
         }
       } else if constexpr (E == EPI_ACC_F32) {
         uint32_t off[16];
@@ -181,32 +197,32 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
         if (ncol0 < a.split) {  // z half
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            bst_bf16<F16>(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, sigmoidf_(v[r]));
+            st16<OT>(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, (uint32_t)a.out0_stride, sigmoidf_(v[r]));
         } else {  // r half: r*h and r
           const int c = n - a.split;
           float h[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            h[r] = bld_bf16<F16>(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + c) * 2u : OOB);
+            h[r] = ld16<OT>(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + c) * 2u : OOB, (uint32_t)a.aux0_stride);
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const float g = sigmoidf_(v[r]);
-            bst_bf16<F16>(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + c) * 2u : OOB, g * h[r]);
-            bst_bf16<F16>(o2, ok[r] ? (uint32_t)(mrow[r] * a.out2_stride + c) * 2u : OOB, g);
+            st16<OT>(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + c) * 2u : OOB, (uint32_t)a.out1_stride, g * h[r]);
+            st16<OT>(o2, ok[r] ? (uint32_t)(mrow[r] * a.out2_stride + c) * 2u : OOB, (uint32_t)a.out2_stride, g);
           }
         }
       } else if constexpr (E == EPI_GRU_Q) {
         float h[16], z[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          h[r] = bld_bf16<F16>(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + n) * 2u : OOB);
-          z[r] = bld_bf16<F16>(x1, ok[r] ? (uint32_t)(mrow[r] * a.aux1_stride + n) * 2u : OOB);
+          h[r] = ld16<OT>(x0, ok[r] ? (uint32_t)(mrow[r] * a.aux0_stride + n) * 2u : OOB, (uint32_t)a.aux0_stride);
+          z[r] = ld16<OT>(x1, ok[r] ? (uint32_t)(mrow[r] * a.aux1_stride + n) * 2u : OOB, (uint32_t)a.aux1_stride);
         }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float q = tanhf_(v[r]);
-          bst_bf16<F16>(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, h[r] + z[r] * (q - h[r]));
-          bst_bf16<F16>(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + n) * 2u : OOB, q);
+          st16<OT>(o0, ok[r] ? (uint32_t)(mrow[r] * a.out0_stride + n) * 2u : OOB, (uint32_t)a.out0_stride, h[r] + z[r] * (q - h[r]));
+          st16<OT>(o1, ok[r] ? (uint32_t)(mrow[r] * a.out1_stride + n) * 2u : OOB, (uint32_t)a.out1_stride, q);
         }
       } else if constexpr (E == EPI_DGRAD || E == EPI_DGRAD_GATE) {
         // output segment of this 32-column tile (uniform)
@@ -236,19 +252,19 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
                 const bool e = ok[r] && cok;
                 pre[u] = bld_f32(od, e ? (uint32_t)(mrow[r] * o.stride + c) * 4u : OOB);
                 const uint32_t oa = e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB;
-                zz[u] = bld_bf16<F16>(rz, oa);
-                qq[u] = bld_bf16<F16>(rq, oa);
-                hh[u] = bld_bf16<F16>(rh, oa);
+                zz[u] = ld16<OT>(rz, oa, (uint32_t)o.ga_stride);
+                qq[u] = ld16<OT>(rq, oa, (uint32_t)o.ga_stride);
+                hh[u] = ld16<OT>(rh, oa, (uint32_t)o.ga_stride);
               }
 #pragma unroll
               for (int u = 0; u < 8; ++u) {
                 const int r = h8 + u;
                 const bool e = ok[r] && cok;
                 const float g = pre[u] + v[r];
-                bst_bf16<F16>(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB,
+                st16<OT>(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB, (uint32_t)o.gb_stride,
                          g * zz[u] * (1.f - qq[u] * qq[u]));
                 const float dz = g * (qq[u] - hh[u]);
-                bst_bf16<F16>(gz, e ? (uint32_t)(mrow[r] * o.gz_stride + c) * 2u : OOB,
+                st16<OT>(gz, e ? (uint32_t)(mrow[r] * o.gz_stride + c) * 2u : OOB, (uint32_t)o.gz_stride,
                          dz * zz[u] * (1.f - zz[u]));
                 bst_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB, g * (1.f - zz[u]));
               }
@@ -266,13 +282,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
                 const int r = h8 + u;
                 const bool e = ok[r] && cok;
                 pre[u] = bld_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB);
-                yv[u] = bld_bf16<F16>(ry, e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB);
+                yv[u] = ld16<OT>(ry, e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB, (uint32_t)o.ga_stride);
               }
 #pragma unroll
               for (int u = 0; u < 8; ++u) {
                 const int r = h8 + u;
                 const bool e = ok[r] && cok;
-                bst_bf16<F16>(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB,
+                st16<OT>(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + c) * 2u : OOB, (uint32_t)o.gb_stride,
                          yv[u] > 0.f ? pre[u] + v[r] : 0.f);
               }
             }
@@ -290,14 +306,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
                 const bool e = ok[r] && cok;
                 const uint32_t oa = e ? (uint32_t)(mrow[r] * o.ga_stride + c) * 2u : OOB;
                 dh[u] = bld_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB);
-                rv[u] = bld_bf16<F16>(rr, oa);
-                hh[u] = bld_bf16<F16>(rh, oa);
+                rv[u] = ld16<OT>(rr, oa, (uint32_t)o.ga_stride);
+                hh[u] = ld16<OT>(rh, oa, (uint32_t)o.ga_stride);
               }
 #pragma unroll
               for (int u = 0; u < 8; ++u) {
                 const int r = h8 + u;
                 const bool e = ok[r] && cok;
-                bst_bf16<F16>(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + o.real + c) * 2u : OOB,
+                st16<OT>(gb, e ? (uint32_t)(mrow[r] * o.gb_stride + o.real + c) * 2u : OOB, (uint32_t)o.gb_stride,
                          v[r] * hh[u] * rv[u] * (1.f - rv[u]));
                 bst_f32(f1, e ? (uint32_t)(mrow[r] * o.gf_stride + c) * 4u : OOB,
                         dh[u] + v[r] * rv[u]);
@@ -311,17 +327,17 @@ __device__ __forceinline__ void conv_epilogue(const ConvFwdArgs& a, f32x16 (&acc
           const rsrc_t ob = make_rsrc(o.ob, P_u * (uint32_t)o.ob_stride * 2u);
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            bst_bf16<F16>(ob, ok[r] && cok ? (uint32_t)(mrow[r] * o.ob_stride + c) * 2u : OOB, v[r]);
+            st16<OT>(ob, ok[r] && cok ? (uint32_t)(mrow[r] * o.ob_stride + c) * 2u : OOB, (uint32_t)o.ob_stride, v[r]);
         } else if (o.ob != nullptr) {  // relu-gated bf16 gradient
           const rsrc_t ob = make_rsrc(o.ob, P_u * (uint32_t)o.ob_stride * 2u);
           const rsrc_t ry = make_rsrc(o.ry, P_u * (uint32_t)o.ry_stride * 2u);
           float y[16];
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            y[r] = bld_bf16<F16>(ry, ok[r] && cok ? (uint32_t)(mrow[r] * o.ry_stride + c) * 2u : OOB);
+            y[r] = ld16<OT>(ry, ok[r] && cok ? (uint32_t)(mrow[r] * o.ry_stride + c) * 2u : OOB, (uint32_t)o.ry_stride);
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            bst_bf16<F16>(ob, ok[r] && cok ? (uint32_t)(mrow[r] * o.ob_stride + c) * 2u : OOB,
+            st16<OT>(ob, ok[r] && cok ? (uint32_t)(mrow[r] * o.ob_stride + c) * 2u : OOB, (uint32_t)o.ob_stride,
                      y[r] > 0.f ? v[r] : 0.f);
         } else if (o.ptr != nullptr) {
           const rsrc_t od = make_rsrc(o.ptr, P_u * (uint32_t)o.stride * 4u);

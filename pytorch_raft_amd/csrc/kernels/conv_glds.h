@@ -95,7 +95,12 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
   auto issue = [&](int t, int buf) {
     const int ch = t / ntap, tap = t - ch * ntap;
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
-    const int c0 = ch * BK;
+    int c0 = ch * BK, lo = 0;
+    if constexpr (epi_spl(EPI)) {  // split-fp32 K thirds [hi | lo | hi]
+      const int third = a.cin_pad / 3, part = c0 / third;
+      c0 -= part * third;
+      lo = part == 1;
+    }
     int s = 0, sbase = 0;
 #pragma unroll
     for (int q = 0; q < 2; ++q)
@@ -105,6 +110,7 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
     const int dy = kh - a.PH, dx = kw - a.PW;
     const int dpix = dy * a.W + dx;
     const int coff = c0 - sbase;
+    const int cshift = lo ? stride / 2 : 0;
     const int creal = a.seg[s].real;
     const uint32_t base = lds0 + (uint32_t)(buf * STAGE * 16);
 #pragma unroll
@@ -112,10 +118,10 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
       const int yy = a_y[j] + dy, xx = a_x[j] + dx;
       const bool ok = (unsigned)yy < (unsigned)a.H && (unsigned)xx < (unsigned)a.W &&
                       coff + a_lc[j] < creal;
-      const uint32_t off = (uint32_t)(((a_pix[j] + dpix) * stride + coff + a_lc[j]) * 2);
+      const uint32_t off = (uint32_t)(((a_pix[j] + dpix) * stride + coff + cshift + a_lc[j]) * 2);
       raft_dma16(rs, base + j * NT * 16, ok ? off : OOB);
     }
-    const uint32_t kb = (uint32_t)((tap * a.cin_pad + c0) * 2);
+    const uint32_t kb = (uint32_t)((tap * a.cin_pad + ch * BK) * 2);  // packed K: unsplit index
 #pragma unroll
     for (int j = 0; j < B_PER; ++j)
       raft_dma16(w_rs, base + (A_CHUNKS + j * NT) * 16, b_off[j] == OOB ? OOB : b_off[j] + kb);
@@ -255,5 +261,6 @@ bool launch_glds_epi(const ConvFwdArgs& a, int idx, hipStream_t stream) {
 
 }  // namespace conv_detail
 
-// fp16-operand epilogues (EPI_F16 set): conv_glds_f16.hip
+// fp16-operand epilogues (EPI_F16 set): conv_glds_f16.hip; split-fp32 (EPI_SPL): conv_glds_spl.hip
 bool launch_conv_glds_f16(const ConvFwdArgs& a, int epi, int idx, hipStream_t stream);
+bool launch_conv_glds_spl(const ConvFwdArgs& a, int epi, int idx, hipStream_t stream);

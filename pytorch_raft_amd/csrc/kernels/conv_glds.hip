@@ -5,6 +5,7 @@
 bool launch_conv_glds(const ConvFwdArgs& a, int epi, int idx, hipStream_t stream) {
   using namespace conv_detail;
   if (epi_f16(epi)) return launch_conv_glds_f16(a, epi, idx, stream);
+  if (epi_spl(epi)) return launch_conv_glds_spl(a, epi, idx, stream);
   switch (epi) {
     case EPI_BF16: return launch_glds_epi<EPI_BF16>(a, idx, stream);
     case EPI_RELU_BF16: return launch_glds_epi<EPI_RELU_BF16>(a, idx, stream);

@@ -89,7 +89,12 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_halo_kernel(ConvFwdArgs a) {
   // chunk c's halo image into buffer c & 1 (c >= nchunk: dummy pieces, nothing is read)
   auto issue_a = [&](int c) {
     const bool real = c < nchunk;
-    const int c0 = (real ? c : 0) * BK;
+    int c0 = (real ? c : 0) * BK, lo = 0;
+    if constexpr (epi_spl(EPI)) {  // split-fp32 K thirds [hi | lo | hi]
+      const int third = a.cin_pad / 3, part = c0 / third;
+      c0 -= part * third;
+      lo = part == 1;
+    }
     int s = 0, sbase = 0;
 #pragma unroll
     for (int q = 0; q < 2; ++q)
@@ -97,6 +102,7 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_halo_kernel(ConvFwdArgs a) {
     const rsrc_t rs = s == 0 ? seg_rs[0] : (s == 1 ? seg_rs[1] : seg_rs[2]);
     const int stride = a.seg[s].stride;
     const int coff = c0 - sbase;
+    const int cshift = lo ? stride / 2 : 0;
     const int creal = a.seg[s].real;
     const uint32_t base = lds0 + (uint32_t)((c & 1) * ABUF) + wave_off;
     // thread slot g = j * NT + tid of the image -> (row g / 9, 16-B slot g % 9; slot 8 = pad)
@@ -106,7 +112,7 @@ __global__ __launch_bounds__(NT, 1) void conv_fwd_halo_kernel(ConvFwdArgs a) {
       const int row = g / 9, slot = g - row * 9;
       const int q = m0 - HL + row;
       const bool ok = real && slot < 8 && q >= 0 && q < P && coff + slot * 8 < creal;
-      raft_dma16(rs, base + j * NT * 16, ok ? (uint32_t)((q * stride + coff + slot * 8) * 2) : OOB);
+      raft_dma16(rs, base + j * NT * 16, ok ? (uint32_t)((q * stride + coff + cshift + slot * 8) * 2) : OOB);
     }
   };
 
@@ -270,7 +276,8 @@ bool halo_cfg(const ConvFwdArgs& a, int tm, int tn, int wvm, hipStream_t s) {
   return false;
 }
 
-// the epilogues the halo kernel serves, for one operand type (TY = 0 bf16, EPI_F16 fp16)
+// the epilogues the halo kernel serves, for one operand type (TY = 0 bf16, EPI_F16 fp16,
+// EPI_SPL split fp32)
 template <int NPA, int TY>
 bool halo_switch(const ConvFwdArgs& a, int epi, int tm, int tn, int wvm, hipStream_t s) {
   switch (epi_kind(epi)) {
@@ -285,21 +292,22 @@ bool halo_switch(const ConvFwdArgs& a, int epi, int tm, int tn, int wvm, hipStre
   }
 }
 
-// one translation unit per (image size, operand type): conv_halo_<NPA>[_f16].hip
-template <int NPA, bool F16>
+// one translation unit per (image size, operand type TY): conv_halo_<NPA>[_f16|_spl].hip
+template <int NPA, int TY>
 bool launch_conv_halo_npa(const ConvFwdArgs& a, int epi, int tm, int tn, int wvm, hipStream_t stream);
 #define RAFT_HALO_DECL(N)                                                                       \
-  template <> bool launch_conv_halo_npa<N, false>(const ConvFwdArgs&, int, int, int, int, hipStream_t); \
-  template <> bool launch_conv_halo_npa<N, true>(const ConvFwdArgs&, int, int, int, int, hipStream_t);
+  template <> bool launch_conv_halo_npa<N, 0>(const ConvFwdArgs&, int, int, int, int, hipStream_t); \
+  template <> bool launch_conv_halo_npa<N, EPI_F16>(const ConvFwdArgs&, int, int, int, int, hipStream_t); \
+  template <> bool launch_conv_halo_npa<N, EPI_SPL>(const ConvFwdArgs&, int, int, int, int, hipStream_t);
 RAFT_HALO_DECL(6)
 RAFT_HALO_DECL(11)
 RAFT_HALO_DECL(16)
 #undef RAFT_HALO_DECL
-#define RAFT_HALO_TU(N, F16)                                                                    \
+#define RAFT_HALO_TU(N, TY)                                                                     \
   template <>                                                                                   \
-  bool launch_conv_halo_npa<N, F16>(const ConvFwdArgs& a, int epi, int tm, int tn, int wvm,    \
-                                    hipStream_t s) {                                            \
-    return halo_switch<N, (F16) ? EPI_F16 : 0>(a, epi, tm, tn, wvm, s);                         \
+  bool launch_conv_halo_npa<N, TY>(const ConvFwdArgs& a, int epi, int tm, int tn, int wvm,     \
+                                   hipStream_t s) {                                             \
+    return halo_switch<N, TY>(a, epi, tm, tn, wvm, s);                                          \
   }
 
 }  // namespace conv_detail

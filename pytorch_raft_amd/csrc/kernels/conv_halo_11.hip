@@ -4,5 +4,5 @@
 #include "conv_halo.h"
 
 namespace conv_detail {
-RAFT_HALO_TU(11, false)
+RAFT_HALO_TU(11, 0)
 }  // namespace conv_detail

@@ -4,5 +4,5 @@
 #include "conv_halo.h"
 
 namespace conv_detail {
-RAFT_HALO_TU(16, true)
+RAFT_HALO_TU(16, EPI_F16)
 }  // namespace conv_detail

@@ -1,8 +1,8 @@
 // Instantiations of the halo-tile conv kernel (conv_halo.h) whose A image takes 6 LDS-DMA
-// pieces per thread and chunk, fp16 operands; one translation unit per (image size, operand type)
+// pieces per thread and chunk, split-fp32 operands (EPI_SPL); one translation unit per (image size, operand type)
 // so they compile in parallel.
 #include "conv_halo.h"
 
 namespace conv_detail {
-RAFT_HALO_TU(6, EPI_F16)
+RAFT_HALO_TU(6, EPI_SPL)
 }  // namespace conv_detail

@@ -340,7 +340,15 @@ bool launch_epi_idx(const ConvFwdArgs& a, int epi, int idx, bool smallc, hipStre
     case EPI_GRU_Q | EPI_F16: return launch_cfg_idx<EPI_GRU_Q | EPI_F16, false>(a, idx, stream);
     case EPI_DGRAD | EPI_F16: return launch_cfg_idx<EPI_DGRAD | EPI_F16, false>(a, idx, stream);
     case EPI_DGRAD_GATE | EPI_F16: return launch_cfg_idx<EPI_DGRAD_GATE | EPI_F16, false>(a, idx, stream);
-    default: return false;
+    default:
+      // split fp32 (ConvFwdArgs.spl): LDS-DMA / halo configs only (cfg_allowed), dispatched by
+      // conv_glds.hip / conv_halo_6.hip on the full epilogue id
+      if (epi_spl(epi) && !epi_f16(epi) && !smallc && idx >= 0 && idx < kNumCfgs && kCfgs[idx].glds) {
+        if (kCfgs[idx].glds == HALO)
+          return launch_conv_halo(a, epi, kCfgs[idx].tm, kCfgs[idx].tn, kCfgs[idx].wvm, stream);
+        return launch_conv_glds(a, epi, idx, stream);
+      }
+      return false;
   }
 #undef RAFT_EPI_CASE
 }
@@ -363,7 +371,8 @@ bool glds_disabled() {
 
 bool cfg_allowed(int idx, int cout, bool smallc, int epi) {
   const CfgDesc& c = kCfgs[idx];
-  if (epi_f16(epi) && (smallc || !c.glds)) return false;  // fp16: LDS-DMA / halo kernels only
+  // fp16 / split fp32: LDS-DMA / halo kernels only
+  if ((epi_f16(epi) || epi_spl(epi)) && (smallc || !c.glds)) return false;
   if (smallc && !c.small_ok) return false;
   if (c.glds && glds_disabled()) return false;
   if (c.glds == HALO && halo_disabled()) return false;
@@ -375,7 +384,7 @@ bool cfg_allowed(int idx, int cout, bool smallc, int epi) {
 // Analytic fallback (stream capture / autotune disabled): rounds of workgroups x tile cost,
 // with the 2x2-wave tiles' LDS-bandwidth penalty.
 int heuristic_cfg(int P, int cout, bool smallc, int epi) {
-  const bool f16 = epi_f16(epi);  // fp16: the 2-stage LDS-DMA configs stand in
+  const bool f16 = epi_f16(epi) || epi_spl(epi);  // fp16 / split: the 2-stage LDS-DMA configs
   double best = 1e30;
   int bi = f16 ? 17 : 0;
   for (int i = 0; i < kNumCfgs; ++i) {
@@ -506,7 +515,7 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   if (real_epi && outputs_overlap_inputs(a, epi)) real_epi = false;
   const bool dgr = dgrad_real && g_scratch2 != nullptr;
   const ConvFwdArgs& ta = dgr ? td : (real_epi ? a : t);
-  const int te = (real_epi || dgr) ? epi : (EPI_F32 | (epi & EPI_F16));
+  const int te = (real_epi || dgr) ? epi : (EPI_F32 | (epi & (EPI_F16 | EPI_SPL)));
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -557,7 +566,7 @@ int choose_cfg(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   // epilogue is timed for real); fp16 operands tune apart from bf16 (LDS-DMA / halo only)
   const int eclass = (ek == EPI_DGRAD_GATE ? 3
                       : (f32out ? 1 : ((ek == EPI_GRU_ZR || ek == EPI_GRU_Q) ? 2 : 0))) +
-                     (epi_f16(epi) ? 4 : 0);
+                     (epi_f16(epi) ? 4 : 0) + (epi_spl(epi) ? 8 : 0);
   int creal = 0;
   for (int q = 0; q < a.nseg && q < 3; ++q) creal += a.seg[q].real;
   const TuneKey key{P, a.H, a.W, a.KH, a.KW, smallc ? a.cin_small : a.cin_pad, a.cout, (int)smallc,

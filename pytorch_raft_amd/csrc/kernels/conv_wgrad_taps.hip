@@ -184,6 +184,11 @@ __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_t
   const int a_col = wm * 64 + (gi & 1) * 16 + 4 * pp;   // Cout column of this lane's A reads (+32 i)
   const int b_col = wn * 32 + (gi & 1) * 16 + 4 * pp;   // Cin column of its B reads
 
+  // split-fp32 items (binding): only the leading db_items items' G columns enter the bias sum
+  bool bias_now = bias_wave;
+  auto set_bias = [&](int c) {
+    bias_now = bias_wave && (ta.db_items == 0 || c / ta.chunks_per_item < ta.db_items);
+  };
   auto compute = [&](int buf) {
     const uint8_t* Gs = smem + buf * Geo::STAGE;
     const uint8_t* Xs = Gs + Geo::G_BYTES;
@@ -197,7 +202,7 @@ __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_t
         const bf16x4_t hi = rd_tr(Gs, GRB, swz_rows<GRB>(k + 4), k + 4, a_col + 32 * i);
         af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
-      if (bias_wave) {
+      if (bias_now) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -233,6 +238,7 @@ __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_t
           raft_wait_vmcnt<0>();
         }
         __builtin_amdgcn_s_barrier();
+        set_bias(c_begin + t);
         compute(t & 1);
         __builtin_amdgcn_s_barrier();
       }
@@ -256,6 +262,7 @@ __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_t
         nb = nb >= NS ? nb - NS : nb;
         issue(c_begin + t + NS - 1, nb);
       }
+      set_bias(c_begin + t);
       compute(cur);
       cur = cur + 1 == NS ? 0 : cur + 1;
     }

@@ -105,7 +105,9 @@ __global__ __launch_bounds__(256) void corr_lookup_tile_kernel(PyrC4 pyr, const 
 // then interpolated from LDS into the bf16 pixel-row tile, which is streamed out as above.
 constexpr int TPW = 32;  // pixels per workgroup
 
-template <int R, bool BF, bool OF16 = false>
+// OT: output taps 0 bf16, 1 fp16, 2 split fp32 (bf16 hi at channel c, bf16(v - hi) at cbuf + c
+// of a 2 cbuf-wide row: the fp32 schedule's fused update block)
+template <int R, bool BF, int OT = 0>
 __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const float* __restrict__ coords,
                                                               uint16_t* __restrict__ out, int cbuf,
                                                               int B, int H, int W, int levels) {
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
   constexpr uint32_t OOB = 0x80000000u;
   __shared__ float win[TPW * 4 * EES];
   __shared__ float cxy[TPW * 4 * 2];
-  __shared__ __attribute__((aligned(16))) uint16_t tile[TPW * ROW];
+  __shared__ __attribute__((aligned(16))) uint16_t tile[(OT == 2 ? 2 : 1) * TPW * ROW];
   const int N = H * W;
   const int tiles = (N + TPW - 1) / TPW;
   const int b = blockIdx.x / tiles;
@@ -179,28 +181,34 @@ __global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const f
     const float* w = win + (px * 4 + l) * EES + iy * WRS + ix;
     const float top = (1.f - ax) * w[0] + ax * w[1];
     const float bot = (1.f - ax) * w[WRS] + ax * w[WRS + 1];
-    tile[px * ROW + ch] = raft_f2h<OF16>((1.f - ay) * top + ay * bot);
+    const float v = (1.f - ay) * top + ay * bot;
+    const uint16_t h = raft_f2h<OT == 1>(v);
+    tile[px * ROW + ch] = h;
+    if constexpr (OT == 2) tile[TPW * ROW + px * ROW + ch] = raft_f32_to_bf16(v - raft_bf16_to_f32(h));
   }
   __syncthreads();
   const int chunks = cbuf / 8;
-  for (int e = tid; e < TPW * chunks; e += 256) {
-    const int px = e / chunks, ch = e % chunks;
+  constexpr int NH = OT == 2 ? 2 : 1;  // halves of an output row
+  for (int e = tid; e < NH * TPW * chunks; e += 256) {
+    const int hf = e / (TPW * chunks), e2 = e - hf * (TPW * chunks);
+    const int px = e2 / chunks, ch = e2 % chunks;
     const int i = i0 + px;
     if (i >= N) continue;
+    const uint16_t* tl = tile + hf * (TPW * ROW);
     uint4 o;
     if (ch * 8 + 8 <= ctot) {  // whole 16-B piece of taps: one LDS read (ROW % 8 == 0)
-      o = *reinterpret_cast<const uint4*>(tile + px * ROW + ch * 8);
+      o = *reinterpret_cast<const uint4*>(tl + px * ROW + ch * 8);
     } else {
       uint16_t q8[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int c = ch * 8 + q;
-        q8[q] = c < ctot ? tile[px * ROW + c] : (uint16_t)0;
+        q8[q] = c < ctot ? tl[px * ROW + c] : (uint16_t)0;
       }
       o = make_uint4(q8[0] | ((uint32_t)q8[1] << 16), q8[2] | ((uint32_t)q8[3] << 16),
                      q8[4] | ((uint32_t)q8[5] << 16), q8[6] | ((uint32_t)q8[7] << 16));
     }
-    *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i) * cbuf + ch * 8) = o;
+    *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i) * (NH * cbuf) + hf * cbuf + ch * 8) = o;
   }
 }
 
@@ -1046,13 +1054,20 @@ bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* w
     p.w[l] = l < levels ? ws[l] : 0;
   }
   const int N = H * W;
-  if (out_f16) {
-    // fp16 taps (fp16 autocast) from the fp32 pyramid of the reference's fp32 correlation
+  if (out_f16 == 1 || out_f16 == 2) {
+    // fp16 taps (fp16 autocast; out_f16 = 1) or split-fp32 taps (fp32 schedule; 2) from the
+    // fp32 pyramid of the reference's fp32 correlation
     if (pyr_bf16) return false;
     dim3 grid((unsigned)(B * ((N + TPW - 1) / TPW)));
-    if (radius == 4) hipLaunchKernelGGL((corr_lookup_win_kernel<4, false, true>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-    else if (radius == 3) hipLaunchKernelGGL((corr_lookup_win_kernel<3, false, true>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-    else return false;
+    if (out_f16 == 1) {
+      if (radius == 4) hipLaunchKernelGGL((corr_lookup_win_kernel<4, false, 1>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+      else if (radius == 3) hipLaunchKernelGGL((corr_lookup_win_kernel<3, false, 1>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+      else return false;
+    } else {
+      if (radius == 4) hipLaunchKernelGGL((corr_lookup_win_kernel<4, false, 2>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+      else if (radius == 3) hipLaunchKernelGGL((corr_lookup_win_kernel<3, false, 2>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
+      else return false;
+    }
     return true;
   }
   static const bool legacy = [] {

@@ -95,9 +95,18 @@ enum ConvEpilogue {
   // for "16-bit operand type".  LDS-DMA and halo kernels only (the register-staged configs
   // are bf16-only)
   EPI_F16 = 16,
+  // split-fp32 flag (the fp32 schedule): every 16-bit activation the epilogue reads or writes is
+  // an fp32 value carried as a bf16 pair -- hi at channel c, lo = bf16(v - hi) at channel
+  // c + stride / 2 of the same pixel row -- and the conv runs with ConvFwdArgs.spl (K read as
+  // [hi | lo | hi] against packed weights [w_hi | w_hi | w_lo]: three bf16 products, fp32
+  // accumulation).  LDS-DMA and halo kernels only
+  EPI_SPL = 32,
 };
 inline constexpr int epi_kind(int epi) { return epi & 15; }
 inline constexpr bool epi_f16(int epi) { return (epi & EPI_F16) != 0; }
+inline constexpr bool epi_spl(int epi) { return (epi & EPI_SPL) != 0; }
+// operand type of the epilogue's 16-bit loads / stores: 0 bf16, 1 fp16, 2 split bf16 pair
+inline constexpr int epi_ot(int epi) { return epi_f16(epi) ? 1 : (epi_spl(epi) ? 2 : 0); }
 
 struct Seg {
   const uint16_t* ptr;  // bf16 NHWC base, already offset to the segment's first channel
@@ -176,6 +185,10 @@ struct ConvFwdArgs {
   OSeg oseg[3];
   int noseg;
   int kprefix;  // 1: some output segment has kcin != 0 (per-tile K steps, tile_nchunk)
+  // split-fp32 operands (set with EPI_SPL; the K map is compiled into the EPI_SPL
+  // instantiations only): cin_pad = 3 x the segments' channel sum (a multiple of 64 each
+  // third); K thirds 0 and 2 read the segments' hi halves, third 1 their lo halves (+ stride / 2)
+  int spl;
   int nullmem;  // timing experiments only: operand loads read zeros (descriptor with 0 records)
 };
 
@@ -237,6 +250,7 @@ struct WgradTapArgs {
   float* db_part;                        // [splits][cout] or null
   uint16_t* dw_bf16;                     // non-null: dW stored as bf16 here (no accumulate)
   int dw_f16;                            // ... as fp16 instead (fp16 autocast)
+  int db_items;                          // > 0: only items < db_items add to the bias gradient
 };
 bool launch_conv_wgrad_taps(const ConvWgradArgs& a, const WgradItems& it, const WgradTapArgs& ta,
                             float* db, hipStream_t stream);

@@ -91,8 +91,9 @@ __global__ __launch_bounds__(256) void flow_prep_kernel(const float* __restrict_
 // weight of the small-Cin path has exactly this K order, so the forward and the batched
 // weight gradient both run through the regular MFMA kernels.  Also writes the flow into the
 // motion-feature slot (`core/update.py:96`, cat([out, flow])).
-// thread = (pixel, 8-channel chunk of 16)
-template <bool F16>
+// thread = (pixel, 8-channel chunk of 16).  OT: 0 bf16, 1 fp16, 2 split fp32 (bf16 hi | lo
+// halves: patch rows of 256, the slot's lo half at + slot_stride / 2)
+template <int OT>
 __global__ __launch_bounds__(256) void f1_patch_kernel(const float* __restrict__ flow,
                                                        uint16_t* __restrict__ patch,
                                                        uint16_t* __restrict__ slot, int slot_stride,
@@ -107,24 +108,38 @@ __global__ __launch_bounds__(256) void f1_patch_kernel(const float* __restrict__
     const int yx = (int)(p - b * HW);
     const int y = yx / W, x = yx - y * W;
     const float* fx = flow + b * 2 * HW;
-    uint32_t w[4];
+    constexpr bool F16 = OT == 1;
+    constexpr int PROW = OT == 2 ? 256 : 128;
+    uint32_t w[4], wl[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int tap = chunk * 4 + j;
-      uint32_t v = 0u;
+      uint32_t v = 0u, vl = 0u;
       if (tap < 49) {
         const int yy = y + tap / 7 - 3, xx = x + tap % 7 - 3;
         if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
           const int64_t o = (int64_t)yy * W + xx;
-          v = (uint32_t)raft_f2h<F16>(fx[o]) | ((uint32_t)raft_f2h<F16>(fx[HW + o]) << 16);
+          const uint16_t h0 = raft_f2h<F16>(fx[o]), h1 = raft_f2h<F16>(fx[HW + o]);
+          v = (uint32_t)h0 | ((uint32_t)h1 << 16);
+          if constexpr (OT == 2)
+            vl = (uint32_t)raft_f32_to_bf16(fx[o] - raft_bf16_to_f32(h0)) |
+                 ((uint32_t)raft_f32_to_bf16(fx[HW + o] - raft_bf16_to_f32(h1)) << 16);
         }
       }
       w[j] = v;
+      wl[j] = vl;
     }
-    *reinterpret_cast<uint4*>(patch + p * 128 + chunk * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+    *reinterpret_cast<uint4*>(patch + p * PROW + chunk * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+    if constexpr (OT == 2)
+      *reinterpret_cast<uint4*>(patch + p * PROW + 128 + chunk * 8) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
     if (slot != nullptr && chunk == 0) {
-      slot[p * slot_stride] = raft_f2h<F16>(fx[yx]);
-      slot[p * slot_stride + 1] = raft_f2h<F16>(fx[HW + yx]);
+      const uint16_t h0 = raft_f2h<F16>(fx[yx]), h1 = raft_f2h<F16>(fx[HW + yx]);
+      slot[p * slot_stride] = h0;
+      slot[p * slot_stride + 1] = h1;
+      if constexpr (OT == 2) {
+        slot[p * slot_stride + slot_stride / 2] = raft_f32_to_bf16(fx[yx] - raft_bf16_to_f32(h0));
+        slot[p * slot_stride + slot_stride / 2 + 1] = raft_f32_to_bf16(fx[HW + yx] - raft_bf16_to_f32(h1));
+      }
     }
   }
 }
@@ -275,11 +290,14 @@ void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int sl
 void launch_f1_patch(const float* flow, uint16_t* patch, uint16_t* slot, int slot_stride, int B, int H,
                      int W, int f16, hipStream_t stream) {
   const int64_t total = (int64_t)B * H * W * 16;
-  if (f16)
-    hipLaunchKernelGGL(f1_patch_kernel<true>, dim3(ew_blocks(total)), dim3(256), 0, stream, flow, patch,
+  if (f16 == 2)
+    hipLaunchKernelGGL(f1_patch_kernel<2>, dim3(ew_blocks(total)), dim3(256), 0, stream, flow, patch,
+                       slot, slot_stride, B, H, W);
+  else if (f16)
+    hipLaunchKernelGGL(f1_patch_kernel<1>, dim3(ew_blocks(total)), dim3(256), 0, stream, flow, patch,
                        slot, slot_stride, B, H, W);
   else
-    hipLaunchKernelGGL(f1_patch_kernel<false>, dim3(ew_blocks(total)), dim3(256), 0, stream, flow, patch,
+    hipLaunchKernelGGL(f1_patch_kernel<0>, dim3(ew_blocks(total)), dim3(256), 0, stream, flow, patch,
                        slot, slot_stride, B, H, W);
 }
 

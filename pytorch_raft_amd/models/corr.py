@@ -189,7 +189,11 @@ class AlternateCorrBlock:
 
     def lookup_nhwc(self, coords, cbuf, dtype=torch.bfloat16):
         """(B,H,W,cbuf) zero-padded taps for the fused HIP update block (bf16 MFMA taps; an fp16
-        update block gets them converted)."""
+        update block gets them converted; dtype fp32: split-fp32 [hi | lo] taps of the fp32
+        on-the-fly lookup)."""
+        if dtype == torch.float32:
+            from ..ops.update_hip import split_nhwc
+            return split_nhwc(self(coords), cbuf)
         if self.hip:
             out = self.volume.lookup_nhwc(coords, self.radius, cbuf)
             return out if out.dtype == dtype else out.to(dtype)

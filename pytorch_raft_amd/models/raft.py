@@ -42,6 +42,8 @@ from ..ops import conv_fp32
 
 # RAFT_FP32_ENC_MFMA=0: an fp32 model's encoders keep MIOpen fp32 convs (A/B measurements)
 _FP32_ENC_MFMA = os.environ.get('RAFT_FP32_ENC_MFMA', '1') != '0'
+# RAFT_FP32_FUSED=0: an fp32 model's update block runs eagerly with per-conv split-bf16 convs
+_FP32_FUSED = os.environ.get('RAFT_FP32_FUSED', '1') != '0'
 
 
 def _get(args, name, default):
@@ -241,12 +243,15 @@ class RAFT(nn.Module):
 
     def _use_fused_update(self, img):
         """Fused MFMA update block: GPU and mixed precision -- bf16 (full and small model) or
-        fp16 autocast (full model; the operand dtype of the conv kernels' MFMAs)."""
+        fp16 autocast (full model; the operand dtype of the conv kernels' MFMAs) -- or the fp32
+        schedule of the full model (split-fp32 operands: bf16 [hi | lo] pairs, three products
+        per conv; RAFT_FP32_FUSED=0 keeps the per-conv split path of ops/conv_fp32.py)."""
         impl = _get(self.args, 'update_impl', 'auto')
         if impl == 'torch' or self.corr_impl == 'torch' or not _ext.device_ok(img):
             return False
         ok = self.args.mixed_precision and (
             self.amp_dtype == torch.bfloat16 or (self.amp_dtype == torch.float16 and not self.args.small))
+        ok = ok or (not self.args.mixed_precision and not self.args.small and _FP32_FUSED)
         if not ok:
             if impl == 'hip':
                 raise ValueError("update_impl='hip' needs mixed precision (bf16, or fp16 for the "
@@ -283,11 +288,15 @@ class RAFT(nn.Module):
     def _iterate_fused(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
         if self.args.small:
             return self._iterate_fused_small(net, inp, corr_fn, coords0, coords1, iters, test_mode)
-        from ..ops.update_hip import HipUpdateBlock, CORR_BUF
-        adt = self.amp_dtype   # operand dtype of the fused block: bf16, or fp16 autocast
+        from ..ops.update_hip import HipUpdateBlock, CORR_BUF, split_nhwc
+        # operand dtype of the fused block: bf16, fp16 autocast, or fp32 (split bf16 pairs)
+        adt = self.amp_dtype if self.args.mixed_precision else torch.float32
         hub = HipUpdateBlock(self.update_block, dtype=adt)
-        h = net.to(adt).permute(0, 2, 3, 1).contiguous()
-        x = inp.to(adt).permute(0, 2, 3, 1).contiguous()
+        if adt == torch.float32:
+            h, x = split_nhwc(net.float()), split_nhwc(inp.float())
+        else:
+            h = net.to(adt).permute(0, 2, 3, 1).contiguous()
+            x = inp.to(adt).permute(0, 2, 3, 1).contiguous()
         flow_predictions = []
         flow_up = None
         flow = coords1 - coords0

@@ -18,6 +18,19 @@ from . import _ext
 
 (EPI_BF16, EPI_RELU_BF16, EPI_F32, EPI_ACC_F32, EPI_GRU_ZR, EPI_GRU_Q, EPI_DGRAD,
  EPI_F32_NCHW) = range(8)
+# split-fp32 flag OR-ed into an epilogue id (launchers.h EPI_SPL): the fp32 schedule's operands as
+# bf16 [hi | lo] pair buffers, three bf16 products per conv (``split_weight``)
+EPI_SPL = 32
+
+
+def split_weight(wp, taps):
+    """Packed fp32 weight (Npad, taps * cin) -> the split-fp32 operand (Npad, taps * 3 cin) bf16:
+    per tap [w_hi | w_hi | w_lo] against the split convs' K thirds [x_hi | x_lo | x_hi]."""
+    n, k = wp.shape
+    w = wp.float().view(n, taps, k // taps)
+    hi = w.to(torch.bfloat16)
+    lo = (w - hi.float()).to(torch.bfloat16)
+    return torch.cat([hi, hi, lo], 2).reshape(n, 3 * k).contiguous()
 
 
 def round_up(x, m):
@@ -144,28 +157,33 @@ def _taps_ok(in_off, in_cnt, ksize):
             and sum(int(c) for c in in_cnt) // 64 <= 16)
 
 
-def conv_wgrad_taps(items, g_off, in_off, in_cnt, ksize, pad, cout, dw, db=None, splits=0):
+def conv_wgrad_taps(items, g_off, in_off, in_cnt, ksize, pad, cout, dw, db=None, splits=0,
+                    split=False):
     """Tap-fused variant of :func:`conv_wgrad_multi` (segments must be multiples of 64 channels).
-    Partial tiles of the ``splits`` chunk ranges are reduced deterministically (no atomics)."""
+    Partial tiles of the ``splits`` chunk ranges are reduced deterministically (no atomics).
+    ``split``: split-fp32 [hi | lo] operands (three products per item, at most 10 items)."""
     ins = [b for _, bufs in items for b in bufs]
     _ext.ops().conv_wgrad_taps_([g for g, _ in items], int(g_off), ins, [int(o) for o in in_off],
                                 [int(c) for c in in_cnt], int(ksize[0]), int(ksize[1]),
-                                int(pad[0]), int(pad[1]), int(cout), dw, db, int(splits))
+                                int(pad[0]), int(pad[1]), int(cout), dw, db, int(splits),
+                                bool(split))
 
 
 def conv_wgrad_multi(items, g_off, in_off, in_cnt, ksize, pad, cout, dw, db=None,
-                     pix_per_split=None):
+                     pix_per_split=None, split=False):
     """dw / db += the weight / bias gradient summed over ``items`` = [(g, [input buffers])] of one
     conv geometry (the GRU iterations of a step), in ONE launch.  Segment i of every item is
     channels [in_off[i], in_off[i] + in_cnt[i]) of that item's i-th buffer."""
     ops = _ext.ops()
     n = len(items)
     assert 1 <= n <= MAX_WG_ITEMS
-    if pix_per_split is None and _taps_ok(in_off, in_cnt, ksize):
+    if split or (pix_per_split is None and _taps_ok(in_off, in_cnt, ksize)):
+        # split fp32: the tap-fused kernel only (three products per item)
+        assert not split or n * 3 <= MAX_WG_ITEMS, 'split wgrad: at most 10 items per launch'
         ins = [b for _, bufs in items for b in bufs]
         ops.conv_wgrad_taps_([g for g, _ in items], int(g_off), ins, [int(o) for o in in_off],
                              [int(c) for c in in_cnt], int(ksize[0]), int(ksize[1]), int(pad[0]),
-                             int(pad[1]), int(cout), dw, db, 0)
+                             int(pad[1]), int(cout), dw, db, 0, bool(split))
         return
     if pix_per_split is None:
         g0 = items[0][0]

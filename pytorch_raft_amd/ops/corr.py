@@ -41,6 +41,7 @@ class _State:
         self.grad_f1 = None
         self.windows = []
         self.taps = []       # (coords, bf16 NHWC lookup-output gradient) per iteration
+        self.taps_split = False  # the taps are split-fp32 [hi | lo] rows (the fp32 schedule)
         self.radius = None
         self.bf16_bwd = False
         self.pyr_bf16 = False  # bf16 pyramid: NHWC (bf16-output) lookups only
@@ -96,7 +97,7 @@ class _AllPairsBuild(torch.autograd.Function):
         if st.taps:
             dt = _ext.ops().corr_tap_reduce([x[0] for x in st.taps], [x[1] for x in st.taps],
                                             h, w, len(st.pyramid), st.radius, 1.0 / math.sqrt(c),
-                                            bf16, 64 if native_gemm else 0)
+                                            bf16, 64 if native_gemm else 0, st.taps_split)
             dcorr = dt if dcorr is None else dcorr + dt
         st.grad = None
         st.windows = []
@@ -152,11 +153,15 @@ class _AllPairsLookupNHWC(torch.autograd.Function):
     def forward(ctx, token, coords, radius, state, cbuf, dtype=torch.bfloat16):
         b, _, h, w = coords.shape
         # the tile kernel writes every channel of each pixel row, padding included; fp16 taps
-        # (fp16 autocast) come from an fp32 pyramid
-        out = torch.empty(b, h, w, cbuf, device=coords.device, dtype=dtype)
-        _ext.ops().corr_lookup_nhwc_(state.pyramid, coords, radius, out)
+        # (fp16 autocast) come from an fp32 pyramid; dtype fp32 (the fp32 schedule): split
+        # [hi | lo] bf16 taps, 2 cbuf channels (ops/update_hip.py's split-fp32 operands)
+        spl = dtype == torch.float32
+        out = torch.empty(b, h, w, 2 * cbuf if spl else cbuf, device=coords.device,
+                          dtype=torch.bfloat16 if spl else dtype)
+        _ext.ops().corr_lookup_nhwc_(state.pyramid, coords, radius, out, spl)
         ctx.state = state
         ctx.radius = radius
+        ctx.spl = spl
         ctx.save_for_backward(coords)
         return out
 
@@ -166,16 +171,24 @@ class _AllPairsLookupNHWC(torch.autograd.Function):
         (coords,) = ctx.saved_tensors
         b, _, h, w = coords.shape
         levels = len(st.pyramid)
-        if _window_reduce_fits(h, w, levels) and len(st.taps) < 32 and dout.shape[-1] % 8 == 0:
+        spl = ctx.spl
+        # split taps enter the fold twice (hi and lo rows): at most 16 iterations per fold
+        if (_window_reduce_fits(h, w, levels) and len(st.taps) < (16 if spl else 32)
+                and dout.shape[-1] % 8 == 0 and (not st.taps or st.taps_split == spl)
+                and (not spl or dout.dtype == torch.bfloat16)):
             # keep the iteration's 16-bit tap gradient (bf16, or fp16 under fp16 autocast); all
             # iterations are folded into dcorr once per step straight from these rows
             # (corr_tap_reduce)
             td = dout.dtype if dout.dtype in (torch.bfloat16, torch.float16) else torch.bfloat16
             st.taps.append((coords, dout.to(td).contiguous()))
+            st.taps_split = spl
             st.radius = ctx.radius
         else:
             if st.grad is None:
                 st.grad = [torch.zeros_like(p) for p in st.pyramid]
+            if spl:   # split-encoded fp32 tap gradient
+                c = dout.shape[-1] // 2
+                dout = dout[..., :c].float() + dout[..., c:].float()
             _ext.ops().corr_lookup_bwd_(st.grad, coords, dout.float().contiguous(), ctx.radius)
         return None, None, None, None, None, None
 
@@ -216,6 +229,8 @@ class AllPairsVolume:
         return _AllPairsLookup.apply(self.token, coords.contiguous().float(), radius, self.state)
 
     def lookup_nhwc(self, coords, radius, cbuf, dtype=torch.bfloat16):
+        """(B,H,W,cbuf) taps in ``dtype`` (bf16 / fp16); dtype fp32: split-fp32 [hi | lo] bf16
+        taps (B,H,W,2 cbuf) from the fp32 pyramid."""
         if dtype != torch.bfloat16 and self.state.pyr_bf16:
             raise RuntimeError('bf16 pyramid: the NHWC lookup writes bf16 taps')
         return _AllPairsLookupNHWC.apply(self.token, coords.contiguous().float(), radius, self.state,

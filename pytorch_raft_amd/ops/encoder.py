@@ -48,7 +48,7 @@ class _NormAct(torch.autograd.Function):
     """y = act(norm(x + conv_bias)) on channels_last bf16 / fp16; x is the bias-free conv output."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, cbias, norm, mode, relu):
+    def forward(ctx, x, gamma, beta, cbias, norm, mode, relu, holder=None):
         y = torch.empty_like(x, memory_format=torch.channels_last)
         rm = rv = None
         momentum = 0.1
@@ -64,8 +64,11 @@ class _NormAct(torch.autograd.Function):
                     1.0 / float(norm.num_batches_tracked.item())
         mean, invstd = _ext.ops().norm_fwd_(x, mode, int(relu), gamma, beta, cbias, rm, rv,
                                             float(momentum), float(eps), None, y)
-        # y is not kept: the backward recomputes the ReLU mask from x
-        ctx.save_for_backward(x, mean, invstd, gamma, beta)
+        # y is not kept (the backward recomputes the ReLU mask from x) unless an identity-residual
+        # consumer stashes its gradient in `holder` (the stem output feeding layer1): the stash
+        # is then added where the ReLU mask is applied, in the statistics pass (no add kernel)
+        ctx.holder = holder
+        ctx.save_for_backward(x, mean, invstd, gamma, beta, y if holder is not None else None)
         ctx.mode = mode
         ctx.relu = relu
         ctx.has = (gamma is not None, beta is not None, cbias is not None)
@@ -73,7 +76,7 @@ class _NormAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, mean, invstd, gamma, beta = ctx.saved_tensors
+        x, mean, invstd, gamma, beta, y = ctx.saved_tensors
         dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
         c = x.shape[1]
         dev = x.device
@@ -82,9 +85,19 @@ class _NormAct(torch.autograd.Function):
         db = torch.empty(c, device=dev) if ctx.has[1] else None
         dc = torch.empty(c, device=dev) if ctx.has[2] else None
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        _ext.ops().norm_bwd_(dy, x, None, mean, invstd, ctx.mode, int(ctx.relu), gamma, beta, dg, db, dc,
-                             dx)
-        return dx, dg, db, dc, None, None, None
+        stash = ctx.holder.pop('g', None) if ctx.holder is not None else None
+        if stash is not None and ctx.relu:
+            # g = (dy + stash) [y > 0] formed in the statistics pass (y = relu(norm(x)): the
+            # recomputed mask from x is the same one)
+            g = torch.empty_like(x, memory_format=torch.channels_last)
+            _ext.ops().norm_bwd_(dy, x, None, mean, invstd, ctx.mode, 1, gamma, beta, dg, db, dc,
+                                 dx, stash, y, g)
+        else:
+            if stash is not None:
+                dy = dy + stash
+            _ext.ops().norm_bwd_(dy, x, None, mean, invstd, ctx.mode, int(ctx.relu), gamma, beta,
+                                 dg, db, dc, dx)
+        return dx, dg, db, dc, None, None, None, None
 
 
 class _NormActAddRelu(torch.autograd.Function):
@@ -144,6 +157,25 @@ class _NormActAddRelu(torch.autograd.Function):
         return dx, dg, db, dc, gres, None, None, None, None
 
 
+class _StashGrad(torch.autograd.Function):
+    """Identity whose input gradient goes into the producer's stash (``holder``) instead of
+    autograd: a downsample block's input feeds its stride-2 conv1 AND its downsample conv, and
+    the two input gradients would otherwise be summed by an add kernel before the producing
+    block's norm backward, which adds the stash in its statistics pass anyway."""
+
+    @staticmethod
+    def forward(ctx, x, holder):
+        ctx.holder = holder
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous(memory_format=torch.channels_last)
+        prev = ctx.holder.get('g')
+        ctx.holder['g'] = g if prev is None else prev + g
+        return None, None
+
+
 class _AddRelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a, b):
@@ -194,6 +226,9 @@ class _CastWeightsCL(torch.autograd.Function):
         ctx.maps = maps
         ctx.dt = dt
         ctx.mark_non_differentiable(*ext)
+        # the extra packs never get a gradient: no zero-filled stand-ins for them (13 fills of a
+        # BasicEncoder's packs per backward); a weight without one is zero-filled below
+        ctx.set_materialize_grads(False)
         return tuple(outs) + tuple(ext)
 
     @staticmethod
@@ -504,21 +539,28 @@ def _conv_one(ps, x, conv, with_bias=False):
     return F.conv2d(x, w, b, conv.stride, conv.padding, conv.dilation, conv.groups)
 
 
-def conv_norm_act(ps, x, conv, norm, relu=True):
+def conv_norm_act(ps, x, conv, norm, relu=True, holder=None):
     mode = _norm_mode(norm)
     y = _conv(ps, x, conv)
     y = y.contiguous(memory_format=torch.channels_last)
     gamma = beta = None
     if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and norm.affine:
         gamma, beta = norm.weight, norm.bias
-    return _NormAct.apply(y, gamma, beta, conv.bias, norm, mode, relu)
+    out = _NormAct.apply(y, gamma, beta, conv.bias, norm, mode, relu, holder)
+    if holder is not None:
+        ps.holders[id(out)] = (out, holder)
+    return out
 
 
 def residual_block(ps, blk, x):
     """`core/extractor.py:47-56` on the fast path (conv2 + norm2 + ReLU + add + ReLU fused)."""
     y = conv_norm_act(ps, x, blk.conv1, blk.norm1)
     if blk.downsample is not None:
-        x = conv_norm_act(ps, x, blk.downsample[0], blk.downsample[1], relu=False)
+        xd = x
+        prod = ps.holders.get(id(x)) if _STASH else None
+        if prod is not None and prod[0] is x:
+            xd = _StashGrad.apply(x, prod[1])   # its gradient joins the producer's stash
+        x = conv_norm_act(ps, xd, blk.downsample[0], blk.downsample[1], relu=False)
     mode = _norm_mode(blk.norm2)
     y2 = _conv(ps, y, blk.conv2).contiguous(memory_format=torch.channels_last)
     gamma = beta = None
@@ -609,7 +651,8 @@ def encoder_forward(enc, x):
 
 def _encoder_body(ps, enc, x, dt=torch.bfloat16):
     x = x.to(dt).contiguous(memory_format=torch.channels_last)
-    x = conv_norm_act(ps, x, enc.conv1, enc.norm1)
+    # the stem output's identity-residual gradient (layer1's first block) goes to its stash
+    x = conv_norm_act(ps, x, enc.conv1, enc.norm1, holder={} if _STASH else None)
     block_fn = residual_block if enc.block.__name__ == 'ResidualBlock' else bottleneck_block
     for layer in (enc.layer1, enc.layer2, enc.layer3):
         for blk in layer:

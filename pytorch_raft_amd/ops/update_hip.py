@@ -148,11 +148,12 @@ def flat_params(ub, design=FULL):
     return design.flat_params(ub)
 
 
-def _pack_layers(params_by_layer, need_grad, dtype, design=FULL):
+def _pack_layers(params_by_layer, need_grad, dtype, design=FULL, spl=False):
     """Kernel-layout weights of every fused conv: ({name: forward [Npad][K]}, {name: adjoint
     [Npad'][K']}, {name: bias}, {extra tables}).  Runs on real parameters or on index tensors
     (``_PackPlan``).  Extras: flow_head.conv2's bf16 pair tables for its VALU kernels, forward
-    [t][o][c] and adjoint [t][c][o]."""
+    [t][o][c] and adjoint [t][c][o].  ``spl`` (the fp32 schedule): flow_head.conv2 runs on the
+    MFMA conv kernels too, so its adjoint is packed (64-wide K slot of its 2 output channels)."""
     w_out, wd_out, b_out, x_out = {}, {}, {}, {}
     w_mod = {}   # per layer: the module weight as the fused conv sees it (in_sel / row_pad applied)
     F_ = torch.nn.functional
@@ -173,9 +174,12 @@ def _pack_layers(params_by_layer, need_grad, dtype, design=FULL):
             w_out[s.name] = C.pack_weight_small(w, dtype=dtype)
         else:
             w_out[s.name] = C.pack_weight(w, s.in_real, s.in_pad, dtype=dtype)
-        if need_grad and not s.patch and not (design is FULL and s.name in _NO_ADJOINT):
+        no_adj = design is FULL and s.name in _NO_ADJOINT and not (spl and s.name == 'fh2')
+        if need_grad and not s.patch and not no_adj:
             # adjoint conv: inputs = this layer's output channels, outputs = its inputs
             cout_pad = s.adj_pad or C.round_up(s.cout, 32)
+            if spl and s.name == 'fh2':
+                cout_pad = 64
             wt = w
             if cout_pad > s.cout:
                 wt = F_.pad(w, (0, 0, 0, 0, 0, 0, s.adj_off, cout_pad - s.cout - s.adj_off))
@@ -227,7 +231,7 @@ class _PackPlan:
     cast kernels per training step.  Built once per parameter geometry by running the packing
     code on index tensors (float64 holds the element ids exactly; 0 marks zero padding)."""
 
-    def __init__(self, ub, need_grad, device, design=FULL):
+    def __init__(self, ub, need_grad, device, design=FULL, spl=False):
         SPECS = design.specs
         module_params = design.module_params
         params = design.flat_params(ub)
@@ -241,7 +245,7 @@ class _PackPlan:
         idmap = {id(p): t for p, t in zip(params, ids)}
         by_layer = {s.name: [(idmap[id(w)], idmap[id(b)]) for w, b in module_params(ub)[s.name]]
                     for s in SPECS}
-        w_idx, wd_idx, b_idx, x_idx = _pack_layers(by_layer, need_grad, torch.float64, design)
+        w_idx, wd_idx, b_idx, x_idx = _pack_layers(by_layer, need_grad, torch.float64, design, spl)
         # gather index: element id - 1; padding (id 0) -> the zero slot appended after the params
         self.views = []       # (kind, name, shape) in gather order
         parts = []
@@ -281,23 +285,36 @@ class _PackPlan:
         self.uidx = uidx.to(device)
 
 
-def _plan(ub, need_grad, device, design=FULL):
-    key = (need_grad, str(device), tuple(tuple(p.shape) for p in design.flat_params(ub)))
+def _plan(ub, need_grad, device, design=FULL, spl=False):
+    key = (need_grad, str(device), tuple(tuple(p.shape) for p in design.flat_params(ub)), spl)
     cache = ub.__dict__.setdefault('_raft_pack_plans', {})
     if key not in cache:
-        cache[key] = _PackPlan(ub, need_grad, device, design)
+        cache[key] = _PackPlan(ub, need_grad, device, design, spl)
     return cache[key]
 
 
+def _taps_of(design, kind, name):
+    """Filter taps of a packed weight view (its K = taps x input channels)."""
+    if kind == 'x':
+        return design.spec['zr' + name[-1]].k[0] * design.spec['zr' + name[-1]].k[1] \
+            if name.startswith('zrq') else 1
+    s = design.spec[name]
+    if kind == 'w' and s.patch:
+        return 1
+    return s.k[0] * s.k[1]
+
+
 class _Packed:
-    """Per-step packed weights (bf16) + packed fp32 gradient accumulators."""
+    """Per-step packed weights (bf16, fp16, or -- dtype fp32, the fp32 schedule -- split-fp32
+    [w_hi | w_hi | w_lo] bf16 per tap) + packed fp32 gradient accumulators."""
 
     def defer_wgrad(self, name, g, g_off, segs):
         self.pending.setdefault(name, []).append((g, g_off, segs))
 
     def __init__(self, ub, params, device, need_grad, design=FULL, dtype=torch.bfloat16):
         self.design = design
-        self.dtype = dtype   # operand dtype of the packed weights (bf16, or fp16 autocast)
+        self.dtype = dtype   # operand dtype: bf16, fp16 autocast, or fp32 (split bf16 pairs)
+        self.spl = dtype == torch.float32
         self.w = {}
         self.wd = {}
         self.x = {}
@@ -309,16 +326,23 @@ class _Packed:
         self.ctx = None      # GRU conv -> bf16 (B,H,W,cout) context bias map (see ctx_maps)
         self.ctx_key = None
         self.device = device
-        plan = self.plan = _plan(ub, need_grad, device, design)
+        plan = self.plan = _plan(ub, need_grad, device, design, self.spl)
         self.kpad = plan.kpad
         with torch.no_grad():
             flat = torch.cat([p.detach().float().reshape(-1) for p in params] +
                              [torch.zeros(1, device=device)])
-            packed = flat.index_select(0, plan.widx).to(dtype)
+            packed = flat.index_select(0, plan.widx)
+            if not self.spl:
+                packed = packed.to(dtype)
             off = 0
             for kind, name, shape in plan.views:
                 n = shape[0] * shape[1]
-                {'w': self.w, 'wd': self.wd, 'x': self.x}[kind][name] = packed[off:off + n].view(shape)
+                v = packed[off:off + n].view(shape)
+                if self.spl:
+                    # the VALU kernels' flow_head.conv2 tables are not used by the split convs
+                    v = (v.to(torch.bfloat16) if name in ('fh2f', 'fh2d')
+                         else C.split_weight(v, _taps_of(design, kind, name)))
+                {'w': self.w, 'wd': self.wd, 'x': self.x}[kind][name] = v
                 off += n
             bias = flat.index_select(0, plan.bidx)
             off = 0
@@ -340,7 +364,9 @@ class _Packed:
 def _flush_wgrad(pk):
     """Weight gradients of every deferred (conv, iteration) item: one multi-item launch per conv
     (the weights are shared by all iterations; convf1 as a 1x1 conv over its patch buffers),
-    the flow-head conv2 by its own VALU kernel."""
+    the flow-head conv2 by its own VALU kernel (split fp32: by the tap-fused MFMA kernel, three
+    products per item, so at most MAX_WG_ITEMS / 3 items per launch)."""
+    spl = pk.spl
     for name, items in pk.pending.items():
         s = pk.design.spec[name]
         dw, db = pk.dw[name], pk.db[name]
@@ -350,6 +376,17 @@ def _flush_wgrad(pk):
         cnts = [c for _, _, c in items[0][2]]
         offs = [o for _, o, _ in items[0][2]]
         batched = C._taps_ok(offs, cnts, k) or not any(c % 128 for c in cnts)
+        if spl:
+            assert same and not small, 'split wgrad items must share one layout'
+            g_off = items[0][1]
+            in_off = [o for _, o, _ in items[0][2]]
+            in_cnt = [c for _, _, c in items[0][2]]
+            per = C.MAX_WG_ITEMS // 3
+            for i in range(0, len(items), per):
+                chunk = items[i:i + per]
+                C.conv_wgrad_multi([(g, [b for b, _, _ in segs]) for g, _, segs in chunk], g_off,
+                                   in_off, in_cnt, k, pad, s.cout, dw, db, split=True)
+            continue
         if small or not same or not batched:
             for g, g_off, segs in items:
                 C.conv_wgrad(g, g_off, segs, k, pad, s.cout, dw, db, cin_small=2 if small else 0)
@@ -388,7 +425,7 @@ class _State:
         self.dinp_acc = None   # fp32 gradient w.r.t. the context input, summed over iterations
         self.ctx_g = {}        # GRU conv -> its pre-activation gradients of the iterations run
         self.design = FULL
-        self.dtype = torch.bfloat16  # operand dtype (fp16 under fp16 autocast)
+        self.dtype = torch.bfloat16  # operand dtype (fp16 under fp16 autocast, fp32 split pairs)
 
 
 class _UpdateWeights(torch.autograd.Function):
@@ -544,8 +581,51 @@ class _Branch:
 
 
 def _bf16(shape, dev, dt=torch.bfloat16):
-    """16-bit activation buffer: bf16, or fp16 under fp16 autocast (the operand dtype of a step)."""
+    """16-bit activation buffer: bf16, or fp16 under fp16 autocast (the operand dtype of a step);
+    dt fp32 (the fp32 schedule): a bf16 [hi | lo] pair buffer of twice the channels, the value
+    being hi + lo (split fp32, ~2^-16 relative)."""
+    if dt == torch.float32:
+        return torch.empty(*shape[:-1], 2 * shape[-1], device=dev, dtype=torch.bfloat16)
     return torch.empty(*shape, device=dev, dtype=dt)
+
+
+def _to_split(x32, buf=None):
+    """fp32 (B,C,H,W) tensor of any strides (an NHWC tensor as .permute(0, 3, 1, 2)) -> split
+    bf16 NHWC [hi | lo] (B,H,W,2C) (csrc/kernels/update_ew.hip split_hilo_kernel)."""
+    b, c, h, w = x32.shape
+    if buf is None:
+        buf = torch.empty(b, h, w, 2 * c, device=x32.device, dtype=torch.bfloat16)
+    _ext.ops().split_hilo_(x32, buf)
+    return buf
+
+
+def _from_split(xs):
+    """split bf16 NHWC [hi | lo] (B,H,W,2C) -> fp32 NHWC (B,H,W,C)."""
+    c = xs.shape[-1] // 2
+    return xs[..., :c].float() + xs[..., c:].float()
+
+
+class _SplitNHWC(torch.autograd.Function):
+    """fp32 (B,C,H,W) -> split-fp32 NHWC operand (B,H,W,2 cpad) bf16 [hi | lo], channels past C
+    zero; the gradient arrives split-encoded the same way and leaves as fp32 (B,C,H,W)."""
+
+    @staticmethod
+    def forward(ctx, x, cpad):
+        b, c, h, w = x.shape
+        ctx.c = c
+        buf = torch.empty(b, h, w, 2 * cpad, device=x.device, dtype=torch.bfloat16)
+        return _to_split(x.float(), buf)
+
+    @staticmethod
+    def backward(ctx, gs):
+        g = _from_split(gs)[..., :ctx.c]
+        return g.permute(0, 3, 1, 2), None
+
+
+def split_nhwc(x, cpad=None):
+    """Autograd-aware fp32 (B,C,H,W) -> split-fp32 NHWC operand of the fused update block's
+    fp32 schedule (``HipUpdateBlock(dtype=torch.float32)``)."""
+    return _SplitNHWC.apply(x, cpad or x.shape[1])
 
 
 def _f32(shape, dev, zero=False):
@@ -569,22 +649,29 @@ def ctx_maps(pk, inp):
         return pk.ctx
     B, H, W, _ = inp.shape
     pk.ctx = {}
+    c16 = _CTX_BF16 and not pk.spl   # split fp32: fp32 maps
     for name in GRU_CONVS:
         s = SPEC[name + 'i']
         m = torch.empty(B, H, W, s.cout, device=inp.device,
-                        dtype=inp.dtype if _CTX_BF16 else torch.float32)
+                        dtype=inp.dtype if c16 else torch.float32)
         C.conv_fwd([(inp, 0, HD)], pk.w[s.name], pk.b[s.name], s.k, s.pad, s.cout,
-                   C.EPI_BF16 if _CTX_BF16 else C.EPI_F32, [m], [0])
+                   (C.EPI_BF16 if c16 else C.EPI_F32) | (C.EPI_SPL if pk.spl else 0), [m], [0])
         pk.ctx[name] = m
     pk.ctx_key = key
     return pk.ctx
 
 
-def _sum_bf16(gs):
-    """bf16 sum (fp32 accumulation) of same-shape bf16 tensors."""
+def _sum_bf16(gs, spl=False):
+    """bf16 sum (fp32 accumulation) of same-shape bf16 tensors (split fp32 pairs: the hi and lo
+    halves summed in fp32, then recombined and re-split)."""
     ops = _ext.ops()
-    out = torch.empty_like(gs[0])
     n = _ext.SUM_MAX
+    if spl:
+        acc = torch.empty(gs[0].shape, device=gs[0].device, dtype=torch.float32)
+        for i in range(0, len(gs), n):
+            ops.sum_bf16_(gs[i:i + n], acc if i else None, acc)
+        return _to_split(_from_split(acc).permute(0, 3, 1, 2))
+    out = torch.empty_like(gs[0])
     if len(gs) <= n:
         ops.sum_bf16_(gs, None, out)
         return out
@@ -602,7 +689,8 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
     flow-head half of the fused head conv and skips the mask conv: ~20 % of the iteration."""
     B, H, W, _ = h.shape
     dev = h.device
-    dt = h.dtype   # operand dtype: bf16, or fp16 under fp16 autocast
+    dt = pk.dtype  # operand dtype: bf16, fp16 autocast, or fp32 (split bf16 pair buffers)
+    spl = pk.spl
     sh = (B, H, W)
     patch = _bf16(sh + (128,), dev, dt)  # f1_patch writes all 128 channels
     mf = _bf16(sh + (128,), dev, dt)
@@ -619,7 +707,7 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
         if cout != s.cout:  # leading output rows of a fused conv (packed rows are cout-major)
             w, b = w[:C.round_up(cout, 128)], b[:cout]
         k, pad, small = ((1, 1), (0, 0), False) if s.patch else (s.k, s.pad, s.small)
-        C.conv_fwd(segs, w, b, k, pad, cout, epi, outs, offs, aux,
+        C.conv_fwd(segs, w, b, k, pad, cout, epi | (C.EPI_SPL if spl else 0), outs, offs, aux,
                    aux_offs, scale=s.scale, split=split, cin_small=2 if small else 0)
 
     br = _Branch(dev)
@@ -644,19 +732,28 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
         hin = hn
     h2 = hin
     delta = torch.empty(B, 2, H, W, device=dev, dtype=torch.float32)
+    def fh2(fm):
+        if spl:  # split fp32: the MFMA conv kernel (NCHW fp32 epilogue), not the VALU one
+            conv('fh2', [(fm, 0, 256)], C.EPI_F32_NCHW, [delta], [0])
+        else:
+            ops.fh2_fwd_(fm, pk.fh2_wf, pk.b32, delta)
+
     if need_mask:
         fm = _bf16(sh + (512,), dev, dt)
         conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0])
-        mask = _bf16(sh + (576,), dev, dt)
+        if spl:  # fp32 (B,H,W,576) mask for the upsampling (the fp32 schedule's precision)
+            mask = torch.empty(sh + (576,), device=dev, dtype=torch.float32)
+        else:
+            mask = _bf16(sh + (576,), dev, dt)
         br = _Branch(dev)
         with br:
-            conv('m2', [(fm, 256, 256)], C.EPI_BF16, [mask], [0])
-        ops.fh2_fwd_(fm, pk.fh2_wf, pk.b32, delta)
+            conv('m2', [(fm, 256, 256)], C.EPI_F32 if spl else C.EPI_BF16, [mask], [0])
+        fh2(fm)
         br.join()
     else:
         fm = _bf16(sh + (256,), dev, dt)
         conv('head', [(h2, 0, HD)], C.EPI_RELU_BF16, [fm], [0], cout=256)
-        ops.fh2_fwd_(fm, pk.fh2_wf, pk.b32, delta)
+        fh2(fm)
         mask = None
     g1, g2 = gates['1'], gates['2']
     return h2, delta, mask, (corr, patch, c1, cf, f1, mf, inp, *g1, *g2, h2, fm)
@@ -697,7 +794,8 @@ class _UpdateIter(torch.autograd.Function):
         B, H, W, _ = h2.shape
         P = B * H * W
         dev = h2.device
-        dt = h2.dtype
+        dt = pk.dtype   # bf16 / fp16, or fp32: split bf16 pair buffers
+        spl = pk.spl
         sh = (B, H, W)
         ops = _ext.ops()
 
@@ -728,15 +826,17 @@ class _UpdateIter(torch.autograd.Function):
                             s.pad[1], 2 if small else 0,
                             float(scale), [o[0] for o in outs], [o[1] for o in outs],
                             [o[2] for o in outs], [o[3] for o in outs], [o[4] for o in outs],
-                            ry, roff, gmode, gt, list(kcin or []))
+                            ry, roff, gmode, gt, list(kcin or []), spl)
 
         # ---- mask head (mask = 0.25 * conv(fm[256:]))
         if gmask is None:
             gmask = _bf16(sh + (576,), dev, dt).zero_()
+        elif spl:   # fp32 mask gradient -> split pair operand of the m2 dgrad / wgrad
+            gmask = _to_split(gmask.permute(0, 3, 1, 2))
         if gdelta is None:
             gdelta = torch.zeros(B, 2, H, W, device=dev, dtype=torch.float32)
         gmask = gmask.contiguous()
-        if gmask.dtype != dt:
+        if gmask.dtype != dt and not spl:
             gmask = gmask.to(dt)
         # the head's ReLU backward is fused into both dgrad epilogues (bf16 pre-activation grads)
         dpre_head = _bf16(sh + (512,), dev, dt)
@@ -745,9 +845,16 @@ class _UpdateIter(torch.autograd.Function):
         br = _Branch(dev)
         with br:
             dgrad('m2', [(gmask, 0, 576)], [(dpre_head, 256, 256, 256, 0, fm, 256)], scale=0.25)
-        # ---- flow head conv2 -> delta (VALU kernels; fp32 output gradient read directly)
-        pk.fh2_items.append((gd, fm))
-        ops.fh2_dgrad_(gd, pk.fh2_wd, fm, dpre_head)
+        if spl:
+            # ---- flow head conv2 on the MFMA kernels: the delta gradient as a split operand
+            # (2 channels in a 64-wide slot per half)
+            gds = _to_split(gd, _bf16(sh + (64,), dev, dt))
+            wgrad('fh2', gds, 0, [(fm, 0, 256)])
+            dgrad('fh2', [(gds, 0, 64)], [(dpre_head, 0, 256, 256, 0, fm, 0)])
+        else:
+            # ---- flow head conv2 -> delta (VALU kernels; fp32 output gradient read directly)
+            pk.fh2_items.append((gd, fm))
+            ops.fh2_dgrad_(gd, pk.fh2_wd, fm, dpre_head)
         br.join()
         # ---- head
         wgrad('head', dpre_head, 0, [(h2, 0, HD)])
@@ -757,6 +864,8 @@ class _UpdateIter(torch.autograd.Function):
         carry, st.dh_carry = st.dh_carry, None
         if gh is not None and st.zero_h is not None and gh.data_ptr() == st.zero_h.data_ptr():
             gh = None   # the stand-in zero of a carried gradient (below)
+        if gh is not None and spl:
+            gh = _from_split(gh)   # a split-encoded state gradient from outside the block
         if gh is not None:
             dh = gh.float().contiguous() if carry is None else carry.add_(gh)
         else:
@@ -849,8 +958,8 @@ class _UpdateIter(torch.autograd.Function):
             # context input / weight gradients of the four GRU convs on the summed gradients
             dinp = _f32(sh + (HD,), dev)
             for j, name in enumerate(GRU_CONVS):
-                gsum = _sum_bf16(ctx_g.pop(name))
-                cnt = gsum.shape[-1]
+                gsum = _sum_bf16(ctx_g.pop(name), spl)
+                cnt = gsum.shape[-1] // 2 if spl else gsum.shape[-1]
                 dgrad(name + 'i', [(gsum, 0, cnt)], [(dinp, 0, HD, HD, int(j > 0))])
                 wgrad(name + 'i', gsum, 0, [(inp, 0, HD)])
             st.ctx_g = {}
@@ -862,8 +971,15 @@ class _UpdateIter(torch.autograd.Function):
             # still runs that backward, which takes the real fp32 gradient from dh_carry
             st.dh_carry = dh
             if st.zero_h is None:
-                st.zero_h = torch.zeros((), device=dev, dtype=dt)
+                st.zero_h = torch.zeros((), device=dev, dtype=h0.dtype)
+            if spl and dinp is not None:
+                dinp = _to_split(dinp.permute(0, 3, 1, 2))
             return (None, st.zero_h.expand(B, H, W, h0.shape[-1]), dinp, dcorr, None, None)
+        if spl:
+            # split fp32 inputs take split-encoded gradients (same shape and dtype as h / inp)
+            dh = _to_split(dh.permute(0, 3, 1, 2))
+            if dinp is not None:
+                dinp = _to_split(dinp.permute(0, 3, 1, 2))
         return (None, dh, dinp, dcorr, None, None)
 
 

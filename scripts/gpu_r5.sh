@@ -27,7 +27,7 @@ timeout -k 10 300 python bench.py $BENCH_ARGS > $O/bench.log 2>&1 || { tail -3 $
 grep metric $O/bench.log | cut -c1-330
 step profile
 RAFT_PHASE_MARKS=1 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d /tmp/prof_$TAG -o run -- python bench.py --steps 4 --warmup 3 --trace_markers $BENCH_ARGS > $O/prof_bench.log 2>&1 || { tail -3 $O/prof_bench.log; exit 1; }
-python scripts/prof_diff.py --phases /tmp/prof_$TAG 4 > $O/summary.txt 2>&1
+python scripts/prof_diff.py --phases /tmp/prof_$TAG 4 > $O/summary.txt 2>&1 && python scripts/prof_diff.py --sequence /tmp/prof_$TAG > $O/sequence.txt 2>&1
 python scripts/categorize.py $O/summary.txt > $O/categories.txt
 cat $O/categories.txt
 step trace_update

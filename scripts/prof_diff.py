@@ -4,6 +4,7 @@ usage: prof_diff.py <dir_warm_only> <dir_warm_plus_steps> <steps>
        prof_diff.py --single <dir_of_timed_region_trace> <steps>
        prof_diff.py --markers <dir_of_full_trace> <steps>   (bench.py --trace_markers)
        prof_diff.py --phases <dir_of_full_trace> <steps>    (+ RAFT_PHASE_MARKS=1: [decode] / [encoder])
+       prof_diff.py --sequence <dir_of_full_trace>          (dispatch order of the last step's tail)
 """
 import csv, glob, os, sys
 
@@ -55,6 +56,30 @@ def load_phases(d):
     return out
 
 
+def sequence(d):
+    """Dispatch-ordered kernels from the end of the second-to-last decode replay to the last
+    timing marker: the previous step's encoder backward + optimizer, this step's encoder forward,
+    decode replay and encoder backward (RAFT_PHASE_MARKS=1 + --trace_markers)."""
+    f = glob.glob(os.path.join(d, '**', '*kernel_trace.csv'), recursive=True)
+    rows = sorted(csv.DictReader(open(f[0])), key=lambda r: int(r['Start_Timestamp']))
+    marks = [i for i, r in enumerate(rows) if 'spin' in r['Kernel_Name'].lower() or 'sleep' in r['Kernel_Name'].lower()]
+    i1 = marks[-1]
+    pm = [i for i in range(i1) if 'raft_phase_marker' in rows[i]['Kernel_Name']]
+    start = pm[-3] if len(pm) >= 3 else 0
+    phase = 'encoder'
+    for r in rows[start + 1:i1]:
+        name = r['Kernel_Name']
+        if 'raft_phase_marker' in name:
+            phase = 'decode' if phase == 'encoder' else 'encoder'
+            print('---- %s' % phase)
+            continue
+        us = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
+        print('%8.1f  [%s] %s' % (us, phase, name[:150]))
+
+
+if sys.argv[1] == '--sequence':
+    sequence(sys.argv[2])
+    sys.exit(0)
 if sys.argv[1] == '--phases':
     a, b, steps = {}, load_phases(sys.argv[2]), int(sys.argv[3])
 elif sys.argv[1] == '--markers':

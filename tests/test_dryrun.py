@@ -54,7 +54,7 @@ def _returns():
         b, _, h, w = coords.shape
         return torch.zeros(b, h * w, levels, 2 * r + 2, 2 * r + 2)
 
-    def tap_reduce(coords, douts, h, w, levels, r, s, bf16=False, pitch=0):
+    def tap_reduce(coords, douts, h, w, levels, r, s, bf16=False, pitch=0, split=False):
         ld = (h * w + pitch - 1) // pitch * pitch if pitch else h * w
         return torch.zeros(coords[0].shape[0], h * w, ld,
                            dtype=torch.bfloat16 if bf16 else torch.float32)
@@ -134,3 +134,28 @@ def test_dry_run_inference():
         lo, up = m(x, x, iters=3, test_mode=True)
     assert up.shape == (1, 2, 128, 128) and lo.shape == (1, 2, 16, 16)
     assert ops.calls.count('convex_up_fwd') == 1  # only after the last iteration
+
+
+@pytest.mark.parametrize('alternate', [False, True])
+def test_dry_run_fp32_fused_training_step(alternate):
+    """fp32 schedule (no mixed precision) through the fused block on split-fp32 operands: the
+    conv schemas take the split flags, the flow head runs on the MFMA convs (no fh2_* VALU ops),
+    and every update-block parameter gets a gradient of its own shape."""
+    from pytorch_raft_amd import RAFT
+    from pytorch_raft_amd.ops.loss import sequence_loss
+    from pytorch_raft_amd.data.synthetic import make_pair_batch
+    args = argparse.Namespace(small=False, mixed_precision=False, corr_impl='hip', update_impl='hip',
+                              alternate_corr=alternate)
+    torch.manual_seed(0)
+    m = RAFT(args).train()
+    i1, i2, flow, valid = make_pair_batch(2, 128, 160)
+    with _ext.dry_run(_returns()) as ops:
+        preds = m(i1, i2, iters=2)
+        loss, _ = sequence_loss(preds, flow, valid, 0.8)
+        loss.backward()
+    names = set(ops.calls)
+    assert {'conv_fwd_', 'conv_dgrad_', 'conv_wgrad_taps_', 'f1_patch_', 'split_hilo_'} <= names, names
+    assert not ({'fh2_fwd_', 'fh2_dgrad_', 'fh2_wgrad_'} & names), names
+    for n, p in m.named_parameters():
+        if n.startswith('update_block'):
+            assert p.grad is not None and p.grad.shape == p.shape, n
