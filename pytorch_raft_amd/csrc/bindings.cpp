@@ -1212,8 +1212,17 @@ void conv_dgrad_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_
 }
 
 // ------------------------------------------------------------------ encoder norm + activation
-// Tensors are NCHW-shaped channels_last bf16, or fp16 under fp16 autocast (the memory is NHWC);
-// every 16-bit tensor of one call has the dtype st of its first.
+// Tensors are NCHW-shaped channels_last bf16, fp16 under fp16 autocast, or fp32 (the fp32
+// schedule) -- the memory is NHWC; every activation tensor of one call has the dtype st of its
+// first.
+at::ScalarType opnorm(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf ||
+                  t.scalar_type() == at::kFloat,
+              "encoder norm tensors must be bfloat16, float16 or float32, got ", t.scalar_type());
+  return t.scalar_type();
+}
+// the launchers' storage-type flag: 0 bf16, 1 fp16, 2 fp32
+int norm_ty(at::ScalarType st) { return st == at::kHalf ? 1 : (st == at::kFloat ? 2 : 0); }
 void check_cl16(at::ScalarType st, const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == st && t.dim() == 4, name,
               ": must be a 4-D GPU tensor of dtype ", st);
@@ -1234,7 +1243,7 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
                               const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
                               double momentum, double eps, const c10::optional<Tensor>& res,
                               const Tensor& y) {
-  const at::ScalarType st = op16(x);
+  const at::ScalarType st = opnorm(x);
   check_cl16(st, x, "x");
   check_cl16(st, y, "y");
   TORCH_CHECK(y.sizes() == x.sizes(), "y shape");
@@ -1264,14 +1273,14 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
     nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
     part = at::empty({groups * (nblk + 1) * 2 * C}, fo);  // partials + per-group sums
     launch_norm_stats(xp, (int)N, (int)HW, (int)C, mode == 0, part.data_ptr<float>(), nblk, ppb,
-                      st == at::kHalf, cur_stream());
+                      norm_ty(st), cur_stream());
   }
   launch_norm_finalize(mode <= 1 ? part.data_ptr<float>() : nullptr, xp, (int)N, (int)HW, (int)C,
                        (int)mode, nblk, gp, bp, cb, rm, rv, (float)momentum, (float)eps,
                        mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
-                       shift.data_ptr<float>(), st == at::kHalf, cur_stream());
+                       shift.data_ptr<float>(), norm_ty(st), cur_stream());
   launch_norm_apply(xp, scale.data_ptr<float>(), shift.data_ptr<float>(), (int)N, (int)HW, (int)C,
-                    (int)relu, rp, u16m(y), st == at::kHalf, cur_stream());
+                    (int)relu, rp, u16m(y), norm_ty(st), cur_stream());
   return {mean, invstd};
 }
 
@@ -1282,7 +1291,7 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y
                const c10::optional<Tensor>& dbeta, const c10::optional<Tensor>& dcbias,
                const Tensor& dx, const c10::optional<Tensor>& dy2, const c10::optional<Tensor>& yres,
                const c10::optional<Tensor>& gout) {
-  const at::ScalarType st = op16(dy);
+  const at::ScalarType st = opnorm(dy);
   check_cl16(st, dy, "dy");
   check_cl16(st, x, "x");
   check_cl16(st, dx, "dx");
@@ -1331,11 +1340,11 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y
                   u16(x), yp, mean.data_ptr<float>(),
                   invstd.data_ptr<float>(), (int)N, (int)HW, (int)C, (int)mode, (int)relu, gp, bp,
                   part.data_ptr<float>(), nblk, ppb, coef.data_ptr<float>(), dg, db, dc,
-                  u16m(dx), d2, yr, go, st == at::kHalf, cur_stream());
+                  u16m(dx), d2, yr, go, norm_ty(st), cur_stream());
 }
 
 void add_relu_(const Tensor& a, const Tensor& b, const Tensor& out) {
-  const at::ScalarType st = op16(a);
+  const at::ScalarType st = opnorm(a);
   check_cl16(st, a, "a");
   check_cl16(st, b, "b");
   check_cl16(st, out, "out");
@@ -1343,11 +1352,11 @@ void add_relu_(const Tensor& a, const Tensor& b, const Tensor& out) {
   c10::DeviceGuard g(a.device());
   launch_add_relu(u16(a),
                   u16(b),
-                  u16m(out), a.numel(), st == at::kHalf, cur_stream());
+                  u16m(out), a.numel(), norm_ty(st), cur_stream());
 }
 
 void relu_mask_(const Tensor& dy, const Tensor& y, const Tensor& g, const c10::optional<Tensor>& dy2) {
-  const at::ScalarType st = op16(dy);
+  const at::ScalarType st = opnorm(dy);
   check_cl16(st, dy, "dy");
   check_cl16(st, y, "y");
   check_cl16(st, g, "g");
@@ -1361,7 +1370,7 @@ void relu_mask_(const Tensor& dy, const Tensor& y, const Tensor& g, const c10::o
   c10::DeviceGuard gd(y.device());
   launch_relu_mask(u16(dy), d2,
                    u16(y),
-                   u16m(g), y.numel(), st == at::kHalf, cur_stream());
+                   u16m(g), y.numel(), norm_ty(st), cur_stream());
 }
 
 // ------------------------------------------------------------------ update-block elementwise

@@ -25,28 +25,95 @@ namespace {
 
 constexpr int NT = 256;
 
-// 8 x 16-bit (bf16, or fp16 under fp16 autocast: F16) <-> fp32
-template <bool F16>
-__device__ __forceinline__ void unpack8(uint4 v, float (&f)[8]) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+// f16 arguments of the launchers: the storage type TY below (0 bf16, 1 fp16, 2 fp32)
+// 8 channels of one pixel in the storage type TY: 0 bf16, 1 fp16 (fp16 autocast), 2 fp32 (the
+// fp32 schedule); element offsets, 16-B (32-B for fp32) aligned groups of 8
+template <int TY> struct V8 { uint4 r; };
+template <> struct V8<2> { uint4 a, b; };
+
+template <int TY>
+__device__ __forceinline__ V8<TY> ld8(const uint16_t* p, int64_t off) {
+  V8<TY> v;
+  if constexpr (TY == 2) {
+    const uint4* q = reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(p) + off);
+    v.a = q[0];
+    v.b = q[1];
+  } else {
+    v.r = *reinterpret_cast<const uint4*>(p + off);
+  }
+  return v;
+}
+template <int TY>
+__device__ __forceinline__ void st8(uint16_t* p, int64_t off, const V8<TY>& v) {
+  if constexpr (TY == 2) {
+    uint4* q = reinterpret_cast<uint4*>(reinterpret_cast<float*>(p) + off);
+    q[0] = v.a;
+    q[1] = v.b;
+  } else {
+    *reinterpret_cast<uint4*>(p + off) = v.r;
+  }
+}
+template <int TY>
+__device__ __forceinline__ float ld1(const uint16_t* p, int64_t off) {
+  if constexpr (TY == 2) return reinterpret_cast<const float*>(p)[off];
+  else return raft_h2f<TY == 1>(p[off]);
+}
+template <int TY>
+__device__ __forceinline__ void unpack8(const V8<TY>& v, float (&f)[8]) {
+  if constexpr (TY == 2) {
+    const uint32_t w[8] = {v.a.x, v.a.y, v.a.z, v.a.w, v.b.x, v.b.y, v.b.z, v.b.w};
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if constexpr (F16) {
-      f[2 * i] = raft_h2f<true>((uint16_t)(w[i] & 0xffffu));
-      f[2 * i + 1] = raft_h2f<true>((uint16_t)(w[i] >> 16));
-    } else {
-      f[2 * i] = __uint_as_float(w[i] << 16);
-      f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    for (int i = 0; i < 8; ++i) f[i] = __uint_as_float(w[i]);
+  } else {
+    const uint32_t w[4] = {v.r.x, v.r.y, v.r.z, v.r.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (TY == 1) {
+        f[2 * i] = raft_h2f<true>((uint16_t)(w[i] & 0xffffu));
+        f[2 * i + 1] = raft_h2f<true>((uint16_t)(w[i] >> 16));
+      } else {
+        f[2 * i] = __uint_as_float(w[i] << 16);
+        f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      }
     }
   }
 }
-template <bool F16>
-__device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
-  uint32_t w[4];
+template <int TY>
+__device__ __forceinline__ V8<TY> pack8(const float (&f)[8]) {
+  V8<TY> v;
+  if constexpr (TY == 2) {
+    v.a = make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+    v.b = make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]), __float_as_uint(f[6]), __float_as_uint(f[7]));
+  } else {
+    uint32_t w[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    w[i] = (uint32_t)raft_f2h<F16>(f[2 * i]) | ((uint32_t)raft_f2h<F16>(f[2 * i + 1]) << 16);
-  return make_uint4(w[0], w[1], w[2], w[3]);
+    for (int i = 0; i < 4; ++i)
+      w[i] = (uint32_t)raft_f2h<TY == 1>(f[2 * i]) | ((uint32_t)raft_f2h<TY == 1>(f[2 * i + 1]) << 16);
+    v.r = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  return v;
+}
+
+// 16-bit value > 0 per half of a packed word: sign bit clear and magnitude non-zero (bf16 and
+// fp16 alike)
+__device__ __forceinline__ uint32_t pos_mask(uint32_t w) {
+  const uint32_t lo = ((w & 0x8000u) == 0 && (w & 0x7fffu) != 0) ? 0xffffu : 0u;
+  const uint32_t hi = ((w & 0x80000000u) == 0 && (w & 0x7fff0000u) != 0) ? 0xffff0000u : 0u;
+  return lo | hi;
+}
+// d where o > 0, else 0 (the ReLU backward on the stored forward output o)
+template <int TY>
+__device__ __forceinline__ V8<TY> mask_pos(const V8<TY>& d, const V8<TY>& o) {
+  V8<TY> r;
+  if constexpr (TY == 2) {
+    auto m = [](uint32_t dv, uint32_t ov) { return __uint_as_float(ov) > 0.f ? dv : 0u; };
+    r.a = make_uint4(m(d.a.x, o.a.x), m(d.a.y, o.a.y), m(d.a.z, o.a.z), m(d.a.w, o.a.w));
+    r.b = make_uint4(m(d.b.x, o.b.x), m(d.b.y, o.b.y), m(d.b.z, o.b.z), m(d.b.w, o.b.w));
+  } else {
+    r.r = make_uint4(d.r.x & pos_mask(o.r.x), d.r.y & pos_mask(o.r.y), d.r.z & pos_mask(o.r.z),
+                     d.r.w & pos_mask(o.r.w));
+  }
+  return r;
 }
 
 // The forward's per-(group, channel) affine of the normalised value, evaluated with exactly the
@@ -63,7 +130,7 @@ __device__ __forceinline__ void norm_affine(int mode, const float* __restrict__ 
 
 // grid.x = blocks per group-range, grid.y = image (instance) or 1 (batch: range = all images)
 // partial layout [group_img][blk][2][C]
-template <bool F16>
+template <int TY>
 __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restrict__ x, int HW,
                                                         int C, int per_image, int pix_per_blk,
                                                         int total_pix, float* __restrict__ part) {
@@ -78,7 +145,7 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
   const int p0 = blockIdx.x * pix_per_blk, p1 = min(range, p0 + pix_per_blk);
   // shift: the group's first pixel (keeps the one-pass variance well conditioned)
   float K[8];
-  unpack8<F16>(*reinterpret_cast<const uint4*>(x + base * C + g * 8), K);
+  unpack8<TY>(ld8<TY>(x, base * C + g * 8), K);
   float s1[8], s2[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) s1[i] = s2[i] = 0.f;
@@ -87,14 +154,13 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
     // thread left this pass latency-bound at ~3 TB/s
     int p = p0 + pl;
     for (; p + 7 * lanes < p1; p += 8 * lanes) {
-      uint4 raw[8];
+      V8<TY> raw[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        raw[u] = *reinterpret_cast<const uint4*>(x + (base + p + u * lanes) * C + g * 8);
+      for (int u = 0; u < 8; ++u) raw[u] = ld8<TY>(x, (base + p + u * lanes) * C + g * 8);
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         float v[8];
-        unpack8<F16>(raw[u], v);
+        unpack8<TY>(raw[u], v);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const float d = v[i] - K[i];
@@ -105,7 +171,7 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
     }
     for (; p < p1; p += lanes) {
       float v[8];
-      unpack8<F16>(*reinterpret_cast<const uint4*>(x + (base + p) * C + g * 8), v);
+      unpack8<TY>(ld8<TY>(x, (base + p) * C + g * 8), v);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float d = v[i] - K[i];
@@ -153,7 +219,7 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
 // mode: 0 instance (train or eval: always batch statistics), 1 batch-train, 2 batch-eval, 3 none
 // one thread per (group image, channel); the training-statistics modes run
 // norm_reduce_finalize_kernel instead
-template <bool F16>
+template <int TY>
 __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint16_t* __restrict__ x,
                                      int HW, int C, int groups_img, int nblk, int cnt, int mode,
                                      const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -168,7 +234,7 @@ __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint1
   float mean = 0.f, invstd = 1.f;
   if (mode == 0 || mode == 1) {
     const double a = part[(int64_t)gi * 2 * C + c], q = part[(int64_t)gi * 2 * C + C + c];
-    const float K = raft_h2f<F16>(x[(int64_t)(mode == 0 ? gi : 0) * HW * C + c]);
+    const float K = ld1<TY>(x, (int64_t)(mode == 0 ? gi : 0) * HW * C + c);
     const double m = a / cnt;
     double var = q / cnt - m * m;
     if (var < 0.0) var = 0.0;
@@ -201,7 +267,7 @@ __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint1
 // LANES lanes of one group (grid (groups, ceil(C / COLS))); the lanes stride over the group's
 // per-workgroup partials, a fixed-order LDS combine (deterministic), then lane 0 finalizes its
 // (group, channel).  16 lanes for the long batch-norm partial lists, 4 for per-image ones.
-template <int LANES, bool F16>
+template <int LANES, int TY>
 __global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(
     const float* __restrict__ part, int nblk, const uint16_t* __restrict__ x, int HW, int C,
     int cnt, int mode, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -235,7 +301,7 @@ __global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(
   const double m = (double)sa / cnt;
   double var = (double)sq / cnt - m * m;
   if (var < 0.0) var = 0.0;
-  const float K = raft_h2f<F16>(x[(int64_t)(mode == 0 ? gi : 0) * HW * C + c]);
+  const float K = ld1<TY>(x, (int64_t)(mode == 0 ? gi : 0) * HW * C + c);
   const float mean = (float)(m + K);
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   if (mode == 1 && rmean != nullptr) {
@@ -257,7 +323,7 @@ __global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(
 // y = act(x*scale + shift) [+ res -> relu];  act: relu when relu != 0.  Block size is a multiple
 // of the channel-group count: each thread keeps one channel group and reloads its scale / shift
 // only when the image changes.
-template <bool F16>
+template <int TY>
 __global__ __launch_bounds__(NT) void norm_apply_kernel(const uint16_t* __restrict__ x,
                                                         const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int HW,
@@ -281,7 +347,7 @@ __global__ __launch_bounds__(NT) void norm_apply_kernel(const uint16_t* __restri
       }
     }
     float f[8];
-    unpack8<F16>(*reinterpret_cast<const uint4*>(x + v * 8), f);
+    unpack8<TY>(ld8<TY>(x, v * 8), f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       f[i] = f[i] * sc[i] + sh[i];
@@ -289,94 +355,71 @@ __global__ __launch_bounds__(NT) void norm_apply_kernel(const uint16_t* __restri
     }
     if (res) {
       float r[8];
-      unpack8<F16>(*reinterpret_cast<const uint4*>(res + v * 8), r);
+      unpack8<TY>(ld8<TY>(res, v * 8), r);
 #pragma unroll
       for (int i = 0; i < 8; ++i) f[i] = fmaxf(f[i] + r[i], 0.f);
     }
-    *reinterpret_cast<uint4*>(y + v * 8) = pack8<F16>(f);
+    st8<TY>(y, v * 8, pack8<TY>(f));
   }
 }
 
 // out = relu(a + b)
-template <bool F16>
+template <int TY>
 __global__ __launch_bounds__(NT) void add_relu_kernel(const uint16_t* __restrict__ a,
                                                       const uint16_t* __restrict__ b,
                                                       uint16_t* __restrict__ out, int64_t nvec) {
   for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
     float fa[8], fb[8];
-    unpack8<F16>(*reinterpret_cast<const uint4*>(a + v * 8), fa);
-    unpack8<F16>(*reinterpret_cast<const uint4*>(b + v * 8), fb);
+    unpack8<TY>(ld8<TY>(a, v * 8), fa);
+    unpack8<TY>(ld8<TY>(b, v * 8), fb);
 #pragma unroll
     for (int i = 0; i < 8; ++i) fa[i] = fmaxf(fa[i] + fb[i], 0.f);
-    *reinterpret_cast<uint4*>(out + v * 8) = pack8<F16>(fa);
+    st8<TY>(out, v * 8, pack8<TY>(fa));
   }
 }
 
 // g = (dy [+ dy2]) * [y > 0]   (the ReLU backward, also the block-end residual ReLU)
-template <bool F16>
+template <int TY>
 __global__ __launch_bounds__(NT) void relu_mask_kernel(const uint16_t* __restrict__ dy,
                                                        const uint16_t* __restrict__ dy2,
                                                        const uint16_t* __restrict__ y,
                                                        uint16_t* __restrict__ g, int64_t nvec) {
   for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
-    const uint4 m = *reinterpret_cast<const uint4*>(y + v * 8);
-    const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
-    uint32_t o[4];
+    V8<TY> d = ld8<TY>(dy, v * 8);
     if (dy2 != nullptr) {
       // g = (dy + dy2) * [y > 0]: the residual-branch gradient folded in (no separate add pass)
       float a[8], b[8];
-      unpack8<F16>(*reinterpret_cast<const uint4*>(dy + v * 8), a);
-      unpack8<F16>(*reinterpret_cast<const uint4*>(dy2 + v * 8), b);
+      unpack8<TY>(d, a);
+      unpack8<TY>(ld8<TY>(dy2, v * 8), b);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t yw = (i & 1) ? (mw[i >> 1] >> 16) : (mw[i >> 1] & 0xffffu);
-        a[i] = ((yw & 0x8000u) == 0 && (yw & 0x7fffu) != 0) ? a[i] + b[i] : 0.f;
-      }
-      const uint4 r = pack8<F16>(a);
-      *reinterpret_cast<uint4*>(g + v * 8) = r;
-      continue;
+      for (int i = 0; i < 8; ++i) a[i] += b[i];
+      d = pack8<TY>(a);
     }
-    const uint4 d = *reinterpret_cast<const uint4*>(dy + v * 8);
-    const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      // bf16 > 0  <=>  sign bit clear and magnitude non-zero
-      const uint32_t lo = ((mw[i] & 0x8000u) == 0 && (mw[i] & 0x7fffu) != 0) ? 0xffffu : 0u;
-      const uint32_t hi = ((mw[i] & 0x80000000u) == 0 && (mw[i] & 0x7fff0000u) != 0) ? 0xffff0000u : 0u;
-      o[i] = dw[i] & (lo | hi);
-    }
-    *reinterpret_cast<uint4*>(g + v * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+    st8<TY>(g, v * 8, mask_pos<TY>(d, ld8<TY>(y, v * 8)));
   }
-}
-
-// bf16 > 0 per 16-bit half of a packed word: sign bit clear and magnitude non-zero
-__device__ __forceinline__ uint32_t pos_mask(uint32_t w) {
-  const uint32_t lo = ((w & 0x8000u) == 0 && (w & 0x7fffu) != 0) ? 0xffffu : 0u;
-  const uint32_t hi = ((w & 0x80000000u) == 0 && (w & 0x7fff0000u) != 0) ? 0xffff0000u : 0u;
-  return lo | hi;
 }
 
 // The block-end ReLU of a residual block (out = relu(branch + res)) folded into the norm
 // backward's statistics pass: g = (dy [+ dy2]) * [out > 0] is formed on load, written once (it
 // is also the residual's gradient and the apply pass's input) and summed -- the separate
 // relu_mask pass and its re-read of g are gone.
-template <bool F16>
-__device__ __forceinline__ uint4 block_end_grad(uint4 d, const uint16_t* dy2, int64_t off, uint4 o) {
+template <int TY>
+__device__ __forceinline__ V8<TY> block_end_grad(V8<TY> d, const uint16_t* dy2, int64_t off, const V8<TY>& o) {
   if (dy2 != nullptr) {
     float a[8], b[8];
-    unpack8<F16>(d, a);
-    unpack8<F16>(*reinterpret_cast<const uint4*>(dy2 + off), b);
+    unpack8<TY>(d, a);
+    unpack8<TY>(ld8<TY>(dy2, off), b);
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] += b[i];
-    d = pack8<F16>(a);
+    d = pack8<TY>(a);
   }
-  return make_uint4(d.x & pos_mask(o.x), d.y & pos_mask(o.y), d.z & pos_mask(o.z), d.w & pos_mask(o.w));
+  return mask_pos<TY>(d, o);
 }
 
 // backward partial sums per (group image, blk): sum g, sum g*xhat, sum xhat;
 // g = dy * [y > 0] when relu; xhat = (x - mean) * invstd.  yres != null: dy is the block output's
 // gradient, g0 = (dy [+ dy2]) * [yres > 0] is formed first and stored to gout (see above)
-template <bool F16>
+template <int TY>
 __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -403,10 +446,10 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
   float sg[8], sgx[8], sx[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) sg[i] = sgx[i] = sx[i] = 0.f;
-  auto accum = [&](const uint4& rd, const uint4& rx) {
+  auto accum = [&](const V8<TY>& rd, const V8<TY>& rx) {
     float d[8], xv[8];
-    unpack8<F16>(rd, d);
-    unpack8<F16>(rx, xv);
+    unpack8<TY>(rd, d);
+    unpack8<TY>(rx, xv);
     if (relu) {
       // the forward ReLU mask, recomputed from x with the forward's own scale / shift
 #pragma unroll
@@ -424,19 +467,19 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
     // 4 pixels (8 loads) in flight per round (see norm_stats_kernel)
     int p = p0 + pl;
     for (; p + 7 * lanes < p1; p += 8 * lanes) {
-      uint4 rd[8], rx[8];
+      V8<TY> rd[8], rx[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int64_t off = (base + p + u * lanes) * C + g * 8;
-        rd[u] = *reinterpret_cast<const uint4*>(dy + off);
-        rx[u] = *reinterpret_cast<const uint4*>(x + off);
+        rd[u] = ld8<TY>(dy, off);
+        rx[u] = ld8<TY>(x, off);
       }
       if (yres != nullptr) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int64_t off = (base + p + u * lanes) * C + g * 8;
-          rd[u] = block_end_grad<F16>(rd[u], dy2, off, *reinterpret_cast<const uint4*>(yres + off));
-          *reinterpret_cast<uint4*>(gout + off) = rd[u];
+          rd[u] = block_end_grad<TY>(rd[u], dy2, off, ld8<TY>(yres, off));
+          st8<TY>(gout, off, rd[u]);
         }
       }
 #pragma unroll
@@ -444,12 +487,12 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
     }
     for (; p < p1; p += lanes) {
       const int64_t off = (base + p) * C + g * 8;
-      uint4 d = *reinterpret_cast<const uint4*>(dy + off);
+      V8<TY> d = ld8<TY>(dy, off);
       if (yres != nullptr) {
-        d = block_end_grad<F16>(d, dy2, off, *reinterpret_cast<const uint4*>(yres + off));
-        *reinterpret_cast<uint4*>(gout + off) = d;
+        d = block_end_grad<TY>(d, dy2, off, ld8<TY>(yres, off));
+        st8<TY>(gout, off, d);
       }
-      accum(d, *reinterpret_cast<const uint4*>(x + off));
+      accum(d, ld8<TY>(x, off));
     }
   }
 #pragma unroll
@@ -496,7 +539,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
 // group's partials, fixed-order LDS combine, then lane 0 writes the group's coefficients and its
 // contributions (sum g*xhat, sum g, conv-bias term) to pg [groups][3][C]; the apply kernel's
 // first workgroup sums pg over the groups (fixed order) into dgamma / dbeta / dcbias.
-template <int LANES, bool F16>
+template <int LANES, int TY>
 __global__ __launch_bounds__(256) void norm_bwd_reduce_finalize_kernel(
     const float* __restrict__ part, int nblk, int C, int cnt, int mode,
     const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean,
@@ -561,7 +604,7 @@ __global__ __launch_bounds__(256) void norm_bwd_reduce_finalize_kernel(
 // dx = A*g + B'*x + C' with g = dy masked by the forward ReLU (read from y when given, else
 // recomputed from x with the forward's scale / shift); per-element coefficient reads (L1-resident
 // table) measured faster than per-thread register caching across the grid-stride loop
-template <bool F16>
+template <int TY>
 __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint16_t* __restrict__ y,
     const float* __restrict__ coef, int HW, int C, int per_image, int64_t nvec, int relu,
@@ -588,33 +631,33 @@ __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     const int g = (int)(v - pix * cg);
     const int gi = per_image ? (int)(pix / HW) : 0;
     float d[8], xv[8];
-    unpack8<F16>(*reinterpret_cast<const uint4*>(dy + v * 8), d);
-    unpack8<F16>(*reinterpret_cast<const uint4*>(x + v * 8), xv);
+    unpack8<TY>(ld8<TY>(dy, v * 8), d);
+    unpack8<TY>(ld8<TY>(x, v * 8), xv);
     const float* co = coef + (int64_t)gi * 5 * C + g * 8;
-    auto ld8 = [&](int f, float (&r)[8]) {
+    auto ldc = [&](int f, float (&r)[8]) {
       const float4 a = *reinterpret_cast<const float4*>(co + f * C);
       const float4 b = *reinterpret_cast<const float4*>(co + f * C + 4);
       r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w; r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
     };
     if (relu && y != nullptr) {
       float yv[8];
-      unpack8<F16>(*reinterpret_cast<const uint4*>(y + v * 8), yv);
+      unpack8<TY>(ld8<TY>(y, v * 8), yv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) d[i] = yv[i] > 0.f ? d[i] : 0.f;
     } else if (relu) {
       float sc[8], sh[8];
-      ld8(3, sc);
-      ld8(4, sh);
+      ldc(3, sc);
+      ldc(4, sh);
 #pragma unroll
       for (int i = 0; i < 8; ++i) d[i] = xv[i] * sc[i] + sh[i] > 0.f ? d[i] : 0.f;
     }
     float A[8], Bp[8], Cp[8], o[8];
-    ld8(0, A);
-    ld8(1, Bp);
-    ld8(2, Cp);
+    ldc(0, A);
+    ldc(1, Bp);
+    ldc(2, Cp);
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + Bp[i] * xv[i] + Cp[i];
-    *reinterpret_cast<uint4*>(dx + v * 8) = pack8<F16>(o);
+    st8<TY>(dx, v * 8, pack8<TY>(o));
   }
 }
 
@@ -639,9 +682,11 @@ int encoder_norm_blocks(int64_t range, int C, int* pix_per_blk) {
 void launch_norm_stats(const uint16_t* x, int N, int HW, int C, int per_image, float* part,
                        int nblk, int pix_per_blk, int f16, hipStream_t stream) {
   dim3 grid(nblk, per_image ? N : 1);
-  if (f16) hipLaunchKernelGGL(norm_stats_kernel<true>, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
+  if (f16 == 2) hipLaunchKernelGGL(norm_stats_kernel<2>, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
                      N * HW, part);
-  else hipLaunchKernelGGL(norm_stats_kernel<false>, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
+  else if (f16) hipLaunchKernelGGL(norm_stats_kernel<1>, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
+                     N * HW, part);
+  else hipLaunchKernelGGL(norm_stats_kernel<0>, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
                      N * HW, part);
 }
 
@@ -655,27 +700,36 @@ void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, i
   if (mode <= 1) {
     // training statistics: partial reduce + finalize in one launch
     if (nblk > 64) {
-      if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, true>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+      if (f16 == 2) hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 2>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                          stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
                          momentum, eps, mean, invstd, scale, shift, N);
-      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, false>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+      else if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 1>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
+      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 0>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                          stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
                          momentum, eps, mean, invstd, scale, shift, N);
     } else {
-      if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, true>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+      if (f16 == 2) hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, 2>), dim3(groups, (C + 63) / 64), dim3(256), 0,
                          stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
                          momentum, eps, mean, invstd, scale, shift, N);
-      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, false>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+      else if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, 1>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
+      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, 0>), dim3(groups, (C + 63) / 64), dim3(256), 0,
                          stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
                          momentum, eps, mean, invstd, scale, shift, N);
     }
     return;
   }
   float* sums = nullptr;
-  if (f16) hipLaunchKernelGGL(norm_finalize_kernel<true>, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
+  if (f16 == 2) hipLaunchKernelGGL(norm_finalize_kernel<2>, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
                      C, groups, nblk, cnt, mode, gamma, beta, cbias, rmean, rvar, momentum, eps, mean,
                      invstd, scale, shift, N);
-  else hipLaunchKernelGGL(norm_finalize_kernel<false>, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
+  else if (f16) hipLaunchKernelGGL(norm_finalize_kernel<1>, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
+                     C, groups, nblk, cnt, mode, gamma, beta, cbias, rmean, rvar, momentum, eps, mean,
+                     invstd, scale, shift, N);
+  else hipLaunchKernelGGL(norm_finalize_kernel<0>, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
                      C, groups, nblk, cnt, mode, gamma, beta, cbias, rmean, rvar, momentum, eps, mean,
                      invstd, scale, shift, N);
 }
@@ -684,24 +738,28 @@ void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift
                        int C, int relu, const uint16_t* res, uint16_t* y, int f16, hipStream_t stream) {
   const int64_t nvec = (int64_t)N * HW * C / 8;
   const int bt = (NT / (C / 8)) * (C / 8);  // multiple of the channel-group count
-  if (f16) hipLaunchKernelGGL(norm_apply_kernel<true>, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
+  if (f16 == 2) hipLaunchKernelGGL(norm_apply_kernel<2>, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
                      C, nvec, relu, res, y);
-  else hipLaunchKernelGGL(norm_apply_kernel<false>, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
+  else if (f16) hipLaunchKernelGGL(norm_apply_kernel<1>, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
+                     C, nvec, relu, res, y);
+  else hipLaunchKernelGGL(norm_apply_kernel<0>, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
                      C, nvec, relu, res, y);
 }
 
 void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_t n,
                      int f16, hipStream_t stream) {
   const int64_t nvec = n / 8;
-  if (f16) hipLaunchKernelGGL(add_relu_kernel<true>, dim3(grid_for(nvec)), dim3(NT), 0, stream, a, b, out, nvec);
-  else hipLaunchKernelGGL(add_relu_kernel<false>, dim3(grid_for(nvec)), dim3(NT), 0, stream, a, b, out, nvec);
+  if (f16 == 2) hipLaunchKernelGGL(add_relu_kernel<2>, dim3(grid_for(nvec)), dim3(NT), 0, stream, a, b, out, nvec);
+  else if (f16) hipLaunchKernelGGL(add_relu_kernel<1>, dim3(grid_for(nvec)), dim3(NT), 0, stream, a, b, out, nvec);
+  else hipLaunchKernelGGL(add_relu_kernel<0>, dim3(grid_for(nvec)), dim3(NT), 0, stream, a, b, out, nvec);
 }
 
 void launch_relu_mask(const uint16_t* dy, const uint16_t* dy2, const uint16_t* y, uint16_t* g, int64_t n,
                       int f16, hipStream_t stream) {
   const int64_t nvec = n / 8;
-  if (f16) hipLaunchKernelGGL(relu_mask_kernel<true>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, dy2, y, g, nvec);
-  else hipLaunchKernelGGL(relu_mask_kernel<false>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, dy2, y, g, nvec);
+  if (f16 == 2) hipLaunchKernelGGL(relu_mask_kernel<2>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, dy2, y, g, nvec);
+  else if (f16) hipLaunchKernelGGL(relu_mask_kernel<1>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, dy2, y, g, nvec);
+  else hipLaunchKernelGGL(relu_mask_kernel<0>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, dy2, y, g, nvec);
 }
 
 void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
@@ -715,16 +773,20 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
   const int cnt = per_image ? HW : N * HW;
   if (mode == 0 || mode == 1) {
     dim3 grid(nblk, groups);
-    if (f16) hipLaunchKernelGGL(norm_bwd_stats_kernel<true>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+    if (f16 == 2) hipLaunchKernelGGL(norm_bwd_stats_kernel<2>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
                        beta, mode, HW, C, per_image, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
-    else hipLaunchKernelGGL(norm_bwd_stats_kernel<false>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+    else if (f16) hipLaunchKernelGGL(norm_bwd_stats_kernel<1>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, per_image, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
+    else hipLaunchKernelGGL(norm_bwd_stats_kernel<0>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
                        beta, mode, HW, C, per_image, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
   } else {
     // eval / none: only sum(g) and sum(g*xhat) are needed for the parameter grads
     dim3 grid(nblk, 1);
-    if (f16) hipLaunchKernelGGL(norm_bwd_stats_kernel<true>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+    if (f16 == 2) hipLaunchKernelGGL(norm_bwd_stats_kernel<2>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
                        beta, mode, HW, C, 0, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
-    else hipLaunchKernelGGL(norm_bwd_stats_kernel<false>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+    else if (f16) hipLaunchKernelGGL(norm_bwd_stats_kernel<1>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, 0, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
+    else hipLaunchKernelGGL(norm_bwd_stats_kernel<0>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
                        beta, mode, HW, C, 0, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
   }
   // the block-end ReLU ran in the statistics pass: the apply pass reads its result
@@ -733,19 +795,25 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
   // after the partials in `part`
   float* pg = part + (int64_t)groups * nblk * 3 * C;
   if (nblk > 64) {
-    if (f16) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, true>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+    if (f16 == 2) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, 2>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                        stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
-    else hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, false>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+    else if (f16) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, 1>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
+    else hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, 0>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                        stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
   } else {
-    if (f16) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<4, true>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+    if (f16 == 2) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<4, 2>), dim3(groups, (C + 63) / 64), dim3(256), 0,
                        stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
-    else hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<4, false>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+    else if (f16) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<4, 1>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
+    else hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<4, 0>), dim3(groups, (C + 63) / 64), dim3(256), 0,
                        stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
   }
   const int64_t nvec = (int64_t)N * HW * C / 8;
-  if (f16) hipLaunchKernelGGL(norm_bwd_apply_kernel<true>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
+  if (f16 == 2) hipLaunchKernelGGL(norm_bwd_apply_kernel<2>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
                      HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias);
-  else hipLaunchKernelGGL(norm_bwd_apply_kernel<false>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
+  else if (f16) hipLaunchKernelGGL(norm_bwd_apply_kernel<1>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
+                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias);
+  else hipLaunchKernelGGL(norm_bwd_apply_kernel<0>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
                      HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias);
 }

@@ -16,7 +16,10 @@ Reference: `core/extractor.py:6-56` (ResidualBlock), `:60-116` (BottleneckBlock)
 Used automatically by ``_Encoder.forward`` on the GPU under bf16 or fp16 autocast
 (``fast_path_ok``; the reference's ``--mixed_precision`` is fp16 autocast, `core/raft.py:99`):
 activations, weights and weight gradients are in the autocast dtype, statistics and accumulation
-in fp32.
+in fp32.  An fp32 model (the reference's default schedule) takes the same path in fp32 -- the
+stride-1 convs as split-bf16 MFMA convs (ops/conv_fp32.py), the strided ones on MIOpen fp32, the
+norm / ReLU / residual nodes on the fp32 instantiations of the same kernels -- instead of the
+eager NCHW modules (ATen instance norm on channels_last tensors, separate ReLU / add kernels).
 """
 import os
 
@@ -28,6 +31,8 @@ from . import _ext
 
 MODE_INSTANCE, MODE_BATCH_TRAIN, MODE_BATCH_EVAL, MODE_NONE = range(4)
 _DTYPES = (torch.bfloat16, torch.float16)
+# RAFT_FP32_ENC_FAST=0: an fp32 model's encoders run the eager modules (split convs per module)
+_FP32_FAST = os.environ.get('RAFT_FP32_ENC_FAST', '1') != '0'
 
 
 def _norm_mode(norm):
@@ -306,9 +311,10 @@ def _cast_maps(shapes, device, native=()):
 def cast_conv_weights(convs, dt=torch.bfloat16):
     """({conv: 16-bit channels_last weight}, {conv: packed adjoint weight}, {conv: packed forward
     weight with 64-aligned K slots, when Cin % 64 != 0}) for a list of nn.Conv2d, one batched cast
-    node; ``dt`` = bf16 or fp16."""
+    node; ``dt`` = bf16 or fp16 (fp32: channels_last fp32 weights only -- the split convs pack
+    their own operands)."""
     ws = [c.weight for c in convs]
-    native = tuple(j for j, c in enumerate(convs) if _native_geom(c))
+    native = () if dt == torch.float32 else tuple(j for j, c in enumerate(convs) if _native_geom(c))
     maps = _cast_maps([tuple(w.shape) for w in ws], ws[0].device, native)
     outs = _CastWeightsCL.apply(maps, dt, *ws)
     ext = outs[len(convs):]
@@ -366,10 +372,10 @@ class _Head1x1(torch.autograd.Function):
         return dx.permute(0, 3, 1, 2), dw.view(cout, cin, 1, 1), db
 
 
-def _head_ok(x, conv):
+def _head_ok(x, conv, dt=torch.bfloat16):
     return (conv.kernel_size == (1, 1) and conv.stride == (1, 1) and conv.bias is not None
             and conv.in_channels % 64 == 0 and conv.out_channels % 32 == 0 and x.is_cuda
-            and _HEAD_NATIVE)
+            and _HEAD_NATIVE and dt in _DTYPES)
 
 
 _HEAD_NATIVE = os.environ.get('RAFT_ENCODER_HEAD_NATIVE', '1') != '0'
@@ -514,7 +520,7 @@ def _conv(ps, x, conv, with_bias=False):
     sh, sw = conv.stride
     ho = (h + 2 * conv.padding[0] - conv.dilation[0] * (conv.kernel_size[0] - 1) - 1) // sh + 1
     wo = (w + 2 * conv.padding[1] - conv.dilation[1] * (conv.kernel_size[1] - 1) - 1) // sw + 1
-    per = max(x[0].numel(), conv.out_channels * ho * wo) * 2
+    per = max(x[0].numel(), conv.out_channels * ho * wo) * x.element_size()
     if n > 1 and n * per > _CONV_BYTES:
         k = max(1, _CONV_BYTES // per)
         parts = -(-n // k)
@@ -524,10 +530,26 @@ def _conv(ps, x, conv, with_bias=False):
     return _conv_one(ps, x, conv, with_bias)
 
 
+def _split_ok(x, conv):
+    """fp32 stride-1 'same' conv on the split-bf16 MFMA kernels (ops/conv_fp32.py)."""
+    from . import conv_fp32
+    k = conv.kernel_size
+    return (x.dtype == torch.float32 and conv.stride == (1, 1) and conv.dilation == (1, 1)
+            and conv.groups == 1 and conv.padding == (k[0] // 2, k[1] // 2)
+            and conv_fp32.fits(x, conv.out_channels))
+
+
 def _conv_one(ps, x, conv, with_bias=False):
     w = ps.weights.get(conv)
     if w is None:
         w = conv.weight.to(x.dtype).contiguous(memory_format=torch.channels_last)
+    if x.dtype == torch.float32:
+        # fp32 schedule: split-bf16 MFMA for the stride-1 convs, MIOpen fp32 for the strided ones
+        b = conv.bias if (with_bias and conv.bias is not None) else None
+        if _split_ok(x, conv):
+            from . import conv_fp32
+            return conv_fp32.conv2d(x, w, b, conv.padding)
+        return F.conv2d(x, w, b, conv.stride, conv.padding, conv.dilation, conv.groups)
     if not with_bias and _conv_native_ok(x, conv) and w.is_contiguous(memory_format=torch.channels_last):
         if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
             return _Conv3x3Native.apply(x, w, ps.adjoint.get(conv), ps.fwdpack.get(conv))
@@ -605,9 +627,15 @@ def fast_path_ok(enc, x):
         return False
     if not (isinstance(x, torch.Tensor) and x.is_cuda and _ext.device_ok(x)):
         return False
-    if not (torch.is_autocast_enabled('cuda') and
-            torch.get_autocast_dtype('cuda') in _DTYPES):
-        return False
+    if torch.is_autocast_enabled('cuda'):
+        if torch.get_autocast_dtype('cuda') not in _DTYPES:
+            return False
+    else:
+        # fp32 model: inside the encoders' split-conv scope (RAFT.encode, conv_fp32.enabled)
+        from . import conv_fp32
+        if not (_FP32_FAST and x.dtype == torch.float32 and conv_fp32._ACTIVE['on']
+                and conv_fp32._ENV_ON):
+            return False
     if enc.training and enc.dropout is not None:
         return False
     if not _ext.gpu_path_enabled(required=False):
@@ -634,11 +662,11 @@ class _Pass:
 
 def encoder_forward(enc, x):
     """`core/extractor.py:168-192` (both encoders): returns channels_last features in the
-    autocast dtype (bf16 / fp16)."""
-    dt = torch.get_autocast_dtype('cuda')
+    autocast dtype (bf16 / fp16), or fp32 for an fp32 model."""
+    dt = torch.get_autocast_dtype('cuda') if torch.is_autocast_enabled('cuda') else torch.float32
     with torch.autocast('cuda', enabled=False):
         convs = [m for m in enc.modules() if isinstance(m, nn.Conv2d)]
-        if _head_ok(x, enc.conv2):
+        if _head_ok(x, enc.conv2, dt):
             convs = [c for c in convs if c is not enc.conv2]  # runs on _Head1x1 (fp32 weight)
         counters = [m.num_batches_tracked for m in enc.modules()
                     if isinstance(m, nn.BatchNorm2d) and _norm_mode(m) == MODE_BATCH_TRAIN
@@ -657,7 +685,7 @@ def _encoder_body(ps, enc, x, dt=torch.bfloat16):
     for layer in (enc.layer1, enc.layer2, enc.layer3):
         for blk in layer:
             x = block_fn(ps, blk, x)
-    if _head_ok(x, enc.conv2):
+    if _head_ok(x, enc.conv2, dt):
         return _Head1x1.apply(x, enc.conv2.weight, enc.conv2.bias)
     x = _conv(ps, x, enc.conv2, with_bias=True)
     return x

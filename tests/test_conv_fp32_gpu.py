@@ -104,9 +104,12 @@ def test_fp32_model_update_block_split_vs_miopen(ext_ops):
                                            if p.grad is not None})
     (fa, ga), (fb, gb) = outs['auto'], outs['torch']
     assert _rel(fa, fb) < 1e-3
+    # one ReLU pre-activation within the split scheme's ~2^-16 of zero flips its mask and moves a
+    # 16 x 20-cell decode's upstream gradients by ~1e-2; the kernels' precision itself is pinned
+    # with shared masks by test_fp32_fused_gpu.py::test_fp32_fused_update_iteration_vs_fp64 (1e-4)
     for n in gb:
         if n.startswith('update_block'):
-            assert _rel(ga[n], gb[n]) < 2e-3, n
+            assert _rel(ga[n], gb[n]) < 2e-2, n
 
 
 def test_fp32_training_trajectory_split_vs_miopen(ext_ops):

@@ -177,3 +177,58 @@ def test_native_conv_3x3_matches_conv2d(ext_ops, cin, cout, hw, packed, dt):
     with torch.no_grad():
         y2 = fast._conv3x3_native_fwd(x.detach(), w.detach(), wf)
     assert torch.equal(y2, y.detach())
+
+
+@pytest.mark.parametrize('cls,norm,train', [
+    (BasicEncoder, 'instance', True), (BasicEncoder, 'batch', True), (BasicEncoder, 'batch', False),
+    (SmallEncoder, 'instance', True)])
+def test_fast_encoder_fp32_matches_eager_split(ext_ops, cls, norm, train):
+    """fp32 model (no autocast) inside the split-conv scope: the channels-last fast path (fp32
+    norm kernels, split-bf16 stride-1 convs, MIOpen fp32 strided convs) gives the eager module
+    path's outputs, parameter gradients and BatchNorm running statistics (same split convs,
+    ATen norms) to fp32 rounding."""
+    from pytorch_raft_amd.ops import conv_fp32
+    torch.manual_seed(0)
+    enc = cls(output_dim=256 if cls is BasicEncoder else 128, norm_fn=norm).to(DEV)
+    for m in enc.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+            m.running_mean.uniform_(-0.1, 0.1)
+            m.running_var.uniform_(0.8, 1.2)
+        if isinstance(m, torch.nn.Conv2d):
+            m.bias.data.uniform_(-0.1, 0.1)
+    enc.train(train)
+    x = torch.randn(4, 3, 96, 128, device=DEV)
+    state = {k: v.clone() for k, v in enc.state_dict().items()}
+    outs, grads, bufs = {}, {}, {}
+    for path in ('eager', 'fast'):
+        enc.load_state_dict(state)
+        enc.zero_grad(set_to_none=True)
+        orig = fast.fast_path_ok
+        if path == 'eager':
+            fast.fast_path_ok = lambda *a: False
+        try:
+            with conv_fp32.enabled():
+                if path == 'fast':
+                    assert fast.fast_path_ok(enc, x)
+                y = enc(x)
+        finally:
+            fast.fast_path_ok = orig
+        assert y.dtype == torch.float32
+        (y * torch.linspace(-1, 1, y.numel(), device=DEV).view(y.shape)).sum().backward()
+        outs[path] = y.detach()
+        grads[path] = {n: p.grad.clone() for n, p in enc.named_parameters() if p.grad is not None}
+        bufs[path] = {k: v.clone() for k, v in enc.state_dict().items() if 'running' in k}
+    rel = ((outs['fast'] - outs['eager']).norm() / outs['eager'].norm()).item()
+    assert rel < 1e-4, rel
+    for n, g in grads['eager'].items():
+        normed_bias = n != 'conv2.bias' and n.endswith(('conv1.bias', 'conv2.bias', 'conv3.bias',
+                                                         'downsample.0.bias'))
+        if normed_bias and norm != 'none' and not (norm == 'batch' and not train):
+            continue   # ~0 in exact arithmetic (the bias cancels in a batch-statistics norm)
+        # the two paths round differently near ReLU kinks (norm statistics summed in another
+        # order, conv bias folded into the norm): gradients agree to ~1e-4 in direction
+        assert _cos(grads['fast'][n], g) > 0.999, (n, _cos(grads['fast'][n], g))
+    for k, v in bufs['eager'].items():
+        torch.testing.assert_close(bufs['fast'][k], v, atol=1e-5, rtol=1e-4)

