@@ -185,11 +185,10 @@ __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_t
   const int b_col = wn * 32 + (gi & 1) * 16 + 4 * pp;   // Cin column of its B reads
 
   // split-fp32 items (binding): only the leading db_items items' G columns enter the bias sum
-  bool bias_now = bias_wave;
-  auto set_bias = [&](int c) {
-    bias_now = bias_wave && (ta.db_items == 0 || c / ta.chunks_per_item < ta.db_items);
-  };
-  auto compute = [&](int buf) {
+  // (chunks are item-major: a chunk index bound, no division)
+  const int db_end = ta.db_items > 0 ? ta.db_items * ta.chunks_per_item : 0x7fffffff;
+  auto compute = [&](int buf, int cidx) {
+    const bool bias_now = bias_wave && cidx < db_end;
     const uint8_t* Gs = smem + buf * Geo::STAGE;
     const uint8_t* Xs = Gs + Geo::G_BYTES;
 #pragma unroll
@@ -238,8 +237,7 @@ __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_t
           raft_wait_vmcnt<0>();
         }
         __builtin_amdgcn_s_barrier();
-        set_bias(c_begin + t);
-        compute(t & 1);
+        compute(t & 1, c_begin + t);
         __builtin_amdgcn_s_barrier();
       }
     }
@@ -262,8 +260,7 @@ __global__ __launch_bounds__((TapGeo<KH, KW, TG, BMT>::NT), 1) void conv_wgrad_t
         nb = nb >= NS ? nb - NS : nb;
         issue(c_begin + t + NS - 1, nb);
       }
-      set_bias(c_begin + t);
-      compute(cur);
+      compute(cur, c_begin + t);
       cur = cur + 1 == NS ? 0 : cur + 1;
     }
   }
