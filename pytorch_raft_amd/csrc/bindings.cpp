@@ -1700,7 +1700,11 @@ const uint32_t* fh2_pairs(const Tensor& t, int64_t n, const char* name, at::Scal
 }
 
 // out (B,2,H,W) fp32 = conv3x3(in[..., 0:256]) + bias
-void fh2_fwd_(const Tensor& in, const Tensor& wf, const Tensor& b, const Tensor& out) {
+// coords (optional): cnew = coords + out, fnew = cnew - coords_grid (the iteration's coordinate
+// update, `core/raft.py:134-135`, in the same launch)
+void fh2_fwd_(const Tensor& in, const Tensor& wf, const Tensor& b, const Tensor& out,
+              const c10::optional<Tensor>& coords, const c10::optional<Tensor>& cnew,
+              const c10::optional<Tensor>& fnew) {
   TORCH_CHECK(in.dim() == 4, "in must be (B,H,W,C)");
   const int64_t B = in.size(0), H = in.size(1), W = in.size(2), cs = in.size(3);
   const at::ScalarType st = op16(in);
@@ -1711,9 +1715,20 @@ void fh2_fwd_(const Tensor& in, const Tensor& wf, const Tensor& b, const Tensor&
   check_cuda_f32(out, "fh2 out");
   TORCH_CHECK(out.dim() == 4 && out.size(0) == B && out.size(1) == 2 && out.size(2) == H &&
               out.size(3) == W, "fh2 out must be (B,2,H,W)");
+  const bool upd = coords.has_value() && coords->defined();
+  if (upd) {
+    TORCH_CHECK(cnew.has_value() && fnew.has_value(), "fh2_fwd: coords needs cnew and fnew");
+    for (const Tensor* t : {&*coords, &*cnew, &*fnew}) {
+      check_cuda_f32(*t, "fh2 coords");
+      TORCH_CHECK(t->sizes() == out.sizes() && t->is_contiguous(), "fh2 coords must be (B,2,H,W)");
+    }
+  }
   c10::DeviceGuard gd(in.device());
   TORCH_CHECK(launch_fh2_fwd(u16(in), (int)cs, wp, b.data_ptr<float>(), out.data_ptr<float>(),
-                             (int)B, (int)H, (int)W, st == at::kHalf, cur_stream()),
+                             (int)B, (int)H, (int)W, st == at::kHalf, cur_stream(),
+                             upd ? coords->data_ptr<float>() : nullptr,
+                             upd ? cnew->data_ptr<float>() : nullptr,
+                             upd ? fnew->data_ptr<float>() : nullptr),
               "fh2_fwd: input needs >= 256 channels, a multiple of 8");
 }
 
@@ -1838,7 +1853,8 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("adamw_step_(Tensor(a!)[] params, Tensor(b!)[] grads, Tensor(c!)[] exp_avg, Tensor(d!)[] exp_avg_sq, Tensor(e!)[] steps, int[] group_of, Tensor[] lr_t, float[] lr, float[] beta1, float[] beta2, float[] eps, float[] wd, float max_norm, Tensor? inv_scale=None, Tensor(f!)? found_inf=None, bool write_grad=False) -> Tensor");
   m.def("corr_tap_reduce(Tensor[] coords, Tensor[] douts, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16, int pitch_mult=0, bool split=False) -> Tensor");
   m.def("corr_bwd_fmaps(Tensor dc, Tensor f1, Tensor f2) -> Tensor[]");
-  m.def("fh2_fwd_(Tensor inp, Tensor wf, Tensor b, Tensor(a!) out) -> ()");
+  m.def("fh2_fwd_(Tensor inp, Tensor wf, Tensor b, Tensor(a!) out, Tensor? coords=None, "
+        "Tensor(b!)? cnew=None, Tensor(c!)? fnew=None) -> ()");
   m.def("fh2_dgrad_(Tensor gout, Tensor wd, Tensor fm, Tensor(a!) dx) -> ()");
   m.def("fh2_wgrad_(Tensor[] gouts, Tensor[] ins, Tensor(a!) part) -> ()");
   m.def("conv_wgrad_(Tensor g, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, int cin_small, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");

@@ -464,23 +464,45 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
     }
   };
   if (pl < lanes) {
-    // 4 pixels (8 loads) in flight per round (see norm_stats_kernel)
     int p = p0 + pl;
-    for (; p + 7 * lanes < p1; p += 8 * lanes) {
+    if (yres != nullptr) {
+      // block-end ReLU: 4 pixels' dy, x, yres [, dy2] loads in flight per round, all issued
+      // before any math (8 pixels x 4 streams would hold ~190 VGPRs: 2 waves per SIMD)
+      for (; p + 3 * lanes < p1; p += 4 * lanes) {
+        V8<TY> rd[4], rx[4], ry[4], r2[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t off = (base + p + u * lanes) * C + g * 8;
+          rd[u] = ld8<TY>(dy, off);
+          rx[u] = ld8<TY>(x, off);
+          ry[u] = ld8<TY>(yres, off);
+          if (dy2 != nullptr) r2[u] = ld8<TY>(dy2, off);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t off = (base + p + u * lanes) * C + g * 8;
+          if (dy2 != nullptr) {
+            float a[8], b[8];
+            unpack8<TY>(rd[u], a);
+            unpack8<TY>(r2[u], b);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a[i] += b[i];
+            rd[u] = pack8<TY>(a);
+          }
+          rd[u] = mask_pos<TY>(rd[u], ry[u]);
+          st8<TY>(gout, off, rd[u]);
+          accum(rd[u], rx[u]);
+        }
+      }
+    }
+    // 8 pixels (16 loads) in flight per round (see norm_stats_kernel)
+    for (; yres == nullptr && p + 7 * lanes < p1; p += 8 * lanes) {
       V8<TY> rd[8], rx[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int64_t off = (base + p + u * lanes) * C + g * 8;
         rd[u] = ld8<TY>(dy, off);
         rx[u] = ld8<TY>(x, off);
-      }
-      if (yres != nullptr) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int64_t off = (base + p + u * lanes) * C + g * 8;
-          rd[u] = block_end_grad<TY>(rd[u], dy2, off, ld8<TY>(yres, off));
-          st8<TY>(gout, off, rd[u]);
-        }
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) accum(rd[u], rx[u]);

@@ -65,7 +65,9 @@ __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict
                                                       const uint32_t* __restrict__ wf,
                                                       const float* __restrict__ bias,
                                                       float* __restrict__ out, int B, int H,
-                                                      int W) {
+                                                      int W, const float* __restrict__ coords,
+                                                      float* __restrict__ cnew,
+                                                      float* __restrict__ fnew) {
   const int g = threadIdx.x & 31;
   const int64_t hw = (int64_t)H * W, P = (int64_t)B * hw;
   uint4 w0[9], w1[9];
@@ -113,8 +115,19 @@ __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict
     const int64_t p = ((int64_t)blockIdx.x * NPIX + k) * 8 + (threadIdx.x >> 5);
     if (g == 0 && p < P) {
       const int64_t b = p / hw, yx = p - b * hw;
-      out[b * 2 * hw + yx] = s0 + bias[0];
-      out[b * 2 * hw + hw + yx] = s1 + bias[1];
+      const float d0 = s0 + bias[0], d1 = s1 + bias[1];
+      out[b * 2 * hw + yx] = d0;
+      out[b * 2 * hw + hw + yx] = d1;
+      if (coords) {
+        // coords1 + delta and (coords1 + delta) - coords0 of `core/raft.py:134-135`, with
+        // coords0 = (x, y) the pixel grid: the same two fp32 roundings as the eager ops
+        const int y = (int)(yx / W), x = (int)(yx - (int64_t)y * W);
+        const float c0 = coords[b * 2 * hw + yx] + d0, c1 = coords[b * 2 * hw + hw + yx] + d1;
+        cnew[b * 2 * hw + yx] = c0;
+        cnew[b * 2 * hw + hw + yx] = c1;
+        fnew[b * 2 * hw + yx] = c0 - (float)x;
+        fnew[b * 2 * hw + hw + yx] = c1 - (float)y;
+      }
     }
   }
 }
@@ -379,15 +392,16 @@ __global__ __launch_bounds__(256) void fh2_wgrad_kernel(Fh2Items it, int cs, int
 }  // namespace
 
 bool launch_fh2_fwd(const uint16_t* in, int cs, const uint32_t* wf, const float* bias, float* out,
-                    int B, int H, int W, int f16, hipStream_t stream) {
+                    int B, int H, int W, int f16, hipStream_t stream, const float* coords,
+                    float* cnew, float* fnew) {
   if (cs % 8 != 0 || cs < FH_C) return false;
   const int64_t P = (int64_t)B * H * W;
   if (f16)
     hipLaunchKernelGGL((fh2_fwd_kernel<2, true>), dim3(raft_cdiv(P, 16)), dim3(256), 0, stream, in, cs, wf,
-                       bias, out, B, H, W);
+                       bias, out, B, H, W, coords, cnew, fnew);
   else
     hipLaunchKernelGGL((fh2_fwd_kernel<2, false>), dim3(raft_cdiv(P, 16)), dim3(256), 0, stream, in, cs, wf,
-                       bias, out, B, H, W);
+                       bias, out, B, H, W, coords, cnew, fnew);
   return true;
 }
 

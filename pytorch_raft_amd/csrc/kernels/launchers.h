@@ -297,8 +297,10 @@ struct Fh2Items {
 };
 // wf: bf16 pairs [t][o][c/2] (9*2*128 uint32); wd: bf16 pairs (W0[c], W1[c]) [t][c] (9*256 uint32)
 // f16: fp16 activations / weight pairs (v_dot2_f32_f16) instead of bf16
+// coords (optional, (B,2,H,W) fp32): also writes cnew = coords + out and fnew = cnew - (x, y)
 bool launch_fh2_fwd(const uint16_t* in, int cs, const uint32_t* wf, const float* bias, float* out,
-                    int B, int H, int W, int f16, hipStream_t stream);
+                    int B, int H, int W, int f16, hipStream_t stream, const float* coords = nullptr,
+                    float* cnew = nullptr, float* fnew = nullptr);
 bool launch_fh2_dgrad(const float* gout, const uint32_t* wd, const uint16_t* fm, int fs, uint16_t* dx,
                       int ds, int B, int H, int W, int f16, hipStream_t stream);
 // part: (blocks, 2*2304 + 2) fp32 per-workgroup partial [dw | db] rows (fully written)

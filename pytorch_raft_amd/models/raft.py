@@ -20,9 +20,9 @@ MI355X-specific extensions (all optional ``args`` attributes, defaults chosen fo
                   used while it fits in ``RAFT_CORR_BUDGET_GB`` (default: a quarter of the GPU's
                   HBM, 72 GB on MI355X), the O(HW) on-the-fly correlation beyond that.  Both give
                   the same values; all-pairs is the faster of the two at every batch that fits
-                  (profiles/r2/sweep measured the gap when it was last swept: training and
-                  Sintel inference both a few percent faster on all-pairs), on-the-fly is what
-                  makes batch-1024 Sintel inference or 4K frames fit.
+                  (training, bf16, per-GPU batch 12: on-the-fly runs at 0.90x all-pairs at
+                  both the chairs and the KITTI 288x960 shapes, profiles/r4/cfg/),
+                  on-the-fly is what makes batch-1024 Sintel inference or 4K frames fit.
 
 In test mode the convex upsampling runs only after the last iteration (the reference computes and
 discards it every iteration, `core/raft.py:133-142`); outputs are identical.
@@ -307,9 +307,9 @@ class RAFT(nn.Module):
             # input, detached (same values; one subtraction kernel per iteration instead of two)
             flow = flow.detach()
             last = itr == iters - 1
-            h, delta_flow, up_mask = hub(h, x, corr, flow, need_mask=last or not test_mode)
-            coords1 = coords1 + delta_flow
-            flow = coords1 - coords0
+            # coords1 + delta and the new flow come out of the flow-head kernel (no add kernels)
+            h, _, up_mask, coords1, flow = hub(h, x, corr, flow, need_mask=last or not test_mode,
+                                               coords=coords1)
             if test_mode and itr < iters - 1:
                 continue
             flow_up = convex_upsample(flow, up_mask, nhwc=True)

@@ -33,6 +33,7 @@ import torch
 
 from . import _ext
 from . import conv as C
+from ..utils.utils import coords_grid
 
 HD = 128  # hidden / context width of the full model
 CORR_BUF = 384  # lookup taps (4 x 81 = 324) zero-padded to a multiple of the conv K step (64)
@@ -682,11 +683,14 @@ def _sum_bf16(gs, spl=False):
     return out
 
 
-def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
-    """Forward of one fused iteration; returns (h2, delta, mask, saved tensors).
+def _iter_forward(pk, h, inp, corr, flow, need_mask=True, coords=None):
+    """Forward of one fused iteration; returns (h2, delta, mask, saved tensors, upd).
 
     ``need_mask=False`` (inference iterations whose flow is not upsampled) computes only the
-    flow-head half of the fused head conv and skips the mask conv: ~20 % of the iteration."""
+    flow-head half of the fused head conv and skips the mask conv: ~20 % of the iteration.
+    ``coords`` (the iteration's detached coords1, (B,2,H,W) fp32): ``upd`` = (coords1 + delta,
+    coords1 + delta - coords0) of `core/raft.py:134-135`, written by the flow-head kernel (two
+    fewer launches per iteration); None without coords."""
     B, H, W, _ = h.shape
     dev = h.device
     dt = pk.dtype  # operand dtype: bf16, fp16 autocast, or fp32 (split bf16 pair buffers)
@@ -732,9 +736,21 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
         hin = hn
     h2 = hin
     delta = torch.empty(B, 2, H, W, device=dev, dtype=torch.float32)
+    upd = None
+
     def fh2(fm):
+        nonlocal upd
         if spl:  # split fp32: the MFMA conv kernel (NCHW fp32 epilogue), not the VALU one
             conv('fh2', [(fm, 0, 256)], C.EPI_F32_NCHW, [delta], [0])
+            if coords is not None:
+                cn = coords + delta
+                g0 = getattr(pk, 'grid0', None)
+                if g0 is None or g0.shape != cn.shape:
+                    g0 = pk.grid0 = coords_grid(B, H, W, device=dev)
+                upd = (cn, cn - g0)
+        elif coords is not None:
+            upd = (torch.empty_like(delta), torch.empty_like(delta))
+            ops.fh2_fwd_(fm, pk.fh2_wf, pk.b32, delta, coords.contiguous(), upd[0], upd[1])
         else:
             ops.fh2_fwd_(fm, pk.fh2_wf, pk.b32, delta)
 
@@ -756,17 +772,18 @@ def _iter_forward(pk, h, inp, corr, flow, need_mask=True):
         fh2(fm)
         mask = None
     g1, g2 = gates['1'], gates['2']
-    return h2, delta, mask, (corr, patch, c1, cf, f1, mf, inp, *g1, *g2, h2, fm)
+    return h2, delta, mask, (corr, patch, c1, cf, f1, mf, inp, *g1, *g2, h2, fm), upd
 
 
 class _UpdateIter(torch.autograd.Function):
     """One GRU iteration.  Inputs: token, h (B,H,W,128) bf16, inp (B,H,W,128) bf16,
     corr (B,H,W,CORR_BUF) bf16, flow (B,2,H,W) fp32.  Outputs: h', delta (B,2,H,W) fp32,
-    mask (B,H,W,576) bf16 (already x0.25)."""
+    mask (B,H,W,576) bf16 (already x0.25); with ``coords`` also coords1 + delta and the new
+    flow (see ``_iter_forward``), whose gradients are the delta's."""
 
     @staticmethod
-    def forward(ctx, token, h, inp, corr, flow, state):
-        h2, delta, mask, saved = _iter_forward(state.packed, h, inp, corr, flow)
+    def forward(ctx, token, h, inp, corr, flow, state, coords=None):
+        h2, delta, mask, saved, upd = _iter_forward(state.packed, h, inp, corr, flow, coords=coords)
         ctx.state = state
         ctx.itr = state.n_iter
         state.n_iter += 1
@@ -774,10 +791,14 @@ class _UpdateIter(torch.autograd.Function):
         # an output nobody differentiates arrives as None, not as a zero-filled tensor (the
         # recurrent state's gradient comes through state.dh_carry, see backward)
         ctx.set_materialize_grads(False)
-        return h2, delta, mask
+        cnew, fnew = upd if upd is not None else (None, None)
+        return h2, delta, mask, cnew, fnew
 
     @staticmethod
-    def backward(ctx, gh, gdelta, gmask):
+    def backward(ctx, gh, gdelta, gmask, gcoords=None, gflow=None):
+        for g in (gcoords, gflow):   # d(coords1 + delta) / d delta = d(flow) / d delta = 1
+            if g is not None:
+                gdelta = g if gdelta is None else gdelta + g
         st = ctx.state
         # the shared context gradient is accumulated across the iterations' backwards in one
         # buffer (see below), which needs them strictly in reverse order n-1 .. 0
@@ -974,13 +995,13 @@ class _UpdateIter(torch.autograd.Function):
                 st.zero_h = torch.zeros((), device=dev, dtype=h0.dtype)
             if spl and dinp is not None:
                 dinp = _to_split(dinp.permute(0, 3, 1, 2))
-            return (None, st.zero_h.expand(B, H, W, h0.shape[-1]), dinp, dcorr, None, None)
+            return (None, st.zero_h.expand(B, H, W, h0.shape[-1]), dinp, dcorr, None, None, None)
         if spl:
             # split fp32 inputs take split-encoded gradients (same shape and dtype as h / inp)
             dh = _to_split(dh.permute(0, 3, 1, 2))
             if dinp is not None:
                 dinp = _to_split(dinp.permute(0, 3, 1, 2))
-        return (None, dh, dinp, dcorr, None, None)
+        return (None, dh, dinp, dcorr, None, None, None)
 
 
 class HipUpdateBlock:
@@ -996,13 +1017,16 @@ class HipUpdateBlock:
         self.state.overlap = _OVERLAP
         self.token = _UpdateWeights.apply(self.state, *params)
 
-    def __call__(self, h, inp, corr, flow, need_mask=True):
-        """-> (h', delta, mask).  Without gradients (inference) the iteration runs outside
-        autograd and ``need_mask=False`` skips the mask head (mask is then None)."""
+    def __call__(self, h, inp, corr, flow, need_mask=True, coords=None):
+        """-> (h', delta, mask), or with ``coords`` (the detached coords1) (h', delta, mask,
+        coords1 + delta, coords1 + delta - coords0).  Without gradients (inference) the iteration
+        runs outside autograd and ``need_mask=False`` skips the mask head (mask is then None)."""
         if not self.state.need_grad and not torch.is_grad_enabled():
-            h2, delta, mask, _ = _iter_forward(self.state.packed, h, inp, corr, flow, need_mask)
-            return h2, delta, mask
-        return _UpdateIter.apply(self.token, h, inp, corr, flow, self.state)
+            h2, delta, mask, _, upd = _iter_forward(self.state.packed, h, inp, corr, flow,
+                                                    need_mask, coords)
+            return (h2, delta, mask) + (upd if coords is not None else ())
+        out = _UpdateIter.apply(self.token, h, inp, corr, flow, self.state, coords)
+        return out if coords is not None else out[:3]
 
 
 def available(required=False):

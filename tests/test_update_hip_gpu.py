@@ -24,6 +24,13 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
 
 
+def _slope(a, ref):
+    """Least-squares gain of a on ref: bf16 rounding noise averages out of it, a systematic
+    scale error (a mis-scaled gate, a dropped bias) does not."""
+    a, ref = a.reshape(-1).double(), ref.reshape(-1).double()
+    return (a @ ref / (ref @ ref + 1e-30)).item()
+
+
 def test_fused_forward_matches_eager(ext_ops):
     i1, i2, _, _ = make_pair_batch(2, 128, 160, device=DEV)
     ref = _model('torch', mixed=False).eval()   # fp32 eager reference
@@ -36,6 +43,10 @@ def test_fused_forward_matches_eager(ext_ops):
     scale = lr.abs().max().item()
     assert err < 0.05 * max(scale, 1.0), (err, scale)
     assert _cos(uh, ur) > 0.995
+    # no systematic error: the gain of the fused flow on the fp32 one is 1 to well under 1 %
+    k, kl = _slope(uh, ur), _slope(lh, lr)
+    print('flow gain %.5f, low-res %.5f' % (k, kl))
+    assert abs(k - 1) < 5e-3 and abs(kl - 1) < 5e-3, (k, kl)
 
 
 def test_fused_training_grads_match_eager(ext_ops):
@@ -55,8 +66,12 @@ def test_fused_training_grads_match_eager(ext_ops):
         if not n.startswith('update_block'):
             continue
         c = _cos(grads['hip'][n], g)
-        if c < 0.98:
-            bad.append((n, c))
+        k = _slope(grads['hip'][n], g)
+        if c < 0.98 or abs(k - 1) > 3e-2:
+            bad.append((n, c, k))
+    print('loss', losses, 'worst gains', sorted((abs(_slope(grads['hip'][n], g) - 1), n)
+                                                 for n, g in grads['torch'].items()
+                                                 if n.startswith('update_block'))[-3:])
     assert not bad, bad
     # encoder grads flow back through corr / net / inp
     # (bf16 encoder activations: the stem's gradient sits ~0.95 cos from fp32 under eager bf16
@@ -98,6 +113,14 @@ def test_flow_head2_kernels_match_fp32(ext_ops, cs, shape):
     ref = F.conv2d(x, w, b, padding=1)
     # bf16 weights (v_dot2_f32_bf16), fp32 accumulation: ~0.2 % relative per product
     torch.testing.assert_close(out, ref, atol=3e-2, rtol=1e-2)
+    # the iteration's coordinate update in the same launch: bitwise the eager fp32 ops
+    from pytorch_raft_amd.utils.utils import coords_grid
+    c0 = coords_grid(B, H, W, device=DEV)
+    c1 = c0 + torch.randn(B, 2, H, W, device=DEV, generator=g) * 20
+    out2, cn, fn = (torch.empty_like(out) for _ in range(3))
+    ext_ops.fh2_fwd_(fm, wf, b, out2, c1, cn, fn)
+    assert torch.equal(out2, out)
+    assert torch.equal(cn, c1 + out) and torch.equal(fn, (c1 + out) - c0)
     # input gradient, gated by fm > 0, written into channels 0..255 of a cs-wide buffer
     gout = torch.randn(B, 2, H, W, device=DEV, generator=g)
     dx = torch.full((B, H, W, cs), 7.0, device=DEV, dtype=torch.bfloat16)
