@@ -1012,7 +1012,14 @@ void conv_wgrad_taps_(const std::vector<Tensor>& gs, int64_t g_off, const std::v
     // costs a cout x kpad fp32 partial written and re-read
     const int64_t per_cu = kh * kw == 9 ? (ta.bm == 64 ? 2 : 1) : (kh * kw == 5 ? 2 : 3);
     const int64_t pairs = (int64_t)ta.n_co * ta.n_ci;
-    splits = std::max<int64_t>(1, std::min<int64_t>(256 * per_cu / pairs, ta.total_chunks / 8));
+    // RAFT_WG_SPLIT_PCT: percentage of that split count (A/B measurements of partial traffic
+    // against occupancy; default 100)
+    static const int64_t pct = [] {
+      const char* e = getenv("RAFT_WG_SPLIT_PCT");
+      return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)100;
+    }();
+    splits = std::max<int64_t>(1, std::min<int64_t>(256 * per_cu * pct / (100 * pairs),
+                                                    ta.total_chunks / 8));
   }
   ta.chunks_per_split = (int)((ta.total_chunks + splits - 1) / splits);
   ta.splits = (int)((ta.total_chunks + ta.chunks_per_split - 1) / ta.chunks_per_split);
@@ -1353,6 +1360,37 @@ void add_relu_(const Tensor& a, const Tensor& b, const Tensor& out) {
   launch_add_relu(u16(a),
                   u16(b),
                   u16m(out), a.numel(), norm_ty(st), cur_stream());
+}
+
+// out[i] = cast(srcs[k][off]) for idx[i] = k << 26 | off (k = 63: zero); srcs contiguous GPU
+// tensors of one dtype and device, out 1-D with idx.numel() elements: fp32 sources -> bf16 /
+// fp16 / fp32 out, or bf16 / fp16 sources -> fp32 out
+void gather_cast_(const std::vector<Tensor>& srcs, const Tensor& idx, const Tensor& out) {
+  TORCH_CHECK(!srcs.empty() && (int64_t)srcs.size() <= RAFT_GATHER_MAX, "gather: 1..",
+              RAFT_GATHER_MAX, " sources");
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kInt && idx.is_contiguous() && idx.dim() == 1,
+              "gather: idx must be a contiguous 1-D int32 GPU tensor");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.numel() == idx.numel(),
+              "gather: out must be contiguous with idx.numel() elements");
+  const at::ScalarType ot = out.scalar_type();
+  TORCH_CHECK(ot == at::kBFloat16 || ot == at::kHalf || ot == at::kFloat, "gather: out dtype");
+  const at::ScalarType it = srcs[0].scalar_type();
+  TORCH_CHECK(it == at::kBFloat16 || it == at::kHalf || it == at::kFloat, "gather: source dtype");
+  TORCH_CHECK(it == at::kFloat || ot == at::kFloat, "gather: 16-bit sources need an fp32 output");
+  GatherSrcs gs{};
+  gs.n = (int)srcs.size();
+  for (int k = 0; k < gs.n; ++k) {
+    TORCH_CHECK(srcs[k].is_cuda() && srcs[k].scalar_type() == it && srcs[k].is_contiguous() &&
+                srcs[k].device() == idx.device() && srcs[k].numel() <= (1 << 26),
+                "gather: sources must be contiguous GPU tensors of one dtype and device");
+    gs.p[k] = srcs[k].data_ptr();
+  }
+  TORCH_CHECK(out.device() == idx.device(), "gather: devices");
+  auto ty = [](at::ScalarType t) { return t == at::kBFloat16 ? 0 : (t == at::kHalf ? 1 : 2); };
+  c10::DeviceGuard gd(idx.device());
+  TORCH_CHECK(launch_gather_cast(gs, idx.data_ptr<int32_t>(), out.data_ptr(), idx.numel(), ty(it),
+                                 ty(ot), cur_stream()),
+              "gather launch");
 }
 
 void relu_mask_(const Tensor& dy, const Tensor& y, const Tensor& g, const c10::optional<Tensor>& dy2) {
@@ -1826,6 +1864,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx, Tensor? dy2=None, Tensor? yres=None, Tensor(e!)? gout=None) -> ()");
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
+  m.def("gather_cast_(Tensor[] srcs, Tensor idx, Tensor(a!) out) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] douts, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("corr_build_bf16(Tensor f1, Tensor f2, int levels, bool pyr_bf16=False) -> Tensor[]");
   m.def("conv_wgrad_taps_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, "
@@ -1879,6 +1918,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("fh2_wgrad_", &fh2_wgrad_);
   m.impl("add_relu_", &add_relu_);
   m.impl("relu_mask_", &relu_mask_);
+  m.impl("gather_cast_", &gather_cast_);
   m.impl("corr_build_bf16", &corr_build_bf16);
   m.impl("conv_wgrad_taps_", &conv_wgrad_taps_);
   m.impl("convex_up_fwd", &convex_up_fwd);

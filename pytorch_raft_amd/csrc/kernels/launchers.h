@@ -403,3 +403,15 @@ int adam_chunk_elems();
 void launch_adamw_multi(const AdamTensor* tab, const int* cum, int T, int nchunks, const AdamGroup* groups,
                         float max_norm, const float* inv_scale, int need_norm, int write_grad,
                         float* part, float* coef, float* found_inf, hipStream_t stream);
+
+// ---- gather.hip: multi-source gather + cast (per-step weight packing)
+#define RAFT_GATHER_MAX 62   // sources per launch (index field 63 = the zero padding slot)
+#define RAFT_GATHER_ZERO 63
+struct GatherSrcs {
+  const void* p[RAFT_GATHER_MAX];
+  int n;
+};
+// out[i] = cast(p[idx[i] >> 26][idx[i] & (2^26 - 1)]), 0 for the zero slot; it / ot (source /
+// output type): 0 bf16, 1 fp16, 2 fp32 -- fp32 -> any, or bf16 / fp16 -> fp32
+bool launch_gather_cast(const GatherSrcs& s, const int32_t* idx, void* out, int64_t n, int it, int ot,
+                        hipStream_t stream);

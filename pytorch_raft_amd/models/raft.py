@@ -181,9 +181,8 @@ class RAFT(nn.Module):
         dev = fmap1.device
         b, _, h8, w8 = fmap1.shape
         coords0 = coords_grid(b, h8, w8, device=dev)
-        coords1 = coords_grid(b, h8, w8, device=dev)
-        if flow_init is not None:
-            coords1 = coords1 + flow_init
+        # the same grid: coords1 is only ever rebound (coords1 + delta), never written in place
+        coords1 = coords0 if flow_init is None else coords0 + flow_init
 
         if self._use_fused_update(fmap1):
             return self._iterate_fused(net, inp, corr_fn, coords0, coords1, iters, test_mode)

@@ -33,6 +33,23 @@ def split_weight(wp, taps):
     return torch.cat([hi, hi, lo], 2).reshape(n, 3 * k).contiguous()
 
 
+GATHER_MAX = 62   # sources of one gather_cast_ launch (csrc/kernels/gather.hip)
+
+
+def gather_index(flat_ids, numels):
+    """int64 element ids into the concatenation of tensors with ``numels`` elements (id ==
+    sum(numels): the zero padding slot) -> gather_cast_'s int32 (source << 26 | offset) codes."""
+    assert len(numels) <= GATHER_MAX and max(numels) <= 1 << 26
+    starts = torch.tensor([0] + list(numels), dtype=torch.long).cumsum(0)
+    ids = flat_ids.to(torch.long)
+    k = torch.searchsorted(starts, ids, right=True) - 1     # source holding each id
+    zero = ids >= starts[-1]
+    off = ids - starts[k.clamp(max=len(numels) - 1)]
+    code = (k << 26) | off
+    code[zero] = 63 << 26
+    return code.to(torch.int32)
+
+
 def round_up(x, m):
     return (x + m - 1) // m * m
 

@@ -206,7 +206,8 @@ class _CastWeightsCL(torch.autograd.Function):
 
     Per conv, ``weight.to(bf16).contiguous(channels_last)`` and the backward cast of its bf16
     gradient are 2-3 tiny kernels each (~100 launches per step for both encoders).  Here the
-    forward is cat -> permuting gather -> cast and the backward cat -> cast -> inverse gather, with
+    forward is ONE native permuting gather + cast over the weights in place (gather_cast_) and
+    the backward one inverse gather + cast over the per-conv gradients, with
     the index maps built once per weight geometry.  The same gather also lays out, for every
     native stride-1 3x3 conv, the ADJOINT weight (flipped taps, Cin <-> Cout: the input-gradient
     conv's packed [ci][tap * co' + o] operand) and -- when Cin is not a multiple of 64 (the 96-
@@ -217,8 +218,9 @@ class _CastWeightsCL(torch.autograd.Function):
     @staticmethod
     def forward(ctx, maps, dt, *ws):
         perm, inv, shapes, extra = maps
-        flat = torch.cat([w.reshape(-1) for w in ws] + [ws[0].new_zeros(1)])
-        packed = flat.index_select(0, perm).to(dt)
+        # one gather + cast launch over the weights in place (csrc/kernels/gather.hip)
+        packed = torch.empty(perm.numel(), device=ws[0].device, dtype=dt)
+        _ext.ops().gather_cast_([w.detach().float().contiguous() for w in ws], perm, packed)
         outs, off = [], 0
         for (co, ci, kh, kw) in shapes:
             n = co * ci * kh * kw
@@ -243,8 +245,11 @@ class _CastWeightsCL(torch.autograd.Function):
         for g, (co, ci, kh, kw) in zip(gs[:len(shapes)], shapes):
             if g is None:
                 g = torch.zeros(co, ci, kh, kw, device=perm.device, dtype=ctx.dt)
-            parts.append(g.permute(0, 2, 3, 1).reshape(-1))
-        flat = torch.cat(parts).float().index_select(0, inv)
+            # (co, kh, kw, ci) memory order: a view of a channels_last gradient
+            parts.append(g.to(ctx.dt).permute(0, 2, 3, 1).contiguous())
+        # fp32 parameter-layout gradients of every weight: ONE inverse gather + cast launch
+        flat = torch.empty(inv.numel(), device=perm.device)
+        _ext.ops().gather_cast_(parts, inv, flat)
         grads, off = [], 0
         for (co, ci, kh, kw) in shapes:
             n = co * ci * kh * kw
@@ -304,7 +309,12 @@ def _cast_maps(shapes, device, native=()):
         perm = torch.cat(perm)
         inv = torch.empty(n_fwd, dtype=torch.long)
         inv[perm[:n_fwd]] = torch.arange(n_fwd)
-        _MAPS[key] = (perm.to(device), inv.to(device), list(shapes), tuple(extra))
+        # forward: (weight, offset) codes of the native gather; backward: flat inverse permutation
+        from . import conv as C
+        numels = [co * ci * kh * kw for (co, ci, kh, kw) in shapes]
+        code = C.gather_index(perm, numels)
+        inv_code = C.gather_index(inv, numels)   # packed position -> (weight, offset)
+        _MAPS[key] = (code.to(device), inv_code.to(device), list(shapes), tuple(extra))
     return _MAPS[key]
 
 

@@ -258,11 +258,12 @@ class _PackPlan:
                     parts.append(t.reshape(-1))
         gidx = torch.cat(parts).round().long() - 1
         gidx[gidx < 0] = total
-        self.widx = gidx.to(device)
+        # (parameter, offset) codes of the native gather: the parameters are read in place
+        self.widx = C.gather_index(gidx, self.numels).to(device)
         self.bshapes = [(s.name, b_idx[s.name].numel()) for s in SPECS]
         bidx = torch.cat([b_idx[s.name].reshape(-1) for s in SPECS]).round().long() - 1
         bidx[bidx < 0] = total   # padded rows (row_pad) read the zero slot
-        self.bidx = bidx.to(device)
+        self.bidx = C.gather_index(bidx, self.numels).to(device)
         self.kpad = {s.name: w_idx[s.name].shape[1] for s in SPECS}
         # gradient buffer: per layer dw (cout, kpad) then db (cout), concatenated in SPECS order;
         # uidx[e] = the buffer position holding parameter element e's gradient
@@ -283,7 +284,7 @@ class _PackPlan:
             pos += s.cout
         assert (uidx >= 0).all(), 'every parameter element must have a gradient slot'
         self.dw_total = pos
-        self.uidx = uidx.to(device)
+        self.uidx = C.gather_index(uidx, [pos]).to(device)   # single source: the gradient buffer
 
 
 def _plan(ub, need_grad, device, design=FULL, spl=False):
@@ -330,11 +331,12 @@ class _Packed:
         plan = self.plan = _plan(ub, need_grad, device, design, self.spl)
         self.kpad = plan.kpad
         with torch.no_grad():
-            flat = torch.cat([p.detach().float().reshape(-1) for p in params] +
-                             [torch.zeros(1, device=device)])
-            packed = flat.index_select(0, plan.widx)
-            if not self.spl:
-                packed = packed.to(dtype)
+            ops = _ext.ops()
+            srcs = [p.detach().float().contiguous() for p in params]
+            # every kernel-layout weight in ONE gather + cast launch (csrc/kernels/gather.hip)
+            packed = torch.empty(plan.widx.numel(), device=device,
+                                 dtype=torch.float32 if self.spl else dtype)
+            ops.gather_cast_(srcs, plan.widx, packed)
             off = 0
             for kind, name, shape in plan.views:
                 n = shape[0] * shape[1]
@@ -345,7 +347,8 @@ class _Packed:
                          else C.split_weight(v, _taps_of(design, kind, name)))
                 {'w': self.w, 'wd': self.wd, 'x': self.x}[kind][name] = v
                 off += n
-            bias = flat.index_select(0, plan.bidx)
+            bias = torch.empty(plan.bidx.numel(), device=device)
+            ops.gather_cast_(srcs, plan.bidx, bias)
             off = 0
             for name, n in plan.bshapes:
                 self.b[name] = bias[off:off + n]
@@ -462,7 +465,8 @@ def _unpack_grads(pk):
             pk.dw[s.name].mul_(s.scale)
             pk.db[s.name].mul_(s.scale)
     plan = pk.plan
-    g = pk.dwflat.index_select(0, plan.uidx)
+    g = torch.empty(plan.uidx.numel(), device=pk.dwflat.device)
+    _ext.ops().gather_cast_([pk.dwflat], plan.uidx, g)
     grads, off = [], 0
     for n, shape in zip(plan.numels, plan.shapes):
         grads.append(g[off:off + n].view(shape))

@@ -1,0 +1,51 @@
+"""Native multi-source gather + cast (csrc/kernels/gather.hip) vs torch.cat + index_select + cast."""
+import pytest
+import torch
+
+from pytorch_raft_amd.ops.conv import gather_index
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16, torch.float32])
+@pytest.mark.parametrize('n_out', [1, 7, 4099, 300001])
+def test_gather_cast_matches_index_select(ext_ops, dt, n_out):
+    g = torch.Generator().manual_seed(n_out)
+    numels = [int(x) for x in torch.randint(1, 5000, (23,), generator=g)]
+    srcs = [torch.randn(n, generator=g).to(DEV) for n in numels]
+    total = sum(numels)
+    ids = torch.randint(0, total + 1, (n_out,), generator=g)   # total = the zero slot
+    ids[0] = total
+    flat = torch.cat([s for s in srcs] + [torch.zeros(1, device=DEV)])
+    ref = flat.index_select(0, ids.to(DEV)).to(dt)
+    out = torch.full((n_out,), 7.0, device=DEV, dtype=dt)
+    ext_ops.gather_cast_(srcs, gather_index(ids, numels).to(DEV), out)
+    assert torch.equal(out, ref)
+    assert out[0].item() == 0.0
+
+
+@pytest.mark.parametrize('st', [torch.bfloat16, torch.float16])
+def test_gather_16bit_sources_to_fp32(ext_ops, st):
+    g = torch.Generator().manual_seed(1)
+    numels = [300, 17, 4096, 5]
+    srcs = [torch.randn(n, generator=g).to(DEV).to(st) for n in numels]
+    total = sum(numels)
+    ids = torch.randperm(total, generator=g)
+    flat = torch.cat(srcs).float()
+    out = torch.empty(total, device=DEV)
+    ext_ops.gather_cast_(srcs, gather_index(ids, numels).to(DEV), out)
+    assert torch.equal(out, flat[ids.to(DEV)])
+
+
+def test_gather_rejects_bad_args(ext_ops):
+    src = [torch.randn(10, device=DEV)]
+    idx = torch.zeros(4, dtype=torch.int32, device=DEV)
+    with pytest.raises(RuntimeError):
+        ext_ops.gather_cast_(src, idx, torch.empty(5, device=DEV))            # size mismatch
+    with pytest.raises(RuntimeError):
+        ext_ops.gather_cast_(src, idx.long(), torch.empty(4, device=DEV))     # int64 index
+    with pytest.raises(RuntimeError):
+        ext_ops.gather_cast_([s.double() for s in src], idx, torch.empty(4, device=DEV))
+    with pytest.raises(RuntimeError):    # 16-bit -> 16-bit is not a packing direction
+        ext_ops.gather_cast_([s.half() for s in src], idx, torch.empty(4, device=DEV).half())
