@@ -220,7 +220,8 @@ class _CastWeightsCL(torch.autograd.Function):
         perm, inv, shapes, extra = maps
         # one gather + cast launch over the weights in place (csrc/kernels/gather.hip)
         packed = torch.empty(perm.numel(), device=ws[0].device, dtype=dt)
-        _ext.ops().gather_cast_([w.detach().float().contiguous() for w in ws], perm, packed)
+        from . import conv as C
+        C.gather_cast([w.detach().float().contiguous() for w in ws], perm, packed)
         outs, off = [], 0
         for (co, ci, kh, kw) in shapes:
             n = co * ci * kh * kw
@@ -249,7 +250,8 @@ class _CastWeightsCL(torch.autograd.Function):
             parts.append(g.to(ctx.dt).permute(0, 2, 3, 1).contiguous())
         # fp32 parameter-layout gradients of every weight: ONE inverse gather + cast launch
         flat = torch.empty(inv.numel(), device=perm.device)
-        _ext.ops().gather_cast_(parts, inv, flat)
+        from . import conv as C
+        C.gather_cast(parts, inv, flat)
         grads, off = [], 0
         for (co, ci, kh, kw) in shapes:
             n = co * ci * kh * kw

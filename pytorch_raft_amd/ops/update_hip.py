@@ -331,12 +331,11 @@ class _Packed:
         plan = self.plan = _plan(ub, need_grad, device, design, self.spl)
         self.kpad = plan.kpad
         with torch.no_grad():
-            ops = _ext.ops()
             srcs = [p.detach().float().contiguous() for p in params]
             # every kernel-layout weight in ONE gather + cast launch (csrc/kernels/gather.hip)
             packed = torch.empty(plan.widx.numel(), device=device,
                                  dtype=torch.float32 if self.spl else dtype)
-            ops.gather_cast_(srcs, plan.widx, packed)
+            C.gather_cast(srcs, plan.widx, packed)
             off = 0
             for kind, name, shape in plan.views:
                 n = shape[0] * shape[1]
@@ -348,7 +347,7 @@ class _Packed:
                 {'w': self.w, 'wd': self.wd, 'x': self.x}[kind][name] = v
                 off += n
             bias = torch.empty(plan.bidx.numel(), device=device)
-            ops.gather_cast_(srcs, plan.bidx, bias)
+            C.gather_cast(srcs, plan.bidx, bias)
             off = 0
             for name, n in plan.bshapes:
                 self.b[name] = bias[off:off + n]
@@ -466,7 +465,7 @@ def _unpack_grads(pk):
             pk.db[s.name].mul_(s.scale)
     plan = pk.plan
     g = torch.empty(plan.uidx.numel(), device=pk.dwflat.device)
-    _ext.ops().gather_cast_([pk.dwflat], plan.uidx, g)
+    C.gather_cast([pk.dwflat], plan.uidx, g)
     grads, off = [], 0
     for n, shape in zip(plan.numels, plan.shapes):
         grads.append(g[off:off + n].view(shape))
