@@ -9,6 +9,9 @@
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "kernels/launchers.h"
@@ -18,6 +21,32 @@ namespace {
 using at::Tensor;
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+// Per-(device, stream) zeroed int counters of the encoder norms' last-workgroup finalize
+// (encoder_norm.hip: every launch leaves them zeroed again).  Allocated on first use outside a
+// stream capture (nullptr while capturing before that: the separate finalize launch runs);
+// RAFT_NORM_FUSED_FIN=0 disables the fused finalize.
+int* norm_counters(const Tensor& like, int64_t n) {
+  static const bool on = [] {
+    const char* e = getenv("RAFT_NORM_FUSED_FIN");
+    return !(e && e[0] == '0');
+  }();
+  constexpr int64_t kMax = 1 << 16;
+  if (!on || n > kMax) return nullptr;
+  static std::mutex mu;
+  // never destroyed: no tensor teardown after the HIP runtime at process exit
+  static auto& bufs = *new std::map<std::pair<int, hipStream_t>, Tensor>();
+  const hipStream_t st = cur_stream();
+  const auto key = std::make_pair((int)like.device().index(), st);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = bufs.find(key);
+  if (it == bufs.end()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    it = bufs.emplace(key, at::zeros({kMax}, like.options().dtype(at::kInt))).first;
+  }
+  return it->second.data_ptr<int>();
+}
 
 void check_cuda_f32(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -1279,13 +1308,13 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
   if (mode <= 1) {
     nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
     part = at::empty({groups * (nblk + 1) * 2 * C}, fo);  // partials + per-group sums
-    launch_norm_stats(xp, (int)N, (int)HW, (int)C, mode == 0, part.data_ptr<float>(), nblk, ppb,
-                      norm_ty(st), cur_stream());
   }
-  launch_norm_finalize(mode <= 1 ? part.data_ptr<float>() : nullptr, xp, (int)N, (int)HW, (int)C,
-                       (int)mode, nblk, gp, bp, cb, rm, rv, (float)momentum, (float)eps,
-                       mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
-                       shift.data_ptr<float>(), norm_ty(st), cur_stream());
+  launch_norm_stats_finalize(xp, (int)N, (int)HW, (int)C, (int)mode,
+                             mode <= 1 ? part.data_ptr<float>() : nullptr, nblk, ppb, gp, bp, cb, rm,
+                             rv, (float)momentum, (float)eps, mean.data_ptr<float>(),
+                             invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                             shift.data_ptr<float>(), mode == 0 ? norm_counters(x, N) : nullptr,
+                             norm_ty(st), cur_stream());
   launch_norm_apply(xp, scale.data_ptr<float>(), shift.data_ptr<float>(), (int)N, (int)HW, (int)C,
                     (int)relu, rp, u16m(y), norm_ty(st), cur_stream());
   return {mean, invstd};
@@ -1347,7 +1376,8 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y
                   u16(x), yp, mean.data_ptr<float>(),
                   invstd.data_ptr<float>(), (int)N, (int)HW, (int)C, (int)mode, (int)relu, gp, bp,
                   part.data_ptr<float>(), nblk, ppb, coef.data_ptr<float>(), dg, db, dc,
-                  u16m(dx), d2, yr, go, norm_ty(st), cur_stream());
+                  u16m(dx), d2, yr, go, mode == 0 ? norm_counters(x, N) : nullptr, norm_ty(st),
+                  cur_stream());
 }
 
 void add_relu_(const Tensor& a, const Tensor& b, const Tensor& out) {
