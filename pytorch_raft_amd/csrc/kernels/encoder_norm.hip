@@ -9,8 +9,8 @@
 //   stats     per (image, channel) [instance] or per channel [batch] shifted sums  sum(x-K),
 //             sum((x-K)^2) -> per-workgroup partials (deterministic, no atomics)
 //   finalize  partials reduced -> mean / invstd, the affine fold into one scale/shift per (image, channel),
-//             per-image norms: by the last workgroup of each image inside the stats launch
-//             (counter handoff, last_of_group); batch norms: one reduce + finalize launch,
+//             by the last workgroup of each group inside the stats launch (counter handoff,
+//             last_of_group; two levels of 64-row chunks for long batch-norm partial lists),
 //             BatchNorm running-stat update; the conv bias is folded here too (it cancels in a
 //             training-mode norm, and shifts the eval-mode one), so the conv runs without bias
 //   apply     y = act(x * scale + shift) [+ residual, ReLU]     (16-B vectors, 8 channels/thread)
@@ -173,6 +173,8 @@ __device__ __forceinline__ void fwd_finalize_one(float sa, float sq, int gi, int
 // the group's counter, and the one that sees nblk - 1 reduces the group (fixed order: the result
 // does not depend on which workgroup came last) and resets the counter for the next launch.  Saves
 // the separate reduce / finalize launch where a group's partial list is short (per-image norms).
+constexpr int FIN_CHUNK = 64;   // partial rows reduced by one last workgroup
+
 __device__ __forceinline__ bool last_of_group(int* counter, int gi, int nblk) {
   __shared__ int last;
   __threadfence();   // this workgroup's partial row, visible device-wide (all XCDs)
@@ -186,6 +188,15 @@ __device__ __forceinline__ bool last_of_group(int* counter, int gi, int nblk) {
   if (last) __threadfence();     // acquire: the other workgroups' partial rows
   return last;
 }
+
+// Last-workgroup finalize of group `img` over its nb partial rows (NV values per channel):
+// single level when nb <= FIN_CHUNK (counter[img]); else two levels -- the last workgroup of
+// each FIN_CHUNK-block chunk reduces the chunk into a chunk row (crows), and the last chunk
+// reducer reduces the chunk rows (counters [img * (nch + 1), +nch]).  Returns true in the one
+// workgroup that holds the group's sums in r (threads < C).
+template <int NV>
+__device__ bool group_sums(int* counter, const float* rows, float* crows, int img, int nb, int C,
+                           float (&r)[NV]);
 
 // Reduce a group's nblk partial rows of W floats each ([nblk][NV][C] at rows) in a fixed order:
 // lane = tid / C strides over the rows, then lane 0 of each channel combines the lanes in order.
@@ -214,13 +225,36 @@ __device__ __forceinline__ void reduce_group_rows(const float* rows, int nblk, i
       for (int v = 0; v < NV; ++v) out[v] += red[v][l * C + threadIdx.x];
 }
 
+template <int NV>
+__device__ bool group_sums(int* counter, const float* rows, float* crows, int img, int nb, int C,
+                           float (&r)[NV]) {
+  if (nb <= FIN_CHUNK) {
+    if (!last_of_group(counter, img, nb)) return false;
+    reduce_group_rows<NV>(rows, nb, C, r);
+    return true;
+  }
+  const int nch = (nb + FIN_CHUNK - 1) / FIN_CHUNK;
+  const int k = blockIdx.x / FIN_CHUNK, k0 = k * FIN_CHUNK, kn = min(FIN_CHUNK, nb - k0);
+  int* base = counter + (int64_t)img * (nch + 1);
+  if (!last_of_group(base, k, kn)) return false;
+  reduce_group_rows<NV>(rows + (int64_t)k0 * NV * C, kn, C, r);
+  float* crow = crows + ((int64_t)img * nch + k) * NV * C;
+  if ((int)threadIdx.x < C)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) crow[v * C + threadIdx.x] = r[v];
+  if (!last_of_group(base, nch, nch)) return false;
+  reduce_group_rows<NV>(crows + (int64_t)img * nch * NV * C, nch, C, r);
+  return true;
+}
+
 // grid.x = blocks per group-range, grid.y = image (instance) or 1 (batch: range = all images)
 // partial layout [group_img][blk][2][C]
 template <int TY>
 __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restrict__ x, int HW,
                                                         int C, int per_image, int pix_per_blk,
                                                         int total_pix, float* __restrict__ part,
-                                                        int* __restrict__ counter, NormFin fin) {
+                                                        int* __restrict__ counter, float* __restrict__ crows,
+                                                        NormFin fin) {
   __shared__ float red[2][NT * 8];
   const int cg = C / 8;
   const int lanes = NT / cg;
@@ -302,11 +336,11 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
     }
   }
   // counter: the group's last workgroup finalizes it (no reduce / finalize launch)
-  if (counter != nullptr && last_of_group(counter, img, gridDim.x)) {
-    float r[2];
-    reduce_group_rows<2>(part + (int64_t)img * gridDim.x * 2 * C, gridDim.x, C, r);
-    if (tid < C) fwd_finalize_one<TY>(r[0], r[1], img, tid, fin);
-  }
+  float r[2];
+  if (counter != nullptr &&
+      group_sums<2>(counter, part + (int64_t)img * gridDim.x * 2 * C, crows, img, gridDim.x, C, r) &&
+      tid < C)
+    fwd_finalize_one<TY>(r[0], r[1], img, tid, fin);
 }
 
 // mode: 0 instance (train or eval: always batch statistics), 1 batch-train, 2 batch-eval, 3 none
@@ -538,7 +572,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
     const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ beta,
     int mode, int HW, int C, int per_image, int pix_per_blk, int total_pix, int relu,
     float* __restrict__ part, const uint16_t* __restrict__ dy2, const uint16_t* __restrict__ yres,
-    uint16_t* __restrict__ gout, int* __restrict__ counter, NormBwdFin fin) {
+    uint16_t* __restrict__ gout, int* __restrict__ counter, float* __restrict__ crows, NormBwdFin fin) {
   __shared__ float red[3][NT * 8];
   const int cg = C / 8;
   const int lanes = NT / cg;
@@ -668,11 +702,11 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
     }
   }
   // counter: the group's last workgroup finalizes it (no reduce / finalize launch)
-  if (counter != nullptr && last_of_group(counter, img, gridDim.x)) {
-    float r[3];
-    reduce_group_rows<3>(part + (int64_t)img * gridDim.x * 3 * C, gridDim.x, C, r);
-    if (tid < C) bwd_finalize_one(r[0], r[1], r[2], img, tid, fin);
-  }
+  float r[3];
+  if (counter != nullptr &&
+      group_sums<3>(counter, part + (int64_t)img * gridDim.x * 3 * C, crows, img, gridDim.x, C, r) &&
+      tid < C)
+    bwd_finalize_one(r[0], r[1], r[2], img, tid, fin);
 }
 
 // Backward partial reduce + per-group finalize in ONE launch: block =
@@ -801,16 +835,18 @@ void launch_norm_stats_finalize(const uint16_t* x, int N, int HW, int C, int mod
   const NormFin fin{x, HW, C, cnt, mode, N, gamma, beta, cbias, rmean, rvar, momentum, eps,
                     mean, invstd, scale, shift};
   if (mode <= 1) {
-    // per-image statistics with a counter: the last workgroup of each image finalizes it in the
-    // statistics launch; otherwise partial reduce + finalize in one more launch
-    int* ctr = (counter != nullptr && mode == 0 && C <= NT) ? counter : nullptr;
+    // with a counter the statistics launch also finalizes (last workgroup per group, two levels
+    // for long batch-norm partial lists); otherwise partial reduce + finalize in one more launch.
+    // Chunk rows of the two-level reduce: after the partials and per-group rows of `part`
+    int* ctr = (counter != nullptr && C <= NT) ? counter : nullptr;
+    float* crows = part + (int64_t)groups * (nblk + 1) * 2 * C;
     dim3 grid(nblk, mode == 0 ? N : 1);
     if (f16 == 2) hipLaunchKernelGGL(norm_stats_kernel<2>, grid, dim3(NT), 0, stream, x, HW, C, mode == 0,
-                                     pix_per_blk, N * HW, part, ctr, fin);
+                                     pix_per_blk, N * HW, part, ctr, crows, fin);
     else if (f16) hipLaunchKernelGGL(norm_stats_kernel<1>, grid, dim3(NT), 0, stream, x, HW, C, mode == 0,
-                                     pix_per_blk, N * HW, part, ctr, fin);
+                                     pix_per_blk, N * HW, part, ctr, crows, fin);
     else hipLaunchKernelGGL(norm_stats_kernel<0>, grid, dim3(NT), 0, stream, x, HW, C, mode == 0,
-                            pix_per_blk, N * HW, part, ctr, fin);
+                            pix_per_blk, N * HW, part, ctr, crows, fin);
     if (ctr != nullptr) return;
     if (nblk > 64) {
       const dim3 g2(groups, (C + 15) / 16);
@@ -878,17 +914,19 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
   // pg (the groups' parameter-gradient terms) sits after the partials in `part`
   float* pg = part + (int64_t)groups * nblk * 3 * C;
   const NormBwdFin fin{C, cnt, mode, gamma, beta, mean, invstd, coef, pg};
-  // per-image statistics with a counter: the last workgroup of each image finalizes it in the
-  // statistics launch (eval / none modes: one group over all images, sum(g) and sum(g*xhat) only)
-  int* ctr = (counter != nullptr && mode == 0 && C <= NT) ? counter : nullptr;
+  // with a counter the statistics launch also finalizes (last workgroup per group, two levels
+  // for long batch-norm partial lists; eval / none modes: one group over all images, sum(g) and
+  // sum(g*xhat) only).  Chunk rows of the two-level reduce: after pg in `part`
+  int* ctr = (counter != nullptr && C <= NT) ? counter : nullptr;
+  float* crows = part + (int64_t)groups * (nblk + 1) * 3 * C;
   const dim3 grid(nblk, (mode == 0 || mode == 1) ? groups : 1);
   const int pi = (mode == 0 || mode == 1) ? per_image : 0;
   if (f16 == 2) hipLaunchKernelGGL(norm_bwd_stats_kernel<2>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
-                     beta, mode, HW, C, pi, pix_per_blk, N * HW, relu, part, dy2, yres, gout, ctr, fin);
+                     beta, mode, HW, C, pi, pix_per_blk, N * HW, relu, part, dy2, yres, gout, ctr, crows, fin);
   else if (f16) hipLaunchKernelGGL(norm_bwd_stats_kernel<1>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
-                     beta, mode, HW, C, pi, pix_per_blk, N * HW, relu, part, dy2, yres, gout, ctr, fin);
+                     beta, mode, HW, C, pi, pix_per_blk, N * HW, relu, part, dy2, yres, gout, ctr, crows, fin);
   else hipLaunchKernelGGL(norm_bwd_stats_kernel<0>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
-                     beta, mode, HW, C, pi, pix_per_blk, N * HW, relu, part, dy2, yres, gout, ctr, fin);
+                     beta, mode, HW, C, pi, pix_per_blk, N * HW, relu, part, dy2, yres, gout, ctr, crows, fin);
   // the block-end ReLU ran in the statistics pass: the apply pass reads its result
   if (yres != nullptr) dy = gout;
   if (ctr == nullptr) {

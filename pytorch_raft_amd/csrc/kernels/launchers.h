@@ -358,7 +358,8 @@ bool launch_convex_up_nhwc_bwd(const float* flow, const void* mask, int mask_is_
 // mode: 0 instance, 1 batch (training statistics), 2 batch (running statistics), 3 none
 int encoder_norm_blocks(int64_t range, int C, int* pix_per_blk);
 // statistics (modes 0 / 1) + finalize -> mean / invstd / per-image scale, shift; counter
-// (nullable; >= N zeroed ints, left zeroed): per-image statistics finalize in the statistics launch
+// (nullable; >= groups * (chunks + 1) zeroed ints, left zeroed): the statistics launch finalizes
+// (part then also holds groups * chunks chunk rows after its groups * (nblk + 1) rows)
 void launch_norm_stats_finalize(const uint16_t* x, int N, int HW, int C, int mode, float* part,
                                 int nblk, int pix_per_blk, const float* gamma, const float* beta,
                                 const float* cbias, float* rmean, float* rvar, float momentum,

@@ -261,3 +261,39 @@ def test_instance_norm_fused_finalize(ext_ops, C):
         outs.append((y.clone(), dx.clone(), mean.clone(), invstd.clone()))
     for a, b in zip(outs[0], outs[2]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('C,hw', [(64, (160, 120)), (128, (48, 64))])
+def test_batch_norm_fused_finalize(ext_ops, C, hw):
+    """Training-mode batch norm: the statistics launch finalizes through two levels of 64-row
+    chunks when the partial list is long (C=64 here: 75 partial rows); forward, running stats
+    and backward vs the fp32 batch norm, reproducible across calls."""
+    import torch.nn.functional as F
+    outs = []
+    for rep in range(2):
+        torch.manual_seed(3)
+        x = (torch.randn(4, C, *hw, device=DEV) * 1.5 - 0.3).to(torch.bfloat16)
+        x = x.contiguous(memory_format=torch.channels_last)
+        gm = torch.rand(C, device=DEV) + 0.5
+        bt = torch.randn(C, device=DEV) * 0.2
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        y = torch.empty_like(x)
+        mean, invstd = ext_ops.norm_fwd_(x, 1, 1, gm, bt, None, rm, rv, 0.1, 1e-5, None, y)
+        dy = torch.randn(x.shape, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dx = torch.empty_like(x)
+        dg, db = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        ext_ops.norm_bwd_(dy, x, None, mean, invstd, 1, 1, gm, bt, dg, db, None, dx)
+        xr = x.float().requires_grad_(True)
+        gr, br = gm.clone().requires_grad_(True), bt.clone().requires_grad_(True)
+        rm2, rv2 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        yr = F.relu(F.batch_norm(xr, rm2, rv2, gr, br, training=True, momentum=0.1, eps=1e-5))
+        yr.backward(dy.float())
+        torch.testing.assert_close(y.float(), yr.detach(), atol=3e-2, rtol=2e-2)
+        torch.testing.assert_close(rm, rm2, atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(rv, rv2, atol=1e-4, rtol=1e-3)
+        torch.testing.assert_close(dx.float(), xr.grad, atol=3e-2, rtol=3e-2)
+        torch.testing.assert_close(dg, gr.grad, atol=5e-2, rtol=1e-2)
+        torch.testing.assert_close(db, br.grad, atol=5e-2, rtol=1e-2)
+        outs.append((y.clone(), dx.clone(), dg.clone(), db.clone()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
