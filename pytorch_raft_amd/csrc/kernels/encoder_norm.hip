@@ -8,9 +8,7 @@
 //
 //   stats     per (image, channel) [instance] or per channel [batch] shifted sums  sum(x-K),
 //             sum((x-K)^2) -> per-workgroup partials (deterministic, no atomics)
-//   finalize  partials reduced -> mean / invstd, the affine fold into one scale/shift per (image, channel),
-//             by the last workgroup of each group inside the stats launch (counter handoff,
-//             last_of_group; two levels of 64-row chunks for long batch-norm partial lists),
+//   finalize  partials reduced (same launch) -> mean / invstd, the affine fold into one scale/shift per (image, channel),
 //             BatchNorm running-stat update; the conv bias is folded here too (it cancels in a
 //             training-mode norm, and shifts the eval-mode one), so the conv runs without bias
 //   apply     y = act(x * scale + shift) [+ residual, ReLU]     (16-B vectors, 8 channels/thread)
@@ -130,131 +128,12 @@ __device__ __forceinline__ void norm_affine(int mode, const float* __restrict__ 
   sh = bt - mean * gm * invstd;
 }
 
-// Finalize arguments of the training statistics (norm_reduce_finalize_kernel, or the last
-// workgroup of a group in norm_stats_kernel)
-struct NormFin {
-  const uint16_t* x;
-  int HW, C, cnt, mode, nimg;
-  const float *gamma, *beta, *cbias;
-  float *rmean, *rvar;
-  float momentum, eps;
-  float *mean, *invstd, *scale, *shift;
-};
-
-// (group gi, channel c): mean / invstd from the shifted sums, BatchNorm running stats, the
-// per-image scale / shift table
-template <int TY>
-__device__ __forceinline__ void fwd_finalize_one(float sa, float sq, int gi, int c, const NormFin& f) {
-  const int mode = f.mode, C = f.C, cnt = f.cnt;
-  const float b = f.cbias ? f.cbias[c] : 0.f;
-  const double m = (double)sa / cnt;
-  double var = (double)sq / cnt - m * m;
-  if (var < 0.0) var = 0.0;
-  const float K = ld1<TY>(f.x, (int64_t)(mode == 0 ? gi : 0) * f.HW * C + c);
-  const float mean = (float)(m + K);
-  const float invstd = (float)(1.0 / sqrt(var + (double)f.eps));
-  if (mode == 1 && f.rmean != nullptr) {
-    const double unb = cnt > 1 ? var * cnt / (cnt - 1) : var;
-    f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * (mean + b);
-    f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * (float)unb;
-  }
-  const float gm = mode == 1 && f.gamma ? f.gamma[c] : 1.f;
-  const float bt = mode == 1 && f.beta ? f.beta[c] : 0.f;
-  const int idx = gi * C + c;
-  f.mean[idx] = mean;
-  f.invstd[idx] = invstd;
-  for (int n = (mode == 0 ? gi : 0); n < (mode == 0 ? gi + 1 : f.nimg); ++n) {
-    f.scale[(int64_t)n * C + c] = gm * invstd;
-    f.shift[(int64_t)n * C + c] = bt - mean * gm * invstd;
-  }
-}
-
-// Last-workgroup handoff of a group's partials: every workgroup publishes its partial row, bumps
-// the group's counter, and the one that sees nblk - 1 reduces the group (fixed order: the result
-// does not depend on which workgroup came last) and resets the counter for the next launch.  Saves
-// the separate reduce / finalize launch where a group's partial list is short (per-image norms).
-constexpr int FIN_CHUNK = 64;   // partial rows reduced by one last workgroup
-
-__device__ __forceinline__ bool last_of_group(int* counter, int gi, int nblk) {
-  __shared__ int last;
-  __threadfence();   // this workgroup's partial row, visible device-wide (all XCDs)
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int prev = atomicAdd(counter + gi, 1);
-    last = prev == nblk - 1;
-    if (last) atomicExch(counter + gi, 0);   // every other workgroup has already counted
-  }
-  __syncthreads();
-  if (last) __threadfence();     // acquire: the other workgroups' partial rows
-  return last;
-}
-
-// Last-workgroup finalize of group `img` over its nb partial rows (NV values per channel):
-// single level when nb <= FIN_CHUNK (counter[img]); else two levels -- the last workgroup of
-// each FIN_CHUNK-block chunk reduces the chunk into a chunk row (crows), and the last chunk
-// reducer reduces the chunk rows (counters [img * (nch + 1), +nch]).  Returns true in the one
-// workgroup that holds the group's sums in r (threads < C).
-template <int NV>
-__device__ bool group_sums(int* counter, const float* rows, float* crows, int img, int nb, int C,
-                           float (&r)[NV]);
-
-// Reduce a group's nblk partial rows of W floats each ([nblk][NV][C] at rows) in a fixed order:
-// lane = tid / C strides over the rows, then lane 0 of each channel combines the lanes in order.
-template <int NV>
-__device__ __forceinline__ void reduce_group_rows(const float* rows, int nblk, int C, float (&out)[NV]) {
-  __shared__ float red[NV][NT];
-  const int L = NT / C;
-  const int c = threadIdx.x % C, lane = threadIdx.x / C;
-  float acc[NV];
-#pragma unroll
-  for (int v = 0; v < NV; ++v) acc[v] = 0.f;
-  if (lane < L)
-    for (int k = lane; k < nblk; k += L) {
-      const float* pk = rows + (int64_t)k * NV * C;
-#pragma unroll
-      for (int v = 0; v < NV; ++v) acc[v] += pk[v * C + c];
-    }
-#pragma unroll
-  for (int v = 0; v < NV; ++v) red[v][threadIdx.x] = acc[v];
-  __syncthreads();
-#pragma unroll
-  for (int v = 0; v < NV; ++v) out[v] = 0.f;
-  if (threadIdx.x < C)
-    for (int l = 0; l < L; ++l)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) out[v] += red[v][l * C + threadIdx.x];
-}
-
-template <int NV>
-__device__ bool group_sums(int* counter, const float* rows, float* crows, int img, int nb, int C,
-                           float (&r)[NV]) {
-  if (nb <= FIN_CHUNK) {
-    if (!last_of_group(counter, img, nb)) return false;
-    reduce_group_rows<NV>(rows, nb, C, r);
-    return true;
-  }
-  const int nch = (nb + FIN_CHUNK - 1) / FIN_CHUNK;
-  const int k = blockIdx.x / FIN_CHUNK, k0 = k * FIN_CHUNK, kn = min(FIN_CHUNK, nb - k0);
-  int* base = counter + (int64_t)img * (nch + 1);
-  if (!last_of_group(base, k, kn)) return false;
-  reduce_group_rows<NV>(rows + (int64_t)k0 * NV * C, kn, C, r);
-  float* crow = crows + ((int64_t)img * nch + k) * NV * C;
-  if ((int)threadIdx.x < C)
-#pragma unroll
-    for (int v = 0; v < NV; ++v) crow[v * C + threadIdx.x] = r[v];
-  if (!last_of_group(base, nch, nch)) return false;
-  reduce_group_rows<NV>(crows + (int64_t)img * nch * NV * C, nch, C, r);
-  return true;
-}
-
 // grid.x = blocks per group-range, grid.y = image (instance) or 1 (batch: range = all images)
 // partial layout [group_img][blk][2][C]
 template <int TY>
 __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restrict__ x, int HW,
                                                         int C, int per_image, int pix_per_blk,
-                                                        int total_pix, float* __restrict__ part,
-                                                        int* __restrict__ counter, float* __restrict__ crows,
-                                                        NormFin fin) {
+                                                        int total_pix, float* __restrict__ part) {
   __shared__ float red[2][NT * 8];
   const int cg = C / 8;
   const int lanes = NT / cg;
@@ -335,12 +214,6 @@ __global__ __launch_bounds__(NT) void norm_stats_kernel(const uint16_t* __restri
       dst[C + tid] = sb;
     }
   }
-  // counter: the group's last workgroup finalizes it (no reduce / finalize launch)
-  float r[2];
-  if (counter != nullptr &&
-      group_sums<2>(counter, part + (int64_t)img * gridDim.x * 2 * C, crows, img, gridDim.x, C, r) &&
-      tid < C)
-    fwd_finalize_one<TY>(r[0], r[1], img, tid, fin);
 }
 
 // mode: 0 instance (train or eval: always batch statistics), 1 batch-train, 2 batch-eval, 3 none
@@ -395,11 +268,14 @@ __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint1
 // per-workgroup partials, a fixed-order LDS combine (deterministic), then lane 0 finalizes its
 // (group, channel).  16 lanes for the long batch-norm partial lists, 4 for per-image ones.
 template <int LANES, int TY>
-__global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(const float* __restrict__ part,
-                                                                   int nblk, NormFin f) {
+__global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(
+    const float* __restrict__ part, int nblk, const uint16_t* __restrict__ x, int HW, int C,
+    int cnt, int mode, const float* __restrict__ gamma, const float* __restrict__ beta,
+    const float* __restrict__ cbias, float* __restrict__ rmean, float* __restrict__ rvar,
+    float momentum, float eps, float* __restrict__ mean_out, float* __restrict__ invstd_out,
+    float* __restrict__ scale, float* __restrict__ shift, int nimg) {
   constexpr int COLS = 256 / LANES;
   __shared__ float red[2][LANES][COLS];
-  const int C = f.C;
   const int gi = blockIdx.x;
   const int t = threadIdx.x % COLS, lane = threadIdx.x / COLS;
   const int c = blockIdx.y * COLS + t;
@@ -421,7 +297,27 @@ __global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(const float* 
     sa += red[0][l][t];
     sq += red[1][l][t];
   }
-  fwd_finalize_one<TY>(sa, sq, gi, c, f);
+  const float b = cbias ? cbias[c] : 0.f;
+  const double m = (double)sa / cnt;
+  double var = (double)sq / cnt - m * m;
+  if (var < 0.0) var = 0.0;
+  const float K = ld1<TY>(x, (int64_t)(mode == 0 ? gi : 0) * HW * C + c);
+  const float mean = (float)(m + K);
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  if (mode == 1 && rmean != nullptr) {
+    const double unb = cnt > 1 ? var * cnt / (cnt - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (mean + b);
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unb;
+  }
+  const float gm = mode == 1 && gamma ? gamma[c] : 1.f;
+  const float bt = mode == 1 && beta ? beta[c] : 0.f;
+  const int idx = gi * C + c;
+  mean_out[idx] = mean;
+  invstd_out[idx] = invstd;
+  for (int n = (mode == 0 ? gi : 0); n < (mode == 0 ? gi + 1 : nimg); ++n) {
+    scale[(int64_t)n * C + c] = gm * invstd;
+    shift[(int64_t)n * C + c] = bt - mean * gm * invstd;
+  }
 }
 
 // y = act(x*scale + shift) [+ res -> relu];  act: relu when relu != 0.  Block size is a multiple
@@ -520,49 +416,6 @@ __device__ __forceinline__ V8<TY> block_end_grad(V8<TY> d, const uint16_t* dy2, 
   return mask_pos<TY>(d, o);
 }
 
-// Finalize arguments of the backward statistics
-struct NormBwdFin {
-  int C, cnt, mode;
-  const float *gamma, *beta, *mean, *invstd;
-  float *coef, *pg;
-};
-
-// (group gi, channel c): the apply pass's coefficients and the group's parameter-gradient terms
-__device__ __forceinline__ void bwd_finalize_one(float fsg, float fsgx, float fsx, int gi, int c,
-                                                 const NormBwdFin& f) {
-  const int C = f.C, cnt = f.cnt, mode = f.mode;
-  const double sg = fsg, sgx = fsgx, sx = fsx;
-  const float gm = (mode == 1 || mode == 2) && f.gamma ? f.gamma[c] : 1.f;
-  const float is = f.invstd[(int64_t)gi * C + c];
-  float A, B, Cc;
-  double dcb;
-  if (mode == 0 || mode == 1) {
-    const double mg = sg / cnt, mgx = sgx / cnt;
-    A = gm * is;
-    B = (float)(-gm * is * mgx);
-    Cc = (float)(-gm * is * mg);
-    dcb = A * sg + B * sx + (double)Cc * cnt;
-  } else {
-    A = gm * is;
-    B = 0.f;
-    Cc = 0.f;
-    dcb = A * sg;
-  }
-  const float mu = f.mean[(int64_t)gi * C + c];
-  float sc, sh;
-  norm_affine(mode, f.gamma, f.beta, c, mu, is, sc, sh);
-  float* co = f.coef + (int64_t)gi * 5 * C + c;
-  co[0] = A;
-  co[C] = B * is;
-  co[2 * C] = Cc - B * is * mu;
-  co[3 * C] = sc;
-  co[4 * C] = sh;
-  float* q = f.pg + (int64_t)gi * 3 * C + c;
-  q[0] = fsgx;
-  q[C] = fsg;
-  q[2 * C] = (float)dcb;
-}
-
 // backward partial sums per (group image, blk): sum g, sum g*xhat, sum xhat;
 // g = dy * [y > 0] when relu; xhat = (x - mean) * invstd.  yres != null: dy is the block output's
 // gradient, g0 = (dy [+ dy2]) * [yres > 0] is formed first and stored to gout (see above)
@@ -572,7 +425,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
     const float* __restrict__ invstd, const float* __restrict__ gamma, const float* __restrict__ beta,
     int mode, int HW, int C, int per_image, int pix_per_blk, int total_pix, int relu,
     float* __restrict__ part, const uint16_t* __restrict__ dy2, const uint16_t* __restrict__ yres,
-    uint16_t* __restrict__ gout, int* __restrict__ counter, float* __restrict__ crows, NormBwdFin fin) {
+    uint16_t* __restrict__ gout) {
   __shared__ float red[3][NT * 8];
   const int cg = C / 8;
   const int lanes = NT / cg;
@@ -701,12 +554,6 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
       dst[2 * C + tid] = ss;
     }
   }
-  // counter: the group's last workgroup finalizes it (no reduce / finalize launch)
-  float r[3];
-  if (counter != nullptr &&
-      group_sums<3>(counter, part + (int64_t)img * gridDim.x * 3 * C, crows, img, gridDim.x, C, r) &&
-      tid < C)
-    bwd_finalize_one(r[0], r[1], r[2], img, tid, fin);
 }
 
 // Backward partial reduce + per-group finalize in ONE launch: block =
@@ -714,12 +561,13 @@ __global__ __launch_bounds__(NT) void norm_bwd_stats_kernel(
 // group's partials, fixed-order LDS combine, then lane 0 writes the group's coefficients and its
 // contributions (sum g*xhat, sum g, conv-bias term) to pg [groups][3][C]; the apply kernel's
 // first workgroup sums pg over the groups (fixed order) into dgamma / dbeta / dcbias.
-template <int LANES>
-__global__ __launch_bounds__(256) void norm_bwd_reduce_finalize_kernel(const float* __restrict__ part,
-                                                                       int nblk, NormBwdFin f) {
+template <int LANES, int TY>
+__global__ __launch_bounds__(256) void norm_bwd_reduce_finalize_kernel(
+    const float* __restrict__ part, int nblk, int C, int cnt, int mode,
+    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean,
+    const float* __restrict__ invstd, float* __restrict__ coef, float* __restrict__ pg) {
   constexpr int COLS = 256 / LANES;
   __shared__ float red[3][LANES][COLS];
-  const int C = f.C;
   const int gi = blockIdx.x;
   const int t = threadIdx.x % COLS, lane = threadIdx.x / COLS;
   const int c = blockIdx.y * COLS + t;
@@ -743,7 +591,36 @@ __global__ __launch_bounds__(256) void norm_bwd_reduce_finalize_kernel(const flo
     fsgx += red[1][l][t];
     fsx += red[2][l][t];
   }
-  bwd_finalize_one(fsg, fsgx, fsx, gi, c, f);
+  const double sg = fsg, sgx = fsgx, sx = fsx;
+  const float gm = (mode == 1 || mode == 2) && gamma ? gamma[c] : 1.f;
+  const float is = invstd[(int64_t)gi * C + c];
+  float A, B, Cc;
+  double dcb;
+  if (mode == 0 || mode == 1) {
+    const double mg = sg / cnt, mgx = sgx / cnt;
+    A = gm * is;
+    B = (float)(-gm * is * mgx);
+    Cc = (float)(-gm * is * mg);
+    dcb = A * sg + B * sx + (double)Cc * cnt;
+  } else {
+    A = gm * is;
+    B = 0.f;
+    Cc = 0.f;
+    dcb = A * sg;
+  }
+  const float mu = mean[(int64_t)gi * C + c];
+  float sc, sh;
+  norm_affine(mode, gamma, beta, c, mu, is, sc, sh);
+  float* co = coef + (int64_t)gi * 5 * C + c;
+  co[0] = A;
+  co[C] = B * is;
+  co[2 * C] = Cc - B * is * mu;
+  co[3 * C] = sc;
+  co[4 * C] = sh;
+  float* q = pg + (int64_t)gi * 3 * C + c;
+  q[0] = fsgx;
+  q[C] = fsg;
+  q[2 * C] = (float)dcb;
 }
 
 // dx = A*g + B'*x + C' with g = dy masked by the forward ReLU (read from y when given, else
@@ -824,40 +701,46 @@ int encoder_norm_blocks(int64_t range, int C, int* pix_per_blk) {
   return (int)nb;
 }
 
-void launch_norm_stats_finalize(const uint16_t* x, int N, int HW, int C, int mode, float* part,
-                                int nblk, int pix_per_blk, const float* gamma, const float* beta,
-                                const float* cbias, float* rmean, float* rvar, float momentum,
-                                float eps, float* mean, float* invstd, float* scale, float* shift,
-                                int* counter, int f16, hipStream_t stream) {
+void launch_norm_stats(const uint16_t* x, int N, int HW, int C, int per_image, float* part,
+                       int nblk, int pix_per_blk, int f16, hipStream_t stream) {
+  dim3 grid(nblk, per_image ? N : 1);
+  if (f16 == 2) hipLaunchKernelGGL(norm_stats_kernel<2>, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
+                     N * HW, part);
+  else if (f16) hipLaunchKernelGGL(norm_stats_kernel<1>, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
+                     N * HW, part);
+  else hipLaunchKernelGGL(norm_stats_kernel<0>, grid, dim3(NT), 0, stream, x, HW, C, per_image, pix_per_blk,
+                     N * HW, part);
+}
+
+void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, int C, int mode,
+                          int nblk, const float* gamma, const float* beta, const float* cbias,
+                          float* rmean, float* rvar, float momentum, float eps, float* mean,
+                          float* invstd, float* scale, float* shift, int f16, hipStream_t stream) {
   const int groups = mode == 0 ? N : 1;
   const int cnt = mode == 0 ? HW : N * HW;
   const int tot = groups * C;
-  const NormFin fin{x, HW, C, cnt, mode, N, gamma, beta, cbias, rmean, rvar, momentum, eps,
-                    mean, invstd, scale, shift};
   if (mode <= 1) {
-    // with a counter the statistics launch also finalizes (last workgroup per group, two levels
-    // for long batch-norm partial lists); otherwise partial reduce + finalize in one more launch.
-    // Chunk rows of the two-level reduce: after the partials and per-group rows of `part`
-    int* ctr = (counter != nullptr && C <= NT) ? counter : nullptr;
-    float* crows = part + (int64_t)groups * (nblk + 1) * 2 * C;
-    dim3 grid(nblk, mode == 0 ? N : 1);
-    if (f16 == 2) hipLaunchKernelGGL(norm_stats_kernel<2>, grid, dim3(NT), 0, stream, x, HW, C, mode == 0,
-                                     pix_per_blk, N * HW, part, ctr, crows, fin);
-    else if (f16) hipLaunchKernelGGL(norm_stats_kernel<1>, grid, dim3(NT), 0, stream, x, HW, C, mode == 0,
-                                     pix_per_blk, N * HW, part, ctr, crows, fin);
-    else hipLaunchKernelGGL(norm_stats_kernel<0>, grid, dim3(NT), 0, stream, x, HW, C, mode == 0,
-                            pix_per_blk, N * HW, part, ctr, crows, fin);
-    if (ctr != nullptr) return;
+    // training statistics: partial reduce + finalize in one launch
     if (nblk > 64) {
-      const dim3 g2(groups, (C + 15) / 16);
-      if (f16 == 2) hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 2>), g2, dim3(256), 0, stream, part, nblk, fin);
-      else if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 1>), g2, dim3(256), 0, stream, part, nblk, fin);
-      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 0>), g2, dim3(256), 0, stream, part, nblk, fin);
+      if (f16 == 2) hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 2>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
+      else if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 1>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
+      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 0>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
     } else {
-      const dim3 g2(groups, (C + 63) / 64);
-      if (f16 == 2) hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, 2>), g2, dim3(256), 0, stream, part, nblk, fin);
-      else if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, 1>), g2, dim3(256), 0, stream, part, nblk, fin);
-      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, 0>), g2, dim3(256), 0, stream, part, nblk, fin);
+      if (f16 == 2) hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, 2>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
+      else if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, 1>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
+      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<4, 0>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                         stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                         momentum, eps, mean, invstd, scale, shift, N);
     }
     return;
   }
@@ -906,37 +789,47 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
                      int N, int HW, int C, int mode, int relu, const float* gamma,
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
                      float* dgamma, float* dbeta, float* dcbias, uint16_t* dx,
-                     const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int* counter, int f16,
-                     hipStream_t stream) {
+                     const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int f16, hipStream_t stream) {
   const int per_image = mode == 0 ? 1 : 0;
   const int groups = per_image ? N : 1;
   const int cnt = per_image ? HW : N * HW;
-  // pg (the groups' parameter-gradient terms) sits after the partials in `part`
-  float* pg = part + (int64_t)groups * nblk * 3 * C;
-  const NormBwdFin fin{C, cnt, mode, gamma, beta, mean, invstd, coef, pg};
-  // with a counter the statistics launch also finalizes (last workgroup per group, two levels
-  // for long batch-norm partial lists; eval / none modes: one group over all images, sum(g) and
-  // sum(g*xhat) only).  Chunk rows of the two-level reduce: after pg in `part`
-  int* ctr = (counter != nullptr && C <= NT) ? counter : nullptr;
-  float* crows = part + (int64_t)groups * (nblk + 1) * 3 * C;
-  const dim3 grid(nblk, (mode == 0 || mode == 1) ? groups : 1);
-  const int pi = (mode == 0 || mode == 1) ? per_image : 0;
-  if (f16 == 2) hipLaunchKernelGGL(norm_bwd_stats_kernel<2>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
-                     beta, mode, HW, C, pi, pix_per_blk, N * HW, relu, part, dy2, yres, gout, ctr, crows, fin);
-  else if (f16) hipLaunchKernelGGL(norm_bwd_stats_kernel<1>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
-                     beta, mode, HW, C, pi, pix_per_blk, N * HW, relu, part, dy2, yres, gout, ctr, crows, fin);
-  else hipLaunchKernelGGL(norm_bwd_stats_kernel<0>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
-                     beta, mode, HW, C, pi, pix_per_blk, N * HW, relu, part, dy2, yres, gout, ctr, crows, fin);
+  if (mode == 0 || mode == 1) {
+    dim3 grid(nblk, groups);
+    if (f16 == 2) hipLaunchKernelGGL(norm_bwd_stats_kernel<2>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, per_image, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
+    else if (f16) hipLaunchKernelGGL(norm_bwd_stats_kernel<1>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, per_image, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
+    else hipLaunchKernelGGL(norm_bwd_stats_kernel<0>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, per_image, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
+  } else {
+    // eval / none: only sum(g) and sum(g*xhat) are needed for the parameter grads
+    dim3 grid(nblk, 1);
+    if (f16 == 2) hipLaunchKernelGGL(norm_bwd_stats_kernel<2>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, 0, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
+    else if (f16) hipLaunchKernelGGL(norm_bwd_stats_kernel<1>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, 0, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
+    else hipLaunchKernelGGL(norm_bwd_stats_kernel<0>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
+                       beta, mode, HW, C, 0, pix_per_blk, N * HW, relu, part, dy2, yres, gout);
+  }
   // the block-end ReLU ran in the statistics pass: the apply pass reads its result
   if (yres != nullptr) dy = gout;
-  if (ctr == nullptr) {
-    // per-group sums + coefficients in one launch
-    if (nblk > 64)
-      hipLaunchKernelGGL(norm_bwd_reduce_finalize_kernel<16>, dim3(groups, (C + 15) / 16), dim3(256), 0,
-                         stream, part, nblk, fin);
-    else
-      hipLaunchKernelGGL(norm_bwd_reduce_finalize_kernel<4>, dim3(groups, (C + 63) / 64), dim3(256), 0,
-                         stream, part, nblk, fin);
+  // per-group sums + coefficients in one launch; pg (the groups' parameter-gradient terms) sits
+  // after the partials in `part`
+  float* pg = part + (int64_t)groups * nblk * 3 * C;
+  if (nblk > 64) {
+    if (f16 == 2) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, 2>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
+    else if (f16) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, 1>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
+    else hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, 0>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
+  } else {
+    if (f16 == 2) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<4, 2>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
+    else if (f16) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<4, 1>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
+    else hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<4, 0>), dim3(groups, (C + 63) / 64), dim3(256), 0,
+                       stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
   }
   const int64_t nvec = (int64_t)N * HW * C / 8;
   if (f16 == 2) hipLaunchKernelGGL(norm_bwd_apply_kernel<2>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,

@@ -357,14 +357,12 @@ bool launch_convex_up_nhwc_bwd(const float* flow, const void* mask, int mask_is_
 // ---- encoder norm + activation, NHWC bf16 / fp16 (f16) (encoder_norm.hip)
 // mode: 0 instance, 1 batch (training statistics), 2 batch (running statistics), 3 none
 int encoder_norm_blocks(int64_t range, int C, int* pix_per_blk);
-// statistics (modes 0 / 1) + finalize -> mean / invstd / per-image scale, shift; counter
-// (nullable; >= groups * (chunks + 1) zeroed ints, left zeroed): the statistics launch finalizes
-// (part then also holds groups * chunks chunk rows after its groups * (nblk + 1) rows)
-void launch_norm_stats_finalize(const uint16_t* x, int N, int HW, int C, int mode, float* part,
-                                int nblk, int pix_per_blk, const float* gamma, const float* beta,
-                                const float* cbias, float* rmean, float* rvar, float momentum,
-                                float eps, float* mean, float* invstd, float* scale, float* shift,
-                                int* counter, int f16, hipStream_t stream);
+void launch_norm_stats(const uint16_t* x, int N, int HW, int C, int per_image, float* part,
+                       int nblk, int pix_per_blk, int f16, hipStream_t stream);
+void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, int C, int mode,
+                          int nblk, const float* gamma, const float* beta, const float* cbias,
+                          float* rmean, float* rvar, float momentum, float eps, float* mean,
+                          float* invstd, float* scale, float* shift, int f16, hipStream_t stream);
 void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift, int N, int HW,
                        int C, int relu, const uint16_t* res, uint16_t* y, int f16, hipStream_t stream);
 void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_t n,
@@ -381,8 +379,7 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
                      int N, int HW, int C, int mode, int relu, const float* gamma,
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
                      float* dgamma, float* dbeta, float* dcbias, uint16_t* dx,
-                     const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int* counter, int f16,
-                     hipStream_t stream);
+                     const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int f16, hipStream_t stream);
 
 // ---- multi-tensor AdamW + global-norm clip + GradScaler unscale / overflow skip (adamw.hip)
 struct AdamTensor {

@@ -235,10 +235,10 @@ def test_fast_encoder_fp32_matches_eager_split(ext_ops, cls, norm, train):
 
 
 @pytest.mark.parametrize('C', [64, 96, 128])
-def test_instance_norm_fused_finalize(ext_ops, C):
-    """Per-image norms finalize in the statistics launch (the last workgroup of each image, a
-    counter handoff that leaves the counters zeroed): forward and backward match the fp32
-    instance norm, and repeated calls with different batch sizes are bitwise reproducible."""
+def test_instance_norm_kernels_match_fp32(ext_ops, C):
+    """Instance-norm kernels (statistics, fixed-order reduce + finalize, apply; backward): forward
+    and backward match the fp32 instance norm, and repeated calls with different batch sizes are
+    bitwise reproducible."""
     import torch.nn.functional as F
     outs = []
     for n in (3, 5, 3):
@@ -264,10 +264,10 @@ def test_instance_norm_fused_finalize(ext_ops, C):
 
 
 @pytest.mark.parametrize('C,hw', [(64, (160, 120)), (128, (48, 64))])
-def test_batch_norm_fused_finalize(ext_ops, C, hw):
-    """Training-mode batch norm: the statistics launch finalizes through two levels of 64-row
-    chunks when the partial list is long (C=64 here: 75 partial rows); forward, running stats
-    and backward vs the fp32 batch norm, reproducible across calls."""
+def test_batch_norm_kernels_match_fp32(ext_ops, C, hw):
+    """Training-mode batch norm with a long partial list (C=64 here: 75 per-workgroup partial
+    rows, the 16-lane reduce + finalize): forward, running stats and backward vs the fp32 batch
+    norm, bitwise reproducible across calls."""
     import torch.nn.functional as F
     outs = []
     for rep in range(2):
