@@ -1362,6 +1362,24 @@ void add_relu_(const Tensor& a, const Tensor& b, const Tensor& out) {
                   u16m(out), a.numel(), norm_ty(st), cur_stream());
 }
 
+// out (2B,3,H,W) channels_last = 2 * ([a ; b] / 255) - 1 in out's dtype; a, b (B,3,H,W) fp32
+void image_prep_(const Tensor& a, const Tensor& b, const Tensor& out) {
+  check_cuda_f32(a, "image a");
+  check_cuda_f32(b, "image b");
+  TORCH_CHECK(a.dim() == 4 && a.size(1) == 3 && a.sizes() == b.sizes(), "images must be (B,3,H,W)");
+  TORCH_CHECK(a.device() == b.device() && out.device() == a.device(), "image_prep: devices");
+  const int64_t B = a.size(0), H = a.size(2), W = a.size(3);
+  TORCH_CHECK(out.dim() == 4 && out.size(0) == 2 * B && out.size(1) == 3 && out.size(2) == H &&
+              out.size(3) == W && out.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "image_prep: out must be a channels_last (2B,3,H,W) tensor");
+  const at::ScalarType ot = out.scalar_type();
+  TORCH_CHECK(ot == at::kBFloat16 || ot == at::kHalf || ot == at::kFloat, "image_prep: out dtype");
+  c10::DeviceGuard gd(a.device());
+  TORCH_CHECK(launch_image_prep(a.data_ptr<float>(), b.data_ptr<float>(), out.data_ptr(), (int)B, H * W,
+                                ot == at::kBFloat16 ? 0 : (ot == at::kHalf ? 1 : 2), cur_stream()),
+              "image_prep launch");
+}
+
 // out[i] = cast(srcs[k][off]) for idx[i] = k << 26 | off (k = 63: zero); srcs contiguous GPU
 // tensors of one dtype and device, out 1-D with idx.numel() elements: fp32 sources -> bf16 /
 // fp16 / fp32 out, or bf16 / fp16 sources -> fp32 out
@@ -1865,6 +1883,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
   m.def("gather_cast_(Tensor[] srcs, Tensor idx, Tensor(a!) out) -> ()");
+  m.def("image_prep_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] douts, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("corr_build_bf16(Tensor f1, Tensor f2, int levels, bool pyr_bf16=False) -> Tensor[]");
   m.def("conv_wgrad_taps_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, "
@@ -1919,6 +1938,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("add_relu_", &add_relu_);
   m.impl("relu_mask_", &relu_mask_);
   m.impl("gather_cast_", &gather_cast_);
+  m.impl("image_prep_", &image_prep_);
   m.impl("corr_build_bf16", &corr_build_bf16);
   m.impl("conv_wgrad_taps_", &conv_wgrad_taps_);
   m.impl("convex_up_fwd", &convex_up_fwd);

@@ -415,3 +415,8 @@ struct GatherSrcs {
 // output type): 0 bf16, 1 fp16, 2 fp32 -- fp32 -> any, or bf16 / fp16 -> fp32
 bool launch_gather_cast(const GatherSrcs& s, const int32_t* idx, void* out, int64_t n, int it, int ot,
                         hipStream_t stream);
+
+// ---- image_prep.hip: both frames -> 2 * (x / 255) - 1 as one channels_last (2B,H,W,3) batch;
+// ot: 0 bf16, 1 fp16, 2 fp32
+bool launch_image_prep(const float* a, const float* b, void* out, int B, int64_t HW, int ot,
+                       hipStream_t stream);

@@ -50,6 +50,31 @@ def _get(args, name, default):
     return getattr(args, name, default)
 
 
+def _prep_pair(image1, image2, fnet, cnet):
+    """``2 * (x / 255) - 1`` of both frames as ONE channels_last (2B,3,H,W) batch in the encoders'
+    compute dtype (`core/raft.py:94-95`, `core/extractor.py:176-179`), by the native
+    ``image_prep_`` kernel -- when both encoders take the native fast path on it (they would cast
+    and lay the frames out exactly so); None otherwise (the eager ops run)."""
+    from ..ops import encoder as fast
+    if not (image1.is_cuda and image1.dtype == torch.float32 and image2.dtype == torch.float32
+            and image1.dim() == 4 and image1.shape[1] == 3 and image1.shape == image2.shape
+            and not (image1.requires_grad or image2.requires_grad) and _ext.device_ok(image1)):
+        return None
+    if not (fast.fast_path_ok(fnet, image1) and fast.fast_path_ok(cnet, image1)):
+        return None
+    dt = torch.get_autocast_dtype('cuda') if torch.is_autocast_enabled('cuda') else torch.float32
+    b, _, h, w = image1.shape
+    # image-chunked encoders (huge batches, extractor.py:_chunk_images): the eager preparation
+    limit = int(os.environ.get('RAFT_ENC_CHUNK_BYTES', str(2 ** 31 - 1)))
+    per_img = fnet.widths[0] * ((h + 1) // 2) * ((w + 1) // 2) * torch.finfo(dt).bits // 8
+    if 2 * b > max(1, limit // per_img):
+        return None
+    out = torch.empty(2 * b, 3, h, w, device=image1.device, dtype=dt,
+                      memory_format=torch.channels_last)
+    _ext.ops().image_prep_(image1.contiguous(), image2.contiguous(), out)
+    return out
+
+
 _BUDGET = {}
 
 
@@ -134,14 +159,8 @@ class RAFT(nn.Module):
 
         Split from ``decode`` so the hipGraph training step can replay the launch-bound recurrent
         part while the encoders (a few large MIOpen convolutions) run eagerly."""
-        image1 = (2 * (image1 / 255.0) - 1.0).contiguous()
-        image2 = (2 * (image2 / 255.0) - 1.0).contiguous()
         hdim, cdim = self.hidden_dim, self.context_dim
         dev = image1.device
-        cl = bool(_get(self.args, 'channels_last', False))
-        if cl:
-            image1 = image1.contiguous(memory_format=torch.channels_last)
-            image2 = image2.contiguous(memory_format=torch.channels_last)
         # corr_impl='torch' = stock reference-semantics ops everywhere (the baseline): no HIP
         # encoder kernels either
         native = self.corr_impl != 'torch'
@@ -150,9 +169,23 @@ class RAFT(nn.Module):
         # encoder call, so each conv's deferred weight gradient covers exactly that call)
         fp32_mfma = native and self._use_fp32_mfma(image1) and _FP32_ENC_MFMA
         with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
-            fmap1, fmap2 = self.fnet([image1, image2])
+            # both encoders on the native fast path: normalisation, batch cat, cast and
+            # channels_last layout of the frames in one kernel; the context encoder reads frame1's
+            # half of that batch in place
+            pair = _prep_pair(image1, image2, self.fnet, self.cnet) if native else None
+        if pair is None:
+            image1 = (2 * (image1 / 255.0) - 1.0).contiguous()
+            image2 = (2 * (image2 / 255.0) - 1.0).contiguous()
+            if bool(_get(self.args, 'channels_last', False)):
+                image1 = image1.contiguous(memory_format=torch.channels_last)
+                image2 = image2.contiguous(memory_format=torch.channels_last)
         with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
-            cnet = self.cnet(image1)
+            if pair is None:
+                fmap1, fmap2 = self.fnet([image1, image2])
+            else:
+                fmap1, fmap2 = torch.split(self.fnet(pair), [image1.shape[0]] * 2, dim=0)
+        with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
+            cnet = self.cnet(image1 if pair is None else pair[:image1.shape[0]])
             net, inp = torch.split(cnet, [hdim, cdim], dim=1)
             net = torch.tanh(net)
             inp = torch.relu(inp)

@@ -49,3 +49,16 @@ def test_gather_rejects_bad_args(ext_ops):
         ext_ops.gather_cast_([s.double() for s in src], idx, torch.empty(4, device=DEV))
     with pytest.raises(RuntimeError):    # 16-bit -> 16-bit is not a packing direction
         ext_ops.gather_cast_([s.half() for s in src], idx, torch.empty(4, device=DEV).half())
+
+
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float16, torch.float32])
+def test_image_prep_matches_eager(ext_ops, dt):
+    """image_prep_: both frames -> 2 * (x / 255) - 1 -> one channels_last batch, bitwise the
+    eager chain (ATen's scalar division = multiply by the float reciprocal)."""
+    g = torch.Generator().manual_seed(0)
+    a = (torch.rand(3, 3, 37, 53, generator=g) * 255).to(DEV)
+    b = (torch.rand(3, 3, 37, 53, generator=g) * 255).to(DEV)
+    ref = torch.cat([2 * (a / 255.0) - 1.0, 2 * (b / 255.0) - 1.0]).to(dt)
+    out = torch.empty(6, 3, 37, 53, device=DEV, dtype=dt, memory_format=torch.channels_last)
+    ext_ops.image_prep_(a, b, out)
+    assert torch.equal(out, ref)
