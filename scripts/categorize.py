@@ -4,6 +4,7 @@ import sys
 
 CATS = [('ours conv fwd', r'conv_fwd_kernel<[^>]*, [0-57], (true|false)>|conv_fwd_(glds|halo)_kernel<\d+, \d+, \d+, [0-57], \d+>|fh2_fwd'),
         ('ours dgrad', r'conv_fwd_kernel<[^>]*, [68], |conv_fwd_(glds|halo)_kernel<\d+, \d+, \d+, [68], \d+>|fh2_dgrad'),
+        ('ours split', r'split_hilo'),
         ('ours conv fwd', r'conv_enc64'),
         ('ours wgrad', r'fh2_wgrad'),
         ('ours wgrad', r'conv_wgrad'),
@@ -31,6 +32,9 @@ for line in open(sys.argv[1]):
     if m:
         phase, name = m.group(1), m.group(2)
         phase_tot[phase] = phase_tot.get(phase, 0) + ms
+    # fp16 (EPI_F16 = 16) and split-fp32 (EPI_SPL = 32) instantiations: the base epilogue's category
+    name = re.sub(r'(conv_fwd_(?:glds|halo)_kernel<\d+, \d+, \d+, )(\d+)',
+                  lambda k: k.group(1) + str(int(k.group(2)) & 15), name)
     for c, pat in CATS:
         if re.search(pat, name):
             if phase and c.startswith('ours'):

@@ -165,8 +165,9 @@ def test_fp16_gradscaler_grads_match_fp32(ext_ops):
         m = RAFT(args).to(DEV).train()
         m.freeze_bn()
         scaler = torch.amp.GradScaler('cuda', init_scale=2.0 ** 12, enabled=prec == 'fp16')
-        # fp16 autocast runs the fused MFMA update block (v_mfma_f32_32x32x16_f16), not eager ops
-        assert m._use_fused_update(i1) == (prec != 'fp32'), prec
+        # every precision runs the fused MFMA update block (fp16: v_mfma_f32_32x32x16_f16; fp32:
+        # split-fp32 operands), not eager ops
+        assert m._use_fused_update(i1), prec
         preds = m(i1, i2, iters=3)
         loss, _ = sequence_loss(preds, flow, valid, 0.8)
         scaler.scale(loss).backward()
