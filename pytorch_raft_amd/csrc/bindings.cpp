@@ -1350,6 +1350,49 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y
                   u16m(dx), d2, yr, go, norm_ty(st), cur_stream());
 }
 
+// context-encoder output: cnet (B,C,H,W) channels_last bf16 / fp16 -> h (B,H,W,hdim) =
+// tanh(cnet[:, :hdim]), x (B,H,W,C-hdim) = relu(cnet[:, hdim:]), both contiguous NHWC
+void check_nhwc_like(const Tensor& t, const Tensor& cnet, int64_t c, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == cnet.scalar_type() && t.is_contiguous() && t.dim() == 4 &&
+                  t.size(0) == cnet.size(0) && t.size(1) == cnet.size(2) && t.size(2) == cnet.size(3) &&
+                  t.size(3) == c,
+              name, ": must be a contiguous (B,H,W,", c, ") tensor of the input's dtype");
+}
+void ctx_act_(const Tensor& cnet, int64_t hdim, const Tensor& h, const Tensor& x) {
+  const at::ScalarType st = opnorm(cnet);
+  TORCH_CHECK(st != at::kFloat, "ctx_act: bf16 / fp16 only");
+  check_cl16(st, cnet, "cnet");
+  const int64_t C = cnet.size(1);
+  TORCH_CHECK(hdim % 8 == 0 && hdim > 0 && hdim < C, "ctx_act: hdim must be a multiple of 8 below C");
+  check_nhwc_like(h, cnet, hdim, "h");
+  check_nhwc_like(x, cnet, C - hdim, "x");
+  c10::DeviceGuard g(cnet.device());
+  launch_ctx_act(u16(cnet), cnet.size(0) * cnet.size(2) * cnet.size(3), (int)C, (int)hdim, u16m(h), u16m(x),
+                 norm_ty(st), cur_stream());
+}
+void ctx_act_bwd_(const c10::optional<Tensor>& gh, const c10::optional<Tensor>& gx, const Tensor& h,
+                  const Tensor& x, const Tensor& gin) {
+  const at::ScalarType st = opnorm(gin);
+  TORCH_CHECK(st != at::kFloat, "ctx_act_bwd: bf16 / fp16 only");
+  check_cl16(st, gin, "gin");
+  const int64_t C = gin.size(1), hdim = h.size(3);
+  TORCH_CHECK(hdim % 8 == 0 && hdim > 0 && hdim < C, "ctx_act_bwd: hdim");
+  check_nhwc_like(h, gin, hdim, "h");
+  check_nhwc_like(x, gin, C - hdim, "x");
+  const uint16_t *ghp = nullptr, *gxp = nullptr;
+  if (gh.has_value() && gh->defined()) {
+    check_nhwc_like(*gh, gin, hdim, "gh");
+    ghp = u16(*gh);
+  }
+  if (gx.has_value() && gx->defined()) {
+    check_nhwc_like(*gx, gin, C - hdim, "gx");
+    gxp = u16(*gx);
+  }
+  c10::DeviceGuard g(gin.device());
+  launch_ctx_act_bwd(ghp, gxp, u16(h), u16(x), gin.size(0) * gin.size(2) * gin.size(3), (int)C, (int)hdim,
+                     u16m(gin), norm_ty(st), cur_stream());
+}
+
 void add_relu_(const Tensor& a, const Tensor& b, const Tensor& out) {
   const at::ScalarType st = opnorm(a);
   check_cl16(st, a, "a");
@@ -1884,6 +1927,8 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
   m.def("gather_cast_(Tensor[] srcs, Tensor idx, Tensor(a!) out) -> ()");
   m.def("image_prep_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
+  m.def("ctx_act_(Tensor cnet, int hdim, Tensor(a!) h, Tensor(b!) x) -> ()");
+  m.def("ctx_act_bwd_(Tensor? gh, Tensor? gx, Tensor h, Tensor x, Tensor(a!) gin) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] douts, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
   m.def("corr_build_bf16(Tensor f1, Tensor f2, int levels, bool pyr_bf16=False) -> Tensor[]");
   m.def("conv_wgrad_taps_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, "
@@ -1939,6 +1984,8 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("relu_mask_", &relu_mask_);
   m.impl("gather_cast_", &gather_cast_);
   m.impl("image_prep_", &image_prep_);
+  m.impl("ctx_act_", &ctx_act_);
+  m.impl("ctx_act_bwd_", &ctx_act_bwd_);
   m.impl("corr_build_bf16", &corr_build_bf16);
   m.impl("conv_wgrad_taps_", &conv_wgrad_taps_);
   m.impl("convex_up_fwd", &convex_up_fwd);

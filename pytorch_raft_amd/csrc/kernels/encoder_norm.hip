@@ -683,6 +683,65 @@ __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
   }
 }
 
+// Context-encoder output (`core/raft.py:111-113`): cnet (NHWC, C = hdim + cdim) -> h = tanh of
+// channels [0, hdim), x = relu of [hdim, C), each written as its own contiguous NHWC tensor (the
+// fused update block's operands); one pass instead of split + tanh + relu + two layout copies
+template <int TY>
+__global__ __launch_bounds__(NT) void ctx_act_kernel(const uint16_t* __restrict__ in, int C, int hdim,
+                                                     int64_t nvec, uint16_t* __restrict__ h,
+                                                     uint16_t* __restrict__ xo) {
+  const int cg = C / 8, hg = hdim / 8, xg = cg - hg;
+  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+    const int64_t pix = v / cg;
+    const int g = (int)(v - pix * cg);
+    float f[8];
+    unpack8<TY>(ld8<TY>(in, v * 8), f);
+    if (g < hg) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = tanhf(f[i]);
+      st8<TY>(h, (pix * hg + g) * 8, pack8<TY>(f));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = f[i] > 0.f ? f[i] : 0.f;
+      st8<TY>(xo, (pix * xg + g - hg) * 8, pack8<TY>(f));
+    }
+  }
+}
+
+// its backward: gin[..., :hdim] = gh * (1 - h^2), gin[..., hdim:] = gx * [x > 0]; a missing
+// gradient (nullptr) is zero
+template <int TY>
+__global__ __launch_bounds__(NT) void ctx_act_bwd_kernel(const uint16_t* __restrict__ gh,
+                                                         const uint16_t* __restrict__ gx,
+                                                         const uint16_t* __restrict__ h,
+                                                         const uint16_t* __restrict__ xo, int C, int hdim,
+                                                         int64_t nvec, uint16_t* __restrict__ gin) {
+  const int cg = C / 8, hg = hdim / 8, xg = cg - hg;
+  for (int64_t v = blockIdx.x * (int64_t)NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * NT) {
+    const int64_t pix = v / cg;
+    const int g = (int)(v - pix * cg);
+    float d[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d[i] = 0.f;
+    if (g < hg) {
+      if (gh != nullptr) {
+        const int64_t off = (pix * hg + g) * 8;
+        float hv[8];
+        unpack8<TY>(ld8<TY>(gh, off), d);
+        unpack8<TY>(ld8<TY>(h, off), hv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d[i] = d[i] * (1.f - hv[i] * hv[i]);
+      }
+      st8<TY>(gin, v * 8, pack8<TY>(d));
+    } else if (gx != nullptr) {
+      const int64_t off = (pix * xg + g - hg) * 8;
+      st8<TY>(gin, v * 8, mask_pos<TY>(ld8<TY>(gx, off), ld8<TY>(xo, off)));
+    } else {
+      st8<TY>(gin, v * 8, pack8<TY>(d));
+    }
+  }
+}
+
 unsigned grid_for(int64_t nvec) {
   const int64_t b = (nvec + NT - 1) / NT;
   return (unsigned)std::min<int64_t>(b, 256 * 16);
@@ -838,4 +897,20 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
                      HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias);
   else hipLaunchKernelGGL(norm_bwd_apply_kernel<0>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
                      HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias);
+}
+
+void launch_ctx_act(const uint16_t* in, int64_t P, int C, int hdim, uint16_t* h, uint16_t* x, int f16,
+                    hipStream_t stream) {
+  const int64_t nvec = P * C / 8;
+  if (f16) hipLaunchKernelGGL(ctx_act_kernel<1>, dim3(grid_for(nvec)), dim3(NT), 0, stream, in, C, hdim, nvec, h, x);
+  else hipLaunchKernelGGL(ctx_act_kernel<0>, dim3(grid_for(nvec)), dim3(NT), 0, stream, in, C, hdim, nvec, h, x);
+}
+
+void launch_ctx_act_bwd(const uint16_t* gh, const uint16_t* gx, const uint16_t* h, const uint16_t* x,
+                        int64_t P, int C, int hdim, uint16_t* gin, int f16, hipStream_t stream) {
+  const int64_t nvec = P * C / 8;
+  if (f16) hipLaunchKernelGGL(ctx_act_bwd_kernel<1>, dim3(grid_for(nvec)), dim3(NT), 0, stream, gh, gx, h, x, C,
+                              hdim, nvec, gin);
+  else hipLaunchKernelGGL(ctx_act_bwd_kernel<0>, dim3(grid_for(nvec)), dim3(NT), 0, stream, gh, gx, h, x, C,
+                          hdim, nvec, gin);
 }

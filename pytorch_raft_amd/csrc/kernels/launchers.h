@@ -367,6 +367,12 @@ void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift
                        int C, int relu, const uint16_t* res, uint16_t* y, int f16, hipStream_t stream);
 void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_t n,
                      int f16, hipStream_t stream);
+// context-encoder output: in (P pixels x C, NHWC) -> h = tanh(in[:, :hdim]) (P x hdim), x =
+// relu(in[:, hdim:]) (P x (C - hdim)); bf16 / fp16 (f16); and its backward (gh / gx nullable)
+void launch_ctx_act(const uint16_t* in, int64_t P, int C, int hdim, uint16_t* h, uint16_t* x, int f16,
+                    hipStream_t stream);
+void launch_ctx_act_bwd(const uint16_t* gh, const uint16_t* gx, const uint16_t* h, const uint16_t* x,
+                        int64_t P, int C, int hdim, uint16_t* gin, int f16, hipStream_t stream);
 // g = (dy [+ dy2]) * [y > 0]; dy2 nullable
 void launch_relu_mask(const uint16_t* dy, const uint16_t* dy2, const uint16_t* y, uint16_t* g, int64_t n,
                       int f16, hipStream_t stream);

@@ -50,6 +50,11 @@ def _get(args, name, default):
     return getattr(args, name, default)
 
 
+def _context_act(cnet, hdim):
+    from ..ops import encoder as fast
+    return fast.context_act(cnet, hdim)
+
+
 def _prep_pair(image1, image2, fnet, cnet):
     """``2 * (x / 255) - 1`` of both frames as ONE channels_last (2B,3,H,W) batch in the encoders'
     compute dtype (`core/raft.py:94-95`, `core/extractor.py:176-179`), by the native
@@ -186,9 +191,14 @@ class RAFT(nn.Module):
                 fmap1, fmap2 = torch.split(self.fnet(pair), [image1.shape[0]] * 2, dim=0)
         with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
             cnet = self.cnet(image1 if pair is None else pair[:image1.shape[0]])
-            net, inp = torch.split(cnet, [hdim, cdim], dim=1)
-            net = torch.tanh(net)
-            inp = torch.relu(inp)
+            # native: both activations in one pass, as the fused block's NHWC operands
+            act = _context_act(cnet, hdim) if native else None
+            if act is not None:
+                net, inp = act
+            else:
+                net, inp = torch.split(cnet, [hdim, cdim], dim=1)
+                net = torch.tanh(net)
+                inp = torch.relu(inp)
         return fmap1, fmap2, net, inp
 
     def decode(self, fmap1, fmap2, net, inp, iters=12, flow_init=None, test_mode=False):

@@ -200,6 +200,44 @@ class _AddRelu(torch.autograd.Function):
         return g, g
 
 
+class _ContextAct(torch.autograd.Function):
+    """net, inp = tanh / relu of the context encoder's two channel halves (`core/raft.py:111-113`)
+    in one native pass, each as its own contiguous NHWC tensor (returned as NCHW views) -- the
+    fused update block's operand layout, so no split / activation / layout-copy kernels."""
+
+    @staticmethod
+    def forward(ctx, cnet, hdim):
+        b, c, hh, ww = cnet.shape
+        h = torch.empty(b, hh, ww, hdim, device=cnet.device, dtype=cnet.dtype)
+        x = torch.empty(b, hh, ww, c - hdim, device=cnet.device, dtype=cnet.dtype)
+        _ext.ops().ctx_act_(cnet, hdim, h, x)
+        ctx.save_for_backward(h, x)
+        ctx.set_materialize_grads(False)
+        return h.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gh, gx):
+        h, x = ctx.saved_tensors
+        b, hh, ww, hd = h.shape
+        gin = torch.empty(b, hd + x.shape[-1], hh, ww, device=h.device, dtype=h.dtype,
+                          memory_format=torch.channels_last)
+        nhwc = (lambda g: None if g is None else g.to(h.dtype).permute(0, 2, 3, 1).contiguous())
+        _ext.ops().ctx_act_bwd_(nhwc(gh), nhwc(gx), h, x, gin)
+        return gin, None
+
+
+def context_act(cnet, hdim):
+    """(tanh(cnet[:, :hdim]), relu(cnet[:, hdim:])) by the native kernel when cnet is a 16-bit
+    channels_last GPU tensor the kernel takes; None otherwise (the caller runs the eager ops)."""
+    c = cnet.shape[1]
+    if not (cnet.is_cuda and cnet.dtype in (torch.bfloat16, torch.float16) and cnet.dim() == 4
+            and cnet.is_contiguous(memory_format=torch.channels_last) and c % 8 == 0 and c <= 256
+            and hdim % 8 == 0 and 0 < hdim < c and _ext.device_ok(cnet)
+            and _ext.gpu_path_enabled(required=False)):
+        return None
+    return _ContextAct.apply(cnet, hdim)
+
+
 class _CastWeightsCL(torch.autograd.Function):
     """All conv weights of an encoder -> 16-bit (bf16 / fp16: the autocast dtype) channels_last
     views of ONE buffer, and back.

@@ -297,3 +297,27 @@ def test_batch_norm_kernels_match_fp32(ext_ops, C, hw):
         outs.append((y.clone(), dx.clone(), dg.clone(), db.clone()))
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('dt,hd,c', [(torch.bfloat16, 128, 256), (torch.float16, 128, 256),
+                                     (torch.bfloat16, 96, 160)])
+def test_context_act_matches_eager(ext_ops, dt, hd, c):
+    """net, inp = tanh / relu of the context encoder's halves in one native pass (NHWC outputs)
+    vs the eager split + tanh + relu, forward and backward (one missing gradient included)."""
+    torch.manual_seed(0)
+    cnet = (torch.randn(3, c, 23, 31, device=DEV) * 2).to(dt).contiguous(memory_format=torch.channels_last)
+    gh = torch.randn(3, hd, 23, 31, device=DEV).to(dt)
+    gx = torch.randn(3, c - hd, 23, 31, device=DEV).to(dt)
+    for use_gh in (True, False):
+        a = cnet.clone().requires_grad_(True)
+        net, inp = fast.context_act(a, hd)
+        assert net.permute(0, 2, 3, 1).is_contiguous() and inp.permute(0, 2, 3, 1).is_contiguous()
+        b = cnet.clone().requires_grad_(True)
+        rn, ri = torch.split(b, [hd, c - hd], dim=1)
+        rn, ri = torch.tanh(rn), torch.relu(ri)
+        torch.testing.assert_close(net.float(), rn.float(), atol=0, rtol=1e-2)
+        assert torch.equal(inp, ri)
+        # without use_gh the net output takes no part: its gradient arrives as None
+        (((net * gh).float().sum() if use_gh else 0) + (inp * gx).float().sum()).backward()
+        (((rn * gh).float().sum() if use_gh else 0) + (ri * gx).float().sum()).backward()
+        torch.testing.assert_close(a.grad.float(), b.grad.float(), atol=1e-2, rtol=2e-2)
