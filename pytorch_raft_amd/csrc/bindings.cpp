@@ -1426,7 +1426,7 @@ void image_prep_(const Tensor& a, const Tensor& b, const Tensor& out) {
 // out[i] = cast(srcs[k][off]) for idx[i] = k << 26 | off (k = 63: zero); srcs contiguous GPU
 // tensors of one dtype and device, out 1-D with idx.numel() elements: fp32 sources -> bf16 /
 // fp16 / fp32 out, or bf16 / fp16 sources -> fp32 out
-void gather_cast_(const std::vector<Tensor>& srcs, const Tensor& idx, const Tensor& out) {
+void gather_cast_(const std::vector<Tensor>& srcs, const Tensor& idx, const Tensor& out, int64_t lo_from) {
   TORCH_CHECK(!srcs.empty() && (int64_t)srcs.size() <= RAFT_GATHER_MAX, "gather: 1..",
               RAFT_GATHER_MAX, " sources");
   TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kInt && idx.is_contiguous() && idx.dim() == 1,
@@ -1440,6 +1440,9 @@ void gather_cast_(const std::vector<Tensor>& srcs, const Tensor& idx, const Tens
   TORCH_CHECK(it == at::kFloat || ot == at::kFloat, "gather: 16-bit sources need an fp32 output");
   GatherSrcs gs{};
   gs.n = (int)srcs.size();
+  // lo_from >= 0: sources [lo_from, n) give split-fp32 residuals (fp32 sources, bf16 output)
+  gs.lo_from = lo_from < 0 ? RAFT_GATHER_MAX : (int)lo_from;
+  TORCH_CHECK(lo_from < 0 || (it == at::kFloat && ot == at::kBFloat16), "gather: residuals need fp32 -> bf16");
   for (int k = 0; k < gs.n; ++k) {
     TORCH_CHECK(srcs[k].is_cuda() && srcs[k].scalar_type() == it && srcs[k].is_contiguous() &&
                 srcs[k].device() == idx.device() && srcs[k].numel() <= (1 << 26),
@@ -1925,7 +1928,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx, Tensor? dy2=None, Tensor? yres=None, Tensor(e!)? gout=None) -> ()");
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
-  m.def("gather_cast_(Tensor[] srcs, Tensor idx, Tensor(a!) out) -> ()");
+  m.def("gather_cast_(Tensor[] srcs, Tensor idx, Tensor(a!) out, int lo_from=-1) -> ()");
   m.def("image_prep_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("ctx_act_(Tensor cnet, int hdim, Tensor(a!) h, Tensor(b!) x) -> ()");
   m.def("ctx_act_bwd_(Tensor? gh, Tensor? gx, Tensor h, Tensor x, Tensor(a!) gin) -> ()");

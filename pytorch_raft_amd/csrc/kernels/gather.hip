@@ -57,6 +57,8 @@ __global__ __launch_bounds__(256) void gather_cast_kernel(GatherSrcs s, const in
       const int k = (int)((uint32_t)e[u] >> 26);
       const int off = e[u] & ((1 << 26) - 1);
       v[u] = k == RAFT_GATHER_ZERO ? 0.f : load1<IT>(s.p[k], off);
+      // split-fp32 weight packs: the residual of the bf16 rounding (bf16(v - bf16(v)) stored)
+      if (k >= s.lo_from && k != RAFT_GATHER_ZERO) v[u] -= __bfloat162float(__float2bfloat16(v[u]));
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)

@@ -416,6 +416,7 @@ void launch_adamw_multi(const AdamTensor* tab, const int* cum, int T, int nchunk
 struct GatherSrcs {
   const void* p[RAFT_GATHER_MAX];
   int n;
+  int lo_from;   // sources k >= lo_from yield the split-fp32 residual v - bf16(v) (bf16 output)
 };
 // out[i] = cast(p[idx[i] >> 26][idx[i] & (2^26 - 1)]), 0 for the zero slot; it / ot (source /
 // output type): 0 bf16, 1 fp16, 2 fp32 -- fp32 -> any, or bf16 / fp16 -> fp32

@@ -50,16 +50,20 @@ def gather_index(flat_ids, numels):
     return code.to(torch.int32)
 
 
-def gather_cast(srcs, code, out):
-    """out[i] = srcs[k][off] cast to out.dtype for code[i] = k << 26 | off (k = 63: zero):
+def gather_cast(srcs, code, out, lo_from=-1):
+    """out[i] = srcs[k][off] cast to out.dtype for code[i] = k << 26 | off (k = 63: zero);
+    sources k >= lo_from (>= 0) give the split-fp32 residual v - bf16(v) instead (bf16 out):
     the native one-launch gather on the GPU; the same values by torch ops on the CPU (tests)."""
     if out.device.type == 'cuda':
-        _ext.ops().gather_cast_(list(srcs), code, out)
+        _ext.ops().gather_cast_(list(srcs), code, out, int(lo_from))
         return out
     c = code.long() & 0xFFFFFFFF
     k, off = c >> 26, c & ((1 << 26) - 1)
     starts = torch.tensor([0] + [int(t.numel()) for t in srcs], dtype=torch.long).cumsum(0)
     flat = torch.cat([t.reshape(-1).float() for t in srcs] + [torch.zeros(1)])
+    if lo_from >= 0:
+        lo = flat[starts[lo_from]:starts[-1]]
+        flat[starts[lo_from]:starts[-1]] = lo - lo.to(torch.bfloat16).float()
     pos = torch.where(k == 63, starts[-1], starts[k.clamp(max=len(srcs) - 1)] + off)
     out.copy_(flat[pos])
     return out

@@ -118,6 +118,65 @@ def _packed(cache, weight, cpad, adjoint):
     return w
 
 
+_PREPACK_PLANS = {}
+
+
+def _prepack_plan(shapes):
+    """Gather codes of every split-packed weight ([w_hi | w_hi | w_lo] per tap, forward and
+    adjoint, as _pack3 lays them out) of convs with ``shapes``: built once per geometry by running
+    the packing on element-id tensors (float64 ids, 0 = zero padding); ids past the weights'
+    total are the same elements' residual halves (gather sources n..2n-1)."""
+    if shapes in _PREPACK_PLANS:
+        return _PREPACK_PLANS[shapes]
+    numels = [co * ci * kh * kw for co, ci, kh, kw in shapes]
+    total = sum(numels)
+    parts, views, off = [], [], 0
+    for (co, ci, kh, kw), n in zip(shapes, numels):
+        ids = torch.arange(n, dtype=torch.float64).view(co, ci, kh, kw) + off + 1
+        off += n
+        for adjoint in (False, True):
+            src = ids.flip(2, 3).transpose(0, 1) if adjoint else ids
+            seg = src.shape[1]
+            cpad = C.round_up(seg, 64)
+            w3 = torch.cat([src, src, src + total], dim=1)   # [hi | hi | lo]
+            t = C.pack_weight(w3, [seg] * 3, [cpad] * 3, dtype=torch.float64)
+            views.append((adjoint, cpad, tuple(t.shape)))
+            parts.append(t.reshape(-1))
+    e = torch.cat(parts).round().long() - 1
+    e[e < 0] = 2 * total                                    # zero padding -> the zero slot
+    plan = (C.gather_index(e, numels + numels), views)
+    _PREPACK_PLANS[shapes] = plan
+    return plan
+
+
+def prepack(pairs):
+    """Split-pack the weights of several fp32 convs in ONE gather launch into the current scope's
+    pack cache (what :func:`_packed` would build per conv with ~10 small kernels, forward and
+    adjoint).  ``pairs`` = [(weight as the convs will see it, fp32 contiguous source of the
+    same values)]; at most GATHER_MAX / 2 convs per launch."""
+    cache = _ACTIVE.get('packed')
+    if cache is None or not pairs:
+        return
+    half = C.GATHER_MAX // 2
+    for i in range(0, len(pairs), half):
+        chunk = pairs[i:i + half]
+        shapes = tuple(tuple(w.shape) for w, _ in chunk)
+        dev = chunk[0][1].device
+        code, views = _prepack_plan(shapes)
+        if code.device != dev:
+            code = code.to(dev)
+            _PREPACK_PLANS[shapes] = (code, views)
+        srcs = [src for _, src in chunk]
+        out = torch.empty(code.numel(), device=dev, dtype=torch.bfloat16)
+        C.gather_cast(srcs + srcs, code, out, lo_from=len(srcs))
+        off = 0
+        for j, (adjoint, cpad, shape) in enumerate(views):
+            w = chunk[j // 2][0]
+            n = shape[0] * shape[1]
+            cache[(w.data_ptr(), w._version, tuple(w.shape), cpad, adjoint)] = out[off:off + n].view(shape)
+            off += n
+
+
 class _ModState:
     """One MfmaConv2d module within one decode: its detached parameters, their split packs, and
     the (split output gradient, split input) pairs of every call, whose weight / bias gradients

@@ -580,13 +580,16 @@ def _conv(ps, x, conv, with_bias=False):
     return _conv_one(ps, x, conv, with_bias)
 
 
+def _split_geom(conv):
+    k = conv.kernel_size
+    return (conv.stride == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
+            and conv.padding == (k[0] // 2, k[1] // 2))
+
+
 def _split_ok(x, conv):
     """fp32 stride-1 'same' conv on the split-bf16 MFMA kernels (ops/conv_fp32.py)."""
     from . import conv_fp32
-    k = conv.kernel_size
-    return (x.dtype == torch.float32 and conv.stride == (1, 1) and conv.dilation == (1, 1)
-            and conv.groups == 1 and conv.padding == (k[0] // 2, k[1] // 2)
-            and conv_fp32.fits(x, conv.out_channels))
+    return x.dtype == torch.float32 and _split_geom(conv) and conv_fp32.fits(x, conv.out_channels)
 
 
 def _conv_one(ps, x, conv, with_bias=False):
@@ -724,7 +727,14 @@ def encoder_forward(enc, x):
         if counters:
             with torch.no_grad():
                 torch._foreach_add_(counters, 1)
-        return _encoder_body(_Pass(*cast_conv_weights(convs, dt)), enc, x, dt)
+        ps = _Pass(*cast_conv_weights(convs, dt))
+        if dt == torch.float32:
+            # fp32 schedule: every split-conv's [w_hi | w_hi | w_lo] packs (forward and adjoint)
+            # in one gather launch instead of ~10 small kernels per conv and direction
+            from . import conv_fp32
+            conv_fp32.prepack([(ps.weights[c], c.weight.detach().float().contiguous())
+                               for c in convs if c in ps.weights and _split_geom(c)])
+        return _encoder_body(ps, enc, x, dt)
 
 
 def _encoder_body(ps, enc, x, dt=torch.bfloat16):

@@ -62,3 +62,20 @@ def test_image_prep_matches_eager(ext_ops, dt):
     out = torch.empty(6, 3, 37, 53, device=DEV, dtype=dt, memory_format=torch.channels_last)
     ext_ops.image_prep_(a, b, out)
     assert torch.equal(out, ref)
+
+
+def test_gather_split_residual_sources(ext_ops):
+    """lo_from: sources from that index on yield bf16(v - bf16(v)) -- the split-fp32 weight packs'
+    w_lo -- while the others yield bf16(v)."""
+    g = torch.Generator().manual_seed(2)
+    numels = [500, 37, 1200]
+    srcs = [torch.randn(n, generator=g).to(DEV) for n in numels]
+    total = sum(numels)
+    ids = torch.randint(0, 2 * total + 1, (20000,), generator=g)
+    out = torch.empty(ids.numel(), device=DEV, dtype=torch.bfloat16)
+    ext_ops.gather_cast_(srcs + srcs, gather_index(ids, numels + numels).to(DEV), out, len(srcs))
+    flat = torch.cat(srcs)
+    hi = flat.to(torch.bfloat16)
+    lo = (flat - hi.float()).to(torch.bfloat16)
+    ref = torch.cat([hi, lo, torch.zeros(1, device=DEV, dtype=torch.bfloat16)])[ids.to(DEV)]
+    assert torch.equal(out, ref)

@@ -101,3 +101,21 @@ def test_batched_encoder_weight_cast():
     for i, c in enumerate(convs):
         ref = 2 * (i + 1) * c.weight.to(torch.bfloat16).float()
         torch.testing.assert_close(c.weight.grad, ref, rtol=1e-2, atol=1e-3)
+
+
+def test_fp32_prepack_matches_per_conv_split_packs():
+    """conv_fp32.prepack (one gather over all convs, residual halves from the same sources) lays
+    out exactly the [w_hi | w_hi | w_lo] forward and adjoint packs _pack3 builds per conv."""
+    from pytorch_raft_amd.ops import conv_fp32
+    g = torch.Generator().manual_seed(0)
+    ws = [torch.randn(s, generator=g) for s in [(64, 64, 3, 3), (96, 64, 3, 3), (128, 96, 3, 3),
+                                                 (96, 96, 1, 1)]]
+    with conv_fp32.enabled(True):
+        conv_fp32.prepack([(w, w) for w in ws])
+        cache = conv_fp32._ACTIVE['packed']
+        for w in ws:
+            co, ci = w.shape[:2]
+            fwd = conv_fp32._pack3(w, C.round_up(ci, 64))
+            adj = conv_fp32._pack3(w.flip(2, 3).transpose(0, 1).contiguous(), C.round_up(co, 64))
+            assert torch.equal(cache[(w.data_ptr(), w._version, tuple(w.shape), C.round_up(ci, 64), False)], fwd)
+            assert torch.equal(cache[(w.data_ptr(), w._version, tuple(w.shape), C.round_up(co, 64), True)], adj)
