@@ -259,7 +259,10 @@ class _PackPlan:
         gidx = torch.cat(parts).round().long() - 1
         gidx[gidx < 0] = total
         # (parameter, offset) codes of the native gather: the parameters are read in place
-        self.widx = C.gather_index(gidx, self.numels).to(device)
+        widx = C.gather_index(gidx, self.numels)
+        if spl:
+            widx, self.views = self._split_codes(widx, design)
+        self.widx = widx.to(device)
         self.bshapes = [(s.name, b_idx[s.name].numel()) for s in SPECS]
         bidx = torch.cat([b_idx[s.name].reshape(-1) for s in SPECS]).round().long() - 1
         bidx[bidx < 0] = total   # padded rows (row_pad) read the zero slot
@@ -285,6 +288,31 @@ class _PackPlan:
         assert (uidx >= 0).all(), 'every parameter element must have a gradient slot'
         self.dw_total = pos
         self.uidx = C.gather_index(uidx, [pos]).to(device)   # single source: the gradient buffer
+
+
+    def _split_codes(self, widx, design):
+        """The fp32 schedule's packs straight from the parameters: per tap [w_hi | w_hi | w_lo]
+        (C.split_weight's layout) with the w_lo codes on the residual sources n..2n-1 of the
+        gather (lo_from = n); the VALU flow-head tables stay plain bf16 casts."""
+        n_src = len(self.numels)
+        c = widx.long() & 0xFFFFFFFF
+        parts, views, off = [], [], 0
+        for kind, name, shape in self.views:
+            n = shape[0] * shape[1]
+            cv = c[off:off + n].view(shape)
+            off += n
+            if name in ('fh2f', 'fh2d'):
+                parts.append(cv.reshape(-1))
+                views.append((kind, name, shape))
+                continue
+            t = _taps_of(design, kind, name)
+            cv3 = cv.view(shape[0], t, shape[1] // t)
+            lo = torch.where((cv3 >> 26) == 63, cv3, cv3 + (n_src << 26))
+            parts.append(torch.cat([cv3, cv3, lo], 2).reshape(-1))
+            views.append((kind, name, (shape[0], 3 * shape[1])))
+        sc = torch.cat(parts)
+        sc = torch.where(sc >= 2 ** 31, sc - 2 ** 32, sc)   # uint32 codes as int32
+        return sc.to(torch.int32), views
 
 
 def _plan(ub, need_grad, device, design=FULL, spl=False):
@@ -332,19 +360,19 @@ class _Packed:
         self.kpad = plan.kpad
         with torch.no_grad():
             srcs = [p.detach().float().contiguous() for p in params]
-            # every kernel-layout weight in ONE gather + cast launch (csrc/kernels/gather.hip)
+            # every kernel-layout weight in ONE gather + cast launch (csrc/kernels/gather.hip);
+            # fp32 schedule: straight into the split [w_hi | w_hi | w_lo] packs (residual
+            # halves from the second copy of the sources)
             packed = torch.empty(plan.widx.numel(), device=device,
-                                 dtype=torch.float32 if self.spl else dtype)
-            C.gather_cast(srcs, plan.widx, packed)
+                                 dtype=torch.bfloat16 if self.spl else dtype)
+            if self.spl:
+                C.gather_cast(srcs + srcs, plan.widx, packed, lo_from=len(srcs))
+            else:
+                C.gather_cast(srcs, plan.widx, packed)
             off = 0
             for kind, name, shape in plan.views:
                 n = shape[0] * shape[1]
-                v = packed[off:off + n].view(shape)
-                if self.spl:
-                    # the VALU kernels' flow_head.conv2 tables are not used by the split convs
-                    v = (v.to(torch.bfloat16) if name in ('fh2f', 'fh2d')
-                         else C.split_weight(v, _taps_of(design, kind, name)))
-                {'w': self.w, 'wd': self.wd, 'x': self.x}[kind][name] = v
+                {'w': self.w, 'wd': self.wd, 'x': self.x}[kind][name] = packed[off:off + n].view(shape)
                 off += n
             bias = torch.empty(plan.bidx.numel(), device=device)
             C.gather_cast(srcs, plan.bidx, bias)

@@ -119,3 +119,21 @@ def test_fp32_prepack_matches_per_conv_split_packs():
             adj = conv_fp32._pack3(w.flip(2, 3).transpose(0, 1).contiguous(), C.round_up(co, 64))
             assert torch.equal(cache[(w.data_ptr(), w._version, tuple(w.shape), C.round_up(ci, 64), False)], fwd)
             assert torch.equal(cache[(w.data_ptr(), w._version, tuple(w.shape), C.round_up(co, 64), True)], adj)
+
+
+def test_split_pack_plan_matches_split_weight():
+    """fp32 schedule: the one-gather split packs equal the fp32 packs run through
+    C.split_weight ([w_hi | w_hi | w_lo] per tap) view by view."""
+    ub = _ub()
+    params = U.flat_params(ub)
+    pk = U._Packed(ub, params, torch.device('cpu'), need_grad=True, dtype=torch.float32)
+    with torch.no_grad():
+        w, wd, b, x = U._pack_layers(U.module_params(ub), True, torch.float32, spl=True)
+    for kind, d, ref in (('w', pk.w, w), ('wd', pk.wd, wd)):
+        assert set(d) == set(ref), kind
+        for name in ref:
+            exp = C.split_weight(ref[name], U._taps_of(U.FULL, kind, name))
+            assert torch.equal(d[name], exp), (kind, name)
+    for name in ('zrq1', 'zrq2'):
+        assert torch.equal(pk.x[name], C.split_weight(x[name], U._taps_of(U.FULL, 'x', name))), name
+    assert torch.equal(pk.x['fh2f'], x['fh2f'].to(torch.bfloat16))
