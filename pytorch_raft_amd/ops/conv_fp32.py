@@ -340,13 +340,11 @@ class _SplitConv(torch.autograd.Function):
                              memory_format=torch.channels_last)
             C.conv_fwd([(gs, 0, cop), (gs, cop, cop), (gs, 0, cop)], _packed(ctx.packed, weight, cop, True), None,
                        (kh, kw), pad, cin, C.EPI_F32, [dx.permute(0, 2, 3, 1)], [0])
-        need_b = ctx.has_bias and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] and C._taps_ok([0], [cp], (kh, kw)):
             # ONE tap-fused launch of the three products g_hi x_hi + g_lo x_hi + g_hi x_lo
-            # (split=True, the fused decode's split weight gradient) and the bias sum with it
+            # (split=True, the fused decode's split weight gradient)
             dwp = torch.zeros(cout, kh * kw * cp, device=g.device)
-            db = torch.zeros(cout, device=g.device) if need_b else None
-            C.conv_wgrad_multi([(gs, [xs])], 0, [0], [cp], (kh, kw), pad, cout, dwp, db, split=True)
+            C.conv_wgrad_multi([(gs, [xs])], 0, [0], [cp], (kh, kw), pad, cout, dwp, None, split=True)
             dw = C.unpack_weight_grad(dwp, cout, [cin], [cp], (kh, kw))
         elif ctx.needs_input_grad[1]:
             k = kh * kw
@@ -356,7 +354,9 @@ class _SplitConv(torch.autograd.Function):
             _wgrad(gs, cop, xs, [0], [cp], (kh, kw), pad, cout, d2)
             g1 = C.unpack_weight_grad(d1, cout, [cin, cin], [cp, cp], (kh, kw))
             dw = g1[:, :cin] + g1[:, cin:] + C.unpack_weight_grad(d2, cout, [cin], [cp], (kh, kw))
-        if need_b and db is None:
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            # the fp32 gradient's exact sum (the encoders fold their conv biases into the norms:
+            # only bias-carrying calls pay this reduce)
             db = g.sum((0, 2, 3))
         return dx, dw, db, None
 
