@@ -1236,6 +1236,17 @@ void check_cl16(at::ScalarType st, const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name, ": must be channels_last");
   TORCH_CHECK(t.size(1) % 8 == 0 && t.size(1) <= 256, name, ": channels must be a multiple of 8, <= 256");
 }
+// optional split-bf16 operand buffer of an fp32 NCHW-shaped channels_last tensor x: contiguous
+// (N, H, W, 2 spad) bf16 with spad >= C a multiple of 8 -> (pointer, spad)
+std::pair<uint16_t*, int> opt_split(const c10::optional<Tensor>& t, const Tensor& x, const char* name) {
+  if (!t.has_value() || !t->defined()) return {nullptr, 0};
+  TORCH_CHECK(x.scalar_type() == at::kFloat, name, ": split operands are for fp32 tensors");
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->dim() == 4 &&
+                  t->size(0) == x.size(0) && t->size(1) == x.size(2) && t->size(2) == x.size(3) &&
+                  t->size(3) % 16 == 0 && t->size(3) / 2 >= x.size(1),
+              name, ": must be a contiguous (N, H, W, 2 spad) bf16 tensor, spad >= C");
+  return {u16m(*t), (int)(t->size(3) / 2)};
+}
 const float* opt_f32(const c10::optional<Tensor>& t, int64_t n, const char* name) {
   if (!t.has_value() || !t->defined()) return nullptr;
   check_cuda_f32(*t, name);
@@ -1249,7 +1260,7 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
                               const c10::optional<Tensor>& cbias,
                               const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
                               double momentum, double eps, const c10::optional<Tensor>& res,
-                              const Tensor& y) {
+                              const Tensor& y, const c10::optional<Tensor>& ysplit) {
   const at::ScalarType st = opnorm(x);
   check_cl16(st, x, "x");
   check_cl16(st, y, "y");
@@ -1286,8 +1297,9 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
                        (int)mode, nblk, gp, bp, cb, rm, rv, (float)momentum, (float)eps,
                        mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
                        shift.data_ptr<float>(), norm_ty(st), cur_stream());
+  const auto ys = opt_split(ysplit, x, "ysplit");
   launch_norm_apply(xp, scale.data_ptr<float>(), shift.data_ptr<float>(), (int)N, (int)HW, (int)C,
-                    (int)relu, rp, u16m(y), norm_ty(st), cur_stream());
+                    (int)relu, rp, u16m(y), norm_ty(st), cur_stream(), ys.first, ys.second);
   return {mean, invstd};
 }
 
@@ -1297,7 +1309,7 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y
                const c10::optional<Tensor>& beta, const c10::optional<Tensor>& dgamma,
                const c10::optional<Tensor>& dbeta, const c10::optional<Tensor>& dcbias,
                const Tensor& dx, const c10::optional<Tensor>& dy2, const c10::optional<Tensor>& yres,
-               const c10::optional<Tensor>& gout) {
+               const c10::optional<Tensor>& gout, const c10::optional<Tensor>& dxsplit) {
   const at::ScalarType st = opnorm(dy);
   check_cl16(st, dy, "dy");
   check_cl16(st, x, "x");
@@ -1343,11 +1355,12 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y
   } else {
     TORCH_CHECK(!(dy2.has_value() && dy2->defined()), "dy2 needs yres");
   }
+  const auto dxs = opt_split(dxsplit, x, "dxsplit");
   launch_norm_bwd(u16(dy),
                   u16(x), yp, mean.data_ptr<float>(),
                   invstd.data_ptr<float>(), (int)N, (int)HW, (int)C, (int)mode, (int)relu, gp, bp,
                   part.data_ptr<float>(), nblk, ppb, coef.data_ptr<float>(), dg, db, dc,
-                  u16m(dx), d2, yr, go, norm_ty(st), cur_stream());
+                  u16m(dx), d2, yr, go, norm_ty(st), cur_stream(), dxs.first, dxs.second);
 }
 
 // context-encoder output: cnet (B,C,H,W) channels_last bf16 / fp16 -> h (B,H,W,hdim) =
@@ -1924,8 +1937,8 @@ TORCH_LIBRARY(raft_amd, m) {
     std::vector<int> r(rows.begin(), rows.end());
     return conv_import_tuned(r.data(), (int)(r.size() / 13));
   });
-  m.def("norm_fwd_(Tensor x, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor? cbias, Tensor(a!)? rmean, Tensor(b!)? rvar, float momentum, float eps, Tensor? res, Tensor(c!) y) -> Tensor[]");
-  m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx, Tensor? dy2=None, Tensor? yres=None, Tensor(e!)? gout=None) -> ()");
+  m.def("norm_fwd_(Tensor x, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor? cbias, Tensor(a!)? rmean, Tensor(b!)? rvar, float momentum, float eps, Tensor? res, Tensor(c!) y, Tensor(d!)? ysplit=None) -> Tensor[]");
+  m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx, Tensor? dy2=None, Tensor? yres=None, Tensor(e!)? gout=None, Tensor(f!)? dxsplit=None) -> ()");
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
   m.def("gather_cast_(Tensor[] srcs, Tensor idx, Tensor(a!) out, int lo_from=-1) -> ()");

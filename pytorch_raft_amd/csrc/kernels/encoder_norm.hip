@@ -116,6 +116,31 @@ __device__ __forceinline__ V8<TY> mask_pos(const V8<TY>& d, const V8<TY>& o) {
   return r;
 }
 
+// fp32 schedule: the 8 values of channel group g of pixel pix also as the split-bf16 operand of
+// the consuming conv ([hi | lo] halves of a (P, 2 spad) bf16 buffer, ops/conv_fp32.py's
+// split_hilo layout); the pixel's last group also zeroes the padding channels [C, spad) of both
+// halves
+__device__ __forceinline__ void store_split8(uint16_t* __restrict__ s, int spad, int64_t pix, int g,
+                                             int cg, const float (&f)[8]) {
+  uint32_t wh[4], wl[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint16_t h0 = raft_f32_to_bf16(f[2 * k]), h1 = raft_f32_to_bf16(f[2 * k + 1]);
+    const uint16_t l0 = raft_f32_to_bf16(f[2 * k] - raft_bf16_to_f32(h0));
+    const uint16_t l1 = raft_f32_to_bf16(f[2 * k + 1] - raft_bf16_to_f32(h1));
+    wh[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+    wl[k] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+  }
+  uint16_t* o = s + pix * 2 * spad + g * 8;
+  *reinterpret_cast<uint4*>(o) = make_uint4(wh[0], wh[1], wh[2], wh[3]);
+  *reinterpret_cast<uint4*>(o + spad) = make_uint4(wl[0], wl[1], wl[2], wl[3]);
+  if (g == cg - 1)
+    for (int c = cg * 8; c < spad; c += 8) {
+      *reinterpret_cast<uint4*>(s + pix * 2 * spad + c) = make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(s + pix * 2 * spad + spad + c) = make_uint4(0, 0, 0, 0);
+    }
+}
+
 // The forward's per-(group, channel) affine of the normalised value, evaluated with exactly the
 // float expressions of norm_finalize_kernel (so a backward ReLU mask recomputed from x matches the
 // forward's y > 0 without reading y).
@@ -329,7 +354,8 @@ __global__ __launch_bounds__(NT) void norm_apply_kernel(const uint16_t* __restri
                                                         const float* __restrict__ shift, int HW,
                                                         int C, int64_t nvec, int relu,
                                                         const uint16_t* __restrict__ res,
-                                                        uint16_t* __restrict__ y) {
+                                                        uint16_t* __restrict__ y,
+                                                        uint16_t* __restrict__ ys, int spad) {
   const int cg = C / 8;
   const int64_t step = (int64_t)gridDim.x * blockDim.x;
   int cur = -1;
@@ -360,6 +386,7 @@ __global__ __launch_bounds__(NT) void norm_apply_kernel(const uint16_t* __restri
       for (int i = 0; i < 8; ++i) f[i] = fmaxf(f[i] + r[i], 0.f);
     }
     st8<TY>(y, v * 8, pack8<TY>(f));
+    if (ys != nullptr) store_split8(ys, spad, pix, g, cg, f);
   }
 }
 
@@ -631,7 +658,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, const uint16_t* __restrict__ y,
     const float* __restrict__ coef, int HW, int C, int per_image, int64_t nvec, int relu,
     uint16_t* __restrict__ dx, const float* __restrict__ pg, int groups, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, float* __restrict__ dcbias) {
+    float* __restrict__ dbeta, float* __restrict__ dcbias, uint16_t* __restrict__ dxs, int spad) {
   const int cg = C / 8;
   if (pg != nullptr && blockIdx.x == 0) {
     // parameter gradients: the groups' contributions summed in a fixed order
@@ -680,6 +707,7 @@ __global__ __launch_bounds__(NT) void norm_bwd_apply_kernel(
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[i] = A[i] * d[i] + Bp[i] * xv[i] + Cp[i];
     st8<TY>(dx, v * 8, pack8<TY>(o));
+    if (dxs != nullptr) store_split8(dxs, spad, pix, g, cg, o);
   }
 }
 
@@ -816,15 +844,17 @@ void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, i
 }
 
 void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift, int N, int HW,
-                       int C, int relu, const uint16_t* res, uint16_t* y, int f16, hipStream_t stream) {
+                       int C, int relu, const uint16_t* res, uint16_t* y, int f16, hipStream_t stream,
+                       uint16_t* ys, int spad) {
+  if (f16 != 2) ys = nullptr;   // split operands exist for the fp32 schedule only
   const int64_t nvec = (int64_t)N * HW * C / 8;
   const int bt = (NT / (C / 8)) * (C / 8);  // multiple of the channel-group count
   if (f16 == 2) hipLaunchKernelGGL(norm_apply_kernel<2>, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
-                     C, nvec, relu, res, y);
+                     C, nvec, relu, res, y, ys, spad);
   else if (f16) hipLaunchKernelGGL(norm_apply_kernel<1>, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
-                     C, nvec, relu, res, y);
+                     C, nvec, relu, res, y, ys, spad);
   else hipLaunchKernelGGL(norm_apply_kernel<0>, dim3(grid_for(nvec)), dim3(bt), 0, stream, x, scale, shift, HW,
-                     C, nvec, relu, res, y);
+                     C, nvec, relu, res, y, ys, spad);
 }
 
 void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_t n,
@@ -848,7 +878,9 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
                      int N, int HW, int C, int mode, int relu, const float* gamma,
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
                      float* dgamma, float* dbeta, float* dcbias, uint16_t* dx,
-                     const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int f16, hipStream_t stream) {
+                     const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int f16, hipStream_t stream,
+                     uint16_t* dxs, int spad) {
+  if (f16 != 2) dxs = nullptr;
   const int per_image = mode == 0 ? 1 : 0;
   const int groups = per_image ? N : 1;
   const int cnt = per_image ? HW : N * HW;
@@ -892,11 +924,11 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
   }
   const int64_t nvec = (int64_t)N * HW * C / 8;
   if (f16 == 2) hipLaunchKernelGGL(norm_bwd_apply_kernel<2>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
-                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias);
+                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias, dxs, spad);
   else if (f16) hipLaunchKernelGGL(norm_bwd_apply_kernel<1>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
-                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias);
+                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias, dxs, spad);
   else hipLaunchKernelGGL(norm_bwd_apply_kernel<0>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
-                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias);
+                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias, dxs, spad);
 }
 
 void launch_ctx_act(const uint16_t* in, int64_t P, int C, int hdim, uint16_t* h, uint16_t* x, int f16,

@@ -363,8 +363,10 @@ void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, i
                           int nblk, const float* gamma, const float* beta, const float* cbias,
                           float* rmean, float* rvar, float momentum, float eps, float* mean,
                           float* invstd, float* scale, float* shift, int f16, hipStream_t stream);
+// ys (nullable, fp32 only): y also as the split-bf16 conv operand, (N*HW, 2 spad) [hi | lo]
 void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift, int N, int HW,
-                       int C, int relu, const uint16_t* res, uint16_t* y, int f16, hipStream_t stream);
+                       int C, int relu, const uint16_t* res, uint16_t* y, int f16, hipStream_t stream,
+                       uint16_t* ys = nullptr, int spad = 0);
 void launch_add_relu(const uint16_t* a, const uint16_t* b, uint16_t* out, int64_t n,
                      int f16, hipStream_t stream);
 // context-encoder output: in (P pixels x C, NHWC) -> h = tanh(in[:, :hdim]) (P x hdim), x =
@@ -380,12 +382,14 @@ void launch_relu_mask(const uint16_t* dy, const uint16_t* dy2, const uint16_t* y
 // yres (nullable): dy is the gradient of a residual block's output relu(branch + res) = yres;
 // g = (dy [+ dy2]) * [yres > 0] is formed in the statistics pass and stored to gout (the
 // residual's gradient), and the norm backward runs on it (the block-end ReLU mask fused)
+// dxs (nullable, fp32 only): dx also as the split-bf16 operand (N*HW, 2 spad) [hi | lo]
 void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, const float* mean,
                      const float* invstd,
                      int N, int HW, int C, int mode, int relu, const float* gamma,
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
                      float* dgamma, float* dbeta, float* dcbias, uint16_t* dx,
-                     const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int f16, hipStream_t stream);
+                     const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int f16, hipStream_t stream,
+                     uint16_t* dxs = nullptr, int spad = 0);
 
 // ---- multi-tensor AdamW + global-norm clip + GradScaler unscale / overflow skip (adamw.hip)
 struct AdamTensor {

@@ -49,12 +49,43 @@ def _norm_mode(norm):
     return None
 
 
+def _split_buf(t, pad):
+    """Empty split-pair buffer (N, H, W, 2 pad) bf16 for the fp32 tensor t, or None."""
+    if not pad or t.dtype != torch.float32:
+        return None
+    n, _, h, w = t.shape
+    return torch.empty(n, h, w, 2 * pad, device=t.device, dtype=torch.bfloat16)
+
+
+def _offer(t, buf):
+    if buf is not None:
+        from . import conv_fp32
+        conv_fp32.offer_split(t, buf)
+
+
+def _split_pads(x, conv):
+    """(input, output-gradient) split-operand widths -- the 64-padded channel counts -- of conv
+    applied to x when that call runs as ONE split conv (fp32 schedule, stride-1 'same' geometry,
+    no image chunking), else (0, 0): then nothing is handed over."""
+    if conv is None or x.dtype != torch.float32 or not _split_ok(x, conv):
+        return 0, 0
+    n, _, h, w = x.shape
+    per = max(x[0].numel(), conv.out_channels * h * w) * x.element_size()
+    if n > 1 and n * per > _CONV_BYTES:
+        return 0, 0
+    return _kslot(conv.in_channels), _kslot(conv.out_channels)
+
+
 class _NormAct(torch.autograd.Function):
     """y = act(norm(x + conv_bias)) on channels_last bf16 / fp16; x is the bias-free conv output."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, cbias, norm, mode, relu, holder=None):
+    def forward(ctx, x, gamma, beta, cbias, norm, mode, relu, holder=None, sp=(0, 0)):
+        # sp = (ysp, gsp): fp32 schedule, the consuming / producing conv is a split conv -- y
+        # (its input) and dx (its output gradient) are also written as the split pair
+        # (2 x the 64-padded channels) and handed over (conv_fp32.offer_split)
         y = torch.empty_like(x, memory_format=torch.channels_last)
+        ys = _split_buf(y, sp[0])
         rm = rv = None
         momentum = 0.1
         eps = 1e-5
@@ -68,7 +99,9 @@ class _NormAct(torch.autograd.Function):
                 momentum = norm.momentum if norm.momentum is not None else \
                     1.0 / float(norm.num_batches_tracked.item())
         mean, invstd = _ext.ops().norm_fwd_(x, mode, int(relu), gamma, beta, cbias, rm, rv,
-                                            float(momentum), float(eps), None, y)
+                                            float(momentum), float(eps), None, y, ys)
+        _offer(y, ys)
+        ctx.gsp = sp[1]
         # y is not kept (the backward recomputes the ReLU mask from x) unless an identity-residual
         # consumer stashes its gradient in `holder` (the stem output feeding layer1): the stash
         # is then added where the ReLU mask is applied, in the statistics pass (no add kernel)
@@ -90,19 +123,21 @@ class _NormAct(torch.autograd.Function):
         db = torch.empty(c, device=dev) if ctx.has[1] else None
         dc = torch.empty(c, device=dev) if ctx.has[2] else None
         dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dxs = _split_buf(dx, ctx.gsp)
         stash = ctx.holder.pop('g', None) if ctx.holder is not None else None
         if stash is not None and ctx.relu:
             # g = (dy + stash) [y > 0] formed in the statistics pass (y = relu(norm(x)): the
             # recomputed mask from x is the same one)
             g = torch.empty_like(x, memory_format=torch.channels_last)
             _ext.ops().norm_bwd_(dy, x, None, mean, invstd, ctx.mode, 1, gamma, beta, dg, db, dc,
-                                 dx, stash, y, g)
+                                 dx, stash, y, g, dxs)
         else:
             if stash is not None:
                 dy = dy + stash
             _ext.ops().norm_bwd_(dy, x, None, mean, invstd, ctx.mode, int(ctx.relu), gamma, beta,
-                                 dg, db, dc, dx)
-        return dx, dg, db, dc, None, None, None, None
+                                 dg, db, dc, dx, None, None, None, dxs)
+        _offer(dx, dxs)
+        return dx, dg, db, dc, None, None, None, None, None
 
 
 class _NormActAddRelu(torch.autograd.Function):
@@ -111,8 +146,10 @@ class _NormActAddRelu(torch.autograd.Function):
     so the branch output is never written (`core/extractor.py:47-56`)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, cbias, res, norm, mode, holder, res_holder):
+    def forward(ctx, x, gamma, beta, cbias, res, norm, mode, holder, res_holder, sp=(0, 0)):
         out = torch.empty_like(x, memory_format=torch.channels_last)
+        outs = _split_buf(out, sp[0])   # see _NormAct: the block output's split pair
+        ctx.gsp = sp[1]
         ctx.holder = holder          # receives the NEXT block's residual gradient (see backward)
         ctx.res_holder = res_holder  # this block's residual comes from such a block: stash into it
         rm = rv = None
@@ -129,7 +166,8 @@ class _NormActAddRelu(torch.autograd.Function):
                     1.0 / float(norm.num_batches_tracked.item())
         res = res.contiguous(memory_format=torch.channels_last)
         mean, invstd = _ext.ops().norm_fwd_(x, mode, 1, gamma, beta, cbias, rm, rv, float(momentum),
-                                            float(eps), res, out)
+                                            float(eps), res, out, outs)
+        _offer(out, outs)
         ctx.save_for_backward(x, out, mean, invstd, gamma, beta)
         ctx.mode = mode
         ctx.has = (gamma is not None, beta is not None, cbias is not None)
@@ -151,15 +189,17 @@ class _NormActAddRelu(torch.autograd.Function):
         db = torch.empty(c, device=dev) if ctx.has[1] else None
         dc = torch.empty(c, device=dev) if ctx.has[2] else None
         dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dxs = _split_buf(dx, ctx.gsp)
         # block-end ReLU fused into the norm backward's statistics pass: g = (dout [+ stash]) *
         # [out > 0] is formed there and stored once (it is also the residual's gradient)
         _ext.ops().norm_bwd_(dout, x, None, mean, invstd, ctx.mode, 1, gamma, beta, dg, db, dc, dx,
-                             stash, out, g)
+                             stash, out, g, dxs)
+        _offer(dx, dxs)
         gres = g
         if ctx.res_holder is not None:
             ctx.res_holder['g'] = g
             gres = None
-        return dx, dg, db, dc, gres, None, None, None, None
+        return dx, dg, db, dc, gres, None, None, None, None, None
 
 
 class _StashGrad(torch.autograd.Function):
@@ -614,22 +654,26 @@ def _conv_one(ps, x, conv, with_bias=False):
     return F.conv2d(x, w, b, conv.stride, conv.padding, conv.dilation, conv.groups)
 
 
-def conv_norm_act(ps, x, conv, norm, relu=True, holder=None):
+def conv_norm_act(ps, x, conv, norm, relu=True, holder=None, consumer=None):
+    """``consumer``: the conv that reads this output (fp32 schedule: when both are split convs
+    the norm kernels also write the split operands, see _NormAct)."""
     mode = _norm_mode(norm)
     y = _conv(ps, x, conv)
     y = y.contiguous(memory_format=torch.channels_last)
     gamma = beta = None
     if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and norm.affine:
         gamma, beta = norm.weight, norm.bias
-    out = _NormAct.apply(y, gamma, beta, conv.bias, norm, mode, relu, holder)
+    sp = (_split_pads(y, consumer)[0], _split_pads(x, conv)[1])
+    out = _NormAct.apply(y, gamma, beta, conv.bias, norm, mode, relu, holder, sp)
     if holder is not None:
         ps.holders[id(out)] = (out, holder)
     return out
 
 
-def residual_block(ps, blk, x):
-    """`core/extractor.py:47-56` on the fast path (conv2 + norm2 + ReLU + add + ReLU fused)."""
-    y = conv_norm_act(ps, x, blk.conv1, blk.norm1)
+def residual_block(ps, blk, x, consumer=None):
+    """`core/extractor.py:47-56` on the fast path (conv2 + norm2 + ReLU + add + ReLU fused);
+    ``consumer``: the conv reading the block output (see conv_norm_act)."""
+    y = conv_norm_act(ps, x, blk.conv1, blk.norm1, consumer=blk.conv2)
     if blk.downsample is not None:
         xd = x
         prod = ps.holders.get(id(x)) if _STASH else None
@@ -646,8 +690,9 @@ def residual_block(ps, blk, x):
     if res_holder is not None and res_holder[0] is not x:
         res_holder = None
     holder = {}
+    sp = (_split_pads(y2, consumer)[0], _split_pads(y, blk.conv2)[1])
     out = _NormActAddRelu.apply(y2, gamma, beta, blk.conv2.bias, x, blk.norm2, mode, holder,
-                                res_holder[1] if res_holder is not None else None)
+                                res_holder[1] if res_holder is not None else None, sp)
     ps.holders[id(out)] = (out, holder)
     return out
 
@@ -662,7 +707,7 @@ def residual_block(ps, blk, x):
 _STASH = os.environ.get('RAFT_ENCODER_STASH', '1') != '0'
 
 
-def bottleneck_block(ps, blk, x):
+def bottleneck_block(ps, blk, x, consumer=None):
     """`core/extractor.py:105-116` on the fast path."""
     y = conv_norm_act(ps, x, blk.conv1, blk.norm1)
     y = conv_norm_act(ps, y, blk.conv2, blk.norm2)
@@ -739,12 +784,20 @@ def encoder_forward(enc, x):
 
 def _encoder_body(ps, enc, x, dt=torch.bfloat16):
     x = x.to(dt).contiguous(memory_format=torch.channels_last)
-    # the stem output's identity-residual gradient (layer1's first block) goes to its stash
-    x = conv_norm_act(ps, x, enc.conv1, enc.norm1, holder={} if _STASH else None)
     block_fn = residual_block if enc.block.__name__ == 'ResidualBlock' else bottleneck_block
-    for layer in (enc.layer1, enc.layer2, enc.layer3):
-        for blk in layer:
-            x = block_fn(ps, blk, x)
+    blocks = [blk for layer in (enc.layer1, enc.layer2, enc.layer3) for blk in layer]
+    # the conv reading each block's output: the next block's conv1 when nothing else does (a
+    # downsample conv reads it too); the head after the last block
+    nxt = [b.conv1 if (block_fn is residual_block and b.downsample is None) else None
+           for b in blocks[1:]] + [None if _head_ok(x, enc.conv2, dt) else enc.conv2]
+    first = blocks[0].conv1 if (block_fn is residual_block and blocks[0].downsample is None) else None
+    if dt == torch.float32:
+        from . import conv_fp32
+        conv_fp32.clear_handoff()   # nothing left over from an earlier pass
+    # the stem output's identity-residual gradient (layer1's first block) goes to its stash
+    x = conv_norm_act(ps, x, enc.conv1, enc.norm1, holder={} if _STASH else None, consumer=first)
+    for blk, consumer in zip(blocks, nxt):
+        x = block_fn(ps, blk, x, consumer)
     if _head_ok(x, enc.conv2, dt):
         return _Head1x1.apply(x, enc.conv2.weight, enc.conv2.bias)
     x = _conv(ps, x, enc.conv2, with_bias=True)

@@ -321,3 +321,23 @@ def test_context_act_matches_eager(ext_ops, dt, hd, c):
         (((net * gh).float().sum() if use_gh else 0) + (inp * gx).float().sum()).backward()
         (((rn * gh).float().sum() if use_gh else 0) + (ri * gx).float().sum()).backward()
         torch.testing.assert_close(a.grad.float(), b.grad.float(), atol=1e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize('C', [64, 96])
+def test_norm_split_outputs_match_split_hilo(ext_ops, C):
+    """fp32 schedule: the norm apply passes also write y / dx as the split-bf16 conv operand --
+    bitwise what split_hilo makes of them, padding channels zero."""
+    from pytorch_raft_amd.ops import conv_fp32
+    torch.manual_seed(0)
+    x = torch.randn(2, C, 19, 27, device=DEV).contiguous(memory_format=torch.channels_last)
+    pad = (C + 63) // 64 * 64
+    y = torch.empty_like(x)
+    ys = torch.full((2, 19, 27, 2 * pad), 3.0, device=DEV, dtype=torch.bfloat16)
+    mean, invstd = ext_ops.norm_fwd_(x, 0, 1, None, None, None, None, None, 0.1, 1e-5, None, y, ys)
+    assert torch.equal(ys, conv_fp32._split_nhwc(y, pad))
+    dy = torch.randn(x.shape, device=DEV).contiguous(memory_format=torch.channels_last)
+    dx = torch.empty_like(x)
+    dxs = torch.full((2, 19, 27, 2 * pad), 3.0, device=DEV, dtype=torch.bfloat16)
+    ext_ops.norm_bwd_(dy, x, None, mean, invstd, 0, 1, None, None, None, None, None, dx,
+                      None, None, None, dxs)
+    assert torch.equal(dxs, conv_fp32._split_nhwc(dx, pad))
