@@ -868,10 +868,10 @@ BoxGeo box_geo(int H, int W, int levels, int radius) {
   return g;
 }
 
-template <int R, bool TF16 = false>
+template <int R, bool TF16 = false, bool OUT32 = false>
 __global__ __launch_bounds__(256) void corr_tap_fold_box_kernel(TapList tl, BoxGeo bg, int levels, int B,
                                                                 int H, int W, float inv_sqrt_c,
-                                                                uint16_t* __restrict__ out, int* __restrict__ list) {
+                                                                void* __restrict__ out, int* __restrict__ list) {
   constexpr int D = 2 * R + 1, E = D + 1;
   extern __shared__ float lds_all[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1010,9 +1010,16 @@ __global__ __launch_bounds__(256) void corr_tap_fold_box_kernel(TapList tl, BoxG
     __builtin_amdgcn_wave_barrier();
   }
   }
-  uint32_t* Ob = reinterpret_cast<uint32_t*>(out + ((int64_t)b * N + i) * tl.ldo);
+  // dC row: bf16 pairs (mixed precision: the bf16 GEMMs' operand) or fp32 pairs (fp16 / fp32
+  // schedules: the reference's fp32 correlation gradient)
+  const int64_t row = ((int64_t)b * N + i) * tl.ldo;
+  uint32_t* Ob = reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(out) + row);
+  float2* Of = reinterpret_cast<float2*>(static_cast<float*>(out) + row);
   const float inv_w = 1.0f / (float)W;
-  for (int e2 = N / 2 + lane; e2 < tl.ldo / 2; e2 += 64) Ob[e2] = 0u;
+  for (int e2 = N / 2 + lane; e2 < tl.ldo / 2; e2 += 64) {
+    if constexpr (OUT32) Of[e2] = make_float2(0.f, 0.f);
+    else Ob[e2] = 0u;
+  }
   for (int e2 = lane; e2 < N / 2; e2 += 64) {
     const int e = 2 * e2;
     const int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W;
@@ -1038,7 +1045,8 @@ __global__ __launch_bounds__(256) void corr_tap_fold_box_kernel(TapList tl, BoxG
       }
       sc *= 0.25f;
     }
-    Ob[e2] = (uint32_t)raft_f32_to_bf16(v0 * inv_sqrt_c) | ((uint32_t)raft_f32_to_bf16(v1 * inv_sqrt_c) << 16);
+    if constexpr (OUT32) Of[e2] = make_float2(v0 * inv_sqrt_c, v1 * inv_sqrt_c);
+    else Ob[e2] = (uint32_t)raft_f32_to_bf16(v0 * inv_sqrt_c) | ((uint32_t)raft_f32_to_bf16(v1 * inv_sqrt_c) << 16);
   }
 }
 
@@ -1161,27 +1169,42 @@ bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, 
   }();
   const int64_t P = (int64_t)B * H * W;
   const int lds = corr_tap_reduce_lds_bytes(H, W, levels, radius);
-  if (tl.tf16) {
-    // fp16 tap gradients (fp16 autocast; fp32 dC as the reference's fp32 correlation): the
-    // workgroup-per-pixel fold
-    dim3 grid((unsigned)P);
-    if (radius == 4) hipLaunchKernelGGL((corr_tap_reduce_kernel<4, true>), grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)nullptr);
-    else hipLaunchKernelGGL((corr_tap_reduce_kernel<3, true>), grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)nullptr);
-    return true;
-  }
-  if (mode == 0 && out_bf16 && (W & 1) == 0 && list != nullptr && tl.n <= 32 &&
-      (levels * D * D + 7) / 8 <= 64) {
+  if (mode == 0 && (W & 1) == 0 && list != nullptr && tl.n <= 32 && (levels * D * D + 7) / 8 <= 64) {
+    // union-box fold for every tap type (bf16, fp16, split-fp32 rows) and dC type (bf16 pairs
+    // for the mixed-precision GEMMs, fp32 for the fp16 / fp32 schedules' fp32 correlation)
     const BoxGeo bg = box_geo(H, W, levels, radius);
     const int wpb = 4;
     (void)hipMemsetAsync(list, 0, sizeof(int), stream);
     dim3 grid((unsigned)((P + wpb - 1) / wpb));
     const size_t sh = (size_t)wpb * bg.wave_floats * 4;
-    if (radius == 4) hipLaunchKernelGGL(corr_tap_fold_box_kernel<4>, grid, dim3(64 * wpb), sh, stream, tl, bg, levels, B, H, W, inv_sqrt_c, (uint16_t*)out, list);
-    else hipLaunchKernelGGL(corr_tap_fold_box_kernel<3>, grid, dim3(64 * wpb), sh, stream, tl, bg, levels, B, H, W, inv_sqrt_c, (uint16_t*)out, list);
+#define RAFT_BOX(RR, TF, O32)                                                                        \
+  hipLaunchKernelGGL((corr_tap_fold_box_kernel<RR, TF, O32>), grid, dim3(64 * wpb), sh, stream, tl, bg, \
+                     levels, B, H, W, inv_sqrt_c, out, list)
+    const bool o32 = !out_bf16;
+    if (radius == 4) {
+      if (tl.tf16) { if (o32) RAFT_BOX(4, true, true); else RAFT_BOX(4, true, false); }
+      else { if (o32) RAFT_BOX(4, false, true); else RAFT_BOX(4, false, false); }
+    } else {
+      if (tl.tf16) { if (o32) RAFT_BOX(3, true, true); else RAFT_BOX(3, true, false); }
+      else { if (o32) RAFT_BOX(3, false, true); else RAFT_BOX(3, false, false); }
+    }
+#undef RAFT_BOX
     // the pixels whose windows spread past the box cap (usually none): grid-strided over the list
     dim3 g2((unsigned)std::min<int64_t>(P, 1024));
-    if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_kernel<4>, g2, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)list);
-    else hipLaunchKernelGGL(corr_tap_reduce_kernel<3>, g2, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)list);
+    if (tl.tf16) {
+      if (radius == 4) hipLaunchKernelGGL((corr_tap_reduce_kernel<4, true>), g2, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)list);
+      else hipLaunchKernelGGL((corr_tap_reduce_kernel<3, true>), g2, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)list);
+    } else {
+      if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_kernel<4>, g2, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)list);
+      else hipLaunchKernelGGL(corr_tap_reduce_kernel<3>, g2, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)list);
+    }
+    return true;
+  }
+  if (tl.tf16) {
+    // fp16 tap gradients, other fold modes: the workgroup-per-pixel fold
+    dim3 grid((unsigned)P);
+    if (radius == 4) hipLaunchKernelGGL((corr_tap_reduce_kernel<4, true>), grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)nullptr);
+    else hipLaunchKernelGGL((corr_tap_reduce_kernel<3, true>), grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)nullptr);
     return true;
   }
   if (mode == 2) {

@@ -144,11 +144,12 @@ def test_flow_head2_fp16(ext_ops):
                                atol=1e-2, rtol=1e-3)
 
 
-def test_lookup_and_fold_fp16(ext_ops):
+@pytest.mark.parametrize('w', [31, 32])
+def test_lookup_and_fold_fp16(ext_ops, w):
     """fp16 taps from the fp32 pyramid (the reference's fp32 correlation under fp16 autocast)
-    and the correlation fold from fp16 tap gradients: equal to the bf16 / fp32 paths up to the
-    16-bit rounding of the taps."""
-    b, c, h, w = 2, 256, 23, 31
+    and the correlation fold from fp16 tap gradients (even width: the union-box fold with fp32
+    dC): equal to the bf16 / fp32 paths up to the 16-bit rounding of the taps."""
+    b, c, h = 2, 256, 23
     f1 = torch.randn(b, c, h, w, device=DEV)
     f2 = torch.randn(b, c, h, w, device=DEV)
     pyr = ext_ops.corr_build(f1, f2, 4)
@@ -171,3 +172,9 @@ def test_lookup_and_fold_fp16(ext_ops):
     # the two differ only by the taps' 16-bit rounding (fp16: 11 bits, bf16: 8 bits)
     rel = ((d16 - d32).norm() / d32.norm()).item()
     assert rel < 1e-2, rel
+    # and the fp16 fold is the generic fp32 lookup backward of the fp16-rounded taps
+    gp = [torch.zeros_like(p) for p in pyr]
+    for cc, t in zip(cs, taps):
+        ext_ops.corr_lookup_bwd_(gp, cc, t.to(H16).float().contiguous(), 4)
+    dref = ext_ops.corr_pyr_grad_reduce(gp, 1 / 16)
+    assert ((d16 - dref).norm() / dref.norm()).item() < 1e-5

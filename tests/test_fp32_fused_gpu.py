@@ -148,10 +148,12 @@ def test_split_dgrad_and_wgrad(ext_ops):
     assert _rel(db, 2 * br.grad) < 1e-5
 
 
-def test_split_lookup_patch_and_fold(ext_ops):
+@pytest.mark.parametrize('w', [31, 32])
+def test_split_lookup_patch_and_fold(ext_ops, w):
     """Split taps from the fp32 pyramid == the fp32 lookup to 2^-16; the fold of split tap
-    gradients == the generic fp32 lookup backward; the split im2col patch == the fp32 flow."""
-    b, c, h, w = 2, 256, 23, 31
+    gradients (even width: the union-box fold with fp32 dC) == the generic fp32 lookup
+    backward; the split im2col patch == the fp32 flow."""
+    b, c, h = 2, 256, 23
     f1 = torch.randn(b, c, h, w, device=DEV)
     f2 = torch.randn(b, c, h, w, device=DEV)
     pyr = ext_ops.corr_build(f1, f2, 4)
