@@ -76,7 +76,7 @@ std::vector<Tensor> corr_build(const Tensor& f1, const Tensor& f2, int64_t level
 
 // bf16 fmaps in NHWC memory, (B,H,W,C) contiguous (the channels_last encoder outputs, permuted)
 std::vector<Tensor> corr_build_bf16(const Tensor& f1, const Tensor& f2, int64_t levels,
-                                    bool pyr_bf16, int64_t c_scale) {
+                                    bool pyr_bf16) {
   TORCH_CHECK(f1.is_cuda() && f2.is_cuda() && f1.scalar_type() == at::kBFloat16 &&
                   f2.scalar_type() == at::kBFloat16 && f1.is_contiguous() && f2.is_contiguous(),
               "fmaps must be contiguous bf16 (B,H,W,C) GPU tensors");
@@ -106,7 +106,7 @@ std::vector<Tensor> corr_build_bf16(const Tensor& f1, const Tensor& f2, int64_t 
   launch_corr_build_bf16(reinterpret_cast<const uint16_t*>(f1.data_ptr()),
                          reinterpret_cast<const uint16_t*>(f2.data_ptr()), ptr.data(), hs.data(),
                          ws.data(), (int)B, (int)C, (int)H, (int)W, (int)levels, pyr_bf16,
-                         cur_stream(), (int)c_scale);
+                         cur_stream());
   return out;
 }
 
@@ -1946,7 +1946,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("ctx_act_(Tensor cnet, int hdim, Tensor(a!) h, Tensor(b!) x) -> ()");
   m.def("ctx_act_bwd_(Tensor? gh, Tensor? gx, Tensor h, Tensor x, Tensor(a!) gin) -> ()");
   m.def("corr_otf_window_bwd_(Tensor f1, Tensor[] f2, Tensor[] coords, Tensor[] douts, Tensor(a!) df1, Tensor(b!)[] df2, int radius) -> ()");
-  m.def("corr_build_bf16(Tensor f1, Tensor f2, int levels, bool pyr_bf16=False, int c_scale=0) -> Tensor[]");
+  m.def("corr_build_bf16(Tensor f1, Tensor f2, int levels, bool pyr_bf16=False) -> Tensor[]");
   m.def("conv_wgrad_taps_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, "
         "int kw, int ph, int pw, int cout, Tensor dw, Tensor? db, int splits=0, bool split=False) -> ()");
   m.def("convex_up_fwd(Tensor flow, Tensor mask, bool nhwc=False) -> Tensor");

@@ -372,8 +372,7 @@ void launch_corr_build(const float* f1, const float* f2, float* const* lvl, cons
 
 void launch_corr_build_bf16(const uint16_t* f1, const uint16_t* f2, void* const* lvl, const int* hs,
                             const int* ws, int B, int C, int H, int W, int levels, bool pyr_bf16,
-                            hipStream_t stream, int c_scale) {
-  const float inv_sqrt_c = 1.0f / sqrtf((float)(c_scale > 0 ? c_scale : C));
+                            hipStream_t stream) {
   const int N = H * W;
   const int tiles_i = (int)raft_cdiv(N, BB_I), bands_y = (int)raft_cdiv(H, BB_Y);
   const int tiles_x = (int)raft_cdiv(W, BB_X);
@@ -387,7 +386,7 @@ void launch_corr_build_bf16(const uint16_t* f1, const uint16_t* f2, void* const*
       p.w[l] = l < levels ? ws[l] : 0;
     }
     hipLaunchKernelGGL(corr_build_bf16_kernel<T>, grid, dim3(256), 0, stream, f1, f2, p, C, H, W,
-                       levels, inv_sqrt_c, tiles_i, bands_y, tiles_x);
+                       levels, 1.0f / sqrtf((float)C), tiles_i, bands_y, tiles_x);
   };
   if (pyr_bf16) go((uint16_t*)nullptr);
   else go((float*)nullptr);

@@ -47,23 +47,6 @@ class _State:
         self.pyr_bf16 = False  # bf16 pyramid: NHWC (bf16-output) lookups only
 
 
-# RAFT_CORR_SPLIT_BUILD=0: the fp32 correlation on the fp32 VALU build kernel
-_SPLIT_BUILD = os.environ.get('RAFT_CORR_SPLIT_BUILD', '1') != '0'
-
-
-def _split_build_ok(f):
-    return (_SPLIT_BUILD and f.is_cuda and f.dtype == torch.float32 and f.dim() == 4
-            and f.shape[1] % 64 == 0)
-
-
-def _split_cat(f, parts):
-    """(B,C,H,W) fp32 -> (B,H,W,3C) bf16: the hi (0) / lo (1) halves of f in ``parts`` order."""
-    from .conv_fp32 import _split_nhwc
-    c = f.shape[1]
-    s = _split_nhwc(f, c)                         # (B,H,W,2C) [hi | lo]
-    return torch.cat([s[..., p * c:(p + 1) * c] for p in parts], dim=-1)
-
-
 def _nhwc_bf16(f):
     """(B,C,H,W) bf16 (channels_last memory, as the encoders produce it) -> (B,H,W,C) contiguous."""
     return f.permute(0, 2, 3, 1).contiguous()
@@ -80,14 +63,6 @@ class _AllPairsBuild(torch.autograd.Function):
             f1, f2 = _nhwc_bf16(fmap1), _nhwc_bf16(fmap2)
             pyr = ops.corr_build_bf16(f1, f2, levels, bool(state.pyr_bf16))
             ctx.save_for_backward(f1, f2)
-        elif _split_build_ok(fmap1):
-            # fp32 correlation (fp32 / fp16 schedules) as ONE bf16 MFMA GEMM over the split-fp32
-            # K concatenation [f1_hi | f1_lo | f1_hi] . [f2_hi | f2_hi | f2_lo] (~2^-16, the
-            # split scheme of the fp32 convs) instead of the fp32 VALU GEMM; fp32 pyramid
-            c = fmap1.shape[1]
-            f1s, f2s = _split_cat(fmap1, (0, 1, 0)), _split_cat(fmap2, (0, 0, 1))
-            pyr = ops.corr_build_bf16(f1s, f2s, levels, False, c)
-            ctx.save_for_backward(fmap1, fmap2)
         else:
             pyr = ops.corr_build(fmap1, fmap2, levels)
             ctx.save_for_backward(fmap1, fmap2)

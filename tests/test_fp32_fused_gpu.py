@@ -345,21 +345,3 @@ def test_split_dgrad_1x1_sliced_relu_output(ext_ops, cfg):
     got = _join(out)
     assert (got[..., :256] == 0).all()
     assert _rel(got[..., 256:].permute(0, 3, 1, 2), ref) < 3e-5
-
-
-def test_split_corr_build_vs_fp64(ext_ops):
-    """fp32 correlation as one bf16 MFMA GEMM over the split-fp32 K concatenation
-    (ops/corr.py:_split_cat): every pyramid level within the split scheme's ~2^-16 of fp64."""
-    from pytorch_raft_amd.ops.corr import _split_cat
-    torch.manual_seed(0)
-    b, c, h, w = 2, 256, 22, 30
-    f1 = torch.randn(b, c, h, w, device=DEV)
-    f2 = torch.randn(b, c, h, w, device=DEV)
-    pyr = ext_ops.corr_build_bf16(_split_cat(f1, (0, 1, 0)), _split_cat(f2, (0, 0, 1)), 4, False, c)
-    ref = ext_ops.corr_build(f1, f2, 4)
-    c64 = torch.einsum('bchw,bcxy->bhwxy', f1.double(), f2.double()).reshape(b * h * w, 1, h, w) / c ** 0.5
-    for lvl, (p, r) in enumerate(zip(pyr, ref)):
-        assert p.dtype == torch.float32 and p.shape == r.shape
-        want = c64 if lvl == 0 else F.avg_pool2d(c64, 2 ** lvl, stride=2 ** lvl)
-        want = want.reshape(r.shape)
-        assert _rel(p.double(), want) < 3e-5, lvl
