@@ -93,7 +93,10 @@ def _split_nhwc(x, cpad):
 # Split operands handed over by their producers (the encoders' fp32 norm kernels write a conv's
 # input, or a conv output's gradient, also as the [hi | lo] pair): tensor -> split buffer, taken
 # once by the consuming split conv.  An entry holds its tensor, so no other tensor can reuse its
-# storage while it waits (matching by storage address, layout and version is then exact).
+# storage while it waits (matching by storage address, layout and version is then exact).  Each
+# encoder pass starts by clearing it (encoder.py:_encoder_body): an encoder pass on another
+# thread can only make a consumer fall back to its own split_hilo pass, never hand it a wrong
+# operand.
 _HANDOFF = {}
 
 
