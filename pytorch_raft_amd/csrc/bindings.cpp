@@ -1664,9 +1664,12 @@ Tensor adamw_step_(const std::vector<Tensor>& params, const std::vector<Tensor>&
   const auto dev = params[0].device();
   for (size_t i = 0; i < T; ++i) {
     for (const Tensor* t : {&params[i], &grads[i], &exp_avg[i], &exp_avg_sq[i]}) {
+      // the kernels walk the four tensors as flat arrays: any dense layout, the same for all four
+      // (a channels_last model's weights, their gradients and moments)
       TORCH_CHECK(t->is_cuda() && t->device() == dev && t->scalar_type() == at::kFloat &&
-                      t->is_contiguous() && t->numel() == params[i].numel(),
-                  "adamw: contiguous fp32 tensors of equal size on one GPU");
+                      t->is_non_overlapping_and_dense() && t->strides() == params[i].strides() &&
+                      t->numel() == params[i].numel(),
+                  "adamw: dense fp32 tensors of one size and layout on one GPU");
     }
     TORCH_CHECK(steps[i].is_cuda() && steps[i].device() == dev && steps[i].scalar_type() == at::kFloat &&
                     steps[i].numel() == 1,

@@ -47,14 +47,19 @@ class FusedAdamW(optim.Optimizer):
                 if p.grad is None:
                     continue
                 st = self.state[p]
+                # the native kernels walk parameter, gradient and moments as flat arrays: all
+                # four in the parameter's dense layout (contiguous, or a channels_last model's)
                 if not st:
                     st['step'] = torch.zeros((), dtype=torch.float32, device=p.device)
-                    st['exp_avg'] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                    st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st['exp_avg'] = torch.zeros_like(p)
+                    st['exp_avg_sq'] = torch.zeros_like(p)
                 elif st['step'].device != p.device or st['step'].dtype != torch.float32:
                     st['step'] = st['step'].to(p.device, torch.float32)  # a loaded CPU counter
-                if not p.grad.is_contiguous():
-                    p.grad = p.grad.contiguous()
+                for k in ('exp_avg', 'exp_avg_sq'):
+                    if st[k].stride() != p.stride():  # loaded state / model re-laid out since
+                        st[k] = torch.empty_like(p).copy_(st[k])
+                if p.grad.stride() != p.stride():
+                    p.grad = torch.empty_like(p).copy_(p.grad)
                 ps.append(p)
                 gs.append(p.grad)
                 ms.append(st['exp_avg'])

@@ -57,6 +57,38 @@ def test_fused_adamw_matches_torch(ext_ops, lr_tensor, max_norm):
         assert o_my.last_norm.shape == (2,)
 
 
+def test_fused_adamw_channels_last_params(ext_ops):
+    """A channels_last model's conv weights (bench.py / train.py --channels_last): parameter,
+    gradient and moments are walked flat in the parameter's own dense layout -- including a
+    contiguous gradient and moments loaded before the model was re-laid out."""
+    g = torch.Generator(device='cpu').manual_seed(1)
+    shapes = [(64, 3, 7, 7), (128, 64, 3, 3), (96,)]
+    ref = [torch.randn(s, generator=g).to(DEV) for s in shapes]
+    pr = [torch.nn.Parameter(t.clone()) for t in ref]
+    pm = [torch.nn.Parameter(t.clone().contiguous(memory_format=torch.channels_last) if t.dim() == 4
+                             else t.clone()) for t in ref]
+    o_ref = torch.optim.AdamW(pr, lr=1e-3, weight_decay=1e-4, eps=1e-8)
+    o_my = FusedAdamW(pm, lr=1e-3, weight_decay=1e-4, eps=1e-8)
+    for step in range(4):
+        for a, b in zip(pr, pm):
+            gr = torch.randn(a.shape, generator=g).to(DEV)
+            a.grad = gr.clone()
+            b.grad = gr.clone()   # contiguous gradient of a channels_last weight
+        if step == 2:   # state laid out contiguously (as a loaded checkpoint's)
+            for b in pm:
+                for k in ('exp_avg', 'exp_avg_sq'):
+                    o_my.state[b][k] = o_my.state[b][k].contiguous()
+        torch.nn.utils.clip_grad_norm_(pr, 1.0)
+        o_ref.step()
+        o_my.step(max_norm=1.0)
+        torch.cuda.synchronize()
+        for a, b in zip(pr, pm):
+            assert b.stride() == (b.contiguous(memory_format=torch.channels_last).stride()
+                                  if b.dim() == 4 else b.stride())
+            assert _rel(b.detach(), a.detach()) < 1e-6, step
+            assert _rel(b.grad, a.grad) < 1e-6, step
+
+
 def test_fused_adamw_global_norm_over_groups(ext_ops):
     """Two parameter groups (different lr / weight decay): the clip coefficient comes from the
     norm over ALL groups, as clip_grad_norm_ over every parameter."""
