@@ -167,7 +167,13 @@ __global__ __launch_bounds__(NT, SPLIT ? 1 : 2) void corr_otf_fwd_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mb = wave & 1, nh = wave >> 1;
+  // one workgroup per (pyramid level, query tile), level-major: the heavy level-0 boxes are
+  // dispatched first and the light coarse levels fill the tail (one launch is ~4.5 rounds of the
+  // chip instead of ~1.1 with a last round 1/8 full); levels write disjoint output channels
   int t = blockIdx.x;
+  const int ntile = B * tiles_x * tiles_y;
+  const int lev = t / ntile;
+  t -= lev * ntile;
   const int tx = t % tiles_x;
   t /= tiles_x;
   const int ty = t % tiles_y;
@@ -201,7 +207,8 @@ __global__ __launch_bounds__(NT, SPLIT ? 1 : 2) void corr_otf_fwd_kernel(
   }
 
   ChunkLoader<C> ld, ldl;
-  for (int l = 0; l < levels; ++l) {
+  {
+    const int l = lev;
     const int hl = lv.h[l], wl = lv.w[l];
     if (wave == 0) tile_geometry<R>(geo, lane, cact, cxv, cyv, l, hl, wl);
     for (int e = tid; e < TP * NP; e += NT) win[e] = 0.f;
@@ -266,7 +273,7 @@ __global__ __launch_bounds__(NT, SPLIT ? 1 : 2) void corr_otf_fwd_kernel(
     __syncthreads();
   }
   const int pad = ostride - levels * DD;
-  if (pad > 0) {
+  if (pad > 0 && lev == levels - 1) {
     for (int e = tid; e < TP * pad; e += NT) {
       const int p = e / pad, cc = e % pad;
       const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
@@ -276,19 +283,34 @@ __global__ __launch_bounds__(NT, SPLIT ? 1 : 2) void corr_otf_fwd_kernel(
   }
 }
 
-// wave 0, lane = tile pixel: window origins of every iteration in `wl` at level l + the union box
-template <int R>
-__device__ __forceinline__ void tile_geometry_multi(int (*gx)[TP], int (*gy)[TP], int* box,
-                                                    const WinList& wl, int lane, bool act,
-                                                    int64_t cidx, int HW, int l, int hl, int w_l) {
+// Window origins of the multi-iteration backward, packed (x0 & 0xffff) | (y0 << 16): a window
+// that hits the map has -E < x0 < w_l, -E < y0 < h_l (the launcher bounds the maps below 2^15)
+constexpr int WMISS = -32768;
+__device__ __forceinline__ int pack_xy(int x0, int y0) { return (int)(((unsigned)x0 & 0xffffu) | ((unsigned)y0 << 16)); }
+__device__ __forceinline__ int unpack_x(int v) { return (int)(short)(v & 0xffff); }
+__device__ __forceinline__ int unpack_y(int v) { return v >> 16; }
+
+// wave 0, lane = tile pixel: window origins (packed) and bilinear fractions of every iteration in
+// `wl` at level l + the union box.  The pixel's coordinates of all iterations were loaded into
+// registers once per tile (cx/cy, NIT entries, the first wl.n valid): no global load here.
+template <int R, int NIT>
+__device__ __forceinline__ void tile_geometry_multi(int (*gxy)[TP], float (*fx)[TP], float (*fy)[TP],
+                                                    int* box, const float* cxr, const float* cyr,
+                                                    int n, int lane, bool act, int l, int hl,
+                                                    int w_l) {
   constexpr int E = 2 * R + 2;
   const float inv = 1.f / (float)(1 << l);
   int mnx = 0x7fffffff, mxx = -0x7fffffff, mny = 0x7fffffff, mxy = -0x7fffffff;
-  for (int it = 0; it < wl.n; ++it) {
-    int x0 = -(1 << 28), y0 = -(1 << 28);
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    if (it >= n) break;
+    int x0 = WMISS, y0 = WMISS;
+    float ax = 0.f, ay = 0.f;
     if (act) {
-      const float cx = clampc(wl.coords[it][cidx] * inv);
-      const float cy = clampc(wl.coords[it][cidx + HW] * inv);
+      const float cx = clampc(cxr[it] * inv);
+      const float cy = clampc(cyr[it] * inv);
+      ax = cx - floorf(cx);
+      ay = cy - floorf(cy);
       x0 = (int)floorf(cx) - R;
       y0 = (int)floorf(cy) - R;
       if (x0 <= w_l - 1 && x0 + E - 1 >= 0 && y0 <= hl - 1 && y0 + E - 1 >= 0) {
@@ -297,11 +319,12 @@ __device__ __forceinline__ void tile_geometry_multi(int (*gx)[TP], int (*gy)[TP]
         mny = min(mny, y0);
         mxy = max(mxy, y0 + E - 1);
       } else {
-        x0 = y0 = -(1 << 28);  // misses the map: contributes nothing
+        x0 = y0 = WMISS;  // misses the map: contributes nothing
       }
     }
-    gx[it][lane] = x0;
-    gy[it][lane] = y0;
+    gxy[it][lane] = pack_xy(x0, y0);
+    fx[it][lane] = ax;
+    fy[it][lane] = ay;
   }
   mnx = wave_min_i(mnx);
   mxx = wave_max_i(mxx);
@@ -357,15 +380,18 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
   __shared__ __attribute__((aligned(16))) uint16_t Bs[NCH * RS];
   __shared__ __attribute__((aligned(16))) uint16_t dS[TP * SS];
   __shared__ float dwin[MULTI ? 1 : TP * NP];
-  __shared__ int gx[NIT][TP], gy[NIT][TP];
-  __shared__ Geo geo;
+  __shared__ int gx[1][TP], gy[1][TP];   // !MULTI: the lookup's window origins
+  // MULTI: every iteration's packed window origins and bilinear fractions at the current level
+  __shared__ int gxy[NIT][TP];
+  __shared__ float pax[NIT][TP], pay[NIT][TP];
+  struct GeoBox { int box[4]; };
+  __shared__ std::conditional_t<MULTI, GeoBox, Geo> geo;
   // MULTI: per pixel, the sum over the iterations of its window gradients on a UG x UG grid at
   // the union of its windows (the windows of one pixel move only a few positions over a step),
   // so building a dS chunk element is one LDS read instead of a global read per iteration
   constexpr int UG = 15, UGG = UG * UG;
   __shared__ float ugrid[MULTI ? TP * UGG : 1];
   __shared__ int uxy[MULTI ? 2 * TP + 1 : 1];
-  __shared__ float pax[2][MULTI ? TP : 1], pay[2][MULTI ? TP : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int t = blockIdx.x;
@@ -396,6 +422,18 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
       cyv = coords[cidx + HW];
     }
   }
+  // MULTI: wave 0's pixel coordinates of every iteration, all loads in flight at once (the
+  // per-level geometry then reads registers, not a chain of dependent global loads)
+  float cxr[NIT], cyr[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    cxr[it] = 0.f;
+    cyr[it] = 0.f;
+    if (MULTI && wave == 0 && cact && it < wl.n) {
+      cxr[it] = wl.coords[it][cidx];
+      cyr[it] = wl.coords[it][cidx + HW];
+    }
+  }
 
   f32x16 g1[2][TN];  // dF1: 64 pixels x this wave's WC channels
 #pragma unroll
@@ -410,7 +448,7 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
     const int hl = lv.h[l], wl_ = lv.w[l];
     if (wave == 0) {
       if constexpr (MULTI) {
-        tile_geometry_multi<R>(gx, gy, geo.box, wl, lane, cact, cidx, HW, l, hl, wl_);
+        tile_geometry_multi<R, NIT>(gxy, pax, pay, geo.box, cxr, cyr, wl.n, lane, cact, l, hl, wl_);
       } else {
         tile_geometry<R>(geo, lane, cact, cxv, cyv, l, hl, wl_);
         gx[0][lane] = geo.x0[lane];
@@ -447,8 +485,9 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
       if (wave == 0) {
         int mnx = 0x7fffffff, mxx = -0x7fffffff, mny = 0x7fffffff, mxy = -0x7fffffff;
         for (int it = 0; it < wl.n; ++it) {
-          const int x0 = gx[it][lane], y0 = gy[it][lane];
-          if (x0 > -(1 << 27)) {
+          const int v = gxy[it][lane];
+          const int x0 = unpack_x(v), y0 = unpack_y(v);
+          if (x0 != WMISS) {
             mnx = min(mnx, x0);
             mxx = max(mxx, x0);
             mny = min(mny, y0);
@@ -469,57 +508,70 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
         // up to 4 of its bf16 tap gradients into the pixel's union grid: within one iteration the
         // cells of a pixel's window are distinct grid cells (one writer each), and a barrier
         // separates the iterations -- deterministic, no atomics.  The 64 pixels' level-l taps of
-        // iteration it+1 (16-B pieces of the 8-aligned span around l*D*D) are staged in LDS (the
-        // fmap2 chunk buffer, free here; two slots) while iteration it's cells are added: the
-        // window gradients never go through global memory.
+        // iteration it+1 (16-B pieces of the 8-aligned span around l*D*D) are loaded into
+        // registers before iteration it's cells are added and written to LDS after them (the
+        // fmap2 chunk buffer, free here; two slots), so the loads' latency hides behind the adds:
+        // the window gradients never go through global memory.
         constexpr int TROW = ((DD + 7 + 7) / 8) * 8;  // staged taps per pixel (8-aligned span)
+        constexpr int SPT = (TP * (TROW / 8) + NT - 1) / NT;  // 16-B pieces per thread
         // two slots (stage it+1 during it) where the chunk buffer holds them (C = 256), else one
         constexpr int NSLOT = 2 * TP * TROW <= NCH * RS ? 2 : 1;
         static_assert(TP * TROW <= NCH * RS, "a tap slot fits the chunk buffer");
         const int t0 = (l * DD) & ~7, tpieces = ((l * DD + DD + 7) & ~7) / 8 - t0 / 8;
-        const float inv = 1.f / (float)(1 << l);
-        auto stage = [&](int it) {
-          uint16_t* Ts = Bs + (it % NSLOT) * TP * TROW;
-          for (int e = tid; e < TP * tpieces; e += NT) {
+        uint4 sv[SPT];
+        auto issue = [&](int it) {
+#pragma unroll
+          for (int j = 0; j < SPT; ++j) {
+            const int e = tid + j * NT;
             const int p = e / tpieces, q = e - p * tpieces;
             const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
             uint4 v = make_uint4(0, 0, 0, 0);
-            if (py < H && px < W)
+            if (e < TP * tpieces && py < H && px < W)
               v = *reinterpret_cast<const uint4*>(wl.dout[it] + ((int64_t)b * HW + py * W + px) * wl.cbuf + t0 + q * 8);
-            *reinterpret_cast<uint4*>(Ts + p * TROW + q * 8) = v;
+            sv[j] = v;
           }
-          if (tid < TP) {
-            const int py = ty * TPX + tid / TPX, px = tx * TPX + tid % TPX;
-            float ax = 0.f, ay = 0.f;
-            if (py < H && px < W) {
-              const int64_t ci = (int64_t)b * 2 * HW + py * W + px;
-              const float cx = clampc(wl.coords[it][ci] * inv), cy = clampc(wl.coords[it][ci + HW] * inv);
-              ax = cx - floorf(cx);
-              ay = cy - floorf(cy);
-            }
-            pax[it % NSLOT][tid] = ax;
-            pay[it % NSLOT][tid] = ay;
+        };
+        auto commit = [&](int it) {
+          uint16_t* Ts = Bs + (it % NSLOT) * TP * TROW;
+#pragma unroll
+          for (int j = 0; j < SPT; ++j) {
+            const int e = tid + j * NT;
+            const int p = e / tpieces, q = e - p * tpieces;
+            if (e < TP * tpieces) *reinterpret_cast<uint4*>(Ts + p * TROW + q * 8) = sv[j];
           }
         };
         for (int e = tid; e < TP * UGG; e += NT) ugrid[e] = 0.f;
-        if (NSLOT == 2 && wl.n > 0) stage(0);
+        if (NSLOT == 2 && wl.n > 0) {
+          issue(0);
+          commit(0);
+        }
         for (int it = 0; it < wl.n; ++it) {
-          __syncthreads();  // iteration it-1's adds done (its slot is free); 2 slots: it staged
+          __syncthreads();  // iteration it-1's adds done; 2 slots: it committed
           if (NSLOT == 1) {
-            stage(it);
+            issue(it);
+            commit(it);
             __syncthreads();
           } else if (it + 1 < wl.n) {
-            stage(it + 1);
+            issue(it + 1);
           }
           const uint16_t* Ts = Bs + (it % NSLOT) * TP * TROW + (l * DD - t0);
-          for (int e = tid; e < TP * NP; e += NT) {
+          // fixed trip count, unrolled: several cells' LDS reads in flight per wave (one wave
+          // per SIMD here, so a cell-at-a-time loop waits out every LDS latency)
+          static_assert(TP * NP % NT == 0, "whole cells per thread");
+#pragma unroll 4
+          for (int k = 0; k < TP * NP / NT; ++k) {
+            const int e = tid + k * NT;
             const int p = e / NP, qq = e - p * NP;
-            const int x0 = gx[it][p];  // -(1 << 28): this iteration's window misses the map
-            if (x0 <= -(1 << 27)) continue;
-            const int ry = qq / E, rx = qq - ry * E;
-            const int cy = gy[it][p] - uxy[TP + p] + ry, cxg = x0 - uxy[p] + rx;
-            ugrid[p * UGG + cy * UG + cxg] += win_cell<R>(Ts + p * TROW, rx, ry, pax[it % NSLOT][p], pay[it % NSLOT][p]);
+            const int v = gxy[it][p];
+            const int x0 = unpack_x(v);
+            if (x0 != WMISS) {  // WMISS: this iteration's window misses the map
+              const int ry = qq / E, rx = qq - ry * E;
+              const int cy = unpack_y(v) - uxy[TP + p] + ry, cxg = x0 - uxy[p] + rx;
+              ugrid[p * UGG + cy * UG + cxg] += win_cell<R>(Ts + p * TROW, rx, ry, pax[it][p], pay[it][p]);
+            }
           }
+          // 2 slots: slot (it+1) % 2 was last read by iteration it-1's adds (before the barrier)
+          if (NSLOT == 2 && it + 1 < wl.n) commit(it + 1);
         }
         __syncthreads();
       }
@@ -542,7 +594,10 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
     for (int c = 0; c < nchunk; ++c) {
       ld.store(Bs, RS, tid);
       // dS chunk (64 px x 64 positions)
-      for (int e = tid; e < TP * NCH; e += NT) {
+      static_assert(TP * NCH % NT == 0, "whole dS elements per thread");
+#pragma unroll 4
+      for (int k = 0; k < TP * NCH / NT; ++k) {
+        const int e = tid + k * NT;
         const int p = e / NCH, n = e % NCH;
         const int pos = c * NCH + n;
         float v = 0.f;
@@ -556,15 +611,11 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
             } else {  // a pixel's windows spread wider than the grid: from the global taps
               const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
               const int64_t pix = (int64_t)b * HW + py * W + px;
-              const int64_t ci = (int64_t)b * 2 * HW + py * W + px;
-              const float inv = 1.f / (float)(1 << l);
               for (int it = 0; it < wl.n; ++it) {  // fixed order -> deterministic
-                const int rx = ix - gx[it][p], ry = iy - gy[it][p];
-                if ((unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E) {
-                  const float cx = clampc(wl.coords[it][ci] * inv), cy = clampc(wl.coords[it][ci + HW] * inv);
-                  v += win_cell<R>(wl.dout[it] + pix * wl.cbuf + l * DD, rx, ry, cx - floorf(cx),
-                                   cy - floorf(cy));
-                }
+                const int g = gxy[it][p];  // WMISS: rx out of range
+                const int rx = ix - unpack_x(g), ry = iy - unpack_y(g);
+                if ((unsigned)rx < (unsigned)E && (unsigned)ry < (unsigned)E)
+                  v += win_cell<R>(wl.dout[it] + pix * wl.cbuf + l * DD, rx, ry, pax[it][p], pay[it][p]);
               }
             }
             v *= isc;
@@ -737,7 +788,8 @@ bool launch_corr_otf_fwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
   const OtfLvls q = make_lvls(f2lo ? f2lo : f2lvl, nullptr, hs, ws, levels);
   const bool split = f1lo != nullptr && f2lo != nullptr;
   const int tx = (W + TPX - 1) / TPX, ty = (H + TPX - 1) / TPX;
-  const dim3 grid((unsigned)(B * tx * ty));
+  if (levels < 1 || levels > 4) return false;
+  const dim3 grid((unsigned)(B * tx * ty * levels));
   const float isc = 1.f / sqrtf((float)C);
 #define FWD(RR, CC, TO, SP)                                                                     \
   hipLaunchKernelGGL((corr_otf_fwd_kernel<RR, CC, TO, SP>), grid, dim3(NT), 0, stream, f1, f1lo, \
@@ -823,6 +875,8 @@ bool launch_corr_otf_window_bwd(const uint16_t* f1, const uint16_t* const* f2lvl
                                 hipStream_t stream) {
   if (wl.n < 1 || wl.n > RAFT_MAX_WIN) return false;
   if (!((radius == 4 || radius == 3) && (C == 128 || C == 256))) return false;
+  for (int l = 0; l < levels; ++l)
+    if (hs[l] >= 32000 || ws[l] >= 32000) return false;  // 16-bit packed window origins
   OtfLvls p = make_lvls(f2lvl, df2lvl, hs, ws, levels);
   if (slab != nullptr) {
     for (int l = 0; l < levels; ++l) {
