@@ -15,11 +15,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _port():
-    s = socket.socket()
-    s.bind(('127.0.0.1', 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    # a free port below the kernel's ephemeral range (32768+): a port handed out by bind(0) is an
+    # ephemeral one that an outgoing connection on the shared box can take before the launcher
+    # binds it (EADDRINUSE)
+    import random
+    for _ in range(64):
+        p = random.randrange(20000, 32000)
+        s = socket.socket()
+        try:
+            s.bind(('127.0.0.1', p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    raise RuntimeError('no free port in 20000-32000')
 
 
 def _run(mode, precision, backend):
@@ -32,11 +42,17 @@ def _run(mode, precision, backend):
         env['RAFT_DIST_BACKEND'] = 'gloo'
     else:
         env.pop('RAFT_DIST_BACKEND', None)
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-           '--master-addr', '127.0.0.1', '--master-port', str(_port()),
-           os.path.join(ROOT, 'scripts', 'dp_rehearsal.py')] + \
-        (['--graph'] if mode == 'graph' else []) + (['--fp32'] if precision == 'fp32' else [])
-    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
+    for attempt in range(3):
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node',
+               '2', '--master-addr', '127.0.0.1', '--master-port', str(_port()),
+               os.path.join(ROOT, 'scripts', 'dp_rehearsal.py')] + \
+            (['--graph'] if mode == 'graph' else []) + (['--fp32'] if precision == 'fp32' else [])
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
+        # the rendezvous store failing to bind its port ends the launcher before any rank starts
+        # (nothing has touched the GPU): only that case takes another port
+        if r.returncode == 0 or 'EADDRINUSE' not in r.stdout + r.stderr:
+            return r
+    return r
 
 
 @pytest.mark.parametrize('precision', ['bf16', 'fp32'])
