@@ -460,10 +460,14 @@ void corr_otf_window_bwd_(const Tensor& f1, const std::vector<Tensor>& f2,
     gp.push_back(df2[l].data_ptr<float>());
   }
   OtfSlabs sl(L, levels, B, H, W, C, df1.options());
+  // the coarse levels' dF1 part (two workgroups per query tile; summed into df1 in fixed order)
+  Tensor df1b;
+  if (levels >= 2) df1b = at::empty_like(df1, at::MemoryFormat::Contiguous);
   TORCH_CHECK(launch_corr_otf_window_bwd(reinterpret_cast<const uint16_t*>(f1.data_ptr()),
                                          L.ptr.data(), L.h.data(), L.w.data(), (int)levels, wl,
                                          df1.data_ptr<float>(), gp.data(), (int)B, (int)C, (int)H,
                                          (int)W, (int)radius, sl.slab(), sl.caps(), sl.box(),
+                                         df1b.defined() ? df1b.data_ptr<float>() : nullptr,
                                          cur_stream()),
               "on-the-fly corr supports radius 3/4 with C = 128/256");
 }

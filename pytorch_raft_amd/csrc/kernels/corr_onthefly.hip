@@ -368,8 +368,8 @@ __device__ __forceinline__ float win_cell(const uint16_t* T, int rx, int ry, flo
 template <int R, int C, typename TD, bool MULTI>
 __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
     const uint16_t* __restrict__ f1, OtfLvls lv, const float* __restrict__ coords,
-    const TD* __restrict__ dout, int dstride, WinList wl, float* __restrict__ df1, int B, int H,
-    int W, int levels, int tiles_x, int tiles_y, float isc) {
+    const TD* __restrict__ dout, int dstride, WinList wl, float* __restrict__ df1,
+    float* __restrict__ df1b, int B, int H, int W, int levels, int tiles_x, int tiles_y, float isc) {
   constexpr int D = 2 * R + 1, E = D + 1, NP = E * E, DD = D * D;
   constexpr int RS = C + 16;       // [row][channel] bf16 rows (fmap1 tile, fmap2 chunk)
   constexpr int SS = NCH + 16;     // dS [pixel][position] bf16 rows
@@ -394,7 +394,25 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
   __shared__ int uxy[MULTI ? 2 * TP + 1 : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // df1b != nullptr (MULTI, levels >= 2): two workgroups per query tile -- the first ntile
+  // blocks take levels 1..levels-1 (three union grids: the heavier half, dispatched first) and
+  // store their dF1 part to df1b; the next ntile take level 0 and add theirs to df1.  The
+  // launcher then adds df1b to df1 (fixed order).  At one workgroup per CU (160 KB LDS) the
+  // 2x tiles fill the chip's rounds instead of leaving a 1/4-full last one.
+  const int ntile = B * tiles_x * tiles_y;
   int t = blockIdx.x;
+  int lbeg = 0, lend = levels;
+  bool part = false;
+  if (df1b != nullptr) {
+    part = t < ntile;
+    if (part) {
+      lbeg = 1;
+    } else {
+      lend = 1;
+      t -= ntile;
+    }
+  }
+  const int tile = t;
   const int tx = t % tiles_x;
   t /= tiles_x;
   const int ty = t % tiles_y;
@@ -444,7 +462,7 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
       for (int r = 0; r < 16; ++r) g1[i][j][r] = 0.f;
 
   ChunkLoader<C> ld;
-  for (int l = 0; l < levels; ++l) {
+  for (int l = lbeg; l < lend; ++l) {
     const int hl = lv.h[l], wl_ = lv.w[l];
     if (wave == 0) {
       if constexpr (MULTI) {
@@ -582,9 +600,9 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
     const uint16_t* F2 = lv.f2[l] + (int64_t)b * hl * wl_ * C;
     float* G2 = lv.g2[l] + (int64_t)b * hl * wl_ * C;
     const bool slabbed = lv.slab[l] != nullptr && U > 0 && U <= lv.cap[l];
-    float* S2 = slabbed ? lv.slab[l] + (int64_t)blockIdx.x * lv.cap[l] * C : nullptr;
+    float* S2 = slabbed ? lv.slab[l] + (int64_t)tile * lv.cap[l] * C : nullptr;
     if (lv.boxes != nullptr && tid == 0) {
-      int* bx = lv.boxes + ((int64_t)blockIdx.x * 4 + l) * 4;
+      int* bx = lv.boxes + ((int64_t)tile * 4 + l) * 4;
       bx[0] = bx0;
       bx[1] = by0;
       bx[2] = slabbed ? bw : 0;
@@ -689,6 +707,7 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
     __syncthreads();  // every wave has read this level's box before wave 0 rewrites it
   }
   // dF1: the tile owns its pixels (launches on one stream are ordered) -> plain read-modify-write
+  // (the coarse-level part: a plain store into its own buffer)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -696,10 +715,26 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
       const int p = i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       const int py = ty * TPX + p / TPX, px = tx * TPX + p % TPX;
       if (py >= H || px >= W) continue;
-      float* dst = df1 + ((int64_t)b * HW + py * W + px) * C + wave * WC + (lane & 31);
+      const int64_t o = ((int64_t)b * HW + py * W + px) * C + wave * WC + (lane & 31);
+      if (part) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) dst[j * 32] += g1[i][j][r];
+        for (int j = 0; j < TN; ++j) df1b[o + j * 32] = g1[i][j][r];
+      } else {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) df1[o + j * 32] += g1[i][j][r];
+      }
     }
+}
+
+// df1 += df1b (the coarse levels' dF1 part of the split multi-iteration backward)
+__global__ __launch_bounds__(256) void add_f32_kernel(float* __restrict__ a, const float* __restrict__ b,
+                                                      int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 x = reinterpret_cast<float4*>(a)[i];
+    const float4 y = reinterpret_cast<const float4*>(b)[i];
+    x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
+    reinterpret_cast<float4*>(a)[i] = x;
+  }
 }
 
 OtfLvls make_lvls(const uint16_t* const* f2, float* const* g2, const int* hs, const int* ws,
@@ -833,7 +868,7 @@ bool launch_corr_otf_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
   none.n = 0;
 #define BWD(RR, CC, TD)                                                                        \
   hipLaunchKernelGGL((corr_otf_bwd_kernel<RR, CC, TD, false>), grid, dim3(NT), 0, stream, f1, p, \
-                     coords, (const TD*)dout, dstride, none, df1, B, H, W, levels, tx, ty, isc)
+                     coords, (const TD*)dout, dstride, none, df1, nullptr, B, H, W, levels, tx, ty, isc)
 #define BWD_BF16(RR, CC) BWD(RR, CC, uint16_t)
 #define BWD_F32(RR, CC) BWD(RR, CC, float)
   if (dout_bf16) {
@@ -871,7 +906,7 @@ int otf_tiles(int B, int H, int W) { return B * ((W + TPX - 1) / TPX) * ((H + TP
 bool launch_corr_otf_window_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const int* hs,
                                 const int* ws, int levels, const WinList& wl, float* df1,
                                 float* const* df2lvl, int B, int C, int H, int W, int radius,
-                                float* const* slab, const int* cap, int* boxes,
+                                float* const* slab, const int* cap, int* boxes, float* df1b,
                                 hipStream_t stream) {
   if (wl.n < 1 || wl.n > RAFT_MAX_WIN) return false;
   if (!((radius == 4 || radius == 3) && (C == 128 || C == 256))) return false;
@@ -886,16 +921,22 @@ bool launch_corr_otf_window_bwd(const uint16_t* f1, const uint16_t* const* f2lvl
     p.boxes = boxes;
   }
   const int tx = (W + TPX - 1) / TPX, ty = (H + TPX - 1) / TPX;
-  const dim3 grid((unsigned)(B * tx * ty));
+  if (levels < 2) df1b = nullptr;
+  const dim3 grid((unsigned)(B * tx * ty * (df1b != nullptr ? 2 : 1)));
   const float isc = 1.f / sqrtf((float)C);
 #define BWDW(RR, CC)                                                                           \
   hipLaunchKernelGGL((corr_otf_bwd_kernel<RR, CC, float, true>), grid, dim3(NT), 0, stream, f1, \
-                     p, nullptr, (const float*)nullptr, 0, wl, df1, B, H, W, levels, tx, ty, isc)
+                     p, nullptr, (const float*)nullptr, 0, wl, df1, df1b, B, H, W, levels, tx, ty, isc)
   if (radius == 4 && C == 256) BWDW(4, 256);
   else if (radius == 3 && C == 128) BWDW(3, 128);
   else if (radius == 4 && C == 128) BWDW(4, 128);
   else BWDW(3, 256);
 #undef BWDW
+  if (df1b != nullptr) {
+    const int64_t n4 = (int64_t)B * H * W * C / 4;
+    const unsigned blocks = (unsigned)std::min<int64_t>((n4 + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(add_f32_kernel, dim3(blocks), dim3(256), 0, stream, df1, df1b, n4);
+  }
   if (slab != nullptr) launch_df2_reduce(slab, cap, boxes, levels, hs, ws, tx * ty, B, C, df2lvl, stream);
   return true;
 }

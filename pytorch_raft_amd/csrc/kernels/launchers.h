@@ -50,7 +50,7 @@ int otf_tiles(int B, int H, int W);
 bool launch_corr_otf_window_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const int* hs,
                                 const int* ws, int levels, const WinList& wl, float* df1,
                                 float* const* df2lvl, int B, int C, int H, int W, int radius,
-                                float* const* slab, const int* cap, int* boxes,
+                                float* const* slab, const int* cap, int* boxes, float* df1b,
                                 hipStream_t stream);
 
 // ---- convex upsample (upsample.hip)
