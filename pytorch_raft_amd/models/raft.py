@@ -20,8 +20,8 @@ MI355X-specific extensions (all optional ``args`` attributes, defaults chosen fo
                   used while it fits in ``RAFT_CORR_BUDGET_GB`` (default: a quarter of the GPU's
                   HBM, 72 GB on MI355X), the O(HW) on-the-fly correlation beyond that.  Both give
                   the same values; all-pairs is the faster of the two at every batch that fits
-                  (training, bf16, per-GPU batch 12: on-the-fly runs at 0.90x all-pairs at
-                  both the chairs and the KITTI 288x960 shapes, profiles/r4/cfg/),
+                  (training, bf16, per-GPU batch 12: on-the-fly runs at 0.91x all-pairs at
+                  the chairs shape, profiles/r5/otf_split/, 0.90x at KITTI 288x960),
                   on-the-fly is what makes batch-1024 Sintel inference or 4K frames fit.
 
 In test mode the convex upsampling runs only after the last iteration (the reference computes and
