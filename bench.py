@@ -61,6 +61,9 @@ def parse(argv=None):
                     help='with --profile: record Python stacks and write stacks.txt (ops grouped by '
                          'the source lines that issued them; use with --eager to see the decode)')
     ap.add_argument('--json_out', type=str, default=None)
+    ap.add_argument('--dump_tune', type=str, default=None,
+                    help='rank 0 writes the conv tile table it ran with (persisted picks + fresh '
+                         'autotune picks) to this path (see pytorch_raft_amd/tune_db/)')
     ap.add_argument('--trace_markers', action='store_true',
                     help='launch a marker spin kernel right before and after the timed steps')
     ap.add_argument('--roctx_region', action='store_true',
@@ -116,9 +119,13 @@ def main(argv=None):
     if int(os.environ.get('WORLD_SIZE', '1')) != a.gpus and a.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         # convenience: self-launch when run directly with --gpus N
         import subprocess
+        import socket
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:  # a free rendezvous port
+            s.bind(('127.0.0.1', 0))
+            port = s.getsockname()[1]
         cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
                '--nproc-per-node', str(a.gpus), '--master-addr', '127.0.0.1',
-               '--master-port', '29533', os.path.abspath(__file__)] + (argv or sys.argv[1:])
+               '--master-port', str(port), os.path.abspath(__file__)] + (argv or sys.argv[1:])
         sys.exit(subprocess.call(cmd))
 
     device = pdist.init_distributed()
@@ -239,6 +246,10 @@ def main(argv=None):
         probe.append(time.perf_counter() - t_issue)
     if device.type == 'cuda':
         torch.cuda.synchronize()
+    if a.dump_tune and rank == 0 and device.type == 'cuda':
+        from pytorch_raft_amd.ops import _ext
+        n = _ext.dump_conv_tune_db(a.dump_tune)
+        print('bench: %d conv tile picks -> %s' % (n, a.dump_tune), file=sys.stderr, flush=True)
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)
     if pdist.is_dist():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

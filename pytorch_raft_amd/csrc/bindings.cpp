@@ -1666,12 +1666,20 @@ Tensor adamw_step_(const std::vector<Tensor>& params, const std::vector<Tensor>&
                   eps.size() == G && wd.size() == G,
               "adamw: per-group hyper-parameter lists must have the same length");
   const auto dev = params[0].device();
+  // same flat walk: equal sizes and equal strides over the dims of size > 1 (a size-1 dim's stride
+  // does not move the walk: a channels_last 1x1 conv weight and its contiguous gradient agree)
+  auto same_walk = [](const Tensor& x, const Tensor& y) {
+    if (x.sizes() != y.sizes()) return false;
+    for (int64_t d = 0; d < x.dim(); ++d)
+      if (x.size(d) > 1 && x.stride(d) != y.stride(d)) return false;
+    return true;
+  };
   for (size_t i = 0; i < T; ++i) {
     for (const Tensor* t : {&params[i], &grads[i], &exp_avg[i], &exp_avg_sq[i]}) {
       // the kernels walk the four tensors as flat arrays: any dense layout, the same for all four
       // (a channels_last model's weights, their gradients and moments)
       TORCH_CHECK(t->is_cuda() && t->device() == dev && t->scalar_type() == at::kFloat &&
-                      t->is_non_overlapping_and_dense() && t->strides() == params[i].strides() &&
+                      t->is_non_overlapping_and_dense() && same_walk(*t, params[i]) &&
                       t->numel() == params[i].numel(),
                   "adamw: dense fp32 tensors of one size and layout on one GPU");
     }

@@ -55,7 +55,10 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return s;
 }
 
-__global__ __launch_bounds__(ADAM_NT) void adam_sumsq_kernel(AdamTab tab, float* __restrict__ part) {
+// sum of squares of the UNSCALED gradients (g / S): the fp16 scale (up to 2^24) squared would
+// overflow fp32 on gradients that torch's per-element unscale_ check passes
+__global__ __launch_bounds__(ADAM_NT) void adam_sumsq_kernel(AdamTab tab, const float* __restrict__ inv_scale,
+                                                             float* __restrict__ part) {
   __shared__ float red[ADAM_NT / 64];
   const int c = blockIdx.x;
   const int ti = find_tensor(tab.cum, tab.T, c);
@@ -63,8 +66,12 @@ __global__ __launch_bounds__(ADAM_NT) void adam_sumsq_kernel(AdamTab tab, float*
   const int64_t s0 = (int64_t)(c - tab.cum[ti]) * ADAM_CH;
   const int64_t n = min((int64_t)ADAM_CH, t.numel - s0);
   const float* g = t.g + s0;
+  const float is = inv_scale != nullptr ? inv_scale[0] : 1.f;
   float acc = 0.f;
-  for (int64_t e = threadIdx.x; e < n; e += ADAM_NT) acc += g[e] * g[e];
+  for (int64_t e = threadIdx.x; e < n; e += ADAM_NT) {
+    const float u = g[e] * is;
+    acc += u * u;
+  }
   const float s = block_sum(acc, red);
   if (threadIdx.x == 0) part[c] = s;
 }
@@ -87,7 +94,7 @@ __global__ __launch_bounds__(ADAM_NT) void adam_clip_kernel(AdamTab tab, const f
     float tot = 0.f;
     for (int i = 0; i < ADAM_NT; ++i) tot += red[i];
     const float is = inv_scale != nullptr ? inv_scale[0] : 1.f;
-    const float norm = sqrtf(tot) * is;
+    const float norm = sqrtf(tot);  // partials are of unscaled gradients
     const bool finite = isfinite(norm);
     const float k = max_norm > 0.f ? fminf(1.f, max_norm / (norm + 1e-6f)) : 1.f;
     coef[0] = k * is;
@@ -145,7 +152,7 @@ void launch_adamw_multi(const AdamTensor* tab, const int* cum, int T, int nchunk
                         float* part, float* coef, float* found_inf, hipStream_t stream) {
   AdamTab at{tab, cum, T};
   if (need_norm)
-    hipLaunchKernelGGL(adam_sumsq_kernel, dim3((unsigned)nchunks), dim3(ADAM_NT), 0, stream, at, part);
+    hipLaunchKernelGGL(adam_sumsq_kernel, dim3((unsigned)nchunks), dim3(ADAM_NT), 0, stream, at, inv_scale, part);
   hipLaunchKernelGGL(adam_clip_kernel, dim3(1), dim3(ADAM_NT), 0, stream, at, need_norm ? part : nullptr,
                      nchunks, max_norm, inv_scale, coef, found_inf);
   hipLaunchKernelGGL(adam_update_kernel, dim3((unsigned)nchunks), dim3(ADAM_NT), 0, stream, at, groups,

@@ -521,13 +521,18 @@ int autotune(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
   (void)hipEventCreate(&e1);
   int best = -1;
   float best_ms = 1e30f;
+  static const int trials = [] {
+    const char* e = getenv("RAFT_CONV_TUNE_TRIALS");  // more trials when building tune_db/
+    const int n = e ? atoi(e) : 3;
+    return n < 1 ? 1 : (n > 50 ? 50 : n);
+  }();
   for (int i = 0; i < kNumCfgs; ++i) {
     if (!cfg_allowed(i, a.cout, smallc, epi)) continue;
     if (!launch_epi_idx(ta, te, i, smallc, stream)) continue;  // warm (code load, caches)
     // min over 3 trials of 2 launches: one noisy trial (clock ramp, a co-running stream) must
     // not flip the choice -- run-to-run step time varied by ~0.8 ms with single-trial timing
     float ms = 1e30f;
-    for (int trial = 0; trial < 3; ++trial) {
+    for (int trial = 0; trial < trials; ++trial) {
       (void)hipEventRecord(e0, stream);
       for (int r = 0; r < 2; ++r) launch_epi_idx(ta, te, i, smallc, stream);
       (void)hipEventRecord(e1, stream);
@@ -619,6 +624,12 @@ int conv_import_tuned(const int* rows, int n) {
   for (int i = 0; i < n; ++i) {
     const int* r = rows + 13 * i;
     if (r[9] < 0 || r[9] >= kNumCfgs) continue;  // a table from another build: keep our choice
+    // the row names its config by index AND tile shape: a renumbered config table since the row
+    // was written leaves the key to the autotuner instead of launching the wrong tile
+    if (kCfgs[r[9]].bm != r[10] || kCfgs[r[9]].bn != r[11]) continue;
+    const int ec = r[8];  // TuneKey.f32out: the epilogue class of choose_cfg
+    const int epi = ((ec & 3) == 2 ? EPI_GRU_ZR : EPI_BF16) | ((ec & 4) ? EPI_F16 : 0) | ((ec & 8) ? EPI_SPL : 0);
+    if (!cfg_allowed(r[9], r[6], r[7] != 0, epi)) continue;
     g_tuned[TuneKey{r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7], r[8], r[12]}] = r[9];
     ++done;
   }

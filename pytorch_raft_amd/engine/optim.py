@@ -13,6 +13,15 @@ import torch
 import torch.optim as optim
 
 
+def _same_walk(x, y):
+    """True when the flat walks of two dense tensors of one shape visit the same elements in the
+    same order: equal strides over every dim of size > 1 (a size-1 dim's stride is irrelevant --
+    a channels_last 1x1 conv weight and its contiguous gradient agree)."""
+    if x.shape != y.shape:
+        return False
+    return all(n <= 1 or a == b for n, a, b in zip(x.shape, x.stride(), y.stride()))
+
+
 class FusedAdamW(optim.Optimizer):
     """torch.optim.AdamW semantics (non-amsgrad, decoupled weight decay) on the native multi-tensor
     kernel.  ``step(max_norm=c, scaler=s)`` is, in one pass over the gradients of EVERY group,
@@ -40,7 +49,7 @@ class FusedAdamW(optim.Optimizer):
         assert closure is None, 'FusedAdamW takes no closure'
         from ..ops import _ext
         ops = _ext.ops()
-        ps, gs, ms, vs, steps, gof = [], [], [], [], [], []
+        ps, gs, ms, vs, steps, gof, copy_back = [], [], [], [], [], [], []
         lr_t, lrs, b1s, b2s, epss, wds = [], [], [], [], [], []
         for gi, group in enumerate(self.param_groups):
             for p in group['params']:
@@ -56,12 +65,17 @@ class FusedAdamW(optim.Optimizer):
                 elif st['step'].device != p.device or st['step'].dtype != torch.float32:
                     st['step'] = st['step'].to(p.device, torch.float32)  # a loaded CPU counter
                 for k in ('exp_avg', 'exp_avg_sq'):
-                    if st[k].stride() != p.stride():  # loaded state / model re-laid out since
+                    if not _same_walk(st[k], p):  # loaded state / model re-laid out since
                         st[k] = torch.empty_like(p).copy_(st[k])
-                if p.grad.stride() != p.stride():
-                    p.grad = torch.empty_like(p).copy_(p.grad)
+                g = p.grad
+                if not _same_walk(g, p):
+                    # never rebind p.grad: a replayed graph keeps writing the tensor it captured.
+                    # The kernel gets a re-laid-out copy; the clipped gradient is copied back.
+                    tmp = torch.empty_like(p).copy_(g)
+                    copy_back.append((g, tmp))
+                    g = tmp
                 ps.append(p)
-                gs.append(p.grad)
+                gs.append(g)
                 ms.append(st['exp_avg'])
                 vs.append(st['exp_avg_sq'])
                 steps.append(st['step'])
@@ -86,6 +100,10 @@ class FusedAdamW(optim.Optimizer):
         res = ops.adamw_step_(ps, gs, ms, vs, steps, gof, lr_t, lrs, b1s, b2s, epss, wds,
                               float(max_norm) if max_norm else 0.0, inv, found, bool(write_grad))
         self.last_norm = res[:2]
+        self.last_skipped = res[2:3]  # 1.0 when a non-finite gradient norm skipped the step
+        if write_grad:
+            for g, tmp in copy_back:
+                g.copy_(tmp)
         if use_scaler:
             torch._amp_update_scale_(scaler._scale, scaler._growth_tracker, found,
                                      scaler._growth_factor, scaler._backoff_factor,

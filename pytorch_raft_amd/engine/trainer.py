@@ -88,6 +88,7 @@ class TrainState:
     def apply_update(self, loss):
         clip_and_step(self.optimizer, self.model.parameters(), self.args.clip, self.scaler)
         self.nonfinite += (~torch.isfinite(loss.detach())).float()
+        _count_skipped(self.optimizer, self.scaler, self.nonfinite)
 
     def step(self, image1, image2, flow, valid):
         self.optimizer.zero_grad(set_to_none=True)
@@ -113,6 +114,15 @@ class TrainState:
             torch.distributed.all_reduce(t)
             bad = float(t.item())
         return bad == 0.0
+
+
+def _count_skipped(optimizer, scaler, counter):
+    """A finite loss with a non-finite gradient norm makes the native AdamW skip the step on the
+    device.  Without an enabled GradScaler (bf16 / fp32 training) that is a failure, not an
+    overflow back-off: add it to the device non-finite counter so ``check_finite`` reports it."""
+    skipped = getattr(optimizer, 'last_skipped', None)
+    if skipped is not None and not (scaler is not None and scaler.is_enabled()):
+        counter += skipped.reshape(())
 
 
 class GraphedTrainStep:
@@ -344,6 +354,7 @@ class GraphedTrainStep:
         st = self.st
         clip_and_step(st.optimizer, self.params, st.args.clip, st.scaler)
         st.nonfinite += (~torch.isfinite(loss.detach())).float()
+        _count_skipped(st.optimizer, st.scaler, st.nonfinite)
 
     def _sched(self):
         st = self.st

@@ -34,7 +34,74 @@ def _try_load():
         except Exception as e:  # pragma: no cover - depends on the build
             _STATE['loaded'] = False
             _STATE['error'] = 'failed to load %s: %r' % (LIB_PATH, e)
+        if _STATE['loaded']:
+            _STATE['tune_rows'] = load_conv_tune_db()
         return _STATE['loaded']
+
+
+# ---------------------------------------------------------------------------------------------
+# Persisted conv tile table.  The implicit-GEMM convs pick a tile config per geometry by timing
+# every candidate once per process (conv_igemm.hip: autotune).  Isolated timings of near-tied
+# candidates flip from box to box, so the step time did too.  A checked-in table of picks
+# (tune_db/conv_gfx950.txt: one row of 13 ints per key -- P H W KH KW cin cout small eclass cfg
+# bm bn creal, as conv_tune_table() returns them) is imported when the library loads; the
+# autotuner then runs only for keys the table lacks.  RAFT_CONV_TUNE_DB=<path> picks another
+# table, RAFT_CONV_TUNE_DB=0 disables it.
+TUNE_DB = os.path.join(_PKG_DIR, 'tune_db', 'conv_gfx950.txt')
+
+
+def tune_db_path():
+    p = os.environ.get('RAFT_CONV_TUNE_DB', TUNE_DB)
+    return None if p in ('', '0') else p
+
+
+def read_tune_rows(path):
+    rows = []
+    with open(path) as f:
+        for line in f:
+            line = line.split('#', 1)[0].strip()
+            if not line:
+                continue
+            r = [int(x) for x in line.split()]
+            if len(r) != 13:
+                raise ValueError('%s: tune row of %d ints (13 expected): %r' % (path, len(r), line))
+            rows.append(r)
+    return rows
+
+
+def load_conv_tune_db(path=None):
+    """Import the persisted conv tile picks into the native cache; returns the rows imported."""
+    path = path or tune_db_path()
+    if not path or not os.path.exists(path):
+        return 0
+    rows = read_tune_rows(path)
+    if not rows:
+        return 0
+    flat = [v for r in rows for v in r]
+    return int(torch.ops.raft_amd.conv_tune_import(flat))
+
+
+def dump_conv_tune_db(path, merge=True):
+    """Write this process's conv tile table (imported rows + fresh autotune picks) to ``path``;
+    with ``merge`` the rows already in ``path`` whose keys this process did not touch are kept."""
+    rows = list(torch.ops.raft_amd.conv_tune_table())
+    new = [rows[i:i + 13] for i in range(0, len(rows), 13)]
+    key = lambda r: tuple(r[:9]) + (r[12],)  # noqa: E731
+    table = {}
+    if merge and os.path.exists(path):
+        for r in read_tune_rows(path):
+            table[key(r)] = r
+    for r in new:
+        table[key(r)] = r
+    d = os.path.dirname(path)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    with open(path, 'w') as f:
+        f.write('# conv tile picks for gfx950 (pytorch_raft_amd/ops/_ext.py: load_conv_tune_db)\n')
+        f.write('# P H W KH KW cin cout small eclass cfg bm bn creal\n')
+        for k in sorted(table):
+            f.write(' '.join(str(v) for v in table[k]) + '\n')
+    return len(table)
 
 
 def loaded():

@@ -22,6 +22,13 @@ if [ -n "$TESTS" ]; then
   rc=$?; tail -n 2 $O/pytest.log; [ $rc -ne 0 ] && grep -E "^E |FAILED" $O/pytest.log | grep -v amdgpu.ids | head -20
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi
+if [ -n "$TUNE" ]; then
+  # fresh conv tile table: every key autotuned with $TUNE timing trials (no persisted picks),
+  # written to $O/conv_gfx950.txt (copy it to pytorch_raft_amd/tune_db/ to persist it)
+  step tune
+  RAFT_CONV_TUNE_DB=0 RAFT_CONV_TUNE_TRIALS=$TUNE timeout -k 10 300 python bench.py $BENCH_ARGS --dump_tune $O/conv_gfx950.txt > $O/tune_bench.log 2>&1 || { tail -3 $O/tune_bench.log; exit 1; }
+  grep metric $O/tune_bench.log | cut -c1-200
+fi
 step bench
 timeout -k 10 300 python bench.py $BENCH_ARGS > $O/bench.log 2>&1 || { tail -3 $O/bench.log; exit 1; }
 grep metric $O/bench.log | cut -c1-330

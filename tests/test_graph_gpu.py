@@ -137,3 +137,38 @@ def test_graph_step_host_cost(ext_ops):
     g = GraphedTrainStep(TrainState(m2, args, dev, graph_ready=True), batches[0], warmup=1)
     graphed = host_time(g)
     assert graphed < 0.75 * eager, (graphed, eager)
+
+
+def test_graph_step_channels_last_1x1(ext_ops):
+    """A channels_last model re-strides the size-1 dims of its 1x1 conv weights (update block
+    convc1, mask head).  Their gradients from the fused block are contiguous, which walks the
+    same flat order: the native AdamW must take them as they are and never rebind ``p.grad``
+    (a replayed graph keeps writing the tensor it captured -- a rebound gradient would feed step
+    1's values to every later step).  The graphed run's AdamW moments after 3 steps match the
+    eager run's for those weights."""
+    from pytorch_raft_amd.engine.trainer import TrainState, GraphedTrainStep
+    from pytorch_raft_amd.data.synthetic import device_batches
+    dev = torch.device('cuda', 0)
+    batches = device_batches(4, 128, 192, dev, count=3, seed=11)
+
+    def run(graphed):
+        m = _model(_args(channels_last=True), dev).to(memory_format=torch.channels_last)
+        st = TrainState(m, _args(channels_last=True), dev, graph_ready=graphed)
+        stepper = GraphedTrainStep(st, batches[0], warmup=2) if graphed else st
+        for k in range(3):
+            stepper.step(*batches[k])
+        torch.cuda.synchronize()
+        return m, st
+
+    m_e, st_e = run(False)
+    m_g, st_g = run(True)
+    ones = [(n, p) for n, p in m_g.named_parameters()
+            if p.dim() == 4 and p.shape[2] == 1 and p.shape[3] == 1 and p.shape[1] > 1]
+    assert ones and any(not p.is_contiguous() for _, p in ones), 'no re-strided 1x1 weight'
+    pe = dict(m_e.named_parameters())
+    for n, p in ones:
+        me = st_e.optimizer.state[pe[n]]['exp_avg']
+        mg = st_g.optimizer.state[p]['exp_avg']
+        err = float((mg - me).norm() / me.norm().clamp_min(1e-12))
+        assert err < 5e-2, (n, err)
+        assert p.grad is not None
