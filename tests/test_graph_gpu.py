@@ -164,7 +164,9 @@ def test_graph_step_channels_last_1x1(ext_ops):
     m_g, st_g = run(True)
     ones = [(n, p) for n, p in m_g.named_parameters()
             if p.dim() == 4 and p.shape[2] == 1 and p.shape[3] == 1 and p.shape[1] > 1]
-    assert ones and any(not p.is_contiguous() for _, p in ones), 'no re-strided 1x1 weight'
+    # is_contiguous() ignores size-1 dims: compare the strides themselves
+    assert ones and any(p.stride() != torch.empty(p.shape).stride() for _, p in ones), \
+        'no re-strided 1x1 weight'
     pe = dict(m_e.named_parameters())
     for n, p in ones:
         me = st_e.optimizer.state[pe[n]]['exp_avg']
