@@ -1744,7 +1744,7 @@ Tensor adamw_step_(const std::vector<Tensor>& params, const std::vector<Tensor>&
 // dcorr level 0 (B, N, N) straight from the iterations' bf16 lookup-output gradients
 Tensor corr_tap_reduce(const std::vector<Tensor>& coords, const std::vector<Tensor>& douts,
                        int64_t H, int64_t W, int64_t levels, int64_t radius, double inv_sqrt_c,
-                       bool out_bf16, int64_t pitch_mult, bool split) {
+                       bool out_bf16, int64_t pitch_mult, bool split, bool split_out) {
   // split fp32 tap gradients ([hi | lo] bf16 halves): the fold is linear in the taps, so each
   // iteration enters twice -- its hi and its lo half -- with the same coordinates
   const size_t rep = split ? 2 : 1;
@@ -1783,11 +1783,14 @@ Tensor corr_tap_reduce(const std::vector<Tensor>& coords, const std::vector<Tens
   const int lds = corr_tap_reduce_lds_bytes((int)H, (int)W, (int)levels, (int)radius);
   TORCH_CHECK(lds <= 64 * 1024, "feature map too large for the LDS plane reduction");
   c10::DeviceGuard g(coords[0].device());
-  Tensor out = at::empty({B, N, ldo}, coords[0].options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  // split_out: the fp32 dC as its split-bf16 planes [hi | lo] (2, B, N, ldo) -- the operand of
+  // the split MFMA backward GEMMs (corr_bwd_fmaps_split)
+  Tensor out = split_out ? at::empty({2, B, N, ldo}, coords[0].options().dtype(at::kBFloat16))
+                         : at::empty({B, N, ldo}, coords[0].options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
   // overflow list of the union-box fold (count + pixel indices)
   Tensor list = at::empty({1 + B * N}, coords[0].options().dtype(at::kInt));
   TORCH_CHECK(launch_corr_tap_reduce(tl, (int)levels, (int)B, (int)H, (int)W, (int)radius,
-                                     (float)inv_sqrt_c, out.data_ptr(), out_bf16 ? 1 : 0,
+                                     (float)inv_sqrt_c, out.data_ptr(), split_out ? 2 : (out_bf16 ? 1 : 0),
                                      list.data_ptr<int>(), cur_stream()),
               "unsupported radius / levels");
   return out;
@@ -1815,6 +1818,37 @@ std::vector<Tensor> corr_bwd_fmaps(const Tensor& dc, const Tensor& f1, const Ten
   TORCH_CHECK(launch_corr_bwd_fmaps(bf16p(dc), (int)ldc, bf16p(f1), bf16p(f2), bf16m(f2t), bf16m(g1),
                                     bf16m(g2), (int)B, (int)N, (int)C, cur_stream()),
               "corr backward GEMM launch");
+  return {g1, g2};
+}
+
+// fp32 correlation (fp16 / fp32 schedules): dc2 (2, B, N, ldc) bf16 split planes from
+// corr_tap_reduce(split_out=True, pitch_mult=64), f1 / f2 fp32 (B, C, H, W) contiguous ->
+// [dF1 = dC F2, dF2 = dC^T F1] fp32 (B, H, W, C), three split-bf16 MFMA passes per GEMM
+std::vector<Tensor> corr_bwd_fmaps_split(const Tensor& dc2, const Tensor& f1, const Tensor& f2) {
+  TORCH_CHECK(f1.dim() == 4 && f1.sizes() == f2.sizes(), "fmaps must be (B, C, H, W) of one shape");
+  const int64_t B = f1.size(0), C = f1.size(1), H = f1.size(2), W = f1.size(3), N = H * W;
+  for (const Tensor* t : {&f1, &f2}) {
+    check_cuda_f32(*t, "fmap");
+    TORCH_CHECK(t->is_contiguous(), "fmaps must be contiguous NCHW fp32");
+  }
+  TORCH_CHECK(dc2.is_cuda() && dc2.is_contiguous() && dc2.scalar_type() == at::kBFloat16 && dc2.dim() == 4 &&
+                  dc2.size(0) == 2 && dc2.size(1) == B && dc2.size(2) == N && dc2.size(3) >= N &&
+                  dc2.size(3) % 64 == 0,
+              "dcorr must be the contiguous split planes (2, B, N, ldc) bf16, ldc a multiple of 64 >= N");
+  TORCH_CHECK(C % 128 == 0, "channels must be a multiple of 128");
+  const int64_t ldc = dc2.size(3);
+  TORCH_CHECK(N * ldc * 2 < (int64_t(1) << 31) && C * ldc * 2 < (int64_t(1) << 31) &&
+                  N * C * 2 < (int64_t(1) << 31),
+              "per-image operands exceed the 2 GiB buffer-descriptor range");
+  c10::DeviceGuard g(dc2.device());
+  Tensor f2s = at::empty({2, B, C, ldc}, dc2.options());
+  Tensor f1s = at::empty({2, B, N, C}, dc2.options());
+  Tensor g1 = at::empty({B, H, W, C}, f1.options());
+  Tensor g2 = at::empty({B, H, W, C}, f1.options());
+  TORCH_CHECK(launch_corr_bwd_fmaps_split(bf16p(dc2), (int)ldc, f1.data_ptr<float>(), f2.data_ptr<float>(),
+                                          bf16m(f2s), bf16m(f1s), g1.data_ptr<float>(), g2.data_ptr<float>(),
+                                          (int)B, (int)N, (int)C, cur_stream()),
+              "split corr backward GEMM launch");
   return {g1, g2};
 }
 
@@ -1985,8 +2019,9 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("conv_wgrad_multi_(Tensor[] gs, int g_off, Tensor[] ins, int[] in_off, int[] in_cnt, int kh, int kw, int ph, int pw, int cout, Tensor(a!) dw, Tensor(b!)? db, int pix_per_split) -> ()");
   m.def("f1_patch_(Tensor flow, Tensor(a!) patch, Tensor(b!)? slot, int slot_off) -> ()");
   m.def("adamw_step_(Tensor(a!)[] params, Tensor(b!)[] grads, Tensor(c!)[] exp_avg, Tensor(d!)[] exp_avg_sq, Tensor(e!)[] steps, int[] group_of, Tensor[] lr_t, float[] lr, float[] beta1, float[] beta2, float[] eps, float[] wd, float max_norm, Tensor? inv_scale=None, Tensor(f!)? found_inf=None, bool write_grad=False) -> Tensor");
-  m.def("corr_tap_reduce(Tensor[] coords, Tensor[] douts, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16, int pitch_mult=0, bool split=False) -> Tensor");
+  m.def("corr_tap_reduce(Tensor[] coords, Tensor[] douts, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16, int pitch_mult=0, bool split=False, bool split_out=False) -> Tensor");
   m.def("corr_bwd_fmaps(Tensor dc, Tensor f1, Tensor f2) -> Tensor[]");
+  m.def("corr_bwd_fmaps_split(Tensor dc2, Tensor f1, Tensor f2) -> Tensor[]");
   m.def("fh2_fwd_(Tensor inp, Tensor wf, Tensor b, Tensor(a!) out, Tensor? coords=None, "
         "Tensor(b!)? cnew=None, Tensor(c!)? fnew=None) -> ()");
   m.def("fh2_dgrad_(Tensor gout, Tensor wd, Tensor fm, Tensor(a!) dx) -> ()");
@@ -2008,6 +2043,7 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("adamw_step_", &adamw_step_);
   m.impl("corr_tap_reduce", &corr_tap_reduce);
   m.impl("corr_bwd_fmaps", &corr_bwd_fmaps);
+  m.impl("corr_bwd_fmaps_split", &corr_bwd_fmaps_split);
   m.impl("fh2_fwd_", &fh2_fwd_);
   m.impl("fh2_dgrad_", &fh2_dgrad_);
   m.impl("fh2_wgrad_", &fh2_wgrad_);

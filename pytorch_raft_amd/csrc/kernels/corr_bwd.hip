@@ -16,9 +16,16 @@
 //
 // dC comes from the correlation fold (corr_window.hip) with its rows padded to a multiple of 64
 // columns (zeros), so every A row is 16-B aligned and MODE 0's K runs whole 64-wide steps.
+// fp32 correlation (the fp16 / fp32 schedules: the reference runs the correlation in fp32 outside
+// autocast): dC and the fp32 feature maps are carried as bf16 pairs x = hi + lo, and each GEMM is
+// ONE launch over three K passes -- dC_hi F_hi + dC_lo F_hi + dC_hi F_lo, fp32 accumulation, fp32
+// output (~2^-16 relative; the dropped lo*lo term is ~2^-18) -- the split-bf16 scheme of the conv
+// kernels, at 3x the bf16 MFMA work instead of the 1/8-rate fp32 MFMA.
 // Workgroup = 4 waves in 2 x 2, tile 128 x 128, 64-deep K steps double-buffered through LDS
 // (64 KB), XCD-aware tile order (the two C tiles of one row block share an L2).  The bf16 outputs
 // are the NHWC (B, N, C) gradients the channels_last encoder outputs take.
+#include <algorithm>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -41,10 +48,16 @@ __device__ __forceinline__ int swz128(int row, int chunk) { return row * 8 + (ch
 // MODE 1 layout: [64 rows][16 x 16-B chunks], chunk c of row r at slot c ^ 4 (r & 3)
 __device__ __forceinline__ int swz256(int row) { return 4 * (row & 3); }
 
-template <int MODE>
-__global__ __launch_bounds__(NT, 2) void corr_bwd_gemm_kernel(const uint16_t* __restrict__ A, int lda,
-                                                              const uint16_t* __restrict__ Bm, int ldb,
-                                                              uint16_t* __restrict__ out, int B, int N,
+// K passes of one launch: pass p multiplies A operand a[p] by B operand b[p] (bf16: one pass;
+// split fp32: the three products above)
+struct GemmOps {
+  const uint16_t* a[3];
+  const uint16_t* b[3];
+};
+
+template <int MODE, int NPROD, bool OUT32>
+__global__ __launch_bounds__(NT, 2) void corr_bwd_gemm_kernel(GemmOps ops, int lda, int ldb,
+                                                              void* __restrict__ out, int B, int N,
                                                               int C, int K, int64_t a_bstride,
                                                               int64_t b_bstride) {
   constexpr int STAGE = (BM + BN) * BK * 2;  // bytes: 32 KB
@@ -62,11 +75,13 @@ __global__ __launch_bounds__(NT, 2) void corr_bwd_gemm_kernel(const uint16_t* __
   const int mt = rem / nt_n, nt = rem - mt * nt_n;
   const int m0 = mt * BM, n0 = nt * BN;
 
-  const uint16_t* Ab = A + (int64_t)b * a_bstride;
-  const uint16_t* Bb = Bm + (int64_t)b * b_bstride;
-  // descriptors sized to the image's operand (rows past the end read zeros)
-  const rsrc_t a_rs = mk_rsrc(Ab, (uint32_t)(a_bstride * 2));
-  const rsrc_t b_rs = mk_rsrc(Bb, (uint32_t)(b_bstride * 2));
+  // descriptors sized to the image's operand (rows past the end read zeros), one per pass
+  rsrc_t a_rs[NPROD], b_rs[NPROD];
+#pragma unroll
+  for (int p = 0; p < NPROD; ++p) {
+    a_rs[p] = mk_rsrc(ops.a[p] + (int64_t)b * a_bstride, (uint32_t)(a_bstride * 2));
+    b_rs[p] = mk_rsrc(ops.b[p] + (int64_t)b * b_bstride, (uint32_t)(b_bstride * 2));
+  }
   const uint32_t lds0 = raft_lds_addr(smem);
   const uint32_t wave_off = __builtin_amdgcn_readfirstlane(wave * 64 * 16);
 
@@ -96,9 +111,16 @@ __global__ __launch_bounds__(NT, 2) void corr_bwd_gemm_kernel(const uint16_t* __
     a_kstep = (uint32_t)(BK * lda * 2);
     b_kstep = (uint32_t)(BK * ldb * 2);
   }
-  const int steps = (K + BK - 1) / BK;
+  const int ksteps = (K + BK - 1) / BK;
+  const int steps = NPROD * ksteps;
 
-  auto issue = [&](int t, int buf) {
+  auto issue = [&](int t2, int buf) {
+    const int p = t2 / ksteps, t = t2 - p * ksteps;   // pass, K step of the pass (uniform)
+    rsrc_t ar = a_rs[0], br = b_rs[0];
+    if constexpr (NPROD > 1) {
+      if (p == 1) { ar = a_rs[1]; br = b_rs[1]; }
+      else if (p == 2) { ar = a_rs[NPROD - 1]; br = b_rs[NPROD - 1]; }
+    }
     const uint32_t base = lds0 + (uint32_t)(buf * STAGE) + wave_off;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -109,8 +131,8 @@ __global__ __launch_bounds__(NT, 2) void corr_bwd_gemm_kernel(const uint16_t* __
         const int k = t * BK + ((tid + j * NT) >> 4);
         if (k >= K) { ao = OOB; bo = OOB; }
       }
-      raft_dma16(a_rs, base + j * NT * 16, ao);
-      raft_dma16(b_rs, base + (BM * BK * 2) + j * NT * 16, bo);
+      raft_dma16(ar, base + j * NT * 16, ao);
+      raft_dma16(br, base + (BM * BK * 2) + j * NT * 16, bo);
     }
   };
 
@@ -190,8 +212,7 @@ __global__ __launch_bounds__(NT, 2) void corr_bwd_gemm_kernel(const uint16_t* __
     __builtin_amdgcn_s_barrier();   // step t's buffer is free for step t + 2
   }
 
-  // bf16 store of the (m, c) tile: out[b][m][c]
-  uint16_t* Ob = out + (int64_t)b * N * C;
+  // bf16 (or fp32) store of the (m, c) tile: out[b][m][c]
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -200,9 +221,72 @@ __global__ __launch_bounds__(NT, 2) void corr_bwd_gemm_kernel(const uint16_t* __
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m < N) Ob[(int64_t)m * C + n] = raft_f32_to_bf16(acc[i][j][r]);
+        if (m >= N) continue;
+        const int64_t o = ((int64_t)b * N + m) * C + n;
+        if constexpr (OUT32) static_cast<float*>(out)[o] = acc[i][j][r];
+        else static_cast<uint16_t*>(out)[o] = raft_f32_to_bf16(acc[i][j][r]);
       }
     }
+}
+
+// fp32 F (B, C, N) -> the split pair [hi | lo] as two (B, C, ldt) bf16 planes (hi plane, then lo
+// plane at + B C ldt), columns N..ldt-1 zero: MODE 0's B operand (F2^T rows, k = j contiguous)
+__global__ __launch_bounds__(256) void corr_split_pad_kernel(const float* __restrict__ F,
+                                                             uint16_t* __restrict__ out, int64_t rows,
+                                                             int N, int ldt) {
+  const int64_t per_row = ldt / 4;   // 4 columns per thread
+  const int64_t tot = rows * per_row;
+  uint16_t* lo_plane = out + rows * ldt;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < tot; e += (int64_t)gridDim.x * 256) {
+    const int64_t r = e / per_row;
+    const int c0 = (int)(e - r * per_row) * 4;
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float v = c0 + u < N ? F[r * N + c0 + u] : 0.f;
+      h[u] = raft_f32_to_bf16(v);
+      l[u] = raft_f32_to_bf16(v - raft_bf16_to_f32(h[u]));
+    }
+    *reinterpret_cast<uint2*>(out + r * ldt + c0) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+    *reinterpret_cast<uint2*>(lo_plane + r * ldt + c0) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+  }
+}
+
+// fp32 F (B, C, N) -> split pair planes (B, N, C) bf16 (hi, then lo at + B N C): MODE 1's B
+// operand (F1 rows k = i, channel-contiguous).  64 pixels x 64 channels per workgroup through LDS.
+__global__ __launch_bounds__(256) void corr_split_transpose_kernel(const float* __restrict__ F,
+                                                                   uint16_t* __restrict__ out, int B,
+                                                                   int N, int C) {
+  __shared__ float tile[64][64 + 1];
+  const int b = blockIdx.z;
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+  const float* Fb = F + (int64_t)b * C * N;
+  // load: 64 channel rows x 64 pixels (coalesced along N)
+  for (int e = tid; e < 64 * 64; e += 256) {
+    const int c = e >> 6, p = e & 63;
+    tile[c][p] = (p0 + p < N && c0 + c < C) ? Fb[(int64_t)(c0 + c) * N + p0 + p] : 0.f;
+  }
+  __syncthreads();
+  uint16_t* hi = out + (int64_t)b * N * C;
+  uint16_t* lo = hi + (int64_t)B * N * C;
+  // store: 64 pixel rows x 8 chunks of 8 channels (16-B stores along C)
+  for (int e = tid; e < 64 * 8; e += 256) {
+    const int p = e >> 3, ch = e & 7;
+    if (p0 + p >= N) continue;
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float v0 = tile[ch * 8 + 2 * u][p], v1 = tile[ch * 8 + 2 * u + 1][p];
+      const uint16_t h0 = raft_f32_to_bf16(v0), h1 = raft_f32_to_bf16(v1);
+      hw[u] = h0 | ((uint32_t)h1 << 16);
+      lw[u] = raft_f32_to_bf16(v0 - raft_bf16_to_f32(h0)) |
+              ((uint32_t)raft_f32_to_bf16(v1 - raft_bf16_to_f32(h1)) << 16);
+    }
+    const int64_t o = (int64_t)(p0 + p) * C + c0 + ch * 8;
+    *reinterpret_cast<uint4*>(hi + o) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    *reinterpret_cast<uint4*>(lo + o) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+  }
 }
 
 // F (B, N, C) bf16 -> Ft (B, C, ldt) bf16, columns N..ldt-1 zero: 64 pixels x 64 channels per
@@ -243,13 +327,13 @@ __global__ __launch_bounds__(256) void corr_transpose_pad_kernel(const uint16_t*
   }
 }
 
-template <int MODE>
-void launch_gemm(const uint16_t* A, int lda, const uint16_t* Bm, int ldb, uint16_t* out, int B, int N,
-                 int C, int K, int64_t as, int64_t bs, hipStream_t stream) {
+template <int MODE, int NPROD, bool OUT32>
+void launch_gemm(const GemmOps& ops, int lda, int ldb, void* out, int B, int N, int C, int K,
+                 int64_t as, int64_t bs, hipStream_t stream) {
   const int tiles = B * ((N + BM - 1) / BM) * (C / BN);
   dim3 grid((unsigned)((tiles + 7) / 8 * 8));
-  hipLaunchKernelGGL(corr_bwd_gemm_kernel<MODE>, grid, dim3(NT), 0, stream, A, lda, Bm, ldb, out, B, N,
-                     C, K, as, bs);
+  hipLaunchKernelGGL((corr_bwd_gemm_kernel<MODE, NPROD, OUT32>), grid, dim3(NT), 0, stream, ops, lda, ldb,
+                     out, B, N, C, K, as, bs);
 }
 
 }  // namespace
@@ -263,8 +347,36 @@ bool launch_corr_bwd_fmaps(const uint16_t* dc, int ldc, const uint16_t* f1, cons
   dim3 tg((unsigned)((ldc + 63) / 64), (unsigned)(C / 64), (unsigned)B);
   hipLaunchKernelGGL(corr_transpose_pad_kernel, tg, dim3(256), 0, stream, f2, f2t, N, C, ldc);
   // dF1 = dC F2:  rows of dC (k = j) against rows of F2^T (k = j), K = the padded pitch
-  launch_gemm<0>(dc, ldc, f2t, ldc, g1, B, N, C, ldc, (int64_t)N * ldc, (int64_t)C * ldc, stream);
+  launch_gemm<0, 1, false>(GemmOps{{dc}, {f2t}}, ldc, ldc, g1, B, N, C, ldc, (int64_t)N * ldc,
+                           (int64_t)C * ldc, stream);
   // dF2 = dC^T F1:  k = i rows of dC (columns j) and of F1 (columns c), K = N
-  launch_gemm<1>(dc, ldc, f1, C, g2, B, N, C, N, (int64_t)N * ldc, (int64_t)N * C, stream);
+  launch_gemm<1, 1, false>(GemmOps{{dc}, {f1}}, ldc, C, g2, B, N, C, N, (int64_t)N * ldc,
+                           (int64_t)N * C, stream);
+  return true;
+}
+
+// fp32 correlation: dc2 = split dC planes [hi | lo] (2, B, N, ldc) bf16 from the fold; f1 / f2
+// fp32 (B, C, N) (NCHW fmaps); scratch: f2s (2, B, C, ldc), f1s (2, B, N, C) bf16; g1 / g2 fp32
+// (B, N, C)
+bool launch_corr_bwd_fmaps_split(const uint16_t* dc2, int ldc, const float* f1, const float* f2,
+                                 uint16_t* f2s, uint16_t* f1s, float* g1, float* g2, int B, int N, int C,
+                                 hipStream_t stream) {
+  if (C % BN != 0 || C % 64 != 0 || ldc % BK != 0 || ldc < N) return false;
+  if ((int64_t)N * ldc * 2 >= (int64_t(1) << 31) || (int64_t)C * ldc * 2 >= (int64_t(1) << 31))
+    return false;
+  const int64_t rows = (int64_t)B * C;
+  const int64_t work = rows * (ldc / 4);
+  hipLaunchKernelGGL(corr_split_pad_kernel, dim3((unsigned)std::min<int64_t>((work + 255) / 256, 8192)),
+                     dim3(256), 0, stream, f2, f2s, rows, N, ldc);
+  dim3 tg((unsigned)((N + 63) / 64), (unsigned)(C / 64), (unsigned)B);
+  hipLaunchKernelGGL(corr_split_transpose_kernel, tg, dim3(256), 0, stream, f1, f1s, B, N, C);
+  const uint16_t* dlo = dc2 + (int64_t)B * N * ldc;
+  const uint16_t* f2lo = f2s + (int64_t)B * C * ldc;
+  const uint16_t* f1lo = f1s + (int64_t)B * N * C;
+  // passes: dC_hi F_hi + dC_lo F_hi + dC_hi F_lo
+  launch_gemm<0, 3, true>(GemmOps{{dc2, dlo, dc2}, {f2s, f2s, f2lo}}, ldc, ldc, g1, B, N, C, ldc,
+                          (int64_t)N * ldc, (int64_t)C * ldc, stream);
+  launch_gemm<1, 3, true>(GemmOps{{dc2, dlo, dc2}, {f1s, f1s, f1lo}}, ldc, C, g2, B, N, C, N,
+                          (int64_t)N * ldc, (int64_t)N * C, stream);
   return true;
 }

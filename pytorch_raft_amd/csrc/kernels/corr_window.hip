@@ -1,9 +1,11 @@
 // NHWC correlation lookup for the fused update block + window-compact backward.
 //
-// Forward (corr_lookup_tile_kernel): a workgroup owns 64 consecutive query pixels; 256 threads
-// compute the (levels x (2r+1)) tap rows of all 64 pixels into an LDS tile, then the tile is
-// written out as whole 704-B pixel rows of the bf16 (B,H,W,Cbuf) buffer the first 1x1 conv reads,
-// zero padding included (no separate memset, no scattered 2-byte stores).
+// Forward (corr_lookup_rows_kernel): a workgroup owns 4 consecutive query pixels; every window
+// row of every (pixel, level) is fetched as whole aligned 16-B pieces into LDS, the (2r+1)^2
+// bilinear taps are interpolated into an LDS tile, and the tile is written out as whole pixel
+// rows of the 16-bit (B,H,W,Cbuf) buffer the first 1x1 conv reads, zero padding included (no
+// separate memset, no scattered 2-byte stores).  bf16 or fp32 pyramids; bf16, fp16 or split-fp32
+// taps.
 //
 // Backward, two phases instead of a dense read-modify-write of the whole pyramid gradient:
 //  1. per iteration (corr_window_grad_kernel): the adjoint of one pixel's bilinear window is a
@@ -31,194 +33,19 @@ struct PyrC4 {
 
 __device__ __forceinline__ float clampc(float v) { return fminf(fmaxf(v, -1.0e7f), 1.0e7f); }
 
-constexpr int TP = 64;  // pixels per workgroup
+constexpr int TP = 64;  // pixels per workgroup of the window-gradient kernel
 
-template <int R>
-__global__ __launch_bounds__(256) void corr_lookup_tile_kernel(PyrC4 pyr, const float* __restrict__ coords,
-                                                               uint16_t* __restrict__ out, int cbuf,
-                                                               int B, int H, int W, int levels) {
-  constexpr int D = 2 * R + 1;
-  constexpr int ROW = (4 * D * D + 7) / 8 * 8;  // bf16 per LDS pixel row (16-B multiple)
-  __shared__ __attribute__((aligned(16))) uint16_t tile[TP * ROW];
-  const int N = H * W;
-  const int tiles = (N + TP - 1) / TP;
-  const int b = blockIdx.x / tiles;
-  const int i0 = (blockIdx.x % tiles) * TP;
-  const int items = TP * levels * D;
-  for (int it = threadIdx.x; it < items; it += 256) {
-    const int px = it % TP;
-    const int rest = it / TP;
-    const int iy = rest % D, l = rest / D;
-    const int i = i0 + px;
-    if (i >= N) continue;
-    const int hl = pyr.h[l], wl = pyr.w[l];
-    const float inv = 1.0f / (float)(1 << l);
-    const float cx = clampc(coords[((int64_t)b * 2) * N + i] * inv);
-    const float cy = clampc(coords[((int64_t)b * 2 + 1) * N + i] * inv);
-    const float fx = floorf(cx), fy = floorf(cy);
-    const float ax = cx - fx, ay = cy - fy;
-    const int xs = (int)fx - R, ys = (int)fy - R;
-    const float* P = pyr.lvl[l] + ((int64_t)b * N + i) * hl * wl;
-    float hr[2][D];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int gy = ys + iy + k;
-      const bool rowok = gy >= 0 && gy < hl;
-      float v[D + 1];
-#pragma unroll
-      for (int xx = 0; xx <= D; ++xx) {
-        const int gx = xs + xx;
-        v[xx] = (rowok && gx >= 0 && gx < wl) ? P[(int64_t)gy * wl + gx] : 0.f;
-      }
-#pragma unroll
-      for (int ix = 0; ix < D; ++ix) hr[k][ix] = (1.f - ax) * v[ix] + ax * v[ix + 1];
-    }
-    uint16_t* T = tile + px * ROW + l * D * D;
-#pragma unroll
-    for (int ix = 0; ix < D; ++ix)
-      T[ix * D + iy] = raft_f32_to_bf16((1.f - ay) * hr[0][ix] + ay * hr[1][ix]);
-  }
-  __syncthreads();
-  const int ctot = levels * D * D;
-  const int chunks = cbuf / 8;
-  for (int e = threadIdx.x; e < TP * chunks; e += 256) {
-    const int px = e / chunks, ch = e % chunks;
-    const int i = i0 + px;
-    if (i >= N) continue;
-    uint16_t v[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int c = ch * 8 + q;
-      v[q] = c < ctot ? tile[px * ROW + c] : (uint16_t)0;
-    }
-    *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i) * cbuf + ch * 8) =
-        make_uint4(v[0] | ((uint32_t)v[1] << 16), v[2] | ((uint32_t)v[3] << 16),
-                   v[4] | ((uint32_t)v[5] << 16), v[6] | ((uint32_t)v[7] << 16));
-  }
-}
-
-// Window-staged lookup (the launcher's kernel): the (2r+2)^2 integer window of every (pixel,
-// level) is first gathered into LDS with lanes running along the window rows (each row is 2r+2
-// consecutive floats of the pixel's correlation plane: a few wide requests per wave instead of a
-// scalar load per lane per tap), all loads of a level issued before any is consumed (range-checked
-// buffer loads: out-of-plane window cells read 0 with no branch).  The (2r+1)^2 bilinear taps are
-// then interpolated from LDS into the bf16 pixel-row tile, which is streamed out as above.
-constexpr int TPW = 32;  // pixels per workgroup
-
-// OT: output taps 0 bf16, 1 fp16, 2 split fp32 (bf16 hi at channel c, bf16(v - hi) at cbuf + c
-// of a 2 cbuf-wide row: the fp32 schedule's fused update block)
-template <int R, bool BF, int OT = 0>
-__global__ __launch_bounds__(256) void corr_lookup_win_kernel(PyrC4 pyr, const float* __restrict__ coords,
-                                                              uint16_t* __restrict__ out, int cbuf,
-                                                              int B, int H, int W, int levels) {
-  constexpr int D = 2 * R + 1, E = D + 1, EE = E * E, DD = D * D;
-  // window rows padded to an odd stride in LDS: the interpolation reads of consecutive taps (iy
-  // fastest) are one row apart, and a stride of E = 10 floats put them on 16 banks (2-way
-  // conflicts on every read)
-  constexpr int WRS = E + 1, EES = E * WRS;
-  constexpr int ROW = (4 * DD + 7) / 8 * 8;
-  constexpr int PER = (TPW * EE + 255) / 256;  // window cells per thread per level
-  constexpr uint32_t OOB = 0x80000000u;
-  __shared__ float win[TPW * 4 * EES];
-  __shared__ float cxy[TPW * 4 * 2];
-  __shared__ __attribute__((aligned(16))) uint16_t tile[(OT == 2 ? 2 : 1) * TPW * ROW];
-  const int N = H * W;
-  const int tiles = (N + TPW - 1) / TPW;
-  const int b = blockIdx.x / tiles;
-  const int i0 = (blockIdx.x % tiles) * TPW;
-  const int tid = threadIdx.x;
-  if (tid < TPW * 4) {  // level-scaled lookup centre per (pixel, level)
-    const int px = tid >> 2, l = tid & 3;
-    const int i = min(i0 + px, N - 1);
-    const float inv = 1.0f / (float)(1 << l);
-    cxy[tid * 2] = clampc(coords[((int64_t)b * 2) * N + i] * inv);
-    cxy[tid * 2 + 1] = clampc(coords[((int64_t)b * 2 + 1) * N + i] * inv);
-  }
-  __syncthreads();
-  for (int l = 0; l < levels; ++l) {
-    const int hl = pyr.h[l], wl = pyr.w[l];
-    const uint32_t plane = (uint32_t)(hl * wl);
-    // this workgroup's planes of level l: pixels i0 .. i0+TPW-1 of image b (fp32 or bf16 cells)
-    constexpr uint32_t ES = BF ? 2u : 4u;
-    const char* base = reinterpret_cast<const char*>(pyr.lvl[l]) +
-                       ((int64_t)b * N + i0) * (int64_t)plane * ES;
-    const uint32_t nplanes = (uint32_t)min(TPW, N - i0);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<char*>(base), (short)0, (int)(nplanes * plane * ES), 0x00020000);
-    float v[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = tid + k * 256;
-      const int px = e / EE, rc = e - px * EE, r = rc / E, c = rc - r * E;
-      uint32_t off = OOB;
-      if (e < TPW * EE) {
-        const float cx = cxy[(px * 4 + l) * 2], cy = cxy[(px * 4 + l) * 2 + 1];
-        const int gx = (int)floorf(cx) - R + c, gy = (int)floorf(cy) - R + r;
-        if ((unsigned)gy < (unsigned)hl && (unsigned)gx < (unsigned)wl)
-          off = ((uint32_t)px * plane + (uint32_t)(gy * wl + gx)) * ES;
-      }
-      if constexpr (BF)
-        v[k] = raft_bf16_to_f32(__builtin_amdgcn_raw_buffer_load_b16(rs, off, 0, 0));
-      else
-        v[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = tid + k * 256;
-      if (e < TPW * EE) {
-        const int px = e / EE, rc = e - px * EE, r = rc / E, c = rc - r * E;
-        win[(px * 4 + l) * EES + r * WRS + c] = v[k];
-      }
-    }
-  }
-  __syncthreads();
-  const int ctot = levels * DD;
-  for (int it = tid; it < TPW * ctot; it += 256) {
-    const int px = it / ctot, ch = it - px * ctot;
-    const int l = ch / DD, t = ch - l * DD, ix = t / D, iy = t - ix * D;
-    const float cx = cxy[(px * 4 + l) * 2], cy = cxy[(px * 4 + l) * 2 + 1];
-    const float ax = cx - floorf(cx), ay = cy - floorf(cy);
-    const float* w = win + (px * 4 + l) * EES + iy * WRS + ix;
-    const float top = (1.f - ax) * w[0] + ax * w[1];
-    const float bot = (1.f - ax) * w[WRS] + ax * w[WRS + 1];
-    const float v = (1.f - ay) * top + ay * bot;
-    const uint16_t h = raft_f2h<OT == 1>(v);
-    tile[px * ROW + ch] = h;
-    if constexpr (OT == 2) tile[TPW * ROW + px * ROW + ch] = raft_f32_to_bf16(v - raft_bf16_to_f32(h));
-  }
-  __syncthreads();
-  const int chunks = cbuf / 8;
-  constexpr int NH = OT == 2 ? 2 : 1;  // halves of an output row
-  for (int e = tid; e < NH * TPW * chunks; e += 256) {
-    const int hf = e / (TPW * chunks), e2 = e - hf * (TPW * chunks);
-    const int px = e2 / chunks, ch = e2 % chunks;
-    const int i = i0 + px;
-    if (i >= N) continue;
-    const uint16_t* tl = tile + hf * (TPW * ROW);
-    uint4 o;
-    if (ch * 8 + 8 <= ctot) {  // whole 16-B piece of taps: one LDS read (ROW % 8 == 0)
-      o = *reinterpret_cast<const uint4*>(tl + px * ROW + ch * 8);
-    } else {
-      uint16_t q8[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int c = ch * 8 + q;
-        q8[q] = c < ctot ? tl[px * ROW + c] : (uint16_t)0;
-      }
-      o = make_uint4(q8[0] | ((uint32_t)q8[1] << 16), q8[2] | ((uint32_t)q8[3] << 16),
-                     q8[4] | ((uint32_t)q8[5] << 16), q8[6] | ((uint32_t)q8[7] << 16));
-    }
-    *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i) * (NH * cbuf) + hf * cbuf + ch * 8) = o;
-  }
-}
-
-// Row-vector lookup (bf16 pyramid; the launcher's default): the window of a (pixel, level) is
-// 2r+2 rows of 2r+2 consecutive bf16 cells of the pixel's correlation plane.  Phase 1 fetches
-// every window row as whole ALIGNED 16-B pieces (2, or 3 when the row straddles a third piece) --
-// 2-3 vector loads per row instead of 2r+2 two-byte gathers, all of a thread's rows in flight at
-// once -- and parks them raw in LDS; phase 2 reads the row cells at the row's start offset inside
-// its pieces (LDS indexing is free), masks cells outside the plane and interpolates the (2r+1)^2
-// taps into the bf16 pixel-row tile; phase 3 streams the tile out as 16-B pixel-row pieces.
+// Row-vector lookup (the launcher's kernel for every pyramid / tap type): the window of a
+// (pixel, level) is 2r+2 rows of 2r+2 consecutive cells of the pixel's correlation plane.  Phase 1
+// fetches every window row as whole ALIGNED 16-B pieces (bf16 cells: 2, or 3 when the row
+// straddles a third piece; fp32 cells: 3 or 4) -- a few vector loads per row instead of 2r+2
+// scalar gathers, all of a thread's rows in flight at once -- and parks them raw in LDS; phase 2
+// reads the row cells at the row's start offset inside its pieces (LDS indexing is free), masks
+// cells outside the plane and interpolates the (2r+1)^2 taps into the pixel-row tile; phase 3
+// streams the tile out as 16-B pixel-row pieces.
+//   PF32: fp32 pyramid (the fp16 / fp32 schedules: the reference's fp32 correlation), else bf16
+//   OT:   output taps 0 bf16, 1 fp16, 2 split fp32 (bf16 hi at channel c, bf16(v - hi) at
+//         cbuf + c of a 2 cbuf-wide row: the fp32 schedule's fused update block)
 // pixels per workgroup: the TPVK template parameter (16: 42 KB LDS, three workgroups per CU; 8: 21 KB)
 
 // one aligned 16-B piece; a piece that runs past the range end (the last rows of the range's
@@ -233,16 +60,20 @@ __device__ __forceinline__ uint4 piece16(__amdgpu_buffer_rsrc_t r, uint32_t off,
                     __builtin_amdgcn_raw_buffer_load_b32(r, off + 12u, 0, 0));
 }
 
-template <int R, int TPVK>
+template <int R, int TPVK, bool PF32 = false, int OT = 0>
 __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const float* __restrict__ coords,
                                                                uint16_t* __restrict__ out, int cbuf,
                                                                int B, int H, int W, int levels) {
   constexpr int D = 2 * R + 1, E = D + 1;
   constexpr int ROWT = (4 * D * D + 7) / 8 * 8;
   constexpr uint32_t OOB = 0x80000000u;
-  __shared__ __attribute__((aligned(16))) uint4 rows[TPVK * 4 * E * 3];
+  constexpr int ES = PF32 ? 4 : 2;         // bytes per pyramid cell
+  constexpr int EPP = 16 / ES;             // cells per 16-B piece
+  constexpr int NPC = (EPP - 1 + E + EPP - 1) / EPP;  // pieces a row can touch
+  constexpr int NH = OT == 2 ? 2 : 1;      // halves of an output row
+  __shared__ __attribute__((aligned(16))) uint4 rows[TPVK * 4 * E * NPC];
   __shared__ float cxy[TPVK * 4 * 2];
-  __shared__ __attribute__((aligned(16))) uint16_t tile[TPVK * ROWT];
+  __shared__ __attribute__((aligned(16))) uint16_t tile[NH * TPVK * ROWT];
   const int N = H * W;
   const int tiles = (N + TPVK - 1) / TPVK;
   const int b = blockIdx.x / tiles;
@@ -256,8 +87,8 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
     cxy[tid * 2] = clampc(coords[((int64_t)b * 2) * N + i] * inv);
     cxy[tid * 2 + 1] = clampc(coords[((int64_t)b * 2 + 1) * N + i] * inv);
   }
-  // per level: a 16-B aligned base at or below this workgroup's first plane; `dl` = elements
-  // between that base and the first plane (0..7)
+  // per level: a 16-B aligned base at or below this workgroup's first plane; `dl` = cells
+  // between that base and the first plane (0..EPP-1)
   __amdgpu_buffer_rsrc_t rs[4];
   int dl[4];
   uint32_t nbytes[4];
@@ -265,17 +96,16 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
   for (int l = 0; l < 4; ++l) {
     const int ll = l < levels ? l : 0;
     const int64_t plane = (int64_t)pyr.h[ll] * pyr.w[ll];
-    const int64_t first = ((int64_t)b * N + i0) * plane;  // element index of the first plane
-    const int64_t abase = first & ~(int64_t)7;
+    const int64_t first = ((int64_t)b * N + i0) * plane;  // cell index of the first plane
+    const int64_t abase = first & ~(int64_t)(EPP - 1);
     dl[l] = (int)(first - abase);
-    const uint16_t* base = reinterpret_cast<const uint16_t*>(pyr.lvl[ll]) + abase;
+    const char* base = reinterpret_cast<const char*>(pyr.lvl[ll]) + abase * ES;
     // rounded up to whole dwords: a dword read only partly inside num_records returns zero, so
-    // an odd element count would lose the last plane's last element (the allocation is padded,
+    // an odd bf16 cell count would lose the last plane's last cell (the allocation is padded,
     // the extra bytes are masked cells)
-    const uint32_t bytes = (uint32_t)(((dl[l] + (int64_t)npx * plane) * 2 + 3) & ~(int64_t)3);
+    const uint32_t bytes = (uint32_t)(((dl[l] + (int64_t)npx * plane) * ES + 3) & ~(int64_t)3);
     nbytes[l] = bytes;
-    rs[l] = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(base), (short)0, (int)bytes,
-                                             0x00020000);
+    rs[l] = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, (int)bytes, 0x00020000);
   }
   __syncthreads();
   // ---- phase 1: every window row's aligned 16-B pieces -> LDS (all loads before any store).
@@ -284,7 +114,7 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
   constexpr int IPL = (TPVK * E + 63) / 64 * 64;  // items per level (padded)
   constexpr int ITEMS = 4 * IPL;
   constexpr int PER = (ITEMS + 255) / 256;
-  uint4 v[PER][3];
+  uint4 v[PER][NPC];
   int slot[PER];
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
@@ -292,32 +122,34 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
     const int l = __builtin_amdgcn_readfirstlane(e / IPL), rem = e - l * IPL;
     const int px = rem / E, r = rem - px * E;
     slot[k] = rem < TPVK * E && l < 4 ? (px * 4 + l) * E + r : -1;
-    uint32_t o0 = OOB, o1 = OOB, o2 = OOB;
+    uint32_t o[NPC];
+#pragma unroll
+    for (int u = 0; u < NPC; ++u) o[u] = OOB;
     const int lq = l < levels ? l : 0;
     if (rem < TPVK * E && px < npx && l < levels) {
       const int hl = pyr.h[l], wl = pyr.w[l];
       const float cx = cxy[(px * 4 + l) * 2], cy = cxy[(px * 4 + l) * 2 + 1];
       const int xs = (int)floorf(cx) - R, gy = (int)floorf(cy) - R + r;
       if ((unsigned)gy < (unsigned)hl) {
-        const int er = dl[l] + px * hl * wl + gy * wl + xs;  // element offset of the row start
-        const int q0 = er >> 3;  // floor: er < 0 only before the first plane (cells masked)
-        o0 = q0 >= 0 ? (uint32_t)q0 * 16u : OOB;
-        o1 = q0 + 1 >= 0 ? (uint32_t)(q0 + 1) * 16u : OOB;
-        o2 = (er & 7) + E > 16 && q0 + 2 >= 0 ? (uint32_t)(q0 + 2) * 16u : OOB;
+        const int er = dl[l] + px * hl * wl + gy * wl + xs;  // cell offset of the row start
+        // floor division: er < 0 only before the first plane (those cells are masked)
+        const int q0 = er >= 0 ? er / EPP : -((-er + EPP - 1) / EPP);
+        const int lead = er - q0 * EPP;
+#pragma unroll
+        for (int u = 0; u < NPC; ++u)
+          o[u] = (q0 + u >= 0 && (u < 2 || lead + E > u * EPP)) ? (uint32_t)(q0 + u) * 16u : OOB;
       }
     }
     const __amdgpu_buffer_rsrc_t r0 = lq == 0 ? rs[0] : (lq == 1 ? rs[1] : (lq == 2 ? rs[2] : rs[3]));
     const uint32_t lim = nbytes[lq];
-    v[k][0] = piece16(r0, o0, lim);
-    v[k][1] = piece16(r0, o1, lim);
-    v[k][2] = piece16(r0, o2, lim);
+#pragma unroll
+    for (int u = 0; u < NPC; ++u) v[k][u] = piece16(r0, o[u], lim);
   }
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (slot[k] >= 0) {
-      rows[slot[k] * 3] = v[k][0];
-      rows[slot[k] * 3 + 1] = v[k][1];
-      rows[slot[k] * 3 + 2] = v[k][2];
+#pragma unroll
+      for (int u = 0; u < NPC; ++u) rows[slot[k] * NPC + u] = v[k][u];
     }
   }
   __syncthreads();
@@ -336,40 +168,51 @@ __global__ __launch_bounds__(256) void corr_lookup_rows_kernel(PyrC4 pyr, const 
       const int r = iy + k, gy = ys + r;
       const bool rowok = (unsigned)gy < (unsigned)hl;
       const int er = dl[l] + px * hl * wl + gy * wl + xs;
-      const uint16_t* src = reinterpret_cast<const uint16_t*>(rows + ((px * 4 + l) * E + r) * 3) + (er & 7);
+      const int lead = ((er % EPP) + EPP) % EPP;
+      const char* src = reinterpret_cast<const char*>(rows + ((px * 4 + l) * E + r) * NPC) + lead * ES;
       float c[E];
 #pragma unroll
       for (int xx = 0; xx < E; ++xx) {
         const int gx = xs + xx;
-        c[xx] = (rowok && (unsigned)gx < (unsigned)wl) ? raft_bf16_to_f32(src[xx]) : 0.f;
+        float cv;
+        if constexpr (PF32) cv = reinterpret_cast<const float*>(src)[xx];
+        else cv = raft_bf16_to_f32(reinterpret_cast<const uint16_t*>(src)[xx]);
+        c[xx] = (rowok && (unsigned)gx < (unsigned)wl) ? cv : 0.f;
       }
 #pragma unroll
       for (int ix = 0; ix < D; ++ix) hr[k][ix] = (1.f - ax) * c[ix] + ax * c[ix + 1];
     }
     uint16_t* T = tile + px * ROWT + l * D * D;
 #pragma unroll
-    for (int ix = 0; ix < D; ++ix) T[ix * D + iy] = raft_f32_to_bf16((1.f - ay) * hr[0][ix] + ay * hr[1][ix]);
+    for (int ix = 0; ix < D; ++ix) {
+      const float tv = (1.f - ay) * hr[0][ix] + ay * hr[1][ix];
+      const uint16_t h = raft_f2h<OT == 1>(tv);
+      T[ix * D + iy] = h;
+      if constexpr (OT == 2) T[TPVK * ROWT + ix * D + iy] = raft_f32_to_bf16(tv - raft_bf16_to_f32(h));
+    }
   }
   __syncthreads();
-  // ---- phase 3: whole 16-B pieces of the (B,H,W,cbuf) rows, zero padding included
+  // ---- phase 3: whole 16-B pieces of the (B,H,W,NH cbuf) rows, zero padding included
   const int ctot = levels * D * D;
   const int chunks = cbuf / 8;
-  for (int e = tid; e < npx * chunks; e += 256) {
-    const int px = e / chunks, ch = e - px * chunks;
+  for (int e = tid; e < NH * npx * chunks; e += 256) {
+    const int hf = e / (npx * chunks), e2 = e - hf * (npx * chunks);
+    const int px = e2 / chunks, ch = e2 - px * chunks;
+    const uint16_t* tl = tile + hf * (TPVK * ROWT);
     uint4 o;
     if (ch * 8 + 8 <= ctot) {
-      o = *reinterpret_cast<const uint4*>(tile + px * ROWT + ch * 8);
+      o = *reinterpret_cast<const uint4*>(tl + px * ROWT + ch * 8);
     } else {
       uint16_t q8[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int c = ch * 8 + q;
-        q8[q] = c < ctot ? tile[px * ROWT + c] : (uint16_t)0;
+        q8[q] = c < ctot ? tl[px * ROWT + c] : (uint16_t)0;
       }
       o = make_uint4(q8[0] | ((uint32_t)q8[1] << 16), q8[2] | ((uint32_t)q8[3] << 16),
                      q8[4] | ((uint32_t)q8[5] << 16), q8[6] | ((uint32_t)q8[7] << 16));
     }
-    *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i0 + px) * cbuf + ch * 8) = o;
+    *reinterpret_cast<uint4*>(out + ((int64_t)b * N + i0 + px) * (NH * cbuf) + hf * cbuf + ch * 8) = o;
   }
 }
 
@@ -626,7 +469,17 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
     }
     return v * inv_sqrt_c;
   };
-  if (out_bf16 && (N & 1) == 0) {
+  if (out_bf16 == 2) {
+    // split fp32: bf16 hi plane at out, lo plane at out + B N ldo
+    uint16_t* Oh = (uint16_t*)out + row;
+    uint16_t* Ol = (uint16_t*)out + (int64_t)B * N * ldo + row;
+    for (int e = threadIdx.x; e < ldo; e += 256) {
+      const float v = e < N ? cell(e) : 0.f;
+      const uint16_t h = raft_f32_to_bf16(v);
+      Oh[e] = h;
+      Ol[e] = raft_f32_to_bf16(v - raft_bf16_to_f32(h));
+    }
+  } else if (out_bf16 && (N & 1) == 0) {
     uint32_t* Ob = reinterpret_cast<uint32_t*>((uint16_t*)out + row);
     for (int e2 = threadIdx.x; e2 < ldo / 2; e2 += 256)
       Ob[e2] = 2 * e2 < N ? (uint32_t)raft_f32_to_bf16(cell(2 * e2)) |
@@ -642,195 +495,6 @@ __global__ __launch_bounds__(256) void corr_tap_reduce_kernel(TapList tl, int le
   __syncthreads();  // the next listed pixel reuses the planes
   }
 }
-
-// Wave-per-query-pixel fold (opt-in, RAFT_TAPRED=2): the same per-cell arithmetic and iteration
-// order as corr_tap_reduce_kernel (bitwise the same dC), but each WAVE owns one query pixel's
-// level planes in its own LDS slice, so there is no workgroup barrier at all: a wave's LDS
-// operations execute in issue order, which orders the iterations' read-modify-writes and makes
-// the staged tap rows visible to the wave's other lanes.
-//  * Latency: the coordinates and tap rows of the next TG iterations are loaded (wave-uniform
-//    coordinate loads, one 16-B tap piece per lane and iteration) while the current TG are folded;
-//    a dependent global load per iteration made the first version of this kernel 3x slower than
-//    the workgroup-per-pixel one.
-//  * Banks: a half-wave's 32 window cells span ~3 rows of 10; level rows of >= 16 cells are padded
-//    to a stride = 10 (mod 32) so those rows land on disjoint banks (unpadded, a 62-cell row stride
-//    = -2 (mod 32) put them 3-way on the same banks: 25 M conflict cycles per step).
-//  * Write-out: two columns per lane (8-B plane reads, one coarse-level read per pair, 4-B bf16
-//    pair stores) when W is even.
-constexpr int TG = 2;  // iterations per prefetch group
-struct TapGeo {
-  int ps[4];   // padded row stride of each level plane (floats)
-  int off[4];  // offset of each level plane in the wave's slice (floats)
-  int tot4;    // plane floats (16-B multiple)
-  int wave_floats;
-};
-
-TapGeo tap_geo(int H, int W, int levels, int radius) {
-  TapGeo g{};
-  int h = H, w = W, tot = 0;
-  for (int l = 0; l < 4; ++l) {
-    int ps = w;
-    if (w >= 16) {
-      ps = w + ((10 - w) % 32 + 32) % 32;
-    }
-    g.ps[l] = ps;
-    g.off[l] = tot;
-    if (l < levels) tot += ((h * ps + 1) & ~1);  // even: the next level's plane stays 8-B aligned
-    h >>= 1;
-    w >>= 1;
-  }
-  g.tot4 = (tot + 3) & ~3;
-  const int D = 2 * radius + 1;
-  const int trow = (levels * D * D + 7) / 8 * 8;
-  g.wave_floats = g.tot4 + TG * trow / 2;
-  return g;
-}
-
-template <int R, bool TF16 = false>
-__global__ __launch_bounds__(256) void corr_tap_reduce_wave_kernel(TapList tl, TapGeo tg, int levels, int B,
-                                                                   int H, int W, float inv_sqrt_c,
-                                                                   void* __restrict__ out, int out_bf16) {
-  constexpr int D = 2 * R + 1, E = D + 1;
-  constexpr int CPL = (4 * E * E + 63) / 64;  // window cells per lane (all levels)
-  extern __shared__ float lds_all[];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int N = H * W;
-  const int64_t q = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-  if (q >= (int64_t)B * N) return;  // no workgroup barrier below: waves retire independently
-  const int b = (int)(q / N), i = (int)(q - (int64_t)b * N);
-  float* planes = lds_all + wv * tg.wave_floats;
-  int hs[4], ws[4];
-  {
-    int h = H, w = W;
-    for (int l = 0; l < 4; ++l) {
-      hs[l] = h; ws[l] = w;
-      h >>= 1; w >>= 1;
-    }
-  }
-  const int ctot = levels * D * D;
-  const int chunks = (ctot + 7) / 8;
-  const int trow = chunks * 8;
-  uint16_t* taps = reinterpret_cast<uint16_t*>(planes + tg.tot4);  // [TG][trow]
-  const int64_t prow = ((int64_t)b * N + i) * tl.cbuf;
-  const int64_t cix = (int64_t)b * 2 * N + i;
-  // prefetch group 0 before the zero fill
-  uint4 pc[TG];
-  float ncx[TG], ncy[TG];
-  auto fetch = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < TG; ++j) {
-      const int k = min(k0 + j, tl.n - 1);
-      const float* C = tl.coords[k];
-      ncx[j] = C[cix];
-      ncy[j] = C[cix + N];
-      pc[j] = lane < chunks ? *reinterpret_cast<const uint4*>(tl.dout[k] + prow + lane * 8)
-                            : make_uint4(0, 0, 0, 0);
-    }
-  };
-  if (tl.n > 0) fetch(0);
-  for (int e = lane; e < tg.tot4 / 4; e += 64) reinterpret_cast<uint4*>(planes)[e] = make_uint4(0, 0, 0, 0);
-  int cbase[CPL], cgy[CPL], cgx[CPL], cps[CPL], cl[CPL];
-  float cinv[CPL];
-#pragma unroll
-  for (int k = 0; k < CPL; ++k) {
-    const int e = lane + k * 64;
-    const int l = e < levels * E * E ? e / (E * E) : -1;
-    cl[k] = l;
-    const int ll = l < 0 ? 0 : l;
-    cgy[k] = (e / E) % E;
-    cgx[k] = e % E;
-    // (selects, not a dynamic index into the kernel-argument struct)
-    cps[k] = ll == 0 ? tg.ps[0] : ll == 1 ? tg.ps[1] : ll == 2 ? tg.ps[2] : tg.ps[3];
-    cbase[k] = ll == 0 ? tg.off[0] : ll == 1 ? tg.off[1] : ll == 2 ? tg.off[2] : tg.off[3];
-    cinv[k] = 1.0f / (float)(1 << ll);
-  }
-  for (int k0 = 0; k0 < tl.n; k0 += TG) {
-    float cx[TG], cy[TG];
-#pragma unroll
-    for (int j = 0; j < TG; ++j) {
-      if (lane < chunks) reinterpret_cast<uint4*>(taps + j * trow)[lane] = pc[j];
-      cx[j] = ncx[j];
-      cy[j] = ncy[j];
-    }
-    if (k0 + TG < tl.n) fetch(k0 + TG);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int j = 0; j < TG; ++j) {
-      if (k0 + j >= tl.n) break;
-      const uint16_t* T0 = taps + j * trow;
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        const int l = cl[c];
-        if (l < 0) continue;
-        const int yy = cgy[c], xx = cgx[c];
-        const float fxc = clampc(cx[j] * cinv[c]), fyc = clampc(cy[j] * cinv[c]);
-        const float flx = floorf(fxc), fly = floorf(fyc);
-        const int gy = (int)fly - R + yy, gx = (int)flx - R + xx;
-        if (gy < 0 || gy >= (H >> l) || gx < 0 || gx >= (W >> l)) continue;
-        const float ax = fxc - flx, ay = fyc - fly;
-        const uint16_t* T = T0 + l * D * D;
-        float acc = 0.f;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          const int iy = yy - kk;
-          if (iy < 0 || iy >= D) continue;
-          const float wy = kk == 0 ? (1.f - ay) : ay;
-          float sx = 0.f;
-          if (xx < D) sx += (1.f - ax) * raft_h2f<TF16>(T[xx * D + iy]);
-          if (xx > 0) sx += ax * raft_h2f<TF16>(T[(xx - 1) * D + iy]);
-          acc += wy * sx;
-        }
-        planes[cbase[c] + gy * cps[c] + gx] += acc;
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  const int ldo = tl.ldo;
-  const int64_t row = ((int64_t)b * N + i) * ldo;
-  const float inv_w = 1.0f / (float)W;
-  if (out_bf16 && (W & 1) == 0) {
-    // pairs (x, x+1), x even: one coarse-level read serves both columns
-    uint32_t* Ob = reinterpret_cast<uint32_t*>((uint16_t*)out + row);
-    for (int e2 = N / 2 + lane; e2 < ldo / 2; e2 += 64) Ob[e2] = 0u;
-    for (int e2 = lane; e2 < N / 2; e2 += 64) {
-      const int e = 2 * e2;
-      const int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W;
-      const float2 p0 = *reinterpret_cast<const float2*>(planes + y * tg.ps[0] + x);
-      float v0 = p0.x, v1 = p0.y;
-      float sc = 0.25f;
-      for (int l = 1; l < levels; ++l) {
-        const int yl = y >> l, xl = x >> l;
-        if (yl < hs[l] && xl < ws[l]) {
-          const float c = sc * planes[tg.off[l] + yl * tg.ps[l] + xl];
-          v0 += c;
-          v1 += c;
-        }
-        sc *= 0.25f;
-      }
-      Ob[e2] = (uint32_t)raft_f32_to_bf16(v0 * inv_sqrt_c) | ((uint32_t)raft_f32_to_bf16(v1 * inv_sqrt_c) << 16);
-    }
-    return;
-  }
-  auto cell = [&](int e) {
-    const int y = (int)(((float)e + 0.5f) * inv_w), x = e - y * W;  // exact for e < 2^22
-    float v = planes[y * tg.ps[0] + x];
-    float sc = 0.25f;
-    for (int l = 1; l < levels; ++l) {
-      const int yl = y >> l, xl = x >> l;
-      if (yl < hs[l] && xl < ws[l]) v += sc * planes[tg.off[l] + yl * tg.ps[l] + xl];
-      sc *= 0.25f;
-    }
-    return v * inv_sqrt_c;
-  };
-  if (out_bf16) {
-    uint16_t* Ob = (uint16_t*)out + row;
-    for (int e = lane; e < ldo; e += 64) Ob[e] = e < N ? raft_f32_to_bf16(cell(e)) : (uint16_t)0;
-  } else {
-    float* O = (float*)out + row;
-    for (int e = lane; e < ldo; e += 64) O[e] = e < N ? cell(e) : 0.f;
-  }
-}
-
 
 // Union-box fold (the launcher's default, W even): one WAVE per query pixel whose level planes
 // are held only over the union box of its windows across the step's iterations (<= 24 x 24 cells
@@ -868,7 +532,8 @@ BoxGeo box_geo(int H, int W, int levels, int radius) {
   return g;
 }
 
-template <int R, bool TF16 = false, bool OUT32 = false>
+// OM: dC output 0 bf16, 1 fp32, 2 split bf16 planes (hi at out, lo at out + B N ldo)
+template <int R, bool TF16 = false, int OM = 0>
 __global__ __launch_bounds__(256) void corr_tap_fold_box_kernel(TapList tl, BoxGeo bg, int levels, int B,
                                                                 int H, int W, float inv_sqrt_c,
                                                                 void* __restrict__ out, int* __restrict__ list) {
@@ -1014,11 +679,13 @@ __global__ __launch_bounds__(256) void corr_tap_fold_box_kernel(TapList tl, BoxG
   // schedules: the reference's fp32 correlation gradient)
   const int64_t row = ((int64_t)b * N + i) * tl.ldo;
   uint32_t* Ob = reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(out) + row);
+  uint32_t* Ol = reinterpret_cast<uint32_t*>(static_cast<uint16_t*>(out) + (int64_t)B * N * tl.ldo + row);
   float2* Of = reinterpret_cast<float2*>(static_cast<float*>(out) + row);
   const float inv_w = 1.0f / (float)W;
   for (int e2 = N / 2 + lane; e2 < tl.ldo / 2; e2 += 64) {
-    if constexpr (OUT32) Of[e2] = make_float2(0.f, 0.f);
+    if constexpr (OM == 1) Of[e2] = make_float2(0.f, 0.f);
     else Ob[e2] = 0u;
+    if constexpr (OM == 2) Ol[e2] = 0u;
   }
   for (int e2 = lane; e2 < N / 2; e2 += 64) {
     const int e = 2 * e2;
@@ -1045,8 +712,16 @@ __global__ __launch_bounds__(256) void corr_tap_fold_box_kernel(TapList tl, BoxG
       }
       sc *= 0.25f;
     }
-    if constexpr (OUT32) Of[e2] = make_float2(v0 * inv_sqrt_c, v1 * inv_sqrt_c);
-    else Ob[e2] = (uint32_t)raft_f32_to_bf16(v0 * inv_sqrt_c) | ((uint32_t)raft_f32_to_bf16(v1 * inv_sqrt_c) << 16);
+    if constexpr (OM == 1) {
+      Of[e2] = make_float2(v0 * inv_sqrt_c, v1 * inv_sqrt_c);
+    } else {
+      const float s0 = v0 * inv_sqrt_c, s1 = v1 * inv_sqrt_c;
+      const uint16_t h0 = raft_f32_to_bf16(s0), h1 = raft_f32_to_bf16(s1);
+      Ob[e2] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+      if constexpr (OM == 2)
+        Ol[e2] = (uint32_t)raft_f32_to_bf16(s0 - raft_bf16_to_f32(h0)) |
+                 ((uint32_t)raft_f32_to_bf16(s1 - raft_bf16_to_f32(h1)) << 16);
+    }
   }
 }
 
@@ -1061,39 +736,10 @@ bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* w
     p.h[l] = l < levels ? hs[l] : 0;
     p.w[l] = l < levels ? ws[l] : 0;
   }
+  if (radius != 4 && radius != 3) return false;
+  if (pyr_bf16 && out_f16 != 0) return false;  // a bf16 pyramid feeds bf16 taps only
   const int N = H * W;
-  if (out_f16 == 1 || out_f16 == 2) {
-    // fp16 taps (fp16 autocast; out_f16 = 1) or split-fp32 taps (fp32 schedule; 2) from the
-    // fp32 pyramid of the reference's fp32 correlation
-    if (pyr_bf16) return false;
-    dim3 grid((unsigned)(B * ((N + TPW - 1) / TPW)));
-    if (out_f16 == 1) {
-      if (radius == 4) hipLaunchKernelGGL((corr_lookup_win_kernel<4, false, 1>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-      else if (radius == 3) hipLaunchKernelGGL((corr_lookup_win_kernel<3, false, 1>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-      else return false;
-    } else {
-      if (radius == 4) hipLaunchKernelGGL((corr_lookup_win_kernel<4, false, 2>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-      else if (radius == 3) hipLaunchKernelGGL((corr_lookup_win_kernel<3, false, 2>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-      else return false;
-    }
-    return true;
-  }
-  static const bool legacy = [] {
-    const char* e = getenv("RAFT_LOOKUP_LEGACY");
-    return e && e[0] == '1';
-  }();
-  if (legacy && !pyr_bf16) {
-    dim3 grid((unsigned)(B * ((N + TP - 1) / TP)));
-    if (radius == 4) hipLaunchKernelGGL(corr_lookup_tile_kernel<4>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-    else if (radius == 3) hipLaunchKernelGGL(corr_lookup_tile_kernel<3>, grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-    else return false;
-    return true;
-  }
-  static const bool v1 = [] {
-    const char* e = getenv("RAFT_LOOKUP_V1");
-    return e && e[0] == '1';
-  }();
-  if (pyr_bf16 && !v1 && (radius == 4 || radius == 3)) {
+  if (pyr_bf16) {
     // pixels per workgroup (RAFT_LOOKUP_TPV): 4 (default, 10.5 KB LDS) -- 27.7 / 28.8 / 34.7 us
     // per call for 4 / 8 / 16 at chairs (profiles/r4/lookup_tpv.txt): more workgroups in flight
     // per CU keep more window-row loads outstanding
@@ -1103,24 +749,25 @@ bool launch_corr_lookup_tile(const void* const* lvl, const int* hs, const int* w
       return v == 8 || v == 16 ? v : 4;
     }();
     dim3 grid((unsigned)(B * ((N + tpv - 1) / tpv)));
-    if (tpv == 4) {
-      if (radius == 4) hipLaunchKernelGGL((corr_lookup_rows_kernel<4, 4>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-      else hipLaunchKernelGGL((corr_lookup_rows_kernel<3, 4>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-    } else if (tpv == 8) {
-      if (radius == 4) hipLaunchKernelGGL((corr_lookup_rows_kernel<4, 8>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-      else hipLaunchKernelGGL((corr_lookup_rows_kernel<3, 8>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-    } else {
-      if (radius == 4) hipLaunchKernelGGL((corr_lookup_rows_kernel<4, 16>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-      else hipLaunchKernelGGL((corr_lookup_rows_kernel<3, 16>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-    }
+#define RAFT_ROWS(RR, TT) \
+  hipLaunchKernelGGL((corr_lookup_rows_kernel<RR, TT>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels)
+    if (tpv == 4) { if (radius == 4) RAFT_ROWS(4, 4); else RAFT_ROWS(3, 4); }
+    else if (tpv == 8) { if (radius == 4) RAFT_ROWS(4, 8); else RAFT_ROWS(3, 8); }
+    else { if (radius == 4) RAFT_ROWS(4, 16); else RAFT_ROWS(3, 16); }
+#undef RAFT_ROWS
     return true;
   }
-  dim3 grid((unsigned)(B * ((N + TPW - 1) / TPW)));
-  if (radius == 4 && pyr_bf16) hipLaunchKernelGGL((corr_lookup_win_kernel<4, true>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-  else if (radius == 4) hipLaunchKernelGGL((corr_lookup_win_kernel<4, false>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-  else if (radius == 3 && pyr_bf16) hipLaunchKernelGGL((corr_lookup_win_kernel<3, true>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-  else if (radius == 3) hipLaunchKernelGGL((corr_lookup_win_kernel<3, false>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels);
-  else return false;
+  // fp32 pyramid (the reference's fp32 correlation: fp16 autocast and the fp32 schedule): bf16,
+  // fp16 (out_f16 = 1) or split-fp32 (out_f16 = 2) taps, 4 pixels per workgroup
+  dim3 grid((unsigned)(B * ((N + 3) / 4)));
+#define RAFT_ROWS32(RR, OT) \
+  hipLaunchKernelGGL((corr_lookup_rows_kernel<RR, 4, true, OT>), grid, dim3(256), 0, stream, p, coords, out, cbuf, B, H, W, levels)
+  if (radius == 4) {
+    if (out_f16 == 1) RAFT_ROWS32(4, 1); else if (out_f16 == 2) RAFT_ROWS32(4, 2); else RAFT_ROWS32(4, 0);
+  } else {
+    if (out_f16 == 1) RAFT_ROWS32(3, 1); else if (out_f16 == 2) RAFT_ROWS32(3, 2); else RAFT_ROWS32(3, 0);
+  }
+#undef RAFT_ROWS32
   return true;
 }
 
@@ -1163,13 +810,9 @@ bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, 
   const int D = 2 * radius + 1;
   if ((levels * D * D + 7) / 8 * 6 > 256) return false;  // one 16-B piece per thread per chunk
   if (radius != 3 && radius != 4) return false;
-  static const int mode = [] {  // 0 = box (default), 1 = workgroup per pixel, 2 = wave per pixel
-    const char* e = getenv("RAFT_TAPRED");
-    return e ? atoi(e) : 0;
-  }();
   const int64_t P = (int64_t)B * H * W;
   const int lds = corr_tap_reduce_lds_bytes(H, W, levels, radius);
-  if (mode == 0 && (W & 1) == 0 && list != nullptr && tl.n <= 32 && (levels * D * D + 7) / 8 <= 64) {
+  if ((W & 1) == 0 && list != nullptr && tl.n <= 32 && (levels * D * D + 7) / 8 <= 64) {
     // union-box fold for every tap type (bf16, fp16, split-fp32 rows) and dC type (bf16 pairs
     // for the mixed-precision GEMMs, fp32 for the fp16 / fp32 schedules' fp32 correlation)
     const BoxGeo bg = box_geo(H, W, levels, radius);
@@ -1177,17 +820,17 @@ bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, 
     (void)hipMemsetAsync(list, 0, sizeof(int), stream);
     dim3 grid((unsigned)((P + wpb - 1) / wpb));
     const size_t sh = (size_t)wpb * bg.wave_floats * 4;
-#define RAFT_BOX(RR, TF, O32)                                                                        \
-  hipLaunchKernelGGL((corr_tap_fold_box_kernel<RR, TF, O32>), grid, dim3(64 * wpb), sh, stream, tl, bg, \
+#define RAFT_BOX(RR, TF, OM)                                                                         \
+  hipLaunchKernelGGL((corr_tap_fold_box_kernel<RR, TF, OM>), grid, dim3(64 * wpb), sh, stream, tl, bg, \
                      levels, B, H, W, inv_sqrt_c, out, list)
-    const bool o32 = !out_bf16;
+#define RAFT_BOX_OM(RR, TF) \
+  do { if (out_bf16 == 2) RAFT_BOX(RR, TF, 2); else if (out_bf16) RAFT_BOX(RR, TF, 0); else RAFT_BOX(RR, TF, 1); } while (0)
     if (radius == 4) {
-      if (tl.tf16) { if (o32) RAFT_BOX(4, true, true); else RAFT_BOX(4, true, false); }
-      else { if (o32) RAFT_BOX(4, false, true); else RAFT_BOX(4, false, false); }
+      if (tl.tf16) RAFT_BOX_OM(4, true); else RAFT_BOX_OM(4, false);
     } else {
-      if (tl.tf16) { if (o32) RAFT_BOX(3, true, true); else RAFT_BOX(3, true, false); }
-      else { if (o32) RAFT_BOX(3, false, true); else RAFT_BOX(3, false, false); }
+      if (tl.tf16) RAFT_BOX_OM(3, true); else RAFT_BOX_OM(3, false);
     }
+#undef RAFT_BOX_OM
 #undef RAFT_BOX
     // the pixels whose windows spread past the box cap (usually none): grid-strided over the list
     dim3 g2((unsigned)std::min<int64_t>(P, 1024));
@@ -1206,24 +849,6 @@ bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, 
     if (radius == 4) hipLaunchKernelGGL((corr_tap_reduce_kernel<4, true>), grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)nullptr);
     else hipLaunchKernelGGL((corr_tap_reduce_kernel<3, true>), grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)nullptr);
     return true;
-  }
-  if (mode == 2) {
-    // one wave per query pixel: its (padded) level planes + TG staged tap rows in its LDS slice;
-    // waves per workgroup chosen for the most resident waves per CU (160 KB, <= 64 KB a group)
-    const TapGeo tg = tap_geo(H, W, levels, radius);
-    const int wave_bytes = tg.wave_floats * 4;
-    int wpb = 1, best = 0;
-    for (int c = 1; c <= 4; ++c) {
-      if (c * wave_bytes > 64 * 1024) break;
-      const int waves = c * ((160 * 1024) / (c * wave_bytes));
-      if (waves >= best) { best = waves; wpb = c; }
-    }
-    if (best > 0) {
-      dim3 grid((unsigned)((P + wpb - 1) / wpb));
-      if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<4>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, tg, levels, B, H, W, inv_sqrt_c, out, out_bf16);
-      else hipLaunchKernelGGL(corr_tap_reduce_wave_kernel<3>, grid, dim3(64 * wpb), wpb * wave_bytes, stream, tl, tg, levels, B, H, W, inv_sqrt_c, out, out_bf16);
-      return true;
-    }
   }
   dim3 grid((unsigned)P);
   if (radius == 4) hipLaunchKernelGGL(corr_tap_reduce_kernel<4>, grid, dim3(256), lds, stream, tl, levels, B, H, W, inv_sqrt_c, out, out_bf16, (const int*)nullptr);

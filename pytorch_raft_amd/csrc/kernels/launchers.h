@@ -342,6 +342,11 @@ bool launch_corr_tap_reduce(const TapList& tl, int levels, int B, int H, int W, 
 bool launch_corr_bwd_fmaps(const uint16_t* dc, int ldc, const uint16_t* f1, const uint16_t* f2,
                            uint16_t* f2t, uint16_t* g1, uint16_t* g2, int B, int N, int C,
                            hipStream_t stream);
+// fp32 correlation (split-bf16, three passes per GEMM): dc2 (2, B, N, ldc) bf16 [hi | lo] planes,
+// f1 / f2 fp32 (B, C, N); scratch f2s (2, B, C, ldc), f1s (2, B, N, C) bf16; g1 / g2 fp32 (B, N, C)
+bool launch_corr_bwd_fmaps_split(const uint16_t* dc2, int ldc, const float* f1, const float* f2,
+                                 uint16_t* f2s, uint16_t* f1s, float* g1, float* g2, int B, int N, int C,
+                                 hipStream_t stream);
 int corr_window_reduce_lds_bytes(int H, int W, int levels);
 // out: (B, N, N) fp32, or bf16 when out_bf16 (mixed-precision backward GEMMs)
 bool launch_corr_window_reduce(const WinList& wl, int levels, int B, int H, int W, int radius,

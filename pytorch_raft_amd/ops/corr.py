@@ -25,7 +25,8 @@ from . import _ext
 
 
 # RAFT_CORR_BWD_GEMM=0: the feature-map gradients of the all-pairs correlation on torch.bmm
-# (hipBLASLt) instead of the MFMA kernel of corr_bwd.hip (A/B, tests)
+# (hipBLASLt) instead of the MFMA kernels of corr_bwd.hip (bf16, and the split-bf16 passes of the
+# fp32 correlation) -- A/B and tests
 _NATIVE_BWD_GEMM = os.environ.get('RAFT_CORR_BWD_GEMM', '1') != '0'
 
 
@@ -94,10 +95,15 @@ class _AllPairsBuild(torch.autograd.Function):
         # the two feature-map GEMMs run on the hand-written MFMA kernel (corr_bwd.hip)
         native_gemm = (ctx.nhwc and bf16 and dcorr is None and bool(st.taps) and c % 128 == 0
                        and _NATIVE_BWD_GEMM)
+        # fp32 correlation (fp16 / fp32 schedules), tap path only: the fold writes dC as its
+        # split-bf16 planes and the two GEMMs run as three-pass split MFMA kernels (fp32 output)
+        split_gemm = (not ctx.nhwc and not bf16 and dcorr is None and bool(st.taps)
+                      and c % 128 == 0 and _NATIVE_BWD_GEMM)
         if st.taps:
             dt = _ext.ops().corr_tap_reduce([x[0] for x in st.taps], [x[1] for x in st.taps],
                                             h, w, len(st.pyramid), st.radius, 1.0 / math.sqrt(c),
-                                            bf16, 64 if native_gemm else 0, st.taps_split)
+                                            bf16, 64 if (native_gemm or split_gemm) else 0,
+                                            st.taps_split, split_gemm)
             dcorr = dt if dcorr is None else dcorr + dt
         st.grad = None
         st.windows = []
@@ -105,6 +111,10 @@ class _AllPairsBuild(torch.autograd.Function):
         st.pyramid = None
         if native_gemm:
             g1, g2 = _ext.ops().corr_bwd_fmaps(dcorr, fmap1, fmap2)
+            return g1.permute(0, 3, 1, 2), g2.permute(0, 3, 1, 2), None, None
+        if split_gemm:
+            # fp32 (B, H, W, C) gradients, returned as channels_last-strided (B, C, H, W) views
+            g1, g2 = _ext.ops().corr_bwd_fmaps_split(dcorr, fmap1, fmap2)
             return g1.permute(0, 3, 1, 2), g2.permute(0, 3, 1, 2), None, None
         if ctx.nhwc:
             # (B,N,C) operands: dF1 = dC F2, dF2 = dC^T F1 -> NHWC results, returned as

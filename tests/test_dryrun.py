@@ -54,13 +54,20 @@ def _returns():
         b, _, h, w = coords.shape
         return torch.zeros(b, h * w, levels, 2 * r + 2, 2 * r + 2)
 
-    def tap_reduce(coords, douts, h, w, levels, r, s, bf16=False, pitch=0, split=False):
+    def tap_reduce(coords, douts, h, w, levels, r, s, bf16=False, pitch=0, split=False,
+                   split_out=False):
         ld = (h * w + pitch - 1) // pitch * pitch if pitch else h * w
+        if split_out:
+            return torch.zeros(2, coords[0].shape[0], h * w, ld, dtype=torch.bfloat16)
         return torch.zeros(coords[0].shape[0], h * w, ld,
                            dtype=torch.bfloat16 if bf16 else torch.float32)
 
     def bwd_fmaps(dc, f1, f2):
         return [torch.zeros_like(f1), torch.zeros_like(f2)]
+
+    def bwd_fmaps_split(dc2, f1, f2):
+        b, c, h, w = f1.shape
+        return [torch.zeros(b, h, w, c), torch.zeros(b, h, w, c)]
 
     def win_reduce(coords, wgs, h, w, levels, r, s, bf16=False):
         return torch.zeros(coords[0].shape[0], h * w, h * w,
@@ -69,6 +76,7 @@ def _returns():
     return {'corr_build': corr_build, 'corr_build_bf16': corr_build_bf16, 'corr_lookup_fwd': lookup, 'corr_pyr_grad_reduce': reduce,
             'corr_window_grad': win_grad, 'corr_window_reduce': win_reduce,
             'corr_tap_reduce': tap_reduce, 'corr_bwd_fmaps': bwd_fmaps,
+            'corr_bwd_fmaps_split': bwd_fmaps_split,
             'convex_up_fwd': cup_fwd, 'convex_up_bwd': cup_bwd, 'seq_loss_fwd': loss_fwd,
             'seq_loss_bwd': loss_bwd}
 

@@ -144,8 +144,8 @@ def test_graph_step_channels_last_1x1(ext_ops):
     convc1, mask head).  Their gradients from the fused block are contiguous, which walks the
     same flat order: the native AdamW must take them as they are and never rebind ``p.grad``
     (a replayed graph keeps writing the tensor it captured -- a rebound gradient would feed step
-    1's values to every later step).  The graphed run's AdamW moments after 3 steps match the
-    eager run's for those weights."""
+    1's values to every later step).  The graphed run's AdamW first moments after 3 steps match
+    the eager run's for those weights as closely as two eager runs match each other."""
     from pytorch_raft_amd.engine.trainer import TrainState, GraphedTrainStep
     from pytorch_raft_amd.data.synthetic import device_batches
     dev = torch.device('cuda', 0)
@@ -161,16 +161,18 @@ def test_graph_step_channels_last_1x1(ext_ops):
         return m, st
 
     m_e, st_e = run(False)
+    m_e2, st_e2 = run(False)
     m_g, st_g = run(True)
     ones = [(n, p) for n, p in m_g.named_parameters()
-            if p.dim() == 4 and p.shape[2] == 1 and p.shape[3] == 1 and p.shape[1] > 1]
+            if n.startswith('update_block') and p.dim() == 4 and p.shape[2] == 1 and p.shape[3] == 1
+            and p.shape[1] > 1]
     # is_contiguous() ignores size-1 dims: compare the strides themselves
     assert ones and any(p.stride() != torch.empty(p.shape).stride() for _, p in ones), \
         'no re-strided 1x1 weight'
-    pe = dict(m_e.named_parameters())
+    pe, pe2 = dict(m_e.named_parameters()), dict(m_e2.named_parameters())
     for n, p in ones:
         me = st_e.optimizer.state[pe[n]]['exp_avg']
-        mg = st_g.optimizer.state[p]['exp_avg']
-        err = float((mg - me).norm() / me.norm().clamp_min(1e-12))
-        assert err < 5e-2, (n, err)
+        noise = float((st_e2.optimizer.state[pe2[n]]['exp_avg'] - me).norm() / me.norm().clamp_min(1e-12))
+        err = float((st_g.optimizer.state[p]['exp_avg'] - me).norm() / me.norm().clamp_min(1e-12))
+        assert err <= max(3 * noise, 2e-2), (n, err, noise)
         assert p.grad is not None

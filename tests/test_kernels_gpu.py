@@ -522,3 +522,51 @@ def test_warp_sampler_matches_grid_sample(ext_ops, convention, shape):
     (ref * gout).sum().backward()
     torch.testing.assert_close(x.grad, x2.grad, atol=5e-3, rtol=1e-3)
     torch.testing.assert_close(flo.grad, f2.grad, atol=5e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize('b,hw,c', [(2, (46, 62), 256), (3, (7, 9), 128), (1, (23, 31), 256)])
+def test_corr_bwd_fmaps_split_matches_fp64(ext_ops, b, hw, c):
+    """The fp32 correlation's feature-map gradients (fp16 / fp32 schedules, `core/corr.py:52-60`
+    in fp32): dC and the fp32 fmaps as split-bf16 pairs, three MFMA passes per GEMM, fp32 output,
+    vs fp64 matmuls -- fp32-accurate (~2^-16 relative to the largest entry)."""
+    h, w = hw
+    n = h * w
+    ld = (n + 63) // 64 * 64
+    g = torch.Generator(device=DEV).manual_seed(12)
+    d = torch.randn(b, n, n, device=DEV, generator=g)
+    dc2 = torch.zeros(2, b, n, ld, device=DEV, dtype=torch.bfloat16)
+    hi = d.to(torch.bfloat16)
+    dc2[0, ..., :n] = hi
+    dc2[1, ..., :n] = (d - hi.float()).to(torch.bfloat16)
+    f1 = torch.randn(b, c, h, w, device=DEV, generator=g)
+    f2 = torch.randn(b, c, h, w, device=DEV, generator=g)
+    g1, g2 = ext_ops.corr_bwd_fmaps_split(dc2, f1, f2)
+    dd = d.double()
+    r1 = torch.bmm(dd, f2.double().view(b, c, n).transpose(1, 2)).view(b, h, w, c)
+    r2 = torch.bmm(dd.transpose(1, 2), f1.double().view(b, c, n).transpose(1, 2)).view(b, h, w, c)
+    for got, ref in ((g1, r1), (g2, r2)):
+        assert got.shape == ref.shape and got.dtype == torch.float32
+        err = (got.double() - ref).abs().max().item()
+        assert err <= 1e-4 * ref.abs().max().item(), err
+    g1b, g2b = ext_ops.corr_bwd_fmaps_split(dc2, f1, f2)
+    assert torch.equal(g1, g1b) and torch.equal(g2, g2b)
+
+
+@pytest.mark.parametrize('hw', [(12, 16), (23, 30)])
+def test_tap_reduce_split_planes(ext_ops, hw):
+    """corr_tap_reduce(split_out=True): the fp32 dC of the fold as bf16 planes hi + lo (padded
+    pitch, zero columns) -- hi + lo reproduces the fp32 fold to ~2^-16."""
+    h, w = hw
+    b, levels, radius = 2, 4, 4
+    n = h * w
+    g = torch.Generator(device=DEV).manual_seed(5)
+    coords = [(torch.rand(b, 2, h, w, device=DEV, generator=g) * torch.tensor([w, h], device=DEV).view(1, 2, 1, 1)).contiguous()
+              for _ in range(3)]
+    douts = [torch.randn(b, h, w, 328, device=DEV, generator=g).to(torch.bfloat16) for _ in range(3)]
+    s = 1 / 16
+    ref = ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, False, 64)
+    got = ext_ops.corr_tap_reduce(coords, douts, h, w, levels, radius, s, False, 64, False, True)
+    assert got.shape == (2, b, n, ref.shape[-1]) and got.dtype == torch.bfloat16
+    v = got[0].float() + got[1].float()
+    assert (v - ref).abs().max().item() <= 2.0 ** -15 * ref.abs().max().item()
+    assert (got[..., n:] == 0).all()
