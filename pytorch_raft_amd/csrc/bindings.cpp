@@ -749,7 +749,7 @@ void conv_fwd_(const std::vector<Tensor>& ins, const std::vector<int64_t>& in_of
     a.out0 = o.data_ptr<float>();
     a.out0_stride = 0;
     TORCH_CHECK(aux.empty(), "no aux for the NCHW epilogue");
-    TORCH_CHECK(launch_conv_fwd(a, (int)epi | (spl ? EPI_SPL : 0), (int)bn, cin_small != 0, cur_stream()),
+    TORCH_CHECK(launch_conv_fwd(a, (int)epi | ef16 | (spl ? EPI_SPL : 0), (int)bn, cin_small != 0, cur_stream()),
                 "bad epilogue");
     return;
   }
@@ -1547,51 +1547,56 @@ void relu_bwd_(const Tensor& g, int64_t g_off, const c10::optional<Tensor>& y, i
   TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.scalar_type() == at::kFloat && g.dim() == 4, "g: fp32 NHWC");
   const int64_t B = g.size(0), H = g.size(1), W = g.size(2), P = B * H * W;
   TORCH_CHECK(g_off + C <= g.size(3), "g slice");
-  check_nhwc(out, B, H, W, "relu_bwd out", at::kBFloat16);
+  const at::ScalarType st = op16(out);   // bf16, or fp16 under fp16 autocast
+  check_nhwc(out, B, H, W, "relu_bwd out", st);
   TORCH_CHECK(o_off + C <= out.size(3), "out slice");
   const uint16_t* yp = nullptr;
   int ys = 0;
   if (y.has_value() && y->defined()) {
-    check_nhwc(*y, B, H, W, "relu_bwd y", at::kBFloat16);
+    check_nhwc(*y, B, H, W, "relu_bwd y", st);
     TORCH_CHECK(y_off + C <= y->size(3), "y slice");
-    yp = bf16p(*y) + y_off;
+    yp = u16(*y) + y_off;
     ys = (int)y->size(3);
   }
   c10::DeviceGuard gd(g.device());
-  launch_relu_bwd(g.data_ptr<float>() + g_off, (int)g.size(3), yp, ys, bf16m(out) + o_off,
-                  (int)out.size(3), (int)P, (int)C, (float)scale, cur_stream());
+  launch_relu_bwd(g.data_ptr<float>() + g_off, (int)g.size(3), yp, ys, u16m(out) + o_off,
+                  (int)out.size(3), (int)P, (int)C, (float)scale, cur_stream(), st == at::kHalf);
 }
 
 void gru_q_bwd_(const Tensor& dh, const Tensor& z, const Tensor& q, const Tensor& hprev,
                 const Tensor& dpre_q, const Tensor& dz, const Tensor& dhprev) {
   TORCH_CHECK(dh.dim() == 4, "dh must be (B,H,W,hd)");
   const int64_t P = dh.size(0) * dh.size(1) * dh.size(2), hd = dh.size(3);
+  const at::ScalarType st = op16(z);   // bf16, or fp16 under fp16 autocast
   check_pc(dh, P, hd, at::kFloat, "dh");
-  check_pc(z, P, hd, at::kBFloat16, "z");
-  check_pc(q, P, hd, at::kBFloat16, "q");
-  check_pc(hprev, P, hd, at::kBFloat16, "hprev");
-  check_pc(dpre_q, P, hd, at::kBFloat16, "dpre_q");
+  check_pc(z, P, hd, st, "z");
+  check_pc(q, P, hd, st, "q");
+  check_pc(hprev, P, hd, st, "hprev");
+  check_pc(dpre_q, P, hd, st, "dpre_q");
   check_pc(dz, P, hd, at::kFloat, "dz");
   check_pc(dhprev, P, hd, at::kFloat, "dhprev");
   c10::DeviceGuard gd(dh.device());
-  launch_gru_q_bwd(dh.data_ptr<float>(), bf16p(z), bf16p(q), bf16p(hprev), bf16m(dpre_q),
-                   dz.data_ptr<float>(), dhprev.data_ptr<float>(), (int)P, (int)hd, cur_stream());
+  launch_gru_q_bwd(dh.data_ptr<float>(), u16(z), u16(q), u16(hprev), u16m(dpre_q),
+                   dz.data_ptr<float>(), dhprev.data_ptr<float>(), (int)P, (int)hd, cur_stream(),
+                   st == at::kHalf);
 }
 
 void gru_zr_bwd_(const Tensor& drh, const Tensor& dz, const Tensor& z, const Tensor& r,
                  const Tensor& hprev, const Tensor& dpre_zr, const Tensor& dhprev) {
   TORCH_CHECK(drh.dim() == 4, "drh must be (B,H,W,hd)");
   const int64_t P = drh.size(0) * drh.size(1) * drh.size(2), hd = drh.size(3);
+  const at::ScalarType st = op16(z);
   check_pc(drh, P, hd, at::kFloat, "drh");
   check_pc(dz, P, hd, at::kFloat, "dz");
-  check_pc(z, P, hd, at::kBFloat16, "z");
-  check_pc(r, P, hd, at::kBFloat16, "r");
-  check_pc(hprev, P, hd, at::kBFloat16, "hprev");
-  check_pc(dpre_zr, P, 2 * hd, at::kBFloat16, "dpre_zr");
+  check_pc(z, P, hd, st, "z");
+  check_pc(r, P, hd, st, "r");
+  check_pc(hprev, P, hd, st, "hprev");
+  check_pc(dpre_zr, P, 2 * hd, st, "dpre_zr");
   check_pc(dhprev, P, hd, at::kFloat, "dhprev");
   c10::DeviceGuard gd(drh.device());
-  launch_gru_zr_bwd(drh.data_ptr<float>(), dz.data_ptr<float>(), bf16p(z), bf16p(r), bf16p(hprev),
-                    bf16m(dpre_zr), dhprev.data_ptr<float>(), (int)P, (int)hd, cur_stream());
+  launch_gru_zr_bwd(drh.data_ptr<float>(), dz.data_ptr<float>(), u16(z), u16(r), u16(hprev),
+                    u16m(dpre_zr), dhprev.data_ptr<float>(), (int)P, (int)hd, cur_stream(),
+                    st == at::kHalf);
 }
 
 // out = sum(ins) (+ carry): n <= RAFT_SUM_MAX same-shape contiguous bf16 tensors, fp32 accumulation,

@@ -13,6 +13,7 @@ bool launch_conv_glds_f16(const ConvFwdArgs& a, int epi, int idx, hipStream_t st
     case EPI_GRU_Q: return launch_glds_epi<EPI_GRU_Q | EPI_F16>(a, idx, stream);
     case EPI_DGRAD: return launch_glds_epi<EPI_DGRAD | EPI_F16>(a, idx, stream);
     case EPI_DGRAD_GATE: return launch_glds_epi<EPI_DGRAD_GATE | EPI_F16>(a, idx, stream);
+    case EPI_F32_NCHW: return launch_glds_epi<EPI_F32_NCHW | EPI_F16>(a, idx, stream);
     default: return false;
   }
 }

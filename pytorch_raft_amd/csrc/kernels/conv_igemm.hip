@@ -340,6 +340,7 @@ bool launch_epi_idx(const ConvFwdArgs& a, int epi, int idx, bool smallc, hipStre
     case EPI_GRU_Q | EPI_F16: return launch_cfg_idx<EPI_GRU_Q | EPI_F16, false>(a, idx, stream);
     case EPI_DGRAD | EPI_F16: return launch_cfg_idx<EPI_DGRAD | EPI_F16, false>(a, idx, stream);
     case EPI_DGRAD_GATE | EPI_F16: return launch_cfg_idx<EPI_DGRAD_GATE | EPI_F16, false>(a, idx, stream);
+    case EPI_F32_NCHW | EPI_F16: return launch_cfg_idx<EPI_F32_NCHW | EPI_F16, false>(a, idx, stream);
     default:
       // split fp32 (ConvFwdArgs.spl): LDS-DMA / halo configs only (cfg_allowed), dispatched by
       // conv_glds.hip / conv_halo_6.hip on the full epilogue id

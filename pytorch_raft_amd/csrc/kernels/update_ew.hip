@@ -18,6 +18,8 @@
 
 namespace {
 
+// F16: the 16-bit buffers are fp16 (fp16 autocast), else bf16
+template <bool F16>
 __global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__ g, int gs,
                                                        const uint16_t* __restrict__ y, int ys,
                                                        uint16_t* __restrict__ out, int os, int P,
@@ -28,12 +30,13 @@ __global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__
     const int64_t p = t / C;
     const int c = (int)(t - p * C);
     float v = g[p * gs + c] * scale;
-    if (y != nullptr && !(raft_bf16_to_f32(y[p * ys + c]) > 0.f)) v = 0.f;
-    out[p * os + c] = raft_f32_to_bf16(v);
+    if (y != nullptr && !(raft_h2f<F16>(y[p * ys + c]) > 0.f)) v = 0.f;
+    out[p * os + c] = raft_f2h<F16>(v);
   }
 }
 
 // hd = hidden width (128 / 96).  dpre_q (bf16, stride dq_s), dz (f32 P x hd), dh_prev (f32 P x hd)
+template <bool F16>
 __global__ __launch_bounds__(256) void gru_q_bwd_kernel(const float* __restrict__ dh, const uint16_t* __restrict__ z,
                                                         const uint16_t* __restrict__ q, const uint16_t* __restrict__ hprev,
                                                         uint16_t* __restrict__ dpre_q, float* __restrict__ dz,
@@ -42,16 +45,17 @@ __global__ __launch_bounds__(256) void gru_q_bwd_kernel(const float* __restrict_
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const float g = dh[t];
-    const float zz = raft_bf16_to_f32(z[t]);
-    const float qq = raft_bf16_to_f32(q[t]);
-    const float hh = raft_bf16_to_f32(hprev[t]);
-    dpre_q[t] = raft_f32_to_bf16(g * zz * (1.f - qq * qq));
+    const float zz = raft_h2f<F16>(z[t]);
+    const float qq = raft_h2f<F16>(q[t]);
+    const float hh = raft_h2f<F16>(hprev[t]);
+    dpre_q[t] = raft_f2h<F16>(g * zz * (1.f - qq * qq));
     dz[t] = g * (qq - hh);
     dhprev[t] = g * (1.f - zz);
   }
 }
 
 // dpre_zr (bf16 P x 2hd: [z | r]), dhprev += drh * r
+template <bool F16>
 __global__ __launch_bounds__(256) void gru_zr_bwd_kernel(const float* __restrict__ drh, const float* __restrict__ dz,
                                                          const uint16_t* __restrict__ z, const uint16_t* __restrict__ r,
                                                          const uint16_t* __restrict__ hprev, uint16_t* __restrict__ dpre_zr,
@@ -61,12 +65,12 @@ __global__ __launch_bounds__(256) void gru_zr_bwd_kernel(const float* __restrict
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = t / hd;
     const int c = (int)(t - p * hd);
-    const float zz = raft_bf16_to_f32(z[t]);
-    const float rr = raft_bf16_to_f32(r[t]);
-    const float hh = raft_bf16_to_f32(hprev[t]);
+    const float zz = raft_h2f<F16>(z[t]);
+    const float rr = raft_h2f<F16>(r[t]);
+    const float hh = raft_h2f<F16>(hprev[t]);
     const float g = drh[t];
-    dpre_zr[p * 2 * hd + c] = raft_f32_to_bf16(dz[t] * zz * (1.f - zz));
-    dpre_zr[p * 2 * hd + hd + c] = raft_f32_to_bf16(g * hh * rr * (1.f - rr));
+    dpre_zr[p * 2 * hd + c] = raft_f2h<F16>(dz[t] * zz * (1.f - zz));
+    dpre_zr[p * 2 * hd + hd + c] = raft_f2h<F16>(g * hh * rr * (1.f - rr));
     dhprev[t] += g * rr;
   }
 }
@@ -262,22 +266,35 @@ void launch_sum_bf16(const BfPtrs& ins, int n, const float* carry, void* out, bo
 }
 
 void launch_relu_bwd(const float* g, int gs, const uint16_t* y, int ys, uint16_t* out, int os, int P,
-                     int C, float scale, hipStream_t stream) {
-  hipLaunchKernelGGL(relu_bwd_kernel, dim3(ew_blocks((int64_t)P * C)), dim3(256), 0, stream, g, gs, y,
-                     ys, out, os, P, C, scale);
+                     int C, float scale, hipStream_t stream, bool f16) {
+  if (f16)
+    hipLaunchKernelGGL(relu_bwd_kernel<true>, dim3(ew_blocks((int64_t)P * C)), dim3(256), 0, stream, g, gs,
+                       y, ys, out, os, P, C, scale);
+  else
+    hipLaunchKernelGGL(relu_bwd_kernel<false>, dim3(ew_blocks((int64_t)P * C)), dim3(256), 0, stream, g, gs,
+                       y, ys, out, os, P, C, scale);
 }
 
 void launch_gru_q_bwd(const float* dh, const uint16_t* z, const uint16_t* q, const uint16_t* hprev,
-                      uint16_t* dpre_q, float* dz, float* dhprev, int P, int hd, hipStream_t stream) {
-  hipLaunchKernelGGL(gru_q_bwd_kernel, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream, dh, z, q,
-                     hprev, dpre_q, dz, dhprev, P, hd);
+                      uint16_t* dpre_q, float* dz, float* dhprev, int P, int hd, hipStream_t stream,
+                      bool f16) {
+  if (f16)
+    hipLaunchKernelGGL(gru_q_bwd_kernel<true>, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream, dh,
+                       z, q, hprev, dpre_q, dz, dhprev, P, hd);
+  else
+    hipLaunchKernelGGL(gru_q_bwd_kernel<false>, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream, dh,
+                       z, q, hprev, dpre_q, dz, dhprev, P, hd);
 }
 
 void launch_gru_zr_bwd(const float* drh, const float* dz, const uint16_t* z, const uint16_t* r,
                        const uint16_t* hprev, uint16_t* dpre_zr, float* dhprev, int P, int hd,
-                       hipStream_t stream) {
-  hipLaunchKernelGGL(gru_zr_bwd_kernel, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream, drh, dz,
-                     z, r, hprev, dpre_zr, dhprev, P, hd);
+                       hipStream_t stream, bool f16) {
+  if (f16)
+    hipLaunchKernelGGL(gru_zr_bwd_kernel<true>, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream,
+                       drh, dz, z, r, hprev, dpre_zr, dhprev, P, hd);
+  else
+    hipLaunchKernelGGL(gru_zr_bwd_kernel<false>, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream,
+                       drh, dz, z, r, hprev, dpre_zr, dhprev, P, hd);
 }
 
 void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int slot_stride, int B,

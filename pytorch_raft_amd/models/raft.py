@@ -290,20 +290,19 @@ class RAFT(nn.Module):
                 and _ext.device_ok(img) and _ext.gpu_path_enabled())
 
     def _use_fused_update(self, img):
-        """Fused MFMA update block: GPU and mixed precision -- bf16 (full and small model) or
-        fp16 autocast (full model; the operand dtype of the conv kernels' MFMAs) -- or the fp32
-        schedule of the full model (split-fp32 operands: bf16 [hi | lo] pairs, three products
+        """Fused MFMA update block: GPU and mixed precision -- bf16 or fp16 autocast (full and
+        small model; the operand dtype of the conv kernels' MFMAs) -- or the fp32 schedule of the
+        full model (split-fp32 operands: bf16 [hi | lo] pairs, three products
         per conv; RAFT_FP32_FUSED=0 keeps the per-conv split path of ops/conv_fp32.py)."""
         impl = _get(self.args, 'update_impl', 'auto')
         if impl == 'torch' or self.corr_impl == 'torch' or not _ext.device_ok(img):
             return False
-        ok = self.args.mixed_precision and (
-            self.amp_dtype == torch.bfloat16 or (self.amp_dtype == torch.float16 and not self.args.small))
+        ok = self.args.mixed_precision and self.amp_dtype in (torch.bfloat16, torch.float16)
         ok = ok or (not self.args.mixed_precision and not self.args.small and _FP32_FUSED)
         if not ok:
             if impl == 'hip':
-                raise ValueError("update_impl='hip' needs mixed precision (bf16, or fp16 for the "
-                                 "full model)")
+                raise ValueError("update_impl='hip' needs mixed precision (bf16 / fp16), or the "
+                                 "full model in fp32")
             return False
         from ..ops import update_hip
         return update_hip.available(required=(impl == 'hip'))
@@ -311,16 +310,17 @@ class RAFT(nn.Module):
     def _iterate_fused_small(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
         """RAFT-small: fused ConvGRU iterations (ops/update_hip_small.py), upflow8 output."""
         from ..ops.update_hip_small import HipSmallUpdateBlock, CORR_BUF_SMALL, HDP
-        hub = HipSmallUpdateBlock(self.update_block)
-        h = torch.nn.functional.pad(net.to(torch.bfloat16).permute(0, 2, 3, 1),
+        adt = self.amp_dtype   # bf16 or fp16 operands
+        hub = HipSmallUpdateBlock(self.update_block, dtype=adt)
+        h = torch.nn.functional.pad(net.to(adt).permute(0, 2, 3, 1),
                                     (0, HDP - net.shape[1])).contiguous()
-        x = inp.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+        x = inp.to(adt).permute(0, 2, 3, 1).contiguous()
         flow_predictions = []
         flow_up = None
         flow = coords1 - coords0
         for itr in range(iters):
             coords1 = coords1.detach()
-            corr = corr_fn.lookup_nhwc(coords1, CORR_BUF_SMALL)
+            corr = corr_fn.lookup_nhwc(coords1, CORR_BUF_SMALL, adt)
             flow = flow.detach()   # = coords1 - coords0 (see _iterate_fused)
             h, delta_flow = hub(h, x, corr, flow)
             coords1 = coords1 + delta_flow

@@ -20,6 +20,10 @@ zeros, with the padding folded into the packed weights:
 
 The backward keeps the accumulating gradients (dh, d inp, d motion) in fp32 and feeds bf16
 pre-activation gradients to the dgrad / wgrad kernels, like the full block.
+
+Operand dtype: bf16 (bf16 autocast) or fp16 (fp16 autocast, the reference's --mixed_precision,
+`core/raft.py:99`): every 16-bit buffer, packed weight and MFMA of a step is of that type
+(``HipSmallUpdateBlock(ub, dtype)``); accumulation and the carried gradients stay fp32.
 """
 import torch
 
@@ -70,8 +74,8 @@ def small_module_params(ub):
 SMALL = Design(SMALL_SPECS, small_module_params)
 
 
-def _zeros_bf16(shape, dev):
-    return torch.zeros(*shape, device=dev, dtype=torch.bfloat16)
+def _zeros_bf16(shape, dev, dt=torch.bfloat16):
+    return torch.zeros(*shape, device=dev, dtype=dt)
 
 
 def _conv(pk, name, segs, epi, outs, offs, aux=(), aux_offs=(), split=0, bias=None):
@@ -105,24 +109,25 @@ def _iter_forward(pk, h, inp, corr, flow):
     B, H, W, _ = h.shape
     dev = h.device
     sh = (B, H, W)
+    dt = pk.dtype   # bf16 / fp16 operand dtype
     ops = _ext.ops()
-    patch = _bf16(sh + (128,), dev)
-    mf = _zeros_bf16(sh + (128,), dev)        # [conv 80 | flow 2 | zeros]
+    patch = _bf16(sh + (128,), dev, dt)
+    mf = _zeros_bf16(sh + (128,), dev, dt)    # [conv 80 | flow 2 | zeros]
     ops.f1_patch_(flow, patch, mf, 80)
-    cf = _bf16(sh + (128,), dev)              # [cor 96 | flo 32]
-    f1 = _bf16(sh + (64,), dev)
+    cf = _bf16(sh + (128,), dev, dt)          # [cor 96 | flo 32]
+    f1 = _bf16(sh + (64,), dev, dt)
     _conv(pk, 'c1', [(corr, 0, CORR_BUF_SMALL)], C.EPI_RELU_BF16, [cf], [0])
     _conv(pk, 'f1', [(patch, 0, 128)], C.EPI_RELU_BF16, [f1], [0])
     _conv(pk, 'f2', [(f1, 0, 64)], C.EPI_RELU_BF16, [cf], [96])
     _conv(pk, 'conv', [(cf, 0, 128)], C.EPI_RELU_BF16, [mf], [0])
-    z, rh, r = _bf16(sh + (HDP,), dev), _bf16(sh + (HDP,), dev), _bf16(sh + (HDP,), dev)
+    z, rh, r = _bf16(sh + (HDP,), dev, dt), _bf16(sh + (HDP,), dev, dt), _bf16(sh + (HDP,), dev, dt)
     ctx = _ctx_maps(pk, inp)
     _conv(pk, 'zr', [(h, 0, HDP), (mf, 0, 128)], C.EPI_GRU_ZR, [z, rh, r], [0, 0, 0], aux=[h],
           aux_offs=[0], split=HDP, bias=ctx['zr'])
-    hn, q = _bf16(sh + (HDP,), dev), _bf16(sh + (HDP,), dev)
+    hn, q = _bf16(sh + (HDP,), dev, dt), _bf16(sh + (HDP,), dev, dt)
     _conv(pk, 'q', [(rh, 0, HDP), (mf, 0, 128)], C.EPI_GRU_Q, [hn, q], [0, 0],
           aux=[h, z], aux_offs=[0, 0], bias=ctx['q'])
-    fm = _bf16(sh + (128,), dev)
+    fm = _bf16(sh + (128,), dev, dt)
     _conv(pk, 'fh1', [(hn, 0, HDP)], C.EPI_RELU_BF16, [fm], [0])
     delta = torch.empty(B, 2, H, W, device=dev, dtype=torch.float32)
     _conv(pk, 'fh2', [(fm, 0, 128)], C.EPI_F32_NCHW, [delta], [0])
@@ -155,12 +160,13 @@ class _SmallUpdateIter(torch.autograd.Function):
         B, H, W, _ = hn.shape
         dev = hn.device
         sh = (B, H, W)
+        dt = pk.dtype
         ops = _ext.ops()
 
         def dgrad(name, gsegs, outs, scale=1.0):
             s = SMALL.spec[name]
             ry = [o[5] if len(o) > 5 else o[0] for o in outs]
-            roff = [int(o[6]) if len(o) > 5 else (-1 if o[0].dtype == torch.bfloat16 else 0)
+            roff = [int(o[6]) if len(o) > 5 else (-1 if o[0].dtype != torch.float32 else 0)
                     for o in outs]
             ops.conv_dgrad_([g[0] for g in gsegs], [g[1] for g in gsegs], [g[2] for g in gsegs],
                             pk.wd[name], s.k[0], s.k[1], s.pad[0], s.pad[1], 0, float(scale),
@@ -168,10 +174,10 @@ class _SmallUpdateIter(torch.autograd.Function):
                             [o[3] for o in outs], [o[4] for o in outs], ry, roff, [], [])
 
         # ---- flow head: conv2 (128 -> 2) as an MFMA conv on a 64-wide bf16 gradient
-        g2 = _zeros_bf16(sh + (64,), dev)
+        g2 = _zeros_bf16(sh + (64,), dev, dt)
         g2[..., :2] = gdelta.permute(0, 2, 3, 1)
         pk.defer_wgrad('fh2', g2, 0, [(fm, 0, 128)])
-        dpre_fm = _zeros_bf16(sh + (128,), dev)
+        dpre_fm = _zeros_bf16(sh + (128,), dev, dt)
         dgrad('fh2', [(g2, 0, 64)], [(dpre_fm, 0, 128, 128, 0, fm, 0)])
         pk.defer_wgrad('fh1', dpre_fm, 0, [(hn, 0, HDP)])
         dh = gh.float().contiguous() if gh is not None else _f32(sh + (HDP,), dev, zero=True)
@@ -179,33 +185,33 @@ class _SmallUpdateIter(torch.autograd.Function):
         # ---- ConvGRU (pads: every gradient buffer is zero beyond the 96 real channels); the
         # context part's input / weight gradients come once from the summed gradients (below)
         dmf = _f32(sh + (128,), dev, zero=True)
-        dpre_q = _bf16(sh + (HDP,), dev)
+        dpre_q = _bf16(sh + (HDP,), dev, dt)
         dz = _f32(sh + (HDP,), dev)
         dhp = _f32(sh + (HDP,), dev)
         ops.gru_q_bwd_(dh, z, q, h, dpre_q, dz, dhp)
         pk.defer_wgrad('q', dpre_q, 0, [(rh, 0, HDP), (mf, 0, 128)])
         drh = _f32(sh + (HDP,), dev, zero=True)
         dgrad('q', [(dpre_q, 0, HDP)], [(drh, 0, HDP, 96, 0), (dmf, 0, 128, 82, 1)])
-        dpre_zr = _bf16(sh + (2 * HDP,), dev)
+        dpre_zr = _bf16(sh + (2 * HDP,), dev, dt)
         ops.gru_zr_bwd_(drh, dz, z, r, h, dpre_zr, dhp)
         pk.defer_wgrad('zr', dpre_zr, 0, [(h, 0, HDP), (mf, 0, 128)])
         dgrad('zr', [(dpre_zr, 0, 2 * HDP)], [(dhp, 0, HDP, 96, 1), (dmf, 0, 128, 82, 1)])
         st.ctx_g.setdefault('q', []).append(dpre_q)
         st.ctx_g.setdefault('zr', []).append(dpre_zr)
         # ---- motion encoder
-        dpre_conv = _zeros_bf16(sh + (128,), dev)
+        dpre_conv = _zeros_bf16(sh + (128,), dev, dt)
         ops.relu_bwd_(dmf, 0, mf, 0, dpre_conv, 0, 80, 1.0)
         pk.defer_wgrad('conv', dpre_conv, 0, [(cf, 0, 128)])
-        dpre_cf = _bf16(sh + (128,), dev)
+        dpre_cf = _bf16(sh + (128,), dev, dt)
         dgrad('conv', [(dpre_conv, 0, 128)], [(dpre_cf, 0, 128, 128, 0, cf, 0)])
         pk.defer_wgrad('c1', dpre_cf, 0, [(corr, 0, CORR_BUF_SMALL)])
         pk.defer_wgrad('f2', dpre_cf, 96, [(f1, 0, 64)])
-        dpre_f1 = _bf16(sh + (64,), dev)
+        dpre_f1 = _bf16(sh + (64,), dev, dt)
         # f2's outputs are channels 96..127 of dpre_cf: the adjoint reads [64, 128) with the
         # layer's rows at offset 32 of it (adj_off), c1's rows at [0, 96) of [0, 128)
         dgrad('f2', [(dpre_cf, 64, 64)], [(dpre_f1, 0, 64, 64, 0, f1, 0)])
         pk.defer_wgrad('f1', dpre_f1, 0, [(patch, 0, 128)])
-        dcorr = _bf16(sh + (CORR_BUF_SMALL,), dev)
+        dcorr = _bf16(sh + (CORR_BUF_SMALL,), dev, dt)
         dgrad('c1', [(dpre_cf, 0, 128)], [(dcorr, 0, CORR_BUF_SMALL, 196, 0)])
         dinp = None
         if ctx.itr == 0:
@@ -222,10 +228,12 @@ class _SmallUpdateIter(torch.autograd.Function):
 class HipSmallUpdateBlock:
     """Drives the fused iterations for one forward pass of a SmallUpdateBlock."""
 
-    def __init__(self, update_block):
+    def __init__(self, update_block, dtype=torch.bfloat16):
+        assert dtype in (torch.bfloat16, torch.float16), dtype
         self.state = _State()
         self.state.ub = update_block
         self.state.design = SMALL
+        self.state.dtype = dtype
         params = SMALL.flat_params(update_block)
         self.state.need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         self.state.params = params

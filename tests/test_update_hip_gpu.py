@@ -273,16 +273,18 @@ def test_fused_iterations_match_eager_bf16_same_precision(ext_ops):
     assert not bad, '\n'.join('%s: %s' % r for r in bad)
 
 
-def test_small_model_fused_matches_eager_bf16(ext_ops):
+@pytest.mark.parametrize('amp', ['bfloat16', 'float16'])
+def test_small_model_fused_matches_eager_bf16(ext_ops, amp):
     """RAFT-small on the fused ConvGRU path (ops/update_hip_small.py) vs the eager small model
-    under bf16 autocast (`core/update.py:16-31,62-77,99-112`): same loss, flow and gradients
-    within bf16 tolerance, and the fused path is the one that ran."""
+    under bf16 / fp16 autocast (`core/update.py:16-31,62-77,99-112`; fp16 is the reference's
+    --mixed_precision): same loss, flow and gradients within 16-bit tolerance, and the fused
+    path is the one that ran."""
     from pytorch_raft_amd.ops import update_hip_small
     i1, i2, flow, valid = make_pair_batch(2, 128, 160, device=DEV)
     outs = {}
     for impl in ('torch', 'hip'):
         args = argparse.Namespace(small=True, mixed_precision=True, corr_impl='hip',
-                                  update_impl=impl)
+                                  update_impl=impl, amp_dtype=amp)
         torch.manual_seed(0)
         m = RAFT(args).to(DEV).train()
         assert m._use_fused_update(i1) == (impl == 'hip')
