@@ -74,15 +74,12 @@ std::vector<Tensor> corr_build(const Tensor& f1, const Tensor& f2, int64_t level
   return out;
 }
 
-// bf16 (or fp16: fp16 autocast, fp32 pyramid only) fmaps in NHWC memory, (B,H,W,C) contiguous
-// (the channels_last encoder outputs, permuted)
+// bf16 fmaps in NHWC memory, (B,H,W,C) contiguous (the channels_last encoder outputs, permuted)
 std::vector<Tensor> corr_build_bf16(const Tensor& f1, const Tensor& f2, int64_t levels,
                                     bool pyr_bf16) {
-  const bool f16 = f1.scalar_type() == at::kHalf;
-  TORCH_CHECK(f1.is_cuda() && f2.is_cuda() && (f1.scalar_type() == at::kBFloat16 || f16) &&
-                  f2.scalar_type() == f1.scalar_type() && f1.is_contiguous() && f2.is_contiguous(),
-              "fmaps must be contiguous bf16 / fp16 (B,H,W,C) GPU tensors");
-  TORCH_CHECK(!(f16 && pyr_bf16), "fp16 fmaps build an fp32 pyramid");
+  TORCH_CHECK(f1.is_cuda() && f2.is_cuda() && f1.scalar_type() == at::kBFloat16 &&
+                  f2.scalar_type() == at::kBFloat16 && f1.is_contiguous() && f2.is_contiguous(),
+              "fmaps must be contiguous bf16 (B,H,W,C) GPU tensors");
   TORCH_CHECK(f1.dim() == 4 && f1.sizes() == f2.sizes(), "fmap1/fmap2 must be equal (B,H,W,C)");
   TORCH_CHECK(levels >= 1 && levels <= 4, "levels must be 1..4");
   const int64_t B = f1.size(0), H = f1.size(1), W = f1.size(2), C = f1.size(3);
@@ -109,7 +106,7 @@ std::vector<Tensor> corr_build_bf16(const Tensor& f1, const Tensor& f2, int64_t 
   launch_corr_build_bf16(reinterpret_cast<const uint16_t*>(f1.data_ptr()),
                          reinterpret_cast<const uint16_t*>(f2.data_ptr()), ptr.data(), hs.data(),
                          ws.data(), (int)B, (int)C, (int)H, (int)W, (int)levels, pyr_bf16,
-                         cur_stream(), f16);
+                         cur_stream());
   return out;
 }
 

@@ -187,10 +187,7 @@ struct PyrO {
   int w[4];
 };
 
-// F16: fp16 fmaps (fp16 autocast).  An fp16 x fp16 product is exact in fp32 (22 significant
-// bits), so v_mfma_f32_32x32x16_f16 forms exactly the products of the reference's fp32 matmul on
-// the .float() fmaps (`core/raft.py:102-103`), like the bf16 form does for bf16 fmaps.
-template <typename OutT, bool F16 = false>
+template <typename OutT>
 __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(const uint16_t* __restrict__ f1,
                                                                  const uint16_t* __restrict__ f2,
                                                                  PyrO<OutT> out, int C, int H, int W,
@@ -259,16 +256,14 @@ __global__ __launch_bounds__(256, 2) void corr_build_bf16_kernel(const uint16_t*
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[a][j] = raft_mfma32<F16>(__builtin_bit_cast(raft_v8bf16, fa[0][a]),
-                                     __builtin_bit_cast(raft_v8bf16, fb[0][j]), acc[a][j]);
+        acc[a][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0][a], fb[0][j], acc[a][j], 0, 0, 0);
     if (kk + 1 >= ksteps) break;
     if (kk + 2 < ksteps) load((kk + 2) * 16, 0);
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[a][j] = raft_mfma32<F16>(__builtin_bit_cast(raft_v8bf16, fa[1][a]),
-                                     __builtin_bit_cast(raft_v8bf16, fb[1][j]), acc[a][j]);
+        acc[a][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1][a], fb[1][j], acc[a][j], 0, 0, 0);
   }
 
   // ---- level 0 straight from the accumulators; level 1 from the wave's row pair
@@ -377,7 +372,7 @@ void launch_corr_build(const float* f1, const float* f2, float* const* lvl, cons
 
 void launch_corr_build_bf16(const uint16_t* f1, const uint16_t* f2, void* const* lvl, const int* hs,
                             const int* ws, int B, int C, int H, int W, int levels, bool pyr_bf16,
-                            hipStream_t stream, bool f16) {
+                            hipStream_t stream) {
   const int N = H * W;
   const int tiles_i = (int)raft_cdiv(N, BB_I), bands_y = (int)raft_cdiv(H, BB_Y);
   const int tiles_x = (int)raft_cdiv(W, BB_X);
@@ -390,14 +385,10 @@ void launch_corr_build_bf16(const uint16_t* f1, const uint16_t* f2, void* const*
       p.h[l] = l < levels ? hs[l] : 0;
       p.w[l] = l < levels ? ws[l] : 0;
     }
-    if (f16)
-      hipLaunchKernelGGL((corr_build_bf16_kernel<T, true>), grid, dim3(256), 0, stream, f1, f2, p, C, H,
-                         W, levels, 1.0f / sqrtf((float)C), tiles_i, bands_y, tiles_x);
-    else
-      hipLaunchKernelGGL((corr_build_bf16_kernel<T, false>), grid, dim3(256), 0, stream, f1, f2, p, C,
-                         H, W, levels, 1.0f / sqrtf((float)C), tiles_i, bands_y, tiles_x);
+    hipLaunchKernelGGL(corr_build_bf16_kernel<T>, grid, dim3(256), 0, stream, f1, f2, p, C, H, W,
+                       levels, 1.0f / sqrtf((float)C), tiles_i, bands_y, tiles_x);
   };
-  if (pyr_bf16) go((uint16_t*)nullptr);   // bf16 pyramid: bf16 operands only (binding checks)
+  if (pyr_bf16) go((uint16_t*)nullptr);
   else go((float*)nullptr);
 }
 

@@ -18,7 +18,7 @@ void launch_corr_build(const float* f1, const float* f2, float* const* lvl, cons
 // bf16 NHWC fmaps (B,H,W,C), C % 16 == 0
 void launch_corr_build_bf16(const uint16_t* f1, const uint16_t* f2, void* const* lvl, const int* hs,
                             const int* ws, int B, int C, int H, int W, int levels, bool pyr_bf16,
-                            hipStream_t stream, bool f16 = false);
+                            hipStream_t stream);
 void launch_corr_pyr_grad_reduce(float* const* glvl, const int* hs, const int* ws, int64_t planes,
                                  int levels, float inv_sqrt_c, float* out, hipStream_t stream);
 

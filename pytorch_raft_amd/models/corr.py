@@ -130,9 +130,6 @@ class CorrBlock:
             # backward GEMMs take a bf16 dcorr.  fp32 fmaps use the exact-f32 MFMA build.
             if precision == 'bf16' and fmap1.dtype == torch.bfloat16 and fmap1.shape[1] % 16 == 0:
                 f1, f2 = fmap1, fmap2
-            elif precision == 'fp32' and fmap1.dtype == torch.float16 and fmap1.shape[1] % 16 == 0:
-                # fp16 autocast: fp16 MFMA build with exact products, fp32 pyramid and backward
-                f1, f2 = fmap1, fmap2
             else:
                 f1, f2 = fmap1.float().contiguous(), fmap2.float().contiguous()
             self.volume = corr_ops.AllPairsVolume(

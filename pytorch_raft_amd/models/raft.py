@@ -205,10 +205,9 @@ class RAFT(nn.Module):
         """Correlation volume + GRU iterations + upsampling (`core/raft.py:102-144`)."""
         otf = self._use_onthefly(fmap1)
         self.last_corr = 'on-the-fly' if otf else 'all-pairs'
-        if not (self._16bit_corr_ok(fmap1) and not otf):
-            # the reference runs the correlation in fp32 (`core/raft.py:102-103`); the bf16 / fp16
-            # HIP builds take the 16-bit encoder outputs as they are (same products, fp32
-            # accumulation; fp16: fp32 pyramid and fp32 backward)
+        if not (self._bf16_corr_ok(fmap1) and not otf):
+            # the reference runs the correlation in fp32 (`core/raft.py:102-103`); the bf16 HIP
+            # build takes the bf16 encoder outputs as they are (same products, fp32 accumulation)
             fmap1 = fmap1.float().contiguous()
             fmap2 = fmap2.float().contiguous()
         # bf16 mixed precision: bf16 MFMA correlation; fp32 model and fp16 autocast: the
@@ -271,11 +270,6 @@ class RAFT(nn.Module):
         esz = 2 if self._bf16_corr_ok(fmap) else 4
         pyramid = b * n * n * esz * (1 + 1 / 4 + 1 / 16 + 1 / 64)
         return pyramid > corr_budget_bytes(fmap.device)
-
-    def _16bit_corr_ok(self, fmap):
-        return self._bf16_corr_ok(fmap) or (
-            fmap.dtype == torch.float16 and self.corr_impl != 'torch' and
-            bool(self.args.mixed_precision) and _ext.device_ok(fmap))
 
     def _bf16_corr_ok(self, fmap):
         return (fmap.dtype == torch.bfloat16 and self.corr_impl != 'torch' and

@@ -58,19 +58,12 @@ class _AllPairsBuild(torch.autograd.Function):
     def forward(ctx, fmap1, fmap2, levels, state):
         ops = _ext.ops()
         ctx.nhwc = fmap1.dtype == torch.bfloat16
-        ctx.f16 = fmap1.dtype == torch.float16
         if ctx.nhwc:
             # mixed precision: bf16 MFMA straight from the NHWC encoder outputs (no fp32 copy);
             # a bf16 pyramid when only the NHWC lookup (fused update block, bf16 output) reads it
             f1, f2 = _nhwc_bf16(fmap1), _nhwc_bf16(fmap2)
             pyr = ops.corr_build_bf16(f1, f2, levels, bool(state.pyr_bf16))
             ctx.save_for_backward(f1, f2)
-        elif ctx.f16:
-            # fp16 autocast: the reference correlates fmap.float() in fp32 (`core/raft.py:102-103`).
-            # fp16 x fp16 products are exact in fp32, so the fp16 MFMA build (fp32 accumulation,
-            # fp32 pyramid) forms the same products from the fp16 encoder outputs as they are
-            pyr = ops.corr_build_bf16(_nhwc_bf16(fmap1), _nhwc_bf16(fmap2), levels, False)
-            ctx.save_for_backward(fmap1, fmap2)
         else:
             pyr = ops.corr_build(fmap1, fmap2, levels)
             ctx.save_for_backward(fmap1, fmap2)
@@ -87,11 +80,6 @@ class _AllPairsBuild(torch.autograd.Function):
         if st.grad is None and not st.windows and not st.taps:
             return None, None, None, None
         b, c, h, w = ctx.shape
-        if ctx.f16:
-            # the fp32 correlation's backward (below) on the fp32 values of the fp16 fmaps; the
-            # fp32 gradients are cast back to fp16 by autograd, as the reference's .float() does
-            fmap1 = fmap1.float().contiguous()
-            fmap2 = fmap2.float().contiguous()
         dcorr = None
         # mixed precision, window path only: dcorr in bf16 and bf16 GEMMs (fp32 accumulation);
         # the fmaps are bf16 encoder outputs, so only the dcorr rounding differs from fp32
@@ -234,7 +222,7 @@ class AllPairsVolume:
         # bf16 encoder outputs are channels_last: kept as they are, so _nhwc_bf16's permute is
         # already contiguous (a plain .contiguous() here made an NCHW copy that _nhwc_bf16 then
         # permuted back: two full copies of each fmap per step)
-        if fmap1.dtype in (torch.bfloat16, torch.float16):
+        if fmap1.dtype == torch.bfloat16:
             fmap1 = fmap1.contiguous(memory_format=torch.channels_last)
             fmap2 = fmap2.contiguous(memory_format=torch.channels_last)
         else:
