@@ -1258,22 +1258,6 @@ const float* opt_f32(const c10::optional<Tensor>& t, int64_t n, const char* name
   return t->data_ptr<float>();
 }
 
-// Image chunking of the instance-norm passes (statistics are per image, so a chunk is exact):
-// with RAFT_NORM_CHUNK_MB = M > 0, a call whose passes touch more than M MB runs stats +
-// finalize + apply per chunk of images, so the apply pass re-reads a chunk the statistics pass
-// has just read while it is still in the 256 MB Infinity Cache.  Returns the images per chunk.
-int64_t norm_chunk_images(int64_t N, int64_t bytes_per_image) {
-  static const int64_t mb = [] {
-    const char* e = getenv("RAFT_NORM_CHUNK_MB");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-  }();
-  if (mb <= 0 || N <= 1 || bytes_per_image <= 0) return N;
-  const int64_t per = std::max<int64_t>(1, (mb << 20) / bytes_per_image);
-  if (per >= N) return N;
-  const int64_t parts = (N + per - 1) / per;
-  return (N + parts - 1) / parts;   // equal chunks
-}
-
 // y = act(norm(x + cbias)) [+ res, relu]; returns (mean, invstd) for the backward
 std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
                               const c10::optional<Tensor>& gamma, const c10::optional<Tensor>& beta,
@@ -1307,33 +1291,19 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
   const uint16_t* xp = u16(x);
   int ppb = 0, nblk = 0;
   Tensor part;
-  const auto ys = opt_split(ysplit, x, "ysplit");
-  // 16-bit units per element (fp32 tensors are addressed as uint16 pairs)
-  const int64_t eu = st == at::kFloat ? 2 : 1;
-  // instance norm: image chunks (see norm_chunk_images); x read twice, y written, res read
-  const int64_t nc = mode == 0 ? norm_chunk_images(N, HW * C * eu * 2 * (rp ? 4 : 3)) : N;
   if (mode <= 1) {
     nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
     part = at::empty({groups * (nblk + 1) * 2 * C}, fo);  // partials + per-group sums
+    launch_norm_stats(xp, (int)N, (int)HW, (int)C, mode == 0, part.data_ptr<float>(), nblk, ppb,
+                      norm_ty(st), cur_stream());
   }
-  for (int64_t n0 = 0; n0 < N; n0 += nc) {
-    const int64_t n = std::min(nc, N - n0);
-    const int64_t eo = n0 * HW * C * eu;   // element offset of the chunk (16-bit units)
-    const int64_t go = mode == 0 ? n0 * C : 0;
-    if (mode <= 1)
-      launch_norm_stats(xp + eo, (int)n, (int)HW, (int)C, mode == 0,
-                        part.data_ptr<float>() + (mode == 0 ? n0 * nblk * 2 * C : 0), nblk, ppb,
-                        norm_ty(st), cur_stream());
-    launch_norm_finalize(mode <= 1 ? part.data_ptr<float>() + (mode == 0 ? n0 * nblk * 2 * C : 0) : nullptr,
-                         xp + eo, (int)n, (int)HW, (int)C, (int)mode, nblk, gp, bp, cb, rm, rv,
-                         (float)momentum, (float)eps, mean.data_ptr<float>() + go,
-                         invstd.data_ptr<float>() + go, scale.data_ptr<float>() + n0 * C,
-                         shift.data_ptr<float>() + n0 * C, norm_ty(st), cur_stream());
-    launch_norm_apply(xp + eo, scale.data_ptr<float>() + n0 * C, shift.data_ptr<float>() + n0 * C,
-                      (int)n, (int)HW, (int)C, (int)relu, rp ? rp + eo : nullptr, u16m(y) + eo,
-                      norm_ty(st), cur_stream(), ys.first ? ys.first + n0 * HW * 2 * ys.second : nullptr,
-                      ys.second);
-  }
+  launch_norm_finalize(mode <= 1 ? part.data_ptr<float>() : nullptr, xp, (int)N, (int)HW, (int)C,
+                       (int)mode, nblk, gp, bp, cb, rm, rv, (float)momentum, (float)eps,
+                       mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                       shift.data_ptr<float>(), norm_ty(st), cur_stream());
+  const auto ys = opt_split(ysplit, x, "ysplit");
+  launch_norm_apply(xp, scale.data_ptr<float>(), shift.data_ptr<float>(), (int)N, (int)HW, (int)C,
+                    (int)relu, rp, u16m(y), norm_ty(st), cur_stream(), ys.first, ys.second);
   return {mean, invstd};
 }
 
@@ -1390,34 +1360,11 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y
     TORCH_CHECK(!(dy2.has_value() && dy2->defined()), "dy2 needs yres");
   }
   const auto dxs = opt_split(dxsplit, x, "dxsplit");
-  const int64_t eu = st == at::kFloat ? 2 : 1;
-  // instance norm: image chunks (see norm_chunk_images); dy and x read twice, dx written, the
-  // block-end mask's tensors read and g written once
-  const int64_t nt = 5 + (yp ? 2 : 0) + (yr ? 2 : 0) + (d2 ? 1 : 0) + (go ? 2 : 0);
-  const int64_t nc = mode == 0 ? norm_chunk_images(N, HW * C * eu * 2 * nt) : N;
-  if (nc >= N) {
-    launch_norm_bwd(u16(dy),
-                    u16(x), yp, mean.data_ptr<float>(),
-                    invstd.data_ptr<float>(), (int)N, (int)HW, (int)C, (int)mode, (int)relu, gp, bp,
-                    part.data_ptr<float>(), nblk, ppb, coef.data_ptr<float>(), dg, db, dc,
-                    u16m(dx), d2, yr, go, norm_ty(st), cur_stream(), dxs.first, dxs.second);
-    return;
-  }
-  // per-image groups: chunk k's partials / coefficients / parameter terms are its rows of the
-  // call's tables; the last chunk's apply sums the parameter terms of every image
-  float* pg_all = part.data_ptr<float>() + (int64_t)groups * nblk * 3 * C;
-  for (int64_t n0 = 0; n0 < N; n0 += nc) {
-    const int64_t n = std::min(nc, N - n0);
-    const int64_t eo = n0 * HW * C * eu;
-    const bool last = n0 + n >= N;
-    launch_norm_bwd(u16(dy) + eo, u16(x) + eo, yp ? yp + eo : nullptr, mean.data_ptr<float>() + n0 * C,
-                    invstd.data_ptr<float>() + n0 * C, (int)n, (int)HW, (int)C, (int)mode, (int)relu, gp,
-                    bp, part.data_ptr<float>() + n0 * nblk * 3 * C, nblk, ppb,
-                    coef.data_ptr<float>() + n0 * 5 * C, dg, db, dc, u16m(dx) + eo, d2 ? d2 + eo : nullptr,
-                    yr ? yr + eo : nullptr, go ? go + eo : nullptr, norm_ty(st), cur_stream(),
-                    dxs.first ? dxs.first + n0 * HW * 2 * dxs.second : nullptr, dxs.second,
-                    pg_all + n0 * 3 * C, last ? (int)N : 0);
-  }
+  launch_norm_bwd(u16(dy),
+                  u16(x), yp, mean.data_ptr<float>(),
+                  invstd.data_ptr<float>(), (int)N, (int)HW, (int)C, (int)mode, (int)relu, gp, bp,
+                  part.data_ptr<float>(), nblk, ppb, coef.data_ptr<float>(), dg, db, dc,
+                  u16m(dx), d2, yr, go, norm_ty(st), cur_stream(), dxs.first, dxs.second);
 }
 
 // context-encoder output: cnet (B,C,H,W) channels_last bf16 / fp16 -> h (B,H,W,hdim) =

@@ -879,12 +879,11 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
                      float* dgamma, float* dbeta, float* dcbias, uint16_t* dx,
                      const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int f16, hipStream_t stream,
-                     uint16_t* dxs, int spad, float* pg_out, int sum_groups) {
+                     uint16_t* dxs, int spad) {
   if (f16 != 2) dxs = nullptr;
   const int per_image = mode == 0 ? 1 : 0;
   const int groups = per_image ? N : 1;
   const int cnt = per_image ? HW : N * HW;
-  if (sum_groups < 0) sum_groups = groups;
   if (mode == 0 || mode == 1) {
     dim3 grid(nblk, groups);
     if (f16 == 2) hipLaunchKernelGGL(norm_bwd_stats_kernel<2>, grid, dim3(NT), 0, stream, dy, x, mean, invstd, gamma,
@@ -906,13 +905,8 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
   // the block-end ReLU ran in the statistics pass: the apply pass reads its result
   if (yres != nullptr) dy = gout;
   // per-group sums + coefficients in one launch; pg (the groups' parameter-gradient terms) sits
-  // after the partials in `part`, or at pg_out (an image chunk of a larger call: the chunk's rows
-  // of the whole call's table)
-  float* pg = pg_out != nullptr ? pg_out : part + (int64_t)groups * nblk * 3 * C;
-  // the apply's first workgroup sums sum_groups rows of the table from `pgsum` (the whole call's
-  // table on its last chunk; none on the other chunks: sum_groups = 0)
-  const float* pgsum = sum_groups > 0 ? (pg_out != nullptr ? pg_out - (int64_t)(sum_groups - groups) * 3 * C : pg)
-                                      : nullptr;
+  // after the partials in `part`
+  float* pg = part + (int64_t)groups * nblk * 3 * C;
   if (nblk > 64) {
     if (f16 == 2) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, 2>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                        stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
@@ -930,11 +924,11 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
   }
   const int64_t nvec = (int64_t)N * HW * C / 8;
   if (f16 == 2) hipLaunchKernelGGL(norm_bwd_apply_kernel<2>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
-                     HW, C, per_image, nvec, relu, dx, pgsum, sum_groups, dgamma, dbeta, dcbias, dxs, spad);
+                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias, dxs, spad);
   else if (f16) hipLaunchKernelGGL(norm_bwd_apply_kernel<1>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
-                     HW, C, per_image, nvec, relu, dx, pgsum, sum_groups, dgamma, dbeta, dcbias, dxs, spad);
+                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias, dxs, spad);
   else hipLaunchKernelGGL(norm_bwd_apply_kernel<0>, dim3(grid_for(nvec)), dim3(NT), 0, stream, dy, x, y, coef,
-                     HW, C, per_image, nvec, relu, dx, pgsum, sum_groups, dgamma, dbeta, dcbias, dxs, spad);
+                     HW, C, per_image, nvec, relu, dx, pg, groups, dgamma, dbeta, dcbias, dxs, spad);
 }
 
 void launch_ctx_act(const uint16_t* in, int64_t P, int C, int hdim, uint16_t* h, uint16_t* x, int f16,

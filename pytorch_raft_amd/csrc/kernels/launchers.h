@@ -394,11 +394,7 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
                      const float* beta, float* part, int nblk, int pix_per_blk, float* coef,
                      float* dgamma, float* dbeta, float* dcbias, uint16_t* dx,
                      const uint16_t* dy2, const uint16_t* yres, uint16_t* gout, int f16, hipStream_t stream,
-                     uint16_t* dxs = nullptr, int spad = 0, float* pg_out = nullptr,
-                     int sum_groups = -1);
-// (pg_out, sum_groups): an image chunk of a larger instance-norm call writes its rows of the
-// call's parameter-term table at pg_out; the apply sums sum_groups rows ending with this chunk's
-// into dgamma / dbeta / dcbias (the call's last chunk: all of them; 0: no sum; -1: this call's)
+                     uint16_t* dxs = nullptr, int spad = 0);
 
 // ---- multi-tensor AdamW + global-norm clip + GradScaler unscale / overflow skip (adamw.hip)
 struct AdamTensor {
