@@ -20,8 +20,6 @@
 #include "common.h"
 #include "launchers.h"
 
-#include <cstdlib>
-
 namespace {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -54,14 +52,15 @@ constexpr int OBUF = TH * TW * OROW;           // 18,432 B
 // LDS offset of halo pixel hp (row-major over the 10 x 18 halo; hp >= 180: spare row 10)
 __device__ __forceinline__ int hoff(int hp) { return (hp / HWD) * AROWB + (hp % HWD) * AROW; }
 
-// PIPE: the K loop reads the next tap's 12 fragments (4 weight + 8 halo, ds_read_b128) before
-// the current tap's 8 MFMAs, fenced by scheduling barriers.  Left to itself the compiler issued
-// each MFMA pair's reads just before it and waited on them (lgkmcnt(0..2) ahead of every second
-// MFMA), exposing the LDS latency at one wave per SIMD.  PIPE = false keeps that schedule (A/B).
-// NSET: register sets of halo loads in flight (tiles ahead).  One workgroup per CU moves a tile's
-// 24.6 KB halo per ~3.7 us, so at HBM latency under load the loads in flight, not the MFMAs, set
-// the pace: 3 sets keep ~74 KB per CU outstanding instead of ~49 KB.
-template <bool PIPE, int NSET, bool F16 = false>
+// The K loop reads the next tap's 12 fragments (4 weight + 8 halo, ds_read_b128) before the
+// current tap's 8 MFMAs, fenced by scheduling barriers.  Left to itself the compiler issued each
+// MFMA pair's reads just before it and waited on them (lgkmcnt(0..2) ahead of every second MFMA),
+// exposing the LDS latency at one wave per SIMD.
+// NSET = 3 register sets of halo loads in flight (tiles ahead).  One workgroup per CU moves a
+// tile's 24.6 KB halo per ~3.7 us, so at HBM latency under load the loads in flight, not the
+// MFMAs, set the pace: 3 sets keep ~74 KB per CU outstanding instead of ~49 KB with 2.
+constexpr int NSET = 3;
+template <bool F16 = false>
 __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __restrict__ x,
                                                             const uint16_t* __restrict__ wpk,
                                                             uint16_t* __restrict__ out, int B,
@@ -86,40 +85,26 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
   auto load_a = [&](int t, uint4 (&areg)[APER]) {
     const int b = t / (tiles_y * tiles_x), r = t - b * tiles_y * tiles_x;
     const int y0 = (r / tiles_x) * TH - 1, x0 = (r % tiles_x) * TW - 1;
-    if constexpr (PIPE) {
-      // branch-free: per-image buffer descriptor, out-of-image pieces (and tiles past the end:
-      // zero-sized descriptor) read as zeros -- no control flow, so the wait before this
-      // register set's LDS store counts only its own loads, not the next tile's
-      const rsrc_t rs = mk_rsrc(x + (int64_t)b * H * W * 64, t < ntiles ? (uint32_t)H * W * 128 : 0u);
+    // branch-free: per-image buffer descriptor, out-of-image pieces (and tiles past the end:
+    // zero-sized descriptor) read as zeros -- no control flow, so the wait before this register
+    // set's LDS store counts only its own loads, not the next tile's
+    const rsrc_t rs = mk_rsrc(x + (int64_t)b * H * W * 64, t < ntiles ? (uint32_t)H * W * 128 : 0u);
 #pragma unroll
-      for (int j = 0; j < APER; ++j) {
-        const int e = tid + j * NTH;
-        const int hp = e >> 3, q = e & 7;
-        const int yy = y0 + hp / HWD, xx = x0 + hp % HWD;
-        const bool in = e < APIECES && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-        const uint32_t off = in ? (uint32_t)((yy * W + xx) * 128 + q * 16) : OOB;
-        areg[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < APER; ++j) {
-        const int e = tid + j * NTH;
-        const int hp = e >> 3, q = e & 7;
-        const int yy = y0 + hp / HWD, xx = x0 + hp % HWD;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (e < APIECES && t < ntiles && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
-          v = *reinterpret_cast<const uint4*>(x + (((int64_t)b * H + yy) * W + xx) * 64 + q * 8);
-        areg[j] = v;
-      }
+    for (int j = 0; j < APER; ++j) {
+      const int e = tid + j * NTH;
+      const int hp = e >> 3, q = e & 7;
+      const int yy = y0 + hp / HWD, xx = x0 + hp % HWD;
+      const bool in = e < APIECES && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const uint32_t off = in ? (uint32_t)((yy * W + xx) * 128 + q * 16) : OOB;
+      areg[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
     }
   };
   auto store_a = [&](int buf, const uint4 (&areg)[APER]) {
 #pragma unroll
     for (int j = 0; j < APER; ++j) {
       const int e = tid + j * NTH;
-      // PIPE: pieces past the halo land in the buffer's spare rows (no branch)
-      if (PIPE || e < APIECES)
-        *reinterpret_cast<uint4*>(As + buf * ABUF + hoff(e >> 3) + (e & 7) * 16) = areg[j];
+      // pieces past the halo land in the buffer's spare rows (no branch)
+      *reinterpret_cast<uint4*>(As + buf * ABUF + hoff(e >> 3) + (e & 7) * 16) = areg[j];
     }
   };
 
@@ -132,13 +117,13 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
   }
   const int bbase = (wn * 32 + (lane & 31)) * BROW + (lane >> 5) * 16;
 
-  // two tiles of halo loads in flight per thread (HBM latency x bandwidth per CU needs ~2 tiles'
-  // 23 KB): registers R0 / R1 alternate; the loop is unrolled by two so both stay static
+  // three tiles of halo loads in flight per thread: register sets R0 / R1 / R2 rotate; the loop
+  // is unrolled by three so all stay static
   uint4 R0[APER], R1[APER], R2[APER];
   const int G = gridDim.x;
   load_a(blockIdx.x, R0);
   load_a(blockIdx.x + G, R1);
-  if constexpr (NSET == 3) load_a(blockIdx.x + 2 * G, R2);
+  load_a(blockIdx.x + 2 * G, R2);
   auto tile = [&](int t, int buf, uint4 (&R)[APER]) {
     store_a(buf, R);
     __syncthreads();  // halo (and, first time, weights) visible; the other buffer is free
@@ -167,7 +152,7 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
         for (int i = 0; i < 2; ++i)
           acc[i] = raft_mfma32<F16>(af[kk][i], bfr[kk], acc[i]);
     };
-    if constexpr (PIPE) {
+    {
       bf16x8_t af[2][4][2], bfr[2][4];
       frags(0, af[0], bfr[0]);
 #pragma unroll
@@ -176,13 +161,6 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
         __builtin_amdgcn_sched_barrier(0);
         mma(af[tap & 1], bfr[tap & 1]);
         __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        bf16x8_t af[4][2], bfr[4];
-        frags(tap, af, bfr);
-        mma(af, bfr);
       }
     }
 
@@ -207,29 +185,18 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
       const int p = e >> 3, q = e & 7;
       const int yy = ty0 + p / TW, xx = tx0 + p % TW;
       const uint4 v = *reinterpret_cast<const uint4*>(Os + p * OROW + q * 16);
-      if constexpr (PIPE) {
-        // pixels past the image edge: out-of-range offset, the store is dropped (no branch)
-        const uint32_t off = yy < H && xx < W ? (uint32_t)((yy * W + xx) * 128 + q * 16) : OOB;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
-                                               ro, off, 0, 0);
-      } else if (yy < H && xx < W) {
-        *reinterpret_cast<uint4*>(out + (((int64_t)b * H + yy) * W + xx) * 64 + q * 8) = v;
-      }
+      // pixels past the image edge: out-of-range offset, the store is dropped (no branch)
+      const uint32_t off = yy < H && xx < W ? (uint32_t)((yy * W + xx) * 128 + q * 16) : OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                             ro, off, 0, 0);
     }
   };
-  if constexpr (NSET == 2) {
-    for (int t = blockIdx.x; t < ntiles; t += 2 * G) {
-      tile(t, 0, R0);
-      if (t + G < ntiles) tile(t + G, 1, R1);
-    }
-  } else {
-    // three register sets, two LDS buffers: the buffer index alternates at run time
-    int k = 0;
-    for (int t = blockIdx.x; t < ntiles; t += 3 * G, k += 3) {
-      tile(t, k & 1, R0);
-      if (t + G < ntiles) tile(t + G, (k + 1) & 1, R1);
-      if (t + 2 * G < ntiles) tile(t + 2 * G, k & 1, R2);
-    }
+  // three register sets, two LDS buffers: the buffer index alternates at run time
+  int k = 0;
+  for (int t = blockIdx.x; t < ntiles; t += 3 * G, k += 3) {
+    tile(t, k & 1, R0);
+    if (t + G < ntiles) tile(t + G, (k + 1) & 1, R1);
+    if (t + 2 * G < ntiles) tile(t + 2 * G, k & 1, R2);
   }
 }
 
@@ -242,24 +209,11 @@ bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, in
   const int ntiles = B * ty * tx;
   if (ntiles <= 0) return true;
   const int grid = ntiles < grid_cap ? ntiles : grid_cap;
-  static const int variant = [] {
-    // A/B: 1 = the compiler-scheduled K loop, 2 = pipelined K loop without the overlap
-    const char* e = getenv("RAFT_ENC64_V1");
-    return e ? atoi(e) : 0;
-  }();
-  if (f16) {   // fp16 operands (fp16 autocast): the default schedule
-    hipLaunchKernelGGL((conv_enc64_kernel<true, 3, true>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B,
+  if (f16)   // fp16 operands (fp16 autocast)
+    hipLaunchKernelGGL((conv_enc64_kernel<true>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B,
                        H, W, ty, tx);
-    return true;
-  }
-  if (variant == 1)
-    hipLaunchKernelGGL((conv_enc64_kernel<false, 2>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B, H,
-                       W, ty, tx);
-  else if (variant == 2)
-    hipLaunchKernelGGL((conv_enc64_kernel<true, 2>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B, H,
-                       W, ty, tx);
   else
-    hipLaunchKernelGGL((conv_enc64_kernel<true, 3>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B, H,
+    hipLaunchKernelGGL((conv_enc64_kernel<false>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B, H,
                        W, ty, tx);
   return true;
 }

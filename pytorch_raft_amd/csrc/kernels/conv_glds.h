@@ -87,9 +87,9 @@ __global__ __launch_bounds__(NT, (GldsTile<TM, TN, WVM, NS>::OCC)) void conv_fwd
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
     const int qq = q < a.nseg ? q : 0;
-    seg_rs[q] = make_rsrc(a.seg[qq].ptr, a.nullmem ? 0u : (uint32_t)P * a.seg[qq].stride * 2u);
+    seg_rs[q] = make_rsrc(a.seg[qq].ptr, (uint32_t)P * a.seg[qq].stride * 2u);
   }
-  const rsrc_t w_rs = make_rsrc(a.wpk, a.nullmem ? 0u : (uint32_t)a.cout * a.kpad * 2u);
+  const rsrc_t w_rs = make_rsrc(a.wpk, (uint32_t)a.cout * a.kpad * 2u);
   const uint32_t lds0 = raft_lds_addr(smem) + __builtin_amdgcn_readfirstlane(wave * 64 * 16);
 
   auto issue = [&](int t, int buf) {

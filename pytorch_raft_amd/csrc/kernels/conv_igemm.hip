@@ -89,9 +89,9 @@ __global__ __launch_bounds__(NT, (ConvTile<TM, TN, WVM>::OCC)) void conv_fwd_ker
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
     const int qq = q < a.nseg ? q : 0;
-    seg_rs[q] = make_rsrc(a.seg[qq].ptr, a.nullmem ? 0u : (uint32_t)P * a.seg[qq].stride * 2u);
+    seg_rs[q] = make_rsrc(a.seg[qq].ptr, (uint32_t)P * a.seg[qq].stride * 2u);
   }
-  const rsrc_t w_rs = make_rsrc(a.wpk, a.nullmem ? 0u : (uint32_t)a.cout * a.kpad * 2u);
+  const rsrc_t w_rs = make_rsrc(a.wpk, (uint32_t)a.cout * a.kpad * 2u);
 
   auto load = [&](int t, uint4 (&ra)[A_PER], uint4 (&rb)[B_PER]) {
     if constexpr (!SMALLC) {
@@ -598,15 +598,6 @@ int choose_cfg(const ConvFwdArgs& a, int epi, bool smallc, hipStream_t stream) {
 bool launch_conv_fwd(const ConvFwdArgs& a, int epi, int bn, bool smallc, hipStream_t stream) {
   (void)bn;  // tile shape is chosen per geometry (autotuned once, cached)
   const int idx = choose_cfg(a, epi, smallc, stream);
-  static const int nullmem = [] {
-    const char* e = getenv("RAFT_CONV_NULLMEM");  // timing experiments only
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  if (nullmem) {
-    ConvFwdArgs t = a;
-    t.nullmem = 1;
-    return launch_epi_idx(t, epi, idx, smallc, stream);
-  }
   if (launch_epi_idx(a, epi, idx, smallc, stream)) return true;
   // a cached pick is shared by the epilogues of one class (TuneKey.f32out); should it not offer
   // this epilogue, the analytic register-staged choice (every epilogue instantiated) runs instead

@@ -133,73 +133,11 @@ __global__ __launch_bounds__(256) void fh2_fwd_kernel(const uint16_t* __restrict
 }
 
 // dx[b,y,x,c] = [fm > 0] * sum_{ky,kx,o} gout[b,o,y-ky+1,x-kx+1] * W[o][c][ky][kx]
-// thread = (NPIX pixels, 8-channel group); all loads issued up front as in the forward.  Per
-// channel the two output channels form one bf16 pair: s[c] += dot2<F16>((g0, g1), (W0[c], W1[c])),
-// wd: pairs [t][c] from the packing gather.
-template <int NPIX, bool F16>
-__global__ __launch_bounds__(256) void fh2_dgrad_kernel(const float* __restrict__ gout,
-                                                        const uint32_t* __restrict__ wd,
-                                                        const uint16_t* __restrict__ fm, int fs,
-                                                        uint16_t* __restrict__ dx, int ds, int B,
-                                                        int H, int W) {
-  const int g = threadIdx.x & 31;
-  const int64_t hw = (int64_t)H * W, P = (int64_t)B * hw;
-  uint4 wa[9], wb[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    wa[t] = *reinterpret_cast<const uint4*>(wd + t * FH_C + g * 8);
-    wb[t] = *reinterpret_cast<const uint4*>(wd + t * FH_C + g * 8 + 4);
-  }
-  uint32_t gp[NPIX][9];
-  uint4 m[NPIX];
-#pragma unroll
-  for (int k = 0; k < NPIX; ++k) {
-    const int64_t p = ((int64_t)blockIdx.x * NPIX + k) * 8 + (threadIdx.x >> 5);
-    const int64_t pc = min(p, P - 1);
-    const int b = (int)(pc / hw);
-    const int yx = (int)(pc - (int64_t)b * hw);
-    const int y = yx / W, x = yx - y * W;
-    const float* g0 = gout + (int64_t)b * 2 * hw;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int yy = y - t / 3 + 1, xx = x - t % 3 + 1;
-      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
-      const int64_t o = ok ? (int64_t)yy * W + xx : 0;
-      const float d0 = g0[o], d1 = g0[hw + o];
-      gp[k][t] = ok ? pack_bf2<F16>(d0, d1) : 0u;
-    }
-    m[k] = *reinterpret_cast<const uint4*>(fm + pc * fs + g * 8);
-  }
-#pragma unroll
-  for (int k = 0; k < NPIX; ++k) {
-    float s[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] = 0.f;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const uint32_t wv[8] = {wa[t].x, wa[t].y, wa[t].z, wa[t].w, wb[t].x, wb[t].y, wb[t].z, wb[t].w};
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s[i] = dot2<F16>(gp[k][t], wv[i], s[i]);
-    }
-    const uint32_t mw[4] = {m[k].x, m[k].y, m[k].z, m[k].w};
-    uint32_t ov[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool lo = (mw[q] & 0x8000u) == 0 && (mw[q] & 0x7fffu) != 0;
-      const bool hi = (mw[q] & 0x80000000u) == 0 && (mw[q] & 0x7fff0000u) != 0;
-      const uint32_t a = lo ? raft_f2h<F16>(s[2 * q]) : 0u;
-      const uint32_t c = hi ? raft_f2h<F16>(s[2 * q + 1]) : 0u;
-      ov[q] = a | (c << 16);
-    }
-    const int64_t p = ((int64_t)blockIdx.x * NPIX + k) * 8 + (threadIdx.x >> 5);
-    if (p < P) *reinterpret_cast<uint4*>(dx + p * ds + g * 8) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
-  }
-}
-
-// Tiled variant (the launcher's kernel): a workgroup owns a 4 x 16 pixel tile; the tile's 6 x 18
-// halo of the two fp32 output-gradient planes is staged once in LDS as bf16 pairs (the rounding
-// fh2_dgrad_kernel applies), so a tap is one broadcast LDS read instead of two scattered global
-// loads per lane (the 72 gathers per thread made the per-pixel kernel ~4x slower than its bytes).
+// Per channel the two output channels form one 16-bit pair: s[c] += dot2((g0, g1), (W0[c], W1[c])),
+// wd: pairs [t][c] from the packing gather.  A workgroup owns a 4 x 16 pixel tile; the tile's
+// 6 x 18 halo of the two fp32 output-gradient planes is staged once in LDS as 16-bit pairs, so a
+// tap is one broadcast LDS read instead of two scattered global loads per lane (a per-pixel
+// gather version was ~4x slower than its bytes: 72 gathers per thread).
 // thread = 8-channel group (tid & 31) x 8 of the tile's pixels.
 constexpr int DTH = 4, DTW = 16;
 template <bool F16>
@@ -408,27 +346,13 @@ bool launch_fh2_fwd(const uint16_t* in, int cs, const uint32_t* wf, const float*
 bool launch_fh2_dgrad(const float* gout, const uint32_t* wd, const uint16_t* fm, int fs, uint16_t* dx,
                       int ds, int B, int H, int W, int f16, hipStream_t stream) {
   if (fs % 8 != 0 || ds % 8 != 0 || fs < FH_C || ds < FH_C) return false;
-  static const bool v1 = [] {
-    const char* e = getenv("RAFT_FH2_DGRAD_V1");
-    return e && e[0] == '1';
-  }();
-  if (!v1) {
-    const int ty = (H + DTH - 1) / DTH, tx = (W + DTW - 1) / DTW;
-    if (f16)
-      hipLaunchKernelGGL(fh2_dgrad_tile_kernel<true>, dim3((unsigned)(B * ty * tx)), dim3(256), 0, stream,
-                         gout, wd, fm, fs, dx, ds, B, H, W, ty, tx);
-    else
-      hipLaunchKernelGGL(fh2_dgrad_tile_kernel<false>, dim3((unsigned)(B * ty * tx)), dim3(256), 0, stream,
-                         gout, wd, fm, fs, dx, ds, B, H, W, ty, tx);
-    return true;
-  }
-  const int64_t P = (int64_t)B * H * W;
+  const int ty = (H + DTH - 1) / DTH, tx = (W + DTW - 1) / DTW;
   if (f16)
-    hipLaunchKernelGGL((fh2_dgrad_kernel<4, true>), dim3(raft_cdiv(P, 32)), dim3(256), 0, stream, gout, wd,
-                       fm, fs, dx, ds, B, H, W);
+    hipLaunchKernelGGL(fh2_dgrad_tile_kernel<true>, dim3((unsigned)(B * ty * tx)), dim3(256), 0, stream,
+                       gout, wd, fm, fs, dx, ds, B, H, W, ty, tx);
   else
-    hipLaunchKernelGGL((fh2_dgrad_kernel<4, false>), dim3(raft_cdiv(P, 32)), dim3(256), 0, stream, gout, wd,
-                       fm, fs, dx, ds, B, H, W);
+    hipLaunchKernelGGL(fh2_dgrad_tile_kernel<false>, dim3((unsigned)(B * ty * tx)), dim3(256), 0, stream,
+                       gout, wd, fm, fs, dx, ds, B, H, W, ty, tx);
   return true;
 }
 

@@ -189,7 +189,6 @@ struct ConvFwdArgs {
   // instantiations only): cin_pad = 3 x the segments' channel sum (a multiple of 64 each
   // third); K thirds 0 and 2 read the segments' hi halves, third 1 their lo halves (+ stride / 2)
   int spl;
-  int nullmem;  // timing experiments only: operand loads read zeros (descriptor with 0 records)
 };
 
 // tile shape chosen per geometry: autotuned once (outside stream capture) and cached;
