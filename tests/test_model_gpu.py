@@ -51,20 +51,24 @@ def test_hip_training_grads_match_torch(ext_ops):
 
 
 def test_train_step_bf16_runs(ext_ops):
+    """The HIP training step learns: 12 AdamW steps on one batch (`train.py:161-181`, no noise)
+    must lower the sequence loss -- the last three steps' mean clearly below the first three's.
+    The 2,000-step synthetic-flow run against the stock ops is profiles/r6/parity/."""
     from pytorch_raft_amd.engine.trainer import TrainState
     args = argparse.Namespace(small=False, mixed_precision=True, corr_impl='hip', lr=4e-4,
-                              wdecay=1e-4, epsilon=1e-8, num_steps=100, iters=3, gamma=0.8,
-                              clip=1.0, add_noise=True)
+                              wdecay=1e-4, epsilon=1e-8, num_steps=20, iters=3, gamma=0.8,
+                              clip=1.0, add_noise=False)
     torch.manual_seed(0)
     m = RAFT(args).to(DEV).train()
     st = TrainState(m, args, torch.device(DEV))
     i1, i2, flow, valid = make_pair_batch(2, 128, 160, device=DEV)
     losses = []
-    for _ in range(4):
+    for _ in range(12):
         loss, metrics = st.step(i1, i2, flow, valid)
         losses.append(loss.item())
     assert st.check_finite()
-    assert losses[-1] < losses[0] * 1.5
+    first, last = sum(losses[:3]) / 3, sum(losses[-3:]) / 3
+    assert losses[-1] < losses[0] and last < 0.95 * first, losses
 
 
 def test_native_library_loaded(ext_ops):
