@@ -67,6 +67,20 @@ __device__ __forceinline__ int wave_max_i(int v) {
   return v;
 }
 
+// XCD-aware work decode: the dispatcher deals consecutive workgroups round-robin over the 8 XCDs,
+// so workgroup ids are mapped to give each XCD a contiguous range of ceil(n_items / 8) query
+// tiles (the same images and neighbouring tiles, whose fmap2 boxes overlap, meet in one XCD's L2)
+// for every group (pyramid level / backward half), groups in order inside each XCD.  The grid is
+// 8 * ceil(n_items / 8) * n_groups; false for the padding workgroups.
+__device__ __forceinline__ bool xcd_item(int n_items, int n_groups, int& group, int& item) {
+  const int per = (n_items + 7) / 8;
+  const int x = (int)(blockIdx.x & 7), k = (int)(blockIdx.x >> 3);
+  group = k / per;
+  item = x * per + (k - group * per);
+  return group < n_groups && item < n_items;
+}
+inline unsigned xcd_grid(int n_items, int n_groups) { return 8u * (unsigned)((n_items + 7) / 8) * (unsigned)n_groups; }
+
 struct Geo {
   int x0[TP], y0[TP];
   float ax[TP], ay[TP];
@@ -167,13 +181,13 @@ __global__ __launch_bounds__(NT, SPLIT ? 1 : 2) void corr_otf_fwd_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mb = wave & 1, nh = wave >> 1;
-  // one workgroup per (pyramid level, query tile), level-major: the heavy level-0 boxes are
-  // dispatched first and the light coarse levels fill the tail (one launch is ~4.5 rounds of the
-  // chip instead of ~1.1 with a last round 1/8 full); levels write disjoint output channels
-  int t = blockIdx.x;
+  // one workgroup per (pyramid level, query tile), level-major within each XCD's tile range: the
+  // heavy level-0 boxes are dispatched first and the light coarse levels fill the tail (one launch
+  // is ~4.5 rounds of the chip instead of ~1.1 with a last round 1/8 full); levels write disjoint
+  // output channels
   const int ntile = B * tiles_x * tiles_y;
-  const int lev = t / ntile;
-  t -= lev * ntile;
+  int lev, t;
+  if (!xcd_item(ntile, levels, lev, t)) return;
   const int tx = t % tiles_x;
   t /= tiles_x;
   const int ty = t % tiles_y;
@@ -400,17 +414,14 @@ __global__ __launch_bounds__(NT, 1) void corr_otf_bwd_kernel(
   // launcher then adds df1b to df1 (fixed order).  At one workgroup per CU (160 KB LDS) the
   // 2x tiles fill the chip's rounds instead of leaving a 1/4-full last one.
   const int ntile = B * tiles_x * tiles_y;
-  int t = blockIdx.x;
+  int half, t;
+  if (!xcd_item(ntile, df1b != nullptr ? 2 : 1, half, t)) return;   // no barrier before this
   int lbeg = 0, lend = levels;
   bool part = false;
   if (df1b != nullptr) {
-    part = t < ntile;
-    if (part) {
-      lbeg = 1;
-    } else {
-      lend = 1;
-      t -= ntile;
-    }
+    part = half == 0;
+    if (part) lbeg = 1;
+    else lend = 1;
   }
   const int tile = t;
   const int tx = t % tiles_x;
@@ -824,7 +835,7 @@ bool launch_corr_otf_fwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
   const bool split = f1lo != nullptr && f2lo != nullptr;
   const int tx = (W + TPX - 1) / TPX, ty = (H + TPX - 1) / TPX;
   if (levels < 1 || levels > 4) return false;
-  const dim3 grid((unsigned)(B * tx * ty * levels));
+  const dim3 grid(xcd_grid(B * tx * ty, levels));
   const float isc = 1.f / sqrtf((float)C);
 #define FWD(RR, CC, TO, SP)                                                                     \
   hipLaunchKernelGGL((corr_otf_fwd_kernel<RR, CC, TO, SP>), grid, dim3(NT), 0, stream, f1, f1lo, \
@@ -862,7 +873,7 @@ bool launch_corr_otf_bwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
     p.boxes = boxes;
   }
   const int tx = (W + TPX - 1) / TPX, ty = (H + TPX - 1) / TPX;
-  const dim3 grid((unsigned)(B * tx * ty));
+  const dim3 grid(xcd_grid(B * tx * ty, 1));
   const float isc = 1.f / sqrtf((float)C);
   WinList none;
   none.n = 0;
@@ -922,7 +933,7 @@ bool launch_corr_otf_window_bwd(const uint16_t* f1, const uint16_t* const* f2lvl
   }
   const int tx = (W + TPX - 1) / TPX, ty = (H + TPX - 1) / TPX;
   if (levels < 2) df1b = nullptr;
-  const dim3 grid((unsigned)(B * tx * ty * (df1b != nullptr ? 2 : 1)));
+  const dim3 grid(xcd_grid(B * tx * ty, df1b != nullptr ? 2 : 1));
   const float isc = 1.f / sqrtf((float)C);
 #define BWDW(RR, CC)                                                                           \
   hipLaunchKernelGGL((corr_otf_bwd_kernel<RR, CC, float, true>), grid, dim3(NT), 0, stream, f1, \
