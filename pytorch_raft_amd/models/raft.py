@@ -44,6 +44,17 @@ from ..ops import conv_fp32
 _FP32_ENC_MFMA = os.environ.get('RAFT_FP32_ENC_MFMA', '1') != '0'
 # RAFT_FP32_FUSED=0: an fp32 model's update block runs eagerly with per-conv split-bf16 convs
 _FP32_FUSED = os.environ.get('RAFT_FP32_FUSED', '1') != '0'
+# RAFT_ENC_STREAMS=1: the context encoder runs on a side HIP stream concurrently with the feature
+# encoder (forward, and through autograd's per-stream replay of the nodes, backward)
+_ENC_STREAMS = os.environ.get('RAFT_ENC_STREAMS', '0') == '1'
+_SIDE = {}
+
+
+def _enc_side_stream(dev):
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
 
 
 def _get(args, name, default):
@@ -184,21 +195,40 @@ class RAFT(nn.Module):
             if bool(_get(self.args, 'channels_last', False)):
                 image1 = image1.contiguous(memory_format=torch.channels_last)
                 image2 = image2.contiguous(memory_format=torch.channels_last)
+        side = None
+        if (_ENC_STREAMS and pair is not None and dev.type == 'cuda'
+                and not torch.cuda.is_current_stream_capturing()):
+            # the two encoders are independent until the decode: the context encoder on a side
+            # stream fills the feature encoder's kernel tails and small launches
+            main = torch.cuda.current_stream(dev)
+            side = _enc_side_stream(dev)
+            side.wait_stream(main)
+            pair.record_stream(side)
+
+        def context():
+            with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
+                cnet = self.cnet(image1 if pair is None else pair[:image1.shape[0]])
+                # native: both activations in one pass, as the fused block's NHWC operands
+                act = _context_act(cnet, hdim) if native else None
+                if act is not None:
+                    return act
+                net, inp = torch.split(cnet, [hdim, cdim], dim=1)
+                return torch.tanh(net), torch.relu(inp)
+
+        if side is not None:
+            with torch.cuda.stream(side):
+                net, inp = context()
         with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
             if pair is None:
                 fmap1, fmap2 = self.fnet([image1, image2])
             else:
                 fmap1, fmap2 = torch.split(self.fnet(pair), [image1.shape[0]] * 2, dim=0)
-        with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
-            cnet = self.cnet(image1 if pair is None else pair[:image1.shape[0]])
-            # native: both activations in one pass, as the fused block's NHWC operands
-            act = _context_act(cnet, hdim) if native else None
-            if act is not None:
-                net, inp = act
-            else:
-                net, inp = torch.split(cnet, [hdim, cdim], dim=1)
-                net = torch.tanh(net)
-                inp = torch.relu(inp)
+        if side is None:
+            net, inp = context()
+        else:
+            main.wait_stream(side)
+            net.record_stream(main)
+            inp.record_stream(main)
         return fmap1, fmap2, net, inp
 
     def decode(self, fmap1, fmap2, net, inp, iters=12, flow_init=None, test_mode=False):
