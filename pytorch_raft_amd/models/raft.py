@@ -44,14 +44,18 @@ from ..ops import conv_fp32
 _FP32_ENC_MFMA = os.environ.get('RAFT_FP32_ENC_MFMA', '1') != '0'
 # RAFT_FP32_FUSED=0: an fp32 model's update block runs eagerly with per-conv split-bf16 convs
 _FP32_FUSED = os.environ.get('RAFT_FP32_FUSED', '1') != '0'
-# RAFT_ENC_STREAMS=1: the context encoder runs on a side HIP stream concurrently with the feature
-# encoder (forward, and through autograd's per-stream replay of the nodes, backward)
-_ENC_STREAMS = os.environ.get('RAFT_ENC_STREAMS', '0') == '1'
+# Encoder streams (native path): 1 = one stream; 2 (default) = the context encoder on a side HIP
+# stream beside the feature encoder; 3 = also the feature encoder's two frames on two streams (its
+# instance norms are per image, so the halves are exact).  Autograd replays every node's backward
+# on its forward's stream, so the backwards overlap the same way.  The encoders are independent
+# until the decode; co-running fills each other's kernel tails and small launches (round 6 A/B:
+# 484.3 / 488.3 vs 466.1 / 466.8 pairs/s on one box, profiles/r6/enc_streams/).
+_ENC_STREAMS = int(os.environ.get('RAFT_ENC_STREAMS', '2'))
 _SIDE = {}
 
 
-def _enc_side_stream(dev):
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
+def _enc_side_stream(dev, k=0):
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), k)
     if key not in _SIDE:
         _SIDE[key] = torch.cuda.Stream(device=dev)
     return _SIDE[key]
@@ -195,15 +199,17 @@ class RAFT(nn.Module):
             if bool(_get(self.args, 'channels_last', False)):
                 image1 = image1.contiguous(memory_format=torch.channels_last)
                 image2 = image2.contiguous(memory_format=torch.channels_last)
-        side = None
-        if (_ENC_STREAMS and pair is not None and dev.type == 'cuda'
+        side = side2 = None
+        if (_ENC_STREAMS >= 2 and pair is not None and dev.type == 'cuda'
                 and not torch.cuda.is_current_stream_capturing()):
-            # the two encoders are independent until the decode: the context encoder on a side
-            # stream fills the feature encoder's kernel tails and small launches
             main = torch.cuda.current_stream(dev)
-            side = _enc_side_stream(dev)
+            side = _enc_side_stream(dev, 0)
             side.wait_stream(main)
             pair.record_stream(side)
+            if _ENC_STREAMS >= 3:
+                side2 = _enc_side_stream(dev, 1)
+                side2.wait_stream(main)
+                pair.record_stream(side2)
 
         def context():
             with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
@@ -218,17 +224,26 @@ class RAFT(nn.Module):
         if side is not None:
             with torch.cuda.stream(side):
                 net, inp = context()
+        n1 = image1.shape[0]
+        if side2 is not None:
+            with torch.cuda.stream(side2), self._autocast(dev), conv_fp32.enabled(fp32_mfma):
+                fmap2 = self.fnet(pair[n1:])
         with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
             if pair is None:
                 fmap1, fmap2 = self.fnet([image1, image2])
+            elif side2 is not None:
+                fmap1 = self.fnet(pair[:n1])
             else:
-                fmap1, fmap2 = torch.split(self.fnet(pair), [image1.shape[0]] * 2, dim=0)
+                fmap1, fmap2 = torch.split(self.fnet(pair), [n1] * 2, dim=0)
         if side is None:
             net, inp = context()
         else:
             main.wait_stream(side)
             net.record_stream(main)
             inp.record_stream(main)
+        if side2 is not None:
+            main.wait_stream(side2)
+            fmap2.record_stream(main)
         return fmap1, fmap2, net, inp
 
     def decode(self, fmap1, fmap2, net, inp, iters=12, flow_init=None, test_mode=False):

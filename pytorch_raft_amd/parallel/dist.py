@@ -166,7 +166,7 @@ def all_reduce_mean(t):
 
 
 class _Bucket:
-    __slots__ = ('params', 'numel', 'pending', 'flat', 'work', 'event', 'launched')
+    __slots__ = ('params', 'numel', 'pending', 'flat', 'work', 'event', 'launched', 'streams')
 
     def __init__(self, params):
         self.params = params
@@ -176,6 +176,7 @@ class _Bucket:
         self.work = None
         self.event = None
         self.launched = False
+        self.streams = set()   # streams the bucket's gradients were accumulated on (this step)
 
 
 class GradSync:
@@ -241,6 +242,7 @@ class GradSync:
             b.pending = len(b.params)
             b.work = None
             b.launched = False
+            b.streams = set()
 
     @torch.no_grad()
     def _launch(self, b):
@@ -250,7 +252,11 @@ class GradSync:
         dtype = self.comm_dtype or ref.dtype
         s = self._comm_stream(dev)
         if s is not None:
+            # every stream a gradient of the bucket was accumulated on (the encoders run on
+            # several streams, and autograd replays each backward node on its forward's stream)
             s.wait_stream(torch.cuda.current_stream(dev))
+            for st in b.streams:
+                s.wait_stream(st)
             ctx = torch.cuda.stream(s)
         else:
             ctx = _nullctx()
@@ -276,6 +282,8 @@ class GradSync:
             return
         self.hooks_fired += 1
         b = self.bucket_of[p]
+        if p.is_cuda:
+            b.streams.add(torch.cuda.current_stream(p.device))
         b.pending -= 1
         if b.pending == 0 and not b.launched:
             self.launch_log.append((self.buckets.index(b), self.hooks_fired))
