@@ -37,9 +37,6 @@ from .optim import fetch_optimizer, clip_grad_norm_, clip_and_step, FusedAdamW
 # trace splits into encoder forward / decode (update block, correlation, loss) / encoder backward +
 # update (scripts/prof_diff.py --phases, scripts/categorize.py)
 _PHASE_MARKS = os.environ.get('RAFT_PHASE_MARKS', '0') == '1'
-# RAFT_WGRAD_DEFER=0: the update block's batched weight gradients stay inside the decode graph
-# instead of a second graph replayed on a side stream beside the encoder backward
-_WGRAD_DEFER = os.environ.get('RAFT_WGRAD_DEFER', '1') != '0'
 
 
 def _phase_mark():
@@ -206,31 +203,13 @@ class GraphedTrainStep:
         torch.cuda.current_stream(st.device).wait_stream(stream)
         torch.cuda.synchronize(st.device)
 
-        from ..ops import update_hip
         self.g_dec = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_dec, stream=stream):
-            if _WGRAD_DEFER:
-                with update_hip.defer_wgrad():
-                    self.loss, self.metrics = self._decode()
-            else:
-                self.loss, self.metrics = self._decode()
+            self.loss, self.metrics = self._decode()
         for p in self.dec_params:
-            if p.grad is None:  # no gradient this step / deferred (fixed tensors for the replays)
+            if p.grad is None:  # no gradient this step (fixed tensors for the replays)
                 p.grad = torch.zeros_like(p)
         self.dec_grads = [p.grad for p in self.dec_params]
-        # the update block's batched weight gradients (~3 ms at chairs, MFMA-bound): a second
-        # graph over the decode graph's pool, replayed on a side stream beside the eager encoder
-        # backward (which needs nothing from them); the packed state they read stays referenced
-        self.g_wg = None
-        self.wg_stream = None
-        jobs = update_hip.pending_wgrad()
-        update_hip._DEFER['jobs'] = []
-        if jobs:
-            self.g_wg = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g_wg, stream=stream, pool=self.g_dec.pool()):
-                update_hip.run_deferred_wgrad(jobs)
-            self._wg_jobs = jobs
-            self.wg_stream = torch.cuda.Stream(device=st.device)
         self.warmup_steps = warmup
         self._restore(snap)
 
@@ -318,7 +297,6 @@ class GraphedTrainStep:
         if st.has_buffers and self.world > 1:
             pdist.broadcast_buffers(st.model)  # DataParallel semantics: replica 0's BN stats
         feats = self._encode_and_stage(image1, image2, flow, valid)
-        side = None
         if graphs:
             if _PHASE_MARKS:
                 _phase_mark()
@@ -326,22 +304,12 @@ class GraphedTrainStep:
             if _PHASE_MARKS:
                 _phase_mark()
             loss = self.loss
-            if self.g_wg is not None:
-                # the update-block weight gradients on the side stream, beside the encoder
-                # backward; ranks > 1 start their all-reduce from there once they are final
-                side = self.wg_stream
-                side.wait_stream(torch.cuda.current_stream(st.device))
-                with torch.cuda.stream(side):
-                    self.g_wg.replay()
-                    work = self._allreduce_dec()
-            else:
-                work = self._allreduce_dec()         # overlaps the encoder backward
         else:
             loss, _ = self._decode()
             for p in self.dec_params:
                 if p.grad is None:
                     p.grad = torch.zeros_like(p)
-            work = self._allreduce_dec()             # overlaps the encoder backward
+        work = self._allreduce_dec()                 # overlaps the encoder backward
         if self.enc_sync is not None:
             self.enc_sync.prepare()
         self._encoder_backward(feats)
@@ -351,8 +319,6 @@ class GraphedTrainStep:
         for p in self.enc_params:
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-        if side is not None:
-            torch.cuda.current_stream(st.device).wait_stream(side)
         if work is not None:
             work.wait()
             self._unpack()

@@ -479,11 +479,6 @@ class _UpdateWeights(torch.autograd.Function):
                                'iterations is not supported; use update_impl="torch")')
         pk = st.packed
         st.packed = None
-        if _DEFER['on']:
-            # deferred (graphed training step): the weight gradients are computed later by
-            # run_deferred_wgrad(), into the parameters' existing .grad tensors
-            _DEFER['jobs'].append((pk, list(st.params)))
-            return (None,) * (1 + ctx.n)
         if st.overlap and pk.device.type == 'cuda':
             return _backward_overlapped(st, pk, ctx.n)
         _flush_wgrad(pk)
@@ -504,51 +499,6 @@ def _unpack_grads(pk):
         grads.append(g[off:off + n].view(shape))
         off += n
     return grads
-
-
-# ---------------------------------------------------------------- deferred weight gradients
-# The graphed training step (engine/trainer.py) captures the decode with the update block's
-# batched weight gradients DEFERRED: the backward returns no gradient for the update-block
-# parameters and queues its packed state; a second graph, captured right after the decode's,
-# runs run_deferred_wgrad() -- the batched wgrad launches + the unpack, written into the
-# parameters' persistent .grad tensors -- and is replayed on a side stream concurrently with the
-# eager encoder backward, which needs nothing from it.
-_DEFER = {'on': False, 'jobs': []}
-
-
-class defer_wgrad:
-    """Context manager: update-block backwards inside it queue their weight gradients."""
-
-    def __enter__(self):
-        _DEFER['on'] = True
-        return self
-
-    def __exit__(self, *exc):
-        _DEFER['on'] = False
-        return False
-
-
-def pending_wgrad():
-    return list(_DEFER['jobs'])
-
-
-@torch.no_grad()
-def run_deferred_wgrad(jobs=None):
-    """Every queued update-block weight gradient -> .grad (copied into an existing .grad of the
-    parameter's layout, else assigned).  Returns the jobs run (their packed buffers must stay
-    referenced while a graph that captured this call can replay)."""
-    if jobs is None:
-        jobs, _DEFER['jobs'] = _DEFER['jobs'], []
-    for pk, params in jobs:
-        _flush_wgrad(pk)
-        for prm, g in zip(params, _unpack_grads(pk)):
-            if not prm.requires_grad:
-                continue
-            if prm.grad is None:
-                prm.grad = g if g.stride() == prm.stride() else torch.empty_like(prm).copy_(g)
-            else:
-                prm.grad.copy_(g)
-    return jobs
 
 
 # ---------------------------------------------------------------- wgrad / encoder-backward overlap
