@@ -45,17 +45,17 @@ _FP32_ENC_MFMA = os.environ.get('RAFT_FP32_ENC_MFMA', '1') != '0'
 # RAFT_FP32_FUSED=0: an fp32 model's update block runs eagerly with per-conv split-bf16 convs
 _FP32_FUSED = os.environ.get('RAFT_FP32_FUSED', '1') != '0'
 # Encoder streams (native path): 1 = one stream; 2 (default) = the context encoder on a side HIP
-# stream beside the feature encoder; 3 = also the feature encoder's two frames on two streams (its
-# instance norms are per image, so the halves are exact).  Autograd replays every node's backward
-# on its forward's stream, so the backwards overlap the same way.  The encoders are independent
-# until the decode; co-running fills each other's kernel tails and small launches (round 6 A/B:
-# 484.3 / 488.3 vs 466.1 / 466.8 pairs/s on one box, profiles/r6/enc_streams/).
+# stream beside the feature encoder.  Autograd replays every node's backward on its forward's
+# stream, so the backwards overlap the same way.  The encoders are independent until the decode;
+# co-running fills each other's kernel tails and small launches (round 6 A/B: 484.3 / 488.3 vs
+# 466.1 / 466.8 pairs/s on one box; the feature encoder's two frames on a third stream as well:
+# 468.6 / 468.0 vs 476.6 / 480.3 -- profiles/r6/enc_streams/).
 _ENC_STREAMS = int(os.environ.get('RAFT_ENC_STREAMS', '2'))
 _SIDE = {}
 
 
-def _enc_side_stream(dev, k=0):
-    key = (dev.index if dev.index is not None else torch.cuda.current_device(), k)
+def _enc_side_stream(dev):
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
     if key not in _SIDE:
         _SIDE[key] = torch.cuda.Stream(device=dev)
     return _SIDE[key]
@@ -199,17 +199,13 @@ class RAFT(nn.Module):
             if bool(_get(self.args, 'channels_last', False)):
                 image1 = image1.contiguous(memory_format=torch.channels_last)
                 image2 = image2.contiguous(memory_format=torch.channels_last)
-        side = side2 = None
+        side = None
         if (_ENC_STREAMS >= 2 and pair is not None and dev.type == 'cuda'
                 and not torch.cuda.is_current_stream_capturing()):
             main = torch.cuda.current_stream(dev)
-            side = _enc_side_stream(dev, 0)
+            side = _enc_side_stream(dev)
             side.wait_stream(main)
             pair.record_stream(side)
-            if _ENC_STREAMS >= 3:
-                side2 = _enc_side_stream(dev, 1)
-                side2.wait_stream(main)
-                pair.record_stream(side2)
 
         def context():
             with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
@@ -224,26 +220,17 @@ class RAFT(nn.Module):
         if side is not None:
             with torch.cuda.stream(side):
                 net, inp = context()
-        n1 = image1.shape[0]
-        if side2 is not None:
-            with torch.cuda.stream(side2), self._autocast(dev), conv_fp32.enabled(fp32_mfma):
-                fmap2 = self.fnet(pair[n1:])
         with self._autocast(dev), conv_fp32.enabled(fp32_mfma):
             if pair is None:
                 fmap1, fmap2 = self.fnet([image1, image2])
-            elif side2 is not None:
-                fmap1 = self.fnet(pair[:n1])
             else:
-                fmap1, fmap2 = torch.split(self.fnet(pair), [n1] * 2, dim=0)
+                fmap1, fmap2 = torch.split(self.fnet(pair), [image1.shape[0]] * 2, dim=0)
         if side is None:
             net, inp = context()
         else:
             main.wait_stream(side)
             net.record_stream(main)
             inp.record_stream(main)
-        if side2 is not None:
-            main.wait_stream(side2)
-            fmap2.record_stream(main)
         return fmap1, fmap2, net, inp
 
     def decode(self, fmap1, fmap2, net, inp, iters=12, flow_init=None, test_mode=False):
