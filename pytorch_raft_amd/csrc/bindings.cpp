@@ -1540,60 +1540,71 @@ void split_hilo_(const Tensor& x, const Tensor& out) {
 }
 
 void relu_bwd_(const Tensor& g, int64_t g_off, const c10::optional<Tensor>& y, int64_t y_off,
-               const Tensor& out, int64_t o_off, int64_t C, double scale) {
+               const Tensor& out, int64_t o_off, int64_t C, double scale, bool split) {
   TORCH_CHECK(g.is_cuda() && g.is_contiguous() && g.scalar_type() == at::kFloat && g.dim() == 4, "g: fp32 NHWC");
   const int64_t B = g.size(0), H = g.size(1), W = g.size(2), P = B * H * W;
   TORCH_CHECK(g_off + C <= g.size(3), "g slice");
   const at::ScalarType st = op16(out);   // bf16, or fp16 under fp16 autocast
+  TORCH_CHECK(!split || st == at::kBFloat16, "split fp32: bf16 [hi | lo] pairs");
   check_nhwc(out, B, H, W, "relu_bwd out", st);
-  TORCH_CHECK(o_off + C <= out.size(3), "out slice");
+  // split fp32: offsets / C index the hi half, the lo half is the row's second half
+  const int64_t ow = split ? out.size(3) / 2 : out.size(3);
+  TORCH_CHECK(!split || out.size(3) % 2 == 0, "split out: two halves");
+  TORCH_CHECK(o_off + C <= ow, "out slice");
   const uint16_t* yp = nullptr;
   int ys = 0;
   if (y.has_value() && y->defined()) {
     check_nhwc(*y, B, H, W, "relu_bwd y", st);
-    TORCH_CHECK(y_off + C <= y->size(3), "y slice");
+    TORCH_CHECK(!split || y->size(3) % 2 == 0, "split y: two halves");
+    TORCH_CHECK(y_off + C <= (split ? y->size(3) / 2 : y->size(3)), "y slice");
     yp = u16(*y) + y_off;
     ys = (int)y->size(3);
   }
   c10::DeviceGuard gd(g.device());
   launch_relu_bwd(g.data_ptr<float>() + g_off, (int)g.size(3), yp, ys, u16m(out) + o_off,
-                  (int)out.size(3), (int)P, (int)C, (float)scale, cur_stream(), st == at::kHalf);
+                  (int)out.size(3), (int)P, (int)C, (float)scale, cur_stream(),
+                  split ? 2 : (st == at::kHalf ? 1 : 0));
 }
 
+// split fp32 (bf16 [hi | lo] rows of twice the width) is recognised by the 16-bit tensors' width
 void gru_q_bwd_(const Tensor& dh, const Tensor& z, const Tensor& q, const Tensor& hprev,
                 const Tensor& dpre_q, const Tensor& dz, const Tensor& dhprev) {
-  TORCH_CHECK(dh.dim() == 4, "dh must be (B,H,W,hd)");
+  TORCH_CHECK(dh.dim() == 4 && z.dim() == 4, "dh, z must be (B,H,W,hd)");
   const int64_t P = dh.size(0) * dh.size(1) * dh.size(2), hd = dh.size(3);
   const at::ScalarType st = op16(z);   // bf16, or fp16 under fp16 autocast
+  const bool split = st == at::kBFloat16 && z.size(3) == 2 * hd;
+  const int64_t w = split ? 2 * hd : hd;
   check_pc(dh, P, hd, at::kFloat, "dh");
-  check_pc(z, P, hd, st, "z");
-  check_pc(q, P, hd, st, "q");
-  check_pc(hprev, P, hd, st, "hprev");
-  check_pc(dpre_q, P, hd, st, "dpre_q");
+  check_pc(z, P, w, st, "z");
+  check_pc(q, P, w, st, "q");
+  check_pc(hprev, P, w, st, "hprev");
+  check_pc(dpre_q, P, w, st, "dpre_q");
   check_pc(dz, P, hd, at::kFloat, "dz");
   check_pc(dhprev, P, hd, at::kFloat, "dhprev");
   c10::DeviceGuard gd(dh.device());
   launch_gru_q_bwd(dh.data_ptr<float>(), u16(z), u16(q), u16(hprev), u16m(dpre_q),
                    dz.data_ptr<float>(), dhprev.data_ptr<float>(), (int)P, (int)hd, cur_stream(),
-                   st == at::kHalf);
+                   split ? 2 : (st == at::kHalf ? 1 : 0));
 }
 
 void gru_zr_bwd_(const Tensor& drh, const Tensor& dz, const Tensor& z, const Tensor& r,
                  const Tensor& hprev, const Tensor& dpre_zr, const Tensor& dhprev) {
-  TORCH_CHECK(drh.dim() == 4, "drh must be (B,H,W,hd)");
+  TORCH_CHECK(drh.dim() == 4 && z.dim() == 4, "drh, z must be (B,H,W,hd)");
   const int64_t P = drh.size(0) * drh.size(1) * drh.size(2), hd = drh.size(3);
   const at::ScalarType st = op16(z);
+  const bool split = st == at::kBFloat16 && z.size(3) == 2 * hd;
+  const int64_t w = split ? 2 * hd : hd;
   check_pc(drh, P, hd, at::kFloat, "drh");
   check_pc(dz, P, hd, at::kFloat, "dz");
-  check_pc(z, P, hd, st, "z");
-  check_pc(r, P, hd, st, "r");
-  check_pc(hprev, P, hd, st, "hprev");
-  check_pc(dpre_zr, P, 2 * hd, st, "dpre_zr");
+  check_pc(z, P, w, st, "z");
+  check_pc(r, P, w, st, "r");
+  check_pc(hprev, P, w, st, "hprev");
+  check_pc(dpre_zr, P, 2 * w, st, "dpre_zr");
   check_pc(dhprev, P, hd, at::kFloat, "dhprev");
   c10::DeviceGuard gd(drh.device());
   launch_gru_zr_bwd(drh.data_ptr<float>(), dz.data_ptr<float>(), u16(z), u16(r), u16(hprev),
                     u16m(dpre_zr), dhprev.data_ptr<float>(), (int)P, (int)hd, cur_stream(),
-                    st == at::kHalf);
+                    split ? 2 : (st == at::kHalf ? 1 : 0));
 }
 
 // out = sum(ins) (+ carry): n <= RAFT_SUM_MAX same-shape contiguous bf16 tensors, fp32 accumulation,
@@ -2011,7 +2022,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off, int[] gate_mode, Tensor[] gate_t, int[] out_kcin=[], bool split=False) -> ()");
   m.def("split_hilo_(Tensor x, Tensor(a!) out) -> ()");
   m.def("conv_enc64_(Tensor x, Tensor wpk, Tensor(a!) out) -> ()");
-  m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale) -> ()");
+  m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale, bool split=False) -> ()");
   m.def("gru_q_bwd_(Tensor dh, Tensor z, Tensor q, Tensor hprev, Tensor(a!) dpre_q, Tensor(b!) dz, Tensor(c!) dhprev) -> ()");
   m.def("gru_zr_bwd_(Tensor drh, Tensor dz, Tensor z, Tensor r, Tensor hprev, Tensor(a!) dpre_zr, Tensor(b!) dhprev) -> ()");
   m.def("sum_bf16_(Tensor[] ins, Tensor? carry, Tensor(a!) out) -> ()");

@@ -268,12 +268,13 @@ bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, in
 void launch_split_hilo(const float* x, int64_t sb, int64_t sc, int64_t sh, int64_t sw, int B, int C,
                        int H, int W, int cp, uint16_t* out, hipStream_t stream);
 void launch_relu_bwd(const float* g, int gs, const uint16_t* y, int ys, uint16_t* out, int os, int P,
-                     int C, float scale, hipStream_t stream, bool f16 = false);
+                     int C, float scale, hipStream_t stream, int ot = 0);
+// ot: 0 bf16, 1 fp16, 2 split fp32 (bf16 [hi | lo] row halves)
 void launch_gru_q_bwd(const float* dh, const uint16_t* z, const uint16_t* q, const uint16_t* hprev,
-                      uint16_t* dpre_q, float* dz, float* dhprev, int P, int hd, hipStream_t stream, bool f16 = false);
+                      uint16_t* dpre_q, float* dz, float* dhprev, int P, int hd, hipStream_t stream, int ot = 0);
 void launch_gru_zr_bwd(const float* drh, const float* dz, const uint16_t* z, const uint16_t* r,
                        const uint16_t* hprev, uint16_t* dpre_zr, float* dhprev, int P, int hd,
-                       hipStream_t stream, bool f16 = false);
+                       hipStream_t stream, int ot = 0);
 void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int slot_stride, int B,
                       int HW, hipStream_t stream);
 // out (bf16 or fp32) = sum of n <= RAFT_SUM_MAX bf16 tensors (+ fp32 carry); numel % 8 == 0

@@ -18,8 +18,27 @@
 
 namespace {
 
-// F16: the 16-bit buffers are fp16 (fp16 autocast), else bf16
-template <bool F16>
+// OT: the 16-bit buffers are 0 bf16, 1 fp16 (fp16 autocast), 2 split fp32 (bf16 [hi | lo]
+// halves of a row: the value is hi + lo, lo `lo` elements after hi)
+template <int OT>
+__device__ __forceinline__ float ew_ld(const uint16_t* p, int64_t i, int lo) {
+  if constexpr (OT == 2) return raft_bf16_to_f32(p[i]) + raft_bf16_to_f32(p[i + lo]);
+  else return raft_h2f<OT == 1>(p[i]);
+}
+
+template <int OT>
+__device__ __forceinline__ void ew_st(uint16_t* p, int64_t i, int lo, float v) {
+  if constexpr (OT == 2) {
+    const uint16_t h = raft_f32_to_bf16(v);
+    p[i] = h;
+    p[i + lo] = raft_f32_to_bf16(v - raft_bf16_to_f32(h));
+  } else {
+    p[i] = raft_f2h<OT == 1>(v);
+  }
+}
+
+// ys / os: row widths of y / out (split: both halves, the lo half at + width / 2)
+template <int OT>
 __global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__ g, int gs,
                                                        const uint16_t* __restrict__ y, int ys,
                                                        uint16_t* __restrict__ out, int os, int P,
@@ -30,47 +49,53 @@ __global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__
     const int64_t p = t / C;
     const int c = (int)(t - p * C);
     float v = g[p * gs + c] * scale;
-    if (y != nullptr && !(raft_h2f<F16>(y[p * ys + c]) > 0.f)) v = 0.f;
-    out[p * os + c] = raft_f2h<F16>(v);
+    if (y != nullptr && !(ew_ld<OT>(y, p * ys + c, ys >> 1) > 0.f)) v = 0.f;
+    ew_st<OT>(out, p * os + c, os >> 1, v);
   }
 }
 
-// hd = hidden width (128 / 96).  dpre_q (bf16, stride dq_s), dz (f32 P x hd), dh_prev (f32 P x hd)
-template <bool F16>
+// hd = hidden width (128 / 96).  z, q, hprev, dpre_q: rows of hd (split: 2 hd), dz / dh_prev
+// fp32 P x hd
+template <int OT>
 __global__ __launch_bounds__(256) void gru_q_bwd_kernel(const float* __restrict__ dh, const uint16_t* __restrict__ z,
                                                         const uint16_t* __restrict__ q, const uint16_t* __restrict__ hprev,
                                                         uint16_t* __restrict__ dpre_q, float* __restrict__ dz,
                                                         float* __restrict__ dhprev, int P, int hd) {
   const int64_t total = (int64_t)P * hd;
+  const int rw = OT == 2 ? 2 * hd : hd;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = t / hd;
+    const int64_t i = p * rw + (t - p * hd);
     const float g = dh[t];
-    const float zz = raft_h2f<F16>(z[t]);
-    const float qq = raft_h2f<F16>(q[t]);
-    const float hh = raft_h2f<F16>(hprev[t]);
-    dpre_q[t] = raft_f2h<F16>(g * zz * (1.f - qq * qq));
+    const float zz = ew_ld<OT>(z, i, hd);
+    const float qq = ew_ld<OT>(q, i, hd);
+    const float hh = ew_ld<OT>(hprev, i, hd);
+    ew_st<OT>(dpre_q, i, hd, g * zz * (1.f - qq * qq));
     dz[t] = g * (qq - hh);
     dhprev[t] = g * (1.f - zz);
   }
 }
 
-// dpre_zr (bf16 P x 2hd: [z | r]), dhprev += drh * r
-template <bool F16>
+// dpre_zr (P x 2hd: [z | r]; split: [z | r] hi then lo), dhprev += drh * r
+template <int OT>
 __global__ __launch_bounds__(256) void gru_zr_bwd_kernel(const float* __restrict__ drh, const float* __restrict__ dz,
                                                          const uint16_t* __restrict__ z, const uint16_t* __restrict__ r,
                                                          const uint16_t* __restrict__ hprev, uint16_t* __restrict__ dpre_zr,
                                                          float* __restrict__ dhprev, int P, int hd) {
   const int64_t total = (int64_t)P * hd;
+  const int rw = OT == 2 ? 2 * hd : hd;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = t / hd;
     const int c = (int)(t - p * hd);
-    const float zz = raft_h2f<F16>(z[t]);
-    const float rr = raft_h2f<F16>(r[t]);
-    const float hh = raft_h2f<F16>(hprev[t]);
+    const int64_t i = p * rw + c;
+    const float zz = ew_ld<OT>(z, i, hd);
+    const float rr = ew_ld<OT>(r, i, hd);
+    const float hh = ew_ld<OT>(hprev, i, hd);
     const float g = drh[t];
-    dpre_zr[p * 2 * hd + c] = raft_f2h<F16>(dz[t] * zz * (1.f - zz));
-    dpre_zr[p * 2 * hd + hd + c] = raft_f2h<F16>(g * hh * rr * (1.f - rr));
+    ew_st<OT>(dpre_zr, p * 2 * rw + c, 2 * hd, dz[t] * zz * (1.f - zz));
+    ew_st<OT>(dpre_zr, p * 2 * rw + hd + c, 2 * hd, g * hh * rr * (1.f - rr));
     dhprev[t] += g * rr;
   }
 }
@@ -266,35 +291,38 @@ void launch_sum_bf16(const BfPtrs& ins, int n, const float* carry, void* out, bo
 }
 
 void launch_relu_bwd(const float* g, int gs, const uint16_t* y, int ys, uint16_t* out, int os, int P,
-                     int C, float scale, hipStream_t stream, bool f16) {
-  if (f16)
-    hipLaunchKernelGGL(relu_bwd_kernel<true>, dim3(ew_blocks((int64_t)P * C)), dim3(256), 0, stream, g, gs,
-                       y, ys, out, os, P, C, scale);
+                     int C, float scale, hipStream_t stream, int ot) {
+  const dim3 grid(ew_blocks((int64_t)P * C));
+  if (ot == 2)
+    hipLaunchKernelGGL(relu_bwd_kernel<2>, grid, dim3(256), 0, stream, g, gs, y, ys, out, os, P, C, scale);
+  else if (ot == 1)
+    hipLaunchKernelGGL(relu_bwd_kernel<1>, grid, dim3(256), 0, stream, g, gs, y, ys, out, os, P, C, scale);
   else
-    hipLaunchKernelGGL(relu_bwd_kernel<false>, dim3(ew_blocks((int64_t)P * C)), dim3(256), 0, stream, g, gs,
-                       y, ys, out, os, P, C, scale);
+    hipLaunchKernelGGL(relu_bwd_kernel<0>, grid, dim3(256), 0, stream, g, gs, y, ys, out, os, P, C, scale);
 }
 
 void launch_gru_q_bwd(const float* dh, const uint16_t* z, const uint16_t* q, const uint16_t* hprev,
                       uint16_t* dpre_q, float* dz, float* dhprev, int P, int hd, hipStream_t stream,
-                      bool f16) {
-  if (f16)
-    hipLaunchKernelGGL(gru_q_bwd_kernel<true>, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream, dh,
-                       z, q, hprev, dpre_q, dz, dhprev, P, hd);
+                      int ot) {
+  const dim3 grid(ew_blocks((int64_t)P * hd));
+  if (ot == 2)
+    hipLaunchKernelGGL(gru_q_bwd_kernel<2>, grid, dim3(256), 0, stream, dh, z, q, hprev, dpre_q, dz, dhprev, P, hd);
+  else if (ot == 1)
+    hipLaunchKernelGGL(gru_q_bwd_kernel<1>, grid, dim3(256), 0, stream, dh, z, q, hprev, dpre_q, dz, dhprev, P, hd);
   else
-    hipLaunchKernelGGL(gru_q_bwd_kernel<false>, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream, dh,
-                       z, q, hprev, dpre_q, dz, dhprev, P, hd);
+    hipLaunchKernelGGL(gru_q_bwd_kernel<0>, grid, dim3(256), 0, stream, dh, z, q, hprev, dpre_q, dz, dhprev, P, hd);
 }
 
 void launch_gru_zr_bwd(const float* drh, const float* dz, const uint16_t* z, const uint16_t* r,
                        const uint16_t* hprev, uint16_t* dpre_zr, float* dhprev, int P, int hd,
-                       hipStream_t stream, bool f16) {
-  if (f16)
-    hipLaunchKernelGGL(gru_zr_bwd_kernel<true>, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream,
-                       drh, dz, z, r, hprev, dpre_zr, dhprev, P, hd);
+                       hipStream_t stream, int ot) {
+  const dim3 grid(ew_blocks((int64_t)P * hd));
+  if (ot == 2)
+    hipLaunchKernelGGL(gru_zr_bwd_kernel<2>, grid, dim3(256), 0, stream, drh, dz, z, r, hprev, dpre_zr, dhprev, P, hd);
+  else if (ot == 1)
+    hipLaunchKernelGGL(gru_zr_bwd_kernel<1>, grid, dim3(256), 0, stream, drh, dz, z, r, hprev, dpre_zr, dhprev, P, hd);
   else
-    hipLaunchKernelGGL(gru_zr_bwd_kernel<false>, dim3(ew_blocks((int64_t)P * hd)), dim3(256), 0, stream,
-                       drh, dz, z, r, hprev, dpre_zr, dhprev, P, hd);
+    hipLaunchKernelGGL(gru_zr_bwd_kernel<0>, grid, dim3(256), 0, stream, drh, dz, z, r, hprev, dpre_zr, dhprev, P, hd);
 }
 
 void launch_flow_prep(const float* flow, uint16_t* flowb, uint16_t* slot, int slot_stride, int B,

@@ -44,13 +44,16 @@ from ..ops import conv_fp32
 _FP32_ENC_MFMA = os.environ.get('RAFT_FP32_ENC_MFMA', '1') != '0'
 # RAFT_FP32_FUSED=0: an fp32 model's update block runs eagerly with per-conv split-bf16 convs
 _FP32_FUSED = os.environ.get('RAFT_FP32_FUSED', '1') != '0'
-# Encoder streams (native path): 1 = one stream; 2 (default) = the context encoder on a side HIP
-# stream beside the feature encoder.  Autograd replays every node's backward on its forward's
-# stream, so the backwards overlap the same way.  The encoders are independent until the decode;
-# co-running fills each other's kernel tails and small launches (round 6 A/B: 484.3 / 488.3 vs
-# 466.1 / 466.8 pairs/s on one box; the feature encoder's two frames on a third stream as well:
-# 468.6 / 468.0 vs 476.6 / 480.3 -- profiles/r6/enc_streams/).
-_ENC_STREAMS = int(os.environ.get('RAFT_ENC_STREAMS', '2'))
+# Encoder streams (native path): 1 = one stream; 2 = the context encoder on a side HIP stream
+# beside the feature encoder.  Autograd replays every node's backward on its forward's stream, so
+# the backwards overlap the same way.  The encoders are independent until the decode; co-running
+# fills each other's kernel tails and small launches (round 6 A/B: 484.3 / 488.3 vs 466.1 / 466.8
+# pairs/s on one box; the feature encoder's two frames on a third stream as well: 468.6 / 468.0
+# vs 476.6 / 480.3 -- profiles/r6/enc_streams/).  Default (unset): 2 under bf16 autocast only --
+# the configuration validated over thousands of steps; an fp16-autocast bench with two streams
+# hit an illegal address in a late step (profiles/r6/r6i/bench_fp16_2streams.log), as a two-stream
+# attempt in round 4 did inside MIOpen, so fp16 and fp32 keep one stream unless 2 is forced.
+_ENC_STREAMS = os.environ.get('RAFT_ENC_STREAMS', 'auto')
 _SIDE = {}
 
 
@@ -200,7 +203,7 @@ class RAFT(nn.Module):
                 image1 = image1.contiguous(memory_format=torch.channels_last)
                 image2 = image2.contiguous(memory_format=torch.channels_last)
         side = None
-        if (_ENC_STREAMS >= 2 and pair is not None and dev.type == 'cuda'
+        if (self._enc_streams() >= 2 and pair is not None and dev.type == 'cuda'
                 and not torch.cuda.is_current_stream_capturing()):
             main = torch.cuda.current_stream(dev)
             side = _enc_side_stream(dev)
@@ -232,6 +235,11 @@ class RAFT(nn.Module):
             net.record_stream(main)
             inp.record_stream(main)
         return fmap1, fmap2, net, inp
+
+    def _enc_streams(self):
+        if _ENC_STREAMS != 'auto':
+            return int(_ENC_STREAMS)
+        return 2 if (self.args.mixed_precision and self.amp_dtype == torch.bfloat16) else 1
 
     def decode(self, fmap1, fmap2, net, inp, iters=12, flow_init=None, test_mode=False):
         """Correlation volume + GRU iterations + upsampling (`core/raft.py:102-144`)."""
@@ -317,14 +325,14 @@ class RAFT(nn.Module):
 
     def _use_fused_update(self, img):
         """Fused MFMA update block: GPU and mixed precision -- bf16 or fp16 autocast (full and
-        small model; the operand dtype of the conv kernels' MFMAs) -- or the fp32 schedule of the
-        full model (split-fp32 operands: bf16 [hi | lo] pairs, three products
-        per conv; RAFT_FP32_FUSED=0 keeps the per-conv split path of ops/conv_fp32.py)."""
+        small model; the operand dtype of the conv kernels' MFMAs) -- or the fp32 schedule (full and
+        small model; split-fp32 operands: bf16 [hi | lo] pairs, three products per conv;
+        RAFT_FP32_FUSED=0 keeps the per-conv split path of ops/conv_fp32.py)."""
         impl = _get(self.args, 'update_impl', 'auto')
         if impl == 'torch' or self.corr_impl == 'torch' or not _ext.device_ok(img):
             return False
         ok = self.args.mixed_precision and self.amp_dtype in (torch.bfloat16, torch.float16)
-        ok = ok or (not self.args.mixed_precision and not self.args.small and _FP32_FUSED)
+        ok = ok or (not self.args.mixed_precision and _FP32_FUSED)
         if not ok:
             if impl == 'hip':
                 raise ValueError("update_impl='hip' needs mixed precision (bf16 / fp16), or the "
@@ -336,11 +344,16 @@ class RAFT(nn.Module):
     def _iterate_fused_small(self, net, inp, corr_fn, coords0, coords1, iters, test_mode):
         """RAFT-small: fused ConvGRU iterations (ops/update_hip_small.py), upflow8 output."""
         from ..ops.update_hip_small import HipSmallUpdateBlock, CORR_BUF_SMALL, HDP
-        adt = self.amp_dtype   # bf16 or fp16 operands
+        from ..ops.update_hip import split_nhwc
+        # bf16 / fp16 operands, or fp32 (split bf16 pairs)
+        adt = self.amp_dtype if self.args.mixed_precision else torch.float32
         hub = HipSmallUpdateBlock(self.update_block, dtype=adt)
-        h = torch.nn.functional.pad(net.to(adt).permute(0, 2, 3, 1),
-                                    (0, HDP - net.shape[1])).contiguous()
-        x = inp.to(adt).permute(0, 2, 3, 1).contiguous()
+        if adt == torch.float32:
+            h, x = split_nhwc(net.float(), HDP), split_nhwc(inp.float())
+        else:
+            h = torch.nn.functional.pad(net.to(adt).permute(0, 2, 3, 1),
+                                        (0, HDP - net.shape[1])).contiguous()
+            x = inp.to(adt).permute(0, 2, 3, 1).contiguous()
         flow_predictions = []
         flow_up = None
         flow = coords1 - coords0

@@ -23,7 +23,10 @@ pre-activation gradients to the dgrad / wgrad kernels, like the full block.
 
 Operand dtype: bf16 (bf16 autocast) or fp16 (fp16 autocast, the reference's --mixed_precision,
 `core/raft.py:99`): every 16-bit buffer, packed weight and MFMA of a step is of that type
-(``HipSmallUpdateBlock(ub, dtype)``); accumulation and the carried gradients stay fp32.
+(``HipSmallUpdateBlock(ub, dtype)``); accumulation and the carried gradients stay fp32.  dtype
+fp32 is the fp32 schedule of the full block: every 16-bit buffer is a split-fp32 bf16 [hi | lo]
+pair buffer of twice the width, every conv three MFMA products (hi*hi + lo*hi + hi*lo, ~2^-16
+relative to fp32), the elementwise backward kernels read and write the pairs.
 """
 import torch
 
@@ -75,14 +78,15 @@ SMALL = Design(SMALL_SPECS, small_module_params)
 
 
 def _zeros_bf16(shape, dev, dt=torch.bfloat16):
-    return torch.zeros(*shape, device=dev, dtype=dt)
+    return _bf16(shape, dev, dt).zero_()   # dt fp32: a zeroed split pair buffer
 
 
 def _conv(pk, name, segs, epi, outs, offs, aux=(), aux_offs=(), split=0, bias=None):
     s = SMALL.spec[name]
     k, pad, small = ((1, 1), (0, 0), False) if s.patch else (s.k, s.pad, s.small)
-    C.conv_fwd(segs, pk.w[name], pk.b[name] if bias is None else bias, k, pad, s.cout, epi, outs,
-               offs, aux, aux_offs, scale=s.scale, split=split, cin_small=2 if small else 0)
+    C.conv_fwd(segs, pk.w[name], pk.b[name] if bias is None else bias, k, pad, s.cout,
+               epi | (C.EPI_SPL if pk.spl else 0), outs, offs, aux, aux_offs, scale=s.scale,
+               split=split, cin_small=2 if small else 0)
 
 
 def _ctx_maps(pk, inp):
@@ -161,6 +165,7 @@ class _SmallUpdateIter(torch.autograd.Function):
         dev = hn.device
         sh = (B, H, W)
         dt = pk.dtype
+        spl = pk.spl   # fp32 schedule: split pair buffers
         ops = _ext.ops()
 
         def dgrad(name, gsegs, outs, scale=1.0):
@@ -171,15 +176,20 @@ class _SmallUpdateIter(torch.autograd.Function):
             ops.conv_dgrad_([g[0] for g in gsegs], [g[1] for g in gsegs], [g[2] for g in gsegs],
                             pk.wd[name], s.k[0], s.k[1], s.pad[0], s.pad[1], 0, float(scale),
                             [o[0] for o in outs], [o[1] for o in outs], [o[2] for o in outs],
-                            [o[3] for o in outs], [o[4] for o in outs], ry, roff, [], [])
+                            [o[3] for o in outs], [o[4] for o in outs], ry, roff, [], [], [], spl)
 
         # ---- flow head: conv2 (128 -> 2) as an MFMA conv on a 64-wide bf16 gradient
-        g2 = _zeros_bf16(sh + (64,), dev, dt)
-        g2[..., :2] = gdelta.permute(0, 2, 3, 1)
+        if spl:   # the fp32 delta gradient as a split operand (2 channels in a 64-wide slot)
+            g2 = _UH._to_split(gdelta.float(), _bf16(sh + (64,), dev, dt))
+        else:
+            g2 = _zeros_bf16(sh + (64,), dev, dt)
+            g2[..., :2] = gdelta.permute(0, 2, 3, 1)
         pk.defer_wgrad('fh2', g2, 0, [(fm, 0, 128)])
         dpre_fm = _zeros_bf16(sh + (128,), dev, dt)
         dgrad('fh2', [(g2, 0, 64)], [(dpre_fm, 0, 128, 128, 0, fm, 0)])
         pk.defer_wgrad('fh1', dpre_fm, 0, [(hn, 0, HDP)])
+        if gh is not None and spl:
+            gh = _UH._from_split(gh)
         dh = gh.float().contiguous() if gh is not None else _f32(sh + (HDP,), dev, zero=True)
         dgrad('fh1', [(dpre_fm, 0, 128)], [(dh, 0, HDP, 96, 1)])
         # ---- ConvGRU (pads: every gradient buffer is zero beyond the 96 real channels); the
@@ -200,7 +210,7 @@ class _SmallUpdateIter(torch.autograd.Function):
         st.ctx_g.setdefault('zr', []).append(dpre_zr)
         # ---- motion encoder
         dpre_conv = _zeros_bf16(sh + (128,), dev, dt)
-        ops.relu_bwd_(dmf, 0, mf, 0, dpre_conv, 0, 80, 1.0)
+        ops.relu_bwd_(dmf, 0, mf, 0, dpre_conv, 0, 80, 1.0, spl)
         pk.defer_wgrad('conv', dpre_conv, 0, [(cf, 0, 128)])
         dpre_cf = _bf16(sh + (128,), dev, dt)
         dgrad('conv', [(dpre_conv, 0, 128)], [(dpre_cf, 0, 128, 128, 0, cf, 0)])
@@ -217,11 +227,16 @@ class _SmallUpdateIter(torch.autograd.Function):
         if ctx.itr == 0:
             dinp = _f32(sh + (64,), dev)
             for j, name in enumerate(GRU_S):
-                gsum = _UH._sum_bf16(st.ctx_g.pop(name))
-                dgrad(name + 'i', [(gsum, 0, gsum.shape[-1])], [(dinp, 0, 64, 64, int(j > 0))])
+                gsum = _UH._sum_bf16(st.ctx_g.pop(name), spl)
+                cnt = gsum.shape[-1] // 2 if spl else gsum.shape[-1]
+                dgrad(name + 'i', [(gsum, 0, cnt)], [(dinp, 0, 64, 64, int(j > 0))])
                 pk.defer_wgrad(name + 'i', gsum, 0, [(inp, 0, 64)])
             st.ctx_g = {}
             st.next_bwd = None
+        if spl:   # split inputs take split-encoded gradients (same shape and dtype as h / inp)
+            dhp = _UH._to_split(dhp.permute(0, 3, 1, 2))
+            if dinp is not None:
+                dinp = _UH._to_split(dinp.permute(0, 3, 1, 2))
         return (None, dhp, dinp, dcorr, None, None)
 
 
@@ -229,7 +244,7 @@ class HipSmallUpdateBlock:
     """Drives the fused iterations for one forward pass of a SmallUpdateBlock."""
 
     def __init__(self, update_block, dtype=torch.bfloat16):
-        assert dtype in (torch.bfloat16, torch.float16), dtype
+        assert dtype in (torch.bfloat16, torch.float16, torch.float32), dtype
         self.state = _State()
         self.state.ub = update_block
         self.state.design = SMALL

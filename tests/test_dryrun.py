@@ -144,15 +144,15 @@ def test_dry_run_inference():
     assert ops.calls.count('convex_up_fwd') == 1  # only after the last iteration
 
 
-@pytest.mark.parametrize('alternate', [False, True])
-def test_dry_run_fp32_fused_training_step(alternate):
+@pytest.mark.parametrize('alternate,small', [(False, False), (True, False), (False, True), (True, True)])
+def test_dry_run_fp32_fused_training_step(alternate, small):
     """fp32 schedule (no mixed precision) through the fused block on split-fp32 operands: the
     conv schemas take the split flags, the flow head runs on the MFMA convs (no fh2_* VALU ops),
     and every update-block parameter gets a gradient of its own shape."""
     from pytorch_raft_amd import RAFT
     from pytorch_raft_amd.ops.loss import sequence_loss
     from pytorch_raft_amd.data.synthetic import make_pair_batch
-    args = argparse.Namespace(small=False, mixed_precision=False, corr_impl='hip', update_impl='hip',
+    args = argparse.Namespace(small=small, mixed_precision=False, corr_impl='hip', update_impl='hip',
                               alternate_corr=alternate)
     torch.manual_seed(0)
     m = RAFT(args).train()

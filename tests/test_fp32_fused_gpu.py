@@ -345,3 +345,164 @@ def test_split_dgrad_1x1_sliced_relu_output(ext_ops, cfg):
     got = _join(out)
     assert (got[..., :256] == 0).all()
     assert _rel(got[..., 256:].permute(0, 3, 1, 2), ref) < 3e-5
+
+
+def test_split_gru_relu_bwd_kernels_vs_fp64(ext_ops):
+    """gru_q_bwd_ / gru_zr_bwd_ / relu_bwd_ on split pair buffers (the small block's fp32
+    schedule): the GRU gate algebra and the ReLU-gated cast on hi + lo values, outputs re-split."""
+    torch.manual_seed(11)
+    B, H, W, hd = 2, 6, 7, 128
+    z, q, r, hp = (torch.rand(B, H, W, hd, device=DEV) * 2 - 1 for _ in range(4))
+    z, r = z.sigmoid(), r.sigmoid()
+    zs, qs, rs, hs = (_split(t) for t in (z, q, r, hp))
+    zd, qd, rd, hd_ = (_join(t) for t in (zs, qs, rs, hs))
+    dh = torch.randn(B, H, W, hd, device=DEV)
+    dpre_q = torch.empty(B, H, W, 2 * hd, device=DEV, dtype=BF)
+    dz = torch.empty(B, H, W, hd, device=DEV)
+    dhp = torch.empty(B, H, W, hd, device=DEV)
+    ext_ops.gru_q_bwd_(dh, zs, qs, hs, dpre_q, dz, dhp)
+    g = dh.double()
+    assert _rel(_join(dpre_q), g * zd * (1 - qd * qd)) < 1e-5
+    assert _rel(dz, g * (qd - hd_)) < 1e-6
+    assert _rel(dhp, g * (1 - zd)) < 1e-6
+    drh = torch.randn(B, H, W, hd, device=DEV)
+    dhp0 = dhp.double().clone()
+    dzr = torch.empty(B, H, W, 4 * hd, device=DEV, dtype=BF)
+    ext_ops.gru_zr_bwd_(drh, dz, zs, rs, hs, dzr, dhp)
+    zr_hi, zr_lo = dzr[..., :2 * hd].double(), dzr[..., 2 * hd:].double()
+    zr = zr_hi + zr_lo
+    assert _rel(zr[..., :hd], dz.double() * zd * (1 - zd)) < 1e-5
+    assert _rel(zr[..., hd:], drh.double() * hd_ * rd * (1 - rd)) < 1e-5
+    assert _rel(dhp, dhp0 + drh.double() * rd) < 1e-6
+    # relu_bwd_: channels [0, 80) of a 128-wide fp32 gradient, gated by a split forward output
+    gm = torch.randn(B, H, W, 128, device=DEV)
+    y = torch.randn(B, H, W, 128, device=DEV)
+    ys = _split(y)
+    out = torch.zeros(B, H, W, 256, device=DEV, dtype=BF)
+    ext_ops.relu_bwd_(gm, 0, ys, 0, out, 0, 80, 1.0, True)
+    got = _join(out)
+    assert (got[..., 80:] == 0).all()
+    assert _rel(got[..., :80], gm[..., :80].double() * (_join(ys)[..., :80] > 0)) < 1e-5
+
+
+def test_fp32_small_fused_iteration_vs_fp64(ext_ops):
+    """Two iterations of the fused RAFT-small block on split-fp32 operands
+    (HipSmallUpdateBlock(dtype=fp32)) vs the module's eager fp64 forward / backward, ReLU masks
+    shared (see test_fp32_fused_update_iteration_vs_fp64): h', delta and every parameter,
+    state, context and correlation gradient."""
+    from pytorch_raft_amd.models.update import SmallUpdateBlock
+    from pytorch_raft_amd.ops import update_hip_small as S
+    from pytorch_raft_amd.ops.update_hip import split_nhwc
+    torch.manual_seed(6)
+    args = argparse.Namespace(corr_levels=4, corr_radius=3)
+    ub = SmallUpdateBlock(args, hidden_dim=96).to(DEV)
+    for p in ub.parameters():
+        p.data.mul_(1.5)
+    B, H, W, iters = 2, 12, 15, 2
+    net = torch.randn(B, 96, H, W, device=DEV).tanh()
+    inp = torch.randn(B, 64, H, W, device=DEV).relu()
+    corrs = [torch.randn(B, 196, H, W, device=DEV) for _ in range(iters)]
+    flows = [torch.randn(B, 2, H, W, device=DEV) * 3 for _ in range(iters)]
+    gd = [torch.randn(B, 2, H, W, device=DEV) for _ in range(iters)]
+    saved = []
+    orig_fwd = S._iter_forward
+
+    def keep(*a, **k):
+        out = orig_fwd(*a, **k)
+        saved.append(out[2])
+        return out
+
+    S._iter_forward = keep
+    try:
+        leaves = [t.clone().requires_grad_(True) for t in [net, inp] + corrs]
+        hub = S.HipSmallUpdateBlock(ub, dtype=torch.float32)
+        h = split_nhwc(leaves[0], S.HDP)
+        x = split_nhwc(leaves[1])
+        loss = 0
+        for i in range(iters):
+            cs = split_nhwc(leaves[2 + i], S.CORR_BUF_SMALL)
+            h, delta = hub(h, x, cs, flows[i])
+            assert delta.dtype == torch.float32
+            loss = loss + (delta * gd[i]).sum()
+        hf = h
+    finally:
+        S._iter_forward = orig_fwd
+    loss.backward()
+    masks = []   # ReLU call order of one eager iteration (models/update.py SmallUpdateBlock)
+    for sv in saved:   # (corr, patch, cf, f1, mf, inp, h, z, rh, r, q, hn, fm)
+        cf, f1, mf, fm = (_join(t.detach()).permute(0, 3, 1, 2) > 0 for t in
+                          (sv[2], sv[3], sv[4], sv[12]))
+        masks += [cf[:, :96], f1, cf[:, 96:128], mf[:, :80], fm[:, :128]]
+    grads = {n: (p.grad.clone() if p.grad is not None else torch.zeros_like(p))
+             for n, p in ub.named_parameters()}
+    lgrads = [t.grad.clone() if t.grad is not None else None for t in leaves]
+
+    def eager(dtype):
+        m = SmallUpdateBlock(args, hidden_dim=96).to(DEV).to(dtype)
+        m.load_state_dict(ub.state_dict())
+        lv = [t.detach().to(dtype).requires_grad_(True) for t in [net, inp] + corrs]
+        hh, tot = lv[0], 0
+        queue = list(masks)
+        relu = F.relu
+        F.relu = lambda x, inplace=False: x * queue.pop(0).to(x.dtype)
+        try:
+            for i in range(iters):
+                hh, _, dl = m(hh, lv[1], lv[2 + i], flows[i].to(dtype))
+                tot = tot + (dl * gd[i].to(dtype)).sum()
+        finally:
+            F.relu = relu
+        assert not queue
+        tot.backward()
+        return hh.detach(), tot.item(), {n: (p.grad if p.grad is not None else torch.zeros_like(p))
+                                          for n, p in m.named_parameters()}, [t.grad for t in lv]
+
+    h64, loss64, g64, l64 = eager(torch.float64)
+    _, _, g32, l32 = eager(torch.float32)
+    hj = _join(hf).permute(0, 3, 1, 2)
+    assert (hj[:, 96:] == 0).all()   # the padded state channels stay exact zeros
+    assert _rel(hj[:, :96], h64) < 1e-4
+    assert abs(loss.item() - loss64) <= 1e-4 * abs(loss64)
+    report = [(n, _rel(grads[n], g64[n]), _rel(g32[n], g64[n])) for n in g64 if g64[n].norm() > 0]
+    report += [('input%d' % i, _rel(a, b64), _rel(b32, b64))
+               for i, (a, b64, b32) in enumerate(zip(lgrads, l64, l32)) if b64 is not None]
+    for r in report:
+        print('%-32s %.3e %.3e' % r)
+    bad = [r for r in report if not r[1] < max(1e-4, 50 * r[2])]
+    assert not bad, bad[:4]
+
+
+def test_fp32_small_model_uses_fused_split_block(ext_ops):
+    """An fp32 RAFT-small decodes through the fused split-fp32 small block: a training step's
+    flow and update-block gradients match the eager fp32 block (update_impl='torch')."""
+    from pytorch_raft_amd import RAFT
+    from pytorch_raft_amd.ops.loss import sequence_loss
+    from pytorch_raft_amd.data.synthetic import make_pair_batch
+    from pytorch_raft_amd.ops import update_hip_small as S
+    outs = {}
+    calls = {'n': 0}
+    orig = S._iter_forward
+
+    def counting(pk, *a, **k):
+        calls['n'] += int(pk.spl)
+        return orig(pk, *a, **k)
+
+    S._iter_forward = counting
+    try:
+        for impl in ('auto', 'torch'):
+            args = argparse.Namespace(small=True, mixed_precision=False, update_impl=impl)
+            torch.manual_seed(0)
+            m = RAFT(args).to(DEV).train()
+            i1, i2, flow, valid = (t.to(DEV) for t in make_pair_batch(2, 128, 160, seed=3))
+            preds = m(i1, i2, iters=3)
+            loss, _ = sequence_loss(preds, flow, valid, 0.8)
+            loss.backward()
+            outs[impl] = (preds[-1].detach(), {n: p.grad.detach().clone()
+                                               for n, p in m.named_parameters() if p.grad is not None})
+    finally:
+        S._iter_forward = orig
+    assert calls['n'] == 3
+    (fa, ga), (fb, gb) = outs['auto'], outs['torch']
+    assert _rel(fa, fb) < 1e-3
+    for n in gb:
+        if n.startswith('update_block'):
+            assert _rel(ga[n], gb[n]) < 2e-2, n
