@@ -577,7 +577,8 @@ def _backward_overlapped(st, pk, n):
 # OFF by default (RAFT_UPDATE_BRANCHES=1 enables it): measured 381-383 vs 397-398 pairs/s
 # without -- co-running convs slow each other more than the overlap gains (kernel sum per step
 # 31.0 -> 33.0 ms: the XCD-local tile order and L2 reuse of each conv are lost when two grids
-# share the XCDs).
+# share the XCDs).  Round 6 re-check with the persisted tile table: 471.3 / 475.1 vs 476.0 / 478.3
+# pairs/s (profiles/r6/r6i/ab_*.log) -- still off.
 _BRANCHES = os.environ.get('RAFT_UPDATE_BRANCHES', '0') == '1'
 # ConvGRU gate backward (gru_q_bwd / gru_zr_bwd) fused into the dgrad epilogues (OSeg.gate);
 # RAFT_GRU_GATES_FUSED=0 runs the separate elementwise kernels
