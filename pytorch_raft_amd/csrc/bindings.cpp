@@ -333,13 +333,15 @@ void corr_otf_fwd_(const Tensor& f1, const std::vector<Tensor>& f2, const Tensor
   TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.dim() == 4 && out.size(0) == B &&
                   out.size(1) == H && out.size(2) == W && out.size(3) >= (int64_t)f2.size() * D * D,
               "out must be contiguous (B,H,W,S) with S >= levels*(2r+1)^2");
-  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16,
-              "out must be float32 or bfloat16");
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16 ||
+                  (out.scalar_type() == at::kHalf && f1lo != nullptr),
+              "out must be float32 or bfloat16 (float16: the fp32-accurate split forward only)");
+  const int omode = out.scalar_type() == at::kHalf ? 2 : (out.scalar_type() == at::kBFloat16 ? 1 : 0);
   TORCH_CHECK(launch_corr_otf_fwd(reinterpret_cast<const uint16_t*>(f1.data_ptr()), L.ptr.data(),
                                   f1lo, f1lo ? LL.ptr.data() : nullptr, L.h.data(), L.w.data(),
                                   (int)f2.size(),
                                   coords.data_ptr<float>(), out.data_ptr(),
-                                  out.scalar_type() == at::kBFloat16, (int)out.size(3), (int)B,
+                                  omode, (int)out.size(3), (int)B,
                                   (int)C, (int)H, (int)W, (int)radius, cur_stream()),
               "on-the-fly corr supports radius 3/4 with C = 128/256");
 }

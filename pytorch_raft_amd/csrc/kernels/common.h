@@ -68,6 +68,13 @@ template <> struct St<uint16_t> {
     p[i] = raft_f32_to_bf16(v);
   }
 };
+// fp16 bits (fp16 autocast outputs)
+struct Fp16Bits { uint16_t v; };
+template <> struct St<Fp16Bits> {
+  __device__ __forceinline__ static void put(Fp16Bits* p, int64_t i, float v) {
+    reinterpret_cast<uint16_t*>(p)[i] = raft_f2h<true>(v);
+  }
+};
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

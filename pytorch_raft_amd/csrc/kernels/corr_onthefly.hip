@@ -843,11 +843,15 @@ bool launch_corr_otf_fwd(const uint16_t* f1, const uint16_t* const* f2lvl, const
 #define FWD_BF16(RR, CC) FWD(RR, CC, uint16_t, false)
 #define FWD_F32(RR, CC) FWD(RR, CC, float, false)
 #define FWD_BF16_SPLIT(RR, CC) FWD(RR, CC, uint16_t, true)
+#define FWD_F16_SPLIT(RR, CC) FWD(RR, CC, Fp16Bits, true)
 #define FWD_F32_SPLIT(RR, CC) FWD(RR, CC, float, true)
+  // out_bf16: 0 fp32, 1 bf16, 2 fp16 (the fp32-accurate split forward under fp16 autocast)
   if (split) {
+    if (out_bf16 == 2) OTF_CASES(FWD_F16_SPLIT);
     if (out_bf16) OTF_CASES(FWD_BF16_SPLIT);
     OTF_CASES(FWD_F32_SPLIT);
   }
+  if (out_bf16 == 2) return false;
   if (out_bf16) OTF_CASES(FWD_BF16);
   OTF_CASES(FWD_F32);
 #undef FWD

@@ -188,13 +188,13 @@ class AlternateCorrBlock:
         return torch_onthefly_corr(self.pyramid2, self.fmap1, coords, self.radius)
 
     def lookup_nhwc(self, coords, cbuf, dtype=torch.bfloat16):
-        """(B,H,W,cbuf) zero-padded taps for the fused HIP update block (bf16 MFMA taps; an fp16
-        update block gets them converted; dtype fp32: split-fp32 [hi | lo] taps of the fp32
-        on-the-fly lookup)."""
+        """(B,H,W,cbuf) zero-padded taps for the fused HIP update block (bf16 MFMA taps; fp16
+        taps under fp16 autocast, written as fp16 by the fp32-accurate split forward; dtype fp32:
+        split-fp32 [hi | lo] taps of the fp32 on-the-fly lookup)."""
         if dtype == torch.float32:
             from ..ops.update_hip import split_nhwc
             return split_nhwc(self(coords), cbuf)
         if self.hip:
-            out = self.volume.lookup_nhwc(coords, self.radius, cbuf)
+            out = self.volume.lookup_nhwc(coords, self.radius, cbuf, dtype)
             return out if out.dtype == dtype else out.to(dtype)
         return _to_nhwc_padded(self(coords), cbuf, dtype)

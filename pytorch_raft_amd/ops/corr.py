@@ -334,12 +334,14 @@ class _OTFLookup(torch.autograd.Function):
 
 
 class _OTFLookupNHWC(torch.autograd.Function):
-    """bf16 taps straight into the zero-padded (B,H,W,cbuf) input of the fused update block."""
+    """bf16 taps straight into the zero-padded (B,H,W,cbuf) input of the fused update block; fp16
+    taps (fp16 autocast) from the fp32-accurate split forward, stored as fp16 by the kernel."""
 
     @staticmethod
-    def forward(ctx, token, coords, radius, state, cbuf):
+    def forward(ctx, token, coords, radius, state, cbuf, dtype=torch.bfloat16):
         b, _, h, w = coords.shape
-        out = torch.empty(b, h, w, cbuf, device=coords.device, dtype=torch.bfloat16)
+        dt = torch.float16 if (dtype == torch.float16 and state.lo) else torch.bfloat16
+        out = torch.empty(b, h, w, cbuf, device=coords.device, dtype=dt)
         _ext.ops().corr_otf_fwd_(state.f1, state.f2, coords, radius, out, state.lo)
         ctx.state = state
         ctx.radius = radius
@@ -354,11 +356,12 @@ class _OTFLookupNHWC(torch.autograd.Function):
             # the iteration's bf16 tap gradient is kept; the MFMA box GEMMs + dF2 atomics then run
             # ONCE per step over all iterations (build node backward) instead of once per
             # iteration, forming each pixel's window gradients from the taps in LDS
+            # (fp16 tap gradients are rounded to bf16 here: the backward's MFMA operand type)
             st.windows.append((coords, dout.to(torch.bfloat16).contiguous()))
             st.radius = ctx.radius
         else:
             _otf_backward(st, coords, dout, ctx.radius)
-        return None, None, None, None, None
+        return None, None, None, None, None, None
 
 
 class OnTheFlyVolume:
@@ -374,6 +377,6 @@ class OnTheFlyVolume:
     def lookup(self, coords, radius):
         return _OTFLookup.apply(self.token, coords.contiguous().float(), radius, self.state)
 
-    def lookup_nhwc(self, coords, radius, cbuf):
+    def lookup_nhwc(self, coords, radius, cbuf, dtype=torch.bfloat16):
         return _OTFLookupNHWC.apply(self.token, coords.contiguous().float(), radius, self.state,
-                                    cbuf)
+                                    cbuf, dtype)

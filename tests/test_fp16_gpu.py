@@ -178,3 +178,23 @@ def test_lookup_and_fold_fp16(ext_ops, w):
         ext_ops.corr_lookup_bwd_(gp, cc, t.to(H16).float().contiguous(), 4)
     dref = ext_ops.corr_pyr_grad_reduce(gp, 1 / 16)
     assert ((d16 - dref).norm() / dref.norm()).item() < 1e-5
+
+
+def test_onthefly_lookup_nhwc_fp16_taps(ext_ops):
+    """On-the-fly correlation under fp16 autocast: the fp32-accurate split forward writes fp16
+    taps itself (no bf16 rounding + cast), within fp16 rounding of the fp32 all-pairs lookup."""
+    from pytorch_raft_amd.models.corr import AlternateCorrBlock
+    b, c, h, w = 2, 256, 16, 24
+    g = torch.Generator(device='cpu').manual_seed(4)
+    f1 = torch.randn(b, c, h, w, generator=g).to(DEV)
+    f2 = torch.randn(b, c, h, w, generator=g).to(DEV)
+    ys, xs = torch.meshgrid(torch.arange(h).float(), torch.arange(w).float(), indexing='ij')
+    coords = (torch.stack([xs, ys])[None].repeat(b, 1, 1, 1) +
+              2 * torch.randn(b, 2, h, w, generator=g)).to(DEV)
+    blk = AlternateCorrBlock(f1, f2, radius=4, impl='hip', precision='fp32')
+    out = blk.lookup_nhwc(coords, 384, H16)
+    assert out.dtype == H16 and out.shape == (b, h, w, 384)
+    assert (out[..., 324:] == 0).all()
+    ref = ext_ops.corr_lookup_fwd(ext_ops.corr_build(f1, f2, 4), coords, 4).permute(0, 2, 3, 1)
+    err = (out[..., :324].float() - ref).abs().max().item()
+    assert err <= 2.0 ** -10 * ref.abs().max().item() + 1e-4, err
