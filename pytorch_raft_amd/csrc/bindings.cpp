@@ -1266,7 +1266,8 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
                               const c10::optional<Tensor>& cbias,
                               const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
                               double momentum, double eps, const c10::optional<Tensor>& res,
-                              const Tensor& y, const c10::optional<Tensor>& ysplit) {
+                              const Tensor& y, const c10::optional<Tensor>& ysplit,
+                              const c10::optional<Tensor>& tstats, int64_t tiles) {
   const at::ScalarType st = opnorm(x);
   check_cl16(st, x, "x");
   check_cl16(st, y, "y");
@@ -1293,16 +1294,29 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
   const uint16_t* xp = u16(x);
   int ppb = 0, nblk = 0;
   Tensor part;
-  if (mode <= 1) {
-    nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
-    part = at::empty({groups * (nblk + 1) * 2 * C}, fo);  // partials + per-group sums
-    launch_norm_stats(xp, (int)N, (int)HW, (int)C, mode == 0, part.data_ptr<float>(), nblk, ppb,
-                      norm_ty(st), cur_stream());
+  const bool tiled = mode <= 1 && tstats.has_value() && tstats->defined();
+  if (tiled) {
+    // the producing conv's per-tile statistics: no statistics pass over x
+    check_cuda_f32(*tstats, "tstats");
+    TORCH_CHECK(tiles > 0 && tstats->is_contiguous() && tstats->numel() == N * tiles * 4 * C,
+                "tstats must be a contiguous (N * tiles, 4, C) fp32 tensor");
+    launch_norm_finalize_tiled(tstats->data_ptr<float>(), mode == 0 ? (int)tiles : (int)(N * tiles),
+                               (int)N, (int)HW, (int)C, (int)mode, gp, bp, cb, rm, rv,
+                               (float)momentum, (float)eps, mean.data_ptr<float>(),
+                               invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                               shift.data_ptr<float>(), cur_stream());
+  } else {
+    if (mode <= 1) {
+      nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
+      part = at::empty({groups * (nblk + 1) * 2 * C}, fo);  // partials + per-group sums
+      launch_norm_stats(xp, (int)N, (int)HW, (int)C, mode == 0, part.data_ptr<float>(), nblk, ppb,
+                        norm_ty(st), cur_stream());
+    }
+    launch_norm_finalize(mode <= 1 ? part.data_ptr<float>() : nullptr, xp, (int)N, (int)HW, (int)C,
+                         (int)mode, nblk, gp, bp, cb, rm, rv, (float)momentum, (float)eps,
+                         mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
+                         shift.data_ptr<float>(), norm_ty(st), cur_stream());
   }
-  launch_norm_finalize(mode <= 1 ? part.data_ptr<float>() : nullptr, xp, (int)N, (int)HW, (int)C,
-                       (int)mode, nblk, gp, bp, cb, rm, rv, (float)momentum, (float)eps,
-                       mean.data_ptr<float>(), invstd.data_ptr<float>(), scale.data_ptr<float>(),
-                       shift.data_ptr<float>(), norm_ty(st), cur_stream());
   const auto ys = opt_split(ysplit, x, "ysplit");
   launch_norm_apply(xp, scale.data_ptr<float>(), shift.data_ptr<float>(), (int)N, (int)HW, (int)C,
                     (int)relu, rp, u16m(y), norm_ty(st), cur_stream(), ys.first, ys.second);
@@ -1506,7 +1520,9 @@ void check_pc(const Tensor& t, int64_t P, int64_t C, at::ScalarType st, const ch
 // out[:, o_off:o_off+C] (bf16) = g[:, g_off:g_off+C] * scale * [y[:, y_off:] > 0]
 // stride-1 3x3 conv, 64 -> 64 channels, NHWC bf16 (the encoders' layer1; forward, or the input
 // gradient with the adjoint weight pack)
-void conv_enc64_(const Tensor& x, const Tensor& wpk, const Tensor& out) {
+// part (optional): the norm statistics of the output per 8 x 16 tile, (B * tiles, 4, 64) fp32
+// (see launch_conv_enc64), for norm_fwd_'s tstats
+void conv_enc64_(const Tensor& x, const Tensor& wpk, const Tensor& out, const c10::optional<Tensor>& part) {
   TORCH_CHECK(x.dim() == 4 && x.size(3) == 64, "x must be (B,H,W,64)");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2);
   const at::ScalarType st = op16(x);
@@ -1524,8 +1540,16 @@ void conv_enc64_(const Tensor& x, const Tensor& wpk, const Tensor& out) {
     (void)hipGetDevice(&dev);
     return hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
   }();
+  float* pp = nullptr;
+  if (part.has_value() && part->defined()) {
+    check_cuda_f32(*part, "conv_enc64 part");
+    TORCH_CHECK(part->is_contiguous() &&
+                    part->numel() == B * conv_enc64_tiles((int)H, (int)W) * 4 * 64,
+                "conv_enc64 part must be a contiguous (B * tiles, 4, 64) fp32 tensor");
+    pp = part->data_ptr<float>();
+  }
   TORCH_CHECK(launch_conv_enc64(u16(x), u16(wpk), u16m(out), (int)B, (int)H, (int)W, cus,
-                                st == at::kHalf, cur_stream()),
+                                st == at::kHalf, cur_stream(), pp),
               "conv_enc64 launch failed");
 }
 
@@ -2004,7 +2028,7 @@ TORCH_LIBRARY(raft_amd, m) {
     std::vector<int> r(rows.begin(), rows.end());
     return conv_import_tuned(r.data(), (int)(r.size() / 13));
   });
-  m.def("norm_fwd_(Tensor x, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor? cbias, Tensor(a!)? rmean, Tensor(b!)? rvar, float momentum, float eps, Tensor? res, Tensor(c!) y, Tensor(d!)? ysplit=None) -> Tensor[]");
+  m.def("norm_fwd_(Tensor x, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor? cbias, Tensor(a!)? rmean, Tensor(b!)? rvar, float momentum, float eps, Tensor? res, Tensor(c!) y, Tensor(d!)? ysplit=None, Tensor? tstats=None, int tiles=0) -> Tensor[]");
   m.def("norm_bwd_(Tensor dy, Tensor x, Tensor? y, Tensor mean, Tensor invstd, int mode, int relu, Tensor? gamma, Tensor? beta, Tensor(a!)? dgamma, Tensor(b!)? dbeta, Tensor(c!)? dcbias, Tensor(d!) dx, Tensor? dy2=None, Tensor? yres=None, Tensor(e!)? gout=None, Tensor(f!)? dxsplit=None) -> ()");
   m.def("add_relu_(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("relu_mask_(Tensor dy, Tensor y, Tensor(a!) g, Tensor? dy2=None) -> ()");
@@ -2023,7 +2047,7 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("corr_window_reduce(Tensor[] coords, Tensor[] wgs, int H, int W, int levels, int radius, float inv_sqrt_c, bool out_bf16=False) -> Tensor");
   m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off, int[] gate_mode, Tensor[] gate_t, int[] out_kcin=[], bool split=False) -> ()");
   m.def("split_hilo_(Tensor x, Tensor(a!) out) -> ()");
-  m.def("conv_enc64_(Tensor x, Tensor wpk, Tensor(a!) out) -> ()");
+  m.def("conv_enc64_(Tensor x, Tensor wpk, Tensor(a!) out, Tensor(b!)? part=None) -> ()");
   m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale, bool split=False) -> ()");
   m.def("gru_q_bwd_(Tensor dh, Tensor z, Tensor q, Tensor hprev, Tensor(a!) dpre_q, Tensor(b!) dz, Tensor(c!) dhprev) -> ()");
   m.def("gru_zr_bwd_(Tensor drh, Tensor dz, Tensor z, Tensor r, Tensor hprev, Tensor(a!) dpre_zr, Tensor(b!) dhprev) -> ()");

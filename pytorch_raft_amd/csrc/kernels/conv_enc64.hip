@@ -15,7 +15,11 @@
 //     no branches) while a tile's 72 MFMAs per wave run, the K loop reading the next tap's
 //     fragments ahead of the current tap's MFMAs;
 //   * writes the output tile through LDS as 16-B rows (per-lane 2-B stores of the MFMA layout
-//     were store-issue bound: ~115 us per call either way, profiles/r3/c2_kernel_summary.txt).
+//     were store-issue bound: ~115 us per call either way, profiles/r3/c2_kernel_summary.txt);
+//   * optionally (part != null: the output feeds a training-statistics norm) reduces the tile's
+//     rounded outputs into per-channel statistics of the norm that follows -- count, mean and
+//     sum of squared deviations, one [4][64] row per tile (encoder_norm.hip's tiled finalize) --
+//     so the norm skips its statistics pass over the output.
 // 4 waves as 2 (pixels) x 2 (channels): a wave owns 64 pixels (4 tile rows) x 32 channels.
 #include "common.h"
 #include "launchers.h"
@@ -48,6 +52,7 @@ constexpr int ABUF = 11 * AROWB;               // 10 halo rows + the spare piece
 constexpr int BBUF = 64 * BROW;                // 74,752 B
 constexpr int OROW = 144;                      // LDS bytes per staged output pixel (128 + 16 pad)
 constexpr int OBUF = TH * TW * OROW;           // 18,432 B
+constexpr int SBUF = 3 * 2 * 64 * 4;           // tile-statistics halves (count, mean, M2), 1,536 B
 
 // LDS offset of halo pixel hp (row-major over the 10 x 18 halo; hp >= 180: spare row 10)
 __device__ __forceinline__ int hoff(int hp) { return (hp / HWD) * AROWB + (hp % HWD) * AROW; }
@@ -65,8 +70,8 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
                                                             const uint16_t* __restrict__ wpk,
                                                             uint16_t* __restrict__ out, int B,
                                                             int H, int W, int tiles_y,
-                                                            int tiles_x) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * ABUF + BBUF + OBUF];
+                                                            int tiles_x, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * ABUF + BBUF + OBUF + SBUF];
   char* As = smem;                 // 2 halo buffers
   char* Bs = smem + 2 * ABUF;      // weights
   char* Os = Bs + BBUF;            // output tile staging (bf16 [pixel][channel])
@@ -164,6 +169,8 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
       }
     }
 
+    const int b = t / (tiles_y * tiles_x), r = t - b * tiles_y * tiles_x;
+    const int ty0 = (r / tiles_x) * TH, tx0 = (r % tiles_x) * TW;
     // epilogue: the accumulators go to an LDS [pixel][channel] bf16 tile, then out as 16-B rows
     // of 8 channels (4 stores per thread instead of 32 scattered 2-B stores per lane, whose issue
     // set the tile time); pixels past the image edge dropped
@@ -175,9 +182,46 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
         const int p = wm * 64 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
         *reinterpret_cast<uint16_t*>(Os + p * OROW + n * 2) = raft_f2h<F16>(acc[i][rr]);
       }
-    __syncthreads();  // staged tile complete (the next tile's stores come after its own barrier)
-    const int b = t / (tiles_y * tiles_x), r = t - b * tiles_y * tiles_x;
-    const int ty0 = (r / tiles_x) * TH, tx0 = (r % tiles_x) * TW;
+    float* red = reinterpret_cast<float*>(Os + OBUF);
+    if (part != nullptr) {
+      // norm statistics from the registers: this lane's 32 rounded values of channel n (two
+      // passes: mean, then squared deviations), merged with lane + 32's (Chan) and staged per
+      // pixel half wm; the two halves are merged after the staging barrier -- no extra barrier,
+      // no LDS re-read of the tile
+      float v[2][16];
+      float cnt = 0.f, sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int p = wm * 64 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
+          const bool ok = ty0 + p / TW < H && tx0 + p % TW < W;
+          v[i][rr] = ok ? raft_h2f<F16>(raft_f2h<F16>(acc[i][rr])) : 0.f;
+          cnt += ok ? 1.f : 0.f;
+          sum += v[i][rr];
+        }
+      const float mu = cnt > 0.f ? sum / cnt : 0.f;
+      float m2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int p = wm * 64 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
+          const bool ok = ty0 + p / TW < H && tx0 + p % TW < W;
+          const float d = v[i][rr] - mu;
+          m2 += ok ? d * d : 0.f;
+        }
+      const float cb = __shfl_xor(cnt, 32, 64), mb = __shfl_xor(mu, 32, 64), qb = __shfl_xor(m2, 32, 64);
+      const float nn = cnt + cb;
+      const float dl = mb - mu;
+      if (lane < 32) {
+        red[wm * 64 + n] = nn;
+        red[128 + wm * 64 + n] = nn > 0.f ? mu + dl * (cb / nn) : 0.f;
+        red[256 + wm * 64 + n] = m2 + qb + (nn > 0.f ? dl * dl * cnt * cb / nn : 0.f);
+      }
+    }
+    __syncthreads();  // staged tile (and statistics halves) complete; the next tile's stores come
+                      // after its own barrier
     const rsrc_t ro = mk_rsrc(out + (int64_t)b * H * W * 64, (uint32_t)H * W * 128);
 #pragma unroll
     for (int j = 0; j < TH * TW * 8 / NTH; ++j) {
@@ -189,6 +233,18 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
       const uint32_t off = yy < H && xx < W ? (uint32_t)((yy * W + xx) * 128 + q * 16) : OOB;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
                                              ro, off, 0, 0);
+    }
+    if (part != nullptr && tid < 64) {
+      // the tile's row for the tiled norm finalize: sum (x - K) = 0 with K = the tile mean,
+      // sum (x - K)^2 = M2, K, count (halves merged in a fixed order: deterministic)
+      const float na = red[tid], nb = red[64 + tid];
+      const float ma = red[128 + tid], mb = red[192 + tid];
+      const float nn = na + nb, dl = mb - ma;
+      float* dst = part + (int64_t)t * 256;
+      dst[tid] = 0.f;
+      dst[64 + tid] = red[256 + tid] + red[320 + tid] + (nn > 0.f ? dl * dl * na * nb / nn : 0.f);
+      dst[128 + tid] = nn > 0.f ? ma + dl * (nb / nn) : 0.f;
+      dst[192 + tid] = nn;
     }
   };
   // three register sets, two LDS buffers: the buffer index alternates at run time
@@ -204,16 +260,16 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
 
 // persistent grid: one workgroup per CU (152 KB of LDS each), capped by the tile count
 bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, int B, int H, int W,
-                       int grid_cap, int f16, hipStream_t stream) {
+                       int grid_cap, int f16, hipStream_t stream, float* part) {
   const int ty = (H + TH - 1) / TH, tx = (W + TW - 1) / TW;
   const int ntiles = B * ty * tx;
   if (ntiles <= 0) return true;
   const int grid = ntiles < grid_cap ? ntiles : grid_cap;
   if (f16)   // fp16 operands (fp16 autocast)
     hipLaunchKernelGGL((conv_enc64_kernel<true>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B,
-                       H, W, ty, tx);
+                       H, W, ty, tx, part);
   else
     hipLaunchKernelGGL((conv_enc64_kernel<false>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B, H,
-                       W, ty, tx);
+                       W, ty, tx, part);
   return true;
 }

@@ -292,7 +292,11 @@ __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint1
 // LANES lanes of one group (grid (groups, ceil(C / COLS))); the lanes stride over the group's
 // per-workgroup partials, a fixed-order LDS combine (deterministic), then lane 0 finalizes its
 // (group, channel).  16 lanes for the long batch-norm partial lists, 4 for per-image ones.
-template <int LANES, int TY>
+// TILED: the partials are a producing conv's per-tile rows [4][C] -- sum (x - K_t), sum
+// (x - K_t)^2, K_t, count (conv_enc64.hip) -- re-shifted to the group's first tile's K in double
+// (sum (x - K) = s1 + n d, sum (x - K)^2 = s2 + 2 d s1 + n d^2 with d = K_t - K), so the norm runs
+// no statistics pass of its own
+template <int LANES, int TY, bool TILED = false>
 __global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(
     const float* __restrict__ part, int nblk, const uint16_t* __restrict__ x, int HW, int C,
     int cnt, int mode, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -304,14 +308,30 @@ __global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(
   const int gi = blockIdx.x;
   const int t = threadIdx.x % COLS, lane = threadIdx.x / COLS;
   const int c = blockIdx.y * COLS + t;
-  const int SC = 2 * C;
+  const int SC = (TILED ? 4 : 2) * C;
   float a = 0.f, q = 0.f;
-  if (c < C)
-    for (int k = lane; k < nblk; k += LANES) {
-      const float* pk = part + ((int64_t)gi * nblk + k) * SC;
-      a += pk[c];
-      q += pk[C + c];
+  float K0 = 0.f;
+  if (c < C) {
+    if constexpr (TILED) {
+      K0 = part[(int64_t)gi * nblk * SC + 2 * C + c];
+      double ad = 0.0, qd = 0.0;
+      for (int k = lane; k < nblk; k += LANES) {
+        const float* pk = part + ((int64_t)gi * nblk + k) * SC;
+        const double s1 = pk[c], s2 = pk[C + c], n = pk[3 * C + c];
+        const double d = (double)pk[2 * C + c] - (double)K0;
+        ad += s1 + n * d;
+        qd += s2 + 2.0 * d * s1 + n * d * d;
+      }
+      a = (float)ad;
+      q = (float)qd;
+    } else {
+      for (int k = lane; k < nblk; k += LANES) {
+        const float* pk = part + ((int64_t)gi * nblk + k) * SC;
+        a += pk[c];
+        q += pk[C + c];
+      }
     }
+  }
   red[0][lane][t] = a;
   red[1][lane][t] = q;
   __syncthreads();
@@ -326,7 +346,7 @@ __global__ __launch_bounds__(256) void norm_reduce_finalize_kernel(
   const double m = (double)sa / cnt;
   double var = (double)sq / cnt - m * m;
   if (var < 0.0) var = 0.0;
-  const float K = ld1<TY>(x, (int64_t)(mode == 0 ? gi : 0) * HW * C + c);
+  const float K = TILED ? K0 : ld1<TY>(x, (int64_t)(mode == 0 ? gi : 0) * HW * C + c);
   const float mean = (float)(m + K);
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   if (mode == 1 && rmean != nullptr) {
@@ -841,6 +861,18 @@ void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, i
   else hipLaunchKernelGGL(norm_finalize_kernel<0>, dim3((tot + 255) / 256), dim3(256), 0, stream, sums, x, HW,
                      C, groups, nblk, cnt, mode, gamma, beta, cbias, rmean, rvar, momentum, eps, mean,
                      invstd, scale, shift, N);
+}
+
+void launch_norm_finalize_tiled(const float* part, int nblk, int N, int HW, int C, int mode,
+                                const float* gamma, const float* beta, const float* cbias,
+                                float* rmean, float* rvar, float momentum, float eps, float* mean,
+                                float* invstd, float* scale, float* shift, hipStream_t stream) {
+  const int groups = mode == 0 ? N : 1;
+  const int cnt = mode == 0 ? HW : N * HW;
+  // 64 lanes per channel: ~6 tile rows each at chairs (368 tiles per 184 x 248 image)
+  hipLaunchKernelGGL((norm_reduce_finalize_kernel<64, 0, true>), dim3(groups, (C + 3) / 4), dim3(256), 0,
+                     stream, part, nblk, nullptr, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
+                     momentum, eps, mean, invstd, scale, shift, N);
 }
 
 void launch_norm_apply(const uint16_t* x, const float* scale, const float* shift, int N, int HW,

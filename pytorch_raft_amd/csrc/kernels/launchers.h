@@ -262,8 +262,11 @@ void launch_col_sum(const uint16_t* g, int stride, int cout, int P, float* db, h
 // empty kernel `raft_phase_marker_kernel` (trace phase boundaries, scripts/prof_diff.py --phases)
 void launch_phase_marker(hipStream_t stream);
 // stride-1 3x3 64 -> 64 NHWC bf16 conv (conv_enc64.hip); wpk = (64, 9*64) packed [n][tap*64 + c]
+// part != null: per-tile norm statistics [tile][4][64] (sum(x-K), sum((x-K)^2), K, count), tiles
+// image-major, ceil(H/8) x ceil(W/16) per image (conv_enc64_tiles)
 bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, int B, int H, int W,
-                       int grid_cap, int f16, hipStream_t stream);
+                       int grid_cap, int f16, hipStream_t stream, float* part = nullptr);
+inline int conv_enc64_tiles(int H, int W) { return ((H + 7) / 8) * ((W + 15) / 16); }
 // fp32 (B,C,H,W) any strides -> (B,H,W,2cp) bf16 [hi | lo], zero padded (ops/conv_fp32.py)
 void launch_split_hilo(const float* x, int64_t sb, int64_t sc, int64_t sh, int64_t sw, int B, int C,
                        int H, int W, int cp, uint16_t* out, hipStream_t stream);
@@ -364,6 +367,12 @@ bool launch_convex_up_nhwc_bwd(const float* flow, const void* mask, int mask_is_
 int encoder_norm_blocks(int64_t range, int C, int* pix_per_blk);
 void launch_norm_stats(const uint16_t* x, int N, int HW, int C, int per_image, float* part,
                        int nblk, int pix_per_blk, int f16, hipStream_t stream);
+// training statistics (mode 0 / 1) from a producing conv's per-tile rows [tile][4][C]
+// (conv_enc64.hip); nblk = tiles per group (image for mode 0, the whole batch for mode 1)
+void launch_norm_finalize_tiled(const float* part, int nblk, int N, int HW, int C, int mode,
+                                const float* gamma, const float* beta, const float* cbias,
+                                float* rmean, float* rvar, float momentum, float eps, float* mean,
+                                float* invstd, float* scale, float* shift, hipStream_t stream);
 void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, int C, int mode,
                           int nblk, const float* gamma, const float* beta, const float* cbias,
                           float* rmean, float* rvar, float momentum, float eps, float* mean,

@@ -80,7 +80,9 @@ class _NormAct(torch.autograd.Function):
     """y = act(norm(x + conv_bias)) on channels_last bf16 / fp16; x is the bias-free conv output."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, cbias, norm, mode, relu, holder=None, sp=(0, 0)):
+    def forward(ctx, x, gamma, beta, cbias, norm, mode, relu, holder=None, sp=(0, 0), tst=None):
+        # tst: (per-tile statistics, tiles per image) of x from its producing conv (conv_enc64's
+        # epilogue) -- the norm then runs no statistics pass over x
         # sp = (ysp, gsp): fp32 schedule, the consuming / producing conv is a split conv -- y
         # (its input) and dx (its output gradient) are also written as the split pair
         # (2 x the 64-padded channels) and handed over (conv_fp32.offer_split)
@@ -99,7 +101,8 @@ class _NormAct(torch.autograd.Function):
                 momentum = norm.momentum if norm.momentum is not None else \
                     1.0 / float(norm.num_batches_tracked.item())
         mean, invstd = _ext.ops().norm_fwd_(x, mode, int(relu), gamma, beta, cbias, rm, rv,
-                                            float(momentum), float(eps), None, y, ys)
+                                            float(momentum), float(eps), None, y, ys,
+                                            *(tst if tst is not None else (None, 0)))
         _offer(y, ys)
         ctx.gsp = sp[1]
         # y is not kept (the backward recomputes the ReLU mask from x) unless an identity-residual
@@ -137,7 +140,7 @@ class _NormAct(torch.autograd.Function):
             _ext.ops().norm_bwd_(dy, x, None, mean, invstd, ctx.mode, int(ctx.relu), gamma, beta,
                                  dg, db, dc, dx, None, None, None, dxs)
         _offer(dx, dxs)
-        return dx, dg, db, dc, None, None, None, None, None
+        return dx, dg, db, dc, None, None, None, None, None, None
 
 
 class _NormActAddRelu(torch.autograd.Function):
@@ -146,7 +149,8 @@ class _NormActAddRelu(torch.autograd.Function):
     so the branch output is never written (`core/extractor.py:47-56`)."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, cbias, res, norm, mode, holder, res_holder, sp=(0, 0)):
+    def forward(ctx, x, gamma, beta, cbias, res, norm, mode, holder, res_holder, sp=(0, 0),
+                tst=None):
         out = torch.empty_like(x, memory_format=torch.channels_last)
         outs = _split_buf(out, sp[0])   # see _NormAct: the block output's split pair
         ctx.gsp = sp[1]
@@ -166,7 +170,8 @@ class _NormActAddRelu(torch.autograd.Function):
                     1.0 / float(norm.num_batches_tracked.item())
         res = res.contiguous(memory_format=torch.channels_last)
         mean, invstd = _ext.ops().norm_fwd_(x, mode, 1, gamma, beta, cbias, rm, rv, float(momentum),
-                                            float(eps), res, out, outs)
+                                            float(eps), res, out, outs,
+                                            *(tst if tst is not None else (None, 0)))
         _offer(out, outs)
         ctx.save_for_backward(x, out, mean, invstd, gamma, beta)
         ctx.mode = mode
@@ -199,7 +204,7 @@ class _NormActAddRelu(torch.autograd.Function):
         if ctx.res_holder is not None:
             ctx.res_holder['g'] = g
             gres = None
-        return dx, dg, db, dc, gres, None, None, None, None, None
+        return dx, dg, db, dc, gres, None, None, None, None, None, None
 
 
 class _StashGrad(torch.autograd.Function):
@@ -509,29 +514,45 @@ _WGRAD_NATIVE = os.environ.get('RAFT_ENCODER_WGRAD_NATIVE', '1') != '0'
 _ENC64 = os.environ.get('RAFT_ENC64', '1') != '0'
 
 
-def _conv3x3_nhwc(xn, wpk, ci, co):
+# RAFT_ENC64_STATS=1: the norm after a conv_enc64 conv takes its statistics from the conv's
+# epilogue instead of running its own statistics pass (A/B; see README)
+_ENC64_STATS = os.environ.get('RAFT_ENC64_STATS', '0') == '1'
+
+
+def _enc64_tiles(h, w):
+    return ((h + 7) // 8) * ((w + 15) // 16)
+
+
+def _conv3x3_nhwc(xn, wpk, ci, co, sink=None):
     """NHWC 16-bit stride-1 3x3 conv with a packed [co][tap * ci' + c] weight (ci' = ci rounded up
     to 64; the K slot past ci reads zeros): 64 -> 64 channels on the persistent 2-D halo-tile
-    kernel (conv_enc64.hip), anything else on the implicit GEMM."""
+    kernel (conv_enc64.hip), anything else on the implicit GEMM.  ``sink`` (dict): the 64 -> 64
+    kernel also reduces its output into per-tile norm statistics, left in sink['tst'] as
+    (tensor, tiles per image) for the norm that follows."""
     from . import conv as C
     B, H, W, _ = xn.shape
     out = torch.empty(B, H, W, co, device=xn.device, dtype=xn.dtype)
     if _ENC64 and ci == 64 and co == 64:
-        _ext.ops().conv_enc64_(xn, wpk, out)
+        part = None
+        if sink is not None and _ENC64_STATS:
+            tiles = _enc64_tiles(H, W)
+            part = torch.empty(B * tiles, 4, 64, device=xn.device, dtype=torch.float32)
+            sink['tst'] = (part, tiles)
+        _ext.ops().conv_enc64_(xn, wpk, out, part)
     else:
         C.conv_fwd([(xn, 0, _kslot(ci))], wpk, None, (3, 3), (1, 1), co, C.EPI_BF16, [out], [0],
                    bn=32)
     return out
 
 
-def _conv3x3_native_fwd(x, w, wf=None):
+def _conv3x3_native_fwd(x, w, wf=None, sink=None):
     ci, co = x.shape[1], w.shape[0]
     xn = x.permute(0, 2, 3, 1)                     # channels_last memory: a view
     if wf is None:
         wf = w.permute(0, 2, 3, 1).reshape(co, 9 * ci)
         if _kslot(ci) != ci:
             wf = torch.nn.functional.pad(wf.view(co, 9, ci), (0, _kslot(ci) - ci)).reshape(co, -1)
-    return _conv3x3_nhwc(xn, wf, ci, co).permute(0, 3, 1, 2)
+    return _conv3x3_nhwc(xn, wf, ci, co, sink).permute(0, 3, 1, 2)
 
 
 class _Conv3x3Native(torch.autograd.Function):
@@ -546,9 +567,9 @@ class _Conv3x3Native(torch.autograd.Function):
     [co][tap * ci + c]: the forward packs nothing."""
 
     @staticmethod
-    def forward(ctx, x, w, wd=None, wf=None):
+    def forward(ctx, x, w, wd=None, wf=None, sink=None):
         ctx.save_for_backward(x, w, wd)
-        return _conv3x3_native_fwd(x, w, wf)
+        return _conv3x3_native_fwd(x, w, wf, sink)
 
     @staticmethod
     def backward(ctx, dy):
@@ -577,7 +598,7 @@ class _Conv3x3Native(torch.autograd.Function):
             C.conv_wgrad_taps([(gn, [x.permute(0, 2, 3, 1)])], 0, [0], [ci], (3, 3), (1, 1), co,
                               dwp, None)
             dw = dwp.view(co, 3, 3, ci).permute(0, 3, 1, 2)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 _CONV_NATIVE = os.environ.get('RAFT_ENCODER_CONV_NATIVE', '1') != '0'
@@ -602,7 +623,7 @@ def _wgrad_native_ok(x, conv):
 _CONV_BYTES = int(os.environ.get('RAFT_CONV_CHUNK_BYTES', str(2 ** 31 - 1)))
 
 
-def _conv(ps, x, conv, with_bias=False):
+def _conv(ps, x, conv, with_bias=False, sink=None):
     """One encoder conv; batches whose input or output passes 2 GiB run as equal image chunks
     (a conv is per-image; the batch norm that couples the images runs on the whole batch, so a
     training-mode batch-norm encoder -- the chairs stage -- no longer caps the per-GPU batch)."""
@@ -617,7 +638,7 @@ def _conv(ps, x, conv, with_bias=False):
         size = -(-n // parts)   # equal chunks: the same kernel choices for every chunk
         outs = [_conv_one(ps, c, conv, with_bias) for c in torch.split(x, size, dim=0)]
         return torch.cat(outs, dim=0).contiguous(memory_format=torch.channels_last)
-    return _conv_one(ps, x, conv, with_bias)
+    return _conv_one(ps, x, conv, with_bias, sink)
 
 
 def _split_geom(conv):
@@ -632,7 +653,7 @@ def _split_ok(x, conv):
     return x.dtype == torch.float32 and _split_geom(conv) and conv_fp32.fits(x, conv.out_channels)
 
 
-def _conv_one(ps, x, conv, with_bias=False):
+def _conv_one(ps, x, conv, with_bias=False, sink=None):
     w = ps.weights.get(conv)
     if w is None:
         w = conv.weight.to(x.dtype).contiguous(memory_format=torch.channels_last)
@@ -645,8 +666,8 @@ def _conv_one(ps, x, conv, with_bias=False):
         return F.conv2d(x, w, b, conv.stride, conv.padding, conv.dilation, conv.groups)
     if not with_bias and _conv_native_ok(x, conv) and w.is_contiguous(memory_format=torch.channels_last):
         if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
-            return _Conv3x3Native.apply(x, w, ps.adjoint.get(conv), ps.fwdpack.get(conv))
-        return _conv3x3_native_fwd(x, w, ps.fwdpack.get(conv))
+            return _Conv3x3Native.apply(x, w, ps.adjoint.get(conv), ps.fwdpack.get(conv), sink)
+        return _conv3x3_native_fwd(x, w, ps.fwdpack.get(conv), sink)
     if not with_bias and _wgrad_native_ok(x, conv) and torch.is_grad_enabled() and \
             (x.requires_grad or w.requires_grad):
         return _Conv3x3WgradNative.apply(x, w)
@@ -658,13 +679,16 @@ def conv_norm_act(ps, x, conv, norm, relu=True, holder=None, consumer=None):
     """``consumer``: the conv that reads this output (fp32 schedule: when both are split convs
     the norm kernels also write the split operands, see _NormAct)."""
     mode = _norm_mode(norm)
-    y = _conv(ps, x, conv)
+    # training statistics: the 64 -> 64 conv kernel reduces its own output (no stats pass)
+    sink = {} if mode in (MODE_INSTANCE, MODE_BATCH_TRAIN) else None
+    y = _conv(ps, x, conv, sink=sink)
     y = y.contiguous(memory_format=torch.channels_last)
     gamma = beta = None
     if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and norm.affine:
         gamma, beta = norm.weight, norm.bias
     sp = (_split_pads(y, consumer)[0], _split_pads(x, conv)[1])
-    out = _NormAct.apply(y, gamma, beta, conv.bias, norm, mode, relu, holder, sp)
+    out = _NormAct.apply(y, gamma, beta, conv.bias, norm, mode, relu, holder, sp,
+                         sink.get('tst') if sink else None)
     if holder is not None:
         ps.holders[id(out)] = (out, holder)
     return out
@@ -681,7 +705,8 @@ def residual_block(ps, blk, x, consumer=None):
             xd = _StashGrad.apply(x, prod[1])   # its gradient joins the producer's stash
         x = conv_norm_act(ps, xd, blk.downsample[0], blk.downsample[1], relu=False)
     mode = _norm_mode(blk.norm2)
-    y2 = _conv(ps, y, blk.conv2).contiguous(memory_format=torch.channels_last)
+    sink = {} if mode in (MODE_INSTANCE, MODE_BATCH_TRAIN) else None
+    y2 = _conv(ps, y, blk.conv2, sink=sink).contiguous(memory_format=torch.channels_last)
     gamma = beta = None
     if mode in (MODE_BATCH_TRAIN, MODE_BATCH_EVAL) and blk.norm2.affine:
         gamma, beta = blk.norm2.weight, blk.norm2.bias
@@ -692,7 +717,8 @@ def residual_block(ps, blk, x, consumer=None):
     holder = {}
     sp = (_split_pads(y2, consumer)[0], _split_pads(y, blk.conv2)[1])
     out = _NormActAddRelu.apply(y2, gamma, beta, blk.conv2.bias, x, blk.norm2, mode, holder,
-                                res_holder[1] if res_holder is not None else None, sp)
+                                res_holder[1] if res_holder is not None else None, sp,
+                                sink.get('tst') if sink else None)
     ps.holders[id(out)] = (out, holder)
     return out
 

@@ -341,3 +341,45 @@ def test_norm_split_outputs_match_split_hilo(ext_ops, C):
     ext_ops.norm_bwd_(dy, x, None, mean, invstd, 0, 1, None, None, None, None, None, dx,
                       None, None, None, dxs)
     assert torch.equal(dxs, conv_fp32._split_nhwc(dx, pad))
+
+
+@pytest.mark.parametrize('mode,dt', [(0, torch.bfloat16), (1, torch.bfloat16), (0, H16)])
+@pytest.mark.parametrize('hw', [(40, 64), (23, 37)])
+def test_enc64_tile_stats_feed_the_norm(ext_ops, mode, dt, hw):
+    """conv_enc64's epilogue statistics (per 8 x 16 tile: shifted sums, shift, count) give the
+    norm the same mean / invstd / output as its own statistics pass over the conv output, also
+    with partial edge tiles (23 x 37) and a mean far from zero."""
+    from pytorch_raft_amd.ops.encoder import _enc64_tiles
+    torch.manual_seed(5)
+    n, (h, w) = 3, hw
+    x = (torch.randn(n, h, w, 64, device=DEV) + 0.3).to(dt)
+    # weights with a positive mean: conv outputs with a per-channel mean of ~3.5 at std ~1
+    wpk = (torch.randn(64, 9 * 64, device=DEV) / 24 + 0.02).to(dt)
+    out = torch.empty(n, h, w, 64, device=DEV, dtype=dt)
+    tiles = _enc64_tiles(h, w)
+    part = torch.empty(n * tiles, 4, 64, device=DEV)
+    ext_ops.conv_enc64_(x, wpk, out, part)
+    out2 = torch.empty_like(out)
+    ext_ops.conv_enc64_(x, wpk, out2)
+    assert torch.equal(out, out2)
+    assert (part[:, 3].sum(0) == n * h * w).all()
+    xc = out.permute(0, 3, 1, 2)                 # channels_last (B, C, H, W) view
+    assert xc.is_contiguous(memory_format=torch.channels_last)
+    assert out.float().mean().item() > 2.0
+    gm = torch.rand(64, device=DEV) + 0.5 if mode == 1 else None
+    bt = torch.randn(64, device=DEV) * 0.2 if mode == 1 else None
+    res = {}
+    for key, extra in (('pass', ()), ('tiles', (part, tiles))):
+        rm = torch.zeros(64, device=DEV) if mode == 1 else None
+        rv = torch.ones(64, device=DEV) if mode == 1 else None
+        y = torch.empty_like(xc)
+        mean, invstd = ext_ops.norm_fwd_(xc, mode, 1, gm, bt, None, rm, rv, 0.1, 1e-5, None, y,
+                                         None, *extra)
+        res[key] = (mean, invstd, y, rm, rv)
+    (m0, i0, y0, rm0, rv0), (m1, i1, y1, rm1, rv1) = res['pass'], res['tiles']
+    torch.testing.assert_close(m1, m0, atol=1e-5, rtol=1e-5)   # same values, other sum order
+    torch.testing.assert_close(i1, i0, atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(y1.float(), y0.float(), atol=2e-2, rtol=1e-2)
+    if mode == 1:
+        torch.testing.assert_close(rm1, rm0, atol=1e-5, rtol=1e-5)
+        torch.testing.assert_close(rv1, rv0, atol=1e-5, rtol=1e-4)
