@@ -1520,6 +1520,66 @@ void check_pc(const Tensor& t, int64_t P, int64_t C, at::ScalarType st, const ch
 // out[:, o_off:o_off+C] (bf16) = g[:, g_off:g_off+C] * scale * [y[:, y_off:] > 0]
 // stride-1 3x3 conv, 64 -> 64 channels, NHWC bf16 (the encoders' layer1; forward, or the input
 // gradient with the adjoint weight pack)
+// ---- encoder stem conv (stem_conv.hip): 7x7, stride 2, pad 3, 3 -> C (64 / 32) channels.
+// x (B,H,W,3) and out (B,Ho,Wo,C) contiguous NHWC 16-bit; w the (C,7,7,3)-ordered weight (the
+// memory of a channels_last (C,3,7,7) weight)
+int device_cus() {
+  static const int cus = [] {
+    hipDeviceProp_t p{};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return hipGetDeviceProperties(&p, dev) == hipSuccess && p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
+  }();
+  return cus;
+}
+void stem_checks(const Tensor& x, at::ScalarType st, int64_t& B, int64_t& H, int64_t& W, int64_t& Ho, int64_t& Wo) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.size(3) == 3 && x.is_contiguous() && x.scalar_type() == st,
+              "stem conv: x must be a contiguous (B,H,W,3) 16-bit NHWC tensor");
+  B = x.size(0), H = x.size(1), W = x.size(2);
+  Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  TORCH_CHECK(H * W * 6 < (int64_t(1) << 31), "stem conv: image too large");
+}
+void stem_conv_fwd_(const Tensor& x, const Tensor& w, const Tensor& out) {
+  const at::ScalarType st = op16(x);
+  int64_t B, H, W, Ho, Wo;
+  stem_checks(x, st, B, H, W, Ho, Wo);
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous() && w.scalar_type() == st && w.dim() == 4 &&
+                  w.size(1) == 7 && w.size(2) == 7 && w.size(3) == 3 && (w.size(0) == 64 || w.size(0) == 32),
+              "stem conv: w must be a contiguous (C,7,7,3) 16-bit tensor, C = 64 or 32");
+  const int64_t C = w.size(0);
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.scalar_type() == st && out.dim() == 4 &&
+                  out.size(0) == B && out.size(1) == Ho && out.size(2) == Wo && out.size(3) == C,
+              "stem conv: out must be a contiguous (B,Ho,Wo,C) tensor of x's dtype");
+  TORCH_CHECK(Ho * Wo * C * 2 < (int64_t(1) << 31), "stem conv: output too large");
+  c10::DeviceGuard gd(x.device());
+  const int tiles = stem_conv_tiles((int)B, (int)Ho, (int)Wo);
+  const int grid = std::min(tiles, 2 * device_cus());
+  TORCH_CHECK(launch_stem_conv_fwd(u16(x), u16(w), u16m(out), (int)B, (int)H, (int)W, (int)Ho, (int)Wo,
+                                   (int)C, grid, st == at::kHalf, cur_stream()),
+              "stem conv forward launch");
+}
+// -> dw (C,7,7,3), x's dtype: the weight gradient for the output gradient gy (B,Ho,Wo,C)
+Tensor stem_conv_wgrad(const Tensor& x, const Tensor& gy) {
+  const at::ScalarType st = op16(x);
+  int64_t B, H, W, Ho, Wo;
+  stem_checks(x, st, B, H, W, Ho, Wo);
+  TORCH_CHECK(gy.is_cuda() && gy.is_contiguous() && gy.scalar_type() == st && gy.dim() == 4 &&
+                  gy.size(0) == B && gy.size(1) == Ho && gy.size(2) == Wo &&
+                  (gy.size(3) == 64 || gy.size(3) == 32),
+              "stem conv: gy must be a contiguous (B,Ho,Wo,C) tensor of x's dtype, C = 64 or 32");
+  const int64_t C = gy.size(3);
+  TORCH_CHECK(Ho * Wo * C * 2 < (int64_t(1) << 31), "stem conv: output gradient too large");
+  c10::DeviceGuard gd(x.device());
+  const int tiles = stem_conv_tiles((int)B, (int)Ho, (int)Wo);
+  const int grid = std::min(tiles, 2 * device_cus());
+  Tensor part = at::empty({grid, C, 224}, x.options().dtype(at::kFloat));
+  Tensor dw = at::empty({C, 7, 7, 3}, x.options());
+  TORCH_CHECK(launch_stem_conv_wgrad(u16(x), u16(gy), part.data_ptr<float>(), u16m(dw), (int)B, (int)H,
+                                     (int)W, (int)Ho, (int)Wo, (int)C, grid, st == at::kHalf, cur_stream()),
+              "stem conv weight-gradient launch");
+  return dw;
+}
+
 // part (optional): the norm statistics of the output per 8 x 16 tile, (B * tiles, 4, 64) fp32
 // (see launch_conv_enc64), for norm_fwd_'s tstats
 void conv_enc64_(const Tensor& x, const Tensor& wpk, const Tensor& out, const c10::optional<Tensor>& part) {
@@ -2048,6 +2108,8 @@ TORCH_LIBRARY(raft_amd, m) {
   m.def("conv_dgrad_(Tensor[] ins, int[] in_off, int[] in_cnt, Tensor wpk, int kh, int kw, int ph, int pw, int cin_small, float scale, Tensor(a!)[] outs, int[] out_off, int[] out_cnt, int[] out_real, int[] out_acc, Tensor[] relu_y, int[] relu_off, int[] gate_mode, Tensor[] gate_t, int[] out_kcin=[], bool split=False) -> ()");
   m.def("split_hilo_(Tensor x, Tensor(a!) out) -> ()");
   m.def("conv_enc64_(Tensor x, Tensor wpk, Tensor(a!) out, Tensor(b!)? part=None) -> ()");
+  m.def("stem_conv_fwd_(Tensor x, Tensor w, Tensor(a!) out) -> ()");
+  m.def("stem_conv_wgrad(Tensor x, Tensor gy) -> Tensor");
   m.def("relu_bwd_(Tensor g, int g_off, Tensor? y, int y_off, Tensor(a!) out, int o_off, int C, float scale, bool split=False) -> ()");
   m.def("gru_q_bwd_(Tensor dh, Tensor z, Tensor q, Tensor hprev, Tensor(a!) dpre_q, Tensor(b!) dz, Tensor(c!) dhprev) -> ()");
   m.def("gru_zr_bwd_(Tensor drh, Tensor dz, Tensor z, Tensor r, Tensor hprev, Tensor(a!) dpre_zr, Tensor(b!) dhprev) -> ()");
@@ -2113,6 +2175,8 @@ TORCH_LIBRARY_IMPL(raft_amd, CUDA, m) {
   m.impl("relu_bwd_", &relu_bwd_);
   m.impl("split_hilo_", &split_hilo_);
   m.impl("conv_enc64_", &conv_enc64_);
+  m.impl("stem_conv_fwd_", &stem_conv_fwd_);
+  m.impl("stem_conv_wgrad", &stem_conv_wgrad);
   m.impl("gru_q_bwd_", &gru_q_bwd_);
   m.impl("gru_zr_bwd_", &gru_zr_bwd_);
   m.impl("flow_prep_", &flow_prep_);

@@ -262,6 +262,14 @@ void launch_col_sum(const uint16_t* g, int stride, int cout, int P, float* db, h
 // empty kernel `raft_phase_marker_kernel` (trace phase boundaries, scripts/prof_diff.py --phases)
 void launch_phase_marker(hipStream_t stream);
 // stride-1 3x3 64 -> 64 NHWC bf16 conv (conv_enc64.hip); wpk = (64, 9*64) packed [n][tap*64 + c]
+// encoder stem conv (stem_conv.hip): 7x7 stride 2 pad 3, 3 -> C (64 / 32) channels, NHWC 16-bit;
+// w = the (C, 7, 7, 3)-ordered weight; out (B, Ho, Wo, C); grid = persistent workgroups
+int stem_conv_tiles(int B, int Ho, int Wo);
+bool launch_stem_conv_fwd(const uint16_t* x, const uint16_t* w, uint16_t* out, int B, int H, int W,
+                          int Ho, int Wo, int C, int grid, int f16, hipStream_t stream);
+// weight gradient: part = grid x C x 224 fp32 scratch, dw = (C, 7, 7, 3) 16-bit result
+bool launch_stem_conv_wgrad(const uint16_t* x, const uint16_t* gy, float* part, uint16_t* dw, int B,
+                            int H, int W, int Ho, int Wo, int C, int grid, int f16, hipStream_t stream);
 // part != null: per-tile norm statistics [tile][4][64] (sum(x-K), sum((x-K)^2), K, count), tiles
 // image-major, ceil(H/8) x ceil(W/16) per image (conv_enc64_tiles)
 bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, int B, int H, int W,

@@ -601,6 +601,53 @@ class _Conv3x3Native(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+# RAFT_STEM_NATIVE=0: the encoders' 7x7 stride-2 stem conv on MIOpen instead of stem_conv.hip
+_STEM_NATIVE = os.environ.get('RAFT_STEM_NATIVE', '1') != '0'
+
+
+def _stem_ok(x, conv, w):
+    """The encoders' stem (`core/extractor.py:129,165`: 7x7, stride 2, pad 3, 3 -> 64 / 32) on the
+    MFMA stem kernels: 16-bit channels_last input and weight."""
+    return (_STEM_NATIVE and conv.kernel_size == (7, 7) and conv.stride == (2, 2)
+            and conv.padding == (3, 3) and conv.dilation == (1, 1) and conv.groups == 1
+            and conv.in_channels == 3 and conv.out_channels in (32, 64) and x.is_cuda
+            and x.dtype in _DTYPES and w.dtype == x.dtype
+            and x.is_contiguous(memory_format=torch.channels_last)
+            and w.is_contiguous(memory_format=torch.channels_last))
+
+
+def _stem_fwd(x, w):
+    b, _, h, wd = x.shape
+    out = torch.empty(b, (h - 1) // 2 + 1, (wd - 1) // 2 + 1, w.shape[0], device=x.device,
+                      dtype=x.dtype)
+    # channels_last memory: (B, H, W, 3) and (C, 7, 7, 3) are contiguous views
+    _ext.ops().stem_conv_fwd_(x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1), out)
+    return out.permute(0, 3, 1, 2)
+
+
+class _StemConv(torch.autograd.Function):
+    """Stem conv on stem_conv.hip: forward and weight gradient on MFMA (MIOpen: ~100 us forward +
+    ~134 us weight gradient per call at chairs, plus a zero fill); the input gradient -- never
+    needed for images -- falls back to ATen."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return _stem_fwd(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = dw = None
+        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        if ctx.needs_input_grad[1]:
+            dw = _ext.ops().stem_conv_wgrad(x.permute(0, 2, 3, 1), dy.permute(0, 2, 3, 1))
+            dw = dw.permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[0]:
+            dx = torch.nn.grad.conv2d_input(x.shape, w, dy, stride=2, padding=3)
+        return dx, dw
+
+
 _CONV_NATIVE = os.environ.get('RAFT_ENCODER_CONV_NATIVE', '1') != '0'
 
 
@@ -668,6 +715,10 @@ def _conv_one(ps, x, conv, with_bias=False, sink=None):
         if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
             return _Conv3x3Native.apply(x, w, ps.adjoint.get(conv), ps.fwdpack.get(conv), sink)
         return _conv3x3_native_fwd(x, w, ps.fwdpack.get(conv), sink)
+    if not with_bias and _stem_ok(x, conv, w):
+        if torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
+            return _StemConv.apply(x, w)
+        return _stem_fwd(x, w)
     if not with_bias and _wgrad_native_ok(x, conv) and torch.is_grad_enabled() and \
             (x.requires_grad or w.requires_grad):
         return _Conv3x3WgradNative.apply(x, w)

@@ -383,3 +383,39 @@ def test_enc64_tile_stats_feed_the_norm(ext_ops, mode, dt, hw):
     if mode == 1:
         torch.testing.assert_close(rm1, rm0, atol=1e-5, rtol=1e-5)
         torch.testing.assert_close(rv1, rv0, atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize('C,dt', [(64, torch.bfloat16), (32, torch.bfloat16), (64, H16)])
+@pytest.mark.parametrize('hw', [(40, 64), (37, 50)])
+def test_stem_conv_matches_fp32(ext_ops, C, dt, hw):
+    """The encoders' 7x7 stride-2 stem conv on stem_conv.hip (forward and weight gradient) vs the
+    fp32 conv of the same 16-bit operands, also with partial edge tiles (37 x 50 -> 19 x 25)."""
+    import torch.nn.functional as F
+    torch.manual_seed(2)
+    B, (H, W) = 3, hw
+    x = torch.randn(B, 3, H, W, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(C, 3, 7, 7, device=DEV) / 8).to(dt).contiguous(memory_format=torch.channels_last)
+    y = fast._stem_fwd(x, w)
+    ref = F.conv2d(x.float(), w.float(), stride=2, padding=3)
+    assert y.shape == ref.shape and y.dtype == dt
+    err = (y.float() - ref).abs().max().item()
+    assert err <= 2 ** -7 * ref.abs().max().item(), err
+    gy = torch.randn(ref.shape, device=DEV).to(dt).contiguous(memory_format=torch.channels_last)
+    dw = ext_ops.stem_conv_wgrad(x.permute(0, 2, 3, 1), gy.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+    wr = w.float().requires_grad_(True)
+    F.conv2d(x.float(), wr, stride=2, padding=3).backward(gy.float())
+    assert dw.shape == w.shape
+    rel = ((dw.float() - wr.grad).norm() / wr.grad.norm()).item()
+    assert rel < 5e-3, rel
+    # deterministic: fixed-order partial sums
+    dw2 = ext_ops.stem_conv_wgrad(x.permute(0, 2, 3, 1), gy.permute(0, 2, 3, 1)).permute(0, 3, 1, 2)
+    assert torch.equal(dw, dw2)
+    # the autograd node (weight gradient through the kernel, input gradient through ATen)
+    xg = x.clone().requires_grad_(True)
+    wg = w.clone().requires_grad_(True)
+    fast._StemConv.apply(xg, wg).backward(gy)
+    assert torch.equal(wg.grad.contiguous(), dw.contiguous())
+    xr = x.float().requires_grad_(True)
+    F.conv2d(xr, w.float(), stride=2, padding=3).backward(gy.float())
+    rel = ((xg.grad.float() - xr.grad).norm() / xr.grad.norm()).item()
+    assert rel < 1e-2, rel
