@@ -1571,7 +1571,8 @@ Tensor stem_conv_wgrad(const Tensor& x, const Tensor& gy) {
   TORCH_CHECK(Ho * Wo * C * 2 < (int64_t(1) << 31), "stem conv: output gradient too large");
   c10::DeviceGuard gd(x.device());
   const int tiles = stem_conv_tiles((int)B, (int)Ho, (int)Wo);
-  const int grid = std::min(tiles, 2 * device_cus());
+  // 3 workgroups per CU (50 KB of LDS each): more tile loads in flight
+  const int grid = std::min(tiles, 3 * device_cus());
   Tensor part = at::empty({grid, C, 224}, x.options().dtype(at::kFloat));
   Tensor dw = at::empty({C, 7, 7, 3}, x.options());
   TORCH_CHECK(launch_stem_conv_wgrad(u16(x), u16(gy), part.data_ptr<float>(), u16m(dw), (int)B, (int)H,

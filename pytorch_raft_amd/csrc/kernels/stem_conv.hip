@@ -183,7 +183,7 @@ __device__ __forceinline__ bf16x8_t tr_frag8(const uint16_t* X, int S, int kbase
 
 // dW partials: part[blockIdx.x][C][224] = sum over this workgroup's tiles of G^T A
 template <int NB, bool F16>
-__global__ __launch_bounds__(NTH, 2) void stem_conv_wgrad_kernel(const uint16_t* __restrict__ x,
+__global__ __launch_bounds__(NTH, 3) void stem_conv_wgrad_kernel(const uint16_t* __restrict__ x,
                                                                  const uint16_t* __restrict__ gy,
                                                                  float* __restrict__ part, int B,
                                                                  int H, int W, int Ho, int Wo) {
@@ -283,25 +283,30 @@ __global__ __launch_bounds__(NTH, 2) void stem_conv_wgrad_kernel(const uint16_t*
 }
 
 // dw[n][ky][kx][c] (16-bit, the (C, 7, 7, 3) order of a channels_last (C, 3, 7, 7) weight) = sum
-// over the nparts workgroup partials, fixed order: block = 64 elements x 4 lanes, lane L sums
-// partials L, L + 4, ..., then the 4 lane sums in order
+// over the nparts workgroup partials, fixed order: block = 16 elements x 16 lanes, lane L sums
+// partials L, L + 16, ..., then the 16 lane sums in order (588 blocks for C = 64: every CU
+// streams partial rows; 4 lanes per element and 64 elements per block left the reduce waiting
+// on one strided load chain per element on 37 CUs: 41 us per call)
 template <bool F16>
 __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __restrict__ part, int nparts,
                                                                 int C, uint16_t* __restrict__ dw) {
-  __shared__ float red[4][64];
-  const int e = blockIdx.x * 64 + (threadIdx.x & 63), l4 = threadIdx.x >> 6;
+  constexpr int LANES = 16, EPB = 16;
+  __shared__ float red[LANES][EPB];
+  const int el = threadIdx.x & (EPB - 1), l = threadIdx.x / EPB;
+  const int e = blockIdx.x * EPB + el;
   const int total = C * 147;
   float s = 0.f;
-  int src = 0;
   if (e < total) {
     const int n = e / 147, k = e - n * 147, ky = k / 21, j = k - ky * 21;
-    src = n * KP + ky * 32 + j;
-    for (int q = l4; q < nparts; q += 4) s += part[(int64_t)q * C * KP + src];
+    const int src = n * KP + ky * 32 + j;
+    for (int q = l; q < nparts; q += LANES) s += part[(int64_t)q * C * KP + src];
   }
-  red[l4][threadIdx.x & 63] = s;
+  red[l][el] = s;
   __syncthreads();
-  if (l4 == 0 && e < total) {
-    const float v = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+  if (l == 0 && e < total) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < LANES; ++q) v += red[q][el];
     dw[e] = raft_f2h<F16>(v);
   }
 }
@@ -335,7 +340,7 @@ bool launch_stem_conv_wgrad(const uint16_t* x, const uint16_t* gy, float* part, 
   else if (C == 32) { if (f16) STEM_WG(1, true); else STEM_WG(1, false); }
   else return false;
 #undef STEM_WG
-  const dim3 rg((unsigned)((C * 147 + 63) / 64));
+  const dim3 rg((unsigned)((C * 147 + 15) / 16));
   if (f16) hipLaunchKernelGGL((stem_wgrad_reduce_kernel<true>), rg, dim3(256), 0, stream, part, grid, C, dw);
   else hipLaunchKernelGGL((stem_wgrad_reduce_kernel<false>), rg, dim3(256), 0, stream, part, grid, C, dw);
   return true;
