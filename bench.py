@@ -64,6 +64,9 @@ def parse(argv=None):
     ap.add_argument('--dump_tune', type=str, default=None,
                     help='rank 0 writes the conv tile table it ran with (persisted picks + fresh '
                          'autotune picks) to this path (see pytorch_raft_amd/tune_db/)')
+    ap.add_argument('--probe_steps', type=int, default=3,
+                    help='steps issued on an idle queue after the timed region (host-issue probe; '
+                         'more of them = a synchronized-step stress run)')
     ap.add_argument('--trace_markers', action='store_true',
                     help='launch a marker spin kernel right before and after the timed steps')
     ap.add_argument('--roctx_region', action='store_true',
@@ -237,7 +240,7 @@ def main(argv=None):
     # loop the host runs ahead until the HIP queue is full, so per-step issue time there is
     # back-pressure, not host work
     probe = []
-    for k in range(3):
+    for k in range(max(1, a.probe_steps)):
         if device.type == 'cuda':
             torch.cuda.synchronize()
         i1, i2, fl, va = batches[k % len(batches)]
