@@ -37,6 +37,30 @@ from .optim import fetch_optimizer, clip_grad_norm_, clip_and_step, FusedAdamW
 # trace splits into encoder forward / decode (update block, correlation, loss) / encoder backward +
 # update (scripts/prof_diff.py --phases, scripts/categorize.py)
 _PHASE_MARKS = os.environ.get('RAFT_PHASE_MARKS', '0') == '1'
+# RAFT_HOST_TIMING=1: host wall time of each part of a graphed step (encode issue, replay call,
+# encoder-backward issue, update issue), averaged and printed to stderr at exit -- shows where the
+# host waits on the device
+_HOST_TIMING = os.environ.get('RAFT_HOST_TIMING', '0') == '1'
+_HT = {}
+
+
+def _ht(key, t0):
+    import time
+    t = time.perf_counter()
+    _HT.setdefault(key, []).append(t - t0)
+    return t
+
+
+if _HOST_TIMING:
+    import atexit
+    import sys as _sys
+
+    def _ht_report():
+        for k, v in _HT.items():
+            v = sorted(v)
+            print('host %-16s median %8.3f ms  p90 %8.3f ms  over %d steps'
+                  % (k, 1e3 * v[len(v) // 2], 1e3 * v[int(len(v) * 0.9)], len(v)), file=_sys.stderr)
+    atexit.register(_ht_report)
 
 
 def _phase_mark():
@@ -292,17 +316,24 @@ class GraphedTrainStep:
         st = self.st
         # encoder gradients are handed over by AccumulateGrad each step (no zero fill, no add
         # kernel per parameter); the update-block gradients live in the decode graph's pool
+        if _HOST_TIMING:
+            import time
+            t0 = time.perf_counter()
         for p in (self.enc_params if graphs else self.params):
             p.grad = None
         if st.has_buffers and self.world > 1:
             pdist.broadcast_buffers(st.model)  # DataParallel semantics: replica 0's BN stats
         feats = self._encode_and_stage(image1, image2, flow, valid)
+        if _HOST_TIMING:
+            t0 = _ht('encode', t0)
         if graphs:
             if _PHASE_MARKS:
                 _phase_mark()
             self.g_dec.replay()
             if _PHASE_MARKS:
                 _phase_mark()
+            if _HOST_TIMING:
+                t0 = _ht('replay', t0)
             loss = self.loss
         else:
             loss, _ = self._decode()
@@ -314,6 +345,8 @@ class GraphedTrainStep:
             self.enc_sync.prepare()
         self._encoder_backward(feats)
         del feats
+        if _HOST_TIMING:
+            t0 = _ht('enc_backward', t0)
         if self.enc_sync is not None:
             self.enc_sync.finish()                   # buckets with no gradient go out as zeros
         for p in self.enc_params:
@@ -327,10 +360,15 @@ class GraphedTrainStep:
 
     def _step_body(self, image1, image2, flow, valid, graphs=True):
         loss = self._forward_backward_sync(image1, image2, flow, valid, graphs)
+        if _HOST_TIMING:
+            import time
+            t0 = time.perf_counter()
         # clip + fused AdamW: a handful of multi-tensor launches, issued eagerly (the encoder
         # gradients are fresh tensors every step)
         self._update_graphable(loss)
         self._sched()
+        if _HOST_TIMING:
+            _ht('update', t0)
         return loss
 
     def _allreduce_dec(self):

@@ -64,6 +64,24 @@ def main():
     print('largest gaps (us, kernel before -> kernel after):')
     for g, a, b in sorted(gaps, reverse=True)[:top]:
         print('%9.1f  %s -> %s' % (g / 1e3, a[:70], b[:70]))
+    # the dispatch sequence of the last step boundary: kernels with start offsets, durations and
+    # queue / stream ids around the largest gap of the last quarter of the region
+    qcol = next((c for c in ('Stream_Id', 'Queue_Id') if c in rows[0]), None)
+    tail = [iv for iv in ivs if iv[0] > t_begin + 0.75 * wall]
+    if tail:
+        best, at = 0, 0
+        last = tail[0][1]
+        for k in range(1, len(tail)):
+            if tail[k][0] - last > best:
+                best, at = tail[k][0] - last, k
+            last = max(last, tail[k][1])
+        lo, hi = max(0, at - 25), min(len(tail), at + 25)
+        sid = {(int(r['Start_Timestamp']), r['Kernel_Name']): (r.get(qcol, '?') if qcol else '?')
+               for r in rows[i0 + 1:i1]}
+        print('around the largest late gap (%.1f us): start(us) dur(us) %s kernel' % (best / 1e3, qcol or ''))
+        for s0, e0, name in tail[lo:hi]:
+            print('%10.1f %8.1f %5s  %s' % ((s0 - t_begin) / 1e3, (e0 - s0) / 1e3,
+                                           sid.get((s0, name), '?'), name[:90]))
 
 
 if __name__ == '__main__':
