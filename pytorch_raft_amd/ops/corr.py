@@ -77,20 +77,15 @@ class _AllPairsBuild(torch.autograd.Function):
     def backward(ctx, _dtoken):
         st = ctx.state
         fmap1, fmap2 = ctx.saved_tensors
-        if st.grad is None and not st.windows and not st.taps:
+        if st.grad is None and not st.taps:
             return None, None, None, None
         b, c, h, w = ctx.shape
         dcorr = None
-        # mixed precision, window path only: dcorr in bf16 and bf16 GEMMs (fp32 accumulation);
-        # the fmaps are bf16 encoder outputs, so only the dcorr rounding differs from fp32
-        bf16 = (st.bf16_bwd or ctx.nhwc) and st.grad is None and bool(st.windows or st.taps)
+        # mixed precision, tap path only: dcorr in bf16 and bf16 GEMMs (fp32 accumulation); the
+        # fmaps are bf16 encoder outputs, so only the dcorr rounding differs from fp32
+        bf16 = (st.bf16_bwd or ctx.nhwc) and st.grad is None and bool(st.taps)
         if st.grad is not None:
             dcorr = _ext.ops().corr_pyr_grad_reduce(st.grad, 1.0 / math.sqrt(c))  # (B, N, N)
-        if st.windows:
-            dw = _ext.ops().corr_window_reduce([x[0] for x in st.windows], [x[1] for x in st.windows],
-                                               h, w, len(st.pyramid), st.radius, 1.0 / math.sqrt(c),
-                                               bf16)
-            dcorr = dw if dcorr is None else dcorr + dw
         # mixed precision, tap path only: the fold writes dC with rows padded to 64 columns and
         # the two feature-map GEMMs run on the hand-written MFMA kernel (corr_bwd.hip)
         native_gemm = (ctx.nhwc and bf16 and dcorr is None and bool(st.taps) and c % 128 == 0
@@ -106,7 +101,6 @@ class _AllPairsBuild(torch.autograd.Function):
                                             st.taps_split, split_gemm)
             dcorr = dt if dcorr is None else dcorr + dt
         st.grad = None
-        st.windows = []
         st.taps = []
         st.pyramid = None
         if native_gemm:
