@@ -5,7 +5,9 @@ import sys
 CATS = [('ours conv fwd', r'conv_fwd_kernel<[^>]*, [0-57], (true|false)>|conv_fwd_(glds|halo)_kernel<\d+, \d+, \d+, [0-57], \d+>|fh2_fwd'),
         ('ours dgrad', r'conv_fwd_kernel<[^>]*, [68], |conv_fwd_(glds|halo)_kernel<\d+, \d+, \d+, [68], \d+>|fh2_dgrad'),
         ('ours split', r'split_hilo'),
-        ('ours conv fwd', r'conv_enc64'),
+        ('ours conv fwd', r'conv_enc64|stem_conv_fwd'),
+        # the 7x7 stem's weight gradient: per-workgroup partials + their fixed-order reduce
+        ('ours wgrad', r'stem_conv_wgrad|stem_wgrad_reduce'),
         ('ours wgrad', r'fh2_wgrad'),
         ('ours wgrad', r'conv_wgrad'),
         ('encoder norm', r'norm_(bwd_)?(stats|apply|finalize|reduce_finalize)|partial_reduce|add_relu|relu_mask'),

@@ -62,3 +62,22 @@ def test_grid_fill_reads_the_persisted_table():
     lines = [l for l in out.splitlines()[1:] if l.strip()]
     assert len(lines) >= 20                     # the chairs-geometry keys of tune_db/
     assert all('%' in l for l in lines)
+
+
+def test_categorize_splits_ours_by_phase_and_places_the_stem(tmp_path):
+    p = tmp_path / 'summary.txt'
+    p.write_text(
+        '  5.00%   36.0  44.1  1.500  [decode] void conv_detail::conv_fwd_glds_kernel<3, 1, 1, 8, 2>(ConvFwdArgs)\n'
+        '  1.00%    2.0  46.9  0.100  [encoder] void (anonymous namespace)::stem_conv_fwd_kernel<2, false>(x)\n'
+        '  1.00%    2.0  58.9  0.120  [encoder] void (anonymous namespace)::stem_conv_wgrad_kernel<2, false>(x)\n'
+        '  0.50%    2.0  23.3  0.040  [encoder] void (anonymous namespace)::stem_wgrad_reduce_kernel<false>(x)\n'
+        '  0.50%    2.0  20.0  0.200  [encoder] void (anonymous namespace)::norm_bwd_stats_kernel<0>(x)\n')
+    out = subprocess.run([sys.executable, os.path.join(ROOT, 'scripts', 'categorize.py'), str(p)],
+                         capture_output=True, text=True, check=True).stdout
+    cats = {l.rsplit(None, 1)[0]: float(l.rsplit(None, 1)[1]) for l in out.splitlines()}
+    assert cats['update-block dgrad'] == 1.5           # EPI 8 = dgrad, decode phase
+    assert cats['encoder conv fwd'] == 0.1
+    assert abs(cats['encoder wgrad'] - 0.16) < 1e-9
+    assert cats['encoder norm'] == 0.2
+    assert 'other' not in cats and 'reduce' not in cats
+    assert abs(cats['total'] - 1.96) < 1e-9
