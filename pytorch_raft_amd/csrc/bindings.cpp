@@ -1307,7 +1307,7 @@ std::vector<Tensor> norm_fwd_(const Tensor& x, int64_t mode, int64_t relu,
                                shift.data_ptr<float>(), cur_stream());
   } else {
     if (mode <= 1) {
-      nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
+      nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, groups, &ppb);
       part = at::empty({groups * (nblk + 1) * 2 * C}, fo);  // partials + per-group sums
       launch_norm_stats(xp, (int)N, (int)HW, (int)C, mode == 0, part.data_ptr<float>(), nblk, ppb,
                         norm_ty(st), cur_stream());
@@ -1347,7 +1347,7 @@ void norm_bwd_(const Tensor& dy, const Tensor& x, const c10::optional<Tensor>& y
   float* db = const_cast<float*>(opt_f32(dbeta, C, "dbeta"));
   float* dc = const_cast<float*>(opt_f32(dcbias, C, "dcbias"));
   int ppb = 0;
-  const int nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, &ppb);
+  const int nblk = encoder_norm_blocks(mode == 0 ? HW : N * HW, (int)C, groups, &ppb);
   auto fo = x.options().dtype(at::kFloat);
   Tensor part = at::empty({groups * (nblk + 1) * 3 * C}, fo);  // partials + per-group sums
   Tensor coef = at::empty({groups, 5, C}, fo);  // A, B', C', scale, shift per (group, c), SoA

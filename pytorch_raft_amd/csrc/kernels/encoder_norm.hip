@@ -21,6 +21,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int NT = 256;
@@ -797,11 +799,21 @@ unsigned grid_for(int64_t nvec) {
 
 }  // namespace
 
-int encoder_norm_blocks(int64_t range, int C, int* pix_per_blk) {
-  // ~ one workgroup per 2 K pixel-rows of 8 channels -> enough blocks to fill the chip
+int encoder_norm_blocks(int64_t range, int C, int groups, int* pix_per_blk) {
+  // 32 pixels per lane: ~1 K workgroups for the 64-channel full-resolution layers, 70-400 for the
+  // 96 / 128-channel stages and the batch-norm encoder's single group.  RAFT_NORM_MIN_WG = n > 0
+  // halves the chunk (down to 8 pixels per lane, the statistics kernels' unrolled round) until a
+  // launch has n workgroups: measured slower at chairs (encoder norms 4.01 -> 4.26 / 4.38 ms/step
+  // at n = 1024 / 2048, profiles/r6/norm_wg/): the statistics passes did not speed up and the
+  // finalize kernels pay for the extra partial rows
+  static const int min_wg = [] {
+    const char* e = std::getenv("RAFT_NORM_MIN_WG");
+    return e ? std::atoi(e) : 0;
+  }();
   const int cg = C / 8;
   const int lanes = NT / cg;
   int64_t ppb = (int64_t)lanes * 32;
+  while ((range + ppb - 1) / ppb * groups < min_wg && ppb > (int64_t)lanes * 8) ppb /= 2;
   if (ppb < 64) ppb = 64;
   const int64_t nb = (range + ppb - 1) / ppb;
   *pix_per_blk = (int)ppb;

@@ -372,7 +372,7 @@ bool launch_convex_up_nhwc_bwd(const float* flow, const void* mask, int mask_is_
 
 // ---- encoder norm + activation, NHWC bf16 / fp16 (f16) (encoder_norm.hip)
 // mode: 0 instance, 1 batch (training statistics), 2 batch (running statistics), 3 none
-int encoder_norm_blocks(int64_t range, int C, int* pix_per_blk);
+int encoder_norm_blocks(int64_t range, int C, int groups, int* pix_per_blk);
 void launch_norm_stats(const uint16_t* x, int N, int HW, int C, int per_image, float* part,
                        int nblk, int pix_per_blk, int f16, hipStream_t stream);
 // training statistics (mode 0 / 1) from a producing conv's per-tile rows [tile][4][C]
