@@ -24,6 +24,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
+
 namespace {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -256,14 +258,160 @@ __global__ __launch_bounds__(NTH, 1) void conv_enc64_kernel(const uint16_t* __re
   }
 }
 
+// ---- channel-half variant: two workgroups per CU.
+// The kernel above holds ~152 KB of LDS, so one workgroup (one wave per SIMD) owns a CU and its
+// phases -- halo store, barrier, K loop, output staging, barrier, stores -- never overlap: 27 %
+// MFMA-busy at 2.4 TB/s (profiles/r6/final/pmc.txt).  Here a workgroup computes one 32-channel
+// half of a tile: the half's 32 weight rows (37 KB), ONE halo buffer (the staging barrier already
+// orders the next tile's halo store after every wave's K loop) and a 32-channel output stage fit
+// in ~77 KB, so two workgroups share a CU and one's MFMAs run beside the other's barriers and
+// epilogue.  4 waves x 32 pixels (two tile rows) x 32 channels, 36 MFMAs per wave per tile.
+// Work items (tile, half): i = 16a + 8h + r -> tile 8a + r, half h.  The grid is a multiple of 16,
+// so a workgroup keeps one half for its whole life (weights loaded once) and the two halves of a
+// tile go to workgroups b and b + 8 -- the same XCD under round-robin dispatch, where the second
+// read of the halo hits L2.
+constexpr int HBBUF = 32 * BROW;               // 37,376 B
+constexpr int HOROW = 80;                      // staged pixel: 32 channels (64 B) + 16 pad
+constexpr int HOBUF = TH * TW * HOROW;         // 10,240 B
+template <bool F16 = false>
+__global__ __launch_bounds__(NTH, 2) void conv_enc64h_kernel(const uint16_t* __restrict__ x,
+                                                             const uint16_t* __restrict__ wpk,
+                                                             uint16_t* __restrict__ out, int B,
+                                                             int H, int W, int tiles_y,
+                                                             int tiles_x, int nitems) {
+  __shared__ __attribute__((aligned(16))) char smem[ABUF + HBBUF + HOBUF];
+  char* As = smem;                 // halo
+  char* Bs = smem + ABUF;          // the half's weights
+  char* Os = Bs + HBBUF;           // output staging (bf16 [pixel][32 channels])
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntiles = B * tiles_y * tiles_x;
+  const int G = gridDim.x;
+  const int h = (blockIdx.x >> 3) & 1;
+
+  for (int e = tid; e < 32 * (KTOT / 8); e += NTH) {
+    const int n = e / (KTOT / 8), q = e - n * (KTOT / 8);
+    *reinterpret_cast<uint4*>(Bs + n * BROW + q * 16) =
+        *reinterpret_cast<const uint4*>(wpk + (int64_t)(h * 32 + n) * KTOT + q * 8);
+  }
+  auto tile_of = [](int i) { return (i >> 4) * 8 + (i & 7); };
+  auto load_a = [&](int i, uint4 (&areg)[APER]) {
+    const int t = tile_of(i);
+    const bool live = i < nitems && t < ntiles;
+    const int tt = live ? t : 0;
+    const int b = tt / (tiles_y * tiles_x), r = tt - b * tiles_y * tiles_x;
+    const int y0 = (r / tiles_x) * TH - 1, x0 = (r % tiles_x) * TW - 1;
+    const rsrc_t rs = mk_rsrc(x + (int64_t)b * H * W * 64, live ? (uint32_t)H * W * 128 : 0u);
+#pragma unroll
+    for (int j = 0; j < APER; ++j) {
+      const int e = tid + j * NTH;
+      const int hp = e >> 3, q = e & 7;
+      const int yy = y0 + hp / HWD, xx = x0 + hp % HWD;
+      const bool in = e < APIECES && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const uint32_t off = in ? (uint32_t)((yy * W + xx) * 128 + q * 16) : OOB;
+      areg[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+  };
+  auto store_a = [&](const uint4 (&areg)[APER]) {
+#pragma unroll
+    for (int j = 0; j < APER; ++j) {
+      const int e = tid + j * NTH;
+      *reinterpret_cast<uint4*>(As + hoff(e >> 3) + (e & 7) * 16) = areg[j];
+    }
+  };
+  const int hbase = (2 * wave + ((lane & 31) >> 4)) * AROWB + (lane & 15) * AROW + (lane >> 5) * 16;
+  const int bbase = (lane & 31) * BROW + (lane >> 5) * 16;
+
+  uint4 R0[APER], R1[APER], R2[APER];
+  load_a(blockIdx.x, R0);
+  load_a(blockIdx.x + G, R1);
+  load_a(blockIdx.x + 2 * G, R2);
+  auto tile = [&](int i, uint4 (&R)[APER]) {
+    store_a(R);
+    __syncthreads();  // halo (and, first time, weights) visible
+    load_a(i + NSET * G, R);
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    auto frags = [&](int tap, bf16x8_t (&af)[4], bf16x8_t (&bfr)[4]) {
+      const int shift = (tap / 3) * AROWB + (tap % 3) * AROW;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        bfr[kk] = *reinterpret_cast<const bf16x8_t*>(Bs + bbase + (tap * 64 + kk * 16) * 2);
+        af[kk] = *reinterpret_cast<const bf16x8_t*>(As + hbase + shift + kk * 32);
+      }
+    };
+    {
+      bf16x8_t af[2][4], bfr[2][4];
+      frags(0, af[0], bfr[0]);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        if (tap + 1 < 9) frags(tap + 1, af[(tap + 1) & 1], bfr[(tap + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) acc = raft_mfma32<F16>(af[tap & 1][kk], bfr[tap & 1][kk], acc);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    const int t = tile_of(i);
+    const bool live = t < ntiles;   // i < nitems here
+    const int tt = live ? t : 0;
+    const int b = tt / (tiles_y * tiles_x), r = tt - b * tiles_y * tiles_x;
+    const int ty0 = (r / tiles_x) * TH, tx0 = (r % tiles_x) * TW;
+    const int n = lane & 31;
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) {
+      const int p = wave * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
+      *reinterpret_cast<uint16_t*>(Os + p * HOROW + n * 2) = raft_f2h<F16>(acc[rr]);
+    }
+    __syncthreads();  // staged tile complete; the next tile's staging comes after its own barrier
+    const rsrc_t ro = mk_rsrc(out + (int64_t)b * H * W * 64, live ? (uint32_t)H * W * 128 : 0u);
+#pragma unroll
+    for (int j = 0; j < TH * TW * 4 / NTH; ++j) {
+      const int e = tid + j * NTH;
+      const int p = e >> 2, q = e & 3;
+      const int yy = ty0 + p / TW, xx = tx0 + p % TW;
+      const uint4 v = *reinterpret_cast<const uint4*>(Os + p * HOROW + q * 16);
+      const uint32_t off = yy < H && xx < W ? (uint32_t)((yy * W + xx) * 128 + h * 64 + q * 16) : OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                             ro, off, 0, 0);
+    }
+  };
+  for (int i = blockIdx.x; i < nitems; i += 3 * G) {
+    tile(i, R0);
+    if (i + G < nitems) tile(i + G, R1);
+    if (i + 2 * G < nitems) tile(i + 2 * G, R2);
+  }
+}
+
 }  // namespace
 
-// persistent grid: one workgroup per CU (152 KB of LDS each), capped by the tile count
+// persistent grids: the channel-half kernel (default, plain launches) runs 2 x CUs workgroups of
+// ~77 KB of LDS, the statistics kernel one workgroup per CU (~153 KB), capped by the work items.
+// Channel-half vs one-per-CU at chairs: fnet 127.3 -> 119.6 us, cnet 66.5 -> 58.5 us per call,
+// bitwise-equal outputs (profiles/r6/enc64h/)
 bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, int B, int H, int W,
                        int grid_cap, int f16, hipStream_t stream, float* part) {
   const int ty = (H + TH - 1) / TH, tx = (W + TW - 1) / TW;
   const int ntiles = B * ty * tx;
   if (ntiles <= 0) return true;
+  // RAFT_ENC64_HALF=0: the one-workgroup-per-CU kernel for the plain conv too (A/B); the tile
+  // statistics (part) are only in that kernel
+  static const bool half = [] {
+    const char* e = std::getenv("RAFT_ENC64_HALF");
+    return !(e && e[0] == '0');
+  }();
+  if (half && part == nullptr) {
+    const int nitems = (ntiles + 7) / 8 * 16;
+    int g = 2 * grid_cap < nitems ? 2 * grid_cap : nitems;
+    g = g / 16 * 16;
+    if (f16)
+      hipLaunchKernelGGL((conv_enc64h_kernel<true>), dim3(g), dim3(NTH), 0, stream, x, wpk, out, B, H, W,
+                         ty, tx, nitems);
+    else
+      hipLaunchKernelGGL((conv_enc64h_kernel<false>), dim3(g), dim3(NTH), 0, stream, x, wpk, out, B, H, W,
+                         ty, tx, nitems);
+    return true;
+  }
   const int grid = ntiles < grid_cap ? ntiles : grid_cap;
   if (f16)   // fp16 operands (fp16 autocast)
     hipLaunchKernelGGL((conv_enc64_kernel<true>), dim3(grid), dim3(NTH), 0, stream, x, wpk, out, B,

@@ -343,6 +343,30 @@ def test_norm_split_outputs_match_split_hilo(ext_ops, C):
     assert torch.equal(dxs, conv_fp32._split_nhwc(dx, pad))
 
 
+@pytest.mark.parametrize('dt', [torch.bfloat16, H16])
+@pytest.mark.parametrize('n,hw', [(6, (184, 248)), (5, (37, 45)), (1, (9, 17))])
+def test_enc64_channel_half_kernel_matches(ext_ops, dt, n, hw):
+    """The two-workgroups-per-CU channel-half conv_enc64 kernel (the default plain launch) gives
+    bitwise the output of the one-workgroup-per-CU kernel (the statistics launch), over many
+    persistent rounds (6 x 184 x 248: 2,208 tiles), with partial edge tiles and with a tile count
+    that is not a multiple of 8 (dead work items); and both match an fp32 conv."""
+    from pytorch_raft_amd.ops.encoder import _enc64_tiles
+    torch.manual_seed(11)
+    h, w = hw
+    x = torch.randn(n, h, w, 64, device=DEV).to(dt)
+    wt = (torch.randn(64, 64, 3, 3, device=DEV) / 24.0).to(dt)
+    wpk = wt.permute(0, 2, 3, 1).reshape(64, 576).contiguous()
+    out = torch.full((n, h, w, 64), 7.0, device=DEV, dtype=dt)
+    ext_ops.conv_enc64_(x, wpk, out)
+    ref_out = torch.empty_like(out)
+    part = torch.empty(n * _enc64_tiles(h, w), 4, 64, device=DEV)
+    ext_ops.conv_enc64_(x, wpk, ref_out, part)
+    assert torch.equal(out, ref_out)
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), wt.float(), None, 1, 1)
+    err = (out.permute(0, 3, 1, 2).float() - ref).abs().max() / ref.abs().max()
+    assert err.item() < 1e-2
+
+
 @pytest.mark.parametrize('mode,dt', [(0, torch.bfloat16), (1, torch.bfloat16), (0, H16)])
 @pytest.mark.parametrize('hw', [(40, 64), (23, 37)])
 def test_enc64_tile_stats_feed_the_norm(ext_ops, mode, dt, hw):
