@@ -76,6 +76,24 @@ template <> struct St<Fp16Bits> {
   }
 };
 
+// ---- cross-lane sums on DPP (VALU: no ds_bpermute traffic through the LDS pipe).  Fixed pairing
+// order, and every lane of the group ends with the same bits (deterministic).  Used where it
+// measured faster (the convex upsample backward); in the correlation build's epilogue the same
+// lane-pair sum on DPP made the compiler spill 243 VGPRs (0.28 -> 0.98 ms), and the flow head's
+// 32-lane sums showed no clear gain (20.1 vs 21.5 us, across boxes): both keep __shfl_xor.
+template <int CTRL>
+__device__ __forceinline__ float raft_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// sum over a 16-lane DPP row
+__device__ __forceinline__ float raft_row16_sum(float v) {
+  v += raft_dpp<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
+  v += raft_dpp<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
+  v += raft_dpp<0x141>(v);  // row_half_mirror: lane i <-> 7 - i of its 8
+  v += raft_dpp<0x140>(v);  // row_mirror: lane i <-> 15 - i of its 16
+  return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

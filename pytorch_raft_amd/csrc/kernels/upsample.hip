@@ -255,19 +255,6 @@ __global__ __launch_bounds__(256) void convex_up_nhwc_fwd_kernel(const float* __
   *reinterpret_cast<float4*>(O + 64 * HW + o) = make_float4(o1[0], o1[1], o1[2], o1[3]);
 }
 
-// sum over a 16-lane DPP row, left in every lane of the row (fixed order: deterministic)
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dppf<0xB1>(v);   // quad_perm [1,0,3,2]: lane ^ 1
-  v += dppf<0x4E>(v);   // quad_perm [2,3,0,1]: lane ^ 2
-  v += dppf<0x141>(v);  // row_half_mirror: lane i <-> 7 - i of its 8
-  v += dppf<0x140>(v);  // row_mirror: lane i <-> 15 - i of its 16
-  return v;
-}
-
 // 16 lanes per cell, 4 consecutive sub-pixels per lane (4 cells per wave): the mask / dmask rows
 // move as 8-B pieces, dout as 16-B pieces, and the 18 neighbour-weight sums are reduced over the
 // lane's 4 sub-pixels in registers first, leaving 4 shuffle steps per sum (was 6 over 64 lanes).
@@ -332,8 +319,8 @@ __global__ __launch_bounds__(256) void convex_up_nhwc_bwd_kernel(const float* __
   float wq = 0.f, wq2 = 0.f;
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    const float w0 = row16_sum((p[k][0] * d0[0] + p[k][1] * d0[1]) + (p[k][2] * d0[2] + p[k][3] * d0[3]));
-    const float w1 = row16_sum((p[k][0] * d1[0] + p[k][1] * d1[1]) + (p[k][2] * d1[2] + p[k][3] * d1[3]));
+    const float w0 = raft_row16_sum((p[k][0] * d0[0] + p[k][1] * d0[1]) + (p[k][2] * d0[2] + p[k][3] * d0[3]));
+    const float w1 = raft_row16_sum((p[k][0] * d1[0] + p[k][1] * d1[1]) + (p[k][2] * d1[2] + p[k][3] * d1[3]));
     wq = q == 2 * k ? w0 : (q == 2 * k + 1 ? w1 : wq);
     if (k == 8) wq2 = q == 0 ? w0 : w1;
   }
