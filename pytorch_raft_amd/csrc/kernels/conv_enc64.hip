@@ -25,6 +25,7 @@
 #include "launchers.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace {
 
@@ -383,6 +384,136 @@ __global__ __launch_bounds__(NTH, 2) void conv_enc64h_kernel(const uint16_t* __r
   }
 }
 
+// ---- producer / MFMA wave split (the per-phase stamps of the kernel above: the K loop is 44 % of
+// a wave's time, the halo loads, LDS stores, output staging, stores and barriers the rest, and
+// those phases never overlap the wave's own MFMAs).  8 waves: waves 0-3 run only the K loop and
+// the output staging of a 32-channel tile half (as above), waves 4-7 only move data -- the next
+// item's halo registers -> LDS, the item after that global -> registers, the previous item's
+// staged output LDS -> global.  Two halo buffers and two output stages in LDS (119,808 B, one
+// workgroup per CU), ONE barrier per item: in phase k the MFMA waves work on item k while the
+// producers store item k + 1's halo and drain item k - 1's output.
+constexpr int NTH2 = 512;                      // 4 MFMA waves + 4 producer waves
+constexpr int NPT = NTH2 - 256;                // producer threads
+constexpr int APERP = (APIECES + NPT - 1) / NPT;  // 6 halo pieces per producer thread
+template <bool F16 = false>
+__global__ __launch_bounds__(NTH2, 1) void conv_enc64p_kernel(const uint16_t* __restrict__ x,
+                                                              const uint16_t* __restrict__ wpk,
+                                                              uint16_t* __restrict__ out, int B,
+                                                              int H, int W, int tiles_y,
+                                                              int tiles_x, int nitems) {
+  __shared__ __attribute__((aligned(16))) char smem[HBBUF + 2 * ABUF + 2 * HOBUF];
+  char* Bs = smem;                         // the half's weights
+  char* As = smem + HBBUF;                 // 2 halo buffers
+  char* Os = As + 2 * ABUF;                // 2 output stages
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool producer = wave >= 4;
+  const int ptid = tid - 256;              // producer thread index (valid when producer)
+  const int ntiles = B * tiles_y * tiles_x;
+  const int G = gridDim.x;
+  const int h = (blockIdx.x >> 3) & 1;
+  const int K = (nitems - (int)blockIdx.x + G - 1) / G;   // items of this workgroup (>= 1)
+
+  for (int e = tid; e < 32 * (KTOT / 8); e += NTH2) {
+    const int n = e / (KTOT / 8), q = e - n * (KTOT / 8);
+    *reinterpret_cast<uint4*>(Bs + n * BROW + q * 16) =
+        *reinterpret_cast<const uint4*>(wpk + (int64_t)(h * 32 + n) * KTOT + q * 8);
+  }
+  auto tile_of = [](int i) { return (i >> 4) * 8 + (i & 7); };
+  auto item = [&](int k) { return (int)blockIdx.x + k * G; };
+  auto load_a = [&](int i, uint4 (&areg)[APERP]) {
+    const int t = tile_of(i);
+    const bool live = i < nitems && t < ntiles;
+    const int tt = live ? t : 0;
+    const int b = tt / (tiles_y * tiles_x), r = tt - b * tiles_y * tiles_x;
+    const int y0 = (r / tiles_x) * TH - 1, x0 = (r % tiles_x) * TW - 1;
+    const rsrc_t rs = mk_rsrc(x + (int64_t)b * H * W * 64, live ? (uint32_t)H * W * 128 : 0u);
+#pragma unroll
+    for (int j = 0; j < APERP; ++j) {
+      const int e = ptid + j * NPT;
+      const int hp = e >> 3, q = e & 7;
+      const int yy = y0 + hp / HWD, xx = x0 + hp % HWD;
+      const bool in = e < APIECES && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const uint32_t off = in ? (uint32_t)((yy * W + xx) * 128 + q * 16) : OOB;
+      areg[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+  };
+  auto store_a = [&](char* dst, const uint4 (&areg)[APERP]) {
+#pragma unroll
+    for (int j = 0; j < APERP; ++j) {
+      const int e = ptid + j * NPT;   // pieces past the halo land in the spare row (no branch)
+      *reinterpret_cast<uint4*>(dst + hoff(e >> 3) + (e & 7) * 16) = areg[j];
+    }
+  };
+  auto drain = [&](int i, const char* src) {   // staged output of item i -> global
+    const int t = tile_of(i);
+    const bool live = t < ntiles;
+    const int tt = live ? t : 0;
+    const int b = tt / (tiles_y * tiles_x), r = tt - b * tiles_y * tiles_x;
+    const int ty0 = (r / tiles_x) * TH, tx0 = (r % tiles_x) * TW;
+    const rsrc_t ro = mk_rsrc(out + (int64_t)b * H * W * 64, live ? (uint32_t)H * W * 128 : 0u);
+#pragma unroll
+    for (int j = 0; j < TH * TW * 4 / NPT; ++j) {
+      const int e = ptid + j * NPT;
+      const int p = e >> 2, q = e & 3;
+      const int yy = ty0 + p / TW, xx = tx0 + p % TW;
+      const uint4 v = *reinterpret_cast<const uint4*>(src + p * HOROW + q * 16);
+      const uint32_t off = yy < H && xx < W ? (uint32_t)((yy * W + xx) * 128 + h * 64 + q * 16) : OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) uint32_t, v),
+                                             ro, off, 0, 0);
+    }
+  };
+
+  uint4 R[APERP];
+  if (producer) {
+    load_a(item(0), R);
+    store_a(As, R);
+    load_a(item(1), R);   // item >= nitems: zero-size descriptor, zeros
+  }
+  __syncthreads();        // weights and item 0's halo visible
+
+  const int hbase = (2 * (wave & 3) + ((lane & 31) >> 4)) * AROWB + (lane & 15) * AROW + (lane >> 5) * 16;
+  const int bbase = (lane & 31) * BROW + (lane >> 5) * 16;
+  for (int k = 0; k < K; ++k) {
+    if (!producer) {
+      const char* Ab = As + (k & 1) * ABUF;
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      auto frags = [&](int tap, bf16x8_t (&af)[4], bf16x8_t (&bfr)[4]) {
+        const int shift = (tap / 3) * AROWB + (tap % 3) * AROW;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          bfr[kk] = *reinterpret_cast<const bf16x8_t*>(Bs + bbase + (tap * 64 + kk * 16) * 2);
+          af[kk] = *reinterpret_cast<const bf16x8_t*>(Ab + hbase + shift + kk * 32);
+        }
+      };
+      bf16x8_t af[2][4], bfr[2][4];
+      frags(0, af[0], bfr[0]);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        if (tap + 1 < 9) frags(tap + 1, af[(tap + 1) & 1], bfr[(tap + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) acc = raft_mfma32<F16>(af[tap & 1][kk], bfr[tap & 1][kk], acc);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      char* Ob = Os + (k & 1) * HOBUF;
+      const int n = lane & 31;
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int p = (wave & 3) * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
+        *reinterpret_cast<uint16_t*>(Ob + p * HOROW + n * 2) = raft_f2h<F16>(acc[rr]);
+      }
+    } else {
+      if (k + 1 < K) store_a(As + ((k + 1) & 1) * ABUF, R);
+      if (k + 2 < K) load_a(item(k + 2), R);
+      if (k >= 1) drain(item(k - 1), Os + ((k - 1) & 1) * HOBUF);
+    }
+    __syncthreads();  // item k's output staged, item k + 1's halo stored
+  }
+  if (producer) drain(item(K - 1), Os + ((K - 1) & 1) * HOBUF);
+}
+
 }  // namespace
 
 // persistent grids: the channel-half kernel (default, plain launches) runs 2 x CUs workgroups of
@@ -394,13 +525,27 @@ bool launch_conv_enc64(const uint16_t* x, const uint16_t* wpk, uint16_t* out, in
   const int ty = (H + TH - 1) / TH, tx = (W + TW - 1) / TW;
   const int ntiles = B * ty * tx;
   if (ntiles <= 0) return true;
-  // RAFT_ENC64_HALF=0: the one-workgroup-per-CU kernel for the plain conv too (A/B); the tile
-  // statistics (part) are only in that kernel
-  static const bool half = [] {
-    const char* e = std::getenv("RAFT_ENC64_HALF");
-    return !(e && e[0] == '0');
+  // RAFT_ENC64_KERNEL (A/B of the plain conv; the tile statistics, part != null, are only in the
+  // one-workgroup-per-CU kernel): pipe (producer / MFMA waves, default) | half | wg1
+  static const int kind = [] {
+    const char* e = std::getenv("RAFT_ENC64_KERNEL");
+    if (e && std::strcmp(e, "half") == 0) return 1;
+    if (e && std::strcmp(e, "wg1") == 0) return 2;
+    return 0;
   }();
-  if (half && part == nullptr) {
+  if (kind == 0 && part == nullptr) {
+    const int nitems = (ntiles + 7) / 8 * 16;
+    int g = grid_cap < nitems ? grid_cap : nitems;
+    g = g / 16 * 16;
+    if (f16)
+      hipLaunchKernelGGL((conv_enc64p_kernel<true>), dim3(g), dim3(NTH2), 0, stream, x, wpk, out, B, H, W,
+                         ty, tx, nitems);
+    else
+      hipLaunchKernelGGL((conv_enc64p_kernel<false>), dim3(g), dim3(NTH2), 0, stream, x, wpk, out, B, H, W,
+                         ty, tx, nitems);
+    return true;
+  }
+  if (kind == 1 && part == nullptr) {
     const int nitems = (ntiles + 7) / 8 * 16;
     int g = 2 * grid_cap < nitems ? 2 * grid_cap : nitems;
     g = g / 16 * 16;

@@ -1,8 +1,8 @@
 """conv_enc64 (the encoders' 64 -> 64 stride-1 3x3 conv, conv_enc64.hip) at the chairs layer1
-shapes: time per call of the kernel selected by RAFT_ENC64_HALF (1: the two-workgroups-per-CU
-channel-half kernel, the default; 0: one workgroup per CU) and the error vs an fp32 F.conv2d of the
-same bf16 operands.
-usage: RAFT_ENC64_HALF=0|1 PYTHONPATH=. python scripts/bench_enc64.py"""
+shapes: time per call of the kernel selected by RAFT_ENC64_KERNEL (pipe: producer / MFMA waves, the
+default; half: channel halves at two workgroups per CU; wg1: one workgroup per CU) and the error vs
+an fp32 F.conv2d of the same bf16 operands.
+usage: RAFT_ENC64_KERNEL=pipe|half|wg1 PYTHONPATH=. python scripts/bench_enc64.py"""
 import os
 
 import torch
@@ -13,7 +13,7 @@ from scripts.conv_bench import timeit
 
 dev = torch.device('cuda')
 ops = _ext.ops()
-v1 = os.environ.get('RAFT_ENC64_HALF', '1')
+v1 = os.environ.get('RAFT_ENC64_KERNEL', 'pipe')
 for name, B, H, W in [('fnet.l1', 24, 184, 248), ('cnet.l1', 12, 184, 248), ('odd', 3, 37, 45)]:
     torch.manual_seed(0)
     x = torch.randn(B, H, W, 64, device=dev).to(torch.bfloat16)
@@ -25,4 +25,4 @@ for name, B, H, W in [('fnet.l1', 24, 184, 248), ('cnet.l1', 12, 184, 248), ('od
     err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
     tf = 2 * B * H * W * 64 * 576 / t / 1e6
     ck = out.view(torch.int16).double().sum().item()  # bitwise fingerprint: the variants must agree
-    print(f'HALF={v1} {name}: {t:7.1f} us  {tf:6.1f} TF/s  err {err:.1e}  ck {ck:.0f}', flush=True)
+    print(f'{v1} {name}: {t:7.1f} us  {tf:6.1f} TF/s  err {err:.1e}  ck {ck:.0f}', flush=True)

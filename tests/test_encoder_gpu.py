@@ -346,10 +346,11 @@ def test_norm_split_outputs_match_split_hilo(ext_ops, C):
 @pytest.mark.parametrize('dt', [torch.bfloat16, H16])
 @pytest.mark.parametrize('n,hw', [(6, (184, 248)), (5, (37, 45)), (1, (9, 17))])
 def test_enc64_plain_kernel_matches(ext_ops, dt, n, hw):
-    """The plain conv_enc64 launch (the two-workgroups-per-CU channel-half kernel) gives bitwise
-    the output of the one-workgroup-per-CU kernel (the statistics launch), over many persistent
-    rounds (6 x 184 x 248: 2,208 tiles), with partial edge tiles and with a tile count that is
-    not a multiple of 8 (dead work items); and both match an fp32 conv."""
+    """The plain conv_enc64 launch (the producer / MFMA-wave kernel; RAFT_ENC64_KERNEL=half / wg1
+    select the others) gives bitwise the output of the one-workgroup-per-CU kernel (the
+    statistics launch), over many persistent items per workgroup (6 x 184 x 248: 2,208 tiles),
+    with partial edge tiles and with a tile count that is not a multiple of 8 (dead work items);
+    and both match an fp32 conv."""
     from pytorch_raft_amd.ops.encoder import _enc64_tiles
     torch.manual_seed(11)
     h, w = hw
