@@ -473,6 +473,10 @@ __global__ __launch_bounds__(NTH2, 1) void conv_enc64p_kernel(const uint16_t* __
 
   const int hbase = (2 * (wave & 3) + ((lane & 31) >> 4)) * AROWB + (lane & 15) * AROW + (lane >> 5) * 16;
   const int bbase = (lane & 31) * BROW + (lane >> 5) * 16;
+  // producers first at issue arbitration, so their loads go out while the MFMA waves run: fnet
+  // 113.4 / 113.5 vs 116.9 / 118.3 us per call (MFMA waves first: 112.9 / 118.5;
+  // profiles/r6/enc64h/pipe_prio_ab.log)
+  if (producer) __builtin_amdgcn_s_setprio(1);
   for (int k = 0; k < K; ++k) {
     if (!producer) {
       const char* Ab = As + (k & 1) * ABUF;
