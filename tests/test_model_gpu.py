@@ -217,3 +217,30 @@ def test_fp16_train_step_gradscaler(ext_ops):
     w2 = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
     assert not torch.equal(w1, w2), 'no step was taken once the scale came down'
     assert all(l == l for l in losses) and losses[-1] < losses[0] * 1.5, losses
+
+
+def test_bf16_encoder_streams_first_call_serial(ext_ops):
+    """bf16 autocast runs the context encoder on a side stream -- from the SECOND call of an input
+    signature on: the first call (MIOpen's solver search for the strided convs) stays on one
+    stream.  The two-stream call gives the same features, flows and gradients as the one-stream
+    call (the encoders are deterministic)."""
+    from pytorch_raft_amd.models import raft as raft_mod
+    from pytorch_raft_amd.ops.loss import sequence_loss
+    if raft_mod._ENC_STREAMS != 'auto':
+        pytest.skip('RAFT_ENC_STREAMS forced')
+    raft_mod._ENC_SEEN.clear()
+    i1, i2, flow, valid = make_pair_batch(2, 96, 128, device=DEV)
+    m = _model('hip', mixed=True).train()
+    m.freeze_bn()
+    outs = []
+    for _ in range(2):
+        m.zero_grad(set_to_none=True)
+        preds = m(i1, i2, iters=2)
+        loss, _ = sequence_loss(preds, flow, valid, 0.8)
+        loss.backward()
+        outs.append((m.last_enc_streams, preds[-1].detach().float(),
+                     torch.cat([p.grad.reshape(-1).float() for p in m.parameters() if p.grad is not None])))
+    assert outs[0][0] == 1 and outs[1][0] == 2
+    torch.testing.assert_close(outs[1][1], outs[0][1], atol=1e-3, rtol=1e-3)
+    rel = ((outs[1][2] - outs[0][2]).norm() / outs[0][2].norm()).item()
+    assert rel < 1e-3, rel
