@@ -293,7 +293,9 @@ __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint1
 // Partial reduce + finalize of the training statistics in ONE launch: block = COLS channels x
 // LANES lanes of one group (grid (groups, ceil(C / COLS))); the lanes stride over the group's
 // per-workgroup partials, a fixed-order LDS combine (deterministic), then lane 0 finalizes its
-// (group, channel).  16 lanes for the long batch-norm partial lists, 4 for per-image ones.
+// (group, channel).  64 lanes for the long batch-norm partial lists (4 channels per block: 8.3 ->
+// 5.6 us per call vs 16 lanes' 4 blocks of 256 threads for a 64-channel batch norm; the backward
+// finalize keeps 16 lanes: 9.2 -> 14.8 us with 64, profiles/r6/norm_wg/), 4 for per-image ones.
 // TILED: the partials are a producing conv's per-tile rows [4][C] -- sum (x - K_t), sum
 // (x - K_t)^2, K_t, count (conv_enc64.hip) -- re-shifted to the group's first tile's K in double
 // (sum (x - K) = s1 + n d, sum (x - K)^2 = s2 + 2 d s1 + n d^2 with d = K_t - K), so the norm runs
@@ -841,13 +843,13 @@ void launch_norm_finalize(const float* part, const uint16_t* x, int N, int HW, i
   if (mode <= 1) {
     // training statistics: partial reduce + finalize in one launch
     if (nblk > 64) {
-      if (f16 == 2) hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 2>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+      if (f16 == 2) hipLaunchKernelGGL((norm_reduce_finalize_kernel<64, 2>), dim3(groups, (C + 3) / 4), dim3(256), 0,
                          stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
                          momentum, eps, mean, invstd, scale, shift, N);
-      else if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 1>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+      else if (f16) hipLaunchKernelGGL((norm_reduce_finalize_kernel<64, 1>), dim3(groups, (C + 3) / 4), dim3(256), 0,
                          stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
                          momentum, eps, mean, invstd, scale, shift, N);
-      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<16, 0>), dim3(groups, (C + 15) / 16), dim3(256), 0,
+      else hipLaunchKernelGGL((norm_reduce_finalize_kernel<64, 0>), dim3(groups, (C + 3) / 4), dim3(256), 0,
                          stream, part, nblk, x, HW, C, cnt, mode, gamma, beta, cbias, rmean, rvar,
                          momentum, eps, mean, invstd, scale, shift, N);
     } else {
