@@ -29,11 +29,24 @@ __global__ __launch_bounds__(256) void seq_loss_partial_kernel(PredPtrs preds, i
     const float mag = sqrtf(gx * gx + gy * gy);
     const bool v = (valid[t] >= 0.5f) && (mag < max_flow);
     if (!v) continue;
+    // predictions four at a time, their 8 loads issued before the sums (the same accumulation
+    // order as one at a time: newest first, w = gamma^(n-1-i))
     float w = 1.f, wl = 0.f;
-    for (int i = n - 1; i >= 0; --i) {
-      const float* P = preds.p[i];
-      wl += w * (fabsf(P[o0] - gx) + fabsf(P[o1] - gy));
-      w *= gamma;
+    for (int i0 = n - 1; i0 >= 0; i0 -= 4) {
+      float px[4], py[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 - u >= 0 ? i0 - u : 0;   // past the oldest: a valid (unused) read
+        px[u] = preds.p[i][o0];
+        py[u] = preds.p[i][o1];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (i0 - u >= 0) {
+          wl += w * (fabsf(px[u] - gx) + fabsf(py[u] - gy));
+          w *= gamma;
+        }
+      }
     }
     const float* P = preds.p[n - 1];
     const float dx = P[o0] - gx, dy = P[o1] - gy;

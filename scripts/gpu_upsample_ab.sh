@@ -12,5 +12,5 @@ timeout -k 10 300 python bench.py > gpurun_out/up_bench.log 2>&1 || { tail -3 gp
 grep -o '"value": [0-9.]*' gpurun_out/up_bench.log
 bash scripts/gpu_profile.sh up > /dev/null 2>&1 || exit 1
 python scripts/categorize.py gpurun_out/up_summary.txt > gpurun_out/up_categories.txt
-grep -E "convex|fh2_fwd|corr_build" gpurun_out/up_summary.txt | cut -c1-130
+grep -E "convex|seq_loss" gpurun_out/up_summary.txt | cut -c1-130
 grep -E "upsample|total" gpurun_out/up_categories.txt
