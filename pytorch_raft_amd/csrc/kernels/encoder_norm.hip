@@ -295,8 +295,8 @@ __global__ void norm_finalize_kernel(const float* __restrict__ part, const uint1
 // per-workgroup partials, a fixed-order LDS combine (deterministic), then lane 0 finalizes its
 // (group, channel).  64 lanes for the long batch-norm partial lists (4 channels per block: 8.3 ->
 // 5.6 us per call vs 16 lanes' 4 blocks of 256 threads for a 64-channel batch norm; the backward
-// finalize runs 32 lanes: 8.6 -> 7.8 us, while 64 gave 14.8, profiles/r6/norm_wg/), 4 for
-// per-image ones.
+// finalize keeps 16 lanes: 64 gave 14.8 vs 9.2 us, 32 gave 7.8 / 9.0 vs 8.6 us on two boxes --
+// noise, profiles/r6/norm_wg/, profiles/r6/final8/), 4 for per-image ones.
 // TILED: the partials are a producing conv's per-tile rows [4][C] -- sum (x - K_t), sum
 // (x - K_t)^2, K_t, count (conv_enc64.hip) -- re-shifted to the group's first tile's K in double
 // (sum (x - K) = s1 + n d, sum (x - K)^2 = s2 + 2 d s1 + n d^2 with d = K_t - K), so the norm runs
@@ -955,11 +955,11 @@ void launch_norm_bwd(const uint16_t* dy, const uint16_t* x, const uint16_t* y, c
   // after the partials in `part`
   float* pg = part + (int64_t)groups * nblk * 3 * C;
   if (nblk > 64) {
-    if (f16 == 2) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<32, 2>), dim3(groups, (C + 7) / 8), dim3(256), 0,
+    if (f16 == 2) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, 2>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                        stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
-    else if (f16) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<32, 1>), dim3(groups, (C + 7) / 8), dim3(256), 0,
+    else if (f16) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, 1>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                        stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
-    else hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<32, 0>), dim3(groups, (C + 7) / 8), dim3(256), 0,
+    else hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<16, 0>), dim3(groups, (C + 15) / 16), dim3(256), 0,
                        stream, part, nblk, C, cnt, mode, gamma, beta, mean, invstd, coef, pg);
   } else {
     if (f16 == 2) hipLaunchKernelGGL((norm_bwd_reduce_finalize_kernel<4, 2>), dim3(groups, (C + 63) / 64), dim3(256), 0,
