@@ -49,10 +49,11 @@ _FP32_FUSED = os.environ.get('RAFT_FP32_FUSED', '1') != '0'
 # the backwards overlap the same way.  The encoders are independent until the decode; co-running
 # fills each other's kernel tails and small launches (round 6 A/B: 484.3 / 488.3 vs 466.1 / 466.8
 # pairs/s on one box; the feature encoder's two frames on a third stream as well: 468.6 / 468.0
-# vs 476.6 / 480.3 -- profiles/r6/enc_streams/).  Default (unset): 2 under bf16 autocast only --
-# the configuration validated over thousands of steps; an fp16-autocast bench with two streams
-# hit an illegal address in a late step (profiles/r6/r6i/bench_fp16_2streams.log), as a two-stream
-# attempt in round 4 did inside MIOpen, so fp16 and fp32 keep one stream unless 2 is forced.
+# vs 476.6 / 480.3 -- profiles/r6/enc_streams/).  Default (unset): 2 under autocast (bf16 and
+# fp16), 1 for fp32.  fp16 had kept one stream after an fp16 bench with two streams hit an
+# illegal address (profiles/r6/r6i/bench_fp16_2streams.log); with the first call of each input
+# signature serial (_ENC_SEEN below) two fp16 runs of 1,500 + 300 and 2,500 + 500 steps ran clean
+# at 472.9 / 475.9 pairs/s vs 454.8 on one stream (profiles/r6/stress/).
 _ENC_STREAMS = os.environ.get('RAFT_ENC_STREAMS', 'auto')
 _SIDE = {}
 # Encoder call signatures (input shape, dtypes, grad / train mode, device) already run once: the
@@ -252,7 +253,7 @@ class RAFT(nn.Module):
     def _enc_streams(self):
         if _ENC_STREAMS != 'auto':
             return int(_ENC_STREAMS)
-        return 2 if (self.args.mixed_precision and self.amp_dtype == torch.bfloat16) else 1
+        return 2 if self.args.mixed_precision else 1
 
     def decode(self, fmap1, fmap2, net, inp, iters=12, flow_init=None, test_mode=False):
         """Correlation volume + GRU iterations + upsampling (`core/raft.py:102-144`)."""
